@@ -1,0 +1,117 @@
+#!/usr/bin/env python3
+"""Headline benchmark: FL rounds/sec — FedAvg, 100 clients, ResNet-56, CIFAR-100-shaped
+synthetic data, on N MI355X GPUs of one node (BASELINE.json config 3).
+
+Per round: 100 clients × 500 samples × 1 local epoch (batch 64, SGD lr 1e-3), then FedAvg
+aggregation (on-GPU weighted sum + one RCCL all-reduce over xGMI). Weights are random-init,
+data is synthetic (no network). The total work is fixed at 100 clients as N grows
+(strong scaling). Every timed round is a complete FL round: local training of all clients,
+optimizer steps, aggregation and the global-model update.
+
+    python bench.py --gpus 1 --steps 3 --warmup 1
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3, help="timed FL rounds")
+    p.add_argument("--warmup", type=int, default=1, help="untimed FL rounds")
+    p.add_argument("--clients", type=int, default=100)
+    p.add_argument("--samples-per-client", type=int, default=500)
+    p.add_argument("--batch-size", type=int, default=64)
+    p.add_argument("--epochs", type=int, default=1)
+    p.add_argument("--model", default="resnet56")
+    p.add_argument("--dataset", default="cifar100")
+    p.add_argument("--dtype", default="bf16")
+    p.add_argument("--lr", type=float, default=0.001)
+    p.add_argument("--profile-rounds", type=int, default=0)
+    return p.parse_args()
+
+
+def main():
+    a = parse()
+    import torch
+    from fedml_amd.arguments import Arguments
+    from fedml_amd.data.synthetic import get_spec
+    from fedml_amd.models import create
+    from fedml_amd.parallel import comm
+    from fedml_amd.simulation.rccl.client_store import DeviceClientStore
+    from fedml_amd.simulation.rccl.simulator import RCCLSimulator
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    use_gpu = torch.cuda.is_available()
+    if use_gpu:
+        torch.cuda.set_device(local_rank)
+        device = torch.device(f"cuda:{local_rank}")
+    else:
+        device = torch.device("cpu")
+    spec = get_spec(a.dataset)
+    args = Arguments.from_dict({"x": {
+        "training_type": "simulation", "backend": "RCCL", "federated_optimizer": "FedAvg",
+        "dataset": a.dataset, "model": a.model, "client_num_in_total": a.clients,
+        "client_num_per_round": a.clients, "comm_round": a.steps, "epochs": a.epochs,
+        "batch_size": a.batch_size, "client_optimizer": "sgd", "learning_rate": a.lr, "weight_decay": 0.001,
+        "frequency_of_the_test": 0, "compute_dtype": a.dtype if use_gpu else "fp32", "random_seed": 0,
+    }})
+    torch.manual_seed(0)
+    model = create(args, spec.num_classes)
+    rank, ws = comm.init_process_group(device=device if use_gpu else None)
+    counts = [a.samples_per_client] * a.clients
+    store = DeviceClientStore.synthetic_on_device(spec, counts, device, seed=0,
+                                                  dtype=torch.float32)
+    sim = RCCLSimulator(args, device, None, model, store=store)
+    for _ in range(a.warmup):
+        sim.run(1)
+    if use_gpu:
+        torch.cuda.synchronize(device)
+    comm.barrier(device if use_gpu else None)
+    if use_gpu:
+        torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    sim.run(a.steps)
+    if use_gpu:
+        torch.cuda.synchronize(device)
+    comm.barrier(device if use_gpu else None)
+    if use_gpu:
+        torch.cuda.synchronize(device)
+    elapsed = time.perf_counter() - t0
+    elapsed = comm.max_over_ranks(elapsed, device)
+    loss = float(sim.engine.last_loss)
+    if rank == 0:
+        rounds_per_s = a.steps / elapsed
+        out = {
+            "metric": "FL rounds/sec (FedAvg, 100 clients, ResNet-56)",
+            "value": round(rounds_per_s, 4),
+            "unit": "rounds/s",
+            "n_gpus": ws,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1000.0 * elapsed / a.steps, 2),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": a.dtype if use_gpu else "fp32",
+            "data": "synthetic (CIFAR-100-shaped, class-conditional), random-init weights",
+            "config": {"model": a.model, "dataset": a.dataset, "clients": a.clients,
+                       "samples_per_client": a.samples_per_client, "global_batch": a.batch_size * a.clients,
+                       "local_batch": a.batch_size, "local_epochs": a.epochs, "seq_len": None,
+                       "parallelism": f"client-parallel x{ws} (dp{ws}), RCCL all-reduce aggregation"},
+            "samples_per_s": round(a.clients * a.samples_per_client * a.epochs * a.steps / elapsed, 1),
+            "final_train_loss": round(loss, 4),
+        }
+        print(json.dumps(out), flush=True)
+    comm.destroy()
+
+
+if __name__ == "__main__":
+    main()

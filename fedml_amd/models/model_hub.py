@@ -1,0 +1,74 @@
+"""``fedml_amd.model.create(args, output_dim)`` (reference: `model/model_hub.py:13-53`).
+
+Same (model, dataset) → module mapping as the reference, including its
+fallback to LogisticRegression, plus the north-star models the reference lacks
+(``resnet18`` for CIFAR, ``distilbert``, ``vit_b16``) and the rest of the zoo
+(resnet110, vgg, gan, darts, gkt split nets).
+"""
+import logging
+
+from .cv.cnn import CNN_DropOut, CNN_OriginalFedAvg
+from .cv.darts import Network as DartsNetwork
+from .cv.efficientnet import EfficientNet
+from .cv.mnist_gan import MNISTGAN
+from .cv.mobilenet import mobilenet
+from .cv.mobilenet_v3 import MobileNetV3
+from .cv.resnet import resnet18_cifar, resnet56, resnet110
+from .cv.resnet_gkt import resnet8_56, resnet56_server
+from .cv.resnet_gn import resnet18 as resnet18_gn
+from .cv.vgg import VGG
+from .linear.lr import LogisticRegression
+from .nlp.rnn import RNN_OriginalFedAvg, RNN_StackOverFlow
+from .transformer.distilbert import distilbert
+from .transformer.vit import vit_b16, vit_tiny
+
+_INPUT_DIMS = {"mnist": 784, "stackoverflow_lr": 10000, "synthetic_1_1": 60, "mit-bih": 187,
+               "lending_club_loan": 90, "NUS_WIDE": 1634, "UCI_SUSY": 18}
+
+
+def create(args, output_dim):
+    name = args.model
+    ds = getattr(args, "dataset", "")
+    logging.info("create_model. model_name = %s, output_dim = %s", name, output_dim)
+    if name == "lr":
+        return LogisticRegression(_INPUT_DIMS.get(ds, 28 * 28), output_dim)
+    if name == "cnn":
+        if ds in ("femnist", "fed_emnist"):
+            return CNN_DropOut(False)
+        return CNN_DropOut(output_dim == 10)
+    if name == "cnn_original":
+        return CNN_OriginalFedAvg(output_dim == 10)
+    if name in ("resnet18_gn",):
+        return resnet18_gn(num_classes=output_dim, group_norm=int(getattr(args, "group_norm_channels", 32)))
+    if name == "rnn":
+        if ds == "stackoverflow_nwp":
+            return RNN_StackOverFlow()
+        return RNN_OriginalFedAvg()
+    if name == "resnet56":
+        return resnet56(class_num=output_dim)
+    if name == "resnet110":
+        return resnet110(class_num=output_dim)
+    if name in ("resnet18", "resnet18_cifar"):
+        return resnet18_cifar(class_num=output_dim)
+    if name == "mobilenet":
+        return mobilenet(class_num=output_dim)
+    if name == "mobilenet_v3":
+        return MobileNetV3(model_mode=getattr(args, "model_mode", "LARGE"), num_classes=output_dim)
+    if name == "efficientnet":
+        return EfficientNet(num_classes=output_dim)
+    if name.startswith("vgg"):
+        return VGG(name, output_dim)
+    if name in ("distilbert", "distilbert-base-uncased"):
+        return distilbert(num_labels=output_dim, max_pos=int(getattr(args, "max_seq_len", 512)))
+    if name in ("vit", "vit_b16", "vit-b/16"):
+        return vit_b16(num_classes=output_dim, img_size=int(getattr(args, "img_size", 224)))
+    if name == "vit_tiny":
+        return vit_tiny(num_classes=output_dim)
+    if name == "gan":
+        return MNISTGAN(int(getattr(args, "nz", 100)))
+    if name == "darts":
+        return DartsNetwork(int(getattr(args, "init_channels", 8)), output_dim, int(getattr(args, "layers", 3)))
+    if name == "resnet56_gkt":
+        return resnet8_56(output_dim), resnet56_server(output_dim)
+    logging.warning("unknown model %s → LogisticRegression fallback (reference behaviour)", name)
+    return LogisticRegression(28 * 28, output_dim)

@@ -1,0 +1,40 @@
+"""Hand-written HIP/CDNA4 kernels (``csrc/*.hip``) and their PyTorch references.
+
+``fl_ops``   — aggregation (FedAvg weighted sum, MFMA subset aggregation), fused
+               multi-client SGD/Adam, FedOpt server step, robust aggregation,
+               int8/fp8 quantisation, top-k sparsification, fused CE, confusion matrix.
+``nn_ops``   — client-batched (grouped) conv / BN / ReLU / pooling / linear kernels
+               used by the virtual-client engine (MFMA implicit GEMM).
+"""
+from . import _native
+from .fl_ops import (
+    weighted_sum,
+    weighted_average,
+    subset_aggregate,
+    sgd_step,
+    adam_step,
+    fedopt_step,
+    client_sqnorm,
+    norm_diff_clip_,
+    gaussian_noise_,
+    coordinate_median,
+    quantize_int8,
+    dequantize_int8_axpy,
+    quantize_fp8,
+    dequantize_fp8_axpy,
+    topk_abs,
+    scatter_axpy,
+    softmax_xent_fwd_bwd,
+    FusedCrossEntropy,
+    confusion_matrix,
+    cast_bf16,
+    use_native,
+)
+
+
+def build(force: bool = False):
+    return _native.build(force=force)
+
+
+def native_available() -> bool:
+    return _native.available()

@@ -1,0 +1,486 @@
+"""Python entry points for the FL kernels (``csrc/fl_kernels.hip``).
+
+Dispatch: CUDA(HIP) tensors → native kernel (mandatory on GPU: raises if the
+library is missing); CPU tensors → the plain-PyTorch fp32 reference of the same
+op (also the oracle the GPU tests compare against). ``FEDML_AMD_FORCE_TORCH=1``
+forces the reference on GPU for A/B measurements only.
+"""
+import ctypes
+import os
+
+import torch
+
+from . import _native
+
+_c = ctypes
+_FORCE_TORCH = os.environ.get("FEDML_AMD_FORCE_TORCH", "0") == "1"
+_SIGS = {}
+
+
+def _p(t):
+    return None if t is None else _c.c_void_p(t.data_ptr())
+
+
+def _stream(t):
+    return _c.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def use_native(t: torch.Tensor) -> bool:
+    return t.is_cuda and not _FORCE_TORCH
+
+
+def _fn(name, restype=_c.c_int):
+    lib = _native.lib(required=True)
+    f = _SIGS.get(name)
+    if f is None:
+        f = getattr(lib, name)
+        f.restype = restype
+        _SIGS[name] = f
+    return f
+
+
+def _check(rc, name):
+    if rc != 0:
+        raise RuntimeError(f"{name} failed with HIP error {rc}")
+
+
+def _i64(v):
+    return _c.c_int64(int(v))
+
+
+def _f(v):
+    return _c.c_float(float(v))
+
+
+def _u64(v):
+    return _c.c_uint64(int(v) & ((1 << 64) - 1))
+
+
+# ----------------------------------------------------------------------------- K1
+def weighted_sum(stack: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None, beta: float = 0.0) -> torch.Tensor:
+    """out = beta*out + Σ_c w[c]·stack[c]  for a [C, P] fp32/bf16 stack (fp32 result)."""
+    assert stack.dim() == 2
+    C, P = stack.shape
+    if out is None:
+        out = torch.empty(P, dtype=torch.float32, device=stack.device)
+        beta = 0.0
+    if use_native(stack):
+        assert stack.stride(1) == 1 and stack.dtype in (torch.float32, torch.bfloat16)
+        w = w.to(device=stack.device, dtype=torch.float32).contiguous()
+        rc = _fn("fa_weighted_sum")(_p(stack), _c.c_int(stack.dtype == torch.bfloat16), _i64(stack.stride(0)),
+                                     _c.c_int(C), _p(w), _p(out), _i64(P), _f(beta), _stream(stack))
+        _check(rc, "fa_weighted_sum")
+        return out
+    res = (w.to(torch.float32).view(C, 1) * stack.to(torch.float32)).sum(0)
+    if beta != 0.0:
+        res = res + beta * out
+    out.copy_(res)
+    return out
+
+
+def weighted_average(stack: torch.Tensor, counts) -> torch.Tensor:
+    """FedAvg: Σ_c (n_c / Σn) · stack[c]."""
+    w = torch.as_tensor(counts, dtype=torch.float64)
+    w = (w / w.sum()).to(torch.float32)
+    return weighted_sum(stack, w.to(stack.device))
+
+
+def subset_aggregate(W: torch.Tensor, X: torch.Tensor) -> torch.Tensor:
+    """OUT[S, P] = W[S, C] @ X[C, P]  (exact-fp32 MFMA on GPU)."""
+    S, C = W.shape
+    P = X.shape[1]
+    if use_native(X):
+        W = W.to(device=X.device, dtype=torch.float32).contiguous()
+        X = X.to(torch.float32)
+        out = torch.zeros(S, P, dtype=torch.float32, device=X.device)
+        for c0 in range(0, C, 64):
+            c1 = min(C, c0 + 64)
+            part = out if c0 == 0 else torch.empty_like(out)
+            rc = _fn("fa_subset_aggregate")(_p(W[:, c0:c1].contiguous()), _c.c_int(S), _c.c_int(c1 - c0),
+                                             _p(X[c0:c1]), _i64(X.stride(0)), _i64(P), _p(part), _i64(P),
+                                             _stream(X))
+            _check(rc, "fa_subset_aggregate")
+            if c0:
+                out += part
+        return out
+    return W.to(torch.float32) @ X.to(torch.float32)
+
+
+# ----------------------------------------------------------------------------- K2
+def sgd_step(param, grad, lr, weight_decay=0.0, momentum=0.0, mom_buf=None, dampening=0.0, nesterov=False,
+             mu=0.0, global_ref=None, first_step=False, active=None, lr_scale=None):
+    """In-place fused SGD over a [C, P] stack (torch.optim.SGD semantics; FedProx term μ(w − w_g))."""
+    C, P = param.shape
+    if use_native(param):
+        assert param.dtype == torch.float32 and param.stride(1) == 1 and grad.stride(1) == 1
+        assert grad.stride(0) == param.stride(0)
+        rc = _fn("fa_sgd_step")(_p(param), _p(grad), _c.c_int(grad.dtype == torch.bfloat16),
+                                _p(mom_buf if momentum != 0.0 else None), _p(global_ref), _c.c_int(C), _i64(P),
+                                _i64(param.stride(0)), _f(lr), _f(weight_decay), _f(momentum), _f(dampening),
+                                _c.c_int(int(nesterov)), _f(mu), _c.c_int(int(first_step)), _p(active),
+                                _p(lr_scale), _stream(param))
+        _check(rc, "fa_sgd_step")
+        return param
+    g = grad.to(torch.float32)
+    if mu != 0.0:
+        g = g + mu * (param - global_ref.view(1, -1))
+    if weight_decay != 0.0:
+        g = g + weight_decay * param
+    d = g
+    on = torch.ones(C, 1, dtype=torch.bool) if active is None else (active.view(C, 1) > 0)
+    if momentum != 0.0:
+        nb = g if first_step else momentum * mom_buf + (1.0 - dampening) * g
+        mom_buf.copy_(torch.where(on, nb, mom_buf))
+        d = g + momentum * mom_buf if nesterov else mom_buf
+    scale = torch.ones(C, 1, dtype=torch.float32) if active is None else active.view(C, 1).to(torch.float32)
+    if lr_scale is not None:
+        scale = scale * lr_scale.view(1, 1)
+    # inactive clients are skipped entirely (their gradients may hold garbage), as in the kernel
+    param.copy_(torch.where(scale > 0, param - lr * scale * d, param))
+    return param
+
+
+def adam_step(param, grad, exp_avg, exp_avg_sq, step, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0,
+              amsgrad=False, max_exp_avg_sq=None, decoupled=False, active=None):
+    """In-place fused Adam/AMSGrad/AdamW over a [C, P] stack; ``step`` is a [C] fp32 device tensor
+    holding the (already incremented) step count of each client."""
+    C, P = param.shape
+    if use_native(param):
+        rc = _fn("fa_adam_step")(_p(param), _p(grad), _c.c_int(grad.dtype == torch.bfloat16), _p(exp_avg),
+                                 _p(exp_avg_sq), _p(max_exp_avg_sq if amsgrad else None), _p(step), _c.c_int(C),
+                                 _i64(P), _i64(param.stride(0)), _f(lr), _f(beta1), _f(beta2), _f(eps),
+                                 _f(weight_decay), _c.c_int(int(decoupled)), _p(active), _stream(param))
+        _check(rc, "fa_adam_step")
+        return param
+    g = grad.to(torch.float32)
+    t = step.view(C, 1).to(torch.float32)
+    if weight_decay != 0.0:
+        if decoupled:
+            param.mul_(1 - lr * weight_decay)
+        else:
+            g = g + weight_decay * param
+    exp_avg.mul_(beta1).add_(g, alpha=1 - beta1)
+    exp_avg_sq.mul_(beta2).addcmul_(g, g, value=1 - beta2)
+    bc1 = 1 - beta1 ** t
+    bc2 = 1 - beta2 ** t
+    if amsgrad:
+        torch.maximum(max_exp_avg_sq, exp_avg_sq, out=max_exp_avg_sq)
+        den = max_exp_avg_sq.sqrt() / bc2.sqrt() + eps
+    else:
+        den = exp_avg_sq.sqrt() / bc2.sqrt() + eps
+    upd = (lr / bc1) * exp_avg / den
+    if active is not None:
+        upd = upd * active.view(C, 1)
+    param.sub_(upd)
+    return param
+
+
+# ----------------------------------------------------------------------------- K10
+_FEDOPT_IDS = {"sgd": 0, "fedavgm": 0, "adam": 1, "fedadam": 1, "yogi": 2, "fedyogi": 2, "adagrad": 3,
+               "fedadagrad": 3}
+
+
+def fedopt_step(stack, w, glob, opt="sgd", lr=1.0, beta1=0.9, beta2=0.99, eps=1e-3, momentum=0.0, nesterov=False,
+                state1=None, state2=None, step=1, first_step=False):
+    """Fused FedOpt server update: avg = Σ w_c stack_c; g = glob − avg; glob ← ServerOpt(glob, g)."""
+    C, P = stack.shape
+    oid = _FEDOPT_IDS[opt.lower()]
+    bc1 = 1 - beta1 ** step
+    bc2 = 1 - beta2 ** step
+    if use_native(stack):
+        w = w.to(device=stack.device, dtype=torch.float32).contiguous()
+        rc = _fn("fa_fedopt_step")(_p(stack), _i64(stack.stride(0)), _c.c_int(C), _p(w), _p(glob), _p(state1),
+                                   _p(state2), _i64(P), _c.c_int(oid), _f(lr), _f(beta1), _f(beta2), _f(eps),
+                                   _f(bc1), _f(bc2), _f(momentum), _c.c_int(int(nesterov)),
+                                   _c.c_int(int(first_step)), _stream(stack))
+        _check(rc, "fa_fedopt_step")
+        return glob
+    avg = (w.view(C, 1).to(torch.float32) * stack).sum(0)
+    g = glob - avg
+    if oid == 0:
+        d = g
+        if momentum != 0.0:
+            if first_step:
+                state1.copy_(g)
+            else:
+                state1.mul_(momentum).add_(g)
+            d = g + momentum * state1 if nesterov else state1
+        glob.sub_(lr * d)
+    elif oid in (1, 2):
+        state1.mul_(beta1).add_(g, alpha=1 - beta1)
+        if oid == 1:
+            state2.mul_(beta2).addcmul_(g, g, value=1 - beta2)
+        else:
+            g2 = g * g
+            sgn = torch.where(state2 - g2 < 0, -torch.ones_like(g2), torch.ones_like(g2))
+            state2.sub_((1 - beta2) * g2 * sgn)
+        glob.sub_(lr * (state1 / bc1) / ((state2.clamp_min(0) / bc2).sqrt() + eps))
+    else:
+        state2.add_(g * g)
+        glob.sub_(lr * g / (state2.sqrt() + eps))
+    return glob
+
+
+# ----------------------------------------------------------------------------- K9
+def client_sqnorm(stack, ref=None, mask=None):
+    """[C] squared L2 norms of (stack_c − ref) over the masked coordinates (deterministic)."""
+    C, P = stack.shape
+    if use_native(stack):
+        out = torch.empty(C, dtype=torch.float32, device=stack.device)
+        partial = torch.empty(C * 64, dtype=torch.float32, device=stack.device)
+        rc = _fn("fa_client_sqnorm")(_p(stack), _i64(stack.stride(0)), _c.c_int(C), _p(ref), _p(mask), _i64(P),
+                                     _p(partial), _p(out), _stream(stack))
+        _check(rc, "fa_client_sqnorm")
+        return out
+    d = stack - (ref.view(1, -1) if ref is not None else 0.0)
+    if mask is not None:
+        d = d * mask.view(1, -1).to(d.dtype)
+    return (d.double() ** 2).sum(1).to(torch.float32)
+
+
+def norm_diff_clip_(stack, ref, bound, mask=None, sqnorm=None):
+    """stack_c ← ref + (stack_c − ref) / max(1, ‖stack_c − ref‖ / bound)  (in place)."""
+    C, P = stack.shape
+    if sqnorm is None:
+        sqnorm = client_sqnorm(stack, ref, mask)
+    if use_native(stack):
+        rc = _fn("fa_norm_clip")(_p(stack), _i64(stack.stride(0)), _c.c_int(C), _p(ref), _p(mask), _p(sqnorm),
+                                 _i64(P), _f(bound), _stream(stack))
+        _check(rc, "fa_norm_clip")
+        return stack
+    scale = 1.0 / torch.clamp(sqnorm.sqrt() / bound, min=1.0)
+    r = ref.view(1, -1) if ref is not None else torch.zeros(1, P, dtype=stack.dtype)
+    new = r + (stack - r) * scale.view(C, 1)
+    if mask is not None:
+        m = mask.view(1, -1).bool()
+        new = torch.where(m, new, stack)
+    stack.copy_(new)
+    return stack
+
+
+def gaussian_noise_(x, stddev, seed=0, offset=0, mask=None):
+    """x += stddev·N(0,1) (counter-based Philox on GPU; torch generator on CPU)."""
+    if use_native(x):
+        assert x.is_contiguous() and x.dtype == torch.float32
+        rc = _fn("fa_gaussian_noise")(_p(x), _p(mask), _i64(x.numel()), _f(stddev), _u64(seed), _u64(offset),
+                                      _stream(x))
+        _check(rc, "fa_gaussian_noise")
+        return x
+    g = torch.Generator().manual_seed(int(seed) + int(offset))
+    noise = torch.randn(x.shape, generator=g, dtype=torch.float32) * stddev
+    if mask is not None:
+        noise = noise * mask.view(x.shape).to(noise.dtype)
+    x.add_(noise)
+    return x
+
+
+def coordinate_median(stack):
+    """Coordinate-wise (lower) median over clients: [C, P] → [P]."""
+    C, P = stack.shape
+    if use_native(stack) and C <= 64:
+        out = torch.empty(P, dtype=torch.float32, device=stack.device)
+        rc = _fn("fa_coordinate_median")(_p(stack), _i64(stack.stride(0)), _c.c_int(C), _i64(P), _p(out),
+                                         _stream(stack))
+        _check(rc, "fa_coordinate_median")
+        return out
+    return torch.median(stack.to(torch.float32), dim=0).values
+
+
+# ----------------------------------------------------------------------------- K15
+def quantize_int8(x, residual=None, stochastic=True, seed=0):
+    """Block-256 int8 quantisation with optional stochastic rounding and error feedback.
+    Returns (q int8 [n], scales f32 [ceil(n/256)]); ``residual`` (if given) is updated to x+r−deq."""
+    n = x.numel()
+    nb = (n + 255) // 256
+    if use_native(x):
+        q = torch.empty(n, dtype=torch.int8, device=x.device)
+        s = torch.empty(nb, dtype=torch.float32, device=x.device)
+        rc = _fn("fa_quant_int8")(_p(x), _p(residual), _p(q), _p(s), _i64(n), _c.c_int(int(stochastic)), _u64(seed),
+                                  _stream(x))
+        _check(rc, "fa_quant_int8")
+        return q, s
+    v = x.reshape(-1).to(torch.float32) + (residual.reshape(-1) if residual is not None else 0.0)
+    pad = nb * 256 - n
+    vp = torch.nn.functional.pad(v, (0, pad)).view(nb, 256)
+    amax = vp.abs().amax(1)
+    scale = torch.where(amax > 0, amax / 127.0, torch.ones_like(amax))
+    t = vp / scale.view(-1, 1)
+    if stochastic:
+        g = torch.Generator().manual_seed(int(seed))
+        t = torch.floor(t + torch.rand(t.shape, generator=g))
+    else:
+        t = torch.round(t)
+    t = t.clamp(-127, 127)
+    q = t.reshape(-1)[:n].to(torch.int8)
+    if residual is not None:
+        residual.copy_((v - (t * scale.view(-1, 1)).reshape(-1)[:n]).view_as(residual))
+    return q, scale
+
+
+def dequantize_int8_axpy(q, scales, w, acc):
+    """acc += w · dequant(q)."""
+    n = q.numel()
+    if use_native(acc):
+        rc = _fn("fa_dequant_int8_axpy")(_p(q), _p(scales), _f(w), _p(acc), _i64(n), _stream(acc))
+        _check(rc, "fa_dequant_int8_axpy")
+        return acc
+    s = scales.repeat_interleave(256)[:n]
+    acc.add_(w * q.to(torch.float32) * s)
+    return acc
+
+
+def quantize_fp8(x, residual=None):
+    """Block-256 OCP fp8 e4m3fn quantisation (+ optional error feedback). Returns (q uint8, scales)."""
+    n = x.numel()
+    nb = (n + 255) // 256
+    if use_native(x):
+        q = torch.empty(n, dtype=torch.uint8, device=x.device)
+        s = torch.empty(nb, dtype=torch.float32, device=x.device)
+        rc = _fn("fa_quant_fp8")(_p(x), _p(residual), _p(q), _p(s), _i64(n), _stream(x))
+        _check(rc, "fa_quant_fp8")
+        return q, s
+    v = x.reshape(-1).to(torch.float32) + (residual.reshape(-1) if residual is not None else 0.0)
+    pad = nb * 256 - n
+    vp = torch.nn.functional.pad(v, (0, pad)).view(nb, 256)
+    amax = vp.abs().amax(1)
+    scale = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
+    t = (vp / scale.view(-1, 1)).clamp(-448, 448).to(torch.float8_e4m3fn)
+    q = t.reshape(-1)[:n].view(torch.uint8)
+    if residual is not None:
+        back = t.to(torch.float32) * scale.view(-1, 1)
+        residual.copy_((v - back.reshape(-1)[:n]).view_as(residual))
+    return q, scale
+
+
+def dequantize_fp8_axpy(q, scales, w, acc):
+    n = q.numel()
+    if use_native(acc):
+        rc = _fn("fa_dequant_fp8_axpy")(_p(q), _p(scales), _f(w), _p(acc), _i64(n), _stream(acc))
+        _check(rc, "fa_dequant_fp8_axpy")
+        return acc
+    s = scales.repeat_interleave(256)[:n]
+    acc.add_(w * q.view(torch.float8_e4m3fn).to(torch.float32) * s)
+    return acc
+
+
+class _TopkScratch:
+    cache = {}
+
+    @classmethod
+    def get(cls, device):
+        key = str(device)
+        if key not in cls.cache:
+            cls.cache[key] = (torch.zeros(8, dtype=torch.int32, device=device),
+                              torch.zeros(2048, dtype=torch.int32, device=device))
+        return cls.cache[key]
+
+
+def topk_abs(x, k, residual=None):
+    """Exact top-k of |x| (radix select on device). Returns (idx int32 [k], val f32 [k]) — order unspecified.
+    ``residual`` (if given) receives x with the selected entries zeroed (error feedback)."""
+    n = x.numel()
+    k = int(min(max(k, 1), n))
+    xf = x.reshape(-1)
+    if use_native(x):
+        idx = torch.empty(k, dtype=torch.int32, device=x.device)
+        val = torch.empty(k, dtype=torch.float32, device=x.device)
+        state, hist = _TopkScratch.get(x.device)
+        rc = _fn("fa_topk_abs")(_p(xf), _i64(n), _i64(k), _p(state), _p(hist), _p(idx), _p(val),
+                                _p(residual.reshape(-1) if residual is not None else None), _stream(x))
+        _check(rc, "fa_topk_abs")
+        return idx, val
+    _, i = torch.topk(xf.abs(), k)
+    val = xf[i].to(torch.float32)
+    if residual is not None:
+        r = xf.to(torch.float32).clone()
+        r[i] = 0.0
+        residual.copy_(r.view_as(residual))
+    return i.to(torch.int32), val
+
+
+def scatter_axpy(idx, val, w, acc):
+    """acc[idx] += w · val (indices unique within one call)."""
+    if use_native(acc):
+        rc = _fn("fa_scatter_axpy")(_p(idx), _p(val), _i64(idx.numel()), _f(w), _p(acc), _stream(acc))
+        _check(rc, "fa_scatter_axpy")
+        return acc
+    acc.index_add_(0, idx.long(), w * val.to(acc.dtype))
+    return acc
+
+
+# ----------------------------------------------------------------------------- K7
+def softmax_xent_fwd_bwd(logits, labels, class_weight=None, row_scale=None, ignore_index=-100, need_grad=True):
+    """Fused per-row CE: returns (loss_rows [R], dlogits [R, K] or None) where
+    dlogits = cw[y]·row_scale·(softmax − onehot)."""
+    R, K = logits.shape
+    if use_native(logits):
+        assert logits.is_contiguous() and logits.dtype in (torch.float32, torch.bfloat16)
+        loss = torch.empty(R, dtype=torch.float32, device=logits.device)
+        dz = torch.empty_like(logits) if need_grad else None
+        lab = labels.to(torch.int64).contiguous()
+        rc = _fn("fa_softmax_xent")(_p(logits), _c.c_int(logits.dtype == torch.bfloat16), _p(lab),
+                                    _p(class_weight), _p(row_scale), _p(dz), _p(loss), _i64(R), _c.c_int(K),
+                                    _i64(ignore_index), _stream(logits))
+        _check(rc, "fa_softmax_xent")
+        return loss, dz
+    z = logits.to(torch.float32)
+    lab = labels.to(torch.int64)
+    ign = (lab == ignore_index) | (lab < 0) | (lab >= K)
+    safe = lab.clamp(0, K - 1)
+    lse = torch.logsumexp(z, 1)
+    cw = class_weight[safe] if class_weight is not None else torch.ones(R)
+    cw = torch.where(ign, torch.zeros_like(cw), cw)
+    loss = cw * (lse - z.gather(1, safe.view(-1, 1)).squeeze(1))
+    dz = None
+    if need_grad:
+        p = torch.softmax(z, 1)
+        p[torch.arange(R), safe] -= 1.0
+        rs = row_scale if row_scale is not None else torch.ones(R)
+        dz = (p * (cw * rs).view(-1, 1)).to(logits.dtype)
+    return loss, dz
+
+
+class FusedCrossEntropy(torch.autograd.Function):
+    """Autograd wrapper: mean CE per group of rows (per virtual client) summed over groups."""
+
+    @staticmethod
+    def forward(ctx, logits, labels, row_scale, class_weight):
+        loss_rows, dz = softmax_xent_fwd_bwd(logits, labels, class_weight, row_scale, need_grad=True)
+        ctx.save_for_backward(dz)
+        return (loss_rows * row_scale).sum()
+
+    @staticmethod
+    def backward(ctx, g):
+        (dz,) = ctx.saved_tensors
+        return dz * g.to(dz.dtype), None, None, None
+
+
+# ----------------------------------------------------------------------------- K8
+def confusion_matrix(logits, labels, num_groups=1, rows_per_group=None):
+    """[G, K, K] int32 counts of (label, argmax) per group of rows."""
+    R, K = logits.shape
+    rpg = rows_per_group or max(1, R // max(1, num_groups))
+    if use_native(logits):
+        cm = torch.zeros(num_groups, K, K, dtype=torch.int32, device=logits.device)
+        rc = _fn("fa_confusion")(_p(logits.contiguous()), _c.c_int(logits.dtype == torch.bfloat16),
+                                 _p(labels.to(torch.int64).contiguous()), _p(cm), _i64(R), _c.c_int(K), _i64(rpg),
+                                 _stream(logits))
+        _check(rc, "fa_confusion")
+        return cm
+    pred = logits.to(torch.float32).argmax(1)
+    g = torch.arange(R) // rpg
+    flat = (g * K + labels.long()) * K + pred
+    return torch.bincount(flat, minlength=num_groups * K * K).view(num_groups, K, K).to(torch.int32)
+
+
+def cast_bf16(x, out=None):
+    if use_native(x):
+        out = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device) if out is None else out
+        rc = _fn("fa_cast_bf16")(_p(x), _p(out), _i64(x.numel()), _stream(x))
+        _check(rc, "fa_cast_bf16")
+        return out
+    r = x.to(torch.bfloat16)
+    if out is not None:
+        out.copy_(r)
+        return out
+    return r

@@ -1,0 +1,323 @@
+"""Client-batched ("virtual clients as a batch dimension") execution of a single-client model.
+
+C clients that each own a private copy of the same architecture are run as ONE
+program: activations use a *client-stacked channel* layout ``[B, C·F, ...]``
+(client-major inside the channel dimension), so
+
+* conv2d      → one grouped conv with ``groups = C·g`` and weights ``[C·Cout, Cin/g, k, k]``
+* batch norm  → one per-(client, channel) normalisation (stats are per client by construction)
+* linear      → one batched GEMM ``[C, B, in] × [C, in, out]``
+* elementwise / pooling → unchanged
+
+The single-client model is traced once with ``torch.fx``; the interpreter
+below replays the graph with these batched ops. Parameters are zero-copy views
+into the flat client-stack arena ``[C, P]`` and gradients land directly in the
+gradient arena (``p.grad`` pre-assigned to arena views, accumulated in place),
+so the fused multi-client optimizer kernel consumes them without any copy.
+
+On the GPU the conv / BN / ReLU / linear / loss ops dispatch to the HIP
+kernels in ``ops.nn_ops`` when those support the shape; the torch ops here are
+the reference semantics (and the CPU path).
+"""
+import operator
+from typing import Dict, Optional
+
+import torch
+import torch.fx as fx
+import torch.nn as nn
+import torch.nn.functional as F
+
+SUPPORTED_MODULES = (nn.Conv2d, nn.BatchNorm2d, nn.Linear, nn.ReLU, nn.Sigmoid, nn.Tanh, nn.MaxPool2d, nn.AvgPool2d,
+                     nn.AdaptiveAvgPool2d, nn.Flatten, nn.Dropout, nn.Identity, nn.GroupNorm, nn.LeakyReLU)
+
+
+class UnsupportedForBatching(Exception):
+    pass
+
+
+class _Tracer(fx.Tracer):
+    def is_leaf_module(self, m, qualname):
+        return isinstance(m, SUPPORTED_MODULES) or super().is_leaf_module(m, qualname)
+
+
+def trace(model: nn.Module) -> fx.GraphModule:
+    try:
+        graph = _Tracer().trace(model)
+    except Exception as e:  # data-dependent control flow etc.
+        raise UnsupportedForBatching(f"fx trace failed: {e}")
+    gm = fx.GraphModule(model, graph)
+    for n in gm.graph.nodes:
+        if n.op == "call_module":
+            m = gm.get_submodule(n.target)
+            if not isinstance(m, SUPPORTED_MODULES):
+                raise UnsupportedForBatching(f"module {type(m).__name__} at {n.target}")
+    return gm
+
+
+# ------------------------------------------------------------------------------------------------
+# batched primitives (torch reference semantics)
+# ------------------------------------------------------------------------------------------------
+def bconv2d(x, w, b, C, stride, padding, dilation, groups):
+    """x [B, C·Cin, H, W]; w [C, Cout, Cin/g, k, k]; b [C, Cout] or None."""
+    cout = w.shape[1]
+    wf = w.reshape(C * cout, *w.shape[2:])
+    bf = b.reshape(C * cout) if b is not None else None
+    return F.conv2d(x, wf, bf, stride, padding, dilation, groups * C)
+
+
+@torch.no_grad()
+def apply_bn_update(running_mean, running_var, nbt, mean, var_b, n, momentum, active):
+    C = mean.shape[0]
+    unb = var_b * (n / (n - 1).clamp_min(1.0))
+    a = torch.ones(C, 1, device=mean.device) if active is None else active.view(C, 1).to(mean.dtype)
+    on = a > 0
+    new_m = (1 - momentum) * running_mean + momentum * mean.to(running_mean.dtype)
+    new_v = (1 - momentum) * running_var + momentum * unb.to(running_var.dtype)
+    running_mean.copy_(torch.where(on, new_m, running_mean))
+    running_var.copy_(torch.where(on, new_v, running_var))
+    if nbt is not None:
+        nbt.add_(a.view(nbt.shape).to(nbt.dtype))
+
+
+def bbatch_norm(x, C, weight, bias, running_mean, running_var, training, momentum, eps, sample_mask=None,
+                active=None, nbt=None, deferred=None):
+    """Per-(client, channel) batch norm on x [B, C·Ch, ...].
+
+    running_mean/var are [C, Ch] (strided arena views, updated in place for active clients only);
+    ``sample_mask`` [B, C] excludes padded samples from the statistics (exact semantics for
+    clients whose last batch is shorter)."""
+    B = x.shape[0]
+    ch = x.shape[1] // C
+    if not training:
+        rm = running_mean.reshape(C * ch)
+        rv = running_var.reshape(C * ch)
+        return F.batch_norm(x, rm, rv, weight.reshape(-1) if weight is not None else None,
+                            bias.reshape(-1) if bias is not None else None, False, 0.0, eps)
+    spatial = x.shape[2:]
+    if sample_mask is None:
+        out, mean, invstd = torch.ops.aten.native_batch_norm(
+            x, weight.reshape(-1) if weight is not None else None, bias.reshape(-1) if bias is not None else None,
+            None, None, True, 0.0, eps)[:3]
+        hw = 1
+        for d in spatial:
+            hw *= int(d)
+        n = torch.full((C, 1), float(B * hw), device=x.device)
+        mean = mean.view(C, ch)
+        var_b = (1.0 / (invstd.view(C, ch) ** 2)) - eps
+    else:
+        xs = x.view(B, C, ch, *spatial)
+        m = sample_mask.view(B, C, 1, *([1] * len(spatial))).to(x.dtype)
+        red = [0] + list(range(3, 3 + len(spatial)))
+        hw = 1
+        for d in spatial:
+            hw *= int(d)
+        cnt = m.sum(red, keepdim=True) * hw
+        empty = cnt == 0
+        cnt = cnt.clamp_min(1.0)
+        mu = (xs * m).sum(red, keepdim=True) / cnt
+        var = ((xs - mu) ** 2 * m).sum(red, keepdim=True) / cnt
+        # an inactive client (no samples this step) gets an identity normalisation so its
+        # (discarded) activations stay finite
+        var = torch.where(empty, torch.ones_like(var), var)
+        xh = (xs - mu) * torch.rsqrt(var + eps)
+        if weight is not None:
+            xh = xh * weight.view(1, C, ch, *([1] * len(spatial))) + bias.view(1, C, ch, *([1] * len(spatial)))
+        out = xh.reshape(x.shape)
+        mean = mu.detach().view(C, ch)
+        var_b = var.detach().view(C, ch)
+        n = cnt.view(C, 1)
+    if running_mean is not None:
+        upd = (running_mean, running_var, nbt, mean.detach(), var_b.detach(), n, momentum, active)
+        if deferred is not None:
+            deferred.append(upd)   # applied after backward: the buffers share storage with the weights
+        else:
+            apply_bn_update(*upd)
+    return out
+
+
+def bgroup_norm(x, C, groups, weight, bias, eps):
+    B = x.shape[0]
+    ch = x.shape[1] // C
+    out = F.group_norm(x.reshape(B * C, ch, *x.shape[2:]), groups, None, None, eps).reshape(x.shape)
+    if weight is not None:
+        shape = (1, C * ch) + (1,) * (x.dim() - 2)
+        out = out * weight.reshape(shape) + bias.reshape(shape)
+    return out
+
+
+def blinear(x, w, b, C):
+    """x [B, C·in] (or [B, ..., C·in] for sequence inputs); w [C, out, in]; b [C, out] → [B, C·out]."""
+    lead = x.shape[:-1]
+    fin = x.shape[-1] // C
+    xx = x.reshape(-1, C, fin).transpose(0, 1)           # [C, N, in]
+    if b is not None:
+        y = torch.baddbmm(b.unsqueeze(1), xx, w.transpose(1, 2))
+    else:
+        y = torch.bmm(xx, w.transpose(1, 2))
+    return y.transpose(0, 1).reshape(*lead, C * w.shape[1])
+
+
+# ------------------------------------------------------------------------------------------------
+class BatchedInterpreter:
+    """Replays an fx graph of a single-client model for C clients at once."""
+
+    def __init__(self, model: nn.Module, layout, C: int):
+        self.template = model
+        self.gm = trace(model)
+        self.layout = layout
+        self.C = C
+        self.modules = dict(self.gm.named_modules())
+        self.native = None  # set by the engine: ops.nn_ops-backed fast path
+        self.deferred = []  # BN running-stat updates, applied after backward by ``flush_deferred``
+        for n in self.gm.graph.nodes:
+            if n.op == "call_function" and n.target in (torch.cat, torch.stack):
+                raise UnsupportedForBatching("channel concatenation is not client-stackable")
+
+    def flush_deferred(self):
+        for upd in self.deferred:
+            apply_bn_update(*upd)
+        self.deferred.clear()
+
+    def _p(self, params: Dict[str, torch.Tensor], name: str) -> Optional[torch.Tensor]:
+        return params.get(name)
+
+    def run(self, params: Dict[str, torch.Tensor], x: torch.Tensor, training: bool = True, sample_mask=None,
+            active=None, dtype=None):
+        """params: key → [C, *shape] view; x: [C, B, *in] → returns [C, B, *out]."""
+        C = self.C
+        B = x.shape[1]
+        # to client-stacked layout [B, C·F, ...]
+        if x.dim() >= 3:
+            h = x.transpose(0, 1).reshape(B, C * x.shape[2], *x.shape[3:])
+        else:
+            h = x.transpose(0, 1).reshape(B, C)
+        if dtype is not None and h.is_floating_point():
+            h = h.to(dtype)
+        env = {}
+        for node in self.gm.graph.nodes:
+            if node.op == "placeholder":
+                env[node.name] = h
+                continue
+            if node.op == "output":
+                out = env[node.args[0].name] if isinstance(node.args[0], fx.Node) else node.args[0]
+                if isinstance(out, tuple):
+                    out = out[-1]
+                # back to [C, B, ...]
+                if out.dim() == 2:
+                    return out.view(B, C, -1).transpose(0, 1)
+                return out.view(B, C, out.shape[1] // C, *out.shape[2:]).transpose(0, 1)
+            args = fx.node.map_arg(node.args, lambda n: env[n.name])
+            kwargs = fx.node.map_arg(node.kwargs, lambda n: env[n.name])
+            if node.op == "call_module":
+                env[node.name] = self._call_module(node.target, self.modules[node.target], args, params, training,
+                                                   sample_mask, active)
+            elif node.op == "call_function":
+                env[node.name] = self._call_function(node.target, args, kwargs)
+            elif node.op == "call_method":
+                env[node.name] = self._call_method(node.target, args, kwargs)
+            elif node.op == "get_attr":
+                raise UnsupportedForBatching(f"get_attr {node.target}")
+        raise RuntimeError("graph has no output")
+
+    # ---- node handlers ---------------------------------------------------------------------------
+    def _call_module(self, name, m, args, params, training, sample_mask, active):
+        x = args[0]
+        C = self.C
+        nat = self.native
+        if isinstance(m, nn.Conv2d):
+            w = params[f"{name}.weight"]
+            b = params.get(f"{name}.bias")
+            if w.dtype != x.dtype:
+                w = w.to(x.dtype)
+                b = b.to(x.dtype) if b is not None else None
+            if nat is not None and nat.supports_conv(m, x):
+                return nat.conv2d(x, w, b, C, m)
+            return bconv2d(x, w, b, C, m.stride, m.padding, m.dilation, m.groups)
+        if isinstance(m, nn.BatchNorm2d):
+            rm = params.get(f"{name}.running_mean")
+            rv = params.get(f"{name}.running_var")
+            nbt = params.get(f"{name}.num_batches_tracked")
+            w = params.get(f"{name}.weight")
+            b = params.get(f"{name}.bias")
+            use_batch = training or not m.track_running_stats
+            mom = m.momentum if m.momentum is not None else 0.1
+            return bbatch_norm(x, C, w, b, rm, rv, use_batch, mom, m.eps, sample_mask, active, nbt,
+                               deferred=self.deferred if training else None)
+        if isinstance(m, nn.GroupNorm):
+            return bgroup_norm(x, C, m.num_groups, params.get(f"{name}.weight"), params.get(f"{name}.bias"), m.eps)
+        if isinstance(m, nn.Linear):
+            w = params[f"{name}.weight"]
+            b = params.get(f"{name}.bias")
+            if w.dtype != x.dtype:
+                w = w.to(x.dtype)
+                b = b.to(x.dtype) if b is not None else None
+            return blinear(x, w, b, C)
+        if isinstance(m, nn.ReLU):
+            return F.relu(x)
+        if isinstance(m, nn.LeakyReLU):
+            return F.leaky_relu(x, m.negative_slope)
+        if isinstance(m, nn.Sigmoid):
+            return torch.sigmoid(x)
+        if isinstance(m, nn.Tanh):
+            return torch.tanh(x)
+        if isinstance(m, nn.MaxPool2d):
+            return F.max_pool2d(x, m.kernel_size, m.stride, m.padding, m.dilation, m.ceil_mode)
+        if isinstance(m, nn.AvgPool2d):
+            return F.avg_pool2d(x, m.kernel_size, m.stride, m.padding, m.ceil_mode, m.count_include_pad)
+        if isinstance(m, nn.AdaptiveAvgPool2d):
+            return F.adaptive_avg_pool2d(x, m.output_size)
+        if isinstance(m, nn.Flatten):
+            return torch.flatten(x, m.start_dim, m.end_dim)
+        if isinstance(m, nn.Dropout):
+            return F.dropout(x, m.p, training)
+        if isinstance(m, nn.Identity):
+            return x
+        raise UnsupportedForBatching(type(m).__name__)
+
+    def _call_function(self, fn, args, kwargs):
+        if fn in (operator.add, torch.add, operator.iadd):
+            return args[0] + args[1]
+        if fn in (operator.mul, torch.mul):
+            return args[0] * args[1]
+        if fn in (F.relu, torch.relu):
+            return F.relu(args[0])
+        if fn in (torch.sigmoid, F.sigmoid):
+            return torch.sigmoid(args[0])
+        if fn is torch.flatten:
+            return torch.flatten(*args, **kwargs)
+        if fn is F.adaptive_avg_pool2d:
+            return F.adaptive_avg_pool2d(*args, **kwargs)
+        if fn is F.max_pool2d:
+            return F.max_pool2d(*args, **kwargs)
+        if fn is operator.getitem:
+            if isinstance(args[0], torch.Size) and args[1] != 0:
+                raise UnsupportedForBatching("only the batch dimension of .shape is client-invariant")
+            return args[0][args[1]]
+        if fn is getattr and args[1] == "shape":
+            return args[0].shape
+        raise UnsupportedForBatching(f"function {getattr(fn, '__name__', fn)}")
+
+    def _call_method(self, name, args, kwargs):
+        x = args[0]
+        if name in ("view", "reshape"):
+            shape = list(args[1:]) if not isinstance(args[1], (tuple, list)) else list(args[1])
+            # batch-preserving reshapes are client-stackable: per-client (B, d1, d2, ...) is
+            # (B, C·d1, d2, ...) in the client-major stacked layout
+            B = x.shape[0]
+            if len(shape) >= 2 and shape[0] in (-1, B):
+                d1 = shape[1]
+                return x.reshape(B, -1 if d1 == -1 else self.C * d1, *shape[2:])
+            raise UnsupportedForBatching(f"{name}{tuple(shape)}")
+        if name == "size":
+            return x.size(*args[1:])
+        if name == "flatten":
+            return x.flatten(*args[1:], **kwargs)
+        if name in ("relu", "sigmoid", "tanh", "contiguous", "float"):
+            return getattr(x, name)()
+        raise UnsupportedForBatching(f"method {name}")
+
+
+import warnings as _warnings
+
+# grads are pre-assigned strided views into the [C, P] gradient arena on purpose
+_warnings.filterwarnings("ignore", message="grad and param do not obey the gradient layout contract")

@@ -1,0 +1,188 @@
+"""Virtual-client engine: local training of C clients on one GPU as one batched program.
+
+State lives in flat arenas (``core.arena``):
+    params [C, P] fp32 master weights (+ BN running stats / counters)
+    grads  [C, P] fp32, filled in place by backward
+    mom    [C, P] SGD momentum (or Adam moments)
+One local step = gather C mini-batches from the HBM data store → client-batched
+forward (``parallel.batched_nn``; HIP kernels on GPU) → fused per-client
+cross-entropy → backward → one fused multi-client optimizer kernel.
+Clients whose data ran out (heterogeneous partitions) are masked with an
+``active`` vector; short last batches use masked (exact) batch-norm statistics.
+After local training, ``partial_sum`` emits Σ_c n_c·w_c (+ Σ n_c) for the RCCL
+all-reduce.
+"""
+import logging
+import math
+from typing import List, Optional
+
+import torch
+
+from ... import ops
+from ...core.arena import ParamLayout
+from ...parallel.batched_nn import BatchedInterpreter, UnsupportedForBatching
+
+
+class ClientBatchEngine:
+    def __init__(self, model: torch.nn.Module, C: int, device, args, compute_dtype: Optional[torch.dtype] = None):
+        self.C = int(C)
+        self.device = torch.device(device)
+        self.args = args
+        self.model = model
+        self.layout = ParamLayout.from_module(model)
+        self.P = self.layout.size
+        self.compute_dtype = compute_dtype
+        self.params = self.layout.alloc_stack(self.C, self.device)
+        self.grads = self.layout.alloc_stack(self.C, self.device)
+        opt = str(getattr(args, "client_optimizer", "sgd")).lower()
+        self.optimizer = opt
+        self.momentum = float(getattr(args, "momentum", 0.0) or 0.0)
+        self.weight_decay = float(getattr(args, "weight_decay", 0.0) or 0.0)
+        self.sgd_wd = bool(getattr(args, "sgd_weight_decay", False))
+        self.mu = float(getattr(args, "fedprox_mu", getattr(args, "mu", 0.0)) or 0.0) if \
+            str(getattr(args, "federated_optimizer", "")) == "FedProx" else 0.0
+        self.mom = self.layout.alloc_stack(self.C, self.device) if (opt == "sgd" and self.momentum) else None
+        if opt != "sgd":
+            self.m1 = self.layout.alloc_stack(self.C, self.device)
+            self.m2 = self.layout.alloc_stack(self.C, self.device)
+            self.vmax = self.layout.alloc_stack(self.C, self.device) if opt in ("adam", "amsgrad") else None
+            self.step_t = torch.zeros(self.C, dtype=torch.float32, device=self.device)
+        self.interp = BatchedInterpreter(model, self.layout, self.C)
+        self.native = None
+        if self.device.type == "cuda":
+            try:
+                from ...ops import nn_ops
+                self.native = nn_ops.NativeBatchedOps(self.C, self.compute_dtype)
+                self.interp.native = self.native
+            except (ImportError, AttributeError):
+                self.native = None
+        self._build_views()
+        self.global_ref = None
+        self.loss_history: List[float] = []
+
+    # ------------------------------------------------------------------------------------------
+    def _build_views(self):
+        self.views = {}
+        for s in self.layout.slots:
+            v = self.params[:, s.offset:s.offset + s.numel].view(self.C, *s.shape)
+            if s.trainable:
+                v = v.detach().requires_grad_(True)
+                v.grad = self.grads[:, s.offset:s.offset + s.numel].view(self.C, *s.shape)
+            self.views[s.key] = v
+
+    def load_global(self, flat: torch.Tensor):
+        with torch.no_grad():
+            self.params.copy_(flat.view(1, -1).expand(self.C, -1))
+        if self.mu:
+            self.global_ref = flat
+
+    def set_client_params(self, slot: int, flat: torch.Tensor):
+        with torch.no_grad():
+            self.params[slot].copy_(flat)
+
+    # ------------------------------------------------------------------------------------------
+    def train(self, store, slots: torch.Tensor, epochs: int, batch_size: int, lr: float,
+              generator: Optional[torch.Generator] = None, shuffle: bool = True, valid_slots: Optional[torch.Tensor] = None,
+              loss_scale_by_count: bool = True):
+        """Run local training for the C client slots (indices into ``store``).
+
+        ``valid_slots`` [C] bool marks real clients (padding slots are never active)."""
+        C = self.C
+        counts = store.counts[slots].clone()
+        if valid_slots is not None:
+            counts = torch.where(valid_slots, counts, torch.zeros_like(counts))
+        counts_h = counts.tolist()
+        n_max = max(1, max(counts_h))
+        steps_per_epoch = math.ceil(n_max / batch_size)
+        use_native_loss = self.device.type == "cuda"
+        first = True
+        if self.optimizer != "sgd":
+            self.m1.zero_()
+            self.m2.zero_()
+            if self.vmax is not None:
+                self.vmax.zero_()
+            self.step_t.zero_()
+        total_loss = torch.zeros((), device=self.device)
+        n_steps = 0
+        for ep in range(int(epochs)):
+            order = store.epoch_order(slots, n_max, generator, shuffle)
+            for s in range(steps_per_epoch):
+                lo = s * batch_size
+                b_c = [max(0, min(batch_size, n - lo)) for n in counts_h]
+                bmax = max(b_c)
+                if bmax == 0:
+                    break
+                active_list = [1.0 if b > 0 else 0.0 for b in b_c]
+                uniform = all(b == bmax for b in b_c)
+                idx = order[:, lo:lo + bmax]
+                x, y, mask = store.gather(idx)
+                active = torch.tensor(active_list, dtype=torch.float32, device=self.device)
+                sample_mask = None if uniform else mask.t().contiguous()     # [B, C]
+                loss = self._step_loss(x, y, mask, b_c, active, sample_mask, use_native_loss)
+                total_loss += loss.detach()
+                n_steps += 1
+                self._optimizer_step(lr, active, first)
+                first = False
+        n_real = max(1, sum(1 for n in counts_h if n > 0))
+        self.last_loss = total_loss / max(1, n_steps * n_real)   # device scalar: no host sync here
+        return self.last_loss
+
+    def _step_loss(self, x, y, mask, b_c, active, sample_mask, use_native_loss):
+        self.grads.zero_()
+        out = self.interp.run(self.views, x, training=True, sample_mask=sample_mask, active=active,
+                              dtype=self.compute_dtype)                       # [C, B, K]
+        C, B = out.shape[0], out.shape[1]
+        logits = out.reshape(C * B, -1)
+        if not logits.is_contiguous():
+            logits = logits.contiguous()
+        labels = y.reshape(C * B)
+        bc = torch.tensor([max(1, b) for b in b_c], dtype=torch.float32, device=self.device)
+        row_scale = (mask.to(torch.float32) / bc.view(C, 1)).reshape(C * B)
+        if use_native_loss:
+            loss = ops.FusedCrossEntropy.apply(logits, labels, row_scale, None)
+        else:
+            lr_ = torch.nn.functional.cross_entropy(logits.float(), labels, reduction="none")
+            loss = (lr_ * row_scale).sum()
+        loss.backward()
+        self.interp.flush_deferred()
+        return loss.detach()
+
+    def _optimizer_step(self, lr, active, first):
+        if self.optimizer == "sgd":
+            ops.sgd_step(self.params, self.grads, lr, weight_decay=self.weight_decay if self.sgd_wd else 0.0,
+                         momentum=self.momentum, mom_buf=self.mom, mu=self.mu, global_ref=self.global_ref,
+                         first_step=first, active=active)
+        else:
+            self.step_t += active
+            ops.adam_step(self.params, self.grads, self.m1, self.m2, self.step_t.clamp_min(1.0), lr,
+                          weight_decay=self.weight_decay, amsgrad=self.vmax is not None, max_exp_avg_sq=self.vmax,
+                          decoupled=self.optimizer == "adamw", active=active)
+
+    # ------------------------------------------------------------------------------------------
+    def partial_sum(self, weights: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """[P + 1]: Σ_c weights[c]·params[c]  ‖  Σ_c weights[c]  (one buffer → one all-reduce)."""
+        if out is None:
+            out = torch.empty(self.P + 1, dtype=torch.float32, device=self.device)
+        ops.weighted_sum(self.params, weights.to(torch.float32), out=out[:self.P])
+        out[self.P:].copy_(weights.to(torch.float32).sum().view(1))
+        return out
+
+    @torch.no_grad()
+    def evaluate(self, store, slots, batch_size: int = 256):
+        """Per-client accuracy/loss of the current client params on their own data (batched)."""
+        C = self.C
+        counts = store.counts[slots]
+        n_max = int(counts.max())
+        order = store.epoch_order(slots, n_max, None, shuffle=False)
+        correct = torch.zeros(C, device=self.device)
+        loss = torch.zeros(C, device=self.device)
+        for lo in range(0, n_max, batch_size):
+            idx = order[:, lo:lo + batch_size]
+            x, y, mask = store.gather(idx)
+            out = self.interp.run(self.views, x, training=False, dtype=self.compute_dtype).float()
+            pred = out.argmax(-1)
+            correct += ((pred == y) & mask).sum(1)
+            l = torch.nn.functional.cross_entropy(out.reshape(-1, out.shape[-1]), y.reshape(-1), reduction="none")
+            loss += (l.view(C, -1) * mask).sum(1)
+        cnt = counts.clamp_min(1).float()
+        return correct / cnt, loss / cnt

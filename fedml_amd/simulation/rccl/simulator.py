@@ -1,0 +1,222 @@
+"""Parrot-RCCL: the MI355X-native FL simulator (reference NCCL simulator is a stub,
+`simulation/simulator.py:100-108`; intent: "AllReduce-based FL with resource scheduling",
+`simulation/nccl/README.md`).
+
+One process per GPU. Per round:
+  1. every rank derives the same client sample (reference RNG: ``np.random.seed(round)``) and the
+     same client→GPU packing (native branch-and-bound scheduler, ``core.schedule``);
+  2. each rank expands the global flat model into its [C, P] client stack and trains all its
+     virtual clients at once (``ClientBatchEngine``);
+  3. each rank reduces its clients to Σ n_c·w_c ‖ Σ n_c on-GPU (FedAvg kernel) and ONE RCCL
+     all-reduce over xGMI produces the next global model on every rank (no server process,
+     no per-client messages, no pickling);
+  4. optional server optimizer (FedOpt: fused HIP kernel), robust aggregation, evaluation,
+     checkpointing.
+"""
+import logging
+import math
+import os
+import time
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ... import ops
+from ...core.arena import ParamLayout
+from ...core.mlops import MLOpsMetrics
+from ...core.schedule import pack_clients_to_gpus
+from ...core.tracing import tracer
+from ...parallel import comm
+from ..common import client_sampling
+from .client_store import DeviceClientStore
+from .engine import ClientBatchEngine
+
+
+def _dtype(name):
+    return {"bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp16": torch.float16, "fp32": None,
+            "float32": None, None: None}.get(name, None)
+
+
+class RCCLSimulator:
+    def __init__(self, args, device, dataset, model, store: Optional[DeviceClientStore] = None):
+        self.args = args
+        self.device = torch.device(device)
+        self.rank, self.world = comm.init_process_group(device=self.device if self.device.type == "cuda" else None)
+        self.model = model.to(self.device)
+        self.dataset = dataset
+        self.K_total = int(args.client_num_in_total)
+        self.K = int(args.client_num_per_round)
+        self.C = math.ceil(self.K / self.world)
+        self.compute_dtype = _dtype(getattr(args, "compute_dtype", None)) if self.device.type == "cuda" else None
+        if dataset is not None:
+            train_local = dataset[5]
+            self.sample_counts = [int(dataset[4][c]) for c in range(self.K_total)]
+        else:
+            train_local = None
+            self.sample_counts = None
+        with tracer().span("store.build"):
+            self.store = store if store is not None else DeviceClientStore.from_client_data(train_local, self.device)
+        if self.sample_counts is None:
+            self.sample_counts = self.store.counts_host
+        self.engine = ClientBatchEngine(self.model, self.C, self.device, args, self.compute_dtype)
+        self.layout: ParamLayout = self.engine.layout
+        self.global_flat = self.layout.flatten(self.model.state_dict(), device=self.device)
+        comm.broadcast_flat(self.global_flat, 0)
+        self.partial = torch.empty(self.layout.size + 1, dtype=torch.float32, device=self.device)
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(int(getattr(args, "random_seed", 0)) * 7777 + self.rank)
+        self.server_opt = None
+        if str(args.federated_optimizer) == "FedOpt":
+            self.server_opt = _ServerOptState(args, self.layout.size, self.device)
+        self.round_times: List[float] = []
+        self.history: Dict[int, dict] = {}
+        self.round_idx = 0
+
+    # ---------------------------------------------------------------------------------------------
+    def assignment(self, round_idx: int):
+        ids = client_sampling(round_idx, self.K_total, self.K)
+        counts = [self.sample_counts[i] for i in ids]
+        packs = pack_clients_to_gpus(counts, self.world)
+        mine = [ids[j] for j in packs[self.rank]]
+        return ids, mine
+
+    def run_round(self, round_idx: int):
+        tr = tracer()
+        args = self.args
+        with tr.span("round.assign"):
+            _, mine = self.assignment(round_idx)
+            slots = torch.full((self.C,), 0, dtype=torch.int64)
+            valid = torch.zeros(self.C, dtype=torch.bool)
+            for i, cid in enumerate(mine):
+                slots[i] = cid
+                valid[i] = True
+            slots = slots.to(self.device)
+            valid = valid.to(self.device)
+        with tr.span("round.broadcast_local"):
+            self.engine.load_global(self.global_flat)
+        with tr.span("round.local_train"):
+            self.engine.train(self.store, slots, int(args.epochs), int(args.batch_size), float(args.learning_rate),
+                              generator=self.gen, shuffle=bool(getattr(args, "shuffle", True)), valid_slots=valid)
+        with tr.span("round.aggregate"):
+            w = torch.where(valid, self.store.counts[slots].to(torch.float32), torch.zeros(self.C, device=self.device))
+            self._robust_preaggregate(w)
+            self.engine.partial_sum(w, out=self.partial)
+            comm.all_reduce_flat(self.partial)
+            total = self.partial[self.layout.size:self.layout.size + 1]
+            avg = self.partial[:self.layout.size] / total
+            if self.server_opt is not None:
+                self.server_opt.step(self.global_flat, avg)
+            else:
+                self.global_flat.copy_(avg)
+            self._post_aggregate()
+
+    def _robust_preaggregate(self, w):
+        dt = getattr(self.args, "defense_type", None)
+        if dt in ("norm_diff_clipping", "weak_dp"):
+            mask = self.layout.weight_mask(self.device)
+            ops.norm_diff_clip_(self.engine.params, self.global_flat, float(self.args.norm_bound), mask=mask)
+
+    def _post_aggregate(self):
+        if getattr(self.args, "defense_type", None) == "weak_dp":
+            mask = self.layout.weight_mask(self.device)
+            ops.gaussian_noise_(self.global_flat, float(self.args.stddev), seed=int(getattr(self.args, "random_seed", 0)),
+                                offset=self.round_idx * self.layout.size, mask=mask)
+
+    def run(self, rounds: Optional[int] = None):
+        n = int(self.args.comm_round) if rounds is None else int(rounds)
+        freq = int(getattr(self.args, "frequency_of_the_test", 0) or 0)
+        for r in range(n):
+            t0 = time.perf_counter()
+            self.run_round(self.round_idx)
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+            dt = time.perf_counter() - t0
+            self.round_times.append(dt)
+            rec = {"round_time_s": dt, "train_loss": float(self.engine.last_loss)}
+            if freq > 0 and (self.round_idx % freq == 0 or r == n - 1):
+                rec.update(self.evaluate())
+            self.history[self.round_idx] = rec
+            if self.rank == 0:
+                logging.info("[RCCL-sim] round %d: %s", self.round_idx, rec)
+                MLOpsMetrics.get_instance().log(dict(rec, round=self.round_idx), step=self.round_idx)
+            ck = getattr(self.args, "checkpoint_dir", None)
+            if ck and (self.round_idx + 1) % int(getattr(self.args, "checkpoint_every", 1) or 1) == 0:
+                self.save_checkpoint(ck)
+            self.round_idx += 1
+        return self.global_model_state()
+
+    # ---------------------------------------------------------------------------------------------
+    def global_model_state(self):
+        return self.layout.unflatten(self.global_flat.detach().cpu())
+
+    @torch.no_grad()
+    def evaluate(self):
+        """Global model on the (sharded) global test set; confusion counts all-reduced."""
+        if self.dataset is None:
+            return {}
+        test = self.dataset[3]
+        self.model.load_state_dict(self.layout.unflatten(self.global_flat))
+        self.model.eval()
+        n = test.num_samples
+        per = math.ceil(n / self.world)
+        lo, hi = self.rank * per, min(n, (self.rank + 1) * per)
+        stats = torch.zeros(3, device=self.device, dtype=torch.float32)
+        bs = 512
+        for s in range(lo, hi, bs):
+            e = min(hi, s + bs)
+            x = test.x[s:e].to(self.device)
+            y = test.y[s:e].to(self.device)
+            out = self.model(x).float()
+            stats[0] += (out.argmax(-1) == y).sum()
+            stats[1] += torch.nn.functional.cross_entropy(out, y, reduction="sum")
+            stats[2] += (e - s)
+        comm.all_reduce_flat(stats)
+        self.model.train()
+        tot = max(1.0, float(stats[2]))
+        return {"Test/Acc": float(stats[0]) / tot, "Test/Loss": float(stats[1]) / tot}
+
+    def save_checkpoint(self, directory):
+        from ...core.checkpoint import save_round_checkpoint
+        if self.rank == 0:
+            save_round_checkpoint(directory, self.round_idx, self.global_model_state(), self.args,
+                                  server_opt=self.server_opt.state_dict() if self.server_opt else None)
+
+    def load_checkpoint(self, directory, round_idx=None):
+        from ...core.checkpoint import load_round_checkpoint
+        ck = load_round_checkpoint(directory, round_idx)
+        self.global_flat.copy_(self.layout.flatten(ck["global"], device=self.device))
+        if self.server_opt is not None and ck.get("server_opt") is not None:
+            self.server_opt.load_state_dict(ck["server_opt"])
+        self.round_idx = int(ck["round"]) + 1
+        return self.round_idx
+
+
+class _ServerOptState:
+    """FedOpt server optimizer on the flat global model (fused HIP kernel `fa_fedopt_step`)."""
+
+    def __init__(self, args, P, device):
+        self.opt = str(getattr(args, "server_optimizer", "sgd")).lower()
+        self.lr = float(getattr(args, "server_lr", 1.0))
+        self.momentum = float(getattr(args, "server_momentum", 0.0) or 0.0)
+        self.b1 = float(getattr(args, "server_beta1", 0.9))
+        self.b2 = float(getattr(args, "server_beta2", 0.99))
+        self.eps = float(getattr(args, "server_eps", 1e-3))
+        self.s1 = torch.zeros(P, device=device)
+        self.s2 = torch.zeros(P, device=device)
+        if self.opt in ("adagrad", "fedadagrad"):
+            self.s2.fill_(float(getattr(args, "server_tau", 0.0)) ** 2)
+        self.t = 0
+
+    def step(self, glob, avg):
+        self.t += 1
+        ops.fedopt_step(avg.view(1, -1), torch.ones(1, device=avg.device), glob, self.opt, self.lr, self.b1, self.b2,
+                        self.eps, self.momentum, False, self.s1, self.s2, self.t, first_step=self.t == 1)
+
+    def state_dict(self):
+        return {"s1": self.s1.cpu(), "s2": self.s2.cpu(), "t": self.t, "opt": self.opt}
+
+    def load_state_dict(self, sd):
+        self.s1.copy_(sd["s1"])
+        self.s2.copy_(sd["s2"])
+        self.t = int(sd["t"])

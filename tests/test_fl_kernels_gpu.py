@@ -1,0 +1,194 @@
+"""Numerics of the FL HIP kernels vs the plain-PyTorch fp32 references (CPU path of the same op)."""
+import pytest
+import torch
+
+from fedml_amd import ops
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _both(fn, *tensors, **kw):
+    cpu = fn(*[t.clone() if isinstance(t, torch.Tensor) else t for t in tensors], **kw)
+    gpu = fn(*[t.clone().to(DEV) if isinstance(t, torch.Tensor) else t for t in tensors], **kw)
+    return cpu, gpu
+
+
+def test_native_library_loads():
+    assert ops.native_available()
+    assert ops.use_native(torch.zeros(1, device=DEV))
+
+
+@pytest.mark.parametrize("C,P", [(1, 7), (3, 1000), (100, 614452 + 3), (7, 33)])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_weighted_sum(C, P, dtype):
+    X = torch.randn(C, P).to(dtype)
+    w = torch.rand(C)
+    ref = (w.view(C, 1) * X.float()).sum(0)
+    out = ops.weighted_sum(X.to(DEV), w.to(DEV)).cpu()
+    assert torch.allclose(out, ref, atol=1e-4, rtol=1e-4)
+    # accumulate form
+    base = torch.randn(P)
+    out2 = ops.weighted_sum(X.to(DEV), w.to(DEV), out=base.clone().to(DEV), beta=0.5).cpu()
+    assert torch.allclose(out2, ref + 0.5 * base, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("S,C,P", [(1024, 10, 5000), (37, 3, 129), (64, 64, 1000), (10, 70, 300)])
+def test_subset_aggregate_mfma(S, C, P):
+    W = torch.rand(S, C)
+    X = torch.randn(C, P)
+    ref = (W.double() @ X.double()).float()
+    out = ops.subset_aggregate(W.to(DEV), X.to(DEV)).cpu()
+    assert torch.allclose(out, ref, atol=1e-4, rtol=1e-4)
+
+
+@pytest.mark.parametrize("momentum,mu,grad_dtype", [(0.0, 0.0, torch.float32), (0.9, 0.0, torch.float32),
+                                                    (0.9, 0.01, torch.bfloat16)])
+def test_sgd_step(momentum, mu, grad_dtype):
+    C, P = 5, 3001
+    p = torch.randn(C, P)
+    g = torch.randn(C, P).to(grad_dtype)
+    ref_g = torch.randn(P)
+    active = torch.tensor([1.0, 0.0, 1.0, 1.0, 0.0])
+    for first in (True, False):
+        mom = torch.randn(C, P)
+        pc, mc = p.clone(), mom.clone()
+        ops.sgd_step(pc, g, 0.1, weight_decay=0.01, momentum=momentum, mom_buf=mc, mu=mu, global_ref=ref_g,
+                     first_step=first, active=active)
+        pg, mg = p.clone().to(DEV), mom.clone().to(DEV)
+        ops.sgd_step(pg, g.to(DEV), 0.1, weight_decay=0.01, momentum=momentum, mom_buf=mg, mu=mu,
+                     global_ref=ref_g.to(DEV), first_step=first, active=active.to(DEV))
+        assert torch.allclose(pg.cpu(), pc, atol=1e-5, rtol=1e-5)
+        if momentum:
+            assert torch.allclose(mg.cpu(), mc, atol=1e-5, rtol=1e-5)
+
+
+@pytest.mark.parametrize("amsgrad,decoupled", [(False, False), (True, False), (False, True)])
+def test_adam_step(amsgrad, decoupled):
+    C, P = 3, 2049
+    p = torch.randn(C, P)
+    g = torch.randn(C, P)
+    st = [torch.rand(C, P), torch.rand(C, P), torch.rand(C, P)]
+    step = torch.tensor([1.0, 2.0, 5.0])
+    cpu = [t.clone() for t in [p] + st]
+    gpu = [t.clone().to(DEV) for t in [p] + st]
+    ops.adam_step(cpu[0], g, cpu[1], cpu[2], step, 1e-3, weight_decay=0.01, amsgrad=amsgrad,
+                  max_exp_avg_sq=cpu[3], decoupled=decoupled)
+    ops.adam_step(gpu[0], g.to(DEV), gpu[1], gpu[2], step.to(DEV), 1e-3, weight_decay=0.01, amsgrad=amsgrad,
+                  max_exp_avg_sq=gpu[3], decoupled=decoupled)
+    for a, b in zip(cpu, gpu):
+        assert torch.allclose(a, b.cpu(), atol=1e-5, rtol=1e-4)
+
+
+@pytest.mark.parametrize("opt", ["sgd", "adam", "yogi", "adagrad"])
+def test_fedopt_step(opt):
+    C, P = 4, 5000
+    X = torch.randn(C, P)
+    w = torch.rand(C)
+    w = w / w.sum()
+    glob = torch.randn(P)
+    s1, s2 = torch.rand(P), torch.rand(P)
+    cpu = [glob.clone(), s1.clone(), s2.clone()]
+    gpu = [t.clone().to(DEV) for t in (glob, s1, s2)]
+    for step in (1, 2):
+        ops.fedopt_step(X, w, cpu[0], opt, lr=0.5, momentum=0.9, state1=cpu[1], state2=cpu[2], step=step,
+                        first_step=step == 1)
+        ops.fedopt_step(X.to(DEV), w.to(DEV), gpu[0], opt, lr=0.5, momentum=0.9, state1=gpu[1], state2=gpu[2],
+                        step=step, first_step=step == 1)
+    for a, b in zip(cpu, gpu):
+        assert torch.allclose(a, b.cpu(), atol=1e-4, rtol=1e-4)
+
+
+def test_norm_clip_and_noise():
+    C, P = 6, 10007
+    X = torch.randn(C, P)
+    G = torch.randn(P)
+    mask = (torch.rand(P) > 0.1).to(torch.uint8)
+    nc = ops.client_sqnorm(X, G, mask)
+    ng = ops.client_sqnorm(X.to(DEV), G.to(DEV), mask.to(DEV)).cpu()
+    assert torch.allclose(nc, ng, rtol=1e-4)
+    xc, xg = X.clone(), X.clone().to(DEV)
+    ops.norm_diff_clip_(xc, G, 5.0, mask=mask)
+    ops.norm_diff_clip_(xg, G.to(DEV), 5.0, mask=mask.to(DEV))
+    assert torch.allclose(xc, xg.cpu(), atol=1e-5)
+    z = torch.zeros(1 << 20, device=DEV)
+    ops.gaussian_noise_(z, 2.0, seed=3)
+    assert abs(float(z.mean())) < 0.02 and abs(float(z.std()) - 2.0) < 0.02
+
+
+@pytest.mark.parametrize("C", [1, 2, 5, 8, 13, 33, 64])
+def test_coordinate_median(C):
+    X = torch.randn(C, 4099)
+    ref = torch.median(X, dim=0).values
+    out = ops.coordinate_median(X.to(DEV)).cpu()
+    assert torch.equal(out, ref)
+
+
+def test_int8_quant_roundtrip_and_error_feedback():
+    n = 100003
+    x = torch.randn(n) * 3
+    r = torch.zeros(n, device=DEV)
+    q, s = ops.quantize_int8(x.to(DEV), residual=r, stochastic=True, seed=1)
+    acc = torch.zeros(n, device=DEV)
+    ops.dequantize_int8_axpy(q, s, 1.0, acc)
+    # error feedback identity: deq + residual == x (up to fp32 rounding)
+    assert torch.allclose((acc + r).cpu(), x, atol=1e-5)
+    blk_err = (acc.cpu() - x).abs().view(-1)[: n // 256 * 256].view(-1, 256).amax(1)
+    assert (blk_err <= s.cpu()[: n // 256] * 1.0001).all()
+    # deterministic rounding matches the reference exactly
+    qc, sc = ops.quantize_int8(x, stochastic=False)
+    qg, sg = ops.quantize_int8(x.to(DEV), stochastic=False)
+    assert torch.allclose(sc, sg.cpu()) and (qc.int() - qg.cpu().int()).abs().max() <= 1
+
+
+def test_fp8_quant_matches_torch():
+    n = 70001
+    x = torch.randn(n) * 10
+    qc, sc = ops.quantize_fp8(x)
+    qg, sg = ops.quantize_fp8(x.to(DEV))
+    assert torch.allclose(sc, sg.cpu())
+    dc = torch.zeros(n)
+    dg = torch.zeros(n, device=DEV)
+    ops.dequantize_fp8_axpy(qc, sc, 1.0, dc)
+    ops.dequantize_fp8_axpy(qg, sg, 1.0, dg)
+    assert torch.allclose(dc, dg.cpu(), rtol=0, atol=1e-6)
+
+
+@pytest.mark.parametrize("n,k", [(1000, 10), (614452, 6144), (100000, 1), (5000, 5000)])
+def test_topk_exact(n, k):
+    x = torch.randn(n)
+    x[::7] = x[::7].round()    # force ties
+    r = torch.zeros(n, device=DEV)
+    idx, val = ops.topk_abs(x.to(DEV), k, residual=r)
+    idx, val = idx.cpu().long(), val.cpu()
+    assert len(torch.unique(idx)) == k
+    thr = torch.topk(x.abs(), k).values.min()
+    assert (x[idx].abs() >= thr).all()
+    assert torch.equal(x[idx], val)
+    acc = torch.zeros(n, device=DEV)
+    ops.scatter_axpy(idx.int().to(DEV), val.to(DEV), 1.0, acc)
+    assert torch.allclose((acc + r).cpu(), x)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_softmax_xent(dtype):
+    R, K = 1000, 100
+    z = (torch.randn(R, K) * 3).to(dtype)
+    y = torch.randint(0, K, (R,))
+    y[::10] = -100
+    cw = torch.rand(K)
+    rs = torch.rand(R)
+    lc, dc = ops.softmax_xent_fwd_bwd(z, y, cw, rs)
+    lg, dg = ops.softmax_xent_fwd_bwd(z.to(DEV), y.to(DEV), cw.to(DEV), rs.to(DEV))
+    tol = 1e-4 if dtype == torch.float32 else 2e-2
+    assert torch.allclose(lc, lg.cpu(), atol=tol, rtol=tol)
+    assert torch.allclose(dc.float(), dg.cpu().float(), atol=tol, rtol=tol)
+
+
+def test_confusion_matrix():
+    R, K, G = 999, 10, 3
+    z = torch.randn(R, K)
+    y = torch.randint(0, K, (R,))
+    c = ops.confusion_matrix(z, y, num_groups=G, rows_per_group=333)
+    g = ops.confusion_matrix(z.to(DEV), y.to(DEV), num_groups=G, rows_per_group=333).cpu()
+    assert torch.equal(c, g)
