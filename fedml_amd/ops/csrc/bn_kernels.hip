@@ -1,0 +1,224 @@
+// Per-(client, channel) BatchNorm finalisation, fused block epilogues and small layout kernels
+// for the native client-batched ResNet executor. Layout as in conv_kernels.hip:
+// activations [C][N][H][W][Ch] bf16; vectors [C][Ch] fp32; parameters/grads in the client-stacked
+// fp32 arenas [C][ldw] addressed by offset.
+#include "common.h"
+
+__device__ __forceinline__ void unpack8f(uint4 v, float* f) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+__device__ __forceinline__ uint4 pack8f(const float* f) {
+  uint4 r;
+  r.x = (uint32_t)f32_to_bf16(f[0]) | ((uint32_t)f32_to_bf16(f[1]) << 16);
+  r.y = (uint32_t)f32_to_bf16(f[2]) | ((uint32_t)f32_to_bf16(f[3]) << 16);
+  r.z = (uint32_t)f32_to_bf16(f[4]) | ((uint32_t)f32_to_bf16(f[5]) << 16);
+  r.w = (uint32_t)f32_to_bf16(f[6]) | ((uint32_t)f32_to_bf16(f[7]) << 16);
+  return r;
+}
+
+// ---- forward finalisation: statistics → folded scale/shift, running-stat update ----
+// stats[c][ch][2] = (Σy, Σy²) over n = N·H·W elements of client c.
+// scale = γ·rstd, shift = β − mean·scale; mean/rstd saved for the backward.
+// Running statistics (torch semantics: unbiased variance, momentum) and num_batches_tracked
+// are updated in the parameter arena for ACTIVE clients only.
+__global__ void bn_fwd_finalize_kernel(const float* __restrict__ stats, int Ch, float n, float* __restrict__ arena,
+                                       int64_t ldw, int64_t off_gamma, int64_t off_beta, int64_t off_rm,
+                                       int64_t off_rv, int64_t off_nbt, float momentum, float eps,
+                                       const float* __restrict__ active, float* __restrict__ scale,
+                                       float* __restrict__ shift, float* __restrict__ mean_out,
+                                       float* __restrict__ rstd_out, int update_running) {
+  const int c = blockIdx.y;
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= Ch) return;
+  float* pa = arena + (int64_t)c * ldw;
+  const float s1 = stats[((int64_t)c * Ch + ch) * 2 + 0];
+  const float s2 = stats[((int64_t)c * Ch + ch) * 2 + 1];
+  const float mean = s1 / n;
+  const float var = fmaxf(s2 / n - mean * mean, 0.f);
+  const float rstd = rsqrtf(var + eps);
+  const float g = off_gamma >= 0 ? pa[off_gamma + ch] : 1.f;
+  const float b = off_beta >= 0 ? pa[off_beta + ch] : 0.f;
+  const int64_t v = (int64_t)c * Ch + ch;
+  scale[v] = g * rstd;
+  shift[v] = b - mean * g * rstd;
+  mean_out[v] = mean;
+  rstd_out[v] = rstd;
+  const bool on = active ? active[c] > 0.f : true;
+  if (update_running && on) {
+    if (off_rm >= 0) pa[off_rm + ch] = (1.f - momentum) * pa[off_rm + ch] + momentum * mean;
+    if (off_rv >= 0) pa[off_rv + ch] = (1.f - momentum) * pa[off_rv + ch] + momentum * var * n / fmaxf(n - 1.f, 1.f);
+    if (off_nbt >= 0 && ch == 0) pa[off_nbt] += 1.f;
+  }
+}
+
+FA_EXPORT int fa_bn_fwd_finalize(const float* stats, int C, int Ch, float n, float* arena, int64_t ldw,
+                                 int64_t off_gamma, int64_t off_beta, int64_t off_rm, int64_t off_rv, int64_t off_nbt,
+                                 float momentum, float eps, const float* active, float* scale, float* shift,
+                                 float* mean_out, float* rstd_out, int update_running, hipStream_t stream) {
+  hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((Ch + 63) / 64, C), dim3(64), 0, stream, stats, Ch, n, arena, ldw,
+                     off_gamma, off_beta, off_rm, off_rv, off_nbt, momentum, eps, active, scale, shift, mean_out,
+                     rstd_out, update_running);
+  return (int)hipGetLastError();
+}
+
+// ---- backward finalisation: (Σg, Σg·y) → dγ, dβ into the gradient arena and the folded
+// coefficients of dy = α·g + β·y + γc consumed by the conv backward kernels.
+__global__ void bn_bwd_finalize_kernel(const float* __restrict__ bstats, int NS, int q_gy, int Ch, float n,
+                                       const float* __restrict__ mean, const float* __restrict__ rstd,
+                                       const float* __restrict__ arena, float* __restrict__ garena, int64_t ldw,
+                                       int64_t off_gamma, int64_t off_beta, float* __restrict__ alpha,
+                                       float* __restrict__ beta_c, float* __restrict__ gamma_c) {
+  const int c = blockIdx.y;
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= Ch) return;
+  const int64_t v = (int64_t)c * Ch + ch;
+  const float sg = bstats[v * NS + 0];
+  const float sgy = bstats[v * NS + q_gy];
+  const float mu = mean[v], r = rstd[v];
+  const float dbeta = sg;
+  const float dgamma = r * (sgy - mu * sg);
+  const float g = off_gamma >= 0 ? arena[(int64_t)c * ldw + off_gamma + ch] : 1.f;
+  if (off_gamma >= 0) garena[(int64_t)c * ldw + off_gamma + ch] += dgamma;
+  if (off_beta >= 0) garena[(int64_t)c * ldw + off_beta + ch] += dbeta;
+  const float a = g * r;
+  const float b = -g * r * r * dgamma / n;
+  alpha[v] = a;
+  beta_c[v] = b;
+  gamma_c[v] = -a * dbeta / n - b * mu;
+}
+
+FA_EXPORT int fa_bn_bwd_finalize(const float* bstats, int NS, int q_gy, int C, int Ch, float n, const float* mean,
+                                 const float* rstd, const float* arena, float* garena, int64_t ldw, int64_t off_gamma,
+                                 int64_t off_beta, float* alpha, float* beta_c, float* gamma_c, hipStream_t stream) {
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((Ch + 63) / 64, C), dim3(64), 0, stream, bstats, NS, q_gy, Ch, n,
+                     mean, rstd, arena, garena, ldw, off_gamma, off_beta, alpha, beta_c, gamma_c);
+  return (int)hipGetLastError();
+}
+
+// ---- fused block output: out = relu(y·s + t + R), R = yd·sd + td (downsample) | x (identity) | 0
+__global__ __launch_bounds__(256) void block_out_kernel(const uint16_t* __restrict__ y, const float* __restrict__ s,
+                                                        const float* __restrict__ t, const uint16_t* __restrict__ r,
+                                                        const float* __restrict__ rs, const float* __restrict__ rt,
+                                                        uint16_t* __restrict__ out, int64_t per_client, int Ch) {
+  const int c = blockIdx.y;
+  const int64_t nvec = per_client / 8;
+  const uint16_t* yc = y + (int64_t)c * per_client;
+  const uint16_t* rc = r ? r + (int64_t)c * per_client : nullptr;
+  uint16_t* oc = out + (int64_t)c * per_client;
+  const float* sc = s + (int64_t)c * Ch;
+  const float* tc = t + (int64_t)c * Ch;
+  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * blockDim.x) {
+    const int ch0 = (int)((v * 8) % Ch);
+    float f[8];
+    unpack8f(*reinterpret_cast<const uint4*>(yc + v * 8), f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = f[j] * sc[ch0 + j] + tc[ch0 + j];
+    if (rc) {
+      float g[8];
+      unpack8f(*reinterpret_cast<const uint4*>(rc + v * 8), g);
+      if (rs) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] += g[j] * rs[(int64_t)c * Ch + ch0 + j] + rt[(int64_t)c * Ch + ch0 + j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) f[j] += g[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+    *reinterpret_cast<uint4*>(oc + v * 8) = pack8f(f);
+  }
+}
+
+FA_EXPORT int fa_block_out(const uint16_t* y, const float* s, const float* t, const uint16_t* r, const float* rs,
+                           const float* rt, uint16_t* out, int C, int64_t per_client, int Ch, hipStream_t stream) {
+  if (Ch % 8 != 0) return -3;
+  hipLaunchKernelGGL(block_out_kernel, dim3(fa_grid(per_client / 8, 256, 256), C), dim3(256), 0, stream, y, s, t, r,
+                     rs, rt, out, per_client, Ch);
+  return (int)hipGetLastError();
+}
+
+// ---- global average pool (forward): pooled[c][n][ch] = mean_hw out[c][n][hw][ch] (fp32 out)
+__global__ __launch_bounds__(256) void avgpool_kernel(const uint16_t* __restrict__ x, float* __restrict__ pooled,
+                                                      int HW, int Ch) {
+  const int cn = blockIdx.x;  // flattened (client, sample)
+  const uint16_t* xs = x + (int64_t)cn * HW * Ch;
+  for (int ch = threadIdx.x; ch < Ch; ch += blockDim.x) {
+    float s = 0.f;
+    for (int p = 0; p < HW; ++p) s += bf16_to_f32(xs[(int64_t)p * Ch + ch]);
+    pooled[(int64_t)cn * Ch + ch] = s / (float)HW;
+  }
+}
+
+FA_EXPORT int fa_avgpool(const uint16_t* x, float* pooled, int CN, int HW, int Ch, hipStream_t stream) {
+  hipLaunchKernelGGL(avgpool_kernel, dim3(CN), dim3(Ch < 256 ? 64 * ((Ch + 63) / 64) : 256), 0, stream, x, pooled,
+                     HW, Ch);
+  return (int)hipGetLastError();
+}
+
+// ---- head backward: gpre = (dpool/HW)·[out > 0]; stats (Σg, Σg·y3, Σg·yd)
+// one workgroup per (client, sample): channels across threads, spatial loop inside,
+// per-channel partial sums atomically added once per workgroup.
+__global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__ dpool, const uint16_t* __restrict__ out,
+                                                       const uint16_t* __restrict__ y3, const uint16_t* __restrict__ yd,
+                                                       uint16_t* __restrict__ gpre, float* __restrict__ stats, int N,
+                                                       int HW, int Ch, int NS) {
+  const int cn = blockIdx.x;
+  const int c = cn / N;
+  const int64_t base = (int64_t)cn * HW * Ch;
+  const float inv = 1.f / (float)HW;
+  for (int ch = threadIdx.x; ch < Ch; ch += blockDim.x) {
+    const float d = dpool[(int64_t)cn * Ch + ch] * inv;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f;
+    for (int p = 0; p < HW; ++p) {
+      const int64_t i = base + (int64_t)p * Ch + ch;
+      const float g = bf16_to_f32(out[i]) > 0.f ? d : 0.f;
+      const uint16_t gb = f32_to_bf16(g);
+      gpre[i] = gb;
+      const float gr = bf16_to_f32(gb);
+      a0 += gr;
+      a1 += gr * bf16_to_f32(y3[i]);
+      if (yd) a2 += gr * bf16_to_f32(yd[i]);
+    }
+    float* st = stats + ((int64_t)c * Ch + ch) * NS;
+    atomicAdd(st + 0, a0);
+    atomicAdd(st + 1, a1);
+    if (yd && NS > 2) atomicAdd(st + 2, a2);
+  }
+}
+
+FA_EXPORT int fa_head_bwd(const float* dpool, const uint16_t* out, const uint16_t* y3, const uint16_t* yd,
+                          uint16_t* gpre, float* stats, int C, int N, int HW, int Ch, int NS, hipStream_t stream) {
+  hipLaunchKernelGGL(head_bwd_kernel, dim3(C * N), dim3(Ch < 256 ? 64 * ((Ch + 63) / 64) : 256), 0, stream, dpool,
+                     out, y3, yd, gpre, stats, N, HW, Ch, NS);
+  return (int)hipGetLastError();
+}
+
+// ---- input conversion: x [C][N][Cin][H][W] fp32 (NCHW per client) → [C][N][H][W][Cpad] bf16
+__global__ __launch_bounds__(256) void nchw_to_nhwc_pad_kernel(const float* __restrict__ x, uint16_t* __restrict__ y,
+                                                               int64_t CN, int Cin, int HW, int Cpad) {
+  const int64_t total = CN * HW;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t cn = i / HW;
+    const int p = (int)(i % HW);
+    const float* src = x + cn * Cin * HW + p;
+    uint16_t* dst = y + i * Cpad;
+    for (int ch = 0; ch < Cpad; ++ch) dst[ch] = ch < Cin ? f32_to_bf16(src[(int64_t)ch * HW]) : (uint16_t)0;
+  }
+}
+
+FA_EXPORT int fa_nchw_to_nhwc_pad(const float* x, uint16_t* y, int64_t CN, int Cin, int HW, int Cpad,
+                                  hipStream_t stream) {
+  hipLaunchKernelGGL(nchw_to_nhwc_pad_kernel, dim3(fa_grid(CN * HW, 256, 4096)), dim3(256), 0, stream, x, y, CN, Cin,
+                     HW, Cpad);
+  return (int)hipGetLastError();
+}
+
+// ---- bn_relu_apply: out = relu(y·s + t) (stem activation materialisation)
+FA_EXPORT int fa_bn_relu_apply(const uint16_t* y, const float* s, const float* t, uint16_t* out, int C,
+                               int64_t per_client, int Ch, hipStream_t stream) {
+  return fa_block_out(y, s, t, nullptr, nullptr, nullptr, out, C, per_client, Ch, stream);
+}

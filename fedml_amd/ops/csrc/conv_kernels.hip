@@ -1,0 +1,593 @@
+// Client-batched convolution kernels for the virtual-client engine (gfx950, wave64, bf16 MFMA).
+//
+// Layouts (per virtual client c, all clients of a GPU in one launch, grid.y = client):
+//   activations  X [C][N][H][W][Ch]   bf16, NHWC inside a client
+//   packed fwd W  Wf[C][Cout][ldk]    bf16, k = (kh*KW + kw)*Cin + ci, zero padded to Kp
+//   packed bwd W  Wb[C][Cin][ldk2]    bf16, k = (kh*KW + kw)*Cout + co (taps NOT flipped: the data
+//                                            kernel maps each tap to the dy pixel it came from)
+//   BN / scale vectors [C][Ch] fp32; BN statistics [C][Ch][NS] fp32 (atomics)
+//
+// Every conv is an implicit GEMM per client: M = N·Ho·Wo pixels, N = Cout, K = KH·KW·Cin.
+// ResNet-56 channels are 16–256, so these GEMMs are skinny and HBM-bound; the kernels are
+// built to move each activation byte once:
+//   * forward : A operand = relu(x·s + t) of the PREVIOUS conv's raw output (its BatchNorm
+//               folded into this conv's operand load), epilogue writes the raw output once
+//               and accumulates this layer's BN statistics (Σy, Σy²) per (client, channel).
+//   * bwd-data: A operand = dy = α·g + β·y + γ (the BN backward of the following BN folded
+//               into the load), epilogue applies the previous ReLU mask and accumulates the
+//               previous BN's backward statistics (Σg, Σg·x), writing g once.
+//   * bwd-weight: dW = Σ_pixels dyᵀ ⊗ act(x), pixel-chunk per workgroup, fp32 atomics
+//               straight into the client-stacked gradient arena (OIHW positions, stride ldw).
+// MFMA: v_mfma_f32_16x16x32_bf16. Lane l holds A[row l&15][k 8(l>>4)..+7], B[k 8(l>>4)..+7][col l&15];
+// D: col = l&15, row = 4(l>>4) + i.
+#include "common.h"
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
+
+enum { PRO_NONE = 0, PRO_BNRELU = 1 };
+enum { EPI_FWD = 0, EPI_STORE = 1, EPI_MASK = 2, EPI_BLOCK = 3 };
+
+__device__ __forceinline__ bf16x8 as_bf16x8(uint4 v) {
+  union { uint4 u; bf16x8 b; } c;
+  c.u = v;
+  return c.b;
+}
+__device__ __forceinline__ void unpack8(uint4 v, float* f) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  return (uint32_t)f32_to_bf16(a) | ((uint32_t)f32_to_bf16(b) << 16);
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint4 r;
+  r.x = pack2(f[0], f[1]); r.y = pack2(f[2], f[3]); r.z = pack2(f[4], f[5]); r.w = pack2(f[6], f[7]);
+  return r;
+}
+__device__ __forceinline__ float rbf(float x) { return bf16_to_f32(f32_to_bf16(x)); }
+
+// =====================================================================================
+// Weight packing: fp32 OIHW (client-stacked arena, stride ldw) → bf16 GEMM layouts.
+// One launch packs every conv layer of the model (segment table), both directions.
+// =====================================================================================
+struct PackSeg {
+  int64_t src_off;   // offset of the OIHW weight inside one client's arena row
+  int64_t dst_f;     // offset of this layer's Wf block (elements, per client stride = dst_ld)
+  int64_t dst_b;     // offset of this layer's Wb block
+  int cout, cin, kh, kw, ldk, ldk2;
+  int cin_src;       // channels of the stored weight (cin may be padded up to a multiple of 8)
+};
+
+__global__ __launch_bounds__(256) void pack_weights_kernel(const float* __restrict__ arena, int64_t ldw,
+                                                           const PackSeg* __restrict__ segs, int nseg,
+                                                           uint16_t* __restrict__ dst, int64_t dst_ld) {
+  const int c = blockIdx.y;
+  const PackSeg s = segs[blockIdx.z];
+  const float* w = arena + (int64_t)c * ldw + s.src_off;
+  uint16_t* df = dst + (int64_t)c * dst_ld + s.dst_f;
+  uint16_t* db = dst + (int64_t)c * dst_ld + s.dst_b;
+  const int taps = s.kh * s.kw;
+  const int nf = s.cout * s.ldk;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nf; i += gridDim.x * blockDim.x) {
+    const int co = i / s.ldk, k = i % s.ldk;
+    float v = 0.f;
+    if (k < taps * s.cin) {
+      const int tap = k / s.cin, ci = k % s.cin;
+      if (ci < s.cin_src) v = w[((int64_t)co * s.cin_src + ci) * taps + tap];
+    }
+    df[i] = f32_to_bf16(v);
+  }
+  if (s.dst_b >= 0) {
+    const int nb = s.cin * s.ldk2;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nb; i += gridDim.x * blockDim.x) {
+      const int ci = i / s.ldk2, k = i % s.ldk2;
+      float v = 0.f;
+      if (k < taps * s.cout) {
+        const int tap = k / s.cout, co = k % s.cout;
+        if (ci < s.cin_src) v = w[((int64_t)co * s.cin_src + ci) * taps + tap];
+      }
+      db[i] = f32_to_bf16(v);
+    }
+  }
+}
+
+FA_EXPORT int fa_pack_weights(const float* arena, int64_t ldw, const void* segs_dev, int nseg, uint16_t* dst,
+                              int64_t dst_ld, int C, hipStream_t stream) {
+  hipLaunchKernelGGL(pack_weights_kernel, dim3(16, C, nseg), dim3(256), 0, stream, arena, ldw,
+                     (const PackSeg*)segs_dev, nseg, dst, dst_ld);
+  return (int)hipGetLastError();
+}
+
+// =====================================================================================
+// Implicit-GEMM convolution (forward and backward-data share this body).
+//
+//   out[c][m][n] = Σ_k A[c][m][k] · B[c][n][k],   m = output pixel, n = output channel
+//
+// A is gathered on the fly from `src` ([C][N][Hs][Ws][KC]) at the input pixel each tap maps
+// to, with the operand transform chosen by AOP:
+//   AOP_ACT   : a = PRO ? relu(x·s + t) : x           (forward; s,t = previous BN folded)
+//   AOP_DY    : a = α·g + β·y + γ                       (bwd-data; g = `src`, y = `src2`)
+// Geometry: MODE_FWD  → input pixel = o·stride − pad + tap offset (bounds → 0)
+//           MODE_BWD  → dy pixel = (i + pad − tap)/stride when divisible and in range (else 0)
+// The workgroup owns one client and a run of 16-pixel tiles; 4 waves, each wave a 16 × NOUT tile
+// per iteration; B (packed weights) and the per-channel vectors live in LDS.
+// =====================================================================================
+enum { AOP_ACT = 0, AOP_DY = 1 };
+enum { MODE_FWD = 0, MODE_BWD = 1 };
+
+struct ConvArgs {
+  const uint16_t* src;   // A source activations / g
+  const uint16_t* src2;  // y for AOP_DY
+  const uint16_t* wpk;   // packed B [C][NOUT][ldk]
+  int64_t wpk_ld;        // per-client stride of the packed weights (elements)
+  const float* vec0;     // PRO scale  | α
+  const float* vec1;     // PRO shift  | β
+  const float* vec2;     //            | γ
+  uint16_t* out;         // [C][M][NOUT]
+  // epilogue inputs
+  const uint16_t* e_x;   // EPI_MASK: previous raw activation (mask + Σg·x); EPI_BLOCK: block input (mask)
+  const float* e_s;      // EPI_MASK: previous BN scale
+  const float* e_t;      // EPI_MASK: previous BN shift
+  const uint16_t* e_add; // EPI_BLOCK: extra gradient (downsample / identity path)
+  const uint16_t* e_y1;  // EPI_BLOCK: previous block's bn3 input (Σg·y)
+  const uint16_t* e_y2;  // EPI_BLOCK: previous block's downsample-bn input (optional)
+  float* stats;          // [C][NOUT][NS]
+  int NS;
+  int Nb, Hs, Ws, KC;    // source geometry (KC = channels of the A source = GEMM K per tap)
+  int Ho, Wo;            // output geometry
+  int KH, KW, stride, pad;
+  int ldk;               // packed row length (≥ K, multiple of 32, +8 pad)
+  int Kp;                // K rounded to 32
+  int tiles_per_wave;
+};
+
+template <int NT, int AOP, int PRO, int MODE, int EPI>
+__global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
+  constexpr int NOUT = NT * 16;
+  const int c = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int K = a.KH * a.KW * a.KC;
+  const int M = a.Nb * a.Ho * a.Wo;
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint16_t* wl = reinterpret_cast<uint16_t*>(smem);                       // [NOUT][ldk]
+  float* v0 = reinterpret_cast<float*>(smem + (size_t)NOUT * a.ldk * 2);  // [KC]
+  float* v1 = v0 + a.KC;
+  float* v2 = v1 + a.KC;
+  float* red = v2 + a.KC;                                                  // [4][NOUT][3]
+  uint16_t* stage = reinterpret_cast<uint16_t*>(red + 4 * NOUT * 3);      // [4][16][NOUT]
+  uint16_t* my_stage = stage + wid * 16 * NOUT;
+
+  // ---- stage packed weights (16-B copies) and per-channel vectors ----
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(a.wpk + (int64_t)c * a.wpk_ld);
+    uint4* dst = reinterpret_cast<uint4*>(wl);
+    const int n16 = NOUT * a.ldk / 8;
+    for (int i = threadIdx.x; i < n16; i += 256) dst[i] = src[i];
+    if (AOP == AOP_DY || PRO == PRO_BNRELU) {
+      for (int i = threadIdx.x; i < a.KC; i += 256) {
+        v0[i] = a.vec0[(int64_t)c * a.KC + i];
+        v1[i] = a.vec1[(int64_t)c * a.KC + i];
+        if (AOP == AOP_DY) v2[i] = a.vec2[(int64_t)c * a.KC + i];
+      }
+    }
+    for (int i = threadIdx.x; i < 4 * NOUT * 3; i += 256) red[i] = 0.f;
+  }
+  __syncthreads();
+
+  const int64_t src_client = (int64_t)c * a.Nb * a.Hs * a.Ws * a.KC;
+  const uint16_t* src = a.src + src_client;
+  const uint16_t* src2 = (AOP == AOP_DY) ? a.src2 + src_client : nullptr;
+  uint16_t* out = a.out + (int64_t)c * M * NOUT;
+
+  // epilogue per-lane statistics: lane owns the 8 channels (lane % (NOUT/8))*8 .. +7
+  constexpr int CG = NOUT / 8;                 // 16-B chunks per output row
+  constexpr int ROWS_PER_PASS = 64 / CG;       // rows covered by one 64-lane pass (CG ≤ 64)
+  float st0[8], st1[8], st2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { st0[j] = 0.f; st1[j] = 0.f; st2[j] = 0.f; }
+  const int my_cg = lane % CG;
+
+  const int tiles_total = (M + 15) / 16;
+  const int tile0 = (blockIdx.x * 4 + wid) * a.tiles_per_wave;
+  for (int tt = 0; tt < a.tiles_per_wave; ++tt) {
+    const int tile = tile0 + tt;
+    if (tile >= tiles_total) break;
+    const int m = tile * 16 + (lane & 15);
+    const bool mvalid = m < M;
+    const int mm = mvalid ? m : 0;
+    const int on = mm / (a.Ho * a.Wo);
+    const int orem = mm % (a.Ho * a.Wo);
+    const int oh = orem / a.Wo, ow = orem % a.Wo;
+
+    f32x4 acc[NT];
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[nt] = {0.f, 0.f, 0.f, 0.f};
+
+    for (int k0 = 0; k0 < a.Kp; k0 += 32) {
+      const int k = k0 + 8 * (lane >> 4);
+      uint4 av = make_uint4(0, 0, 0, 0);
+      if (mvalid && k < K) {
+        const int tap = k / a.KC, ci = k % a.KC;
+        const int kh = tap / a.KW, kw = tap % a.KW;
+        int ih, iw;
+        bool ok;
+        if (MODE == MODE_FWD) {
+          ih = oh * a.stride - a.pad + kh;
+          iw = ow * a.stride - a.pad + kw;
+          ok = ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws;
+        } else {
+          const int th = oh + a.pad - kh, tw = ow + a.pad - kw;
+          ok = th >= 0 && tw >= 0 && (th % a.stride) == 0 && (tw % a.stride) == 0;
+          ih = th / a.stride;
+          iw = tw / a.stride;
+          ok = ok && ih < a.Hs && iw < a.Ws;
+        }
+        if (ok) {
+          const int64_t off = (((int64_t)on * a.Hs + ih) * a.Ws + iw) * a.KC + ci;
+          const uint4 raw = *reinterpret_cast<const uint4*>(src + off);
+          if (AOP == AOP_ACT && PRO == PRO_NONE) {
+            av = raw;
+          } else {
+            float f[8];
+            unpack8(raw, f);
+            if (AOP == AOP_ACT) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j] * v0[ci + j] + v1[ci + j], 0.f);
+            } else {
+              float yv[8];
+              unpack8(*reinterpret_cast<const uint4*>(src2 + off), yv);
+#pragma unroll
+              for (int j = 0; j < 8; ++j) f[j] = v0[ci + j] * f[j] + v1[ci + j] * yv[j] + v2[ci + j];
+            }
+            av = pack8(f);
+          }
+        }
+      }
+      const bf16x8 afrag = as_bf16x8(av);
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const uint4 bv = *reinterpret_cast<const uint4*>(wl + (nt * 16 + (lane & 15)) * a.ldk + k0 + 8 * (lane >> 4));
+        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag, as_bf16x8(bv), acc[nt], 0, 0, 0);
+      }
+    }
+
+    // ---- stage the 16 × NOUT tile (bf16) in LDS ----
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = 4 * (lane >> 4) + i;
+        my_stage[row * NOUT + nt * 16 + (lane & 15)] = f32_to_bf16(acc[nt][i]);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): LDS writes visible to this wave
+    __builtin_amdgcn_wave_barrier();
+
+    // ---- vectorised epilogue: each lane handles 8 channels of one row per pass ----
+    const int rows_valid = min(16, M - tile * 16);
+#pragma unroll
+    for (int pass = 0; pass < (16 + ROWS_PER_PASS - 1) / ROWS_PER_PASS; ++pass) {
+      const int row = pass * ROWS_PER_PASS + lane / CG;
+      if (lane / CG < ROWS_PER_PASS && row < rows_valid) {
+        const int ch0 = my_cg * 8;
+        const uint4 dv = *reinterpret_cast<const uint4*>(my_stage + row * NOUT + ch0);
+        const int64_t goff = ((int64_t)(tile * 16 + row)) * NOUT + ch0;
+        if (EPI == EPI_FWD || EPI == EPI_STORE) {
+          *reinterpret_cast<uint4*>(out + goff) = dv;
+          if (EPI == EPI_FWD) {
+            float f[8];
+            unpack8(dv, f);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { st0[j] += f[j]; st1[j] += f[j] * f[j]; }
+          }
+        } else {
+          const int64_t eoff = (int64_t)c * M * NOUT + goff;
+          float g[8], xv[8];
+          unpack8(dv, g);
+          unpack8(*reinterpret_cast<const uint4*>(a.e_x + eoff), xv);
+          if (EPI == EPI_MASK) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+              const int ch = ch0 + j;
+              const bool on_ = xv[j] * a.e_s[(int64_t)c * NOUT + ch] + a.e_t[(int64_t)c * NOUT + ch] > 0.f;
+              g[j] = on_ ? g[j] : 0.f;
+            }
+          } else {  // EPI_BLOCK: g = (g + extra) · [block_input > 0]
+            float ex[8];
+            unpack8(*reinterpret_cast<const uint4*>(a.e_add + eoff), ex);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) g[j] = (xv[j] > 0.f) ? g[j] + ex[j] : 0.f;
+          }
+          const uint4 gp = pack8(g);
+          *reinterpret_cast<uint4*>(out + goff) = gp;
+          float gr[8];
+          unpack8(gp, gr);
+          if (EPI == EPI_MASK) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { st0[j] += gr[j]; st1[j] += gr[j] * xv[j]; }
+          } else {
+            float y1[8];
+            unpack8(*reinterpret_cast<const uint4*>(a.e_y1 + eoff), y1);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) { st0[j] += gr[j]; st1[j] += gr[j] * y1[j]; }
+            if (a.e_y2) {
+              float y2[8];
+              unpack8(*reinterpret_cast<const uint4*>(a.e_y2 + eoff), y2);
+#pragma unroll
+              for (int j = 0; j < 8; ++j) st2[j] += gr[j] * y2[j];
+            }
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+
+  // ---- statistics: reduce lanes sharing a channel group, then waves, then one atomic ----
+  if (EPI != EPI_STORE) {
+#pragma unroll
+    for (int o = CG; o < 64; o <<= 1) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        st0[j] += __shfl_xor(st0[j], o, 64);
+        st1[j] += __shfl_xor(st1[j], o, 64);
+        if (EPI == EPI_BLOCK) st2[j] += __shfl_xor(st2[j], o, 64);
+      }
+    }
+    if (lane < CG) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int ch = lane * 8 + j;
+        red[(wid * NOUT + ch) * 3 + 0] = st0[j];
+        red[(wid * NOUT + ch) * 3 + 1] = st1[j];
+        red[(wid * NOUT + ch) * 3 + 2] = st2[j];
+      }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < NOUT * a.NS; i += 256) {
+      const int ch = i / a.NS, q = i % a.NS;
+      const float s = red[(0 * NOUT + ch) * 3 + q] + red[(1 * NOUT + ch) * 3 + q] + red[(2 * NOUT + ch) * 3 + q] +
+                      red[(3 * NOUT + ch) * 3 + q];
+      atomicAdd(&a.stats[((int64_t)c * NOUT + ch) * a.NS + q], s);
+    }
+  }
+}
+
+static size_t conv_smem_bytes(int nout, int ldk, int kc) {
+  return (size_t)nout * ldk * 2 + (size_t)3 * kc * 4 + (size_t)4 * nout * 3 * 4 + (size_t)4 * 16 * nout * 2;
+}
+
+template <int NT, int AOP, int PRO, int MODE, int EPI>
+static int launch_conv(const ConvArgs& a, int C, hipStream_t stream) {
+  const int M = a.Nb * a.Ho * a.Wo;
+  const int tiles = (M + 15) / 16;
+  const int per_wg = 4 * a.tiles_per_wave;
+  const int gx = (tiles + per_wg - 1) / per_wg;
+  const size_t smem = conv_smem_bytes(NT * 16, a.ldk, a.KC);
+  auto kern = conv_gemm_kernel<NT, AOP, PRO, MODE, EPI>;
+  if (smem > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  hipLaunchKernelGGL(kern, dim3(gx, C), dim3(256), smem, stream, a);
+  return (int)hipGetLastError();
+}
+
+template <int AOP, int PRO, int MODE, int EPI>
+static int dispatch_nt(int nout, const ConvArgs& a, int C, hipStream_t s) {
+  switch (nout) {
+    case 16: return launch_conv<1, AOP, PRO, MODE, EPI>(a, C, s);
+    case 32: return launch_conv<2, AOP, PRO, MODE, EPI>(a, C, s);
+    case 64: return launch_conv<4, AOP, PRO, MODE, EPI>(a, C, s);
+    case 128: return launch_conv<8, AOP, PRO, MODE, EPI>(a, C, s);
+    case 256: return launch_conv<16, AOP, PRO, MODE, EPI>(a, C, s);
+    default: return -2;
+  }
+}
+
+// forward: y = conv(pro(x)), stats[c][co][2] += (Σy, Σy²)
+FA_EXPORT int fa_conv_fwd(const uint16_t* x, const uint16_t* wpk, int64_t wpk_ld, const float* pscale,
+                          const float* pshift, uint16_t* y, float* stats, int C, int Nb, int H, int W, int Cin,
+                          int Cout, int KH, int KW, int stride, int pad, int Ho, int Wo, int ldk, int tiles_per_wave,
+                          hipStream_t stream) {
+  if (Cin % 8 != 0) return -3;
+  ConvArgs a = {};
+  a.src = x; a.wpk = wpk; a.wpk_ld = wpk_ld; a.vec0 = pscale; a.vec1 = pshift; a.out = y; a.stats = stats; a.NS = 2;
+  a.Nb = Nb; a.Hs = H; a.Ws = W; a.KC = Cin; a.Ho = Ho; a.Wo = Wo; a.KH = KH; a.KW = KW; a.stride = stride;
+  a.pad = pad; a.ldk = ldk; a.Kp = (KH * KW * Cin + 31) / 32 * 32; a.tiles_per_wave = tiles_per_wave;
+  if (pscale)
+    return dispatch_nt<AOP_ACT, PRO_BNRELU, MODE_FWD, EPI_FWD>(Cout, a, C, stream);
+  return dispatch_nt<AOP_ACT, PRO_NONE, MODE_FWD, EPI_FWD>(Cout, a, C, stream);
+}
+
+// backward-data: dx = convᵀ(α·g + β·y + γ) with epilogue
+//   epi 1 (STORE): out = dx
+//   epi 2 (MASK) : out = g' = dx·[e_x·e_s + e_t > 0];  stats (Σg', Σg'·e_x)
+//   epi 3 (BLOCK): out = g' = (dx + e_add)·[e_x > 0];   stats (Σg', Σg'·e_y1, Σg'·e_y2)
+FA_EXPORT int fa_conv_bwd_data(const uint16_t* g, const uint16_t* yv, const float* alpha, const float* beta,
+                               const float* gamma, const uint16_t* wpk_b, int64_t wpk_ld, uint16_t* dx, int epi,
+                               const uint16_t* e_x, const float* e_s, const float* e_t, const uint16_t* e_add,
+                               const uint16_t* e_y1, const uint16_t* e_y2, float* stats, int C, int Nb, int Hy,
+                               int Wy, int Cout, int Cin, int KH, int KW, int stride, int pad, int Hx, int Wx,
+                               int ldk2, int tiles_per_wave, hipStream_t stream) {
+  if (Cout % 8 != 0) return -3;
+  ConvArgs a = {};
+  a.src = g; a.src2 = yv; a.wpk = wpk_b; a.wpk_ld = wpk_ld; a.vec0 = alpha; a.vec1 = beta; a.vec2 = gamma;
+  a.out = dx; a.e_x = e_x; a.e_s = e_s; a.e_t = e_t; a.e_add = e_add; a.e_y1 = e_y1; a.e_y2 = e_y2;
+  a.stats = stats; a.NS = 3;  // backward statistics are always laid out [C][Ch][3]
+  a.Nb = Nb; a.Hs = Hy; a.Ws = Wy; a.KC = Cout; a.Ho = Hx; a.Wo = Wx; a.KH = KH; a.KW = KW; a.stride = stride;
+  a.pad = pad; a.ldk = ldk2; a.Kp = (KH * KW * Cout + 31) / 32 * 32; a.tiles_per_wave = tiles_per_wave;
+  switch (epi) {
+    case EPI_STORE: return dispatch_nt<AOP_DY, PRO_NONE, MODE_BWD, EPI_STORE>(Cin, a, C, stream);
+    case EPI_MASK: return dispatch_nt<AOP_DY, PRO_NONE, MODE_BWD, EPI_MASK>(Cin, a, C, stream);
+    case EPI_BLOCK: return dispatch_nt<AOP_DY, PRO_NONE, MODE_BWD, EPI_BLOCK>(Cin, a, C, stream);
+    default: return -4;
+  }
+}
+
+// =====================================================================================
+// Backward-weight: dW[co][tap][ci] += Σ_p dy[p][co] · act(x)[p ⊕ tap][ci]
+//   dy = α·g + β·y + γ (BN backward folded), act = PRO ? relu(x·s + t) : x.
+// A workgroup owns one client and a chunk of output pixels; per 32-pixel sub-tile it stages
+// dyᵀ [Cout][32] and im2col(act)ᵀ [K][32] in LDS (bf16, transposed on the way in), then the 4
+// waves run 16×16×32 MFMAs over their share of the Cout×K output tiles, accumulating in
+// registers across the whole chunk. The chunk's partial dW is atomically added (fp32) into the
+// gradient arena at the OIHW position of each element (client stride ldw).
+// =====================================================================================
+template <int TPW, int PRO>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(
+    const uint16_t* __restrict__ g, const uint16_t* __restrict__ yv, const float* __restrict__ alpha,
+    const float* __restrict__ beta, const float* __restrict__ gamma, const uint16_t* __restrict__ x,
+    const float* __restrict__ ps, const float* __restrict__ pt, float* __restrict__ garena, int64_t ldw, int64_t woff,
+    int Nb, int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int pix_per_wg,
+    int cin_src) {
+  const int c = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int K = KH * KW * Cin;
+  const int Kp16 = (K + 15) / 16 * 16;
+  const int M = Nb * Ho * Wo;
+  constexpr int LDP = 32 + 8;  // padded pixel stride in LDS (bf16 elements)
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint16_t* dyT = reinterpret_cast<uint16_t*>(smem);   // [Cout][LDP]
+  uint16_t* aT = dyT + Cout * LDP;                      // [Kp16][LDP]
+  float* vv = reinterpret_cast<float*>(aT + Kp16 * LDP);  // α β γ [Cout] + s t [Cin]
+
+  for (int i = threadIdx.x; i < Cout; i += 256) {
+    vv[i] = alpha[(int64_t)c * Cout + i];
+    vv[Cout + i] = beta[(int64_t)c * Cout + i];
+    vv[2 * Cout + i] = gamma[(int64_t)c * Cout + i];
+  }
+  if (PRO)
+    for (int i = threadIdx.x; i < Cin; i += 256) {
+      vv[3 * Cout + i] = ps[(int64_t)c * Cin + i];
+      vv[3 * Cout + Cin + i] = pt[(int64_t)c * Cin + i];
+    }
+
+  const int MT = Cout / 16, NT2 = Kp16 / 16;
+  const int ntiles = MT * NT2;
+  f32x4 acc[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) acc[t] = {0.f, 0.f, 0.f, 0.f};
+
+  const uint16_t* gc = g + (int64_t)c * M * Cout;
+  const uint16_t* yc = yv + (int64_t)c * M * Cout;
+  const uint16_t* xc = x + (int64_t)c * Nb * H * W * Cin;
+  const int p_begin = blockIdx.x * pix_per_wg;
+  const int p_end = min(M, p_begin + pix_per_wg);
+  __syncthreads();
+
+  for (int p0 = p_begin; p0 < p_end; p0 += 32) {
+    // stage dyᵀ: 32 pixels × Cout channels, 8 channels per thread-iteration
+    const int cg = Cout / 8;
+    for (int i = threadIdx.x; i < 32 * cg; i += 256) {
+      const int pp = i / cg, co0 = (i % cg) * 8;
+      const int p = p0 + pp;
+      float d[8];
+      if (p < p_end) {
+        float gf[8], yf[8];
+        unpack8(*reinterpret_cast<const uint4*>(gc + (int64_t)p * Cout + co0), gf);
+        unpack8(*reinterpret_cast<const uint4*>(yc + (int64_t)p * Cout + co0), yf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] = vv[co0 + j] * gf[j] + vv[Cout + co0 + j] * yf[j] + vv[2 * Cout + co0 + j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d[j] = 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) dyT[(co0 + j) * LDP + pp] = f32_to_bf16(d[j]);
+    }
+    // stage im2col(act)ᵀ: 32 pixels × K (tap-major, 8 input channels per thread-iteration)
+    const int kg = K / 8;
+    for (int i = threadIdx.x; i < 32 * kg; i += 256) {
+      const int pp = i / kg, k0 = (i % kg) * 8;
+      const int p = p0 + pp;
+      const int tap = k0 / Cin, ci0 = k0 % Cin;
+      float f[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) f[j] = 0.f;
+      if (p < p_end) {
+        const int n = p / (Ho * Wo), r = p % (Ho * Wo);
+        const int oh = r / Wo, ow = r % Wo;
+        const int ih = oh * stride - pad + tap / KW, iw = ow * stride - pad + tap % KW;
+        if (ih >= 0 && ih < H && iw >= 0 && iw < W) {
+          unpack8(*reinterpret_cast<const uint4*>(xc + (((int64_t)n * H + ih) * W + iw) * Cin + ci0), f);
+          if (PRO) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j] * vv[3 * Cout + ci0 + j] + vv[3 * Cout + Cin + ci0 + j], 0.f);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) aT[(k0 + j) * LDP + pp] = f32_to_bf16(f[j]);
+    }
+    for (int i = threadIdx.x; i < (Kp16 - K) * 32; i += 256) aT[(K + i / 32) * LDP + (i % 32)] = 0;
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      const int tile = wid + 4 * t;
+      if (tile < ntiles) {
+        const int mt = tile / NT2, nt = tile % NT2;
+        const uint4 av = *reinterpret_cast<const uint4*>(dyT + (mt * 16 + (lane & 15)) * LDP + 8 * (lane >> 4));
+        const uint4 bv = *reinterpret_cast<const uint4*>(aT + (nt * 16 + (lane & 15)) * LDP + 8 * (lane >> 4));
+        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(av), as_bf16x8(bv), acc[t], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  // scatter-add the partial dW into the OIHW gradient (fp32 atomics, client stride ldw)
+  float* gw = garena + (int64_t)c * ldw + woff;
+  const int taps = KH * KW;
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    const int tile = wid + 4 * t;
+    if (tile < ntiles) {
+      const int mt = tile / NT2, nt = tile % NT2;
+      const int k = nt * 16 + (lane & 15);
+      if (k < K) {
+        const int tap = k / Cin, ci = k % Cin;
+        if (ci < cin_src) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int co = mt * 16 + 4 * (lane >> 4) + i;
+            atomicAdd(&gw[((int64_t)co * cin_src + ci) * taps + tap], acc[t][i]);
+          }
+        }
+      }
+    }
+  }
+}
+
+FA_EXPORT int fa_conv_wgrad(const uint16_t* g, const uint16_t* yv, const float* alpha, const float* beta,
+                            const float* gamma, const uint16_t* x, const float* ps, const float* pt, float* garena,
+                            int64_t ldw, int64_t woff, int C, int Nb, int H, int W, int Cin, int Ho, int Wo, int Cout,
+                            int KH, int KW, int stride, int pad, int pix_per_wg, int cin_src, hipStream_t stream) {
+  if (Cin % 8 != 0 || Cout % 16 != 0) return -3;
+  const int K = KH * KW * Cin;
+  const int Kp16 = (K + 15) / 16 * 16;
+  const int ntiles = (Cout / 16) * (Kp16 / 16);
+  const int tpw = (ntiles + 3) / 4;
+  const int M = Nb * Ho * Wo;
+  const int gx = (M + pix_per_wg - 1) / pix_per_wg;
+  const size_t smem = (size_t)(Cout + Kp16) * 40 * 2 + (size_t)(3 * Cout + 2 * Cin) * 4;
+  dim3 grid(gx, C);
+#define WG_LAUNCH(T)                                                                                          \
+  {                                                                                                           \
+    auto kern = ps ? conv_wgrad_kernel<T, 1> : conv_wgrad_kernel<T, 0>;                                       \
+    if (smem > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,  \
+                                              (int)smem);                                                     \
+    hipLaunchKernelGGL(kern, grid, dim3(256), smem, stream, g, yv, alpha, beta, gamma, x, ps, pt, garena, ldw, \
+                       woff, Nb, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, pix_per_wg, cin_src);                   \
+  }
+  if (tpw <= 4) WG_LAUNCH(4)
+  else if (tpw <= 8) WG_LAUNCH(8)
+  else if (tpw <= 16) WG_LAUNCH(16)
+  else if (tpw <= 36) WG_LAUNCH(36)
+  else if (tpw <= 72) WG_LAUNCH(72)
+  else return -5;
+#undef WG_LAUNCH
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,111 @@
+"""ctypes bindings for the client-batched NN kernels (``csrc/conv_kernels.hip``, ``csrc/bn_kernels.hip``).
+
+All tensors are CUDA(HIP) tensors; layouts are documented in the .hip files. These are thin
+launchers — the model-level orchestration lives in ``parallel.native_resnet``.
+"""
+import ctypes
+
+import torch
+
+from . import _native
+from .fl_ops import _check, _f, _fn, _i64, _p, _stream
+
+_c = ctypes
+
+
+def _i(v):
+    return _c.c_int(int(v))
+
+
+class PackSeg(ctypes.Structure):
+    _fields_ = [("src_off", ctypes.c_int64), ("dst_f", ctypes.c_int64), ("dst_b", ctypes.c_int64),
+                ("cout", ctypes.c_int), ("cin", ctypes.c_int), ("kh", ctypes.c_int), ("kw", ctypes.c_int),
+                ("ldk", ctypes.c_int), ("ldk2", ctypes.c_int), ("cin_src", ctypes.c_int)]
+
+
+def pack_weights(arena, segs_dev, nseg, dst, dst_ld, C):
+    rc = _fn("fa_pack_weights")(_p(arena), _i64(arena.stride(0)), _p(segs_dev), _i(nseg), _p(dst), _i64(dst_ld),
+                                _i(C), _stream(arena))
+    _check(rc, "fa_pack_weights")
+
+
+def conv_fwd(x, wpk, wpk_ld, pscale, pshift, y, stats, C, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, ldk,
+             tiles_per_wave):
+    rc = _fn("fa_conv_fwd")(_p(x), _p(wpk), _i64(wpk_ld), _p(pscale), _p(pshift), _p(y), _p(stats), _i(C), _i(N),
+                            _i(H), _i(W), _i(Cin), _i(Cout), _i(KH), _i(KW), _i(stride), _i(pad), _i(Ho), _i(Wo),
+                            _i(ldk), _i(tiles_per_wave), _stream(x))
+    _check(rc, "fa_conv_fwd")
+
+
+EPI_STORE, EPI_MASK, EPI_BLOCK = 1, 2, 3
+
+
+def conv_bwd_data(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, dx, epi, e_x, e_s, e_t, e_add, e_y1, e_y2, stats, C, N,
+                  Hy, Wy, Cout, Cin, KH, KW, stride, pad, Hx, Wx, ldk2, tiles_per_wave):
+    rc = _fn("fa_conv_bwd_data")(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(wpk_b), _i64(wpk_ld), _p(dx),
+                                 _i(epi), _p(e_x), _p(e_s), _p(e_t), _p(e_add), _p(e_y1), _p(e_y2), _p(stats), _i(C),
+                                 _i(N), _i(Hy), _i(Wy), _i(Cout), _i(Cin), _i(KH), _i(KW), _i(stride), _i(pad),
+                                 _i(Hx), _i(Wx), _i(ldk2), _i(tiles_per_wave), _stream(g))
+    _check(rc, "fa_conv_bwd_data")
+
+
+def conv_wgrad(g, yv, alpha, beta, gamma, x, ps, pt, garena, woff, C, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
+               pad, pix_per_wg, cin_src):
+    rc = _fn("fa_conv_wgrad")(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(x), _p(ps), _p(pt), _p(garena),
+                              _i64(garena.stride(0)), _i64(woff), _i(C), _i(N), _i(H), _i(W), _i(Cin), _i(Ho), _i(Wo),
+                              _i(Cout), _i(KH), _i(KW), _i(stride), _i(pad), _i(pix_per_wg), _i(cin_src), _stream(g))
+    _check(rc, "fa_conv_wgrad")
+
+
+def bn_fwd_finalize(stats, C, Ch, n, arena, off_gamma, off_beta, off_rm, off_rv, off_nbt, momentum, eps, active,
+                    scale, shift, mean, rstd, update_running=True):
+    rc = _fn("fa_bn_fwd_finalize")(_p(stats), _i(C), _i(Ch), _f(n), _p(arena), _i64(arena.stride(0)),
+                                   _i64(off_gamma), _i64(off_beta), _i64(off_rm), _i64(off_rv), _i64(off_nbt),
+                                   _f(momentum), _f(eps), _p(active), _p(scale), _p(shift), _p(mean), _p(rstd),
+                                   _i(int(update_running)), _stream(stats))
+    _check(rc, "fa_bn_fwd_finalize")
+
+
+def bn_bwd_finalize(bstats, NS, q_gy, C, Ch, n, mean, rstd, arena, garena, off_gamma, off_beta, alpha, beta_c,
+                    gamma_c):
+    rc = _fn("fa_bn_bwd_finalize")(_p(bstats), _i(NS), _i(q_gy), _i(C), _i(Ch), _f(n), _p(mean), _p(rstd),
+                                   _p(arena), _p(garena), _i64(arena.stride(0)), _i64(off_gamma), _i64(off_beta),
+                                   _p(alpha), _p(beta_c), _p(gamma_c), _stream(bstats))
+    _check(rc, "fa_bn_bwd_finalize")
+
+
+def block_out(y, s, t, r, rs, rt, out, C, per_client, Ch):
+    rc = _fn("fa_block_out")(_p(y), _p(s), _p(t), _p(r), _p(rs), _p(rt), _p(out), _i(C), _i64(per_client), _i(Ch),
+                             _stream(y))
+    _check(rc, "fa_block_out")
+
+
+def avgpool(x, pooled, CN, HW, Ch):
+    rc = _fn("fa_avgpool")(_p(x), _p(pooled), _i(CN), _i(HW), _i(Ch), _stream(x))
+    _check(rc, "fa_avgpool")
+
+
+def head_bwd(dpool, out, y3, yd, gpre, stats, C, N, HW, Ch, NS):
+    rc = _fn("fa_head_bwd")(_p(dpool), _p(out), _p(y3), _p(yd), _p(gpre), _p(stats), _i(C), _i(N), _i(HW), _i(Ch),
+                            _i(NS), _stream(out))
+    _check(rc, "fa_head_bwd")
+
+
+def nchw_to_nhwc_pad(x, y, CN, Cin, HW, Cpad):
+    rc = _fn("fa_nchw_to_nhwc_pad")(_p(x), _p(y), _i64(CN), _i(Cin), _i(HW), _i(Cpad), _stream(x))
+    _check(rc, "fa_nchw_to_nhwc_pad")
+
+
+class NativeBatchedOps:
+    """Marker object handed to the fx interpreter; the native executor is model-level instead."""
+
+    def __init__(self, C, compute_dtype):
+        _native.lib(required=True)
+        self.C = C
+        self.compute_dtype = compute_dtype
+
+    def supports_conv(self, m, x):
+        return False
+
+    def conv2d(self, x, w, b, C, m):  # pragma: no cover - not used (model-level executor)
+        raise NotImplementedError

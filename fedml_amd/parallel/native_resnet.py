@@ -1,0 +1,424 @@
+"""Native client-batched ResNet training step (forward + backward) on the HIP kernels.
+
+Executes one local SGD step for C virtual clients at once on CIFAR-style ResNets
+(``models.cv.resnet.ResNet`` with Bottleneck / BasicBlock blocks — ResNet-56/110, and
+``ResNet18Cifar``), reading weights from and writing gradients to the client-stacked
+fp32 arenas [C, P] directly. Activations are bf16 NHWC per client; every BatchNorm is
+folded into its neighbours' kernels (forward: consumer operand load + producer epilogue
+statistics; backward: consumer operand load + producer epilogue statistics), so each
+activation tensor is written once and read by exactly the kernels that need it.
+
+Per block (k chained convs, last BN joins the residual):
+  forward   y0 = conv(act_in) ; y_j = conv(relu(bn_{j-1}(y_{j-1}))) ; [yd = conv_ds(act_in)]
+            out = relu(bn_{k-1}(y_{k-1}) + (bn_d(yd) | act_in))
+  backward  dy_j = α_j g_j + β_j y_j + γ_j  (folded BN backward, from Σg, Σg·y)
+            wgrad_j(dy_j, act(y_{j-1})) ; g_{j-1} = bwd_data_j(dy_j) · mask  (+ stats)
+            conv_0 bwd-data adds the shortcut gradient, applies the previous block's ReLU mask and
+            produces the previous block's g and BN statistics in its epilogue.
+"""
+import ctypes
+import math
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import torch
+import torch.nn as nn
+
+from ..ops import nn_ops
+from ..ops.fl_ops import softmax_xent_fwd_bwd
+
+
+@dataclass
+class ConvSpec:
+    key: str
+    cin: int
+    cout: int
+    k: int
+    stride: int
+    pad: int
+    cin_pad: int
+    H: int = 0          # input spatial
+    W: int = 0
+    Ho: int = 0
+    Wo: int = 0
+    ldk: int = 0
+    ldk2: int = 0
+    off_f: int = 0      # packed-buffer offsets (elements, per client)
+    off_b: int = -1
+
+
+@dataclass
+class BNSpec:
+    key: str
+    ch: int
+    eps: float
+    momentum: float
+
+
+@dataclass
+class BlockSpec:
+    convs: List[ConvSpec]
+    bns: List[BNSpec]
+    ds_conv: Optional[ConvSpec] = None
+    ds_bn: Optional[BNSpec] = None
+    # runtime buffers
+    ys: list = field(default_factory=list)
+    yd: Optional[torch.Tensor] = None
+    out: Optional[torch.Tensor] = None
+
+
+class UnsupportedNative(Exception):
+    pass
+
+
+def _round_up(v, m):
+    return (v + m - 1) // m * m
+
+
+def _conv_spec(name, m: nn.Conv2d) -> ConvSpec:
+    if m.groups != 1 or m.dilation != (1, 1) or m.bias is not None or m.kernel_size[0] != m.kernel_size[1]:
+        raise UnsupportedNative(f"conv {name}: unsupported config")
+    cin = m.in_channels
+    cin_pad = _round_up(cin, 8)
+    if m.out_channels % 16 != 0 or m.out_channels > 256 or (cin_pad > 256 and cin_pad != cin):
+        raise UnsupportedNative(f"conv {name}: channels {cin}->{m.out_channels}")
+    return ConvSpec(f"{name}.weight", cin, m.out_channels, m.kernel_size[0], m.stride[0], m.padding[0], cin_pad)
+
+
+def _bn_spec(name, m: nn.BatchNorm2d) -> BNSpec:
+    if not m.affine or not m.track_running_stats:
+        raise UnsupportedNative(f"bn {name}")
+    return BNSpec(name, m.num_features, m.eps, m.momentum if m.momentum is not None else 0.1)
+
+
+def parse_resnet(model: nn.Module):
+    from ..models.cv.resnet import BasicBlock, Bottleneck, ResNet, ResNet18Cifar
+    if not isinstance(model, (ResNet, ResNet18Cifar)):
+        raise UnsupportedNative(type(model).__name__)
+    if getattr(model, "KD", False):
+        raise UnsupportedNative("KD output")
+    stem = (_conv_spec("conv1", model.conv1), _bn_spec("bn1", model.bn1))
+    blocks = []
+    layers = [model.layer1, model.layer2, model.layer3] + ([model.layer4] if hasattr(model, "layer4") else [])
+    for li, layer in enumerate(layers):
+        for bi, blk in enumerate(layer):
+            pre = f"layer{li + 1}.{bi}"
+            if isinstance(blk, Bottleneck):
+                convs = [_conv_spec(f"{pre}.conv{j}", getattr(blk, f"conv{j}")) for j in (1, 2, 3)]
+                bns = [_bn_spec(f"{pre}.bn{j}", getattr(blk, f"bn{j}")) for j in (1, 2, 3)]
+            elif isinstance(blk, BasicBlock):
+                convs = [_conv_spec(f"{pre}.conv{j}", getattr(blk, f"conv{j}")) for j in (1, 2)]
+                bns = [_bn_spec(f"{pre}.bn{j}", getattr(blk, f"bn{j}")) for j in (1, 2)]
+            else:
+                raise UnsupportedNative(type(blk).__name__)
+            b = BlockSpec(convs, bns)
+            if blk.downsample is not None:
+                b.ds_conv = _conv_spec(f"{pre}.downsample.0", blk.downsample[0])
+                b.ds_bn = _bn_spec(f"{pre}.downsample.1", blk.downsample[1])
+            blocks.append(b)
+    if not isinstance(model.avgpool, nn.AdaptiveAvgPool2d) or tuple(
+            model.avgpool.output_size if isinstance(model.avgpool.output_size, tuple)
+            else (model.avgpool.output_size,) * 2) != (1, 1):
+        raise UnsupportedNative("avgpool")
+    return stem, blocks, model.fc
+
+
+class NativeResNetStep:
+    """Owns the activation / statistics buffers for one (C, N, H, W) geometry."""
+
+    def __init__(self, model: nn.Module, layout, C: int, device):
+        self.layout = layout
+        self.C = C
+        self.device = torch.device(device)
+        self.stem, self.blocks, fc = parse_resnet(model)
+        self.fc_in = fc.in_features
+        self.fc_out = fc.out_features
+        self.off = {s.key: s.offset for s in layout.slots}
+        self.geom = None
+        self._segs = None
+
+    # ------------------------------------------------------------------ setup
+    def _all_convs(self):
+        yield self.stem[0]
+        for b in self.blocks:
+            yield from b.convs
+            if b.ds_conv is not None:
+                yield b.ds_conv
+
+    def _setup(self, N, H, W):
+        C = self.C
+        dev = self.device
+        # geometry
+        st = self.stem[0]
+        st.H, st.W = H, W
+        st.Ho = (H + 2 * st.pad - st.k) // st.stride + 1
+        st.Wo = (W + 2 * st.pad - st.k) // st.stride + 1
+        h, w = st.Ho, st.Wo
+        for b in self.blocks:
+            hin, win = h, w
+            for cv in b.convs:
+                cv.H, cv.W = h, w
+                cv.Ho = (h + 2 * cv.pad - cv.k) // cv.stride + 1
+                cv.Wo = (w + 2 * cv.pad - cv.k) // cv.stride + 1
+                h, w = cv.Ho, cv.Wo
+            if b.ds_conv is not None:
+                d = b.ds_conv
+                d.H, d.W = hin, win
+                d.Ho = (hin + 2 * d.pad - d.k) // d.stride + 1
+                d.Wo = (win + 2 * d.pad - d.k) // d.stride + 1
+        self.final_hw = (h, w)
+        # packed weight layout
+        segs = []
+        off = 0
+        for i, cv in enumerate(self._all_convs()):
+            K = cv.k * cv.k * cv.cin_pad
+            cv.ldk = _round_up(K, 32) + 8
+            cv.off_f = off
+            off += cv.cout * cv.ldk
+            off = _round_up(off, 8)
+            if cv is not self.stem[0]:
+                K2 = cv.k * cv.k * cv.cout
+                cv.ldk2 = _round_up(K2, 32) + 8
+                cv.off_b = off
+                off += cv.cin_pad * cv.ldk2
+                off = _round_up(off, 8)
+            else:
+                cv.off_b = -1
+                cv.ldk2 = 0
+            segs.append((self.off[cv.key], cv.off_f, cv.off_b, cv.cout, cv.cin_pad, cv.k, cv.k, cv.ldk, cv.ldk2,
+                         cv.cin))
+        self.packed_ld = _round_up(off, 64)
+        self.packed = torch.zeros(C, self.packed_ld, dtype=torch.bfloat16, device=dev)
+        arr = (nn_ops.PackSeg * len(segs))(*[nn_ops.PackSeg(*s) for s in segs])
+        raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+        self._segs = raw.to(dev)
+        self._nseg = len(segs)
+        # activations (bf16) and per-BN vectors
+        bf = torch.bfloat16
+
+        def act(hh, ww, ch):
+            return torch.empty(C, N, hh, ww, ch, dtype=bf, device=dev)
+
+        self.x_in = act(H, W, st.cin_pad)
+        self.stem_y = act(st.Ho, st.Wo, st.cout)
+        self.stem_out = act(st.Ho, st.Wo, st.cout)
+        maxel = st.Ho * st.Wo * st.cout
+        for b in self.blocks:
+            b.ys = [act(cv.Ho, cv.Wo, cv.cout) for cv in b.convs]
+            b.yd = act(b.ds_conv.Ho, b.ds_conv.Wo, b.ds_conv.cout) if b.ds_conv is not None else None
+            last = b.convs[-1]
+            b.out = act(last.Ho, last.Wo, last.cout)
+            for cv in b.convs + ([b.ds_conv] if b.ds_conv else []):
+                maxel = max(maxel, cv.H * cv.W * cv.cin_pad, cv.Ho * cv.Wo * cv.cout)
+        # gradient scratch: block-output g (kept until the block's conv0 is done), two ping-pong
+        # buffers for the inner chain, one for the shortcut gradient
+        self.gbuf = [torch.empty(C * N * maxel, dtype=bf, device=dev) for _ in range(4)]
+        # per-BN vectors: scale, shift, mean, rstd, alpha, beta, gamma   + stats
+        self.bn_vec = {}
+        nstat = 0
+        for bn in self._all_bns():
+            self.bn_vec[bn.key] = torch.empty(7, C, bn.ch, dtype=torch.float32, device=dev)
+            nstat += bn.ch * 5
+        self.stats = torch.zeros(C * nstat, dtype=torch.float32, device=dev)
+        self.stat_views = {}
+        o = 0
+        for bn in self._all_bns():
+            fwd = self.stats[o:o + C * bn.ch * 2].view(C, bn.ch, 2)
+            o += C * bn.ch * 2
+            bwd = self.stats[o:o + C * bn.ch * 3].view(C, bn.ch, 3)
+            o += C * bn.ch * 3
+            self.stat_views[bn.key] = (fwd, bwd)
+        fh, fw = self.final_hw
+        self.pooled = torch.empty(C, N, self.fc_in, dtype=torch.float32, device=dev)
+        self.geom = (N, H, W)
+
+    def _all_bns(self):
+        yield self.stem[1]
+        for b in self.blocks:
+            yield from b.bns
+            if b.ds_bn is not None:
+                yield b.ds_bn
+
+    # ------------------------------------------------------------------ helpers
+    def _tiles_per_wave(self, M):
+        tiles = (M + 15) // 16
+        target_wgs = 2048
+        tpw = max(1, min(16, (tiles * self.C) // (4 * target_wgs)))
+        return tpw
+
+    def _pix_per_wg(self, M):
+        per = max(256, _round_up((M * self.C) // 1024, 32))
+        return min(per, _round_up(M, 32))
+
+    def _bn_offsets(self, bn):
+        o = self.off
+        return (o[f"{bn.key}.weight"], o[f"{bn.key}.bias"], o[f"{bn.key}.running_mean"],
+                o[f"{bn.key}.running_var"], o.get(f"{bn.key}.num_batches_tracked", -1))
+
+    def _conv_fwd(self, cv, x, pro_bn, y, N):
+        vec = self.bn_vec[pro_bn.key] if pro_bn is not None else None
+        fst = None
+        # the stats buffer of the BN that follows this conv is resolved by the caller
+        return vec
+
+    def _fwd(self, cv: ConvSpec, x, y, pro_vec, stats, N):
+        M = N * cv.Ho * cv.Wo
+        nn_ops.conv_fwd(x, self.packed.view(-1)[cv.off_f:], self.packed_ld, pro_vec[0] if pro_vec is not None else None,
+                        pro_vec[1] if pro_vec is not None else None, y, stats, self.C, N, cv.H, cv.W, cv.cin_pad,
+                        cv.cout, cv.k, cv.k, cv.stride, cv.pad, cv.Ho, cv.Wo, cv.ldk, self._tiles_per_wave(M))
+
+    def _bn_fwd(self, bn, N, hw, arena, active, training=True):
+        v = self.bn_vec[bn.key]
+        fst = self.stat_views[bn.key][0]
+        g, b, rm, rv, nbt = self._bn_offsets(bn)
+        nn_ops.bn_fwd_finalize(fst, self.C, bn.ch, float(N * hw), arena, g, b, rm, rv, nbt, bn.momentum, bn.eps,
+                               active, v[0], v[1], v[2], v[3], training)
+
+    def _bn_bwd(self, bn, q, N, hw, arena, garena):
+        v = self.bn_vec[bn.key]
+        bst = self.stat_views[bn.key][1]
+        g, b = self.off[f"{bn.key}.weight"], self.off[f"{bn.key}.bias"]
+        nn_ops.bn_bwd_finalize(bst, 3, q, self.C, bn.ch, float(N * hw), v[2], v[3], arena, garena, g, b, v[4], v[5],
+                               v[6])
+
+    # ------------------------------------------------------------------ step
+    def step(self, arena, garena, x, labels, row_scale, active):
+        """x [C, N, Cin, H, W] fp32, labels [C, N] → summed per-client mean loss (device scalar).
+        Fills ``garena`` (must be zeroed by the caller) with this step's gradients."""
+        C, N = x.shape[0], x.shape[1]
+        H, W = x.shape[3], x.shape[4]
+        if self.geom != (N, H, W):
+            self._setup(N, H, W)
+        self.stats.zero_()
+        nn_ops.pack_weights(arena, self._segs, self._nseg, self.packed, self.packed_ld, C)
+        st_conv, st_bn = self.stem
+        nn_ops.nchw_to_nhwc_pad(x.contiguous(), self.x_in, C * N, st_conv.cin, H * W, st_conv.cin_pad)
+
+        # ---------------- forward ----------------
+        self._fwd(st_conv, self.x_in, self.stem_y, None, self.stat_views[st_bn.key][0], N)
+        self._bn_fwd(st_bn, N, st_conv.Ho * st_conv.Wo, arena, active)
+        v0 = self.bn_vec[st_bn.key]
+        nn_ops.block_out(self.stem_y, v0[0], v0[1], None, None, None, self.stem_out, C,
+                         N * st_conv.Ho * st_conv.Wo * st_conv.cout, st_conv.cout)
+        act_in = self.stem_out
+        for b in self.blocks:
+            b.act_in = act_in
+            prev = None
+            for j, (cv, bn) in enumerate(zip(b.convs, b.bns)):
+                src = act_in if j == 0 else b.ys[j - 1]
+                pro = None if j == 0 else self.bn_vec[b.bns[j - 1].key]
+                self._fwd(cv, src, b.ys[j], pro, self.stat_views[bn.key][0], N)
+                self._bn_fwd(bn, N, cv.Ho * cv.Wo, arena, active)
+            last, lbn = b.convs[-1], b.bns[-1]
+            vl = self.bn_vec[lbn.key]
+            if b.ds_conv is not None:
+                d = b.ds_conv
+                self._fwd(d, act_in, b.yd, None, self.stat_views[b.ds_bn.key][0], N)
+                self._bn_fwd(b.ds_bn, N, d.Ho * d.Wo, arena, active)
+                vd = self.bn_vec[b.ds_bn.key]
+                nn_ops.block_out(b.ys[-1], vl[0], vl[1], b.yd, vd[0], vd[1], b.out, C,
+                                 N * last.Ho * last.Wo * last.cout, last.cout)
+            else:
+                nn_ops.block_out(b.ys[-1], vl[0], vl[1], act_in, None, None, b.out, C,
+                                 N * last.Ho * last.Wo * last.cout, last.cout)
+            act_in = b.out
+        fh, fw = self.final_hw
+        chl = self.blocks[-1].convs[-1].cout
+        nn_ops.avgpool(act_in, self.pooled, C * N, fh * fw, chl)
+        # ---------------- head: fc + fused CE (fp32, tiny) ----------------
+        ow = self.off["fc.weight"]
+        ob = self.off["fc.bias"]
+        Wfc = arena[:, ow:ow + self.fc_out * self.fc_in].view(C, self.fc_out, self.fc_in)
+        bfc = arena[:, ob:ob + self.fc_out]
+        logits = torch.baddbmm(bfc.unsqueeze(1), self.pooled, Wfc.transpose(1, 2))       # [C, N, K]
+        loss_rows, dlogits = softmax_xent_fwd_bwd(logits.view(C * N, -1), labels.reshape(-1), None,
+                                                  row_scale.reshape(-1))
+        loss = (loss_rows * row_scale.reshape(-1)).sum()
+        dl = dlogits.view(C, N, -1)
+        gW = garena[:, ow:ow + self.fc_out * self.fc_in].view(C, self.fc_out, self.fc_in)
+        gW.add_(torch.bmm(dl.transpose(1, 2), self.pooled))
+        garena[:, ob:ob + self.fc_out].add_(dl.sum(1))
+        dpool = torch.bmm(dl, Wfc)                                                         # [C, N, fc_in]
+
+        # ---------------- backward ----------------
+        bufs = list(self.gbuf)
+        gpre = bufs[0]
+        bl = self.blocks[-1]
+        nn_ops.head_bwd(dpool, bl.out, bl.ys[-1], bl.yd, gpre, self.stat_views[bl.bns[-1].key][1].view(-1), C, N,
+                        fh * fw, chl, 3)
+        # head_bwd wrote (Σg, Σg·y_last, Σg·yd) into the last BN's bwd stats; the downsample BN needs
+        # (Σg, Σg·yd) → copy slots into its own stats buffer below (same g)
+        for bi in range(len(self.blocks) - 1, -1, -1):
+            b = self.blocks[bi]
+            prev_block = self.blocks[bi - 1] if bi > 0 else None
+            lbn = b.bns[-1]
+            last = b.convs[-1]
+            hw_last = last.Ho * last.Wo
+            self._bn_bwd(lbn, 1, N, hw_last, arena, garena)
+            if b.ds_bn is not None:
+                # the shortcut BN sees the same g: its (Σg, Σg·yd) live in slots 0 and 2 of lbn's stats
+                self.stat_views[b.ds_bn.key][1].copy_(self.stat_views[lbn.key][1])
+                self._bn_bwd(b.ds_bn, 2, N, b.ds_conv.Ho * b.ds_conv.Wo, arena, garena)
+            free = [t for t in bufs if t is not gpre]           # three buffers besides gpre
+            g_j = gpre  # gradient at the output of conv j (pre-BN), starting with the last conv
+            for j in range(len(b.convs) - 1, 0, -1):
+                cv, bn = b.convs[j], b.bns[j]
+                v = self.bn_vec[bn.key]
+                pv = self.bn_vec[b.bns[j - 1].key]
+                M = N * cv.Ho * cv.Wo
+                nn_ops.conv_wgrad(g_j, b.ys[j], v[4], v[5], v[6], b.ys[j - 1], pv[0], pv[1], garena,
+                                  self.off[cv.key], C, N, cv.H, cv.W, cv.cin_pad, cv.Ho, cv.Wo, cv.cout, cv.k, cv.k,
+                                  cv.stride, cv.pad, self._pix_per_wg(M), cv.cin)
+                out_g = free[0] if g_j is not free[0] else free[1]
+                nn_ops.conv_bwd_data(g_j, b.ys[j], v[4], v[5], v[6], self.packed.view(-1)[cv.off_b:],
+                                     self.packed_ld, out_g, nn_ops.EPI_MASK, b.ys[j - 1], pv[0], pv[1], None, None,
+                                     None, self.stat_views[b.bns[j - 1].key][1], C, N, cv.Ho, cv.Wo, cv.cout,
+                                     cv.cin_pad, cv.k, cv.k, cv.stride, cv.pad, cv.H, cv.W, cv.ldk2,
+                                     self._tiles_per_wave(N * cv.H * cv.W))
+                self._bn_bwd(b.bns[j - 1], 1, N, cv.H * cv.W, arena, garena)
+                g_j = out_g
+            # shortcut gradient D into free[2] (downsample) or the block's own gpre (identity)
+            gadd = free[2]
+            if b.ds_conv is not None:
+                d = b.ds_conv
+                vd = self.bn_vec[b.ds_bn.key]
+                nn_ops.conv_wgrad(gpre, b.yd, vd[4], vd[5], vd[6], b.act_in, None, None, garena, self.off[d.key], C, N,
+                                  d.H, d.W, d.cin_pad, d.Ho, d.Wo, d.cout, d.k, d.k, d.stride, d.pad,
+                                  self._pix_per_wg(N * d.Ho * d.Wo), d.cin)
+                nn_ops.conv_bwd_data(gpre, b.yd, vd[4], vd[5], vd[6], self.packed.view(-1)[d.off_b:], self.packed_ld,
+                                     gadd, nn_ops.EPI_STORE, None, None, None, None, None, None, self.stats, C, N,
+                                     d.Ho, d.Wo, d.cout, d.cin_pad, d.k, d.k, d.stride, d.pad, d.H, d.W, d.ldk2,
+                                     self._tiles_per_wave(N * d.H * d.W))
+                shortcut = gadd
+            else:
+                shortcut = gpre
+            # conv 0: weight grad, then data grad with the block epilogue (→ previous block's g)
+            cv0, bn0 = b.convs[0], b.bns[0]
+            v = self.bn_vec[bn0.key]
+            nn_ops.conv_wgrad(g_j, b.ys[0], v[4], v[5], v[6], b.act_in, None, None, garena, self.off[cv0.key], C, N,
+                              cv0.H, cv0.W, cv0.cin_pad, cv0.Ho, cv0.Wo, cv0.cout, cv0.k, cv0.k, cv0.stride, cv0.pad,
+                              self._pix_per_wg(N * cv0.Ho * cv0.Wo), cv0.cin)
+            if prev_block is not None:
+                ey1, ey2 = prev_block.ys[-1], prev_block.yd
+                pstats = self.stat_views[prev_block.bns[-1].key][1]
+            else:
+                ey1, ey2 = self.stem_y, None
+                pstats = self.stat_views[st_bn.key][1]
+            # output buffer must differ from g_j and the shortcut source (gpre itself is free again once
+            # the downsample path has consumed it)
+            busy = {id(g_j), id(shortcut)}
+            out_buf = next(t for t in bufs if id(t) not in busy)
+            nn_ops.conv_bwd_data(g_j, b.ys[0], v[4], v[5], v[6], self.packed.view(-1)[cv0.off_b:], self.packed_ld,
+                                 out_buf, nn_ops.EPI_BLOCK, b.act_in, None, None, shortcut, ey1, ey2, pstats, C, N,
+                                 cv0.Ho, cv0.Wo, cv0.cout, cv0.cin_pad, cv0.k, cv0.k, cv0.stride, cv0.pad, cv0.H,
+                                 cv0.W, cv0.ldk2, self._tiles_per_wave(N * cv0.H * cv0.W))
+            # the previous block's gpre is out_buf
+            gpre = out_buf
+        # stem backward: bn0 bwd then weight grad only
+        self._bn_bwd(st_bn, 1, N, st_conv.Ho * st_conv.Wo, arena, garena)
+        v = self.bn_vec[st_bn.key]
+        nn_ops.conv_wgrad(gpre, self.stem_y, v[4], v[5], v[6], self.x_in, None, None, garena, self.off[st_conv.key], C,
+                          N, st_conv.H, st_conv.W, st_conv.cin_pad, st_conv.Ho, st_conv.Wo, st_conv.cout, st_conv.k,
+                          st_conv.k, st_conv.stride, st_conv.pad, self._pix_per_wg(N * st_conv.Ho * st_conv.Wo),
+                          st_conv.cin)
+        return loss.detach()

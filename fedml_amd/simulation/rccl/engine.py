@@ -14,6 +14,7 @@ all-reduce.
 """
 import logging
 import math
+import os
 from typing import List, Optional
 
 import torch
@@ -49,13 +50,14 @@ class ClientBatchEngine:
             self.step_t = torch.zeros(self.C, dtype=torch.float32, device=self.device)
         self.interp = BatchedInterpreter(model, self.layout, self.C)
         self.native = None
-        if self.device.type == "cuda":
+        self.native_step = None
+        if self.device.type == "cuda" and os.environ.get("FEDML_AMD_NATIVE_CONV", "1") != "0":
+            from ...parallel.native_resnet import NativeResNetStep, UnsupportedNative
             try:
-                from ...ops import nn_ops
-                self.native = nn_ops.NativeBatchedOps(self.C, self.compute_dtype)
-                self.interp.native = self.native
-            except (ImportError, AttributeError):
-                self.native = None
+                self.native_step = NativeResNetStep(model, self.layout, self.C, self.device)
+                logging.info("virtual-client engine: native HIP ResNet path (C=%d)", self.C)
+            except UnsupportedNative as e:
+                logging.info("virtual-client engine: torch batched path (%s)", e)
         self._build_views()
         self.global_ref = None
         self.loss_history: List[float] = []
@@ -129,6 +131,10 @@ class ClientBatchEngine:
 
     def _step_loss(self, x, y, mask, b_c, active, sample_mask, use_native_loss):
         self.grads.zero_()
+        if self.native_step is not None and sample_mask is None:
+            bc = torch.tensor([max(1, b) for b in b_c], dtype=torch.float32, device=self.device)
+            row_scale = mask.to(torch.float32) / bc.view(-1, 1)
+            return self.native_step.step(self.params, self.grads, x, y, row_scale, active)
         out = self.interp.run(self.views, x, training=True, sample_mask=sample_mask, active=active,
                               dtype=self.compute_dtype)                       # [C, B, K]
         C, B = out.shape[0], out.shape[1]
