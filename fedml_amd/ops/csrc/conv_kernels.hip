@@ -426,168 +426,3 @@ FA_EXPORT int fa_conv_bwd_data(const uint16_t* g, const uint16_t* yv, const floa
     default: return -4;
   }
 }
-
-// =====================================================================================
-// Backward-weight: dW[co][tap][ci] += Σ_p dy[p][co] · act(x)[p ⊕ tap][ci]
-//   dy = α·g + β·y + γ (BN backward folded), act = PRO ? relu(x·s + t) : x.
-// A workgroup owns one client and a chunk of output pixels; per 32-pixel sub-tile it stages
-// dyᵀ [Cout][32] and im2col(act)ᵀ [K][32] in LDS (bf16, transposed on the way in), then the 4
-// waves run 16×16×32 MFMAs over their share of the Cout×K output tiles, accumulating in
-// registers across the whole chunk. The chunk's partial dW is atomically added (fp32) into the
-// gradient arena at the OIHW position of each element (client stride ldw).
-// =====================================================================================
-template <int TPW, int PRO>
-__global__ __launch_bounds__(256) void conv_wgrad_kernel(
-    const uint16_t* __restrict__ g, const uint16_t* __restrict__ yv, const float* __restrict__ alpha,
-    const float* __restrict__ beta, const float* __restrict__ gamma, const uint16_t* __restrict__ x,
-    const float* __restrict__ ps, const float* __restrict__ pt, float* __restrict__ garena, int64_t ldw, int64_t woff,
-    int Nb, int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int pix_per_wg,
-    int cin_src) {
-  const int c = blockIdx.y;
-  const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
-  const int K = KH * KW * Cin;
-  const int Kp16 = (K + 15) / 16 * 16;
-  const int M = Nb * Ho * Wo;
-  constexpr int LDP = 32 + 8;  // padded pixel stride in LDS (bf16 elements)
-
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint16_t* dyT = reinterpret_cast<uint16_t*>(smem);   // [Cout][LDP]
-  uint16_t* aT = dyT + Cout * LDP;                      // [Kp16][LDP]
-  float* vv = reinterpret_cast<float*>(aT + Kp16 * LDP);  // α β γ [Cout] + s t [Cin]
-
-  for (int i = threadIdx.x; i < Cout; i += 256) {
-    vv[i] = alpha[(int64_t)c * Cout + i];
-    vv[Cout + i] = beta[(int64_t)c * Cout + i];
-    vv[2 * Cout + i] = gamma[(int64_t)c * Cout + i];
-  }
-  if (PRO)
-    for (int i = threadIdx.x; i < Cin; i += 256) {
-      vv[3 * Cout + i] = ps[(int64_t)c * Cin + i];
-      vv[3 * Cout + Cin + i] = pt[(int64_t)c * Cin + i];
-    }
-
-  const int MT = Cout / 16, NT2 = Kp16 / 16;
-  const int ntiles = MT * NT2;
-  f32x4 acc[TPW];
-#pragma unroll
-  for (int t = 0; t < TPW; ++t) acc[t] = {0.f, 0.f, 0.f, 0.f};
-
-  const uint16_t* gc = g + (int64_t)c * M * Cout;
-  const uint16_t* yc = yv + (int64_t)c * M * Cout;
-  const uint16_t* xc = x + (int64_t)c * Nb * H * W * Cin;
-  const int p_begin = blockIdx.x * pix_per_wg;
-  const int p_end = min(M, p_begin + pix_per_wg);
-  __syncthreads();
-
-  for (int p0 = p_begin; p0 < p_end; p0 += 32) {
-    // stage dyᵀ: 32 pixels × Cout channels, 8 channels per thread-iteration
-    const int cg = Cout / 8;
-    for (int i = threadIdx.x; i < 32 * cg; i += 256) {
-      const int pp = i / cg, co0 = (i % cg) * 8;
-      const int p = p0 + pp;
-      float d[8];
-      if (p < p_end) {
-        float gf[8], yf[8];
-        unpack8(*reinterpret_cast<const uint4*>(gc + (int64_t)p * Cout + co0), gf);
-        unpack8(*reinterpret_cast<const uint4*>(yc + (int64_t)p * Cout + co0), yf);
-#pragma unroll
-        for (int j = 0; j < 8; ++j) d[j] = vv[co0 + j] * gf[j] + vv[Cout + co0 + j] * yf[j] + vv[2 * Cout + co0 + j];
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) d[j] = 0.f;
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) dyT[(co0 + j) * LDP + pp] = f32_to_bf16(d[j]);
-    }
-    // stage im2col(act)ᵀ: 32 pixels × K (tap-major, 8 input channels per thread-iteration)
-    const int kg = K / 8;
-    for (int i = threadIdx.x; i < 32 * kg; i += 256) {
-      const int pp = i / kg, k0 = (i % kg) * 8;
-      const int p = p0 + pp;
-      const int tap = k0 / Cin, ci0 = k0 % Cin;
-      float f[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] = 0.f;
-      if (p < p_end) {
-        const int n = p / (Ho * Wo), r = p % (Ho * Wo);
-        const int oh = r / Wo, ow = r % Wo;
-        const int ih = oh * stride - pad + tap / KW, iw = ow * stride - pad + tap % KW;
-        if (ih >= 0 && ih < H && iw >= 0 && iw < W) {
-          unpack8(*reinterpret_cast<const uint4*>(xc + (((int64_t)n * H + ih) * W + iw) * Cin + ci0), f);
-          if (PRO) {
-#pragma unroll
-            for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j] * vv[3 * Cout + ci0 + j] + vv[3 * Cout + Cin + ci0 + j], 0.f);
-          }
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) aT[(k0 + j) * LDP + pp] = f32_to_bf16(f[j]);
-    }
-    for (int i = threadIdx.x; i < (Kp16 - K) * 32; i += 256) aT[(K + i / 32) * LDP + (i % 32)] = 0;
-    __syncthreads();
-#pragma unroll
-    for (int t = 0; t < TPW; ++t) {
-      const int tile = wid + 4 * t;
-      if (tile < ntiles) {
-        const int mt = tile / NT2, nt = tile % NT2;
-        const uint4 av = *reinterpret_cast<const uint4*>(dyT + (mt * 16 + (lane & 15)) * LDP + 8 * (lane >> 4));
-        const uint4 bv = *reinterpret_cast<const uint4*>(aT + (nt * 16 + (lane & 15)) * LDP + 8 * (lane >> 4));
-        acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(as_bf16x8(av), as_bf16x8(bv), acc[t], 0, 0, 0);
-      }
-    }
-    __syncthreads();
-  }
-  // scatter-add the partial dW into the OIHW gradient (fp32 atomics, client stride ldw)
-  float* gw = garena + (int64_t)c * ldw + woff;
-  const int taps = KH * KW;
-#pragma unroll
-  for (int t = 0; t < TPW; ++t) {
-    const int tile = wid + 4 * t;
-    if (tile < ntiles) {
-      const int mt = tile / NT2, nt = tile % NT2;
-      const int k = nt * 16 + (lane & 15);
-      if (k < K) {
-        const int tap = k / Cin, ci = k % Cin;
-        if (ci < cin_src) {
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const int co = mt * 16 + 4 * (lane >> 4) + i;
-            atomicAdd(&gw[((int64_t)co * cin_src + ci) * taps + tap], acc[t][i]);
-          }
-        }
-      }
-    }
-  }
-}
-
-FA_EXPORT int fa_conv_wgrad(const uint16_t* g, const uint16_t* yv, const float* alpha, const float* beta,
-                            const float* gamma, const uint16_t* x, const float* ps, const float* pt, float* garena,
-                            int64_t ldw, int64_t woff, int C, int Nb, int H, int W, int Cin, int Ho, int Wo, int Cout,
-                            int KH, int KW, int stride, int pad, int pix_per_wg, int cin_src, hipStream_t stream) {
-  if (Cin % 8 != 0 || Cout % 16 != 0) return -3;
-  const int K = KH * KW * Cin;
-  const int Kp16 = (K + 15) / 16 * 16;
-  const int ntiles = (Cout / 16) * (Kp16 / 16);
-  const int tpw = (ntiles + 3) / 4;
-  const int M = Nb * Ho * Wo;
-  const int gx = (M + pix_per_wg - 1) / pix_per_wg;
-  const size_t smem = (size_t)(Cout + Kp16) * 40 * 2 + (size_t)(3 * Cout + 2 * Cin) * 4;
-  dim3 grid(gx, C);
-#define WG_LAUNCH(T)                                                                                          \
-  {                                                                                                           \
-    auto kern = ps ? conv_wgrad_kernel<T, 1> : conv_wgrad_kernel<T, 0>;                                       \
-    if (smem > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize,  \
-                                              (int)smem);                                                     \
-    hipLaunchKernelGGL(kern, grid, dim3(256), smem, stream, g, yv, alpha, beta, gamma, x, ps, pt, garena, ldw, \
-                       woff, Nb, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, pix_per_wg, cin_src);                   \
-  }
-  if (tpw <= 4) WG_LAUNCH(4)
-  else if (tpw <= 8) WG_LAUNCH(8)
-  else if (tpw <= 16) WG_LAUNCH(16)
-  else if (tpw <= 36) WG_LAUNCH(36)
-  else if (tpw <= 72) WG_LAUNCH(72)
-  else return -5;
-#undef WG_LAUNCH
-  return (int)hipGetLastError();
-}

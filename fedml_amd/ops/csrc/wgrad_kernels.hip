@@ -1,0 +1,289 @@
+// Backward-weight kernel for the client-batched convolutions (gfx950, bf16 MFMA).
+//
+//   dW[c][co][tap][ci] += Σ_p dy[c][p][co] · act(x)[c][p ⊕ tap][ci]
+//   dy = α·g + β·y + γ   (the following BatchNorm's backward, folded)
+//   act = PRO ? relu(x·s + t) : x   (the preceding BatchNorm + ReLU, recomputed — never stored)
+//
+// The reduction runs over pixels, so both MFMA operands must be pixel-major per lane
+// (A = dyᵀ: lane holds 8 consecutive pixels of one output channel; B = im2col(act): 8
+// consecutive pixels of one (tap, ci)). Tiles are staged into LDS in their NATURAL layout
+// ([pixel][channel], 16-B vector writes after the operand transform) and the fragments are
+// read with gfx950's transposing LDS read `ds_read_b64_tr_b16` (two per operand: pixels
+// 8g..8g+3 and 8g+4..8g+7 of column l&15), so no scalar transposed LDS traffic is needed.
+// A workgroup owns one client and a contiguous pixel chunk; its 4 waves split the Cout×K output
+// tiles and keep them in registers for the whole chunk; the partial dW is added (fp32 atomics)
+// into the client-stacked gradient arena at the OIHW position of each element.
+#include "common.h"
+
+typedef __bf16 wbf16x8 __attribute__((ext_vector_type(8)));
+typedef short wv4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) wv4i16 lds_v4i16;
+
+__device__ __forceinline__ void wg_unpack8(uint4 v, float* f) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+__device__ __forceinline__ uint4 wg_pack8(const float* f) {
+  uint4 r;
+  r.x = (uint32_t)f32_to_bf16(f[0]) | ((uint32_t)f32_to_bf16(f[1]) << 16);
+  r.y = (uint32_t)f32_to_bf16(f[2]) | ((uint32_t)f32_to_bf16(f[3]) << 16);
+  r.z = (uint32_t)f32_to_bf16(f[4]) | ((uint32_t)f32_to_bf16(f[5]) << 16);
+  r.w = (uint32_t)f32_to_bf16(f[6]) | ((uint32_t)f32_to_bf16(f[7]) << 16);
+  return r;
+}
+
+// fragment of 8 consecutive rows (pixels) of column block [col0, col0+16) from a natural
+// [rows][ld] bf16 LDS tile, rows row0..row0+31 (lane group g takes rows row0+8g..+7)
+__device__ __forceinline__ wbf16x8 tr_frag(const uint16_t* tile, int ld, int row0, int col0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const uint16_t* a0 = tile + (row0 + 8 * g + q) * ld + col0 + 4 * p;
+  const uint16_t* a1 = a0 + 4 * ld;
+  const wv4i16 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a0));
+  const wv4i16 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a1));
+  union {
+    short s[8];
+    wbf16x8 b;
+  } u;
+  u.s[0] = r0[0]; u.s[1] = r0[1]; u.s[2] = r0[2]; u.s[3] = r0[3];
+  u.s[4] = r1[0]; u.s[5] = r1[1]; u.s[6] = r1[2]; u.s[7] = r1[3];
+  return u.b;
+}
+
+
+// One workgroup = (client c, pixel chunk, K-slice z). The K-slice keeps the per-wave output
+// tile count ≤ 16 (≤ 64 accumulator registers) and means each workgroup only stages the im2col
+// columns it needs. Raw global data of sub-tile i+1 is prefetched into registers while the
+// MFMAs of sub-tile i run. Partial dW goes to a GEMM-layout fp32 scratch [C][Cout][K] with
+// row-contiguous atomics (16 consecutive k per lane group), then one scatter pass adds it into
+// the OIHW gradient arena.
+template <int TPW, int PRO, int DYI, int AI>
+__global__ __launch_bounds__(256) void conv_wgrad_tr_kernel(
+    const uint16_t* __restrict__ g, const uint16_t* __restrict__ yv, const float* __restrict__ alpha,
+    const float* __restrict__ beta, const float* __restrict__ gamma, const uint16_t* __restrict__ x,
+    const float* __restrict__ ps, const float* __restrict__ pt, float* __restrict__ dw, int Nb, int H, int W,
+    int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int pix_per_wg, int nt_per_z) {
+  constexpr int PT = 64;
+  const int c = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int K = KH * KW * Cin;
+  const int NT2 = (K + 15) / 16;
+  const int nt_lo = blockIdx.z * nt_per_z;
+  const int nt_hi = min(NT2, nt_lo + nt_per_z);
+  const int k_lo = nt_lo * 16;
+  const int k_hi = min(K, nt_hi * 16);
+  const int kw_ = (nt_hi - nt_lo) * 16;     // staged columns (zero beyond K)
+  const int M = Nb * Ho * Wo;
+  const int ldd = Cout + 8;
+  const int lda = kw_ + 8;
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint16_t* dyL = reinterpret_cast<uint16_t*>(smem);   // [PT][ldd]
+  uint16_t* aL = dyL + PT * ldd;                        // [PT][lda]
+  float* vv = reinterpret_cast<float*>(aL + PT * lda);  // α β γ [Cout], s t [Cin]
+
+  for (int i = threadIdx.x; i < Cout; i += 256) {
+    vv[i] = alpha[(int64_t)c * Cout + i];
+    vv[Cout + i] = beta[(int64_t)c * Cout + i];
+    vv[2 * Cout + i] = gamma[(int64_t)c * Cout + i];
+  }
+  if (PRO)
+    for (int i = threadIdx.x; i < Cin; i += 256) {
+      vv[3 * Cout + i] = ps[(int64_t)c * Cin + i];
+      vv[3 * Cout + Cin + i] = pt[(int64_t)c * Cin + i];
+    }
+  const int padc = kw_ - (k_hi - k_lo);
+  for (int i = threadIdx.x; i < PT * padc; i += 256) aL[(i / padc) * lda + (k_hi - k_lo) + i % padc] = 0;
+
+  const int MT = Cout / 16, NTZ = nt_hi - nt_lo;
+  const int ntiles = MT * NTZ;
+  f32x4 acc[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) acc[t] = {0.f, 0.f, 0.f, 0.f};
+
+  const uint16_t* gc = g + (int64_t)c * M * Cout;
+  const uint16_t* yc = yv + (int64_t)c * M * Cout;
+  const uint16_t* xc = x + (int64_t)c * Nb * H * W * Cin;
+  const int p_begin = blockIdx.x * pix_per_wg;
+  const int p_end = min(M, p_begin + pix_per_wg);
+  const int cg = Cout / 8, kg = (k_hi - k_lo) / 8;
+  const int n_dy = PT * cg, n_a = PT * kg;
+  __syncthreads();
+
+  uint4 rg[DYI], ry[DYI], rx[AI];
+  uint32_t dvalid = 0, avalid = 0;
+  auto load_sub = [&](int p0) {
+    dvalid = 0;
+    avalid = 0;
+#pragma unroll
+    for (int it = 0; it < DYI; ++it) {
+      const int i = threadIdx.x + it * 256;
+      rg[it] = make_uint4(0, 0, 0, 0);
+      ry[it] = make_uint4(0, 0, 0, 0);
+      if (i < n_dy) {
+        const int p = p0 + i / cg, co0 = (i % cg) * 8;
+        if (p < p_end) {
+          rg[it] = *reinterpret_cast<const uint4*>(gc + (int64_t)p * Cout + co0);
+          ry[it] = *reinterpret_cast<const uint4*>(yc + (int64_t)p * Cout + co0);
+          dvalid |= 1u << it;
+        }
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < AI; ++it) {
+      const int i = threadIdx.x + it * 256;
+      rx[it] = make_uint4(0, 0, 0, 0);
+      if (i < n_a) {
+        const int p = p0 + i / kg, k0 = k_lo + (i % kg) * 8;
+        if (p < p_end) {
+          const int tap = k0 / Cin, ci0 = k0 % Cin;
+          const int n = p / (Ho * Wo), r = p % (Ho * Wo);
+          const int oh = r / Wo, ow = r % Wo;
+          const int ih = oh * stride - pad + tap / KW, iw = ow * stride - pad + tap % KW;
+          if (ih >= 0 && ih < H && iw >= 0 && iw < W) {
+            rx[it] = *reinterpret_cast<const uint4*>(xc + (((int64_t)n * H + ih) * W + iw) * Cin + ci0);
+            avalid |= 1u << it;
+          }
+        }
+      }
+    }
+  };
+  auto store_sub = [&]() {
+#pragma unroll
+    for (int it = 0; it < DYI; ++it) {
+      const int i = threadIdx.x + it * 256;
+      if (i < n_dy) {
+        const int pp = i / cg, co0 = (i % cg) * 8;
+        float gf[8], yf[8], d[8];
+        wg_unpack8(rg[it], gf);
+        wg_unpack8(ry[it], yf);
+        const bool live = (dvalid >> it) & 1u;
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          d[j] = live ? vv[co0 + j] * gf[j] + vv[Cout + co0 + j] * yf[j] + vv[2 * Cout + co0 + j] : 0.f;
+        *reinterpret_cast<uint4*>(dyL + pp * ldd + co0) = wg_pack8(d);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < AI; ++it) {
+      const int i = threadIdx.x + it * 256;
+      if (i < n_a) {
+        const int pp = i / kg, kk = (i % kg) * 8;
+        uint4 v = rx[it];
+        if (!((avalid >> it) & 1u)) {
+          v = make_uint4(0, 0, 0, 0);   // zero padding / out-of-range pixel (not relu(shift))
+        } else if (PRO) {
+          const int ci0 = (k_lo + kk) % Cin;
+          float f[8];
+          wg_unpack8(v, f);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j] * vv[3 * Cout + ci0 + j] + vv[3 * Cout + Cin + ci0 + j], 0.f);
+          v = wg_pack8(f);
+        }
+        *reinterpret_cast<uint4*>(aL + pp * lda + kk) = v;
+      }
+    }
+  };
+
+  if (p_begin < p_end) load_sub(p_begin);
+  for (int p0 = p_begin; p0 < p_end; p0 += PT) {
+    store_sub();
+    __syncthreads();
+    if (p0 + PT < p_end) load_sub(p0 + PT);
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      const int tile = wid + 4 * t;
+      if (tile < ntiles) {
+        const int mt = tile / NTZ, nt = tile % NTZ;
+#pragma unroll
+        for (int ks = 0; ks < PT / 32; ++ks) {
+          const wbf16x8 af = tr_frag(dyL, ldd, ks * 32, mt * 16, lane);
+          const wbf16x8 bf = tr_frag(aL, lda, ks * 32, nt * 16, lane);
+          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc[t], 0, 0, 0);
+        }
+      }
+    }
+    __syncthreads();
+  }
+  float* dwc = dw + (int64_t)c * Cout * K;
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    const int tile = wid + 4 * t;
+    if (tile < ntiles) {
+      const int mt = tile / NTZ, nt = tile % NTZ;
+      const int k = k_lo + nt * 16 + (lane & 15);
+      if (k < K) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int co = mt * 16 + 4 * (lane >> 4) + i;
+          atomicAdd(&dwc[(int64_t)co * K + k], acc[t][i]);
+        }
+      }
+    }
+  }
+}
+
+// dW GEMM layout [c][co][tap*Cin + ci] → OIHW gradient arena (+=), and clear the scratch
+__global__ __launch_bounds__(256) void wgrad_scatter_kernel(float* __restrict__ dw, float* __restrict__ garena,
+                                                            int64_t ldw, int64_t woff, int Cout, int Cin, int taps,
+                                                            int cin_src) {
+  const int c = blockIdx.y;
+  const int K = taps * Cin;
+  const int n = Cout * K;
+  float* d = dw + (int64_t)c * n;
+  float* gw = garena + (int64_t)c * ldw + woff;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int co = i / K, k = i % K;
+    const int tap = k / Cin, ci = k % Cin;
+    if (ci < cin_src) gw[((int64_t)co * cin_src + ci) * taps + tap] += d[i];
+    d[i] = 0.f;
+  }
+}
+
+// `dw` scratch: C × Cout × K fp32, zero on entry (left zeroed on exit by the scatter pass)
+FA_EXPORT int fa_conv_wgrad(const uint16_t* g, const uint16_t* yv, const float* alpha, const float* beta,
+                            const float* gamma, const uint16_t* x, const float* ps, const float* pt, float* garena,
+                            int64_t ldw, int64_t woff, int C, int Nb, int H, int W, int Cin, int Ho, int Wo, int Cout,
+                            int KH, int KW, int stride, int pad, int pix_per_wg, int cin_src, float* dw,
+                            hipStream_t stream) {
+  if (Cin % 8 != 0 || Cout % 16 != 0 || Cout > 256) return -3;
+  const int K = KH * KW * Cin;
+  const int NT2 = (K + 15) / 16;
+  const int MT = Cout / 16;
+  const int nt_per_z = max(1, min(NT2, 64 / MT));   // ≤ 64 tiles per workgroup → ≤ 16 per wave
+  const int nz = (NT2 + nt_per_z - 1) / nt_per_z;
+  const int tpw = (MT * nt_per_z + 3) / 4;
+  const int M = Nb * Ho * Wo;
+  const int gx = (M + pix_per_wg - 1) / pix_per_wg;
+  const int kw_ = nt_per_z * 16;
+  const int dyi = (64 * (Cout / 8) + 255) / 256;
+  const int ai = (64 * (kw_ / 8) + 255) / 256;
+  const size_t smem = (size_t)64 * ((Cout + 8) + (kw_ + 8)) * 2 + (size_t)(3 * Cout + 2 * Cin) * 4;
+  dim3 grid(gx, C, nz);
+#define WG_LAUNCH(T, D, A)                                                                                       \
+  {                                                                                                              \
+    auto kern = ps ? conv_wgrad_tr_kernel<T, 1, D, A> : conv_wgrad_tr_kernel<T, 0, D, A>;                        \
+    if (smem > 64 * 1024)                                                                                        \
+      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);             \
+    hipLaunchKernelGGL(kern, grid, dim3(256), smem, stream, g, yv, alpha, beta, gamma, x, ps, pt, dw, Nb, H, W,   \
+                       Cin, Ho, Wo, Cout, KH, KW, stride, pad, pix_per_wg, nt_per_z);                            \
+  }
+#define WG_AI(T, D)                          \
+  if (ai <= 2) WG_LAUNCH(T, D, 2)            \
+  else if (ai <= 4) WG_LAUNCH(T, D, 4)       \
+  else WG_LAUNCH(T, D, 8)
+#define WG_D(T)                              \
+  if (dyi <= 2) { WG_AI(T, 2) }              \
+  else { WG_AI(T, 8) }
+  if (tpw <= 4) { WG_D(4) }
+  else if (tpw <= 8) { WG_D(8) }
+  else { WG_D(16) }
+#undef WG_D
+#undef WG_AI
+#undef WG_LAUNCH
+  hipLaunchKernelGGL(wgrad_scatter_kernel, dim3(fa_grid((int64_t)Cout * K, 256, 64), C), dim3(256), 0, stream, dw,
+                     garena, ldw, woff, Cout, Cin, KH * KW, cin_src);
+  return (int)hipGetLastError();
+}

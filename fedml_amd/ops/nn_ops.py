@@ -50,10 +50,12 @@ def conv_bwd_data(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, dx, epi, e_x, e_s, e
 
 
 def conv_wgrad(g, yv, alpha, beta, gamma, x, ps, pt, garena, woff, C, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
-               pad, pix_per_wg, cin_src):
+               pad, pix_per_wg, cin_src, dw_scratch):
+    """``dw_scratch``: ≥ C·Cout·KH·KW·Cin fp32, zero on entry; the kernel leaves it zeroed."""
     rc = _fn("fa_conv_wgrad")(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(x), _p(ps), _p(pt), _p(garena),
                               _i64(garena.stride(0)), _i64(woff), _i(C), _i(N), _i(H), _i(W), _i(Cin), _i(Ho), _i(Wo),
-                              _i(Cout), _i(KH), _i(KW), _i(stride), _i(pad), _i(pix_per_wg), _i(cin_src), _stream(g))
+                              _i(Cout), _i(KH), _i(KW), _i(stride), _i(pad), _i(pix_per_wg), _i(cin_src),
+                              _p(dw_scratch), _stream(g))
     _check(rc, "fa_conv_wgrad")
 
 

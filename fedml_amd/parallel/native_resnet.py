@@ -230,6 +230,9 @@ class NativeResNetStep:
             self.stat_views[bn.key] = (fwd, bwd)
         fh, fw = self.final_hw
         self.pooled = torch.empty(C, N, self.fc_in, dtype=torch.float32, device=dev)
+        # GEMM-layout dW scratch for the weight-gradient kernel (kept zeroed by its scatter pass)
+        mx = max(cv.cout * cv.k * cv.k * cv.cin_pad for cv in self._all_convs())
+        self.dw_scratch = torch.zeros(C * mx, dtype=torch.float32, device=dev)
         self.geom = (N, H, W)
 
     def _all_bns(self):
@@ -368,7 +371,7 @@ class NativeResNetStep:
                 M = N * cv.Ho * cv.Wo
                 nn_ops.conv_wgrad(g_j, b.ys[j], v[4], v[5], v[6], b.ys[j - 1], pv[0], pv[1], garena,
                                   self.off[cv.key], C, N, cv.H, cv.W, cv.cin_pad, cv.Ho, cv.Wo, cv.cout, cv.k, cv.k,
-                                  cv.stride, cv.pad, self._pix_per_wg(M), cv.cin)
+                                  cv.stride, cv.pad, self._pix_per_wg(M), cv.cin, self.dw_scratch)
                 out_g = free[0] if g_j is not free[0] else free[1]
                 nn_ops.conv_bwd_data(g_j, b.ys[j], v[4], v[5], v[6], self.packed.view(-1)[cv.off_b:],
                                      self.packed_ld, out_g, nn_ops.EPI_MASK, b.ys[j - 1], pv[0], pv[1], None, None,
@@ -384,7 +387,7 @@ class NativeResNetStep:
                 vd = self.bn_vec[b.ds_bn.key]
                 nn_ops.conv_wgrad(gpre, b.yd, vd[4], vd[5], vd[6], b.act_in, None, None, garena, self.off[d.key], C, N,
                                   d.H, d.W, d.cin_pad, d.Ho, d.Wo, d.cout, d.k, d.k, d.stride, d.pad,
-                                  self._pix_per_wg(N * d.Ho * d.Wo), d.cin)
+                                  self._pix_per_wg(N * d.Ho * d.Wo), d.cin, self.dw_scratch)
                 nn_ops.conv_bwd_data(gpre, b.yd, vd[4], vd[5], vd[6], self.packed.view(-1)[d.off_b:], self.packed_ld,
                                      gadd, nn_ops.EPI_STORE, None, None, None, None, None, None, self.stats, C, N,
                                      d.Ho, d.Wo, d.cout, d.cin_pad, d.k, d.k, d.stride, d.pad, d.H, d.W, d.ldk2,
@@ -397,7 +400,7 @@ class NativeResNetStep:
             v = self.bn_vec[bn0.key]
             nn_ops.conv_wgrad(g_j, b.ys[0], v[4], v[5], v[6], b.act_in, None, None, garena, self.off[cv0.key], C, N,
                               cv0.H, cv0.W, cv0.cin_pad, cv0.Ho, cv0.Wo, cv0.cout, cv0.k, cv0.k, cv0.stride, cv0.pad,
-                              self._pix_per_wg(N * cv0.Ho * cv0.Wo), cv0.cin)
+                              self._pix_per_wg(N * cv0.Ho * cv0.Wo), cv0.cin, self.dw_scratch)
             if prev_block is not None:
                 ey1, ey2 = prev_block.ys[-1], prev_block.yd
                 pstats = self.stat_views[prev_block.bns[-1].key][1]
@@ -420,5 +423,5 @@ class NativeResNetStep:
         nn_ops.conv_wgrad(gpre, self.stem_y, v[4], v[5], v[6], self.x_in, None, None, garena, self.off[st_conv.key], C,
                           N, st_conv.H, st_conv.W, st_conv.cin_pad, st_conv.Ho, st_conv.Wo, st_conv.cout, st_conv.k,
                           st_conv.k, st_conv.stride, st_conv.pad, self._pix_per_wg(N * st_conv.Ho * st_conv.Wo),
-                          st_conv.cin)
+                          st_conv.cin, self.dw_scratch)
         return loss.detach()
