@@ -1,0 +1,89 @@
+"""Message serialisation and every transport's round trip (loopback, TCP, gRPC, pub/sub+blob)."""
+import threading
+from collections import OrderedDict
+
+import numpy as np
+import pytest
+import torch
+
+from fedml_amd.core.distributed.communication import Message
+from fedml_amd.core.distributed.communication.pubsub import InProcessBroker, MemoryBlobStore, MqttS3CommManager
+from fedml_amd.core.distributed.communication.serialization import decode, encode
+from fedml_amd.core.distributed.communication.transports import (GRPCCommManager, LoopbackCommManager, LoopbackRouter,
+                                                                  TCPCommManager)
+
+
+def _msg():
+    m = Message(3, 1, 0)
+    m.add_params("model_params", OrderedDict(w=torch.randn(4, 5), b=torch.arange(3), h=torch.randn(2).bfloat16()))
+    m.add_params("num_samples", 17)
+    m.add_params("arr", np.arange(6, dtype=np.float32).reshape(2, 3))
+    return m
+
+
+def test_serialization_roundtrip_no_pickle():
+    m = _msg()
+    out = decode(encode(m.get_params()))
+    assert out["num_samples"] == 17
+    assert torch.equal(out["model_params"]["w"], m.get("model_params")["w"])
+    assert out["model_params"]["h"].dtype == torch.bfloat16
+    assert np.array_equal(out["arr"], m.get("arr"))
+    with pytest.raises(TypeError):
+        encode({"bad": object()})
+
+
+def _echo_pair(make):
+    a, b = make(0), make(1)
+    got = []
+    done = threading.Event()
+
+    class Obs:
+        def receive_message(self, t, m):
+            got.append(m)
+            done.set()
+            b.stop_receive_message()
+
+    b.add_observer(Obs())
+    th = threading.Thread(target=b.handle_receive_message, daemon=True)
+    th.start()
+    m = _msg()
+    m.receiver_id = 1
+    m.add_params(Message.MSG_ARG_KEY_RECEIVER, 1)
+    a.send_message(m)
+    assert done.wait(30)
+    th.join(10)
+    assert torch.equal(got[0].get("model_params")["w"], m.get("model_params")["w"])
+    a.stop_receive_message()
+
+
+def test_loopback():
+    r = LoopbackRouter(2)
+    _echo_pair(lambda rank: LoopbackCommManager(r, rank, 2))
+
+
+def test_tcp():
+    _echo_pair(lambda rank: TCPCommManager(rank, 2, base_port=39411))
+
+
+def test_grpc():
+    _echo_pair(lambda rank: GRPCCommManager(rank, 2, base_port=28931))
+
+
+def test_pubsub_blob_store_and_last_will():
+    broker = InProcessBroker()
+    store = MemoryBlobStore()
+    server = MqttS3CommManager(broker, store, 0, 2, run_id="t")
+    client = MqttS3CommManager(broker, store, 1, 2, run_id="t")
+    # CONNECTION_IS_READY delivered locally first
+    assert str(server.inbox.get().get_type()) == "0"
+    assert str(client.inbox.get().get_type()) == "0"
+    m = _msg()
+    m.sender_id, m.receiver_id = 1, 0
+    m.add_params(Message.MSG_ARG_KEY_SENDER, 1)
+    m.add_params(Message.MSG_ARG_KEY_RECEIVER, 0)
+    client.send_message(m)
+    got = server.inbox.get(timeout=5)
+    assert got.get("model_params_url", "").startswith("mem://")
+    assert torch.equal(got.get("model_params")["w"], m.get("model_params")["w"])
+    client.stop_receive_message(clean=False)   # unclean → last will published
+    assert 0 in server.offline or 1 in server.offline
