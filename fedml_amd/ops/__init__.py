@@ -28,6 +28,8 @@ from .fl_ops import (
     FusedCrossEntropy,
     confusion_matrix,
     cast_bf16,
+    mod_matmul,
+    mod_sum,
     use_native,
 )
 

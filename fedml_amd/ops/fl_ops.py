@@ -484,3 +484,41 @@ def cast_bf16(x, out=None):
         out.copy_(r)
         return out
     return r
+
+
+# ----------------------------------------------------------------------------- K13
+def _mod_matmul_ref(A, B, p):
+    A = A.to(torch.int64).remainder(p)
+    B2 = B.reshape(B.shape[0], -1).to(torch.int64).remainder(p)
+    out = torch.zeros(A.shape[0], B2.shape[1], dtype=torch.int64, device=B.device)
+    for k in range(A.shape[1]):
+        out = (out + (A[:, k:k + 1] * B2[k:k + 1]) % p) % p
+    return out
+
+
+def mod_matmul(A: torch.Tensor, B: torch.Tensor, p: int) -> torch.Tensor:
+    """(A @ B) mod p on int64 residues (A: [M,K], B: [K, ...]); exact for p < 2^31."""
+    shp = (A.shape[0],) + tuple(B.shape[1:])
+    if use_native(B):
+        A_ = A.to(device=B.device, dtype=torch.int64).remainder(p).contiguous()
+        B_ = B.to(torch.int64).reshape(B.shape[0], -1).contiguous()
+        out = torch.empty(A_.shape[0], B_.shape[1], dtype=torch.int64, device=B.device)
+        rc = _fn("fa_mod_matmul")(_p(A_), _p(B_), _p(out), _c.c_int(A_.shape[0]), _c.c_int(A_.shape[1]),
+                                  _i64(B_.shape[1]), _i64(p), _stream(B))
+        _check(rc, "fa_mod_matmul")
+        return out.reshape(shp)
+    return _mod_matmul_ref(A, B, p).reshape(shp)
+
+
+def mod_sum(X: torch.Tensor, p: int) -> torch.Tensor:
+    """Σ_c X[c] mod p over residues (X: [C, ...])."""
+    if use_native(X):
+        X_ = X.to(torch.int64).contiguous()
+        out = torch.empty(X_.shape[1:], dtype=torch.int64, device=X.device)
+        rc = _fn("fa_mod_sum")(_p(X_), _p(out), _c.c_int(X_.shape[0]), _i64(out.numel()), _i64(p), _stream(X))
+        _check(rc, "fa_mod_sum")
+        return out
+    acc = torch.zeros(X.shape[1:], dtype=torch.int64, device=X.device)
+    for c in range(X.shape[0]):
+        acc = (acc + X[c]) % p
+    return acc

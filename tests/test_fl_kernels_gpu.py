@@ -192,3 +192,38 @@ def test_confusion_matrix():
     c = ops.confusion_matrix(z, y, num_groups=G, rows_per_group=333)
     g = ops.confusion_matrix(z.to(DEV), y.to(DEV), num_groups=G, rows_per_group=333).cpu()
     assert torch.equal(c, g)
+
+
+@pytest.mark.parametrize("p", [2 ** 31 - 1, 1000003])
+@pytest.mark.parametrize("M,K,N", [(1, 4, 1000), (11, 9, 70001), (64, 64, 4096)])
+def test_mod_matmul(p, M, K, N):
+    g = torch.Generator().manual_seed(M * K)
+    A = torch.randint(0, p, (M, K), generator=g, dtype=torch.int64)
+    B = torch.randint(0, p, (K, N), generator=g, dtype=torch.int64)
+    ref = ops.mod_matmul(A, B, p)
+    out = ops.mod_matmul(A.to(DEV), B.to(DEV), p).cpu()
+    assert torch.equal(ref, out)
+    # spot-check the CPU reference against python big-int arithmetic
+    i, j = M - 1, N // 2
+    assert int(ref[i, j]) == sum(int(A[i, k]) * int(B[k, j]) for k in range(K)) % p
+
+
+@pytest.mark.parametrize("p", [2 ** 31 - 1, 65521])
+def test_mod_sum(p):
+    X = torch.randint(0, p, (17, 123457), dtype=torch.int64)
+    assert torch.equal(ops.mod_sum(X, p), ops.mod_sum(X.to(DEV), p).cpu())
+
+
+def test_secagg_on_device():
+    from fedml_amd.core.mpc import SecAggClient, SecureAggregator
+    n, T = 5, 2
+    cl = [SecAggClient(i, n, T, seed=i) for i in range(n)]
+    sa = SecureAggregator(n, T)
+    for c in cl:
+        sa.add_public_key(c.cid, c.pk)
+        for h, s in enumerate(c.sk_shares()):
+            sa.add_share(c.cid, h, s)
+    xs = [torch.randn(100_000, device=DEV) for _ in range(n)]
+    alive = [0, 1, 3]
+    out = sa.aggregate({c: cl[c].masked_input(xs[c], sa.pks) for c in alive})
+    assert torch.allclose(out, sum(xs[c] for c in alive).double(), atol=1e-5)

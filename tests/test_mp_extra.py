@@ -1,0 +1,183 @@
+"""Message-passing algorithms beyond the FedAvg family (reference `mpi_p2p_mp/*`), all ranks as
+threads over the loopback transport (serialized frames, like a real wire)."""
+import logging
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+import fedml_amd
+from fedml_amd.arguments import Arguments
+from fedml_amd.simulation.mp.launcher import run_message_passing
+
+
+def _args(opt, **kw):
+    cfg = {"training_type": "simulation", "dataset": "mnist", "model": "lr", "client_num_in_total": 6,
+           "client_num_per_round": 3, "comm_round": 2, "epochs": 1, "batch_size": 16, "learning_rate": 0.03,
+           "frequency_of_the_test": 1, "backend": "LOOPBACK", "federated_optimizer": opt}
+    cfg.update(kw)
+    a = fedml_amd.init(Arguments.from_dict({"x": cfg}))
+    logging.getLogger().setLevel(logging.WARNING)
+    return a
+
+
+def test_base_framework():
+    from fedml_amd.simulation.mp.base_framework import FedML_Base_distributed
+    a = _args("base_framework", comm_round=3)
+    res = run_message_passing(FedML_Base_distributed, a, None, None, None, size=4)
+    assert len(res["history"]) == 3
+
+
+def test_decentralized_framework_converges_to_mean():
+    from fedml_amd.simulation.mp.decentralized_framework import FedML_Decentralized_Demo_distributed
+    a = _args("decentralized_fl", comm_round=30)
+    res = run_message_passing(FedML_Decentralized_Demo_distributed, a, None, None, None, size=6)
+    # symmetric doubly-stochastic gossip → consensus on the average of the initial values (0..5)
+    assert abs(res["value"] - 2.5) < 0.05
+
+
+def _image_dataset(n_clients=3, n=32, hw=32, classes=10, seed=0):
+    from fedml_amd.data.client_data import ClientData
+    g = torch.Generator().manual_seed(seed)
+    tr, te, nums = {}, {}, {}
+    for c in range(n_clients):
+        y = torch.randint(0, classes, (n,), generator=g)
+        x = torch.randn(n, 3, hw, hw, generator=g) * 0.5 + y.view(-1, 1, 1, 1).float() / classes
+        tr[c] = ClientData(x, y, 16)
+        te[c] = ClientData(x[:16], y[:16], 16)
+        nums[c] = n
+    return [n * n_clients, 16 * n_clients, None, None, nums, tr, te, classes]
+
+
+def test_fedgkt():
+    from fedml_amd.models.cv.resnet_gkt import ResNetClient, ResNetServer
+    from fedml_amd.simulation.mp.fedgkt import FedML_FedGKT_distributed
+    a = _args("FedGKT", epochs_server=1, temperature=3.0, alpha=1.0, learning_rate=0.01)
+    ds = _image_dataset()
+    res = run_message_passing(FedML_FedGKT_distributed, a, torch.device("cpu"), ds,
+                              (ResNetClient(10, 1), ResNetServer(10, (1, 1, 1))), size=4)
+    assert len(res["history"]) == 2 and res["history"][-1]["test_acc"] is not None
+
+
+def test_split_nn_learns():
+    from fedml_amd.simulation.mp.split_nn import SplitNN_distributed
+    a = _args("split_nn", epochs=3, learning_rate=0.05)
+    ds = _image_dataset(n_clients=2, n=64, hw=8)
+    bottom = nn.Sequential(nn.Flatten(), nn.Linear(3 * 64, 32), nn.ReLU())
+    top = nn.Linear(32, 10)
+    res = run_message_passing(SplitNN_distributed, a, torch.device("cpu"), ds, (bottom, top), size=3)
+    # 3 turns per client, each turn followed by a validation report
+    assert len(res["history"]) == 6
+    assert res["history"][-1]["val_acc"] > 0.3
+
+
+def test_classical_vfl_beats_single_party():
+    from fedml_amd.data.vertical import synthetic_vertical
+    from fedml_amd.models.finance.vfl_models import DenseModel, LocalModel
+    from fedml_amd.simulation.mp.classical_vertical_fl import FedML_VFL_distributed
+    tr, ytr, te, yte = synthetic_vertical(1000, 400, (6, 6, 6), seed=1)
+    a = _args("classical_vertical_fl", comm_round=8, batch_size=100, learning_rate=0.05, frequency_of_the_test=10)
+    models = [(LocalModel(6, 8), DenseModel(8, 1)) for _ in range(3)]
+    res = run_message_passing(FedML_VFL_distributed, a, torch.device("cpu"), (tr, ytr, te, yte), models, size=3)
+    assert res["history"][-1]["test_auc"] > 0.85
+
+
+def test_fedgan_runs():
+    from fedml_amd.data.client_data import ClientData
+    from fedml_amd.models.cv.mnist_gan import MNISTGAN
+    from fedml_amd.simulation.mp.fedgan import FedML_FedGan_distributed
+    a = _args("FedGAN", learning_rate=2e-4, frequency_of_the_test=0)
+    g = torch.Generator().manual_seed(0)
+    tr = {c: ClientData(torch.rand(32, 784, generator=g), torch.zeros(32, dtype=torch.long), 16) for c in range(6)}
+    ds = [192, 0, None, None, {c: 32 for c in range(6)}, tr, {}, 10]
+    m = MNISTGAN()
+    before = {k: v.clone() for k, v in m.state_dict().items()}
+    res = run_message_passing(FedML_FedGan_distributed, a, torch.device("cpu"), ds, m)
+    moved = [k for k in before if not torch.equal(before[k], res["global_model"][k])]
+    assert any(k.startswith("netg.") for k in moved) and any(k.startswith("netd.") for k in moved)
+
+
+def test_fednas_search():
+    from fedml_amd.models.cv.darts import Network
+    from fedml_amd.simulation.mp.fednas import FedML_FedNAS_distributed
+    a = _args("FedNAS", comm_round=1, learning_rate=0.025, frequency_of_the_test=0, stage="search")
+    ds = _image_dataset(n_clients=6, n=16, hw=8)
+    m = Network(C=4, num_classes=10, layers=2, steps=2, multiplier=2)
+    alphas0 = m.alphas_normal.detach().clone()
+    res = run_message_passing(FedML_FedNAS_distributed, a, torch.device("cpu"), ds, m)
+    assert not torch.equal(res["global_model"]["alphas_normal"], alphas0)
+    assert len(res["genotype"].normal) == 4
+
+
+def test_fedseg():
+    from fedml_amd.data.segmentation import load_synthetic_segmentation
+    from fedml_amd.models.cv.segmentation import UNet
+    from fedml_amd.simulation.mp.fedseg import FedML_FedSeg_distributed
+    ds, ncls = load_synthetic_segmentation(6, samples_per_client=8, n_classes=4, hw=16, batch_size=4)
+    a = _args("FedSeg", learning_rate=0.05, comm_round=2)
+    res = run_message_passing(FedML_FedSeg_distributed, a, torch.device("cpu"), ds, UNet(ncls, width=8, depth=2))
+    h = res["history"][-1]
+    assert 0.0 <= h["test_mIoU"] <= 1.0 and h["test_acc"] > 0.2
+
+
+@pytest.mark.parametrize("drop", [None, {1: [2]}])
+def test_turboaggregate_secure_equals_plain_fedavg(drop):
+    """The securely aggregated model equals plain FedAvg over the same (surviving) clients up to the
+    2^-20 fixed-point resolution."""
+    from fedml_amd.simulation.mp.fedavg import FedML_FedAvg_distributed
+    from fedml_amd.simulation.mp.turboaggregate import FedML_TurboAggregate_distributed
+    import copy
+    a = _args("turbo_aggregate", frequency_of_the_test=0, ta_threshold=1)
+    dev, ds, m = fedml_amd._prepare(a)
+    res = run_message_passing(FedML_TurboAggregate_distributed, a, dev, ds, copy.deepcopy(m))
+    if drop is None:
+        ref = run_message_passing(FedML_FedAvg_distributed, _args("FedAvg", frequency_of_the_test=0), dev, ds,
+                                  copy.deepcopy(m))
+        for k, v in ref["global_model"].items():
+            assert torch.allclose(v.float(), res["global_model"][k].float(), atol=1e-5), k
+    else:
+        b = _args("turbo_aggregate", frequency_of_the_test=0, ta_threshold=1, ta_dropout_ranks=drop)
+        res2 = run_message_passing(FedML_TurboAggregate_distributed, b, dev, ds, copy.deepcopy(m))
+        assert res2["dropped"] == [[], [1]]
+        assert all(torch.isfinite(v.float()).all() for v in res2["global_model"].values())
+
+
+def test_mpc_primitives():
+    from fedml_amd.core import mpc
+    p = mpc.DEFAULT_PRIME
+    rng = np.random.RandomState(0)
+    X = rng.randint(0, p, size=(4, 5)).astype(np.int64)
+    sh = mpc.BGW_encoding(X, 7, 3, p, rng=rng)
+    assert (mpc.BGW_decoding(sh[[1, 2, 5, 6]].reshape(4, -1), [1, 2, 5, 6], p).reshape(4, 5) == X).all()
+    enc = mpc.LCC_encoding(X, 8, 2, 2, p, rng=rng)
+    assert (mpc.LCC_decoding(enc[[0, 3, 5, 7]], 1, 8, 2, 2, [0, 3, 5, 7], p).reshape(4, 5) == X).all()
+    assert (mpc.Gen_Additive_SS(10, 4, p, rng=rng).sum(0) % p == 0).all()
+    sh = mpc.additive_share(X, 3, p, rng=rng)
+    assert (sh.sum(0) % p == X).all()
+    assert mpc.divmod(6, 3, 7) == 2 and mpc.modular_inv(3, 7) == 5
+    # exact modular GEMM vs python big-int
+    A = rng.randint(0, p, size=(3, 9)).astype(np.int64)
+    B = rng.randint(0, p, size=(9, 11)).astype(np.int64)
+    ref = [[sum(int(A[i, k]) * int(B[k, j]) for k in range(9)) % p for j in range(11)] for i in range(3)]
+    assert (mpc.mod_matmul(A, B, p) == np.array(ref)).all()
+    At, Bt = torch.from_numpy(A), torch.from_numpy(B)
+    assert (mpc.mod_matmul(At, Bt, p).numpy() == np.array(ref)).all()
+
+
+def test_secagg_dropout_recovery():
+    from fedml_amd.core.mpc import SecAggClient, SecureAggregator
+    n, T = 6, 2
+    cl = [SecAggClient(i, n, T, seed=10 + i) for i in range(n)]
+    sa = SecureAggregator(n, T)
+    for c in cl:
+        sa.add_public_key(c.cid, c.pk)
+        for h, s in enumerate(c.sk_shares()):
+            sa.add_share(c.cid, h, s)
+    xs = [torch.randn(257) for _ in range(n)]
+    alive = [0, 2, 3, 5]
+    out = sa.aggregate({c: cl[c].masked_input(xs[c], sa.pks) for c in alive})
+    assert torch.allclose(out, sum(xs[c] for c in alive).double(), atol=1e-5)
+    # a single masked upload reveals nothing close to the input
+    single = cl[0].masked_input(xs[0], sa.pks)
+    assert not torch.allclose(single.double() / 2 ** 20, xs[0].double(), atol=1.0)
