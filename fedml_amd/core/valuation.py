@@ -1,0 +1,218 @@
+"""Client valuation (Shapley-style) for S-FedAvg / HS-FedAvg
+(reference: `single_process/s_fedavg/fedavg_api.py:196-325`, `hs_fedavg/fedavg_api.py:177-230`).
+
+The reference evaluates every coalition model one at a time: deep-copy the trainer, aggregate
+the subset's state dicts in Python, run the validation loader — ``2·(2^(K-1)−1)·K + K``
+aggregate+evaluate pairs per round for K clients. Here:
+
+1. every distinct coalition is aggregated ONCE: the sample-weighted coalition averages are one
+   ``[S, K] @ [K, P]`` product (``ops.subset_aggregate`` — fp32 MFMA kernel on MI355X);
+2. the coalition models are evaluated TOGETHER: ``BatchedModelEvaluator`` runs up to
+   ``max_models`` of them as one client-batched forward (grouped conv / bmm through
+   ``parallel.batched_nn``) over the shared validation set;
+3. the per-client values are then table lookups over the coalition scores ``v[mask]``.
+
+So the reference's 2^(K-1)·2K evaluations become 2^K − 1, executed in ⌈(2^K−1)/max_models⌉
+batched passes.
+"""
+import itertools
+import logging
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .. import ops
+from .arena import ParamLayout
+
+
+class BatchedModelEvaluator:
+    def __init__(self, model: torch.nn.Module, device, max_models: int = 32, compute_dtype=None):
+        self.model = model
+        self.device = torch.device(device)
+        self.layout = ParamLayout.from_module(model)
+        self.max_models = max_models
+        self.compute_dtype = compute_dtype
+        self._interps = {}
+        self._batched_ok = True
+
+    def flatten(self, state_dict) -> torch.Tensor:
+        return self.layout.flatten(state_dict, device=self.device)
+
+    def _interp(self, c):
+        from ..parallel.batched_nn import BatchedInterpreter
+        if c not in self._interps:
+            self._interps[c] = BatchedInterpreter(self.model, self.layout, c)
+        return self._interps[c]
+
+    @torch.no_grad()
+    def evaluate(self, flats: torch.Tensor, data, target_label: Optional[int] = None) -> Dict[str, torch.Tensor]:
+        """flats: [S, P] models in this layout; data: iterable of (x, y). Returns per-model
+        ``correct``, ``loss`` (sum), ``total`` and, with ``target_label``, ``tp``/``fp``/``fn``."""
+        S = flats.shape[0]
+        res = {k: torch.zeros(S, dtype=torch.float64) for k in ("correct", "loss", "tp", "fp", "fn")}
+        total = 0
+        batches = [(x.to(self.device), y.to(self.device)) for x, y in data]
+        for y in (b[1] for b in batches):
+            total += y.numel()
+        for lo in range(0, S, self.max_models):
+            chunk = flats[lo:lo + self.max_models].to(self.device)
+            outs = self._run_chunk(chunk, batches)
+            for k, v in self._score(outs, batches, target_label).items():
+                res[k][lo:lo + chunk.shape[0]] = v.double().cpu()
+        res["total"] = torch.full((S,), float(total), dtype=torch.float64)
+        return res
+
+    def _run_chunk(self, chunk, batches):
+        c = chunk.shape[0]
+        if self._batched_ok:
+            try:
+                interp = self._interp(c)
+                views = {s.key: chunk[:, s.offset:s.offset + s.numel].view(c, *s.shape) for s in self.layout.slots}
+                return [interp.run(views, x.unsqueeze(0).expand(c, *x.shape).contiguous(), training=False,
+                                   dtype=self.compute_dtype).float() for x, _ in batches]
+            except Exception as e:  # models the fx tracer cannot batch → sequential functional calls
+                logging.info("batched evaluation unavailable (%s); evaluating models sequentially", e)
+                self._batched_ok = False
+        outs = [[] for _ in batches]
+        for i in range(c):
+            sd = self.layout.unflatten(chunk[i])
+            params = {k: v.to(self.device) for k, v in sd.items()}
+            self.model.to(self.device).eval()
+            for bi, (x, _) in enumerate(batches):
+                outs[bi].append(torch.func.functional_call(self.model, params, (x,)).float())
+        return [torch.stack(o) for o in outs]
+
+    @staticmethod
+    def _score(outs, batches, target_label):
+        c = outs[0].shape[0]
+        acc = {k: torch.zeros(c, device=outs[0].device) for k in ("correct", "loss", "tp", "fp", "fn")}
+        for out, (_, y) in zip(outs, batches):
+            pred = out.argmax(-1)
+            yy = y.unsqueeze(0).expand_as(pred)
+            acc["correct"] += (pred == yy).sum(1)
+            acc["loss"] += torch.nn.functional.cross_entropy(out.reshape(-1, out.shape[-1]), yy.reshape(-1),
+                                                             reduction="none").view(c, -1).sum(1)
+            if target_label is not None:
+                t = int(target_label)
+                acc["tp"] += ((pred == t) & (yy == t)).sum(1)
+                acc["fp"] += ((pred == t) & (yy != t)).sum(1)
+                acc["fn"] += ((pred != t) & (yy == t)).sum(1)
+        return acc
+
+
+def coalition_weights(masks: Sequence[int], sample_nums: Sequence[float]) -> torch.Tensor:
+    """[S, K] sample-weighted averaging matrix for coalitions given as bitmasks."""
+    K = len(sample_nums)
+    n = torch.tensor([float(v) for v in sample_nums], dtype=torch.float64)
+    W = torch.zeros(len(masks), K, dtype=torch.float64)
+    for r, m in enumerate(masks):
+        sel = torch.tensor([(m >> k) & 1 for k in range(K)], dtype=torch.bool)
+        W[r, sel] = n[sel] / n[sel].sum()
+    return W.float()
+
+
+def score_from_metrics(m: Dict[str, torch.Tensor], score: str = "acc", target_label=None) -> torch.Tensor:
+    """Per-model score used as the coalition value: accuracy or target-label F1/recall/precision."""
+    if target_label is None or score.lower() in ("acc", "accuracy"):
+        return m["correct"] / m["total"].clamp_min(1)
+    tp, fp, fn = m["tp"], m["fp"], m["fn"]
+    s = score.lower()
+    if s == "f1":
+        return torch.where(2 * tp + fp + fn > 0, 2 * tp / (2 * tp + fp + fn).clamp_min(1e-12), torch.zeros_like(tp))
+    if s in ("sensitivity", "recall", "tpr"):
+        return torch.where(tp + fn > 0, tp / (tp + fn).clamp_min(1e-12), torch.zeros_like(tp))
+    if s in ("precision", "ppv"):
+        return torch.where(tp + fp > 0, tp / (tp + fp).clamp_min(1e-12), torch.zeros_like(tp))
+    return m["correct"] / m["total"].clamp_min(1)
+
+
+class CoalitionValuer:
+    """Caches coalition values v(mask) for one round's K local models."""
+
+    def __init__(self, evaluator: BatchedModelEvaluator, flats: torch.Tensor, sample_nums, valid_data,
+                 score="acc", target_label=None):
+        self.ev = evaluator
+        self.flats = flats.to(evaluator.device)
+        self.n = list(sample_nums)
+        self.K = len(self.n)
+        self.data = list(valid_data)
+        self.score = score
+        self.target = target_label
+        self.v: Dict[int, float] = {0: 0.0}
+        self.metrics: Dict[int, Dict[str, float]] = {}
+        self.evaluations = 0
+
+    def ensure(self, masks: Sequence[int]):
+        todo = sorted({m for m in masks if m not in self.v})
+        if not todo:
+            return
+        W = coalition_weights(todo, self.n).to(self.flats.device)
+        models = ops.subset_aggregate(W, self.flats)
+        m = self.ev.evaluate(models, self.data, self.target)
+        vals = score_from_metrics(m, self.score, self.target)
+        for i, mask in enumerate(todo):
+            self.v[mask] = float(vals[i])
+            self.metrics[mask] = {k: float(t[i]) for k, t in m.items()}
+        self.evaluations += len(todo)
+
+    def exact_reference_sv(self) -> List[float]:
+        """The reference's exact estimator: for client i, average over every non-empty coalition
+        S of the others of [v(S ∪ i) − v(S)], plus v({i}) as one more term (accuracy deltas are
+        normalised by the partial model's total, identical to accuracy differences here)."""
+        K = self.K
+        full = (1 << K) - 1
+        self.ensure(range(1, full + 1))
+        sv = []
+        for i in range(K):
+            bit = 1 << i
+            ap, cnt = 0.0, 0
+            for S in range(1, full + 1):
+                if S & bit:
+                    continue
+                ap += self.v[S | bit] - self.v[S]
+                cnt += 1
+            ap += self.v[bit]
+            cnt += 1
+            sv.append(ap / cnt)
+        return sv
+
+    def monte_carlo_sv(self, rng: np.random.RandomState, tol=0.005, max_perms=None, batch_perms=None) -> List[float]:
+        """Permutation-sampling Shapley values (Castro et al.): average marginal contribution of
+        each client over random orderings; stops when the last three SV updates moved < ``tol``
+        (Euclidean) or after K² permutations — the reference's stopping rule. Unlike the reference
+        (which shuffles but then evaluates the UNshuffled prefixes), marginals are
+        credited to the permuted client. Prefix coalitions of a batch of permutations are
+        evaluated together."""
+        K = self.K
+        max_perms = max_perms or K * K
+        batch_perms = batch_perms or max(1, K)
+        sv = np.zeros(K)
+        d: List[float] = []
+        done = 0
+        while True:
+            perms = [rng.permutation(K) for _ in range(min(batch_perms, max_perms - done))]
+            prefixes = []
+            for p in perms:
+                m = 0
+                for c in p:
+                    m |= 1 << int(c)
+                    prefixes.append(m)
+            self.ensure(prefixes)
+            for p in perms:
+                last = sv.copy()
+                m, prev = 0, 0.0
+                contrib = np.zeros(K)
+                for c in p:
+                    m |= 1 << int(c)
+                    contrib[int(c)] = self.v[m] - prev
+                    prev = self.v[m]
+                sv = (done * sv + contrib) / (done + 1)
+                if done:
+                    d.append(float(np.linalg.norm(sv - last)))
+                done += 1
+            if done >= max_perms:
+                break
+            if done > K and all(x < tol for x in d[-3:]):
+                break
+        return sv.tolist()

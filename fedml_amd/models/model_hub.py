@@ -5,6 +5,7 @@ fallback to LogisticRegression, plus the north-star models the reference lacks
 (``resnet18`` for CIFAR, ``distilbert``, ``vit_b16``) and the rest of the zoo
 (resnet110, vgg, gan, darts, gkt split nets).
 """
+import math
 import logging
 
 from .cv.cnn import CNN_DropOut, CNN_OriginalFedAvg
@@ -31,7 +32,14 @@ def create(args, output_dim):
     ds = getattr(args, "dataset", "")
     logging.info("create_model. model_name = %s, output_dim = %s", name, output_dim)
     if name == "lr":
-        return LogisticRegression(_INPUT_DIMS.get(ds, 28 * 28), output_dim)
+        dim = _INPUT_DIMS.get(ds)
+        if dim is None:
+            from ..data.synthetic import get_spec
+            try:
+                dim = int(math.prod(get_spec(ds).shape))
+            except (KeyError, ValueError):
+                dim = 28 * 28
+        return LogisticRegression(dim, output_dim)
     if name == "cnn":
         if ds in ("femnist", "fed_emnist"):
             return CNN_DropOut(False)

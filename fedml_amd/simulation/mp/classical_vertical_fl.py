@@ -16,29 +16,12 @@ import torch
 import torch.nn as nn
 
 from ...core.distributed import ClientManager, Message, ServerManager
+from ...utils.metrics import roc_auc as _auc
 
 MSG_S2C_INIT_CONFIG = 1
 MSG_S2C_GRADIENT = 2
 MSG_C2S_LOGITS = 3
 MSG_S2C_FINISH = 4
-
-
-def _auc(scores, labels):
-    """Rank-based ROC AUC (Mann–Whitney U); ties get average rank."""
-    s = scores.double()
-    order = torch.argsort(s)
-    ranks = torch.empty_like(s)
-    ranks[order] = torch.arange(1, len(s) + 1, dtype=s.dtype)
-    uniq, inv = torch.unique(s, return_inverse=True)
-    if len(uniq) < len(s):
-        sums = torch.zeros(len(uniq), dtype=s.dtype).index_add_(0, inv, ranks)
-        cnt = torch.zeros(len(uniq), dtype=s.dtype).index_add_(0, inv, torch.ones_like(s))
-        ranks = (sums / cnt)[inv]
-    pos = labels > 0.5
-    n1, n0 = int(pos.sum()), int((~pos).sum())
-    if n1 == 0 or n0 == 0:
-        return float("nan")
-    return float((ranks[pos].sum() - n1 * (n1 + 1) / 2) / (n1 * n0))
 
 
 class _Party:

@@ -9,12 +9,11 @@ import logging
 
 import torch
 
-from ...core.arena import ParamLayout, fedavg_state_dicts, stack_state_dicts
+from ...core.server_update import robust_aggregate
 from ...core.robustness import RobustAggregator
 from ...data.backdoor import backdoor_test_set, poison_client_data
 from ...data.client_data import concat_client_data
 from .fl_protocol import FedAVGAggregator, FedAVGTrainer, run_fl
-from ... import ops
 
 
 class FedAvgRobustAggregator(FedAVGAggregator):
@@ -27,24 +26,7 @@ class FedAvgRobustAggregator(FedAVGAggregator):
             if self.test_data_local_dict else None
 
     def aggregate(self):
-        w_locals = self._w_locals()
-        dt = self.robust.defense_type
-        glob = self.get_global_model_params()
-        layout = ParamLayout(glob)
-        if dt == "coordinate_median":
-            avg = self.robust.coordinate_median_agg(w_locals)
-        else:
-            if dt in ("norm_diff_clipping", "weak_dp"):
-                stack = stack_state_dicts(layout, [sd for _, sd in w_locals])
-                gflat = layout.flatten(glob)
-                self.robust.clip_stack_(stack, gflat, layout)
-                counts = torch.tensor([float(n) for n, _ in w_locals])
-                avg_flat = ops.weighted_average(stack, counts)
-                if dt == "weak_dp":
-                    self.robust.noise_flat_(avg_flat, layout, self.round)
-                avg = layout.unflatten(avg_flat)
-            else:
-                avg = fedavg_state_dicts(w_locals)
+        avg = robust_aggregate(self.robust, self._w_locals(), self.get_global_model_params(), self.round)
         self.set_global_model_params(avg)
         self.round += 1
         return avg

@@ -21,6 +21,7 @@ class ModelTrainerCLS(ClientTrainer, FunctionalTrainerMixin):
         super().__init__(model, args)
         self.class_weight = None
         self.clip_grad_norm = None
+        self.input_hook = None  # optional per-batch input transform on device (HS-FedAvg amplitude mixing)
 
     def get_model_params(self):
         return {k: v.detach().cpu().clone() for k, v in self.model.state_dict().items()}
@@ -43,6 +44,8 @@ class ModelTrainerCLS(ClientTrainer, FunctionalTrainerMixin):
             batch_loss = []
             for x, labels in train_data:
                 x, labels = x.to(device, non_blocking=True), labels.to(device, non_blocking=True)
+                if self.input_hook is not None:
+                    x = self.input_hook(x)
                 optimizer.zero_grad(set_to_none=True)
                 loss = criterion(model(x), labels)
                 loss.backward()
