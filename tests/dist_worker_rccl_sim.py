@@ -1,0 +1,44 @@
+"""Worker for tests/test_rccl_dist.py: one rank of the RCCL simulator on CPU (gloo)."""
+import os
+import sys
+
+import torch
+
+
+def run(rank, world, port, out_path, model_name, clients, counts_seed):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    torch.set_num_threads(2)
+    from fedml_amd.arguments import Arguments
+    from fedml_amd.data.synthetic import get_spec
+    from fedml_amd.models import create
+    from fedml_amd.simulation.rccl.client_store import DeviceClientStore
+    from fedml_amd.simulation.rccl.simulator import RCCLSimulator
+    from fedml_amd.parallel import comm
+    ds = "mnist" if model_name == "lr" else "cifar10"
+    model_arg = "resnet56" if model_name == "resnet_shallow" else model_name
+    args = Arguments.from_dict({"x": {
+        "training_type": "simulation", "backend": "RCCL", "federated_optimizer": "FedAvg", "dataset": ds,
+        "model": model_arg, "client_num_in_total": clients, "client_num_per_round": clients, "comm_round": 2,
+        "epochs": 1, "batch_size": 8, "client_optimizer": "sgd", "learning_rate": 0.05, "frequency_of_the_test": 0,
+        "random_seed": 0, "shuffle": False}})
+    spec = get_spec(ds)
+    torch.manual_seed(0)
+    if model_name == "resnet_shallow":  # deep ResNets at init are chaotic in fp32 (see test_batched_engine)
+        from fedml_amd.models.cv.resnet import Bottleneck, ResNet
+        model = ResNet(Bottleneck, [1, 1, 1], spec.num_classes)
+    else:
+        model = create(args, spec.num_classes)
+    g = torch.Generator().manual_seed(counts_seed)
+    counts = [int(v) for v in torch.randint(8, 24, (clients,), generator=g)]
+    store = DeviceClientStore.synthetic_on_device(spec, counts, torch.device("cpu"), seed=0)
+    sim = RCCLSimulator(args, torch.device("cpu"), None, model, store=store)
+    sim.run(2)
+    if rank == 0:
+        torch.save(sim.global_flat.clone(), out_path)
+    comm.destroy()
+
+
+if __name__ == "__main__":
+    r, w, p = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
+    run(r, w, p, sys.argv[4], sys.argv[5], int(sys.argv[6]), int(sys.argv[7]))
