@@ -108,12 +108,13 @@ def init(args=None, argv=None):
             else:
                 args.n_node_in_silo = getattr(args, "n_node_in_silo", 1)
                 args.n_proc_per_node = getattr(args, "n_proc_per_node", 1)
-                args.n_proc_in_silo = int(os.environ.get("WORLD_SIZE", 1))
-                args.rank_in_node = int(os.environ.get("LOCAL_RANK", 0))
+                # torchrun env when launched per silo (reference); explicit config keys otherwise
+                args.n_proc_in_silo = int(os.environ.get("WORLD_SIZE", getattr(args, "n_proc_in_silo", 1)))
+                args.rank_in_node = int(os.environ.get("LOCAL_RANK", getattr(args, "rank_in_node", 0)))
                 args.process_id = args.rank_in_node
-                args.proc_rank_in_silo = int(os.environ.get("RANK", 0))
-                args.pg_master_address = os.environ.get("MASTER_ADDR", "127.0.0.1")
-                args.pg_master_port = int(os.environ.get("MASTER_PORT", 29300))
+                args.proc_rank_in_silo = int(os.environ.get("RANK", getattr(args, "proc_rank_in_silo", 0)))
+                args.pg_master_address = os.environ.get("MASTER_ADDR", getattr(args, "pg_master_address", "127.0.0.1"))
+                args.pg_master_port = int(os.environ.get("MASTER_PORT", getattr(args, "pg_master_port", 29300)))
                 args.launcher_rdzv_port = getattr(args, "launcher_rdzv_port", 29400)
     elif tt == FEDML_TRAINING_PLATFORM_CROSS_DEVICE:
         args.rank = 0
@@ -210,7 +211,7 @@ def run_distributed(args=None):
     args = init(args)
     from .distributed import CheetahTrainer
     dev, dataset, mdl = _prepare(args)
-    return CheetahTrainer(args, dev, dataset, mdl).run()
+    return CheetahTrainer(args, dev, mdl, dataset).train()
 
 
 def __getattr__(name):

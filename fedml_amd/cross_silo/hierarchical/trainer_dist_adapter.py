@@ -1,0 +1,79 @@
+"""Silo-side data-parallel trainer (reference: `cross_silo/hierarchical/trainer_dist_adapter.py:40-141`).
+
+Every process of a silo holds a ``FlatDDP`` replica (bucketed RCCL all-reduce overlapped with
+backward, see ``distributed.ddp``) and trains on its shard of the silo's data; the model trainer
+is unchanged — gradient averaging completes automatically at the end of each backward. The
+master broadcasts the global model to the silo with ONE flat-buffer broadcast (the reference uses
+``broadcast_object_list`` of a pickled state dict)."""
+import torch
+import torch.distributed as dist
+
+from ...data.client_data import ClientData, split_client_data
+from ...distributed.ddp import FlatDDP
+from ...trainers import create_model_trainer
+from .process_group_manager import ProcessGroupManager
+
+
+class TrainerDistAdapter:
+    def __init__(self, args, device, client_rank, model, train_data_num, train_data_local_num_dict,
+                 train_data_local_dict, test_data_local_dict, model_trainer=None):
+        self.args = args
+        self.device = torch.device(device) if device is not None else torch.device("cpu")
+        self.n_proc = int(getattr(args, "n_proc_in_silo", 1) or 1)
+        self.rank_in_silo = int(getattr(args, "proc_rank_in_silo", 0) or 0)
+        self.pg = None
+        if self.n_proc > 1:
+            self.pg = ProcessGroupManager(self.rank_in_silo, self.n_proc, getattr(args, "pg_master_address", "127.0.0.1"),
+                                          int(getattr(args, "pg_master_port", 29700)),
+                                          only_gpu=self.device.type == "cuda")
+        model = model.to(self.device)
+        self.ddp = FlatDDP(model, self.device, bucket_mb=float(getattr(args, "ddp_bucket_mb", 64.0))) \
+            if self.n_proc > 1 else None
+        self.model = model
+        self.trainer = model_trainer or create_model_trainer(model, args)
+        self.trainer.model = self.ddp if self.ddp is not None else model
+        self.client_rank = client_rank
+        self.train_data_local_dict = train_data_local_dict
+        self.train_data_local_num_dict = train_data_local_num_dict
+        self.test_data_local_dict = test_data_local_dict
+        self.client_index = None
+        self.train_local = None
+
+    def _shard(self, data):
+        if isinstance(data, (list, tuple)):  # already sharded by data.load_cross_silo
+            return data[self.rank_in_silo]
+        if isinstance(data, ClientData) and self.n_proc > 1:
+            return split_client_data(data, self.n_proc)[self.rank_in_silo]
+        return data
+
+    def update_dataset(self, client_index):
+        self.client_index = int(client_index)
+        self.train_local = self._shard(self.train_data_local_dict[self.client_index])
+        self.local_sample_number = self.train_data_local_num_dict[self.client_index]
+        self.trainer.set_id(self.client_index)
+
+    def update_model(self, params):
+        if params is not None:
+            self.model.load_state_dict(params)
+
+    def get_model_params(self):
+        return {k: v.detach().cpu().clone() for k, v in self.model.state_dict().items()}
+
+    def sync_model(self):
+        """Collective: every silo rank leaves with rank 0's parameters and buffers."""
+        if self.ddp is None:
+            return
+        dist.broadcast(self.ddp.flat, 0)
+        for b in self.model.buffers():
+            dist.broadcast(b, 0)
+
+    def train(self, round_idx=None):
+        self.args.round_idx = round_idx
+        if self.ddp is not None:
+            dist.barrier()
+        self.trainer.train(self.train_local, self.device, self.args)
+        return self.get_model_params(), self.local_sample_number
+
+    def cleanup_pg(self):
+        if self.pg is not None:
+            self.pg.cleanup()

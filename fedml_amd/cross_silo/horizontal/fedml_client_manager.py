@@ -1,0 +1,106 @@
+"""Cross-silo client state machine (reference: `cross_silo/horizontal/fedml_client_manager.py:14-173`).
+
+On connection-ready: report ONLINE, start a system-metrics reporter (a daemon thread sampling
+CPU / host memory / GPU utilisation via rocm-smi every ``sys_perf_interval`` seconds — the
+reference forks a process). On init / sync: load the global model, switch to the assigned
+data silo, train, upload (tensors travel as raw frames; no tensor→list conversion).
+"""
+import json
+import logging
+import platform
+import threading
+
+from ...core.distributed import ClientManager, Message
+from ...core.mlops import MLOpsMetrics, MLOpsProfilerEvent
+from ..message_define import MyMessage
+from .fedml_server_manager import inject_connection_ready, parse_client_ids
+
+
+class FedMLClientManager(ClientManager):
+    def __init__(self, args, trainer, comm=None, client_rank=0, client_num=0, backend="TCP"):
+        super().__init__(args, comm, client_rank, client_num, backend)
+        self.trainer = trainer
+        self.num_rounds = int(args.comm_round)
+        self.round_idx = 0
+        self.client_real_ids = parse_client_ids(args, client_num - 1)
+        self.client_real_id = self.client_real_ids[self.get_sender_id() - 1]
+        self.has_sent_online_msg = False
+        self._stop_stats = threading.Event()
+        self.final_model = None
+
+    def run(self):
+        inject_connection_ready(self)
+        super().run()
+
+    def register_message_receive_handlers(self):
+        self.register_message_receive_handler(MyMessage.MSG_TYPE_CONNECTION_IS_READY,
+                                              self.handle_message_connection_ready)
+        self.register_message_receive_handler(MyMessage.MSG_TYPE_S2C_INIT_CONFIG, self.handle_message_init)
+        self.register_message_receive_handler(MyMessage.MSG_TYPE_S2C_SYNC_MODEL_TO_CLIENT,
+                                              self.handle_message_receive_model_from_server)
+        self.register_message_receive_handler(MyMessage.MSG_TYPE_S2C_FINISH, self.handle_finish)
+
+    def handle_message_connection_ready(self, msg):
+        if self.has_sent_online_msg:
+            return
+        self.has_sent_online_msg = True
+        self.send_client_status(0)
+        MLOpsMetrics.get_instance().report_client_training_status(self.client_real_id,
+                                                                  MyMessage.MSG_MLOPS_CLIENT_STATUS_INITIALIZING)
+        interval = float(getattr(self.args, "sys_perf_interval", 30.0) or 0)
+        if interval > 0:
+            threading.Thread(target=self.report_sys_performances, args=(interval,), daemon=True).start()
+
+    def handle_message_init(self, msg):
+        MLOpsMetrics.get_instance().report_client_training_status(self.client_real_id,
+                                                                  MyMessage.MSG_MLOPS_CLIENT_STATUS_TRAINING)
+        self.trainer.update_model(msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS))
+        self.trainer.update_dataset(int(msg.get(MyMessage.MSG_ARG_KEY_CLIENT_INDEX)))
+        self.round_idx = int(msg.get(MyMessage.MSG_ARG_KEY_ROUND_INDEX, 0))
+        self.__train()
+
+    def handle_message_receive_model_from_server(self, msg):
+        self.trainer.update_model(msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS))
+        self.trainer.update_dataset(int(msg.get(MyMessage.MSG_ARG_KEY_CLIENT_INDEX)))
+        self.round_idx = int(msg.get(MyMessage.MSG_ARG_KEY_ROUND_INDEX, self.round_idx + 1))
+        self.__train()
+
+    def handle_finish(self, msg):
+        params = msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS)
+        if params is not None:
+            self.trainer.update_model(params)
+            self.final_model = params
+        MLOpsMetrics.get_instance().report_client_training_status(self.client_real_id,
+                                                                  MyMessage.MSG_MLOPS_CLIENT_STATUS_FINISHED)
+        self._stop_stats.set()
+        self.finish()
+
+    def send_model_to_server(self, receive_id, weights, local_sample_num):
+        MLOpsProfilerEvent.get_instance().log_event_started("comm_c2s", event_value=str(self.round_idx))
+        m = Message(MyMessage.MSG_TYPE_C2S_SEND_MODEL_TO_SERVER, self.client_real_id, receive_id)
+        m.add_params(MyMessage.MSG_ARG_KEY_MODEL_PARAMS, weights)
+        m.add_params(MyMessage.MSG_ARG_KEY_NUM_SAMPLES, local_sample_num)
+        self.send_message(m)
+
+    def send_client_status(self, receive_id, status="ONLINE"):
+        m = Message(MyMessage.MSG_TYPE_C2S_CLIENT_STATUS, self.client_real_id, receive_id)
+        name = platform.system()
+        m.add_params(MyMessage.MSG_ARG_KEY_CLIENT_STATUS, status)
+        m.add_params(MyMessage.MSG_ARG_KEY_CLIENT_OS, "Mac" if name == "Darwin" else name)
+        self.send_message(m)
+
+    def report_sys_performances(self, interval):
+        from ...core.mlops import SysStats
+        stats = SysStats()
+        while not self._stop_stats.wait(interval):
+            try:
+                MLOpsMetrics.get_instance().report_system_metric(stats.produce_info())
+            except Exception:
+                logging.debug("system metric sampling failed", exc_info=True)
+
+    def __train(self):
+        prof = MLOpsProfilerEvent.get_instance()
+        prof.log_event_started("train", event_value=str(self.round_idx))
+        weights, n = self.trainer.train(self.round_idx)
+        prof.log_event_ended("train", event_value=str(self.round_idx))
+        self.send_model_to_server(0, weights, n)

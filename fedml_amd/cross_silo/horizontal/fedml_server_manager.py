@@ -1,0 +1,147 @@
+"""Cross-silo server state machine (reference: `cross_silo/horizontal/fedml_server_manager.py:15-263`).
+
+Handshake: every client reports ``C2S_CLIENT_STATUS = ONLINE``; when all ids of
+``client_id_list`` are online the server sends ``S2C_INIT_CONFIG`` (global model + data-silo
+index) to the round's selected clients. Each round: collect ``C2S_SEND_MODEL_TO_SERVER`` from
+the selected clients, aggregate (flat-arena kernel), test, report round info, send
+``S2C_SYNC_MODEL_TO_CLIENT``. After ``comm_round`` rounds the server stops (clients stop after
+the final sync, as in the reference, and additionally on ``S2C_FINISH``).
+"""
+import json
+import logging
+import time
+
+from ...core.distributed import Message, ServerManager
+from ...core.mlops import MLOpsMetrics, MLOpsProfilerEvent
+from ..message_define import MyMessage
+
+
+def parse_client_ids(args, n_clients):
+    ids = getattr(args, "client_id_list", None)
+    if isinstance(ids, str) and ids.strip():
+        return [int(v) for v in json.loads(ids)]
+    if isinstance(ids, (list, tuple)) and ids:
+        return [int(v) for v in ids]
+    return list(range(1, n_clients + 1))
+
+
+def federation_size(args):
+    """Transport world = server + silos: from ``client_id_list`` when given, else
+    ``client_num_per_round + 1`` (``worker_num`` in hierarchical mode counts silos only)."""
+    ids = getattr(args, "client_id_list", None)
+    if ids:
+        return len(parse_client_ids(args, 0)) + 1
+    return int(getattr(args, "client_num_per_round", 1)) + 1
+
+
+class FedMLServerManager(ServerManager):
+    def __init__(self, args, aggregator, comm=None, client_rank=0, client_num=0, backend="TCP",
+                 is_preprocessed=False, preprocessed_client_lists=None):
+        super().__init__(args, comm, client_rank, client_num, backend)
+        self.aggregator = aggregator
+        self.round_num = int(args.comm_round)
+        self.round_idx = 0
+        self.is_preprocessed = is_preprocessed
+        self.preprocessed_client_lists = preprocessed_client_lists
+        self.client_real_ids = parse_client_ids(args, client_num - 1)
+        self.client_online_mapping = {}
+        self.start_running_time = 0.0
+        self.round_times = []
+        self._selected = []
+        self._started = False
+
+    def run(self):
+        inject_connection_ready(self)
+        super().run()
+
+    # ------------------------------------------------------------------------------------------
+    def register_message_receive_handlers(self):
+        self.register_message_receive_handler(MyMessage.MSG_TYPE_CONNECTION_IS_READY, self.handle_connection_ready)
+        self.register_message_receive_handler(MyMessage.MSG_TYPE_C2S_CLIENT_STATUS,
+                                              self.handle_message_client_status_update)
+        self.register_message_receive_handler(MyMessage.MSG_TYPE_C2S_SEND_MODEL_TO_SERVER,
+                                              self.handle_message_receive_model_from_client)
+
+    def handle_connection_ready(self, msg):
+        MLOpsMetrics.get_instance().report_server_training_status(getattr(self.args, "run_id", "0"),
+                                                                  MyMessage.MSG_MLOPS_SERVER_STATUS_STARTING)
+
+    def handle_message_client_status_update(self, msg):
+        if msg.get(MyMessage.MSG_ARG_KEY_CLIENT_STATUS) == "ONLINE":
+            self.client_online_mapping[int(msg.get_sender_id())] = True
+        if not self._started and all(self.client_online_mapping.get(c, False) for c in self.client_real_ids):
+            self._started = True
+            MLOpsMetrics.get_instance().report_server_training_status(getattr(self.args, "run_id", "0"),
+                                                                      MyMessage.MSG_MLOPS_SERVER_STATUS_RUNNING)
+            self.send_init_msg()
+
+    def _selection(self):
+        ids = self.aggregator.client_selection(self.round_idx, self.client_real_ids,
+                                               int(getattr(self.args, "client_num_per_round", len(self.client_real_ids))))
+        silos = self.aggregator.data_silo_selection(self.round_idx, int(self.args.client_num_in_total), len(ids))
+        return ids, silos
+
+    def send_init_msg(self):
+        self.start_running_time = time.time()
+        self._t0 = time.time()
+        g = self.aggregator.get_global_model_params()
+        ids, silos = self._selection()
+        self._selected = ids
+        self.aggregator.flag_client_model_uploaded_dict = {i: False for i in range(len(ids))}
+        for cid, silo in zip(ids, silos):
+            self._send(MyMessage.MSG_TYPE_S2C_INIT_CONFIG, cid, g, silo)
+        MLOpsProfilerEvent.get_instance().log_event_started("server.wait", event_value=str(self.round_idx))
+
+    def _send(self, mtype, receiver, params, silo):
+        m = Message(mtype, self.get_sender_id(), receiver)
+        m.add_params(MyMessage.MSG_ARG_KEY_MODEL_PARAMS, params)
+        m.add_params(MyMessage.MSG_ARG_KEY_CLIENT_INDEX, str(silo))
+        m.add_params(MyMessage.MSG_ARG_KEY_ROUND_INDEX, self.round_idx)
+        self.send_message(m)
+
+    def handle_message_receive_model_from_client(self, msg):
+        sender = int(msg.get(MyMessage.MSG_ARG_KEY_SENDER))
+        prof = MLOpsProfilerEvent.get_instance()
+        prof.log_event_ended("comm_c2s", event_value=str(self.round_idx), event_edge_id=sender)
+        self.aggregator.add_local_trained_result(self._selected.index(sender),
+                                                 msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS),
+                                                 msg.get(MyMessage.MSG_ARG_KEY_NUM_SAMPLES))
+        if not self.aggregator.check_whether_all_receive():
+            return
+        prof.log_event_ended("server.wait", event_value=str(self.round_idx))
+        prof.log_event_started("aggregate", event_value=str(self.round_idx))
+        g = self.aggregator.aggregate()
+        prof.log_event_ended("aggregate", event_value=str(self.round_idx))
+        try:
+            self.aggregator.test_on_server_for_all_clients(self.round_idx)
+        except Exception:  # evaluation must never stall the federation (reference behaviour)
+            logging.exception("server-side test failed")
+        now = time.time()
+        self.round_times.append(now - self._t0)
+        self._t0 = now
+        MLOpsMetrics.get_instance().report_server_training_round_info(
+            {"run_id": getattr(self.args, "run_id", "0"), "round_index": self.round_idx,
+             "total_rounds": self.round_num, "running_time": round(now - self.start_running_time, 4)})
+        self.round_idx += 1
+        if self.round_idx == self.round_num:
+            # final sync lets clients see the final model; then everyone stops
+            for cid in self.client_real_ids:
+                self._send(MyMessage.MSG_TYPE_S2C_FINISH, cid, g, 0)
+            MLOpsMetrics.get_instance().report_server_training_status(getattr(self.args, "run_id", "0"),
+                                                                      MyMessage.MSG_MLOPS_SERVER_STATUS_FINISHED)
+            self.finish()
+            return
+        ids, silos = self._selection()
+        self._selected = ids
+        self.aggregator.flag_client_model_uploaded_dict = {i: False for i in range(len(ids))}
+        for cid, silo in zip(ids, silos):
+            self._send(MyMessage.MSG_TYPE_S2C_SYNC_MODEL_TO_CLIENT, cid, g, silo)
+        prof.log_event_started("server.wait", event_value=str(self.round_idx))
+
+
+def inject_connection_ready(mgr):
+    """Transports without a broker (loopback, TCP, gRPC) get the local CONNECTION_IS_READY the
+    MQTT transport emits on connect (`mqtt_s3_multi_clients_comm_manager.py:175-180`)."""
+    from ...core.distributed.communication.pubsub import MqttS3CommManager
+    if not isinstance(mgr.com_manager, MqttS3CommManager):
+        mgr.com_manager.deliver(Message(MyMessage.MSG_TYPE_CONNECTION_IS_READY, mgr.rank, mgr.rank))
