@@ -1,0 +1,130 @@
+#!/usr/bin/env python3
+"""Per-kernel roofline table for one native ResNet training step (C clients × N samples).
+
+Wraps every ``ops.nn_ops`` launch with HIP events, derives the ideal HBM bytes and MFMA flops of
+each launch from its arguments, and prints time, achieved GB/s and TFLOP/s aggregated by
+(op, geometry). Usage: python scripts/layer_prof.py [--C 100] [--N 64] [--model resnet56]
+"""
+import argparse
+import collections
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch
+
+from fedml_amd.core.arena import ParamLayout
+from fedml_amd.models.cv.resnet import resnet56, resnet110
+from fedml_amd.ops import nn_ops
+from fedml_amd.parallel.native_resnet import NativeResNetStep
+
+REC = []
+ENABLED = [False]
+
+
+def _wrap(name, cost):
+    orig = getattr(nn_ops, name)
+
+    def f(*a, **k):
+        if not ENABLED[0]:
+            return orig(*a, **k)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        r = orig(*a, **k)
+        e.record()
+        label, nbytes, flops = cost(*a)
+        REC.append((name, label, s, e, nbytes, flops))
+        return r
+    setattr(nn_ops, name, f)
+
+
+def c_fwd(x, wpk, ld, ps, pt, y, st, C, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, ldk, tpw):
+    return (f"{KH}x{KW} {Cin}->{Cout} s{stride} @{H}" + (" +bnrelu" if ps is not None else ""),
+            C * N * (H * W * Cin + Ho * Wo * Cout) * 2, 2 * C * N * Ho * Wo * Cout * KH * KW * Cin)
+
+
+def c_bwd(g, y, al, be, ga, wpk, ld, dx, epi, ex, es, et, eadd, ey1, ey2, st, C, N, Hy, Wy, Cout, Cin, KH, KW, stride,
+          pad, Hx, Wx, ldk2, tpw):
+    extra = {1: 0, 2: 1, 3: 3 + (ey2 is not None)}[epi]
+    return (f"{KH}x{KW} {Cin}<-{Cout} s{stride} @{Hx} epi{epi}",
+            C * N * (2 * Hy * Wy * Cout + (1 + extra) * Hx * Wx * Cin) * 2,
+            2 * C * N * Hx * Wx * Cin * KH * KW * Cout)
+
+
+def c_wgrad(g, y, al, be, ga, x, ps, pt, garena, woff, C, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ppw, cs,
+            scratch):
+    return (f"{KH}x{KW} {Cin}->{Cout} s{stride} @{H}" + (" +bnrelu" if ps is not None else ""),
+            C * N * (2 * Ho * Wo * Cout + H * W * Cin) * 2, 2 * C * N * Ho * Wo * Cout * KH * KW * Cin)
+
+
+def c_block(y, s, t, r, rs, rt, out, C, per, Ch):
+    return (f"ch{Ch} n{per // Ch}" + (" ds" if rs is not None else ""), C * per * 2 * (3 if r is not None else 2), 0)
+
+
+def c_other(*a):
+    return ("", 0, 0)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--C", type=int, default=100)
+    ap.add_argument("--N", type=int, default=64)
+    ap.add_argument("--model", default="resnet56")
+    ap.add_argument("--steps", type=int, default=3)
+    a = ap.parse_args()
+    _wrap("conv_fwd", c_fwd)
+    _wrap("conv_bwd_data", c_bwd)
+    _wrap("conv_wgrad", c_wgrad)
+    _wrap("block_out", c_block)
+    for n in ("bn_fwd_finalize", "bn_bwd_finalize", "pack_weights", "avgpool", "head_bwd", "nchw_to_nhwc_pad"):
+        _wrap(n, c_other)
+    torch.manual_seed(0)
+    model = {"resnet56": resnet56, "resnet110": resnet110}[a.model](class_num=100)
+    layout = ParamLayout.from_module(model)
+    dev = "cuda"
+    flat = layout.flatten(model.state_dict()).to(dev)
+    arena = flat.view(1, -1).repeat(a.C, 1).contiguous()
+    garena = torch.zeros_like(arena)
+    x = torch.randn(a.C, a.N, 3, 32, 32, device=dev)
+    y = torch.randint(0, 100, (a.C, a.N), device=dev)
+    rs = torch.full((a.C, a.N), 1.0 / a.N, device=dev)
+    act = torch.ones(a.C, device=dev)
+    step = NativeResNetStep(model, layout, a.C, dev)
+    for _ in range(2):
+        step.step(arena, garena, x, y, rs, act)
+    torch.cuda.synchronize()
+    ENABLED[0] = True
+    t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0.record()
+    for _ in range(a.steps):
+        garena.zero_()
+        step.step(arena, garena, x, y, rs, act)
+    t1.record()
+    torch.cuda.synchronize()
+    ENABLED[0] = False
+    total_ms = t0.elapsed_time(t1) / a.steps
+    agg = collections.OrderedDict()
+    for name, label, s, e, nb, fl in REC:
+        k = (name, label)
+        d = agg.setdefault(k, [0, 0.0, 0, 0])
+        d[0] += 1
+        d[1] += s.elapsed_time(e)
+        d[2] += nb
+        d[3] += fl
+    rows = sorted(agg.items(), key=lambda kv: -kv[1][1])
+    by_op = collections.Counter()
+    print(f"step time {total_ms:.2f} ms  (C={a.C}, N={a.N}, {a.model}); per-step numbers below")
+    print(f"{'op':16s} {'geometry':34s} {'calls':>5s} {'ms':>8s} {'us/call':>8s} {'GB/s':>7s} {'TF/s':>6s}")
+    for (name, label), (n, ms, nb, fl) in rows:
+        ms_s = ms / a.steps
+        by_op[name] += ms_s
+        gbs = nb / (ms * 1e-3) / 1e9 if ms else 0
+        tfs = fl / (ms * 1e-3) / 1e12 if ms else 0
+        print(f"{name:16s} {label:34s} {n // a.steps:5d} {ms_s:8.3f} {1000 * ms / n:8.1f} {gbs:7.0f} {tfs:6.1f}")
+    print("-- by op:", ", ".join(f"{k} {v:.2f} ms" for k, v in by_op.most_common()))
+    print(f"-- kernels {sum(by_op.values()):.2f} ms of {total_ms:.2f} ms step (rest = torch head/zeroing/launch gaps)")
+
+
+if __name__ == "__main__":
+    main()
