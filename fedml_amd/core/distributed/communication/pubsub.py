@@ -162,8 +162,9 @@ def default_blob_store(args=None):
 
 class MqttS3CommManager(QueueCommManager):
     def __init__(self, broker, blob_store, rank: int, size: int, run_id: str = "0", file_mode: bool = False,
-                 client_ids: Optional[List[int]] = None):
+                 client_ids: Optional[List[int]] = None, file_cache_dir: Optional[str] = None):
         super().__init__(rank, size)
+        self.file_cache_dir = file_cache_dir or os.path.join(".", "model_file_cache", f"rank{rank}")
         self.broker = broker
         self.blobs = blob_store
         self.run_id = run_id
@@ -197,6 +198,14 @@ class MqttS3CommManager(QueueCommManager):
         url = params.get(Message.MSG_ARG_KEY_MODEL_PARAMS_URL)
         if url and self.blobs is not None and not self.file_mode:
             params[Message.MSG_ARG_KEY_MODEL_PARAMS] = decode(self.blobs.read(url))
+        elif url and self.blobs is not None:
+            # model FILE transfer (MQTT_S3_MNN): materialise the blob as a local file, hand over its path
+            os.makedirs(self.file_cache_dir, exist_ok=True)
+            path = os.path.join(self.file_cache_dir, os.path.basename(url.split("://", 1)[1]) + params.get(
+                "model_file_suffix", ""))
+            with open(path, "wb") as f:
+                f.write(self.blobs.read(url))
+            params[Message.MSG_ARG_KEY_MODEL_PARAMS] = path
         m = Message()
         m.init(params)
         self.deliver(m)
@@ -210,6 +219,7 @@ class MqttS3CommManager(QueueCommManager):
             if self.file_mode and isinstance(model, str):
                 with open(model, "rb") as f:
                     url = self.blobs.write(key, f.read())
+                params["model_file_suffix"] = os.path.splitext(model)[1]
             else:
                 url = self.blobs.write(key, encode(model))
             params.pop(Message.MSG_ARG_KEY_MODEL_PARAMS)

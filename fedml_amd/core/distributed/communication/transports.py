@@ -296,5 +296,7 @@ def create_comm_manager(backend: str, rank: int, size: int, args=None, router: L
     if b in ("MQTT", "MQTT_S3", "MQTT_S3_MNN"):
         from .pubsub import MqttS3CommManager, default_broker, default_blob_store
         return MqttS3CommManager(default_broker(args), default_blob_store(args) if b != "MQTT" else None, rank,
-                                 size, run_id=str(getattr(args, "run_id", "0")), file_mode=(b == "MQTT_S3_MNN"))
+                                 size, run_id=str(getattr(args, "run_id", "0")), file_mode=(b == "MQTT_S3_MNN"),
+                                 file_cache_dir=os.path.join(getattr(args, "model_file_cache_folder", None)
+                                                             or "./model_file_cache", f"rank{rank}"))
     raise ValueError(f"unknown comm backend {backend}")
