@@ -1,0 +1,553 @@
+// Spatially tiled 3×3 / stride-1 / pad-1 convolution kernels for the client-batched ResNet
+// (gfx950, wave64, v_mfma_f32_16x16x32_bf16).
+//
+// Why a dedicated path: the generic implicit-GEMM kernels gather every A element per tap from
+// global memory (9 × the input bytes through L2, an integer divide per K step, the BatchNorm
+// operand transform re-applied 9 times) and reach only 5–15 % of HBM bandwidth on the 3×3 layers
+// of ResNet-56 (16/32/64 channels at 32²/16²/8²). Here a workgroup stages whole images of one
+// client ONCE into LDS — already transformed (relu(x·s+t) forward, α·g+β·y+γ backward), with a
+// zero halo of one pixel — and all nine taps read the tile from LDS:
+//
+//   conv3x3_gemm_kernel  forward (out = conv(act(x)), epilogue BN statistics Σy, Σy²)  and
+//                        backward-data (dx = convᵀ(dy), epilogue ReLU mask of the previous BN
+//                        + its backward statistics Σg', Σg'·x)  — taps flipped via the halo index
+//   conv3x3_wgrad_kernel dW[co][tap][ci] = Σ_p dy[p][co] · act(x)[p ⊕ tap][ci]; both operands are
+//                        read pixel-major with gfx950's transposing LDS read ds_read_b64_tr_b16,
+//                        the im2col shift is only an address offset into the haloed tile.
+//
+// LDS pixel stride = channels + 8 (bf16): 16-B-aligned for the vector staging writes and
+// bank-spread for both the row reads (ds_read_b128) and the transposed reads.
+#include "common.h"
+
+namespace c3 {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+__device__ __forceinline__ bf16x8 as_bf16x8(uint4 v) {
+  union { uint4 u; bf16x8 b; } c;
+  c.u = v;
+  return c.b;
+}
+__device__ __forceinline__ void unpack8(uint4 v, float* f) {
+  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
+  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
+}
+__device__ __forceinline__ uint32_t pack2(float a, float b) {
+  return (uint32_t)f32_to_bf16(a) | ((uint32_t)f32_to_bf16(b) << 16);
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint4 r;
+  r.x = pack2(f[0], f[1]); r.y = pack2(f[2], f[3]); r.z = pack2(f[4], f[5]); r.w = pack2(f[6], f[7]);
+  return r;
+}
+
+enum { XF_NONE = 0, XF_BNRELU = 1, XF_DY = 2 };
+enum { EPI_FWD = 0, EPI_MASK = 2 };
+
+// Stage images [s0, s0+ns) of one client into a zero-haloed LDS tile [ns][H+2][W+2][ld],
+// applying the operand transform. `src`/`src2` already point at the client.
+template <int KC, int XF>
+__device__ __forceinline__ void stage_tile(uint16_t* tile, const uint16_t* __restrict__ src,
+                                           const uint16_t* __restrict__ src2, const float* v0, const float* v1,
+                                           const float* v2, int s0, int ns, int H, int W) {
+  constexpr int LD = KC + 8;
+  constexpr int CG = KC / 8;
+  const int Hp = H + 2, Wp = W + 2;
+  const int total = ns * Hp * Wp * CG;
+  for (int i = threadIdx.x; i < total; i += 256) {
+    const int cg = i % CG;
+    const int pix = i / CG;
+    const int im = pix / (Hp * Wp);
+    const int r = pix % (Hp * Wp);
+    const int pr = r / Wp, pc = r % Wp;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (pr >= 1 && pr <= H && pc >= 1 && pc <= W) {
+      const int64_t off = ((((int64_t)(s0 + im) * H) + (pr - 1)) * W + (pc - 1)) * KC + cg * 8;
+      v = *reinterpret_cast<const uint4*>(src + off);
+      if (XF != XF_NONE) {
+        float f[8];
+        unpack8(v, f);
+        if (XF == XF_BNRELU) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j] * v0[cg * 8 + j] + v1[cg * 8 + j], 0.f);
+        } else {
+          float y[8];
+          unpack8(*reinterpret_cast<const uint4*>(src2 + off), y);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = v0[cg * 8 + j] * f[j] + v1[cg * 8 + j] * y[j] + v2[cg * 8 + j];
+        }
+        v = pack8(f);
+      }
+    }
+    *reinterpret_cast<uint4*>(tile + (int64_t)pix * LD + cg * 8) = v;
+  }
+}
+
+struct Args {
+  const uint16_t* src;   // x (forward) or g (backward-data)        [C][N][H][W][KC]
+  const uint16_t* src2;  // y for XF_DY
+  const uint16_t* wpk;   // packed weights [C][NOUT][ldk], k = tap·KC + kc
+  int64_t wpk_ld;
+  const float* vec0;     // scale | α
+  const float* vec1;     // shift | β
+  const float* vec2;     //       | γ
+  uint16_t* out;         // [C][N][H][W][NOUT]
+  const uint16_t* e_x;   // EPI_MASK: previous raw activation [C][N][H][W][NOUT]
+  const float* e_s;
+  const float* e_t;
+  float* stats;          // [C][NOUT][NS]
+  int NS;
+  int N, H, W;
+  int ldk;
+  int imgs_per_wg, imgs_per_stage;
+};
+
+// MTW 16-pixel tiles per wave share every B fragment read.
+template <int KC, int NOUT, int XF, int BWD, int EPI, int MTW>
+__global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
+  constexpr int NT = NOUT / 16;
+  constexpr int LD = KC + 8;
+  constexpr int K = 9 * KC;
+  constexpr int KSTEPS = (K + 31) / 32;
+  constexpr int CG = NOUT / 8;
+  constexpr int ROWS_PER_PASS = 64 / CG;
+  const int c = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int g = lane >> 4;
+  const int H = a.H, W = a.W, HW = H * W;
+  const int Wp = W + 2, HpWp = (H + 2) * (W + 2);
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  uint16_t* wl = reinterpret_cast<uint16_t*>(smem);                        // [NOUT][ldk]
+  float* v0 = reinterpret_cast<float*>(smem + (size_t)NOUT * a.ldk * 2);   // [KC] ×3
+  float* v1 = v0 + KC;
+  float* v2 = v1 + KC;
+  float* red = v2 + KC;                                                     // [4][NOUT][3]
+  uint16_t* stage = reinterpret_cast<uint16_t*>(red + 4 * NOUT * 3);       // [4][16][NOUT]
+  uint16_t* my_stage = stage + wid * 16 * NOUT;
+  uint16_t* tile = stage + 4 * 16 * NOUT;                                   // [S][H+2][W+2][LD]
+
+  {
+    const uint4* s = reinterpret_cast<const uint4*>(a.wpk + (int64_t)c * a.wpk_ld);
+    uint4* d = reinterpret_cast<uint4*>(wl);
+    const int n16 = NOUT * a.ldk / 8;
+    for (int i = threadIdx.x; i < n16; i += 256) d[i] = s[i];
+    if (XF != XF_NONE)
+      for (int i = threadIdx.x; i < KC; i += 256) {
+        v0[i] = a.vec0[(int64_t)c * KC + i];
+        v1[i] = a.vec1[(int64_t)c * KC + i];
+        if (XF == XF_DY) v2[i] = a.vec2[(int64_t)c * KC + i];
+      }
+    for (int i = threadIdx.x; i < 4 * NOUT * 3; i += 256) red[i] = 0.f;
+  }
+
+  const uint16_t* src = a.src + (int64_t)c * a.N * HW * KC;
+  const uint16_t* src2 = (XF == XF_DY) ? a.src2 + (int64_t)c * a.N * HW * KC : nullptr;
+  uint16_t* out = a.out + (int64_t)c * a.N * HW * NOUT;
+
+  float st0[8], st1[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) { st0[j] = 0.f; st1[j] = 0.f; }
+  const int my_cg = lane % CG;
+
+  // per-lane K-step geometry (compile-time KC): k = ks·32 + 8g → (tap, ci)
+  const int img_lo = blockIdx.x * a.imgs_per_wg;
+  const int img_hi = min(a.N, img_lo + a.imgs_per_wg);
+  for (int s0 = img_lo; s0 < img_hi; s0 += a.imgs_per_stage) {
+    const int ns = min(a.imgs_per_stage, img_hi - s0);
+    __syncthreads();  // previous stage fully consumed (and, first time, weights/vectors visible)
+    stage_tile<KC, XF>(tile, src, src2, v0, v1, v2, s0, ns, H, W);
+    __syncthreads();
+    const int P = ns * HW;
+    const int ntile = (P + 15) / 16;
+    for (int t0 = wid * MTW; t0 < ntile; t0 += 4 * MTW) {
+      int base[MTW];
+      bool valid[MTW];
+#pragma unroll
+      for (int mt = 0; mt < MTW; ++mt) {
+        const int p = (t0 + mt) * 16 + (lane & 15);
+        valid[mt] = (t0 + mt) < ntile && p < P;
+        const int pp = valid[mt] ? p : 0;
+        const int im = pp / HW, r = pp % HW;
+        base[mt] = ((im * (H + 2) + r / W) * Wp + r % W) * LD;
+      }
+      f32x4 acc[MTW][NT];
+#pragma unroll
+      for (int mt = 0; mt < MTW; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KSTEPS; ++ks) {
+        const int k = ks * 32 + 8 * g;
+        const int tap = k / KC, ci = k % KC;
+        const int kh = tap / 3, kw = tap % 3;
+        // forward reads x_pad(pr + kh, pc + kw); backward reads dy_pad(pr + 2 − kh, pc + 2 − kw)
+        const int toff = BWD ? ((2 - kh) * Wp + (2 - kw)) * LD + ci : (kh * Wp + kw) * LD + ci;
+        const bool kin = k < K;
+        bf16x8 af[MTW];
+#pragma unroll
+        for (int mt = 0; mt < MTW; ++mt) {
+          uint4 v = make_uint4(0, 0, 0, 0);
+          if (valid[mt] && kin) v = *reinterpret_cast<const uint4*>(tile + base[mt] + toff);
+          af[mt] = as_bf16x8(v);
+        }
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt) {
+          const uint4 bv = *reinterpret_cast<const uint4*>(wl + (nt * 16 + (lane & 15)) * a.ldk + ks * 32 + 8 * g);
+#pragma unroll
+          for (int mt = 0; mt < MTW; ++mt)
+            acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt], as_bf16x8(bv), acc[mt][nt], 0, 0, 0);
+        }
+      }
+      // ---- epilogue, one 16-pixel tile at a time ----
+#pragma unroll
+      for (int mt = 0; mt < MTW; ++mt) {
+        if (t0 + mt >= ntile) break;
+#pragma unroll
+        for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) my_stage[(4 * g + i) * NOUT + nt * 16 + (lane & 15)] = f32_to_bf16(acc[mt][nt][i]);
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+        const int rows_valid = min(16, P - (t0 + mt) * 16);
+#pragma unroll
+        for (int pass = 0; pass < (16 + ROWS_PER_PASS - 1) / ROWS_PER_PASS; ++pass) {
+          const int row = pass * ROWS_PER_PASS + lane / CG;
+          if (lane / CG < ROWS_PER_PASS && row < rows_valid) {
+            const int ch0 = my_cg * 8;
+            const uint4 dv = *reinterpret_cast<const uint4*>(my_stage + row * NOUT + ch0);
+            const int64_t goff = ((int64_t)s0 * HW + (t0 + mt) * 16 + row) * NOUT + ch0;
+            if (EPI == EPI_FWD) {
+              *reinterpret_cast<uint4*>(out + goff) = dv;
+              float f[8];
+              unpack8(dv, f);
+#pragma unroll
+              for (int j = 0; j < 8; ++j) { st0[j] += f[j]; st1[j] += f[j] * f[j]; }
+            } else {
+              const int64_t eoff = (int64_t)c * a.N * HW * NOUT + goff;
+              float gv[8], xv[8];
+              unpack8(dv, gv);
+              unpack8(*reinterpret_cast<const uint4*>(a.e_x + eoff), xv);
+#pragma unroll
+              for (int j = 0; j < 8; ++j) {
+                const int ch = ch0 + j;
+                const bool on = xv[j] * a.e_s[(int64_t)c * NOUT + ch] + a.e_t[(int64_t)c * NOUT + ch] > 0.f;
+                gv[j] = on ? gv[j] : 0.f;
+              }
+              const uint4 gp = pack8(gv);
+              *reinterpret_cast<uint4*>(out + goff) = gp;
+              float gr[8];
+              unpack8(gp, gr);
+#pragma unroll
+              for (int j = 0; j < 8; ++j) { st0[j] += gr[j]; st1[j] += gr[j] * xv[j]; }
+            }
+          }
+        }
+        __builtin_amdgcn_wave_barrier();
+      }
+    }
+  }
+
+  // ---- statistics: lanes sharing a channel group → waves → one atomic per (client, channel) ----
+#pragma unroll
+  for (int o = CG; o < 64; o <<= 1) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      st0[j] += __shfl_xor(st0[j], o, 64);
+      st1[j] += __shfl_xor(st1[j], o, 64);
+    }
+  }
+  if (lane < CG) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      red[(wid * NOUT + lane * 8 + j) * 3 + 0] = st0[j];
+      red[(wid * NOUT + lane * 8 + j) * 3 + 1] = st1[j];
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < NOUT * 2; i += 256) {
+    const int ch = i / 2, q = i % 2;
+    const float s = red[(0 * NOUT + ch) * 3 + q] + red[(1 * NOUT + ch) * 3 + q] + red[(2 * NOUT + ch) * 3 + q] +
+                    red[(3 * NOUT + ch) * 3 + q];
+    atomicAdd(&a.stats[((int64_t)c * NOUT + ch) * a.NS + q], s);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// weight gradient
+// ---------------------------------------------------------------------------------------------
+// 8 consecutive pixels × 16 columns, transposed read from a natural [pixel][ld] LDS tile: lane
+// (g, i = q·4 + p) addresses pixel row0 + 8g + q, columns col0 + 4p (and pixel + 4).
+__device__ __forceinline__ bf16x8 tr_read(const uint16_t* a0, int ld4) {
+  const v4i16 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a0));
+  const v4i16 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a0 + ld4));
+  union { short s[8]; bf16x8 b; } u;
+  u.s[0] = r0[0]; u.s[1] = r0[1]; u.s[2] = r0[2]; u.s[3] = r0[3];
+  u.s[4] = r1[0]; u.s[5] = r1[1]; u.s[6] = r1[2]; u.s[7] = r1[3];
+  return u.b;
+}
+
+struct WArgs {
+  const uint16_t* g;      // [C][N][H][W][COUT]
+  const uint16_t* yv;
+  const float* alpha;
+  const float* beta;
+  const float* gamma;
+  const uint16_t* x;      // [C][N][H][W][CIN]
+  const float* ps;
+  const float* pt;
+  float* dw;              // GEMM-layout scratch [C][COUT][9·CIN]
+  int N, H, W;
+  int imgs_per_wg, imgs_per_stage;
+  int nt_per_z;           // GEMM column tiles (16 wide) per blockIdx.z
+};
+
+// WN waves split the column tiles of this z-slice, WK = 4/WN waves split the pixel K-steps.
+template <int CIN, int COUT, int PRO, int WN, int TPW>
+__global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WArgs a) {
+  constexpr int WK = 4 / WN;
+  constexpr int MT = COUT / 16;
+  constexpr int LDX = CIN + 8, LDD = COUT + 8;
+  constexpr int K = 9 * CIN;
+  const int c = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int g = lane >> 4, q = (lane & 15) >> 2, pq = lane & 3;
+  const int kgrp = wid / WN, ngrp = wid % WN;
+  const int H = a.H, W = a.W, HW = H * W, Wp = W + 2;
+  const int nt_lo = blockIdx.z * a.nt_per_z;
+  const int nt_hi = min(K / 16, nt_lo + a.nt_per_z);
+  const int my_nt0 = nt_lo + ngrp * TPW;  // this wave's column tiles [my_nt0, my_nt0 + TPW) ∩ [.., nt_hi)
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* vv = reinterpret_cast<float*>(smem);                          // α β γ [COUT], s t [CIN]
+  uint16_t* dyL = reinterpret_cast<uint16_t*>(vv + 3 * COUT + 2 * CIN);  // [S·HW][LDD]
+  uint16_t* xt = dyL + (size_t)a.imgs_per_stage * HW * LDD;              // [S][H+2][W+2][LDX]
+
+  for (int i = threadIdx.x; i < COUT; i += 256) {
+    vv[i] = a.alpha[(int64_t)c * COUT + i];
+    vv[COUT + i] = a.beta[(int64_t)c * COUT + i];
+    vv[2 * COUT + i] = a.gamma[(int64_t)c * COUT + i];
+  }
+  if (PRO)
+    for (int i = threadIdx.x; i < CIN; i += 256) {
+      vv[3 * COUT + i] = a.ps[(int64_t)c * CIN + i];
+      vv[3 * COUT + CIN + i] = a.pt[(int64_t)c * CIN + i];
+    }
+
+  f32x4 acc[MT][TPW];
+#pragma unroll
+  for (int m = 0; m < MT; ++m)
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) acc[m][t] = {0.f, 0.f, 0.f, 0.f};
+
+  const uint16_t* gc = a.g + (int64_t)c * a.N * HW * COUT;
+  const uint16_t* yc = a.yv + (int64_t)c * a.N * HW * COUT;
+  const uint16_t* xc = a.x + (int64_t)c * a.N * HW * CIN;
+  const int img_lo = blockIdx.x * a.imgs_per_wg;
+  const int img_hi = min(a.N, img_lo + a.imgs_per_wg);
+
+  for (int s0 = img_lo; s0 < img_hi; s0 += a.imgs_per_stage) {
+    const int ns = min(a.imgs_per_stage, img_hi - s0);
+    __syncthreads();
+    // dy = α·g + β·y + γ, natural [pixel][co] (no halo)
+    {
+      constexpr int CGD = COUT / 8;
+      const int total = ns * HW * CGD;
+      for (int i = threadIdx.x; i < total; i += 256) {
+        const int cg = i % CGD, p = i / CGD;
+        const int64_t off = ((int64_t)s0 * HW + p) * COUT + cg * 8;
+        float gf[8], yf[8];
+        unpack8(*reinterpret_cast<const uint4*>(gc + off), gf);
+        unpack8(*reinterpret_cast<const uint4*>(yc + off), yf);
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+          gf[j] = vv[cg * 8 + j] * gf[j] + vv[COUT + cg * 8 + j] * yf[j] + vv[2 * COUT + cg * 8 + j];
+        *reinterpret_cast<uint4*>(dyL + (size_t)p * LDD + cg * 8) = pack8(gf);
+      }
+    }
+    stage_tile<CIN, PRO ? XF_BNRELU : XF_NONE>(xt, xc, nullptr, vv + 3 * COUT, vv + 3 * COUT + CIN, nullptr, s0,
+                                              ns, H, W);
+    __syncthreads();
+    const int KS = ns * HW / 32;  // HW is a multiple of 64
+    for (int ks = kgrp; ks < KS; ks += WK) {
+      const int p0 = ks * 32;
+      // this lane's pixel row of the fragment (8-pixel groups never straddle an image row: W % 8 == 0)
+      const int pix = p0 + 8 * g + q;
+      const int im = pix / HW, r = pix % HW;
+      const uint16_t* xrow = xt + (size_t)((im * (H + 2) + r / W) * Wp + r % W) * LDX + 4 * pq;
+      const uint16_t* drow = dyL + (size_t)pix * LDD + 4 * pq;
+      bf16x8 af[MT];
+#pragma unroll
+      for (int m = 0; m < MT; ++m) af[m] = tr_read(drow + m * 16, 4 * LDD);
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) {
+        const int nt = my_nt0 + t;
+        if (nt < nt_hi) {
+          const int k0 = nt * 16;
+          const int tap = k0 / CIN, ci0 = k0 % CIN;
+          const int kh = tap / 3, kw = tap % 3;
+          const bf16x8 bf = tr_read(xrow + (kh * Wp + kw) * LDX + ci0, 4 * LDX);
+#pragma unroll
+          for (int m = 0; m < MT; ++m)
+            acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bf, acc[m][t], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  // ---- reduce the WK pixel groups through LDS, then contiguous fp32 atomics (GEMM layout) ----
+  float* dwc = a.dw + (int64_t)c * COUT * K;
+  if (WK > 1) {
+    __syncthreads();
+    float* rbuf = reinterpret_cast<float*>(dyL);  // [WK-1][WN][MT][TPW][4][64]
+    if (kgrp > 0) {
+#pragma unroll
+      for (int m = 0; m < MT; ++m)
+#pragma unroll
+        for (int t = 0; t < TPW; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            rbuf[((((kgrp - 1) * WN + ngrp) * MT + m) * TPW + t) * 256 + i * 64 + lane] = acc[m][t][i];
+    }
+    __syncthreads();
+    if (kgrp == 0) {
+      for (int kg2 = 1; kg2 < WK; ++kg2)
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int t = 0; t < TPW; ++t)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+              acc[m][t][i] += rbuf[((((kg2 - 1) * WN + ngrp) * MT + m) * TPW + t) * 256 + i * 64 + lane];
+    }
+  }
+  if (kgrp == 0) {
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      const int nt = my_nt0 + t;
+      if (nt < nt_hi) {
+        const int k = nt * 16 + (lane & 15);
+#pragma unroll
+        for (int m = 0; m < MT; ++m)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) atomicAdd(&dwc[(int64_t)(m * 16 + 4 * g + i) * K + k], acc[m][t][i]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// host side
+// ---------------------------------------------------------------------------------------------
+static size_t gemm_smem(int kc, int nout, int ldk, int S, int H, int W) {
+  return (size_t)nout * ldk * 2 + (size_t)3 * kc * 4 + (size_t)4 * nout * 3 * 4 + (size_t)4 * 16 * nout * 2 +
+         (size_t)S * (H + 2) * (W + 2) * (kc + 8) * 2;
+}
+
+template <int KC, int NOUT, int XF, int BWD, int EPI>
+static int launch_gemm(const Args& a, int C, hipStream_t stream) {
+  constexpr int MTW = NOUT >= 64 ? 2 : 4;
+  const size_t smem = gemm_smem(KC, NOUT, a.ldk, a.imgs_per_stage, a.H, a.W);
+  if (smem > 160 * 1024) return -5;
+  auto kern = conv3x3_gemm_kernel<KC, NOUT, XF, BWD, EPI, MTW>;
+  hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  const int gx = (a.N + a.imgs_per_wg - 1) / a.imgs_per_wg;
+  hipLaunchKernelGGL(kern, dim3(gx, C), dim3(256), smem, stream, a);
+  return (int)hipGetLastError();
+}
+
+template <int XF, int BWD, int EPI>
+static int dispatch_gemm(int kc, int nout, const Args& a, int C, hipStream_t s) {
+  if (kc != nout) return -2;
+  switch (kc) {
+    case 16: return launch_gemm<16, 16, XF, BWD, EPI>(a, C, s);
+    case 32: return launch_gemm<32, 32, XF, BWD, EPI>(a, C, s);
+    case 64: return launch_gemm<64, 64, XF, BWD, EPI>(a, C, s);
+    default: return -2;
+  }
+}
+
+// images per workgroup / per LDS stage: ≥ ~1K pixels per stage, ≈4 workgroups per CU overall
+static void plan(int N, int H, int W, int C, int max_stage_px, int* per_wg, int* per_stage) {
+  const int hw = H * W;
+  int stage = max(1, min(N, max_stage_px / hw));
+  int wgs_per_client = max(1, (2048 + C - 1) / C);
+  int pw = max(1, (N + wgs_per_client - 1) / wgs_per_client);
+  pw = max(pw, 1);
+  stage = min(stage, pw);
+  *per_wg = pw;
+  *per_stage = stage;
+}
+
+}  // namespace c3
+
+// forward 3×3/s1/p1: y = conv(pro(x)); stats[c][co][2] += (Σy, Σy²). Returns <0 if unsupported.
+FA_EXPORT int fa_conv3x3_fwd(const uint16_t* x, const uint16_t* wpk, int64_t wpk_ld, const float* pscale,
+                             const float* pshift, uint16_t* y, float* stats, int C, int N, int H, int W, int Cin,
+                             int Cout, int ldk, hipStream_t stream) {
+  if (W % 8 != 0) return -3;
+  c3::Args a = {};
+  a.src = x; a.wpk = wpk; a.wpk_ld = wpk_ld; a.vec0 = pscale; a.vec1 = pshift; a.out = y; a.stats = stats; a.NS = 2;
+  a.N = N; a.H = H; a.W = W; a.ldk = ldk;
+  c3::plan(N, H, W, C, Cin >= 64 ? 128 : (Cin >= 32 ? 512 : 1024), &a.imgs_per_wg, &a.imgs_per_stage);
+  if (pscale) return c3::dispatch_gemm<c3::XF_BNRELU, 0, c3::EPI_FWD>(Cin, Cout, a, C, stream);
+  return c3::dispatch_gemm<c3::XF_NONE, 0, c3::EPI_FWD>(Cin, Cout, a, C, stream);
+}
+
+// backward-data 3×3/s1/p1 with the ReLU-mask epilogue (EPI_MASK of the generic kernel):
+//   g' = convᵀ(α·g + β·y + γ) · [e_x·e_s + e_t > 0];  stats[c][ci][3] += (Σg', Σg'·e_x, ·)
+FA_EXPORT int fa_conv3x3_bwd_data(const uint16_t* g, const uint16_t* yv, const float* alpha, const float* beta,
+                                  const float* gamma, const uint16_t* wpk_b, int64_t wpk_ld, uint16_t* dx,
+                                  const uint16_t* e_x, const float* e_s, const float* e_t, float* stats, int C, int N,
+                                  int H, int W, int Cout, int Cin, int ldk2, hipStream_t stream) {
+  if (W % 8 != 0) return -3;
+  c3::Args a = {};
+  a.src = g; a.src2 = yv; a.wpk = wpk_b; a.wpk_ld = wpk_ld; a.vec0 = alpha; a.vec1 = beta; a.vec2 = gamma;
+  a.out = dx; a.e_x = e_x; a.e_s = e_s; a.e_t = e_t; a.stats = stats; a.NS = 3;
+  a.N = N; a.H = H; a.W = W; a.ldk = ldk2;
+  c3::plan(N, H, W, C, Cout >= 64 ? 128 : (Cout >= 32 ? 512 : 1024), &a.imgs_per_wg, &a.imgs_per_stage);
+  return c3::dispatch_gemm<c3::XF_DY, 1, c3::EPI_MASK>(Cout, Cin, a, C, stream);
+}
+
+// weight gradient 3×3/s1/p1 into the GEMM-layout scratch `dw` [C][Cout][9·Cin] (zero on entry);
+// the caller runs the scatter pass (fa_wgrad_scatter) into the OIHW arena.
+FA_EXPORT int fa_conv3x3_wgrad(const uint16_t* g, const uint16_t* yv, const float* alpha, const float* beta,
+                               const float* gamma, const uint16_t* x, const float* ps, const float* pt, float* dw,
+                               int C, int N, int H, int W, int Cin, int Cout, hipStream_t stream) {
+  if (W % 8 != 0 || (H * W) % 64 != 0 || Cin != Cout) return -3;
+  c3::WArgs a = {};
+  a.g = g; a.yv = yv; a.alpha = alpha; a.beta = beta; a.gamma = gamma; a.x = x; a.ps = ps; a.pt = pt; a.dw = dw;
+  a.N = N; a.H = H; a.W = W;
+  int stage_px = Cin >= 64 ? 256 : (Cin >= 32 ? 512 : 1024);
+  c3::plan(N, H, W, C, stage_px, &a.imgs_per_wg, &a.imgs_per_stage);
+  const int NTK = 9 * Cin / 16;
+  const size_t smem_base = (size_t)(3 * Cout + 2 * Cin) * 4 +
+                           (size_t)a.imgs_per_stage * H * W * (Cout + 8) * 2 +
+                           (size_t)a.imgs_per_stage * (H + 2) * (W + 2) * (Cin + 8) * 2;
+#define W3_LAUNCH(CI, CO, WN, TPW, NZ)                                                                         \
+  {                                                                                                            \
+    a.nt_per_z = (NTK + (NZ) - 1) / (NZ);                                                                      \
+    auto kern = ps ? c3::conv3x3_wgrad_kernel<CI, CO, 1, WN, TPW> : c3::conv3x3_wgrad_kernel<CI, CO, 0, WN, TPW>; \
+    const size_t red = (size_t)(4 / (WN) - 1) * (WN) * ((CO) / 16) * (TPW) * 256 * 4;                          \
+    const size_t smem = smem_base > red + (size_t)(3 * Cout + 2 * Cin) * 4 ? smem_base                         \
+                                                                          : red + (3 * Cout + 2 * Cin) * 4;    \
+    if (smem > 160 * 1024) return -5;                                                                          \
+    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);             \
+    const int gx = (N + a.imgs_per_wg - 1) / a.imgs_per_wg;                                                    \
+    hipLaunchKernelGGL(kern, dim3(gx, C, NZ), dim3(256), smem, stream, a);                                     \
+    return (int)hipGetLastError();                                                                             \
+  }
+  switch (Cin) {
+    case 16: W3_LAUNCH(16, 16, 1, 9, 1)    // 9 column tiles, 4 waves split the pixels
+    case 32: W3_LAUNCH(32, 32, 2, 9, 1)    // 18 tiles: 2 column groups × 2 pixel groups
+    case 64: W3_LAUNCH(64, 64, 4, 5, 2)    // 36 tiles: 2 z-slices × 4 column groups
+    default: return -2;
+  }
+#undef W3_LAUNCH
+}

@@ -287,3 +287,11 @@ FA_EXPORT int fa_conv_wgrad(const uint16_t* g, const uint16_t* yv, const float* 
                      garena, ldw, woff, Cout, Cin, KH * KW, cin_src);
   return (int)hipGetLastError();
 }
+
+// scatter a GEMM-layout dW scratch [C][Cout][taps·Cin] into the OIHW arena (+=) and clear it
+FA_EXPORT int fa_wgrad_scatter(float* dw, float* garena, int64_t ldw, int64_t woff, int C, int Cout, int Cin,
+                               int taps, int cin_src, hipStream_t stream) {
+  hipLaunchKernelGGL(wgrad_scatter_kernel, dim3(fa_grid((int64_t)Cout * taps * Cin, 256, 64), C), dim3(256), 0,
+                     stream, dw, garena, ldw, woff, Cout, Cin, taps, cin_src);
+  return (int)hipGetLastError();
+}

@@ -136,6 +136,8 @@ class NativeResNetStep:
         self.off = {s.key: s.offset for s in layout.slots}
         self.geom = None
         self._segs = None
+        import os
+        self.use_c3 = os.environ.get("FEDML_AMD_CONV3X3", "1") != "0"
 
     # ------------------------------------------------------------------ setup
     def _all_convs(self):
@@ -264,8 +266,17 @@ class NativeResNetStep:
         # the stats buffer of the BN that follows this conv is resolved by the caller
         return vec
 
+    def _c3(self, cv: ConvSpec):
+        return self.use_c3 and nn_ops.conv3x3_supported(cv.cin_pad, cv.cout, cv.k, cv.stride, cv.pad, cv.H, cv.W)
+
     def _fwd(self, cv: ConvSpec, x, y, pro_vec, stats, N):
         M = N * cv.Ho * cv.Wo
+        if self._c3(cv):
+            nn_ops.conv3x3_fwd(x, self.packed.view(-1)[cv.off_f:], self.packed_ld,
+                               pro_vec[0] if pro_vec is not None else None,
+                               pro_vec[1] if pro_vec is not None else None, y, stats, self.C, N, cv.H, cv.W,
+                               cv.cin_pad, cv.cout, cv.ldk)
+            return
         nn_ops.conv_fwd(x, self.packed.view(-1)[cv.off_f:], self.packed_ld, pro_vec[0] if pro_vec is not None else None,
                         pro_vec[1] if pro_vec is not None else None, y, stats, self.C, N, cv.H, cv.W, cv.cin_pad,
                         cv.cout, cv.k, cv.k, cv.stride, cv.pad, cv.Ho, cv.Wo, cv.ldk, self._tiles_per_wave(M))
@@ -369,10 +380,21 @@ class NativeResNetStep:
                 v = self.bn_vec[bn.key]
                 pv = self.bn_vec[b.bns[j - 1].key]
                 M = N * cv.Ho * cv.Wo
+                out_g = free[0] if g_j is not free[0] else free[1]
+                if self._c3(cv):
+                    nn_ops.conv3x3_wgrad(g_j, b.ys[j], v[4], v[5], v[6], b.ys[j - 1], pv[0], pv[1], garena,
+                                         self.off[cv.key], C, N, cv.H, cv.W, cv.cin_pad, cv.cout, cv.cin,
+                                         self.dw_scratch)
+                    nn_ops.conv3x3_bwd_data(g_j, b.ys[j], v[4], v[5], v[6], self.packed.view(-1)[cv.off_b:],
+                                            self.packed_ld, out_g, b.ys[j - 1], pv[0], pv[1],
+                                            self.stat_views[b.bns[j - 1].key][1], C, N, cv.H, cv.W, cv.cout,
+                                            cv.cin_pad, cv.ldk2)
+                    self._bn_bwd(b.bns[j - 1], 1, N, cv.H * cv.W, arena, garena)
+                    g_j = out_g
+                    continue
                 nn_ops.conv_wgrad(g_j, b.ys[j], v[4], v[5], v[6], b.ys[j - 1], pv[0], pv[1], garena,
                                   self.off[cv.key], C, N, cv.H, cv.W, cv.cin_pad, cv.Ho, cv.Wo, cv.cout, cv.k, cv.k,
                                   cv.stride, cv.pad, self._pix_per_wg(M), cv.cin, self.dw_scratch)
-                out_g = free[0] if g_j is not free[0] else free[1]
                 nn_ops.conv_bwd_data(g_j, b.ys[j], v[4], v[5], v[6], self.packed.view(-1)[cv.off_b:],
                                      self.packed_ld, out_g, nn_ops.EPI_MASK, b.ys[j - 1], pv[0], pv[1], None, None,
                                      None, self.stat_views[b.bns[j - 1].key][1], C, N, cv.Ho, cv.Wo, cv.cout,
