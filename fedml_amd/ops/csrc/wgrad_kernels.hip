@@ -260,6 +260,9 @@ FA_EXPORT int fa_conv_wgrad(const uint16_t* g, const uint16_t* yv, const float* 
   const int kw_ = nt_per_z * 16;
   const int dyi = (64 * (Cout / 8) + 255) / 256;
   const int ai = (64 * (kw_ / 8) + 255) / 256;
+  // the staging loops cover DYI·256 / AI·256 16-B chunks: a sub-tile larger than the largest
+  // instantiation would leave LDS rows unwritten
+  if (dyi > 8 || ai > 16) return -6;
   const size_t smem = (size_t)64 * ((Cout + 8) + (kw_ + 8)) * 2 + (size_t)(3 * Cout + 2 * Cin) * 4;
   dim3 grid(gx, C, nz);
 #define WG_LAUNCH(T, D, A)                                                                                       \
@@ -273,7 +276,8 @@ FA_EXPORT int fa_conv_wgrad(const uint16_t* g, const uint16_t* yv, const float* 
 #define WG_AI(T, D)                          \
   if (ai <= 2) WG_LAUNCH(T, D, 2)            \
   else if (ai <= 4) WG_LAUNCH(T, D, 4)       \
-  else WG_LAUNCH(T, D, 8)
+  else if (ai <= 8) WG_LAUNCH(T, D, 8)       \
+  else WG_LAUNCH(T, D, 16)
 #define WG_D(T)                              \
   if (dyi <= 2) { WG_AI(T, 2) }              \
   else { WG_AI(T, 8) }

@@ -58,6 +58,19 @@ def c_wgrad(g, y, al, be, ga, x, ps, pt, garena, woff, C, N, H, W, Cin, Ho, Wo, 
             C * N * (2 * Ho * Wo * Cout + H * W * Cin) * 2, 2 * C * N * Ho * Wo * Cout * KH * KW * Cin)
 
 
+def c3_fwd(x, wpk, ld, ps, pt, y, st, C, N, H, W, Cin, Cout, ldk):
+    return c_fwd(x, wpk, ld, ps, pt, y, st, C, N, H, W, Cin, Cout, 3, 3, 1, 1, H, W, ldk, 0)
+
+
+def c3_bwd(g, y, al, be, ga, wpk, ld, dx, ex, es, et, st, C, N, H, W, Cout, Cin, ldk2):
+    return c_bwd(g, y, al, be, ga, wpk, ld, dx, 2, ex, es, et, None, None, None, st, C, N, H, W, Cout, Cin, 3, 3, 1, 1,
+                 H, W, ldk2, 0)
+
+
+def c3_wgrad(g, y, al, be, ga, x, ps, pt, garena, woff, C, N, H, W, Cin, Cout, cs, scratch):
+    return c_wgrad(g, y, al, be, ga, x, ps, pt, garena, woff, C, N, H, W, Cin, H, W, Cout, 3, 3, 1, 1, 0, cs, scratch)
+
+
 def c_block(y, s, t, r, rs, rt, out, C, per, Ch):
     return (f"ch{Ch} n{per // Ch}" + (" ds" if rs is not None else ""), C * per * 2 * (3 if r is not None else 2), 0)
 
@@ -77,6 +90,9 @@ def main():
     _wrap("conv_bwd_data", c_bwd)
     _wrap("conv_wgrad", c_wgrad)
     _wrap("block_out", c_block)
+    _wrap("conv3x3_fwd", c3_fwd)
+    _wrap("conv3x3_bwd_data", c3_bwd)
+    _wrap("conv3x3_wgrad", c3_wgrad)
     for n in ("bn_fwd_finalize", "bn_bwd_finalize", "pack_weights", "avgpool", "head_bwd", "nchw_to_nhwc_pad"):
         _wrap(n, c_other)
     torch.manual_seed(0)

@@ -103,31 +103,69 @@ def test_native_resnet56_engine_round():
     assert losses[-1] < losses[0]   # memorising the same data → loss decreases
 
 
-@pytest.mark.parametrize("hw", [32, 16])
-def test_conv3x3_tiled_path_matches_generic_kernels(hw):
-    """The LDS-tiled 3×3 kernels (fwd, bwd-data, wgrad) reproduce the generic implicit-GEMM kernels:
-    same bf16 operands, fp32 accumulation — only the summation order differs."""
+@pytest.mark.parametrize("ch,hw", [(16, 32), (32, 16), (64, 8), (16, 16)])
+def test_conv3x3_kernels_vs_fp32_reference(ch, hw):
+    """LDS-tiled 3×3 kernels against torch fp32 convolutions of the same bf16 operands, and against
+    the generic implicit-GEMM kernels (forward / backward-data are bit-identical to the latter)."""
+    from fedml_amd.ops import nn_ops
     torch.manual_seed(0)
-    model = ResNet(Bottleneck, [2, 2, 2], 100)
-    layout = ParamLayout.from_module(model)
-    C, N = 3, 8
-    flat = layout.flatten(model.state_dict()).to(DEV)
-    x = torch.randn(C, N, 3, hw, hw, device=DEV)
-    y = torch.randint(0, 100, (C, N), device=DEV)
-    row_scale = torch.full((C, N), 1.0 / N, device=DEV)
-    active = torch.ones(C, device=DEV)
-    out = []
-    for use_c3 in (False, True):
-        arena = flat.view(1, -1).repeat(C, 1).contiguous()
-        garena = torch.zeros_like(arena)
-        step = NativeResNetStep(model, layout, C, DEV)
-        step.use_c3 = use_c3
-        loss = float(step.step(arena, garena, x, y, row_scale, active))
-        torch.cuda.synchronize()
-        out.append((loss, garena.clone(), arena.clone()))
-    (l0, g0, a0), (l1, g1, a1) = out
-    assert abs(l0 - l1) / abs(l0) < 1e-3
-    rel = float((g0 - g1).norm() / g0.norm())
-    assert rel < 2e-2, rel
-    # running statistics (BN buffers updated from the forward statistics) agree too
-    assert float((a0 - a1).norm() / a0.norm()) < 1e-3
+    C, N, bf = 3, 8, torch.bfloat16
+    K = 9 * ch
+    ldk = (K + 31) // 32 * 32 + 8
+    x = torch.randn(C, N, hw, hw, ch, device=DEV).to(bf)
+    wpk = torch.zeros(C, ch, ldk, device=DEV)
+    wpk[:, :, :K] = torch.randn(C, ch, K, device=DEV) * 0.1
+    wpk = wpk.to(bf).contiguous()
+    s = torch.rand(C, ch, device=DEV) + 0.5
+    t = torch.randn(C, ch, device=DEV) * 0.1
+    wt = wpk[:, :, :K].float().view(C, ch, 3, 3, ch).permute(0, 1, 4, 2, 3)  # [C][co][ci][kh][kw]
+
+    def rel(a, b):
+        return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
+
+    # forward: y = conv(relu(x·s + t)), BN statistics (Σy, Σy²)
+    y3 = torch.zeros(C, N, hw, hw, ch, device=DEV, dtype=bf)
+    st3 = torch.zeros(C, ch, 2, device=DEV)
+    nn_ops.conv3x3_fwd(x, wpk, ch * ldk, s, t, y3, st3, C, N, hw, hw, ch, ch, ldk)
+    yg = torch.zeros_like(y3)
+    stg = torch.zeros_like(st3)
+    nn_ops.conv_fwd(x, wpk, ch * ldk, s, t, yg, stg, C, N, hw, hw, ch, ch, 3, 3, 1, 1, hw, hw, ldk, 1)
+    torch.cuda.synchronize()
+    assert torch.equal(y3, yg)
+    for c in range(C):
+        xa = torch.relu(x[c].float() * s[c] + t[c]).to(bf).float().permute(0, 3, 1, 2)
+        ref = torch.nn.functional.conv2d(xa, wt[c], padding=1).permute(0, 2, 3, 1)
+        assert rel(y3[c], ref) < 1e-2
+        assert rel(st3[c, :, 0], y3[c].float().sum((0, 1, 2))) < 1e-4
+    # backward-data with the ReLU-mask epilogue
+    g = torch.randn(C, N, hw, hw, ch, device=DEV).to(bf)
+    yv = torch.randn(C, N, hw, hw, ch, device=DEV).to(bf)
+    al, be = torch.rand(C, ch, device=DEV), torch.randn(C, ch, device=DEV) * 0.1
+    ga = torch.randn(C, ch, device=DEV) * 0.01
+    ex = torch.randn(C, N, hw, hw, ch, device=DEV).to(bf)
+    dx = torch.zeros_like(g)
+    st = torch.zeros(C, ch, 3, device=DEV)
+    nn_ops.conv3x3_bwd_data(g, yv, al, be, ga, wpk, ch * ldk, dx, ex, s, t, st, C, N, hw, hw, ch, ch, ldk)
+    dxg = torch.zeros_like(g)
+    stg = torch.zeros_like(st)
+    nn_ops.conv_bwd_data(g, yv, al, be, ga, wpk, ch * ldk, dxg, nn_ops.EPI_MASK, ex, s, t, None, None, None, stg,
+                         C, N, hw, hw, ch, ch, 3, 3, 1, 1, hw, hw, ldk, 1)
+    torch.cuda.synchronize()
+    assert torch.equal(dx, dxg)
+    for c in range(C):
+        dy = (al[c] * g[c].float() + be[c] * yv[c].float() + ga[c]).to(bf).float().permute(0, 3, 1, 2)
+        ref = torch.nn.grad.conv2d_input(dy.shape, wt[c], dy, padding=1).permute(0, 2, 3, 1)
+        mask = (ex[c].float() * s[c] + t[c]) > 0
+        assert rel(dx[c], ref * mask) < 1e-2
+    # weight gradient
+    P = ch * ch * 9 + 64
+    garena = torch.zeros(C, P, device=DEV)
+    scratch = torch.zeros(C * ch * K, device=DEV)
+    nn_ops.conv3x3_wgrad(g, yv, al, be, ga, x, s, t, garena, 16, C, N, hw, hw, ch, ch, ch, scratch)
+    torch.cuda.synchronize()
+    assert float(scratch.abs().max()) == 0.0  # scatter pass leaves the scratch zeroed
+    for c in range(C):
+        dy = (al[c] * g[c].float() + be[c] * yv[c].float() + ga[c]).to(bf).float().permute(0, 3, 1, 2)
+        xa = torch.relu(x[c].float() * s[c] + t[c]).to(bf).float().permute(0, 3, 1, 2)
+        ref = torch.nn.grad.conv2d_weight(xa, (ch, ch, 3, 3), dy, padding=1)
+        assert rel(garena[c, 16:16 + ch * ch * 9], ref.reshape(-1)) < 1e-4
