@@ -119,6 +119,8 @@ def test_conv3x3_kernels_vs_fp32_reference(ch, hw):
     s = torch.rand(C, ch, device=DEV) + 0.5
     t = torch.randn(C, ch, device=DEV) * 0.1
     wt = wpk[:, :, :K].float().view(C, ch, 3, 3, ch).permute(0, 1, 4, 2, 3)  # [C][co][ci][kh][kw]
+    # the same buffer read as the backward packing Wb[ci][tap·Cout + co] → W[co][ci][kh][kw]
+    wt_b = wpk[:, :, :K].float().view(C, ch, 3, 3, ch).permute(0, 4, 1, 2, 3)
 
     def rel(a, b):
         return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
@@ -154,7 +156,7 @@ def test_conv3x3_kernels_vs_fp32_reference(ch, hw):
     assert torch.equal(dx, dxg)
     for c in range(C):
         dy = (al[c] * g[c].float() + be[c] * yv[c].float() + ga[c]).to(bf).float().permute(0, 3, 1, 2)
-        ref = torch.nn.grad.conv2d_input(dy.shape, wt[c], dy, padding=1).permute(0, 2, 3, 1)
+        ref = torch.nn.grad.conv2d_input(dy.shape, wt_b[c], dy, padding=1).permute(0, 2, 3, 1)
         mask = (ex[c].float() * s[c] + t[c]) > 0
         assert rel(dx[c], ref * mask) < 1e-2
     # weight gradient
