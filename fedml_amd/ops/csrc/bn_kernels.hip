@@ -99,45 +99,60 @@ FA_EXPORT int fa_bn_bwd_finalize(const float* bstats, int NS, int q_gy, int C, i
 }
 
 // ---- fused block output: out = relu(y·s + t + R), R = yd·sd + td (downsample) | x (identity) | 0
+// One 16-B vector per thread (no grid-stride loop, no 64-bit modulo); the per-channel vectors are
+// read as float4 (L1-resident). Streams 3 bf16 tensors: HBM-bound by construction.
+template <int RES>  // 0: no residual, 1: identity, 2: downsample-BN residual
 __global__ __launch_bounds__(256) void block_out_kernel(const uint16_t* __restrict__ y, const float* __restrict__ s,
                                                         const float* __restrict__ t, const uint16_t* __restrict__ r,
                                                         const float* __restrict__ rs, const float* __restrict__ rt,
-                                                        uint16_t* __restrict__ out, int64_t per_client, int Ch) {
+                                                        uint16_t* __restrict__ out, int nvec, int cg) {
   const int c = blockIdx.y;
-  const int64_t nvec = per_client / 8;
-  const uint16_t* yc = y + (int64_t)c * per_client;
-  const uint16_t* rc = r ? r + (int64_t)c * per_client : nullptr;
-  uint16_t* oc = out + (int64_t)c * per_client;
-  const float* sc = s + (int64_t)c * Ch;
-  const float* tc = t + (int64_t)c * Ch;
-  for (int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; v < nvec; v += (int64_t)gridDim.x * blockDim.x) {
-    const int ch0 = (int)((v * 8) % Ch);
-    float f[8];
-    unpack8f(*reinterpret_cast<const uint4*>(yc + v * 8), f);
+  const int v = blockIdx.x * 256 + threadIdx.x;
+  if (v >= nvec) return;
+  const int64_t base = (int64_t)c * nvec * 8 + (int64_t)v * 8;
+  const int ch0 = (v % cg) * 8;
+  const int64_t co = (int64_t)c * cg * 8 + ch0;
+  const uint4 yv = *reinterpret_cast<const uint4*>(y + base);
+  uint4 rv = make_uint4(0, 0, 0, 0);
+  if (RES) rv = *reinterpret_cast<const uint4*>(r + base);
+  const float4 s0 = *reinterpret_cast<const float4*>(s + co), s1 = *reinterpret_cast<const float4*>(s + co + 4);
+  const float4 t0 = *reinterpret_cast<const float4*>(t + co), t1 = *reinterpret_cast<const float4*>(t + co + 4);
+  const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+  const float tv[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+  float f[8], g[8];
+  unpack8f(yv, f);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = f[j] * sc[ch0 + j] + tc[ch0 + j];
-    if (rc) {
-      float g[8];
-      unpack8f(*reinterpret_cast<const uint4*>(rc + v * 8), g);
-      if (rs) {
+  for (int j = 0; j < 8; ++j) f[j] = f[j] * sv[j] + tv[j];
+  if (RES) {
+    unpack8f(rv, g);
+    if (RES == 2) {
+      const float4 a0 = *reinterpret_cast<const float4*>(rs + co), a1 = *reinterpret_cast<const float4*>(rs + co + 4);
+      const float4 b0 = *reinterpret_cast<const float4*>(rt + co), b1 = *reinterpret_cast<const float4*>(rt + co + 4);
+      const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+      const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] += g[j] * rs[(int64_t)c * Ch + ch0 + j] + rt[(int64_t)c * Ch + ch0 + j];
-      } else {
+      for (int j = 0; j < 8; ++j) f[j] += g[j] * av[j] + bv[j];
+    } else {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) f[j] += g[j];
-      }
+      for (int j = 0; j < 8; ++j) f[j] += g[j];
     }
-#pragma unroll
-    for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
-    *reinterpret_cast<uint4*>(oc + v * 8) = pack8f(f);
   }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
+  *reinterpret_cast<uint4*>(out + base) = pack8f(f);
 }
 
 FA_EXPORT int fa_block_out(const uint16_t* y, const float* s, const float* t, const uint16_t* r, const float* rs,
                            const float* rt, uint16_t* out, int C, int64_t per_client, int Ch, hipStream_t stream) {
-  if (Ch % 8 != 0) return -3;
-  hipLaunchKernelGGL(block_out_kernel, dim3(fa_grid(per_client / 8, 256, 256), C), dim3(256), 0, stream, y, s, t, r,
-                     rs, rt, out, per_client, Ch);
+  if (Ch % 8 != 0 || per_client / 8 > INT32_MAX) return -3;
+  const int nvec = (int)(per_client / 8);
+  dim3 grid((nvec + 255) / 256, C);
+  if (!r)
+    hipLaunchKernelGGL(block_out_kernel<0>, grid, dim3(256), 0, stream, y, s, t, r, rs, rt, out, nvec, Ch / 8);
+  else if (!rs)
+    hipLaunchKernelGGL(block_out_kernel<1>, grid, dim3(256), 0, stream, y, s, t, r, rs, rt, out, nvec, Ch / 8);
+  else
+    hipLaunchKernelGGL(block_out_kernel<2>, grid, dim3(256), 0, stream, y, s, t, r, rs, rt, out, nvec, Ch / 8);
   return (int)hipGetLastError();
 }
 

@@ -48,25 +48,26 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
 enum { XF_NONE = 0, XF_BNRELU = 1, XF_DY = 2 };
 enum { EPI_FWD = 0, EPI_MASK = 2 };
 
-// Stage images [s0, s0+ns) of one client into a zero-haloed LDS tile [ns][H+2][W+2][ld],
-// applying the operand transform. `src`/`src2` already point at the client.
+// Stage one work unit of a client into a zero-haloed LDS tile [ns][R+2][W+2][KC+8]: images
+// [img0, img0+ns), output rows [r0, r0+R) plus one halo row/column on each side, with the operand
+// transform applied. `src`/`src2` already point at the client.
 template <int KC, int XF>
 __device__ __forceinline__ void stage_tile(uint16_t* tile, const uint16_t* __restrict__ src,
                                            const uint16_t* __restrict__ src2, const float* v0, const float* v1,
-                                           const float* v2, int s0, int ns, int H, int W) {
+                                           const float* v2, int img0, int ns, int r0, int R, int H, int W) {
   constexpr int LD = KC + 8;
   constexpr int CG = KC / 8;
-  const int Hp = H + 2, Wp = W + 2;
-  const int total = ns * Hp * Wp * CG;
+  const int Rp = R + 2, Wp = W + 2;
+  const int total = ns * Rp * Wp * CG;
   for (int i = threadIdx.x; i < total; i += 256) {
     const int cg = i % CG;
     const int pix = i / CG;
-    const int im = pix / (Hp * Wp);
-    const int r = pix % (Hp * Wp);
-    const int pr = r / Wp, pc = r % Wp;
+    const int im = pix / (Rp * Wp);
+    const int r = pix % (Rp * Wp);
+    const int ih = r0 - 1 + r / Wp, iw = r % Wp - 1;
     uint4 v = make_uint4(0, 0, 0, 0);
-    if (pr >= 1 && pr <= H && pc >= 1 && pc <= W) {
-      const int64_t off = ((((int64_t)(s0 + im) * H) + (pr - 1)) * W + (pc - 1)) * KC + cg * 8;
+    if (ih >= 0 && ih < H && iw >= 0 && iw < W) {
+      const int64_t off = ((((int64_t)(img0 + im) * H) + ih) * W + iw) * KC + cg * 8;
       v = *reinterpret_cast<const uint4*>(src + off);
       if (XF != XF_NONE) {
         float f[8];
@@ -87,6 +88,21 @@ __device__ __forceinline__ void stage_tile(uint16_t* tile, const uint16_t* __res
   }
 }
 
+// Work unit u of a client: S > 1 → images [u·S, u·S + S) whole; S == 1 → image u / (H/R),
+// output rows [(u mod H/R)·R, +R).
+__device__ __forceinline__ void unit_geom(int u, int N, int H, int R, int S, int& img0, int& ns, int& r0) {
+  if (S > 1) {
+    img0 = u * S;
+    ns = min(S, N - img0);
+    r0 = 0;
+  } else {
+    const int rb = H / R;
+    img0 = u / rb;
+    ns = 1;
+    r0 = (u % rb) * R;
+  }
+}
+
 struct Args {
   const uint16_t* src;   // x (forward) or g (backward-data)        [C][N][H][W][KC]
   const uint16_t* src2;  // y for XF_DY
@@ -103,7 +119,8 @@ struct Args {
   int NS;
   int N, H, W;
   int ldk;
-  int imgs_per_wg, imgs_per_stage;
+  int R, S, units, units_per_wg;  // stage geometry (see unit_geom) and work split
+  int nout_total;                 // output channels of the layer (a workgroup computes NOUT of them)
 };
 
 // MTW 16-pixel tiles per wave share every B fragment read.
@@ -120,7 +137,7 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
   const int wid = threadIdx.x >> 6;
   const int g = lane >> 4;
   const int H = a.H, W = a.W, HW = H * W;
-  const int Wp = W + 2, HpWp = (H + 2) * (W + 2);
+  const int Wp = W + 2;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint16_t* wl = reinterpret_cast<uint16_t*>(smem);                        // [NOUT][ldk]
@@ -132,8 +149,10 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
   uint16_t* my_stage = stage + wid * 16 * NOUT;
   uint16_t* tile = stage + 4 * 16 * NOUT;                                   // [S][H+2][W+2][LD]
 
+  const int ch_base = blockIdx.z * NOUT;  // output-channel slice of this workgroup
+  const int NO = a.nout_total;
   {
-    const uint4* s = reinterpret_cast<const uint4*>(a.wpk + (int64_t)c * a.wpk_ld);
+    const uint4* s = reinterpret_cast<const uint4*>(a.wpk + (int64_t)c * a.wpk_ld + (int64_t)ch_base * a.ldk);
     uint4* d = reinterpret_cast<uint4*>(wl);
     const int n16 = NOUT * a.ldk / 8;
     for (int i = threadIdx.x; i < n16; i += 256) d[i] = s[i];
@@ -148,22 +167,24 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
 
   const uint16_t* src = a.src + (int64_t)c * a.N * HW * KC;
   const uint16_t* src2 = (XF == XF_DY) ? a.src2 + (int64_t)c * a.N * HW * KC : nullptr;
-  uint16_t* out = a.out + (int64_t)c * a.N * HW * NOUT;
+  uint16_t* out = a.out + (int64_t)c * a.N * HW * NO;
 
   float st0[8], st1[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) { st0[j] = 0.f; st1[j] = 0.f; }
   const int my_cg = lane % CG;
 
-  // per-lane K-step geometry (compile-time KC): k = ks·32 + 8g → (tap, ci)
-  const int img_lo = blockIdx.x * a.imgs_per_wg;
-  const int img_hi = min(a.N, img_lo + a.imgs_per_wg);
-  for (int s0 = img_lo; s0 < img_hi; s0 += a.imgs_per_stage) {
-    const int ns = min(a.imgs_per_stage, img_hi - s0);
-    __syncthreads();  // previous stage fully consumed (and, first time, weights/vectors visible)
-    stage_tile<KC, XF>(tile, src, src2, v0, v1, v2, s0, ns, H, W);
+  const int R = a.R, RW = R * W;
+  const int u_lo = blockIdx.x * a.units_per_wg;
+  const int u_hi = min(a.units, u_lo + a.units_per_wg);
+  for (int u = u_lo; u < u_hi; ++u) {
+    int img0, ns, r0;
+    unit_geom(u, a.N, H, R, a.S, img0, ns, r0);
+    const int64_t pix0 = (int64_t)img0 * HW + (int64_t)r0 * W;  // first output pixel of the unit
+    __syncthreads();  // previous unit fully consumed (and, first time, weights/vectors visible)
+    stage_tile<KC, XF>(tile, src, src2, v0, v1, v2, img0, ns, r0, R, H, W);
     __syncthreads();
-    const int P = ns * HW;
+    const int P = ns * RW;
     const int ntile = (P + 15) / 16;
     for (int t0 = wid * MTW; t0 < ntile; t0 += 4 * MTW) {
       int base[MTW];
@@ -173,8 +194,8 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
         const int p = (t0 + mt) * 16 + (lane & 15);
         valid[mt] = (t0 + mt) < ntile && p < P;
         const int pp = valid[mt] ? p : 0;
-        const int im = pp / HW, r = pp % HW;
-        base[mt] = ((im * (H + 2) + r / W) * Wp + r % W) * LD;
+        const int im = pp / RW, r = pp % RW;
+        base[mt] = ((im * (R + 2) + r / W) * Wp + r % W) * LD;
       }
       f32x4 acc[MTW][NT];
 #pragma unroll
@@ -221,7 +242,7 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
           if (lane / CG < ROWS_PER_PASS && row < rows_valid) {
             const int ch0 = my_cg * 8;
             const uint4 dv = *reinterpret_cast<const uint4*>(my_stage + row * NOUT + ch0);
-            const int64_t goff = ((int64_t)s0 * HW + (t0 + mt) * 16 + row) * NOUT + ch0;
+            const int64_t goff = (pix0 + (t0 + mt) * 16 + row) * NO + ch_base + ch0;
             if (EPI == EPI_FWD) {
               *reinterpret_cast<uint4*>(out + goff) = dv;
               float f[8];
@@ -229,14 +250,14 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
 #pragma unroll
               for (int j = 0; j < 8; ++j) { st0[j] += f[j]; st1[j] += f[j] * f[j]; }
             } else {
-              const int64_t eoff = (int64_t)c * a.N * HW * NOUT + goff;
+              const int64_t eoff = (int64_t)c * a.N * HW * NO + goff;
               float gv[8], xv[8];
               unpack8(dv, gv);
               unpack8(*reinterpret_cast<const uint4*>(a.e_x + eoff), xv);
 #pragma unroll
               for (int j = 0; j < 8; ++j) {
                 const int ch = ch0 + j;
-                const bool on = xv[j] * a.e_s[(int64_t)c * NOUT + ch] + a.e_t[(int64_t)c * NOUT + ch] > 0.f;
+                const bool on = xv[j] * a.e_s[(int64_t)c * NO + ch_base + ch] + a.e_t[(int64_t)c * NO + ch_base + ch] > 0.f;
                 gv[j] = on ? gv[j] : 0.f;
               }
               const uint4 gp = pack8(gv);
@@ -274,7 +295,7 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
     const int ch = i / 2, q = i % 2;
     const float s = red[(0 * NOUT + ch) * 3 + q] + red[(1 * NOUT + ch) * 3 + q] + red[(2 * NOUT + ch) * 3 + q] +
                     red[(3 * NOUT + ch) * 3 + q];
-    atomicAdd(&a.stats[((int64_t)c * NOUT + ch) * a.NS + q], s);
+    atomicAdd(&a.stats[((int64_t)c * NO + ch_base + ch) * a.NS + q], s);
   }
 }
 
@@ -303,7 +324,7 @@ struct WArgs {
   const float* pt;
   float* dw;              // GEMM-layout scratch [C][COUT][9·CIN]
   int N, H, W;
-  int imgs_per_wg, imgs_per_stage;
+  int R, S, units, units_per_wg;
   int nt_per_z;           // GEMM column tiles (16 wide) per blockIdx.z
 };
 
@@ -327,7 +348,7 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* vv = reinterpret_cast<float*>(smem);                          // α β γ [COUT], s t [CIN]
   uint16_t* dyL = reinterpret_cast<uint16_t*>(vv + 3 * COUT + 2 * CIN);  // [S·HW][LDD]
-  uint16_t* xt = dyL + (size_t)a.imgs_per_stage * HW * LDD;              // [S][H+2][W+2][LDX]
+  uint16_t* xt = dyL + (size_t)a.S * a.R * W * LDD;                    // [S][R+2][W+2][LDX]
 
   for (int i = threadIdx.x; i < COUT; i += 256) {
     vv[i] = a.alpha[(int64_t)c * COUT + i];
@@ -349,19 +370,22 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WArgs a) {
   const uint16_t* gc = a.g + (int64_t)c * a.N * HW * COUT;
   const uint16_t* yc = a.yv + (int64_t)c * a.N * HW * COUT;
   const uint16_t* xc = a.x + (int64_t)c * a.N * HW * CIN;
-  const int img_lo = blockIdx.x * a.imgs_per_wg;
-  const int img_hi = min(a.N, img_lo + a.imgs_per_wg);
+  const int R = a.R, RW = R * W;
+  const int u_lo = blockIdx.x * a.units_per_wg;
+  const int u_hi = min(a.units, u_lo + a.units_per_wg);
 
-  for (int s0 = img_lo; s0 < img_hi; s0 += a.imgs_per_stage) {
-    const int ns = min(a.imgs_per_stage, img_hi - s0);
+  for (int u = u_lo; u < u_hi; ++u) {
+    int img0, ns, r0;
+    unit_geom(u, a.N, H, R, a.S, img0, ns, r0);
+    const int64_t pix0 = (int64_t)img0 * HW + (int64_t)r0 * W;
     __syncthreads();
     // dy = α·g + β·y + γ, natural [pixel][co] (no halo)
     {
       constexpr int CGD = COUT / 8;
-      const int total = ns * HW * CGD;
+      const int total = ns * RW * CGD;
       for (int i = threadIdx.x; i < total; i += 256) {
         const int cg = i % CGD, p = i / CGD;
-        const int64_t off = ((int64_t)s0 * HW + p) * COUT + cg * 8;
+        const int64_t off = (pix0 + p) * COUT + cg * 8;
         float gf[8], yf[8];
         unpack8(*reinterpret_cast<const uint4*>(gc + off), gf);
         unpack8(*reinterpret_cast<const uint4*>(yc + off), yf);
@@ -371,16 +395,16 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WArgs a) {
         *reinterpret_cast<uint4*>(dyL + (size_t)p * LDD + cg * 8) = pack8(gf);
       }
     }
-    stage_tile<CIN, PRO ? XF_BNRELU : XF_NONE>(xt, xc, nullptr, vv + 3 * COUT, vv + 3 * COUT + CIN, nullptr, s0,
-                                              ns, H, W);
+    stage_tile<CIN, PRO ? XF_BNRELU : XF_NONE>(xt, xc, nullptr, vv + 3 * COUT, vv + 3 * COUT + CIN, nullptr, img0,
+                                              ns, r0, R, H, W);
     __syncthreads();
-    const int KS = ns * HW / 32;  // HW is a multiple of 64
+    const int KS = ns * RW / 32;  // R·W is a multiple of 32
     for (int ks = kgrp; ks < KS; ks += WK) {
       const int p0 = ks * 32;
       // this lane's pixel row of the fragment (8-pixel groups never straddle an image row: W % 8 == 0)
       const int pix = p0 + 8 * g + q;
-      const int im = pix / HW, r = pix % HW;
-      const uint16_t* xrow = xt + (size_t)((im * (H + 2) + r / W) * Wp + r % W) * LDX + 4 * pq;
+      const int im = pix / RW, r = pix % RW;
+      const uint16_t* xrow = xt + (size_t)((im * (R + 2) + r / W) * Wp + r % W) * LDX + 4 * pq;
       const uint16_t* drow = dyL + (size_t)pix * LDD + 4 * pq;
       bf16x8 af[MT];
 #pragma unroll
@@ -445,20 +469,49 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WArgs a) {
 // ---------------------------------------------------------------------------------------------
 // host side
 // ---------------------------------------------------------------------------------------------
-static size_t gemm_smem(int kc, int nout, int ldk, int S, int H, int W) {
-  return (size_t)nout * ldk * 2 + (size_t)3 * kc * 4 + (size_t)4 * nout * 3 * 4 + (size_t)4 * 16 * nout * 2 +
-         (size_t)S * (H + 2) * (W + 2) * (kc + 8) * 2;
+struct Plan {
+  int R, S, units, units_per_wg, gx;
+};
+
+// Stage ≈ `target_px` output pixels: whole images when they are small (S images), otherwise a
+// block of R rows of one image (R·W a multiple of 32). ~`target_wgs` workgroups in total, each
+// looping over a contiguous run of units (amortises the weight staging).
+static Plan make_plan(int N, int H, int W, int C, int target_px, int target_wgs) {
+  Plan p;
+  const int hw = H * W;
+  if (hw <= target_px) {
+    p.R = H;
+    p.S = max(1, min(N, target_px / hw));
+    p.units = (N + p.S - 1) / p.S;
+  } else {
+    p.S = 1;
+    p.R = 1;
+    for (int r = H; r >= 1; --r)
+      if (H % r == 0 && r * W <= target_px && (r * W) % 32 == 0) { p.R = r; break; }
+    p.units = N * (H / p.R);
+  }
+  const int wpc = max(1, (target_wgs + C - 1) / C);
+  p.units_per_wg = max(1, (p.units + wpc - 1) / wpc);
+  p.gx = (p.units + p.units_per_wg - 1) / p.units_per_wg;
+  return p;
 }
 
-template <int KC, int NOUT, int XF, int BWD, int EPI>
-static int launch_gemm(const Args& a, int C, hipStream_t stream) {
-  constexpr int MTW = NOUT >= 64 ? 2 : 4;
-  const size_t smem = gemm_smem(KC, NOUT, a.ldk, a.imgs_per_stage, a.H, a.W);
+static size_t gemm_smem(int kc, int nout, int ldk, const Plan& p, int W) {
+  return (size_t)nout * ldk * 2 + (size_t)3 * kc * 4 + (size_t)4 * nout * 3 * 4 + (size_t)4 * 16 * nout * 2 +
+         (size_t)p.S * (p.R + 2) * (W + 2) * (kc + 8) * 2;
+}
+
+// NOUT_WG output channels per workgroup (blockIdx.z slices the layer's NOUT)
+template <int KC, int NOUT_WG, int XF, int BWD, int EPI>
+static int launch_gemm(Args a, int nout, int C, int target_px, hipStream_t stream) {
+  constexpr int MTW = NOUT_WG >= 64 ? 2 : 4;
+  const Plan p = make_plan(a.N, a.H, a.W, C, target_px, 2048);
+  a.R = p.R; a.S = p.S; a.units = p.units; a.units_per_wg = p.units_per_wg; a.nout_total = nout;
+  const size_t smem = gemm_smem(KC, NOUT_WG, a.ldk, p, a.W);
   if (smem > 160 * 1024) return -5;
-  auto kern = conv3x3_gemm_kernel<KC, NOUT, XF, BWD, EPI, MTW>;
-  hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-  const int gx = (a.N + a.imgs_per_wg - 1) / a.imgs_per_wg;
-  hipLaunchKernelGGL(kern, dim3(gx, C), dim3(256), smem, stream, a);
+  auto kern = conv3x3_gemm_kernel<KC, NOUT_WG, XF, BWD, EPI, MTW>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  hipLaunchKernelGGL(kern, dim3(p.gx, C, nout / NOUT_WG), dim3(256), smem, stream, a);
   return (int)hipGetLastError();
 }
 
@@ -466,23 +519,11 @@ template <int XF, int BWD, int EPI>
 static int dispatch_gemm(int kc, int nout, const Args& a, int C, hipStream_t s) {
   if (kc != nout) return -2;
   switch (kc) {
-    case 16: return launch_gemm<16, 16, XF, BWD, EPI>(a, C, s);
-    case 32: return launch_gemm<32, 32, XF, BWD, EPI>(a, C, s);
-    case 64: return launch_gemm<64, 64, XF, BWD, EPI>(a, C, s);
+    case 16: return launch_gemm<16, 16, XF, BWD, EPI>(a, nout, C, 256, s);
+    case 32: return launch_gemm<32, 32, XF, BWD, EPI>(a, nout, C, 256, s);
+    case 64: return launch_gemm<64, 32, XF, BWD, EPI>(a, nout, C, 128, s);  // weights split over z
     default: return -2;
   }
-}
-
-// images per workgroup / per LDS stage: ≥ ~1K pixels per stage, ≈4 workgroups per CU overall
-static void plan(int N, int H, int W, int C, int max_stage_px, int* per_wg, int* per_stage) {
-  const int hw = H * W;
-  int stage = max(1, min(N, max_stage_px / hw));
-  int wgs_per_client = max(1, (2048 + C - 1) / C);
-  int pw = max(1, (N + wgs_per_client - 1) / wgs_per_client);
-  pw = max(pw, 1);
-  stage = min(stage, pw);
-  *per_wg = pw;
-  *per_stage = stage;
 }
 
 }  // namespace c3
@@ -495,7 +536,6 @@ FA_EXPORT int fa_conv3x3_fwd(const uint16_t* x, const uint16_t* wpk, int64_t wpk
   c3::Args a = {};
   a.src = x; a.wpk = wpk; a.wpk_ld = wpk_ld; a.vec0 = pscale; a.vec1 = pshift; a.out = y; a.stats = stats; a.NS = 2;
   a.N = N; a.H = H; a.W = W; a.ldk = ldk;
-  c3::plan(N, H, W, C, Cin >= 64 ? 128 : (Cin >= 32 ? 512 : 1024), &a.imgs_per_wg, &a.imgs_per_stage);
   if (pscale) return c3::dispatch_gemm<c3::XF_BNRELU, 0, c3::EPI_FWD>(Cin, Cout, a, C, stream);
   return c3::dispatch_gemm<c3::XF_NONE, 0, c3::EPI_FWD>(Cin, Cout, a, C, stream);
 }
@@ -511,7 +551,6 @@ FA_EXPORT int fa_conv3x3_bwd_data(const uint16_t* g, const uint16_t* yv, const f
   a.src = g; a.src2 = yv; a.wpk = wpk_b; a.wpk_ld = wpk_ld; a.vec0 = alpha; a.vec1 = beta; a.vec2 = gamma;
   a.out = dx; a.e_x = e_x; a.e_s = e_s; a.e_t = e_t; a.stats = stats; a.NS = 3;
   a.N = N; a.H = H; a.W = W; a.ldk = ldk2;
-  c3::plan(N, H, W, C, Cout >= 64 ? 128 : (Cout >= 32 ? 512 : 1024), &a.imgs_per_wg, &a.imgs_per_stage);
   return c3::dispatch_gemm<c3::XF_DY, 1, c3::EPI_MASK>(Cout, Cin, a, C, stream);
 }
 
@@ -520,27 +559,25 @@ FA_EXPORT int fa_conv3x3_bwd_data(const uint16_t* g, const uint16_t* yv, const f
 FA_EXPORT int fa_conv3x3_wgrad(const uint16_t* g, const uint16_t* yv, const float* alpha, const float* beta,
                                const float* gamma, const uint16_t* x, const float* ps, const float* pt, float* dw,
                                int C, int N, int H, int W, int Cin, int Cout, hipStream_t stream) {
-  if (W % 8 != 0 || (H * W) % 64 != 0 || Cin != Cout) return -3;
+  if (W % 8 != 0 || (H * W) % 32 != 0 || Cin != Cout) return -3;
   c3::WArgs a = {};
   a.g = g; a.yv = yv; a.alpha = alpha; a.beta = beta; a.gamma = gamma; a.x = x; a.ps = ps; a.pt = pt; a.dw = dw;
   a.N = N; a.H = H; a.W = W;
-  int stage_px = Cin >= 64 ? 256 : (Cin >= 32 ? 512 : 1024);
-  c3::plan(N, H, W, C, stage_px, &a.imgs_per_wg, &a.imgs_per_stage);
+  const c3::Plan p = c3::make_plan(N, H, W, C, Cin >= 64 ? 128 : 256, 2048);
+  a.R = p.R; a.S = p.S; a.units = p.units; a.units_per_wg = p.units_per_wg;
   const int NTK = 9 * Cin / 16;
-  const size_t smem_base = (size_t)(3 * Cout + 2 * Cin) * 4 +
-                           (size_t)a.imgs_per_stage * H * W * (Cout + 8) * 2 +
-                           (size_t)a.imgs_per_stage * (H + 2) * (W + 2) * (Cin + 8) * 2;
+  const size_t vv = (size_t)(3 * Cout + 2 * Cin) * 4;
+  const size_t smem_base = vv + (size_t)p.S * p.R * W * (Cout + 8) * 2 +
+                           (size_t)p.S * (p.R + 2) * (W + 2) * (Cin + 8) * 2;
 #define W3_LAUNCH(CI, CO, WN, TPW, NZ)                                                                         \
   {                                                                                                            \
     a.nt_per_z = (NTK + (NZ) - 1) / (NZ);                                                                      \
     auto kern = ps ? c3::conv3x3_wgrad_kernel<CI, CO, 1, WN, TPW> : c3::conv3x3_wgrad_kernel<CI, CO, 0, WN, TPW>; \
     const size_t red = (size_t)(4 / (WN) - 1) * (WN) * ((CO) / 16) * (TPW) * 256 * 4;                          \
-    const size_t smem = smem_base > red + (size_t)(3 * Cout + 2 * Cin) * 4 ? smem_base                         \
-                                                                          : red + (3 * Cout + 2 * Cin) * 4;    \
+    const size_t smem = smem_base > red + vv ? smem_base : red + vv;                                           \
     if (smem > 160 * 1024) return -5;                                                                          \
-    hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);             \
-    const int gx = (N + a.imgs_per_wg - 1) / a.imgs_per_wg;                                                    \
-    hipLaunchKernelGGL(kern, dim3(gx, C, NZ), dim3(256), smem, stream, a);                                     \
+    (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);       \
+    hipLaunchKernelGGL(kern, dim3(p.gx, C, NZ), dim3(256), smem, stream, a);                                   \
     return (int)hipGetLastError();                                                                             \
   }
   switch (Cin) {
