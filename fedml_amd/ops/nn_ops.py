@@ -89,6 +89,23 @@ def conv3x3_wgrad(g, yv, alpha, beta, gamma, x, ps, pt, garena, woff, C, N, H, W
     _check(rc, "fa_wgrad_scatter")
 
 
+# ---- 1×1 / stride-1 weight gradient (csrc/conv1x1_kernels.hip) ----
+_C1_SHAPES = {(16, 64), (64, 16), (16, 16), (32, 128), (128, 32), (32, 32), (64, 256), (256, 64), (64, 64),
+              (128, 128), (64, 128)}
+
+
+def conv1x1_wgrad_supported(cin, cout, k, stride, pad):
+    return k == 1 and stride == 1 and pad == 0 and (cin, cout) in _C1_SHAPES
+
+
+def conv1x1_wgrad(g, yv, alpha, beta, gamma, x, ps, pt, garena, woff, C, M, Cin, Cout, pix_per_wg):
+    """dW += Σ_p dyᵀ·act(x) straight into the OIHW arena rows (stride garena.stride(0))."""
+    rc = _fn("fa_conv1x1_wgrad")(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(x), _p(ps), _p(pt), _p(garena),
+                                 _i64(garena.stride(0)), _i64(woff), _i(C), _i(M), _i(Cin), _i(Cout), _i(pix_per_wg),
+                                 _stream(g))
+    _check(rc, "fa_conv1x1_wgrad")
+
+
 def bn_fwd_finalize(stats, C, Ch, n, arena, off_gamma, off_beta, off_rm, off_rv, off_nbt, momentum, eps, active,
                     scale, shift, mean, rstd, update_running=True):
     rc = _fn("fa_bn_fwd_finalize")(_p(stats), _i(C), _i(Ch), _f(n), _p(arena), _i64(arena.stride(0)),

@@ -18,6 +18,7 @@ Per block (k chained convs, last BN joins the residual):
 """
 import ctypes
 import math
+import os
 from dataclasses import dataclass, field
 from typing import List, Optional
 
@@ -136,8 +137,8 @@ class NativeResNetStep:
         self.off = {s.key: s.offset for s in layout.slots}
         self.geom = None
         self._segs = None
-        import os
         self.use_c3 = os.environ.get("FEDML_AMD_CONV3X3", "1") != "0"
+        self.use_c1 = os.environ.get("FEDML_AMD_CONV1X1", "1") != "0"
 
     # ------------------------------------------------------------------ setup
     def _all_convs(self):
@@ -269,6 +270,32 @@ class NativeResNetStep:
     def _c3(self, cv: ConvSpec):
         return self.use_c3 and nn_ops.conv3x3_supported(cv.cin_pad, cv.cout, cv.k, cv.stride, cv.pad, cv.H, cv.W)
 
+    def _wgrad(self, cv: ConvSpec, g, y, vec, x, pro_vec, garena, N):
+        """Weight gradient of conv ``cv`` (dy from (g, y, α β γ), x the conv input with an optional
+        BN+ReLU prologue) accumulated into the arena: tiled 3×3 / 1×1 kernels when they apply."""
+        C = self.C
+        ps = pro_vec[0] if pro_vec is not None else None
+        pt = pro_vec[1] if pro_vec is not None else None
+        if self._c3(cv):
+            nn_ops.conv3x3_wgrad(g, y, vec[4], vec[5], vec[6], x, ps, pt, garena, self.off[cv.key], C, N, cv.H, cv.W,
+                                 cv.cin_pad, cv.cout, cv.cin, self.dw_scratch)
+            return
+        M = N * cv.Ho * cv.Wo
+        if self.use_c1 and cv.cin == cv.cin_pad and nn_ops.conv1x1_wgrad_supported(cv.cin, cv.cout, cv.k, cv.stride,
+                                                                                  cv.pad):
+            nn_ops.conv1x1_wgrad(g, y, vec[4], vec[5], vec[6], x, ps, pt, garena, self.off[cv.key], C, M, cv.cin,
+                                 cv.cout, self._c1_pix_per_wg(M))
+            return
+        nn_ops.conv_wgrad(g, y, vec[4], vec[5], vec[6], x, ps, pt, garena, self.off[cv.key], C, N, cv.H, cv.W,
+                          cv.cin_pad, cv.Ho, cv.Wo, cv.cout, cv.k, cv.k, cv.stride, cv.pad, self._pix_per_wg(M), cv.cin,
+                          self.dw_scratch)
+
+    def _c1_pix_per_wg(self, M):
+        ppw = int(os.environ.get("FEDML_AMD_C1_PPW", "0"))
+        if ppw:
+            return ppw
+        return max(512, min(2048, _round_up(max(1, (M * self.C) // 1024), 128)))
+
     def _fwd(self, cv: ConvSpec, x, y, pro_vec, stats, N):
         M = N * cv.Ho * cv.Wo
         if self._c3(cv):
@@ -381,10 +408,8 @@ class NativeResNetStep:
                 pv = self.bn_vec[b.bns[j - 1].key]
                 M = N * cv.Ho * cv.Wo
                 out_g = free[0] if g_j is not free[0] else free[1]
+                self._wgrad(cv, g_j, b.ys[j], v, b.ys[j - 1], pv, garena, N)
                 if self._c3(cv):
-                    nn_ops.conv3x3_wgrad(g_j, b.ys[j], v[4], v[5], v[6], b.ys[j - 1], pv[0], pv[1], garena,
-                                         self.off[cv.key], C, N, cv.H, cv.W, cv.cin_pad, cv.cout, cv.cin,
-                                         self.dw_scratch)
                     nn_ops.conv3x3_bwd_data(g_j, b.ys[j], v[4], v[5], v[6], self.packed.view(-1)[cv.off_b:],
                                             self.packed_ld, out_g, b.ys[j - 1], pv[0], pv[1],
                                             self.stat_views[b.bns[j - 1].key][1], C, N, cv.H, cv.W, cv.cout,
@@ -392,9 +417,6 @@ class NativeResNetStep:
                     self._bn_bwd(b.bns[j - 1], 1, N, cv.H * cv.W, arena, garena)
                     g_j = out_g
                     continue
-                nn_ops.conv_wgrad(g_j, b.ys[j], v[4], v[5], v[6], b.ys[j - 1], pv[0], pv[1], garena,
-                                  self.off[cv.key], C, N, cv.H, cv.W, cv.cin_pad, cv.Ho, cv.Wo, cv.cout, cv.k, cv.k,
-                                  cv.stride, cv.pad, self._pix_per_wg(M), cv.cin, self.dw_scratch)
                 nn_ops.conv_bwd_data(g_j, b.ys[j], v[4], v[5], v[6], self.packed.view(-1)[cv.off_b:],
                                      self.packed_ld, out_g, nn_ops.EPI_MASK, b.ys[j - 1], pv[0], pv[1], None, None,
                                      None, self.stat_views[b.bns[j - 1].key][1], C, N, cv.Ho, cv.Wo, cv.cout,
@@ -407,9 +429,7 @@ class NativeResNetStep:
             if b.ds_conv is not None:
                 d = b.ds_conv
                 vd = self.bn_vec[b.ds_bn.key]
-                nn_ops.conv_wgrad(gpre, b.yd, vd[4], vd[5], vd[6], b.act_in, None, None, garena, self.off[d.key], C, N,
-                                  d.H, d.W, d.cin_pad, d.Ho, d.Wo, d.cout, d.k, d.k, d.stride, d.pad,
-                                  self._pix_per_wg(N * d.Ho * d.Wo), d.cin, self.dw_scratch)
+                self._wgrad(d, gpre, b.yd, vd, b.act_in, None, garena, N)
                 nn_ops.conv_bwd_data(gpre, b.yd, vd[4], vd[5], vd[6], self.packed.view(-1)[d.off_b:], self.packed_ld,
                                      gadd, nn_ops.EPI_STORE, None, None, None, None, None, None, self.stats, C, N,
                                      d.Ho, d.Wo, d.cout, d.cin_pad, d.k, d.k, d.stride, d.pad, d.H, d.W, d.ldk2,
@@ -420,9 +440,7 @@ class NativeResNetStep:
             # conv 0: weight grad, then data grad with the block epilogue (→ previous block's g)
             cv0, bn0 = b.convs[0], b.bns[0]
             v = self.bn_vec[bn0.key]
-            nn_ops.conv_wgrad(g_j, b.ys[0], v[4], v[5], v[6], b.act_in, None, None, garena, self.off[cv0.key], C, N,
-                              cv0.H, cv0.W, cv0.cin_pad, cv0.Ho, cv0.Wo, cv0.cout, cv0.k, cv0.k, cv0.stride, cv0.pad,
-                              self._pix_per_wg(N * cv0.Ho * cv0.Wo), cv0.cin, self.dw_scratch)
+            self._wgrad(cv0, g_j, b.ys[0], v, b.act_in, None, garena, N)
             if prev_block is not None:
                 ey1, ey2 = prev_block.ys[-1], prev_block.yd
                 pstats = self.stat_views[prev_block.bns[-1].key][1]
@@ -442,8 +460,5 @@ class NativeResNetStep:
         # stem backward: bn0 bwd then weight grad only
         self._bn_bwd(st_bn, 1, N, st_conv.Ho * st_conv.Wo, arena, garena)
         v = self.bn_vec[st_bn.key]
-        nn_ops.conv_wgrad(gpre, self.stem_y, v[4], v[5], v[6], self.x_in, None, None, garena, self.off[st_conv.key], C,
-                          N, st_conv.H, st_conv.W, st_conv.cin_pad, st_conv.Ho, st_conv.Wo, st_conv.cout, st_conv.k,
-                          st_conv.k, st_conv.stride, st_conv.pad, self._pix_per_wg(N * st_conv.Ho * st_conv.Wo),
-                          st_conv.cin, self.dw_scratch)
+        self._wgrad(st_conv, gpre, self.stem_y, v, self.x_in, None, garena, N)
         return loss.detach()

@@ -71,6 +71,11 @@ def c3_wgrad(g, y, al, be, ga, x, ps, pt, garena, woff, C, N, H, W, Cin, Cout, c
     return c_wgrad(g, y, al, be, ga, x, ps, pt, garena, woff, C, N, H, W, Cin, H, W, Cout, 3, 3, 1, 1, 0, cs, scratch)
 
 
+def c1_wgrad(g, y, al, be, ga, x, ps, pt, garena, woff, C, M, Cin, Cout, ppw):
+    return (f"1x1 {Cin}->{Cout} M{M}" + (" +bnrelu" if ps is not None else ""), C * M * (2 * Cout + Cin) * 2,
+            2 * C * M * Cout * Cin)
+
+
 def c_block(y, s, t, r, rs, rt, out, C, per, Ch):
     return (f"ch{Ch} n{per // Ch}" + (" ds" if rs is not None else ""), C * per * 2 * (3 if r is not None else 2), 0)
 
@@ -93,6 +98,7 @@ def main():
     _wrap("conv3x3_fwd", c3_fwd)
     _wrap("conv3x3_bwd_data", c3_bwd)
     _wrap("conv3x3_wgrad", c3_wgrad)
+    _wrap("conv1x1_wgrad", c1_wgrad)
     for n in ("bn_fwd_finalize", "bn_bwd_finalize", "pack_weights", "avgpool", "head_bwd", "nchw_to_nhwc_pad"):
         _wrap(n, c_other)
     torch.manual_seed(0)

@@ -171,3 +171,31 @@ def test_conv3x3_kernels_vs_fp32_reference(ch, hw):
         xa = torch.relu(x[c].float() * s[c] + t[c]).to(bf).float().permute(0, 3, 1, 2)
         ref = torch.nn.grad.conv2d_weight(xa, (ch, ch, 3, 3), dy, padding=1)
         assert rel(garena[c, 16:16 + ch * ch * 9], ref.reshape(-1)) < 1e-4
+
+
+@pytest.mark.parametrize("cin,cout,hw", [(16, 64, 32), (64, 16, 32), (32, 128, 16), (128, 32, 16), (64, 256, 8),
+                                         (256, 64, 8), (64, 64, 8)])
+@pytest.mark.parametrize("pro", [False, True])
+def test_conv1x1_wgrad_vs_fp32_reference(cin, cout, hw, pro):
+    from fedml_amd.ops import nn_ops
+    torch.manual_seed(1)
+    C, N, bf = 3, 8, torch.bfloat16
+    x = torch.randn(C, N, hw, hw, cin, device=DEV).to(bf)
+    g = torch.randn(C, N, hw, hw, cout, device=DEV).to(bf)
+    yv = torch.randn(C, N, hw, hw, cout, device=DEV).to(bf)
+    al, be = torch.rand(C, cout, device=DEV), torch.randn(C, cout, device=DEV) * 0.1
+    ga = torch.randn(C, cout, device=DEV) * 0.01
+    s = torch.rand(C, cin, device=DEV) + 0.5 if pro else None
+    t = torch.randn(C, cin, device=DEV) * 0.1 if pro else None
+    garena = torch.zeros(C, cin * cout + 48, device=DEV)
+    M = N * hw * hw
+    nn_ops.conv1x1_wgrad(g, yv, al, be, ga, x, s, t, garena, 16, C, M, cin, cout, 512)
+    torch.cuda.synchronize()
+    for c in range(C):
+        dy = (al[c] * g[c].float() + be[c] * yv[c].float() + ga[c]).to(bf).float().reshape(-1, cout)
+        xa = x[c].float()
+        if pro:
+            xa = torch.relu(xa * s[c] + t[c]).to(bf).float()
+        ref = dy.t() @ xa.reshape(-1, cin)
+        got = garena[c, 16:16 + cin * cout].view(cout, cin)
+        assert float((got - ref).norm() / ref.norm()) < 1e-4
