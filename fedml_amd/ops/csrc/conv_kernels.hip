@@ -142,12 +142,15 @@ struct ConvArgs {
   int ldk;               // packed row length (≥ K, multiple of 32, +8 pad)
   int Kp;                // K rounded to 32
   int tiles_per_wave;
+  int nout_total;        // output channels of the layer; a workgroup computes NOUT of them (blockIdx.z)
 };
 
 template <int NT, int AOP, int PRO, int MODE, int EPI>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
   constexpr int NOUT = NT * 16;
   const int c = blockIdx.y;
+  const int NO = a.nout_total;
+  const int ch_base = blockIdx.z * NOUT;
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int K = a.KH * a.KW * a.KC;
@@ -164,7 +167,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
 
   // ---- stage packed weights (16-B copies) and per-channel vectors ----
   {
-    const uint4* src = reinterpret_cast<const uint4*>(a.wpk + (int64_t)c * a.wpk_ld);
+    const uint4* src = reinterpret_cast<const uint4*>(a.wpk + (int64_t)c * a.wpk_ld + (int64_t)ch_base * a.ldk);
     uint4* dst = reinterpret_cast<uint4*>(wl);
     const int n16 = NOUT * a.ldk / 8;
     for (int i = threadIdx.x; i < n16; i += 256) dst[i] = src[i];
@@ -182,7 +185,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
   const int64_t src_client = (int64_t)c * a.Nb * a.Hs * a.Ws * a.KC;
   const uint16_t* src = a.src + src_client;
   const uint16_t* src2 = (AOP == AOP_DY) ? a.src2 + src_client : nullptr;
-  uint16_t* out = a.out + (int64_t)c * M * NOUT;
+  uint16_t* out = a.out + (int64_t)c * M * NO;
 
   // epilogue per-lane statistics: lane owns the 8 channels (lane % (NOUT/8))*8 .. +7
   constexpr int CG = NOUT / 8;                 // 16-B chunks per output row
@@ -276,7 +279,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
       if (lane / CG < ROWS_PER_PASS && row < rows_valid) {
         const int ch0 = my_cg * 8;
         const uint4 dv = *reinterpret_cast<const uint4*>(my_stage + row * NOUT + ch0);
-        const int64_t goff = ((int64_t)(tile * 16 + row)) * NOUT + ch0;
+        const int64_t goff = ((int64_t)(tile * 16 + row)) * NO + ch_base + ch0;
         if (EPI == EPI_FWD || EPI == EPI_STORE) {
           *reinterpret_cast<uint4*>(out + goff) = dv;
           if (EPI == EPI_FWD) {
@@ -286,7 +289,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
             for (int j = 0; j < 8; ++j) { st0[j] += f[j]; st1[j] += f[j] * f[j]; }
           }
         } else {
-          const int64_t eoff = (int64_t)c * M * NOUT + goff;
+          const int64_t eoff = (int64_t)c * M * NO + goff;
           float g[8], xv[8];
           unpack8(dv, g);
           unpack8(*reinterpret_cast<const uint4*>(a.e_x + eoff), xv);
@@ -294,7 +297,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
               const int ch = ch0 + j;
-              const bool on_ = xv[j] * a.e_s[(int64_t)c * NOUT + ch] + a.e_t[(int64_t)c * NOUT + ch] > 0.f;
+              const bool on_ = xv[j] * a.e_s[(int64_t)c * NO + ch_base + ch] + a.e_t[(int64_t)c * NO + ch_base + ch] > 0.f;
               g[j] = on_ ? g[j] : 0.f;
             }
           } else {  // EPI_BLOCK: g = (g + extra) · [block_input > 0]
@@ -353,7 +356,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
       const int ch = i / a.NS, q = i % a.NS;
       const float s = red[(0 * NOUT + ch) * 3 + q] + red[(1 * NOUT + ch) * 3 + q] + red[(2 * NOUT + ch) * 3 + q] +
                       red[(3 * NOUT + ch) * 3 + q];
-      atomicAdd(&a.stats[((int64_t)c * NOUT + ch) * a.NS + q], s);
+      atomicAdd(&a.stats[((int64_t)c * NO + ch_base + ch) * a.NS + q], s);
     }
   }
 }
@@ -363,7 +366,8 @@ static size_t conv_smem_bytes(int nout, int ldk, int kc) {
 }
 
 template <int NT, int AOP, int PRO, int MODE, int EPI>
-static int launch_conv(const ConvArgs& a, int C, hipStream_t stream) {
+static int launch_conv(ConvArgs a, int nout, int C, hipStream_t stream) {
+  a.nout_total = nout;
   const int M = a.Nb * a.Ho * a.Wo;
   const int tiles = (M + 15) / 16;
   const int per_wg = 4 * a.tiles_per_wave;
@@ -371,18 +375,21 @@ static int launch_conv(const ConvArgs& a, int C, hipStream_t stream) {
   const size_t smem = conv_smem_bytes(NT * 16, a.ldk, a.KC);
   auto kern = conv_gemm_kernel<NT, AOP, PRO, MODE, EPI>;
   if (smem > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-  hipLaunchKernelGGL(kern, dim3(gx, C), dim3(256), smem, stream, a);
+  hipLaunchKernelGGL(kern, dim3(gx, C, nout / (NT * 16)), dim3(256), smem, stream, a);
   return (int)hipGetLastError();
 }
 
+// Wide outputs (128/256 channels) are split over blockIdx.z in 64-channel slices: the per-WG weight
+// and epilogue-staging LDS shrinks 2–4× (several workgroups per CU instead of one), at the cost of
+// re-reading the (narrow) A operand once per slice.
 template <int AOP, int PRO, int MODE, int EPI>
 static int dispatch_nt(int nout, const ConvArgs& a, int C, hipStream_t s) {
   switch (nout) {
-    case 16: return launch_conv<1, AOP, PRO, MODE, EPI>(a, C, s);
-    case 32: return launch_conv<2, AOP, PRO, MODE, EPI>(a, C, s);
-    case 64: return launch_conv<4, AOP, PRO, MODE, EPI>(a, C, s);
-    case 128: return launch_conv<8, AOP, PRO, MODE, EPI>(a, C, s);
-    case 256: return launch_conv<16, AOP, PRO, MODE, EPI>(a, C, s);
+    case 16: return launch_conv<1, AOP, PRO, MODE, EPI>(a, nout, C, s);
+    case 32: return launch_conv<2, AOP, PRO, MODE, EPI>(a, nout, C, s);
+    case 64:
+    case 128:
+    case 256: return launch_conv<4, AOP, PRO, MODE, EPI>(a, nout, C, s);
     default: return -2;
   }
 }
