@@ -29,6 +29,7 @@ from .fl_ops import (
     confusion_matrix,
     cast_bf16,
     mod_matmul,
+    augment,
     mod_sum,
     use_native,
 )

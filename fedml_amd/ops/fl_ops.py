@@ -522,3 +522,60 @@ def mod_sum(X: torch.Tensor, p: int) -> torch.Tensor:
     for c in range(X.shape[0]):
         acc = (acc + X[c]) % p
     return acc
+
+
+# ----------------------------------------------------------------------------- K16
+def _philox4x32(c0, c1, c2, c3, k0, k1):
+    """Host twin of common.h's Philox4x32-10 (used by the CPU reference of ``augment``)."""
+    M0, M1, W0, W1 = 0xD2511F53, 0xCD9E8D57, 0x9E3779B9, 0xBB67AE85
+    m = 0xFFFFFFFF
+    for _ in range(10):
+        p0, p1 = M0 * c0, M1 * c2
+        hi0, lo0, hi1, lo1 = p0 >> 32, p0 & m, p1 >> 32, p1 & m
+        c0, c1, c2, c3 = (hi1 ^ c1 ^ k0) & m, lo1, (hi0 ^ c3 ^ k1) & m, lo0
+        k0, k1 = (k0 + W0) & m, (k1 + W1) & m
+    return c0, c1, c2, c3
+
+
+def augment(x, seed=0, sample_ids=None, pad=4, cutout=16, flip=True, mean=None, std=None):
+    """RandomCrop(pad) + HorizontalFlip + Cutout + Normalize of a [B, C, H, W] fp32 batch (fused
+    HIP kernel on GPU; per-sample Philox randomness keyed by (seed, sample id))."""
+    B, C, H, W = x.shape
+    mean_t = torch.as_tensor(mean, dtype=torch.float32, device=x.device) if mean is not None else None
+    inv_t = (1.0 / torch.as_tensor(std, dtype=torch.float32, device=x.device)) if std is not None else None
+    if use_native(x):
+        xin = x.contiguous().float()
+        out = torch.empty_like(xin)
+        ids = sample_ids.to(device=x.device, dtype=torch.int64).contiguous() if sample_ids is not None else None
+        rc = _fn("fa_augment")(_p(xin), _p(out), _p(ids), _c.c_int(B), _c.c_int(C), _c.c_int(H), _c.c_int(W),
+                               _c.c_int(pad), _c.c_int(cutout), _c.c_int(int(flip)), _p(mean_t), _p(inv_t),
+                               _c.c_uint32(seed & 0xFFFFFFFF), _stream(x))
+        _check(rc, "fa_augment")
+        return out
+    out = torch.empty_like(x, dtype=torch.float32)
+    ids = sample_ids.tolist() if sample_ids is not None else list(range(B))
+    for b in range(B):
+        sid = int(ids[b])
+        r = _philox4x32(sid & 0xFFFFFFFF, (sid >> 32) & 0xFFFFFFFF, 0x41554721, 0, seed & 0xFFFFFFFF, 0x9E3779B9)
+        dy = (r[0] % (2 * pad + 1)) - pad if pad else 0
+        dx = (r[1] % (2 * pad + 1)) - pad if pad else 0
+        fl = bool(flip and (r[2] & 1))
+        shifted = torch.zeros_like(x[b], dtype=torch.float32)
+        # out[oh, ow] = src[oh+dy, flip(ow)+dx]: crop offset applies in the unflipped frame
+        src = x[b].float()
+        ow = torch.arange(W)
+        sw0 = (W - 1 - ow) if fl else ow
+        for oh in range(H):
+            sh = oh + dy
+            if 0 <= sh < H:
+                sw = sw0 + dx
+                ok = (sw >= 0) & (sw < W)
+                shifted[:, oh, ok] = src[:, sh, sw[ok]]
+        if cutout:
+            cy, cx = r[3] % H, (r[3] >> 16) % W
+            h = cutout // 2
+            shifted[:, max(0, cy - h):max(0, cy + h), max(0, cx - h):max(0, cx + h)] = 0
+        if mean_t is not None:
+            shifted = (shifted - mean_t.view(-1, 1, 1)) * inv_t.view(-1, 1, 1)
+        out[b] = shifted
+    return out

@@ -61,6 +61,11 @@ class ClientBatchEngine:
         self._build_views()
         self.global_ref = None
         self.loss_history: List[float] = []
+        # on-device CIFAR augmentation (RandomCrop(pad) + flip + Cutout), reference transforms
+        self.augment = bool(getattr(args, "data_augmentation", False))
+        self.aug_pad = int(getattr(args, "augment_pad", 4))
+        self.aug_cutout = int(getattr(args, "cutout_length", 16))
+        self._aug_calls = 0
 
     # ------------------------------------------------------------------------------------------
     def _build_views(self):
@@ -118,6 +123,11 @@ class ClientBatchEngine:
                 uniform = all(b == bmax for b in b_c)
                 idx = order[:, lo:lo + bmax]
                 x, y, mask = store.gather(idx)
+                if self.augment and x.dim() == 5:
+                    self._aug_calls += 1
+                    x = ops.augment(x.reshape(-1, *x.shape[2:]), seed=int(getattr(self.args, "random_seed", 0)) * 7919
+                                    + self._aug_calls, sample_ids=idx.reshape(-1), pad=self.aug_pad,
+                                    cutout=self.aug_cutout).view_as(x)
                 active = torch.tensor(active_list, dtype=torch.float32, device=self.device)
                 sample_mask = None if uniform else mask.t().contiguous()     # [B, C]
                 loss = self._step_loss(x, y, mask, b_c, active, sample_mask, use_native_loss)

@@ -227,3 +227,13 @@ def test_secagg_on_device():
     alive = [0, 1, 3]
     out = sa.aggregate({c: cl[c].masked_input(xs[c], sa.pks) for c in alive})
     assert torch.allclose(out, sum(xs[c] for c in alive).double(), atol=1e-5)
+
+
+@pytest.mark.parametrize("pad,cutout,flip", [(4, 16, True), (0, 0, True), (2, 8, False)])
+def test_augment_matches_cpu_reference(pad, cutout, flip):
+    x = torch.randn(6, 3, 32, 32)
+    ids = torch.tensor([5, 17, 1 << 33, 0, 2, 99])
+    kw = dict(seed=11, sample_ids=ids, pad=pad, cutout=cutout, flip=flip, mean=[0.4, 0.5, 0.6], std=[0.2, 0.3, 0.4])
+    ref = ops.augment(x, **kw)
+    got = ops.augment(x.to(DEV), **kw).cpu()
+    assert torch.allclose(ref, got, atol=1e-5)
