@@ -143,6 +143,56 @@ def _load_synthetic(args, spec):
     return tl, te, nd, spec.num_classes
 
 
+def _clients_to_loaded(train: Dict[int, tuple], test: Dict[int, tuple], bs, class_num):
+    tl = {c: ClientData(x, y, bs, shuffle=True, seed=c) for c, (x, y) in train.items()}
+    te = {c: ClientData(x, y, bs) for c, (x, y) in test.items()} if test else {
+        c: ClientData(tl[c].x[:0], tl[c].y[:0], bs) for c in tl}
+    return tl, te, {c: d.num_samples for c, d in tl.items()}, class_num
+
+
+def _load_files(args, name, spec):
+    """Real files when present: TFF (.npz / .h5), image folders (ImageNet, CINIC-10), Landmarks CSVs."""
+    base = getattr(args, "data_cache_dir", "") or ""
+    bs = args.batch_size
+    try:
+        if name in ("femnist", "fed_emnist", "fed_cifar100", "fed_shakespeare", "stackoverflow_lr",
+                    "stackoverflow_nwp"):
+            from .tff import find_tff_file, load_tff_clients
+            tr, te = find_tff_file(base, name, True), find_tff_file(base, name, False)
+            if tr:
+                train = load_tff_clients(tr, name)
+                test = load_tff_clients(te, name) if te else {}
+                args.client_num_in_total = len(train)
+                return _clients_to_loaded(train, test, bs, spec.num_classes)
+        if name in ("ILSVRC2012", "ILSVRC2012_hdf5", "cinic10") and os.path.isdir(os.path.join(base, "train")):
+            from .image_folder import load_image_folder
+            size = 32 if name == "cinic10" else int(getattr(args, "image_size", 224))
+            xtr, ytr, classes = load_image_folder(os.path.join(base, "train"), size,
+                                                  getattr(args, "max_images_per_class", None))
+            val_dir = next((os.path.join(base, d) for d in ("val", "test", "valid") if
+                            os.path.isdir(os.path.join(base, d))), None)
+            parts = _partition(ytr.numpy(), int(args.client_num_in_total), args.partition_method,
+                               float(args.partition_alpha), len(classes))
+            train = {c: (xtr[torch.as_tensor(v, dtype=torch.long)], ytr[torch.as_tensor(v, dtype=torch.long)])
+                     for c, v in parts.items()}
+            test = {}
+            if val_dir:
+                xte, yte, _ = load_image_folder(val_dir, size, getattr(args, "max_images_per_class", None))
+                for c, v in enumerate(np.array_split(np.arange(len(yte)), int(args.client_num_in_total))):
+                    test[c] = (xte[torch.as_tensor(v, dtype=torch.long)], yte[torch.as_tensor(v, dtype=torch.long)])
+            return _clients_to_loaded(train, test, bs, len(classes))
+        if name in ("gld23k", "gld160k"):
+            from .image_folder import load_landmarks
+            train = load_landmarks(base, name, int(getattr(args, "image_size", 224)), True)
+            test = load_landmarks(base, name, int(getattr(args, "image_size", 224)), False)
+            if train:
+                args.client_num_in_total = len(train)
+                return _clients_to_loaded(train, test, bs, spec.num_classes)
+    except FileNotFoundError:
+        return None
+    return None
+
+
 def load_synthetic_data(args):
     dataset_name = args.dataset
     centralized = int(args.client_num_in_total) == 1 and getattr(args, "training_type", "") != "cross_silo"
@@ -171,6 +221,8 @@ def load_synthetic_data(args):
             te = {c: ClientData(xte[torch.as_tensor(v)], yte[torch.as_tensor(v)], args.batch_size)
                   for c, v in enumerate(te_parts)}
             loaded = (tl, te, nd, spec.num_classes)
+    if loaded is None and not force_syn:
+        loaded = _load_files(args, dataset_name, spec)
     if loaded is None:
         if not force_syn:
             logging.info("dataset %s: no local files under %s → synthetic data of the same shape", dataset_name,
