@@ -48,10 +48,19 @@ class ClientBatchEngine:
             self.m2 = self.layout.alloc_stack(self.C, self.device)
             self.vmax = self.layout.alloc_stack(self.C, self.device) if opt in ("adam", "amsgrad") else None
             self.step_t = torch.zeros(self.C, dtype=torch.float32, device=self.device)
-        self.interp = BatchedInterpreter(model, self.layout, self.C)
+        # client-batched program when the model is client-stackable; otherwise clients run one after
+        # another on the same arenas (transformers, models with data-dependent control flow)
+        try:
+            self.interp = BatchedInterpreter(model, self.layout, self.C)
+            self.sequential = False
+        except UnsupportedForBatching as e:
+            logging.info("virtual-client engine: sequential per-client path (%s)", e)
+            self.interp = None
+            self.sequential = True
+        self._seq_views = None
         self.native = None
         self.native_step = None
-        if self.device.type == "cuda" and os.environ.get("FEDML_AMD_NATIVE_CONV", "1") != "0":
+        if self.device.type == "cuda" and not self.sequential and os.environ.get("FEDML_AMD_NATIVE_CONV", "1") != "0":
             from ...parallel.native_resnet import NativeResNetStep, UnsupportedNative
             try:
                 self.native_step = NativeResNetStep(model, self.layout, self.C, self.device)
@@ -145,8 +154,16 @@ class ClientBatchEngine:
             bc = torch.tensor([max(1, b) for b in b_c], dtype=torch.float32, device=self.device)
             row_scale = mask.to(torch.float32) / bc.view(-1, 1)
             return self.native_step.step(self.params, self.grads, x, y, row_scale, active)
-        out = self.interp.run(self.views, x, training=True, sample_mask=sample_mask, active=active,
-                              dtype=self.compute_dtype)                       # [C, B, K]
+        if not self.sequential:
+            try:
+                out = self.interp.run(self.views, x, training=True, sample_mask=sample_mask, active=active,
+                                      dtype=self.compute_dtype)                   # [C, B, K]
+            except UnsupportedForBatching as e:
+                logging.info("virtual-client engine: switching to the sequential path (%s)", e)
+                self.sequential = True
+                self.interp.deferred.clear()
+        if self.sequential:
+            return self._seq_step_loss(x, y, b_c)
         C, B = out.shape[0], out.shape[1]
         logits = out.reshape(C * B, -1)
         if not logits.is_contiguous():
@@ -162,6 +179,51 @@ class ClientBatchEngine:
         loss.backward()
         self.interp.flush_deferred()
         return loss.detach()
+
+    # ---------------------------------------------------------------- sequential per-client path
+    def _seq_param_views(self):
+        """Per-client leaf views into the arenas: parameters train in place (``.grad`` = grad arena
+        rows); buffers (BN statistics) are handed over as copies and written back after backward
+        (an in-place update of an arena view would bump the version counter every leaf shares)."""
+        if self._seq_views is None:
+            self._seq_views = []
+            for c in range(self.C):
+                d = {}
+                for sl in self.layout.slots:
+                    if sl.trainable:
+                        v = self.params[c, sl.offset:sl.offset + sl.numel].view(sl.shape).detach().requires_grad_(True)
+                        v.grad = self.grads[c, sl.offset:sl.offset + sl.numel].view(sl.shape)
+                        d[sl.key] = v
+                self._seq_views.append(d)
+        return self._seq_views
+
+    def _buffers_of(self, c):
+        out = {}
+        for sl in self.layout.slots:
+            if not sl.trainable:
+                out[sl.key] = self.params[c, sl.offset:sl.offset + sl.numel].view(sl.shape).to(sl.dtype).clone()
+        return out
+
+    def _seq_step_loss(self, x, y, b_c):
+        views = self._seq_param_views()
+        total = torch.zeros((), device=self.device)
+        amp = self.compute_dtype is not None and self.device.type == "cuda"
+        for c, b in enumerate(b_c):
+            if b <= 0:
+                continue
+            bufs = self._buffers_of(c)
+            with torch.autocast("cuda", dtype=self.compute_dtype or torch.bfloat16, enabled=amp):
+                out = torch.func.functional_call(self.model, {**views[c], **bufs}, (x[c, :b],))
+            if isinstance(out, tuple):
+                out = out[-1]
+            loss = torch.nn.functional.cross_entropy(out.float().reshape(b, -1), y[c, :b].reshape(b))
+            loss.backward()
+            with torch.no_grad():
+                for sl in self.layout.slots:
+                    if not sl.trainable:
+                        self.params[c, sl.offset:sl.offset + sl.numel].copy_(bufs[sl.key].reshape(-1))
+            total += loss.detach()
+        return total
 
     def _optimizer_step(self, lr, active, first):
         if self.optimizer == "sgd":
@@ -184,6 +246,47 @@ class ClientBatchEngine:
         return out
 
     @torch.no_grad()
+    def compressed_partial_sum(self, weights: torch.Tensor, global_flat: torch.Tensor, client_ids, residual,
+                               method: str, ratio: float, seed: int, out: Optional[torch.Tensor] = None):
+        """Like ``partial_sum`` but each client's update Δ_c = w_c − w_global travels compressed:
+        block-256 int8 (stochastic rounding) / fp8-e4m3 quantisation, or exact top-k sparsification,
+        all with per-client error feedback (``residual`` [K_total, P], indexed by client id). The
+        server side decompresses straight into the accumulator (fused dequant-axpy / scatter-axpy
+        kernels): Σ_c n_c·(w_global + D(C(Δ_c))). Returns (out, uploaded_bytes)."""
+        if out is None:
+            out = torch.empty(self.P + 1, dtype=torch.float32, device=self.device)
+        acc = out[:self.P]
+        acc.zero_()
+        w_host = weights.to(torch.float32).tolist()
+        delta = torch.empty(self.P, dtype=torch.float32, device=self.device)
+        nbytes = 0
+        k = max(1, int(self.P * ratio))
+        for c, w in enumerate(w_host):
+            if w == 0.0:
+                continue
+            r = residual[int(client_ids[c])]
+            torch.sub(self.params[c], global_flat, out=delta)
+            if method == "int8":
+                q, sc = ops.quantize_int8(delta, residual=r, stochastic=True, seed=seed * 1000003 + int(client_ids[c]))
+                ops.dequantize_int8_axpy(q, sc, w, acc)
+                nbytes += q.numel() + sc.numel() * 4
+            elif method == "fp8":
+                q, sc = ops.quantize_fp8(delta, residual=r)
+                ops.dequantize_fp8_axpy(q, sc, w, acc)
+                nbytes += q.numel() + sc.numel() * 4
+            elif method == "topk":
+                delta.add_(r)
+                idx, val = ops.topk_abs(delta, k, residual=r)
+                ops.scatter_axpy(idx, val, w, acc)
+                nbytes += k * 8
+            else:
+                raise ValueError(f"unknown compression {method}")
+        total = float(sum(w_host))
+        acc.add_(global_flat, alpha=total)
+        out[self.P:].fill_(total)
+        return out, nbytes
+
+    @torch.no_grad()
     def evaluate(self, store, slots, batch_size: int = 256):
         """Per-client accuracy/loss of the current client params on their own data (batched)."""
         C = self.C
@@ -195,7 +298,18 @@ class ClientBatchEngine:
         for lo in range(0, n_max, batch_size):
             idx = order[:, lo:lo + batch_size]
             x, y, mask = store.gather(idx)
-            out = self.interp.run(self.views, x, training=False, dtype=self.compute_dtype).float()
+            if self.sequential:
+                outs = []
+                for c in range(C):
+                    with torch.autocast("cuda", dtype=self.compute_dtype or torch.bfloat16,
+                                        enabled=self.compute_dtype is not None and self.device.type == "cuda"):
+                        o = torch.func.functional_call(self.model, {**{k: v.detach() for k, v in
+                                                                       self._seq_param_views()[c].items()},
+                                                                    **self._buffers_of(c)}, (x[c],))
+                    outs.append((o[-1] if isinstance(o, tuple) else o).float())
+                out = torch.stack(outs)
+            else:
+                out = self.interp.run(self.views, x, training=False, dtype=self.compute_dtype).float()
             pred = out.argmax(-1)
             correct += ((pred == y) & mask).sum(1)
             l = torch.nn.functional.cross_entropy(out.reshape(-1, out.shape[-1]), y.reshape(-1), reduction="none")

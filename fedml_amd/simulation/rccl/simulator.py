@@ -70,6 +70,12 @@ class RCCLSimulator:
         if str(args.federated_optimizer) == "FedOpt":
             self.server_opt = _ServerOptState(args, self.layout.size, self.device)
         self.round_times: List[float] = []
+        # update compression (north-star config: FedOpt + int8/fp8/top-k with error feedback)
+        self.compression = str(getattr(args, "compression", "") or "").lower() or None
+        self.compress_ratio = float(getattr(args, "compression_ratio", 0.01) or 0.01)
+        self.residual = torch.zeros(self.K_total, self.layout.size, dtype=torch.float32, device=self.device) \
+            if self.compression else None
+        self.upload_bytes: List[int] = []
         self.history: Dict[int, dict] = {}
         self.round_idx = 0
 
@@ -101,7 +107,13 @@ class RCCLSimulator:
         with tr.span("round.aggregate"):
             w = torch.where(valid, self.store.counts[slots].to(torch.float32), torch.zeros(self.C, device=self.device))
             self._robust_preaggregate(w)
-            self.engine.partial_sum(w, out=self.partial)
+            if self.compression:
+                ids = list(mine) + [0] * (self.C - len(mine))
+                _, nb = self.engine.compressed_partial_sum(w, self.global_flat, ids, self.residual, self.compression,
+                                                           self.compress_ratio, round_idx, out=self.partial)
+                self.upload_bytes.append(nb)
+            else:
+                self.engine.partial_sum(w, out=self.partial)
             comm.all_reduce_flat(self.partial)
             total = self.partial[self.layout.size:self.layout.size + 1]
             avg = self.partial[:self.layout.size] / total
