@@ -34,7 +34,26 @@ def parse():
     p.add_argument("--dtype", default="bf16")
     p.add_argument("--lr", type=float, default=0.001)
     p.add_argument("--profile-rounds", type=int, default=0)
-    return p.parse_args()
+    p.add_argument("--optimizer", default="FedAvg", help="FedAvg | FedOpt (server Adam)")
+    p.add_argument("--compression", default="", help="'' | int8 | fp8 | topk (client-update compression)")
+    p.add_argument("--compression-ratio", type=float, default=0.01)
+    p.add_argument("--client-optimizer", default="sgd")
+    p.add_argument("--preset", default="", help="resnet18_cifar10_10 | distilbert_fedopt_32 | vit_b16_32 "
+                                                "(other BASELINE.json configs; the default is the headline)")
+    a = p.parse_args()
+    presets = {
+        "resnet18_cifar10_10": dict(model="resnet18", dataset="cifar10", clients=10, samples_per_client=5000,
+                                    batch_size=64, lr=0.001),
+        "distilbert_fedopt_32": dict(model="distilbert", dataset="text_cls", clients=32, samples_per_client=64,
+                                     batch_size=16, lr=5e-5, optimizer="FedOpt", compression="int8",
+                                     client_optimizer="adamw"),
+        "vit_b16_32": dict(model="vit_b16", dataset="ILSVRC2012", clients=32, samples_per_client=32, batch_size=16,
+                           lr=1e-4, client_optimizer="adamw"),
+    }
+    if a.preset:
+        for k, v in presets[a.preset].items():
+            setattr(a, k, v)
+    return a
 
 
 def main():
@@ -57,10 +76,12 @@ def main():
         device = torch.device("cpu")
     spec = get_spec(a.dataset)
     args = Arguments.from_dict({"x": {
-        "training_type": "simulation", "backend": "RCCL", "federated_optimizer": "FedAvg",
+        "training_type": "simulation", "backend": "RCCL", "federated_optimizer": a.optimizer,
+        "server_optimizer": "adam", "server_lr": 1e-3, "compression": a.compression,
+        "compression_ratio": a.compression_ratio,
         "dataset": a.dataset, "model": a.model, "client_num_in_total": a.clients,
         "client_num_per_round": a.clients, "comm_round": a.steps, "epochs": a.epochs,
-        "batch_size": a.batch_size, "client_optimizer": "sgd", "learning_rate": a.lr, "weight_decay": 0.001,
+        "batch_size": a.batch_size, "client_optimizer": a.client_optimizer, "learning_rate": a.lr, "weight_decay": 0.001,
         "frequency_of_the_test": 0, "compute_dtype": a.dtype if use_gpu else "fp32", "random_seed": 0,
     }})
     torch.manual_seed(0)
@@ -90,7 +111,9 @@ def main():
     if rank == 0:
         rounds_per_s = a.steps / elapsed
         out = {
-            "metric": "FL rounds/sec (FedAvg, 100 clients, ResNet-56)",
+            "metric": ("FL rounds/sec (FedAvg, 100 clients, ResNet-56)" if not a.preset else
+                       f"FL rounds/sec ({a.optimizer}, {a.clients} clients, {a.model}"
+                       + (f", {a.compression} updates" if a.compression else "") + ")"),
             "value": round(rounds_per_s, 4),
             "unit": "rounds/s",
             "n_gpus": ws,
