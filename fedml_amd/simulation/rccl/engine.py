@@ -58,6 +58,8 @@ class ClientBatchEngine:
             self.interp = None
             self.sequential = True
         self._seq_views = None
+        self._graphs = {}
+        self.use_graphs = self.device.type == "cuda" and os.environ.get("FEDML_AMD_HIP_GRAPHS", "1") != "0"
         self.native = None
         self.native_step = None
         if self.device.type == "cuda" and not self.sequential and os.environ.get("FEDML_AMD_NATIVE_CONV", "1") != "0":
@@ -139,10 +141,13 @@ class ClientBatchEngine:
                                     cutout=self.aug_cutout).view_as(x)
                 active = torch.tensor(active_list, dtype=torch.float32, device=self.device)
                 sample_mask = None if uniform else mask.t().contiguous()     # [B, C]
-                loss = self._step_loss(x, y, mask, b_c, active, sample_mask, use_native_loss)
+                if self.native_step is not None and sample_mask is None and self.use_graphs:
+                    loss = self._graph_step(x, y, mask, b_c, active, lr, first)
+                else:
+                    loss = self._step_loss(x, y, mask, b_c, active, sample_mask, use_native_loss)
+                    self._optimizer_step(lr, active, first)
                 total_loss += loss.detach()
                 n_steps += 1
-                self._optimizer_step(lr, active, first)
                 first = False
         n_real = max(1, sum(1 for n in counts_h if n > 0))
         self.last_loss = total_loss / max(1, n_steps * n_real)   # device scalar: no host sync here
@@ -179,6 +184,53 @@ class ClientBatchEngine:
         loss.backward()
         self.interp.flush_deferred()
         return loss.detach()
+
+    # ---------------------------------------------------------------- HIP-graph local step
+    def _graph_step(self, x, y, mask, b_c, active, lr, first):
+        """One local step of the native path replayed from a captured HIP graph: grad zeroing, the
+        ~150 conv/BN kernels of forward+backward, the fused CE head and the fused optimizer — one
+        launch instead of hundreds (the launch gaps dominate once each GPU holds only a few
+        clients). Inputs are copied into the graph's static buffers first; the graph is keyed by
+        batch geometry, learning rate and the first-step flag (momentum initialisation)."""
+        key = (tuple(x.shape), tuple(y.shape), float(lr), bool(first))
+        ent = self._graphs.get(key)
+        if ent is None:
+            st = {"x": torch.empty_like(x), "y": torch.empty_like(y),
+                  "rs": torch.empty(mask.shape, dtype=torch.float32, device=self.device),
+                  "act": torch.empty_like(active)}
+            self._fill_static(st, x, y, mask, b_c, active)
+            # warm-up on a side stream (allocations, kernel attributes), then capture
+            s = torch.cuda.Stream(device=self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            params_snapshot = self.params.clone()
+            mom_snapshot = self.mom.clone() if self.mom is not None else None
+            with torch.cuda.stream(s):
+                self.grads.zero_()
+                self.native_step.step(self.params, self.grads, st["x"], st["y"], st["rs"], st["act"])
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+                self.grads.zero_()
+                loss = self.native_step.step(self.params, self.grads, st["x"], st["y"], st["rs"], st["act"])
+                self._optimizer_step(lr, st["act"], first)
+            # the warm-up/capture touched nothing observable except BN running stats: restore
+            with torch.no_grad():
+                self.params.copy_(params_snapshot)
+                if mom_snapshot is not None:
+                    self.mom.copy_(mom_snapshot)
+            ent = self._graphs[key] = (g, st, loss)
+        g, st, loss = ent
+        self._fill_static(st, x, y, mask, b_c, active)
+        g.replay()
+        return loss
+
+    def _fill_static(self, st, x, y, mask, b_c, active):
+        st["x"].copy_(x, non_blocking=True)
+        st["y"].copy_(y, non_blocking=True)
+        bc = torch.tensor([max(1, b) for b in b_c], dtype=torch.float32).pin_memory() \
+            .to(self.device, non_blocking=True)
+        torch.div(mask.to(torch.float32), bc.view(-1, 1), out=st["rs"])
+        st["act"].copy_(active, non_blocking=True)
 
     # ---------------------------------------------------------------- sequential per-client path
     def _seq_param_views(self):
