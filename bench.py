@@ -133,6 +133,7 @@ def main():
             "final_train_loss": round(loss, 4),
         }
         print(json.dumps(out), flush=True)
+    sim.close()
     comm.destroy()
 
 

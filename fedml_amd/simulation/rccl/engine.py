@@ -12,9 +12,11 @@ Clients whose data ran out (heterogeneous partitions) are masked with an
 After local training, ``partial_sum`` emits Σ_c n_c·w_c (+ Σ n_c) for the RCCL
 all-reduce.
 """
+import atexit
 import logging
 import math
 import os
+import weakref
 from typing import List, Optional
 
 import torch
@@ -22,6 +24,18 @@ import torch
 from ... import ops
 from ...core.arena import ParamLayout
 from ...parallel.batched_nn import BatchedInterpreter, UnsupportedForBatching
+
+
+_LIVE_ENGINES = weakref.WeakSet()
+
+
+@atexit.register
+def _close_engines():
+    for e in list(_LIVE_ENGINES):
+        try:
+            e.close()
+        except Exception:
+            pass
 
 
 class ClientBatchEngine:
@@ -59,6 +73,7 @@ class ClientBatchEngine:
             self.sequential = True
         self._seq_views = None
         self._graphs = {}
+        _LIVE_ENGINES.add(self)
         self.use_graphs = self.device.type == "cuda" and os.environ.get("FEDML_AMD_HIP_GRAPHS", "1") != "0"
         self.native = None
         self.native_step = None
@@ -223,6 +238,13 @@ class ClientBatchEngine:
         self._fill_static(st, x, y, mask, b_c, active)
         g.replay()
         return loss
+
+    def close(self):
+        """Drop captured graphs while the HIP runtime is alive (graph destructors at interpreter
+        teardown run after the device context is gone)."""
+        if self._graphs:
+            torch.cuda.synchronize(self.device)
+            self._graphs.clear()
 
     def _fill_static(self, st, x, y, mask, b_c, active):
         st["x"].copy_(x, non_blocking=True)

@@ -135,6 +135,9 @@ class RCCLSimulator:
             ops.gaussian_noise_(self.global_flat, float(self.args.stddev), seed=int(getattr(self.args, "random_seed", 0)),
                                 offset=self.round_idx * self.layout.size, mask=mask)
 
+    def close(self):
+        self.engine.close()
+
     def run(self, rounds: Optional[int] = None):
         n = int(self.args.comm_round) if rounds is None else int(rounds)
         freq = int(getattr(self.args, "frequency_of_the_test", 0) or 0)
