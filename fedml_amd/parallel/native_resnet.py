@@ -137,6 +137,7 @@ class NativeResNetStep:
         self.off = {s.key: s.offset for s in layout.slots}
         self.geom = None
         self._segs = None
+        self._states = {}
         self.use_c3 = os.environ.get("FEDML_AMD_CONV3X3", "1") != "0"
         self.use_c1 = os.environ.get("FEDML_AMD_CONV1X1", "1") != "0"
 
@@ -238,6 +239,22 @@ class NativeResNetStep:
         self.dw_scratch = torch.zeros(C * mx, dtype=torch.float32, device=dev)
         self.geom = (N, H, W)
 
+    # Every geometry keeps its own buffers alive: a captured HIP graph of one batch size must stay
+    # valid while another batch size (the ragged last step of an epoch) is being run.
+    _STATE_ATTRS = ("x_in", "stem_y", "stem_out", "gbuf", "bn_vec", "stats", "stat_views", "pooled", "dw_scratch",
+                    "packed", "packed_ld", "_segs", "_nseg", "final_hw", "geom")
+
+    def _snapshot(self):
+        st = {k: getattr(self, k) for k in self._STATE_ATTRS}
+        st["blocks"] = [(b.ys, b.yd, b.out) for b in self.blocks]
+        return st
+
+    def _restore(self, st):
+        for k in self._STATE_ATTRS:
+            setattr(self, k, st[k])
+        for b, (ys, yd, out) in zip(self.blocks, st["blocks"]):
+            b.ys, b.yd, b.out = ys, yd, out
+
     def _all_bns(self):
         yield self.stem[1]
         for b in self.blocks:
@@ -329,7 +346,11 @@ class NativeResNetStep:
         C, N = x.shape[0], x.shape[1]
         H, W = x.shape[3], x.shape[4]
         if self.geom != (N, H, W):
-            self._setup(N, H, W)
+            if (N, H, W) in self._states:
+                self._restore(self._states[(N, H, W)])
+            else:
+                self._setup(N, H, W)
+                self._states[(N, H, W)] = self._snapshot()
         self.stats.zero_()
         nn_ops.pack_weights(arena, self._segs, self._nseg, self.packed, self.packed_ld, C)
         st_conv, st_bn = self.stem
