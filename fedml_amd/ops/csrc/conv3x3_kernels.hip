@@ -48,26 +48,37 @@ __device__ __forceinline__ uint4 pack8(const float* f) {
 enum { XF_NONE = 0, XF_BNRELU = 1, XF_DY = 2 };
 enum { EPI_FWD = 0, EPI_MASK = 2 };
 
-// Stage one work unit of a client into a zero-haloed LDS tile [ns][R+2][W+2][KC+8]: images
-// [img0, img0+ns), output rows [r0, r0+R) plus one halo row/column on each side, with the operand
-// transform applied. `src`/`src2` already point at the client.
-template <int KC, int XF>
+// Stage one work unit of a client into an LDS tile [ns][TR][TW][KC+8] with the operand transform
+// applied. Tile row tr / column tc hold source pixel (t0 + tr, tc − 1); outside the source image
+// the tile is zero (the convolution's zero padding). UPS: the source is read zero-upsampled by 2
+// (stride-2 backward-data: dy sits at the even positions of the dx grid). `src`/`src2` already
+// point at the client.
+template <int KC, int XF, int UPS>
 __device__ __forceinline__ void stage_tile(uint16_t* tile, const uint16_t* __restrict__ src,
                                            const uint16_t* __restrict__ src2, const float* v0, const float* v1,
-                                           const float* v2, int img0, int ns, int r0, int R, int H, int W) {
+                                           const float* v2, int img0, int ns, int t0, int TR, int TW, int Hs,
+                                           int Ws) {
   constexpr int LD = KC + 8;
   constexpr int CG = KC / 8;
-  const int Rp = R + 2, Wp = W + 2;
-  const int total = ns * Rp * Wp * CG;
+  const int total = ns * TR * TW * CG;
   for (int i = threadIdx.x; i < total; i += 256) {
     const int cg = i % CG;
     const int pix = i / CG;
-    const int im = pix / (Rp * Wp);
-    const int r = pix % (Rp * Wp);
-    const int ih = r0 - 1 + r / Wp, iw = r % Wp - 1;
+    const int im = pix / (TR * TW);
+    const int r = pix % (TR * TW);
+    int t = t0 + r / TW, u = r % TW - 1;
+    bool ok;
+    if (UPS) {
+      ok = t >= 0 && u >= 0 && !(t & 1) && !(u & 1);
+      t >>= 1;
+      u >>= 1;
+      ok = ok && t < Hs && u < Ws;
+    } else {
+      ok = t >= 0 && t < Hs && u >= 0 && u < Ws;
+    }
     uint4 v = make_uint4(0, 0, 0, 0);
-    if (ih >= 0 && ih < H && iw >= 0 && iw < W) {
-      const int64_t off = ((((int64_t)(img0 + im) * H) + ih) * W + iw) * KC + cg * 8;
+    if (ok) {
+      const int64_t off = ((((int64_t)(img0 + im) * Hs) + t) * Ws + u) * KC + cg * 8;
       v = *reinterpret_cast<const uint4*>(src + off);
       if (XF != XF_NONE) {
         float f[8];
@@ -117,14 +128,17 @@ struct Args {
   const float* e_t;
   float* stats;          // [C][NOUT][NS]
   int NS;
-  int N, H, W;
+  int N, H, W;                    // output (iteration) geometry
+  int Hs, Ws;                     // A-operand source geometry (≠ H, W for stride 2)
   int ldk;
   int R, S, units, units_per_wg;  // stage geometry (see unit_geom) and work split
   int nout_total;                 // output channels of the layer (a workgroup computes NOUT of them)
 };
 
 // MTW 16-pixel tiles per wave share every B fragment read.
-template <int KC, int NOUT, int XF, int BWD, int EPI, int MTW>
+// ST = stride: forward stride 2 reads the input at (2·p + tap); backward-data stride 2 reads a
+// zero-upsampled dy tile at the dx resolution (then it is a stride-1 correlation).
+template <int KC, int NOUT, int XF, int BWD, int EPI, int MTW, int ST>
 __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
   constexpr int NT = NOUT / 16;
   constexpr int LD = KC + 8;
@@ -137,7 +151,10 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
   const int wid = threadIdx.x >> 6;
   const int g = lane >> 4;
   const int H = a.H, W = a.W, HW = H * W;
-  const int Wp = W + 2;
+  const int Hs = a.Hs, Ws = a.Ws;
+  constexpr int SP = (!BWD && ST == 2) ? 2 : 1;   // source-pixel step per output pixel
+  constexpr bool UPS = BWD && ST == 2;
+  const int TW = (UPS ? W : Ws) + 2;             // tile width incl. halo
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   uint16_t* wl = reinterpret_cast<uint16_t*>(smem);                        // [NOUT][ldk]
@@ -165,8 +182,8 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
     for (int i = threadIdx.x; i < 4 * NOUT * 3; i += 256) red[i] = 0.f;
   }
 
-  const uint16_t* src = a.src + (int64_t)c * a.N * HW * KC;
-  const uint16_t* src2 = (XF == XF_DY) ? a.src2 + (int64_t)c * a.N * HW * KC : nullptr;
+  const uint16_t* src = a.src + (int64_t)c * a.N * Hs * Ws * KC;
+  const uint16_t* src2 = (XF == XF_DY) ? a.src2 + (int64_t)c * a.N * Hs * Ws * KC : nullptr;
   uint16_t* out = a.out + (int64_t)c * a.N * HW * NO;
 
   float st0[8], st1[8];
@@ -175,6 +192,7 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
   const int my_cg = lane % CG;
 
   const int R = a.R, RW = R * W;
+  const int TR = SP == 2 ? 2 * R + 1 : R + 2;    // tile rows incl. halo
   const int u_lo = blockIdx.x * a.units_per_wg;
   const int u_hi = min(a.units, u_lo + a.units_per_wg);
   for (int u = u_lo; u < u_hi; ++u) {
@@ -182,7 +200,7 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
     unit_geom(u, a.N, H, R, a.S, img0, ns, r0);
     const int64_t pix0 = (int64_t)img0 * HW + (int64_t)r0 * W;  // first output pixel of the unit
     __syncthreads();  // previous unit fully consumed (and, first time, weights/vectors visible)
-    stage_tile<KC, XF>(tile, src, src2, v0, v1, v2, img0, ns, r0, R, H, W);
+    stage_tile<KC, XF, UPS>(tile, src, src2, v0, v1, v2, img0, ns, SP * r0 - 1, TR, TW, Hs, Ws);
     __syncthreads();
     const int P = ns * RW;
     const int ntile = (P + 15) / 16;
@@ -195,7 +213,7 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
         valid[mt] = (t0 + mt) < ntile && p < P;
         const int pp = valid[mt] ? p : 0;
         const int im = pp / RW, r = pp % RW;
-        base[mt] = ((im * (R + 2) + r / W) * Wp + r % W) * LD;
+        base[mt] = ((im * TR + SP * (r / W)) * TW + SP * (r % W)) * LD;
       }
       f32x4 acc[MTW][NT];
 #pragma unroll
@@ -208,7 +226,7 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
         const int tap = k / KC, ci = k % KC;
         const int kh = tap / 3, kw = tap % 3;
         // forward reads x_pad(pr + kh, pc + kw); backward reads dy_pad(pr + 2 − kh, pc + 2 − kw)
-        const int toff = BWD ? ((2 - kh) * Wp + (2 - kw)) * LD + ci : (kh * Wp + kw) * LD + ci;
+        const int toff = BWD ? ((2 - kh) * TW + (2 - kw)) * LD + ci : (kh * TW + kw) * LD + ci;
         const bool kin = k < K;
         bf16x8 af[MTW];
 #pragma unroll
@@ -323,13 +341,14 @@ struct WArgs {
   const float* ps;
   const float* pt;
   float* dw;              // GEMM-layout scratch [C][COUT][9·CIN]
-  int N, H, W;
+  int N, H, W;            // dy (output) geometry
+  int Hs, Ws;             // x (input) geometry
   int R, S, units, units_per_wg;
   int nt_per_z;           // GEMM column tiles (16 wide) per blockIdx.z
 };
 
 // WN waves split the column tiles of this z-slice, WK = 4/WN waves split the pixel K-steps.
-template <int CIN, int COUT, int PRO, int WN, int TPW>
+template <int CIN, int COUT, int PRO, int WN, int TPW, int ST>
 __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WArgs a) {
   constexpr int WK = 4 / WN;
   constexpr int MT = COUT / 16;
@@ -340,7 +359,8 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WArgs a) {
   const int wid = threadIdx.x >> 6;
   const int g = lane >> 4, q = (lane & 15) >> 2, pq = lane & 3;
   const int kgrp = wid / WN, ngrp = wid % WN;
-  const int H = a.H, W = a.W, HW = H * W, Wp = W + 2;
+  const int H = a.H, W = a.W, HW = H * W;
+  const int Hs = a.Hs, Ws = a.Ws, TW = Ws + 2;
   const int nt_lo = blockIdx.z * a.nt_per_z;
   const int nt_hi = min(K / 16, nt_lo + a.nt_per_z);
   const int my_nt0 = nt_lo + ngrp * TPW;  // this wave's column tiles [my_nt0, my_nt0 + TPW) ∩ [.., nt_hi)
@@ -348,7 +368,7 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WArgs a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* vv = reinterpret_cast<float*>(smem);                          // α β γ [COUT], s t [CIN]
   uint16_t* dyL = reinterpret_cast<uint16_t*>(vv + 3 * COUT + 2 * CIN);  // [S·HW][LDD]
-  uint16_t* xt = dyL + (size_t)a.S * a.R * W * LDD;                    // [S][R+2][W+2][LDX]
+  uint16_t* xt = dyL + (size_t)a.S * a.R * W * LDD;                    // [S][TR][TW][LDX]
 
   for (int i = threadIdx.x; i < COUT; i += 256) {
     vv[i] = a.alpha[(int64_t)c * COUT + i];
@@ -369,8 +389,9 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WArgs a) {
 
   const uint16_t* gc = a.g + (int64_t)c * a.N * HW * COUT;
   const uint16_t* yc = a.yv + (int64_t)c * a.N * HW * COUT;
-  const uint16_t* xc = a.x + (int64_t)c * a.N * HW * CIN;
+  const uint16_t* xc = a.x + (int64_t)c * a.N * Hs * Ws * CIN;
   const int R = a.R, RW = R * W;
+  const int TR = ST == 2 ? 2 * R + 1 : R + 2;
   const int u_lo = blockIdx.x * a.units_per_wg;
   const int u_hi = min(a.units, u_lo + a.units_per_wg);
 
@@ -395,8 +416,8 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WArgs a) {
         *reinterpret_cast<uint4*>(dyL + (size_t)p * LDD + cg * 8) = pack8(gf);
       }
     }
-    stage_tile<CIN, PRO ? XF_BNRELU : XF_NONE>(xt, xc, nullptr, vv + 3 * COUT, vv + 3 * COUT + CIN, nullptr, img0,
-                                              ns, r0, R, H, W);
+    stage_tile<CIN, PRO ? XF_BNRELU : XF_NONE, 0>(xt, xc, nullptr, vv + 3 * COUT, vv + 3 * COUT + CIN, nullptr,
+                                                 img0, ns, ST * r0 - 1, TR, TW, Hs, Ws);
     __syncthreads();
     const int KS = ns * RW / 32;  // R·W is a multiple of 32
     for (int ks = kgrp; ks < KS; ks += WK) {
@@ -404,7 +425,7 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WArgs a) {
       // this lane's pixel row of the fragment (8-pixel groups never straddle an image row: W % 8 == 0)
       const int pix = p0 + 8 * g + q;
       const int im = pix / RW, r = pix % RW;
-      const uint16_t* xrow = xt + (size_t)((im * (R + 2) + r / W) * Wp + r % W) * LDX + 4 * pq;
+      const uint16_t* xrow = xt + (size_t)((im * TR + ST * (r / W)) * TW + ST * (r % W)) * LDX + 4 * pq;
       const uint16_t* drow = dyL + (size_t)pix * LDD + 4 * pq;
       bf16x8 af[MT];
 #pragma unroll
@@ -416,7 +437,7 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WArgs a) {
           const int k0 = nt * 16;
           const int tap = k0 / CIN, ci0 = k0 % CIN;
           const int kh = tap / 3, kw = tap % 3;
-          const bf16x8 bf = tr_read(xrow + (kh * Wp + kw) * LDX + ci0, 4 * LDX);
+          const bf16x8 bf = tr_read(xrow + (kh * TW + kw) * LDX + ci0, 4 * ST * LDX);
 #pragma unroll
           for (int m = 0; m < MT; ++m)
             acc[m][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bf, acc[m][t], 0, 0, 0);
@@ -496,83 +517,100 @@ static Plan make_plan(int N, int H, int W, int C, int target_px, int target_wgs)
   return p;
 }
 
-static size_t gemm_smem(int kc, int nout, int ldk, const Plan& p, int W) {
+static size_t gemm_smem(int kc, int nout, int ldk, const Plan& p, int TR, int TW) {
   return (size_t)nout * ldk * 2 + (size_t)3 * kc * 4 + (size_t)4 * nout * 3 * 4 + (size_t)4 * 16 * nout * 2 +
-         (size_t)p.S * (p.R + 2) * (W + 2) * (kc + 8) * 2;
+         (size_t)p.S * TR * TW * (kc + 8) * 2;
 }
 
 // NOUT_WG output channels per workgroup (blockIdx.z slices the layer's NOUT)
-template <int KC, int NOUT_WG, int XF, int BWD, int EPI>
+template <int KC, int NOUT_WG, int XF, int BWD, int EPI, int ST>
 static int launch_gemm(Args a, int nout, int C, int target_px, hipStream_t stream) {
   constexpr int MTW = NOUT_WG >= 64 ? 2 : 4;
   const Plan p = make_plan(a.N, a.H, a.W, C, target_px, 2048);
   a.R = p.R; a.S = p.S; a.units = p.units; a.units_per_wg = p.units_per_wg; a.nout_total = nout;
-  const size_t smem = gemm_smem(KC, NOUT_WG, a.ldk, p, a.W);
+  const bool fwd2 = !BWD && ST == 2;
+  const int TR = fwd2 ? 2 * p.R + 1 : p.R + 2;
+  const int TW = (BWD ? a.W : a.Ws) + 2;
+  const size_t smem = gemm_smem(KC, NOUT_WG, a.ldk, p, TR, TW);
   if (smem > 160 * 1024) return -5;
-  auto kern = conv3x3_gemm_kernel<KC, NOUT_WG, XF, BWD, EPI, MTW>;
+  auto kern = conv3x3_gemm_kernel<KC, NOUT_WG, XF, BWD, EPI, MTW, ST>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   hipLaunchKernelGGL(kern, dim3(p.gx, C, nout / NOUT_WG), dim3(256), smem, stream, a);
   return (int)hipGetLastError();
 }
 
-template <int XF, int BWD, int EPI>
+template <int XF, int BWD, int EPI, int ST>
 static int dispatch_gemm(int kc, int nout, const Args& a, int C, hipStream_t s) {
   if (kc != nout) return -2;
+  constexpr int PX = ST == 2 ? 128 : 256;
   switch (kc) {
-    case 16: return launch_gemm<16, 16, XF, BWD, EPI>(a, nout, C, 256, s);
-    case 32: return launch_gemm<32, 32, XF, BWD, EPI>(a, nout, C, 256, s);
-    case 64: return launch_gemm<64, 32, XF, BWD, EPI>(a, nout, C, 128, s);  // weights split over z
+    case 16: return launch_gemm<16, 16, XF, BWD, EPI, ST>(a, nout, C, PX, s);
+    case 32: return launch_gemm<32, 32, XF, BWD, EPI, ST>(a, nout, C, PX, s);
+    case 64: return launch_gemm<64, 32, XF, BWD, EPI, ST>(a, nout, C, ST == 2 ? 64 : 128, s);  // weights split over z
     default: return -2;
   }
 }
 
 }  // namespace c3
 
-// forward 3×3/s1/p1: y = conv(pro(x)); stats[c][co][2] += (Σy, Σy²). Returns <0 if unsupported.
+// forward 3×3 / pad 1 / stride 1|2: y = conv(pro(x)); stats[c][co][2] += (Σy, Σy²).
+// (H, W) = input resolution. Returns < 0 if unsupported.
 FA_EXPORT int fa_conv3x3_fwd(const uint16_t* x, const uint16_t* wpk, int64_t wpk_ld, const float* pscale,
                              const float* pshift, uint16_t* y, float* stats, int C, int N, int H, int W, int Cin,
-                             int Cout, int ldk, hipStream_t stream) {
-  if (W % 8 != 0) return -3;
+                             int Cout, int ldk, int stride, hipStream_t stream) {
+  if ((stride != 1 && stride != 2) || H % stride || W % stride || (W / stride) % 8 != 0) return -3;
   c3::Args a = {};
   a.src = x; a.wpk = wpk; a.wpk_ld = wpk_ld; a.vec0 = pscale; a.vec1 = pshift; a.out = y; a.stats = stats; a.NS = 2;
-  a.N = N; a.H = H; a.W = W; a.ldk = ldk;
-  if (pscale) return c3::dispatch_gemm<c3::XF_BNRELU, 0, c3::EPI_FWD>(Cin, Cout, a, C, stream);
-  return c3::dispatch_gemm<c3::XF_NONE, 0, c3::EPI_FWD>(Cin, Cout, a, C, stream);
+  a.N = N; a.H = H / stride; a.W = W / stride; a.Hs = H; a.Ws = W; a.ldk = ldk;
+  if (stride == 2) {
+    if (pscale) return c3::dispatch_gemm<c3::XF_BNRELU, 0, c3::EPI_FWD, 2>(Cin, Cout, a, C, stream);
+    return c3::dispatch_gemm<c3::XF_NONE, 0, c3::EPI_FWD, 2>(Cin, Cout, a, C, stream);
+  }
+  if (pscale) return c3::dispatch_gemm<c3::XF_BNRELU, 0, c3::EPI_FWD, 1>(Cin, Cout, a, C, stream);
+  return c3::dispatch_gemm<c3::XF_NONE, 0, c3::EPI_FWD, 1>(Cin, Cout, a, C, stream);
 }
 
-// backward-data 3×3/s1/p1 with the ReLU-mask epilogue (EPI_MASK of the generic kernel):
+// backward-data 3×3 / pad 1 / stride 1|2 with the ReLU-mask epilogue (EPI_MASK of the generic kernel):
 //   g' = convᵀ(α·g + β·y + γ) · [e_x·e_s + e_t > 0];  stats[c][ci][3] += (Σg', Σg'·e_x, ·)
+// (Hx, Wx) = dx resolution; dy is (Hx/stride, Wx/stride).
 FA_EXPORT int fa_conv3x3_bwd_data(const uint16_t* g, const uint16_t* yv, const float* alpha, const float* beta,
                                   const float* gamma, const uint16_t* wpk_b, int64_t wpk_ld, uint16_t* dx,
                                   const uint16_t* e_x, const float* e_s, const float* e_t, float* stats, int C, int N,
-                                  int H, int W, int Cout, int Cin, int ldk2, hipStream_t stream) {
-  if (W % 8 != 0) return -3;
+                                  int Hx, int Wx, int Cout, int Cin, int ldk2, int stride, hipStream_t stream) {
+  if ((stride != 1 && stride != 2) || Hx % stride || Wx % stride || Wx % 8 != 0) return -3;
   c3::Args a = {};
   a.src = g; a.src2 = yv; a.wpk = wpk_b; a.wpk_ld = wpk_ld; a.vec0 = alpha; a.vec1 = beta; a.vec2 = gamma;
   a.out = dx; a.e_x = e_x; a.e_s = e_s; a.e_t = e_t; a.stats = stats; a.NS = 3;
-  a.N = N; a.H = H; a.W = W; a.ldk = ldk2;
-  return c3::dispatch_gemm<c3::XF_DY, 1, c3::EPI_MASK>(Cout, Cin, a, C, stream);
+  a.N = N; a.H = Hx; a.W = Wx; a.Hs = Hx / stride; a.Ws = Wx / stride; a.ldk = ldk2;
+  if (stride == 2) return c3::dispatch_gemm<c3::XF_DY, 1, c3::EPI_MASK, 2>(Cout, Cin, a, C, stream);
+  return c3::dispatch_gemm<c3::XF_DY, 1, c3::EPI_MASK, 1>(Cout, Cin, a, C, stream);
 }
 
-// weight gradient 3×3/s1/p1 into the GEMM-layout scratch `dw` [C][Cout][9·Cin] (zero on entry);
-// the caller runs the scatter pass (fa_wgrad_scatter) into the OIHW arena.
+// weight gradient 3×3 / pad 1 / stride 1|2 into the GEMM-layout scratch `dw` [C][Cout][9·Cin] (zero
+// on entry); the caller runs the scatter pass (fa_wgrad_scatter) into the OIHW arena.
+// (H, W) = input (x) resolution.
 FA_EXPORT int fa_conv3x3_wgrad(const uint16_t* g, const uint16_t* yv, const float* alpha, const float* beta,
                                const float* gamma, const uint16_t* x, const float* ps, const float* pt, float* dw,
-                               int C, int N, int H, int W, int Cin, int Cout, hipStream_t stream) {
-  if (W % 8 != 0 || (H * W) % 32 != 0 || Cin != Cout) return -3;
+                               int C, int N, int H, int W, int Cin, int Cout, int stride, hipStream_t stream) {
+  if ((stride != 1 && stride != 2) || H % stride || W % stride || Cin != Cout) return -3;
+  const int Ho = H / stride, Wo = W / stride;
+  if (Wo % 8 != 0 || (Ho * Wo) % 32 != 0) return -3;
   c3::WArgs a = {};
   a.g = g; a.yv = yv; a.alpha = alpha; a.beta = beta; a.gamma = gamma; a.x = x; a.ps = ps; a.pt = pt; a.dw = dw;
-  a.N = N; a.H = H; a.W = W;
-  const c3::Plan p = c3::make_plan(N, H, W, C, Cin >= 64 ? 128 : 256, 2048);
+  a.N = N; a.H = Ho; a.W = Wo; a.Hs = H; a.Ws = W;
+  const c3::Plan p = c3::make_plan(N, Ho, Wo, C, Cin >= 64 ? (stride == 2 ? 64 : 128) : (stride == 2 ? 128 : 256),
+                                   2048);
   a.R = p.R; a.S = p.S; a.units = p.units; a.units_per_wg = p.units_per_wg;
+  const int TR = stride == 2 ? 2 * p.R + 1 : p.R + 2;
   const int NTK = 9 * Cin / 16;
   const size_t vv = (size_t)(3 * Cout + 2 * Cin) * 4;
-  const size_t smem_base = vv + (size_t)p.S * p.R * W * (Cout + 8) * 2 +
-                           (size_t)p.S * (p.R + 2) * (W + 2) * (Cin + 8) * 2;
-#define W3_LAUNCH(CI, CO, WN, TPW, NZ)                                                                         \
+  const size_t smem_base = vv + (size_t)p.S * p.R * Wo * (Cout + 8) * 2 +
+                           (size_t)p.S * TR * (W + 2) * (Cin + 8) * 2;
+#define W3_LAUNCH(CI, CO, WN, TPW, NZ, ST)                                                                     \
   {                                                                                                            \
     a.nt_per_z = (NTK + (NZ) - 1) / (NZ);                                                                      \
-    auto kern = ps ? c3::conv3x3_wgrad_kernel<CI, CO, 1, WN, TPW> : c3::conv3x3_wgrad_kernel<CI, CO, 0, WN, TPW>; \
+    auto kern = ps ? c3::conv3x3_wgrad_kernel<CI, CO, 1, WN, TPW, ST>                                          \
+                   : c3::conv3x3_wgrad_kernel<CI, CO, 0, WN, TPW, ST>;                                         \
     const size_t red = (size_t)(4 / (WN) - 1) * (WN) * ((CO) / 16) * (TPW) * 256 * 4;                          \
     const size_t smem = smem_base > red + vv ? smem_base : red + vv;                                           \
     if (smem > 160 * 1024) return -5;                                                                          \
@@ -580,11 +618,17 @@ FA_EXPORT int fa_conv3x3_wgrad(const uint16_t* g, const uint16_t* yv, const floa
     hipLaunchKernelGGL(kern, dim3(p.gx, C, NZ), dim3(256), smem, stream, a);                                   \
     return (int)hipGetLastError();                                                                             \
   }
-  switch (Cin) {
-    case 16: W3_LAUNCH(16, 16, 1, 9, 1)    // 9 column tiles, 4 waves split the pixels
-    case 32: W3_LAUNCH(32, 32, 2, 9, 1)    // 18 tiles: 2 column groups × 2 pixel groups
-    case 64: W3_LAUNCH(64, 64, 4, 5, 2)    // 36 tiles: 2 z-slices × 4 column groups
-    default: return -2;
+#define W3_ALL(ST)                                                                                             \
+  switch (Cin) {                                                                                               \
+    case 16: W3_LAUNCH(16, 16, 1, 9, 1, ST)                                                                    \
+    case 32: W3_LAUNCH(32, 32, 2, 9, 1, ST)                                                                    \
+    case 64: W3_LAUNCH(64, 64, 4, 5, 2, ST)                                                                    \
+    default: return -2;                                                                                        \
   }
+  if (stride == 2) {
+    W3_ALL(2)
+  }
+  W3_ALL(1)
+#undef W3_ALL
 #undef W3_LAUNCH
 }

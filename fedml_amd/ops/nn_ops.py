@@ -61,28 +61,36 @@ def conv_wgrad(g, yv, alpha, beta, gamma, x, ps, pt, garena, woff, C, N, H, W, C
 
 # ---- spatially tiled 3×3 / stride-1 / pad-1 path (csrc/conv3x3_kernels.hip) ----
 def conv3x3_supported(cin, cout, k, stride, pad, H, W):
-    return k == 3 and stride == 1 and pad == 1 and cin == cout and cin in (16, 32, 64) and W % 8 == 0 and \
-        (H * W) % 64 == 0
+    """(H, W) = input resolution of the convolution."""
+    if k != 3 or pad != 1 or cin != cout or cin not in (16, 32, 64) or stride not in (1, 2):
+        return False
+    if H % stride or W % stride:
+        return False
+    Ho, Wo = H // stride, W // stride
+    return Wo % 8 == 0 and W % 8 == 0 and (Ho * Wo) % 32 == 0
 
 
-def conv3x3_fwd(x, wpk, wpk_ld, pscale, pshift, y, stats, C, N, H, W, Cin, Cout, ldk):
+def conv3x3_fwd(x, wpk, wpk_ld, pscale, pshift, y, stats, C, N, H, W, Cin, Cout, ldk, stride=1):
     rc = _fn("fa_conv3x3_fwd")(_p(x), _p(wpk), _i64(wpk_ld), _p(pscale), _p(pshift), _p(y), _p(stats), _i(C), _i(N),
-                               _i(H), _i(W), _i(Cin), _i(Cout), _i(ldk), _stream(x))
+                               _i(H), _i(W), _i(Cin), _i(Cout), _i(ldk), _i(stride), _stream(x))
     _check(rc, "fa_conv3x3_fwd")
 
 
 def conv3x3_bwd_data(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, dx, e_x, e_s, e_t, stats, C, N, H, W, Cout, Cin,
-                     ldk2):
+                     ldk2, stride=1):
+    """(H, W) = dx (input) resolution."""
     rc = _fn("fa_conv3x3_bwd_data")(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(wpk_b), _i64(wpk_ld), _p(dx),
                                     _p(e_x), _p(e_s), _p(e_t), _p(stats), _i(C), _i(N), _i(H), _i(W), _i(Cout), _i(Cin),
-                                    _i(ldk2), _stream(g))
+                                    _i(ldk2), _i(stride), _stream(g))
     _check(rc, "fa_conv3x3_bwd_data")
 
 
-def conv3x3_wgrad(g, yv, alpha, beta, gamma, x, ps, pt, garena, woff, C, N, H, W, Cin, Cout, cin_src, dw_scratch):
-    """Weight gradient into the GEMM-layout scratch, then scattered (+=) into the OIHW arena."""
+def conv3x3_wgrad(g, yv, alpha, beta, gamma, x, ps, pt, garena, woff, C, N, H, W, Cin, Cout, cin_src, dw_scratch,
+                  stride=1):
+    """Weight gradient into the GEMM-layout scratch, then scattered (+=) into the OIHW arena.
+    (H, W) = input (x) resolution."""
     rc = _fn("fa_conv3x3_wgrad")(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(x), _p(ps), _p(pt),
-                                 _p(dw_scratch), _i(C), _i(N), _i(H), _i(W), _i(Cin), _i(Cout), _stream(g))
+                                 _p(dw_scratch), _i(C), _i(N), _i(H), _i(W), _i(Cin), _i(Cout), _i(stride), _stream(g))
     _check(rc, "fa_conv3x3_wgrad")
     rc = _fn("fa_wgrad_scatter")(_p(dw_scratch), _p(garena), _i64(garena.stride(0)), _i64(woff), _i(C), _i(Cout),
                                  _i(Cin), _i(9), _i(cin_src), _stream(g))

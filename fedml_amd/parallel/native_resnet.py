@@ -295,7 +295,7 @@ class NativeResNetStep:
         pt = pro_vec[1] if pro_vec is not None else None
         if self._c3(cv):
             nn_ops.conv3x3_wgrad(g, y, vec[4], vec[5], vec[6], x, ps, pt, garena, self.off[cv.key], C, N, cv.H, cv.W,
-                                 cv.cin_pad, cv.cout, cv.cin, self.dw_scratch)
+                                 cv.cin_pad, cv.cout, cv.cin, self.dw_scratch, cv.stride)
             return
         M = N * cv.Ho * cv.Wo
         if self.use_c1 and cv.cin == cv.cin_pad and nn_ops.conv1x1_wgrad_supported(cv.cin, cv.cout, cv.k, cv.stride,
@@ -319,7 +319,7 @@ class NativeResNetStep:
             nn_ops.conv3x3_fwd(x, self.packed.view(-1)[cv.off_f:], self.packed_ld,
                                pro_vec[0] if pro_vec is not None else None,
                                pro_vec[1] if pro_vec is not None else None, y, stats, self.C, N, cv.H, cv.W,
-                               cv.cin_pad, cv.cout, cv.ldk)
+                               cv.cin_pad, cv.cout, cv.ldk, cv.stride)
             return
         nn_ops.conv_fwd(x, self.packed.view(-1)[cv.off_f:], self.packed_ld, pro_vec[0] if pro_vec is not None else None,
                         pro_vec[1] if pro_vec is not None else None, y, stats, self.C, N, cv.H, cv.W, cv.cin_pad,
@@ -434,7 +434,7 @@ class NativeResNetStep:
                     nn_ops.conv3x3_bwd_data(g_j, b.ys[j], v[4], v[5], v[6], self.packed.view(-1)[cv.off_b:],
                                             self.packed_ld, out_g, b.ys[j - 1], pv[0], pv[1],
                                             self.stat_views[b.bns[j - 1].key][1], C, N, cv.H, cv.W, cv.cout,
-                                            cv.cin_pad, cv.ldk2)
+                                            cv.cin_pad, cv.ldk2, cv.stride)
                     self._bn_bwd(b.bns[j - 1], 1, N, cv.H * cv.W, arena, garena)
                     g_j = out_g
                     continue

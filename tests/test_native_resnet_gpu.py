@@ -103,8 +103,9 @@ def test_native_resnet56_engine_round():
     assert losses[-1] < losses[0]   # memorising the same data → loss decreases
 
 
-@pytest.mark.parametrize("ch,hw", [(16, 32), (32, 16), (64, 8), (16, 16)])
-def test_conv3x3_kernels_vs_fp32_reference(ch, hw):
+@pytest.mark.parametrize("ch,hw,stride", [(16, 32, 1), (32, 16, 1), (64, 8, 1), (16, 16, 1), (32, 32, 2),
+                                         (64, 16, 2)])
+def test_conv3x3_kernels_vs_fp32_reference(ch, hw, stride):
     """LDS-tiled 3×3 kernels against torch fp32 convolutions of the same bf16 operands, and against
     the generic implicit-GEMM kernels (forward / backward-data agree with the latter to a bf16 ulp)."""
     from fedml_amd.ops import nn_ops
@@ -125,51 +126,52 @@ def test_conv3x3_kernels_vs_fp32_reference(ch, hw):
     def rel(a, b):
         return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
 
+    ho = hw // stride
     # forward: y = conv(relu(x·s + t)), BN statistics (Σy, Σy²)
-    y3 = torch.zeros(C, N, hw, hw, ch, device=DEV, dtype=bf)
+    y3 = torch.zeros(C, N, ho, ho, ch, device=DEV, dtype=bf)
     st3 = torch.zeros(C, ch, 2, device=DEV)
-    nn_ops.conv3x3_fwd(x, wpk, ch * ldk, s, t, y3, st3, C, N, hw, hw, ch, ch, ldk)
+    nn_ops.conv3x3_fwd(x, wpk, ch * ldk, s, t, y3, st3, C, N, hw, hw, ch, ch, ldk, stride)
     yg = torch.zeros_like(y3)
     stg = torch.zeros_like(st3)
-    nn_ops.conv_fwd(x, wpk, ch * ldk, s, t, yg, stg, C, N, hw, hw, ch, ch, 3, 3, 1, 1, hw, hw, ldk, 1)
+    nn_ops.conv_fwd(x, wpk, ch * ldk, s, t, yg, stg, C, N, hw, hw, ch, ch, 3, 3, stride, 1, ho, ho, ldk, 1)
     torch.cuda.synchronize()
     assert rel(y3, yg) < 5e-3  # same operands; FMA contraction may differ by a bf16 ulp
     for c in range(C):
         xa = torch.relu(x[c].float() * s[c] + t[c]).to(bf).float().permute(0, 3, 1, 2)
-        ref = torch.nn.functional.conv2d(xa, wt[c], padding=1).permute(0, 2, 3, 1)
+        ref = torch.nn.functional.conv2d(xa, wt[c], padding=1, stride=stride).permute(0, 2, 3, 1)
         assert rel(y3[c], ref) < 1e-2
         assert rel(st3[c, :, 0], y3[c].float().sum((0, 1, 2))) < 1e-4
     # backward-data with the ReLU-mask epilogue
-    g = torch.randn(C, N, hw, hw, ch, device=DEV).to(bf)
-    yv = torch.randn(C, N, hw, hw, ch, device=DEV).to(bf)
+    g = torch.randn(C, N, ho, ho, ch, device=DEV).to(bf)
+    yv = torch.randn(C, N, ho, ho, ch, device=DEV).to(bf)
     al, be = torch.rand(C, ch, device=DEV), torch.randn(C, ch, device=DEV) * 0.1
     ga = torch.randn(C, ch, device=DEV) * 0.01
     ex = torch.randn(C, N, hw, hw, ch, device=DEV).to(bf)
-    dx = torch.zeros_like(g)
+    dx = torch.zeros_like(ex)
     st = torch.zeros(C, ch, 3, device=DEV)
-    nn_ops.conv3x3_bwd_data(g, yv, al, be, ga, wpk, ch * ldk, dx, ex, s, t, st, C, N, hw, hw, ch, ch, ldk)
-    dxg = torch.zeros_like(g)
+    nn_ops.conv3x3_bwd_data(g, yv, al, be, ga, wpk, ch * ldk, dx, ex, s, t, st, C, N, hw, hw, ch, ch, ldk, stride)
+    dxg = torch.zeros_like(ex)
     stg = torch.zeros_like(st)
     nn_ops.conv_bwd_data(g, yv, al, be, ga, wpk, ch * ldk, dxg, nn_ops.EPI_MASK, ex, s, t, None, None, None, stg,
-                         C, N, hw, hw, ch, ch, 3, 3, 1, 1, hw, hw, ldk, 1)
+                         C, N, ho, ho, ch, ch, 3, 3, stride, 1, hw, hw, ldk, 1)
     torch.cuda.synchronize()
     assert rel(dx, dxg) < 5e-3
     for c in range(C):
         dy = (al[c] * g[c].float() + be[c] * yv[c].float() + ga[c]).to(bf).float().permute(0, 3, 1, 2)
-        ref = torch.nn.grad.conv2d_input(dy.shape, wt_b[c], dy, padding=1).permute(0, 2, 3, 1)
+        ref = torch.nn.grad.conv2d_input((N, ch, hw, hw), wt_b[c], dy, padding=1, stride=stride).permute(0, 2, 3, 1)
         mask = (ex[c].float() * s[c] + t[c]) > 0
         assert rel(dx[c], ref * mask) < 1e-2
     # weight gradient
     P = ch * ch * 9 + 64
     garena = torch.zeros(C, P, device=DEV)
     scratch = torch.zeros(C * ch * K, device=DEV)
-    nn_ops.conv3x3_wgrad(g, yv, al, be, ga, x, s, t, garena, 16, C, N, hw, hw, ch, ch, ch, scratch)
+    nn_ops.conv3x3_wgrad(g, yv, al, be, ga, x, s, t, garena, 16, C, N, hw, hw, ch, ch, ch, scratch, stride)
     torch.cuda.synchronize()
     assert float(scratch.abs().max()) == 0.0  # scatter pass leaves the scratch zeroed
     for c in range(C):
         dy = (al[c] * g[c].float() + be[c] * yv[c].float() + ga[c]).to(bf).float().permute(0, 3, 1, 2)
         xa = torch.relu(x[c].float() * s[c] + t[c]).to(bf).float().permute(0, 3, 1, 2)
-        ref = torch.nn.grad.conv2d_weight(xa, (ch, ch, 3, 3), dy, padding=1)
+        ref = torch.nn.grad.conv2d_weight(xa, (ch, ch, 3, 3), dy, padding=1, stride=stride)
         assert rel(garena[c, 16:16 + ch * ch * 9], ref.reshape(-1)) < 1e-4
 
 
