@@ -58,17 +58,18 @@ def c_wgrad(g, y, al, be, ga, x, ps, pt, garena, woff, C, N, H, W, Cin, Ho, Wo, 
             C * N * (2 * Ho * Wo * Cout + H * W * Cin) * 2, 2 * C * N * Ho * Wo * Cout * KH * KW * Cin)
 
 
-def c3_fwd(x, wpk, ld, ps, pt, y, st, C, N, H, W, Cin, Cout, ldk):
-    return c_fwd(x, wpk, ld, ps, pt, y, st, C, N, H, W, Cin, Cout, 3, 3, 1, 1, H, W, ldk, 0)
+def c3_fwd(x, wpk, ld, ps, pt, y, st, C, N, H, W, Cin, Cout, ldk, stride=1):
+    return c_fwd(x, wpk, ld, ps, pt, y, st, C, N, H, W, Cin, Cout, 3, 3, stride, 1, H // stride, W // stride, ldk, 0)
 
 
-def c3_bwd(g, y, al, be, ga, wpk, ld, dx, ex, es, et, st, C, N, H, W, Cout, Cin, ldk2):
-    return c_bwd(g, y, al, be, ga, wpk, ld, dx, 2, ex, es, et, None, None, None, st, C, N, H, W, Cout, Cin, 3, 3, 1, 1,
-                 H, W, ldk2, 0)
+def c3_bwd(g, y, al, be, ga, wpk, ld, dx, ex, es, et, st, C, N, H, W, Cout, Cin, ldk2, stride=1):
+    return c_bwd(g, y, al, be, ga, wpk, ld, dx, 2, ex, es, et, None, None, None, st, C, N, H // stride, W // stride,
+                 Cout, Cin, 3, 3, stride, 1, H, W, ldk2, 0)
 
 
-def c3_wgrad(g, y, al, be, ga, x, ps, pt, garena, woff, C, N, H, W, Cin, Cout, cs, scratch):
-    return c_wgrad(g, y, al, be, ga, x, ps, pt, garena, woff, C, N, H, W, Cin, H, W, Cout, 3, 3, 1, 1, 0, cs, scratch)
+def c3_wgrad(g, y, al, be, ga, x, ps, pt, garena, woff, C, N, H, W, Cin, Cout, cs, scratch, stride=1):
+    return c_wgrad(g, y, al, be, ga, x, ps, pt, garena, woff, C, N, H, W, Cin, H // stride, W // stride, Cout, 3, 3,
+                   stride, 1, 0, cs, scratch)
 
 
 def c1_wgrad(g, y, al, be, ga, x, ps, pt, garena, woff, C, M, Cin, Cout, ppw):
