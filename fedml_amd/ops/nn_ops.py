@@ -114,6 +114,36 @@ def conv1x1_wgrad(g, yv, alpha, beta, gamma, x, ps, pt, garena, woff, C, M, Cin,
     _check(rc, "fa_conv1x1_wgrad")
 
 
+_C1F_SHAPES = {(16, 64, 2), (32, 128, 2), (64, 256, 2), (64, 16, 3), (128, 32, 3), (256, 64, 3), (16, 16, 3),
+               (64, 32, 3), (128, 64, 3)}
+
+
+def conv1x1_bwd_fused_supported(cin, cout, k, stride, pad, epi):
+    return k == 1 and stride == 1 and pad == 0 and (cin, cout, epi) in _C1F_SHAPES
+
+
+def conv1x1_bwd_fused_scratch(C, M, Cin, Cout, pix_per_wg):
+    """fp32 elements of the partial-sum scratch :func:`conv1x1_bwd_fused` needs for this shape."""
+    G = -(-M // pix_per_wg)
+    return C * G * (Cout * Cin + 3 * Cin)
+
+
+def conv1x1_bwd_fused(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, ldk2, e_x, e_s, e_t, e_add, e_y1, e_y2, out, stats,
+                      garena, woff, C, M, Cin, Cout, epi, pix_per_wg, part=None):
+    """Data gradient (with the EPI_MASK / EPI_BLOCK epilogue of :func:`conv_bwd_data`) AND weight
+    gradient (+= into the OIHW arena rows) of a 1×1 / stride-1 conv from one pass over g, y, e_x.
+    ``stats`` is [C, Cin, NS] (NS = its last dim). ``part``: optional fp32 scratch of
+    :func:`conv1x1_bwd_fused_scratch` elements → deterministic two-pass reduction, no atomics."""
+    if part is not None and part.numel() < conv1x1_bwd_fused_scratch(C, M, Cin, Cout, pix_per_wg):
+        raise ValueError("conv1x1_bwd_fused: partial-sum scratch too small")
+    rc = _fn("fa_conv1x1_bwd_fused")(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(wpk_b), _i64(wpk_ld),
+                                     _i(ldk2), _p(e_x), _p(e_s), _p(e_t), _p(e_add), _p(e_y1), _p(e_y2), _p(out),
+                                     _p(stats), _i(stats.shape[-1]), _p(garena), _i64(garena.stride(0)), _i64(woff),
+                                     _i(C), _i(M), _i(Cin), _i(Cout), _i(epi), _i(pix_per_wg), _p(part),
+                                     _stream(g))
+    _check(rc, "fa_conv1x1_bwd_fused")
+
+
 def bn_fwd_finalize(stats, C, Ch, n, arena, off_gamma, off_beta, off_rm, off_rv, off_nbt, momentum, eps, active,
                     scale, shift, mean, rstd, update_running=True):
     rc = _fn("fa_bn_fwd_finalize")(_p(stats), _i(C), _i(Ch), _f(n), _p(arena), _i64(arena.stride(0)),

@@ -140,6 +140,7 @@ class NativeResNetStep:
         self._states = {}
         self.use_c3 = os.environ.get("FEDML_AMD_CONV3X3", "1") != "0"
         self.use_c1 = os.environ.get("FEDML_AMD_CONV1X1", "1") != "0"
+        self.use_c1f = os.environ.get("FEDML_AMD_C1_FUSED", "1") != "0"
 
     # ------------------------------------------------------------------ setup
     def _all_convs(self):
@@ -307,6 +308,24 @@ class NativeResNetStep:
                           cv.cin_pad, cv.Ho, cv.Wo, cv.cout, cv.k, cv.k, cv.stride, cv.pad, self._pix_per_wg(M), cv.cin,
                           self.dw_scratch)
 
+    def _c1f(self, cv: ConvSpec, epi):
+        return (self.use_c1f and cv.cin == cv.cin_pad
+                and nn_ops.conv1x1_bwd_fused_supported(cv.cin, cv.cout, cv.k, cv.stride, cv.pad, epi))
+
+    def _c1f_pix_per_wg(self, M):
+        """Measured (scripts/tune_c1f.py, C=100 and C=13): 512 px per workgroup for the 16/32-channel
+        stages; the 64-channel stage (per-workgroup weight tile of 16K fp32) wants ≈200 workgroups."""
+        ppw = int(os.environ.get("FEDML_AMD_C1F_PPW", "0"))
+        if ppw:
+            return ppw
+        if M >= 16384:
+            return 512
+        target = M * self.C // 200
+        p = 256
+        while p < 2048 and 2 * p <= target:
+            p *= 2
+        return p
+
     def _c1_pix_per_wg(self, M):
         ppw = int(os.environ.get("FEDML_AMD_C1_PPW", "0"))
         if ppw:
@@ -430,6 +449,14 @@ class NativeResNetStep:
                 pv = self.bn_vec[b.bns[j - 1].key]
                 M = N * cv.Ho * cv.Wo
                 out_g = free[0] if g_j is not free[0] else free[1]
+                if self._c1f(cv, nn_ops.EPI_MASK):
+                    nn_ops.conv1x1_bwd_fused(g_j, b.ys[j], v[4], v[5], v[6], self.packed.view(-1)[cv.off_b:],
+                                             self.packed_ld, cv.ldk2, b.ys[j - 1], pv[0], pv[1], None, None, None,
+                                             out_g, self.stat_views[b.bns[j - 1].key][1], garena, self.off[cv.key], C,
+                                             M, cv.cin, cv.cout, nn_ops.EPI_MASK, self._c1f_pix_per_wg(M))
+                    self._bn_bwd(b.bns[j - 1], 1, N, cv.H * cv.W, arena, garena)
+                    g_j = out_g
+                    continue
                 self._wgrad(cv, g_j, b.ys[j], v, b.ys[j - 1], pv, garena, N)
                 if self._c3(cv):
                     nn_ops.conv3x3_bwd_data(g_j, b.ys[j], v[4], v[5], v[6], self.packed.view(-1)[cv.off_b:],
@@ -462,7 +489,9 @@ class NativeResNetStep:
             # conv 0: weight grad, then data grad with the block epilogue (→ previous block's g)
             cv0, bn0 = b.convs[0], b.bns[0]
             v = self.bn_vec[bn0.key]
-            self._wgrad(cv0, g_j, b.ys[0], v, b.act_in, None, garena, N)
+            fused0 = self._c1f(cv0, nn_ops.EPI_BLOCK)
+            if not fused0:
+                self._wgrad(cv0, g_j, b.ys[0], v, b.act_in, None, garena, N)
             if prev_block is not None:
                 ey1, ey2 = prev_block.ys[-1], prev_block.yd
                 pstats = self.stat_views[prev_block.bns[-1].key][1]
@@ -473,6 +502,14 @@ class NativeResNetStep:
             # the downsample path has consumed it)
             busy = {id(g_j), id(shortcut)}
             out_buf = next(t for t in bufs if id(t) not in busy)
+            if fused0:
+                M0 = N * cv0.H * cv0.W
+                nn_ops.conv1x1_bwd_fused(g_j, b.ys[0], v[4], v[5], v[6], self.packed.view(-1)[cv0.off_b:],
+                                         self.packed_ld, cv0.ldk2, b.act_in, None, None, shortcut, ey1, ey2, out_buf,
+                                         pstats, garena, self.off[cv0.key], C, M0, cv0.cin, cv0.cout,
+                                         nn_ops.EPI_BLOCK, self._c1f_pix_per_wg(M0))
+                gpre = out_buf
+                continue
             nn_ops.conv_bwd_data(g_j, b.ys[0], v[4], v[5], v[6], self.packed.view(-1)[cv0.off_b:], self.packed_ld,
                                  out_buf, nn_ops.EPI_BLOCK, b.act_in, None, None, shortcut, ey1, ey2, pstats, C, N,
                                  cv0.Ho, cv0.Wo, cv0.cout, cv0.cin_pad, cv0.k, cv0.k, cv0.stride, cv0.pad, cv0.H,

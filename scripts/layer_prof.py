@@ -77,6 +77,12 @@ def c1_wgrad(g, y, al, be, ga, x, ps, pt, garena, woff, C, M, Cin, Cout, ppw):
             2 * C * M * Cout * Cin)
 
 
+def c1_fused(g, y, al, be, ga, wpk, ld, ldk2, ex, es, et, eadd, ey1, ey2, out, st, garena, woff, C, M, Cin, Cout,
+             epi, ppw):
+    extra = 0 if epi == 2 else 2 + (ey2 is not None)
+    return (f"1x1 {Cin}<-{Cout} M{M} epi{epi}", C * M * (2 * Cout + (2 + extra) * Cin) * 2, 4 * C * M * Cout * Cin)
+
+
 def c_block(y, s, t, r, rs, rt, out, C, per, Ch):
     return (f"ch{Ch} n{per // Ch}" + (" ds" if rs is not None else ""), C * per * 2 * (3 if r is not None else 2), 0)
 
@@ -100,6 +106,7 @@ def main():
     _wrap("conv3x3_bwd_data", c3_bwd)
     _wrap("conv3x3_wgrad", c3_wgrad)
     _wrap("conv1x1_wgrad", c1_wgrad)
+    _wrap("conv1x1_bwd_fused", c1_fused)
     for n in ("bn_fwd_finalize", "bn_bwd_finalize", "pack_weights", "avgpool", "head_bwd", "nchw_to_nhwc_pad"):
         _wrap(n, c_other)
     torch.manual_seed(0)

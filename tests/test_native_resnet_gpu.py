@@ -203,6 +203,57 @@ def test_conv1x1_wgrad_vs_fp32_reference(cin, cout, hw, pro):
         assert float((got - ref).norm() / ref.norm()) < 1e-4
 
 
+@pytest.mark.parametrize("cin,cout,epi", [(16, 64, 2), (32, 128, 2), (64, 256, 2), (64, 16, 3), (128, 32, 3),
+                                          (256, 64, 3), (16, 16, 3), (64, 32, 3), (128, 64, 3)])
+@pytest.mark.parametrize("M,ppw", [(8 * 16 * 16, 512), (5 * 7 * 7, 64)])
+@pytest.mark.parametrize("two_pass", [False, True])
+def test_conv1x1_bwd_fused_vs_fp32_reference(cin, cout, epi, M, ppw, two_pass):
+    """Fused 1×1 data+weight gradient vs the fp32 reference of both products and the epilogue."""
+    from fedml_amd.ops import nn_ops
+    torch.manual_seed(2)
+    C, bf = 3, torch.bfloat16
+    rel = lambda a, b: float((a - b).norm() / b.norm().clamp_min(1e-12))
+    g = torch.randn(C, M, cout, device=DEV).to(bf)
+    yv = torch.randn(C, M, cout, device=DEV).to(bf)
+    al, be = torch.rand(C, cout, device=DEV), torch.randn(C, cout, device=DEV) * 0.1
+    ga = torch.randn(C, cout, device=DEV) * 0.01
+    W = (torch.randn(C, cout, cin, device=DEV) / cin ** 0.5).to(bf)
+    ld = (cout + 31) // 32 * 32 + 8
+    wb = torch.zeros(C, cin * ld + 64, device=DEV, dtype=bf)
+    wb[:, :cin * ld].view(C, cin, ld)[:, :, :cout] = W.transpose(1, 2)
+    e_x = torch.randn(C, M, cin, device=DEV).to(bf)
+    s = t = e_add = e_y1 = e_y2 = None
+    if epi == 2:
+        s, t = torch.rand(C, cin, device=DEV) + 0.5, torch.randn(C, cin, device=DEV) * 0.1
+    else:
+        e_add, e_y1, e_y2 = (torch.randn(C, M, cin, device=DEV).to(bf) for _ in range(3))
+    out = torch.empty(C, M, cin, device=DEV, dtype=bf)
+    stats = torch.zeros(C, cin, 3, device=DEV)
+    garena = torch.zeros(C, cin * cout + 48, device=DEV)
+    part = torch.full((nn_ops.conv1x1_bwd_fused_scratch(C, M, cin, cout, ppw),), float("nan"),
+                      device=DEV) if two_pass else None
+    nn_ops.conv1x1_bwd_fused(g, yv, al, be, ga, wb, wb.stride(0), ld, e_x, s, t, e_add, e_y1, e_y2, out, stats,
+                             garena, 16, C, M, cin, cout, epi, ppw, part)
+    torch.cuda.synchronize()
+    for c in range(C):
+        dy = (al[c] * g[c].float() + be[c] * yv[c].float() + ga[c]).to(bf).float()
+        dx = (dy @ W[c].float()).to(bf).float()
+        xr = e_x[c].float()
+        if epi == 2:
+            gp = torch.where(xr * s[c] + t[c] > 0, dx, torch.zeros_like(dx)).to(bf).float()
+            st = torch.stack([gp.sum(0), (gp * xr).sum(0)], -1)
+            act = torch.relu(xr * s[c] + t[c]).to(bf).float()
+        else:
+            gp = torch.where(xr > 0, dx + e_add[c].float(), torch.zeros_like(dx)).to(bf).float()
+            st = torch.stack([gp.sum(0), (gp * e_y1[c].float()).sum(0), (gp * e_y2[c].float()).sum(0)], -1)
+            act = xr
+        assert rel(out[c].float(), gp) < 1e-2
+        assert rel(stats[c, :, :st.shape[-1]], st) < 1e-2
+        ref_dw = dy.t() @ act
+        assert rel(garena[c, 16:16 + cin * cout].view(cout, cin), ref_dw) < 1e-4
+    assert float(garena[:, :16].abs().max()) == 0.0 and float(garena[:, 16 + cin * cout:].abs().max()) == 0.0
+
+
 @pytest.mark.parametrize("momentum", [0.0, 0.9])
 def test_hip_graph_step_matches_eager(momentum):
     """The captured local step (zero grads → forward/backward kernels → fused optimizer) leaves the
