@@ -20,6 +20,12 @@ import time
 os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
 
 
+# Reference SP FedAvg round measured on one MI355X (scripts/reference_sp_baseline.py)
+REF_ROUNDS_PER_S = {"": 0.0835, "resnet18_cifar10_10": 0.254}
+DEFAULT_CLIENTS = {"": 100, "resnet18_cifar10_10": 10}
+DEFAULT_SPC = {"": 500, "resnet18_cifar10_10": 5000}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
