@@ -128,7 +128,9 @@ def main():
             "ms_per_step": round(1000.0 * elapsed / a.steps, 2),
             "higher_is_better": True,
             "scaling": "strong",
-            "vs_baseline": None,
+            "vs_baseline": (round(rounds_per_s / REF_ROUNDS_PER_S[a.preset], 3)
+                            if a.preset in REF_ROUNDS_PER_S and a.samples_per_client == DEFAULT_SPC.get(a.preset)
+                            and a.clients == DEFAULT_CLIENTS.get(a.preset) else None),
             "dtype": a.dtype if use_gpu else "fp32",
             "data": "synthetic (CIFAR-100-shaped, class-conditional), random-init weights",
             "config": {"model": a.model, "dataset": a.dataset, "clients": a.clients,
