@@ -1,0 +1,688 @@
+// Transformer kernels for the client-batched DistilBERT / ViT path:
+//   * fused (residual + dropout +) LayerNorm forward / backward with per-client gamma/beta
+//   * exact-erf GELU forward / backward
+//   * short-sequence attention (S <= 256, head dim 64) forward and backward on
+//     v_mfma_f32_16x16x32_bf16, K/V (or Q/dO) tiles staged in LDS, exact row softmax in
+//     registers, attention-probability dropout from a counter hash (regenerated in backward).
+//
+// Layouts: token-major activations [rows = clients·batch·seq][d] in bf16 (the output of the
+// per-client batched GEMMs), heads interleaved along d (head h = columns 64h..64h+63).
+// MFMA 16x16x32 bf16 operand maps (gfx950): lane l holds A[row l&15][k 8(l>>4)..+7],
+// B[k 8(l>>4)..+7][col l&15]; C/D: col = l&15, row = 4(l>>4) + reg.
+#include "common.h"
+
+typedef __bf16 bf16x8_mf __attribute__((ext_vector_type(8)));
+
+namespace {
+
+__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16;
+  h *= 0x85ebca6bu;
+  h ^= h >> 13;
+  h *= 0xc2b2ae35u;
+  h ^= h >> 16;
+  return h;
+}
+// dropout keep test shared by forward and backward (and mirrored in ops/transformer_ops.py)
+__device__ __forceinline__ bool drop_keep(uint32_t seed, uint32_t a, uint32_t b, uint32_t thr) {
+  return fmix32(fmix32(a ^ seed) + b * 0x9E3779B1u) >= thr;
+}
+
+__device__ __forceinline__ void unpack8(const uint4 u, float* f) {
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  uint32_t w[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = (uint32_t)f32_to_bf16(f[2 * i]) | ((uint32_t)f32_to_bf16(f[2 * i + 1]) << 16);
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// ------------------------------------------------------------------------------------------
+// LayerNorm forward: x = bf16(res + dropout(h)) (res/dropout optional), y = LN(x)*g + b.
+// One wave per row, NV chunks of 8 columns per lane (d <= NV*512, d % 8 == 0).
+// ------------------------------------------------------------------------------------------
+template <int NV>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const uint16_t* __restrict__ h, const uint16_t* __restrict__ res,
+                                                     int R, int d, int rows_per_client, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, float eps, uint32_t thr,
+                                                     float dscale, uint32_t seed, uint16_t* __restrict__ y,
+                                                     uint16_t* __restrict__ xsum, float* __restrict__ mean_out,
+                                                     float* __restrict__ rstd_out) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= R) return;
+  const int c = row / rows_per_client;
+  float x[NV][8];
+  float s = 0.f;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int col = (v * 64 + lane) * 8;
+    if (col < d) {
+      unpack8(*(const uint4*)(h + (size_t)row * d + col), x[v]);
+      if (thr) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[v][j] = drop_keep(seed, (uint32_t)row, (uint32_t)(col + j), thr) ? x[v][j] * dscale : 0.f;
+      }
+      if (res) {
+        float r8[8];
+        unpack8(*(const uint4*)(res + (size_t)row * d + col), r8);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x[v][j] += r8[j];
+      }
+      if (res || thr) {  // the sum is materialised in bf16 (as a bf16 torch graph would): round first
+        const uint4 p = pack8(x[v]);
+        unpack8(p, x[v]);
+        if (xsum) *(uint4*)(xsum + (size_t)row * d + col) = p;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += x[v][j];
+    } else {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[v][j] = 0.f;
+    }
+  }
+  const float mean = wave_sum(s) / (float)d;
+  float q = 0.f;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int col = (v * 64 + lane) * 8;
+    if (col < d) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float t = x[v][j] - mean;
+        q += t * t;
+      }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(q) / (float)d + eps);
+  const float* g = gamma + (size_t)c * d;
+  const float* b = beta + (size_t)c * d;
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int col = (v * 64 + lane) * 8;
+    if (col < d) {
+      float o[8];
+      const float4 g0 = *(const float4*)(g + col), g1 = *(const float4*)(g + col + 4);
+      const float4 b0 = *(const float4*)(b + col), b1 = *(const float4*)(b + col + 4);
+      const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+      const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = (x[v][j] - mean) * rstd * gg[j] + bb[j];
+      *(uint4*)(y + (size_t)row * d + col) = pack8(o);
+    }
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// LayerNorm backward. grid (blocks_per_client, C); each wave walks rows of one client and keeps
+// the d-wide dgamma/dbeta partial sums in registers; the 4 waves combine in LDS and one fp32
+// atomic per column and block lands in dgamma/dbeta [C, d].
+template <int NV>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x,
+                                                     const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                     int rows_per_client, int d, const float* __restrict__ gamma,
+                                                     uint16_t* __restrict__ dx, uint16_t* __restrict__ dh,
+                                                     uint32_t thr, float dscale, uint32_t seed,
+                                                     float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  extern __shared__ float red[];  // [4][2][d]
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int c = blockIdx.y;
+  const float* g = gamma + (size_t)c * d;
+  float ag[NV][8], ab[NV][8];
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ag[v][j] = ab[v][j] = 0.f;
+  for (int r = blockIdx.x * 4 + wid; r < rows_per_client; r += gridDim.x * 4) {
+    const size_t row = (size_t)c * rows_per_client + r;
+    const float mu = mean[row], rs = rstd[row];
+    float xh[NV][8], gy[NV][8], gd[NV][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int col = (v * 64 + lane) * 8;
+      if (col < d) {
+        float xv[8];
+        unpack8(*(const uint4*)(x + row * d + col), xv);
+        unpack8(*(const uint4*)(dy + row * d + col), gy[v]);
+        const float4 g0 = *(const float4*)(g + col), g1 = *(const float4*)(g + col + 4);
+        const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          xh[v][j] = (xv[j] - mu) * rs;
+          gd[v][j] = gy[v][j] * gg[j];
+          s1 += gd[v][j];
+          s2 += gd[v][j] * xh[v][j];
+          ag[v][j] += gy[v][j] * xh[v][j];
+          ab[v][j] += gy[v][j];
+        }
+      }
+    }
+    s1 = wave_sum(s1) / (float)d;
+    s2 = wave_sum(s2) / (float)d;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int col = (v * 64 + lane) * 8;
+      if (col < d) {
+        float o[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = rs * (gd[v][j] - s1 - xh[v][j] * s2);
+        if (dx) *(uint4*)(dx + row * d + col) = pack8(o);
+        if (dh) {
+          if (thr) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+              o[j] = drop_keep(seed, (uint32_t)row, (uint32_t)(col + j), thr) ? o[j] * dscale : 0.f;
+          }
+          *(uint4*)(dh + row * d + col) = pack8(o);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int col = (v * 64 + lane) * 8;
+    if (col < d) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        red[(wid * 2 + 0) * d + col + j] = ag[v][j];
+        red[(wid * 2 + 1) * d + col + j] = ab[v][j];
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < d; i += blockDim.x) {
+    float sg = 0.f, sb = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      sg += red[(w * 2 + 0) * d + i];
+      sb += red[(w * 2 + 1) * d + i];
+    }
+    atomicAdd(dgamma + (size_t)c * d + i, sg);
+    atomicAdd(dbeta + (size_t)c * d + i, sb);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// GELU (erf form, as torch.nn.functional.gelu's default), 8 bf16 per thread
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void gelu_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y,
+                                                       int64_t n8) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    float v[8];
+    unpack8(*(const uint4*)(x + i * 8), v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = 0.5f * v[j] * (1.f + erff(v[j] * 0.70710678118654752f));
+    *(uint4*)(y + i * 8) = pack8(v);
+  }
+}
+
+__global__ __launch_bounds__(256) void gelu_bwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ gy,
+                                                       uint16_t* __restrict__ gx, int64_t n8) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+    float v[8], g[8];
+    unpack8(*(const uint4*)(x + i * 8), v);
+    unpack8(*(const uint4*)(gy + i * 8), g);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float cdf = 0.5f * (1.f + erff(v[j] * 0.70710678118654752f));
+      const float pdf = 0.3989422804014327f * __expf(-0.5f * v[j] * v[j]);
+      g[j] = g[j] * (cdf + v[j] * pdf);
+    }
+    *(uint4*)(gx + i * 8) = pack8(g);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Attention. q/k/v/o: token-major bf16 with row strides ld*, head h at column 64h.
+// lse2: [CB, H, S] fp32, log2-domain log-sum-exp of the scaled scores (+inf for empty rows).
+// ------------------------------------------------------------------------------------------
+constexpr float kLog2e = 1.4426950408889634f;
+constexpr int KST = 72;  // LDS row stride (bf16) of [rows][64] tiles: 144 B, 16-B aligned
+
+__device__ __forceinline__ bf16x8_mf lds8(const uint16_t* p) { return __builtin_bit_cast(bf16x8_mf, *(const uint4*)p); }
+__device__ __forceinline__ bf16x8_mf g8(const uint16_t* p) { return __builtin_bit_cast(bf16x8_mf, *(const uint4*)p); }
+__device__ __forceinline__ bf16x8_mf zero8() { return __builtin_bit_cast(bf16x8_mf, make_uint4(0, 0, 0, 0)); }
+
+// stage rows [r0, r0+nrows) of one head's 64 columns into LDS, row-major [nrows][KST]
+__device__ __forceinline__ void stage_rows(uint16_t* dst, const uint16_t* src, int ld, int r0, int nrows, int S) {
+  for (int i = threadIdx.x; i < nrows * 8; i += blockDim.x) {
+    const int r = i >> 3, ch = i & 7;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r0 + r < S) v = *(const uint4*)(src + (size_t)(r0 + r) * ld + ch * 8);
+    *(uint4*)(dst + r * KST + ch * 8) = v;
+  }
+}
+// stage the same rows transposed: dst[dim][row] with row stride tst
+__device__ __forceinline__ void stage_rows_t(uint16_t* dst, int tst, const uint16_t* src, int ld, int r0, int nrows,
+                                             int S) {
+  for (int i = threadIdx.x; i < nrows * 8; i += blockDim.x) {
+    const int r = i >> 3, ch = i & 7;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r0 + r < S) v = *(const uint4*)(src + (size_t)(r0 + r) * ld + ch * 8);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      dst[(ch * 8 + 2 * j) * tst + r] = (uint16_t)(w[j] & 0xffff);
+      dst[(ch * 8 + 2 * j + 1) * tst + r] = (uint16_t)(w[j] >> 16);
+    }
+  }
+}
+
+// Forward: grid (ceil(S/64), H, CB), 4 waves, wave w owns query rows 64·bx + 16w + [0,16).
+// Whole key range in LDS (SP = padded S), exact softmax over the row in registers.
+template <int SP>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restrict__ q, int ldq,
+                                                       const uint16_t* __restrict__ k, int ldk,
+                                                       const uint16_t* __restrict__ v, int ldv,
+                                                       uint16_t* __restrict__ o, int ldo,
+                                                       const uint8_t* __restrict__ kmask, float* __restrict__ lse2,
+                                                       int S, int H, float scale, uint32_t thr, float dscale,
+                                                       uint32_t seed) {
+  constexpr int NB = SP / 16;
+  constexpr int VST = SP + 8;
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[SP * KST];
+  __shared__ __attribute__((aligned(16))) uint16_t Vt[64 * VST];
+  __shared__ __attribute__((aligned(16))) uint16_t Ps[4 * 16 * VST];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int h = blockIdx.y, cb = blockIdx.z;
+  const size_t tok0 = (size_t)cb * S;
+  stage_rows(Ks, k + tok0 * ldk + h * 64, ldk, 0, SP, S);
+  stage_rows_t(Vt, VST, v + tok0 * ldv + h * 64, ldv, 0, SP, S);
+  const int qr = blockIdx.x * 64 + w * 16 + (lane & 15);  // A-operand row of this lane
+  bf16x8_mf qf[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+    qf[t] = qr < S ? g8(q + (tok0 + qr) * ldq + h * 64 + 32 * t + 8 * (lane >> 4)) : zero8();
+  __syncthreads();
+  const float c2 = scale * kLog2e;
+  f32x4 sc[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[t], lds8(Ks + (nb * 16 + (lane & 15)) * KST + 32 * t + 8 * (lane >> 4)),
+                                                     acc, 0, 0, 0);
+    const int key = nb * 16 + (lane & 15);
+    const bool valid = key < S && (kmask == nullptr || kmask[tok0 + key] != 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) acc[r] = valid ? acc[r] * c2 : -INFINITY;
+    sc[nb] = acc;
+  }
+  float m[4], l[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float mx = -INFINITY;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) mx = fmaxf(mx, sc[nb][r]);
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+    m[r] = mx;
+    l[r] = 0.f;
+  }
+  const int qbase = blockIdx.x * 64 + w * 16 + 4 * (lane >> 4);  // C-layout query row of reg 0
+  const uint32_t bh = (uint32_t)(cb * H + h);
+  uint16_t* P = Ps + w * 16 * VST;
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    const int key = nb * 16 + (lane & 15);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float p = m[r] == -INFINITY ? 0.f : exp2f(sc[nb][r] - m[r]);
+      l[r] += p;
+      if (thr) p = drop_keep(seed, bh * 65536u + (uint32_t)(qbase + r), (uint32_t)key, thr) ? p * dscale : 0.f;
+      P[(4 * (lane >> 4) + r) * VST + key] = f32_to_bf16(p);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) l[r] += __shfl_xor(l[r], off, 64);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int db = 0; db < 4; ++db) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int kt = 0; kt < SP / 32; ++kt)
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(P + (lane & 15) * VST + kt * 32 + 8 * (lane >> 4)),
+                                                     lds8(Vt + (db * 16 + (lane & 15)) * VST + kt * 32 + 8 * (lane >> 4)),
+                                                     acc, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int qrow = qbase + r;
+      if (qrow < S) {
+        const float val = l[r] > 0.f ? acc[r] / l[r] : 0.f;
+        o[(tok0 + qrow) * ldo + h * 64 + db * 16 + (lane & 15)] = f32_to_bf16(val);
+      }
+    }
+  }
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int qrow = qbase + r;
+      if (qrow < S) lse2[((size_t)cb * H + h) * S + qrow] = l[r] > 0.f ? m[r] + log2f(l[r]) : INFINITY;
+    }
+  }
+}
+
+// D[cb,h,q] = Σ_dim dO·O  (one thread per (token, head))
+__global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const uint16_t* __restrict__ o, int ldo,
+                                                            const uint16_t* __restrict__ dout, int lddo,
+                                                            float* __restrict__ D, int CBS, int S, int H) {
+  const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (i >= (int64_t)CBS * H) return;
+  const int h = (int)(i % H);
+  const int64_t tok = i / H;
+  float s = 0.f;
+#pragma unroll
+  for (int ch = 0; ch < 8; ++ch) {
+    float a[8], b[8];
+    unpack8(*(const uint4*)(o + tok * ldo + h * 64 + ch * 8), a);
+    unpack8(*(const uint4*)(dout + tok * lddo + h * 64 + ch * 8), b);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += a[j] * b[j];
+  }
+  const int64_t cb = tok / S, qq = tok % S;
+  D[(cb * H + h) * S + qq] = s;
+}
+
+// dQ: grid (ceil(S/64), H, CB); wave w owns 16 query rows, loops over key chunks of 64.
+__global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const uint16_t* __restrict__ q, int ldq,
+                                                          const uint16_t* __restrict__ k, int ldk,
+                                                          const uint16_t* __restrict__ v, int ldv,
+                                                          const uint16_t* __restrict__ dout, int lddo,
+                                                          const uint8_t* __restrict__ kmask,
+                                                          const float* __restrict__ lse2, const float* __restrict__ D,
+                                                          uint16_t* __restrict__ dq, int lddq, int S, int H,
+                                                          float scale, uint32_t thr, float dscale, uint32_t seed) {
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[64 * KST];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[64 * KST];
+  __shared__ __attribute__((aligned(16))) uint16_t Kt[64 * KST];
+  __shared__ __attribute__((aligned(16))) uint16_t dSs[4 * 16 * KST];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int h = blockIdx.y, cb = blockIdx.z;
+  const size_t tok0 = (size_t)cb * S;
+  const size_t bhS = ((size_t)cb * H + h) * S;
+  const int qr = blockIdx.x * 64 + w * 16 + (lane & 15);
+  bf16x8_mf qf[2], df[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    qf[t] = qr < S ? g8(q + (tok0 + qr) * ldq + h * 64 + 32 * t + 8 * (lane >> 4)) : zero8();
+    df[t] = qr < S ? g8(dout + (tok0 + qr) * lddo + h * 64 + 32 * t + 8 * (lane >> 4)) : zero8();
+  }
+  const int qbase = blockIdx.x * 64 + w * 16 + 4 * (lane >> 4);
+  float L[4], Dr[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int qq = qbase + r;
+    L[r] = qq < S ? lse2[bhS + qq] : INFINITY;
+    Dr[r] = qq < S ? D[bhS + qq] : 0.f;
+  }
+  const float c2 = scale * kLog2e;
+  const uint32_t bh = (uint32_t)(cb * H + h);
+  uint16_t* dS = dSs + w * 16 * KST;
+  f32x4 acc[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) acc[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < S; k0 += 64) {
+    __syncthreads();
+    stage_rows(Ks, k + tok0 * ldk + h * 64, ldk, k0, 64, S);
+    stage_rows(Vs, v + tok0 * ldv + h * 64, ldv, k0, 64, S);
+    stage_rows_t(Kt, KST, k + tok0 * ldk + h * 64, ldk, k0, 64, S);
+    __syncthreads();
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+      f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int off = (nb * 16 + (lane & 15)) * KST + 32 * t + 8 * (lane >> 4);
+        s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[t], lds8(Ks + off), s, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(df[t], lds8(Vs + off), dp, 0, 0, 0);
+      }
+      const int key = k0 + nb * 16 + (lane & 15);
+      const bool valid = key < S && (kmask == nullptr || kmask[tok0 + key] != 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p = valid ? exp2f(s[r] * c2 - L[r]) : 0.f;
+        float g = dp[r];
+        if (thr) g = drop_keep(seed, bh * 65536u + (uint32_t)(qbase + r), (uint32_t)key, thr) ? g * dscale : 0.f;
+        dS[(4 * (lane >> 4) + r) * KST + nb * 16 + (lane & 15)] = f32_to_bf16(p * (g - Dr[r]));
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+        acc[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(dS + (lane & 15) * KST + kt * 32 + 8 * (lane >> 4)),
+                                                          lds8(Kt + (db * 16 + (lane & 15)) * KST + kt * 32 + 8 * (lane >> 4)),
+                                                          acc[db], 0, 0, 0);
+  }
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int qq = qbase + r;
+      if (qq < S) dq[(tok0 + qq) * lddq + h * 64 + db * 16 + (lane & 15)] = f32_to_bf16(acc[db][r] * scale);
+    }
+}
+
+// dK, dV: grid (ceil(S/64), H, CB); wave w owns 16 keys, loops over query chunks of 64.
+__global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const uint16_t* __restrict__ q, int ldq,
+                                                           const uint16_t* __restrict__ k, int ldk,
+                                                           const uint16_t* __restrict__ v, int ldv,
+                                                           const uint16_t* __restrict__ dout, int lddo,
+                                                           const uint8_t* __restrict__ kmask,
+                                                           const float* __restrict__ lse2, const float* __restrict__ D,
+                                                           uint16_t* __restrict__ dk, int lddk,
+                                                           uint16_t* __restrict__ dv, int lddv, int S, int H,
+                                                           float scale, uint32_t thr, float dscale, uint32_t seed) {
+  __shared__ __attribute__((aligned(16))) uint16_t Qs[64 * KST];
+  __shared__ __attribute__((aligned(16))) uint16_t dOs[64 * KST];
+  __shared__ __attribute__((aligned(16))) uint16_t Qt[64 * KST];
+  __shared__ __attribute__((aligned(16))) uint16_t dOt[64 * KST];
+  __shared__ __attribute__((aligned(16))) uint16_t Pst[4 * 16 * KST];
+  __shared__ __attribute__((aligned(16))) uint16_t dSt[4 * 16 * KST];
+  __shared__ float Ls[64], Dsh[64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int h = blockIdx.y, cb = blockIdx.z;
+  const size_t tok0 = (size_t)cb * S;
+  const size_t bhS = ((size_t)cb * H + h) * S;
+  const int kr = blockIdx.x * 64 + w * 16 + (lane & 15);
+  bf16x8_mf kf[2], vf[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    kf[t] = kr < S ? g8(k + (tok0 + kr) * ldk + h * 64 + 32 * t + 8 * (lane >> 4)) : zero8();
+    vf[t] = kr < S ? g8(v + (tok0 + kr) * ldv + h * 64 + 32 * t + 8 * (lane >> 4)) : zero8();
+  }
+  const int kbase = blockIdx.x * 64 + w * 16 + 4 * (lane >> 4);  // C-layout key of reg 0
+  bool kvalid[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int kk = kbase + r;
+    kvalid[r] = kk < S && (kmask == nullptr || kmask[tok0 + kk] != 0);
+  }
+  const float c2 = scale * kLog2e;
+  const uint32_t bh = (uint32_t)(cb * H + h);
+  uint16_t* Pw = Pst + w * 16 * KST;
+  uint16_t* dSw = dSt + w * 16 * KST;
+  f32x4 adk[4], adv[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) adk[db] = adv[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int q0 = 0; q0 < S; q0 += 64) {
+    __syncthreads();
+    stage_rows(Qs, q + tok0 * ldq + h * 64, ldq, q0, 64, S);
+    stage_rows(dOs, dout + tok0 * lddo + h * 64, lddo, q0, 64, S);
+    stage_rows_t(Qt, KST, q + tok0 * ldq + h * 64, ldq, q0, 64, S);
+    stage_rows_t(dOt, KST, dout + tok0 * lddo + h * 64, lddo, q0, 64, S);
+    if (threadIdx.x < 64) {
+      const int qq = q0 + threadIdx.x;
+      Ls[threadIdx.x] = qq < S ? lse2[bhS + qq] : INFINITY;
+      Dsh[threadIdx.x] = qq < S ? D[bhS + qq] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int nb = 0; nb < 4; ++nb) {
+      f32x4 st = {0.f, 0.f, 0.f, 0.f}, dpt = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int off = (nb * 16 + (lane & 15)) * KST + 32 * t + 8 * (lane >> 4);
+        st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[t], lds8(Qs + off), st, 0, 0, 0);
+        dpt = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[t], lds8(dOs + off), dpt, 0, 0, 0);
+      }
+      const int ql = nb * 16 + (lane & 15);
+      const int qq = q0 + ql;
+      const float Lq = Ls[ql], Dq = Dsh[ql];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const bool valid = kvalid[r] && qq < S;
+        const float p = valid ? exp2f(st[r] * c2 - Lq) : 0.f;
+        float pd = p, g = dpt[r];
+        if (thr) {
+          const bool kp = drop_keep(seed, bh * 65536u + (uint32_t)qq, (uint32_t)(kbase + r), thr);
+          pd = kp ? p * dscale : 0.f;
+          g = kp ? g * dscale : 0.f;
+        }
+        Pw[(4 * (lane >> 4) + r) * KST + ql] = f32_to_bf16(pd);
+        dSw[(4 * (lane >> 4) + r) * KST + ql] = f32_to_bf16(p * (g - Dq));
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int db = 0; db < 4; ++db)
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        const int ao = (lane & 15) * KST + kt * 32 + 8 * (lane >> 4);
+        const int bo = (db * 16 + (lane & 15)) * KST + kt * 32 + 8 * (lane >> 4);
+        adv[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(Pw + ao), lds8(dOt + bo), adv[db], 0, 0, 0);
+        adk[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(dSw + ao), lds8(Qt + bo), adk[db], 0, 0, 0);
+      }
+  }
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int kk = kbase + r;
+      if (kk < S) {
+        dk[(tok0 + kk) * lddk + h * 64 + db * 16 + (lane & 15)] = f32_to_bf16(adk[db][r] * scale);
+        dv[(tok0 + kk) * lddv + h * 64 + db * 16 + (lane & 15)] = f32_to_bf16(adv[db][r]);
+      }
+    }
+}
+
+template <int NV>
+int launch_ln_fwd(const uint16_t* h, const uint16_t* res, int R, int d, int rpc, const float* g, const float* b,
+                  float eps, uint32_t thr, float dscale, uint32_t seed, uint16_t* y, uint16_t* xsum, float* mean,
+                  float* rstd, hipStream_t st) {
+  hipLaunchKernelGGL(ln_fwd_kernel<NV>, dim3((R + 3) / 4), dim3(256), 0, st, h, res, R, d, rpc, g, b, eps, thr,
+                     dscale, seed, y, xsum, mean, rstd);
+  return (int)hipGetLastError();
+}
+template <int NV>
+int launch_ln_bwd(const uint16_t* dy, const uint16_t* x, const float* mean, const float* rstd, int C, int rpc, int d,
+                  const float* g, uint16_t* dx, uint16_t* dh, uint32_t thr, float dscale, uint32_t seed, float* dg,
+                  float* db, hipStream_t st) {
+  int bpc = (rpc + 31) / 32;  // ≥8 rows per wave
+  if (bpc < 1) bpc = 1;
+  if (bpc > 1024) bpc = 1024;
+  hipLaunchKernelGGL(ln_bwd_kernel<NV>, dim3(bpc, C), dim3(256), 8 * d * sizeof(float), st, dy, x, mean, rstd, rpc,
+                     d, g, dx, dh, thr, dscale, seed, dg, db);
+  return (int)hipGetLastError();
+}
+
+template <int SP>
+int launch_attn_fwd(const uint16_t* q, int ldq, const uint16_t* k, int ldk, const uint16_t* v, int ldv, uint16_t* o,
+                    int ldo, const uint8_t* kmask, float* lse2, int CB, int S, int H, float scale, uint32_t thr,
+                    float dscale, uint32_t seed, hipStream_t st) {
+  hipLaunchKernelGGL(attn_fwd_kernel<SP>, dim3((S + 63) / 64, H, CB), dim3(256), 0, st, q, ldq, k, ldk, v, ldv, o,
+                     ldo, kmask, lse2, S, H, scale, thr, dscale, seed);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+FA_EXPORT int fa_ln_fwd(const void* h, const void* res, int R, int d, int rows_per_client, const float* gamma,
+                        const float* beta, float eps, uint32_t thr, float dscale, uint32_t seed, void* y, void* xsum,
+                        float* mean, float* rstd, hipStream_t stream) {
+  if (d % 8 != 0 || d > 2048) return (int)hipErrorInvalidValue;
+  auto H = (const uint16_t*)h;
+  auto Rs = (const uint16_t*)res;
+  auto Y = (uint16_t*)y;
+  auto X = (uint16_t*)xsum;
+  if (d <= 512) return launch_ln_fwd<1>(H, Rs, R, d, rows_per_client, gamma, beta, eps, thr, dscale, seed, Y, X, mean, rstd, stream);
+  if (d <= 1024) return launch_ln_fwd<2>(H, Rs, R, d, rows_per_client, gamma, beta, eps, thr, dscale, seed, Y, X, mean, rstd, stream);
+  return launch_ln_fwd<4>(H, Rs, R, d, rows_per_client, gamma, beta, eps, thr, dscale, seed, Y, X, mean, rstd, stream);
+}
+
+FA_EXPORT int fa_ln_bwd(const void* dy, const void* x, const float* mean, const float* rstd, int C,
+                        int rows_per_client, int d, const float* gamma, void* dx, void* dh, uint32_t thr, float dscale,
+                        uint32_t seed, float* dgamma, float* dbeta, hipStream_t stream) {
+  if (d % 8 != 0 || d > 2048) return (int)hipErrorInvalidValue;
+  auto DY = (const uint16_t*)dy;
+  auto X = (const uint16_t*)x;
+  auto DX = (uint16_t*)dx;
+  auto DH = (uint16_t*)dh;
+  if (d <= 512) return launch_ln_bwd<1>(DY, X, mean, rstd, C, rows_per_client, d, gamma, DX, DH, thr, dscale, seed, dgamma, dbeta, stream);
+  if (d <= 1024) return launch_ln_bwd<2>(DY, X, mean, rstd, C, rows_per_client, d, gamma, DX, DH, thr, dscale, seed, dgamma, dbeta, stream);
+  return launch_ln_bwd<4>(DY, X, mean, rstd, C, rows_per_client, d, gamma, DX, DH, thr, dscale, seed, dgamma, dbeta, stream);
+}
+
+FA_EXPORT int fa_gelu_fwd(const void* x, void* y, int64_t n, hipStream_t stream) {
+  if (n % 8 != 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(gelu_fwd_kernel, dim3(fa_grid(n / 8, 256, 8192)), dim3(256), 0, stream, (const uint16_t*)x,
+                     (uint16_t*)y, n / 8);
+  return (int)hipGetLastError();
+}
+
+FA_EXPORT int fa_gelu_bwd(const void* x, const void* gy, void* gx, int64_t n, hipStream_t stream) {
+  if (n % 8 != 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(gelu_bwd_kernel, dim3(fa_grid(n / 8, 256, 8192)), dim3(256), 0, stream, (const uint16_t*)x,
+                     (const uint16_t*)gy, (uint16_t*)gx, n / 8);
+  return (int)hipGetLastError();
+}
+
+FA_EXPORT int fa_attn_fwd(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o, int ldo,
+                          const uint8_t* kmask, float* lse2, int CB, int S, int H, float scale, uint32_t thr,
+                          float dscale, uint32_t seed, hipStream_t stream) {
+  auto Q = (const uint16_t*)q;
+  auto K = (const uint16_t*)k;
+  auto V = (const uint16_t*)v;
+  auto O = (uint16_t*)o;
+  if (S <= 0 || S > 256 || (ldq | ldk | ldv | ldo) % 8 != 0) return (int)hipErrorInvalidValue;
+  if (S <= 64) return launch_attn_fwd<64>(Q, ldq, K, ldk, V, ldv, O, ldo, kmask, lse2, CB, S, H, scale, thr, dscale, seed, stream);
+  if (S <= 128) return launch_attn_fwd<128>(Q, ldq, K, ldk, V, ldv, O, ldo, kmask, lse2, CB, S, H, scale, thr, dscale, seed, stream);
+  if (S <= 160) return launch_attn_fwd<160>(Q, ldq, K, ldk, V, ldv, O, ldo, kmask, lse2, CB, S, H, scale, thr, dscale, seed, stream);
+  if (S <= 192) return launch_attn_fwd<192>(Q, ldq, K, ldk, V, ldv, O, ldo, kmask, lse2, CB, S, H, scale, thr, dscale, seed, stream);
+  if (S <= 224) return launch_attn_fwd<224>(Q, ldq, K, ldk, V, ldv, O, ldo, kmask, lse2, CB, S, H, scale, thr, dscale, seed, stream);
+  return launch_attn_fwd<256>(Q, ldq, K, ldk, V, ldv, O, ldo, kmask, lse2, CB, S, H, scale, thr, dscale, seed, stream);
+}
+
+FA_EXPORT int fa_attn_bwd(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, const void* o,
+                          int ldo, const void* dout, int lddo, const uint8_t* kmask, const float* lse2, float* Dbuf,
+                          void* dq, int lddq, void* dk, int lddk, void* dv, int lddv, int CB, int S, int H,
+                          float scale, uint32_t thr, float dscale, uint32_t seed, hipStream_t stream) {
+  if (S <= 0 || S > 4096 || (ldq | ldk | ldv | ldo | lddo | lddq | lddk | lddv) % 8 != 0)
+    return (int)hipErrorInvalidValue;
+  const int64_t n = (int64_t)CB * S * H;
+  hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
+                     (const uint16_t*)o, ldo, (const uint16_t*)dout, lddo, Dbuf, CB * S, S, H);
+  const dim3 grid((S + 63) / 64, H, CB);
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, grid, dim3(256), 0, stream, (const uint16_t*)q, ldq, (const uint16_t*)k, ldk,
+                     (const uint16_t*)v, ldv, (const uint16_t*)dout, lddo, kmask, lse2, Dbuf, (uint16_t*)dq, lddq, S, H,
+                     scale, thr, dscale, seed);
+  hipLaunchKernelGGL(attn_bwd_dkv_kernel, grid, dim3(256), 0, stream, (const uint16_t*)q, ldq, (const uint16_t*)k,
+                     ldk, (const uint16_t*)v, ldv, (const uint16_t*)dout, lddo, kmask, lse2, Dbuf, (uint16_t*)dk, lddk,
+                     (uint16_t*)dv, lddv, S, H, scale, thr, dscale, seed);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,204 @@
+"""Autograd ops over the transformer HIP kernels (``csrc/transformer_kernels.hip``).
+
+* :func:`layer_norm` — LN(res + dropout(h)) with per-client gamma/beta ``[C, d]`` (rows of client c
+  are ``[c·R_c, (c+1)·R_c)``); backward gives dh (dropout-masked), dres, dgamma, dbeta.
+* :func:`gelu` — exact (erf) GELU.
+* :func:`attention` — softmax(q·kᵀ/√64 + key mask)·v per (row-group, head) for S ≤ 256 and head
+  dim 64, with attention-probability dropout; q/k/v/o are token-major ``[CB·S, H·64]``.
+
+CUDA tensors run the kernels (bf16 in/out, fp32 statistics); CPU tensors run the plain-PyTorch
+fp32 reference of the same math — the same hash-based dropout mask included — which is also the
+oracle of ``tests/test_transformer_kernels_gpu.py``.
+"""
+import ctypes as _c
+import math
+
+import torch
+
+from .fl_ops import _check, _f, _fn, _i64, _p, _stream, use_native
+
+_M32 = 0xFFFFFFFF
+
+
+def _thr(p: float) -> int:
+    return min(_M32, int(round(float(p) * 4294967296.0))) if p > 0 else 0
+
+
+def _fmix32(h: torch.Tensor) -> torch.Tensor:
+    h = h ^ (h >> 16)
+    h = (h * 0x85EBCA6B) & _M32
+    h = h ^ (h >> 13)
+    h = (h * 0xC2B2AE35) & _M32
+    return h ^ (h >> 16)
+
+
+def dropout_keep(seed: int, a: torch.Tensor, b: torch.Tensor, p: float) -> torch.Tensor:
+    """Keep mask of the kernels' counter-hash dropout: fmix32(fmix32(a ^ seed) + b·φ) ≥ p·2³²."""
+    a = a.to(torch.int64) & _M32
+    b = b.to(torch.int64) & _M32
+    h = _fmix32((_fmix32(a ^ (int(seed) & _M32)) + b * 0x9E3779B1) & _M32)
+    return h >= _thr(p)
+
+
+# ------------------------------------------------------------------------------------------- LN
+def _ln_ref(h, res, gamma, beta, eps, p, seed, rpc):
+    R, d = h.shape
+    x = h.float()
+    if p > 0:
+        keep = dropout_keep(seed, torch.arange(R, device=h.device).view(R, 1),
+                            torch.arange(d, device=h.device).view(1, d), p)
+        x = torch.where(keep, x / (1.0 - p), torch.zeros_like(x))
+    if res is not None:
+        x = x + res.float()
+    if (res is not None or p > 0) and h.dtype == torch.bfloat16:
+        x = x.to(torch.bfloat16).float()
+    C = R // rpc
+    xc = x.view(C, rpc, d)
+    mu = xc.mean(-1, keepdim=True)
+    var = ((xc - mu) ** 2).mean(-1, keepdim=True)
+    y = (xc - mu) * torch.rsqrt(var + eps) * gamma.view(C, 1, d).float() + beta.view(C, 1, d).float()
+    return y.view(R, d).to(h.dtype)
+
+
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, h, res, gamma, beta, eps, p, seed, rpc):
+        R, d = h.shape
+        y = torch.empty_like(h)
+        fused = res is not None or p > 0
+        xsum = torch.empty_like(h) if fused else None
+        mean = torch.empty(R, dtype=torch.float32, device=h.device)
+        rstd = torch.empty(R, dtype=torch.float32, device=h.device)
+        g = gamma.detach().float().contiguous()
+        b = beta.detach().float().contiguous()
+        rc = _fn("fa_ln_fwd")(_p(h), _p(res), _c.c_int(R), _c.c_int(d), _c.c_int(rpc), _p(g), _p(b), _f(eps),
+                              _c.c_uint32(_thr(p)), _f(1.0 / (1.0 - p) if p > 0 else 1.0), _c.c_uint32(seed & _M32),
+                              _p(y), _p(xsum), _p(mean), _p(rstd), _stream(h))
+        _check(rc, "fa_ln_fwd")
+        ctx.save_for_backward(xsum if fused else h, mean, rstd, g)
+        ctx.cfg = (p, seed, rpc, res is not None, fused, gamma.dtype)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, mean, rstd, g = ctx.saved_tensors
+        p, seed, rpc, has_res, fused, gdt = ctx.cfg
+        R, d = x.shape
+        C = R // rpc
+        dy = dy.contiguous()
+        dres = torch.empty_like(x) if has_res else None
+        dh = torch.empty_like(x)
+        dg = torch.zeros(C, d, dtype=torch.float32, device=x.device)
+        db = torch.zeros(C, d, dtype=torch.float32, device=x.device)
+        rc = _fn("fa_ln_bwd")(_p(dy), _p(x), _p(mean), _p(rstd), _c.c_int(C), _c.c_int(rpc), _c.c_int(d), _p(g),
+                              _p(dres), _p(dh), _c.c_uint32(_thr(p)), _f(1.0 / (1.0 - p) if p > 0 else 1.0),
+                              _c.c_uint32(seed & _M32), _p(dg), _p(db), _stream(x))
+        _check(rc, "fa_ln_bwd")
+        return dh, dres, dg.to(gdt), db.to(gdt), None, None, None, None
+
+
+def layer_norm(h: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float, rows_per_client: int,
+               res: torch.Tensor = None, p: float = 0.0, seed: int = 0) -> torch.Tensor:
+    """LN(res + dropout_p(h)) over the last dim of 2-D ``h`` [R, d]; gamma/beta ``[C, d]``."""
+    assert h.dim() == 2 and h.shape[0] % rows_per_client == 0
+    if use_native(h):
+        assert h.dtype == torch.bfloat16 and h.is_contiguous() and (res is None or res.is_contiguous())
+        return _LayerNorm.apply(h, res, gamma, beta, float(eps), float(p), int(seed), int(rows_per_client))
+    return _ln_ref(h, res, gamma, beta, eps, p, seed, rows_per_client)
+
+
+# ----------------------------------------------------------------------------------------- GELU
+class _Gelu(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x):
+        y = torch.empty_like(x)
+        _check(_fn("fa_gelu_fwd")(_p(x), _p(y), _i64(x.numel()), _stream(x)), "fa_gelu_fwd")
+        ctx.save_for_backward(x)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        (x,) = ctx.saved_tensors
+        gy = gy.contiguous()
+        gx = torch.empty_like(x)
+        _check(_fn("fa_gelu_bwd")(_p(x), _p(gy), _p(gx), _i64(x.numel()), _stream(x)), "fa_gelu_bwd")
+        return gx
+
+
+def gelu(x: torch.Tensor) -> torch.Tensor:
+    if use_native(x):
+        assert x.dtype == torch.bfloat16 and x.is_contiguous() and x.numel() % 8 == 0
+        return _Gelu.apply(x)
+    return torch.nn.functional.gelu(x.float()).to(x.dtype)
+
+
+# ------------------------------------------------------------------------------------ attention
+def _attn_ref(q, k, v, kmask, S, H, p, seed):
+    T, dm = q.shape
+    CB = T // S
+    qh = q.float().view(CB, S, H, 64).transpose(1, 2)
+    kh = k.float().view(CB, S, H, 64).transpose(1, 2)
+    vh = v.float().view(CB, S, H, 64).transpose(1, 2)
+    s = qh @ kh.transpose(-1, -2) / math.sqrt(64.0)
+    if kmask is not None:
+        s = s.masked_fill(~kmask.view(CB, 1, 1, S).bool(), float("-inf"))
+    pr = torch.softmax(s, -1).nan_to_num(0.0)
+    if p > 0:
+        bh = torch.arange(CB * H, device=q.device).view(CB, H, 1, 1)
+        qi = torch.arange(S, device=q.device).view(1, 1, S, 1)
+        ki = torch.arange(S, device=q.device).view(1, 1, 1, S)
+        keep = dropout_keep(seed, bh * 65536 + qi, ki, p)
+        pr = torch.where(keep, pr / (1.0 - p), torch.zeros_like(pr))
+    o = (pr @ vh).transpose(1, 2).reshape(T, dm)
+    return o.to(q.dtype)
+
+
+class _Attention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, q, k, v, kmask, S, H, p, seed):
+        T, dm = q.shape
+        CB = T // S
+        o = torch.empty(T, dm, dtype=q.dtype, device=q.device)
+        lse = torch.empty(CB, H, S, dtype=torch.float32, device=q.device)
+        scale = 1.0 / math.sqrt(64.0)
+        rc = _fn("fa_attn_fwd")(_p(q), _c.c_int(q.stride(0)), _p(k), _c.c_int(k.stride(0)), _p(v),
+                                _c.c_int(v.stride(0)), _p(o), _c.c_int(dm), _p(kmask), _p(lse), _c.c_int(CB),
+                                _c.c_int(S), _c.c_int(H), _f(scale), _c.c_uint32(_thr(p)),
+                                _f(1.0 / (1.0 - p) if p > 0 else 1.0), _c.c_uint32(seed & _M32), _stream(q))
+        _check(rc, "fa_attn_fwd")
+        ctx.save_for_backward(q, k, v, o, lse, kmask)
+        ctx.cfg = (S, H, p, seed)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse, kmask = ctx.saved_tensors
+        S, H, p, seed = ctx.cfg
+        T, dm = q.shape
+        CB = T // S
+        do = do.contiguous()
+        dq = torch.empty(T, dm, dtype=q.dtype, device=q.device)
+        dk = torch.empty_like(dq)
+        dv = torch.empty_like(dq)
+        D = torch.empty(CB, H, S, dtype=torch.float32, device=q.device)
+        rc = _fn("fa_attn_bwd")(_p(q), _c.c_int(q.stride(0)), _p(k), _c.c_int(k.stride(0)), _p(v),
+                                _c.c_int(v.stride(0)), _p(o), _c.c_int(dm), _p(do), _c.c_int(dm), _p(kmask), _p(lse),
+                                _p(D), _p(dq), _c.c_int(dm), _p(dk), _c.c_int(dm), _p(dv), _c.c_int(dm),
+                                _c.c_int(CB), _c.c_int(S), _c.c_int(H), _f(1.0 / math.sqrt(64.0)),
+                                _c.c_uint32(_thr(p)), _f(1.0 / (1.0 - p) if p > 0 else 1.0),
+                                _c.c_uint32(seed & _M32), _stream(q))
+        _check(rc, "fa_attn_bwd")
+        return dq, dk, dv, None, None, None, None, None
+
+
+def attention(q, k, v, S: int, H: int, kmask: torch.Tensor = None, p: float = 0.0, seed: int = 0):
+    """Multi-head self-attention over token-major ``[CB·S, H·64]`` q/k/v (row stride may exceed
+    H·64, e.g. column slices of a fused QKV output); ``kmask`` [CB, S] (nonzero = attend)."""
+    assert q.dim() == 2 and q.shape[1] == H * 64 and q.shape[0] % S == 0
+    if use_native(q):
+        assert S <= 256 and q.dtype == torch.bfloat16
+        for t in (q, k, v):
+            assert t.stride(1) == 1 and t.stride(0) % 8 == 0
+        km = None if kmask is None else kmask.to(torch.uint8).contiguous()
+        return _Attention.apply(q, k, v, km, int(S), int(H), float(p), int(seed))
+    return _attn_ref(q, k, v, kmask, S, H, p, seed)

@@ -1,0 +1,99 @@
+"""Transformer HIP kernels (LayerNorm, GELU, attention; ``csrc/transformer_kernels.hip``) against
+plain-PyTorch fp32 references of the same ops, forward and backward, including the counter-hash
+dropout masks and key-padding masks."""
+import math
+
+import pytest
+import torch
+
+from fedml_amd.ops import transformer_ops as T
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+
+
+def _close(a, b, tol):
+    a, b = a.float(), b.float()
+    err = (a - b).abs().max().item()
+    ref = b.abs().max().item() + 1e-6
+    assert err <= tol * ref, f"max err {err} vs ref scale {ref}"
+
+
+@pytest.mark.parametrize("d,rpc,C,res,p", [(768, 40, 3, True, 0.1), (768, 33, 2, False, 0.0), (192, 17, 4, True, 0.0),
+                                           (1024, 8, 2, False, 0.2)])
+def test_layer_norm_fwd_bwd(d, rpc, C, res, p):
+    torch.manual_seed(0)
+    R = rpc * C
+    h = (torch.randn(R, d, device=dev) * 2 + 0.5).to(torch.bfloat16).requires_grad_(True)
+    r = torch.randn(R, d, device=dev).to(torch.bfloat16).requires_grad_(True) if res else None
+    g = (1 + 0.1 * torch.randn(C, d, device=dev)).requires_grad_(True)
+    b = (0.1 * torch.randn(C, d, device=dev)).requires_grad_(True)
+    y = T.layer_norm(h, g, b, 1e-12, rpc, res=r, p=p, seed=1234)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    # fp32 reference on the same bf16 inputs
+    h2 = h.detach().float().requires_grad_(True)
+    r2 = r.detach().float().requires_grad_(True) if res else None
+    g2 = g.detach().clone().requires_grad_(True)
+    b2 = b.detach().clone().requires_grad_(True)
+    y2 = T._ln_ref(h2, r2, g2, b2, 1e-12, p, 1234, rpc)
+    y2.backward(gy.float())
+    _close(y, y2, 2e-2)
+    _close(h.grad, h2.grad, 3e-2)
+    if res:
+        _close(r.grad, r2.grad, 3e-2)
+    _close(g.grad, g2.grad, 2e-2)
+    _close(b.grad, b2.grad, 2e-2)
+
+
+def test_gelu_fwd_bwd():
+    torch.manual_seed(0)
+    x = (torch.randn(4096, 96, device=dev) * 3).to(torch.bfloat16).requires_grad_(True)
+    y = T.gelu(x)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    x2 = x.detach().float().requires_grad_(True)
+    y2 = torch.nn.functional.gelu(x2)
+    y2.backward(gy.float())
+    _close(y, y2, 1e-2)
+    _close(x.grad, x2.grad, 2e-2)
+
+
+@pytest.mark.parametrize("S,H,CB,mask,p", [(197, 3, 4, False, 0.0), (128, 2, 3, True, 0.0), (128, 2, 3, True, 0.1),
+                                           (64, 1, 2, False, 0.0), (250, 2, 2, True, 0.0), (37, 2, 5, True, 0.1)])
+def test_attention_fwd_bwd(S, H, CB, mask, p):
+    torch.manual_seed(0)
+    dm = 64 * H
+    # q/k/v as column slices of one fused [T, 3·dm] buffer (row stride 3·dm) — the kernels take strides
+    qkv = torch.randn(CB * S, 3 * dm, device=dev).to(torch.bfloat16).requires_grad_(True)
+    q, k, v = qkv[:, :dm], qkv[:, dm:2 * dm], qkv[:, 2 * dm:]
+    km = None
+    if mask:
+        km = torch.rand(CB, S, device=dev) > 0.3
+        km[:, 0] = True
+    o = T.attention(q, k, v, S, H, kmask=km, p=p, seed=77)
+    go = torch.randn_like(o)
+    o.backward(go)
+    qkv2 = qkv.detach().float().requires_grad_(True)
+    o2 = T._attn_ref(qkv2[:, :dm], qkv2[:, dm:2 * dm], qkv2[:, 2 * dm:], km, S, H, p, 77)
+    o2.backward(go.float())
+    _close(o, o2, 2e-2)
+    _close(qkv.grad, qkv2.grad, 4e-2)
+
+
+def test_attention_fully_masked_row_is_zero():
+    S, H, CB = 64, 1, 2
+    q = torch.randn(CB * S, 64, device=dev).to(torch.bfloat16)
+    km = torch.ones(CB, S, dtype=torch.bool, device=dev)
+    km[1] = False
+    o = T.attention(q, q, q, S, H, kmask=km)
+    assert torch.isfinite(o.float()).all()
+    assert o[S:].abs().max().item() == 0.0
+
+
+def test_dropout_keep_rate():
+    a = torch.arange(1 << 16).view(-1, 1)
+    b = torch.arange(64).view(1, -1)
+    keep = T.dropout_keep(5, a, b, 0.1)
+    assert abs(keep.float().mean().item() - 0.9) < 2e-3
+    assert math.isclose(T._thr(0.5), 2 ** 31, rel_tol=1e-9)
