@@ -46,7 +46,6 @@ def parse():
     p.add_argument("--client-optimizer", default="sgd")
     p.add_argument("--preset", default="", help="resnet18_cifar10_10 | distilbert_fedopt_32 | vit_b16_32 "
                                                 "(other BASELINE.json configs; the default is the headline)")
-    a = p.parse_args()
     presets = {
         "resnet18_cifar10_10": dict(model="resnet18", dataset="cifar10", clients=10, samples_per_client=5000,
                                     batch_size=64, lr=0.001),
@@ -56,10 +55,10 @@ def parse():
         "vit_b16_32": dict(model="vit_b16", dataset="ILSVRC2012", clients=32, samples_per_client=32, batch_size=16,
                            lr=1e-4, client_optimizer="adamw"),
     }
-    if a.preset:
-        for k, v in presets[a.preset].items():
-            setattr(a, k, v)
-    return a
+    pre, _ = p.parse_known_args()
+    if pre.preset:   # a preset changes the defaults; flags given on the command line still win
+        p.set_defaults(**presets[pre.preset])
+    return p.parse_args()
 
 
 def main():

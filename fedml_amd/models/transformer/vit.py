@@ -44,4 +44,6 @@ def vit_b16(num_classes=1000, img_size=224, **kw):
 
 
 def vit_tiny(num_classes=10, img_size=32, patch=4, **kw):
-    return VisionTransformer(img_size=img_size, patch=patch, num_classes=num_classes, dim=192, depth=4, n_heads=3, **kw)
+    cfg = dict(dim=192, depth=4, n_heads=3)
+    cfg.update(kw)
+    return VisionTransformer(img_size=img_size, patch=patch, num_classes=num_classes, **cfg)

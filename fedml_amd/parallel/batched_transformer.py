@@ -1,0 +1,188 @@
+"""Client-batched transformer step (DistilBERT, ViT) for the virtual-client engine.
+
+The C clients' private copies of the model run as ONE program instead of C sequential ones:
+
+* every ``nn.Linear`` becomes one batched GEMM ``[C, T, in] × [C, in, out]`` (``torch.baddbmm`` →
+  hipBLASLt, bf16 operands from the fp32 master views of the client arena, fp32 gradients landing
+  in the gradient arena); q/k/v are fused into one GEMM with N = 3·d;
+* LayerNorm (fused with the residual add and hidden dropout of post-LN blocks), GELU and
+  self-attention run the hand-written HIP kernels of ``ops.transformer_ops`` over token-major
+  ``[C·B·S, d]`` activations, with per-client gamma/beta;
+* the loss is the fused softmax-CE kernel with per-row client scaling (ragged final batches).
+
+Module structure and parameter names follow ``models/transformer`` (HuggingFace DistilBERT / timm
+ViT naming), so the arena layout, aggregation and checkpoints are unchanged. The reference has no
+transformer models; CPU tensors run the same program through the ops'
+PyTorch references (the engine's tests compare it with per-client ``nn.Module`` forward passes).
+"""
+from typing import Dict, Optional
+
+import torch
+import torch.nn.functional as F
+
+from ..models.transformer.distilbert import DistilBertForSequenceClassification
+from ..models.transformer.vit import VisionTransformer
+from ..ops import transformer_ops as T
+
+
+class UnsupportedTransformer(Exception):
+    pass
+
+
+def _bf(t: torch.Tensor, dtype) -> torch.Tensor:
+    return t if dtype is None else t.to(dtype)
+
+
+class _ClientEmbedding(torch.autograd.Function):
+    """rows ``W[c, ids[c, t]]`` of a per-client table ``W`` [C, V, d] (a strided arena view, never
+    copied). Backward scatter-adds straight into ``W.grad`` (the gradient-arena view) when the
+    engine pre-assigned it, instead of materialising a dense [C, V, d] gradient per step."""
+
+    @staticmethod
+    def forward(ctx, W, ids):
+        C = W.shape[0]
+        cidx = torch.arange(C, device=ids.device).view(C, 1)
+        ctx.save_for_backward(cidx, ids)
+        ctx.W = W
+        return W[cidx, ids]
+
+    @staticmethod
+    def backward(ctx, g):
+        cidx, ids = ctx.saved_tensors
+        W = ctx.W
+        idx = (cidx.expand_as(ids), ids)
+        if W.grad is not None:
+            W.grad.index_put_(idx, g.to(W.grad.dtype), accumulate=True)
+            return None, None
+        out = torch.zeros(W.shape, dtype=g.dtype, device=g.device)
+        out.index_put_(idx, g, accumulate=True)
+        return out, None
+
+
+class BatchedTransformer:
+    """Batched forward of a DistilBERT / ViT over a client-stacked parameter dict.
+
+    ``views`` maps state_dict keys to ``[C, *shape]`` fp32 tensors (leaf views of the client arena
+    whose ``.grad`` are gradient-arena views). ``x``: token ids ``[C, B, S]`` (DistilBERT) or images
+    ``[C, B, 3, H, W]`` (ViT). Returns logits ``[C, B, K]`` in fp32."""
+
+    def __init__(self, model: torch.nn.Module, C: int):
+        self.C = int(C)
+        if isinstance(model, DistilBertForSequenceClassification):
+            self.kind = "distilbert"
+            blk = model.layer[0]
+            self.n_layers = len(model.layer)
+            self.heads = blk.attention.n_heads
+            self.dim = blk.attention.dim
+            self.eps = blk.sa_layer_norm.eps
+            self.emb_eps = model.embeddings.LayerNorm.eps
+            self.p_attn = float(blk.attention.dropout)
+            self.p_hidden = float(blk.drop.p)
+            self.p_emb = float(model.embeddings.dropout.p)
+            self.p_cls = float(model.dropout.p)
+        elif isinstance(model, VisionTransformer):
+            self.kind = "vit"
+            blk = model.blocks[0]
+            self.n_layers = len(model.blocks)
+            self.heads = blk.attn.n_heads
+            self.dim = blk.attn.dim
+            self.eps = blk.norm1.eps
+            self.patch = model.patch_embed.proj.kernel_size[0]
+            self.p_attn = float(blk.attn.dropout)
+            self.p_hidden = float(blk.mlp.dropout.p)
+            if self.p_hidden:
+                raise UnsupportedTransformer("ViT MLP dropout is not supported by the batched path")
+        else:
+            raise UnsupportedTransformer(type(model).__name__)
+        if self.dim != 64 * self.heads:
+            raise UnsupportedTransformer(f"head dim {self.dim // self.heads} != 64")
+        self.step_seed = 0
+
+    # -------------------------------------------------------------------------------- helpers
+    def _lin(self, v, x, key, dt, weights=None):
+        """x [C, T, in] → [C, T, out] with per-client W [C, out, in] and bias [C, out]."""
+        if weights is None:
+            w = _bf(v[key + ".weight"], dt)
+            b = _bf(v[key + ".bias"], dt)
+        else:
+            w, b = weights
+        return torch.baddbmm(b.unsqueeze(1), x, w.transpose(1, 2))
+
+    def _qkv(self, v, x, pre, dt):
+        w = torch.cat([_bf(v[f"{pre}.{n}.weight"], dt) for n in ("q_lin", "k_lin", "v_lin")], 1)
+        b = torch.cat([_bf(v[f"{pre}.{n}.bias"], dt) for n in ("q_lin", "k_lin", "v_lin")], 1)
+        return self._lin(v, x, None, dt, (w, b))
+
+    def _ln(self, v, key, h, rows_per_client, res=None, p=0.0, seed=0, eps=None):
+        d = h.shape[-1]
+        y = T.layer_norm(h.reshape(-1, d), v[key + ".weight"], v[key + ".bias"], self.eps if eps is None else eps,
+                         rows_per_client, res=None if res is None else res.reshape(-1, d), p=p, seed=seed)
+        return y.view(h.shape)
+
+    def _attn(self, v, x, pre, S, kmask, training, dt, seed):
+        C, Tk, d = x.shape
+        qkv = self._qkv(v, x, pre, dt).view(C * Tk, 3 * d)
+        a = T.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], S, self.heads, kmask=kmask,
+                        p=self.p_attn if training else 0.0, seed=seed)
+        return self._lin(v, a.view(C, Tk, d), pre + ".out_lin", dt)
+
+    # -------------------------------------------------------------------------------- forward
+    def forward(self, v: Dict[str, torch.Tensor], x: torch.Tensor, training: bool = True,
+                dtype: Optional[torch.dtype] = torch.bfloat16) -> torch.Tensor:
+        self.step_seed = (self.step_seed + 1) & 0x7FFFFFFF
+        base = self.step_seed * 1000003
+        if self.kind == "distilbert":
+            return self._distilbert(v, x, training, dtype, base)
+        return self._vit(v, x, training, dtype, base)
+
+    def _distilbert(self, v, ids, training, dt, base):
+        C, B, S = ids.shape
+        d = self.dim
+        we = _ClientEmbedding.apply(v["embeddings.word_embeddings.weight"], ids.reshape(C, B * S))  # [C, BS, d]
+        pe = v["embeddings.position_embeddings.weight"][:, :S]                                  # [C, S, d]
+        h = _bf((we.view(C, B, S, d) + pe.unsqueeze(1)).view(C, B * S, d), dt).contiguous()
+        rows = B * S
+        x = self._ln(v, "embeddings.LayerNorm", h, rows, eps=self.emb_eps)
+        if training and self.p_emb:
+            x = F.dropout(x, self.p_emb, True)
+        kmask = (ids != 0).reshape(C * B, S)
+        for i in range(self.n_layers):
+            pre = f"layer.{i}"
+            sa = self._attn(v, x, pre + ".attention", S, kmask, training, dt, base + 10 * i + 1)
+            x = self._ln(v, pre + ".sa_layer_norm", sa.contiguous(), rows, res=x,
+                         p=self.p_hidden if training else 0.0, seed=base + 10 * i + 2)
+            f = T.gelu(self._lin(v, x, pre + ".ffn.lin1", dt).contiguous())
+            f = self._lin(v, f, pre + ".ffn.lin2", dt)
+            x = self._ln(v, pre + ".output_layer_norm", f.contiguous(), rows, res=x,
+                         p=self.p_hidden if training else 0.0, seed=base + 10 * i + 3)
+        cls = x.view(C, B, S, d)[:, :, 0]                                                      # [C, B, d]
+        pooled = torch.relu(self._lin(v, cls, "pre_classifier", dt))
+        if training and self.p_cls:
+            pooled = F.dropout(pooled, self.p_cls, True)
+        return self._lin(v, pooled, "classifier", dt).float()
+
+    def _vit(self, v, img, training, dt, base):
+        C, B = img.shape[0], img.shape[1]
+        ch, Hh, Ww = img.shape[2], img.shape[3], img.shape[4]
+        p = self.patch
+        gh, gw = Hh // p, Ww // p
+        d = self.dim
+        patches = _bf(img, dt).reshape(C, B, ch, gh, p, gw, p).permute(0, 1, 3, 5, 2, 4, 6) \
+            .reshape(C, B * gh * gw, ch * p * p)
+        pw = _bf(v["patch_embed.proj.weight"].reshape(C, d, ch * p * p), dt)
+        pb = _bf(v["patch_embed.proj.bias"], dt)
+        tok = self._lin(v, patches, None, dt, (pw, pb)).view(C, B, gh * gw, d)
+        cls = _bf(v["cls_token"], dt).view(C, 1, 1, d).expand(C, B, 1, d)
+        S = gh * gw + 1
+        x = (torch.cat([cls, tok], 2) + _bf(v["pos_embed"], dt).view(C, 1, S, d)).reshape(C, B * S, d).contiguous()
+        rows = B * S
+        for i in range(self.n_layers):
+            pre = f"blocks.{i}"
+            h = self._ln(v, pre + ".norm1", x, rows)
+            x = x + self._attn(v, h, pre + ".attn", S, None, training, dt, base + 10 * i + 1)
+            h = self._ln(v, pre + ".norm2", x, rows)
+            f = T.gelu(self._lin(v, h, pre + ".mlp.lin1", dt).contiguous())
+            x = x + self._lin(v, f, pre + ".mlp.lin2", dt)
+        cls_out = x.view(C, B, S, d)[:, :, 0].contiguous()
+        y = self._ln(v, "norm", cls_out, B)
+        return self._lin(v, y, "head", dt).float()

@@ -23,6 +23,7 @@ import torch
 
 from ... import ops
 from ...core.arena import ParamLayout
+from ...parallel.batched_transformer import BatchedTransformer, UnsupportedTransformer
 from ...parallel.batched_nn import BatchedInterpreter, UnsupportedForBatching
 
 
@@ -36,6 +37,18 @@ def _close_engines():
             e.close()
         except Exception:
             pass
+
+
+def _is_wide_convnet(model: torch.nn.Module, min_channels: int = 128) -> bool:
+    """True when most conv MACs sit in layers with ≥ ``min_channels`` input channels."""
+    wide = total = 0
+    for m in model.modules():
+        if isinstance(m, torch.nn.Conv2d) and m.groups == 1:
+            w = m.weight.numel()
+            total += w
+            if m.in_channels >= min_channels:
+                wide += w
+    return total > 0 and wide >= 0.5 * total
 
 
 class ClientBatchEngine:
@@ -64,13 +77,22 @@ class ClientBatchEngine:
             self.step_t = torch.zeros(self.C, dtype=torch.float32, device=self.device)
         # client-batched program when the model is client-stackable; otherwise clients run one after
         # another on the same arenas (transformers, models with data-dependent control flow)
+        self.tf = None
         try:
             self.interp = BatchedInterpreter(model, self.layout, self.C)
             self.sequential = False
         except UnsupportedForBatching as e:
-            logging.info("virtual-client engine: sequential per-client path (%s)", e)
             self.interp = None
             self.sequential = True
+            self.tf = None
+            if os.environ.get("FEDML_AMD_BATCHED_TRANSFORMER", "1") != "0":
+                try:
+                    self.tf = BatchedTransformer(model, self.C)
+                    logging.info("virtual-client engine: client-batched transformer path (%s)", self.tf.kind)
+                except UnsupportedTransformer:
+                    pass
+            if self.tf is None:
+                logging.info("virtual-client engine: sequential per-client path (%s)", e)
         self._seq_views = None
         self._graphs = {}
         _LIVE_ENGINES.add(self)
@@ -84,6 +106,14 @@ class ClientBatchEngine:
                 logging.info("virtual-client engine: native HIP ResNet path (C=%d)", self.C)
             except UnsupportedNative as e:
                 logging.info("virtual-client engine: torch batched path (%s)", e)
+        # Client-stacked grouped convolutions only pay while each client's conv is too small to fill
+        # the GPU on its own (ResNet-56: 16-64 channels). Wide conv nets (ResNet-18: 64-512 channels)
+        # run faster as one full-width library conv per client than as one C-group grouped conv.
+        mode = os.environ.get("FEDML_AMD_CLIENT_EXEC", str(getattr(args, "client_exec", "auto") or "auto"))
+        if not self.sequential and self.native_step is None and self.tf is None and (
+                mode == "sequential" or (mode == "auto" and self.device.type == "cuda" and _is_wide_convnet(model))):
+            logging.info("virtual-client engine: per-client sequential execution (wide conv net)")
+            self.sequential = True
         self._build_views()
         self.global_ref = None
         self.loss_history: List[float] = []
@@ -174,7 +204,9 @@ class ClientBatchEngine:
             bc = torch.tensor([max(1, b) for b in b_c], dtype=torch.float32, device=self.device)
             row_scale = mask.to(torch.float32) / bc.view(-1, 1)
             return self.native_step.step(self.params, self.grads, x, y, row_scale, active)
-        if not self.sequential:
+        if self.tf is not None:
+            out = self.tf.forward(self.views, x, training=True, dtype=self.compute_dtype)    # [C, B, K]
+        elif not self.sequential:
             try:
                 out = self.interp.run(self.views, x, training=True, sample_mask=sample_mask, active=active,
                                       dtype=self.compute_dtype)                   # [C, B, K]
@@ -182,7 +214,7 @@ class ClientBatchEngine:
                 logging.info("virtual-client engine: switching to the sequential path (%s)", e)
                 self.sequential = True
                 self.interp.deferred.clear()
-        if self.sequential:
+        if self.sequential and self.tf is None:
             return self._seq_step_loss(x, y, b_c)
         C, B = out.shape[0], out.shape[1]
         logits = out.reshape(C * B, -1)
@@ -197,7 +229,8 @@ class ClientBatchEngine:
             lr_ = torch.nn.functional.cross_entropy(logits.float(), labels, reduction="none")
             loss = (lr_ * row_scale).sum()
         loss.backward()
-        self.interp.flush_deferred()
+        if self.interp is not None:
+            self.interp.flush_deferred()
         return loss.detach()
 
     # ---------------------------------------------------------------- HIP-graph local step
