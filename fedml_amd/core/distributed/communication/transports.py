@@ -204,7 +204,8 @@ class GRPCCommManager(QueueCommManager):
             "Send": grpc.unary_unary_rpc_method_handler(_handle, request_deserializer=None, response_serializer=None)
         })
         self.server.add_generic_rpc_handlers((handler,))
-        self.server.add_insecure_port(f"0.0.0.0:{base_port + rank}")
+        if self.server.add_insecure_port(f"0.0.0.0:{base_port + rank}") == 0:
+            raise OSError(f"gRPC: cannot bind port {base_port + rank}")
         self.server.start()
         self._stubs = {}
         self._lock = threading.Lock()

@@ -344,7 +344,8 @@ def quantize_fp8(x, residual=None):
     vp = torch.nn.functional.pad(v, (0, pad)).view(nb, 256)
     amax = vp.abs().amax(1)
     scale = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
-    t = (vp / scale.view(-1, 1)).clamp(-448, 448).to(torch.float8_e4m3fn)
+    inv = 1.0 / scale   # multiply by the reciprocal, exactly as the HIP kernel does
+    t = (vp * inv.view(-1, 1)).clamp(-448, 448).to(torch.float8_e4m3fn)
     q = t.reshape(-1)[:n].view(torch.uint8)
     if residual is not None:
         back = t.to(torch.float32) * scale.view(-1, 1)

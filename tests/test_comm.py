@@ -13,6 +13,30 @@ from fedml_amd.core.distributed.communication.transports import (GRPCCommManager
                                                                   TCPCommManager)
 
 
+def _free_base_port(n=2):
+    """A base port with ``n`` consecutive free ports (fixed ports collide under pytest-xdist)."""
+    import socket
+    for _ in range(100):
+        with socket.socket() as s0:
+            s0.bind(("127.0.0.1", 0))
+            base = s0.getsockname()[1]
+        if base + n >= 65535:
+            continue
+        socks = []
+        try:
+            for r in range(n):
+                s1 = socket.socket()
+                socks.append(s1)
+                s1.bind(("127.0.0.1", base + r))
+            return base
+        except OSError:
+            continue
+        finally:
+            for s1 in socks:
+                s1.close()
+    raise RuntimeError("no free port range")
+
+
 def _msg():
     m = Message(3, 1, 0)
     m.add_params("model_params", OrderedDict(w=torch.randn(4, 5), b=torch.arange(3), h=torch.randn(2).bfloat16()))
@@ -62,11 +86,25 @@ def test_loopback():
 
 
 def test_tcp():
-    _echo_pair(lambda rank: TCPCommManager(rank, 2, base_port=39411))
+    port = _free_base_port()
+    _echo_pair(lambda rank: TCPCommManager(rank, 2, base_port=port))
 
 
 def test_grpc():
-    _echo_pair(lambda rank: GRPCCommManager(rank, 2, base_port=28931))
+    # gRPC's C core does not survive a pytest-xdist worker that already forked (multi-process tests),
+    # so the round trip runs in a fresh interpreter.
+    import subprocess
+    import sys
+    import os
+    code = ("import sys; sys.path.insert(0, %r); sys.path.insert(0, %r)\n"
+            "from test_comm import _echo_pair, _free_base_port\n"
+            "from fedml_amd.core.distributed.communication.transports import GRPCCommManager\n"
+            "port = _free_base_port()\n"
+            "_echo_pair(lambda rank: GRPCCommManager(rank, 2, base_port=port))\n"
+            "print('grpc ok')\n") % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                     os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "grpc ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
 
 
 def test_pubsub_blob_store_and_last_will():
