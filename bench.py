@@ -131,10 +131,11 @@ def main():
                             if a.preset in REF_ROUNDS_PER_S and a.samples_per_client == DEFAULT_SPC.get(a.preset)
                             and a.clients == DEFAULT_CLIENTS.get(a.preset) else None),
             "dtype": a.dtype if use_gpu else "fp32",
-            "data": "synthetic (CIFAR-100-shaped, class-conditional), random-init weights",
+            "data": f"synthetic ({a.dataset}-shaped {tuple(spec.shape)}, class-conditional), random-init weights",
             "config": {"model": a.model, "dataset": a.dataset, "clients": a.clients,
                        "samples_per_client": a.samples_per_client, "global_batch": a.batch_size * a.clients,
-                       "local_batch": a.batch_size, "local_epochs": a.epochs, "seq_len": None,
+                       "local_batch": a.batch_size, "local_epochs": a.epochs,
+                       "seq_len": spec.shape[0] if spec.kind in ("tokens", "nwp") else None,
                        "parallelism": f"client-parallel x{ws} (dp{ws}), RCCL all-reduce aggregation"},
             "samples_per_s": round(a.clients * a.samples_per_client * a.epochs * a.steps / elapsed, 1),
             "final_train_loss": round(loss, 4),

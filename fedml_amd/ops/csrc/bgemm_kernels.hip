@@ -1,0 +1,372 @@
+// Client-batched GEMMs for the transformer linears of the virtual-client engine
+// (gfx950, wave64, bf16 MFMA v_mfma_f32_16x16x32_bf16, fp32 accumulate).
+//
+// Every virtual client c owns private weights that live in the fp32 client arena [C][P]
+// (row stride P, one slot per state_dict key). One launch runs the same linear for all C
+// clients; the weights are read straight from the arena (converted to bf16 while staging
+// into LDS — no per-step bf16 weight copies) and weight gradients are added straight into
+// the fp32 gradient arena. A fused q/k/v projection is ONE GEMM whose weight rows come from
+// three arena slots ("segments").
+//
+//   logical GEMM per client:  D[m][n] = Σ_k A(m, k) · B(n, k)
+//   forward      y  = x · Wᵀ + b      A = x  [M][K]            B = W  [N][K] (arena, fp32)
+//   bwd-data     dx = dy · W          A = dy [M][N]            B = Wᵀ: storage W[n][k], k-major → "TR"
+//   bwd-weight   dW += dyᵀ · x        A = dyᵀ: storage dy[t][n] "TR"  B = xᵀ: storage x[t][k] "TR"
+//
+// An operand whose storage rows run along the REDUCTION index ("TR") is staged into LDS in its
+// natural layout and its MFMA fragments are read with gfx950's transposing LDS read
+// ds_read_b64_tr_b16; a K-major operand is read with plain 16-byte LDS reads.
+// Block tile 128×128×64, 4 waves × (64×64), register-staged double-buffered LDS, XCD-aware
+// block order (consecutive tiles of one client/row-block on one XCD → shared A rows in its L2).
+// The MFMA computes the transposed tile D[n][m], so each lane owns 4 consecutive output columns
+// of one row: 8-byte bf16 / 16-byte fp32 epilogue accesses, bias as one float4.
+#include "common.h"
+
+namespace bg {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+constexpr int BM = 128, BN = 128, BK = 64, NT = 256;
+constexpr int LDK = BK + 8;    // K-major tile [128 rows][64 k] row pitch (elements)
+constexpr int LDT = BM + 16;   // TR tile [64 k][128 cols] row pitch (elements)
+constexpr int TILE_ELEMS = 128 * LDK;  // == 64 * LDT (18 KiB per operand tile)
+static_assert(128 * LDK == 64 * LDT, "tile images must be the same size");
+
+enum { EPI_BF16 = 0, EPI_GELU = 1, EPI_ACC32 = 2 };
+
+struct Segs {        // row segments of an fp32 arena operand (≤ 4 slots)
+  int64_t off[4];    // element offset of segment s's first row, relative to the base pointer
+  int lo[5];         // first logical row of segment s (lo[n] = total rows)
+  int n;
+};
+
+struct Args {
+  const uint16_t* A;
+  int64_t a_bs;
+  int lda;
+  const void* B;     // bf16 [C][..] (b_bs, ldb) or fp32 arena base (b_bs = client stride, ldb = row length)
+  int64_t b_bs;
+  int ldb;
+  Segs bseg;
+  void* Cp;          // bf16 [C][M][ldc] (EPI_BF16/GELU) or fp32 arena base (EPI_ACC32, rows = segs)
+  int64_t c_bs;
+  int ldc;
+  Segs cseg;
+  const float* bias; // fp32 arena base (client stride bias_bs), rows = n segments (may be null)
+  int64_t bias_bs;
+  Segs biasseg;
+  uint16_t* C2;      // EPI_GELU: gelu(D + b) (C keeps the pre-activation for the backward)
+  int64_t c2_bs;
+  int M, N, K;
+  int tiles_m, tiles_n, nclients;
+};
+
+__device__ __forceinline__ int64_t seg_row(const Segs& s, int r, int rowlen) {
+  int i = 0;
+#pragma unroll
+  for (int t = 1; t < 4; ++t)
+    if (t < s.n && r >= s.lo[t]) i = t;
+  return s.off[i] + (int64_t)(r - s.lo[i]) * rowlen;
+}
+
+__device__ __forceinline__ uint32_t pk2(float a, float b) {
+  return (uint32_t)f32_to_bf16(a) | ((uint32_t)f32_to_bf16(b) << 16);
+}
+
+__device__ __forceinline__ bf16x8 row_frag(const uint16_t* tile, int row, int k) {
+  return *reinterpret_cast<const bf16x8*>(tile + row * LDK + k);
+}
+
+// 8 consecutive reduction rows (row0 + 8·(lane>>4) + j) of column col0 + (lane & 15)
+__device__ __forceinline__ bf16x8 tr_frag(const uint16_t* tile, int row0, int col0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const uint16_t* a0 = tile + (row0 + 8 * g + q) * LDT + col0 + 4 * p;
+  const v4i16 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a0));
+  const v4i16 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a0 + 4 * LDT));
+  union {
+    short s[8];
+    bf16x8 b;
+  } u;
+  u.s[0] = r0[0]; u.s[1] = r0[1]; u.s[2] = r0[2]; u.s[3] = r0[3];
+  u.s[4] = r1[0]; u.s[5] = r1[1]; u.s[6] = r1[2]; u.s[7] = r1[3];
+  return u.b;
+}
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+
+// ---- staging of one bf16 operand tile (4 × 16-byte vectors per thread) ----
+// TR = 0: logical rows [r0, r0+128) × k [k0, k0+64) of storage S[row][k]  (pitch ld)
+// TR = 1: storage S[k][col]: k rows [k0, k0+64) × cols [r0, r0+128)       (pitch ld)
+template <int TR>
+__device__ __forceinline__ void load_bf16(uint4 (&r)[4], const uint16_t* __restrict__ S, int ld, int rows, int K,
+                                          int r0, int k0, int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int v = tid + NT * i;
+    int row, col;
+    bool ok;
+    if (!TR) {
+      row = r0 + (v >> 3);
+      col = k0 + 8 * (v & 7);
+      ok = row < rows && col < K;
+    } else {
+      row = k0 + (v >> 4);
+      col = r0 + 8 * (v & 15);
+      ok = row < K && col < rows;
+    }
+    r[i] = ok ? *reinterpret_cast<const uint4*>(S + (int64_t)row * ld + col) : make_uint4(0, 0, 0, 0);
+  }
+}
+
+template <int TR>
+__device__ __forceinline__ void store_bf16(uint16_t* tile, const uint4 (&r)[4], int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int v = tid + NT * i;
+    const int off = TR ? (v >> 4) * LDT + 8 * (v & 15) : (v >> 3) * LDK + 8 * (v & 7);
+    *reinterpret_cast<uint4*>(tile + off) = r[i];
+  }
+}
+
+// ---- fp32 arena operand (segmented rows), converted to bf16 at the LDS write ----
+// TR = 0: storage row = logical row n (segmented), elements k.   TR = 1: storage row = k (segmented), cols n.
+template <int TR>
+__device__ __forceinline__ void load_f32(float4 (&r)[8], const float* __restrict__ base, const Segs& sg, int rowlen,
+                                         int rows, int K, int r0, int k0, int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int v = tid + NT * i;
+    int srow, col;
+    bool ok;
+    if (!TR) {
+      const int n = r0 + (v >> 3);
+      col = k0 + 8 * (v & 7);
+      ok = n < rows && col < K;
+      srow = n;
+    } else {
+      const int k = k0 + (v >> 4);
+      col = r0 + 8 * (v & 15);
+      ok = k < K && col < rows;
+      srow = k;
+    }
+    if (ok) {
+      const float* p = base + seg_row(sg, srow, rowlen) + col;
+      r[2 * i] = *reinterpret_cast<const float4*>(p);
+      r[2 * i + 1] = *reinterpret_cast<const float4*>(p + 4);
+    } else {
+      r[2 * i] = make_float4(0.f, 0.f, 0.f, 0.f);
+      r[2 * i + 1] = r[2 * i];
+    }
+  }
+}
+
+template <int TR>
+__device__ __forceinline__ void store_f32(uint16_t* tile, const float4 (&r)[8], int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int v = tid + NT * i;
+    const int off = TR ? (v >> 4) * LDT + 8 * (v & 15) : (v >> 3) * LDK + 8 * (v & 7);
+    const float4 a = r[2 * i], b = r[2 * i + 1];
+    uint4 o;
+    o.x = pk2(a.x, a.y); o.y = pk2(a.z, a.w); o.z = pk2(b.x, b.y); o.w = pk2(b.z, b.w);
+    *reinterpret_cast<uint4*>(tile + off) = o;
+  }
+}
+
+template <int A_TR, int B_TR, int B_F32, int EPI>
+__global__ __launch_bounds__(NT) void bgemm_kernel(const Args p) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  // [A buf 0][A buf 1][B buf 0][B buf 1]
+#define SA(b) (smem + (b) * TILE_ELEMS)
+#define SB(b) (smem + (2 + (b)) * TILE_ELEMS)
+
+  // XCD-aware order: the 8 XCDs take blocks round-robin, so give each XCD a contiguous range of
+  // (client, m-tile, n-tile) tiles — the n-tiles of one row block then share A in that XCD's L2.
+  const int total = p.tiles_m * p.tiles_n * p.nclients;
+  int L = blockIdx.x;
+  if ((total & 7) == 0) L = (L & 7) * (total >> 3) + (L >> 3);
+  const int tn = L % p.tiles_n;
+  const int tm = (L / p.tiles_n) % p.tiles_m;
+  const int c = L / (p.tiles_n * p.tiles_m);
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = (wid >> 1) * 64, wn = (wid & 1) * 64;
+
+  const uint16_t* A = p.A + (int64_t)c * p.a_bs;
+  const uint16_t* Bh = B_F32 ? nullptr : (const uint16_t*)p.B + (int64_t)c * p.b_bs;
+  const float* Bf = B_F32 ? (const float*)p.B + (int64_t)c * p.b_bs : nullptr;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  uint4 ra[4];
+  uint4 rbh[4];
+  float4 rbf[8];
+  const int nk = (p.K + BK - 1) / BK;
+
+  load_bf16<A_TR>(ra, A, p.lda, p.M, p.K, m0, 0, tid);
+  if (B_F32) load_f32<B_TR>(rbf, Bf, p.bseg, p.ldb, p.N, p.K, n0, 0, tid);
+  else load_bf16<B_TR>(rbh, Bh, p.ldb, p.N, p.K, n0, 0, tid);
+  store_bf16<A_TR>(SA(0), ra, tid);
+  if (B_F32) store_f32<B_TR>(SB(0), rbf, tid);
+  else store_bf16<B_TR>(SB(0), rbh, tid);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) {   // next tile's global reads fly while this tile's MFMAs run
+      load_bf16<A_TR>(ra, A, p.lda, p.M, p.K, m0, (kt + 1) * BK, tid);
+      if (B_F32) load_f32<B_TR>(rbf, Bf, p.bseg, p.ldb, p.N, p.K, n0, (kt + 1) * BK, tid);
+      else load_bf16<B_TR>(rbh, Bh, p.ldb, p.N, p.K, n0, (kt + 1) * BK, tid);
+    }
+    const uint16_t* ta = SA(cur);
+    const uint16_t* tb = SB(cur);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        af[i] = A_TR ? tr_frag(ta, kk * 32, wm + 16 * i, lane)
+                     : row_frag(ta, wm + 16 * i + (lane & 15), kk * 32 + 8 * (lane >> 4));
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        bfr[j] = B_TR ? tr_frag(tb, kk * 32, wn + 16 * j, lane)
+                      : row_frag(tb, wn + 16 * j + (lane & 15), kk * 32 + 8 * (lane >> 4));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      store_bf16<A_TR>(SA(cur ^ 1), ra, tid);
+      if (B_F32) store_f32<B_TR>(SB(cur ^ 1), rbf, tid);
+      else store_bf16<B_TR>(SB(cur ^ 1), rbh, tid);
+    }
+    __syncthreads();
+  }
+
+  // epilogue: lane owns row m = m0 + wm + 16i + (lane & 15), cols n .. n+3, n = n0 + wn + 16j + 4(lane >> 4)
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int m = m0 + wm + 16 * i + (lane & 15);
+    if (m >= p.M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wn + 16 * j + 4 * (lane >> 4);
+      if (n >= p.N) continue;
+      f32x4 v = acc[i][j];
+      if (EPI == EPI_ACC32) {
+        float* dst = (float*)p.Cp + (int64_t)c * p.c_bs + seg_row(p.cseg, m, p.ldc) + n;
+        float4 o = *reinterpret_cast<float4*>(dst);
+        o.x += v[0]; o.y += v[1]; o.z += v[2]; o.w += v[3];
+        *reinterpret_cast<float4*>(dst) = o;
+      } else {
+        if (p.bias) {
+          const float4 b = *reinterpret_cast<const float4*>(p.bias + (int64_t)c * p.bias_bs + seg_row(p.biasseg, n, 1));
+          v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+        }
+        uint2 o;
+        o.x = pk2(v[0], v[1]);
+        o.y = pk2(v[2], v[3]);
+        *reinterpret_cast<uint2*>((uint16_t*)p.Cp + (int64_t)c * p.c_bs + (int64_t)m * p.ldc + n) = o;
+        if (EPI == EPI_GELU) {
+          // GELU of the bf16-rounded pre-activation (what the backward recomputes from)
+          float r[4];
+          r[0] = bf16_to_f32((uint16_t)(o.x & 0xffff)); r[1] = bf16_to_f32((uint16_t)(o.x >> 16));
+          r[2] = bf16_to_f32((uint16_t)(o.y & 0xffff)); r[3] = bf16_to_f32((uint16_t)(o.y >> 16));
+          uint2 g;
+          g.x = pk2(gelu_erf(r[0]), gelu_erf(r[1]));
+          g.y = pk2(gelu_erf(r[2]), gelu_erf(r[3]));
+          *reinterpret_cast<uint2*>(p.C2 + (int64_t)c * p.c2_bs + (int64_t)m * p.ldc + n) = g;
+        }
+      }
+    }
+  }
+}
+
+#undef SA
+#undef SB
+
+template <int A_TR, int B_TR, int B_F32, int EPI>
+int launch(const Args& a, hipStream_t st) {
+  const int64_t blocks = (int64_t)a.tiles_m * a.tiles_n * a.nclients;
+  if (blocks <= 0 || blocks > 0x7fffffff) return (int)hipErrorInvalidValue;
+  const size_t smem = 4 * TILE_ELEMS * sizeof(uint16_t);   // 72 KiB: two blocks per CU
+  auto kern = bgemm_kernel<A_TR, B_TR, B_F32, EPI>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(NT), smem, st, a);
+  return (int)hipGetLastError();
+}
+
+inline void fill_segs(Segs& s, const int64_t* off, const int* lo, int n) {
+  s.n = n < 1 ? 1 : n;
+  for (int i = 0; i < 4; ++i) s.off[i] = (off && i < n) ? off[i] : 0;
+  for (int i = 0; i < 5; ++i) s.lo[i] = (lo && i <= n) ? lo[i] : 0;
+}
+
+}  // namespace bg
+
+// Host-side contract (checked by the Python wrapper before launch): K % 8 == 0; TR operands'
+// contiguous (column) extent % 8 == 0; N % 4 == 0; ldc % 4 == 0; segment boundaries % 8 == 0;
+// every pointer 16-byte aligned. nseg ≤ 4.
+//
+// y[c] = x[c] · W[c]ᵀ + b[c]   (W, b: fp32 arena segments; y bf16; gelu → y2 = gelu(y))
+FA_EXPORT int fa_bgemm_fwd(const void* x, int64_t x_bs, int ldx, const float* w_base, int64_t w_cs,
+                           const int64_t* w_off, const float* b_base, int64_t b_cs, const int64_t* b_off,
+                           const int* seg_lo, int nseg, void* y, int64_t y_bs, int ldy, void* y2, int C, int M, int N,
+                           int K, hipStream_t stream) {
+  using namespace bg;
+  if (nseg < 1 || nseg > 4) return (int)hipErrorInvalidValue;
+  Args a{};
+  a.A = (const uint16_t*)x; a.a_bs = x_bs; a.lda = ldx;
+  a.B = w_base; a.b_bs = w_cs; a.ldb = K;
+  fill_segs(a.bseg, w_off, seg_lo, nseg);
+  a.Cp = y; a.c_bs = y_bs; a.ldc = ldy;
+  a.bias = b_base; a.bias_bs = b_cs;
+  fill_segs(a.biasseg, b_off, seg_lo, nseg);
+  a.C2 = (uint16_t*)y2; a.c2_bs = y_bs;
+  a.M = M; a.N = N; a.K = K;
+  a.tiles_m = (M + BM - 1) / BM; a.tiles_n = (N + BN - 1) / BN; a.nclients = C;
+  return y2 ? launch<0, 0, 1, EPI_GELU>(a, stream) : launch<0, 0, 1, EPI_BF16>(a, stream);
+}
+
+// dx[c] = dy[c] · W[c]      dy [M][N] bf16, W [N][K] fp32 arena segments (rows n), dx [M][K] bf16
+FA_EXPORT int fa_bgemm_dgrad(const void* dy, int64_t dy_bs, int lddy, const float* w_base, int64_t w_cs,
+                             const int64_t* w_off, const int* seg_lo, int nseg, void* dx, int64_t dx_bs, int lddx, int C,
+                             int M, int N, int K, hipStream_t stream) {
+  using namespace bg;
+  if (nseg < 1 || nseg > 4) return (int)hipErrorInvalidValue;
+  Args a{};
+  // GEMM: D[m][k] = Σ_n dy(m, n) · W(n, k): reduction = n (storage rows of W → TR)
+  a.A = (const uint16_t*)dy; a.a_bs = dy_bs; a.lda = lddy;
+  a.B = w_base; a.b_bs = w_cs; a.ldb = K;
+  fill_segs(a.bseg, w_off, seg_lo, nseg);
+  a.Cp = dx; a.c_bs = dx_bs; a.ldc = lddx;
+  a.M = M; a.N = K; a.K = N;
+  a.tiles_m = (M + BM - 1) / BM; a.tiles_n = (K + BN - 1) / BN; a.nclients = C;
+  return launch<0, 1, 1, EPI_BF16>(a, stream);
+}
+
+// dW[c] += dy[c]ᵀ · x[c]    dy [T][N], x [T][K] bf16; dW [N][K] fp32 gradient-arena segments (rows n)
+FA_EXPORT int fa_bgemm_wgrad(const void* dy, int64_t dy_bs, int lddy, const void* x, int64_t x_bs, int ldx,
+                             float* g_base, int64_t g_cs, const int64_t* g_off, const int* seg_lo, int nseg, int C,
+                             int T, int N, int K, hipStream_t stream) {
+  using namespace bg;
+  if (nseg < 1 || nseg > 4) return (int)hipErrorInvalidValue;
+  Args a{};
+  // GEMM: D[n][k] = Σ_t dy(t, n) · x(t, k): both operands have storage rows along t (TR)
+  a.A = (const uint16_t*)dy; a.a_bs = dy_bs; a.lda = lddy;
+  a.B = x; a.b_bs = x_bs; a.ldb = ldx;
+  a.Cp = g_base; a.c_bs = g_cs; a.ldc = K;
+  fill_segs(a.cseg, g_off, seg_lo, nseg);
+  a.M = N; a.N = K; a.K = T;
+  a.tiles_m = (N + BM - 1) / BM; a.tiles_n = (K + BN - 1) / BN; a.nclients = C;
+  return launch<1, 1, 0, EPI_ACC32>(a, stream);
+}

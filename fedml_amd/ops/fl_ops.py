@@ -39,9 +39,21 @@ def _fn(name, restype=_c.c_int):
     return f
 
 
+# Debug mode: FEDML_AMD_KERNEL_SYNC=1 synchronises after every native launch so an asynchronous
+# device fault is attributed to the kernel that caused it (pair with AMD_SERIALIZE_KERNEL=3 to
+# do the same for library kernels).
+_KERNEL_SYNC = os.environ.get("FEDML_AMD_KERNEL_SYNC", "0") == "1"
+
+
 def _check(rc, name):
     if rc != 0:
         raise RuntimeError(f"{name} failed with HIP error {rc}")
+    if _KERNEL_SYNC:
+        import torch as _t
+        try:
+            _t.cuda.synchronize()
+        except Exception as e:  # noqa: BLE001 - re-raise naming the kernel
+            raise RuntimeError(f"device fault in {name}: {e}") from e
 
 
 def _i64(v):

@@ -202,3 +202,122 @@ def attention(q, k, v, S: int, H: int, kmask: torch.Tensor = None, p: float = 0.
         km = None if kmask is None else kmask.to(torch.uint8).contiguous()
         return _Attention.apply(q, k, v, km, int(S), int(H), float(p), int(seed))
     return _attn_ref(q, k, v, kmask, S, H, p, seed)
+
+
+# ------------------------------------------------------------------------ client-batched linear
+def _segments(views):
+    """(base, client stride, per-segment element offsets, row boundaries) of [C, n_i, ...] fp32
+    arena views that share one client stride (the q/k/v slots of a fused projection)."""
+    base = views[0]
+    cs = base.stride(0)
+    off, lo = [], [0]
+    for v in views:
+        assert v.dtype == torch.float32 and v.stride(0) == cs, "segments must share the client stride"
+        assert v.stride(-1) == 1 and (v.dim() < 3 or v.stride(1) == v.shape[2]), "segment rows must be contiguous"
+        off.append((v.data_ptr() - base.data_ptr()) // 4)
+        lo.append(lo[-1] + v.shape[1])
+    return base, cs, (_c.c_int64 * 4)(*(off + [0] * (4 - len(off)))), (_c.c_int * 5)(*(lo + [0] * (5 - len(lo))))
+
+
+def native_linear_ok(M: int, N: int, K: int, nseg: int = 1) -> bool:
+    """Shapes the batched-GEMM kernels take (16-byte vectors along every contiguous dim)."""
+    return K % 8 == 0 and N % 8 == 0 and 1 <= nseg <= 4 and M > 0
+
+
+class _ClientLinear(torch.autograd.Function):
+    """y[c] = act(x[c] · W[c]ᵀ + b[c]) with W, b read straight from the fp32 client arena (one or
+    several slots), bf16 activations; backward adds dW / db straight into the gradient arena
+    (the leaves' pre-assigned ``.grad`` views) — no dense per-step weight copies either way."""
+
+    @staticmethod
+    def forward(ctx, x, gelu, n_w, *params):
+        ws, bs = params[:n_w], params[n_w:]
+        C, M, K = x.shape
+        N = sum(w.shape[1] for w in ws)
+        wb, wcs, woff, lo = _segments(ws)
+        if bs:
+            bb, bcs, boff, blo = _segments(bs)
+            assert list(blo) == list(lo)
+        else:
+            bb, bcs, boff = None, 0, None
+        y = torch.empty(C, M, N, dtype=torch.bfloat16, device=x.device)
+        y2 = torch.empty_like(y) if gelu else None
+        rc = _fn("fa_bgemm_fwd")(_p(x), _i64(M * K), _c.c_int(K), _p(wb), _i64(wcs), woff, _p(bb), _i64(bcs), boff,
+                                 lo, _c.c_int(len(ws)), _p(y), _i64(M * N), _c.c_int(N), _p(y2), _c.c_int(C),
+                                 _c.c_int(M), _c.c_int(N), _c.c_int(K), _stream(x))
+        _check(rc, "fa_bgemm_fwd")
+        ctx.save_for_backward(x, y if gelu else None)
+        ctx.ws, ctx.bs, ctx.gelu = ws, bs, gelu
+        return y2 if gelu else y
+
+    @staticmethod
+    def backward(ctx, g):
+        x, pre = ctx.saved_tensors
+        ws, bs = ctx.ws, ctx.bs
+        C, M, K = x.shape
+        N = sum(w.shape[1] for w in ws)
+        g = g.contiguous()
+        if ctx.gelu:
+            gp = torch.empty_like(pre)
+            _check(_fn("fa_gelu_bwd")(_p(pre), _p(g), _p(gp), _i64(pre.numel()), _stream(pre)), "fa_gelu_bwd")
+            g = gp
+        dx = None
+        if ctx.needs_input_grad[0]:
+            wb, wcs, woff, lo = _segments(ws)
+            dx = torch.empty_like(x)
+            rc = _fn("fa_bgemm_dgrad")(_p(g), _i64(M * N), _c.c_int(N), _p(wb), _i64(wcs), woff, lo,
+                                       _c.c_int(len(ws)), _p(dx), _i64(M * K), _c.c_int(K), _c.c_int(C), _c.c_int(M),
+                                       _c.c_int(N), _c.c_int(K), _stream(x))
+            _check(rc, "fa_bgemm_dgrad")
+        # weight gradients: into the arena views when the engine pre-assigned them, else returned
+        own = all(w.is_leaf and w.grad is not None for w in ws)
+        if own:
+            gviews = [w.grad for w in ws]
+            out_w = [None] * len(ws)
+        else:
+            dense = torch.zeros(C, N, K, dtype=torch.float32, device=x.device)
+            gviews, out_w, r = [], [], 0
+            for w in ws:
+                v = dense[:, r:r + w.shape[1]]
+                gviews.append(v)
+                out_w.append(v.view_as(w))
+                r += w.shape[1]
+        gb, gcs, goff, glo = _segments(gviews)
+        rc = _fn("fa_bgemm_wgrad")(_p(g), _i64(M * N), _c.c_int(N), _p(x), _i64(M * K), _c.c_int(K), _p(gb), _i64(gcs),
+                                   goff, glo, _c.c_int(len(ws)), _c.c_int(C), _c.c_int(M), _c.c_int(N), _c.c_int(K),
+                                   _stream(x))
+        _check(rc, "fa_bgemm_wgrad")
+        out_b = []
+        if bs:
+            db = g.float().sum(1)                                  # [C, N]
+            r = 0
+            for b in bs:
+                part = db[:, r:r + b.shape[1]]
+                r += b.shape[1]
+                if b.is_leaf and b.grad is not None:
+                    b.grad.add_(part)
+                    out_b.append(None)
+                else:
+                    out_b.append(part.contiguous())
+        return (dx, None, None, *out_w, *out_b)
+
+
+def client_linear(x: torch.Tensor, weights, biases=None, gelu: bool = False) -> torch.Tensor:
+    """Per-client linear over client-stacked activations ``x`` [C, M, K]: ``weights`` is a list of
+    [C, n_i, K] fp32 arena views (concatenated along the output dim), ``biases`` the matching
+    [C, n_i] views or None; ``gelu`` fuses the exact-erf GELU into the epilogue. CUDA → the
+    batched MFMA GEMM kernels (bf16 in/out); CPU → the fp32 PyTorch reference."""
+    weights = list(weights)
+    biases = list(biases) if biases else []
+    C, M, K = x.shape
+    N = sum(w.shape[1] for w in weights)
+    if use_native(x) and native_linear_ok(M, N, K, len(weights)):
+        assert x.dtype == torch.bfloat16
+        return _ClientLinear.apply(x.contiguous(), bool(gelu), len(weights), *weights, *biases)
+    w = torch.cat([t.reshape(C, t.shape[1], K) for t in weights], 1)
+    y = torch.bmm(x.float(), w.float().transpose(1, 2))
+    if biases:
+        y = y + torch.cat(list(biases), 1).float().unsqueeze(1)
+    if gelu:
+        y = torch.nn.functional.gelu(y.to(x.dtype).float())
+    return y.to(x.dtype)

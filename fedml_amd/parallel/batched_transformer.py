@@ -2,9 +2,13 @@
 
 The C clients' private copies of the model run as ONE program instead of C sequential ones:
 
-* every ``nn.Linear`` becomes one batched GEMM ``[C, T, in] × [C, in, out]`` (``torch.baddbmm`` →
-  hipBLASLt, bf16 operands from the fp32 master views of the client arena, fp32 gradients landing
-  in the gradient arena); q/k/v are fused into one GEMM with N = 3·d;
+* every ``nn.Linear`` becomes one client-batched MFMA GEMM ``[C, T, in] × [C, in, out]``
+  (``csrc/bgemm_kernels.hip``: weights read straight from the fp32 client arena and converted to
+  bf16 while staged into LDS, weight gradients added straight into the gradient arena, bias and
+  GELU fused into the epilogue); q/k/v are one GEMM whose weight rows come from three arena slots.
+  (hipBLASLt's strided-batched path fails on these shapes at C=32 — HIPBLAS_STATUS_INTERNAL_ERROR
+  followed by an illegal access in the rocBLAS fallback — and needs a dense bf16 weight copy per
+  step besides);
 * LayerNorm (fused with the residual add and hidden dropout of post-LN blocks), GELU and
   self-attention run the hand-written HIP kernels of ``ops.transformer_ops`` over token-major
   ``[C·B·S, d]`` activations, with per-client gamma/beta;
@@ -99,19 +103,21 @@ class BatchedTransformer:
         self.step_seed = 0
 
     # -------------------------------------------------------------------------------- helpers
-    def _lin(self, v, x, key, dt, weights=None):
-        """x [C, T, in] → [C, T, out] with per-client W [C, out, in] and bias [C, out]."""
+    def _lin(self, v, x, key, dt, weights=None, gelu=False):
+        """x [C, T, in] → [C, T, out] with per-client W [C, out, in] and bias [C, out] read straight
+        from the fp32 arena views (``ops.transformer_ops.client_linear``: one batched MFMA GEMM per
+        linear, weight gradients accumulated into the gradient arena; ``gelu`` fuses the
+        activation into the GEMM epilogue)."""
         if weights is None:
-            w = _bf(v[key + ".weight"], dt)
-            b = _bf(v[key + ".bias"], dt)
+            ws, bs = [v[key + ".weight"]], [v[key + ".bias"]]
         else:
-            w, b = weights
-        return torch.baddbmm(b.unsqueeze(1), x, w.transpose(1, 2))
+            ws, bs = weights
+        return T.client_linear(_bf(x, dt), ws, bs, gelu=gelu)
 
     def _qkv(self, v, x, pre, dt):
-        w = torch.cat([_bf(v[f"{pre}.{n}.weight"], dt) for n in ("q_lin", "k_lin", "v_lin")], 1)
-        b = torch.cat([_bf(v[f"{pre}.{n}.bias"], dt) for n in ("q_lin", "k_lin", "v_lin")], 1)
-        return self._lin(v, x, None, dt, (w, b))
+        names = ("q_lin", "k_lin", "v_lin")
+        return self._lin(v, x, None, dt, ([v[f"{pre}.{n}.weight"] for n in names],
+                                          [v[f"{pre}.{n}.bias"] for n in names]))
 
     def _ln(self, v, key, h, rows_per_client, res=None, p=0.0, seed=0, eps=None):
         d = h.shape[-1]
@@ -151,7 +157,7 @@ class BatchedTransformer:
             sa = self._attn(v, x, pre + ".attention", S, kmask, training, dt, base + 10 * i + 1)
             x = self._ln(v, pre + ".sa_layer_norm", sa.contiguous(), rows, res=x,
                          p=self.p_hidden if training else 0.0, seed=base + 10 * i + 2)
-            f = T.gelu(self._lin(v, x, pre + ".ffn.lin1", dt).contiguous())
+            f = self._lin(v, x, pre + ".ffn.lin1", dt, gelu=True)
             f = self._lin(v, f, pre + ".ffn.lin2", dt)
             x = self._ln(v, pre + ".output_layer_norm", f.contiguous(), rows, res=x,
                          p=self.p_hidden if training else 0.0, seed=base + 10 * i + 3)
@@ -169,9 +175,8 @@ class BatchedTransformer:
         d = self.dim
         patches = _bf(img, dt).reshape(C, B, ch, gh, p, gw, p).permute(0, 1, 3, 5, 2, 4, 6) \
             .reshape(C, B * gh * gw, ch * p * p)
-        pw = _bf(v["patch_embed.proj.weight"].reshape(C, d, ch * p * p), dt)
-        pb = _bf(v["patch_embed.proj.bias"], dt)
-        tok = self._lin(v, patches, None, dt, (pw, pb)).view(C, B, gh * gw, d)
+        pw = v["patch_embed.proj.weight"].reshape(C, d, ch * p * p)
+        tok = self._lin(v, patches, None, dt, ([pw], [v["patch_embed.proj.bias"]])).view(C, B, gh * gw, d)
         cls = _bf(v["cls_token"], dt).view(C, 1, 1, d).expand(C, B, 1, d)
         S = gh * gw + 1
         x = (torch.cat([cls, tok], 2) + _bf(v["pos_embed"], dt).view(C, 1, S, d)).reshape(C, B * S, d).contiguous()
@@ -181,7 +186,7 @@ class BatchedTransformer:
             h = self._ln(v, pre + ".norm1", x, rows)
             x = x + self._attn(v, h, pre + ".attn", S, None, training, dt, base + 10 * i + 1)
             h = self._ln(v, pre + ".norm2", x, rows)
-            f = T.gelu(self._lin(v, h, pre + ".mlp.lin1", dt).contiguous())
+            f = self._lin(v, h, pre + ".mlp.lin1", dt, gelu=True)
             x = x + self._lin(v, f, pre + ".mlp.lin2", dt)
         cls_out = x.view(C, B, S, d)[:, :, 0].contiguous()
         y = self._ln(v, "norm", cls_out, B)

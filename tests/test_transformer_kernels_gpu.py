@@ -126,3 +126,54 @@ def test_batched_transformer_gpu_vs_fp32_modules(kind):
     for c, m in enumerate(models):
         ref = m.eval()(x[c])
         _close(out[c].cpu(), ref, 6e-2)
+
+
+def _arena_views(C, shapes, seed=0):
+    """fp32 [C, P] parameter and gradient arenas with 64-element aligned slots; returns leaf views
+    whose ``.grad`` are gradient-arena views (the engine's layout)."""
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    offs, o = [], 0
+    for s in shapes:
+        offs.append(o)
+        o += (math.prod(s) + 63) // 64 * 64
+    P = o + 64
+    params = (0.05 * torch.randn(C, P, generator=g)).to(dev)
+    grads = torch.zeros(C, P, device=dev)
+    views = []
+    for s, off in zip(shapes, offs):
+        n = math.prod(s)
+        v = params[:, off:off + n].view(C, *s).detach().requires_grad_(True)
+        v.grad = grads[:, off:off + n].view(C, *s)
+        views.append(v)
+    return views
+
+
+@pytest.mark.parametrize("C,M,K,ns,gelu,own", [(3, 200, 768, [768, 768, 768], False, True),
+                                               (2, 16, 72, [136], True, False),
+                                               (4, 130, 256, [1024], True, True),
+                                               (2, 2048, 768, [3072], False, True)])
+def test_client_linear_fwd_bwd(C, M, K, ns, gelu, own):
+    torch.manual_seed(0)
+    vs = _arena_views(C, [(n, K) for n in ns] + [(n,) for n in ns])
+    ws, bs = vs[:len(ns)], vs[len(ns):]
+    if not own:
+        for t in vs:
+            t.grad = None
+    x = torch.randn(C, M, K, device=dev).to(torch.bfloat16).requires_grad_(True)
+    y = T.client_linear(x, ws, bs, gelu=gelu)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    # fp32 reference on the same bf16-rounded operands
+    w32 = [w.detach().to(torch.bfloat16).float().requires_grad_(True) for w in ws]
+    b32 = [b.detach().clone().requires_grad_(True) for b in bs]
+    x32 = x.detach().float().requires_grad_(True)
+    y32 = torch.bmm(x32, torch.cat(w32, 1).transpose(1, 2)) + torch.cat(b32, 1).unsqueeze(1)
+    if gelu:
+        y32 = torch.nn.functional.gelu(y32)
+    y32.backward(gy.float())
+    _close(y, y32, 2e-2)
+    _close(x.grad, x32.grad, 2e-2)
+    for w, wr in zip(ws, w32):
+        _close(w.grad, wr.grad, 2e-2)
+    for b, br in zip(bs, b32):
+        _close(b.grad, br.grad, 2e-2)
