@@ -13,6 +13,7 @@ After local training, ``partial_sum`` emits Σ_c n_c·w_c (+ Σ n_c) for the RCC
 all-reduce.
 """
 import atexit
+import contextlib
 import logging
 import math
 import os
@@ -94,6 +95,8 @@ class ClientBatchEngine:
             if self.tf is None:
                 logging.info("virtual-client engine: sequential per-client path (%s)", e)
         self._seq_views = None
+        self._seq_bufs = None
+        self._active_cache = {}
         self._graphs = {}
         _LIVE_ENGINES.add(self)
         self.use_graphs = self.device.type == "cuda" and os.environ.get("FEDML_AMD_HIP_GRAPHS", "1") != "0"
@@ -167,6 +170,7 @@ class ClientBatchEngine:
             self.step_t.zero_()
         total_loss = torch.zeros((), device=self.device)
         n_steps = 0
+        seq_steps = [0] * C
         for ep in range(int(epochs)):
             order = store.epoch_order(slots, n_max, generator, shuffle)
             for s in range(steps_per_epoch):
@@ -184,16 +188,27 @@ class ClientBatchEngine:
                     x = ops.augment(x.reshape(-1, *x.shape[2:]), seed=int(getattr(self.args, "random_seed", 0)) * 7919
                                     + self._aug_calls, sample_ids=idx.reshape(-1), pad=self.aug_pad,
                                     cutout=self.aug_cutout).view_as(x)
-                active = torch.tensor(active_list, dtype=torch.float32, device=self.device)
+                key_a = tuple(active_list)
+                active = self._active_cache.get(key_a)
+                if active is None:   # cached: a fresh host→device tensor per step would sync the stream
+                    active = self._active_cache[key_a] = torch.tensor(active_list, dtype=torch.float32,
+                                                                      device=self.device)
                 sample_mask = None if uniform else mask.t().contiguous()     # [B, C]
                 if self.native_step is not None and sample_mask is None and self.use_graphs:
                     loss = self._graph_step(x, y, mask, b_c, active, lr, first)
+                elif self.sequential and self.tf is None and self.use_graphs and uniform:
+                    loss = self._seq_graph_step(x, y, b_c, active, lr, first)
                 else:
                     loss = self._step_loss(x, y, mask, b_c, active, sample_mask, use_native_loss)
                     self._optimizer_step(lr, active, first)
                 total_loss += loss.detach()
                 n_steps += 1
                 first = False
+                if self.sequential and self.tf is None:
+                    for c, b in enumerate(b_c):
+                        seq_steps[c] += b > 0
+        if self.sequential and self.tf is None:
+            self._nbt_flush(seq_steps)
         n_real = max(1, sum(1 for n in counts_h if n > 0))
         self.last_loss = total_loss / max(1, n_steps * n_real)   # device scalar: no host sync here
         return self.last_loss
@@ -304,6 +319,55 @@ class ClientBatchEngine:
                 self._seq_views.append(d)
         return self._seq_views
 
+    def _seq_buffer_views(self, c):
+        """Client c's fp32 buffers (BN running statistics) as aliases of the arena that carry their
+        OWN version counters (``set_`` on the arena storage; a ``view``/``detach`` would share the
+        counter of every parameter leaf, so BN's in-place statistics update would invalidate the
+        saved weights); non-fp32 buffers (``num_batches_tracked``) are handed over as copies."""
+        if self._seq_bufs is None:
+            st = self.params.untyped_storage()
+            base = self.params.storage_offset()
+            self._seq_bufs = []
+            for cc in range(self.C):
+                d = {}
+                for sl in self.layout.slots:
+                    if not sl.trainable and sl.dtype == torch.float32:
+                        t = torch.empty(0, dtype=torch.float32, device=self.device)
+                        t.set_(st, base + cc * self.params.stride(0) + sl.offset, sl.shape,
+                               torch.empty(sl.shape, device="meta").stride())
+                        d[sl.key] = t
+                self._seq_bufs.append(d)
+        out = dict(self._seq_bufs[c])
+        for sl in self.layout.slots:
+            if not sl.trainable and sl.key not in out and sl.key in self._nbt_keys:
+                out[sl.key] = None        # counted on the host, added once per round (_nbt_flush)
+            elif not sl.trainable and sl.key not in out:
+                out[sl.key] = self.params[c, sl.offset:sl.offset + sl.numel].view(sl.shape).to(sl.dtype).clone()
+        return out
+
+    @property
+    def _nbt_keys(self):
+        """``num_batches_tracked`` buffers of BN layers that never read it (momentum set): the
+        per-client path passes None for them (no increment kernel per layer and step) and adds
+        each client's step count to the arena copy at the end of ``train``."""
+        if not hasattr(self, "_nbt_keys_cache"):
+            keys = set()
+            for name, m in self.model.named_modules():
+                if isinstance(m, torch.nn.modules.batchnorm._BatchNorm) and m.momentum is not None \
+                        and m.track_running_stats:
+                    keys.add(f"{name}.num_batches_tracked" if name else "num_batches_tracked")
+            self._nbt_keys_cache = keys & {sl.key for sl in self.layout.slots}
+        return self._nbt_keys_cache
+
+    def _nbt_flush(self, steps_per_client):
+        if not self._nbt_keys or not any(steps_per_client):
+            return
+        inc = torch.tensor(steps_per_client, dtype=torch.float32, device=self.device)
+        with torch.no_grad():
+            for sl in self.layout.slots:
+                if sl.key in self._nbt_keys:
+                    self.params[:, sl.offset].add_(inc)
+
     def _buffers_of(self, c):
         out = {}
         for sl in self.layout.slots:
@@ -311,26 +375,96 @@ class ClientBatchEngine:
                 out[sl.key] = self.params[c, sl.offset:sl.offset + sl.numel].view(sl.shape).to(sl.dtype).clone()
         return out
 
-    def _seq_step_loss(self, x, y, b_c):
+    def _seq_step_loss(self, x, y, b_c, zero=False, streams=None):
+        """Clients one after another on the arenas (``streams``: client c on ``streams[c % n]``,
+        forked from and joined back into the current stream).
+
+        Per client: forward in channels-last (MIOpen's implicit-GEMM convolutions are NHWC — NCHW
+        activations cost a transpose kernel per conv and direction), ``autograd.grad`` of the loss
+        and ONE multi-tensor copy of the weight gradients into the gradient-arena rows (instead of
+        a zero fill plus one accumulate kernel per parameter); BN running statistics update in place
+        through arena aliases, ``num_batches_tracked`` is counted on the host (``_nbt_flush``)."""
         views = self._seq_param_views()
-        total = torch.zeros((), device=self.device)
+        if zero:
+            self.grads.zero_()
         amp = self.compute_dtype is not None and self.device.type == "cuda"
+        cl = self.device.type == "cuda" and x.dim() == 5 and os.environ.get("FEDML_AMD_SEQ_CHANNELS_LAST", "1") != "0"
+        cur = torch.cuda.current_stream(self.device) if streams else None
+        losses = torch.zeros(self.C, device=self.device)
         for c, b in enumerate(b_c):
             if b <= 0:
                 continue
-            bufs = self._buffers_of(c)
-            with torch.autocast("cuda", dtype=self.compute_dtype or torch.bfloat16, enabled=amp):
-                out = torch.func.functional_call(self.model, {**views[c], **bufs}, (x[c, :b],))
-            if isinstance(out, tuple):
-                out = out[-1]
-            loss = torch.nn.functional.cross_entropy(out.float().reshape(b, -1), y[c, :b].reshape(b))
-            loss.backward()
-            with torch.no_grad():
-                for sl in self.layout.slots:
-                    if not sl.trainable:
-                        self.params[c, sl.offset:sl.offset + sl.numel].copy_(bufs[sl.key].reshape(-1))
-            total += loss.detach()
-        return total
+            ctx = contextlib.nullcontext()
+            if streams:
+                sc = streams[c % len(streams)]
+                sc.wait_stream(cur)
+                ctx = torch.cuda.stream(sc)
+            with ctx:
+                bufs = self._seq_buffer_views(c)
+                xc = x[c, :b]
+                if cl:
+                    xc = xc.contiguous(memory_format=torch.channels_last)
+                # no autocast weight cache under capture (a graph must not keep casts of live weights)
+                with torch.autocast("cuda", dtype=self.compute_dtype or torch.bfloat16, enabled=amp,
+                                    cache_enabled=not streams):
+                    out = torch.func.functional_call(self.model, {**views[c], **bufs}, (xc,))
+                if isinstance(out, tuple):
+                    out = out[-1]
+                loss = torch.nn.functional.cross_entropy(out.float().reshape(b, -1), y[c, :b].reshape(b))
+                leaves = list(views[c].values())
+                grads = torch.autograd.grad(loss, leaves, allow_unused=True)
+                with torch.no_grad():
+                    dst = [v.grad for v, g in zip(leaves, grads) if g is not None]
+                    src = [g for g in grads if g is not None]
+                    if zero:
+                        torch._foreach_add_(dst, src)
+                    else:
+                        torch._foreach_copy_(dst, src)
+                        for v, g in zip(leaves, grads):
+                            if g is None:
+                                v.grad.zero_()
+                    for sl in self.layout.slots:
+                        if not sl.trainable and sl.dtype != torch.float32 and bufs.get(sl.key) is not None:
+                            self.params[c, sl.offset:sl.offset + sl.numel].copy_(bufs[sl.key].reshape(-1))
+                    losses[c].copy_(loss.detach())
+        if streams:
+            for sc in streams[:min(len(streams), len(b_c))]:
+                cur.wait_stream(sc)
+        return losses.sum()
+
+    def _seq_graph_step(self, x, y, b_c, active, lr, first):
+        """Per-client (wide conv net) local step as ONE HIP graph whose C client branches run on C
+        forked HIP streams: each client's forward/backward is a chain of small library kernels
+        (ResNet-18 at batch 64 leaves most of the 256 CUs idle), so the branches overlap on the
+        device and the graph removes the per-kernel launch cost. Grad zeroing, the C branches and
+        the fused optimizer are one replay. The first occurrence of a geometry runs eagerly (it is
+        the warm-up: library algorithm selection, allocator pools) and is captured right after
+        (capture executes nothing), so every later occurrence — including the once-per-round first
+        step and the ragged last batch — replays."""
+        key = ("seq", tuple(x.shape), tuple(y.shape), tuple(b_c), float(lr), bool(first))
+        ent = self._graphs.get(key)
+        if ent is None:
+            loss = self._seq_step_loss(x, y, b_c, zero=True)
+            self._optimizer_step(lr, active, first)
+            st = {"x": torch.empty_like(x), "y": torch.empty_like(y), "act": torch.empty_like(active)}
+            if not hasattr(self, "_client_streams"):
+                self._client_streams = [torch.cuda.Stream(device=self.device) for _ in range(min(self.C, 16))]
+            s = torch.cuda.Stream(device=self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+                self.grads.zero_()
+                gl = self._seq_step_loss(st["x"], st["y"], b_c, streams=self._client_streams)
+                self._optimizer_step(lr, st["act"], first)
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            self._graphs[key] = (g, st, gl)
+            return loss
+        g, st, loss = ent
+        st["x"].copy_(x, non_blocking=True)
+        st["y"].copy_(y, non_blocking=True)
+        st["act"].copy_(active, non_blocking=True)
+        g.replay()
+        return loss
 
     def _optimizer_step(self, lr, active, first):
         if self.optimizer == "sgd":

@@ -61,3 +61,28 @@ def test_batched_equals_sequential(builder, shape, counts):
         upd_ref = ref[c] - flat
         err = (eng.params[c] - ref[c]).norm() / upd_ref.norm().clamp_min(1e-12)
         assert err < 2e-2, (c, float(err))
+
+
+@pytest.mark.parametrize("counts", [[8, 8], [5, 9, 7]])
+def test_per_client_path_equals_sequential(monkeypatch, counts):
+    """The per-client execution path (wide conv nets): parameters train in the arena rows, BN
+    running statistics update in place through version-counter-independent arena aliases."""
+    monkeypatch.setenv("FEDML_AMD_CLIENT_EXEC", "sequential")
+    torch.manual_seed(0)
+    model = ResNet(Bottleneck, [1, 1, 1], 10)
+    args = Arguments.from_dict({"x": {"client_optimizer": "sgd", "learning_rate": 0.02, "momentum": 0.0}})
+    C = len(counts)
+    eng = ClientBatchEngine(model, C, "cpu", args)
+    # CPU engines never pick the per-client path on their own; force it like a wide conv net would
+    eng.sequential = True
+    flat = eng.layout.flatten(model.state_dict())
+    n = sum(counts)
+    x_all, y_all = torch.randn(n, 3, 16, 16), torch.randint(0, 5, (n,))
+    offs = [sum(counts[:i]) for i in range(C)]
+    eng.load_global(flat)
+    eng.train(DeviceClientStore(x_all, y_all, offs, counts), torch.arange(C), 1, 4, 0.02, shuffle=False)
+    ref = _sequential(model, eng.layout, flat, [x_all[o:o + c] for o, c in zip(offs, counts)],
+                      [y_all[o:o + c] for o, c in zip(offs, counts)], 0.02, 4)
+    for c in range(C):
+        err = (eng.params[c] - ref[c]).norm() / (ref[c] - flat).norm().clamp_min(1e-12)
+        assert err < 2e-2, (c, float(err))
