@@ -3,6 +3,8 @@
 ``fl_ops``   — aggregation (FedAvg weighted sum, MFMA subset aggregation), fused
                multi-client SGD/Adam, FedOpt server step, robust aggregation,
                int8/fp8 quantisation, top-k sparsification, fused CE, confusion matrix.
+``norm_ops`` — GroupNorm (+ReLU) forward/backward, single-model and client-stacked.
+``transformer_ops`` — LayerNorm / GELU / attention / client-batched MFMA GEMM.
 ``nn_ops``   — client-batched (grouped) conv / BN / ReLU / pooling / linear kernels
                used by the virtual-client engine (MFMA implicit GEMM).
 """
@@ -33,6 +35,7 @@ from .fl_ops import (
     mod_sum,
     use_native,
 )
+from .norm_ops import FusedGroupNorm, fuse_group_norm, group_norm
 
 
 def build(force: bool = False):

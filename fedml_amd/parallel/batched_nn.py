@@ -136,13 +136,10 @@ def bbatch_norm(x, C, weight, bias, running_mean, running_var, training, momentu
 
 
 def bgroup_norm(x, C, groups, weight, bias, eps):
-    B = x.shape[0]
-    ch = x.shape[1] // C
-    out = F.group_norm(x.reshape(B * C, ch, *x.shape[2:]), groups, None, None, eps).reshape(x.shape)
-    if weight is not None:
-        shape = (1, C * ch) + (1,) * (x.dim() - 2)
-        out = out * weight.reshape(shape) + bias.reshape(shape)
-    return out
+    """GroupNorm of a client-stacked [B, C·ch, ...] tensor with per-client affine ``[C, ch]``
+    (``ops.group_norm``: HIP kernels on GPU, PyTorch reference on CPU)."""
+    from ..ops.norm_ops import group_norm
+    return group_norm(x, groups, weight, bias, eps, clients=C)
 
 
 def blinear(x, w, b, C):

@@ -94,6 +94,11 @@ class ClientBatchEngine:
                     pass
             if self.tf is None:
                 logging.info("virtual-client engine: sequential per-client path (%s)", e)
+        # GroupNorm layers run the HIP GN kernels on GPU (same parameters / state_dict keys); the
+        # per-client path keeps such nets in NCHW (the GN kernels read contiguous group rows)
+        self._has_gn = any(isinstance(m, torch.nn.GroupNorm) for m in model.modules())
+        if self.device.type == "cuda" and self._has_gn:
+            ops.fuse_group_norm(self.model)
         self._seq_views = None
         self._seq_bufs = None
         self._active_cache = {}
@@ -388,7 +393,8 @@ class ClientBatchEngine:
         if zero:
             self.grads.zero_()
         amp = self.compute_dtype is not None and self.device.type == "cuda"
-        cl = self.device.type == "cuda" and x.dim() == 5 and os.environ.get("FEDML_AMD_SEQ_CHANNELS_LAST", "1") != "0"
+        cl = self.device.type == "cuda" and x.dim() == 5 and not self._has_gn and \
+            os.environ.get("FEDML_AMD_SEQ_CHANNELS_LAST", "1") != "0"
         cur = torch.cuda.current_stream(self.device) if streams else None
         losses = torch.zeros(self.C, device=self.device)
         for c, b in enumerate(b_c):

@@ -36,6 +36,10 @@ def _sequential(model, flat_layout, flat, xs, ys, lr, steps_bs, momentum=0.0):
     (lambda: ResNet(Bottleneck, [1, 1, 1], 10), (3, 16, 16), [8, 8]),
     (lambda: ResNet(Bottleneck, [1, 1, 1], 10), (3, 16, 16), [5, 9, 7]),   # ragged → masked BN + inactive clients
     (lambda: CNN_OriginalFedAvg(True), (1, 28, 28), [6, 6]),
+    # GroupNorm with per-client affine (ops.group_norm, client-stacked)
+    (lambda: torch.nn.Sequential(torch.nn.Conv2d(3, 8, 3, padding=1), torch.nn.GroupNorm(2, 8), torch.nn.ReLU(),
+                                 torch.nn.AdaptiveAvgPool2d(1), torch.nn.Flatten(), torch.nn.Linear(8, 5)),
+     (3, 8, 8), [8, 8, 8]),
 ])
 def test_batched_equals_sequential(builder, shape, counts):
     torch.manual_seed(0)
