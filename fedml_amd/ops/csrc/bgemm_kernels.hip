@@ -120,6 +120,29 @@ __device__ __forceinline__ void load_bf16(uint4 (&r)[4], const uint16_t* __restr
   }
 }
 
+// B operand in bf16 with segmented rows (the bf16 weight shadow of the arena, or a plain [rows][ld]
+// matrix as one segment at offset 0)
+template <int TR>
+__device__ __forceinline__ void load_bf16_seg(uint4 (&r)[4], const uint16_t* __restrict__ base, const Segs& sg,
+                                              int rowlen, int rows, int K, int r0, int k0, int tid) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int v = tid + NT * i;
+    int srow, col;
+    bool ok;
+    if (!TR) {
+      srow = r0 + (v >> 3);
+      col = k0 + 8 * (v & 7);
+      ok = srow < rows && col < K;
+    } else {
+      srow = k0 + (v >> 4);
+      col = r0 + 8 * (v & 15);
+      ok = srow < K && col < rows;
+    }
+    r[i] = ok ? *reinterpret_cast<const uint4*>(base + seg_row(sg, srow, rowlen) + col) : make_uint4(0, 0, 0, 0);
+  }
+}
+
 template <int TR>
 __device__ __forceinline__ void store_bf16(uint16_t* tile, const uint4 (&r)[4], int tid) {
 #pragma unroll
@@ -175,7 +198,7 @@ __device__ __forceinline__ void store_f32(uint16_t* tile, const float4 (&r)[8], 
   }
 }
 
-template <int A_TR, int B_TR, int B_F32, int EPI>
+template <int A_TR, int B_TR, int B_F32, int EPI, int BSEG>
 __global__ __launch_bounds__(NT) void bgemm_kernel(const Args p) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
   // [A buf 0][A buf 1][B buf 0][B buf 1]
@@ -196,7 +219,8 @@ __global__ __launch_bounds__(NT) void bgemm_kernel(const Args p) {
   const int wm = (wid >> 1) * 64, wn = (wid & 1) * 64;
 
   const uint16_t* A = p.A + (int64_t)c * p.a_bs;
-  const uint16_t* Bh = B_F32 ? nullptr : (const uint16_t*)p.B + (int64_t)c * p.b_bs;
+  // a single-segment bf16 B is a plain matrix at offset off[0] (no per-vector segment search)
+  const uint16_t* Bh = B_F32 ? nullptr : (const uint16_t*)p.B + (int64_t)c * p.b_bs + (BSEG ? 0 : p.bseg.off[0]);
   const float* Bf = B_F32 ? (const float*)p.B + (int64_t)c * p.b_bs : nullptr;
 
   f32x4 acc[4][4];
@@ -212,7 +236,8 @@ __global__ __launch_bounds__(NT) void bgemm_kernel(const Args p) {
 
   load_bf16<A_TR>(ra, A, p.lda, p.M, p.K, m0, 0, tid);
   if (B_F32) load_f32<B_TR>(rbf, Bf, p.bseg, p.ldb, p.N, p.K, n0, 0, tid);
-  else load_bf16<B_TR>(rbh, Bh, p.ldb, p.N, p.K, n0, 0, tid);
+  else if (BSEG) load_bf16_seg<B_TR>(rbh, Bh, p.bseg, p.ldb, p.N, p.K, n0, 0, tid);
+      else load_bf16<B_TR>(rbh, Bh, p.ldb, p.N, p.K, n0, 0, tid);
   store_bf16<A_TR>(SA(0), ra, tid);
   if (B_F32) store_f32<B_TR>(SB(0), rbf, tid);
   else store_bf16<B_TR>(SB(0), rbh, tid);
@@ -224,6 +249,7 @@ __global__ __launch_bounds__(NT) void bgemm_kernel(const Args p) {
     if (more) {   // next tile's global reads fly while this tile's MFMAs run
       load_bf16<A_TR>(ra, A, p.lda, p.M, p.K, m0, (kt + 1) * BK, tid);
       if (B_F32) load_f32<B_TR>(rbf, Bf, p.bseg, p.ldb, p.N, p.K, n0, (kt + 1) * BK, tid);
+      else if (BSEG) load_bf16_seg<B_TR>(rbh, Bh, p.bseg, p.ldb, p.N, p.K, n0, (kt + 1) * BK, tid);
       else load_bf16<B_TR>(rbh, Bh, p.ldb, p.N, p.K, n0, (kt + 1) * BK, tid);
     }
     const uint16_t* ta = SA(cur);
@@ -299,7 +325,7 @@ int launch(const Args& a, hipStream_t st) {
   const int64_t blocks = (int64_t)a.tiles_m * a.tiles_n * a.nclients;
   if (blocks <= 0 || blocks > 0x7fffffff) return (int)hipErrorInvalidValue;
   const size_t smem = 4 * TILE_ELEMS * sizeof(uint16_t);   // 72 KiB: two blocks per CU
-  auto kern = bgemm_kernel<A_TR, B_TR, B_F32, EPI>;
+  auto kern = (!B_F32 && a.bseg.n > 1) ? bgemm_kernel<A_TR, B_TR, B_F32, EPI, 1> : bgemm_kernel<A_TR, B_TR, B_F32, EPI, 0>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(NT), smem, st, a);
   return (int)hipGetLastError();
@@ -317,8 +343,9 @@ inline void fill_segs(Segs& s, const int64_t* off, const int* lo, int n) {
 // contiguous (column) extent % 8 == 0; N % 4 == 0; ldc % 4 == 0; segment boundaries % 8 == 0;
 // every pointer 16-byte aligned. nseg ≤ 4.
 //
-// y[c] = x[c] · W[c]ᵀ + b[c]   (W, b: fp32 arena segments; y bf16; gelu → y2 = gelu(y))
-FA_EXPORT int fa_bgemm_fwd(const void* x, int64_t x_bs, int ldx, const float* w_base, int64_t w_cs,
+// y[c] = x[c] · W[c]ᵀ + b[c]   (W: fp32 arena segments, or — w_bf16 — the same segments of the arena's
+// bf16 shadow; b: fp32 arena segments; y bf16; gelu → y2 = gelu(y))
+FA_EXPORT int fa_bgemm_fwd(const void* x, int64_t x_bs, int ldx, const void* w_base, int w_bf16, int64_t w_cs,
                            const int64_t* w_off, const float* b_base, int64_t b_cs, const int64_t* b_off,
                            const int* seg_lo, int nseg, void* y, int64_t y_bs, int ldy, void* y2, int C, int M, int N,
                            int K, hipStream_t stream) {
@@ -334,11 +361,12 @@ FA_EXPORT int fa_bgemm_fwd(const void* x, int64_t x_bs, int ldx, const float* w_
   a.C2 = (uint16_t*)y2; a.c2_bs = y_bs;
   a.M = M; a.N = N; a.K = K;
   a.tiles_m = (M + BM - 1) / BM; a.tiles_n = (N + BN - 1) / BN; a.nclients = C;
+  if (w_bf16) return y2 ? launch<0, 0, 0, EPI_GELU>(a, stream) : launch<0, 0, 0, EPI_BF16>(a, stream);
   return y2 ? launch<0, 0, 1, EPI_GELU>(a, stream) : launch<0, 0, 1, EPI_BF16>(a, stream);
 }
 
 // dx[c] = dy[c] · W[c]      dy [M][N] bf16, W [N][K] fp32 arena segments (rows n), dx [M][K] bf16
-FA_EXPORT int fa_bgemm_dgrad(const void* dy, int64_t dy_bs, int lddy, const float* w_base, int64_t w_cs,
+FA_EXPORT int fa_bgemm_dgrad(const void* dy, int64_t dy_bs, int lddy, const void* w_base, int w_bf16, int64_t w_cs,
                              const int64_t* w_off, const int* seg_lo, int nseg, void* dx, int64_t dx_bs, int lddx, int C,
                              int M, int N, int K, hipStream_t stream) {
   using namespace bg;
@@ -351,7 +379,7 @@ FA_EXPORT int fa_bgemm_dgrad(const void* dy, int64_t dy_bs, int lddy, const floa
   a.Cp = dx; a.c_bs = dx_bs; a.ldc = lddx;
   a.M = M; a.N = K; a.K = N;
   a.tiles_m = (M + BM - 1) / BM; a.tiles_n = (K + BN - 1) / BN; a.nclients = C;
-  return launch<0, 1, 1, EPI_BF16>(a, stream);
+  return w_bf16 ? launch<0, 1, 0, EPI_BF16>(a, stream) : launch<0, 1, 1, EPI_BF16>(a, stream);
 }
 
 // dW[c] += dy[c]ᵀ · x[c]    dy [T][N], x [T][K] bf16; dW [N][K] fp32 gradient-arena segments (rows n)
@@ -364,6 +392,7 @@ FA_EXPORT int fa_bgemm_wgrad(const void* dy, int64_t dy_bs, int lddy, const void
   // GEMM: D[n][k] = Σ_t dy(t, n) · x(t, k): both operands have storage rows along t (TR)
   a.A = (const uint16_t*)dy; a.a_bs = dy_bs; a.lda = lddy;
   a.B = x; a.b_bs = x_bs; a.ldb = ldx;
+  fill_segs(a.bseg, nullptr, nullptr, 1);   // plain [T][K] storage: one segment at offset 0
   a.Cp = g_base; a.c_bs = g_cs; a.ldc = K;
   fill_segs(a.cseg, g_off, seg_lo, nseg);
   a.M = N; a.N = K; a.K = T;

@@ -206,15 +206,16 @@ def attention(q, k, v, S: int, H: int, kmask: torch.Tensor = None, p: float = 0.
 
 # ------------------------------------------------------------------------ client-batched linear
 def _segments(views):
-    """(base, client stride, per-segment element offsets, row boundaries) of [C, n_i, ...] fp32
-    arena views that share one client stride (the q/k/v slots of a fused projection)."""
+    """(base, client stride, per-segment element offsets, row boundaries) of [C, n_i, ...] arena
+    views (fp32, or the bf16 shadow) sharing one client stride (the q/k/v slots of a fused projection)."""
     base = views[0]
     cs = base.stride(0)
+    es = base.element_size()
     off, lo = [], [0]
     for v in views:
-        assert v.dtype == torch.float32 and v.stride(0) == cs, "segments must share the client stride"
+        assert v.dtype == base.dtype and v.stride(0) == cs, "segments must share dtype and client stride"
         assert v.stride(-1) == 1 and (v.dim() < 3 or v.stride(1) == v.shape[2]), "segment rows must be contiguous"
-        off.append((v.data_ptr() - base.data_ptr()) // 4)
+        off.append((v.data_ptr() - base.data_ptr()) // es)
         lo.append(lo[-1] + v.shape[1])
     return base, cs, (_c.c_int64 * 4)(*(off + [0] * (4 - len(off)))), (_c.c_int * 5)(*(lo + [0] * (5 - len(lo))))
 
@@ -230,11 +231,15 @@ class _ClientLinear(torch.autograd.Function):
     (the leaves' pre-assigned ``.grad`` views) — no dense per-step weight copies either way."""
 
     @staticmethod
-    def forward(ctx, x, gelu, n_w, *params):
+    def forward(ctx, x, gelu, n_w, shadows, *params):
         ws, bs = params[:n_w], params[n_w:]
         C, M, K = x.shape
         N = sum(w.shape[1] for w in ws)
-        wb, wcs, woff, lo = _segments(ws)
+        # bf16 shadow of the weights (refreshed once per step by the engine) when given: half the
+        # B-operand bytes and no per-tile fp32→bf16 conversion; otherwise the fp32 arena itself
+        wsrc = shadows if shadows else ws
+        wb, wcs, woff, lo = _segments(wsrc)
+        wh = 1 if wsrc[0].dtype == torch.bfloat16 else 0
         if bs:
             bb, bcs, boff, blo = _segments(bs)
             assert list(blo) == list(lo)
@@ -242,12 +247,13 @@ class _ClientLinear(torch.autograd.Function):
             bb, bcs, boff = None, 0, None
         y = torch.empty(C, M, N, dtype=torch.bfloat16, device=x.device)
         y2 = torch.empty_like(y) if gelu else None
-        rc = _fn("fa_bgemm_fwd")(_p(x), _i64(M * K), _c.c_int(K), _p(wb), _i64(wcs), woff, _p(bb), _i64(bcs), boff,
+        rc = _fn("fa_bgemm_fwd")(_p(x), _i64(M * K), _c.c_int(K), _p(wb), _c.c_int(wh), _i64(wcs), woff, _p(bb),
+                                 _i64(bcs), boff,
                                  lo, _c.c_int(len(ws)), _p(y), _i64(M * N), _c.c_int(N), _p(y2), _c.c_int(C),
                                  _c.c_int(M), _c.c_int(N), _c.c_int(K), _stream(x))
         _check(rc, "fa_bgemm_fwd")
         ctx.save_for_backward(x, y if gelu else None)
-        ctx.ws, ctx.bs, ctx.gelu = ws, bs, gelu
+        ctx.ws, ctx.bs, ctx.gelu, ctx.wsrc = ws, bs, gelu, wsrc
         return y2 if gelu else y
 
     @staticmethod
@@ -263,9 +269,10 @@ class _ClientLinear(torch.autograd.Function):
             g = gp
         dx = None
         if ctx.needs_input_grad[0]:
-            wb, wcs, woff, lo = _segments(ws)
+            wb, wcs, woff, lo = _segments(ctx.wsrc)
+            wh = 1 if ctx.wsrc[0].dtype == torch.bfloat16 else 0
             dx = torch.empty_like(x)
-            rc = _fn("fa_bgemm_dgrad")(_p(g), _i64(M * N), _c.c_int(N), _p(wb), _i64(wcs), woff, lo,
+            rc = _fn("fa_bgemm_dgrad")(_p(g), _i64(M * N), _c.c_int(N), _p(wb), _c.c_int(wh), _i64(wcs), woff, lo,
                                        _c.c_int(len(ws)), _p(dx), _i64(M * K), _c.c_int(K), _c.c_int(C), _c.c_int(M),
                                        _c.c_int(N), _c.c_int(K), _stream(x))
             _check(rc, "fa_bgemm_dgrad")
@@ -299,21 +306,26 @@ class _ClientLinear(torch.autograd.Function):
                     out_b.append(None)
                 else:
                     out_b.append(part.contiguous())
-        return (dx, None, None, *out_w, *out_b)
+        return (dx, None, None, None, *out_w, *out_b)
 
 
-def client_linear(x: torch.Tensor, weights, biases=None, gelu: bool = False) -> torch.Tensor:
+def client_linear(x: torch.Tensor, weights, biases=None, gelu: bool = False, shadows=None) -> torch.Tensor:
     """Per-client linear over client-stacked activations ``x`` [C, M, K]: ``weights`` is a list of
     [C, n_i, K] fp32 arena views (concatenated along the output dim), ``biases`` the matching
-    [C, n_i] views or None; ``gelu`` fuses the exact-erf GELU into the epilogue. CUDA → the
-    batched MFMA GEMM kernels (bf16 in/out); CPU → the fp32 PyTorch reference."""
+    [C, n_i] views or None; ``gelu`` fuses the exact-erf GELU into the epilogue. ``shadows``: the
+    same slots of a bf16 copy of the arena (current for this step) — the GEMMs then read bf16
+    weights; gradients always land in the fp32 arena. CUDA → the batched MFMA GEMM kernels (bf16
+    in/out); CPU → the fp32 PyTorch reference."""
     weights = list(weights)
     biases = list(biases) if biases else []
     C, M, K = x.shape
     N = sum(w.shape[1] for w in weights)
     if use_native(x) and native_linear_ok(M, N, K, len(weights)):
         assert x.dtype == torch.bfloat16
-        return _ClientLinear.apply(x.contiguous(), bool(gelu), len(weights), *weights, *biases)
+        sh = tuple(shadows) if shadows else None
+        if sh is not None:
+            assert len(sh) == len(weights) and all(t.shape == w.shape for t, w in zip(sh, weights))
+        return _ClientLinear.apply(x.contiguous(), bool(gelu), len(weights), sh, *weights, *biases)
     w = torch.cat([t.reshape(C, t.shape[1], K) for t in weights], 1)
     y = torch.bmm(x.float(), w.float().transpose(1, 2))
     if biases:

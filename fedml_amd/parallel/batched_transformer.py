@@ -101,6 +101,7 @@ class BatchedTransformer:
         if self.dim != 64 * self.heads:
             raise UnsupportedTransformer(f"head dim {self.dim // self.heads} != 64")
         self.step_seed = 0
+        self._sh = None
 
     # -------------------------------------------------------------------------------- helpers
     def _lin(self, v, x, key, dt, weights=None, gelu=False):
@@ -108,16 +109,20 @@ class BatchedTransformer:
         from the fp32 arena views (``ops.transformer_ops.client_linear``: one batched MFMA GEMM per
         linear, weight gradients accumulated into the gradient arena; ``gelu`` fuses the
         activation into the GEMM epilogue)."""
+        sh = None
         if weights is None:
             ws, bs = [v[key + ".weight"]], [v[key + ".bias"]]
+            if self._sh is not None:
+                sh = [self._sh[key + ".weight"]]
         else:
-            ws, bs = weights
-        return T.client_linear(_bf(x, dt), ws, bs, gelu=gelu)
+            ws, bs, sh = weights
+        return T.client_linear(_bf(x, dt), ws, bs, gelu=gelu, shadows=sh)
 
     def _qkv(self, v, x, pre, dt):
         names = ("q_lin", "k_lin", "v_lin")
+        sh = None if self._sh is None else [self._sh[f"{pre}.{n}.weight"] for n in names]
         return self._lin(v, x, None, dt, ([v[f"{pre}.{n}.weight"] for n in names],
-                                          [v[f"{pre}.{n}.bias"] for n in names]))
+                                          [v[f"{pre}.{n}.bias"] for n in names], sh))
 
     def _ln(self, v, key, h, rows_per_client, res=None, p=0.0, seed=0, eps=None):
         d = h.shape[-1]
@@ -134,7 +139,11 @@ class BatchedTransformer:
 
     # -------------------------------------------------------------------------------- forward
     def forward(self, v: Dict[str, torch.Tensor], x: torch.Tensor, training: bool = True,
-                dtype: Optional[torch.dtype] = torch.bfloat16) -> torch.Tensor:
+                dtype: Optional[torch.dtype] = torch.bfloat16,
+                shadow: Optional[Dict[str, torch.Tensor]] = None) -> torch.Tensor:
+        """``shadow``: key → bf16 view of the same slot in a bf16 copy of the arena that is current
+        for this step (the linears' GEMMs then read bf16 weights)."""
+        self._sh = shadow
         self.step_seed = (self.step_seed + 1) & 0x7FFFFFFF
         base = self.step_seed * 1000003
         if self.kind == "distilbert":
@@ -176,7 +185,8 @@ class BatchedTransformer:
         patches = _bf(img, dt).reshape(C, B, ch, gh, p, gw, p).permute(0, 1, 3, 5, 2, 4, 6) \
             .reshape(C, B * gh * gw, ch * p * p)
         pw = v["patch_embed.proj.weight"].reshape(C, d, ch * p * p)
-        tok = self._lin(v, patches, None, dt, ([pw], [v["patch_embed.proj.bias"]])).view(C, B, gh * gw, d)
+        psh = None if self._sh is None else [self._sh["patch_embed.proj.weight"].reshape(C, d, ch * p * p)]
+        tok = self._lin(v, patches, None, dt, ([pw], [v["patch_embed.proj.bias"]], psh)).view(C, B, gh * gw, d)
         cls = _bf(v["cls_token"], dt).view(C, 1, 1, d).expand(C, B, 1, d)
         S = gh * gw + 1
         x = (torch.cat([cls, tok], 2) + _bf(v["pos_embed"], dt).view(C, 1, S, d)).reshape(C, B * S, d).contiguous()

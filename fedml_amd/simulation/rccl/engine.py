@@ -225,7 +225,8 @@ class ClientBatchEngine:
             row_scale = mask.to(torch.float32) / bc.view(-1, 1)
             return self.native_step.step(self.params, self.grads, x, y, row_scale, active)
         if self.tf is not None:
-            out = self.tf.forward(self.views, x, training=True, dtype=self.compute_dtype)    # [C, B, K]
+            out = self.tf.forward(self.views, x, training=True, dtype=self.compute_dtype,
+                                  shadow=self._bf16_shadow())                                # [C, B, K]
         elif not self.sequential:
             try:
                 out = self.interp.run(self.views, x, training=True, sample_mask=sample_mask, active=active,
@@ -252,6 +253,19 @@ class ClientBatchEngine:
         if self.interp is not None:
             self.interp.flush_deferred()
         return loss.detach()
+
+    def _bf16_shadow(self):
+        """bf16 copy of the parameter arena, refreshed once per step (one streaming cast kernel):
+        the transformer GEMMs read their weights from it — half the bytes of the fp32 masters and
+        no per-tile conversion; gradients and optimizer state stay fp32."""
+        if self.device.type != "cuda" or self.compute_dtype != torch.bfloat16:
+            return None
+        if getattr(self, "_shadow", None) is None:
+            self._shadow = torch.empty(self.params.shape, dtype=torch.bfloat16, device=self.device)
+            self._shadow_views = {s.key: self._shadow[:, s.offset:s.offset + s.numel].view(self.C, *s.shape)
+                                  for s in self.layout.slots}
+        ops.cast_bf16(self.params, out=self._shadow)
+        return self._shadow_views
 
     # ---------------------------------------------------------------- HIP-graph local step
     def _graph_step(self, x, y, mask, b_c, active, lr, first):

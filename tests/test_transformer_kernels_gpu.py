@@ -139,28 +139,32 @@ def _arena_views(C, shapes, seed=0):
     P = o + 64
     params = (0.05 * torch.randn(C, P, generator=g)).to(dev)
     grads = torch.zeros(C, P, device=dev)
-    views = []
+    views, shadows = [], []
+    shadow = params.to(torch.bfloat16)
     for s, off in zip(shapes, offs):
         n = math.prod(s)
         v = params[:, off:off + n].view(C, *s).detach().requires_grad_(True)
         v.grad = grads[:, off:off + n].view(C, *s)
         views.append(v)
-    return views
+        shadows.append(shadow[:, off:off + n].view(C, *s))
+    return views, shadows
 
 
+@pytest.mark.parametrize("shadow", [False, True])
 @pytest.mark.parametrize("C,M,K,ns,gelu,own", [(3, 200, 768, [768, 768, 768], False, True),
                                                (2, 16, 72, [136], True, False),
                                                (4, 130, 256, [1024], True, True),
                                                (2, 2048, 768, [3072], False, True)])
-def test_client_linear_fwd_bwd(C, M, K, ns, gelu, own):
+def test_client_linear_fwd_bwd(C, M, K, ns, gelu, own, shadow):
     torch.manual_seed(0)
-    vs = _arena_views(C, [(n, K) for n in ns] + [(n,) for n in ns])
+    vs, shs = _arena_views(C, [(n, K) for n in ns] + [(n,) for n in ns])
     ws, bs = vs[:len(ns)], vs[len(ns):]
+    sh = shs[:len(ns)] if shadow else None
     if not own:
         for t in vs:
             t.grad = None
     x = torch.randn(C, M, K, device=dev).to(torch.bfloat16).requires_grad_(True)
-    y = T.client_linear(x, ws, bs, gelu=gelu)
+    y = T.client_linear(x, ws, bs, gelu=gelu, shadows=sh)
     gy = torch.randn_like(y)
     y.backward(gy)
     # fp32 reference on the same bf16-rounded operands
