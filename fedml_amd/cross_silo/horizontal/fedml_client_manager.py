@@ -9,8 +9,10 @@ import json
 import logging
 import platform
 import threading
+import time
 
 from ...core.distributed import ClientManager, Message
+from ...core.fault import FaultInjector
 from ...core.mlops import MLOpsMetrics, MLOpsProfilerEvent
 from ..message_define import MyMessage
 from .fedml_server_manager import inject_connection_ready, parse_client_ids
@@ -27,6 +29,7 @@ class FedMLClientManager(ClientManager):
         self.has_sent_online_msg = False
         self._stop_stats = threading.Event()
         self.final_model = None
+        self.faults = FaultInjector(args)
 
     def run(self):
         inject_connection_ready(self)
@@ -80,6 +83,7 @@ class FedMLClientManager(ClientManager):
         m = Message(MyMessage.MSG_TYPE_C2S_SEND_MODEL_TO_SERVER, self.client_real_id, receive_id)
         m.add_params(MyMessage.MSG_ARG_KEY_MODEL_PARAMS, weights)
         m.add_params(MyMessage.MSG_ARG_KEY_NUM_SAMPLES, local_sample_num)
+        m.add_params(MyMessage.MSG_ARG_KEY_ROUND_INDEX, self.round_idx)
         self.send_message(m)
 
     def send_client_status(self, receive_id, status="ONLINE"):
@@ -103,4 +107,11 @@ class FedMLClientManager(ClientManager):
         prof.log_event_started("train", event_value=str(self.round_idx))
         weights, n = self.trainer.train(self.round_idx)
         prof.log_event_ended("train", event_value=str(self.round_idx))
+        # injected faults (core.fault): a dropped client never uploads, a delayed one uploads late
+        if self.faults.dropped(self.round_idx, self.client_real_id):
+            logging.info("client %d: injected dropout in round %d", self.client_real_id, self.round_idx)
+            return
+        d = self.faults.delay(self.round_idx, self.client_real_id)
+        if d > 0:
+            time.sleep(d)
         self.send_model_to_server(0, weights, n)

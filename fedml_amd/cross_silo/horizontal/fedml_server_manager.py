@@ -6,9 +6,15 @@ index) to the round's selected clients. Each round: collect ``C2S_SEND_MODEL_TO_
 the selected clients, aggregate (flat-arena kernel), test, report round info, send
 ``S2C_SYNC_MODEL_TO_CLIENT``. After ``comm_round`` rounds the server stops (clients stop after
 the final sync, as in the reference, and additionally on ``S2C_FINISH``).
+
+Deadline rounds (not in the reference, which waits for every client forever): with
+``round_timeout`` (seconds) the server closes a round when the deadline passes and aggregates the
+uploads that arrived (at least ``min_clients_per_round``, default 1), re-weighted by their sample
+counts; uploads tagged with an older round index are discarded.
 """
 import json
 import logging
+import threading
 import time
 
 from ...core.distributed import Message, ServerManager
@@ -49,6 +55,11 @@ class FedMLServerManager(ServerManager):
         self.round_times = []
         self._selected = []
         self._started = False
+        to = getattr(args, "round_timeout", None)
+        self.round_timeout = float(to) if to not in (None, "", 0, 0.0) else None
+        self.min_clients = max(1, int(getattr(args, "min_clients_per_round", 1) or 1))
+        self._timer = None
+        self.partial_rounds = []     # (round, #arrived, #selected) of rounds closed by the deadline
 
     def run(self):
         inject_connection_ready(self)
@@ -61,6 +72,39 @@ class FedMLServerManager(ServerManager):
                                               self.handle_message_client_status_update)
         self.register_message_receive_handler(MyMessage.MSG_TYPE_C2S_SEND_MODEL_TO_SERVER,
                                               self.handle_message_receive_model_from_client)
+        self.register_message_receive_handler(MyMessage.MSG_TYPE_ROUND_DEADLINE, self.handle_round_deadline)
+
+    # ---- deadline rounds ---------------------------------------------------------------------------
+    def _arm_deadline(self):
+        if self.round_timeout is None:
+            return
+        if self._timer is not None:
+            self._timer.cancel()
+        r = self.round_idx
+
+        def fire():   # delivered through the receive loop: handlers never run concurrently
+            m = Message(MyMessage.MSG_TYPE_ROUND_DEADLINE, self.rank, self.rank)
+            m.add_params(MyMessage.MSG_ARG_KEY_ROUND_INDEX, r)
+            self.com_manager.deliver(m)
+        self._timer = threading.Timer(self.round_timeout, fire)
+        self._timer.daemon = True
+        self._timer.start()
+
+    def handle_round_deadline(self, msg):
+        if int(msg.get(MyMessage.MSG_ARG_KEY_ROUND_INDEX)) != self.round_idx:
+            return
+        arrived = sum(1 for v in self.aggregator.flag_client_model_uploaded_dict.values() if v)
+        if arrived < self.min_clients:
+            logging.warning("round %d deadline: %d/%d uploads (< %d); extending", self.round_idx, arrived,
+                            len(self._selected), self.min_clients)
+            self._arm_deadline()
+            return
+        logging.warning("round %d deadline: aggregating %d of %d uploads", self.round_idx, arrived,
+                        len(self._selected))
+        self.partial_rounds.append((self.round_idx, arrived, len(self._selected)))
+        for i in self.aggregator.flag_client_model_uploaded_dict:
+            self.aggregator.flag_client_model_uploaded_dict[i] = False
+        self._complete_round()
 
     def handle_connection_ready(self, msg):
         MLOpsMetrics.get_instance().report_server_training_status(getattr(self.args, "run_id", "0"),
@@ -91,6 +135,7 @@ class FedMLServerManager(ServerManager):
         for cid, silo in zip(ids, silos):
             self._send(MyMessage.MSG_TYPE_S2C_INIT_CONFIG, cid, g, silo)
         MLOpsProfilerEvent.get_instance().log_event_started("server.wait", event_value=str(self.round_idx))
+        self._arm_deadline()
 
     def _send(self, mtype, receiver, params, silo):
         m = Message(mtype, self.get_sender_id(), receiver)
@@ -101,6 +146,10 @@ class FedMLServerManager(ServerManager):
 
     def handle_message_receive_model_from_client(self, msg):
         sender = int(msg.get(MyMessage.MSG_ARG_KEY_SENDER))
+        r = msg.get(MyMessage.MSG_ARG_KEY_ROUND_INDEX)
+        if (r is not None and int(r) != self.round_idx) or sender not in self._selected:
+            logging.info("discarding stale upload of client %d (round %s, server at %d)", sender, r, self.round_idx)
+            return
         prof = MLOpsProfilerEvent.get_instance()
         prof.log_event_ended("comm_c2s", event_value=str(self.round_idx), event_edge_id=sender)
         self.aggregator.add_local_trained_result(self._selected.index(sender),
@@ -108,6 +157,13 @@ class FedMLServerManager(ServerManager):
                                                  msg.get(MyMessage.MSG_ARG_KEY_NUM_SAMPLES))
         if not self.aggregator.check_whether_all_receive():
             return
+        self._complete_round()
+
+    def _complete_round(self):
+        if self._timer is not None:
+            self._timer.cancel()
+            self._timer = None
+        prof = MLOpsProfilerEvent.get_instance()
         prof.log_event_ended("server.wait", event_value=str(self.round_idx))
         prof.log_event_started("aggregate", event_value=str(self.round_idx))
         g = self.aggregator.aggregate()
@@ -137,6 +193,7 @@ class FedMLServerManager(ServerManager):
         for cid, silo in zip(ids, silos):
             self._send(MyMessage.MSG_TYPE_S2C_SYNC_MODEL_TO_CLIENT, cid, g, silo)
         prof.log_event_started("server.wait", event_value=str(self.round_idx))
+        self._arm_deadline()
 
 
 def inject_connection_ready(mgr):

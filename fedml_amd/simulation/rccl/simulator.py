@@ -24,6 +24,7 @@ import torch
 
 from ... import ops
 from ...core.arena import ParamLayout
+from ...core.fault import FaultInjector
 from ...core.mlops import MLOpsMetrics
 from ...core.schedule import pack_clients_to_gpus
 from ...core.tracing import tracer
@@ -76,6 +77,8 @@ class RCCLSimulator:
         self.residual = torch.zeros(self.K_total, self.layout.size, dtype=torch.float32, device=self.device) \
             if self.compression else None
         self.upload_bytes: List[int] = []
+        self.faults = FaultInjector(args)
+        self.dropped_clients: List[int] = []
         self.history: Dict[int, dict] = {}
         self.round_idx = 0
 
@@ -106,6 +109,13 @@ class RCCLSimulator:
                               generator=self.gen, shuffle=bool(getattr(args, "shuffle", True)), valid_slots=valid)
         with tr.span("round.aggregate"):
             w = torch.where(valid, self.store.counts[slots].to(torch.float32), torch.zeros(self.C, device=self.device))
+            if self.faults.active:
+                # lost uploads (dropout / missed deadline, core.fault): survivors are re-weighted
+                alive = self.faults.survivors(round_idx, mine)
+                self.dropped_clients.append(int((~alive).sum()))
+                keep = torch.zeros(self.C, dtype=torch.float32)
+                keep[:len(mine)] = torch.from_numpy(alive.astype("float32"))
+                w = w * keep.to(self.device)
             self._robust_preaggregate(w)
             if self.compression:
                 ids = list(mine) + [0] * (self.C - len(mine))
@@ -116,7 +126,9 @@ class RCCLSimulator:
                 self.engine.partial_sum(w, out=self.partial)
             comm.all_reduce_flat(self.partial)
             total = self.partial[self.layout.size:self.layout.size + 1]
-            avg = self.partial[:self.layout.size] / total
+            avg = self.partial[:self.layout.size] / total.clamp_min(1e-12)
+            if self.faults.active:   # every upload lost: the global model stays as it was
+                avg = torch.where(total > 0, avg, self.global_flat)
             if self.server_opt is not None:
                 self.server_opt.step(self.global_flat, avg)
             else:

@@ -75,3 +75,54 @@ def test_hierarchical_cross_silo_processes(tmp_path):
     assert codes == [0] * len(cmds), codes
     g = torch.load(out, weights_only=True)
     assert all(torch.isfinite(v.float()).all() for v in g.values())
+
+
+def test_cross_silo_deadline_round_with_dead_silo():
+    """A silo that never uploads (client_dropout_ids) no longer stalls the federation: with
+    round_timeout the server closes each round at the deadline and aggregates the survivors."""
+    from fedml_amd.cross_silo import Client, Server
+    a = _args(client_num_in_total=3, client_num_per_round=3, client_id_list="[1, 2, 3]", worker_num=4, comm_round=2,
+              round_timeout=1.5, client_dropout_ids="[3]")
+    dev, ds, m = fedml_amd._prepare(fedml_amd.init(copy.copy(a)))
+    router = LoopbackRouter(4)
+    out = {}
+
+    def srv():
+        s = Server(copy.copy(a), dev, ds, copy.deepcopy(m), comm=router)
+        out["w"] = s.run()
+        out["partial"] = list(s.manager.partial_rounds)
+
+    def cli(rank):
+        b = copy.copy(a)
+        b.rank = rank
+        Client(b, dev, ds, copy.deepcopy(m), comm=router).run()
+
+    ts = [threading.Thread(target=srv)] + [threading.Thread(target=cli, args=(r,)) for r in (1, 2, 3)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert "w" in out, "server did not finish"
+    assert out["partial"] == [(0, 2, 3), (1, 2, 3)]
+    assert all(torch.isfinite(v.float()).all() for v in out["w"].values())
+
+
+def test_fault_injector_and_rccl_sim_dropout():
+    from fedml_amd.core.fault import FaultInjector
+    f = FaultInjector(dropout_prob=0.3, delay_mean=1.0, deadline=2.0, seed=7)
+    s1 = f.survivors(5, list(range(200)))
+    assert (s1 == f.survivors(5, list(range(200)))).all()          # deterministic per (seed, round, client)
+    assert 0.45 < s1.mean() < 0.8                                   # ≈ 0.7 · P(Exp(1) ≤ 2) ≈ 0.61
+    # the RCCL simulator re-weights the survivors (all dropped → global model unchanged)
+    from fedml_amd.simulation.rccl.simulator import RCCLSimulator
+    from fedml_amd.models.linear.lr import LogisticRegression
+    from fedml_amd.simulation.rccl.client_store import DeviceClientStore
+    torch.manual_seed(0)
+    args = Arguments.from_dict({"x": {"federated_optimizer": "FedAvg", "client_num_in_total": 4,
+                                      "client_num_per_round": 4, "comm_round": 1, "epochs": 1, "batch_size": 8,
+                                      "client_optimizer": "sgd", "learning_rate": 0.1, "client_dropout_prob": 1.0}})
+    store = DeviceClientStore(torch.randn(32, 10), torch.randint(0, 3, (32,)), [0, 8, 16, 24], [8] * 4)
+    sim = RCCLSimulator(args, torch.device("cpu"), None, LogisticRegression(10, 3), store=store)
+    g0 = sim.global_flat.clone()
+    sim.run(1)
+    assert torch.equal(sim.global_flat, g0) and sim.dropped_clients == [4]
