@@ -320,6 +320,29 @@ __global__ __launch_bounds__(NT) void bgemm_kernel(const Args p) {
 #undef SA
 #undef SB
 
+// db[c][n] += Σ_m g[c][m][n] for bf16 g [C][M][ldg]: each thread owns 2 adjacent columns of a
+// 256-row chunk (4-byte coalesced loads), one fp32 atomic pair per thread into the (segmented)
+// fp32 gradient arena — no fp32 copy of g and no separate accumulate kernel.
+__global__ __launch_bounds__(256) void bias_grad_kernel(const uint16_t* __restrict__ g, int64_t g_bs, int ldg,
+                                                        float* __restrict__ out, int64_t o_cs, Segs seg, int M, int N,
+                                                        int rows_per_block) {
+  const int c = blockIdx.z;
+  const int n = 2 * (blockIdx.x * 256 + threadIdx.x);
+  if (n >= N) return;
+  const int m0 = blockIdx.y * rows_per_block;
+  const int m1 = min(M, m0 + rows_per_block);
+  const uint16_t* gp = g + (int64_t)c * g_bs + n;
+  float a0 = 0.f, a1 = 0.f;
+  for (int m = m0; m < m1; ++m) {
+    const uint32_t v = *reinterpret_cast<const uint32_t*>(gp + (int64_t)m * ldg);
+    a0 += bf16_to_f32((uint16_t)(v & 0xffff));
+    a1 += bf16_to_f32((uint16_t)(v >> 16));
+  }
+  float* o = out + (int64_t)c * o_cs;
+  atomicAdd(o + seg_row(seg, n, 1), a0);
+  atomicAdd(o + seg_row(seg, n + 1, 1), a1);
+}
+
 template <int A_TR, int B_TR, int B_F32, int EPI>
 int launch(const Args& a, hipStream_t st) {
   const int64_t blocks = (int64_t)a.tiles_m * a.tiles_n * a.nclients;
@@ -398,4 +421,18 @@ FA_EXPORT int fa_bgemm_wgrad(const void* dy, int64_t dy_bs, int lddy, const void
   a.M = N; a.N = K; a.K = T;
   a.tiles_m = (N + BM - 1) / BM; a.tiles_n = (K + BN - 1) / BN; a.nclients = C;
   return launch<1, 1, 0, EPI_ACC32>(a, stream);
+}
+
+// db[c] += Σ_m dy[c][m][:]   dy bf16 [C][M][N] (N even, segment boundaries even); db: fp32 arena segments
+FA_EXPORT int fa_bias_grad(const void* dy, int64_t dy_bs, int lddy, float* o_base, int64_t o_cs, const int64_t* o_off,
+                           const int* seg_lo, int nseg, int C, int M, int N, hipStream_t stream) {
+  using namespace bg;
+  if (nseg < 1 || nseg > 4 || (N & 1) || C <= 0 || M <= 0 || C > 65535) return (int)hipErrorInvalidValue;
+  Segs sg;
+  fill_segs(sg, o_off, seg_lo, nseg);
+  const int rpb = 128;
+  dim3 grid((unsigned)((N / 2 + 255) / 256), (unsigned)((M + rpb - 1) / rpb), (unsigned)C);
+  hipLaunchKernelGGL(bias_grad_kernel, grid, dim3(256), 0, stream, (const uint16_t*)dy, dy_bs, lddy, o_base, o_cs, sg,
+                     M, N, rpb);
+  return (int)hipGetLastError();
 }

@@ -296,16 +296,22 @@ class _ClientLinear(torch.autograd.Function):
         _check(rc, "fa_bgemm_wgrad")
         out_b = []
         if bs:
-            db = g.float().sum(1)                                  # [C, N]
-            r = 0
-            for b in bs:
-                part = db[:, r:r + b.shape[1]]
-                r += b.shape[1]
-                if b.is_leaf and b.grad is not None:
-                    b.grad.add_(part)
-                    out_b.append(None)
-                else:
-                    out_b.append(part.contiguous())
+            # column sums of g straight into the gradient arena (or a dense [C, N] when not owned)
+            own_b = all(b.is_leaf and b.grad is not None for b in bs)
+            if own_b:
+                bviews = [b.grad for b in bs]
+                out_b = [None] * len(bs)
+            else:
+                dense_b = torch.zeros(C, N, dtype=torch.float32, device=x.device)
+                bviews, r = [], 0
+                for b in bs:
+                    bviews.append(dense_b[:, r:r + b.shape[1]])
+                    out_b.append(dense_b[:, r:r + b.shape[1]])
+                    r += b.shape[1]
+            bb, bcs, boff, blo = _segments(bviews)
+            rc = _fn("fa_bias_grad")(_p(g), _i64(M * N), _c.c_int(N), _p(bb), _i64(bcs), boff, blo,
+                                     _c.c_int(len(bs)), _c.c_int(C), _c.c_int(M), _c.c_int(N), _stream(x))
+            _check(rc, "fa_bias_grad")
         return (dx, None, None, None, *out_w, *out_b)
 
 
