@@ -90,8 +90,27 @@ class Scheduler:
 scheduler = Scheduler
 
 
+def _lpt_balanced(counts, n_gpus, speed, cap):
+    """Longest-processing-time greedy under a per-GPU client cap: O(C log C), within 4/3 of the
+    optimum makespan (Graham) — the per-round path, where the branch-and-bound's tens of ms per
+    round would be serial host time on every rank."""
+    order = sorted(range(len(counts)), key=lambda i: (-counts[i], i))
+    load = [0.0] * n_gpus
+    n = [0] * n_gpus
+    out = [[] for _ in range(n_gpus)]
+    for i in order:
+        best = min((g for g in range(n_gpus) if n[g] < cap[g]), key=lambda g: ((load[g] + counts[i]) / speed[g], g))
+        out[best].append(i)
+        load[best] += counts[i]
+        n[best] += 1
+    return [sorted(o) for o in out]
+
+
+_PACK_CACHE = {}
+
+
 def pack_clients_to_gpus(sample_counts, n_gpus, gpu_speed=None, gpu_mem_bytes=None, bytes_per_client=0.0,
-                         balance_counts=True):
+                         balance_counts=True, exact=False):
     """Assign clients to GPUs minimising the max per-GPU work (samples × speed).
 
     With ``balance_counts`` the assignment is additionally constrained to give each GPU
@@ -101,6 +120,30 @@ def pack_clients_to_gpus(sample_counts, n_gpus, gpu_speed=None, gpu_mem_bytes=No
     Returns a list of client-index lists, one per GPU.
     """
     c = len(sample_counts)
+    # Per-round fast paths (the simulator packs every round on every rank): equal counts → contiguous
+    # balanced chunks; otherwise the LPT greedy, memoised per (counts, GPUs). ``exact`` runs the
+    # native branch-and-bound (fr_schedule) instead.
+    if balance_counts and gpu_mem_bytes is None and not exact:
+        counts = [float(v) for v in sample_counts]
+        sp = [1.0] * n_gpus if gpu_speed is None else [float(v) for v in gpu_speed]
+        key = (tuple(counts), n_gpus, tuple(sp))
+        hit = _PACK_CACHE.get(key)
+        if hit is not None:
+            return [list(v) for v in hit]
+        if len(set(counts)) <= 1 and len(set(sp)) <= 1:
+            q, r = divmod(c, n_gpus)
+            out, lo = [], 0
+            for g in range(n_gpus):
+                hi = lo + q + (1 if g < r else 0)
+                out.append(list(range(lo, hi)))
+                lo = hi
+        else:
+            cap = [int(np.ceil(c / n_gpus))] * n_gpus
+            out = _lpt_balanced(counts, n_gpus, sp, cap)
+        if len(_PACK_CACHE) > 4096:
+            _PACK_CACHE.clear()
+        _PACK_CACHE[key] = [tuple(v) for v in out]
+        return out
     speed = np.ones(n_gpus) if gpu_speed is None else np.asarray(gpu_speed, dtype=np.float64)
     if gpu_mem_bytes is None:
         mem = np.full(n_gpus, np.inf)
