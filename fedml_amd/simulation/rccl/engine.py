@@ -122,6 +122,11 @@ class ClientBatchEngine:
                 mode == "sequential" or (mode == "auto" and self.device.type == "cuda" and _is_wide_convnet(model))):
             logging.info("virtual-client engine: per-client sequential execution (wide conv net)")
             self.sequential = True
+            # MIOpen picks convolution solutions by heuristics unless a find-db entry exists; on a fresh
+            # machine that costs ~40 % of the round. Benchmark mode runs Find once per shape during the
+            # first (eager, uncaptured) step of each geometry; the captured graphs then replay the winners.
+            if os.environ.get("FEDML_AMD_MIOPEN_FIND", "1") != "0":
+                torch.backends.cudnn.benchmark = True
         self._build_views()
         self.global_ref = None
         self.loss_history: List[float] = []
