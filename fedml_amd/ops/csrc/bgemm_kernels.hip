@@ -21,6 +21,7 @@
 // The MFMA computes the transposed tile D[n][m], so each lane owns 4 consecutive output columns
 // of one row: 8-byte bf16 / 16-byte fp32 epilogue accesses, bias as one float4.
 #include "common.h"
+#include <cstdlib>
 
 namespace bg {
 
@@ -198,12 +199,15 @@ __device__ __forceinline__ void store_f32(uint16_t* tile, const float4 (&r)[8], 
   }
 }
 
-template <int A_TR, int B_TR, int B_F32, int EPI, int BSEG>
-__global__ __launch_bounds__(NT) void bgemm_kernel(const Args p) {
+// DB = 1: double-buffered LDS (72 KiB, one barrier per K-step, 2 blocks/CU).
+// DB = 0: single LDS buffer (36 KiB, two barriers per K-step) at 3 waves/SIMD → 3 blocks/CU; the
+//         next tile still streams into registers under the current tile's MFMAs.
+template <int A_TR, int B_TR, int B_F32, int EPI, int BSEG, int DB>
+__global__ __launch_bounds__(NT, 3) void bgemm_kernel(const Args p) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-  // [A buf 0][A buf 1][B buf 0][B buf 1]
-#define SA(b) (smem + (b) * TILE_ELEMS)
-#define SB(b) (smem + (2 + (b)) * TILE_ELEMS)
+  // DB: [A buf 0][A buf 1][B buf 0][B buf 1]      !DB: [A][B]
+#define SA(b) (smem + (DB ? (b) : 0) * TILE_ELEMS)
+#define SB(b) (smem + (DB ? (2 + (b)) : 1) * TILE_ELEMS)
 
   // XCD-aware order: the 8 XCDs take blocks round-robin, so give each XCD a contiguous range of
   // (client, m-tile, n-tile) tiles — the n-tiles of one row block then share A in that XCD's L2.
@@ -270,6 +274,7 @@ __global__ __launch_bounds__(NT) void bgemm_kernel(const Args p) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
+    if (!DB && more) __syncthreads();   // every wave is done reading the single buffer
     if (more) {
       store_bf16<A_TR>(SA(cur ^ 1), ra, tid);
       if (B_F32) store_f32<B_TR>(SB(cur ^ 1), rbf, tid);
@@ -347,8 +352,14 @@ template <int A_TR, int B_TR, int B_F32, int EPI>
 int launch(const Args& a, hipStream_t st) {
   const int64_t blocks = (int64_t)a.tiles_m * a.tiles_n * a.nclients;
   if (blocks <= 0 || blocks > 0x7fffffff) return (int)hipErrorInvalidValue;
-  const size_t smem = 4 * TILE_ELEMS * sizeof(uint16_t);   // 72 KiB: two blocks per CU
-  auto kern = (!B_F32 && a.bseg.n > 1) ? bgemm_kernel<A_TR, B_TR, B_F32, EPI, 1> : bgemm_kernel<A_TR, B_TR, B_F32, EPI, 0>;
+  static const int db = [] {
+    const char* e = getenv("FEDML_AMD_BGEMM_DB");
+    return e ? atoi(e) : 0;
+  }();
+  const size_t smem = (db ? 4 : 2) * TILE_ELEMS * sizeof(uint16_t);   // 72 KiB (2 blocks/CU) | 36 KiB (3)
+  const bool seg = !B_F32 && a.bseg.n > 1;
+  auto kern = db ? (seg ? bgemm_kernel<A_TR, B_TR, B_F32, EPI, 1, 1> : bgemm_kernel<A_TR, B_TR, B_F32, EPI, 0, 1>)
+                 : (seg ? bgemm_kernel<A_TR, B_TR, B_F32, EPI, 1, 0> : bgemm_kernel<A_TR, B_TR, B_F32, EPI, 0, 0>);
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(NT), smem, st, a);
   return (int)hipGetLastError();
