@@ -253,6 +253,27 @@ __device__ __forceinline__ bf16x8_mf lds8(const uint16_t* p) { return __builtin_
 __device__ __forceinline__ bf16x8_mf g8(const uint16_t* p) { return __builtin_bit_cast(bf16x8_mf, *(const uint4*)p); }
 __device__ __forceinline__ bf16x8_mf zero8() { return __builtin_bit_cast(bf16x8_mf, make_uint4(0, 0, 0, 0)); }
 
+typedef short v4i16_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4i16_t lds_v4i16_t;
+
+// MFMA operand fragment "8 consecutive rows row0 + 8·(lane>>4) + j of column col0 + (lane & 15)" of a
+// ROW-MAJOR LDS tile (pitch ld elements) via gfx950's transposing LDS read ds_read_b64_tr_b16: the
+// k-strided operands of P·V, dS·K, Pᵀ·dO and dSᵀ·Q come straight from the row-major K/V/Q/dO
+// images — no transposed copies staged with 2-byte LDS stores.
+__device__ __forceinline__ bf16x8_mf tr8(const uint16_t* tile, int ld, int row0, int col0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const uint16_t* a0 = tile + (row0 + 8 * g + q) * ld + col0 + 4 * p;
+  const v4i16_t r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16_t*)(a0));
+  const v4i16_t r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16_t*)(a0 + 4 * ld));
+  union {
+    short s[8];
+    bf16x8_mf b;
+  } u;
+  u.s[0] = r0[0]; u.s[1] = r0[1]; u.s[2] = r0[2]; u.s[3] = r0[3];
+  u.s[4] = r1[0]; u.s[5] = r1[1]; u.s[6] = r1[2]; u.s[7] = r1[3];
+  return u.b;
+}
+
 // stage rows [r0, r0+nrows) of one head's 64 columns into LDS, row-major [nrows][KST]
 __device__ __forceinline__ void stage_rows(uint16_t* dst, const uint16_t* src, int ld, int r0, int nrows, int S) {
   for (int i = threadIdx.x; i < nrows * 8; i += blockDim.x) {
@@ -262,24 +283,9 @@ __device__ __forceinline__ void stage_rows(uint16_t* dst, const uint16_t* src, i
     *(uint4*)(dst + r * KST + ch * 8) = v;
   }
 }
-// stage the same rows transposed: dst[dim][row] with row stride tst
-__device__ __forceinline__ void stage_rows_t(uint16_t* dst, int tst, const uint16_t* src, int ld, int r0, int nrows,
-                                             int S) {
-  for (int i = threadIdx.x; i < nrows * 8; i += blockDim.x) {
-    const int r = i >> 3, ch = i & 7;
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (r0 + r < S) v = *(const uint4*)(src + (size_t)(r0 + r) * ld + ch * 8);
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      dst[(ch * 8 + 2 * j) * tst + r] = (uint16_t)(w[j] & 0xffff);
-      dst[(ch * 8 + 2 * j + 1) * tst + r] = (uint16_t)(w[j] >> 16);
-    }
-  }
-}
-
-// Forward: grid (ceil(S/64), H, CB), 4 waves, wave w owns query rows 64·bx + 16w + [0,16).
-// Whole key range in LDS (SP = padded S), exact softmax over the row in registers.
+// Forward: grid (H, CB), 4 waves. K and V of the (sequence, head) are staged ONCE (row-major) and the
+// workgroup loops over 64-query chunks; wave w owns query rows q0 + 16w + [0,16). Whole key range in
+// LDS (SP = padded S), exact softmax over the row in registers.
 template <int SP>
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restrict__ q, int ldq,
                                                        const uint16_t* __restrict__ k, int ldk,
@@ -291,87 +297,92 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
   constexpr int NB = SP / 16;
   constexpr int VST = SP + 8;
   __shared__ __attribute__((aligned(16))) uint16_t Ks[SP * KST];
-  __shared__ __attribute__((aligned(16))) uint16_t Vt[64 * VST];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[SP * KST];
   __shared__ __attribute__((aligned(16))) uint16_t Ps[4 * 16 * VST];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int h = blockIdx.y, cb = blockIdx.z;
+  const int h = blockIdx.x, cb = blockIdx.y;
   const size_t tok0 = (size_t)cb * S;
   stage_rows(Ks, k + tok0 * ldk + h * 64, ldk, 0, SP, S);
-  stage_rows_t(Vt, VST, v + tok0 * ldv + h * 64, ldv, 0, SP, S);
-  const int qr = blockIdx.x * 64 + w * 16 + (lane & 15);  // A-operand row of this lane
-  bf16x8_mf qf[2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t)
-    qf[t] = qr < S ? g8(q + (tok0 + qr) * ldq + h * 64 + 32 * t + 8 * (lane >> 4)) : zero8();
-  __syncthreads();
+  stage_rows(Vs, v + tok0 * ldv + h * 64, ldv, 0, SP, S);
   const float c2 = scale * kLog2e;
-  f32x4 sc[NB];
-#pragma unroll
-  for (int nb = 0; nb < NB; ++nb) {
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[t], lds8(Ks + (nb * 16 + (lane & 15)) * KST + 32 * t + 8 * (lane >> 4)),
-                                                     acc, 0, 0, 0);
-    const int key = nb * 16 + (lane & 15);
-    const bool valid = key < S && (kmask == nullptr || kmask[tok0 + key] != 0);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) acc[r] = valid ? acc[r] * c2 : -INFINITY;
-    sc[nb] = acc;
-  }
-  float m[4], l[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    float mx = -INFINITY;
-#pragma unroll
-    for (int nb = 0; nb < NB; ++nb) mx = fmaxf(mx, sc[nb][r]);
-#pragma unroll
-    for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
-    m[r] = mx;
-    l[r] = 0.f;
-  }
-  const int qbase = blockIdx.x * 64 + w * 16 + 4 * (lane >> 4);  // C-layout query row of reg 0
   const uint32_t bh = (uint32_t)(cb * H + h);
   uint16_t* P = Ps + w * 16 * VST;
+  bool kval[NB];
 #pragma unroll
   for (int nb = 0; nb < NB; ++nb) {
     const int key = nb * 16 + (lane & 15);
+    kval[nb] = key < S && (kmask == nullptr || kmask[tok0 + key] != 0);
+  }
+  for (int q0 = 0; q0 < S; q0 += 64) {
+    const int qr = q0 + w * 16 + (lane & 15);  // A-operand row of this lane
+    bf16x8_mf qf[2];
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float p = m[r] == -INFINITY ? 0.f : exp2f(sc[nb][r] - m[r]);
-      l[r] += p;
-      if (thr) p = drop_keep(seed, bh * 65536u + (uint32_t)(qbase + r), (uint32_t)key, thr) ? p * dscale : 0.f;
-      P[(4 * (lane >> 4) + r) * VST + key] = f32_to_bf16(p);
+    for (int t = 0; t < 2; ++t)
+      qf[t] = qr < S ? g8(q + (tok0 + qr) * ldq + h * 64 + 32 * t + 8 * (lane >> 4)) : zero8();
+    __syncthreads();   // staging done (first chunk) / previous chunk's P reads done
+    f32x4 sc[NB];
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[t], lds8(Ks + (nb * 16 + (lane & 15)) * KST + 32 * t + 8 * (lane >> 4)),
+                                                       acc, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r] = kval[nb] ? acc[r] * c2 : -INFINITY;
+      sc[nb] = acc;
     }
-  }
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-#pragma unroll
-    for (int off = 1; off < 16; off <<= 1) l[r] += __shfl_xor(l[r], off, 64);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int db = 0; db < 4; ++db) {
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int kt = 0; kt < SP / 32; ++kt)
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(P + (lane & 15) * VST + kt * 32 + 8 * (lane >> 4)),
-                                                     lds8(Vt + (db * 16 + (lane & 15)) * VST + kt * 32 + 8 * (lane >> 4)),
-                                                     acc, 0, 0, 0);
+    float m[4], l[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int qrow = qbase + r;
-      if (qrow < S) {
-        const float val = l[r] > 0.f ? acc[r] / l[r] : 0.f;
-        o[(tok0 + qrow) * ldo + h * 64 + db * 16 + (lane & 15)] = f32_to_bf16(val);
+      float mx = -INFINITY;
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) mx = fmaxf(mx, sc[nb][r]);
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+      m[r] = mx;
+      l[r] = 0.f;
+    }
+    const int qbase = q0 + w * 16 + 4 * (lane >> 4);  // C-layout query row of reg 0
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      const int key = nb * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float p = m[r] == -INFINITY ? 0.f : exp2f(sc[nb][r] - m[r]);
+        l[r] += p;
+        if (thr) p = drop_keep(seed, bh * 65536u + (uint32_t)(qbase + r), (uint32_t)key, thr) ? p * dscale : 0.f;
+        P[(4 * (lane >> 4) + r) * VST + key] = f32_to_bf16(p);
       }
     }
-  }
-  if ((lane & 15) == 0) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int qrow = qbase + r;
-      if (qrow < S) lse2[((size_t)cb * H + h) * S + qrow] = l[r] > 0.f ? m[r] + log2f(l[r]) : INFINITY;
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) l[r] += __shfl_xor(l[r], off, 64);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kt = 0; kt < SP / 32; ++kt)
+        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(P + (lane & 15) * VST + kt * 32 + 8 * (lane >> 4)),
+                                                       tr8(Vs, KST, kt * 32, db * 16, lane), acc, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qrow = qbase + r;
+        if (qrow < S) {
+          const float val = l[r] > 0.f ? acc[r] / l[r] : 0.f;
+          o[(tok0 + qrow) * ldo + h * 64 + db * 16 + (lane & 15)] = f32_to_bf16(val);
+        }
+      }
+    }
+    if ((lane & 15) == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qrow = qbase + r;
+        if (qrow < S) lse2[((size_t)cb * H + h) * S + qrow] = l[r] > 0.f ? m[r] + log2f(l[r]) : INFINITY;
+      }
     }
   }
 }
@@ -408,7 +419,6 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const uint16_t* __rest
                                                           float scale, uint32_t thr, float dscale, uint32_t seed) {
   __shared__ __attribute__((aligned(16))) uint16_t Ks[64 * KST];
   __shared__ __attribute__((aligned(16))) uint16_t Vs[64 * KST];
-  __shared__ __attribute__((aligned(16))) uint16_t Kt[64 * KST];
   __shared__ __attribute__((aligned(16))) uint16_t dSs[4 * 16 * KST];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int h = blockIdx.y, cb = blockIdx.z;
@@ -439,7 +449,6 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const uint16_t* __rest
     __syncthreads();
     stage_rows(Ks, k + tok0 * ldk + h * 64, ldk, k0, 64, S);
     stage_rows(Vs, v + tok0 * ldv + h * 64, ldv, k0, 64, S);
-    stage_rows_t(Kt, KST, k + tok0 * ldk + h * 64, ldk, k0, 64, S);
     __syncthreads();
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb) {
@@ -466,8 +475,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const uint16_t* __rest
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
         acc[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(dS + (lane & 15) * KST + kt * 32 + 8 * (lane >> 4)),
-                                                          lds8(Kt + (db * 16 + (lane & 15)) * KST + kt * 32 + 8 * (lane >> 4)),
-                                                          acc[db], 0, 0, 0);
+                                                          tr8(Ks, KST, kt * 32, db * 16, lane), acc[db], 0, 0, 0);
   }
 #pragma unroll
   for (int db = 0; db < 4; ++db)
@@ -490,8 +498,6 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const uint16_t* __res
                                                            float scale, uint32_t thr, float dscale, uint32_t seed) {
   __shared__ __attribute__((aligned(16))) uint16_t Qs[64 * KST];
   __shared__ __attribute__((aligned(16))) uint16_t dOs[64 * KST];
-  __shared__ __attribute__((aligned(16))) uint16_t Qt[64 * KST];
-  __shared__ __attribute__((aligned(16))) uint16_t dOt[64 * KST];
   __shared__ __attribute__((aligned(16))) uint16_t Pst[4 * 16 * KST];
   __shared__ __attribute__((aligned(16))) uint16_t dSt[4 * 16 * KST];
   __shared__ float Ls[64], Dsh[64];
@@ -524,8 +530,6 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const uint16_t* __res
     __syncthreads();
     stage_rows(Qs, q + tok0 * ldq + h * 64, ldq, q0, 64, S);
     stage_rows(dOs, dout + tok0 * lddo + h * 64, lddo, q0, 64, S);
-    stage_rows_t(Qt, KST, q + tok0 * ldq + h * 64, ldq, q0, 64, S);
-    stage_rows_t(dOt, KST, dout + tok0 * lddo + h * 64, lddo, q0, 64, S);
     if (threadIdx.x < 64) {
       const int qq = q0 + threadIdx.x;
       Ls[threadIdx.x] = qq < S ? lse2[bhS + qq] : INFINITY;
@@ -564,9 +568,10 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const uint16_t* __res
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
         const int ao = (lane & 15) * KST + kt * 32 + 8 * (lane >> 4);
-        const int bo = (db * 16 + (lane & 15)) * KST + kt * 32 + 8 * (lane >> 4);
-        adv[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(Pw + ao), lds8(dOt + bo), adv[db], 0, 0, 0);
-        adk[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(dSw + ao), lds8(Qt + bo), adk[db], 0, 0, 0);
+        adv[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(Pw + ao), tr8(dOs, KST, kt * 32, db * 16, lane),
+                                                          adv[db], 0, 0, 0);
+        adk[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(dSw + ao), tr8(Qs, KST, kt * 32, db * 16, lane),
+                                                          adk[db], 0, 0, 0);
       }
   }
 #pragma unroll
@@ -605,7 +610,7 @@ template <int SP>
 int launch_attn_fwd(const uint16_t* q, int ldq, const uint16_t* k, int ldk, const uint16_t* v, int ldv, uint16_t* o,
                     int ldo, const uint8_t* kmask, float* lse2, int CB, int S, int H, float scale, uint32_t thr,
                     float dscale, uint32_t seed, hipStream_t st) {
-  hipLaunchKernelGGL(attn_fwd_kernel<SP>, dim3((S + 63) / 64, H, CB), dim3(256), 0, st, q, ldq, k, ldk, v, ldv, o,
+  hipLaunchKernelGGL(attn_fwd_kernel<SP>, dim3(H, CB), dim3(256), 0, st, q, ldq, k, ldk, v, ldv, o,
                      ldo, kmask, lse2, S, H, scale, thr, dscale, seed);
   return (int)hipGetLastError();
 }
