@@ -190,7 +190,10 @@ class ClientBatchEngine:
                 if bmax == 0:
                     break
                 active_list = [1.0 if b > 0 else 0.0 for b in b_c]
-                uniform = all(b == bmax for b in b_c)
+                # clients without samples this step (padding slots of a GPU that hosts fewer clients
+                # than C, exhausted partitions) are masked by ``active`` and zero row scales, so they do
+                # not break uniformity: the fast native / graph-captured paths stay in use
+                uniform = all(b == bmax for b in b_c if b > 0)
                 idx = order[:, lo:lo + bmax]
                 x, y, mask = store.gather(idx)
                 if self.augment and x.dim() == 5:

@@ -316,3 +316,34 @@ def test_multistream_graph_seq_step_matches_eager(momentum):
     init = ParamLayout.from_module(model).flatten(model.state_dict(), device=DEV)
     assert abs(l0 - l1) / abs(l0) < 1e-3
     assert float((p0 - p1).norm() / (p0 - init).norm()) < 1e-3
+
+
+def test_padding_slot_keeps_native_graph_path():
+    """A GPU hosting fewer clients than C (8-GPU run: 12 of 13 slots valid) stays on the captured
+    native step: the padding slot is inactive (unchanged parameters), the valid clients match eager."""
+    from fedml_amd.arguments import Arguments
+    from fedml_amd.simulation.rccl.client_store import DeviceClientStore
+    from fedml_amd.simulation.rccl.engine import ClientBatchEngine
+    torch.manual_seed(0)
+    model = ResNet(Bottleneck, [1, 1, 1], 10)
+    n = 3 * 64
+    store = DeviceClientStore(torch.randn(n, 3, 16, 16, device=DEV), torch.randint(0, 10, (n,), device=DEV),
+                              [0, 64, 128], [64] * 3)
+    valid = torch.tensor([True, True, False], device=DEV)
+    outs = []
+    for graphs in (False, True):
+        args = Arguments.from_dict({"x": {"client_optimizer": "sgd", "learning_rate": 0.05}})
+        eng = ClientBatchEngine(copy.deepcopy(model).to(DEV), 3, DEV, args, compute_dtype=torch.bfloat16)
+        assert eng.native_step is not None
+        eng.use_graphs = graphs
+        flat = eng.layout.flatten(model.state_dict(), device=DEV)
+        eng.load_global(flat)
+        eng.train(store, torch.arange(3, device=DEV), 1, 32, 0.05, shuffle=False, valid_slots=valid)
+        torch.cuda.synchronize()
+        outs.append(eng.params.clone())
+        if graphs:
+            assert len(eng._graphs) >= 1        # captured despite the padding slot
+        assert torch.equal(eng.params[2], flat)  # padding slot untouched
+        eng.close()
+    p0, p1 = outs
+    assert float((p0[:2] - p1[:2]).norm() / p0[:2].norm()) < 1e-3
