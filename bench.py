@@ -75,6 +75,7 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     use_gpu = torch.cuda.is_available()
     if use_gpu:
+        local_rank %= torch.cuda.device_count()    # (rank rehearsals on a smaller box share GPUs)
         torch.cuda.set_device(local_rank)
         device = torch.device(f"cuda:{local_rank}")
     else:

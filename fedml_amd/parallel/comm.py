@@ -27,7 +27,9 @@ def init_process_group(backend: Optional[str] = None, timeout_s: int = 1800, dev
     if world <= 1:
         return 0, 1
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # FEDML_AMD_DIST_BACKEND=gloo rehearses multi-rank GPU runs on a box with fewer GPUs than
+        # ranks (RCCL needs one GPU per rank); production runs use RCCL ("nccl" on ROCm)
+        backend = os.environ.get("FEDML_AMD_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29500")
     kw = {}
@@ -98,7 +100,7 @@ def all_gather_flat(buf: torch.Tensor, group=None) -> List[torch.Tensor]:
 
 def barrier(device=None):
     if is_dist():
-        if device is not None and torch.device(device).type == "cuda":
+        if device is not None and torch.device(device).type == "cuda" and dist.get_backend() == "nccl":
             dist.barrier(device_ids=[torch.device(device).index])
         else:
             dist.barrier()
