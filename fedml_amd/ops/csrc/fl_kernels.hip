@@ -209,7 +209,8 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ param, co
                                                    float* __restrict__ m1, float* __restrict__ m2,
                                                    float* __restrict__ vmax, const float* __restrict__ step, int64_t P,
                                                    int64_t ld, float lr, float beta1, float beta2, float eps, float wd,
-                                                   int decoupled, const float* __restrict__ active) {
+                                                   int decoupled, const float* __restrict__ active,
+                                                   uint16_t* __restrict__ shadow) {
   const int c = blockIdx.y;
   const float scale = active ? active[c] : 1.f;
   if (scale == 0.f) return;
@@ -243,20 +244,23 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ param, co
     } else {
       den = sqrtf(mb) / bc2_sqrt + eps;
     }
-    pc[i] = p - step_size * ma / den;
+    const float np = p - step_size * ma / den;
+    pc[i] = np;
+    if (shadow) shadow[(int64_t)c * ld + i] = f32_to_bf16(np);   // bf16 weight copy for the next forward
   }
 }
 
 FA_EXPORT int fa_adam_step(float* param, const void* grad, int grad_is_bf16, float* m1, float* m2, float* vmax,
                            const float* step, int C, int64_t P, int64_t ld, float lr, float beta1, float beta2,
-                           float eps, float wd, int decoupled, const float* active, hipStream_t stream) {
+                           float eps, float wd, int decoupled, const float* active, void* shadow,
+                           hipStream_t stream) {
   dim3 grid(fa_grid(P, 256, 1024), C);
   if (grad_is_bf16)
     hipLaunchKernelGGL(adam_kernel<uint16_t>, grid, dim3(256), 0, stream, param, (const uint16_t*)grad, m1, m2, vmax,
-                       step, P, ld, lr, beta1, beta2, eps, wd, decoupled, active);
+                       step, P, ld, lr, beta1, beta2, eps, wd, decoupled, active, (uint16_t*)shadow);
   else
     hipLaunchKernelGGL(adam_kernel<float>, grid, dim3(256), 0, stream, param, (const float*)grad, m1, m2, vmax, step,
-                       P, ld, lr, beta1, beta2, eps, wd, decoupled, active);
+                       P, ld, lr, beta1, beta2, eps, wd, decoupled, active, (uint16_t*)shadow);
   return (int)hipGetLastError();
 }
 

@@ -153,15 +153,17 @@ def sgd_step(param, grad, lr, weight_decay=0.0, momentum=0.0, mom_buf=None, damp
 
 
 def adam_step(param, grad, exp_avg, exp_avg_sq, step, lr, beta1=0.9, beta2=0.999, eps=1e-8, weight_decay=0.0,
-              amsgrad=False, max_exp_avg_sq=None, decoupled=False, active=None):
+              amsgrad=False, max_exp_avg_sq=None, decoupled=False, active=None, shadow=None):
     """In-place fused Adam/AMSGrad/AdamW over a [C, P] stack; ``step`` is a [C] fp32 device tensor
-    holding the (already incremented) step count of each client."""
+    holding the (already incremented) step count of each client. ``shadow`` ([C, P] bf16, same
+    strides): also written with bf16(updated param) in the same pass (inactive clients untouched)."""
     C, P = param.shape
     if use_native(param):
+        assert shadow is None or (shadow.dtype == torch.bfloat16 and shadow.stride() == param.stride())
         rc = _fn("fa_adam_step")(_p(param), _p(grad), _c.c_int(grad.dtype == torch.bfloat16), _p(exp_avg),
                                  _p(exp_avg_sq), _p(max_exp_avg_sq if amsgrad else None), _p(step), _c.c_int(C),
                                  _i64(P), _i64(param.stride(0)), _f(lr), _f(beta1), _f(beta2), _f(eps),
-                                 _f(weight_decay), _c.c_int(int(decoupled)), _p(active), _stream(param))
+                                 _f(weight_decay), _c.c_int(int(decoupled)), _p(active), _p(shadow), _stream(param))
         _check(rc, "fa_adam_step")
         return param
     g = grad.to(torch.float32)
@@ -184,6 +186,8 @@ def adam_step(param, grad, exp_avg, exp_avg_sq, step, lr, beta1=0.9, beta2=0.999
     if active is not None:
         upd = upd * active.view(C, 1)
     param.sub_(upd)
+    if shadow is not None:
+        shadow.copy_(param.to(torch.bfloat16))
     return param
 
 

@@ -101,6 +101,8 @@ class ClientBatchEngine:
             ops.fuse_group_norm(self.model)
         self._seq_views = None
         self._seq_bufs = None
+        self._shadow = None            # bf16 copy of the params arena (transformer GEMM operand)
+        self._shadow_stale = True
         self._active_cache = {}
         self._graphs = {}
         _LIVE_ENGINES.add(self)
@@ -147,12 +149,14 @@ class ClientBatchEngine:
             self.views[s.key] = v
 
     def load_global(self, flat: torch.Tensor):
+        self._shadow_stale = True
         with torch.no_grad():
             self.params.copy_(flat.view(1, -1).expand(self.C, -1))
         if self.mu:
             self.global_ref = flat
 
     def set_client_params(self, slot: int, flat: torch.Tensor):
+        self._shadow_stale = True
         with torch.no_grad():
             self.params[slot].copy_(flat)
 
@@ -262,17 +266,29 @@ class ClientBatchEngine:
             self.interp.flush_deferred()
         return loss.detach()
 
+    def _shadow_out(self):
+        """The bf16 shadow for the optimizer to refresh in its own pass (transformer path), else
+        None — and then the shadow is stale after this step."""
+        sh = self._shadow
+        if sh is None or self.tf is None:
+            self._shadow_stale = True
+            return None
+        return sh
+
     def _bf16_shadow(self):
         """bf16 copy of the parameter arena, refreshed once per step (one streaming cast kernel):
         the transformer GEMMs read their weights from it — half the bytes of the fp32 masters and
         no per-tile conversion; gradients and optimizer state stay fp32."""
         if self.device.type != "cuda" or self.compute_dtype != torch.bfloat16:
             return None
-        if getattr(self, "_shadow", None) is None:
+        if self._shadow is None:
             self._shadow = torch.empty(self.params.shape, dtype=torch.bfloat16, device=self.device)
             self._shadow_views = {s.key: self._shadow[:, s.offset:s.offset + s.numel].view(self.C, *s.shape)
                                   for s in self.layout.slots}
-        ops.cast_bf16(self.params, out=self._shadow)
+            self._shadow_stale = True
+        if self._shadow_stale:     # refreshed by the fused AdamW pass otherwise (adam_step(shadow=...))
+            ops.cast_bf16(self.params, out=self._shadow)
+            self._shadow_stale = False
         return self._shadow_views
 
     # ---------------------------------------------------------------- HIP-graph local step
@@ -496,6 +512,7 @@ class ClientBatchEngine:
 
     def _optimizer_step(self, lr, active, first):
         if self.optimizer == "sgd":
+            self._shadow_stale = True
             ops.sgd_step(self.params, self.grads, lr, weight_decay=self.weight_decay if self.sgd_wd else 0.0,
                          momentum=self.momentum, mom_buf=self.mom, mu=self.mu, global_ref=self.global_ref,
                          first_step=first, active=active)
@@ -503,7 +520,7 @@ class ClientBatchEngine:
             self.step_t += active
             ops.adam_step(self.params, self.grads, self.m1, self.m2, self.step_t.clamp_min(1.0), lr,
                           weight_decay=self.weight_decay, amsgrad=self.vmax is not None, max_exp_avg_sq=self.vmax,
-                          decoupled=self.optimizer == "adamw", active=active)
+                          decoupled=self.optimizer == "adamw", active=active, shadow=self._shadow_out())
 
     # ------------------------------------------------------------------------------------------
     def partial_sum(self, weights: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:

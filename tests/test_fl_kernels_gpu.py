@@ -237,3 +237,22 @@ def test_augment_matches_cpu_reference(pad, cutout, flip):
     ref = ops.augment(x, **kw)
     got = ops.augment(x.to(DEV), **kw).cpu()
     assert torch.allclose(ref, got, atol=1e-5)
+
+
+def test_adamw_writes_bf16_shadow():
+    """Fused AdamW also refreshes the bf16 weight shadow the transformer GEMMs read (active clients
+    only); parameters match the step without a shadow."""
+    torch.manual_seed(0)
+    C, P = 3, 10007
+    p = torch.randn(C, P, device=DEV)
+    g = torch.randn(C, P, device=DEV)
+    m1, m2 = torch.zeros_like(p), torch.zeros_like(p)
+    step = torch.ones(C, device=DEV)
+    act = torch.tensor([1.0, 0.0, 1.0], device=DEV)
+    shadow = torch.full((C, P), 7.0, device=DEV).to(torch.bfloat16)
+    ref = p.clone()
+    ops.adam_step(ref, g, m1.clone(), m2.clone(), step, 1e-2, weight_decay=0.01, decoupled=True, active=act)
+    ops.adam_step(p, g, m1, m2, step, 1e-2, weight_decay=0.01, decoupled=True, active=act, shadow=shadow)
+    assert torch.equal(p, ref)
+    assert torch.equal(shadow[0], p[0].to(torch.bfloat16)) and torch.equal(shadow[2], p[2].to(torch.bfloat16))
+    assert (shadow[1] == 7.0).all()
