@@ -120,6 +120,10 @@ class ClientBatchEngine:
         # the GPU on its own (ResNet-56: 16-64 channels). Wide conv nets (ResNet-18: 64-512 channels)
         # run faster as one full-width library conv per client than as one C-group grouped conv.
         mode = os.environ.get("FEDML_AMD_CLIENT_EXEC", str(getattr(args, "client_exec", "auto") or "auto"))
+        # the per-client step is captured in a HIP graph only for plain conv nets (every op capture-safe;
+        # MIOpen RNNs call hipBLASLt paths that are illegal while a stream captures)
+        self._seq_capture = (self.device.type == "cuda" and _is_wide_convnet(model)
+                             and not any(isinstance(m, torch.nn.RNNBase) for m in model.modules()))
         if not self.sequential and self.native_step is None and self.tf is None and (
                 mode == "sequential" or (mode == "auto" and self.device.type == "cuda" and _is_wide_convnet(model))):
             logging.info("virtual-client engine: per-client sequential execution (wide conv net)")
@@ -128,6 +132,7 @@ class ClientBatchEngine:
             # machine that costs ~40 % of the round. Benchmark mode runs Find once per shape during the
             # first (eager, uncaptured) step of each geometry; the captured graphs then replay the winners.
             if os.environ.get("FEDML_AMD_MIOPEN_FIND", "1") != "0":
+                self._prev_benchmark = torch.backends.cudnn.benchmark   # restored by close()
                 torch.backends.cudnn.benchmark = True
         self._build_views()
         self.global_ref = None
@@ -213,7 +218,7 @@ class ClientBatchEngine:
                 sample_mask = None if uniform else mask.t().contiguous()     # [B, C]
                 if self.native_step is not None and sample_mask is None and self.use_graphs:
                     loss = self._graph_step(x, y, mask, b_c, active, lr, first)
-                elif self.sequential and self.tf is None and self.use_graphs and uniform:
+                elif self.sequential and self.tf is None and self.use_graphs and self._seq_capture and uniform:
                     loss = self._seq_graph_step(x, y, b_c, active, lr, first)
                 else:
                     loss = self._step_loss(x, y, mask, b_c, active, sample_mask, use_native_loss)
@@ -336,6 +341,9 @@ class ClientBatchEngine:
         if self._graphs:
             torch.cuda.synchronize(self.device)
             self._graphs.clear()
+        if getattr(self, "_prev_benchmark", None) is not None:
+            torch.backends.cudnn.benchmark = self._prev_benchmark
+            self._prev_benchmark = None
 
     def _fill_static(self, st, x, y, mask, b_c, active):
         st["x"].copy_(x, non_blocking=True)
