@@ -722,14 +722,18 @@ static size_t gemm_smem(int kc, int nout, int ldk, const Plan& p, int TR, int TW
 template <int KC, int NOUT_WG, int XF, int BWD, int EPI, int ST>
 static int launch_gemm(Args a, int nout, int C, int target_px, hipStream_t stream) {
   constexpr int MTW = NOUT_WG >= 64 ? 2 : 4;
-  Plan p = make_plan(a.N, a.H, a.W, C, target_px, 2048);
+  static const int wgs = [] {   // FEDML_AMD_C3G_WGS: workgroup target of the fwd / bwd-data kernels
+    const char* e = getenv("FEDML_AMD_C3G_WGS");
+    return e ? atoi(e) : 2048;
+  }();
+  Plan p = make_plan(a.N, a.H, a.W, C, target_px, wgs);
   {  // a unit's tile must fit the loader's register budget (≤ 12 16-B chunks per thread)
     const bool f2 = !BWD && ST == 2;
     while (target_px > 8) {
       const int tr = f2 ? 2 * p.R + 1 : p.R + 2, tw = (BWD ? a.W : a.Ws) + 2;
       if ((p.S * tr * tw * (KC / 8) + 255) / 256 <= 12) break;
       target_px /= 2;
-      p = make_plan(a.N, a.H, a.W, C, target_px, 2048);
+      p = make_plan(a.N, a.H, a.W, C, target_px, wgs);
     }
   }
   a.R = p.R; a.S = p.S; a.units = p.units; a.units_per_wg = p.units_per_wg; a.nout_total = nout;
@@ -830,12 +834,19 @@ FA_EXPORT int fa_conv3x3_wgrad(const uint16_t* g, const uint16_t* yv, const floa
   a.N = N; a.H = Ho; a.W = Wo; a.Hs = H; a.Ws = W;
   // units sized so one unit's operands fit the loaders' register budget (x tile ≤ 8, dy ≤ 4 chunks/thread)
   int tpx = Cin >= 64 ? (stride == 2 ? 64 : 128) : (stride == 2 ? 128 : 256);
-  c3::Plan p = c3::make_plan(N, Ho, Wo, C, tpx, 2048);
+  // Target workgroup count: every workgroup adds its Cout×9·Cin partial sums with fp32 atomics, so
+  // more, shorter workgroups cost atomics per client (FEDML_AMD_C3W_WGS overrides, for tuning;
+  // scripts/gpu_c3w_sweep*.sh)
+  static const int wgs = [] {
+    const char* e = getenv("FEDML_AMD_C3W_WGS");
+    return e ? atoi(e) : 256;   // measured: +2/+3/+6 % rounds/s at 50/25/13 clients per GPU, neutral at 100
+  }();
+  c3::Plan p = c3::make_plan(N, Ho, Wo, C, tpx, wgs);
   while (tpx > 8) {
     const int tr = stride == 2 ? 2 * p.R + 1 : p.R + 2;
     if ((p.S * tr * (W + 2) * (Cin / 8) + 255) / 256 <= 8 && (p.S * p.R * Wo * (Cout / 8) + 255) / 256 <= 4) break;
     tpx /= 2;
-    p = c3::make_plan(N, Ho, Wo, C, tpx, 2048);
+    p = c3::make_plan(N, Ho, Wo, C, tpx, wgs);
   }
   a.R = p.R; a.S = p.S; a.units = p.units; a.units_per_wg = p.units_per_wg;
   const int TR = stride == 2 ? 2 * p.R + 1 : p.R + 2;

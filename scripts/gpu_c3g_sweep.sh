@@ -1,0 +1,11 @@
+#!/bin/bash
+# Sweep the 3x3 fwd/bwd-data workgroup target (wgrad target at its new default).
+set -o pipefail
+export HSA_ENABLE_IPC_MODE_LEGACY=0
+mkdir -p gpurun_out
+for w in 2048 4096 1024 512; do
+  for c in 100 13; do
+    FEDML_AMD_C3G_WGS=$w timeout -k 10 300 python -u bench.py --clients $c --steps 3 --warmup 1 > gpurun_out/bench_g$w_c$c.log 2>&1 || { tail -20 gpurun_out/bench_g$w_c$c.log; exit 1; }
+    echo "gwgs=$w C=$c $(grep -o '"value": [0-9.]*' gpurun_out/bench_g$w_c$c.log)"
+  done
+done
