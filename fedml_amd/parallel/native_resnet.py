@@ -72,6 +72,9 @@ class UnsupportedNative(Exception):
     pass
 
 
+# workgroup target of the generic conv kernels (FEDML_AMD_CONV_WGS overrides, for tuning)
+_CONV_WGS = int(os.environ.get("FEDML_AMD_CONV_WGS", "1024"))   # scripts/gpu_conv_sweep.sh
+
 def _round_up(v, m):
     return (v + m - 1) // m * m
 
@@ -266,7 +269,7 @@ class NativeResNetStep:
     # ------------------------------------------------------------------ helpers
     def _tiles_per_wave(self, M):
         tiles = (M + 15) // 16
-        target_wgs = 2048
+        target_wgs = _CONV_WGS
         tpw = max(1, min(16, (tiles * self.C) // (4 * target_wgs)))
         return tpw
 
