@@ -299,3 +299,38 @@ FA_EXPORT int fa_wgrad_scatter(float* dw, float* garena, int64_t ldw, int64_t wo
                      stream, dw, garena, ldw, woff, Cout, Cin, taps, cin_src);
   return (int)hipGetLastError();
 }
+
+// ---- deferred scatter of every 3×3 layer's dW in ONE launch at the end of backward ----
+// Each layer owns its GEMM-layout scratch [C][Cout][9·Cin] at `src_off` of one buffer; blockIdx.z
+// selects the layer (replaces one scatter launch per 3×3 layer and step).
+struct ScatterSeg {
+  int64_t src_off;   // element offset of the layer's [C][Cout][9·Cin] scratch
+  int64_t woff;      // OIHW weight offset inside a client row of the gradient arena
+  int cout, cin, cin_src, pad_;
+};
+
+__global__ __launch_bounds__(256) void wgrad_scatter_multi_kernel(float* __restrict__ dw, float* __restrict__ garena,
+                                                                  int64_t ldw, const ScatterSeg* __restrict__ segs) {
+  const ScatterSeg sg = segs[blockIdx.z];
+  const int c = blockIdx.y;
+  const int K = 9 * sg.cin;
+  const int n = sg.cout * K;
+  float* d = dw + sg.src_off + (int64_t)c * n;
+  float* gw = garena + (int64_t)c * ldw + sg.woff;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+    const int co = i / K, k = i - co * K;
+    const int tap = k / sg.cin, ci = k - tap * sg.cin;
+    if (ci < sg.cin_src) gw[((int64_t)co * sg.cin_src + ci) * 9 + tap] += d[i];
+    d[i] = 0.f;
+  }
+}
+
+// segs: device array of `nseg` ScatterSeg; max_n = the largest Cout·9·Cin among them
+FA_EXPORT int fa_wgrad_scatter_multi(float* dw, float* garena, int64_t ldw, const void* segs, int nseg, int max_n,
+                                     int C, hipStream_t stream) {
+  if (nseg <= 0) return 0;
+  if (nseg > 65535 || C > 65535) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(wgrad_scatter_multi_kernel, dim3(fa_grid(max_n, 256, 64), C, nseg), dim3(256), 0, stream, dw,
+                     garena, ldw, (const ScatterSeg*)segs);
+  return (int)hipGetLastError();
+}

@@ -86,15 +86,31 @@ def conv3x3_bwd_data(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, dx, e_x, e_s, e_t
 
 
 def conv3x3_wgrad(g, yv, alpha, beta, gamma, x, ps, pt, garena, woff, C, N, H, W, Cin, Cout, cin_src, dw_scratch,
-                  stride=1):
-    """Weight gradient into the GEMM-layout scratch, then scattered (+=) into the OIHW arena.
-    (H, W) = input (x) resolution."""
+                  stride=1, scatter=True):
+    """Weight gradient into the GEMM-layout scratch, then scattered (+=) into the OIHW arena
+    (``scatter=False``: left in the scratch for :func:`wgrad_scatter_multi`). (H, W) = input (x)
+    resolution."""
     rc = _fn("fa_conv3x3_wgrad")(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(x), _p(ps), _p(pt),
                                  _p(dw_scratch), _i(C), _i(N), _i(H), _i(W), _i(Cin), _i(Cout), _i(stride), _stream(g))
     _check(rc, "fa_conv3x3_wgrad")
+    if not scatter:
+        return
     rc = _fn("fa_wgrad_scatter")(_p(dw_scratch), _p(garena), _i64(garena.stride(0)), _i64(woff), _i(C), _i(Cout),
                                  _i(Cin), _i(9), _i(cin_src), _stream(g))
     _check(rc, "fa_wgrad_scatter")
+
+
+class ScatterSeg(ctypes.Structure):
+    _fields_ = [("src_off", ctypes.c_int64), ("woff", ctypes.c_int64), ("cout", ctypes.c_int), ("cin", ctypes.c_int),
+                ("cin_src", ctypes.c_int), ("pad_", ctypes.c_int)]
+
+
+def wgrad_scatter_multi(dw, garena, segs_dev, nseg, max_n, C):
+    """Scatter (+=) the deferred GEMM-layout dW of ``nseg`` 3×3 layers into the OIHW arena and clear
+    their scratch — one launch (``segs_dev``: uint8 device tensor holding ``ScatterSeg`` records)."""
+    rc = _fn("fa_wgrad_scatter_multi")(_p(dw), _p(garena), _i64(garena.stride(0)), _p(segs_dev), _i(nseg), _i(max_n),
+                                       _i(C), _stream(garena))
+    _check(rc, "fa_wgrad_scatter_multi")
 
 
 # ---- 1×1 / stride-1 weight gradient (csrc/conv1x1_kernels.hip) ----

@@ -241,11 +241,26 @@ class NativeResNetStep:
         # GEMM-layout dW scratch for the weight-gradient kernel (kept zeroed by its scatter pass)
         mx = max(cv.cout * cv.k * cv.k * cv.cin_pad for cv in self._all_convs())
         self.dw_scratch = torch.zeros(C * mx, dtype=torch.float32, device=dev)
+        # the 3×3 layers keep their dW in scratch slices of their own and are scattered into the arena
+        # together, in ONE launch at the end of backward (instead of one scatter launch per layer)
+        segs, o3, self.c3_maxn, self._c3_off = [], 0, 0, {}
+        for cv in self._all_convs():
+            if self._c3(cv):
+                n = cv.cout * 9 * cv.cin_pad
+                self._c3_off[cv.key] = o3
+                segs.append(nn_ops.ScatterSeg(o3, self.off[cv.key], cv.cout, cv.cin_pad, cv.cin, 0))
+                o3 += C * n
+                self.c3_maxn = max(self.c3_maxn, n)
+        self.dw_c3 = torch.zeros(max(1, o3), dtype=torch.float32, device=dev)
+        self.c3_nseg = len(segs)
+        raw = bytes((nn_ops.ScatterSeg * max(1, len(segs)))(*segs))
+        self.c3_segs = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
         self.geom = (N, H, W)
 
     # Every geometry keeps its own buffers alive: a captured HIP graph of one batch size must stay
     # valid while another batch size (the ragged last step of an epoch) is being run.
     _STATE_ATTRS = ("x_in", "stem_y", "stem_out", "gbuf", "bn_vec", "stats", "stat_views", "pooled", "dw_scratch",
+                    "dw_c3", "c3_segs", "c3_nseg", "c3_maxn", "_c3_off",
                     "packed", "packed_ld", "_segs", "_nseg", "final_hw", "geom")
 
     def _snapshot(self):
@@ -299,7 +314,8 @@ class NativeResNetStep:
         pt = pro_vec[1] if pro_vec is not None else None
         if self._c3(cv):
             nn_ops.conv3x3_wgrad(g, y, vec[4], vec[5], vec[6], x, ps, pt, garena, self.off[cv.key], C, N, cv.H, cv.W,
-                                 cv.cin_pad, cv.cout, cv.cin, self.dw_scratch, cv.stride)
+                                 cv.cin_pad, cv.cout, cv.cin, self.dw_c3[self._c3_off[cv.key]:], cv.stride,
+                                 scatter=False)   # scattered with the other 3×3 layers at the end of step()
             return
         M = N * cv.Ho * cv.Wo
         if self.use_c1 and cv.cin == cv.cin_pad and nn_ops.conv1x1_wgrad_supported(cv.cin, cv.cout, cv.k, cv.stride,
@@ -523,4 +539,6 @@ class NativeResNetStep:
         self._bn_bwd(st_bn, 1, N, st_conv.Ho * st_conv.Wo, arena, garena)
         v = self.bn_vec[st_bn.key]
         self._wgrad(st_conv, gpre, self.stem_y, v, self.x_in, None, garena, N)
+        if self.c3_nseg:
+            nn_ops.wgrad_scatter_multi(self.dw_c3, garena, self.c3_segs, self.c3_nseg, self.c3_maxn, C)
         return loss.detach()
