@@ -206,8 +206,15 @@ class RCCLSimulator:
     def save_checkpoint(self, directory):
         from ...core.checkpoint import save_round_checkpoint
         if self.rank == 0:
+            # per-run state beyond the global model: the shuffle generator (an identical data order
+            # after resume) and the clients' error-feedback residuals of compressed updates
+            # (single-rank layout; multi-rank runs re-derive shuffles per rank from the seed)
+            clients = {"gen": self.gen.get_state()}
+            if self.residual is not None:
+                clients["residual"] = self.residual.detach().cpu()
             save_round_checkpoint(directory, self.round_idx, self.global_model_state(), self.args,
-                                  server_opt=self.server_opt.state_dict() if self.server_opt else None)
+                                  server_opt=self.server_opt.state_dict() if self.server_opt else None,
+                                  clients=clients)
 
     def load_checkpoint(self, directory, round_idx=None):
         from ...core.checkpoint import load_round_checkpoint
@@ -215,6 +222,11 @@ class RCCLSimulator:
         self.global_flat.copy_(self.layout.flatten(ck["global"], device=self.device))
         if self.server_opt is not None and ck.get("server_opt") is not None:
             self.server_opt.load_state_dict(ck["server_opt"])
+        cl = ck.get("clients") or {}
+        if cl.get("gen") is not None and self.world == 1:
+            self.gen.set_state(cl["gen"])
+        if cl.get("residual") is not None and self.residual is not None:
+            self.residual.copy_(cl["residual"].to(self.device))
         self.round_idx = int(ck["round"]) + 1
         return self.round_idx
 

@@ -104,3 +104,35 @@ def test_client_packing_is_cheap_and_balanced():
     exact = [sum(cnt[i] for i in g) for g in pack_clients_to_gpus(cnt, 8, exact=True)]
     assert max(loads) <= 1.05 * max(exact)
     assert max(len(g) for g in p) == 13
+
+
+def test_checkpoint_resume_is_exact(tmp_path):
+    """stop after round 2, reload ``ckpt/round_1`` into a fresh simulator and continue —
+    the final global model equals an uninterrupted 4-round run (client sampling by round index,
+    shuffle generator, FedOpt server state and int8 error-feedback residuals all restored)."""
+    from fedml_amd.models.linear.lr import LogisticRegression
+    from fedml_amd.simulation.rccl.client_store import DeviceClientStore
+    from fedml_amd.simulation.rccl.simulator import RCCLSimulator
+
+    def make(ck=None):
+        torch.manual_seed(0)
+        cfg = {"federated_optimizer": "FedOpt", "server_optimizer": "adam", "server_lr": 0.05,
+               "client_num_in_total": 6, "client_num_per_round": 4, "comm_round": 4, "epochs": 1, "batch_size": 4,
+               "client_optimizer": "sgd", "learning_rate": 0.1, "compression": "int8", "shuffle": True,
+               "random_seed": 3}
+        if ck:
+            cfg["checkpoint_dir"] = ck
+        args = Arguments.from_dict({"x": cfg})
+        g = torch.Generator().manual_seed(1)
+        store = DeviceClientStore(torch.randn(60, 10, generator=g), torch.randint(0, 3, (60,), generator=g),
+                                  [10 * i for i in range(6)], [10] * 6)
+        return RCCLSimulator(args, torch.device("cpu"), None, LogisticRegression(10, 3), store=store)
+
+    ref = make().run(4)
+    ck = str(tmp_path / "ckpt")
+    make(ck).run(2)
+    sim = make()
+    assert sim.load_checkpoint(ck) == 2
+    out = sim.run(2)
+    for k in ref:
+        assert torch.equal(ref[k], out[k]), k
