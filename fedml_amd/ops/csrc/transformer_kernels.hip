@@ -53,7 +53,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const uint16_t* __restrict_
                                                      const float* __restrict__ beta, float eps, uint32_t thr,
                                                      float dscale, uint32_t seed, uint16_t* __restrict__ y,
                                                      uint16_t* __restrict__ xsum, float* __restrict__ mean_out,
-                                                     float* __restrict__ rstd_out) {
+                                                     float* __restrict__ rstd_out,
+                                                     const uint32_t* __restrict__ seedp) {
+  if (seedp) seed += *seedp * 1000003u;   // device step counter (graph-captured steps)
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= R) return;
@@ -132,7 +134,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
                                                      int rows_per_client, int d, const float* __restrict__ gamma,
                                                      uint16_t* __restrict__ dx, uint16_t* __restrict__ dh,
                                                      uint32_t thr, float dscale, uint32_t seed,
-                                                     float* __restrict__ dgamma, float* __restrict__ dbeta) {
+                                                     float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                     const uint32_t* __restrict__ seedp) {
+  if (seedp) seed += *seedp * 1000003u;
   extern __shared__ float red[];  // [4][2][d]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int c = blockIdx.y;
@@ -293,7 +297,8 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
                                                        uint16_t* __restrict__ o, int ldo,
                                                        const uint8_t* __restrict__ kmask, float* __restrict__ lse2,
                                                        int S, int H, float scale, uint32_t thr, float dscale,
-                                                       uint32_t seed) {
+                                                       uint32_t seed, const uint32_t* __restrict__ seedp) {
+  if (seedp) seed += *seedp * 1000003u;
   constexpr int NB = SP / 16;
   constexpr int VST = SP + 8;
   __shared__ __attribute__((aligned(16))) uint16_t Ks[SP * KST];
@@ -416,7 +421,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const uint16_t* __rest
                                                           const uint8_t* __restrict__ kmask,
                                                           const float* __restrict__ lse2, const float* __restrict__ D,
                                                           uint16_t* __restrict__ dq, int lddq, int S, int H,
-                                                          float scale, uint32_t thr, float dscale, uint32_t seed) {
+                                                          float scale, uint32_t thr, float dscale, uint32_t seed,
+                                                          const uint32_t* __restrict__ seedp) {
+  if (seedp) seed += *seedp * 1000003u;
   __shared__ __attribute__((aligned(16))) uint16_t Ks[64 * KST];
   __shared__ __attribute__((aligned(16))) uint16_t Vs[64 * KST];
   __shared__ __attribute__((aligned(16))) uint16_t dSs[4 * 16 * KST];
@@ -495,7 +502,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const uint16_t* __res
                                                            const float* __restrict__ lse2, const float* __restrict__ D,
                                                            uint16_t* __restrict__ dk, int lddk,
                                                            uint16_t* __restrict__ dv, int lddv, int S, int H,
-                                                           float scale, uint32_t thr, float dscale, uint32_t seed) {
+                                                           float scale, uint32_t thr, float dscale, uint32_t seed,
+                                                           const uint32_t* __restrict__ seedp) {
+  if (seedp) seed += *seedp * 1000003u;
   __shared__ __attribute__((aligned(16))) uint16_t Qs[64 * KST];
   __shared__ __attribute__((aligned(16))) uint16_t dOs[64 * KST];
   __shared__ __attribute__((aligned(16))) uint16_t Pst[4 * 16 * KST];
@@ -588,30 +597,32 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const uint16_t* __res
 
 template <int NV>
 int launch_ln_fwd(const uint16_t* h, const uint16_t* res, int R, int d, int rpc, const float* g, const float* b,
-                  float eps, uint32_t thr, float dscale, uint32_t seed, uint16_t* y, uint16_t* xsum, float* mean,
+                  float eps, uint32_t thr, float dscale, uint32_t seed, const uint32_t* seedp, uint16_t* y,
+                  uint16_t* xsum, float* mean,
                   float* rstd, hipStream_t st) {
   hipLaunchKernelGGL(ln_fwd_kernel<NV>, dim3((R + 3) / 4), dim3(256), 0, st, h, res, R, d, rpc, g, b, eps, thr,
-                     dscale, seed, y, xsum, mean, rstd);
+                     dscale, seed, y, xsum, mean, rstd, seedp);
   return (int)hipGetLastError();
 }
 template <int NV>
 int launch_ln_bwd(const uint16_t* dy, const uint16_t* x, const float* mean, const float* rstd, int C, int rpc, int d,
-                  const float* g, uint16_t* dx, uint16_t* dh, uint32_t thr, float dscale, uint32_t seed, float* dg,
+                  const float* g, uint16_t* dx, uint16_t* dh, uint32_t thr, float dscale, uint32_t seed,
+                  const uint32_t* seedp, float* dg,
                   float* db, hipStream_t st) {
   int bpc = (rpc + 31) / 32;  // ≥8 rows per wave
   if (bpc < 1) bpc = 1;
   if (bpc > 1024) bpc = 1024;
   hipLaunchKernelGGL(ln_bwd_kernel<NV>, dim3(bpc, C), dim3(256), 8 * d * sizeof(float), st, dy, x, mean, rstd, rpc,
-                     d, g, dx, dh, thr, dscale, seed, dg, db);
+                     d, g, dx, dh, thr, dscale, seed, dg, db, seedp);
   return (int)hipGetLastError();
 }
 
 template <int SP>
 int launch_attn_fwd(const uint16_t* q, int ldq, const uint16_t* k, int ldk, const uint16_t* v, int ldv, uint16_t* o,
                     int ldo, const uint8_t* kmask, float* lse2, int CB, int S, int H, float scale, uint32_t thr,
-                    float dscale, uint32_t seed, hipStream_t st) {
+                    float dscale, uint32_t seed, const uint32_t* seedp, hipStream_t st) {
   hipLaunchKernelGGL(attn_fwd_kernel<SP>, dim3(H, CB), dim3(256), 0, st, q, ldq, k, ldk, v, ldv, o,
-                     ldo, kmask, lse2, S, H, scale, thr, dscale, seed);
+                     ldo, kmask, lse2, S, H, scale, thr, dscale, seed, seedp);
   return (int)hipGetLastError();
 }
 
@@ -619,28 +630,28 @@ int launch_attn_fwd(const uint16_t* q, int ldq, const uint16_t* k, int ldk, cons
 
 FA_EXPORT int fa_ln_fwd(const void* h, const void* res, int R, int d, int rows_per_client, const float* gamma,
                         const float* beta, float eps, uint32_t thr, float dscale, uint32_t seed, void* y, void* xsum,
-                        float* mean, float* rstd, hipStream_t stream) {
+                        float* mean, float* rstd, const uint32_t* seedp, hipStream_t stream) {
   if (d % 8 != 0 || d > 2048) return (int)hipErrorInvalidValue;
   auto H = (const uint16_t*)h;
   auto Rs = (const uint16_t*)res;
   auto Y = (uint16_t*)y;
   auto X = (uint16_t*)xsum;
-  if (d <= 512) return launch_ln_fwd<1>(H, Rs, R, d, rows_per_client, gamma, beta, eps, thr, dscale, seed, Y, X, mean, rstd, stream);
-  if (d <= 1024) return launch_ln_fwd<2>(H, Rs, R, d, rows_per_client, gamma, beta, eps, thr, dscale, seed, Y, X, mean, rstd, stream);
-  return launch_ln_fwd<4>(H, Rs, R, d, rows_per_client, gamma, beta, eps, thr, dscale, seed, Y, X, mean, rstd, stream);
+  if (d <= 512) return launch_ln_fwd<1>(H, Rs, R, d, rows_per_client, gamma, beta, eps, thr, dscale, seed, seedp, Y, X, mean, rstd, stream);
+  if (d <= 1024) return launch_ln_fwd<2>(H, Rs, R, d, rows_per_client, gamma, beta, eps, thr, dscale, seed, seedp, Y, X, mean, rstd, stream);
+  return launch_ln_fwd<4>(H, Rs, R, d, rows_per_client, gamma, beta, eps, thr, dscale, seed, seedp, Y, X, mean, rstd, stream);
 }
 
 FA_EXPORT int fa_ln_bwd(const void* dy, const void* x, const float* mean, const float* rstd, int C,
                         int rows_per_client, int d, const float* gamma, void* dx, void* dh, uint32_t thr, float dscale,
-                        uint32_t seed, float* dgamma, float* dbeta, hipStream_t stream) {
+                        uint32_t seed, float* dgamma, float* dbeta, const uint32_t* seedp, hipStream_t stream) {
   if (d % 8 != 0 || d > 2048) return (int)hipErrorInvalidValue;
   auto DY = (const uint16_t*)dy;
   auto X = (const uint16_t*)x;
   auto DX = (uint16_t*)dx;
   auto DH = (uint16_t*)dh;
-  if (d <= 512) return launch_ln_bwd<1>(DY, X, mean, rstd, C, rows_per_client, d, gamma, DX, DH, thr, dscale, seed, dgamma, dbeta, stream);
-  if (d <= 1024) return launch_ln_bwd<2>(DY, X, mean, rstd, C, rows_per_client, d, gamma, DX, DH, thr, dscale, seed, dgamma, dbeta, stream);
-  return launch_ln_bwd<4>(DY, X, mean, rstd, C, rows_per_client, d, gamma, DX, DH, thr, dscale, seed, dgamma, dbeta, stream);
+  if (d <= 512) return launch_ln_bwd<1>(DY, X, mean, rstd, C, rows_per_client, d, gamma, DX, DH, thr, dscale, seed, seedp, dgamma, dbeta, stream);
+  if (d <= 1024) return launch_ln_bwd<2>(DY, X, mean, rstd, C, rows_per_client, d, gamma, DX, DH, thr, dscale, seed, seedp, dgamma, dbeta, stream);
+  return launch_ln_bwd<4>(DY, X, mean, rstd, C, rows_per_client, d, gamma, DX, DH, thr, dscale, seed, seedp, dgamma, dbeta, stream);
 }
 
 FA_EXPORT int fa_gelu_fwd(const void* x, void* y, int64_t n, hipStream_t stream) {
@@ -659,24 +670,24 @@ FA_EXPORT int fa_gelu_bwd(const void* x, const void* gy, void* gx, int64_t n, hi
 
 FA_EXPORT int fa_attn_fwd(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* o, int ldo,
                           const uint8_t* kmask, float* lse2, int CB, int S, int H, float scale, uint32_t thr,
-                          float dscale, uint32_t seed, hipStream_t stream) {
+                          float dscale, uint32_t seed, const uint32_t* seedp, hipStream_t stream) {
   auto Q = (const uint16_t*)q;
   auto K = (const uint16_t*)k;
   auto V = (const uint16_t*)v;
   auto O = (uint16_t*)o;
   if (S <= 0 || S > 256 || (ldq | ldk | ldv | ldo) % 8 != 0) return (int)hipErrorInvalidValue;
-  if (S <= 64) return launch_attn_fwd<64>(Q, ldq, K, ldk, V, ldv, O, ldo, kmask, lse2, CB, S, H, scale, thr, dscale, seed, stream);
-  if (S <= 128) return launch_attn_fwd<128>(Q, ldq, K, ldk, V, ldv, O, ldo, kmask, lse2, CB, S, H, scale, thr, dscale, seed, stream);
-  if (S <= 160) return launch_attn_fwd<160>(Q, ldq, K, ldk, V, ldv, O, ldo, kmask, lse2, CB, S, H, scale, thr, dscale, seed, stream);
-  if (S <= 192) return launch_attn_fwd<192>(Q, ldq, K, ldk, V, ldv, O, ldo, kmask, lse2, CB, S, H, scale, thr, dscale, seed, stream);
-  if (S <= 224) return launch_attn_fwd<224>(Q, ldq, K, ldk, V, ldv, O, ldo, kmask, lse2, CB, S, H, scale, thr, dscale, seed, stream);
-  return launch_attn_fwd<256>(Q, ldq, K, ldk, V, ldv, O, ldo, kmask, lse2, CB, S, H, scale, thr, dscale, seed, stream);
+  if (S <= 64) return launch_attn_fwd<64>(Q, ldq, K, ldk, V, ldv, O, ldo, kmask, lse2, CB, S, H, scale, thr, dscale, seed, seedp, stream);
+  if (S <= 128) return launch_attn_fwd<128>(Q, ldq, K, ldk, V, ldv, O, ldo, kmask, lse2, CB, S, H, scale, thr, dscale, seed, seedp, stream);
+  if (S <= 160) return launch_attn_fwd<160>(Q, ldq, K, ldk, V, ldv, O, ldo, kmask, lse2, CB, S, H, scale, thr, dscale, seed, seedp, stream);
+  if (S <= 192) return launch_attn_fwd<192>(Q, ldq, K, ldk, V, ldv, O, ldo, kmask, lse2, CB, S, H, scale, thr, dscale, seed, seedp, stream);
+  if (S <= 224) return launch_attn_fwd<224>(Q, ldq, K, ldk, V, ldv, O, ldo, kmask, lse2, CB, S, H, scale, thr, dscale, seed, seedp, stream);
+  return launch_attn_fwd<256>(Q, ldq, K, ldk, V, ldv, O, ldo, kmask, lse2, CB, S, H, scale, thr, dscale, seed, seedp, stream);
 }
 
 FA_EXPORT int fa_attn_bwd(const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, const void* o,
                           int ldo, const void* dout, int lddo, const uint8_t* kmask, const float* lse2, float* Dbuf,
                           void* dq, int lddq, void* dk, int lddk, void* dv, int lddv, int CB, int S, int H,
-                          float scale, uint32_t thr, float dscale, uint32_t seed, hipStream_t stream) {
+                          float scale, uint32_t thr, float dscale, uint32_t seed, const uint32_t* seedp, hipStream_t stream) {
   if (S <= 0 || S > 4096 || (ldq | ldk | ldv | ldo | lddo | lddq | lddk | lddv) % 8 != 0)
     return (int)hipErrorInvalidValue;
   const int64_t n = (int64_t)CB * S * H;
@@ -685,9 +696,9 @@ FA_EXPORT int fa_attn_bwd(const void* q, int ldq, const void* k, int ldk, const 
   const dim3 grid((S + 63) / 64, H, CB);
   hipLaunchKernelGGL(attn_bwd_dq_kernel, grid, dim3(256), 0, stream, (const uint16_t*)q, ldq, (const uint16_t*)k, ldk,
                      (const uint16_t*)v, ldv, (const uint16_t*)dout, lddo, kmask, lse2, Dbuf, (uint16_t*)dq, lddq, S, H,
-                     scale, thr, dscale, seed);
+                     scale, thr, dscale, seed, seedp);
   hipLaunchKernelGGL(attn_bwd_dkv_kernel, grid, dim3(256), 0, stream, (const uint16_t*)q, ldq, (const uint16_t*)k,
                      ldk, (const uint16_t*)v, ldv, (const uint16_t*)dout, lddo, kmask, lse2, Dbuf, (uint16_t*)dk, lddk,
-                     (uint16_t*)dv, lddv, S, H, scale, thr, dscale, seed);
+                     (uint16_t*)dv, lddv, S, H, scale, thr, dscale, seed, seedp);
   return (int)hipGetLastError();
 }

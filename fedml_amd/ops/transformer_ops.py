@@ -62,7 +62,7 @@ def _ln_ref(h, res, gamma, beta, eps, p, seed, rpc):
 
 class _LayerNorm(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, h, res, gamma, beta, eps, p, seed, rpc):
+    def forward(ctx, h, res, gamma, beta, eps, p, seed, rpc, seed_dev):
         R, d = h.shape
         y = torch.empty_like(h)
         fused = res is not None or p > 0
@@ -73,16 +73,18 @@ class _LayerNorm(torch.autograd.Function):
         b = beta.detach().float().contiguous()
         rc = _fn("fa_ln_fwd")(_p(h), _p(res), _c.c_int(R), _c.c_int(d), _c.c_int(rpc), _p(g), _p(b), _f(eps),
                               _c.c_uint32(_thr(p)), _f(1.0 / (1.0 - p) if p > 0 else 1.0), _c.c_uint32(seed & _M32),
-                              _p(y), _p(xsum), _p(mean), _p(rstd), _stream(h))
+                              _p(y), _p(xsum), _p(mean), _p(rstd), _p(seed_dev), _stream(h))
         _check(rc, "fa_ln_fwd")
         ctx.save_for_backward(xsum if fused else h, mean, rstd, g)
         ctx.cfg = (p, seed, rpc, res is not None, fused, gamma.dtype)
+        ctx.seed_dev = seed_dev
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, mean, rstd, g = ctx.saved_tensors
         p, seed, rpc, has_res, fused, gdt = ctx.cfg
+        seed_dev = ctx.seed_dev
         R, d = x.shape
         C = R // rpc
         dy = dy.contiguous()
@@ -92,18 +94,20 @@ class _LayerNorm(torch.autograd.Function):
         db = torch.zeros(C, d, dtype=torch.float32, device=x.device)
         rc = _fn("fa_ln_bwd")(_p(dy), _p(x), _p(mean), _p(rstd), _c.c_int(C), _c.c_int(rpc), _c.c_int(d), _p(g),
                               _p(dres), _p(dh), _c.c_uint32(_thr(p)), _f(1.0 / (1.0 - p) if p > 0 else 1.0),
-                              _c.c_uint32(seed & _M32), _p(dg), _p(db), _stream(x))
+                              _c.c_uint32(seed & _M32), _p(dg), _p(db), _p(seed_dev), _stream(x))
         _check(rc, "fa_ln_bwd")
-        return dh, dres, dg.to(gdt), db.to(gdt), None, None, None, None
+        return dh, dres, dg.to(gdt), db.to(gdt), None, None, None, None, None
 
 
 def layer_norm(h: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float, rows_per_client: int,
-               res: torch.Tensor = None, p: float = 0.0, seed: int = 0) -> torch.Tensor:
-    """LN(res + dropout_p(h)) over the last dim of 2-D ``h`` [R, d]; gamma/beta ``[C, d]``."""
+               res: torch.Tensor = None, p: float = 0.0, seed: int = 0, seed_dev: torch.Tensor = None) -> torch.Tensor:
+    """LN(res + dropout_p(h)) over the last dim of 2-D ``h`` [R, d]; gamma/beta ``[C, d]``.
+    ``seed_dev`` (GPU): a [1] uint32/int32 device step counter — the kernels then use
+    seed + counter·1000003, so a captured HIP graph draws new dropout masks on every replay."""
     assert h.dim() == 2 and h.shape[0] % rows_per_client == 0
     if use_native(h):
         assert h.dtype == torch.bfloat16 and h.is_contiguous() and (res is None or res.is_contiguous())
-        return _LayerNorm.apply(h, res, gamma, beta, float(eps), float(p), int(seed), int(rows_per_client))
+        return _LayerNorm.apply(h, res, gamma, beta, float(eps), float(p), int(seed), int(rows_per_client), seed_dev)
     return _ln_ref(h, res, gamma, beta, eps, p, seed, rows_per_client)
 
 
@@ -155,7 +159,7 @@ def _attn_ref(q, k, v, kmask, S, H, p, seed):
 
 class _Attention(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, q, k, v, kmask, S, H, p, seed):
+    def forward(ctx, q, k, v, kmask, S, H, p, seed, seed_dev):
         T, dm = q.shape
         CB = T // S
         o = torch.empty(T, dm, dtype=q.dtype, device=q.device)
@@ -164,10 +168,12 @@ class _Attention(torch.autograd.Function):
         rc = _fn("fa_attn_fwd")(_p(q), _c.c_int(q.stride(0)), _p(k), _c.c_int(k.stride(0)), _p(v),
                                 _c.c_int(v.stride(0)), _p(o), _c.c_int(dm), _p(kmask), _p(lse), _c.c_int(CB),
                                 _c.c_int(S), _c.c_int(H), _f(scale), _c.c_uint32(_thr(p)),
-                                _f(1.0 / (1.0 - p) if p > 0 else 1.0), _c.c_uint32(seed & _M32), _stream(q))
+                                _f(1.0 / (1.0 - p) if p > 0 else 1.0), _c.c_uint32(seed & _M32), _p(seed_dev),
+                                _stream(q))
         _check(rc, "fa_attn_fwd")
         ctx.save_for_backward(q, k, v, o, lse, kmask)
         ctx.cfg = (S, H, p, seed)
+        ctx.seed_dev = seed_dev
         return o
 
     @staticmethod
@@ -186,21 +192,23 @@ class _Attention(torch.autograd.Function):
                                 _p(D), _p(dq), _c.c_int(dm), _p(dk), _c.c_int(dm), _p(dv), _c.c_int(dm),
                                 _c.c_int(CB), _c.c_int(S), _c.c_int(H), _f(1.0 / math.sqrt(64.0)),
                                 _c.c_uint32(_thr(p)), _f(1.0 / (1.0 - p) if p > 0 else 1.0),
-                                _c.c_uint32(seed & _M32), _stream(q))
+                                _c.c_uint32(seed & _M32), _p(ctx.seed_dev), _stream(q))
         _check(rc, "fa_attn_bwd")
-        return dq, dk, dv, None, None, None, None, None
+        return dq, dk, dv, None, None, None, None, None, None
 
 
-def attention(q, k, v, S: int, H: int, kmask: torch.Tensor = None, p: float = 0.0, seed: int = 0):
+def attention(q, k, v, S: int, H: int, kmask: torch.Tensor = None, p: float = 0.0, seed: int = 0,
+              seed_dev: torch.Tensor = None):
     """Multi-head self-attention over token-major ``[CB·S, H·64]`` q/k/v (row stride may exceed
-    H·64, e.g. column slices of a fused QKV output); ``kmask`` [CB, S] (nonzero = attend)."""
+    H·64, e.g. column slices of a fused QKV output); ``kmask`` [CB, S] (nonzero = attend);
+    ``seed_dev`` as in :func:`layer_norm`."""
     assert q.dim() == 2 and q.shape[1] == H * 64 and q.shape[0] % S == 0
     if use_native(q):
         assert S <= 256 and q.dtype == torch.bfloat16
         for t in (q, k, v):
             assert t.stride(1) == 1 and t.stride(0) % 8 == 0
         km = None if kmask is None else kmask.to(torch.uint8).contiguous()
-        return _Attention.apply(q, k, v, km, int(S), int(H), float(p), int(seed))
+        return _Attention.apply(q, k, v, km, int(S), int(H), float(p), int(seed), seed_dev)
     return _attn_ref(q, k, v, kmask, S, H, p, seed)
 
 

@@ -101,6 +101,7 @@ class BatchedTransformer:
         if self.dim != 64 * self.heads:
             raise UnsupportedTransformer(f"head dim {self.dim // self.heads} != 64")
         self.step_seed = 0
+        self._seed_dev = None
         self._sh = None
 
     # -------------------------------------------------------------------------------- helpers
@@ -127,14 +128,15 @@ class BatchedTransformer:
     def _ln(self, v, key, h, rows_per_client, res=None, p=0.0, seed=0, eps=None):
         d = h.shape[-1]
         y = T.layer_norm(h.reshape(-1, d), v[key + ".weight"], v[key + ".bias"], self.eps if eps is None else eps,
-                         rows_per_client, res=None if res is None else res.reshape(-1, d), p=p, seed=seed)
+                         rows_per_client, res=None if res is None else res.reshape(-1, d), p=p, seed=seed,
+                         seed_dev=self._seed_dev if h.is_cuda else None)
         return y.view(h.shape)
 
     def _attn(self, v, x, pre, S, kmask, training, dt, seed):
         C, Tk, d = x.shape
         qkv = self._qkv(v, x, pre, dt).view(C * Tk, 3 * d)
         a = T.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], S, self.heads, kmask=kmask,
-                        p=self.p_attn if training else 0.0, seed=seed)
+                        p=self.p_attn if training else 0.0, seed=seed, seed_dev=self._seed_dev if x.is_cuda else None)
         return self._lin(v, a.view(C, Tk, d), pre + ".out_lin", dt)
 
     # -------------------------------------------------------------------------------- forward
@@ -144,8 +146,16 @@ class BatchedTransformer:
         """``shadow``: key → bf16 view of the same slot in a bf16 copy of the arena that is current
         for this step (the linears' GEMMs then read bf16 weights)."""
         self._sh = shadow
-        self.step_seed = (self.step_seed + 1) & 0x7FFFFFFF
-        base = self.step_seed * 1000003
+        if x.is_cuda:
+            # dropout step counter on the device (kernels add counter·1000003 to their seeds): a
+            # captured HIP graph of the step then draws fresh masks on every replay
+            if self._seed_dev is None or self._seed_dev.device != x.device:
+                self._seed_dev = torch.zeros(1, dtype=torch.int32, device=x.device)
+            self._seed_dev.add_(1)
+            base = 0
+        else:
+            self.step_seed = (self.step_seed + 1) & 0x7FFFFFFF
+            base = self.step_seed * 1000003
         if self.kind == "distilbert":
             return self._distilbert(v, x, training, dtype, base)
         return self._vit(v, x, training, dtype, base)

@@ -103,6 +103,10 @@ class ClientBatchEngine:
         self._seq_bufs = None
         self._shadow = None            # bf16 copy of the params arena (transformer GEMM operand)
         self._shadow_stale = True
+        # opt-in: the eager transformer step is GPU-bound already (host launches run ahead), so the
+        # captured step measured the same rounds/s (scripts/gpu_tf_graph_ab.sh)
+        self._tf_capture = self.tf is not None and self.device.type == "cuda" and \
+            os.environ.get("FEDML_AMD_TF_GRAPHS", "0") == "1"
         self._active_cache = {}
         self._graphs = {}
         _LIVE_ENGINES.add(self)
@@ -218,6 +222,8 @@ class ClientBatchEngine:
                 sample_mask = None if uniform else mask.t().contiguous()     # [B, C]
                 if self.native_step is not None and sample_mask is None and self.use_graphs:
                     loss = self._graph_step(x, y, mask, b_c, active, lr, first)
+                elif self.tf is not None and self.use_graphs and self._tf_capture and sample_mask is None:
+                    loss = self._tf_graph_step(x, y, mask, b_c, active, lr, first)
                 elif self.sequential and self.tf is None and self.use_graphs and self._seq_capture and uniform:
                     loss = self._seq_graph_step(x, y, b_c, active, lr, first)
                 else:
@@ -483,6 +489,59 @@ class ClientBatchEngine:
             for sc in streams[:min(len(streams), len(b_c))]:
                 cur.wait_stream(sc)
         return losses.sum()
+
+    def _tf_loss(self, x, y, row_scale):
+        """Client-batched transformer forward + fused CE + backward (weight gradients land in the
+        gradient arena); returns the summed per-client mean loss."""
+        sh = self._shadow_views if self._shadow is not None else None    # refreshed outside the graph
+        out = self.tf.forward(self.views, x, training=True, dtype=self.compute_dtype, shadow=sh)
+        C, B = out.shape[0], out.shape[1]
+        logits = out.reshape(C * B, -1)
+        if not logits.is_contiguous():
+            logits = logits.contiguous()
+        loss = ops.FusedCrossEntropy.apply(logits, y.reshape(C * B), row_scale.reshape(C * B), None)
+        loss.backward()
+        return loss.detach()
+
+    def _tf_graph_step(self, x, y, mask, b_c, active, lr, first):
+        """Client-batched transformer step (grad zeroing, forward, CE, backward, fused optimizer that
+        also refreshes the bf16 weight shadow) as ONE HIP graph: the eager step issues ~600 kernel
+        launches from Python per step. The first occurrence of a geometry runs eagerly and is captured
+        right after; dropout masks stay fresh per replay through the device step counter of
+        ``BatchedTransformer`` and torch's graph-safe RNG. A capture failure falls back to eager."""
+        key = ("tf", tuple(x.shape), tuple(y.shape), float(lr), bool(first))
+        ent = self._graphs.get(key)
+        if ent is None:
+            loss = self._step_loss(x, y, mask, b_c, active, None, True)
+            self._optimizer_step(lr, active, first)
+            st = {"x": torch.empty_like(x), "y": torch.empty_like(y),
+                  "rs": torch.empty(mask.shape, dtype=torch.float32, device=self.device),
+                  "act": torch.empty_like(active)}
+            self._bf16_shadow()
+            s = torch.cuda.Stream(device=self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            g = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+                    self.grads.zero_()
+                    gl = self._tf_loss(st["x"], st["y"], st["rs"])
+                    self._optimizer_step(lr, st["act"], first)
+            except Exception as e:  # noqa: BLE001 - any capture problem: keep the eager step
+                logging.warning("transformer step capture failed (%s); running eagerly", e)
+                torch.cuda.current_stream(self.device).wait_stream(s)
+                self._tf_capture = False
+                self._shadow_stale = True
+                return loss
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            self._shadow_stale = self.optimizer == "sgd"
+            self._graphs[key] = (g, st, gl)
+            return loss
+        g, st, loss = ent
+        self._bf16_shadow()      # a cast only when stale (after load_global, or SGD which leaves it stale)
+        self._fill_static(st, x, y, mask, b_c, active)
+        g.replay()
+        self._shadow_stale = self.optimizer == "sgd"
+        return loss
 
     def _seq_graph_step(self, x, y, b_c, active, lr, first):
         """Per-client (wide conv net) local step as ONE HIP graph whose C client branches run on C

@@ -181,3 +181,42 @@ def test_client_linear_fwd_bwd(C, M, K, ns, gelu, own, shadow):
         _close(w.grad, wr.grad, 2e-2)
     for b, br in zip(bs, b32):
         _close(b.grad, br.grad, 2e-2)
+
+
+@pytest.mark.parametrize("opt", ["adamw", "sgd"])
+def test_transformer_graph_step_matches_eager(opt):
+    """The captured client-batched transformer step (HIP graph) leaves the arenas where eager steps
+    do (dropout off: the masks are the only replay-dependent input)."""
+    import copy
+    from fedml_amd.arguments import Arguments
+    from fedml_amd.models.transformer.distilbert import distilbert
+    from fedml_amd.simulation.rccl.client_store import DeviceClientStore
+    from fedml_amd.simulation.rccl.engine import ClientBatchEngine
+    torch.manual_seed(0)
+    model = distilbert(num_labels=3, max_pos=64, n_layers=2)
+    for m in model.modules():
+        if isinstance(m, torch.nn.Dropout):
+            m.p = 0.0
+    C, n, S = 3, 32, 32
+    ids = torch.randint(1, 1000, (C * n, S), device=dev)
+    lab = torch.randint(0, 3, (C * n,), device=dev)
+    outs = []
+    for graphs in (False, True):
+        args = Arguments.from_dict({"x": {"client_optimizer": opt, "learning_rate": 1e-3}})
+        eng = ClientBatchEngine(copy.deepcopy(model).to(dev), C, dev, args, compute_dtype=torch.bfloat16)
+        assert eng.tf is not None
+        eng.tf.p_attn = eng.tf.p_hidden = eng.tf.p_emb = eng.tf.p_cls = 0.0
+        eng.use_graphs = graphs
+        eng._tf_capture = graphs          # opt-in path (FEDML_AMD_TF_GRAPHS=1)
+        eng.load_global(eng.layout.flatten(model.state_dict(), device=dev))
+        store = DeviceClientStore(ids, lab, [i * n for i in range(C)], [n] * C)
+        loss = float(eng.train(store, torch.arange(C, device=dev), 1, 8, 1e-3, shuffle=False))
+        torch.cuda.synchronize()
+        outs.append((loss, eng.params.clone()))
+        if graphs:
+            assert any(isinstance(v, tuple) for v in eng._graphs.values())
+        eng.close()
+    (l0, p0), (l1, p1) = outs
+    init = eng.layout.flatten(model.state_dict(), device=dev)
+    assert abs(l0 - l1) / abs(l0) < 1e-2
+    assert float((p0 - p1).norm() / (p0 - init).norm()) < 2e-2
