@@ -34,6 +34,8 @@ from .fl_ops import (
     augment,
     mod_sum,
     use_native,
+    ShadowSeg,
+    pack_conv_shadow,
 )
 from .norm_ops import FusedGroupNorm, fuse_group_norm, group_norm
 

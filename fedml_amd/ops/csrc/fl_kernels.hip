@@ -826,3 +826,41 @@ FA_EXPORT int fa_cast_bf16(const float* x, uint16_t* y, int64_t n, hipStream_t s
   hipLaunchKernelGGL(cast_bf16_kernel, dim3(fa_grid(n, 256, 2048)), dim3(256), 0, stream, x, y, n);
   return (int)hipGetLastError();
 }
+
+// =====================================================================================
+// bf16 channels-last shadow of conv weights for the per-client (library conv) path: one launch
+// writes every conv layer's OIHW fp32 master as bf16 OHWI (= an NCHW tensor with channels_last
+// strides), so MIOpen's NHWC convolutions read it without a per-layer cast + layout copy.
+// =====================================================================================
+struct ShadowSeg {
+  int64_t off;    // element offset of the weight slot in a client row (same in both arenas)
+  int O, I, KH, KW;
+};
+
+__global__ __launch_bounds__(256) void pack_conv_shadow_kernel(const float* __restrict__ params, int64_t ldp,
+                                                               uint16_t* __restrict__ shadow, int64_t lds,
+                                                               const ShadowSeg* __restrict__ segs) {
+  const ShadowSeg sg = segs[blockIdx.z];
+  const int c = blockIdx.y;
+  const int KK = sg.KH * sg.KW;
+  const int n = sg.O * sg.I * KK;
+  const float* src = params + (int64_t)c * ldp + sg.off;
+  uint16_t* dst = shadow + (int64_t)c * lds + sg.off;
+  for (int j = blockIdx.x * blockDim.x + threadIdx.x; j < n; j += gridDim.x * blockDim.x) {
+    // j indexes the OHWI destination: o, (h, w), i
+    const int i = j % sg.I;
+    const int t = j / sg.I;
+    const int hw = t % KK;
+    const int o = t / KK;
+    dst[j] = f32_to_bf16(src[((int64_t)o * sg.I + i) * KK + hw]);
+  }
+}
+
+FA_EXPORT int fa_pack_conv_shadow(const float* params, int64_t ldp, void* shadow, int64_t lds, const void* segs,
+                                  int nseg, int max_n, int C, hipStream_t stream) {
+  if (nseg <= 0) return 0;
+  if (nseg > 65535 || C > 65535) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(pack_conv_shadow_kernel, dim3(fa_grid(max_n, 256, 128), C, nseg), dim3(256), 0, stream, params,
+                     ldp, (uint16_t*)shadow, lds, (const ShadowSeg*)segs);
+  return (int)hipGetLastError();
+}

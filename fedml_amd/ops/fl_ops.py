@@ -596,3 +596,18 @@ def augment(x, seed=0, sample_ids=None, pad=4, cutout=16, flip=True, mean=None, 
             shifted = (shifted - mean_t.view(-1, 1, 1)) * inv_t.view(-1, 1, 1)
         out[b] = shifted
     return out
+
+
+# ----------------------------------------------------------------------------- conv weight shadow
+class ShadowSeg(ctypes.Structure):
+    _fields_ = [("off", ctypes.c_int64), ("O", ctypes.c_int), ("I", ctypes.c_int), ("KH", ctypes.c_int),
+                ("KW", ctypes.c_int)]
+
+
+def pack_conv_shadow(params, shadow, segs_dev, nseg, max_n):
+    """bf16 OHWI (channels-last) copies of the conv weights of a [C, P] fp32 arena into the same slots
+    of a [C, P] bf16 arena (``segs_dev``: uint8 device tensor of ``ShadowSeg`` records)."""
+    C = params.shape[0]
+    rc = _fn("fa_pack_conv_shadow")(_p(params), _i64(params.stride(0)), _p(shadow), _i64(shadow.stride(0)),
+                                    _p(segs_dev), _c.c_int(nseg), _c.c_int(max_n), _c.c_int(C), _stream(params))
+    _check(rc, "fa_pack_conv_shadow")

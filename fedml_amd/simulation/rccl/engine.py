@@ -432,6 +432,33 @@ class ClientBatchEngine:
                 out[sl.key] = self.params[c, sl.offset:sl.offset + sl.numel].view(sl.shape).to(sl.dtype).clone()
         return out
 
+    def _conv_shadow_views(self):
+        """Refresh (one launch: ``ops.pack_conv_shadow``) and return, per client, bf16 leaves of every
+        dense conv weight laid out OHWI in a packed shadow arena — NCHW tensors with channels-last
+        strides, the layout MIOpen's NHWC convolutions read directly. None if the model has none."""
+        if getattr(self, "_cshadow_views", None) is None:
+            segs, views, mx = [], [dict() for _ in range(self.C)], 0
+            slots = {sl.key: sl for sl in self.layout.slots}
+            self._cshadow = torch.zeros(self.params.shape, dtype=torch.bfloat16, device=self.device)
+            for name, m in self.model.named_modules():
+                sl = slots.get(f"{name}.weight")
+                if not isinstance(m, torch.nn.Conv2d) or m.groups != 1 or sl is None or not sl.trainable:
+                    continue
+                O, I, KH, KW = sl.shape
+                segs.append(ops.ShadowSeg(sl.offset, O, I, KH, KW))
+                mx = max(mx, sl.numel)
+                for c in range(self.C):
+                    t = self._cshadow[c, sl.offset:sl.offset + sl.numel].view(O, KH, KW, I).permute(0, 3, 1, 2)
+                    views[c][sl.key] = t.detach().requires_grad_(True)
+            self._cshadow_views = views if segs else []
+            self._cshadow_n, self._cshadow_max = len(segs), mx
+            raw = bytes((ops.ShadowSeg * max(1, len(segs)))(*segs))
+            self._cshadow_segs = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(self.device)
+        if not self._cshadow_views:
+            return None
+        ops.pack_conv_shadow(self.params, self._cshadow, self._cshadow_segs, self._cshadow_n, self._cshadow_max)
+        return self._cshadow_views
+
     def _seq_step_loss(self, x, y, b_c, zero=False, streams=None):
         """Clients one after another on the arenas (``streams``: client c on ``streams[c % n]``,
         forked from and joined back into the current stream).
@@ -447,6 +474,10 @@ class ClientBatchEngine:
         amp = self.compute_dtype is not None and self.device.type == "cuda"
         cl = self.device.type == "cuda" and x.dim() == 5 and not self._has_gn and \
             os.environ.get("FEDML_AMD_SEQ_CHANNELS_LAST", "1") != "0"
+        # conv weights as bf16 channels-last leaves of one packed shadow (refreshed by ONE launch per
+        # step) instead of an autocast cast + a layout copy per conv and client
+        cviews = self._conv_shadow_views() if (cl and amp and self.compute_dtype == torch.bfloat16 and
+                                               os.environ.get("FEDML_AMD_SEQ_CONV_SHADOW", "1") != "0") else None
         cur = torch.cuda.current_stream(self.device) if streams else None
         losses = torch.zeros(self.C, device=self.device)
         for c, b in enumerate(b_c):
@@ -463,17 +494,22 @@ class ClientBatchEngine:
                 if cl:
                     xc = xc.contiguous(memory_format=torch.channels_last)
                 # no autocast weight cache under capture (a graph must not keep casts of live weights)
+                pv = views[c] if cviews is None else {**views[c], **cviews[c]}
                 with torch.autocast("cuda", dtype=self.compute_dtype or torch.bfloat16, enabled=amp,
                                     cache_enabled=not streams):
-                    out = torch.func.functional_call(self.model, {**views[c], **bufs}, (xc,))
+                    out = torch.func.functional_call(self.model, {**pv, **bufs}, (xc,))
                 if isinstance(out, tuple):
                     out = out[-1]
                 loss = torch.nn.functional.cross_entropy(out.float().reshape(b, -1), y[c, :b].reshape(b))
-                leaves = list(views[c].values())
+                keys = list(pv.keys())
+                leaves = [pv[k] for k in keys]
                 grads = torch.autograd.grad(loss, leaves, allow_unused=True)
                 with torch.no_grad():
-                    dst = [v.grad for v, g in zip(leaves, grads) if g is not None]
+                    # fp32 OIHW gradient-arena rows (conv grads arrive bf16 channels-last: the
+                    # multi-tensor copy converts dtype and layout)
+                    dst = [views[c][k].grad for k, g in zip(keys, grads) if g is not None]
                     src = [g for g in grads if g is not None]
+                    leaves = [views[c][k] for k in keys]
                     if zero:
                         torch._foreach_add_(dst, src)
                     else:

@@ -347,3 +347,33 @@ def test_padding_slot_keeps_native_graph_path():
         eng.close()
     p0, p1 = outs
     assert float((p0[:2] - p1[:2]).norm() / p0[:2].norm()) < 1e-3
+
+
+def test_conv_weight_shadow_matches_autocast_path(monkeypatch):
+    """Per-client path with bf16 channels-last conv-weight leaves from the packed shadow ≡ the
+    autocast path (same bf16 rounding of the fp32 masters; only MIOpen's algorithm choice differs)."""
+    from fedml_amd.arguments import Arguments
+    from fedml_amd.models.cv.resnet import resnet18_cifar
+    from fedml_amd.simulation.rccl.client_store import DeviceClientStore
+    from fedml_amd.simulation.rccl.engine import ClientBatchEngine
+    torch.manual_seed(0)
+    model = resnet18_cifar(10)
+    C, n = 2, 64
+    store = DeviceClientStore(torch.randn(C * n, 3, 16, 16, device=DEV), torch.randint(0, 10, (C * n,), device=DEV),
+                              [i * n for i in range(C)], [n] * C)
+    outs = []
+    for shadow in ("0", "1"):
+        monkeypatch.setenv("FEDML_AMD_SEQ_CONV_SHADOW", shadow)
+        args = Arguments.from_dict({"x": {"client_optimizer": "sgd", "learning_rate": 1e-3}})
+        eng = ClientBatchEngine(copy.deepcopy(model).to(DEV), C, DEV, args, compute_dtype=torch.bfloat16)
+        eng.load_global(eng.layout.flatten(model.state_dict(), device=DEV))
+        loss = float(eng.train(store, torch.arange(C, device=DEV), 1, 32, 1e-3, shuffle=False))
+        torch.cuda.synchronize()
+        outs.append((loss, eng.params.clone()))
+        if shadow == "1":
+            assert eng._cshadow_views      # the shadow path ran
+        eng.close()
+    (l0, p0), (l1, p1) = outs
+    init = ParamLayout.from_module(model).flatten(model.state_dict(), device=DEV)
+    assert abs(l0 - l1) / abs(l0) < 1e-2
+    assert float((p0 - p1).norm() / (p0 - init).norm()) < 5e-2
