@@ -9,6 +9,8 @@ model, which the reference does not ship.
 import torch
 import torch.nn as nn
 
+from ...ops.bn_ops import batch_norm_act
+
 
 def conv3x3(in_planes, out_planes, stride=1, groups=1, dilation=1):
     return nn.Conv2d(in_planes, out_planes, kernel_size=3, stride=stride, padding=dilation, groups=groups,
@@ -35,12 +37,16 @@ class BasicBlock(nn.Module):
         self.stride = stride
 
     def forward(self, x):
+        # act(bn(conv) [+ identity]) as one fused pass on NHWC bf16 GPU activations (ops.bn_ops)
         identity = x
-        out = self.relu(self.bn1(self.conv1(x)))
-        out = self.bn2(self.conv2(out))
+        out = batch_norm_act(self.bn1, self.conv1(x), relu=True)
         if self.downsample is not None:
-            identity = self.downsample(x)
-        return self.relu(out + identity)
+            ds = self.downsample
+            if isinstance(ds, nn.Sequential) and len(ds) == 2 and isinstance(ds[1], nn.BatchNorm2d):
+                identity = batch_norm_act(ds[1], ds[0](x))
+            else:
+                identity = ds(x)
+        return batch_norm_act(self.bn2, self.conv2(out), residual=identity, relu=True)
 
 
 class Bottleneck(nn.Module):
@@ -173,7 +179,7 @@ class ResNet18Cifar(nn.Module):
         return nn.Sequential(*layers)
 
     def forward(self, x):
-        x = self.relu(self.bn1(self.conv1(x)))
+        x = batch_norm_act(self.bn1, self.conv1(x), relu=True)
         x = self.layer4(self.layer3(self.layer2(self.layer1(x))))
         return self.fc(torch.flatten(self.avgpool(x), 1))
 
