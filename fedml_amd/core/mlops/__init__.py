@@ -9,8 +9,9 @@ from .mlops_runtime_log import MLOpsRuntimeLog
 from .mlops_profiler_event import MLOpsProfilerEvent
 from .mlops_metrics import MLOpsMetrics
 from .system_stats import SysStats
+from .mlops_configs import MLOpsConfigs
 
-__all__ = ["MLOpsRuntimeLog", "MLOpsProfilerEvent", "MLOpsMetrics", "SysStats", "log_round_info", "event"]
+__all__ = ["MLOpsRuntimeLog", "MLOpsProfilerEvent", "MLOpsMetrics", "SysStats", "MLOpsConfigs", "log_round_info", "event"]
 
 
 def event(name: str, started: bool = True, value=None, edge_id: int = 0):

@@ -125,3 +125,32 @@ def test_pubsub_blob_store_and_last_will():
     assert torch.equal(got.get("model_params")["w"], m.get("model_params")["w"])
     client.stop_receive_message(clean=False)   # unclean → last will published
     assert 0 in server.offline or 1 in server.offline
+
+
+def test_mlops_configs_resolution(tmp_path, monkeypatch):
+    """MLOpsConfigs (reference core/mlops/mlops_configs.py): args > file > env > defaults, no remote fetch."""
+    import json as _json
+    import types
+    from fedml_amd.core.mlops import MLOpsConfigs
+    monkeypatch.delenv("FEDML_AMD_MQTT_CONFIG", raising=False)
+    monkeypatch.delenv("FEDML_AMD_S3_CONFIG", raising=False)
+    MLOpsConfigs.reset()
+    args = types.SimpleNamespace(blob_root=str(tmp_path / "blobs"))
+    mqtt, s3 = MLOpsConfigs.get_instance(args).fetch_configs()
+    assert mqtt["BROKER_HOST"] == "inproc" and s3["LOCAL_ROOT"] == str(tmp_path / "blobs")
+
+    cfg = tmp_path / "mlops.yaml"
+    cfg.write_text("mqtt_config:\n  BROKER_HOST: inproc\n  BROKER_PORT: 1999\ns3_config:\n  LOCAL_ROOT: %s\n" % (tmp_path / "f"))
+    args.mlops_config_path = str(cfg)
+    monkeypatch.setenv("FEDML_AMD_S3_CONFIG", _json.dumps({"LOCAL_ROOT": "ignored"}))
+    mqtt, s3 = MLOpsConfigs.get_instance(args).fetch_configs()
+    assert mqtt["BROKER_PORT"] == 1999 and s3["LOCAL_ROOT"] == str(tmp_path / "f")
+
+    args.customized_training_mqtt_config = {"BROKER_HOST": "inproc", "BROKER_PORT": 7}
+    mqtt, s3 = MLOpsConfigs.get_instance(args).fetch_configs()
+    assert mqtt["BROKER_PORT"] == 7 and s3["LOCAL_ROOT"] == str(tmp_path / "f")
+
+    broker, store = MLOpsConfigs.get_instance(args).build_backends(run_id="r1")
+    url = store.write("k", b"abc")
+    assert store.read(url) == b"abc"
+    MLOpsConfigs.reset()
