@@ -37,7 +37,7 @@ def parse():
     p.add_argument("--epochs", type=int, default=1)
     p.add_argument("--model", default="resnet56")
     p.add_argument("--dataset", default="cifar100")
-    p.add_argument("--dtype", default="bf16")
+    p.add_argument("--dtype", default="fp32", help="fp32 (the reference's training precision) | bf16")
     p.add_argument("--lr", type=float, default=0.001)
     p.add_argument("--profile-rounds", type=int, default=0)
     p.add_argument("--optimizer", default="FedAvg", help="FedAvg | FedOpt (server Adam)")

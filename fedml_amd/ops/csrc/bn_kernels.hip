@@ -1,23 +1,11 @@
 // Per-(client, channel) BatchNorm finalisation, fused block epilogues and small layout kernels
 // for the native client-batched ResNet executor. Layout as in conv_kernels.hip:
-// activations [C][N][H][W][Ch] bf16; vectors [C][Ch] fp32; parameters/grads in the client-stacked
+// activations [C][N][H][W][Ch] bf16 | fp32 (`_f32` entry points); vectors [C][Ch] fp32; parameters/grads in the client-stacked
 // fp32 arenas [C][ldw] addressed by offset.
-#include "common.h"
+#include "prec.h"
 
-__device__ __forceinline__ void unpack8f(uint4 v, float* f) {
-  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
-  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
-  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
-  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
-}
-__device__ __forceinline__ uint4 pack8f(const float* f) {
-  uint4 r;
-  r.x = (uint32_t)f32_to_bf16(f[0]) | ((uint32_t)f32_to_bf16(f[1]) << 16);
-  r.y = (uint32_t)f32_to_bf16(f[2]) | ((uint32_t)f32_to_bf16(f[3]) << 16);
-  r.z = (uint32_t)f32_to_bf16(f[4]) | ((uint32_t)f32_to_bf16(f[5]) << 16);
-  r.w = (uint32_t)f32_to_bf16(f[6]) | ((uint32_t)f32_to_bf16(f[7]) << 16);
-  return r;
-}
+using prec::BF16;
+using prec::F32;
 
 // ---- forward finalisation: statistics → folded scale/shift, running-stat update ----
 // stats[c][ch][2] = (Σy, Σy²) over n = N·H·W elements of client c.
@@ -99,88 +87,106 @@ FA_EXPORT int fa_bn_bwd_finalize(const float* bstats, int NS, int q_gy, int C, i
 }
 
 // ---- fused block output: out = relu(y·s + t + R), R = yd·sd + td (downsample) | x (identity) | 0
-// One 16-B vector per thread (no grid-stride loop, no 64-bit modulo); the per-channel vectors are
-// read as float4 (L1-resident). Streams 3 bf16 tensors: HBM-bound by construction.
-template <int RES>  // 0: no residual, 1: identity, 2: downsample-BN residual
-__global__ __launch_bounds__(256) void block_out_kernel(const uint16_t* __restrict__ y, const float* __restrict__ s,
-                                                        const float* __restrict__ t, const uint16_t* __restrict__ r,
+// One 16-B vector (P::VEC channels) per thread (no grid-stride loop, no 64-bit modulo); the
+// per-channel vectors are read as float4 (L1-resident). Streams 3 tensors: HBM-bound by construction.
+template <class P, int RES>  // RES 0: no residual, 1: identity, 2: downsample-BN residual
+__global__ __launch_bounds__(256) void block_out_kernel(const typename P::T* __restrict__ y, const float* __restrict__ s,
+                                                        const float* __restrict__ t,
+                                                        const typename P::T* __restrict__ r,
                                                         const float* __restrict__ rs, const float* __restrict__ rt,
-                                                        uint16_t* __restrict__ out, int nvec, int cg) {
+                                                        typename P::T* __restrict__ out, int nvec, int cg) {
+  constexpr int V = P::VEC;
   const int c = blockIdx.y;
   const int v = blockIdx.x * 256 + threadIdx.x;
   if (v >= nvec) return;
-  const int64_t base = (int64_t)c * nvec * 8 + (int64_t)v * 8;
-  const int ch0 = (v % cg) * 8;
-  const int64_t co = (int64_t)c * cg * 8 + ch0;
+  const int64_t base = (int64_t)c * nvec * V + (int64_t)v * V;
+  const int ch0 = (v % cg) * V;
+  const int64_t co = (int64_t)c * cg * V + ch0;
   const uint4 yv = *reinterpret_cast<const uint4*>(y + base);
   uint4 rv = make_uint4(0, 0, 0, 0);
   if (RES) rv = *reinterpret_cast<const uint4*>(r + base);
-  const float4 s0 = *reinterpret_cast<const float4*>(s + co), s1 = *reinterpret_cast<const float4*>(s + co + 4);
-  const float4 t0 = *reinterpret_cast<const float4*>(t + co), t1 = *reinterpret_cast<const float4*>(t + co + 4);
-  const float sv[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
-  const float tv[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
-  float f[8], g[8];
-  unpack8f(yv, f);
+  float f[V], g[V];
+  P::unpack(yv, f);
 #pragma unroll
-  for (int j = 0; j < 8; ++j) f[j] = f[j] * sv[j] + tv[j];
+  for (int j = 0; j < V; ++j) f[j] = f[j] * s[co + j] + t[co + j];
   if (RES) {
-    unpack8f(rv, g);
+    P::unpack(rv, g);
     if (RES == 2) {
-      const float4 a0 = *reinterpret_cast<const float4*>(rs + co), a1 = *reinterpret_cast<const float4*>(rs + co + 4);
-      const float4 b0 = *reinterpret_cast<const float4*>(rt + co), b1 = *reinterpret_cast<const float4*>(rt + co + 4);
-      const float av[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-      const float bv[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
 #pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] += g[j] * av[j] + bv[j];
+      for (int j = 0; j < V; ++j) f[j] += g[j] * rs[co + j] + rt[co + j];
     } else {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) f[j] += g[j];
+      for (int j = 0; j < V; ++j) f[j] += g[j];
     }
   }
 #pragma unroll
-  for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j], 0.f);
-  *reinterpret_cast<uint4*>(out + base) = pack8f(f);
+  for (int j = 0; j < V; ++j) f[j] = fmaxf(f[j], 0.f);
+  *reinterpret_cast<uint4*>(out + base) = P::pack(f);
+}
+
+template <class P>
+static int block_out(const void* y, const float* s, const float* t, const void* r, const float* rs, const float* rt,
+                     void* out, int C, int64_t per_client, int Ch, hipStream_t stream) {
+  using T = typename P::T;
+  constexpr int V = P::VEC;
+  if (Ch % V != 0 || per_client / V > INT32_MAX) return -3;
+  const int nvec = (int)(per_client / V);
+  dim3 grid((nvec + 255) / 256, C);
+  const T* y_ = (const T*)y;
+  const T* r_ = (const T*)r;
+  T* o_ = (T*)out;
+  if (!r)
+    hipLaunchKernelGGL((block_out_kernel<P, 0>), grid, dim3(256), 0, stream, y_, s, t, r_, rs, rt, o_, nvec, Ch / V);
+  else if (!rs)
+    hipLaunchKernelGGL((block_out_kernel<P, 1>), grid, dim3(256), 0, stream, y_, s, t, r_, rs, rt, o_, nvec, Ch / V);
+  else
+    hipLaunchKernelGGL((block_out_kernel<P, 2>), grid, dim3(256), 0, stream, y_, s, t, r_, rs, rt, o_, nvec, Ch / V);
+  return (int)hipGetLastError();
 }
 
 FA_EXPORT int fa_block_out(const uint16_t* y, const float* s, const float* t, const uint16_t* r, const float* rs,
                            const float* rt, uint16_t* out, int C, int64_t per_client, int Ch, hipStream_t stream) {
-  if (Ch % 8 != 0 || per_client / 8 > INT32_MAX) return -3;
-  const int nvec = (int)(per_client / 8);
-  dim3 grid((nvec + 255) / 256, C);
-  if (!r)
-    hipLaunchKernelGGL(block_out_kernel<0>, grid, dim3(256), 0, stream, y, s, t, r, rs, rt, out, nvec, Ch / 8);
-  else if (!rs)
-    hipLaunchKernelGGL(block_out_kernel<1>, grid, dim3(256), 0, stream, y, s, t, r, rs, rt, out, nvec, Ch / 8);
-  else
-    hipLaunchKernelGGL(block_out_kernel<2>, grid, dim3(256), 0, stream, y, s, t, r, rs, rt, out, nvec, Ch / 8);
-  return (int)hipGetLastError();
+  return block_out<BF16>(y, s, t, r, rs, rt, out, C, per_client, Ch, stream);
+}
+FA_EXPORT int fa_block_out_f32(const float* y, const float* s, const float* t, const float* r, const float* rs,
+                               const float* rt, float* out, int C, int64_t per_client, int Ch, hipStream_t stream) {
+  return block_out<F32>(y, s, t, r, rs, rt, out, C, per_client, Ch, stream);
 }
 
 // ---- global average pool (forward): pooled[c][n][ch] = mean_hw out[c][n][hw][ch] (fp32 out)
-__global__ __launch_bounds__(256) void avgpool_kernel(const uint16_t* __restrict__ x, float* __restrict__ pooled,
+template <class P>
+__global__ __launch_bounds__(256) void avgpool_kernel(const typename P::T* __restrict__ x, float* __restrict__ pooled,
                                                       int HW, int Ch) {
   const int cn = blockIdx.x;  // flattened (client, sample)
-  const uint16_t* xs = x + (int64_t)cn * HW * Ch;
+  const typename P::T* xs = x + (int64_t)cn * HW * Ch;
   for (int ch = threadIdx.x; ch < Ch; ch += blockDim.x) {
     float s = 0.f;
-    for (int p = 0; p < HW; ++p) s += bf16_to_f32(xs[(int64_t)p * Ch + ch]);
+    for (int p = 0; p < HW; ++p) s += P::to_f(xs[(int64_t)p * Ch + ch]);
     pooled[(int64_t)cn * Ch + ch] = s / (float)HW;
   }
 }
 
 FA_EXPORT int fa_avgpool(const uint16_t* x, float* pooled, int CN, int HW, int Ch, hipStream_t stream) {
-  hipLaunchKernelGGL(avgpool_kernel, dim3(CN), dim3(Ch < 256 ? 64 * ((Ch + 63) / 64) : 256), 0, stream, x, pooled,
-                     HW, Ch);
+  hipLaunchKernelGGL(avgpool_kernel<BF16>, dim3(CN), dim3(Ch < 256 ? 64 * ((Ch + 63) / 64) : 256), 0, stream, x,
+                     pooled, HW, Ch);
+  return (int)hipGetLastError();
+}
+FA_EXPORT int fa_avgpool_f32(const float* x, float* pooled, int CN, int HW, int Ch, hipStream_t stream) {
+  hipLaunchKernelGGL(avgpool_kernel<F32>, dim3(CN), dim3(Ch < 256 ? 64 * ((Ch + 63) / 64) : 256), 0, stream, x,
+                     pooled, HW, Ch);
   return (int)hipGetLastError();
 }
 
 // ---- head backward: gpre = (dpool/HW)·[out > 0]; stats (Σg, Σg·y3, Σg·yd)
 // one workgroup per (client, sample): channels across threads, spatial loop inside,
 // per-channel partial sums atomically added once per workgroup.
-__global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__ dpool, const uint16_t* __restrict__ out,
-                                                       const uint16_t* __restrict__ y3, const uint16_t* __restrict__ yd,
-                                                       uint16_t* __restrict__ gpre, float* __restrict__ stats, int N,
-                                                       int HW, int Ch, int NS) {
+template <class P>
+__global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__ dpool,
+                                                       const typename P::T* __restrict__ out,
+                                                       const typename P::T* __restrict__ y3,
+                                                       const typename P::T* __restrict__ yd,
+                                                       typename P::T* __restrict__ gpre, float* __restrict__ stats,
+                                                       int N, int HW, int Ch, int NS) {
   const int cn = blockIdx.x;
   const int c = cn / N;
   const int64_t base = (int64_t)cn * HW * Ch;
@@ -190,13 +196,13 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
     float a0 = 0.f, a1 = 0.f, a2 = 0.f;
     for (int p = 0; p < HW; ++p) {
       const int64_t i = base + (int64_t)p * Ch + ch;
-      const float g = bf16_to_f32(out[i]) > 0.f ? d : 0.f;
-      const uint16_t gb = f32_to_bf16(g);
+      const float g = P::to_f(out[i]) > 0.f ? d : 0.f;
+      const typename P::T gb = P::from_f(g);
       gpre[i] = gb;
-      const float gr = bf16_to_f32(gb);
+      const float gr = P::to_f(gb);
       a0 += gr;
-      a1 += gr * bf16_to_f32(y3[i]);
-      if (yd) a2 += gr * bf16_to_f32(yd[i]);
+      a1 += gr * P::to_f(y3[i]);
+      if (yd) a2 += gr * P::to_f(yd[i]);
     }
     float* st = stats + ((int64_t)c * Ch + ch) * NS;
     atomicAdd(st + 0, a0);
@@ -207,28 +213,42 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
 
 FA_EXPORT int fa_head_bwd(const float* dpool, const uint16_t* out, const uint16_t* y3, const uint16_t* yd,
                           uint16_t* gpre, float* stats, int C, int N, int HW, int Ch, int NS, hipStream_t stream) {
-  hipLaunchKernelGGL(head_bwd_kernel, dim3(C * N), dim3(Ch < 256 ? 64 * ((Ch + 63) / 64) : 256), 0, stream, dpool,
-                     out, y3, yd, gpre, stats, N, HW, Ch, NS);
+  hipLaunchKernelGGL(head_bwd_kernel<BF16>, dim3(C * N), dim3(Ch < 256 ? 64 * ((Ch + 63) / 64) : 256), 0, stream,
+                     dpool, out, y3, yd, gpre, stats, N, HW, Ch, NS);
+  return (int)hipGetLastError();
+}
+FA_EXPORT int fa_head_bwd_f32(const float* dpool, const float* out, const float* y3, const float* yd, float* gpre,
+                              float* stats, int C, int N, int HW, int Ch, int NS, hipStream_t stream) {
+  hipLaunchKernelGGL(head_bwd_kernel<F32>, dim3(C * N), dim3(Ch < 256 ? 64 * ((Ch + 63) / 64) : 256), 0, stream,
+                     dpool, out, y3, yd, gpre, stats, N, HW, Ch, NS);
   return (int)hipGetLastError();
 }
 
-// ---- input conversion: x [C][N][Cin][H][W] fp32 (NCHW per client) → [C][N][H][W][Cpad] bf16
-__global__ __launch_bounds__(256) void nchw_to_nhwc_pad_kernel(const float* __restrict__ x, uint16_t* __restrict__ y,
-                                                               int64_t CN, int Cin, int HW, int Cpad) {
+// ---- input conversion: x [C][N][Cin][H][W] fp32 (NCHW per client) → [C][N][H][W][Cpad] bf16 | fp32
+template <class P>
+__global__ __launch_bounds__(256) void nchw_to_nhwc_pad_kernel(const float* __restrict__ x,
+                                                               typename P::T* __restrict__ y, int64_t CN, int Cin,
+                                                               int HW, int Cpad) {
   const int64_t total = CN * HW;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t cn = i / HW;
     const int p = (int)(i % HW);
     const float* src = x + cn * Cin * HW + p;
-    uint16_t* dst = y + i * Cpad;
-    for (int ch = 0; ch < Cpad; ++ch) dst[ch] = ch < Cin ? f32_to_bf16(src[(int64_t)ch * HW]) : (uint16_t)0;
+    typename P::T* dst = y + i * Cpad;
+    for (int ch = 0; ch < Cpad; ++ch) dst[ch] = ch < Cin ? P::from_f(src[(int64_t)ch * HW]) : P::from_f(0.f);
   }
 }
 
 FA_EXPORT int fa_nchw_to_nhwc_pad(const float* x, uint16_t* y, int64_t CN, int Cin, int HW, int Cpad,
                                   hipStream_t stream) {
-  hipLaunchKernelGGL(nchw_to_nhwc_pad_kernel, dim3(fa_grid(CN * HW, 256, 4096)), dim3(256), 0, stream, x, y, CN, Cin,
-                     HW, Cpad);
+  hipLaunchKernelGGL(nchw_to_nhwc_pad_kernel<BF16>, dim3(fa_grid(CN * HW, 256, 4096)), dim3(256), 0, stream, x, y, CN,
+                     Cin, HW, Cpad);
+  return (int)hipGetLastError();
+}
+FA_EXPORT int fa_nchw_to_nhwc_pad_f32(const float* x, float* y, int64_t CN, int Cin, int HW, int Cpad,
+                                      hipStream_t stream) {
+  hipLaunchKernelGGL(nchw_to_nhwc_pad_kernel<F32>, dim3(fa_grid(CN * HW, 256, 4096)), dim3(256), 0, stream, x, y, CN,
+                     Cin, HW, Cpad);
   return (int)hipGetLastError();
 }
 

@@ -10,62 +10,41 @@
 // prefetched into registers while the current one is multiplied. For 1×1 convolutions the GEMM
 // layout [co][ci] IS the OIHW layout, so the partial sums go straight into the gradient arena
 // with fp32 atomics — no scratch / scatter pass.
-#include "common.h"
+#include "prec.h"
 
 namespace c1 {
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef short v4i16 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
-
-__device__ __forceinline__ void unpack8(uint4 v, float* f) {
-  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
-  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
-  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
-  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
-}
-__device__ __forceinline__ uint4 pack8(const float* f) {
-  uint4 r;
-  r.x = (uint32_t)f32_to_bf16(f[0]) | ((uint32_t)f32_to_bf16(f[1]) << 16);
-  r.y = (uint32_t)f32_to_bf16(f[2]) | ((uint32_t)f32_to_bf16(f[3]) << 16);
-  r.z = (uint32_t)f32_to_bf16(f[4]) | ((uint32_t)f32_to_bf16(f[5]) << 16);
-  r.w = (uint32_t)f32_to_bf16(f[6]) | ((uint32_t)f32_to_bf16(f[7]) << 16);
-  return r;
-}
-__device__ __forceinline__ bf16x8 tr_read(const uint16_t* a0, int ld4) {
-  const v4i16 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a0));
-  const v4i16 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a0 + ld4));
-  union { short s[8]; bf16x8 b; } u;
-  u.s[0] = r0[0]; u.s[1] = r0[1]; u.s[2] = r0[2]; u.s[3] = r0[3];
-  u.s[4] = r1[0]; u.s[5] = r1[1]; u.s[6] = r1[2]; u.s[7] = r1[3];
-  return u.b;
-}
+using prec::BF16;
+using prec::F32;
 
 // WM × WN waves tile the (COUT/16) × (CIN/16) output tiles; WK = 4/(WM·WN) waves split the pixels.
-template <int CIN, int COUT, int PRO, int WM, int WN, int PT>
-__global__ __launch_bounds__(256) void conv1x1_wgrad_kernel(const uint16_t* __restrict__ g,
-                                                            const uint16_t* __restrict__ yv,
+template <class P, int CIN, int COUT, int PRO, int WM, int WN, int PT>
+__global__ __launch_bounds__(256) void conv1x1_wgrad_kernel(const typename P::T* __restrict__ g,
+                                                            const typename P::T* __restrict__ yv,
                                                             const float* __restrict__ alpha,
                                                             const float* __restrict__ beta,
                                                             const float* __restrict__ gamma,
-                                                            const uint16_t* __restrict__ x,
+                                                            const typename P::T* __restrict__ x,
                                                             const float* __restrict__ ps, const float* __restrict__ pt,
                                                             float* __restrict__ garena, int64_t ldw, int64_t woff,
                                                             int M, int pix_per_wg) {
+  using T = typename P::T;
+  using frag_t = typename P::frag_t;
+  constexpr int V = P::VEC;
   constexpr int WK = 4 / (WM * WN);
   constexpr int MTW = COUT / 16 / WM, NTW = CIN / 16 / WN;
-  constexpr int LDD = COUT + 8, LDX = CIN + 8;
-  constexpr int DCH = PT * COUT / 8, XCH = PT * CIN / 8;            // 16-B chunks per stage
+  constexpr int LDD = P::pitch_tr(COUT), LDX = P::pitch_tr(CIN);
+  constexpr int DCH = PT * COUT / V, XCH = PT * CIN / V;            // 16-B chunks per stage
   constexpr int DI = (DCH + 255) / 256, XI = (XCH + 255) / 256;    // per thread
   const int c = blockIdx.y;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int g4 = lane >> 4, q = (lane & 15) >> 2, pq = lane & 3;
+  const int g4 = lane >> 4;
   const int kgrp = wid / (WM * WN), mgrp = (wid % (WM * WN)) / WN, ngrp = wid % WN;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* vv = reinterpret_cast<float*>(smem);                              // α β γ [COUT], s t [CIN]
-  uint16_t* dyL = reinterpret_cast<uint16_t*>(vv + 3 * COUT + 2 * CIN);    // [PT][LDD]
-  uint16_t* xL = dyL + PT * LDD;                                           // [PT][LDX]
+  T* dyL = reinterpret_cast<T*>(vv + 3 * COUT + 2 * CIN);                  // [PT][LDD]
+  T* xL = dyL + PT * LDD;                                                  // [PT][LDX]
 
   for (int i = threadIdx.x; i < COUT; i += 256) {
     vv[i] = alpha[(int64_t)c * COUT + i];
@@ -78,9 +57,9 @@ __global__ __launch_bounds__(256) void conv1x1_wgrad_kernel(const uint16_t* __re
       vv[3 * COUT + CIN + i] = pt[(int64_t)c * CIN + i];
     }
 
-  const uint16_t* gc = g + (int64_t)c * M * COUT;
-  const uint16_t* yc = yv + (int64_t)c * M * COUT;
-  const uint16_t* xc = x + (int64_t)c * M * CIN;
+  const T* gc = g + (int64_t)c * M * COUT;
+  const T* yc = yv + (int64_t)c * M * COUT;
+  const T* xc = x + (int64_t)c * M * CIN;
   const int p_begin = blockIdx.x * pix_per_wg;
   const int p_end = min(M, p_begin + pix_per_wg);
 
@@ -92,9 +71,9 @@ __global__ __launch_bounds__(256) void conv1x1_wgrad_kernel(const uint16_t* __re
       rg[it] = make_uint4(0, 0, 0, 0);
       ry[it] = make_uint4(0, 0, 0, 0);
       if (i < DCH) {
-        const int p = p0 + i / (COUT / 8);
+        const int p = p0 + i / (COUT / V);
         if (p < p_end) {
-          const int64_t off = (int64_t)p * COUT + (i % (COUT / 8)) * 8;
+          const int64_t off = (int64_t)p * COUT + (i % (COUT / V)) * V;
           rg[it] = *reinterpret_cast<const uint4*>(gc + off);
           ry[it] = *reinterpret_cast<const uint4*>(yc + off);
         }
@@ -105,8 +84,8 @@ __global__ __launch_bounds__(256) void conv1x1_wgrad_kernel(const uint16_t* __re
       const int i = threadIdx.x + it * 256;
       rx[it] = make_uint4(0, 0, 0, 0);
       if (i < XCH) {
-        const int p = p0 + i / (CIN / 8);
-        if (p < p_end) rx[it] = *reinterpret_cast<const uint4*>(xc + (int64_t)p * CIN + (i % (CIN / 8)) * 8);
+        const int p = p0 + i / (CIN / V);
+        if (p < p_end) rx[it] = *reinterpret_cast<const uint4*>(xc + (int64_t)p * CIN + (i % (CIN / V)) * V);
       }
     }
   };
@@ -115,31 +94,31 @@ __global__ __launch_bounds__(256) void conv1x1_wgrad_kernel(const uint16_t* __re
     for (int it = 0; it < DI; ++it) {
       const int i = threadIdx.x + it * 256;
       if (i < DCH) {
-        const int pp = i / (COUT / 8), co0 = (i % (COUT / 8)) * 8;
-        float gf[8], yf[8];
-        unpack8(rg[it], gf);
-        unpack8(ry[it], yf);
+        const int pp = i / (COUT / V), co0 = (i % (COUT / V)) * V;
+        float gf[V], yf[V];
+        P::unpack(rg[it], gf);
+        P::unpack(ry[it], yf);
         const bool live = p0 + pp < p_end;
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
+        for (int j = 0; j < V; ++j)
           gf[j] = live ? vv[co0 + j] * gf[j] + vv[COUT + co0 + j] * yf[j] + vv[2 * COUT + co0 + j] : 0.f;
-        *reinterpret_cast<uint4*>(dyL + pp * LDD + co0) = pack8(gf);
+        P::st_chunk(dyL + pp * LDD + co0, P::pack(gf));
       }
     }
 #pragma unroll
     for (int it = 0; it < XI; ++it) {
       const int i = threadIdx.x + it * 256;
       if (i < XCH) {
-        const int pp = i / (CIN / 8), ci0 = (i % (CIN / 8)) * 8;
+        const int pp = i / (CIN / V), ci0 = (i % (CIN / V)) * V;
         uint4 v = rx[it];
         if (PRO && p0 + pp < p_end) {
-          float f[8];
-          unpack8(v, f);
+          float f[V];
+          P::unpack(v, f);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j] * vv[3 * COUT + ci0 + j] + vv[3 * COUT + CIN + ci0 + j], 0.f);
-          v = pack8(f);
+          for (int j = 0; j < V; ++j) f[j] = fmaxf(f[j] * vv[3 * COUT + ci0 + j] + vv[3 * COUT + CIN + ci0 + j], 0.f);
+          v = P::pack(f);
         }
-        *reinterpret_cast<uint4*>(xL + pp * LDX + ci0) = v;
+        P::st_chunk(xL + pp * LDX + ci0, v);
       }
     }
   };
@@ -158,17 +137,15 @@ __global__ __launch_bounds__(256) void conv1x1_wgrad_kernel(const uint16_t* __re
     if (p0 + PT < p_end) load(p0 + PT);
 #pragma unroll
     for (int ks = kgrp; ks < PT / 32; ks += WK) {
-      const int row = ks * 32 + 8 * g4 + q;
-      bf16x8 af[MTW], bfr[NTW];
+      frag_t af[MTW], bfr[NTW];
 #pragma unroll
-      for (int m = 0; m < MTW; ++m) af[m] = tr_read(dyL + row * LDD + (mgrp * MTW + m) * 16 + 4 * pq, 4 * LDD);
+      for (int m = 0; m < MTW; ++m) af[m] = P::frag_tr(dyL, LDD, ks * 32, (mgrp * MTW + m) * 16, lane);
 #pragma unroll
-      for (int n = 0; n < NTW; ++n) bfr[n] = tr_read(xL + row * LDX + (ngrp * NTW + n) * 16 + 4 * pq, 4 * LDX);
+      for (int n = 0; n < NTW; ++n) bfr[n] = P::frag_tr(xL, LDX, ks * 32, (ngrp * NTW + n) * 16, lane);
 #pragma unroll
       for (int m = 0; m < MTW; ++m)
 #pragma unroll
-        for (int n = 0; n < NTW; ++n)
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
+        for (int n = 0; n < NTW; ++n) acc[m][n] = P::mma(af[m], bfr[n], acc[m][n]);
     }
     __syncthreads();
   }
@@ -213,17 +190,21 @@ __global__ __launch_bounds__(256) void conv1x1_wgrad_kernel(const uint16_t* __re
   }
 }
 
-template <int CIN, int COUT, int WM, int WN, int PT>
-static int launch(const uint16_t* g, const uint16_t* yv, const float* al, const float* be, const float* ga,
-                  const uint16_t* x, const float* ps, const float* pt, float* garena, int64_t ldw, int64_t woff, int C,
+template <class P, int CIN, int COUT, int WM, int WN, int PT>
+static int launch(const void* g_, const void* yv_, const float* al, const float* be, const float* ga,
+                  const void* x_, const float* ps, const float* pt, float* garena, int64_t ldw, int64_t woff, int C,
                   int M, int pix_per_wg, hipStream_t stream) {
+  using T = typename P::T;
+  const T* g = (const T*)g_;
+  const T* yv = (const T*)yv_;
+  const T* x = (const T*)x_;
   constexpr int WK = 4 / (WM * WN);
   const size_t vv = (size_t)(3 * COUT + 2 * CIN) * 4;
-  const size_t tiles = (size_t)PT * ((COUT + 8) + (CIN + 8)) * 2;
+  const size_t tiles = (size_t)PT * (P::pitch_tr(COUT) + P::pitch_tr(CIN)) * P::ES;
   const size_t red = (size_t)(WK - 1) * (WM * WN) * (COUT / 16 / WM) * (CIN / 16 / WN) * 256 * 4;
   const size_t smem = vv + (tiles > red ? tiles : red);
   if (smem > 160 * 1024) return -5;
-  auto kern = ps ? conv1x1_wgrad_kernel<CIN, COUT, 1, WM, WN, PT> : conv1x1_wgrad_kernel<CIN, COUT, 0, WM, WN, PT>;
+  auto kern = ps ? conv1x1_wgrad_kernel<P, CIN, COUT, 1, WM, WN, PT> : conv1x1_wgrad_kernel<P, CIN, COUT, 0, WM, WN, PT>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   const int gx = (M + pix_per_wg - 1) / pix_per_wg;
   hipLaunchKernelGGL(kern, dim3(gx, C), dim3(256), smem, stream, g, yv, al, be, ga, x, ps, pt, garena, ldw, woff, M,
@@ -235,14 +216,14 @@ static int launch(const uint16_t* g, const uint16_t* yv, const float* al, const 
 
 // weight gradient of a 1×1 / stride-1 convolution, accumulated (+=) into the OIHW arena
 // (cin must equal the stored weight's input channels). Returns < 0 for unsupported shapes.
-FA_EXPORT int fa_conv1x1_wgrad(const uint16_t* g, const uint16_t* yv, const float* alpha, const float* beta,
-                               const float* gamma, const uint16_t* x, const float* ps, const float* pt, float* garena,
-                               int64_t ldw, int64_t woff, int C, int M, int Cin, int Cout, int pix_per_wg,
-                               hipStream_t stream) {
+template <class P>
+static int conv1x1_wgrad(const void* g, const void* yv, const float* alpha, const float* beta, const float* gamma,
+                         const void* x, const float* ps, const float* pt, float* garena, int64_t ldw, int64_t woff,
+                         int C, int M, int Cin, int Cout, int pix_per_wg, hipStream_t stream) {
 #define C1(CI, CO, WM, WN, PT)                                                                                 \
   if (Cin == CI && Cout == CO)                                                                                 \
-    return c1::launch<CI, CO, WM, WN, PT>(g, yv, alpha, beta, gamma, x, ps, pt, garena, ldw, woff, C, M,       \
-                                          pix_per_wg, stream);
+    return c1::launch<P, CI, CO, WM, WN, PT>(g, yv, alpha, beta, gamma, x, ps, pt, garena, ldw, woff, C, M,    \
+                                             pix_per_wg, stream);
   C1(16, 64, 1, 1, 128)    // 4 tiles: 4 pixel groups
   C1(64, 16, 1, 1, 128)
   C1(16, 16, 1, 1, 128)
@@ -256,6 +237,21 @@ FA_EXPORT int fa_conv1x1_wgrad(const uint16_t* g, const uint16_t* yv, const floa
   C1(64, 128, 2, 1, 128)
 #undef C1
   return -2;
+}
+
+FA_EXPORT int fa_conv1x1_wgrad(const uint16_t* g, const uint16_t* yv, const float* alpha, const float* beta,
+                               const float* gamma, const uint16_t* x, const float* ps, const float* pt, float* garena,
+                               int64_t ldw, int64_t woff, int C, int M, int Cin, int Cout, int pix_per_wg,
+                               hipStream_t stream) {
+  return conv1x1_wgrad<c1::BF16>(g, yv, alpha, beta, gamma, x, ps, pt, garena, ldw, woff, C, M, Cin, Cout, pix_per_wg,
+                                 stream);
+}
+FA_EXPORT int fa_conv1x1_wgrad_f32(const float* g, const float* yv, const float* alpha, const float* beta,
+                                   const float* gamma, const float* x, const float* ps, const float* pt, float* garena,
+                                   int64_t ldw, int64_t woff, int C, int M, int Cin, int Cout, int pix_per_wg,
+                                   hipStream_t stream) {
+  return conv1x1_wgrad<c1::F32>(g, yv, alpha, beta, gamma, x, ps, pt, garena, ldw, woff, C, M, Cin, Cout, pix_per_wg,
+                                stream);
 }
 
 // ============================================================================================
@@ -277,26 +273,24 @@ FA_EXPORT int fa_conv1x1_wgrad(const uint16_t* g, const uint16_t* yv, const floa
 // ModelTrainerCLS (reference: python/fedml/model/cv/resnet.py Bottleneck, ml/trainer/my_model_trainer_classification.py).
 // ============================================================================================
 namespace c1f {
-using c1::bf16x8;
-using c1::pack8;
-using c1::tr_read;
-using c1::unpack8;
+using prec::BF16;
+using prec::F32;
 
-struct Args {
-  const uint16_t* g;      // [C][M][CO]
-  const uint16_t* y;      // [C][M][CO]
+struct Args {             // activations are P::T (bf16 | fp32)
+  const void* g;          // [C][M][CO]
+  const void* y;          // [C][M][CO]
   const float* alpha;     // [C][CO]
   const float* beta;
   const float* gamma;
-  const uint16_t* wb;     // packed backward weights, client c at wb + c·wb_ld: [CI][roundup(CO, 32) + 8]
+  const void* wb;         // packed backward weights, client c at wb + c·wb_ld: [CI][roundup(CO, 32) + 8]
   int64_t wb_ld;
-  const uint16_t* e_x;    // [C][M][CI]
+  const void* e_x;        // [C][M][CI]
   const float* e_s;       // [C][CI] (EPI_MASK)
   const float* e_t;
-  const uint16_t* e_add;  // [C][M][CI] (EPI_BLOCK)
-  const uint16_t* e_y1;
-  const uint16_t* e_y2;   // optional
-  uint16_t* out;          // [C][M][CI]
+  const void* e_add;      // [C][M][CI] (EPI_BLOCK)
+  const void* e_y1;
+  const void* e_y2;       // optional
+  void* out;              // [C][M][CI]
   float* stats;           // [C][CI][NS]
   int NS;
   float* garena;
@@ -309,20 +303,25 @@ enum { EPI_MASK = 2, EPI_BLOCK = 3 };
 
 // NW waves per workgroup: the weight-gradient accumulators (CO·CI fp32 per workgroup) are spread
 // over NW waves, so the 64/256-channel layers use 8 waves to stay off the 256-VGPR cliff.
-template <int CI, int CO, int EPI, int WM, int WN, int PT, int NW>
+// LDS: dyL is read both ways (pixel fragments for dW, row fragments for dx), so it takes the
+// frag_tr pitch and its row fragments are read 8-B aligned (P::frag_a8).
+template <class P, int CI, int CO, int EPI, int WM, int WN, int PT, int NW>
 __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
+  using T = typename P::T;
+  using frag_t = typename P::frag_t;
+  constexpr int V = P::VEC;
   constexpr int NT = 64 * NW;
   constexpr int WK = NW / (WM * WN);
   constexpr int MTW = CO / 16 / WM, NTW = CI / 16 / WN;  // weight-gradient tiles per wave
   constexpr int KP = (CO + 31) / 32 * 32;            // dx GEMM depth (zero-padded to the MFMA K)
-  constexpr int LDD = KP + 8, LDX = CI + 8, LDW = KP + 8;
-  constexpr int DCH = PT * CO / 8, XCH = PT * CI / 8;
+  constexpr int LDD = P::pitch_tr(KP), LDX = P::pitch_tr(CI), LDS_ = P::pitch(CI), LDW = KP + 8;
+  constexpr int DCH = PT * CO / V, XCH = PT * CI / V;
   constexpr int DI = (DCH + NT - 1) / NT, XI = (XCH + NT - 1) / NT;
   constexpr int MT = PT / 16;                       // dx row tiles per stage
   constexpr int MPW = MT >= NW ? MT / NW : 1;       // row tiles per wave
   constexpr int WPM = MT >= NW ? 1 : NW / MT;       // waves sharing a row tile (split columns)
   constexpr int NTX = CI / 16 / WPM;                // dx column tiles per wave
-  constexpr int CGX = CI / 8;                       // 16-B chunks per e_x row
+  constexpr int CGX = CI / V;                       // 16-B chunks per e_x row
   static_assert(WK >= 1 && NW % (WM * WN) == 0, "wave grid");
   static_assert((CI / 16) % WPM == 0 && NTX >= 1, "dx column split");
   static_assert(NT % CGX == 0, "fixed channel chunk per thread");
@@ -331,15 +330,15 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
   constexpr bool BLK = (EPI == EPI_BLOCK);
   const int c = blockIdx.y;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  const int g4 = lane >> 4, q = (lane & 15) >> 2, pq = lane & 3;
+  const int g4 = lane >> 4;
   const int kgrp = wid / (WM * WN), mgrp = (wid % (WM * WN)) / WN, ngrp = wid % WN;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* vv = reinterpret_cast<float*>(smem);                            // α β γ [CO], s t [CI]
-  uint16_t* wL = reinterpret_cast<uint16_t*>(vv + 3 * CO + 2 * CI);      // [CI][LDW]
-  uint16_t* dyL = wL + CI * LDW;                                         // [PT][LDD]
-  uint16_t* xL = dyL + PT * LDD;                                         // [PT][LDX]  act(e_x)
-  uint16_t* sL = xL + PT * LDX;                                          // [PT][LDX]  dx staging
+  T* wL = reinterpret_cast<T*>(vv + 3 * CO + 2 * CI);                    // [CI][LDW]
+  T* sL = wL + CI * LDW;                                                 // [PT][LDS_] dx staging
+  T* dyL = sL + PT * LDS_;                                               // [PT][LDD]
+  T* xL = dyL + PT * LDD;                                                // [PT][LDX]  act(e_x)
 
   for (int i = threadIdx.x; i < CO; i += NT) {
     vv[i] = a.alpha[(int64_t)c * CO + i];
@@ -352,21 +351,26 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
       vv[3 * CO + CI + i] = a.e_t[(int64_t)c * CI + i];
     }
   {
-    const uint4* src = reinterpret_cast<const uint4*>(a.wb + (int64_t)c * a.wb_ld);
+    const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.wb) + (int64_t)c * a.wb_ld);
     uint4* dst = reinterpret_cast<uint4*>(wL);
-    for (int i = threadIdx.x; i < CI * LDW / 8; i += NT) dst[i] = src[i];
+    for (int i = threadIdx.x; i < CI * LDW / V; i += NT) dst[i] = src[i];
   }
   if (KP > CO)  // zero K-padding columns of the dy tile (never rewritten by the stage stores)
     for (int i = threadIdx.x; i < PT * (KP - CO); i += NT) dyL[(i / (KP - CO)) * LDD + CO + i % (KP - CO)] = 0;
 
   const int M = a.M;
-  const uint16_t* gc = a.g + (int64_t)c * M * CO;
-  const uint16_t* yc = a.y + (int64_t)c * M * CO;
+  const T* gc = reinterpret_cast<const T*>(a.g) + (int64_t)c * M * CO;
+  const T* yc = reinterpret_cast<const T*>(a.y) + (int64_t)c * M * CO;
+  const T* e_x = reinterpret_cast<const T*>(a.e_x);
+  const T* e_add = reinterpret_cast<const T*>(a.e_add);
+  const T* e_y1 = reinterpret_cast<const T*>(a.e_y1);
+  const T* e_y2 = reinterpret_cast<const T*>(a.e_y2);
+  T* outp = reinterpret_cast<T*>(a.out);
   const int64_t xbase = (int64_t)c * M * CI;
   const int p_begin = blockIdx.x * a.pix_per_wg;
   const int p_end = min(M, p_begin + a.pix_per_wg);
-  const int ci0 = (threadIdx.x % CGX) * 8;  // this thread's channel chunk in every e_x-shaped pass
-  const bool has_y2 = BLK && a.e_y2 != nullptr;
+  const int ci0 = (threadIdx.x % CGX) * V;  // this thread's channel chunk in every e_x-shaped pass
+  const bool has_y2 = BLK && e_y2 != nullptr;
 
   // registers: next stage (r*) and current stage (e*) — every operand is fetched one stage ahead
   uint4 rg[DI], ry[DI], rx[XI], ra[XI], r1[XI], r2[XI];
@@ -378,9 +382,9 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
       rg[it] = make_uint4(0, 0, 0, 0);
       ry[it] = make_uint4(0, 0, 0, 0);
       if (i < DCH) {
-        const int p = p0 + i / (CO / 8);
+        const int p = p0 + i / (CO / V);
         if (p < p_end) {
-          const int64_t off = (int64_t)p * CO + (i % (CO / 8)) * 8;
+          const int64_t off = (int64_t)p * CO + (i % (CO / V)) * V;
           rg[it] = *reinterpret_cast<const uint4*>(gc + off);
           ry[it] = *reinterpret_cast<const uint4*>(yc + off);
         }
@@ -393,11 +397,11 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
       rx[it] = ra[it] = r1[it] = r2[it] = make_uint4(0, 0, 0, 0);
       if (i < XCH && p < p_end) {
         const int64_t off = xbase + (int64_t)p * CI + ci0;
-        rx[it] = *reinterpret_cast<const uint4*>(a.e_x + off);
+        rx[it] = *reinterpret_cast<const uint4*>(e_x + off);
         if (BLK) {
-          ra[it] = *reinterpret_cast<const uint4*>(a.e_add + off);
-          r1[it] = *reinterpret_cast<const uint4*>(a.e_y1 + off);
-          if (has_y2) r2[it] = *reinterpret_cast<const uint4*>(a.e_y2 + off);
+          ra[it] = *reinterpret_cast<const uint4*>(e_add + off);
+          r1[it] = *reinterpret_cast<const uint4*>(e_y1 + off);
+          if (has_y2) r2[it] = *reinterpret_cast<const uint4*>(e_y2 + off);
         }
       }
     }
@@ -407,15 +411,15 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
     for (int it = 0; it < DI; ++it) {
       const int i = threadIdx.x + it * NT;
       if (i < DCH) {
-        const int pp = i / (CO / 8), co0 = (i % (CO / 8)) * 8;
-        float gf[8], yf[8];
-        unpack8(rg[it], gf);
-        unpack8(ry[it], yf);
+        const int pp = i / (CO / V), co0 = (i % (CO / V)) * V;
+        float gf[V], yf[V];
+        P::unpack(rg[it], gf);
+        P::unpack(ry[it], yf);
         const bool live = p0 + pp < p_end;
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
+        for (int j = 0; j < V; ++j)
           gf[j] = live ? vv[co0 + j] * gf[j] + vv[CO + co0 + j] * yf[j] + vv[2 * CO + co0 + j] : 0.f;
-        *reinterpret_cast<uint4*>(dyL + pp * LDD + co0) = pack8(gf);
+        P::st_chunk(dyL + pp * LDD + co0, P::pack(gf));
       }
     }
 #pragma unroll
@@ -427,13 +431,13 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
         const int pp = i / CGX;
         uint4 v = rx[it];
         if (PRO && p0 + pp < p_end) {
-          float f[8];
-          unpack8(v, f);
+          float f[V];
+          P::unpack(v, f);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j] * vv[3 * CO + ci0 + j] + vv[3 * CO + CI + ci0 + j], 0.f);
-          v = pack8(f);
+          for (int j = 0; j < V; ++j) f[j] = fmaxf(f[j] * vv[3 * CO + ci0 + j] + vv[3 * CO + CI + ci0 + j], 0.f);
+          v = P::pack(f);
         }
-        *reinterpret_cast<uint4*>(xL + pp * LDX + ci0) = v;
+        P::st_chunk(xL + pp * LDX + ci0, v);
       }
     }
   };
@@ -443,9 +447,9 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
   for (int m = 0; m < MTW; ++m)
 #pragma unroll
     for (int n = 0; n < NTW; ++n) acc[m][n] = {0.f, 0.f, 0.f, 0.f};
-  float st0[8], st1[8], st2[8];
+  float st0[V], st1[V], st2[V];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { st0[j] = 0.f; st1[j] = 0.f; st2[j] = 0.f; }
+  for (int j = 0; j < V; ++j) { st0[j] = 0.f; st1[j] = 0.f; st2[j] = 0.f; }
 
   __syncthreads();  // vectors + weights
   if (p_begin < p_end) load(p_begin);
@@ -456,19 +460,17 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
     // ---- weight gradient: acc += dyᵀ · act(x) over this stage's pixels ----
 #pragma unroll
     for (int ks = kgrp; ks < PT / 32; ks += WK) {
-      const int row = ks * 32 + 8 * g4 + q;
-      bf16x8 af[MTW], bfr[NTW];
+      frag_t af[MTW], bfr[NTW];
 #pragma unroll
-      for (int m = 0; m < MTW; ++m) af[m] = tr_read(dyL + row * LDD + (mgrp * MTW + m) * 16 + 4 * pq, 4 * LDD);
+      for (int m = 0; m < MTW; ++m) af[m] = P::frag_tr(dyL, LDD, ks * 32, (mgrp * MTW + m) * 16, lane);
 #pragma unroll
-      for (int n = 0; n < NTW; ++n) bfr[n] = tr_read(xL + row * LDX + (ngrp * NTW + n) * 16 + 4 * pq, 4 * LDX);
+      for (int n = 0; n < NTW; ++n) bfr[n] = P::frag_tr(xL, LDX, ks * 32, (ngrp * NTW + n) * 16, lane);
 #pragma unroll
       for (int m = 0; m < MTW; ++m)
 #pragma unroll
-        for (int n = 0; n < NTW; ++n)
-          acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[m], bfr[n], acc[m][n], 0, 0, 0);
+        for (int n = 0; n < NTW; ++n) acc[m][n] = P::mma(af[m], bfr[n], acc[m][n]);
     }
-    // ---- data gradient: dx = dy · W, staged to LDS as bf16 ----
+    // ---- data gradient: dx = dy · W, staged to LDS in storage precision ----
 #pragma unroll
     for (int mi = 0; mi < MPW; ++mi) {
       const int mt = MT >= NW ? wid + NW * mi : wid / WPM;
@@ -478,18 +480,18 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
       for (int n = 0; n < NTX; ++n) dacc[n] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int k0 = 0; k0 < KP; k0 += 32) {
-        const bf16x8 af = *reinterpret_cast<const bf16x8*>(dyL + (mt * 16 + (lane & 15)) * LDD + k0 + 8 * g4);
+        const frag_t af = P::frag_a8(dyL + (mt * 16 + (lane & 15)) * LDD + k0 + 8 * g4);
 #pragma unroll
         for (int n = 0; n < NTX; ++n) {
-          const bf16x8 bw = *reinterpret_cast<const bf16x8*>(wL + ((n0 + n) * 16 + (lane & 15)) * LDW + k0 + 8 * g4);
-          dacc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bw, dacc[n], 0, 0, 0);
+          const frag_t bw = P::frag(wL + ((n0 + n) * 16 + (lane & 15)) * LDW + k0 + 8 * g4);
+          dacc[n] = P::mma(af, bw, dacc[n]);
         }
       }
 #pragma unroll
       for (int n = 0; n < NTX; ++n)
 #pragma unroll
         for (int i = 0; i < 4; ++i)
-          sL[(mt * 16 + 4 * g4 + i) * LDX + (n0 + n) * 16 + (lane & 15)] = f32_to_bf16(dacc[n][i]);
+          sL[(mt * 16 + 4 * g4 + i) * LDS_ + (n0 + n) * 16 + (lane & 15)] = P::from_f(dacc[n][i]);
     }
     __syncthreads();  // dx staged; dyL / xL free for the next stage
     // ---- epilogue on 16-B chunks (same mapping as the e_x loads) ----
@@ -498,32 +500,32 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
       const int i = threadIdx.x + it * NT;
       const int pp = i / CGX;
       if (i < XCH && p0 + pp < p_end) {
-        float gv[8], xv[8];
-        unpack8(*reinterpret_cast<const uint4*>(sL + pp * LDX + ci0), gv);
-        unpack8(ex_[it], xv);
+        float gv[V], xv[V];
+        P::unpack(*reinterpret_cast<const uint4*>(sL + pp * LDS_ + ci0), gv);
+        P::unpack(ex_[it], xv);
         if (PRO) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j)
+          for (int j = 0; j < V; ++j)
             gv[j] = (xv[j] * vv[3 * CO + ci0 + j] + vv[3 * CO + CI + ci0 + j] > 0.f) ? gv[j] : 0.f;
         } else {
-          float ex[8];
-          unpack8(ea[it], ex);
+          float ex[V];
+          P::unpack(ea[it], ex);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) gv[j] = (xv[j] > 0.f) ? gv[j] + ex[j] : 0.f;
+          for (int j = 0; j < V; ++j) gv[j] = (xv[j] > 0.f) ? gv[j] + ex[j] : 0.f;
         }
-        const uint4 gp = pack8(gv);
-        *reinterpret_cast<uint4*>(a.out + xbase + (int64_t)(p0 + pp) * CI + ci0) = gp;
-        float gr[8];
-        unpack8(gp, gr);
+        const uint4 gp = P::pack(gv);
+        *reinterpret_cast<uint4*>(outp + xbase + (int64_t)(p0 + pp) * CI + ci0) = gp;
+        float gr[V];
+        P::unpack(gp, gr);
         if (PRO) {
 #pragma unroll
-          for (int j = 0; j < 8; ++j) { st0[j] += gr[j]; st1[j] += gr[j] * xv[j]; }
+          for (int j = 0; j < V; ++j) { st0[j] += gr[j]; st1[j] += gr[j] * xv[j]; }
         } else {
-          float y1[8], y2[8];
-          unpack8(e1[it], y1);
-          unpack8(e2[it], y2);
+          float y1[V], y2[V];
+          P::unpack(e1[it], y1);
+          P::unpack(e2[it], y2);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) { st0[j] += gr[j]; st1[j] += gr[j] * y1[j]; st2[j] += gr[j] * y2[j]; }
+          for (int j = 0; j < V; ++j) { st0[j] += gr[j]; st1[j] += gr[j] * y1[j]; st2[j] += gr[j] * y2[j]; }
         }
       }
     }
@@ -533,17 +535,17 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
 #pragma unroll
   for (int o = CGX; o < 64; o <<= 1) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < V; ++j) {
       st0[j] += __shfl_xor(st0[j], o, 64);
       st1[j] += __shfl_xor(st1[j], o, 64);
       if (BLK) st2[j] += __shfl_xor(st2[j], o, 64);
     }
   }
   __syncthreads();  // every wave is past its last epilogue: the tile region is free
-  float* sred = reinterpret_cast<float*>(dyL);  // [NW][CI][3]
+  float* sred = reinterpret_cast<float*>(sL);  // [NW][CI][3]
   if (lane < CGX) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < V; ++j) {
       sred[(wid * CI + ci0 + j) * 3 + 0] = st0[j];
       sred[(wid * CI + ci0 + j) * 3 + 1] = st1[j];
       sred[(wid * CI + ci0 + j) * 3 + 2] = st2[j];
@@ -566,7 +568,7 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
   // ---- weight gradient: reduce pixel groups through LDS, then partials or atomics ----
   if (WK > 1) {
     __syncthreads();
-    float* rbuf = reinterpret_cast<float*>(dyL);
+    float* rbuf = reinterpret_cast<float*>(sL);
     if (kgrp > 0) {
 #pragma unroll
       for (int m = 0; m < MTW; ++m)
@@ -636,21 +638,23 @@ __global__ __launch_bounds__(256) void partial_reduce_kernel(const float* __rest
   }
 }
 
-template <int CI, int CO, int EPI, int WM, int WN, int PT, int NW>
+template <class P, int CI, int CO, int EPI, int WM, int WN, int PT, int NW>
 static int launch(const Args& a, int C, hipStream_t stream) {
   constexpr int WK = NW / (WM * WN);
   constexpr int KP = (CO + 31) / 32 * 32;
   const size_t vv = (size_t)(3 * CO + 2 * CI) * 4;
-  const size_t wl = (size_t)CI * (KP + 8) * 2;
-  const size_t tiles = (size_t)PT * ((KP + 8) + 2 * (CI + 8)) * 2;
+  const size_t wl = (size_t)CI * (KP + 8) * P::ES;
+  const size_t stage = (size_t)PT * P::pitch(CI) * P::ES;
+  const size_t tiles = (size_t)PT * (P::pitch_tr(KP) + P::pitch_tr(CI)) * P::ES;
   const size_t red = (size_t)(WK - 1) * (WM * WN) * (CO / 16 / WM) * (CI / 16 / WN) * 256 * 4;
   const size_t sred = (size_t)NW * CI * 3 * 4;
-  size_t region = tiles > red ? tiles : red;
+  size_t region = stage + tiles;   // the reduction buffers reuse the stage + tile region
+  region = region > red ? region : red;
   region = region > sred ? region : sred;
   const size_t smem = vv + wl + region;
   if (smem > 160 * 1024) return -5;
   if (a.NS < 2 || (EPI == EPI_BLOCK && a.e_y2 && a.NS < 3)) return -4;
-  auto kern = conv1x1_bwd_kernel<CI, CO, EPI, WM, WN, PT, NW>;
+  auto kern = conv1x1_bwd_kernel<P, CI, CO, EPI, WM, WN, PT, NW>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   const int gx = (a.M + a.pix_per_wg - 1) / a.pix_per_wg;
   hipLaunchKernelGGL(kern, dim3(gx, C), dim3(64 * NW), smem, stream, a);
@@ -662,27 +666,19 @@ static int launch(const Args& a, int C, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
-}  // namespace c1f
-
-// fused data + weight gradient of a 1×1 / stride-1 bottleneck convolution (Cin = dx channels,
-// Cout = g channels). epi: 2 = BN-ReLU mask epilogue, 3 = block epilogue. With ``part`` (≥ C·G·
-// (Cout·Cin + 3·Cin) floats, G = ceil(M / pix_per_wg)) the per-workgroup weight-gradient and
-// statistics partials are written out and summed by a second pass instead of fp32 atomics:
-// cheaper at many workgroups (atomic contention on the CO·CI addresses) and deterministic.
-// Returns < 0 for unsupported shapes / arguments.
-FA_EXPORT int fa_conv1x1_bwd_fused(const uint16_t* g, const uint16_t* y, const float* alpha, const float* beta,
-                                   const float* gamma, const uint16_t* wb, int64_t wb_ld, int ldk2, const uint16_t* e_x,
-                                   const float* e_s, const float* e_t, const uint16_t* e_add, const uint16_t* e_y1,
-                                   const uint16_t* e_y2, uint16_t* out, float* stats, int NS, float* garena,
-                                   int64_t ldw, int64_t woff, int C, int M, int Cin, int Cout, int epi, int pix_per_wg,
-                                   float* part, hipStream_t stream) {
+template <class P>
+static int bwd_fused(const void* g, const void* y, const float* alpha, const float* beta, const float* gamma,
+                     const void* wb, int64_t wb_ld, int ldk2, const void* e_x, const float* e_s, const float* e_t,
+                     const void* e_add, const void* e_y1, const void* e_y2, void* out, float* stats, int NS,
+                     float* garena, int64_t ldw, int64_t woff, int C, int M, int Cin, int Cout, int epi,
+                     int pix_per_wg, float* part, hipStream_t stream) {
   if (ldk2 != (Cout + 31) / 32 * 32 + 8 || pix_per_wg <= 0) return -3;
-  if (epi == c1f::EPI_MASK && (!e_s || !e_t)) return -4;
-  if (epi == c1f::EPI_BLOCK && (!e_add || !e_y1)) return -4;
-  c1f::Args a{g, y, alpha, beta, gamma, wb, wb_ld, e_x, e_s, e_t, e_add, e_y1, e_y2, out, stats, NS, garena, ldw,
-              woff, M, pix_per_wg, part};
+  if (epi == EPI_MASK && (!e_s || !e_t)) return -4;
+  if (epi == EPI_BLOCK && (!e_add || !e_y1)) return -4;
+  Args a{g, y, alpha, beta, gamma, wb, wb_ld, e_x, e_s, e_t, e_add, e_y1, e_y2, out, stats, NS, garena, ldw,
+         woff, M, pix_per_wg, part};
 #define C1F(CI, CO, E, WM, WN, PT, NW) \
-  if (Cin == CI && Cout == CO && epi == E) return c1f::launch<CI, CO, E, WM, WN, PT, NW>(a, C, stream);
+  if (Cin == CI && Cout == CO && epi == E) return launch<P, CI, CO, E, WM, WN, PT, NW>(a, C, stream);
   // conv2 of a bottleneck (planes → 4·planes): mask epilogue, BN-ReLU prologue on the wgrad operand
   C1F(16, 64, 2, 2, 1, 64, 4)
   C1F(32, 128, 2, 4, 1, 64, 4)
@@ -696,4 +692,31 @@ FA_EXPORT int fa_conv1x1_bwd_fused(const uint16_t* g, const uint16_t* y, const f
   C1F(128, 64, 3, 2, 4, 32, 8)
 #undef C1F
   return -2;
+}
+
+}  // namespace c1f
+
+// fused data + weight gradient of a 1×1 / stride-1 bottleneck convolution (Cin = dx channels,
+// Cout = g channels). epi: 2 = BN-ReLU mask epilogue, 3 = block epilogue. With ``part`` (≥ C·G·
+// (Cout·Cin + 3·Cin) floats, G = ceil(M / pix_per_wg)) the per-workgroup weight-gradient and
+// statistics partials are written out and summed by a second pass instead of fp32 atomics:
+// cheaper at many workgroups (atomic contention on the CO·CI addresses) and deterministic.
+// Returns < 0 for unsupported shapes / arguments. `_f32`: fp32 activations / packed weights.
+FA_EXPORT int fa_conv1x1_bwd_fused(const uint16_t* g, const uint16_t* y, const float* alpha, const float* beta,
+                                   const float* gamma, const uint16_t* wb, int64_t wb_ld, int ldk2, const uint16_t* e_x,
+                                   const float* e_s, const float* e_t, const uint16_t* e_add, const uint16_t* e_y1,
+                                   const uint16_t* e_y2, uint16_t* out, float* stats, int NS, float* garena,
+                                   int64_t ldw, int64_t woff, int C, int M, int Cin, int Cout, int epi, int pix_per_wg,
+                                   float* part, hipStream_t stream) {
+  return c1f::bwd_fused<c1f::BF16>(g, y, alpha, beta, gamma, wb, wb_ld, ldk2, e_x, e_s, e_t, e_add, e_y1, e_y2, out,
+                                   stats, NS, garena, ldw, woff, C, M, Cin, Cout, epi, pix_per_wg, part, stream);
+}
+FA_EXPORT int fa_conv1x1_bwd_fused_f32(const float* g, const float* y, const float* alpha, const float* beta,
+                                       const float* gamma, const float* wb, int64_t wb_ld, int ldk2, const float* e_x,
+                                       const float* e_s, const float* e_t, const float* e_add, const float* e_y1,
+                                       const float* e_y2, float* out, float* stats, int NS, float* garena,
+                                       int64_t ldw, int64_t woff, int C, int M, int Cin, int Cout, int epi,
+                                       int pix_per_wg, float* part, hipStream_t stream) {
+  return c1f::bwd_fused<c1f::F32>(g, y, alpha, beta, gamma, wb, wb_ld, ldk2, e_x, e_s, e_t, e_add, e_y1, e_y2, out,
+                                  stats, NS, garena, ldw, woff, C, M, Cin, Cout, epi, pix_per_wg, part, stream);
 }

@@ -20,37 +20,16 @@
 //               straight into the client-stacked gradient arena (OIHW positions, stride ldw).
 // MFMA: v_mfma_f32_16x16x32_bf16. Lane l holds A[row l&15][k 8(l>>4)..+7], B[k 8(l>>4)..+7][col l&15];
 // D: col = l&15, row = 4(l>>4) + i.
-#include "common.h"
+#include "prec.h"
 
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
+using prec::BF16;
+using prec::F32;
 
 enum { PRO_NONE = 0, PRO_BNRELU = 1 };
 enum { EPI_FWD = 0, EPI_STORE = 1, EPI_MASK = 2, EPI_BLOCK = 3 };
 
-__device__ __forceinline__ bf16x8 as_bf16x8(uint4 v) {
-  union { uint4 u; bf16x8 b; } c;
-  c.u = v;
-  return c.b;
-}
-__device__ __forceinline__ void unpack8(uint4 v, float* f) {
-  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
-  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
-  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
-  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
-}
-__device__ __forceinline__ uint32_t pack2(float a, float b) {
-  return (uint32_t)f32_to_bf16(a) | ((uint32_t)f32_to_bf16(b) << 16);
-}
-__device__ __forceinline__ uint4 pack8(const float* f) {
-  uint4 r;
-  r.x = pack2(f[0], f[1]); r.y = pack2(f[2], f[3]); r.z = pack2(f[4], f[5]); r.w = pack2(f[6], f[7]);
-  return r;
-}
-__device__ __forceinline__ float rbf(float x) { return bf16_to_f32(f32_to_bf16(x)); }
-
 // =====================================================================================
-// Weight packing: fp32 OIHW (client-stacked arena, stride ldw) → bf16 GEMM layouts.
+// Weight packing: fp32 OIHW (client-stacked arena, stride ldw) → bf16 | fp32 GEMM layouts.
 // One launch packs every conv layer of the model (segment table), both directions.
 // =====================================================================================
 struct PackSeg {
@@ -61,14 +40,16 @@ struct PackSeg {
   int cin_src;       // channels of the stored weight (cin may be padded up to a multiple of 8)
 };
 
+template <class P>
 __global__ __launch_bounds__(256) void pack_weights_kernel(const float* __restrict__ arena, int64_t ldw,
                                                            const PackSeg* __restrict__ segs, int nseg,
-                                                           uint16_t* __restrict__ dst, int64_t dst_ld) {
+                                                           typename P::T* __restrict__ dst, int64_t dst_ld) {
+  using T = typename P::T;
   const int c = blockIdx.y;
   const PackSeg s = segs[blockIdx.z];
   const float* w = arena + (int64_t)c * ldw + s.src_off;
-  uint16_t* df = dst + (int64_t)c * dst_ld + s.dst_f;
-  uint16_t* db = dst + (int64_t)c * dst_ld + s.dst_b;
+  T* df = dst + (int64_t)c * dst_ld + s.dst_f;
+  T* db = dst + (int64_t)c * dst_ld + s.dst_b;
   const int taps = s.kh * s.kw;
   const int nf = s.cout * s.ldk;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < nf; i += gridDim.x * blockDim.x) {
@@ -78,7 +59,7 @@ __global__ __launch_bounds__(256) void pack_weights_kernel(const float* __restri
       const int tap = k / s.cin, ci = k % s.cin;
       if (ci < s.cin_src) v = w[((int64_t)co * s.cin_src + ci) * taps + tap];
     }
-    df[i] = f32_to_bf16(v);
+    df[i] = P::from_f(v);
   }
   if (s.dst_b >= 0) {
     const int nb = s.cin * s.ldk2;
@@ -89,14 +70,20 @@ __global__ __launch_bounds__(256) void pack_weights_kernel(const float* __restri
         const int tap = k / s.cout, co = k % s.cout;
         if (ci < s.cin_src) v = w[((int64_t)co * s.cin_src + ci) * taps + tap];
       }
-      db[i] = f32_to_bf16(v);
+      db[i] = P::from_f(v);
     }
   }
 }
 
 FA_EXPORT int fa_pack_weights(const float* arena, int64_t ldw, const void* segs_dev, int nseg, uint16_t* dst,
                               int64_t dst_ld, int C, hipStream_t stream) {
-  hipLaunchKernelGGL(pack_weights_kernel, dim3(16, C, nseg), dim3(256), 0, stream, arena, ldw,
+  hipLaunchKernelGGL(pack_weights_kernel<BF16>, dim3(16, C, nseg), dim3(256), 0, stream, arena, ldw,
+                     (const PackSeg*)segs_dev, nseg, dst, dst_ld);
+  return (int)hipGetLastError();
+}
+FA_EXPORT int fa_pack_weights_f32(const float* arena, int64_t ldw, const void* segs_dev, int nseg, float* dst,
+                                  int64_t dst_ld, int C, hipStream_t stream) {
+  hipLaunchKernelGGL(pack_weights_kernel<F32>, dim3(16, C, nseg), dim3(256), 0, stream, arena, ldw,
                      (const PackSeg*)segs_dev, nseg, dst, dst_ld);
   return (int)hipGetLastError();
 }
@@ -118,22 +105,22 @@ FA_EXPORT int fa_pack_weights(const float* arena, int64_t ldw, const void* segs_
 enum { AOP_ACT = 0, AOP_DY = 1 };
 enum { MODE_FWD = 0, MODE_BWD = 1 };
 
-struct ConvArgs {
-  const uint16_t* src;   // A source activations / g
-  const uint16_t* src2;  // y for AOP_DY
-  const uint16_t* wpk;   // packed B [C][NOUT][ldk]
+struct ConvArgs {        // activations / packed weights are P::T (bf16 | fp32)
+  const void* src;       // A source activations / g
+  const void* src2;      // y for AOP_DY
+  const void* wpk;       // packed B [C][NOUT][ldk]
   int64_t wpk_ld;        // per-client stride of the packed weights (elements)
   const float* vec0;     // PRO scale  | α
   const float* vec1;     // PRO shift  | β
   const float* vec2;     //            | γ
-  uint16_t* out;         // [C][M][NOUT]
+  void* out;             // [C][M][NOUT]
   // epilogue inputs
-  const uint16_t* e_x;   // EPI_MASK: previous raw activation (mask + Σg·x); EPI_BLOCK: block input (mask)
+  const void* e_x;       // EPI_MASK: previous raw activation (mask + Σg·x); EPI_BLOCK: block input (mask)
   const float* e_s;      // EPI_MASK: previous BN scale
   const float* e_t;      // EPI_MASK: previous BN shift
-  const uint16_t* e_add; // EPI_BLOCK: extra gradient (downsample / identity path)
-  const uint16_t* e_y1;  // EPI_BLOCK: previous block's bn3 input (Σg·y)
-  const uint16_t* e_y2;  // EPI_BLOCK: previous block's downsample-bn input (optional)
+  const void* e_add;     // EPI_BLOCK: extra gradient (downsample / identity path)
+  const void* e_y1;      // EPI_BLOCK: previous block's bn3 input (Σg·y)
+  const void* e_y2;      // EPI_BLOCK: previous block's downsample-bn input (optional)
   float* stats;          // [C][NOUT][NS]
   int NS;
   int Nb, Hs, Ws, KC;    // source geometry (KC = channels of the A source = GEMM K per tap)
@@ -145,8 +132,11 @@ struct ConvArgs {
   int nout_total;        // output channels of the layer; a workgroup computes NOUT of them (blockIdx.z)
 };
 
-template <int NT, int AOP, int PRO, int MODE, int EPI>
+template <class P, int NT, int AOP, int PRO, int MODE, int EPI>
 __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
+  using T = typename P::T;
+  using frag_t = typename P::frag_t;
+  constexpr int V = P::VEC;
   constexpr int NOUT = NT * 16;
   const int c = blockIdx.y;
   const int NO = a.nout_total;
@@ -157,19 +147,20 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
   const int M = a.Nb * a.Ho * a.Wo;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint16_t* wl = reinterpret_cast<uint16_t*>(smem);                       // [NOUT][ldk]
-  float* v0 = reinterpret_cast<float*>(smem + (size_t)NOUT * a.ldk * 2);  // [KC]
+  T* wl = reinterpret_cast<T*>(smem);                                            // [NOUT][ldk]
+  float* v0 = reinterpret_cast<float*>(smem + (size_t)NOUT * a.ldk * P::ES);    // [KC]
   float* v1 = v0 + a.KC;
   float* v2 = v1 + a.KC;
-  float* red = v2 + a.KC;                                                  // [4][NOUT][3]
-  uint16_t* stage = reinterpret_cast<uint16_t*>(red + 4 * NOUT * 3);      // [4][16][NOUT]
-  uint16_t* my_stage = stage + wid * 16 * NOUT;
+  float* red = v2 + a.KC;                                                         // [4][NOUT][3]
+  T* stage = reinterpret_cast<T*>(red + 4 * NOUT * 3);                           // [4][16][NOUT]
+  T* my_stage = stage + wid * 16 * NOUT;
 
   // ---- stage packed weights (16-B copies) and per-channel vectors ----
   {
-    const uint4* src = reinterpret_cast<const uint4*>(a.wpk + (int64_t)c * a.wpk_ld + (int64_t)ch_base * a.ldk);
+    const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.wpk) + (int64_t)c * a.wpk_ld +
+                                                      (int64_t)ch_base * a.ldk);
     uint4* dst = reinterpret_cast<uint4*>(wl);
-    const int n16 = NOUT * a.ldk / 8;
+    const int n16 = NOUT * a.ldk / V;
     for (int i = threadIdx.x; i < n16; i += 256) dst[i] = src[i];
     if (AOP == AOP_DY || PRO == PRO_BNRELU) {
       for (int i = threadIdx.x; i < a.KC; i += 256) {
@@ -183,16 +174,20 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
   __syncthreads();
 
   const int64_t src_client = (int64_t)c * a.Nb * a.Hs * a.Ws * a.KC;
-  const uint16_t* src = a.src + src_client;
-  const uint16_t* src2 = (AOP == AOP_DY) ? a.src2 + src_client : nullptr;
-  uint16_t* out = a.out + (int64_t)c * M * NO;
+  const T* src = reinterpret_cast<const T*>(a.src) + src_client;
+  const T* src2 = (AOP == AOP_DY) ? reinterpret_cast<const T*>(a.src2) + src_client : nullptr;
+  T* out = reinterpret_cast<T*>(a.out) + (int64_t)c * M * NO;
+  const T* e_x = reinterpret_cast<const T*>(a.e_x);
+  const T* e_add = reinterpret_cast<const T*>(a.e_add);
+  const T* e_y1 = reinterpret_cast<const T*>(a.e_y1);
+  const T* e_y2 = reinterpret_cast<const T*>(a.e_y2);
 
-  // epilogue per-lane statistics: lane owns the 8 channels (lane % (NOUT/8))*8 .. +7
-  constexpr int CG = NOUT / 8;                 // 16-B chunks per output row
+  // epilogue per-lane statistics: lane owns the V channels (lane % (NOUT/V))*V .. +V-1
+  constexpr int CG = NOUT / V;                 // 16-B chunks per output row
   constexpr int ROWS_PER_PASS = 64 / CG;       // rows covered by one 64-lane pass (CG ≤ 64)
-  float st0[8], st1[8], st2[8];
+  float st0[V], st1[V], st2[V];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) { st0[j] = 0.f; st1[j] = 0.f; st2[j] = 0.f; }
+  for (int j = 0; j < V; ++j) { st0[j] = 0.f; st1[j] = 0.f; st2[j] = 0.f; }
   const int my_cg = lane % CG;
 
   const int tiles_total = (M + 15) / 16;
@@ -213,7 +208,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
 
     for (int k0 = 0; k0 < a.Kp; k0 += 32) {
       const int k = k0 + 8 * (lane >> 4);
-      uint4 av = make_uint4(0, 0, 0, 0);
+      float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
       if (mvalid && k < K) {
         const int tap = k / a.KC, ci = k % a.KC;
         const int kh = tap / a.KW, kw = tap % a.KW;
@@ -232,97 +227,90 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
         }
         if (ok) {
           const int64_t off = (((int64_t)on * a.Hs + ih) * a.Ws + iw) * a.KC + ci;
-          const uint4 raw = *reinterpret_cast<const uint4*>(src + off);
-          if (AOP == AOP_ACT && PRO == PRO_NONE) {
-            av = raw;
-          } else {
-            float f[8];
-            unpack8(raw, f);
-            if (AOP == AOP_ACT) {
+          P::load8(src + off, f);
+          if (AOP == AOP_ACT && PRO == PRO_BNRELU) {
 #pragma unroll
-              for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j] * v0[ci + j] + v1[ci + j], 0.f);
-            } else {
-              float yv[8];
-              unpack8(*reinterpret_cast<const uint4*>(src2 + off), yv);
+            for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j] * v0[ci + j] + v1[ci + j], 0.f);
+          } else if (AOP == AOP_DY) {
+            float yv[8];
+            P::load8(src2 + off, yv);
 #pragma unroll
-              for (int j = 0; j < 8; ++j) f[j] = v0[ci + j] * f[j] + v1[ci + j] * yv[j] + v2[ci + j];
-            }
-            av = pack8(f);
+            for (int j = 0; j < 8; ++j) f[j] = v0[ci + j] * f[j] + v1[ci + j] * yv[j] + v2[ci + j];
           }
         }
       }
-      const bf16x8 afrag = as_bf16x8(av);
+      const frag_t afrag = P::frag8(f);
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
-        const uint4 bv = *reinterpret_cast<const uint4*>(wl + (nt * 16 + (lane & 15)) * a.ldk + k0 + 8 * (lane >> 4));
-        acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afrag, as_bf16x8(bv), acc[nt], 0, 0, 0);
+        const frag_t bv = P::frag(wl + (nt * 16 + (lane & 15)) * a.ldk + k0 + 8 * (lane >> 4));
+        acc[nt] = P::mma(afrag, bv, acc[nt]);
       }
     }
 
-    // ---- stage the 16 × NOUT tile (bf16) in LDS ----
+    // ---- stage the 16 × NOUT tile (storage precision) in LDS ----
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int row = 4 * (lane >> 4) + i;
-        my_stage[row * NOUT + nt * 16 + (lane & 15)] = f32_to_bf16(acc[nt][i]);
+        my_stage[row * NOUT + nt * 16 + (lane & 15)] = P::from_f(acc[nt][i]);
       }
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): LDS writes visible to this wave
     __builtin_amdgcn_wave_barrier();
 
-    // ---- vectorised epilogue: each lane handles 8 channels of one row per pass ----
+    // ---- vectorised epilogue: each lane handles V channels of one row per pass ----
     const int rows_valid = min(16, M - tile * 16);
 #pragma unroll
     for (int pass = 0; pass < (16 + ROWS_PER_PASS - 1) / ROWS_PER_PASS; ++pass) {
       const int row = pass * ROWS_PER_PASS + lane / CG;
       if (lane / CG < ROWS_PER_PASS && row < rows_valid) {
-        const int ch0 = my_cg * 8;
+        const int ch0 = my_cg * V;
         const uint4 dv = *reinterpret_cast<const uint4*>(my_stage + row * NOUT + ch0);
         const int64_t goff = ((int64_t)(tile * 16 + row)) * NO + ch_base + ch0;
         if (EPI == EPI_FWD || EPI == EPI_STORE) {
           *reinterpret_cast<uint4*>(out + goff) = dv;
           if (EPI == EPI_FWD) {
-            float f[8];
-            unpack8(dv, f);
+            float f[V];
+            P::unpack(dv, f);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) { st0[j] += f[j]; st1[j] += f[j] * f[j]; }
+            for (int j = 0; j < V; ++j) { st0[j] += f[j]; st1[j] += f[j] * f[j]; }
           }
         } else {
           const int64_t eoff = (int64_t)c * M * NO + goff;
-          float g[8], xv[8];
-          unpack8(dv, g);
-          unpack8(*reinterpret_cast<const uint4*>(a.e_x + eoff), xv);
+          float g[V], xv[V];
+          P::unpack(dv, g);
+          P::unpack(*reinterpret_cast<const uint4*>(e_x + eoff), xv);
           if (EPI == EPI_MASK) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
+            for (int j = 0; j < V; ++j) {
               const int ch = ch0 + j;
               const bool on_ = xv[j] * a.e_s[(int64_t)c * NO + ch_base + ch] + a.e_t[(int64_t)c * NO + ch_base + ch] > 0.f;
               g[j] = on_ ? g[j] : 0.f;
             }
           } else {  // EPI_BLOCK: g = (g + extra) · [block_input > 0]
-            float ex[8];
-            unpack8(*reinterpret_cast<const uint4*>(a.e_add + eoff), ex);
+            float ex[V];
+            P::unpack(*reinterpret_cast<const uint4*>(e_add + eoff), ex);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) g[j] = (xv[j] > 0.f) ? g[j] + ex[j] : 0.f;
+            for (int j = 0; j < V; ++j) g[j] = (xv[j] > 0.f) ? g[j] + ex[j] : 0.f;
           }
-          const uint4 gp = pack8(g);
+          const uint4 gp = P::pack(g);
           *reinterpret_cast<uint4*>(out + goff) = gp;
-          float gr[8];
-          unpack8(gp, gr);
+          float gr[V];
+          P::unpack(gp, gr);
           if (EPI == EPI_MASK) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) { st0[j] += gr[j]; st1[j] += gr[j] * xv[j]; }
+            for (int j = 0; j < V; ++j) { st0[j] += gr[j]; st1[j] += gr[j] * xv[j]; }
           } else {
-            float y1[8];
-            unpack8(*reinterpret_cast<const uint4*>(a.e_y1 + eoff), y1);
+            float y1[V];
+            P::unpack(*reinterpret_cast<const uint4*>(e_y1 + eoff), y1);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) { st0[j] += gr[j]; st1[j] += gr[j] * y1[j]; }
-            if (a.e_y2) {
-              float y2[8];
-              unpack8(*reinterpret_cast<const uint4*>(a.e_y2 + eoff), y2);
+            for (int j = 0; j < V; ++j) { st0[j] += gr[j]; st1[j] += gr[j] * y1[j]; }
+            if (e_y2) {
+              float y2[V];
+              P::unpack(*reinterpret_cast<const uint4*>(e_y2 + eoff), y2);
 #pragma unroll
-              for (int j = 0; j < 8; ++j) st2[j] += gr[j] * y2[j];
+              for (int j = 0; j < V; ++j) st2[j] += gr[j] * y2[j];
             }
           }
         }
@@ -336,7 +324,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
 #pragma unroll
     for (int o = CG; o < 64; o <<= 1) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
+      for (int j = 0; j < V; ++j) {
         st0[j] += __shfl_xor(st0[j], o, 64);
         st1[j] += __shfl_xor(st1[j], o, 64);
         if (EPI == EPI_BLOCK) st2[j] += __shfl_xor(st2[j], o, 64);
@@ -344,8 +332,8 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
     }
     if (lane < CG) {
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int ch = lane * 8 + j;
+      for (int j = 0; j < V; ++j) {
+        const int ch = lane * V + j;
         red[(wid * NOUT + ch) * 3 + 0] = st0[j];
         red[(wid * NOUT + ch) * 3 + 1] = st1[j];
         red[(wid * NOUT + ch) * 3 + 2] = st2[j];
@@ -361,19 +349,21 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
   }
 }
 
+template <class P>
 static size_t conv_smem_bytes(int nout, int ldk, int kc) {
-  return (size_t)nout * ldk * 2 + (size_t)3 * kc * 4 + (size_t)4 * nout * 3 * 4 + (size_t)4 * 16 * nout * 2;
+  return (size_t)nout * ldk * P::ES + (size_t)3 * kc * 4 + (size_t)4 * nout * 3 * 4 + (size_t)4 * 16 * nout * P::ES;
 }
 
-template <int NT, int AOP, int PRO, int MODE, int EPI>
+template <class P, int NT, int AOP, int PRO, int MODE, int EPI>
 static int launch_conv(ConvArgs a, int nout, int C, hipStream_t stream) {
   a.nout_total = nout;
   const int M = a.Nb * a.Ho * a.Wo;
   const int tiles = (M + 15) / 16;
   const int per_wg = 4 * a.tiles_per_wave;
   const int gx = (tiles + per_wg - 1) / per_wg;
-  const size_t smem = conv_smem_bytes(NT * 16, a.ldk, a.KC);
-  auto kern = conv_gemm_kernel<NT, AOP, PRO, MODE, EPI>;
+  const size_t smem = conv_smem_bytes<P>(NT * 16, a.ldk, a.KC);
+  if (smem > 160 * 1024) return -5;
+  auto kern = conv_gemm_kernel<P, NT, AOP, PRO, MODE, EPI>;
   if (smem > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   hipLaunchKernelGGL(kern, dim3(gx, C, nout / (NT * 16)), dim3(256), smem, stream, a);
   return (int)hipGetLastError();
@@ -382,31 +372,71 @@ static int launch_conv(ConvArgs a, int nout, int C, hipStream_t stream) {
 // Wide outputs (128/256 channels) are split over blockIdx.z in 64-channel slices: the per-WG weight
 // and epilogue-staging LDS shrinks 2–4× (several workgroups per CU instead of one), at the cost of
 // re-reading the (narrow) A operand once per slice.
-template <int AOP, int PRO, int MODE, int EPI>
+template <class P, int AOP, int PRO, int MODE, int EPI>
 static int dispatch_nt(int nout, const ConvArgs& a, int C, hipStream_t s) {
   switch (nout) {
-    case 16: return launch_conv<1, AOP, PRO, MODE, EPI>(a, nout, C, s);
-    case 32: return launch_conv<2, AOP, PRO, MODE, EPI>(a, nout, C, s);
+    case 16: return launch_conv<P, 1, AOP, PRO, MODE, EPI>(a, nout, C, s);
+    case 32: return launch_conv<P, 2, AOP, PRO, MODE, EPI>(a, nout, C, s);
     case 64:
     case 128:
-    case 256: return launch_conv<4, AOP, PRO, MODE, EPI>(a, nout, C, s);
+    case 256:
+      // 64-channel slices; narrower when the packed-weight slice would not fit the LDS (fp32, K ≥ 576)
+      if (conv_smem_bytes<P>(64, a.ldk, a.KC) <= 160 * 1024) return launch_conv<P, 4, AOP, PRO, MODE, EPI>(a, nout, C, s);
+      if (conv_smem_bytes<P>(32, a.ldk, a.KC) <= 160 * 1024) return launch_conv<P, 2, AOP, PRO, MODE, EPI>(a, nout, C, s);
+      return launch_conv<P, 1, AOP, PRO, MODE, EPI>(a, nout, C, s);
     default: return -2;
   }
 }
 
-// forward: y = conv(pro(x)), stats[c][co][2] += (Σy, Σy²)
-FA_EXPORT int fa_conv_fwd(const uint16_t* x, const uint16_t* wpk, int64_t wpk_ld, const float* pscale,
-                          const float* pshift, uint16_t* y, float* stats, int C, int Nb, int H, int W, int Cin,
-                          int Cout, int KH, int KW, int stride, int pad, int Ho, int Wo, int ldk, int tiles_per_wave,
-                          hipStream_t stream) {
+template <class P>
+static int conv_fwd(const void* x, const void* wpk, int64_t wpk_ld, const float* pscale, const float* pshift, void* y,
+                    float* stats, int C, int Nb, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
+                    int Ho, int Wo, int ldk, int tiles_per_wave, hipStream_t stream) {
   if (Cin % 8 != 0) return -3;
   ConvArgs a = {};
   a.src = x; a.wpk = wpk; a.wpk_ld = wpk_ld; a.vec0 = pscale; a.vec1 = pshift; a.out = y; a.stats = stats; a.NS = 2;
   a.Nb = Nb; a.Hs = H; a.Ws = W; a.KC = Cin; a.Ho = Ho; a.Wo = Wo; a.KH = KH; a.KW = KW; a.stride = stride;
   a.pad = pad; a.ldk = ldk; a.Kp = (KH * KW * Cin + 31) / 32 * 32; a.tiles_per_wave = tiles_per_wave;
   if (pscale)
-    return dispatch_nt<AOP_ACT, PRO_BNRELU, MODE_FWD, EPI_FWD>(Cout, a, C, stream);
-  return dispatch_nt<AOP_ACT, PRO_NONE, MODE_FWD, EPI_FWD>(Cout, a, C, stream);
+    return dispatch_nt<P, AOP_ACT, PRO_BNRELU, MODE_FWD, EPI_FWD>(Cout, a, C, stream);
+  return dispatch_nt<P, AOP_ACT, PRO_NONE, MODE_FWD, EPI_FWD>(Cout, a, C, stream);
+}
+
+template <class P>
+static int conv_bwd_data(const void* g, const void* yv, const float* alpha, const float* beta, const float* gamma,
+                         const void* wpk_b, int64_t wpk_ld, void* dx, int epi, const void* e_x, const float* e_s,
+                         const float* e_t, const void* e_add, const void* e_y1, const void* e_y2, float* stats, int C,
+                         int Nb, int Hy, int Wy, int Cout, int Cin, int KH, int KW, int stride, int pad, int Hx, int Wx,
+                         int ldk2, int tiles_per_wave, hipStream_t stream) {
+  if (Cout % 8 != 0) return -3;
+  ConvArgs a = {};
+  a.src = g; a.src2 = yv; a.wpk = wpk_b; a.wpk_ld = wpk_ld; a.vec0 = alpha; a.vec1 = beta; a.vec2 = gamma;
+  a.out = dx; a.e_x = e_x; a.e_s = e_s; a.e_t = e_t; a.e_add = e_add; a.e_y1 = e_y1; a.e_y2 = e_y2;
+  a.stats = stats; a.NS = 3;  // backward statistics are always laid out [C][Ch][3]
+  a.Nb = Nb; a.Hs = Hy; a.Ws = Wy; a.KC = Cout; a.Ho = Hx; a.Wo = Wx; a.KH = KH; a.KW = KW; a.stride = stride;
+  a.pad = pad; a.ldk = ldk2; a.Kp = (KH * KW * Cout + 31) / 32 * 32; a.tiles_per_wave = tiles_per_wave;
+  switch (epi) {
+    case EPI_STORE: return dispatch_nt<P, AOP_DY, PRO_NONE, MODE_BWD, EPI_STORE>(Cin, a, C, stream);
+    case EPI_MASK: return dispatch_nt<P, AOP_DY, PRO_NONE, MODE_BWD, EPI_MASK>(Cin, a, C, stream);
+    case EPI_BLOCK: return dispatch_nt<P, AOP_DY, PRO_NONE, MODE_BWD, EPI_BLOCK>(Cin, a, C, stream);
+    default: return -4;
+  }
+}
+
+// forward: y = conv(pro(x)), stats[c][co][2] += (Σy, Σy²). `_f32`: fp32 activations / packed weights.
+FA_EXPORT int fa_conv_fwd(const uint16_t* x, const uint16_t* wpk, int64_t wpk_ld, const float* pscale,
+                          const float* pshift, uint16_t* y, float* stats, int C, int Nb, int H, int W, int Cin,
+                          int Cout, int KH, int KW, int stride, int pad, int Ho, int Wo, int ldk, int tiles_per_wave,
+                          hipStream_t stream) {
+  return conv_fwd<BF16>(x, wpk, wpk_ld, pscale, pshift, y, stats, C, Nb, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo,
+                        ldk, tiles_per_wave, stream);
+}
+FA_EXPORT int fa_conv_fwd_f32(const float* x, const float* wpk, int64_t wpk_ld, const float* pscale,
+                              const float* pshift, float* y, float* stats, int C, int Nb, int H, int W, int Cin,
+                              int Cout, int KH, int KW, int stride, int pad, int Ho, int Wo, int ldk,
+                              int tiles_per_wave, hipStream_t stream) {
+  return conv_fwd<F32>(x, wpk, wpk_ld, pscale, pshift, y, stats, C, Nb, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo,
+                       ldk, tiles_per_wave, stream);
 }
 
 // backward-data: dx = convᵀ(α·g + β·y + γ) with epilogue
@@ -419,17 +449,15 @@ FA_EXPORT int fa_conv_bwd_data(const uint16_t* g, const uint16_t* yv, const floa
                                const uint16_t* e_y1, const uint16_t* e_y2, float* stats, int C, int Nb, int Hy,
                                int Wy, int Cout, int Cin, int KH, int KW, int stride, int pad, int Hx, int Wx,
                                int ldk2, int tiles_per_wave, hipStream_t stream) {
-  if (Cout % 8 != 0) return -3;
-  ConvArgs a = {};
-  a.src = g; a.src2 = yv; a.wpk = wpk_b; a.wpk_ld = wpk_ld; a.vec0 = alpha; a.vec1 = beta; a.vec2 = gamma;
-  a.out = dx; a.e_x = e_x; a.e_s = e_s; a.e_t = e_t; a.e_add = e_add; a.e_y1 = e_y1; a.e_y2 = e_y2;
-  a.stats = stats; a.NS = 3;  // backward statistics are always laid out [C][Ch][3]
-  a.Nb = Nb; a.Hs = Hy; a.Ws = Wy; a.KC = Cout; a.Ho = Hx; a.Wo = Wx; a.KH = KH; a.KW = KW; a.stride = stride;
-  a.pad = pad; a.ldk = ldk2; a.Kp = (KH * KW * Cout + 31) / 32 * 32; a.tiles_per_wave = tiles_per_wave;
-  switch (epi) {
-    case EPI_STORE: return dispatch_nt<AOP_DY, PRO_NONE, MODE_BWD, EPI_STORE>(Cin, a, C, stream);
-    case EPI_MASK: return dispatch_nt<AOP_DY, PRO_NONE, MODE_BWD, EPI_MASK>(Cin, a, C, stream);
-    case EPI_BLOCK: return dispatch_nt<AOP_DY, PRO_NONE, MODE_BWD, EPI_BLOCK>(Cin, a, C, stream);
-    default: return -4;
-  }
+  return conv_bwd_data<BF16>(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, dx, epi, e_x, e_s, e_t, e_add, e_y1, e_y2,
+                             stats, C, Nb, Hy, Wy, Cout, Cin, KH, KW, stride, pad, Hx, Wx, ldk2, tiles_per_wave, stream);
+}
+FA_EXPORT int fa_conv_bwd_data_f32(const float* g, const float* yv, const float* alpha, const float* beta,
+                                   const float* gamma, const float* wpk_b, int64_t wpk_ld, float* dx, int epi,
+                                   const float* e_x, const float* e_s, const float* e_t, const float* e_add,
+                                   const float* e_y1, const float* e_y2, float* stats, int C, int Nb, int Hy,
+                                   int Wy, int Cout, int Cin, int KH, int KW, int stride, int pad, int Hx, int Wx,
+                                   int ldk2, int tiles_per_wave, hipStream_t stream) {
+  return conv_bwd_data<F32>(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, dx, epi, e_x, e_s, e_t, e_add, e_y1, e_y2,
+                            stats, C, Nb, Hy, Wy, Cout, Cin, KH, KW, stride, pad, Hx, Wx, ldk2, tiles_per_wave, stream);
 }

@@ -13,44 +13,12 @@
 // A workgroup owns one client and a contiguous pixel chunk; its 4 waves split the Cout×K output
 // tiles and keep them in registers for the whole chunk; the partial dW is added (fp32 atomics)
 // into the client-stacked gradient arena at the OIHW position of each element.
-#include "common.h"
+#include "prec.h"
 
-typedef __bf16 wbf16x8 __attribute__((ext_vector_type(8)));
-typedef short wv4i16 __attribute__((ext_vector_type(4)));
-typedef __attribute__((address_space(3))) wv4i16 lds_v4i16;
+#include <type_traits>
 
-__device__ __forceinline__ void wg_unpack8(uint4 v, float* f) {
-  f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
-  f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
-  f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
-  f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
-}
-__device__ __forceinline__ uint4 wg_pack8(const float* f) {
-  uint4 r;
-  r.x = (uint32_t)f32_to_bf16(f[0]) | ((uint32_t)f32_to_bf16(f[1]) << 16);
-  r.y = (uint32_t)f32_to_bf16(f[2]) | ((uint32_t)f32_to_bf16(f[3]) << 16);
-  r.z = (uint32_t)f32_to_bf16(f[4]) | ((uint32_t)f32_to_bf16(f[5]) << 16);
-  r.w = (uint32_t)f32_to_bf16(f[6]) | ((uint32_t)f32_to_bf16(f[7]) << 16);
-  return r;
-}
-
-// fragment of 8 consecutive rows (pixels) of column block [col0, col0+16) from a natural
-// [rows][ld] bf16 LDS tile, rows row0..row0+31 (lane group g takes rows row0+8g..+7)
-__device__ __forceinline__ wbf16x8 tr_frag(const uint16_t* tile, int ld, int row0, int col0, int lane) {
-  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  const uint16_t* a0 = tile + (row0 + 8 * g + q) * ld + col0 + 4 * p;
-  const uint16_t* a1 = a0 + 4 * ld;
-  const wv4i16 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a0));
-  const wv4i16 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a1));
-  union {
-    short s[8];
-    wbf16x8 b;
-  } u;
-  u.s[0] = r0[0]; u.s[1] = r0[1]; u.s[2] = r0[2]; u.s[3] = r0[3];
-  u.s[4] = r1[0]; u.s[5] = r1[1]; u.s[6] = r1[2]; u.s[7] = r1[3];
-  return u.b;
-}
-
+using prec::BF16;
+using prec::F32;
 
 // One workgroup = (client c, pixel chunk, K-slice z). The K-slice keeps the per-wave output
 // tile count ≤ 16 (≤ 64 accumulator registers) and means each workgroup only stages the im2col
@@ -58,13 +26,17 @@ __device__ __forceinline__ wbf16x8 tr_frag(const uint16_t* tile, int ld, int row
 // MFMAs of sub-tile i run. Partial dW goes to a GEMM-layout fp32 scratch [C][Cout][K] with
 // row-contiguous atomics (16 consecutive k per lane group), then one scatter pass adds it into
 // the OIHW gradient arena.
-template <int TPW, int PRO, int DYI, int AI>
+template <class P, int TPW, int DYI, int AI>
 __global__ __launch_bounds__(256) void conv_wgrad_tr_kernel(
-    const uint16_t* __restrict__ g, const uint16_t* __restrict__ yv, const float* __restrict__ alpha,
-    const float* __restrict__ beta, const float* __restrict__ gamma, const uint16_t* __restrict__ x,
+    const typename P::T* __restrict__ g, const typename P::T* __restrict__ yv, const float* __restrict__ alpha,
+    const float* __restrict__ beta, const float* __restrict__ gamma, const typename P::T* __restrict__ x,
     const float* __restrict__ ps, const float* __restrict__ pt, float* __restrict__ dw, int Nb, int H, int W,
     int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int pix_per_wg, int nt_per_z) {
-  constexpr int PT = 64;
+  using T = typename P::T;
+  const bool PRO = ps != nullptr;   // runtime flag: halves the instantiations (uniform branch)
+  using frag_t = typename P::frag_t;
+  constexpr int V = P::VEC;
+  constexpr int PT = P::kF32 ? 32 : 64;   // pixels per staged sub-tile (fp32: half → same register budget)
   const int c = blockIdx.y;
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
@@ -76,12 +48,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_tr_kernel(
   const int k_hi = min(K, nt_hi * 16);
   const int kw_ = (nt_hi - nt_lo) * 16;     // staged columns (zero beyond K)
   const int M = Nb * Ho * Wo;
-  const int ldd = Cout + 8;
-  const int lda = kw_ + 8;
+  const int ldd = P::pitch_tr(Cout);
+  const int lda = P::pitch_tr(kw_);
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  uint16_t* dyL = reinterpret_cast<uint16_t*>(smem);   // [PT][ldd]
-  uint16_t* aL = dyL + PT * ldd;                        // [PT][lda]
+  T* dyL = reinterpret_cast<T*>(smem);                  // [PT][ldd]
+  T* aL = dyL + PT * ldd;                               // [PT][lda]
   float* vv = reinterpret_cast<float*>(aL + PT * lda);  // α β γ [Cout], s t [Cin]
 
   for (int i = threadIdx.x; i < Cout; i += 256) {
@@ -103,12 +75,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_tr_kernel(
 #pragma unroll
   for (int t = 0; t < TPW; ++t) acc[t] = {0.f, 0.f, 0.f, 0.f};
 
-  const uint16_t* gc = g + (int64_t)c * M * Cout;
-  const uint16_t* yc = yv + (int64_t)c * M * Cout;
-  const uint16_t* xc = x + (int64_t)c * Nb * H * W * Cin;
+  const T* gc = g + (int64_t)c * M * Cout;
+  const T* yc = yv + (int64_t)c * M * Cout;
+  const T* xc = x + (int64_t)c * Nb * H * W * Cin;
   const int p_begin = blockIdx.x * pix_per_wg;
   const int p_end = min(M, p_begin + pix_per_wg);
-  const int cg = Cout / 8, kg = (k_hi - k_lo) / 8;
+  const int cg = Cout / V, kg = (k_hi - k_lo) / V;
   const int n_dy = PT * cg, n_a = PT * kg;
   __syncthreads();
 
@@ -123,7 +95,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_tr_kernel(
       rg[it] = make_uint4(0, 0, 0, 0);
       ry[it] = make_uint4(0, 0, 0, 0);
       if (i < n_dy) {
-        const int p = p0 + i / cg, co0 = (i % cg) * 8;
+        const int p = p0 + i / cg, co0 = (i % cg) * V;
         if (p < p_end) {
           rg[it] = *reinterpret_cast<const uint4*>(gc + (int64_t)p * Cout + co0);
           ry[it] = *reinterpret_cast<const uint4*>(yc + (int64_t)p * Cout + co0);
@@ -136,7 +108,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_tr_kernel(
       const int i = threadIdx.x + it * 256;
       rx[it] = make_uint4(0, 0, 0, 0);
       if (i < n_a) {
-        const int p = p0 + i / kg, k0 = k_lo + (i % kg) * 8;
+        const int p = p0 + i / kg, k0 = k_lo + (i % kg) * V;
         if (p < p_end) {
           const int tap = k0 / Cin, ci0 = k0 % Cin;
           const int n = p / (Ho * Wo), r = p % (Ho * Wo);
@@ -155,34 +127,34 @@ __global__ __launch_bounds__(256) void conv_wgrad_tr_kernel(
     for (int it = 0; it < DYI; ++it) {
       const int i = threadIdx.x + it * 256;
       if (i < n_dy) {
-        const int pp = i / cg, co0 = (i % cg) * 8;
-        float gf[8], yf[8], d[8];
-        wg_unpack8(rg[it], gf);
-        wg_unpack8(ry[it], yf);
+        const int pp = i / cg, co0 = (i % cg) * V;
+        float gf[V], yf[V], d[V];
+        P::unpack(rg[it], gf);
+        P::unpack(ry[it], yf);
         const bool live = (dvalid >> it) & 1u;
 #pragma unroll
-        for (int j = 0; j < 8; ++j)
+        for (int j = 0; j < V; ++j)
           d[j] = live ? vv[co0 + j] * gf[j] + vv[Cout + co0 + j] * yf[j] + vv[2 * Cout + co0 + j] : 0.f;
-        *reinterpret_cast<uint4*>(dyL + pp * ldd + co0) = wg_pack8(d);
+        P::st_chunk(dyL + pp * ldd + co0, P::pack(d));
       }
     }
 #pragma unroll
     for (int it = 0; it < AI; ++it) {
       const int i = threadIdx.x + it * 256;
       if (i < n_a) {
-        const int pp = i / kg, kk = (i % kg) * 8;
+        const int pp = i / kg, kk = (i % kg) * V;
         uint4 v = rx[it];
         if (!((avalid >> it) & 1u)) {
           v = make_uint4(0, 0, 0, 0);   // zero padding / out-of-range pixel (not relu(shift))
         } else if (PRO) {
           const int ci0 = (k_lo + kk) % Cin;
-          float f[8];
-          wg_unpack8(v, f);
+          float f[V];
+          P::unpack(v, f);
 #pragma unroll
-          for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j] * vv[3 * Cout + ci0 + j] + vv[3 * Cout + Cin + ci0 + j], 0.f);
-          v = wg_pack8(f);
+          for (int j = 0; j < V; ++j) f[j] = fmaxf(f[j] * vv[3 * Cout + ci0 + j] + vv[3 * Cout + Cin + ci0 + j], 0.f);
+          v = P::pack(f);
         }
-        *reinterpret_cast<uint4*>(aL + pp * lda + kk) = v;
+        P::st_chunk(aL + pp * lda + kk, v);
       }
     }
   };
@@ -199,9 +171,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_tr_kernel(
         const int mt = tile / NTZ, nt = tile % NTZ;
 #pragma unroll
         for (int ks = 0; ks < PT / 32; ++ks) {
-          const wbf16x8 af = tr_frag(dyL, ldd, ks * 32, mt * 16, lane);
-          const wbf16x8 bf = tr_frag(aL, lda, ks * 32, nt * 16, lane);
-          acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf, acc[t], 0, 0, 0);
+          const frag_t af = P::frag_tr(dyL, ldd, ks * 32, mt * 16, lane);
+          const frag_t bf = P::frag_tr(aL, lda, ks * 32, nt * 16, lane);
+          acc[t] = P::mma(af, bf, acc[t]);
         }
       }
     }
@@ -243,11 +215,14 @@ __global__ __launch_bounds__(256) void wgrad_scatter_kernel(float* __restrict__ 
 }
 
 // `dw` scratch: C × Cout × K fp32, zero on entry (left zeroed on exit by the scatter pass)
-FA_EXPORT int fa_conv_wgrad(const uint16_t* g, const uint16_t* yv, const float* alpha, const float* beta,
-                            const float* gamma, const uint16_t* x, const float* ps, const float* pt, float* garena,
-                            int64_t ldw, int64_t woff, int C, int Nb, int H, int W, int Cin, int Ho, int Wo, int Cout,
-                            int KH, int KW, int stride, int pad, int pix_per_wg, int cin_src, float* dw,
-                            hipStream_t stream) {
+template <class P>
+static int conv_wgrad(const typename P::T* g, const typename P::T* yv, const float* alpha, const float* beta,
+                      const float* gamma, const typename P::T* x, const float* ps, const float* pt, float* garena,
+                      int64_t ldw, int64_t woff, int C, int Nb, int H, int W, int Cin, int Ho, int Wo, int Cout,
+                      int KH, int KW, int stride, int pad, int pix_per_wg, int cin_src, float* dw,
+                      hipStream_t stream) {
+  constexpr int V = P::VEC;
+  constexpr int PT = P::kF32 ? 32 : 64;
   if (Cin % 8 != 0 || Cout % 16 != 0 || Cout > 256) return -3;
   const int K = KH * KW * Cin;
   const int NT2 = (K + 15) / 16;
@@ -258,38 +233,54 @@ FA_EXPORT int fa_conv_wgrad(const uint16_t* g, const uint16_t* yv, const float* 
   const int M = Nb * Ho * Wo;
   const int gx = (M + pix_per_wg - 1) / pix_per_wg;
   const int kw_ = nt_per_z * 16;
-  const int dyi = (64 * (Cout / 8) + 255) / 256;
-  const int ai = (64 * (kw_ / 8) + 255) / 256;
+  const int dyi = (PT * (Cout / V) + 255) / 256;
+  const int ai = (PT * (kw_ / V) + 255) / 256;
   // the staging loops cover DYI·256 / AI·256 16-B chunks: a sub-tile larger than the largest
   // instantiation would leave LDS rows unwritten
   if (dyi > 8 || ai > 16) return -6;
-  const size_t smem = (size_t)64 * ((Cout + 8) + (kw_ + 8)) * 2 + (size_t)(3 * Cout + 2 * Cin) * 4;
+  const size_t smem = (size_t)PT * (P::pitch_tr(Cout) + P::pitch_tr(kw_)) * P::ES + (size_t)(3 * Cout + 2 * Cin) * 4;
+  if (smem > 160 * 1024) return -5;
   dim3 grid(gx, C, nz);
-#define WG_LAUNCH(T, D, A)                                                                                       \
-  {                                                                                                              \
-    auto kern = ps ? conv_wgrad_tr_kernel<T, 1, D, A> : conv_wgrad_tr_kernel<T, 0, D, A>;                        \
-    if (smem > 64 * 1024)                                                                                        \
-      hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);             \
-    hipLaunchKernelGGL(kern, grid, dim3(256), smem, stream, g, yv, alpha, beta, gamma, x, ps, pt, dw, Nb, H, W,   \
-                       Cin, Ho, Wo, Cout, KH, KW, stride, pad, pix_per_wg, nt_per_z);                            \
-  }
-#define WG_AI(T, D)                          \
-  if (ai <= 2) WG_LAUNCH(T, D, 2)            \
-  else if (ai <= 4) WG_LAUNCH(T, D, 4)       \
-  else if (ai <= 8) WG_LAUNCH(T, D, 8)       \
-  else WG_LAUNCH(T, D, 16)
-#define WG_D(T)                              \
-  if (dyi <= 2) { WG_AI(T, 2) }              \
-  else { WG_AI(T, 8) }
-  if (tpw <= 4) { WG_D(4) }
-  else if (tpw <= 8) { WG_D(8) }
-  else { WG_D(16) }
-#undef WG_D
-#undef WG_AI
-#undef WG_LAUNCH
+  auto go = [&](auto kern) {
+    if (smem > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    hipLaunchKernelGGL(kern, grid, dim3(256), smem, stream, g, yv, alpha, beta, gamma, x, ps, pt, dw, Nb, H, W, Cin,
+                       Ho, Wo, Cout, KH, KW, stride, pad, pix_per_wg, nt_per_z);
+  };
+  // instantiated register budgets: dy chunks/thread D ∈ {2, 8}, A chunks/thread ∈ {2, 4, 8, 16}
+  auto by_a = [&](auto tpw_c, auto d_c) {
+    constexpr int T_ = decltype(tpw_c)::value, D_ = decltype(d_c)::value;
+    if (ai <= 2) go(conv_wgrad_tr_kernel<P, T_, D_, 2>);
+    else if (ai <= 4) go(conv_wgrad_tr_kernel<P, T_, D_, 4>);
+    else if (ai <= 8) go(conv_wgrad_tr_kernel<P, T_, D_, 8>);
+    else go(conv_wgrad_tr_kernel<P, T_, D_, 16>);
+  };
+  auto by_d = [&](auto tpw_c) {
+    if (dyi <= 2) by_a(tpw_c, std::integral_constant<int, 2>{});
+    else by_a(tpw_c, std::integral_constant<int, 8>{});
+  };
+  if (tpw <= 4) by_d(std::integral_constant<int, 4>{});
+  else if (tpw <= 8) by_d(std::integral_constant<int, 8>{});
+  else by_d(std::integral_constant<int, 16>{});
   hipLaunchKernelGGL(wgrad_scatter_kernel, dim3(fa_grid((int64_t)Cout * K, 256, 64), C), dim3(256), 0, stream, dw,
                      garena, ldw, woff, Cout, Cin, KH * KW, cin_src);
   return (int)hipGetLastError();
+}
+
+FA_EXPORT int fa_conv_wgrad(const uint16_t* g, const uint16_t* yv, const float* alpha, const float* beta,
+                            const float* gamma, const uint16_t* x, const float* ps, const float* pt, float* garena,
+                            int64_t ldw, int64_t woff, int C, int Nb, int H, int W, int Cin, int Ho, int Wo, int Cout,
+                            int KH, int KW, int stride, int pad, int pix_per_wg, int cin_src, float* dw,
+                            hipStream_t stream) {
+  return conv_wgrad<BF16>(g, yv, alpha, beta, gamma, x, ps, pt, garena, ldw, woff, C, Nb, H, W, Cin, Ho, Wo, Cout, KH,
+                          KW, stride, pad, pix_per_wg, cin_src, dw, stream);
+}
+FA_EXPORT int fa_conv_wgrad_f32(const float* g, const float* yv, const float* alpha, const float* beta,
+                                const float* gamma, const float* x, const float* ps, const float* pt, float* garena,
+                                int64_t ldw, int64_t woff, int C, int Nb, int H, int W, int Cin, int Ho, int Wo,
+                                int Cout, int KH, int KW, int stride, int pad, int pix_per_wg, int cin_src, float* dw,
+                                hipStream_t stream) {
+  return conv_wgrad<F32>(g, yv, alpha, beta, gamma, x, ps, pt, garena, ldw, woff, C, Nb, H, W, Cin, Ho, Wo, Cout, KH,
+                         KW, stride, pad, pix_per_wg, cin_src, dw, stream);
 }
 
 // scatter a GEMM-layout dW scratch [C][Cout][taps·Cin] into the OIHW arena (+=) and clear it

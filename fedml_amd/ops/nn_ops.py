@@ -2,6 +2,10 @@
 
 All tensors are CUDA(HIP) tensors; layouts are documented in the .hip files. These are thin
 launchers — the model-level orchestration lives in ``parallel.native_resnet``.
+
+Every conv / block launcher exists for two storage precisions (``csrc/prec.h``): bf16 activations
+(``fa_*``) and fp32 activations with exact fp32 MFMA products (``fa_*_f32``). The entry point is
+chosen from the dtype of the activation tensor, so one orchestration drives both.
 """
 import ctypes
 
@@ -17,6 +21,15 @@ def _i(v):
     return _c.c_int(int(v))
 
 
+def _fnp(name, t):
+    """Kernel entry point for the storage precision of activation tensor ``t``."""
+    if t.dtype == torch.float32:
+        return _fn(name + "_f32")
+    if t.dtype != torch.bfloat16:
+        raise TypeError(f"{name}: activations must be bf16 or fp32, got {t.dtype}")
+    return _fn(name)
+
+
 class PackSeg(ctypes.Structure):
     _fields_ = [("src_off", ctypes.c_int64), ("dst_f", ctypes.c_int64), ("dst_b", ctypes.c_int64),
                 ("cout", ctypes.c_int), ("cin", ctypes.c_int), ("kh", ctypes.c_int), ("kw", ctypes.c_int),
@@ -24,14 +37,14 @@ class PackSeg(ctypes.Structure):
 
 
 def pack_weights(arena, segs_dev, nseg, dst, dst_ld, C):
-    rc = _fn("fa_pack_weights")(_p(arena), _i64(arena.stride(0)), _p(segs_dev), _i(nseg), _p(dst), _i64(dst_ld),
+    rc = _fnp("fa_pack_weights", dst)(_p(arena), _i64(arena.stride(0)), _p(segs_dev), _i(nseg), _p(dst), _i64(dst_ld),
                                 _i(C), _stream(arena))
     _check(rc, "fa_pack_weights")
 
 
 def conv_fwd(x, wpk, wpk_ld, pscale, pshift, y, stats, C, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, ldk,
              tiles_per_wave):
-    rc = _fn("fa_conv_fwd")(_p(x), _p(wpk), _i64(wpk_ld), _p(pscale), _p(pshift), _p(y), _p(stats), _i(C), _i(N),
+    rc = _fnp("fa_conv_fwd", x)(_p(x), _p(wpk), _i64(wpk_ld), _p(pscale), _p(pshift), _p(y), _p(stats), _i(C), _i(N),
                             _i(H), _i(W), _i(Cin), _i(Cout), _i(KH), _i(KW), _i(stride), _i(pad), _i(Ho), _i(Wo),
                             _i(ldk), _i(tiles_per_wave), _stream(x))
     _check(rc, "fa_conv_fwd")
@@ -42,7 +55,7 @@ EPI_STORE, EPI_MASK, EPI_BLOCK = 1, 2, 3
 
 def conv_bwd_data(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, dx, epi, e_x, e_s, e_t, e_add, e_y1, e_y2, stats, C, N,
                   Hy, Wy, Cout, Cin, KH, KW, stride, pad, Hx, Wx, ldk2, tiles_per_wave):
-    rc = _fn("fa_conv_bwd_data")(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(wpk_b), _i64(wpk_ld), _p(dx),
+    rc = _fnp("fa_conv_bwd_data", g)(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(wpk_b), _i64(wpk_ld), _p(dx),
                                  _i(epi), _p(e_x), _p(e_s), _p(e_t), _p(e_add), _p(e_y1), _p(e_y2), _p(stats), _i(C),
                                  _i(N), _i(Hy), _i(Wy), _i(Cout), _i(Cin), _i(KH), _i(KW), _i(stride), _i(pad),
                                  _i(Hx), _i(Wx), _i(ldk2), _i(tiles_per_wave), _stream(g))
@@ -52,7 +65,7 @@ def conv_bwd_data(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, dx, epi, e_x, e_s, e
 def conv_wgrad(g, yv, alpha, beta, gamma, x, ps, pt, garena, woff, C, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
                pad, pix_per_wg, cin_src, dw_scratch):
     """``dw_scratch``: ≥ C·Cout·KH·KW·Cin fp32, zero on entry; the kernel leaves it zeroed."""
-    rc = _fn("fa_conv_wgrad")(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(x), _p(ps), _p(pt), _p(garena),
+    rc = _fnp("fa_conv_wgrad", g)(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(x), _p(ps), _p(pt), _p(garena),
                               _i64(garena.stride(0)), _i64(woff), _i(C), _i(N), _i(H), _i(W), _i(Cin), _i(Ho), _i(Wo),
                               _i(Cout), _i(KH), _i(KW), _i(stride), _i(pad), _i(pix_per_wg), _i(cin_src),
                               _p(dw_scratch), _stream(g))
@@ -71,7 +84,7 @@ def conv3x3_supported(cin, cout, k, stride, pad, H, W):
 
 
 def conv3x3_fwd(x, wpk, wpk_ld, pscale, pshift, y, stats, C, N, H, W, Cin, Cout, ldk, stride=1):
-    rc = _fn("fa_conv3x3_fwd")(_p(x), _p(wpk), _i64(wpk_ld), _p(pscale), _p(pshift), _p(y), _p(stats), _i(C), _i(N),
+    rc = _fnp("fa_conv3x3_fwd", x)(_p(x), _p(wpk), _i64(wpk_ld), _p(pscale), _p(pshift), _p(y), _p(stats), _i(C), _i(N),
                                _i(H), _i(W), _i(Cin), _i(Cout), _i(ldk), _i(stride), _stream(x))
     _check(rc, "fa_conv3x3_fwd")
 
@@ -79,7 +92,7 @@ def conv3x3_fwd(x, wpk, wpk_ld, pscale, pshift, y, stats, C, N, H, W, Cin, Cout,
 def conv3x3_bwd_data(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, dx, e_x, e_s, e_t, stats, C, N, H, W, Cout, Cin,
                      ldk2, stride=1):
     """(H, W) = dx (input) resolution."""
-    rc = _fn("fa_conv3x3_bwd_data")(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(wpk_b), _i64(wpk_ld), _p(dx),
+    rc = _fnp("fa_conv3x3_bwd_data", g)(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(wpk_b), _i64(wpk_ld), _p(dx),
                                     _p(e_x), _p(e_s), _p(e_t), _p(stats), _i(C), _i(N), _i(H), _i(W), _i(Cout), _i(Cin),
                                     _i(ldk2), _i(stride), _stream(g))
     _check(rc, "fa_conv3x3_bwd_data")
@@ -90,7 +103,7 @@ def conv3x3_wgrad(g, yv, alpha, beta, gamma, x, ps, pt, garena, woff, C, N, H, W
     """Weight gradient into the GEMM-layout scratch, then scattered (+=) into the OIHW arena
     (``scatter=False``: left in the scratch for :func:`wgrad_scatter_multi`). (H, W) = input (x)
     resolution."""
-    rc = _fn("fa_conv3x3_wgrad")(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(x), _p(ps), _p(pt),
+    rc = _fnp("fa_conv3x3_wgrad", g)(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(x), _p(ps), _p(pt),
                                  _p(dw_scratch), _i(C), _i(N), _i(H), _i(W), _i(Cin), _i(Cout), _i(stride), _stream(g))
     _check(rc, "fa_conv3x3_wgrad")
     if not scatter:
@@ -124,7 +137,7 @@ def conv1x1_wgrad_supported(cin, cout, k, stride, pad):
 
 def conv1x1_wgrad(g, yv, alpha, beta, gamma, x, ps, pt, garena, woff, C, M, Cin, Cout, pix_per_wg):
     """dW += Σ_p dyᵀ·act(x) straight into the OIHW arena rows (stride garena.stride(0))."""
-    rc = _fn("fa_conv1x1_wgrad")(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(x), _p(ps), _p(pt), _p(garena),
+    rc = _fnp("fa_conv1x1_wgrad", g)(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(x), _p(ps), _p(pt), _p(garena),
                                  _i64(garena.stride(0)), _i64(woff), _i(C), _i(M), _i(Cin), _i(Cout), _i(pix_per_wg),
                                  _stream(g))
     _check(rc, "fa_conv1x1_wgrad")
@@ -152,7 +165,7 @@ def conv1x1_bwd_fused(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, ldk2, e_x, e_s, 
     :func:`conv1x1_bwd_fused_scratch` elements → deterministic two-pass reduction, no atomics."""
     if part is not None and part.numel() < conv1x1_bwd_fused_scratch(C, M, Cin, Cout, pix_per_wg):
         raise ValueError("conv1x1_bwd_fused: partial-sum scratch too small")
-    rc = _fn("fa_conv1x1_bwd_fused")(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(wpk_b), _i64(wpk_ld),
+    rc = _fnp("fa_conv1x1_bwd_fused", g)(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(wpk_b), _i64(wpk_ld),
                                      _i(ldk2), _p(e_x), _p(e_s), _p(e_t), _p(e_add), _p(e_y1), _p(e_y2), _p(out),
                                      _p(stats), _i(stats.shape[-1]), _p(garena), _i64(garena.stride(0)), _i64(woff),
                                      _i(C), _i(M), _i(Cin), _i(Cout), _i(epi), _i(pix_per_wg), _p(part),
@@ -178,24 +191,24 @@ def bn_bwd_finalize(bstats, NS, q_gy, C, Ch, n, mean, rstd, arena, garena, off_g
 
 
 def block_out(y, s, t, r, rs, rt, out, C, per_client, Ch):
-    rc = _fn("fa_block_out")(_p(y), _p(s), _p(t), _p(r), _p(rs), _p(rt), _p(out), _i(C), _i64(per_client), _i(Ch),
+    rc = _fnp("fa_block_out", y)(_p(y), _p(s), _p(t), _p(r), _p(rs), _p(rt), _p(out), _i(C), _i64(per_client), _i(Ch),
                              _stream(y))
     _check(rc, "fa_block_out")
 
 
 def avgpool(x, pooled, CN, HW, Ch):
-    rc = _fn("fa_avgpool")(_p(x), _p(pooled), _i(CN), _i(HW), _i(Ch), _stream(x))
+    rc = _fnp("fa_avgpool", x)(_p(x), _p(pooled), _i(CN), _i(HW), _i(Ch), _stream(x))
     _check(rc, "fa_avgpool")
 
 
 def head_bwd(dpool, out, y3, yd, gpre, stats, C, N, HW, Ch, NS):
-    rc = _fn("fa_head_bwd")(_p(dpool), _p(out), _p(y3), _p(yd), _p(gpre), _p(stats), _i(C), _i(N), _i(HW), _i(Ch),
+    rc = _fnp("fa_head_bwd", out)(_p(dpool), _p(out), _p(y3), _p(yd), _p(gpre), _p(stats), _i(C), _i(N), _i(HW), _i(Ch),
                             _i(NS), _stream(out))
     _check(rc, "fa_head_bwd")
 
 
 def nchw_to_nhwc_pad(x, y, CN, Cin, HW, Cpad):
-    rc = _fn("fa_nchw_to_nhwc_pad")(_p(x), _p(y), _i64(CN), _i(Cin), _i(HW), _i(Cpad), _stream(x))
+    rc = _fnp("fa_nchw_to_nhwc_pad", y)(_p(x), _p(y), _i64(CN), _i(Cin), _i(HW), _i(Cpad), _stream(x))
     _check(rc, "fa_nchw_to_nhwc_pad")
 
 

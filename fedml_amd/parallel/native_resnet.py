@@ -3,7 +3,9 @@
 Executes one local SGD step for C virtual clients at once on CIFAR-style ResNets
 (``models.cv.resnet.ResNet`` with Bottleneck / BasicBlock blocks — ResNet-56/110, and
 ``ResNet18Cifar``), reading weights from and writing gradients to the client-stacked
-fp32 arenas [C, P] directly. Activations are bf16 NHWC per client; every BatchNorm is
+fp32 arenas [C, P] directly. Activations are NHWC per client in the storage precision chosen at
+construction: fp32 (the reference's training precision — exact fp32 MFMA products,
+``csrc/prec.h``) or bf16 (fp32 accumulation and statistics). Every BatchNorm is
 folded into its neighbours' kernels (forward: consumer operand load + producer epilogue
 statistics; backward: consumer operand load + producer epilogue statistics), so each
 activation tensor is written once and read by exactly the kernels that need it.
@@ -130,7 +132,10 @@ def parse_resnet(model: nn.Module):
 class NativeResNetStep:
     """Owns the activation / statistics buffers for one (C, N, H, W) geometry."""
 
-    def __init__(self, model: nn.Module, layout, C: int, device):
+    def __init__(self, model: nn.Module, layout, C: int, device, dtype: torch.dtype = torch.float32):
+        if dtype not in (torch.float32, torch.bfloat16):
+            raise UnsupportedNative(f"storage dtype {dtype} (native kernels: float32 | bfloat16)")
+        self.dtype = dtype
         self.layout = layout
         self.C = C
         self.device = torch.device(device)
@@ -196,13 +201,13 @@ class NativeResNetStep:
             segs.append((self.off[cv.key], cv.off_f, cv.off_b, cv.cout, cv.cin_pad, cv.k, cv.k, cv.ldk, cv.ldk2,
                          cv.cin))
         self.packed_ld = _round_up(off, 64)
-        self.packed = torch.zeros(C, self.packed_ld, dtype=torch.bfloat16, device=dev)
+        self.packed = torch.zeros(C, self.packed_ld, dtype=self.dtype, device=dev)
         arr = (nn_ops.PackSeg * len(segs))(*[nn_ops.PackSeg(*s) for s in segs])
         raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
         self._segs = raw.to(dev)
         self._nseg = len(segs)
-        # activations (bf16) and per-BN vectors
-        bf = torch.bfloat16
+        # activations (storage precision) and per-BN vectors
+        bf = self.dtype
 
         def act(hh, ww, ch):
             return torch.empty(C, N, hh, ww, ch, dtype=bf, device=dev)
@@ -296,12 +301,6 @@ class NativeResNetStep:
         o = self.off
         return (o[f"{bn.key}.weight"], o[f"{bn.key}.bias"], o[f"{bn.key}.running_mean"],
                 o[f"{bn.key}.running_var"], o.get(f"{bn.key}.num_batches_tracked", -1))
-
-    def _conv_fwd(self, cv, x, pro_bn, y, N):
-        vec = self.bn_vec[pro_bn.key] if pro_bn is not None else None
-        fst = None
-        # the stats buffer of the BN that follows this conv is resolved by the caller
-        return vec
 
     def _c3(self, cv: ConvSpec):
         return self.use_c3 and nn_ops.conv3x3_supported(cv.cin_pad, cv.cout, cv.k, cv.stride, cv.pad, cv.H, cv.W)

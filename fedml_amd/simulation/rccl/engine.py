@@ -115,9 +115,13 @@ class ClientBatchEngine:
         self.native_step = None
         if self.device.type == "cuda" and not self.sequential and os.environ.get("FEDML_AMD_NATIVE_CONV", "1") != "0":
             from ...parallel.native_resnet import NativeResNetStep, UnsupportedNative
+            # the native kernels run at the requested precision: fp32 (compute_dtype None / fp32, the
+            # reference's) or bf16; any other dtype keeps the torch path, which honours it
             try:
-                self.native_step = NativeResNetStep(model, self.layout, self.C, self.device)
-                logging.info("virtual-client engine: native HIP ResNet path (C=%d)", self.C)
+                self.native_step = NativeResNetStep(model, self.layout, self.C, self.device,
+                                                    dtype=self.compute_dtype or torch.float32)
+                logging.info("virtual-client engine: native HIP ResNet path (C=%d, %s)", self.C,
+                             self.native_step.dtype)
             except UnsupportedNative as e:
                 logging.info("virtual-client engine: torch batched path (%s)", e)
         # Client-stacked grouped convolutions only pay while each client's conv is too small to fill

@@ -35,8 +35,12 @@ from .engine import ClientBatchEngine
 
 
 def _dtype(name):
-    return {"bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp16": torch.float16, "fp32": None,
-            "float32": None, None: None}.get(name, None)
+    """compute_dtype config value → engine compute dtype (None = fp32, the reference's precision)."""
+    table = {"bf16": torch.bfloat16, "bfloat16": torch.bfloat16, "fp16": torch.float16, "float16": torch.float16,
+             "fp32": None, "float32": None, None: None}
+    if name not in table:
+        raise ValueError(f"compute_dtype {name!r}: expected one of fp32 | bf16 | fp16")
+    return table[name]
 
 
 class RCCLSimulator:

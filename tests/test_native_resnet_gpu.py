@@ -51,7 +51,7 @@ def test_native_step_matches_reference(builder, hw):
     y = torch.randint(0, model.fc.out_features, (C, N), device=DEV)
     row_scale = torch.full((C, N), 1.0 / N, device=DEV)
     active = torch.ones(C, device=DEV)
-    step = NativeResNetStep(model, layout, C, DEV)
+    step = NativeResNetStep(model, layout, C, DEV, dtype=torch.bfloat16)
     loss = float(step.step(arena, garena, x, y, row_scale, active))
     torch.cuda.synchronize()
     ref_loss, ref = _reference_grads(model, layout, flat, x, y)
