@@ -8,8 +8,11 @@ using prec::BF16;
 using prec::F32;
 
 // ---- forward finalisation: statistics → folded scale/shift, running-stat update ----
-// stats[c][ch][2] = (Σy, Σy²) over n = N·H·W elements of client c.
-// scale = γ·rstd, shift = β − mean·scale; mean/rstd saved for the backward.
+// stats[c][ch][2] = (Σy, Σy²) over n = N·H·W elements of client c, of the STORED activation
+// y = conv − K (K = pivot[c][ch], null → 0; the conv epilogue subtracted it). Everything downstream
+// works on the stored values: scale = γ·rstd, shift = β − mean_s·scale with mean_s = mean(y), saved
+// with rstd for the backward. The true mean (mean_s + K) feeds the running statistics and becomes the
+// next step's pivot (written back into `pivot`), so the stored activations stay centred near 0.
 // Running statistics (torch semantics: unbiased variance, momentum) and num_batches_tracked
 // are updated in the parameter arena for ACTIVE clients only.
 __global__ void bn_fwd_finalize_kernel(const float* __restrict__ stats, int Ch, float n, float* __restrict__ arena,
@@ -17,26 +20,29 @@ __global__ void bn_fwd_finalize_kernel(const float* __restrict__ stats, int Ch, 
                                        int64_t off_rv, int64_t off_nbt, float momentum, float eps,
                                        const float* __restrict__ active, float* __restrict__ scale,
                                        float* __restrict__ shift, float* __restrict__ mean_out,
-                                       float* __restrict__ rstd_out, int update_running) {
+                                       float* __restrict__ rstd_out, int update_running, float* __restrict__ pivot) {
   const int c = blockIdx.y;
   const int ch = blockIdx.x * blockDim.x + threadIdx.x;
   if (ch >= Ch) return;
   float* pa = arena + (int64_t)c * ldw;
-  const float s1 = stats[((int64_t)c * Ch + ch) * 2 + 0];
-  const float s2 = stats[((int64_t)c * Ch + ch) * 2 + 1];
+  const int64_t v = (int64_t)c * Ch + ch;
+  const float s1 = stats[v * 2 + 0];
+  const float s2 = stats[v * 2 + 1];
   const float mean = s1 / n;
   const float var = fmaxf(s2 / n - mean * mean, 0.f);
   const float rstd = rsqrtf(var + eps);
   const float g = off_gamma >= 0 ? pa[off_gamma + ch] : 1.f;
   const float b = off_beta >= 0 ? pa[off_beta + ch] : 0.f;
-  const int64_t v = (int64_t)c * Ch + ch;
+  const float k = pivot ? pivot[v] : 0.f;
+  const float true_mean = mean + k;
   scale[v] = g * rstd;
   shift[v] = b - mean * g * rstd;
   mean_out[v] = mean;
   rstd_out[v] = rstd;
   const bool on = active ? active[c] > 0.f : true;
+  if (pivot && on) pivot[v] = true_mean;
   if (update_running && on) {
-    if (off_rm >= 0) pa[off_rm + ch] = (1.f - momentum) * pa[off_rm + ch] + momentum * mean;
+    if (off_rm >= 0) pa[off_rm + ch] = (1.f - momentum) * pa[off_rm + ch] + momentum * true_mean;
     if (off_rv >= 0) pa[off_rv + ch] = (1.f - momentum) * pa[off_rv + ch] + momentum * var * n / fmaxf(n - 1.f, 1.f);
     if (off_nbt >= 0 && ch == 0) pa[off_nbt] += 1.f;
   }
@@ -45,10 +51,11 @@ __global__ void bn_fwd_finalize_kernel(const float* __restrict__ stats, int Ch, 
 FA_EXPORT int fa_bn_fwd_finalize(const float* stats, int C, int Ch, float n, float* arena, int64_t ldw,
                                  int64_t off_gamma, int64_t off_beta, int64_t off_rm, int64_t off_rv, int64_t off_nbt,
                                  float momentum, float eps, const float* active, float* scale, float* shift,
-                                 float* mean_out, float* rstd_out, int update_running, hipStream_t stream) {
+                                 float* mean_out, float* rstd_out, int update_running, float* pivot,
+                                 hipStream_t stream) {
   hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((Ch + 63) / 64, C), dim3(64), 0, stream, stats, Ch, n, arena, ldw,
                      off_gamma, off_beta, off_rm, off_rv, off_nbt, momentum, eps, active, scale, shift, mean_out,
-                     rstd_out, update_running);
+                     rstd_out, update_running, pivot);
   return (int)hipGetLastError();
 }
 

@@ -218,6 +218,7 @@ struct Args {              // tensors are P::T (bf16 | fp32) unless noted
   const float* e_s;
   const float* e_t;
   float* stats;          // [C][NOUT][NS]
+  const float* pivot;    // EPI_FWD: per-(client, channel) shift subtracted from the stored output (or null)
   int NS;
   int N, H, W;                    // output (iteration) geometry
   int Hs, Ws;                     // A-operand source geometry (≠ H, W for stride 2)
@@ -294,8 +295,15 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
   T* out = reinterpret_cast<T*>(a.out) + (int64_t)c * a.N * HW * NO;
   const T* ex = (EPI == EPI_MASK) ? reinterpret_cast<const T*>(a.e_x) + (int64_t)c * a.N * HW * NO : nullptr;
 
-  // per-lane epilogue state: channels ch_base + nt·16 + 4g + i
-  float st0[NT][4], st1[NT][4];
+  // per-lane epilogue state: channels ch_base + nt·16 + 4g + i; forward outputs are stored as y − K with a
+  // per-channel pivot K ≈ the batch mean (BatchNorm statistics and the folded backward then work on
+  // values centred near 0: no E[y²] − mean² cancellation)
+  float st0[NT][4], st1[NT][4], piv[NT][4];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      piv[nt][i] = (EPI == EPI_FWD && a.pivot) ? a.pivot[(int64_t)c * NO + ch_base + nt * 16 + 4 * g + i] : 0.f;
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
@@ -400,6 +408,8 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
         for (int nt = 0; nt < NT; ++nt) {
           float f[4] = {acc[mt][nt][0], acc[mt][nt][1], acc[mt][nt][2], acc[mt][nt][3]};
           if (EPI == EPI_FWD) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) f[i] -= piv[nt][i];
             P::store4(out + prow + nt * 16, f);   // f ← the stored (rounded) values
 #pragma unroll
             for (int i = 0; i < 4; ++i) { st0[nt][i] += f[i]; st1[nt][i] += f[i] * f[i]; }
@@ -728,10 +738,11 @@ static int dispatch_gemm(int kc, int nout, const Args& a, int C, hipStream_t s) 
 template <class P>
 static int conv3x3_fwd(const void* x, const void* wpk, int64_t wpk_ld, const float* pscale, const float* pshift,
                        void* y, float* stats, int C, int N, int H, int W, int Cin, int Cout, int ldk, int stride,
-                       hipStream_t stream) {
+                       const float* pivot, hipStream_t stream) {
   if ((stride != 1 && stride != 2) || H % stride || W % stride || (W / stride) % 8 != 0) return -3;
   Args a = {};
   a.src = x; a.wpk = wpk; a.wpk_ld = wpk_ld; a.vec0 = pscale; a.vec1 = pshift; a.out = y; a.stats = stats; a.NS = 2;
+  a.pivot = pivot;
   a.N = N; a.H = H / stride; a.W = W / stride; a.Hs = H; a.Ws = W; a.ldk = ldk;
   if (stride == 2) {
     if (pscale) return dispatch_gemm<P, XF_BNRELU, 0, EPI_FWD, 2>(Cin, Cout, a, C, stream);
@@ -828,19 +839,20 @@ static int conv3x3_wgrad(const void* g, const void* yv, const float* alpha, cons
 
 }  // namespace c3
 
-// forward 3×3 / pad 1 / stride 1|2: y = conv(pro(x)); stats[c][co][2] += (Σy, Σy²).
-// (H, W) = input resolution. Returns < 0 if unsupported. `_f32`: fp32 activations / packed weights.
+// forward 3×3 / pad 1 / stride 1|2: y = conv(pro(x)) − K; stats[c][co][2] += (Σy, Σy²) of the stored y.
+// K = pivot[c][co] (null: 0). (H, W) = input resolution. Returns < 0 if unsupported.
+// `_f32`: fp32 activations / packed weights.
 FA_EXPORT int fa_conv3x3_fwd(const uint16_t* x, const uint16_t* wpk, int64_t wpk_ld, const float* pscale,
                              const float* pshift, uint16_t* y, float* stats, int C, int N, int H, int W, int Cin,
-                             int Cout, int ldk, int stride, hipStream_t stream) {
+                             int Cout, int ldk, int stride, const float* pivot, hipStream_t stream) {
   return c3::conv3x3_fwd<c3::BF16>(x, wpk, wpk_ld, pscale, pshift, y, stats, C, N, H, W, Cin, Cout, ldk, stride,
-                                   stream);
+                                   pivot, stream);
 }
 FA_EXPORT int fa_conv3x3_fwd_f32(const float* x, const float* wpk, int64_t wpk_ld, const float* pscale,
                                  const float* pshift, float* y, float* stats, int C, int N, int H, int W, int Cin,
-                                 int Cout, int ldk, int stride, hipStream_t stream) {
+                                 int Cout, int ldk, int stride, const float* pivot, hipStream_t stream) {
   return c3::conv3x3_fwd<c3::F32>(x, wpk, wpk_ld, pscale, pshift, y, stats, C, N, H, W, Cin, Cout, ldk, stride,
-                                  stream);
+                                  pivot, stream);
 }
 
 // backward-data 3×3 / pad 1 / stride 1|2 with the ReLU-mask epilogue (EPI_MASK of the generic kernel):

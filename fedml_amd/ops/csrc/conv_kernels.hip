@@ -122,6 +122,7 @@ struct ConvArgs {        // activations / packed weights are P::T (bf16 | fp32)
   const void* e_y1;      // EPI_BLOCK: previous block's bn3 input (Σg·y)
   const void* e_y2;      // EPI_BLOCK: previous block's downsample-bn input (optional)
   float* stats;          // [C][NOUT][NS]
+  const float* pivot;    // EPI_FWD: per-(client, channel) shift subtracted from the stored output (or null)
   int NS;
   int Nb, Hs, Ws, KC;    // source geometry (KC = channels of the A source = GEMM K per tap)
   int Ho, Wo;            // output geometry
@@ -247,13 +248,14 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
       }
     }
 
-    // ---- stage the 16 × NOUT tile (storage precision) in LDS ----
+    // ---- stage the 16 × NOUT tile (storage precision) in LDS; forward outputs as y − K (pivot) ----
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
+      const float k = (EPI == EPI_FWD && a.pivot) ? a.pivot[(int64_t)c * NO + ch_base + nt * 16 + (lane & 15)] : 0.f;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int row = 4 * (lane >> 4) + i;
-        my_stage[row * NOUT + nt * 16 + (lane & 15)] = P::from_f(acc[nt][i]);
+        my_stage[row * NOUT + nt * 16 + (lane & 15)] = P::from_f(acc[nt][i] - k);
       }
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): LDS writes visible to this wave
@@ -391,10 +393,11 @@ static int dispatch_nt(int nout, const ConvArgs& a, int C, hipStream_t s) {
 template <class P>
 static int conv_fwd(const void* x, const void* wpk, int64_t wpk_ld, const float* pscale, const float* pshift, void* y,
                     float* stats, int C, int Nb, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
-                    int Ho, int Wo, int ldk, int tiles_per_wave, hipStream_t stream) {
+                    int Ho, int Wo, int ldk, int tiles_per_wave, const float* pivot, hipStream_t stream) {
   if (Cin % 8 != 0) return -3;
   ConvArgs a = {};
   a.src = x; a.wpk = wpk; a.wpk_ld = wpk_ld; a.vec0 = pscale; a.vec1 = pshift; a.out = y; a.stats = stats; a.NS = 2;
+  a.pivot = pivot;
   a.Nb = Nb; a.Hs = H; a.Ws = W; a.KC = Cin; a.Ho = Ho; a.Wo = Wo; a.KH = KH; a.KW = KW; a.stride = stride;
   a.pad = pad; a.ldk = ldk; a.Kp = (KH * KW * Cin + 31) / 32 * 32; a.tiles_per_wave = tiles_per_wave;
   if (pscale)
@@ -423,20 +426,21 @@ static int conv_bwd_data(const void* g, const void* yv, const float* alpha, cons
   }
 }
 
-// forward: y = conv(pro(x)), stats[c][co][2] += (Σy, Σy²). `_f32`: fp32 activations / packed weights.
+// forward: y = conv(pro(x)) − K, stats[c][co][2] += (Σy, Σy²) of the stored y; K = pivot[c][co] (null: 0).
+// `_f32`: fp32 activations / packed weights.
 FA_EXPORT int fa_conv_fwd(const uint16_t* x, const uint16_t* wpk, int64_t wpk_ld, const float* pscale,
                           const float* pshift, uint16_t* y, float* stats, int C, int Nb, int H, int W, int Cin,
                           int Cout, int KH, int KW, int stride, int pad, int Ho, int Wo, int ldk, int tiles_per_wave,
-                          hipStream_t stream) {
+                          const float* pivot, hipStream_t stream) {
   return conv_fwd<BF16>(x, wpk, wpk_ld, pscale, pshift, y, stats, C, Nb, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo,
-                        ldk, tiles_per_wave, stream);
+                        ldk, tiles_per_wave, pivot, stream);
 }
 FA_EXPORT int fa_conv_fwd_f32(const float* x, const float* wpk, int64_t wpk_ld, const float* pscale,
                               const float* pshift, float* y, float* stats, int C, int Nb, int H, int W, int Cin,
                               int Cout, int KH, int KW, int stride, int pad, int Ho, int Wo, int ldk,
-                              int tiles_per_wave, hipStream_t stream) {
+                              int tiles_per_wave, const float* pivot, hipStream_t stream) {
   return conv_fwd<F32>(x, wpk, wpk_ld, pscale, pshift, y, stats, C, Nb, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo,
-                       ldk, tiles_per_wave, stream);
+                       ldk, tiles_per_wave, pivot, stream);
 }
 
 // backward-data: dx = convᵀ(α·g + β·y + γ) with epilogue

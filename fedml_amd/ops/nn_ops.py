@@ -43,10 +43,11 @@ def pack_weights(arena, segs_dev, nseg, dst, dst_ld, C):
 
 
 def conv_fwd(x, wpk, wpk_ld, pscale, pshift, y, stats, C, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, ldk,
-             tiles_per_wave):
+             tiles_per_wave, pivot=None):
+    """y = conv(pro(x)) − pivot (per client and output channel; None → 0), BN statistics of y."""
     rc = _fnp("fa_conv_fwd", x)(_p(x), _p(wpk), _i64(wpk_ld), _p(pscale), _p(pshift), _p(y), _p(stats), _i(C), _i(N),
                             _i(H), _i(W), _i(Cin), _i(Cout), _i(KH), _i(KW), _i(stride), _i(pad), _i(Ho), _i(Wo),
-                            _i(ldk), _i(tiles_per_wave), _stream(x))
+                            _i(ldk), _i(tiles_per_wave), _p(pivot), _stream(x))
     _check(rc, "fa_conv_fwd")
 
 
@@ -83,9 +84,9 @@ def conv3x3_supported(cin, cout, k, stride, pad, H, W):
     return Wo % 8 == 0 and W % 8 == 0 and (Ho * Wo) % 32 == 0
 
 
-def conv3x3_fwd(x, wpk, wpk_ld, pscale, pshift, y, stats, C, N, H, W, Cin, Cout, ldk, stride=1):
+def conv3x3_fwd(x, wpk, wpk_ld, pscale, pshift, y, stats, C, N, H, W, Cin, Cout, ldk, stride=1, pivot=None):
     rc = _fnp("fa_conv3x3_fwd", x)(_p(x), _p(wpk), _i64(wpk_ld), _p(pscale), _p(pshift), _p(y), _p(stats), _i(C), _i(N),
-                               _i(H), _i(W), _i(Cin), _i(Cout), _i(ldk), _i(stride), _stream(x))
+                               _i(H), _i(W), _i(Cin), _i(Cout), _i(ldk), _i(stride), _p(pivot), _stream(x))
     _check(rc, "fa_conv3x3_fwd")
 
 
@@ -174,11 +175,13 @@ def conv1x1_bwd_fused(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, ldk2, e_x, e_s, 
 
 
 def bn_fwd_finalize(stats, C, Ch, n, arena, off_gamma, off_beta, off_rm, off_rv, off_nbt, momentum, eps, active,
-                    scale, shift, mean, rstd, update_running=True):
+                    scale, shift, mean, rstd, update_running=True, pivot=None):
+    """``pivot`` [C, Ch] (optional, in/out): the shift the producing conv subtracted; replaced by this
+    batch's true mean (the next step's pivot)."""
     rc = _fn("fa_bn_fwd_finalize")(_p(stats), _i(C), _i(Ch), _f(n), _p(arena), _i64(arena.stride(0)),
                                    _i64(off_gamma), _i64(off_beta), _i64(off_rm), _i64(off_rv), _i64(off_nbt),
                                    _f(momentum), _f(eps), _p(active), _p(scale), _p(shift), _p(mean), _p(rstd),
-                                   _i(int(update_running)), _stream(stats))
+                                   _i(int(update_running)), _p(pivot), _stream(stats))
     _check(rc, "fa_bn_fwd_finalize")
 
 

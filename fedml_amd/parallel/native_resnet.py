@@ -149,6 +149,7 @@ class NativeResNetStep:
         self.use_c3 = os.environ.get("FEDML_AMD_CONV3X3", "1") != "0"
         self.use_c1 = os.environ.get("FEDML_AMD_CONV1X1", "1") != "0"
         self.use_c1f = os.environ.get("FEDML_AMD_C1_FUSED", "1") != "0"
+        self.dump = None   # debug: list collecting (name, tensor clone) of every backward gradient buffer
 
     # ------------------------------------------------------------------ setup
     def _all_convs(self):
@@ -226,11 +227,13 @@ class NativeResNetStep:
         # gradient scratch: block-output g (kept until the block's conv0 is done), two ping-pong
         # buffers for the inner chain, one for the shortcut gradient
         self.gbuf = [torch.empty(C * N * maxel, dtype=bf, device=dev) for _ in range(4)]
-        # per-BN vectors: scale, shift, mean, rstd, alpha, beta, gamma   + stats
+        # per-BN vectors: scale, shift, mean, rstd, alpha, beta, gamma, pivot   + stats
+        # (pivot: the per-channel shift K the producing conv subtracts from its stored output — the
+        # previous step's batch mean — so activations and BN sums stay centred; see bn_fwd_finalize)
         self.bn_vec = {}
         nstat = 0
         for bn in self._all_bns():
-            self.bn_vec[bn.key] = torch.empty(7, C, bn.ch, dtype=torch.float32, device=dev)
+            self.bn_vec[bn.key] = torch.zeros(8, C, bn.ch, dtype=torch.float32, device=dev)
             nstat += bn.ch * 5
         self.stats = torch.zeros(C * nstat, dtype=torch.float32, device=dev)
         self.stat_views = {}
@@ -261,6 +264,12 @@ class NativeResNetStep:
         raw = bytes((nn_ops.ScatterSeg * max(1, len(segs)))(*segs))
         self.c3_segs = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
         self.geom = (N, H, W)
+        if os.environ.get("FEDML_AMD_POISON", "0") == "1":   # debug: uninitialised reads show up as NaN
+            for t in [self.x_in, self.stem_y, self.stem_out, self.pooled] + list(self.gbuf):
+                t.fill_(float("nan"))
+            for b in self.blocks:
+                for t in b.ys + [b.out] + ([b.yd] if b.yd is not None else []):
+                    t.fill_(float("nan"))
 
     # Every geometry keeps its own buffers alive: a captured HIP graph of one batch size must stay
     # valid while another batch size (the ragged last step of an epoch) is being run.
@@ -301,6 +310,10 @@ class NativeResNetStep:
         o = self.off
         return (o[f"{bn.key}.weight"], o[f"{bn.key}.bias"], o[f"{bn.key}.running_mean"],
                 o[f"{bn.key}.running_var"], o.get(f"{bn.key}.num_batches_tracked", -1))
+
+    def _dump(self, name, t, n):
+        if self.dump is not None:
+            self.dump.append((name, t.reshape(-1)[:n].clone()))
 
     def _c3(self, cv: ConvSpec):
         return self.use_c3 and nn_ops.conv3x3_supported(cv.cin_pad, cv.cout, cv.k, cv.stride, cv.pad, cv.H, cv.W)
@@ -350,25 +363,29 @@ class NativeResNetStep:
             return ppw
         return max(512, min(2048, _round_up(max(1, (M * self.C) // 1024), 128)))
 
-    def _fwd(self, cv: ConvSpec, x, y, pro_vec, stats, N):
+    def _fwd(self, cv: ConvSpec, x, y, pro_vec, bn: BNSpec, N):
+        """y = conv(pro(x)) − pivot of the BN that follows; that BN's forward statistics."""
         M = N * cv.Ho * cv.Wo
+        stats = self.stat_views[bn.key][0]
+        pivot = self.bn_vec[bn.key][7]
         # the strided 64-channel forward stays on the generic kernel (measured faster: tiny 8×8 outputs)
         if self._c3(cv) and not (cv.stride == 2 and cv.cin_pad >= 64):
             nn_ops.conv3x3_fwd(x, self.packed.view(-1)[cv.off_f:], self.packed_ld,
                                pro_vec[0] if pro_vec is not None else None,
                                pro_vec[1] if pro_vec is not None else None, y, stats, self.C, N, cv.H, cv.W,
-                               cv.cin_pad, cv.cout, cv.ldk, cv.stride)
+                               cv.cin_pad, cv.cout, cv.ldk, cv.stride, pivot=pivot)
             return
         nn_ops.conv_fwd(x, self.packed.view(-1)[cv.off_f:], self.packed_ld, pro_vec[0] if pro_vec is not None else None,
                         pro_vec[1] if pro_vec is not None else None, y, stats, self.C, N, cv.H, cv.W, cv.cin_pad,
-                        cv.cout, cv.k, cv.k, cv.stride, cv.pad, cv.Ho, cv.Wo, cv.ldk, self._tiles_per_wave(M))
+                        cv.cout, cv.k, cv.k, cv.stride, cv.pad, cv.Ho, cv.Wo, cv.ldk, self._tiles_per_wave(M),
+                        pivot=pivot)
 
     def _bn_fwd(self, bn, N, hw, arena, active, training=True):
         v = self.bn_vec[bn.key]
         fst = self.stat_views[bn.key][0]
         g, b, rm, rv, nbt = self._bn_offsets(bn)
         nn_ops.bn_fwd_finalize(fst, self.C, bn.ch, float(N * hw), arena, g, b, rm, rv, nbt, bn.momentum, bn.eps,
-                               active, v[0], v[1], v[2], v[3], training)
+                               active, v[0], v[1], v[2], v[3], training, pivot=v[7])
 
     def _bn_bwd(self, bn, q, N, hw, arena, garena):
         v = self.bn_vec[bn.key]
@@ -395,7 +412,7 @@ class NativeResNetStep:
         nn_ops.nchw_to_nhwc_pad(x.contiguous(), self.x_in, C * N, st_conv.cin, H * W, st_conv.cin_pad)
 
         # ---------------- forward ----------------
-        self._fwd(st_conv, self.x_in, self.stem_y, None, self.stat_views[st_bn.key][0], N)
+        self._fwd(st_conv, self.x_in, self.stem_y, None, st_bn, N)
         self._bn_fwd(st_bn, N, st_conv.Ho * st_conv.Wo, arena, active)
         v0 = self.bn_vec[st_bn.key]
         nn_ops.block_out(self.stem_y, v0[0], v0[1], None, None, None, self.stem_out, C,
@@ -407,13 +424,13 @@ class NativeResNetStep:
             for j, (cv, bn) in enumerate(zip(b.convs, b.bns)):
                 src = act_in if j == 0 else b.ys[j - 1]
                 pro = None if j == 0 else self.bn_vec[b.bns[j - 1].key]
-                self._fwd(cv, src, b.ys[j], pro, self.stat_views[bn.key][0], N)
+                self._fwd(cv, src, b.ys[j], pro, bn, N)
                 self._bn_fwd(bn, N, cv.Ho * cv.Wo, arena, active)
             last, lbn = b.convs[-1], b.bns[-1]
             vl = self.bn_vec[lbn.key]
             if b.ds_conv is not None:
                 d = b.ds_conv
-                self._fwd(d, act_in, b.yd, None, self.stat_views[b.ds_bn.key][0], N)
+                self._fwd(d, act_in, b.yd, None, b.ds_bn, N)
                 self._bn_fwd(b.ds_bn, N, d.Ho * d.Wo, arena, active)
                 vd = self.bn_vec[b.ds_bn.key]
                 nn_ops.block_out(b.ys[-1], vl[0], vl[1], b.yd, vd[0], vd[1], b.out, C,
@@ -474,6 +491,7 @@ class NativeResNetStep:
                                              M, cv.cin, cv.cout, nn_ops.EPI_MASK, self._c1f_pix_per_wg(M))
                     self._bn_bwd(b.bns[j - 1], 1, N, cv.H * cv.W, arena, garena)
                     g_j = out_g
+                    self._dump(f"{cv.key}.dx", out_g, C * N * cv.H * cv.W * cv.cin)
                     continue
                 self._wgrad(cv, g_j, b.ys[j], v, b.ys[j - 1], pv, garena, N)
                 if self._c3(cv):
@@ -483,6 +501,7 @@ class NativeResNetStep:
                                             cv.cin_pad, cv.ldk2, cv.stride)
                     self._bn_bwd(b.bns[j - 1], 1, N, cv.H * cv.W, arena, garena)
                     g_j = out_g
+                    self._dump(f"{cv.key}.dx", out_g, C * N * cv.H * cv.W * cv.cin)
                     continue
                 nn_ops.conv_bwd_data(g_j, b.ys[j], v[4], v[5], v[6], self.packed.view(-1)[cv.off_b:],
                                      self.packed_ld, out_g, nn_ops.EPI_MASK, b.ys[j - 1], pv[0], pv[1], None, None,
@@ -491,6 +510,7 @@ class NativeResNetStep:
                                      self._tiles_per_wave(N * cv.H * cv.W))
                 self._bn_bwd(b.bns[j - 1], 1, N, cv.H * cv.W, arena, garena)
                 g_j = out_g
+                self._dump(f"{cv.key}.dx", out_g, C * N * cv.H * cv.W * cv.cin)
             # shortcut gradient D into free[2] (downsample) or the block's own gpre (identity)
             gadd = free[2]
             if b.ds_conv is not None:
@@ -527,6 +547,7 @@ class NativeResNetStep:
                                          pstats, garena, self.off[cv0.key], C, M0, cv0.cin, cv0.cout,
                                          nn_ops.EPI_BLOCK, self._c1f_pix_per_wg(M0))
                 gpre = out_buf
+                self._dump(f"{cv0.key}.dx", out_buf, C * N * cv0.H * cv0.W * cv0.cin)
                 continue
             nn_ops.conv_bwd_data(g_j, b.ys[0], v[4], v[5], v[6], self.packed.view(-1)[cv0.off_b:], self.packed_ld,
                                  out_buf, nn_ops.EPI_BLOCK, b.act_in, None, None, shortcut, ey1, ey2, pstats, C, N,
@@ -534,6 +555,7 @@ class NativeResNetStep:
                                  cv0.W, cv0.ldk2, self._tiles_per_wave(N * cv0.H * cv0.W))
             # the previous block's gpre is out_buf
             gpre = out_buf
+            self._dump(f"{cv0.key}.dx", out_buf, C * N * cv0.H * cv0.W * cv0.cin)
         # stem backward: bn0 bwd then weight grad only
         self._bn_bwd(st_bn, 1, N, st_conv.Ho * st_conv.Wo, arena, garena)
         v = self.bn_vec[st_bn.key]
