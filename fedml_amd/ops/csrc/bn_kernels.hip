@@ -20,10 +20,13 @@ __global__ void bn_fwd_finalize_kernel(const float* __restrict__ stats, int Ch, 
                                        int64_t off_rv, int64_t off_nbt, float momentum, float eps,
                                        const float* __restrict__ active, float* __restrict__ scale,
                                        float* __restrict__ shift, float* __restrict__ mean_out,
-                                       float* __restrict__ rstd_out, int update_running, float* __restrict__ pivot) {
+                                       float* __restrict__ rstd_out, int update_running, float* __restrict__ pivot,
+                                       const int* __restrict__ nimg, int hw) {
   const int c = blockIdx.y;
   const int ch = blockIdx.x * blockDim.x + threadIdx.x;
   if (ch >= Ch) return;
+  if (nimg) n = (float)nimg[c] * (float)hw;   // heterogeneous batches: this client's valid elements
+  if (n <= 0.f) return;                       // client without data this step: nothing to normalise
   float* pa = arena + (int64_t)c * ldw;
   const int64_t v = (int64_t)c * Ch + ch;
   const float s1 = stats[v * 2 + 0];
@@ -51,11 +54,11 @@ __global__ void bn_fwd_finalize_kernel(const float* __restrict__ stats, int Ch, 
 FA_EXPORT int fa_bn_fwd_finalize(const float* stats, int C, int Ch, float n, float* arena, int64_t ldw,
                                  int64_t off_gamma, int64_t off_beta, int64_t off_rm, int64_t off_rv, int64_t off_nbt,
                                  float momentum, float eps, const float* active, float* scale, float* shift,
-                                 float* mean_out, float* rstd_out, int update_running, float* pivot,
-                                 hipStream_t stream) {
+                                 float* mean_out, float* rstd_out, int update_running, float* pivot, const int* nimg,
+                                 int hw, hipStream_t stream) {
   hipLaunchKernelGGL(bn_fwd_finalize_kernel, dim3((Ch + 63) / 64, C), dim3(64), 0, stream, stats, Ch, n, arena, ldw,
                      off_gamma, off_beta, off_rm, off_rv, off_nbt, momentum, eps, active, scale, shift, mean_out,
-                     rstd_out, update_running, pivot);
+                     rstd_out, update_running, pivot, nimg, hw);
   return (int)hipGetLastError();
 }
 
@@ -65,10 +68,13 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ bstats, int NS,
                                        const float* __restrict__ mean, const float* __restrict__ rstd,
                                        const float* __restrict__ arena, float* __restrict__ garena, int64_t ldw,
                                        int64_t off_gamma, int64_t off_beta, float* __restrict__ alpha,
-                                       float* __restrict__ beta_c, float* __restrict__ gamma_c) {
+                                       float* __restrict__ beta_c, float* __restrict__ gamma_c,
+                                       const int* __restrict__ nimg, int hw) {
   const int c = blockIdx.y;
   const int ch = blockIdx.x * blockDim.x + threadIdx.x;
   if (ch >= Ch) return;
+  if (nimg) n = (float)nimg[c] * (float)hw;
+  if (n <= 0.f) return;
   const int64_t v = (int64_t)c * Ch + ch;
   const float sg = bstats[v * NS + 0];
   const float sgy = bstats[v * NS + q_gy];
@@ -87,9 +93,10 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ bstats, int NS,
 
 FA_EXPORT int fa_bn_bwd_finalize(const float* bstats, int NS, int q_gy, int C, int Ch, float n, const float* mean,
                                  const float* rstd, const float* arena, float* garena, int64_t ldw, int64_t off_gamma,
-                                 int64_t off_beta, float* alpha, float* beta_c, float* gamma_c, hipStream_t stream) {
+                                 int64_t off_beta, float* alpha, float* beta_c, float* gamma_c, const int* nimg, int hw,
+                                 hipStream_t stream) {
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((Ch + 63) / 64, C), dim3(64), 0, stream, bstats, NS, q_gy, Ch, n,
-                     mean, rstd, arena, garena, ldw, off_gamma, off_beta, alpha, beta_c, gamma_c);
+                     mean, rstd, arena, garena, ldw, off_gamma, off_beta, alpha, beta_c, gamma_c, nimg, hw);
   return (int)hipGetLastError();
 }
 
@@ -101,11 +108,12 @@ __global__ __launch_bounds__(256) void block_out_kernel(const typename P::T* __r
                                                         const float* __restrict__ t,
                                                         const typename P::T* __restrict__ r,
                                                         const float* __restrict__ rs, const float* __restrict__ rt,
-                                                        typename P::T* __restrict__ out, int nvec, int cg) {
+                                                        typename P::T* __restrict__ out, int nvec, int cg,
+                                                        const int* __restrict__ nimg, int vec_per_img) {
   constexpr int V = P::VEC;
   const int c = blockIdx.y;
   const int v = blockIdx.x * 256 + threadIdx.x;
-  if (v >= nvec) return;
+  if (v >= (nimg ? min(nvec, nimg[c] * vec_per_img) : nvec)) return;   // valid images of client c only
   const int64_t base = (int64_t)c * nvec * V + (int64_t)v * V;
   const int ch0 = (v % cg) * V;
   const int64_t co = (int64_t)c * cg * V + ch0;
@@ -133,7 +141,8 @@ __global__ __launch_bounds__(256) void block_out_kernel(const typename P::T* __r
 
 template <class P>
 static int block_out(const void* y, const float* s, const float* t, const void* r, const float* rs, const float* rt,
-                     void* out, int C, int64_t per_client, int Ch, hipStream_t stream) {
+                     void* out, int C, int64_t per_client, int Ch, const int* nimg, int per_img,
+                     hipStream_t stream) {
   using T = typename P::T;
   constexpr int V = P::VEC;
   if (Ch % V != 0 || per_client / V > INT32_MAX) return -3;
@@ -143,44 +152,56 @@ static int block_out(const void* y, const float* s, const float* t, const void* 
   const T* r_ = (const T*)r;
   T* o_ = (T*)out;
   if (!r)
-    hipLaunchKernelGGL((block_out_kernel<P, 0>), grid, dim3(256), 0, stream, y_, s, t, r_, rs, rt, o_, nvec, Ch / V);
+    hipLaunchKernelGGL((block_out_kernel<P, 0>), grid, dim3(256), 0, stream, y_, s, t, r_, rs, rt, o_, nvec, Ch / V,
+                       nimg, per_img / V);
   else if (!rs)
-    hipLaunchKernelGGL((block_out_kernel<P, 1>), grid, dim3(256), 0, stream, y_, s, t, r_, rs, rt, o_, nvec, Ch / V);
+    hipLaunchKernelGGL((block_out_kernel<P, 1>), grid, dim3(256), 0, stream, y_, s, t, r_, rs, rt, o_, nvec, Ch / V,
+                       nimg, per_img / V);
   else
-    hipLaunchKernelGGL((block_out_kernel<P, 2>), grid, dim3(256), 0, stream, y_, s, t, r_, rs, rt, o_, nvec, Ch / V);
+    hipLaunchKernelGGL((block_out_kernel<P, 2>), grid, dim3(256), 0, stream, y_, s, t, r_, rs, rt, o_, nvec, Ch / V,
+                       nimg, per_img / V);
   return (int)hipGetLastError();
 }
 
+// per_img: elements of one image (H·W·Ch); nimg: per-client valid images (null: all)
 FA_EXPORT int fa_block_out(const uint16_t* y, const float* s, const float* t, const uint16_t* r, const float* rs,
-                           const float* rt, uint16_t* out, int C, int64_t per_client, int Ch, hipStream_t stream) {
-  return block_out<BF16>(y, s, t, r, rs, rt, out, C, per_client, Ch, stream);
+                           const float* rt, uint16_t* out, int C, int64_t per_client, int Ch, const int* nimg,
+                           int per_img, hipStream_t stream) {
+  return block_out<BF16>(y, s, t, r, rs, rt, out, C, per_client, Ch, nimg, per_img, stream);
 }
 FA_EXPORT int fa_block_out_f32(const float* y, const float* s, const float* t, const float* r, const float* rs,
-                               const float* rt, float* out, int C, int64_t per_client, int Ch, hipStream_t stream) {
-  return block_out<F32>(y, s, t, r, rs, rt, out, C, per_client, Ch, stream);
+                               const float* rt, float* out, int C, int64_t per_client, int Ch, const int* nimg,
+                               int per_img, hipStream_t stream) {
+  return block_out<F32>(y, s, t, r, rs, rt, out, C, per_client, Ch, nimg, per_img, stream);
 }
 
 // ---- global average pool (forward): pooled[c][n][ch] = mean_hw out[c][n][hw][ch] (fp32 out)
+// Padding images (n ≥ nimg[c], N images per client) get zero rows: the head reads them (with zero loss
+// weight) and must see finite values.
 template <class P>
 __global__ __launch_bounds__(256) void avgpool_kernel(const typename P::T* __restrict__ x, float* __restrict__ pooled,
-                                                      int HW, int Ch) {
+                                                      int HW, int Ch, const int* __restrict__ nimg, int N) {
   const int cn = blockIdx.x;  // flattened (client, sample)
+  const bool valid = !nimg || (cn % N) < nimg[cn / N];
   const typename P::T* xs = x + (int64_t)cn * HW * Ch;
   for (int ch = threadIdx.x; ch < Ch; ch += blockDim.x) {
     float s = 0.f;
-    for (int p = 0; p < HW; ++p) s += P::to_f(xs[(int64_t)p * Ch + ch]);
+    if (valid)
+      for (int p = 0; p < HW; ++p) s += P::to_f(xs[(int64_t)p * Ch + ch]);
     pooled[(int64_t)cn * Ch + ch] = s / (float)HW;
   }
 }
 
-FA_EXPORT int fa_avgpool(const uint16_t* x, float* pooled, int CN, int HW, int Ch, hipStream_t stream) {
+FA_EXPORT int fa_avgpool(const uint16_t* x, float* pooled, int CN, int HW, int Ch, const int* nimg, int N,
+                         hipStream_t stream) {
   hipLaunchKernelGGL(avgpool_kernel<BF16>, dim3(CN), dim3(Ch < 256 ? 64 * ((Ch + 63) / 64) : 256), 0, stream, x,
-                     pooled, HW, Ch);
+                     pooled, HW, Ch, nimg, N);
   return (int)hipGetLastError();
 }
-FA_EXPORT int fa_avgpool_f32(const float* x, float* pooled, int CN, int HW, int Ch, hipStream_t stream) {
+FA_EXPORT int fa_avgpool_f32(const float* x, float* pooled, int CN, int HW, int Ch, const int* nimg, int N,
+                             hipStream_t stream) {
   hipLaunchKernelGGL(avgpool_kernel<F32>, dim3(CN), dim3(Ch < 256 ? 64 * ((Ch + 63) / 64) : 256), 0, stream, x,
-                     pooled, HW, Ch);
+                     pooled, HW, Ch, nimg, N);
   return (int)hipGetLastError();
 }
 
@@ -193,9 +214,10 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
                                                        const typename P::T* __restrict__ y3,
                                                        const typename P::T* __restrict__ yd,
                                                        typename P::T* __restrict__ gpre, float* __restrict__ stats,
-                                                       int N, int HW, int Ch, int NS) {
+                                                       int N, int HW, int Ch, int NS, const int* __restrict__ nimg) {
   const int cn = blockIdx.x;
   const int c = cn / N;
+  if (nimg && (cn % N) >= nimg[c]) return;   // padding image: its gradient is never read
   const int64_t base = (int64_t)cn * HW * Ch;
   const float inv = 1.f / (float)HW;
   for (int ch = threadIdx.x; ch < Ch; ch += blockDim.x) {
@@ -219,15 +241,16 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
 }
 
 FA_EXPORT int fa_head_bwd(const float* dpool, const uint16_t* out, const uint16_t* y3, const uint16_t* yd,
-                          uint16_t* gpre, float* stats, int C, int N, int HW, int Ch, int NS, hipStream_t stream) {
+                          uint16_t* gpre, float* stats, int C, int N, int HW, int Ch, int NS, const int* nimg,
+                          hipStream_t stream) {
   hipLaunchKernelGGL(head_bwd_kernel<BF16>, dim3(C * N), dim3(Ch < 256 ? 64 * ((Ch + 63) / 64) : 256), 0, stream,
-                     dpool, out, y3, yd, gpre, stats, N, HW, Ch, NS);
+                     dpool, out, y3, yd, gpre, stats, N, HW, Ch, NS, nimg);
   return (int)hipGetLastError();
 }
 FA_EXPORT int fa_head_bwd_f32(const float* dpool, const float* out, const float* y3, const float* yd, float* gpre,
-                              float* stats, int C, int N, int HW, int Ch, int NS, hipStream_t stream) {
+                              float* stats, int C, int N, int HW, int Ch, int NS, const int* nimg, hipStream_t stream) {
   hipLaunchKernelGGL(head_bwd_kernel<F32>, dim3(C * N), dim3(Ch < 256 ? 64 * ((Ch + 63) / 64) : 256), 0, stream,
-                     dpool, out, y3, yd, gpre, stats, N, HW, Ch, NS);
+                     dpool, out, y3, yd, gpre, stats, N, HW, Ch, NS, nimg);
   return (int)hipGetLastError();
 }
 
@@ -262,5 +285,5 @@ FA_EXPORT int fa_nchw_to_nhwc_pad_f32(const float* x, float* y, int64_t CN, int 
 // ---- bn_relu_apply: out = relu(y·s + t) (stem activation materialisation)
 FA_EXPORT int fa_bn_relu_apply(const uint16_t* y, const float* s, const float* t, uint16_t* out, int C,
                                int64_t per_client, int Ch, hipStream_t stream) {
-  return fa_block_out(y, s, t, nullptr, nullptr, nullptr, out, C, per_client, Ch, stream);
+  return fa_block_out(y, s, t, nullptr, nullptr, nullptr, out, C, per_client, Ch, nullptr, 0, stream);
 }

@@ -27,7 +27,8 @@ __global__ __launch_bounds__(256) void conv1x1_wgrad_kernel(const typename P::T*
                                                             const typename P::T* __restrict__ x,
                                                             const float* __restrict__ ps, const float* __restrict__ pt,
                                                             float* __restrict__ garena, int64_t ldw, int64_t woff,
-                                                            int M, int pix_per_wg) {
+                                                            int M, int pix_per_wg, const int* __restrict__ nimg,
+                                                            int hw) {
   using T = typename P::T;
   using frag_t = typename P::frag_t;
   constexpr int V = P::VEC;
@@ -61,7 +62,8 @@ __global__ __launch_bounds__(256) void conv1x1_wgrad_kernel(const typename P::T*
   const T* yc = yv + (int64_t)c * M * COUT;
   const T* xc = x + (int64_t)c * M * CIN;
   const int p_begin = blockIdx.x * pix_per_wg;
-  const int p_end = min(M, p_begin + pix_per_wg);
+  const int p_end = min(nimg ? min(M, nimg[c] * hw) : M, p_begin + pix_per_wg);   // valid pixels of client c
+  if (p_begin >= p_end) return;
 
   uint4 rg[DI], ry[DI], rx[XI];
   auto load = [&](int p0) {
@@ -193,7 +195,7 @@ __global__ __launch_bounds__(256) void conv1x1_wgrad_kernel(const typename P::T*
 template <class P, int CIN, int COUT, int WM, int WN, int PT>
 static int launch(const void* g_, const void* yv_, const float* al, const float* be, const float* ga,
                   const void* x_, const float* ps, const float* pt, float* garena, int64_t ldw, int64_t woff, int C,
-                  int M, int pix_per_wg, hipStream_t stream) {
+                  int M, int pix_per_wg, const int* nimg, int hw, hipStream_t stream) {
   using T = typename P::T;
   const T* g = (const T*)g_;
   const T* yv = (const T*)yv_;
@@ -208,7 +210,7 @@ static int launch(const void* g_, const void* yv_, const float* al, const float*
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   const int gx = (M + pix_per_wg - 1) / pix_per_wg;
   hipLaunchKernelGGL(kern, dim3(gx, C), dim3(256), smem, stream, g, yv, al, be, ga, x, ps, pt, garena, ldw, woff, M,
-                     pix_per_wg);
+                     pix_per_wg, nimg, hw);
   return (int)hipGetLastError();
 }
 
@@ -219,11 +221,12 @@ static int launch(const void* g_, const void* yv_, const float* al, const float*
 template <class P>
 static int conv1x1_wgrad(const void* g, const void* yv, const float* alpha, const float* beta, const float* gamma,
                          const void* x, const float* ps, const float* pt, float* garena, int64_t ldw, int64_t woff,
-                         int C, int M, int Cin, int Cout, int pix_per_wg, hipStream_t stream) {
+                         int C, int M, int Cin, int Cout, int pix_per_wg, const int* nimg, int hw,
+                         hipStream_t stream) {
 #define C1(CI, CO, WM, WN, PT)                                                                                 \
   if (Cin == CI && Cout == CO)                                                                                 \
     return c1::launch<P, CI, CO, WM, WN, PT>(g, yv, alpha, beta, gamma, x, ps, pt, garena, ldw, woff, C, M,    \
-                                             pix_per_wg, stream);
+                                             pix_per_wg, nimg, hw, stream);
   C1(16, 64, 1, 1, 128)    // 4 tiles: 4 pixel groups
   C1(64, 16, 1, 1, 128)
   C1(16, 16, 1, 1, 128)
@@ -242,16 +245,16 @@ static int conv1x1_wgrad(const void* g, const void* yv, const float* alpha, cons
 FA_EXPORT int fa_conv1x1_wgrad(const uint16_t* g, const uint16_t* yv, const float* alpha, const float* beta,
                                const float* gamma, const uint16_t* x, const float* ps, const float* pt, float* garena,
                                int64_t ldw, int64_t woff, int C, int M, int Cin, int Cout, int pix_per_wg,
-                               hipStream_t stream) {
+                               const int* nimg, int hw, hipStream_t stream) {
   return conv1x1_wgrad<c1::BF16>(g, yv, alpha, beta, gamma, x, ps, pt, garena, ldw, woff, C, M, Cin, Cout, pix_per_wg,
-                                 stream);
+                                 nimg, hw, stream);
 }
 FA_EXPORT int fa_conv1x1_wgrad_f32(const float* g, const float* yv, const float* alpha, const float* beta,
                                    const float* gamma, const float* x, const float* ps, const float* pt, float* garena,
                                    int64_t ldw, int64_t woff, int C, int M, int Cin, int Cout, int pix_per_wg,
-                                   hipStream_t stream) {
+                                   const int* nimg, int hw, hipStream_t stream) {
   return conv1x1_wgrad<c1::F32>(g, yv, alpha, beta, gamma, x, ps, pt, garena, ldw, woff, C, M, Cin, Cout, pix_per_wg,
-                                stream);
+                                nimg, hw, stream);
 }
 
 // ============================================================================================
@@ -297,6 +300,8 @@ struct Args {             // activations are P::T (bf16 | fp32)
   int64_t ldw, woff;
   int M, pix_per_wg;
   float* part;            // optional [C][G][CO·CI + 3·CI] per-workgroup partials (no atomics)
+  const int* nimg;        // per-client valid images (null: all) and pixels per image
+  int hw;
 };
 
 enum { EPI_MASK = 2, EPI_BLOCK = 3 };
@@ -332,6 +337,9 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int g4 = lane >> 4;
   const int kgrp = wid / (WM * WN), mgrp = (wid % (WM * WN)) / WN, ngrp = wid % WN;
+  // workgroups past the client's valid pixels have nothing to add (the partial-sum mode still writes its
+  // zero partials below)
+  if (!a.part && (int)(blockIdx.x * a.pix_per_wg) >= (a.nimg ? min(a.M, a.nimg[c] * a.hw) : a.M)) return;
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* vv = reinterpret_cast<float*>(smem);                            // α β γ [CO], s t [CI]
@@ -359,6 +367,7 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
     for (int i = threadIdx.x; i < PT * (KP - CO); i += NT) dyL[(i / (KP - CO)) * LDD + CO + i % (KP - CO)] = 0;
 
   const int M = a.M;
+  const int Mc = a.nimg ? min(M, a.nimg[c] * a.hw) : M;   // this client's valid pixels
   const T* gc = reinterpret_cast<const T*>(a.g) + (int64_t)c * M * CO;
   const T* yc = reinterpret_cast<const T*>(a.y) + (int64_t)c * M * CO;
   const T* e_x = reinterpret_cast<const T*>(a.e_x);
@@ -368,7 +377,7 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
   T* outp = reinterpret_cast<T*>(a.out);
   const int64_t xbase = (int64_t)c * M * CI;
   const int p_begin = blockIdx.x * a.pix_per_wg;
-  const int p_end = min(M, p_begin + a.pix_per_wg);
+  const int p_end = min(Mc, p_begin + a.pix_per_wg);
   const int ci0 = (threadIdx.x % CGX) * V;  // this thread's channel chunk in every e_x-shaped pass
   const bool has_y2 = BLK && e_y2 != nullptr;
 
@@ -671,12 +680,12 @@ static int bwd_fused(const void* g, const void* y, const float* alpha, const flo
                      const void* wb, int64_t wb_ld, int ldk2, const void* e_x, const float* e_s, const float* e_t,
                      const void* e_add, const void* e_y1, const void* e_y2, void* out, float* stats, int NS,
                      float* garena, int64_t ldw, int64_t woff, int C, int M, int Cin, int Cout, int epi,
-                     int pix_per_wg, float* part, hipStream_t stream) {
+                     int pix_per_wg, float* part, const int* nimg, int hw, hipStream_t stream) {
   if (ldk2 != (Cout + 31) / 32 * 32 + 8 || pix_per_wg <= 0) return -3;
   if (epi == EPI_MASK && (!e_s || !e_t)) return -4;
   if (epi == EPI_BLOCK && (!e_add || !e_y1)) return -4;
   Args a{g, y, alpha, beta, gamma, wb, wb_ld, e_x, e_s, e_t, e_add, e_y1, e_y2, out, stats, NS, garena, ldw,
-         woff, M, pix_per_wg, part};
+         woff, M, pix_per_wg, part, nimg, hw};
 #define C1F(CI, CO, E, WM, WN, PT, NW) \
   if (Cin == CI && Cout == CO && epi == E) return launch<P, CI, CO, E, WM, WN, PT, NW>(a, C, stream);
   // conv2 of a bottleneck (planes → 4·planes): mask epilogue, BN-ReLU prologue on the wgrad operand
@@ -707,16 +716,18 @@ FA_EXPORT int fa_conv1x1_bwd_fused(const uint16_t* g, const uint16_t* y, const f
                                    const float* e_s, const float* e_t, const uint16_t* e_add, const uint16_t* e_y1,
                                    const uint16_t* e_y2, uint16_t* out, float* stats, int NS, float* garena,
                                    int64_t ldw, int64_t woff, int C, int M, int Cin, int Cout, int epi, int pix_per_wg,
-                                   float* part, hipStream_t stream) {
+                                   float* part, const int* nimg, int hw, hipStream_t stream) {
   return c1f::bwd_fused<c1f::BF16>(g, y, alpha, beta, gamma, wb, wb_ld, ldk2, e_x, e_s, e_t, e_add, e_y1, e_y2, out,
-                                   stats, NS, garena, ldw, woff, C, M, Cin, Cout, epi, pix_per_wg, part, stream);
+                                   stats, NS, garena, ldw, woff, C, M, Cin, Cout, epi, pix_per_wg, part, nimg, hw,
+                                   stream);
 }
 FA_EXPORT int fa_conv1x1_bwd_fused_f32(const float* g, const float* y, const float* alpha, const float* beta,
                                        const float* gamma, const float* wb, int64_t wb_ld, int ldk2, const float* e_x,
                                        const float* e_s, const float* e_t, const float* e_add, const float* e_y1,
                                        const float* e_y2, float* out, float* stats, int NS, float* garena,
                                        int64_t ldw, int64_t woff, int C, int M, int Cin, int Cout, int epi,
-                                       int pix_per_wg, float* part, hipStream_t stream) {
+                                       int pix_per_wg, float* part, const int* nimg, int hw, hipStream_t stream) {
   return c1f::bwd_fused<c1f::F32>(g, y, alpha, beta, gamma, wb, wb_ld, ldk2, e_x, e_s, e_t, e_add, e_y1, e_y2, out,
-                                  stats, NS, garena, ldw, woff, C, M, Cin, Cout, epi, pix_per_wg, part, stream);
+                                  stats, NS, garena, ldw, woff, C, M, Cin, Cout, epi, pix_per_wg, part, nimg, hw,
+                                  stream);
 }

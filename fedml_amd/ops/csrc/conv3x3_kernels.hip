@@ -205,6 +205,11 @@ __device__ __forceinline__ void unit_geom(int u, int N, int H, int R, int S, int
   }
 }
 
+// Valid images of client c (heterogeneous batches: images past nimg[c] are padding and never touched)
+// and the work units they span.
+__device__ __forceinline__ int client_images(const int* nimg, int c, int N) { return nimg ? min(N, nimg[c]) : N; }
+__device__ __forceinline__ int client_units(int Ne, int H, int R, int S) { return S > 1 ? (Ne + S - 1) / S : Ne * (H / R); }
+
 struct Args {              // tensors are P::T (bf16 | fp32) unless noted
   const void* src;       // x (forward) or g (backward-data)        [C][N][H][W][KC]
   const void* src2;      // y for XF_DY
@@ -219,6 +224,7 @@ struct Args {              // tensors are P::T (bf16 | fp32) unless noted
   const float* e_t;
   float* stats;          // [C][NOUT][NS]
   const float* pivot;    // EPI_FWD: per-(client, channel) shift subtracted from the stored output (or null)
+  const int* nimg;       // per-client valid images (null: all N) — heterogeneous client batches
   int NS;
   int N, H, W;                    // output (iteration) geometry
   int Hs, Ws;                     // A-operand source geometry (≠ H, W for stride 2)
@@ -255,6 +261,10 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
   constexpr int SP = (!BWD && ST == 2) ? 2 : 1;   // source-pixel step per output pixel
   constexpr bool UPS = BWD && ST == 2;
   const int TW = (UPS ? W : Ws) + 2;             // tile width incl. halo
+  const int Ne = client_images(a.nimg, c, a.N);
+  const int u_lo = blockIdx.x * a.units_per_wg;
+  const int u_hi = min(client_units(Ne, H, a.R, a.S), u_lo + a.units_per_wg);
+  if (u_lo >= u_hi) return;   // no valid images in this workgroup's units (uniform: whole workgroup)
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* wl = reinterpret_cast<T*>(smem);                                             // [NOUT][ldk]
@@ -327,24 +337,22 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
 
   const int R = a.R, RW = R * W;
   const int TR = SP == 2 ? 2 * R + 1 : R + 2;    // tile rows incl. halo
-  const int u_lo = blockIdx.x * a.units_per_wg;
-  const int u_hi = min(a.units, u_lo + a.units_per_wg);
   TileLoader<P, KC, XF, UPS, MAXC> ld;
-  if (u_lo < u_hi) {
+  {
     int img0, ns, r0;
-    unit_geom(u_lo, a.N, H, R, a.S, img0, ns, r0);
+    unit_geom(u_lo, Ne, H, R, a.S, img0, ns, r0);
     ld.load(src, src2, img0, ns, SP * r0 - 1, TR, TW, a.fd_trtw, a.fd_tw, Hs, Ws);
   }
   for (int u = u_lo; u < u_hi; ++u) {
     int img0, ns, r0;
-    unit_geom(u, a.N, H, R, a.S, img0, ns, r0);
+    unit_geom(u, Ne, H, R, a.S, img0, ns, r0);
     const int64_t pix0 = (int64_t)img0 * HW + (int64_t)r0 * W;  // first output pixel of the unit
     __syncthreads();  // previous unit fully consumed
     ld.store(tile, cvec);
     __syncthreads();
     if (u + 1 < u_hi) {  // next unit's global reads in flight during this unit's MFMAs
       int img1, ns1, r1;
-      unit_geom(u + 1, a.N, H, R, a.S, img1, ns1, r1);
+      unit_geom(u + 1, Ne, H, R, a.S, img1, ns1, r1);
       ld.load(src, src2, img1, ns1, SP * r1 - 1, TR, TW, a.fd_trtw, a.fd_tw, Hs, Ws);
     }
     const int P_ = ns * RW;
@@ -473,6 +481,7 @@ struct WArgs {           // activations are P::T
   const float* ps;
   const float* pt;
   float* dw;              // GEMM-layout scratch [C][COUT][9·CIN]
+  const int* nimg;        // per-client valid images (null: all N)
   int N, H, W;            // dy (output) geometry
   int Hs, Ws;             // x (input) geometry
   int R, S, units, units_per_wg;
@@ -499,6 +508,10 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WArgs a) {
   const int nt_lo = blockIdx.z * a.nt_per_z;
   const int nt_hi = min(K / 16, nt_lo + a.nt_per_z);
   const int my_nt0 = nt_lo + ngrp * TPW;  // this wave's column tiles [my_nt0, my_nt0 + TPW) ∩ [.., nt_hi)
+  const int Ne = client_images(a.nimg, c, a.N);
+  const int u_lo = blockIdx.x * a.units_per_wg;
+  const int u_hi = min(client_units(Ne, H, a.R, a.S), u_lo + a.units_per_wg);
+  if (u_lo >= u_hi) return;   // nothing to add (uniform: whole workgroup)
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* vv = reinterpret_cast<float*>(smem);                          // α β γ [COUT], s t [CIN]
@@ -527,8 +540,6 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WArgs a) {
   const T* xc = reinterpret_cast<const T*>(a.x) + (int64_t)c * a.N * Hs * Ws * CIN;
   const int R = a.R, RW = R * W;
   const int TR = ST == 2 ? 2 * R + 1 : R + 2;
-  const int u_lo = blockIdx.x * a.units_per_wg;
-  const int u_hi = min(a.units, u_lo + a.units_per_wg);
 
   constexpr int CGD = COUT / P::VEC;
   static_assert(256 % CGD == 0, "fixed chunk per thread");
@@ -539,22 +550,22 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WArgs a) {
   xvec.load(vv + 3 * COUT, vv + 3 * COUT + CIN, nullptr, (threadIdx.x % (CIN / P::VEC)) * P::VEC);
   TileLoader<P, CIN, PRO ? XF_BNRELU : XF_NONE, 0, MAXC, true> xld;
   DyLoader<P, COUT, MAXD> dld;
-  if (u_lo < u_hi) {
+  {
     int img0, ns, r0;
-    unit_geom(u_lo, a.N, H, R, a.S, img0, ns, r0);
+    unit_geom(u_lo, Ne, H, R, a.S, img0, ns, r0);
     dld.load(gc, yc, (int64_t)img0 * HW + (int64_t)r0 * W, ns * RW);
     xld.load(xc, nullptr, img0, ns, ST * r0 - 1, TR, TW, a.fd_trtw, a.fd_tw, Hs, Ws);
   }
   for (int u = u_lo; u < u_hi; ++u) {
     int img0, ns, r0;
-    unit_geom(u, a.N, H, R, a.S, img0, ns, r0);
+    unit_geom(u, Ne, H, R, a.S, img0, ns, r0);
     __syncthreads();
     dld.store(dyL, dvec);  // dy = α·g + β·y + γ, natural [pixel][co] (no halo)
     xld.store(xt, xvec);
     __syncthreads();
     if (u + 1 < u_hi) {
       int img1, ns1, r1;
-      unit_geom(u + 1, a.N, H, R, a.S, img1, ns1, r1);
+      unit_geom(u + 1, Ne, H, R, a.S, img1, ns1, r1);
       dld.load(gc, yc, (int64_t)img1 * HW + (int64_t)r1 * W, ns1 * RW);
       xld.load(xc, nullptr, img1, ns1, ST * r1 - 1, TR, TW, a.fd_trtw, a.fd_tw, Hs, Ws);
     }
@@ -738,11 +749,11 @@ static int dispatch_gemm(int kc, int nout, const Args& a, int C, hipStream_t s) 
 template <class P>
 static int conv3x3_fwd(const void* x, const void* wpk, int64_t wpk_ld, const float* pscale, const float* pshift,
                        void* y, float* stats, int C, int N, int H, int W, int Cin, int Cout, int ldk, int stride,
-                       const float* pivot, hipStream_t stream) {
+                       const float* pivot, const int* nimg, hipStream_t stream) {
   if ((stride != 1 && stride != 2) || H % stride || W % stride || (W / stride) % 8 != 0) return -3;
   Args a = {};
   a.src = x; a.wpk = wpk; a.wpk_ld = wpk_ld; a.vec0 = pscale; a.vec1 = pshift; a.out = y; a.stats = stats; a.NS = 2;
-  a.pivot = pivot;
+  a.pivot = pivot; a.nimg = nimg;
   a.N = N; a.H = H / stride; a.W = W / stride; a.Hs = H; a.Ws = W; a.ldk = ldk;
   if (stride == 2) {
     if (pscale) return dispatch_gemm<P, XF_BNRELU, 0, EPI_FWD, 2>(Cin, Cout, a, C, stream);
@@ -756,11 +767,11 @@ template <class P>
 static int conv3x3_bwd_data(const void* g, const void* yv, const float* alpha, const float* beta, const float* gamma,
                             const void* wpk_b, int64_t wpk_ld, void* dx, const void* e_x, const float* e_s,
                             const float* e_t, float* stats, int C, int N, int Hx, int Wx, int Cout, int Cin, int ldk2,
-                            int stride, hipStream_t stream) {
+                            int stride, const int* nimg, hipStream_t stream) {
   if ((stride != 1 && stride != 2) || Hx % stride || Wx % stride || Wx % 8 != 0) return -3;
   Args a = {};
   a.src = g; a.src2 = yv; a.wpk = wpk_b; a.wpk_ld = wpk_ld; a.vec0 = alpha; a.vec1 = beta; a.vec2 = gamma;
-  a.out = dx; a.e_x = e_x; a.e_s = e_s; a.e_t = e_t; a.stats = stats; a.NS = 3;
+  a.out = dx; a.e_x = e_x; a.e_s = e_s; a.e_t = e_t; a.stats = stats; a.NS = 3; a.nimg = nimg;
   a.N = N; a.H = Hx; a.W = Wx; a.Hs = Hx / stride; a.Ws = Wx / stride; a.ldk = ldk2;
   if (stride == 2) return dispatch_gemm<P, XF_DY, 1, EPI_MASK, 2>(Cout, Cin, a, C, stream);
   return dispatch_gemm<P, XF_DY, 1, EPI_MASK, 1>(Cout, Cin, a, C, stream);
@@ -769,12 +780,13 @@ static int conv3x3_bwd_data(const void* g, const void* yv, const float* alpha, c
 template <class P>
 static int conv3x3_wgrad(const void* g, const void* yv, const float* alpha, const float* beta, const float* gamma,
                          const void* x, const float* ps, const float* pt, float* dw, int C, int N, int H, int W,
-                         int Cin, int Cout, int stride, hipStream_t stream) {
+                         int Cin, int Cout, int stride, const int* nimg, hipStream_t stream) {
   if ((stride != 1 && stride != 2) || H % stride || W % stride || Cin != Cout) return -3;
   const int Ho = H / stride, Wo = W / stride;
   if (Wo % 8 != 0 || (Ho * Wo) % 32 != 0) return -3;
   WArgs a = {};
   a.g = g; a.yv = yv; a.alpha = alpha; a.beta = beta; a.gamma = gamma; a.x = x; a.ps = ps; a.pt = pt; a.dw = dw;
+  a.nimg = nimg;
   a.N = N; a.H = Ho; a.W = Wo; a.Hs = H; a.Ws = W;
   // units sized so one unit's operands fit the loaders' register budget (x tile ≤ 8, dy ≤ 4 chunks/thread)
   int tpx = Cin >= 64 ? (stride == 2 ? 64 : 128) : (stride == 2 ? 128 : 256);
@@ -844,15 +856,17 @@ static int conv3x3_wgrad(const void* g, const void* yv, const float* alpha, cons
 // `_f32`: fp32 activations / packed weights.
 FA_EXPORT int fa_conv3x3_fwd(const uint16_t* x, const uint16_t* wpk, int64_t wpk_ld, const float* pscale,
                              const float* pshift, uint16_t* y, float* stats, int C, int N, int H, int W, int Cin,
-                             int Cout, int ldk, int stride, const float* pivot, hipStream_t stream) {
+                             int Cout, int ldk, int stride, const float* pivot, const int* nimg,
+                             hipStream_t stream) {
   return c3::conv3x3_fwd<c3::BF16>(x, wpk, wpk_ld, pscale, pshift, y, stats, C, N, H, W, Cin, Cout, ldk, stride,
-                                   pivot, stream);
+                                   pivot, nimg, stream);
 }
 FA_EXPORT int fa_conv3x3_fwd_f32(const float* x, const float* wpk, int64_t wpk_ld, const float* pscale,
                                  const float* pshift, float* y, float* stats, int C, int N, int H, int W, int Cin,
-                                 int Cout, int ldk, int stride, const float* pivot, hipStream_t stream) {
+                                 int Cout, int ldk, int stride, const float* pivot, const int* nimg,
+                                 hipStream_t stream) {
   return c3::conv3x3_fwd<c3::F32>(x, wpk, wpk_ld, pscale, pshift, y, stats, C, N, H, W, Cin, Cout, ldk, stride,
-                                  pivot, stream);
+                                  pivot, nimg, stream);
 }
 
 // backward-data 3×3 / pad 1 / stride 1|2 with the ReLU-mask epilogue (EPI_MASK of the generic kernel):
@@ -861,16 +875,18 @@ FA_EXPORT int fa_conv3x3_fwd_f32(const float* x, const float* wpk, int64_t wpk_l
 FA_EXPORT int fa_conv3x3_bwd_data(const uint16_t* g, const uint16_t* yv, const float* alpha, const float* beta,
                                   const float* gamma, const uint16_t* wpk_b, int64_t wpk_ld, uint16_t* dx,
                                   const uint16_t* e_x, const float* e_s, const float* e_t, float* stats, int C, int N,
-                                  int Hx, int Wx, int Cout, int Cin, int ldk2, int stride, hipStream_t stream) {
+                                  int Hx, int Wx, int Cout, int Cin, int ldk2, int stride, const int* nimg,
+                                  hipStream_t stream) {
   return c3::conv3x3_bwd_data<c3::BF16>(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, dx, e_x, e_s, e_t, stats, C, N, Hx,
-                                        Wx, Cout, Cin, ldk2, stride, stream);
+                                        Wx, Cout, Cin, ldk2, stride, nimg, stream);
 }
 FA_EXPORT int fa_conv3x3_bwd_data_f32(const float* g, const float* yv, const float* alpha, const float* beta,
                                       const float* gamma, const float* wpk_b, int64_t wpk_ld, float* dx,
                                       const float* e_x, const float* e_s, const float* e_t, float* stats, int C, int N,
-                                      int Hx, int Wx, int Cout, int Cin, int ldk2, int stride, hipStream_t stream) {
+                                      int Hx, int Wx, int Cout, int Cin, int ldk2, int stride, const int* nimg,
+                                      hipStream_t stream) {
   return c3::conv3x3_bwd_data<c3::F32>(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, dx, e_x, e_s, e_t, stats, C, N, Hx,
-                                       Wx, Cout, Cin, ldk2, stride, stream);
+                                       Wx, Cout, Cin, ldk2, stride, nimg, stream);
 }
 
 // weight gradient 3×3 / pad 1 / stride 1|2 into the GEMM-layout scratch `dw` [C][Cout][9·Cin] (zero
@@ -878,11 +894,15 @@ FA_EXPORT int fa_conv3x3_bwd_data_f32(const float* g, const float* yv, const flo
 // (H, W) = input (x) resolution.
 FA_EXPORT int fa_conv3x3_wgrad(const uint16_t* g, const uint16_t* yv, const float* alpha, const float* beta,
                                const float* gamma, const uint16_t* x, const float* ps, const float* pt, float* dw,
-                               int C, int N, int H, int W, int Cin, int Cout, int stride, hipStream_t stream) {
-  return c3::conv3x3_wgrad<c3::BF16>(g, yv, alpha, beta, gamma, x, ps, pt, dw, C, N, H, W, Cin, Cout, stride, stream);
+                               int C, int N, int H, int W, int Cin, int Cout, int stride, const int* nimg,
+                               hipStream_t stream) {
+  return c3::conv3x3_wgrad<c3::BF16>(g, yv, alpha, beta, gamma, x, ps, pt, dw, C, N, H, W, Cin, Cout, stride, nimg,
+                                     stream);
 }
 FA_EXPORT int fa_conv3x3_wgrad_f32(const float* g, const float* yv, const float* alpha, const float* beta,
                                    const float* gamma, const float* x, const float* ps, const float* pt, float* dw,
-                                   int C, int N, int H, int W, int Cin, int Cout, int stride, hipStream_t stream) {
-  return c3::conv3x3_wgrad<c3::F32>(g, yv, alpha, beta, gamma, x, ps, pt, dw, C, N, H, W, Cin, Cout, stride, stream);
+                                   int C, int N, int H, int W, int Cin, int Cout, int stride, const int* nimg,
+                                   hipStream_t stream) {
+  return c3::conv3x3_wgrad<c3::F32>(g, yv, alpha, beta, gamma, x, ps, pt, dw, C, N, H, W, Cin, Cout, stride, nimg,
+                                    stream);
 }

@@ -123,6 +123,7 @@ struct ConvArgs {        // activations / packed weights are P::T (bf16 | fp32)
   const void* e_y2;      // EPI_BLOCK: previous block's downsample-bn input (optional)
   float* stats;          // [C][NOUT][NS]
   const float* pivot;    // EPI_FWD: per-(client, channel) shift subtracted from the stored output (or null)
+  const int* nimg;       // per-client valid images (null: all Nb) — heterogeneous client batches
   int NS;
   int Nb, Hs, Ws, KC;    // source geometry (KC = channels of the A source = GEMM K per tap)
   int Ho, Wo;            // output geometry
@@ -146,6 +147,9 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
   const int wid = threadIdx.x >> 6;
   const int K = a.KH * a.KW * a.KC;
   const int M = a.Nb * a.Ho * a.Wo;
+  // this client's valid output pixels: images past nimg[c] are padding (never read or written)
+  const int Mv = a.nimg ? min(M, a.nimg[c] * a.Ho * a.Wo) : M;
+  if ((int)(blockIdx.x * 4 * a.tiles_per_wave) * 16 >= Mv) return;   // uniform: whole workgroup idle
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* wl = reinterpret_cast<T*>(smem);                                            // [NOUT][ldk]
@@ -191,13 +195,13 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
   for (int j = 0; j < V; ++j) { st0[j] = 0.f; st1[j] = 0.f; st2[j] = 0.f; }
   const int my_cg = lane % CG;
 
-  const int tiles_total = (M + 15) / 16;
+  const int tiles_total = (Mv + 15) / 16;
   const int tile0 = (blockIdx.x * 4 + wid) * a.tiles_per_wave;
   for (int tt = 0; tt < a.tiles_per_wave; ++tt) {
     const int tile = tile0 + tt;
     if (tile >= tiles_total) break;
     const int m = tile * 16 + (lane & 15);
-    const bool mvalid = m < M;
+    const bool mvalid = m < Mv;
     const int mm = mvalid ? m : 0;
     const int on = mm / (a.Ho * a.Wo);
     const int orem = mm % (a.Ho * a.Wo);
@@ -262,7 +266,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
     __builtin_amdgcn_wave_barrier();
 
     // ---- vectorised epilogue: each lane handles V channels of one row per pass ----
-    const int rows_valid = min(16, M - tile * 16);
+    const int rows_valid = min(16, Mv - tile * 16);
 #pragma unroll
     for (int pass = 0; pass < (16 + ROWS_PER_PASS - 1) / ROWS_PER_PASS; ++pass) {
       const int row = pass * ROWS_PER_PASS + lane / CG;
@@ -393,11 +397,12 @@ static int dispatch_nt(int nout, const ConvArgs& a, int C, hipStream_t s) {
 template <class P>
 static int conv_fwd(const void* x, const void* wpk, int64_t wpk_ld, const float* pscale, const float* pshift, void* y,
                     float* stats, int C, int Nb, int H, int W, int Cin, int Cout, int KH, int KW, int stride, int pad,
-                    int Ho, int Wo, int ldk, int tiles_per_wave, const float* pivot, hipStream_t stream) {
+                    int Ho, int Wo, int ldk, int tiles_per_wave, const float* pivot, const int* nimg,
+                    hipStream_t stream) {
   if (Cin % 8 != 0) return -3;
   ConvArgs a = {};
   a.src = x; a.wpk = wpk; a.wpk_ld = wpk_ld; a.vec0 = pscale; a.vec1 = pshift; a.out = y; a.stats = stats; a.NS = 2;
-  a.pivot = pivot;
+  a.pivot = pivot; a.nimg = nimg;
   a.Nb = Nb; a.Hs = H; a.Ws = W; a.KC = Cin; a.Ho = Ho; a.Wo = Wo; a.KH = KH; a.KW = KW; a.stride = stride;
   a.pad = pad; a.ldk = ldk; a.Kp = (KH * KW * Cin + 31) / 32 * 32; a.tiles_per_wave = tiles_per_wave;
   if (pscale)
@@ -410,9 +415,10 @@ static int conv_bwd_data(const void* g, const void* yv, const float* alpha, cons
                          const void* wpk_b, int64_t wpk_ld, void* dx, int epi, const void* e_x, const float* e_s,
                          const float* e_t, const void* e_add, const void* e_y1, const void* e_y2, float* stats, int C,
                          int Nb, int Hy, int Wy, int Cout, int Cin, int KH, int KW, int stride, int pad, int Hx, int Wx,
-                         int ldk2, int tiles_per_wave, hipStream_t stream) {
+                         int ldk2, int tiles_per_wave, const int* nimg, hipStream_t stream) {
   if (Cout % 8 != 0) return -3;
   ConvArgs a = {};
+  a.nimg = nimg;
   a.src = g; a.src2 = yv; a.wpk = wpk_b; a.wpk_ld = wpk_ld; a.vec0 = alpha; a.vec1 = beta; a.vec2 = gamma;
   a.out = dx; a.e_x = e_x; a.e_s = e_s; a.e_t = e_t; a.e_add = e_add; a.e_y1 = e_y1; a.e_y2 = e_y2;
   a.stats = stats; a.NS = 3;  // backward statistics are always laid out [C][Ch][3]
@@ -431,16 +437,16 @@ static int conv_bwd_data(const void* g, const void* yv, const float* alpha, cons
 FA_EXPORT int fa_conv_fwd(const uint16_t* x, const uint16_t* wpk, int64_t wpk_ld, const float* pscale,
                           const float* pshift, uint16_t* y, float* stats, int C, int Nb, int H, int W, int Cin,
                           int Cout, int KH, int KW, int stride, int pad, int Ho, int Wo, int ldk, int tiles_per_wave,
-                          const float* pivot, hipStream_t stream) {
+                          const float* pivot, const int* nimg, hipStream_t stream) {
   return conv_fwd<BF16>(x, wpk, wpk_ld, pscale, pshift, y, stats, C, Nb, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo,
-                        ldk, tiles_per_wave, pivot, stream);
+                        ldk, tiles_per_wave, pivot, nimg, stream);
 }
 FA_EXPORT int fa_conv_fwd_f32(const float* x, const float* wpk, int64_t wpk_ld, const float* pscale,
                               const float* pshift, float* y, float* stats, int C, int Nb, int H, int W, int Cin,
                               int Cout, int KH, int KW, int stride, int pad, int Ho, int Wo, int ldk,
-                              int tiles_per_wave, const float* pivot, hipStream_t stream) {
+                              int tiles_per_wave, const float* pivot, const int* nimg, hipStream_t stream) {
   return conv_fwd<F32>(x, wpk, wpk_ld, pscale, pshift, y, stats, C, Nb, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo,
-                       ldk, tiles_per_wave, pivot, stream);
+                       ldk, tiles_per_wave, pivot, nimg, stream);
 }
 
 // backward-data: dx = convᵀ(α·g + β·y + γ) with epilogue
@@ -452,16 +458,18 @@ FA_EXPORT int fa_conv_bwd_data(const uint16_t* g, const uint16_t* yv, const floa
                                const uint16_t* e_x, const float* e_s, const float* e_t, const uint16_t* e_add,
                                const uint16_t* e_y1, const uint16_t* e_y2, float* stats, int C, int Nb, int Hy,
                                int Wy, int Cout, int Cin, int KH, int KW, int stride, int pad, int Hx, int Wx,
-                               int ldk2, int tiles_per_wave, hipStream_t stream) {
+                               int ldk2, int tiles_per_wave, const int* nimg, hipStream_t stream) {
   return conv_bwd_data<BF16>(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, dx, epi, e_x, e_s, e_t, e_add, e_y1, e_y2,
-                             stats, C, Nb, Hy, Wy, Cout, Cin, KH, KW, stride, pad, Hx, Wx, ldk2, tiles_per_wave, stream);
+                             stats, C, Nb, Hy, Wy, Cout, Cin, KH, KW, stride, pad, Hx, Wx, ldk2, tiles_per_wave, nimg,
+                             stream);
 }
 FA_EXPORT int fa_conv_bwd_data_f32(const float* g, const float* yv, const float* alpha, const float* beta,
                                    const float* gamma, const float* wpk_b, int64_t wpk_ld, float* dx, int epi,
                                    const float* e_x, const float* e_s, const float* e_t, const float* e_add,
                                    const float* e_y1, const float* e_y2, float* stats, int C, int Nb, int Hy,
                                    int Wy, int Cout, int Cin, int KH, int KW, int stride, int pad, int Hx, int Wx,
-                                   int ldk2, int tiles_per_wave, hipStream_t stream) {
+                                   int ldk2, int tiles_per_wave, const int* nimg, hipStream_t stream) {
   return conv_bwd_data<F32>(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, dx, epi, e_x, e_s, e_t, e_add, e_y1, e_y2,
-                            stats, C, Nb, Hy, Wy, Cout, Cin, KH, KW, stride, pad, Hx, Wx, ldk2, tiles_per_wave, stream);
+                            stats, C, Nb, Hy, Wy, Cout, Cin, KH, KW, stride, pad, Hx, Wx, ldk2, tiles_per_wave, nimg,
+                            stream);
 }

@@ -31,7 +31,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_tr_kernel(
     const typename P::T* __restrict__ g, const typename P::T* __restrict__ yv, const float* __restrict__ alpha,
     const float* __restrict__ beta, const float* __restrict__ gamma, const typename P::T* __restrict__ x,
     const float* __restrict__ ps, const float* __restrict__ pt, float* __restrict__ dw, int Nb, int H, int W,
-    int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int pix_per_wg, int nt_per_z) {
+    int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int pix_per_wg, int nt_per_z,
+    const int* __restrict__ nimg) {
   using T = typename P::T;
   const bool PRO = ps != nullptr;   // runtime flag: halves the instantiations (uniform branch)
   using frag_t = typename P::frag_t;
@@ -41,6 +42,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_tr_kernel(
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int K = KH * KW * Cin;
+  // this client's valid output pixels (images past nimg[c] are padding)
+  const int Mv = nimg ? min(Nb * Ho * Wo, nimg[c] * Ho * Wo) : Nb * Ho * Wo;
+  if ((int)(blockIdx.x * pix_per_wg) >= Mv) return;   // uniform: whole workgroup idle
   const int NT2 = (K + 15) / 16;
   const int nt_lo = blockIdx.z * nt_per_z;
   const int nt_hi = min(NT2, nt_lo + nt_per_z);
@@ -79,7 +83,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_tr_kernel(
   const T* yc = yv + (int64_t)c * M * Cout;
   const T* xc = x + (int64_t)c * Nb * H * W * Cin;
   const int p_begin = blockIdx.x * pix_per_wg;
-  const int p_end = min(M, p_begin + pix_per_wg);
+  const int p_end = min(Mv, p_begin + pix_per_wg);
   const int cg = Cout / V, kg = (k_hi - k_lo) / V;
   const int n_dy = PT * cg, n_a = PT * kg;
   __syncthreads();
@@ -220,7 +224,7 @@ static int conv_wgrad(const typename P::T* g, const typename P::T* yv, const flo
                       const float* gamma, const typename P::T* x, const float* ps, const float* pt, float* garena,
                       int64_t ldw, int64_t woff, int C, int Nb, int H, int W, int Cin, int Ho, int Wo, int Cout,
                       int KH, int KW, int stride, int pad, int pix_per_wg, int cin_src, float* dw,
-                      hipStream_t stream) {
+                      const int* nimg, hipStream_t stream) {
   constexpr int V = P::VEC;
   constexpr int PT = P::kF32 ? 32 : 64;
   if (Cin % 8 != 0 || Cout % 16 != 0 || Cout > 256) return -3;
@@ -244,7 +248,7 @@ static int conv_wgrad(const typename P::T* g, const typename P::T* yv, const flo
   auto go = [&](auto kern) {
     if (smem > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     hipLaunchKernelGGL(kern, grid, dim3(256), smem, stream, g, yv, alpha, beta, gamma, x, ps, pt, dw, Nb, H, W, Cin,
-                       Ho, Wo, Cout, KH, KW, stride, pad, pix_per_wg, nt_per_z);
+                       Ho, Wo, Cout, KH, KW, stride, pad, pix_per_wg, nt_per_z, nimg);
   };
   // instantiated register budgets: dy chunks/thread D ∈ {2, 8}, A chunks/thread ∈ {2, 4, 8, 16}
   auto by_a = [&](auto tpw_c, auto d_c) {
@@ -270,17 +274,17 @@ FA_EXPORT int fa_conv_wgrad(const uint16_t* g, const uint16_t* yv, const float* 
                             const float* gamma, const uint16_t* x, const float* ps, const float* pt, float* garena,
                             int64_t ldw, int64_t woff, int C, int Nb, int H, int W, int Cin, int Ho, int Wo, int Cout,
                             int KH, int KW, int stride, int pad, int pix_per_wg, int cin_src, float* dw,
-                            hipStream_t stream) {
+                            const int* nimg, hipStream_t stream) {
   return conv_wgrad<BF16>(g, yv, alpha, beta, gamma, x, ps, pt, garena, ldw, woff, C, Nb, H, W, Cin, Ho, Wo, Cout, KH,
-                          KW, stride, pad, pix_per_wg, cin_src, dw, stream);
+                          KW, stride, pad, pix_per_wg, cin_src, dw, nimg, stream);
 }
 FA_EXPORT int fa_conv_wgrad_f32(const float* g, const float* yv, const float* alpha, const float* beta,
                                 const float* gamma, const float* x, const float* ps, const float* pt, float* garena,
                                 int64_t ldw, int64_t woff, int C, int Nb, int H, int W, int Cin, int Ho, int Wo,
                                 int Cout, int KH, int KW, int stride, int pad, int pix_per_wg, int cin_src, float* dw,
-                                hipStream_t stream) {
+                                const int* nimg, hipStream_t stream) {
   return conv_wgrad<F32>(g, yv, alpha, beta, gamma, x, ps, pt, garena, ldw, woff, C, Nb, H, W, Cin, Ho, Wo, Cout, KH,
-                         KW, stride, pad, pix_per_wg, cin_src, dw, stream);
+                         KW, stride, pad, pix_per_wg, cin_src, dw, nimg, stream);
 }
 
 // scatter a GEMM-layout dW scratch [C][Cout][taps·Cin] into the OIHW arena (+=) and clear it

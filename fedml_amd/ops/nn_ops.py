@@ -43,11 +43,11 @@ def pack_weights(arena, segs_dev, nseg, dst, dst_ld, C):
 
 
 def conv_fwd(x, wpk, wpk_ld, pscale, pshift, y, stats, C, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, ldk,
-             tiles_per_wave, pivot=None):
+             tiles_per_wave, pivot=None, nimg=None):
     """y = conv(pro(x)) − pivot (per client and output channel; None → 0), BN statistics of y."""
     rc = _fnp("fa_conv_fwd", x)(_p(x), _p(wpk), _i64(wpk_ld), _p(pscale), _p(pshift), _p(y), _p(stats), _i(C), _i(N),
                             _i(H), _i(W), _i(Cin), _i(Cout), _i(KH), _i(KW), _i(stride), _i(pad), _i(Ho), _i(Wo),
-                            _i(ldk), _i(tiles_per_wave), _p(pivot), _stream(x))
+                            _i(ldk), _i(tiles_per_wave), _p(pivot), _p(nimg), _stream(x))
     _check(rc, "fa_conv_fwd")
 
 
@@ -55,21 +55,21 @@ EPI_STORE, EPI_MASK, EPI_BLOCK = 1, 2, 3
 
 
 def conv_bwd_data(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, dx, epi, e_x, e_s, e_t, e_add, e_y1, e_y2, stats, C, N,
-                  Hy, Wy, Cout, Cin, KH, KW, stride, pad, Hx, Wx, ldk2, tiles_per_wave):
+                  Hy, Wy, Cout, Cin, KH, KW, stride, pad, Hx, Wx, ldk2, tiles_per_wave, nimg=None):
     rc = _fnp("fa_conv_bwd_data", g)(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(wpk_b), _i64(wpk_ld), _p(dx),
                                  _i(epi), _p(e_x), _p(e_s), _p(e_t), _p(e_add), _p(e_y1), _p(e_y2), _p(stats), _i(C),
                                  _i(N), _i(Hy), _i(Wy), _i(Cout), _i(Cin), _i(KH), _i(KW), _i(stride), _i(pad),
-                                 _i(Hx), _i(Wx), _i(ldk2), _i(tiles_per_wave), _stream(g))
+                                 _i(Hx), _i(Wx), _i(ldk2), _i(tiles_per_wave), _p(nimg), _stream(g))
     _check(rc, "fa_conv_bwd_data")
 
 
 def conv_wgrad(g, yv, alpha, beta, gamma, x, ps, pt, garena, woff, C, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
-               pad, pix_per_wg, cin_src, dw_scratch):
+               pad, pix_per_wg, cin_src, dw_scratch, nimg=None):
     """``dw_scratch``: ≥ C·Cout·KH·KW·Cin fp32, zero on entry; the kernel leaves it zeroed."""
     rc = _fnp("fa_conv_wgrad", g)(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(x), _p(ps), _p(pt), _p(garena),
                               _i64(garena.stride(0)), _i64(woff), _i(C), _i(N), _i(H), _i(W), _i(Cin), _i(Ho), _i(Wo),
                               _i(Cout), _i(KH), _i(KW), _i(stride), _i(pad), _i(pix_per_wg), _i(cin_src),
-                              _p(dw_scratch), _stream(g))
+                              _p(dw_scratch), _p(nimg), _stream(g))
     _check(rc, "fa_conv_wgrad")
 
 
@@ -84,28 +84,30 @@ def conv3x3_supported(cin, cout, k, stride, pad, H, W):
     return Wo % 8 == 0 and W % 8 == 0 and (Ho * Wo) % 32 == 0
 
 
-def conv3x3_fwd(x, wpk, wpk_ld, pscale, pshift, y, stats, C, N, H, W, Cin, Cout, ldk, stride=1, pivot=None):
+def conv3x3_fwd(x, wpk, wpk_ld, pscale, pshift, y, stats, C, N, H, W, Cin, Cout, ldk, stride=1, pivot=None,
+                nimg=None):
     rc = _fnp("fa_conv3x3_fwd", x)(_p(x), _p(wpk), _i64(wpk_ld), _p(pscale), _p(pshift), _p(y), _p(stats), _i(C), _i(N),
-                               _i(H), _i(W), _i(Cin), _i(Cout), _i(ldk), _i(stride), _p(pivot), _stream(x))
+                               _i(H), _i(W), _i(Cin), _i(Cout), _i(ldk), _i(stride), _p(pivot), _p(nimg), _stream(x))
     _check(rc, "fa_conv3x3_fwd")
 
 
 def conv3x3_bwd_data(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, dx, e_x, e_s, e_t, stats, C, N, H, W, Cout, Cin,
-                     ldk2, stride=1):
+                     ldk2, stride=1, nimg=None):
     """(H, W) = dx (input) resolution."""
     rc = _fnp("fa_conv3x3_bwd_data", g)(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(wpk_b), _i64(wpk_ld), _p(dx),
                                     _p(e_x), _p(e_s), _p(e_t), _p(stats), _i(C), _i(N), _i(H), _i(W), _i(Cout), _i(Cin),
-                                    _i(ldk2), _i(stride), _stream(g))
+                                    _i(ldk2), _i(stride), _p(nimg), _stream(g))
     _check(rc, "fa_conv3x3_bwd_data")
 
 
 def conv3x3_wgrad(g, yv, alpha, beta, gamma, x, ps, pt, garena, woff, C, N, H, W, Cin, Cout, cin_src, dw_scratch,
-                  stride=1, scatter=True):
+                  stride=1, scatter=True, nimg=None):
     """Weight gradient into the GEMM-layout scratch, then scattered (+=) into the OIHW arena
     (``scatter=False``: left in the scratch for :func:`wgrad_scatter_multi`). (H, W) = input (x)
     resolution."""
     rc = _fnp("fa_conv3x3_wgrad", g)(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(x), _p(ps), _p(pt),
-                                 _p(dw_scratch), _i(C), _i(N), _i(H), _i(W), _i(Cin), _i(Cout), _i(stride), _stream(g))
+                                 _p(dw_scratch), _i(C), _i(N), _i(H), _i(W), _i(Cin), _i(Cout), _i(stride), _p(nimg),
+                                 _stream(g))
     _check(rc, "fa_conv3x3_wgrad")
     if not scatter:
         return
@@ -136,11 +138,11 @@ def conv1x1_wgrad_supported(cin, cout, k, stride, pad):
     return k == 1 and stride == 1 and pad == 0 and (cin, cout) in _C1_SHAPES
 
 
-def conv1x1_wgrad(g, yv, alpha, beta, gamma, x, ps, pt, garena, woff, C, M, Cin, Cout, pix_per_wg):
+def conv1x1_wgrad(g, yv, alpha, beta, gamma, x, ps, pt, garena, woff, C, M, Cin, Cout, pix_per_wg, nimg=None, hw=0):
     """dW += Σ_p dyᵀ·act(x) straight into the OIHW arena rows (stride garena.stride(0))."""
     rc = _fnp("fa_conv1x1_wgrad", g)(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(x), _p(ps), _p(pt), _p(garena),
                                  _i64(garena.stride(0)), _i64(woff), _i(C), _i(M), _i(Cin), _i(Cout), _i(pix_per_wg),
-                                 _stream(g))
+                                 _p(nimg), _i(hw), _stream(g))
     _check(rc, "fa_conv1x1_wgrad")
 
 
@@ -159,7 +161,7 @@ def conv1x1_bwd_fused_scratch(C, M, Cin, Cout, pix_per_wg):
 
 
 def conv1x1_bwd_fused(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, ldk2, e_x, e_s, e_t, e_add, e_y1, e_y2, out, stats,
-                      garena, woff, C, M, Cin, Cout, epi, pix_per_wg, part=None):
+                      garena, woff, C, M, Cin, Cout, epi, pix_per_wg, part=None, nimg=None, hw=0):
     """Data gradient (with the EPI_MASK / EPI_BLOCK epilogue of :func:`conv_bwd_data`) AND weight
     gradient (+= into the OIHW arena rows) of a 1×1 / stride-1 conv from one pass over g, y, e_x.
     ``stats`` is [C, Cin, NS] (NS = its last dim). ``part``: optional fp32 scratch of
@@ -170,43 +172,44 @@ def conv1x1_bwd_fused(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, ldk2, e_x, e_s, 
                                      _i(ldk2), _p(e_x), _p(e_s), _p(e_t), _p(e_add), _p(e_y1), _p(e_y2), _p(out),
                                      _p(stats), _i(stats.shape[-1]), _p(garena), _i64(garena.stride(0)), _i64(woff),
                                      _i(C), _i(M), _i(Cin), _i(Cout), _i(epi), _i(pix_per_wg), _p(part),
-                                     _stream(g))
+                                     _p(nimg), _i(hw), _stream(g))
     _check(rc, "fa_conv1x1_bwd_fused")
 
 
 def bn_fwd_finalize(stats, C, Ch, n, arena, off_gamma, off_beta, off_rm, off_rv, off_nbt, momentum, eps, active,
-                    scale, shift, mean, rstd, update_running=True, pivot=None):
+                    scale, shift, mean, rstd, update_running=True, pivot=None, nimg=None, hw=0):
     """``pivot`` [C, Ch] (optional, in/out): the shift the producing conv subtracted; replaced by this
     batch's true mean (the next step's pivot)."""
     rc = _fn("fa_bn_fwd_finalize")(_p(stats), _i(C), _i(Ch), _f(n), _p(arena), _i64(arena.stride(0)),
                                    _i64(off_gamma), _i64(off_beta), _i64(off_rm), _i64(off_rv), _i64(off_nbt),
                                    _f(momentum), _f(eps), _p(active), _p(scale), _p(shift), _p(mean), _p(rstd),
-                                   _i(int(update_running)), _p(pivot), _stream(stats))
+                                   _i(int(update_running)), _p(pivot), _p(nimg), _i(hw), _stream(stats))
     _check(rc, "fa_bn_fwd_finalize")
 
 
 def bn_bwd_finalize(bstats, NS, q_gy, C, Ch, n, mean, rstd, arena, garena, off_gamma, off_beta, alpha, beta_c,
-                    gamma_c):
+                    gamma_c, nimg=None, hw=0):
     rc = _fn("fa_bn_bwd_finalize")(_p(bstats), _i(NS), _i(q_gy), _i(C), _i(Ch), _f(n), _p(mean), _p(rstd),
                                    _p(arena), _p(garena), _i64(arena.stride(0)), _i64(off_gamma), _i64(off_beta),
-                                   _p(alpha), _p(beta_c), _p(gamma_c), _stream(bstats))
+                                   _p(alpha), _p(beta_c), _p(gamma_c), _p(nimg), _i(hw), _stream(bstats))
     _check(rc, "fa_bn_bwd_finalize")
 
 
-def block_out(y, s, t, r, rs, rt, out, C, per_client, Ch):
+def block_out(y, s, t, r, rs, rt, out, C, per_client, Ch, nimg=None, per_img=0):
+    """out = relu(y·s + t + R) over the first nimg[c] images (per_img elements each) of every client."""
     rc = _fnp("fa_block_out", y)(_p(y), _p(s), _p(t), _p(r), _p(rs), _p(rt), _p(out), _i(C), _i64(per_client), _i(Ch),
-                             _stream(y))
+                             _p(nimg), _i(per_img), _stream(y))
     _check(rc, "fa_block_out")
 
 
-def avgpool(x, pooled, CN, HW, Ch):
-    rc = _fnp("fa_avgpool", x)(_p(x), _p(pooled), _i(CN), _i(HW), _i(Ch), _stream(x))
+def avgpool(x, pooled, CN, HW, Ch, nimg=None, N=1):
+    rc = _fnp("fa_avgpool", x)(_p(x), _p(pooled), _i(CN), _i(HW), _i(Ch), _p(nimg), _i(N), _stream(x))
     _check(rc, "fa_avgpool")
 
 
-def head_bwd(dpool, out, y3, yd, gpre, stats, C, N, HW, Ch, NS):
+def head_bwd(dpool, out, y3, yd, gpre, stats, C, N, HW, Ch, NS, nimg=None):
     rc = _fnp("fa_head_bwd", out)(_p(dpool), _p(out), _p(y3), _p(yd), _p(gpre), _p(stats), _i(C), _i(N), _i(HW), _i(Ch),
-                            _i(NS), _stream(out))
+                            _i(NS), _p(nimg), _stream(out))
     _check(rc, "fa_head_bwd")
 
 

@@ -41,6 +41,14 @@ def init_process_group(backend: Optional[str] = None, timeout_s: int = 1800, dev
     return rank, world
 
 
+def backend_name() -> str:
+    """Human label of the active collective backend: RCCL (``nccl`` on ROCm), gloo, or none."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return "none"
+    b = str(dist.get_backend())
+    return "RCCL" if b == "nccl" else b
+
+
 def is_dist() -> bool:
     return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
 

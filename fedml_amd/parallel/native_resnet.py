@@ -150,6 +150,7 @@ class NativeResNetStep:
         self.use_c1 = os.environ.get("FEDML_AMD_CONV1X1", "1") != "0"
         self.use_c1f = os.environ.get("FEDML_AMD_C1_FUSED", "1") != "0"
         self.dump = None   # debug: list collecting (name, tensor clone) of every backward gradient buffer
+        self._nimg = None
 
     # ------------------------------------------------------------------ setup
     def _all_convs(self):
@@ -210,8 +211,8 @@ class NativeResNetStep:
         # activations (storage precision) and per-BN vectors
         bf = self.dtype
 
-        def act(hh, ww, ch):
-            return torch.empty(C, N, hh, ww, ch, dtype=bf, device=dev)
+        def act(hh, ww, ch):   # zero-initialised: padding images (heterogeneous batches) are never written
+            return torch.zeros(C, N, hh, ww, ch, dtype=bf, device=dev)
 
         self.x_in = act(H, W, st.cin_pad)
         self.stem_y = act(st.Ho, st.Wo, st.cout)
@@ -226,7 +227,7 @@ class NativeResNetStep:
                 maxel = max(maxel, cv.H * cv.W * cv.cin_pad, cv.Ho * cv.Wo * cv.cout)
         # gradient scratch: block-output g (kept until the block's conv0 is done), two ping-pong
         # buffers for the inner chain, one for the shortcut gradient
-        self.gbuf = [torch.empty(C * N * maxel, dtype=bf, device=dev) for _ in range(4)]
+        self.gbuf = [torch.zeros(C * N * maxel, dtype=bf, device=dev) for _ in range(4)]
         # per-BN vectors: scale, shift, mean, rstd, alpha, beta, gamma, pivot   + stats
         # (pivot: the per-channel shift K the producing conv subtracts from its stored output — the
         # previous step's batch mean — so activations and BN sums stay centred; see bn_fwd_finalize)
@@ -245,7 +246,7 @@ class NativeResNetStep:
             o += C * bn.ch * 3
             self.stat_views[bn.key] = (fwd, bwd)
         fh, fw = self.final_hw
-        self.pooled = torch.empty(C, N, self.fc_in, dtype=torch.float32, device=dev)
+        self.pooled = torch.zeros(C, N, self.fc_in, dtype=torch.float32, device=dev)
         # GEMM-layout dW scratch for the weight-gradient kernel (kept zeroed by its scatter pass)
         mx = max(cv.cout * cv.k * cv.k * cv.cin_pad for cv in self._all_convs())
         self.dw_scratch = torch.zeros(C * mx, dtype=torch.float32, device=dev)
@@ -327,17 +328,17 @@ class NativeResNetStep:
         if self._c3(cv):
             nn_ops.conv3x3_wgrad(g, y, vec[4], vec[5], vec[6], x, ps, pt, garena, self.off[cv.key], C, N, cv.H, cv.W,
                                  cv.cin_pad, cv.cout, cv.cin, self.dw_c3[self._c3_off[cv.key]:], cv.stride,
-                                 scatter=False)   # scattered with the other 3×3 layers at the end of step()
+                                 scatter=False, nimg=self._nimg)   # scattered with the other 3×3 layers at the end
             return
         M = N * cv.Ho * cv.Wo
         if self.use_c1 and cv.cin == cv.cin_pad and nn_ops.conv1x1_wgrad_supported(cv.cin, cv.cout, cv.k, cv.stride,
                                                                                   cv.pad):
             nn_ops.conv1x1_wgrad(g, y, vec[4], vec[5], vec[6], x, ps, pt, garena, self.off[cv.key], C, M, cv.cin,
-                                 cv.cout, self._c1_pix_per_wg(M))
+                                 cv.cout, self._c1_pix_per_wg(M), nimg=self._nimg, hw=cv.Ho * cv.Wo)
             return
         nn_ops.conv_wgrad(g, y, vec[4], vec[5], vec[6], x, ps, pt, garena, self.off[cv.key], C, N, cv.H, cv.W,
                           cv.cin_pad, cv.Ho, cv.Wo, cv.cout, cv.k, cv.k, cv.stride, cv.pad, self._pix_per_wg(M), cv.cin,
-                          self.dw_scratch)
+                          self.dw_scratch, nimg=self._nimg)
 
     def _c1f(self, cv: ConvSpec, epi):
         return (self.use_c1f and cv.cin == cv.cin_pad
@@ -373,32 +374,38 @@ class NativeResNetStep:
             nn_ops.conv3x3_fwd(x, self.packed.view(-1)[cv.off_f:], self.packed_ld,
                                pro_vec[0] if pro_vec is not None else None,
                                pro_vec[1] if pro_vec is not None else None, y, stats, self.C, N, cv.H, cv.W,
-                               cv.cin_pad, cv.cout, cv.ldk, cv.stride, pivot=pivot)
+                               cv.cin_pad, cv.cout, cv.ldk, cv.stride, pivot=pivot, nimg=self._nimg)
             return
         nn_ops.conv_fwd(x, self.packed.view(-1)[cv.off_f:], self.packed_ld, pro_vec[0] if pro_vec is not None else None,
                         pro_vec[1] if pro_vec is not None else None, y, stats, self.C, N, cv.H, cv.W, cv.cin_pad,
                         cv.cout, cv.k, cv.k, cv.stride, cv.pad, cv.Ho, cv.Wo, cv.ldk, self._tiles_per_wave(M),
-                        pivot=pivot)
+                        pivot=pivot, nimg=self._nimg)
 
     def _bn_fwd(self, bn, N, hw, arena, active, training=True):
         v = self.bn_vec[bn.key]
         fst = self.stat_views[bn.key][0]
         g, b, rm, rv, nbt = self._bn_offsets(bn)
         nn_ops.bn_fwd_finalize(fst, self.C, bn.ch, float(N * hw), arena, g, b, rm, rv, nbt, bn.momentum, bn.eps,
-                               active, v[0], v[1], v[2], v[3], training, pivot=v[7])
+                               active, v[0], v[1], v[2], v[3], training, pivot=v[7], nimg=self._nimg, hw=hw)
 
     def _bn_bwd(self, bn, q, N, hw, arena, garena):
         v = self.bn_vec[bn.key]
         bst = self.stat_views[bn.key][1]
         g, b = self.off[f"{bn.key}.weight"], self.off[f"{bn.key}.bias"]
         nn_ops.bn_bwd_finalize(bst, 3, q, self.C, bn.ch, float(N * hw), v[2], v[3], arena, garena, g, b, v[4], v[5],
-                               v[6])
+                               v[6], nimg=self._nimg, hw=hw)
 
     # ------------------------------------------------------------------ step
-    def step(self, arena, garena, x, labels, row_scale, active):
+    def step(self, arena, garena, x, labels, row_scale, active, nimg=None):
         """x [C, N, Cin, H, W] fp32, labels [C, N] → summed per-client mean loss (device scalar).
-        Fills ``garena`` (must be zeroed by the caller) with this step's gradients."""
+        Fills ``garena`` (must be zeroed by the caller) with this step's gradients.
+
+        ``nimg`` (int32 [C] device tensor, optional): client c's valid images this step — the first
+        nimg[c] of its N rows (heterogeneous partitions, exhausted clients: 0). Every kernel restricts its
+        pixel range to them (grids of idle clients exit at once), BatchNorm normalises over them, and
+        the padding rows never enter a statistic or a gradient (their ``row_scale`` must be 0)."""
         C, N = x.shape[0], x.shape[1]
+        self._nimg = nimg
         H, W = x.shape[3], x.shape[4]
         if self.geom != (N, H, W):
             if (N, H, W) in self._states:
@@ -416,7 +423,8 @@ class NativeResNetStep:
         self._bn_fwd(st_bn, N, st_conv.Ho * st_conv.Wo, arena, active)
         v0 = self.bn_vec[st_bn.key]
         nn_ops.block_out(self.stem_y, v0[0], v0[1], None, None, None, self.stem_out, C,
-                         N * st_conv.Ho * st_conv.Wo * st_conv.cout, st_conv.cout)
+                         N * st_conv.Ho * st_conv.Wo * st_conv.cout, st_conv.cout, nimg=self._nimg,
+                         per_img=st_conv.Ho * st_conv.Wo * st_conv.cout)
         act_in = self.stem_out
         for b in self.blocks:
             b.act_in = act_in
@@ -434,14 +442,16 @@ class NativeResNetStep:
                 self._bn_fwd(b.ds_bn, N, d.Ho * d.Wo, arena, active)
                 vd = self.bn_vec[b.ds_bn.key]
                 nn_ops.block_out(b.ys[-1], vl[0], vl[1], b.yd, vd[0], vd[1], b.out, C,
-                                 N * last.Ho * last.Wo * last.cout, last.cout)
+                                 N * last.Ho * last.Wo * last.cout, last.cout, nimg=self._nimg,
+                                 per_img=last.Ho * last.Wo * last.cout)
             else:
                 nn_ops.block_out(b.ys[-1], vl[0], vl[1], act_in, None, None, b.out, C,
-                                 N * last.Ho * last.Wo * last.cout, last.cout)
+                                 N * last.Ho * last.Wo * last.cout, last.cout, nimg=self._nimg,
+                                 per_img=last.Ho * last.Wo * last.cout)
             act_in = b.out
         fh, fw = self.final_hw
         chl = self.blocks[-1].convs[-1].cout
-        nn_ops.avgpool(act_in, self.pooled, C * N, fh * fw, chl)
+        nn_ops.avgpool(act_in, self.pooled, C * N, fh * fw, chl, nimg=self._nimg, N=N)
         # ---------------- head: fc + fused CE (fp32, tiny) ----------------
         ow = self.off["fc.weight"]
         ob = self.off["fc.bias"]
@@ -462,7 +472,7 @@ class NativeResNetStep:
         gpre = bufs[0]
         bl = self.blocks[-1]
         nn_ops.head_bwd(dpool, bl.out, bl.ys[-1], bl.yd, gpre, self.stat_views[bl.bns[-1].key][1].view(-1), C, N,
-                        fh * fw, chl, 3)
+                        fh * fw, chl, 3, nimg=self._nimg)
         # head_bwd wrote (Σg, Σg·y_last, Σg·yd) into the last BN's bwd stats; the downsample BN needs
         # (Σg, Σg·yd) → copy slots into its own stats buffer below (same g)
         for bi in range(len(self.blocks) - 1, -1, -1):
@@ -488,7 +498,8 @@ class NativeResNetStep:
                     nn_ops.conv1x1_bwd_fused(g_j, b.ys[j], v[4], v[5], v[6], self.packed.view(-1)[cv.off_b:],
                                              self.packed_ld, cv.ldk2, b.ys[j - 1], pv[0], pv[1], None, None, None,
                                              out_g, self.stat_views[b.bns[j - 1].key][1], garena, self.off[cv.key], C,
-                                             M, cv.cin, cv.cout, nn_ops.EPI_MASK, self._c1f_pix_per_wg(M))
+                                             M, cv.cin, cv.cout, nn_ops.EPI_MASK, self._c1f_pix_per_wg(M),
+                                             nimg=self._nimg, hw=cv.Ho * cv.Wo)
                     self._bn_bwd(b.bns[j - 1], 1, N, cv.H * cv.W, arena, garena)
                     g_j = out_g
                     self._dump(f"{cv.key}.dx", out_g, C * N * cv.H * cv.W * cv.cin)
@@ -498,7 +509,7 @@ class NativeResNetStep:
                     nn_ops.conv3x3_bwd_data(g_j, b.ys[j], v[4], v[5], v[6], self.packed.view(-1)[cv.off_b:],
                                             self.packed_ld, out_g, b.ys[j - 1], pv[0], pv[1],
                                             self.stat_views[b.bns[j - 1].key][1], C, N, cv.H, cv.W, cv.cout,
-                                            cv.cin_pad, cv.ldk2, cv.stride)
+                                            cv.cin_pad, cv.ldk2, cv.stride, nimg=self._nimg)
                     self._bn_bwd(b.bns[j - 1], 1, N, cv.H * cv.W, arena, garena)
                     g_j = out_g
                     self._dump(f"{cv.key}.dx", out_g, C * N * cv.H * cv.W * cv.cin)
@@ -507,7 +518,7 @@ class NativeResNetStep:
                                      self.packed_ld, out_g, nn_ops.EPI_MASK, b.ys[j - 1], pv[0], pv[1], None, None,
                                      None, self.stat_views[b.bns[j - 1].key][1], C, N, cv.Ho, cv.Wo, cv.cout,
                                      cv.cin_pad, cv.k, cv.k, cv.stride, cv.pad, cv.H, cv.W, cv.ldk2,
-                                     self._tiles_per_wave(N * cv.H * cv.W))
+                                     self._tiles_per_wave(N * cv.H * cv.W), nimg=self._nimg)
                 self._bn_bwd(b.bns[j - 1], 1, N, cv.H * cv.W, arena, garena)
                 g_j = out_g
                 self._dump(f"{cv.key}.dx", out_g, C * N * cv.H * cv.W * cv.cin)
@@ -520,7 +531,7 @@ class NativeResNetStep:
                 nn_ops.conv_bwd_data(gpre, b.yd, vd[4], vd[5], vd[6], self.packed.view(-1)[d.off_b:], self.packed_ld,
                                      gadd, nn_ops.EPI_STORE, None, None, None, None, None, None, self.stats, C, N,
                                      d.Ho, d.Wo, d.cout, d.cin_pad, d.k, d.k, d.stride, d.pad, d.H, d.W, d.ldk2,
-                                     self._tiles_per_wave(N * d.H * d.W))
+                                     self._tiles_per_wave(N * d.H * d.W), nimg=self._nimg)
                 shortcut = gadd
             else:
                 shortcut = gpre
@@ -545,14 +556,15 @@ class NativeResNetStep:
                 nn_ops.conv1x1_bwd_fused(g_j, b.ys[0], v[4], v[5], v[6], self.packed.view(-1)[cv0.off_b:],
                                          self.packed_ld, cv0.ldk2, b.act_in, None, None, shortcut, ey1, ey2, out_buf,
                                          pstats, garena, self.off[cv0.key], C, M0, cv0.cin, cv0.cout,
-                                         nn_ops.EPI_BLOCK, self._c1f_pix_per_wg(M0))
+                                         nn_ops.EPI_BLOCK, self._c1f_pix_per_wg(M0), nimg=self._nimg,
+                                         hw=cv0.H * cv0.W)
                 gpre = out_buf
                 self._dump(f"{cv0.key}.dx", out_buf, C * N * cv0.H * cv0.W * cv0.cin)
                 continue
             nn_ops.conv_bwd_data(g_j, b.ys[0], v[4], v[5], v[6], self.packed.view(-1)[cv0.off_b:], self.packed_ld,
                                  out_buf, nn_ops.EPI_BLOCK, b.act_in, None, None, shortcut, ey1, ey2, pstats, C, N,
                                  cv0.Ho, cv0.Wo, cv0.cout, cv0.cin_pad, cv0.k, cv0.k, cv0.stride, cv0.pad, cv0.H,
-                                 cv0.W, cv0.ldk2, self._tiles_per_wave(N * cv0.H * cv0.W))
+                                 cv0.W, cv0.ldk2, self._tiles_per_wave(N * cv0.H * cv0.W), nimg=self._nimg)
             # the previous block's gpre is out_buf
             gpre = out_buf
             self._dump(f"{cv0.key}.dx", out_buf, C * N * cv0.H * cv0.W * cv0.cin)

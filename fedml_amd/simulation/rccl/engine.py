@@ -224,7 +224,8 @@ class ClientBatchEngine:
                     active = self._active_cache[key_a] = torch.tensor(active_list, dtype=torch.float32,
                                                                       device=self.device)
                 sample_mask = None if uniform else mask.t().contiguous()     # [B, C]
-                if self.native_step is not None and sample_mask is None and self.use_graphs:
+                if self.native_step is not None and self.use_graphs:
+                    # heterogeneous batches stay native: per-client valid counts go in as data (nimg)
                     loss = self._graph_step(x, y, mask, b_c, active, lr, first)
                 elif self.tf is not None and self.use_graphs and self._tf_capture and sample_mask is None:
                     loss = self._tf_graph_step(x, y, mask, b_c, active, lr, first)
@@ -247,10 +248,11 @@ class ClientBatchEngine:
 
     def _step_loss(self, x, y, mask, b_c, active, sample_mask, use_native_loss):
         self.grads.zero_()
-        if self.native_step is not None and sample_mask is None:
+        if self.native_step is not None:
             bc = torch.tensor([max(1, b) for b in b_c], dtype=torch.float32, device=self.device)
             row_scale = mask.to(torch.float32) / bc.view(-1, 1)
-            return self.native_step.step(self.params, self.grads, x, y, row_scale, active)
+            nimg = torch.tensor(b_c, dtype=torch.int32, device=self.device)
+            return self.native_step.step(self.params, self.grads, x, y, row_scale, active, nimg=nimg)
         if self.tf is not None:
             out = self.tf.forward(self.views, x, training=True, dtype=self.compute_dtype,
                                   shadow=self._bf16_shadow())                                # [C, B, K]
@@ -318,7 +320,8 @@ class ClientBatchEngine:
         if ent is None:
             st = {"x": torch.empty_like(x), "y": torch.empty_like(y),
                   "rs": torch.empty(mask.shape, dtype=torch.float32, device=self.device),
-                  "act": torch.empty_like(active)}
+                  "act": torch.empty_like(active),
+                  "nimg": torch.empty(len(b_c), dtype=torch.int32, device=self.device)}
             self._fill_static(st, x, y, mask, b_c, active)
             # warm-up on a side stream (allocations, kernel attributes), then capture
             s = torch.cuda.Stream(device=self.device)
@@ -327,12 +330,13 @@ class ClientBatchEngine:
             mom_snapshot = self.mom.clone() if self.mom is not None else None
             with torch.cuda.stream(s):
                 self.grads.zero_()
-                self.native_step.step(self.params, self.grads, st["x"], st["y"], st["rs"], st["act"])
+                self.native_step.step(self.params, self.grads, st["x"], st["y"], st["rs"], st["act"], st["nimg"])
             torch.cuda.current_stream(self.device).wait_stream(s)
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
                 self.grads.zero_()
-                loss = self.native_step.step(self.params, self.grads, st["x"], st["y"], st["rs"], st["act"])
+                loss = self.native_step.step(self.params, self.grads, st["x"], st["y"], st["rs"], st["act"],
+                                             st["nimg"])
                 self._optimizer_step(lr, st["act"], first)
             # the warm-up/capture touched nothing observable except BN running stats: restore
             with torch.no_grad():
@@ -362,6 +366,8 @@ class ClientBatchEngine:
             .to(self.device, non_blocking=True)
         torch.div(mask.to(torch.float32), bc.view(-1, 1), out=st["rs"])
         st["act"].copy_(active, non_blocking=True)
+        if "nimg" in st:
+            st["nimg"].copy_(torch.tensor(b_c, dtype=torch.int32).pin_memory(), non_blocking=True)
 
     # ---------------------------------------------------------------- sequential per-client path
     def _seq_param_views(self):

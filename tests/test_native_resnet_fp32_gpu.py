@@ -323,3 +323,97 @@ def test_fedavg_resnet56_loss_curve_tracks_fp32_torch(dtype):
     else:
         assert dev < 0.05, (dev, list(zip(got, ref)))
     assert got[-1] < got[0] - 0.1      # it learns
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 5e-3), (torch.bfloat16, 0.5)])
+def test_native_step_heterogeneous_counts(dtype, tol):
+    """Clients with different batch sizes in ONE native step (nimg = [16, 11, 3, 0]): every client's
+    gradients equal its own fp64 PyTorch step on its valid samples; BatchNorm normalises over them only;
+    the empty client gets exactly zero gradients and unchanged BN running statistics."""
+    torch.manual_seed(0)
+    model = ResNet(Bottleneck, [1, 1, 1], 10)
+    layout = ParamLayout.from_module(model)
+    C, N, hw = 4, 16, 16
+    counts = [16, 11, 3, 0]
+    flat = layout.flatten(model.state_dict()).to(DEV)
+    arena = flat.view(1, -1).repeat(C, 1).contiguous()
+    garena = torch.zeros_like(arena)
+    x = torch.randn(C, N, 3, hw, hw, device=DEV)
+    y = torch.randint(0, 10, (C, N), device=DEV)
+    mask = torch.arange(N, device=DEV).view(1, -1) < torch.tensor(counts, device=DEV).view(-1, 1)
+    row_scale = mask.float() / torch.tensor([max(1, b) for b in counts], device=DEV).view(-1, 1)
+    active = torch.tensor([1.0 if b else 0.0 for b in counts], device=DEV)
+    nimg = torch.tensor(counts, dtype=torch.int32, device=DEV)
+    step = NativeResNetStep(model, layout, C, DEV, dtype=dtype)
+    loss = float(step.step(arena, garena, x, y, row_scale, active, nimg=nimg))
+    torch.cuda.synchronize()
+    ref_loss = 0.0
+    for c, b in enumerate(counts):
+        g = garena[c]
+        if b == 0:
+            assert float(g.abs().max()) == 0.0
+            assert torch.equal(arena[c], flat)          # running statistics untouched
+            continue
+        m = copy.deepcopy(model).double()
+        m.load_state_dict({k: v.double() if v.is_floating_point() else v
+                           for k, v in layout.unflatten(flat.cpu()).items()})
+        m.train()
+        lo = torch.nn.functional.cross_entropy(m(x[c, :b].cpu().double()), y[c, :b].cpu())
+        lo.backward()
+        ref_loss += float(lo)
+        sd = {k: p.grad for k, p in m.named_parameters()}
+        for s in layout.slots:
+            if s.key in sd:
+                r = sd[s.key].reshape(-1)
+                err = float((g[s.offset:s.offset + s.numel].cpu().double() - r).norm() / r.norm().clamp_min(1e-30))
+                assert err < tol, (c, s.key, err)
+        rm = layout.slot("bn1.running_mean")
+        assert torch.allclose(arena[c, rm.offset:rm.offset + rm.numel].cpu().double(),
+                              m.bn1.running_mean, rtol=1e-3 if dtype == torch.float32 else 5e-2, atol=1e-4)
+    assert abs(loss - ref_loss) / ref_loss < (1e-5 if dtype == torch.float32 else 2e-2)
+
+
+def test_engine_heterogeneous_partition_stays_native():
+    """A Dirichlet-like partition (clients of 150, 97, 20 and 0 samples, batch 32): the engine keeps every
+    step on the captured native program (no torch interpreter fallback) and one local epoch equals each
+    client's own fp32 PyTorch SGD epoch (reference trainer semantics: my_model_trainer_classification.py)."""
+    from fedml_amd.arguments import Arguments
+    from fedml_amd.simulation.rccl.client_store import DeviceClientStore
+    from fedml_amd.simulation.rccl.engine import ClientBatchEngine
+    torch.manual_seed(0)
+    model = ResNet(Bottleneck, [1, 1, 1], 10)
+    counts = [150, 97, 20, 0]
+    n = sum(counts)
+    offs = [0, 150, 247, 267]
+    store = DeviceClientStore(torch.randn(n, 3, 16, 16, device=DEV), torch.randint(0, 10, (n,), device=DEV),
+                              offs, counts)
+    lr, bs = 0.02, 32
+    args = Arguments.from_dict({"x": {"client_optimizer": "sgd", "learning_rate": lr}})
+    eng = ClientBatchEngine(copy.deepcopy(model).to(DEV), 4, DEV, args, compute_dtype=None)
+    assert eng.native_step is not None and eng.native_step.dtype == F32
+    flat = eng.layout.flatten(model.state_dict(), device=DEV)
+    eng.load_global(flat)
+    calls = []
+    orig = eng._step_loss
+    eng._step_loss = lambda *a, **k: calls.append(1) or orig(*a, **k)
+    eng.train(store, torch.arange(4, device=DEV), 1, bs, lr, shuffle=False)
+    torch.cuda.synchronize()
+    assert not calls and len(eng._graphs) >= 2       # every step replayed a native graph
+    for c, cnt in enumerate(counts):
+        if cnt == 0:
+            assert torch.equal(eng.params[c], flat)
+            continue
+        m = copy.deepcopy(model).to(DEV)
+        m.train()
+        opt = torch.optim.SGD(m.parameters(), lr=lr)
+        for lo in range(0, cnt, bs):
+            xb = store.x_all[offs[c] + lo:offs[c] + min(cnt, lo + bs)]
+            yb = store.y_all[offs[c] + lo:offs[c] + min(cnt, lo + bs)]
+            opt.zero_grad()
+            torch.nn.functional.cross_entropy(m(xb), yb).backward()
+            opt.step()
+        ref = eng.layout.flatten(m.state_dict(), device=DEV)
+        upd_ref = ref - flat
+        err = float((eng.params[c] - ref).norm() / upd_ref.norm())
+        assert err < 2e-2, (c, err)
+    eng.close()
