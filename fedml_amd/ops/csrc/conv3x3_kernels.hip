@@ -736,12 +736,14 @@ static int dispatch_gemm(int kc, int nout, const Args& a, int C, hipStream_t s) 
       default: return -2;
     }
   }
-  // unit sizes measured with FEDML_AMD_C3_PX sweeps (profiles/r1_c3_unit_sweep.txt)
-  constexpr int PX = ST == 2 ? 128 : 256;
+  // unit sizes measured with FEDML_AMD_C3_PX sweeps (bf16: profiles/r1_c3_unit_sweep.txt; fp32:
+  // profiles/r2_c3_sweep_fp32.txt — 256-px units for the fp32 backward, stride 2 included)
+  constexpr int PX = ST == 2 ? ((P::kF32 && BWD) ? 256 : 128) : 256;
   switch (kc) {
-    case 16: return launch_gemm<P, 16, 16, XF, BWD, EPI, ST>(a, nout, C, (BWD && ST == 1) ? 512 : PX, s);
+    case 16: return launch_gemm<P, 16, 16, XF, BWD, EPI, ST>(a, nout, C, (BWD && ST == 1 && !P::kF32) ? 512 : PX, s);
     case 32: return launch_gemm<P, 32, 32, XF, BWD, EPI, ST>(a, nout, C, PX, s);
-    case 64: return launch_gemm<P, 64, N64, XF, BWD, EPI, ST>(a, nout, C, ST == 2 ? 64 : 128, s);  // weights split over z
+    case 64: return launch_gemm<P, 64, N64, XF, BWD, EPI, ST>(a, nout, C, ST == 2 ? ((P::kF32 && BWD) ? 256 : 64) : 128,
+                                                               s);  // weights split over z
     default: return -2;
   }
 }
@@ -794,9 +796,12 @@ static int conv3x3_wgrad(const void* g, const void* yv, const float* alpha, cons
   // Target workgroup count: every workgroup adds its Cout×9·Cin partial sums with fp32 atomics, so
   // more, shorter workgroups cost atomics per client (FEDML_AMD_C3W_WGS overrides, for tuning;
   // scripts/gpu_c3w_sweep*.sh)
+  // bf16 256: +2/+3/+6 % rounds/s at 50/25/13 clients per GPU, neutral at 100 (fewer fp32 atomics per
+  // client); fp32 2048: the MFMA work per workgroup dominates the atomics (wgrad 0.72 → 0.54 ms at 16×32²,
+  // profiles/r2_c3_sweep_fp32.txt)
   static const int wgs = [] {
     const char* e = getenv("FEDML_AMD_C3W_WGS");
-    return e ? atoi(e) : 256;   // measured: +2/+3/+6 % rounds/s at 50/25/13 clients per GPU, neutral at 100
+    return e ? atoi(e) : (P::kF32 ? 2048 : 256);
   }();
   const int CGX = Cin / P::VEC, CGD = Cout / P::VEC;
   constexpr int XMAX = P::kF32 ? 16 : 8;   // x-tile 16-B chunks per thread (fp32: twice the chunks per pixel)

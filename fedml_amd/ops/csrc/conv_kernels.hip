@@ -103,7 +103,10 @@ FA_EXPORT int fa_pack_weights_f32(const float* arena, int64_t ldw, const void* s
 // per iteration; B (packed weights) and the per-channel vectors live in LDS.
 // =====================================================================================
 enum { AOP_ACT = 0, AOP_DY = 1 };
-enum { MODE_FWD = 0, MODE_BWD = 1 };
+// MODE_BWD2: backward-data of a 1×1 / stride-2 / pad-0 convolution (the downsample shortcut): iterates
+// over the dy pixels (a quarter of the dx grid), writes dx(2i, 2j) = Wᵀ·dy(i, j) and zeros at the three
+// other pixels of each 2×2 cell — the generic MODE_BWD runs MFMAs over those zero pixels (4× the work).
+enum { MODE_FWD = 0, MODE_BWD = 1, MODE_BWD2 = 2 };
 
 struct ConvArgs {        // activations / packed weights are P::T (bf16 | fp32)
   const void* src;       // A source activations / g
@@ -146,9 +149,11 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int K = a.KH * a.KW * a.KC;
-  const int M = a.Nb * a.Ho * a.Wo;
-  // this client's valid output pixels: images past nimg[c] are padding (never read or written)
-  const int Mv = a.nimg ? min(M, a.nimg[c] * a.Ho * a.Wo) : M;
+  const int Mo = a.Nb * a.Ho * a.Wo;                             // output pixels per client (tensor layout)
+  const int HWi = MODE == MODE_BWD2 ? a.Hs * a.Ws : a.Ho * a.Wo;   // iteration pixels per image
+  const int M = MODE == MODE_BWD2 ? a.Nb * HWi : Mo;
+  // this client's valid iteration pixels: images past nimg[c] are padding (never read or written)
+  const int Mv = a.nimg ? min(M, a.nimg[c] * HWi) : M;
   if ((int)(blockIdx.x * 4 * a.tiles_per_wave) * 16 >= Mv) return;   // uniform: whole workgroup idle
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -181,7 +186,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
   const int64_t src_client = (int64_t)c * a.Nb * a.Hs * a.Ws * a.KC;
   const T* src = reinterpret_cast<const T*>(a.src) + src_client;
   const T* src2 = (AOP == AOP_DY) ? reinterpret_cast<const T*>(a.src2) + src_client : nullptr;
-  T* out = reinterpret_cast<T*>(a.out) + (int64_t)c * M * NO;
+  T* out = reinterpret_cast<T*>(a.out) + (int64_t)c * Mo * NO;
   const T* e_x = reinterpret_cast<const T*>(a.e_x);
   const T* e_add = reinterpret_cast<const T*>(a.e_add);
   const T* e_y1 = reinterpret_cast<const T*>(a.e_y1);
@@ -203,9 +208,10 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
     const int m = tile * 16 + (lane & 15);
     const bool mvalid = m < Mv;
     const int mm = mvalid ? m : 0;
-    const int on = mm / (a.Ho * a.Wo);
-    const int orem = mm % (a.Ho * a.Wo);
-    const int oh = orem / a.Wo, ow = orem % a.Wo;
+    const int IW = MODE == MODE_BWD2 ? a.Ws : a.Wo;
+    const int on = mm / HWi;
+    const int orem = mm % HWi;
+    const int oh = orem / IW, ow = orem % IW;
 
     f32x4 acc[NT];
 #pragma unroll
@@ -219,7 +225,11 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
         const int kh = tap / a.KW, kw = tap % a.KW;
         int ih, iw;
         bool ok;
-        if (MODE == MODE_FWD) {
+        if (MODE == MODE_BWD2) {   // the iteration pixel IS the dy pixel
+          ih = oh;
+          iw = ow;
+          ok = true;
+        } else if (MODE == MODE_FWD) {
           ih = oh * a.stride - a.pad + kh;
           iw = ow * a.stride - a.pad + kw;
           ok = ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws;
@@ -273,7 +283,17 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
       if (lane / CG < ROWS_PER_PASS && row < rows_valid) {
         const int ch0 = my_cg * V;
         const uint4 dv = *reinterpret_cast<const uint4*>(my_stage + row * NOUT + ch0);
-        const int64_t goff = ((int64_t)(tile * 16 + row)) * NO + ch_base + ch0;
+        int64_t goff = ((int64_t)(tile * 16 + row)) * NO + ch_base + ch0;
+        if (MODE == MODE_BWD2) {   // dy pixel → dx (2i, 2j); zeros at the other three pixels of the cell
+          const int pm = tile * 16 + row;
+          const int n_ = pm / HWi, r_ = pm % HWi;
+          const int64_t px = ((int64_t)n_ * a.Ho + 2 * (r_ / a.Ws)) * a.Wo + 2 * (r_ % a.Ws);
+          goff = px * NO + ch_base + ch0;
+          const uint4 z = make_uint4(0, 0, 0, 0);
+          *reinterpret_cast<uint4*>(out + goff + NO) = z;
+          *reinterpret_cast<uint4*>(out + goff + (int64_t)a.Wo * NO) = z;
+          *reinterpret_cast<uint4*>(out + goff + (int64_t)(a.Wo + 1) * NO) = z;
+        }
         if (EPI == EPI_FWD || EPI == EPI_STORE) {
           *reinterpret_cast<uint4*>(out + goff) = dv;
           if (EPI == EPI_FWD) {
@@ -283,7 +303,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
             for (int j = 0; j < V; ++j) { st0[j] += f[j]; st1[j] += f[j] * f[j]; }
           }
         } else {
-          const int64_t eoff = (int64_t)c * M * NO + goff;
+          const int64_t eoff = (int64_t)c * Mo * NO + goff;
           float g[V], xv[V];
           P::unpack(dv, g);
           P::unpack(*reinterpret_cast<const uint4*>(e_x + eoff), xv);
@@ -363,7 +383,7 @@ static size_t conv_smem_bytes(int nout, int ldk, int kc) {
 template <class P, int NT, int AOP, int PRO, int MODE, int EPI>
 static int launch_conv(ConvArgs a, int nout, int C, hipStream_t stream) {
   a.nout_total = nout;
-  const int M = a.Nb * a.Ho * a.Wo;
+  const int M = MODE == MODE_BWD2 ? a.Nb * a.Hs * a.Ws : a.Nb * a.Ho * a.Wo;
   const int tiles = (M + 15) / 16;
   const int per_wg = 4 * a.tiles_per_wave;
   const int gx = (tiles + per_wg - 1) / per_wg;
@@ -425,7 +445,10 @@ static int conv_bwd_data(const void* g, const void* yv, const float* alpha, cons
   a.Nb = Nb; a.Hs = Hy; a.Ws = Wy; a.KC = Cout; a.Ho = Hx; a.Wo = Wx; a.KH = KH; a.KW = KW; a.stride = stride;
   a.pad = pad; a.ldk = ldk2; a.Kp = (KH * KW * Cout + 31) / 32 * 32; a.tiles_per_wave = tiles_per_wave;
   switch (epi) {
-    case EPI_STORE: return dispatch_nt<P, AOP_DY, PRO_NONE, MODE_BWD, EPI_STORE>(Cin, a, C, stream);
+    case EPI_STORE:
+      if (KH == 1 && KW == 1 && stride == 2 && pad == 0 && Hx == 2 * Hy && Wx == 2 * Wy)
+        return dispatch_nt<P, AOP_DY, PRO_NONE, MODE_BWD2, EPI_STORE>(Cin, a, C, stream);
+      return dispatch_nt<P, AOP_DY, PRO_NONE, MODE_BWD, EPI_STORE>(Cin, a, C, stream);
     case EPI_MASK: return dispatch_nt<P, AOP_DY, PRO_NONE, MODE_BWD, EPI_MASK>(Cin, a, C, stream);
     case EPI_BLOCK: return dispatch_nt<P, AOP_DY, PRO_NONE, MODE_BWD, EPI_BLOCK>(Cin, a, C, stream);
     default: return -4;
