@@ -22,6 +22,7 @@ from .fl_ops import (
     coordinate_median,
     quantize_int8,
     dequantize_int8_axpy,
+    compress_accumulate,
     quantize_fp8,
     dequantize_fp8_axpy,
     topk_abs,

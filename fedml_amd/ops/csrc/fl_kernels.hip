@@ -615,6 +615,90 @@ FA_EXPORT int fa_dequant_fp8_axpy(const uint8_t* q, const float* scales, float w
   return (int)hipGetLastError();
 }
 
+// ---- all clients of a GPU in ONE launch: compress (int8 stochastic | fp8) Δ_c = w_c − w_global with
+// error feedback, decompress straight into the aggregate: acc = Σ_c n_c·(w_global + D(C(Δ_c + r_c))),
+// r_c ← Δ_c + r_c − D(C(·)). One wave per 256-value quantisation block loops over the C clients, so acc
+// is written once per element (no atomics, no [C, P] intermediate, no per-client host loop).
+// residual_rows[c] = the client's residual row (0 = none); weights / client ids read on the device.
+template <int MODE>  // 0 int8 stochastic, 1 fp8 e4m3fn
+__global__ __launch_bounds__(256) void compress_accumulate_kernel(
+    const float* __restrict__ params, int64_t ldp, int C, const float* __restrict__ glob,
+    const uint64_t* __restrict__ residual_rows, const float* __restrict__ weights, const int64_t* __restrict__ ids,
+    float* __restrict__ acc, int64_t n, uint32_t seed_lo, uint32_t seed_hi) {
+  const int lane = threadIdx.x & 63;
+  const int64_t blk = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int64_t base = blk * 256 + lane * 4;
+  if (blk * 256 >= n) return;
+  float g[4], a[4] = {0.f, 0.f, 0.f, 0.f};
+  float wsum = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) g[j] = (base + j < n) ? glob[base + j] : 0.f;
+  for (int c = 0; c < C; ++c) {
+    const float w = weights[c];
+    if (w == 0.f) continue;   // wave-uniform
+    wsum += w;
+    float* res = reinterpret_cast<float*>(residual_rows ? residual_rows[c] : 0ull);
+    const float* pc = params + (int64_t)c * ldp;
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int64_t i = base + j;
+      v[j] = (i < n) ? pc[i] - g[j] + (res ? res[i] : 0.f) : 0.f;
+    }
+    float amax = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
+    amax = wave_max(amax);
+    float back[4];
+    if (MODE == 0) {
+      const float scale = amax > 0.f ? amax / 127.f : 1.f;
+      const float inv = 1.f / scale;
+      const uint32_t cid = (uint32_t)ids[c];
+      Philox4 r = philox4x32((uint32_t)base, (uint32_t)(base >> 32), 0x0a11, cid, seed_lo, seed_hi);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float t = floorf(v[j] * inv + u01(r.v[j]) - 1e-7f);
+        t = fminf(fmaxf(t, -127.f), 127.f);
+        back[j] = t * scale;
+      }
+    } else {
+      const float scale = amax > 0.f ? amax / 448.f : 1.f;
+      const float inv = 1.f / scale;
+      float t[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) t[j] = fminf(fmaxf(v[j] * inv, -448.f), 448.f);
+      int pk = __builtin_amdgcn_cvt_pk_fp8_f32(t[0], t[1], 0, false);
+      pk = __builtin_amdgcn_cvt_pk_fp8_f32(t[2], t[3], pk, true);
+      back[0] = __builtin_amdgcn_cvt_f32_fp8(pk, 0) * scale;
+      back[1] = __builtin_amdgcn_cvt_f32_fp8(pk, 1) * scale;
+      back[2] = __builtin_amdgcn_cvt_f32_fp8(pk, 2) * scale;
+      back[3] = __builtin_amdgcn_cvt_f32_fp8(pk, 3) * scale;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if (res && base + j < n) res[base + j] = v[j] - back[j];
+      a[j] += w * back[j];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    if (base + j < n) acc[base + j] = a[j] + wsum * g[j];
+}
+
+FA_EXPORT int fa_compress_accumulate(const float* params, int64_t ldp, int C, const float* glob,
+                                     const uint64_t* residual_rows, const float* weights, const int64_t* ids,
+                                     float* acc, int64_t n, int mode, uint64_t seed, hipStream_t stream) {
+  const int64_t nblk = (n + 255) / 256;
+  const dim3 grid((unsigned)((nblk + 3) / 4));
+  if (mode == 0)
+    hipLaunchKernelGGL(compress_accumulate_kernel<0>, grid, dim3(256), 0, stream, params, ldp, C, glob, residual_rows,
+                       weights, ids, acc, n, (uint32_t)seed, (uint32_t)(seed >> 32));
+  else if (mode == 1)
+    hipLaunchKernelGGL(compress_accumulate_kernel<1>, grid, dim3(256), 0, stream, params, ldp, C, glob, residual_rows,
+                       weights, ids, acc, n, (uint32_t)seed, (uint32_t)(seed >> 32));
+  else
+    return -2;
+  return (int)hipGetLastError();
+}
+
 // ---- top-k: radix select over |x| float bits (31 significant bits: 11 + 11 + 9) ----
 // state[0] = prefix bits fixed so far, state[1] = k still to take inside the prefix,
 // state[2] = output cursor, state[3] = tie cursor, state[4] = threshold bits (final)

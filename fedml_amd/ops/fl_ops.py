@@ -303,6 +303,36 @@ def coordinate_median(stack):
 
 
 # ----------------------------------------------------------------------------- K15
+def compress_accumulate(params, glob, residual_rows, weights, ids, method, seed, out):
+    """One launch over the [C, P] client stack: out = Σ_c w_c·(glob + D(C(Δ_c + r_c))) with Δ_c =
+    params[c] − glob, C = block-256 int8 (stochastic rounding keyed by (seed, client id, element)) or
+    fp8-e4m3 quantisation, and the error-feedback rows r_c updated in place (``residual_rows``: list of
+    C fp32 [P] tensors or None). ``weights`` [C] / ``ids`` [C] stay on the device (no host sync)."""
+    mode = {"int8": 0, "fp8": 1}[method]
+    C, P = params.shape[0], glob.numel()
+    if not use_native(params):
+        out.zero_()
+        for c in range(C):
+            r = residual_rows[c] if residual_rows is not None else None
+            d = params[c] - glob
+            back = torch.zeros_like(glob)
+            if mode == 0:
+                q, sc = quantize_int8(d, residual=r, stochastic=True, seed=seed * 1000003 + int(ids[c]))
+                dequantize_int8_axpy(q, sc, 1.0, back)
+            else:
+                q, sc = quantize_fp8(d, residual=r)
+                dequantize_fp8_axpy(q, sc, 1.0, back)
+            out += float(weights[c]) * (glob + back)
+        return out
+    rows = torch.tensor([r.data_ptr() if r is not None else 0 for r in residual_rows] if residual_rows is not None
+                        else [0] * C, dtype=torch.int64).to(params.device, non_blocking=True)
+    rc = _fn("fa_compress_accumulate")(_p(params), _i64(params.stride(0)), _c.c_int(C), _p(glob), _p(rows),
+                                       _p(weights.to(torch.float32).contiguous()), _p(ids.to(torch.int64).contiguous()),
+                                       _p(out), _i64(P), _c.c_int(mode), _u64(seed), _stream(params))
+    _check(rc, "fa_compress_accumulate")
+    return out
+
+
 def quantize_int8(x, residual=None, stochastic=True, seed=0):
     """Block-256 int8 quantisation with optional stochastic rounding and error feedback.
     Returns (q int8 [n], scales f32 [ceil(n/256)]); ``residual`` (if given) is updated to x+r−deq."""

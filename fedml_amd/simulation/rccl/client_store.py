@@ -11,6 +11,25 @@ from typing import Dict, List, Optional
 import torch
 
 
+def _fmix32(x: torch.Tensor) -> torch.Tensor:
+    """murmur3 finaliser on int64 tensors holding 32-bit values (products stay below 2^63)."""
+    m = 0xFFFFFFFF
+    x = x & m
+    x = x ^ (x >> 16)
+    x = (x * 0x85EBCA6B) & m
+    x = x ^ (x >> 13)
+    x = (x * 0xC2B2AE35) & m
+    return x ^ (x >> 16)
+
+
+def hash_uniform(key: int, a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """Deterministic uniform [0, 1) keys from (key, a, b) integer tensors (broadcast): a counter-based
+    hash, so a client's draws do not depend on a generator's position."""
+    h = _fmix32(a.to(torch.int64) * 0x9E3779B1 + (key & 0xFFFFFFFF))
+    h = _fmix32(h + b.to(torch.int64) * 0x7FEB352D)
+    return h.to(torch.float32) * (1.0 / 4294967296.0)
+
+
 class DeviceClientStore:
     def __init__(self, x_all: torch.Tensor, y_all: torch.Tensor, client_offsets: List[int], client_counts: List[int]):
         self.x_all = x_all
@@ -76,13 +95,21 @@ class DeviceClientStore:
 
     # ------------------------------------------------------------------------------------------
     def epoch_order(self, slots: torch.Tensor, n_max: int, generator: Optional[torch.Generator] = None,
-                    shuffle: bool = True) -> torch.Tensor:
-        """Global sample indices [C, n_max] for the given client slots (−1 for padding)."""
+                    shuffle: bool = True, key: Optional[int] = None) -> torch.Tensor:
+        """Global sample indices [C, n_max] for the given client slots (−1 for padding).
+
+        ``key`` (int): shuffle by a counter hash of (key, client id, position) instead of ``generator``
+        — every client's order is then a function of (seed, round, epoch, client) only, independent of
+        which rank / slot trains it (world-size-invariant runs, exact resume from the round index)."""
         C = len(slots)
         counts = self.counts[slots]                           # [C]
         ar = torch.arange(n_max, device=self.device).unsqueeze(0).expand(C, n_max)
         valid = ar < counts.unsqueeze(1)
-        if shuffle:
+        if shuffle and key is not None:
+            keys = hash_uniform(int(key), slots.to(self.device).view(C, 1), ar)
+            keys = torch.where(valid, keys, torch.full_like(keys, 2.0))
+            local = torch.argsort(keys, dim=1)
+        elif shuffle:
             keys = torch.rand(C, n_max, generator=generator, device=self.device)
             keys = torch.where(valid, keys, torch.full_like(keys, 2.0))
             local = torch.argsort(keys, dim=1)

@@ -176,10 +176,12 @@ class ClientBatchEngine:
     # ------------------------------------------------------------------------------------------
     def train(self, store, slots: torch.Tensor, epochs: int, batch_size: int, lr: float,
               generator: Optional[torch.Generator] = None, shuffle: bool = True, valid_slots: Optional[torch.Tensor] = None,
-              loss_scale_by_count: bool = True):
+              loss_scale_by_count: bool = True, rng_key: Optional[int] = None):
         """Run local training for the C client slots (indices into ``store``).
 
-        ``valid_slots`` [C] bool marks real clients (padding slots are never active)."""
+        ``valid_slots`` [C] bool marks real clients (padding slots are never active). ``rng_key``
+        (seed/round-derived int): data order and augmentation are drawn per (key, epoch, client id,
+        sample) — independent of rank and slot — instead of from ``generator``."""
         C = self.C
         counts = store.counts[slots].clone()
         if valid_slots is not None:
@@ -199,7 +201,8 @@ class ClientBatchEngine:
         n_steps = 0
         seq_steps = [0] * C
         for ep in range(int(epochs)):
-            order = store.epoch_order(slots, n_max, generator, shuffle)
+            order = store.epoch_order(slots, n_max, generator, shuffle,
+                                      key=None if rng_key is None else rng_key * 1009 + ep)
             for s in range(steps_per_epoch):
                 lo = s * batch_size
                 b_c = [max(0, min(batch_size, n - lo)) for n in counts_h]
@@ -215,8 +218,12 @@ class ClientBatchEngine:
                 x, y, mask = store.gather(idx)
                 if self.augment and x.dim() == 5:
                     self._aug_calls += 1
-                    x = ops.augment(x.reshape(-1, *x.shape[2:]), seed=int(getattr(self.args, "random_seed", 0)) * 7919
-                                    + self._aug_calls, sample_ids=idx.reshape(-1), pad=self.aug_pad,
+                    # keyed by (rng_key, epoch, step) and the global sample id: the same sample gets the
+                    # same crop/flip/cutout on whichever rank trains its client
+                    aug_seed = ((rng_key * 1009 + ep) * 4099 + s if rng_key is not None else
+                                int(getattr(self.args, "random_seed", 0)) * 7919 + self._aug_calls)
+                    x = ops.augment(x.reshape(-1, *x.shape[2:]), seed=aug_seed & 0x7FFFFFFF,
+                                    sample_ids=idx.reshape(-1), pad=self.aug_pad,
                                     cutout=self.aug_cutout).view_as(x)
                 key_a = tuple(active_list)
                 active = self._active_cache.get(key_a)
@@ -646,40 +653,44 @@ class ClientBatchEngine:
 
     @torch.no_grad()
     def compressed_partial_sum(self, weights: torch.Tensor, global_flat: torch.Tensor, client_ids, residual,
-                               method: str, ratio: float, seed: int, out: Optional[torch.Tensor] = None):
+                               method: str, ratio: float, seed: int, out: Optional[torch.Tensor] = None,
+                               n_upload: Optional[int] = None):
         """Like ``partial_sum`` but each client's update Δ_c = w_c − w_global travels compressed:
         block-256 int8 (stochastic rounding) / fp8-e4m3 quantisation, or exact top-k sparsification,
-        all with per-client error feedback (``residual`` [K_total, P], indexed by client id). The
-        server side decompresses straight into the accumulator (fused dequant-axpy / scatter-axpy
-        kernels): Σ_c n_c·(w_global + D(C(Δ_c))). Returns (out, uploaded_bytes)."""
+        all with per-client error feedback (``residual``: per-client rows indexed by client id —
+        ``residuals.ShardedResiduals`` or a [K_total, P] tensor). int8 / fp8 run as ONE launch over the
+        [C, P] stack with the decompression fused into the accumulation (``ops.compress_accumulate``);
+        top-k selects per client. Returns (out, uploaded_bytes); ``n_upload`` = clients with a non-zero
+        weight (host-known; avoids a device sync for the byte count)."""
         if out is None:
             out = torch.empty(self.P + 1, dtype=torch.float32, device=self.device)
         acc = out[:self.P]
+        w = weights.to(torch.float32)
+        ids = torch.as_tensor([int(c) for c in client_ids], dtype=torch.int64)
+        if method in ("int8", "fp8"):
+            rows = [residual[int(c)] for c in client_ids] if residual is not None else None
+            ops.compress_accumulate(self.params, global_flat, rows, w, ids.to(self.device, non_blocking=True),
+                                    method, seed, acc)
+            out[self.P:].copy_(w.sum().view(1))
+            n = n_upload if n_upload is not None else int((w != 0).sum())
+            nb = (self.P + ((self.P + 255) // 256) * 4) * n
+            return out, nb
+        if method != "topk":
+            raise ValueError(f"unknown compression {method}")
         acc.zero_()
-        w_host = weights.to(torch.float32).tolist()
+        w_host = w.tolist()     # top-k: one host read of the C weights per round
         delta = torch.empty(self.P, dtype=torch.float32, device=self.device)
         nbytes = 0
         k = max(1, int(self.P * ratio))
-        for c, w in enumerate(w_host):
-            if w == 0.0:
+        for c, wc in enumerate(w_host):
+            if wc == 0.0:
                 continue
             r = residual[int(client_ids[c])]
             torch.sub(self.params[c], global_flat, out=delta)
-            if method == "int8":
-                q, sc = ops.quantize_int8(delta, residual=r, stochastic=True, seed=seed * 1000003 + int(client_ids[c]))
-                ops.dequantize_int8_axpy(q, sc, w, acc)
-                nbytes += q.numel() + sc.numel() * 4
-            elif method == "fp8":
-                q, sc = ops.quantize_fp8(delta, residual=r)
-                ops.dequantize_fp8_axpy(q, sc, w, acc)
-                nbytes += q.numel() + sc.numel() * 4
-            elif method == "topk":
-                delta.add_(r)
-                idx, val = ops.topk_abs(delta, k, residual=r)
-                ops.scatter_axpy(idx, val, w, acc)
-                nbytes += k * 8
-            else:
-                raise ValueError(f"unknown compression {method}")
+            delta.add_(r)
+            idx, val = ops.topk_abs(delta, k, residual=r)
+            ops.scatter_axpy(idx, val, wc, acc)
+            nbytes += k * 8
         total = float(sum(w_host))
         acc.add_(global_flat, alpha=total)
         out[self.P:].fill_(total)

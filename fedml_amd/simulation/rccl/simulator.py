@@ -32,6 +32,7 @@ from ...parallel import comm
 from ..common import client_sampling
 from .client_store import DeviceClientStore
 from .engine import ClientBatchEngine
+from .residuals import ShardedResiduals
 
 
 def _dtype(name):
@@ -78,7 +79,8 @@ class RCCLSimulator:
         # update compression (north-star config: FedOpt + int8/fp8/top-k with error feedback)
         self.compression = str(getattr(args, "compression", "") or "").lower() or None
         self.compress_ratio = float(getattr(args, "compression_ratio", 0.01) or 0.01)
-        self.residual = torch.zeros(self.K_total, self.layout.size, dtype=torch.float32, device=self.device) \
+        # error-feedback residuals: one row per client, on the rank that trains it (residuals.py)
+        self.residual = ShardedResiduals(self.layout.size, self.device, self.rank, self.world) \
             if self.compression else None
         self.upload_bytes: List[int] = []
         self.faults = FaultInjector(args)
@@ -92,6 +94,7 @@ class RCCLSimulator:
         counts = [self.sample_counts[i] for i in ids]
         packs = pack_clients_to_gpus(counts, self.world)
         mine = [ids[j] for j in packs[self.rank]]
+        self.round_owner = {int(ids[j]): r for r, pk in enumerate(packs) for j in pk}   # client → rank
         return ids, mine
 
     def run_round(self, round_idx: int):
@@ -106,11 +109,18 @@ class RCCLSimulator:
                 valid[i] = True
             slots = slots.to(self.device)
             valid = valid.to(self.device)
+        if self.residual is not None:
+            with tr.span("round.residual_migrate"):
+                self.residual.migrate(self.round_owner)
         with tr.span("round.broadcast_local"):
             self.engine.load_global(self.global_flat)
         with tr.span("round.local_train"):
+            # data order / augmentation keyed by (seed, round, client): identical for any world size and
+            # exactly reproducible on resume from the round index alone
+            rng_key = (int(getattr(args, "random_seed", 0)) * 1000003 + int(round_idx) * 7919) & 0x7FFFFFFF
             self.engine.train(self.store, slots, int(args.epochs), int(args.batch_size), float(args.learning_rate),
-                              generator=self.gen, shuffle=bool(getattr(args, "shuffle", True)), valid_slots=valid)
+                              generator=self.gen, shuffle=bool(getattr(args, "shuffle", True)), valid_slots=valid,
+                              rng_key=rng_key)
         with tr.span("round.aggregate"):
             w = torch.where(valid, self.store.counts[slots].to(torch.float32), torch.zeros(self.C, device=self.device))
             if self.faults.active:
@@ -123,8 +133,10 @@ class RCCLSimulator:
             self._robust_preaggregate(w)
             if self.compression:
                 ids = list(mine) + [0] * (self.C - len(mine))
+                n_up = len(mine) if not self.faults.active else int(keep.sum())
                 _, nb = self.engine.compressed_partial_sum(w, self.global_flat, ids, self.residual, self.compression,
-                                                           self.compress_ratio, round_idx, out=self.partial)
+                                                           self.compress_ratio, round_idx, out=self.partial,
+                                                           n_upload=n_up)
                 self.upload_bytes.append(nb)
             else:
                 self.engine.partial_sum(w, out=self.partial)
@@ -209,13 +221,15 @@ class RCCLSimulator:
 
     def save_checkpoint(self, directory):
         from ...core.checkpoint import save_round_checkpoint
+        # per-run state beyond the global model: the clients' error-feedback residuals of compressed
+        # updates (gathered from their owning ranks — every rank takes part). Data order and
+        # augmentation are keyed by (seed, round, client), so the round index alone resumes them exactly
+        # at any world size; the legacy generator state is kept for readers of the checkpoint layout.
+        dense = self.residual.dense(self.K_total) if self.residual is not None else None
         if self.rank == 0:
-            # per-run state beyond the global model: the shuffle generator (an identical data order
-            # after resume) and the clients' error-feedback residuals of compressed updates
-            # (single-rank layout; multi-rank runs re-derive shuffles per rank from the seed)
             clients = {"gen": self.gen.get_state()}
-            if self.residual is not None:
-                clients["residual"] = self.residual.detach().cpu()
+            if dense is not None:
+                clients["residual"] = dense.detach().cpu()
             save_round_checkpoint(directory, self.round_idx, self.global_model_state(), self.args,
                                   server_opt=self.server_opt.state_dict() if self.server_opt else None,
                                   clients=clients)
@@ -230,7 +244,9 @@ class RCCLSimulator:
         if cl.get("gen") is not None and self.world == 1:
             self.gen.set_state(cl["gen"])
         if cl.get("residual") is not None and self.residual is not None:
-            self.residual.copy_(cl["residual"].to(self.device))
+            # rows go to the rank that trains each client in the resumed round
+            self.assignment(int(ck["round"]) + 1)
+            self.residual.load_dense(cl["residual"], self.round_owner)
         self.round_idx = int(ck["round"]) + 1
         return self.round_idx
 

@@ -5,7 +5,7 @@ import sys
 import torch
 
 
-def run(rank, world, port, out_path, model_name, clients, counts_seed):
+def run(rank, world, port, out_path, model_name, clients, counts_seed, shuffle=False, augment=False):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     torch.set_num_threads(2)
@@ -19,9 +19,11 @@ def run(rank, world, port, out_path, model_name, clients, counts_seed):
     model_arg = "resnet56" if model_name == "resnet_shallow" else model_name
     args = Arguments.from_dict({"x": {
         "training_type": "simulation", "backend": "RCCL", "federated_optimizer": "FedAvg", "dataset": ds,
-        "model": model_arg, "client_num_in_total": clients, "client_num_per_round": clients, "comm_round": 2,
+        "model": model_arg, "client_num_in_total": clients, "comm_round": 2,
         "epochs": 1, "batch_size": 8, "client_optimizer": "sgd", "learning_rate": 0.05, "frequency_of_the_test": 0,
-        "random_seed": 0, "shuffle": False}})
+        "random_seed": 0, "shuffle": shuffle, "data_augmentation": augment and ds == "cifar10",
+        "compression": os.environ.get("FEDML_TEST_COMPRESSION", ""),
+        "client_num_per_round": int(os.environ.get("FEDML_TEST_PER_ROUND", clients))}})
     spec = get_spec(ds)
     torch.manual_seed(0)
     if model_name == "resnet_shallow":  # deep ResNets at init are chaotic in fp32 (see test_batched_engine)
@@ -33,7 +35,7 @@ def run(rank, world, port, out_path, model_name, clients, counts_seed):
     counts = [int(v) for v in torch.randint(8, 24, (clients,), generator=g)]
     store = DeviceClientStore.synthetic_on_device(spec, counts, torch.device("cpu"), seed=0)
     sim = RCCLSimulator(args, torch.device("cpu"), None, model, store=store)
-    sim.run(2)
+    sim.run(int(os.environ.get("FEDML_TEST_ROUNDS", "2")))
     if rank == 0:
         torch.save(sim.global_flat.clone(), out_path)
     comm.destroy()
@@ -41,4 +43,5 @@ def run(rank, world, port, out_path, model_name, clients, counts_seed):
 
 if __name__ == "__main__":
     r, w, p = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
-    run(r, w, p, sys.argv[4], sys.argv[5], int(sys.argv[6]), int(sys.argv[7]))
+    run(r, w, p, sys.argv[4], sys.argv[5], int(sys.argv[6]), int(sys.argv[7]),
+        shuffle=len(sys.argv) > 8 and sys.argv[8] == "1", augment=len(sys.argv) > 9 and sys.argv[9] == "1")

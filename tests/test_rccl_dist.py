@@ -1,6 +1,7 @@
 """Multi-process RCCL-simulator path rehearsed on CPU with gloo: the global model after N rounds
 must not depend on how many ranks the clients were packed onto (the all-reduced partial sums
-Σ n_c·w_c ‖ Σ n_c are order-independent up to fp32 summation)."""
+Σ n_c·w_c ‖ Σ n_c are order-independent up to fp32 summation) — with data shuffling and
+augmentation ON: both are keyed by (seed, round, client id), never by rank or slot."""
 import os
 import socket
 import subprocess
@@ -20,21 +21,41 @@ def _free_port():
     return p
 
 
-def _launch(world, out, model, clients):
+def _launch(world, out, model, clients, shuffle=False, augment=False, **extra_env):
     port = _free_port()
-    env = dict(os.environ, PYTHONPATH=os.path.dirname(HERE), OMP_NUM_THREADS="2")
+    env = dict(os.environ, PYTHONPATH=os.path.dirname(HERE), OMP_NUM_THREADS="2", **extra_env)
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker_rccl_sim.py"), str(r), str(world),
-                               str(port), out, model, str(clients), "3"], env=env)
+                               str(port), out, model, str(clients), "3", "1" if shuffle else "0",
+                               "1" if augment else "0"], env=env)
              for r in range(world)]
     codes = [p.wait(timeout=600) for p in procs]
     assert codes == [0] * world, codes
     return torch.load(out, weights_only=True)
 
 
-@pytest.mark.parametrize("model,clients", [("lr", 7), ("resnet_shallow", 3)])
-def test_rccl_sim_world_size_invariance(tmp_path, model, clients):
-    w1 = _launch(1, str(tmp_path / "w1.pt"), model, clients)
-    w2 = _launch(2, str(tmp_path / "w2.pt"), model, clients)
+@pytest.mark.parametrize("model,clients,shuffle", [("lr", 7, False), ("lr", 7, True), ("resnet_shallow", 3, True)])
+def test_rccl_sim_world_size_invariance(tmp_path, model, clients, shuffle):
+    aug = model == "resnet_shallow"
+    w1 = _launch(1, str(tmp_path / "w1.pt"), model, clients, shuffle, aug)
+    w2 = _launch(2, str(tmp_path / "w2.pt"), model, clients, shuffle, aug)
     assert w1.shape == w2.shape
     rel = float((w1 - w2).norm() / w1.norm())
     assert rel < (1e-5 if model == "lr" else 1e-3), rel
+
+
+def test_rccl_sim_world_size_invariance_4_ranks(tmp_path):
+    w1 = _launch(1, str(tmp_path / "w1.pt"), "lr", 9, True)
+    w4 = _launch(4, str(tmp_path / "w4.pt"), "lr", 9, True)
+    assert float((w1 - w4).norm() / w1.norm()) < 1e-5
+
+
+@pytest.mark.parametrize("method", ["int8", "topk"])
+def test_compressed_partial_participation_world_size_invariance(tmp_path, method):
+    """Compressed updates with error feedback and 4 of 9 clients per round: clients move between ranks
+    from round to round, so their residual rows migrate point-to-point (residuals.ShardedResiduals); the
+    4-round result equals the single-rank run."""
+    env = dict(FEDML_TEST_COMPRESSION=method, FEDML_TEST_PER_ROUND="4", FEDML_TEST_ROUNDS="4")
+    w1 = _launch(1, str(tmp_path / "w1.pt"), "lr", 9, True, **env)
+    w2 = _launch(2, str(tmp_path / "w2.pt"), "lr", 9, True, **env)
+    # fp32 summation order only (a lost or stale residual row moves the result by > 1e-2)
+    assert float((w1 - w2).norm() / w1.norm()) < 1e-4

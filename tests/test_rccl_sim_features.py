@@ -80,7 +80,8 @@ def test_topk_error_feedback_converges():
     comp = RCCLSimulator(_args(compression="topk", compression_ratio=0.05, comm_round=8), torch.device("cpu"), None,
                          model, store=_store(spec))
     comp.run(8)
-    assert float(comp.residual.abs().sum()) > 0  # the unsent mass is carried, not dropped
+    assert float(comp.residual.dense(comp.K_total).abs().sum()) > 0  # the unsent mass is carried, not dropped
+    assert comp.residual.nbytes() == 6 * comp.layout.size * 4   # one row per client (single rank)
     acc, _ = comp.engine.evaluate(comp.store, torch.arange(6), 64)
     assert float(acc.mean()) > 0.3
 
