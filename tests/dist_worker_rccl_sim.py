@@ -23,6 +23,7 @@ def run(rank, world, port, out_path, model_name, clients, counts_seed, shuffle=F
         "epochs": 1, "batch_size": 8, "client_optimizer": "sgd", "learning_rate": 0.05, "frequency_of_the_test": 0,
         "random_seed": 0, "shuffle": shuffle, "data_augmentation": augment and ds == "cifar10",
         "compression": os.environ.get("FEDML_TEST_COMPRESSION", ""),
+        "allreduce_bucket_mb": float(os.environ.get("FEDML_TEST_BUCKET_MB", "32")),
         "client_num_per_round": int(os.environ.get("FEDML_TEST_PER_ROUND", clients))}})
     spec = get_spec(ds)
     torch.manual_seed(0)

@@ -59,3 +59,11 @@ def test_compressed_partial_participation_world_size_invariance(tmp_path, method
     w2 = _launch(2, str(tmp_path / "w2.pt"), "lr", 9, True, **env)
     # fp32 summation order only (a lost or stale residual row moves the result by > 1e-2)
     assert float((w1 - w2).norm() / w1.norm()) < 1e-4
+
+
+def test_bucketed_aggregation_matches_single_rank(tmp_path):
+    """The pipelined per-bucket weighted sum + async all-reduce (large-model path; here 0.01 MB buckets
+    over the 7,850-parameter LR model → 3 buckets) equals the single-rank aggregate."""
+    w1 = _launch(1, str(tmp_path / "w1.pt"), "lr", 7, True)
+    w2 = _launch(2, str(tmp_path / "w2.pt"), "lr", 7, True, FEDML_TEST_BUCKET_MB="0.01")
+    assert float((w1 - w2).norm() / w1.norm()) < 1e-5
