@@ -66,15 +66,18 @@ class InProcessBroker:
 
 
 class PahoBroker:  # pragma: no cover - needs paho-mqtt + a running broker
-    def __init__(self, host, port=1883, keepalive=180):
+    def __init__(self, host, port=1883, keepalive=180, username=None, password=None):
         import paho.mqtt.client as mqtt
         self._mqtt = mqtt
         self.host, self.port, self.keepalive = host, port, keepalive
+        self.username, self.password = username, password
         self._clients = {}
         self._subs = defaultdict(list)
 
     def connect(self, client_id, will_topic=None, will_payload=None):
         c = self._mqtt.Client(client_id=client_id, clean_session=True)
+        if self.username:   # brokers that require a login (the reference's cloud mqtt_config)
+            c.username_pw_set(self.username, self.password)
         if will_topic:
             c.will_set(will_topic, payload=will_payload, qos=0, retain=True)
 
@@ -145,19 +148,34 @@ class LocalBlobStore:
 
 
 _DEFAULT_BROKERS = {}
+_DEFAULT_STORES = {}
+
+
+def shared_inproc_broker(run_id="0") -> "InProcessBroker":
+    """The process-wide in-process broker of a run (server and clients built in one process share it)."""
+    return _DEFAULT_BROKERS.setdefault(str(run_id), InProcessBroker())
+
+
+def shared_memory_store(run_id="0") -> "MemoryBlobStore":
+    return _DEFAULT_STORES.setdefault(str(run_id), MemoryBlobStore())
+
+
+def backends_for(args, rank: int = 0, size: int = 1, need_blob: bool = True):
+    """(broker, blob_store) for the MQTT backends, resolved through ``core.mlops.MLOpsConfigs``
+    (args > mlops_config_path file > FEDML_AMD_MQTT/S3_CONFIG env > local config server > in-process
+    defaults) — the reference's ``MLOpsConfigs.get_instance(args).fetch_configs()`` call in its
+    MQTT_S3 client / server managers (``cross_silo/client/fedml_client_manager.py:39``)."""
+    from ...mlops.mlops_configs import MLOpsConfigs
+    return MLOpsConfigs(args).build_backends(rank, size, str(getattr(args, "run_id", "0") if args is not None else "0"),
+                                              need_blob=need_blob)
 
 
 def default_broker(args=None):
-    host = getattr(args, "mqtt_host", None) if args is not None else None
-    if host:
-        return PahoBroker(host, int(getattr(args, "mqtt_port", 1883)))
-    key = str(getattr(args, "run_id", "0")) if args is not None else "0"
-    return _DEFAULT_BROKERS.setdefault(key, InProcessBroker())
+    return backends_for(args, need_blob=False)[0]
 
 
 def default_blob_store(args=None):
-    root = getattr(args, "blob_store_dir", None) if args is not None else None
-    return LocalBlobStore(root) if root else MemoryBlobStore()
+    return backends_for(args)[1]
 
 
 class MqttS3CommManager(QueueCommManager):

@@ -295,8 +295,9 @@ def create_comm_manager(backend: str, rank: int, size: int, args=None, router: L
         return TRPCCommManager(rank, size, getattr(args, "trpc_master_addr", "127.0.0.1"),
                                int(getattr(args, "trpc_master_port", 29600)))
     if b in ("MQTT", "MQTT_S3", "MQTT_S3_MNN"):
-        from .pubsub import MqttS3CommManager, default_broker, default_blob_store
-        return MqttS3CommManager(default_broker(args), default_blob_store(args) if b != "MQTT" else None, rank,
+        from .pubsub import MqttS3CommManager, backends_for
+        broker, store = backends_for(args, rank, size, need_blob=(b != "MQTT"))
+        return MqttS3CommManager(broker, store, rank,
                                  size, run_id=str(getattr(args, "run_id", "0")), file_mode=(b == "MQTT_S3_MNN"),
                                  file_cache_dir=os.path.join(getattr(args, "model_file_cache_folder", None)
                                                              or "./model_file_cache", f"rank{rank}"))

@@ -54,8 +54,18 @@ class MLOpsConfigs:
     # -- sources ------------------------------------------------------------------------------------
     def _from_args(self) -> Tuple[Optional[dict], Optional[dict]]:
         a = self.args
-        return (getattr(a, "customized_training_mqtt_config", None) if a is not None else None,
-                getattr(a, "customized_training_s3_config", None) if a is not None else None)
+        if a is None:
+            return None, None
+        mqtt = getattr(a, "customized_training_mqtt_config", None)
+        s3 = getattr(a, "customized_training_s3_config", None)
+        # short-hand YAML keys of this framework's cross-silo configs (mqtt_host / blob_store_dir)
+        if mqtt is None and getattr(a, "mqtt_host", None):
+            mqtt = {"BROKER_HOST": a.mqtt_host, "BROKER_PORT": int(getattr(a, "mqtt_port", 1883) or 1883),
+                    "MQTT_KEEPALIVE": int(getattr(a, "mqtt_keepalive", 180) or 180),
+                    "MQTT_USER": getattr(a, "mqtt_user", None), "MQTT_PWD": getattr(a, "mqtt_pwd", None)}
+        if s3 is None and getattr(a, "blob_store_dir", None):
+            s3 = {"BUCKET_NAME": "fedml", "LOCAL_ROOT": a.blob_store_dir, "RUN_SUBDIR": False}
+        return mqtt, s3
 
     def _from_file(self) -> Tuple[Optional[dict], Optional[dict]]:
         path = getattr(self.args, "mlops_config_path", None) if self.args is not None else None
@@ -81,8 +91,10 @@ class MLOpsConfigs:
         try:
             with urllib.request.urlopen(req, timeout=5) as r:
                 body = json.loads(r.read().decode())
-        except OSError:
-            return None, None
+        except (OSError, ValueError) as e:
+            # the reference raises here too: a deployment that asked for the local config server must not
+            # fall back to per-process in-memory brokers (it would hang with no error)
+            raise RuntimeError(f"config_version 'local': config server {LOCAL_CONFIG_URL} unavailable ({e})") from e
         if body.get("code") != "SUCCESS":
             raise RuntimeError("failed to fetch device configurations from the local config server")
         data = body.get("data") or {}
@@ -100,13 +112,26 @@ class MLOpsConfigs:
         return (mqtt if mqtt is not None else default_mqtt_config(),
                 s3 if s3 is not None else default_s3_config(getattr(self.args, "blob_root", None)))
 
-    def build_backends(self, rank: int = 0, size: int = 1, run_id: str = "0"):
-        """Instantiate (broker, blob_store) from the resolved configs: in-process broker + local
-        blob directory by default; a paho MQTT broker when ``BROKER_HOST`` names a host."""
-        from ..distributed.communication.pubsub import InProcessBroker, LocalBlobStore, PahoBroker
+    def build_backends(self, rank: int = 0, size: int = 1, run_id: str = "0", need_blob: bool = True):
+        """Instantiate (broker, blob_store) from the resolved configs. ``BROKER_HOST: inproc`` → the
+        process-wide in-process broker of this run id (shared by every server / client manager built
+        in the process); a host name → a paho MQTT client with the configured credentials. The blob
+        store is a local directory when one is configured (``LOCAL_ROOT``; a per-run subdirectory unless
+        ``RUN_SUBDIR: false``), else the process-wide in-memory store of the run."""
+        from ..distributed.communication.pubsub import LocalBlobStore, PahoBroker, shared_inproc_broker, shared_memory_store
         mqtt, s3 = self.fetch_configs()
         host = mqtt.get("BROKER_HOST", "inproc")
-        broker = InProcessBroker() if host in (None, "", "inproc") else PahoBroker(host, int(mqtt.get("BROKER_PORT", 1883)),
-                                                                                  int(mqtt.get("MQTT_KEEPALIVE", 180)))
-        root = s3.get("LOCAL_ROOT") or default_s3_config()["LOCAL_ROOT"]
-        return broker, LocalBlobStore(os.path.join(root, str(run_id)))
+        if host in (None, "", "inproc"):
+            broker = shared_inproc_broker(run_id)
+        else:
+            broker = PahoBroker(host, int(mqtt.get("BROKER_PORT", 1883) or 1883), int(mqtt.get("MQTT_KEEPALIVE", 180) or 180),
+                                username=mqtt.get("MQTT_USER"), password=mqtt.get("MQTT_PWD"))
+        if not need_blob:
+            return broker, None
+        explicit = any(src()[1] is not None for src in (self._from_args, self._from_file, self._from_env))
+        if explicit and s3.get("LOCAL_ROOT"):
+            root = s3["LOCAL_ROOT"] if s3.get("RUN_SUBDIR", True) is False else os.path.join(s3["LOCAL_ROOT"], str(run_id))
+            return broker, LocalBlobStore(root)
+        if getattr(self.args, "blob_root", None):
+            return broker, LocalBlobStore(os.path.join(self.args.blob_root, str(run_id)))
+        return broker, shared_memory_store(run_id)

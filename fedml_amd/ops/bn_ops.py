@@ -77,6 +77,9 @@ class _BNAct(torch.autograd.Function):
         if dy.data_ptr() % 16:
             dy = dy.clone(memory_format=_CL)
         C, M = x.shape[1], ctx.M
+        # the backward sums are accumulated atomically into acc[2C:]: zero them on EVERY backward (a second
+        # backward through a retained graph must not add onto the first one's sums)
+        acc[2 * C:].zero_()
         dx = torch.empty_like(x, memory_format=_CL)
         dres = torch.empty_like(x, memory_format=_CL) if (ctx.has_res and ctx.relu) else None
         dw = torch.empty(C, dtype=torch.float32, device=x.device) if weight is not None else None

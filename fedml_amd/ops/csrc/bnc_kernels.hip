@@ -55,18 +55,24 @@ __device__ __forceinline__ void reduce_to_acc(const float* a, const float* b, in
   }
 }
 
+// Shifted sums: every block accumulates Σ(x − k), Σ(x − k)² with the per-channel pivot k = x[row 0]
+// (read by every block, so all partial sums share it): the variance then has no E[x²] − mean²
+// cancellation when |mean| ≫ std.
 __global__ __launch_bounds__(kThreads) void stats_kernel(const uint4* __restrict__ x, int64_t M, int cg,
                                                          float* __restrict__ acc) {
   __shared__ float red[16 * kThreads];
   const int j = threadIdx.x % cg, rpb = kThreads / cg;
+  float piv[8];
+  unpack8(x[j], piv);
   float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, q[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   for (int64_t r = (int64_t)blockIdx.x * rpb + threadIdx.x / cg; r < M; r += (int64_t)gridDim.x * rpb) {
     float f[8];
     unpack8(x[r * cg + j], f);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      s[k] += f[k];
-      q[k] = fmaf(f[k], f[k], q[k]);
+      const float d = f[k] - piv[k];
+      s[k] += d;
+      q[k] = fmaf(d, d, q[k]);
     }
   }
   reduce_to_acc(s, q, cg, acc, red);
@@ -85,9 +91,11 @@ __global__ __launch_bounds__(kThreads) void apply_kernel(const uint4* __restrict
   float* sh = sc + C;
   const float inv_m = 1.f / (float)M;
   const float unbias = M > 1 ? (float)M / (float)(M - 1) : 1.f;
+  const uint16_t* x16 = reinterpret_cast<const uint16_t*>(x);   // row 0 = the statistics pivot
   for (int c = threadIdx.x; c < C; c += kThreads) {
-    const float mean = acc[c] * inv_m;
-    const float var = fmaxf(acc[C + c] * inv_m - mean * mean, 0.f);
+    const float dm = acc[c] * inv_m;                              // mean of (x − k)
+    const float mean = bf16_to_f32(x16[c]) + dm;
+    const float var = fmaxf(acc[C + c] * inv_m - dm * dm, 0.f);
     const float inv = rsqrtf(var + eps);
     const float s = w ? w[c] * inv : inv;
     sc[c] = s;

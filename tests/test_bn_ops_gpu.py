@@ -78,3 +78,37 @@ def test_bnc_resnet18_no_worse_than_module_path(monkeypatch):
         assert ef <= 1.5 * em + 2e-2, (ef, em)
     torch.testing.assert_close(models[0].layer4[1].bn2.running_var, models[2].layer4[1].bn2.running_var,
                                atol=1e-2, rtol=2e-2)
+
+
+def test_bnc_large_mean_offset():
+    """mean 50, std 0.5 (bf16 input): the shifted statistics sums keep the variance accurate — the
+    E[x²] − mean² form loses it to cancellation."""
+    torch.manual_seed(3)
+    dev = "cuda"
+    C = 64
+    bn = nn.BatchNorm2d(C).to(dev).train()
+    ref = nn.BatchNorm2d(C).to(dev).train()
+    ref.load_state_dict(bn.state_dict())
+    x = (torch.randn(16, C, 16, 16, device=dev) * 0.5 + 50.0).to(torch.bfloat16) \
+        .contiguous(memory_format=torch.channels_last)
+    y = bn_ops.batch_norm_act(bn, x, relu=False)
+    yf = ref(x.float())
+    torch.testing.assert_close(y.float(), yf, atol=5e-2, rtol=2e-2)
+    torch.testing.assert_close(bn.running_var, ref.running_var, atol=1e-4, rtol=2e-3)
+    torch.testing.assert_close(bn.running_mean, ref.running_mean, atol=1e-3, rtol=1e-4)
+
+
+def test_bnc_backward_twice_with_retained_graph():
+    """A second backward through a retained graph (gradient-penalty style ClientTrainers) gives the same
+    gradients as the first: the atomic backward sums are zeroed per backward."""
+    torch.manual_seed(4)
+    dev = "cuda"
+    bn = nn.BatchNorm2d(64).to(dev).train()
+    x = torch.randn(8, 64, 8, 8, device=dev).to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    x.requires_grad_(True)
+    y = bn_ops.batch_norm_act(bn, x, relu=True)
+    dy = torch.randn_like(y)
+    gx1, gw1 = torch.autograd.grad(y, (x, bn.weight), dy, retain_graph=True)
+    gx2, gw2 = torch.autograd.grad(y, (x, bn.weight), dy)
+    torch.testing.assert_close(gx1, gx2)
+    torch.testing.assert_close(gw1, gw2)

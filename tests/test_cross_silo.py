@@ -126,3 +126,66 @@ def test_fault_injector_and_rccl_sim_dropout():
     g0 = sim.global_flat.clone()
     sim.run(1)
     assert torch.equal(sim.global_flat, g0) and sim.dropped_clients == [4]
+
+
+def test_horizontal_cross_silo_over_mqtt_s3_from_config_file(tmp_path, monkeypatch):
+    """Server + 2 silos over MQTT_S3 whose broker and blob store come from an mlops config file
+    (reference: MLOpsConfigs.fetch_configs in the MQTT_S3 managers): in-process broker shared by the run,
+    model payloads through the configured blob directory; result equals the loopback run."""
+    from fedml_amd.core.mlops import MLOpsConfigs
+    from fedml_amd.cross_silo import Client, Server
+    monkeypatch.delenv("FEDML_AMD_MQTT_CONFIG", raising=False)
+    monkeypatch.delenv("FEDML_AMD_S3_CONFIG", raising=False)
+    MLOpsConfigs.reset()
+    cfg = tmp_path / "mlops.yaml"
+    cfg.write_text(f"mqtt_config:\n  BROKER_HOST: inproc\ns3_config:\n  LOCAL_ROOT: {tmp_path / 'blobs'}\n")
+    a = _args(backend="MQTT_S3", mlops_config_path=str(cfg), run_id="mq1")
+    dev, ds, m = fedml_amd._prepare(fedml_amd.init(copy.copy(a)))
+    out = {}
+
+    def srv():
+        b = copy.copy(a)
+        b.rank = 0
+        out["w"] = Server(b, dev, ds, copy.deepcopy(m)).run()
+
+    def cli(rank):
+        b = copy.copy(a)
+        b.rank = rank
+        Client(b, dev, ds, copy.deepcopy(m)).run()
+
+    ts = [threading.Thread(target=srv)] + [threading.Thread(target=cli, args=(r,)) for r in (1, 2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    assert "w" in out
+    blobs = list((tmp_path / "blobs" / "mq1").iterdir())
+    assert blobs, "model payloads did not go through the configured blob store"
+    la = _args()
+    router = LoopbackRouter(3)
+    ref = {}
+
+    def srv2():
+        ref["w"] = Server(copy.copy(la), dev, ds, copy.deepcopy(m), comm=router).run()
+
+    def cli2(rank):
+        b = copy.copy(la)
+        b.rank = rank
+        Client(b, dev, ds, copy.deepcopy(m), comm=router).run()
+
+    ts = [threading.Thread(target=srv2)] + [threading.Thread(target=cli2, args=(r,)) for r in (1, 2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=120)
+    for k in ref["w"]:
+        assert torch.allclose(ref["w"][k].float(), out["w"][k].float(), atol=1e-6), k
+    MLOpsConfigs.reset()
+
+
+def test_mlops_config_local_server_unreachable_raises():
+    import types
+    from fedml_amd.core.mlops import MLOpsConfigs
+    args = types.SimpleNamespace(config_version="local")
+    with pytest.raises(RuntimeError):
+        MLOpsConfigs(args).fetch_configs()
