@@ -75,17 +75,83 @@ __global__ __launch_bounds__(256) void pack_weights_kernel(const float* __restri
   }
 }
 
-FA_EXPORT int fa_pack_weights(const float* arena, int64_t ldw, const void* segs_dev, int nseg, uint16_t* dst,
-                              int64_t dst_ld, int C, hipStream_t stream) {
-  hipLaunchKernelGGL(pack_weights_kernel<BF16>, dim3(16, C, nseg), dim3(256), 0, stream, arena, ldw,
-                     (const PackSeg*)segs_dev, nseg, dst, dst_ld);
+// Tiled packing: one workgroup moves a 32 (co) × 32 (ci) × taps block through LDS — coalesced
+// reads of the OIHW rows, coalesced writes of both GEMM layouts (k = tap·cin + ci rows of Wf, and
+// the co-contiguous rows of Wb, a transpose). The element-wise kernel above reads OIHW with a stride
+// of `taps` floats and issues one integer division chain per element (ResNet-18: 1.45 ms per step).
+constexpr int PK_T = 32;
+constexpr int PK_MAXTAPS = 9;
+
+template <class P>
+__global__ __launch_bounds__(256) void pack_weights_tiled_kernel(const float* __restrict__ arena, int64_t ldw,
+                                                                 const PackSeg* __restrict__ segs,
+                                                                 typename P::T* __restrict__ dst, int64_t dst_ld) {
+  using T = typename P::T;
+  __shared__ float tile[PK_T][PK_T * PK_MAXTAPS + 1];
+  const int c = blockIdx.y;
+  const PackSeg s = segs[blockIdx.z];
+  const int taps = s.kh * s.kw;
+  const int nco = (s.cout + PK_T - 1) / PK_T, nci = (s.cin + PK_T - 1) / PK_T;
+  if ((int)blockIdx.x >= nco * nci) return;
+  const int co0 = (blockIdx.x / nci) * PK_T, ci0 = (blockIdx.x % nci) * PK_T;
+  const int tco = min(PK_T, s.cout - co0), tci = min(PK_T, s.cin - ci0);
+  const float* w = arena + (int64_t)c * ldw + s.src_off;
+  // load: row co holds (ci, tap) pairs ci0.. contiguous in the source (ci < cin_src; padding → 0)
+  const int rowlen = tci * taps;
+  for (int i = threadIdx.x; i < tco * rowlen; i += 256) {
+    const int r = i / rowlen, q = i - r * rowlen;
+    const int ci = ci0 + q / taps;
+    tile[r][q] = ci < s.cin_src ? w[((int64_t)(co0 + r) * s.cin_src + ci0) * taps + q] : 0.f;
+  }
+  __syncthreads();
+  T* df = dst + (int64_t)c * dst_ld + s.dst_f;
+  // Wf[co][tap·cin + ci]: ci fastest
+  for (int i = threadIdx.x; i < tco * taps * tci; i += 256) {
+    const int ci = i % tci, rt = i / tci;
+    const int tap = rt % taps, r = rt / taps;
+    df[(int64_t)(co0 + r) * s.ldk + tap * s.cin + ci0 + ci] = P::from_f(tile[r][ci * taps + tap]);
+  }
+  if (ci0 == 0) {   // zero the K padding of these rows
+    const int kp = s.ldk - taps * s.cin;
+    for (int i = threadIdx.x; i < tco * kp; i += 256)
+      df[(int64_t)(co0 + i / kp) * s.ldk + taps * s.cin + i % kp] = P::from_f(0.f);
+  }
+  if (s.dst_b >= 0) {
+    T* db = dst + (int64_t)c * dst_ld + s.dst_b;
+    // Wb[ci][tap·cout + co]: co fastest
+    for (int i = threadIdx.x; i < tci * taps * tco; i += 256) {
+      const int r = i % tco, ct = i / tco;
+      const int tap = ct % taps, ci = ct / taps;
+      db[(int64_t)(ci0 + ci) * s.ldk2 + tap * s.cout + co0 + r] = P::from_f(tile[r][ci * taps + tap]);
+    }
+    if (co0 == 0) {
+      const int kp = s.ldk2 - taps * s.cout;
+      for (int i = threadIdx.x; i < tci * kp; i += 256)
+        db[(int64_t)(ci0 + i / kp) * s.ldk2 + taps * s.cout + i % kp] = P::from_f(0.f);
+    }
+  }
+}
+
+// max_tiles: the largest ceil(cout/32)·ceil(cin/32) over the segments (0 → the element-wise kernel)
+template <class P>
+static int pack_weights(const float* arena, int64_t ldw, const void* segs_dev, int nseg, typename P::T* dst,
+                        int64_t dst_ld, int C, int max_tiles, int max_taps, hipStream_t stream) {
+  if (max_tiles > 0 && max_taps <= PK_MAXTAPS && max_tiles <= 65535)
+    hipLaunchKernelGGL(pack_weights_tiled_kernel<P>, dim3(max_tiles, C, nseg), dim3(256), 0, stream, arena, ldw,
+                       (const PackSeg*)segs_dev, dst, dst_ld);
+  else
+    hipLaunchKernelGGL(pack_weights_kernel<P>, dim3(16, C, nseg), dim3(256), 0, stream, arena, ldw,
+                       (const PackSeg*)segs_dev, nseg, dst, dst_ld);
   return (int)hipGetLastError();
 }
+
+FA_EXPORT int fa_pack_weights(const float* arena, int64_t ldw, const void* segs_dev, int nseg, uint16_t* dst,
+                              int64_t dst_ld, int C, int max_tiles, int max_taps, hipStream_t stream) {
+  return pack_weights<BF16>(arena, ldw, segs_dev, nseg, dst, dst_ld, C, max_tiles, max_taps, stream);
+}
 FA_EXPORT int fa_pack_weights_f32(const float* arena, int64_t ldw, const void* segs_dev, int nseg, float* dst,
-                                  int64_t dst_ld, int C, hipStream_t stream) {
-  hipLaunchKernelGGL(pack_weights_kernel<F32>, dim3(16, C, nseg), dim3(256), 0, stream, arena, ldw,
-                     (const PackSeg*)segs_dev, nseg, dst, dst_ld);
-  return (int)hipGetLastError();
+                                  int64_t dst_ld, int C, int max_tiles, int max_taps, hipStream_t stream) {
+  return pack_weights<F32>(arena, ldw, segs_dev, nseg, dst, dst_ld, C, max_tiles, max_taps, stream);
 }
 
 // =====================================================================================
@@ -380,6 +446,339 @@ static size_t conv_smem_bytes(int nout, int ldk, int kc) {
   return (size_t)nout * ldk * P::ES + (size_t)3 * kc * 4 + (size_t)4 * nout * 3 * 4 + (size_t)4 * 16 * nout * P::ES;
 }
 
+// =====================================================================================
+// K-streamed implicit GEMM for WIDE layers (ResNet-18: 128–512 channels, K = 9·Cin up to 4608).
+//
+// conv_gemm_kernel keeps the whole [NOUT][K] weight slice resident in LDS, which stops fitting
+// (fp32: 64 × 4608 × 4 B = 1.2 MB) or leaves one workgroup per CU. Here the weights stream through
+// LDS in K-chunks of KB elements ([64][KB], 32–34 KB for both precisions) and every wave keeps
+// TPW 16-pixel tiles × 64 channels of accumulators for the whole K loop, so one staged chunk
+// feeds 4·TPW pixel tiles and each B fragment read from LDS feeds TPW MFMAs. The A operand
+// (im2col of the activation with the operand transform) is gathered straight from global into
+// registers — all TPW tiles' fragments of a K step are issued before their MFMAs, so the loads
+// overlap. The next chunk's weights are prefetched into registers while the current one is used.
+// Epilogue identical to conv_gemm_kernel (stage the tile in LDS, vectorised stores, statistics).
+// =====================================================================================
+template <class P>
+struct ConvK {
+  static constexpr int KB = P::kF32 ? 128 : 256;           // K elements per staged chunk
+  static constexpr int LDB = KB + (P::kF32 ? 4 : 8);       // LDS pitch (elements) of the chunk rows
+  static constexpr int NOUT = 64;
+  static constexpr int PREF = NOUT * KB / P::VEC / 256;    // 16-B chunks per thread per K-chunk (8)
+  static size_t smem(int kc) {
+    return (size_t)NOUT * LDB * P::ES + (size_t)3 * kc * 4 + (size_t)4 * NOUT * 3 * 4 +
+           (size_t)4 * 16 * NOUT * P::ES;
+  }
+};
+
+template <class P, int TPW, int AOP, int PRO, int MODE, int EPI>
+__global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
+  using T = typename P::T;
+  using frag_t = typename P::frag_t;
+  using CK = ConvK<P>;
+  constexpr int V = P::VEC;
+  constexpr int NT = 4;
+  constexpr int NOUT = CK::NOUT;
+  constexpr int KB = CK::KB;
+  constexpr int LDB = CK::LDB;
+  const int c = blockIdx.y;
+  const int NO = a.nout_total;
+  const int ch_base = blockIdx.z * NOUT;
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int K = a.KH * a.KW * a.KC;
+  const int Mo = a.Nb * a.Ho * a.Wo;
+  const int HWi = MODE == MODE_BWD2 ? a.Hs * a.Ws : a.Ho * a.Wo;
+  const int M = MODE == MODE_BWD2 ? a.Nb * HWi : Mo;
+  const int Mv = a.nimg ? min(M, a.nimg[c] * HWi) : M;
+  if ((int)(blockIdx.x * 4 * TPW) * 16 >= Mv) return;   // uniform: whole workgroup idle
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* wl = reinterpret_cast<T*>(smem);                                              // [NOUT][LDB]
+  float* v0 = reinterpret_cast<float*>(smem + (size_t)NOUT * LDB * P::ES);        // [KC]
+  float* v1 = v0 + a.KC;
+  float* v2 = v1 + a.KC;
+  float* red = v2 + a.KC;                                                           // [4][NOUT][3]
+  T* stage = reinterpret_cast<T*>(red + 4 * NOUT * 3);                             // [4][16][NOUT]
+  T* my_stage = stage + wid * 16 * NOUT;
+
+  if (AOP == AOP_DY || PRO == PRO_BNRELU) {
+    for (int i = threadIdx.x; i < a.KC; i += 256) {
+      v0[i] = a.vec0[(int64_t)c * a.KC + i];
+      v1[i] = a.vec1[(int64_t)c * a.KC + i];
+      if (AOP == AOP_DY) v2[i] = a.vec2[(int64_t)c * a.KC + i];
+    }
+  }
+  for (int i = threadIdx.x; i < 4 * NOUT * 3; i += 256) red[i] = 0.f;
+
+  const int64_t src_client = (int64_t)c * a.Nb * a.Hs * a.Ws * a.KC;
+  const T* src = reinterpret_cast<const T*>(a.src) + src_client;
+  const T* src2 = (AOP == AOP_DY) ? reinterpret_cast<const T*>(a.src2) + src_client : nullptr;
+  T* out = reinterpret_cast<T*>(a.out) + (int64_t)c * Mo * NO;
+  const T* wsrc = reinterpret_cast<const T*>(a.wpk) + (int64_t)c * a.wpk_ld + (int64_t)ch_base * a.ldk;
+
+  // per-lane pixel decode of this wave's TPW tiles
+  const int tiles_total = (Mv + 15) / 16;
+  const int tile0 = (blockIdx.x * 4 + wid) * TPW;
+  const int IW = MODE == MODE_BWD2 ? a.Ws : a.Wo;
+  int pn[TPW], ph[TPW], pw[TPW];
+  bool pv[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    const int m = (tile0 + t) * 16 + (lane & 15);
+    pv[t] = m < Mv;
+    const int mm = pv[t] ? m : 0;
+    pn[t] = mm / HWi;
+    const int r = mm % HWi;
+    ph[t] = r / IW;
+    pw[t] = r % IW;
+  }
+
+  f32x4 acc[TPW][NT];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t)
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt) acc[t][nt] = {0.f, 0.f, 0.f, 0.f};
+
+  // weight-chunk staging: thread i moves 16-B chunks i, i+256, ... of the [NOUT][kn] chunk
+  uint4 pre[CK::PREF];
+  auto fetch = [&](int kbase, int kn) {
+    const int cpr = kn / V;
+#pragma unroll
+    for (int it = 0; it < CK::PREF; ++it) {
+      const int i = threadIdx.x + it * 256;
+      pre[it] = make_uint4(0, 0, 0, 0);
+      if (i < NOUT * cpr) {
+        const int row = i / cpr, col = (i % cpr) * V;
+        pre[it] = *reinterpret_cast<const uint4*>(wsrc + (int64_t)row * a.ldk + kbase + col);
+      }
+    }
+  };
+  auto put = [&](int kn) {
+    const int cpr = kn / V;
+#pragma unroll
+    for (int it = 0; it < CK::PREF; ++it) {
+      const int i = threadIdx.x + it * 256;
+      if (i < NOUT * cpr) *reinterpret_cast<uint4*>(wl + (i / cpr) * LDB + (i % cpr) * V) = pre[it];
+    }
+  };
+
+  fetch(0, min(KB, a.Kp));
+  for (int kbase = 0; kbase < a.Kp; kbase += KB) {
+    const int kn = min(KB, a.Kp - kbase);       // multiple of 32
+    __syncthreads();                            // previous chunk fully consumed
+    put(kn);
+    __syncthreads();
+    if (kbase + KB < a.Kp) fetch(kbase + KB, min(KB, a.Kp - kbase - KB));
+    for (int k0 = 0; k0 < kn; k0 += 32) {
+      const int k = kbase + k0 + 8 * (lane >> 4);
+      const bool kval = k < K;
+      const int tap = k / a.KC, ci = k % a.KC;
+      const int kh = tap / a.KW, kw = tap % a.KW;
+      frag_t af[TPW];
+#pragma unroll
+      for (int t = 0; t < TPW; ++t) {
+        float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (pv[t] && kval) {
+          int ih, iw;
+          bool ok;
+          if (MODE == MODE_BWD2) {
+            ih = ph[t]; iw = pw[t]; ok = true;
+          } else if (MODE == MODE_FWD) {
+            ih = ph[t] * a.stride - a.pad + kh;
+            iw = pw[t] * a.stride - a.pad + kw;
+            ok = ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws;
+          } else {
+            const int th = ph[t] + a.pad - kh, tw = pw[t] + a.pad - kw;
+            ok = th >= 0 && tw >= 0 && (th % a.stride) == 0 && (tw % a.stride) == 0;
+            ih = th / a.stride;
+            iw = tw / a.stride;
+            ok = ok && ih < a.Hs && iw < a.Ws;
+          }
+          if (ok) {
+            const int64_t off = (((int64_t)pn[t] * a.Hs + ih) * a.Ws + iw) * a.KC + ci;
+            P::load8(src + off, f);
+            if (AOP == AOP_ACT && PRO == PRO_BNRELU) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j] * v0[ci + j] + v1[ci + j], 0.f);
+            } else if (AOP == AOP_DY) {
+              float yv[8];
+              P::load8(src2 + off, yv);
+#pragma unroll
+              for (int j = 0; j < 8; ++j) f[j] = v0[ci + j] * f[j] + v1[ci + j] * yv[j] + v2[ci + j];
+            }
+          }
+        }
+        af[t] = P::frag8(f);
+      }
+#pragma unroll
+      for (int nt = 0; nt < NT; ++nt) {
+        const frag_t bv = P::frag(wl + (nt * 16 + (lane & 15)) * LDB + k0 + 8 * (lane >> 4));
+#pragma unroll
+        for (int t = 0; t < TPW; ++t) acc[t][nt] = P::mma(af[t], bv, acc[t][nt]);
+      }
+    }
+  }
+
+  const T* e_x = reinterpret_cast<const T*>(a.e_x);
+  const T* e_add = reinterpret_cast<const T*>(a.e_add);
+  const T* e_y1 = reinterpret_cast<const T*>(a.e_y1);
+  const T* e_y2 = reinterpret_cast<const T*>(a.e_y2);
+  constexpr int CG = NOUT / V;
+  constexpr int ROWS_PER_PASS = 64 / CG;
+  float st0[V], st1[V], st2[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) { st0[j] = 0.f; st1[j] = 0.f; st2[j] = 0.f; }
+  const int my_cg = lane % CG;
+  float kpiv[NT];
+#pragma unroll
+  for (int nt = 0; nt < NT; ++nt)
+    kpiv[nt] = (EPI == EPI_FWD && a.pivot) ? a.pivot[(int64_t)c * NO + ch_base + nt * 16 + (lane & 15)] : 0.f;
+
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    const int tile = tile0 + t;
+    if (tile >= tiles_total) break;
+#pragma unroll
+    for (int nt = 0; nt < NT; ++nt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        my_stage[(4 * (lane >> 4) + i) * NOUT + nt * 16 + (lane & 15)] = P::from_f(acc[t][nt][i] - kpiv[nt]);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    const int rows_valid = min(16, Mv - tile * 16);
+#pragma unroll
+    for (int pass = 0; pass < (16 + ROWS_PER_PASS - 1) / ROWS_PER_PASS; ++pass) {
+      const int row = pass * ROWS_PER_PASS + lane / CG;
+      if (lane / CG < ROWS_PER_PASS && row < rows_valid) {
+        const int ch0 = my_cg * V;
+        const uint4 dv = *reinterpret_cast<const uint4*>(my_stage + row * NOUT + ch0);
+        int64_t goff = ((int64_t)(tile * 16 + row)) * NO + ch_base + ch0;
+        if (MODE == MODE_BWD2) {
+          const int pm = tile * 16 + row;
+          const int n_ = pm / HWi, r_ = pm % HWi;
+          const int64_t px = ((int64_t)n_ * a.Ho + 2 * (r_ / a.Ws)) * a.Wo + 2 * (r_ % a.Ws);
+          goff = px * NO + ch_base + ch0;
+          const uint4 z = make_uint4(0, 0, 0, 0);
+          *reinterpret_cast<uint4*>(out + goff + NO) = z;
+          *reinterpret_cast<uint4*>(out + goff + (int64_t)a.Wo * NO) = z;
+          *reinterpret_cast<uint4*>(out + goff + (int64_t)(a.Wo + 1) * NO) = z;
+        }
+        if (EPI == EPI_FWD || EPI == EPI_STORE) {
+          *reinterpret_cast<uint4*>(out + goff) = dv;
+          if (EPI == EPI_FWD) {
+            float f[V];
+            P::unpack(dv, f);
+#pragma unroll
+            for (int j = 0; j < V; ++j) { st0[j] += f[j]; st1[j] += f[j] * f[j]; }
+          }
+        } else {
+          const int64_t eoff = (int64_t)c * Mo * NO + goff;
+          float g[V], xv[V];
+          P::unpack(dv, g);
+          P::unpack(*reinterpret_cast<const uint4*>(e_x + eoff), xv);
+          if (EPI == EPI_MASK) {
+#pragma unroll
+            for (int j = 0; j < V; ++j) {
+              const int ch = ch_base + ch0 + j;
+              const bool on_ = xv[j] * a.e_s[(int64_t)c * NO + ch] + a.e_t[(int64_t)c * NO + ch] > 0.f;
+              g[j] = on_ ? g[j] : 0.f;
+            }
+          } else {
+            float ex[V];
+            P::unpack(*reinterpret_cast<const uint4*>(e_add + eoff), ex);
+#pragma unroll
+            for (int j = 0; j < V; ++j) g[j] = (xv[j] > 0.f) ? g[j] + ex[j] : 0.f;
+          }
+          const uint4 gp = P::pack(g);
+          *reinterpret_cast<uint4*>(out + goff) = gp;
+          float gr[V];
+          P::unpack(gp, gr);
+          if (EPI == EPI_MASK) {
+#pragma unroll
+            for (int j = 0; j < V; ++j) { st0[j] += gr[j]; st1[j] += gr[j] * xv[j]; }
+          } else {
+            float y1[V];
+            P::unpack(*reinterpret_cast<const uint4*>(e_y1 + eoff), y1);
+#pragma unroll
+            for (int j = 0; j < V; ++j) { st0[j] += gr[j]; st1[j] += gr[j] * y1[j]; }
+            if (e_y2) {
+              float y2[V];
+              P::unpack(*reinterpret_cast<const uint4*>(e_y2 + eoff), y2);
+#pragma unroll
+              for (int j = 0; j < V; ++j) st2[j] += gr[j] * y2[j];
+            }
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+
+  if (EPI != EPI_STORE) {
+#pragma unroll
+    for (int o = CG; o < 64; o <<= 1) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        st0[j] += __shfl_xor(st0[j], o, 64);
+        st1[j] += __shfl_xor(st1[j], o, 64);
+        if (EPI == EPI_BLOCK) st2[j] += __shfl_xor(st2[j], o, 64);
+      }
+    }
+    if (lane < CG) {
+#pragma unroll
+      for (int j = 0; j < V; ++j) {
+        const int ch = lane * V + j;
+        red[(wid * NOUT + ch) * 3 + 0] = st0[j];
+        red[(wid * NOUT + ch) * 3 + 1] = st1[j];
+        red[(wid * NOUT + ch) * 3 + 2] = st2[j];
+      }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < NOUT * a.NS; i += 256) {
+      const int ch = i / a.NS, q = i % a.NS;
+      const float s = red[(0 * NOUT + ch) * 3 + q] + red[(1 * NOUT + ch) * 3 + q] + red[(2 * NOUT + ch) * 3 + q] +
+                      red[(3 * NOUT + ch) * 3 + q];
+      atomicAdd(&a.stats[((int64_t)c * NO + ch_base + ch) * a.NS + q], s);
+    }
+  }
+}
+
+// K above which (or outputs above 256) the K-streamed kernel runs; FEDML_AMD_CONVK_MIN_K overrides
+static int convk_min_k() {
+  static int v = -1;
+  if (v < 0) {
+    const char* e = getenv("FEDML_AMD_CONVK_MIN_K");
+    v = e ? atoi(e) : 1024;
+  }
+  return v;
+}
+
+template <class P, int TPW, int AOP, int PRO, int MODE, int EPI>
+static int launch_convk_t(ConvArgs a, int nout, int C, hipStream_t stream) {
+  a.nout_total = nout;
+  const int M = MODE == MODE_BWD2 ? a.Nb * a.Hs * a.Ws : a.Nb * a.Ho * a.Wo;
+  const int tiles = (M + 15) / 16;
+  const int gx = (tiles + 4 * TPW - 1) / (4 * TPW);
+  const size_t smem = ConvK<P>::smem(a.KC);
+  if (smem > 160 * 1024) return -5;
+  auto kern = convk_gemm_kernel<P, TPW, AOP, PRO, MODE, EPI>;
+  if (smem > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  hipLaunchKernelGGL(kern, dim3(gx, C, nout / 64), dim3(256), smem, stream, a);
+  return (int)hipGetLastError();
+}
+
+// tiles per wave: as many as keep ≥ ~2048 workgroups over the chip (8 XCDs × 32 CUs × 8)
+template <class P, int AOP, int PRO, int MODE, int EPI>
+static int launch_convk(ConvArgs a, int nout, int C, hipStream_t s) {
+  if (nout % 64 != 0) return -2;
+  const int M = MODE == MODE_BWD2 ? a.Nb * a.Hs * a.Ws : a.Nb * a.Ho * a.Wo;
+  const int64_t wgs1 = (int64_t)((M + 63) / 64) * C * (nout / 64);
+  if (wgs1 >= 8192) return launch_convk_t<P, 4, AOP, PRO, MODE, EPI>(a, nout, C, s);
+  if (wgs1 >= 4096) return launch_convk_t<P, 2, AOP, PRO, MODE, EPI>(a, nout, C, s);
+  return launch_convk_t<P, 1, AOP, PRO, MODE, EPI>(a, nout, C, s);
+}
+
 template <class P, int NT, int AOP, int PRO, int MODE, int EPI>
 static int launch_conv(ConvArgs a, int nout, int C, hipStream_t stream) {
   a.nout_total = nout;
@@ -400,6 +799,9 @@ static int launch_conv(ConvArgs a, int nout, int C, hipStream_t stream) {
 // re-reading the (narrow) A operand once per slice.
 template <class P, int AOP, int PRO, int MODE, int EPI>
 static int dispatch_nt(int nout, const ConvArgs& a, int C, hipStream_t s) {
+  // wide layers (ResNet-18 stages 2-4): weights streamed through LDS in K-chunks
+  if (nout % 64 == 0 && (nout > 256 || a.KH * a.KW * a.KC > convk_min_k()))
+    return launch_convk<P, AOP, PRO, MODE, EPI>(a, nout, C, s);
   switch (nout) {
     case 16: return launch_conv<P, 1, AOP, PRO, MODE, EPI>(a, nout, C, s);
     case 32: return launch_conv<P, 2, AOP, PRO, MODE, EPI>(a, nout, C, s);

@@ -15,6 +15,7 @@
 // into the client-stacked gradient arena at the OIHW position of each element.
 #include "prec.h"
 
+#include <stdlib.h>
 #include <type_traits>
 
 using prec::BF16;
@@ -32,7 +33,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_tr_kernel(
     const float* __restrict__ beta, const float* __restrict__ gamma, const typename P::T* __restrict__ x,
     const float* __restrict__ ps, const float* __restrict__ pt, float* __restrict__ dw, int Nb, int H, int W,
     int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int pix_per_wg, int nt_per_z,
-    const int* __restrict__ nimg) {
+    const int* __restrict__ nimg, int co_slice) {
   using T = typename P::T;
   const bool PRO = ps != nullptr;   // runtime flag: halves the instantiations (uniform branch)
   using frag_t = typename P::frag_t;
@@ -46,34 +47,39 @@ __global__ __launch_bounds__(256) void conv_wgrad_tr_kernel(
   const int Mv = nimg ? min(Nb * Ho * Wo, nimg[c] * Ho * Wo) : Nb * Ho * Wo;
   if ((int)(blockIdx.x * pix_per_wg) >= Mv) return;   // uniform: whole workgroup idle
   const int NT2 = (K + 15) / 16;
-  const int nt_lo = blockIdx.z * nt_per_z;
+  // blockIdx.z = (K-slice, output-channel slice): wide layers (Cout > 256) split their Cout into
+  // co_slice-wide slices so the staged dy tile and the per-wave tile count stay bounded
+  const int nco = Cout / co_slice;
+  const int co_lo = (blockIdx.z % nco) * co_slice;
+  const int Cs = co_slice;
+  const int nt_lo = (blockIdx.z / nco) * nt_per_z;
   const int nt_hi = min(NT2, nt_lo + nt_per_z);
   const int k_lo = nt_lo * 16;
   const int k_hi = min(K, nt_hi * 16);
   const int kw_ = (nt_hi - nt_lo) * 16;     // staged columns (zero beyond K)
   const int M = Nb * Ho * Wo;
-  const int ldd = P::pitch_tr(Cout);
+  const int ldd = P::pitch_tr(Cs);
   const int lda = P::pitch_tr(kw_);
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* dyL = reinterpret_cast<T*>(smem);                  // [PT][ldd]
   T* aL = dyL + PT * ldd;                               // [PT][lda]
-  float* vv = reinterpret_cast<float*>(aL + PT * lda);  // α β γ [Cout], s t [Cin]
+  float* vv = reinterpret_cast<float*>(aL + PT * lda);  // α β γ [Cs] (this slice), s t [Cin]
 
-  for (int i = threadIdx.x; i < Cout; i += 256) {
-    vv[i] = alpha[(int64_t)c * Cout + i];
-    vv[Cout + i] = beta[(int64_t)c * Cout + i];
-    vv[2 * Cout + i] = gamma[(int64_t)c * Cout + i];
+  for (int i = threadIdx.x; i < Cs; i += 256) {
+    vv[i] = alpha[(int64_t)c * Cout + co_lo + i];
+    vv[Cs + i] = beta[(int64_t)c * Cout + co_lo + i];
+    vv[2 * Cs + i] = gamma[(int64_t)c * Cout + co_lo + i];
   }
   if (PRO)
     for (int i = threadIdx.x; i < Cin; i += 256) {
-      vv[3 * Cout + i] = ps[(int64_t)c * Cin + i];
-      vv[3 * Cout + Cin + i] = pt[(int64_t)c * Cin + i];
+      vv[3 * Cs + i] = ps[(int64_t)c * Cin + i];
+      vv[3 * Cs + Cin + i] = pt[(int64_t)c * Cin + i];
     }
   const int padc = kw_ - (k_hi - k_lo);
   for (int i = threadIdx.x; i < PT * padc; i += 256) aL[(i / padc) * lda + (k_hi - k_lo) + i % padc] = 0;
 
-  const int MT = Cout / 16, NTZ = nt_hi - nt_lo;
+  const int MT = Cs / 16, NTZ = nt_hi - nt_lo;
   const int ntiles = MT * NTZ;
   f32x4 acc[TPW];
 #pragma unroll
@@ -84,7 +90,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_tr_kernel(
   const T* xc = x + (int64_t)c * Nb * H * W * Cin;
   const int p_begin = blockIdx.x * pix_per_wg;
   const int p_end = min(Mv, p_begin + pix_per_wg);
-  const int cg = Cout / V, kg = (k_hi - k_lo) / V;
+  const int cg = Cs / V, kg = (k_hi - k_lo) / V;
   const int n_dy = PT * cg, n_a = PT * kg;
   __syncthreads();
 
@@ -101,8 +107,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_tr_kernel(
       if (i < n_dy) {
         const int p = p0 + i / cg, co0 = (i % cg) * V;
         if (p < p_end) {
-          rg[it] = *reinterpret_cast<const uint4*>(gc + (int64_t)p * Cout + co0);
-          ry[it] = *reinterpret_cast<const uint4*>(yc + (int64_t)p * Cout + co0);
+          rg[it] = *reinterpret_cast<const uint4*>(gc + (int64_t)p * Cout + co_lo + co0);
+          ry[it] = *reinterpret_cast<const uint4*>(yc + (int64_t)p * Cout + co_lo + co0);
           dvalid |= 1u << it;
         }
       }
@@ -138,7 +144,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_tr_kernel(
         const bool live = (dvalid >> it) & 1u;
 #pragma unroll
         for (int j = 0; j < V; ++j)
-          d[j] = live ? vv[co0 + j] * gf[j] + vv[Cout + co0 + j] * yf[j] + vv[2 * Cout + co0 + j] : 0.f;
+          d[j] = live ? vv[co0 + j] * gf[j] + vv[Cs + co0 + j] * yf[j] + vv[2 * Cs + co0 + j] : 0.f;
         P::st_chunk(dyL + pp * ldd + co0, P::pack(d));
       }
     }
@@ -155,7 +161,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_tr_kernel(
           float f[V];
           P::unpack(v, f);
 #pragma unroll
-          for (int j = 0; j < V; ++j) f[j] = fmaxf(f[j] * vv[3 * Cout + ci0 + j] + vv[3 * Cout + Cin + ci0 + j], 0.f);
+          for (int j = 0; j < V; ++j) f[j] = fmaxf(f[j] * vv[3 * Cs + ci0 + j] + vv[3 * Cs + Cin + ci0 + j], 0.f);
           v = P::pack(f);
         }
         P::st_chunk(aL + pp * lda + kk, v);
@@ -193,12 +199,200 @@ __global__ __launch_bounds__(256) void conv_wgrad_tr_kernel(
       if (k < K) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const int co = mt * 16 + 4 * (lane >> 4) + i;
+          const int co = co_lo + mt * 16 + 4 * (lane >> 4) + i;
           atomicAdd(&dwc[(int64_t)co * K + k], acc[t][i]);
         }
       }
     }
   }
+}
+
+__global__ void wgrad_scatter_kernel(float* __restrict__ dw, float* __restrict__ garena, int64_t ldw, int64_t woff,
+                                     int Cout, int Cin, int taps, int cin_src);
+
+// ---- wide layers (Cout ≥ 128: ResNet-18 stages 2-4) ----
+// One workgroup owns a 128 (co) × 128 (k) dW tile of one client and reduces it over a pixel chunk;
+// its 4 waves form a 2 × 2 grid of 64 × 64 sub-tiles (4 × 4 MFMA tiles each), so per 32-pixel K step
+// a wave reads 4 dy fragments + 4 im2col fragments (transposing LDS reads) for 16 MFMAs — the
+// generic kernel above re-reads both per MFMA. The next sub-tile's global data is prefetched into
+// registers during the MFMAs. When one chunk covers the client's pixels (the deep, small-image
+// stages: 4·4·64 px) the tile is owned by exactly one workgroup and is added straight into the
+// OIHW gradient arena — no fp32 atomics, no scratch, no scatter pass.
+template <class P>
+__global__ __launch_bounds__(256) void wgrad_wide_kernel(
+    const typename P::T* __restrict__ g, const typename P::T* __restrict__ yv, const float* __restrict__ alpha,
+    const float* __restrict__ beta, const float* __restrict__ gamma, const typename P::T* __restrict__ x,
+    const float* __restrict__ ps, const float* __restrict__ pt, float* __restrict__ dw, float* __restrict__ garena,
+    int64_t ldw, int64_t woff, int cin_src, int Nb, int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW,
+    int stride, int pad, int pix_per_wg, const int* __restrict__ nimg, int direct) {
+  using T = typename P::T;
+  using frag_t = typename P::frag_t;
+  constexpr int V = P::VEC;
+  constexpr int PT = P::kF32 ? 32 : 64;
+  constexpr int TS = 128;                       // tile edge (co and k)
+  constexpr int NI = PT * (TS / V) / 256;       // 16-B chunks per thread per operand and sub-tile (4)
+  const bool PRO = ps != nullptr;
+  const int c = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int K = KH * KW * Cin;
+  const int nks = (K + TS - 1) / TS;
+  const int co_lo = (blockIdx.z / nks) * TS;
+  const int k_lo = (blockIdx.z % nks) * TS;
+  const int kn = min(TS, K - k_lo);             // multiple of 8 (Cin % 8 == 0)
+  const int M = Nb * Ho * Wo;
+  const int Mv = nimg ? min(M, nimg[c] * Ho * Wo) : M;
+  const int p_begin = blockIdx.x * pix_per_wg;
+  if (p_begin >= Mv) return;   // uniform: whole workgroup idle
+  const int p_end = min(Mv, p_begin + pix_per_wg);
+  constexpr int LD = P::pitch_tr(TS);
+
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* dyL = reinterpret_cast<T*>(smem);                 // [PT][LD]
+  T* aL = dyL + PT * LD;                               // [PT][LD]
+  float* vv = reinterpret_cast<float*>(aL + PT * LD);  // α β γ [TS], s t [Cin]
+  for (int i = threadIdx.x; i < TS; i += 256) {
+    vv[i] = alpha[(int64_t)c * Cout + co_lo + i];
+    vv[TS + i] = beta[(int64_t)c * Cout + co_lo + i];
+    vv[2 * TS + i] = gamma[(int64_t)c * Cout + co_lo + i];
+  }
+  if (PRO)
+    for (int i = threadIdx.x; i < Cin; i += 256) {
+      vv[3 * TS + i] = ps[(int64_t)c * Cin + i];
+      vv[3 * TS + Cin + i] = pt[(int64_t)c * Cin + i];
+    }
+
+  const T* gc = g + (int64_t)c * M * Cout;
+  const T* yc = yv + (int64_t)c * M * Cout;
+  const T* xc = x + (int64_t)c * Nb * H * W * Cin;
+  constexpr int CPR = TS / V;   // chunks per staged row
+  uint4 rg[NI], ry[NI], rx[NI];
+  uint32_t dvalid = 0;
+  auto load_sub = [&](int p0) {
+    dvalid = 0;
+#pragma unroll
+    for (int it = 0; it < NI; ++it) {
+      const int i = threadIdx.x + it * 256;
+      const int pp = i / CPR, col = (i % CPR) * V;
+      const int p = p0 + pp;
+      rg[it] = make_uint4(0, 0, 0, 0);
+      ry[it] = make_uint4(0, 0, 0, 0);
+      rx[it] = make_uint4(0, 0, 0, 0);
+      if (p < p_end) {
+        dvalid |= 1u << it;
+        rg[it] = *reinterpret_cast<const uint4*>(gc + (int64_t)p * Cout + co_lo + col);
+        ry[it] = *reinterpret_cast<const uint4*>(yc + (int64_t)p * Cout + co_lo + col);
+        if (col < kn) {
+          const int k0 = k_lo + col;
+          const int tap = k0 / Cin, ci0 = k0 % Cin;
+          const int n = p / (Ho * Wo), r = p % (Ho * Wo);
+          const int ih = (r / Wo) * stride - pad + tap / KW, iw = (r % Wo) * stride - pad + tap % KW;
+          if (ih >= 0 && ih < H && iw >= 0 && iw < W) {
+            uint4 v = *reinterpret_cast<const uint4*>(xc + (((int64_t)n * H + ih) * W + iw) * Cin + ci0);
+            if (PRO) {
+              float f[V];
+              P::unpack(v, f);
+#pragma unroll
+              for (int j = 0; j < V; ++j) f[j] = fmaxf(f[j] * vv[3 * TS + ci0 + j] + vv[3 * TS + Cin + ci0 + j], 0.f);
+              v = P::pack(f);
+            }
+            rx[it] = v;   // out-of-image taps stay 0 (zero padding, not relu(shift))
+          }
+        }
+      }
+    }
+  };
+  auto store_sub = [&]() {
+#pragma unroll
+    for (int it = 0; it < NI; ++it) {
+      const int i = threadIdx.x + it * 256;
+      const int pp = i / CPR, col = (i % CPR) * V;
+      float gf[V], yf[V], d[V];
+      P::unpack(rg[it], gf);
+      P::unpack(ry[it], yf);
+      const bool live = (dvalid >> it) & 1u;   // pixels past the chunk: dy = 0 (not γ)
+#pragma unroll
+      for (int j = 0; j < V; ++j)
+        d[j] = live ? vv[col + j] * gf[j] + vv[TS + col + j] * yf[j] + vv[2 * TS + col + j] : 0.f;
+      P::st_chunk(dyL + pp * LD + col, P::pack(d));
+      P::st_chunk(aL + pp * LD + col, rx[it]);
+    }
+  };
+
+  const int wm = wid >> 1, wn = wid & 1;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = {0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+  load_sub(p_begin);
+  for (int p0 = p_begin; p0 < p_end; p0 += PT) {
+    store_sub();
+    __syncthreads();
+    if (p0 + PT < p_end) load_sub(p0 + PT);
+#pragma unroll
+    for (int ks = 0; ks < PT / 32; ++ks) {
+      frag_t af[4], bf[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = P::frag_tr(dyL, LD, ks * 32, (wm * 4 + i) * 16, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bf[j] = P::frag_tr(aL, LD, ks * 32, (wn * 4 + j) * 16, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = P::mma(af[i], bf[j], acc[i][j]);
+    }
+    __syncthreads();
+  }
+  const int taps = KH * KW;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int kk = (wn * 4 + j) * 16 + (lane & 15);
+    if (kk >= kn) continue;
+    const int k = k_lo + kk;
+    const int tap = k / Cin, ci = k % Cin;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co_lo + (wm * 4 + i) * 16 + 4 * (lane >> 4) + r;
+        if (direct) {
+          if (ci < cin_src) garena[(int64_t)c * ldw + woff + ((int64_t)co * cin_src + ci) * taps + tap] += acc[i][j][r];
+        } else {
+          atomicAdd(&dw[((int64_t)c * Cout + co) * K + k], acc[i][j][r]);
+        }
+      }
+    }
+  }
+}
+
+template <class P>
+static int wgrad_wide(const typename P::T* g, const typename P::T* yv, const float* alpha, const float* beta,
+                      const float* gamma, const typename P::T* x, const float* ps, const float* pt, float* garena,
+                      int64_t ldw, int64_t woff, int C, int Nb, int H, int W, int Cin, int Ho, int Wo, int Cout,
+                      int KH, int KW, int stride, int pad, int cin_src, float* dw, const int* nimg,
+                      hipStream_t stream) {
+  constexpr int PT = P::kF32 ? 32 : 64;
+  const int K = KH * KW * Cin;
+  const int nks = (K + 127) / 128;
+  const int base = C * nks * (Cout / 128);
+  const int M = Nb * Ho * Wo;
+  // pixel chunks: enough workgroups to fill the chip (≈2048), chunks of ≥ 512 pixels
+  int gx = max(1, min((2048 + base - 1) / base, (M + 511) / 512));
+  int ppw = ((M + gx - 1) / gx + PT - 1) / PT * PT;
+  gx = (M + ppw - 1) / ppw;
+  const int direct = gx == 1;
+  const size_t smem = (size_t)2 * PT * P::pitch_tr(128) * P::ES + (size_t)(3 * 128 + 2 * Cin) * 4;
+  auto kern = wgrad_wide_kernel<P>;
+  if (smem > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  hipLaunchKernelGGL(kern, dim3(gx, C, nks * (Cout / 128)), dim3(256), smem, stream, g, yv, alpha, beta, gamma, x,
+                     ps, pt, dw, garena, ldw, woff, cin_src, Nb, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ppw,
+                     nimg, direct);
+  if (!direct)
+    hipLaunchKernelGGL(wgrad_scatter_kernel, dim3(fa_grid((int64_t)Cout * K, 256, 64), C), dim3(256), 0, stream, dw,
+                       garena, ldw, woff, Cout, Cin, KH * KW, cin_src);
+  return (int)hipGetLastError();
 }
 
 // dW GEMM layout [c][co][tap*Cin + ci] → OIHW gradient arena (+=), and clear the scratch
@@ -227,28 +421,43 @@ static int conv_wgrad(const typename P::T* g, const typename P::T* yv, const flo
                       const int* nimg, hipStream_t stream) {
   constexpr int V = P::VEC;
   constexpr int PT = P::kF32 ? 32 : 64;
-  if (Cin % 8 != 0 || Cout % 16 != 0 || Cout > 256) return -3;
+  if (Cin % 8 != 0 || Cout % 16 != 0) return -3;
+  {
+    // FEDML_AMD_WGRAD_WIDE: 0 off, 1 (default) wide layers with K ≥ 256 or Cout > 256, 2 every Cout % 128 == 0
+    static int mode = -1;
+    if (mode < 0) {
+      const char* e = getenv("FEDML_AMD_WGRAD_WIDE");
+      mode = e ? atoi(e) : 1;
+    }
+    const int K = KH * KW * Cin;
+    if (Cout % 128 == 0 && ((mode == 1 && (K >= 256 || Cout > 256)) || mode == 2))
+      return wgrad_wide<P>(g, yv, alpha, beta, gamma, x, ps, pt, garena, ldw, woff, C, Nb, H, W, Cin, Ho, Wo, Cout, KH,
+                           KW, stride, pad, cin_src, dw, nimg, stream);
+  }
+  const int co_slice = Cout > 256 ? 128 : Cout;   // wide layers: 128-channel dy slices
+  if (Cout % co_slice != 0) return -3;
   const int K = KH * KW * Cin;
   const int NT2 = (K + 15) / 16;
-  const int MT = Cout / 16;
+  const int MT = co_slice / 16;
   const int nt_per_z = max(1, min(NT2, 64 / MT));   // ≤ 64 tiles per workgroup → ≤ 16 per wave
-  const int nz = (NT2 + nt_per_z - 1) / nt_per_z;
+  const int nz = (NT2 + nt_per_z - 1) / nt_per_z * (Cout / co_slice);
   const int tpw = (MT * nt_per_z + 3) / 4;
   const int M = Nb * Ho * Wo;
   const int gx = (M + pix_per_wg - 1) / pix_per_wg;
   const int kw_ = nt_per_z * 16;
-  const int dyi = (PT * (Cout / V) + 255) / 256;
+  const int dyi = (PT * (co_slice / V) + 255) / 256;
   const int ai = (PT * (kw_ / V) + 255) / 256;
   // the staging loops cover DYI·256 / AI·256 16-B chunks: a sub-tile larger than the largest
   // instantiation would leave LDS rows unwritten
   if (dyi > 8 || ai > 16) return -6;
-  const size_t smem = (size_t)PT * (P::pitch_tr(Cout) + P::pitch_tr(kw_)) * P::ES + (size_t)(3 * Cout + 2 * Cin) * 4;
+  const size_t smem =
+      (size_t)PT * (P::pitch_tr(co_slice) + P::pitch_tr(kw_)) * P::ES + (size_t)(3 * co_slice + 2 * Cin) * 4;
   if (smem > 160 * 1024) return -5;
   dim3 grid(gx, C, nz);
   auto go = [&](auto kern) {
     if (smem > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     hipLaunchKernelGGL(kern, grid, dim3(256), smem, stream, g, yv, alpha, beta, gamma, x, ps, pt, dw, Nb, H, W, Cin,
-                       Ho, Wo, Cout, KH, KW, stride, pad, pix_per_wg, nt_per_z, nimg);
+                       Ho, Wo, Cout, KH, KW, stride, pad, pix_per_wg, nt_per_z, nimg, co_slice);
   };
   // instantiated register budgets: dy chunks/thread D ∈ {2, 8}, A chunks/thread ∈ {2, 4, 8, 16}
   auto by_a = [&](auto tpw_c, auto d_c) {

@@ -86,7 +86,9 @@ def _conv_spec(name, m: nn.Conv2d) -> ConvSpec:
         raise UnsupportedNative(f"conv {name}: unsupported config")
     cin = m.in_channels
     cin_pad = _round_up(cin, 8)
-    if m.out_channels % 16 != 0 or m.out_channels > 256 or (cin_pad > 256 and cin_pad != cin):
+    # ≤ 256 outputs: full-K kernels; wider (ResNet-18 stage 4): the K-streamed kernel needs 64-multiples
+    wide_ok = m.out_channels <= 256 or (m.out_channels <= 1024 and m.out_channels % 64 == 0)
+    if m.out_channels % 16 != 0 or not wide_ok or (cin_pad > 256 and (cin_pad != cin or cin % 64 != 0)):
         raise UnsupportedNative(f"conv {name}: channels {cin}->{m.out_channels}")
     return ConvSpec(f"{name}.weight", cin, m.out_channels, m.kernel_size[0], m.stride[0], m.padding[0], cin_pad)
 
@@ -208,6 +210,8 @@ class NativeResNetStep:
         raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
         self._segs = raw.to(dev)
         self._nseg = len(segs)
+        self._pack_tiles = max(-(-cv.cout // 32) * -(-cv.cin_pad // 32) for cv in self._all_convs())
+        self._pack_taps = max(cv.k * cv.k for cv in self._all_convs())
         # activations (storage precision) and per-BN vectors
         bf = self.dtype
 
@@ -276,7 +280,7 @@ class NativeResNetStep:
     # valid while another batch size (the ragged last step of an epoch) is being run.
     _STATE_ATTRS = ("x_in", "stem_y", "stem_out", "gbuf", "bn_vec", "stats", "stat_views", "pooled", "dw_scratch",
                     "dw_c3", "c3_segs", "c3_nseg", "c3_maxn", "_c3_off",
-                    "packed", "packed_ld", "_segs", "_nseg", "final_hw", "geom")
+                    "packed", "packed_ld", "_segs", "_nseg", "_pack_tiles", "_pack_taps", "final_hw", "geom")
 
     def _snapshot(self):
         st = {k: getattr(self, k) for k in self._STATE_ATTRS}
@@ -414,7 +418,8 @@ class NativeResNetStep:
                 self._setup(N, H, W)
                 self._states[(N, H, W)] = self._snapshot()
         self.stats.zero_()
-        nn_ops.pack_weights(arena, self._segs, self._nseg, self.packed, self.packed_ld, C)
+        nn_ops.pack_weights(arena, self._segs, self._nseg, self.packed, self.packed_ld, C, self._pack_tiles,
+                            self._pack_taps)
         st_conv, st_bn = self.stem
         nn_ops.nchw_to_nhwc_pad(x.contiguous(), self.x_in, C * N, st_conv.cin, H * W, st_conv.cin_pad)
 

@@ -221,8 +221,8 @@ def test_native_step_f32_matches_reference(builder, hw):
     last bit of the BN scale/shift, which follows the fp32-atomic order of the statistics sums. A flip
     moves every upstream gradient of this tiny random-init net by ~1e-3 (measured:
     scripts/dbg_dump_runs.py — one element of one data-gradient differs between runs, nothing else);
-    PyTorch fp32 flips the same way against fp64 on other seeds. So: per slot ≤ 5e-3 (bf16 autocast is
-    at 2-4e-1 here), and the loss to 1e-5."""
+    PyTorch fp32 flips the same way against fp64 on other seeds. So: per slot ≤ 1e-2 (one flip measured
+    up to 5.7e-3 on the [2, 2, 2] net; bf16 autocast is at 2-4e-1 here), and the loss to 1e-5."""
     torch.manual_seed(0)
     model = builder()
     layout = ParamLayout.from_module(model)
@@ -248,7 +248,7 @@ def test_native_step_f32_matches_reference(builder, hw):
         sl = slice(s.offset, s.offset + s.numel)
         r = ref64[:, sl]
         err = float((garena[:, sl].double() - r).norm() / r.norm().clamp_min(1e-30))
-        if err > 5e-3:
+        if err > 1e-2:
             bad.append((s.key, err))
     assert not bad, bad[:8]
     s = layout.slot("bn1.running_mean")

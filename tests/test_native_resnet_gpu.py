@@ -284,8 +284,8 @@ def test_hip_graph_step_matches_eager(momentum):
 
 
 @pytest.mark.parametrize("momentum", [0.0, 0.9])
-def test_multistream_graph_seq_step_matches_eager(momentum):
-    """Wide conv nets (ResNet-18) run per client; the captured multi-stream step (C client branches
+def test_multistream_graph_seq_step_matches_eager(momentum, monkeypatch):
+    """Wide conv nets (ResNet-18 with the native kernels switched off: FEDML_AMD_NATIVE_CONV=0) run per client; the captured multi-stream step (C client branches
     on forked HIP streams + fused optimizer, one replay) matches the eager one-client-after-another
     step, BN running statistics included. fp32 compute and a small learning rate: MIOpen's
     backward kernels are not bitwise deterministic, and at lr 0.05 two EAGER runs of ResNet-18 already
@@ -294,6 +294,7 @@ def test_multistream_graph_seq_step_matches_eager(momentum):
     from fedml_amd.models.cv.resnet import resnet18_cifar
     from fedml_amd.simulation.rccl.client_store import DeviceClientStore
     from fedml_amd.simulation.rccl.engine import ClientBatchEngine
+    monkeypatch.setenv("FEDML_AMD_NATIVE_CONV", "0")
     torch.manual_seed(0)
     model = resnet18_cifar(10)
     C, n = 3, 128
@@ -356,6 +357,7 @@ def test_conv_weight_shadow_matches_autocast_path(monkeypatch):
     from fedml_amd.models.cv.resnet import resnet18_cifar
     from fedml_amd.simulation.rccl.client_store import DeviceClientStore
     from fedml_amd.simulation.rccl.engine import ClientBatchEngine
+    monkeypatch.setenv("FEDML_AMD_NATIVE_CONV", "0")   # the per-client library path (ResNet-18 is native now)
     torch.manual_seed(0)
     model = resnet18_cifar(10)
     C, n = 2, 64
