@@ -447,179 +447,219 @@ static size_t conv_smem_bytes(int nout, int ldk, int kc) {
 }
 
 // =====================================================================================
-// K-streamed implicit GEMM for WIDE layers (ResNet-18: 128–512 channels, K = 9·Cin up to 4608).
+// K-streamed implicit GEMM for WIDE layers (ResNet-18: 64–512 channels, K = 9·Cin up to 4608).
 //
 // conv_gemm_kernel keeps the whole [NOUT][K] weight slice resident in LDS, which stops fitting
-// (fp32: 64 × 4608 × 4 B = 1.2 MB) or leaves one workgroup per CU. Here the weights stream through
-// LDS in K-chunks of KB elements ([64][KB], 32–34 KB for both precisions) and every wave keeps
-// TPW 16-pixel tiles × 64 channels of accumulators for the whole K loop, so one staged chunk
-// feeds 4·TPW pixel tiles and each B fragment read from LDS feeds TPW MFMAs. The A operand
-// (im2col of the activation with the operand transform) is gathered straight from global into
-// registers — all TPW tiles' fragments of a K step are issued before their MFMAs, so the loads
-// overlap. The next chunk's weights are prefetched into registers while the current one is used.
-// Epilogue identical to conv_gemm_kernel (stage the tile in LDS, vectorised stores, statistics).
+// (fp32: 64 × 4608 × 4 B = 1.2 MB) or leaves one workgroup per CU. Here BOTH operands stream through
+// LDS in K-chunks: the workgroup tile is BM = 64·TPW pixels × 64 output channels, wave w owns
+// pixel rows [16·TPW·w, 16·TPW·(w+1)) × all 64 channels (TPW × 4 MFMA tiles). Per chunk every thread
+//   * has the chunk's global data already in registers (issued one whole chunk earlier: the
+//     gathers' latency hides behind a chunk of MFMAs, not one K step),
+//   * stores it to LDS applying the operand transform (BN+ReLU prologue | folded BN backward),
+//   * issues the next chunk's loads, then runs the chunk's MFMAs from LDS
+//     (per 32-K step: TPW + 4 fragment reads for 4·TPW MFMAs).
+// Coalesced staging: 16-B vectors, consecutive lanes read consecutive channels of one pixel.
+// Epilogue as conv_gemm_kernel (stage the tile in LDS, vectorised stores, statistics).
 // =====================================================================================
-template <class P>
+template <class P, int TM, int WN>
 struct ConvK {
-  static constexpr int KB = P::kF32 ? 128 : 256;           // K elements per staged chunk
-  static constexpr int LDB = KB + (P::kF32 ? 4 : 8);       // LDS pitch (elements) of the chunk rows
-  static constexpr int NOUT = 64;
-  static constexpr int PREF = NOUT * KB / P::VEC / 256;    // 16-B chunks per thread per K-chunk (8)
-  static size_t smem(int kc) {
-    return (size_t)NOUT * LDB * P::ES + (size_t)3 * kc * 4 + (size_t)4 * NOUT * 3 * 4 +
-           (size_t)4 * 16 * NOUT * P::ES;
-  }
+  static constexpr int WM = 4 / WN;                                        // waves along M
+  static constexpr int KB = 64 / (P::kF32 ? 2 : 1);                        // K elements per chunk (128 B rows)
+  static constexpr int LD = KB + (P::kF32 ? 4 : 8);                        // LDS pitch (elements)
+  static constexpr int BN = 64 * WN;                                       // output channels per workgroup
+  static constexpr int BM = 16 * TM * WM;                                  // pixels per workgroup
+  static constexpr int CPR = KB / P::VEC;                                  // 16-B chunks per row (8)
+  static constexpr int RPI = 256 / CPR;                                    // rows per thread pass (32)
+  static constexpr int NA = BM / RPI;                                      // A chunks per thread
+  static constexpr int NB = BN / RPI;                                      // B chunks per thread
+  static_assert(NA >= 1 && NB >= 1, "tile too small for the staging map");
+  static_assert(4 * 16 * 64 <= (BM + BN) * LD, "epilogue staging must fit the operand tiles");
+  static size_t smem(int kc) { return (size_t)(BM + BN) * LD * P::ES + (size_t)3 * kc * 4 + (size_t)4 * 64 * 3 * 4; }
 };
 
-template <class P, int TPW, int AOP, int PRO, int MODE, int EPI>
+// wave (wm, wn) = (wid / WN, wid % WN) owns pixel rows [16·TM·wm, +16·TM) × channels [64·wn, +64) of the
+// workgroup tile: TM × 4 MFMA tiles, TM + 4 fragment reads per 4·TM MFMAs per 32-K step.
+template <class P, int TM, int WN, int AOP, int PRO, int MODE, int EPI>
 __global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
   using T = typename P::T;
   using frag_t = typename P::frag_t;
-  using CK = ConvK<P>;
+  using CK = ConvK<P, TM, WN>;
   constexpr int V = P::VEC;
   constexpr int NT = 4;
-  constexpr int NOUT = CK::NOUT;
+  constexpr int NOUT = 64;      // channels per wave (epilogue unit)
   constexpr int KB = CK::KB;
-  constexpr int LDB = CK::LDB;
-  const int c = blockIdx.y;
+  constexpr int LD = CK::LD;
+  constexpr bool DY = AOP == AOP_DY;
+  // XCD-aware order: workgroups are dispatched round-robin over the 8 XCDs (linear id mod 8); remap so
+  // each XCD runs a contiguous run of (client, N-tile, M-tile) — the tiles that share one client's
+  // weights and activations hit the same L2
+  const int gx = gridDim.x, gz = gridDim.z;
+  const int total = gx * gridDim.y * gz;
+  int lin = blockIdx.x + gx * (blockIdx.y + gridDim.y * blockIdx.z);
+  const int full = total / 8 * 8;
+  if (lin < full) lin = (lin % 8) * (full / 8) + lin / 8;
+  const int bx = lin % gx;
+  const int bz = (lin / gx) % gz;
+  const int c = lin / (gx * gz);
   const int NO = a.nout_total;
-  const int ch_base = blockIdx.z * NOUT;
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
+  const int wm = wid / WN, wn = wid % WN;
+  const int ch_base = bz * CK::BN;
+  const int ch_w = ch_base + wn * 64;
   const int K = a.KH * a.KW * a.KC;
   const int Mo = a.Nb * a.Ho * a.Wo;
   const int HWi = MODE == MODE_BWD2 ? a.Hs * a.Ws : a.Ho * a.Wo;
   const int M = MODE == MODE_BWD2 ? a.Nb * HWi : Mo;
   const int Mv = a.nimg ? min(M, a.nimg[c] * HWi) : M;
-  if ((int)(blockIdx.x * 4 * TPW) * 16 >= Mv) return;   // uniform: whole workgroup idle
+  const int m0 = bx * CK::BM;
+  if (m0 >= Mv) return;   // uniform: whole workgroup idle
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  T* wl = reinterpret_cast<T*>(smem);                                              // [NOUT][LDB]
-  float* v0 = reinterpret_cast<float*>(smem + (size_t)NOUT * LDB * P::ES);        // [KC]
+  T* al = reinterpret_cast<T*>(smem);                                               // [BM][LD]
+  T* wl = al + CK::BM * LD;                                                         // [BN][LD]
+  float* v0 = reinterpret_cast<float*>(wl + CK::BN * LD);                          // [KC]
   float* v1 = v0 + a.KC;
   float* v2 = v1 + a.KC;
-  float* red = v2 + a.KC;                                                           // [4][NOUT][3]
-  T* stage = reinterpret_cast<T*>(red + 4 * NOUT * 3);                             // [4][16][NOUT]
-  T* my_stage = stage + wid * 16 * NOUT;
+  float* red = v2 + a.KC;                                                           // [4 waves][64][3]
+  T* my_stage = al + wid * 16 * NOUT;   // epilogue staging [4][16][64] reuses the operand tiles
 
-  if (AOP == AOP_DY || PRO == PRO_BNRELU) {
+  if (DY || PRO == PRO_BNRELU) {
     for (int i = threadIdx.x; i < a.KC; i += 256) {
       v0[i] = a.vec0[(int64_t)c * a.KC + i];
       v1[i] = a.vec1[(int64_t)c * a.KC + i];
-      if (AOP == AOP_DY) v2[i] = a.vec2[(int64_t)c * a.KC + i];
+      if (DY) v2[i] = a.vec2[(int64_t)c * a.KC + i];
     }
   }
   for (int i = threadIdx.x; i < 4 * NOUT * 3; i += 256) red[i] = 0.f;
 
   const int64_t src_client = (int64_t)c * a.Nb * a.Hs * a.Ws * a.KC;
   const T* src = reinterpret_cast<const T*>(a.src) + src_client;
-  const T* src2 = (AOP == AOP_DY) ? reinterpret_cast<const T*>(a.src2) + src_client : nullptr;
+  const T* src2 = DY ? reinterpret_cast<const T*>(a.src2) + src_client : nullptr;
   T* out = reinterpret_cast<T*>(a.out) + (int64_t)c * Mo * NO;
   const T* wsrc = reinterpret_cast<const T*>(a.wpk) + (int64_t)c * a.wpk_ld + (int64_t)ch_base * a.ldk;
 
-  // per-lane pixel decode of this wave's TPW tiles
-  const int tiles_total = (Mv + 15) / 16;
-  const int tile0 = (blockIdx.x * 4 + wid) * TPW;
+  // this thread's staging slots: column chunk `col` of rows row0 + RPI·j
+  const int col = threadIdx.x % CK::CPR;
+  const int row0 = threadIdx.x / CK::CPR;
   const int IW = MODE == MODE_BWD2 ? a.Ws : a.Wo;
-  int pn[TPW], ph[TPW], pw[TPW];
-  bool pv[TPW];
+  int rn[CK::NA], rhw[CK::NA];   // image index, (h << 16 | w) of the row's iteration pixel; rn < 0: invalid
 #pragma unroll
-  for (int t = 0; t < TPW; ++t) {
-    const int m = (tile0 + t) * 16 + (lane & 15);
-    pv[t] = m < Mv;
-    const int mm = pv[t] ? m : 0;
-    pn[t] = mm / HWi;
-    const int r = mm % HWi;
-    ph[t] = r / IW;
-    pw[t] = r % IW;
+  for (int j = 0; j < CK::NA; ++j) {
+    const int m = m0 + row0 + CK::RPI * j;
+    if (m < Mv) {
+      rn[j] = m / HWi;
+      const int r = m % HWi;
+      rhw[j] = ((r / IW) << 16) | (r % IW);
+    } else {
+      rn[j] = -1;
+      rhw[j] = 0;
+    }
   }
 
-  f32x4 acc[TPW][NT];
+  f32x4 acc[TM][NT];
 #pragma unroll
-  for (int t = 0; t < TPW; ++t)
+  for (int t = 0; t < TM; ++t)
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[t][nt] = {0.f, 0.f, 0.f, 0.f};
 
-  // weight-chunk staging: thread i moves 16-B chunks i, i+256, ... of the [NOUT][kn] chunk
-  uint4 pre[CK::PREF];
-  auto fetch = [&](int kbase, int kn) {
-    const int cpr = kn / V;
+  uint4 ra[CK::NA], ry[DY ? CK::NA : 1], rb[CK::NB];
+  uint32_t aval = 0;
+  auto fetch = [&](int kbase) {
+    const int k = kbase + col * V;
+    const bool kval = k < K;
+    const int tap = kval ? k / a.KC : 0, ci = kval ? k % a.KC : 0;
+    const int kh = tap / a.KW, kw = tap % a.KW;
+    aval = 0;
 #pragma unroll
-    for (int it = 0; it < CK::PREF; ++it) {
-      const int i = threadIdx.x + it * 256;
-      pre[it] = make_uint4(0, 0, 0, 0);
-      if (i < NOUT * cpr) {
-        const int row = i / cpr, col = (i % cpr) * V;
-        pre[it] = *reinterpret_cast<const uint4*>(wsrc + (int64_t)row * a.ldk + kbase + col);
+    for (int j = 0; j < CK::NA; ++j) {
+      ra[j] = make_uint4(0, 0, 0, 0);
+      if (DY) ry[j] = make_uint4(0, 0, 0, 0);
+      if (rn[j] >= 0 && kval) {
+        const int ph = rhw[j] >> 16, pw = rhw[j] & 0xffff;
+        int ih, iw;
+        bool ok;
+        if (MODE == MODE_BWD2) {
+          ih = ph; iw = pw; ok = true;
+        } else if (MODE == MODE_FWD) {
+          ih = ph * a.stride - a.pad + kh;
+          iw = pw * a.stride - a.pad + kw;
+          ok = ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws;
+        } else {
+          const int th = ph + a.pad - kh, tw = pw + a.pad - kw;
+          ok = th >= 0 && tw >= 0 && (th % a.stride) == 0 && (tw % a.stride) == 0;
+          ih = th / a.stride;
+          iw = tw / a.stride;
+          ok = ok && ih < a.Hs && iw < a.Ws;
+        }
+        if (ok) {
+          const int64_t off = (((int64_t)rn[j] * a.Hs + ih) * a.Ws + iw) * a.KC + ci;
+          ra[j] = *reinterpret_cast<const uint4*>(src + off);
+          if (DY) ry[j] = *reinterpret_cast<const uint4*>(src2 + off);
+          aval |= 1u << j;
+        }
       }
     }
-  };
-  auto put = [&](int kn) {
-    const int cpr = kn / V;
 #pragma unroll
-    for (int it = 0; it < CK::PREF; ++it) {
-      const int i = threadIdx.x + it * 256;
-      if (i < NOUT * cpr) *reinterpret_cast<uint4*>(wl + (i / cpr) * LDB + (i % cpr) * V) = pre[it];
+    for (int j = 0; j < CK::NB; ++j)
+      rb[j] = kval ? *reinterpret_cast<const uint4*>(wsrc + (int64_t)(row0 + CK::RPI * j) * a.ldk + k)
+                   : make_uint4(0, 0, 0, 0);
+  };
+  auto put = [&](int kbase) {
+    const int k = kbase + col * V;
+    const int ci = k < K ? k % a.KC : 0;
+#pragma unroll
+    for (int j = 0; j < CK::NA; ++j) {
+      uint4 v = make_uint4(0, 0, 0, 0);   // out-of-image taps / padding rows: 0 (not the transform of 0)
+      if ((aval >> j) & 1u) {
+        if (PRO == PRO_BNRELU || DY) {
+          float f[V];
+          P::unpack(ra[j], f);
+          if (DY) {
+            float yv[V];
+            P::unpack(ry[j], yv);
+#pragma unroll
+            for (int e = 0; e < V; ++e) f[e] = v0[ci + e] * f[e] + v1[ci + e] * yv[e] + v2[ci + e];
+          } else {
+#pragma unroll
+            for (int e = 0; e < V; ++e) f[e] = fmaxf(f[e] * v0[ci + e] + v1[ci + e], 0.f);
+          }
+          v = P::pack(f);
+        } else {
+          v = ra[j];
+        }
+      }
+      *reinterpret_cast<uint4*>(al + (row0 + CK::RPI * j) * LD + col * V) = v;
     }
+#pragma unroll
+    for (int j = 0; j < CK::NB; ++j) *reinterpret_cast<uint4*>(wl + (row0 + CK::RPI * j) * LD + col * V) = rb[j];
   };
 
-  fetch(0, min(KB, a.Kp));
+  const T* my_a = al + (wm * 16 * TM + (lane & 15)) * LD + 8 * (lane >> 4);
+  const T* my_b = wl + (wn * 64 + (lane & 15)) * LD + 8 * (lane >> 4);
+  __syncthreads();   // prologue vectors visible to put()
+  fetch(0);
   for (int kbase = 0; kbase < a.Kp; kbase += KB) {
-    const int kn = min(KB, a.Kp - kbase);       // multiple of 32
-    __syncthreads();                            // previous chunk fully consumed
-    put(kn);
+    const int kn = min(KB, a.Kp - kbase);   // multiple of 32
+    if (kbase) __syncthreads();             // previous chunk fully consumed
+    put(kbase);
     __syncthreads();
-    if (kbase + KB < a.Kp) fetch(kbase + KB, min(KB, a.Kp - kbase - KB));
+    if (kbase + KB < a.Kp) fetch(kbase + KB);
     for (int k0 = 0; k0 < kn; k0 += 32) {
-      const int k = kbase + k0 + 8 * (lane >> 4);
-      const bool kval = k < K;
-      const int tap = k / a.KC, ci = k % a.KC;
-      const int kh = tap / a.KW, kw = tap % a.KW;
-      frag_t af[TPW];
+      frag_t af[TM];
 #pragma unroll
-      for (int t = 0; t < TPW; ++t) {
-        float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-        if (pv[t] && kval) {
-          int ih, iw;
-          bool ok;
-          if (MODE == MODE_BWD2) {
-            ih = ph[t]; iw = pw[t]; ok = true;
-          } else if (MODE == MODE_FWD) {
-            ih = ph[t] * a.stride - a.pad + kh;
-            iw = pw[t] * a.stride - a.pad + kw;
-            ok = ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws;
-          } else {
-            const int th = ph[t] + a.pad - kh, tw = pw[t] + a.pad - kw;
-            ok = th >= 0 && tw >= 0 && (th % a.stride) == 0 && (tw % a.stride) == 0;
-            ih = th / a.stride;
-            iw = tw / a.stride;
-            ok = ok && ih < a.Hs && iw < a.Ws;
-          }
-          if (ok) {
-            const int64_t off = (((int64_t)pn[t] * a.Hs + ih) * a.Ws + iw) * a.KC + ci;
-            P::load8(src + off, f);
-            if (AOP == AOP_ACT && PRO == PRO_BNRELU) {
-#pragma unroll
-              for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j] * v0[ci + j] + v1[ci + j], 0.f);
-            } else if (AOP == AOP_DY) {
-              float yv[8];
-              P::load8(src2 + off, yv);
-#pragma unroll
-              for (int j = 0; j < 8; ++j) f[j] = v0[ci + j] * f[j] + v1[ci + j] * yv[j] + v2[ci + j];
-            }
-          }
-        }
-        af[t] = P::frag8(f);
-      }
+      for (int t = 0; t < TM; ++t) af[t] = P::frag(my_a + t * 16 * LD + k0);
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
-        const frag_t bv = P::frag(wl + (nt * 16 + (lane & 15)) * LDB + k0 + 8 * (lane >> 4));
+        const frag_t bv = P::frag(my_b + nt * 16 * LD + k0);
 #pragma unroll
-        for (int t = 0; t < TPW; ++t) acc[t][nt] = P::mma(af[t], bv, acc[t][nt]);
+        for (int t = 0; t < TM; ++t) acc[t][nt] = P::mma(af[t], bv, acc[t][nt]);
       }
     }
   }
-
+  __syncthreads();   // every wave done with the operand tiles before they hold the epilogue staging
+  const int tiles_total = (Mv + 15) / 16;
+  const int tile0 = m0 / 16 + wm * TM;
   const T* e_x = reinterpret_cast<const T*>(a.e_x);
   const T* e_add = reinterpret_cast<const T*>(a.e_add);
   const T* e_y1 = reinterpret_cast<const T*>(a.e_y1);
@@ -633,10 +673,10 @@ __global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
   float kpiv[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
-    kpiv[nt] = (EPI == EPI_FWD && a.pivot) ? a.pivot[(int64_t)c * NO + ch_base + nt * 16 + (lane & 15)] : 0.f;
+    kpiv[nt] = (EPI == EPI_FWD && a.pivot) ? a.pivot[(int64_t)c * NO + ch_w + nt * 16 + (lane & 15)] : 0.f;
 
 #pragma unroll
-  for (int t = 0; t < TPW; ++t) {
+  for (int t = 0; t < TM; ++t) {
     const int tile = tile0 + t;
     if (tile >= tiles_total) break;
 #pragma unroll
@@ -653,12 +693,12 @@ __global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
       if (lane / CG < ROWS_PER_PASS && row < rows_valid) {
         const int ch0 = my_cg * V;
         const uint4 dv = *reinterpret_cast<const uint4*>(my_stage + row * NOUT + ch0);
-        int64_t goff = ((int64_t)(tile * 16 + row)) * NO + ch_base + ch0;
+        int64_t goff = ((int64_t)(tile * 16 + row)) * NO + ch_w + ch0;
         if (MODE == MODE_BWD2) {
           const int pm = tile * 16 + row;
           const int n_ = pm / HWi, r_ = pm % HWi;
           const int64_t px = ((int64_t)n_ * a.Ho + 2 * (r_ / a.Ws)) * a.Wo + 2 * (r_ % a.Ws);
-          goff = px * NO + ch_base + ch0;
+          goff = px * NO + ch_w + ch0;
           const uint4 z = make_uint4(0, 0, 0, 0);
           *reinterpret_cast<uint4*>(out + goff + NO) = z;
           *reinterpret_cast<uint4*>(out + goff + (int64_t)a.Wo * NO) = z;
@@ -680,7 +720,7 @@ __global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
           if (EPI == EPI_MASK) {
 #pragma unroll
             for (int j = 0; j < V; ++j) {
-              const int ch = ch_base + ch0 + j;
+              const int ch = ch_w + ch0 + j;
               const bool on_ = xv[j] * a.e_s[(int64_t)c * NO + ch] + a.e_t[(int64_t)c * NO + ch] > 0.f;
               g[j] = on_ ? g[j] : 0.f;
             }
@@ -735,11 +775,13 @@ __global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
       }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < NOUT * a.NS; i += 256) {
-      const int ch = i / a.NS, q = i % a.NS;
-      const float s = red[(0 * NOUT + ch) * 3 + q] + red[(1 * NOUT + ch) * 3 + q] + red[(2 * NOUT + ch) * 3 + q] +
-                      red[(3 * NOUT + ch) * 3 + q];
-      atomicAdd(&a.stats[((int64_t)c * NO + ch_base + ch) * a.NS + q], s);
+    for (int i = threadIdx.x; i < CK::BN * a.NS; i += 256) {
+      const int chb = i / a.NS, q = i % a.NS;
+      const int wn_ = chb / 64, ch = chb % 64;
+      float s = 0.f;
+#pragma unroll
+      for (int m_ = 0; m_ < CK::WM; ++m_) s += red[((m_ * WN + wn_) * NOUT + ch) * 3 + q];
+      atomicAdd(&a.stats[((int64_t)c * NO + ch_base + chb) * a.NS + q], s);
     }
   }
 }
@@ -754,29 +796,41 @@ static int convk_min_k() {
   return v;
 }
 
-template <class P, int TPW, int AOP, int PRO, int MODE, int EPI>
+template <class P, int TM, int WN, int AOP, int PRO, int MODE, int EPI>
 static int launch_convk_t(ConvArgs a, int nout, int C, hipStream_t stream) {
+  using CK = ConvK<P, TM, WN>;
   a.nout_total = nout;
+  if (nout % CK::BN != 0) return -2;
   const int M = MODE == MODE_BWD2 ? a.Nb * a.Hs * a.Ws : a.Nb * a.Ho * a.Wo;
-  const int tiles = (M + 15) / 16;
-  const int gx = (tiles + 4 * TPW - 1) / (4 * TPW);
-  const size_t smem = ConvK<P>::smem(a.KC);
+  const int gx = (M + CK::BM - 1) / CK::BM;
+  const size_t smem = CK::smem(a.KC);
   if (smem > 160 * 1024) return -5;
-  auto kern = convk_gemm_kernel<P, TPW, AOP, PRO, MODE, EPI>;
+  auto kern = convk_gemm_kernel<P, TM, WN, AOP, PRO, MODE, EPI>;
   if (smem > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-  hipLaunchKernelGGL(kern, dim3(gx, C, nout / 64), dim3(256), smem, stream, a);
+  hipLaunchKernelGGL(kern, dim3(gx, C, nout / CK::BN), dim3(256), smem, stream, a);
   return (int)hipGetLastError();
 }
 
-// tiles per wave: as many as keep ≥ ~2048 workgroups over the chip (8 XCDs × 32 CUs × 8)
+// tile shape: 128 × 128 (2 × 2 waves of 64 × 64) for ≥ 128 outputs; 64-output layers 256 / 128 / 64 × 64
+// by the workgroup count (FEDML_AMD_CONVK_TILE forces 0: 128x128, 1: 256x64, 2: 128x64, 3: 64x64)
 template <class P, int AOP, int PRO, int MODE, int EPI>
 static int launch_convk(ConvArgs a, int nout, int C, hipStream_t s) {
+  static int force = -2;
+  if (force == -2) {
+    const char* e = getenv("FEDML_AMD_CONVK_TILE");
+    force = e ? atoi(e) : -1;
+  }
   if (nout % 64 != 0) return -2;
   const int M = MODE == MODE_BWD2 ? a.Nb * a.Hs * a.Ws : a.Nb * a.Ho * a.Wo;
-  const int64_t wgs1 = (int64_t)((M + 63) / 64) * C * (nout / 64);
-  if (wgs1 >= 8192) return launch_convk_t<P, 4, AOP, PRO, MODE, EPI>(a, nout, C, s);
-  if (wgs1 >= 4096) return launch_convk_t<P, 2, AOP, PRO, MODE, EPI>(a, nout, C, s);
-  return launch_convk_t<P, 1, AOP, PRO, MODE, EPI>(a, nout, C, s);
+  const int64_t wgs1 = (int64_t)((M + 63) / 64) * C * (nout / 64);   // workgroups of a 64 × 64 tile
+  int pick = force;
+  if (pick < 0) pick = nout % 128 == 0 ? 0 : (wgs1 >= 4096 ? 1 : (wgs1 >= 1024 ? 2 : 3));
+  switch (pick) {
+    case 0: return launch_convk_t<P, 4, 2, AOP, PRO, MODE, EPI>(a, nout, C, s);
+    case 1: return launch_convk_t<P, 4, 1, AOP, PRO, MODE, EPI>(a, nout, C, s);
+    case 2: return launch_convk_t<P, 2, 1, AOP, PRO, MODE, EPI>(a, nout, C, s);
+    default: return launch_convk_t<P, 1, 1, AOP, PRO, MODE, EPI>(a, nout, C, s);
+  }
 }
 
 template <class P, int NT, int AOP, int PRO, int MODE, int EPI>

@@ -50,11 +50,17 @@ class DeviceClientStore:
         off = 0
         for cid in ids:
             cd = train_local[cid]
-            xs.append(cd.x)
-            ys.append(cd.y)
+            if hasattr(cd, "x"):
+                cx, cy = cd.x, cd.y
+            else:   # a user's loader (DataLoader / list of (x, y) batches): one pass to stage it in HBM
+                batches = list(cd)
+                cx = torch.cat([torch.as_tensor(b[0]) for b in batches])
+                cy = torch.cat([torch.as_tensor(b[1]) for b in batches])
+            xs.append(cx)
+            ys.append(cy)
             offs.append(off)
-            cnts.append(len(cd.x))
-            off += len(cd.x)
+            cnts.append(len(cx))
+            off += len(cx)
         x = torch.cat(xs).to(device)
         if dtype is not None and x.is_floating_point():
             x = x.to(dtype)

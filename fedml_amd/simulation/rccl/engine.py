@@ -40,6 +40,38 @@ def _close_engines():
             pass
 
 
+def _default_loss(args) -> str:
+    """The reference picks the trainer (and so the loss) by dataset (trainers/factory.py)."""
+    ds = str(getattr(args, "dataset", "") or "")
+    if ds == "stackoverflow_lr":
+        return "bce_sum"
+    if ds in ("fed_shakespeare", "stackoverflow_nwp", "shakespeare"):
+        return "nwp_ce"
+    return "ce"
+
+
+def _task_loss(name: str, out: torch.Tensor, y: torch.Tensor, mask: Optional[torch.Tensor]) -> torch.Tensor:
+    """Per-client loss [C] of a client-stacked batch, each exactly the reference criterion on that
+    client's valid rows (``mask`` [C, B] bool; None = all rows).
+      nwp_ce : out [C, B, V, T] logits, y [C, B, T]; CE(ignore_index=0) mean over the client's
+               non-padding tokens (my_model_trainer_nwp.py)
+      bce_sum: out [C, B, K] probabilities, y [C, B, K] {0,1}; BCE summed over rows and labels
+               (my_model_trainer_tag_prediction.py)"""
+    C, B = out.shape[0], out.shape[1]
+    rows = mask.to(torch.float32) if mask is not None else torch.ones(C, B, device=out.device)
+    if name == "nwp_ce":
+        V = out.shape[2]
+        l = torch.nn.functional.cross_entropy(out.float().reshape(C * B, V, -1), y.reshape(C * B, -1), ignore_index=0,
+                                              reduction="none").view(C, B, -1)
+        valid = (y.view(C, B, -1) != 0).to(torch.float32) * rows.unsqueeze(-1)
+        return (l * valid).sum((1, 2)) / valid.sum((1, 2)).clamp_min(1.0)
+    if name == "bce_sum":
+        l = torch.nn.functional.binary_cross_entropy(out.float(), y.to(out.device).float().view_as(out),
+                                                     reduction="none")
+        return (l.sum(-1) * rows).sum(1)
+    raise ValueError(name)
+
+
 def _is_wide_convnet(model: torch.nn.Module, min_channels: int = 128) -> bool:
     """True when most conv MACs sit in layers with ≥ ``min_channels`` input channels."""
     wide = total = 0
@@ -109,11 +141,23 @@ class ClientBatchEngine:
             os.environ.get("FEDML_AMD_TF_GRAPHS", "0") == "1"
         self._active_cache = {}
         self._graphs = {}
+        # task loss of the reference trainer this engine stands in for (core/alg_frame/functional.py):
+        #   ce      my_model_trainer_classification.py  CrossEntropyLoss (per-client batch mean)
+        #   nwp_ce  my_model_trainer_nwp.py             CrossEntropyLoss(ignore_index=0), logits [B, V, T]
+        #   bce_sum my_model_trainer_tag_prediction.py  BCELoss(reduction="sum") on sigmoid outputs
+        self.loss_name = str(getattr(args, "loss_name", None) or _default_loss(args))
+        if self.loss_name not in ("ce", "nwp_ce", "bce_sum"):
+            raise ValueError(f"loss_name {self.loss_name!r}: expected ce | nwp_ce | bce_sum")
+        # per-client global gradient-norm clip before the optimizer (torch.nn.utils.clip_grad_norm_
+        # semantics, e.g. S-FedAvg's clip 1.0: simulation/sp/valuation_base.py)
+        cg = getattr(args, "clip_grad_norm", None)
+        self.clip_grad_norm = float(cg) if cg not in (None, "", 0, 0.0) else None
         _LIVE_ENGINES.add(self)
         self.use_graphs = self.device.type == "cuda" and os.environ.get("FEDML_AMD_HIP_GRAPHS", "1") != "0"
         self.native = None
         self.native_step = None
-        if self.device.type == "cuda" and not self.sequential and os.environ.get("FEDML_AMD_NATIVE_CONV", "1") != "0":
+        if self.device.type == "cuda" and not self.sequential and self.loss_name == "ce" and \
+                os.environ.get("FEDML_AMD_NATIVE_CONV", "1") != "0":
             from ...parallel.native_resnet import NativeResNetStep, UnsupportedNative
             # the native kernels run at the requested precision: fp32 (compute_dtype None / fp32, the
             # reference's) or bf16; any other dtype keeps the torch path, which honours it
@@ -234,7 +278,8 @@ class ClientBatchEngine:
                 if self.native_step is not None and self.use_graphs:
                     # heterogeneous batches stay native: per-client valid counts go in as data (nimg)
                     loss = self._graph_step(x, y, mask, b_c, active, lr, first)
-                elif self.tf is not None and self.use_graphs and self._tf_capture and sample_mask is None:
+                elif self.tf is not None and self.use_graphs and self._tf_capture and sample_mask is None and \
+                        self.loss_name == "ce":
                     loss = self._tf_graph_step(x, y, mask, b_c, active, lr, first)
                 elif self.sequential and self.tf is None and self.use_graphs and self._seq_capture and uniform:
                     loss = self._seq_graph_step(x, y, b_c, active, lr, first)
@@ -274,17 +319,20 @@ class ClientBatchEngine:
         if self.sequential and self.tf is None:
             return self._seq_step_loss(x, y, b_c)
         C, B = out.shape[0], out.shape[1]
-        logits = out.reshape(C * B, -1)
-        if not logits.is_contiguous():
-            logits = logits.contiguous()
-        labels = y.reshape(C * B)
-        bc = torch.tensor([max(1, b) for b in b_c], dtype=torch.float32, device=self.device)
-        row_scale = (mask.to(torch.float32) / bc.view(C, 1)).reshape(C * B)
-        if use_native_loss:
-            loss = ops.FusedCrossEntropy.apply(logits, labels, row_scale, None)
+        if self.loss_name != "ce":
+            loss = _task_loss(self.loss_name, out, y, mask).sum()
         else:
-            lr_ = torch.nn.functional.cross_entropy(logits.float(), labels, reduction="none")
-            loss = (lr_ * row_scale).sum()
+            logits = out.reshape(C * B, -1)
+            if not logits.is_contiguous():
+                logits = logits.contiguous()
+            labels = y.reshape(C * B)
+            bc = torch.tensor([max(1, b) for b in b_c], dtype=torch.float32, device=self.device)
+            row_scale = (mask.to(torch.float32) / bc.view(C, 1)).reshape(C * B)
+            if use_native_loss:
+                loss = ops.FusedCrossEntropy.apply(logits, labels, row_scale, None)
+            else:
+                lr_ = torch.nn.functional.cross_entropy(logits.float(), labels, reduction="none")
+                loss = (lr_ * row_scale).sum()
         loss.backward()
         if self.interp is not None:
             self.interp.flush_deferred()
@@ -517,7 +565,10 @@ class ClientBatchEngine:
                     out = torch.func.functional_call(self.model, {**pv, **bufs}, (xc,))
                 if isinstance(out, tuple):
                     out = out[-1]
-                loss = torch.nn.functional.cross_entropy(out.float().reshape(b, -1), y[c, :b].reshape(b))
+                if self.loss_name == "ce":
+                    loss = torch.nn.functional.cross_entropy(out.float().reshape(b, -1), y[c, :b].reshape(b))
+                else:
+                    loss = _task_loss(self.loss_name, out.unsqueeze(0), y[c:c + 1, :b], None)[0]
                 keys = list(pv.keys())
                 leaves = [pv[k] for k in keys]
                 grads = torch.autograd.grad(loss, leaves, allow_unused=True)
@@ -630,7 +681,14 @@ class ClientBatchEngine:
         g.replay()
         return loss
 
+    def _clip_grads(self):
+        """Per-client clip of the whole gradient row to ``clip_grad_norm`` (capture-safe torch ops)."""
+        norm = torch.linalg.vector_norm(self.grads, dim=1, keepdim=True)
+        self.grads.mul_((self.clip_grad_norm / (norm + 1e-6)).clamp_max(1.0))
+
     def _optimizer_step(self, lr, active, first):
+        if self.clip_grad_norm is not None:
+            self._clip_grads()
         if self.optimizer == "sgd":
             self._shadow_stale = True
             ops.sgd_step(self.params, self.grads, lr, weight_decay=self.weight_decay if self.sgd_wd else 0.0,

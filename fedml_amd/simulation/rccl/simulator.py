@@ -13,6 +13,7 @@ One process per GPU. Per round:
   4. optional server optimizer (FedOpt: fused HIP kernel), robust aggregation, evaluation,
      checkpointing.
 """
+import copy
 import logging
 import math
 import os
@@ -45,8 +46,20 @@ def _dtype(name):
 
 
 class RCCLSimulator:
-    def __init__(self, args, device, dataset, model, store: Optional[DeviceClientStore] = None):
+    def __init__(self, args, device, dataset, model, store: Optional[DeviceClientStore] = None, model_trainer=None):
+        """``model_trainer`` (reference ``fedml.run_simulation(..., model_trainer)``): a functional trainer
+        (``FunctionalTrainerMixin``: standard supervised SGD/Adam with a named loss) configures the
+        client-batched engine (loss_name, clip_grad_norm); any other ``ClientTrainer`` runs its own
+        ``train()`` per client (compatibility path) and only aggregation stays on the GPU."""
         self.args = args
+        self.user_trainer = None
+        if model_trainer is not None:
+            if getattr(model_trainer, "functional", False):
+                args.loss_name = getattr(model_trainer, "loss_name", "ce")
+                if getattr(model_trainer, "clip_grad_norm", None) is not None:
+                    args.clip_grad_norm = model_trainer.clip_grad_norm
+            else:
+                self.user_trainer = model_trainer
         self.device = torch.device(device)
         self.rank, self.world = comm.init_process_group(device=self.device if self.device.type == "cuda" else None)
         self.model = model.to(self.device)
@@ -120,9 +133,12 @@ class RCCLSimulator:
             # data order / augmentation keyed by (seed, round, client): identical for any world size and
             # exactly reproducible on resume from the round index alone
             rng_key = (int(getattr(args, "random_seed", 0)) * 1000003 + int(round_idx) * 7919) & 0x7FFFFFFF
-            self.engine.train(self.store, slots, int(args.epochs), int(args.batch_size), float(args.learning_rate),
-                              generator=self.gen, shuffle=bool(getattr(args, "shuffle", True)), valid_slots=valid,
-                              rng_key=rng_key)
+            if self.user_trainer is not None:
+                self._train_user_trainer(mine)
+            else:
+                self.engine.train(self.store, slots, int(args.epochs), int(args.batch_size),
+                                  float(args.learning_rate), generator=self.gen,
+                                  shuffle=bool(getattr(args, "shuffle", True)), valid_slots=valid, rng_key=rng_key)
         with tr.span("round.aggregate"):
             w = torch.where(valid, self.store.counts[slots].to(torch.float32), torch.zeros(self.C, device=self.device))
             if self.faults.active:
@@ -167,6 +183,26 @@ class RCCLSimulator:
             else:
                 self.global_flat.copy_(avg)
             self._post_aggregate()
+
+    def _train_user_trainer(self, mine):
+        """Compatibility path for a non-functional ``ClientTrainer`` (reference client.py:27-47 call
+        order: set_id → set_model_params(global) → train(local data) → get_model_params): each of this
+        rank's clients trains through the user's own loop; its weights land in the engine's slot so the
+        weighted sum and the all-reduce run exactly as on the batched path."""
+        if self.dataset is None:
+            raise ValueError("a user ClientTrainer needs the dataset's per-client loaders (dataset[5])")
+        tr = self.user_trainer
+        glob = self.layout.unflatten(self.global_flat.detach().cpu())
+        losses = []
+        for slot, cid in enumerate(mine):
+            tr.set_id(int(cid))
+            tr.set_model_params(copy.deepcopy(glob))
+            out = tr.train(self.dataset[5][int(cid)], self.device, self.args)
+            if isinstance(out, (int, float)):
+                losses.append(float(out))
+            sd = tr.get_model_params()
+            self.engine.set_client_params(slot, self.layout.flatten(sd, device=self.device))
+        self.engine.last_loss = torch.tensor(sum(losses) / len(losses) if losses else float("nan"))
 
     def _robust_preaggregate(self, w):
         dt = getattr(self.args, "defense_type", None)
@@ -228,9 +264,20 @@ class RCCLSimulator:
             x = test.x[s:e].to(self.device)
             y = test.y[s:e].to(self.device)
             out = self.model(x).float()
-            stats[0] += (out.argmax(-1) == y).sum()
-            stats[1] += torch.nn.functional.cross_entropy(out, y, reduction="sum")
-            stats[2] += (e - s)
+            ln = self.engine.loss_name
+            if ln == "nwp_ce":   # my_model_trainer_nwp.py test(): accuracy over non-padding tokens
+                tok = y != 0
+                stats[0] += ((out.argmax(1) == y) & tok).sum()
+                stats[1] += torch.nn.functional.cross_entropy(out, y, ignore_index=0, reduction="sum")
+                stats[2] += tok.sum()
+            elif ln == "bce_sum":   # my_model_trainer_tag_prediction.py test(): exact tag-set match
+                stats[0] += ((out > 0.5).int() == y.int()).all(1).sum()
+                stats[1] += torch.nn.functional.binary_cross_entropy(out, y.float(), reduction="sum")
+                stats[2] += (e - s)
+            else:
+                stats[0] += (out.argmax(-1) == y).sum()
+                stats[1] += torch.nn.functional.cross_entropy(out, y, reduction="sum")
+                stats[2] += (e - s)
         comm.all_reduce_flat(stats)
         self.model.train()
         tot = max(1.0, float(stats[2]))

@@ -111,7 +111,7 @@ class SimulatorRCCL:
                             args.federated_optimizer)
             self.simulator = SimulatorSingleProcess(args, device, dataset, model, model_trainer)
         else:
-            self.simulator = RCCLSimulator(args, device, dataset, model)
+            self.simulator = RCCLSimulator(args, device, dataset, model, model_trainer=model_trainer)
 
     def run(self):
         return self.simulator.run()
