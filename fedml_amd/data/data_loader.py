@@ -52,9 +52,16 @@ def read_leaf(train_dir, test_dir):
 
 
 def _leaf_batches(data, batch_size):
-    """Reference batching: seed 100, shuffle x and y with the same RNG state."""
-    x = np.asarray(data["x"], dtype=np.float32)
-    y = np.asarray(data["y"], dtype=np.int64)
+    """Reference batching: seed 100, shuffle x and y with the same RNG state. Text clients (LEAF
+    Shakespeare: 80-character strings → next character) go through the character vocabulary
+    (``shakespeare.process_x/process_y``, reference ``data/shakespeare/data_loader.py:53-63``)."""
+    from .shakespeare import is_char_data, process_x, process_y
+    if is_char_data(data["x"]):
+        x = process_x(data["x"])
+        y = process_y(data["y"])
+    else:
+        x = np.asarray(data["x"], dtype=np.float32)
+        y = np.asarray(data["y"], dtype=np.int64)
     np.random.seed(100)
     state = np.random.get_state()
     np.random.shuffle(x)

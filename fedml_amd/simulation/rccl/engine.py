@@ -45,7 +45,7 @@ def _default_loss(args) -> str:
     ds = str(getattr(args, "dataset", "") or "")
     if ds == "stackoverflow_lr":
         return "bce_sum"
-    if ds in ("fed_shakespeare", "stackoverflow_nwp", "shakespeare"):
+    if ds in ("fed_shakespeare", "stackoverflow_nwp"):   # LEAF "shakespeare" is next-char classification
         return "nwp_ce"
     return "ce"
 
