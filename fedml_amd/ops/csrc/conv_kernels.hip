@@ -82,18 +82,28 @@ __global__ __launch_bounds__(256) void pack_weights_kernel(const float* __restri
 constexpr int PK_T = 32;
 constexpr int PK_MAXTAPS = 9;
 
+// grid.x enumerates the (segment, tile) pairs of all layers back to back (no idle workgroups: one
+// launch per model, the ResNet-18 table has 21 segments from 1 to 256 tiles)
 template <class P>
 __global__ __launch_bounds__(256) void pack_weights_tiled_kernel(const float* __restrict__ arena, int64_t ldw,
-                                                                 const PackSeg* __restrict__ segs,
+                                                                 const PackSeg* __restrict__ segs, int nseg,
                                                                  typename P::T* __restrict__ dst, int64_t dst_ld) {
   using T = typename P::T;
   __shared__ float tile[PK_T][PK_T * PK_MAXTAPS + 1];
   const int c = blockIdx.y;
-  const PackSeg s = segs[blockIdx.z];
+  int si = 0, t0 = 0;
+  for (;;) {   // segment of this tile (uniform per workgroup)
+    const int nt = ((segs[si].cout + PK_T - 1) / PK_T) * ((segs[si].cin + PK_T - 1) / PK_T);
+    if ((int)blockIdx.x < t0 + nt || si == nseg - 1) break;
+    t0 += nt;
+    ++si;
+  }
+  const PackSeg s = segs[si];
   const int taps = s.kh * s.kw;
   const int nco = (s.cout + PK_T - 1) / PK_T, nci = (s.cin + PK_T - 1) / PK_T;
-  if ((int)blockIdx.x >= nco * nci) return;
-  const int co0 = (blockIdx.x / nci) * PK_T, ci0 = (blockIdx.x % nci) * PK_T;
+  const int tix = blockIdx.x - t0;
+  if (tix >= nco * nci) return;
+  const int co0 = (tix / nci) * PK_T, ci0 = (tix % nci) * PK_T;
   const int tco = min(PK_T, s.cout - co0), tci = min(PK_T, s.cin - ci0);
   const float* w = arena + (int64_t)c * ldw + s.src_off;
   // load: row co holds (ci, tap) pairs ci0.. contiguous in the source (ci < cin_src; padding → 0)
@@ -132,13 +142,13 @@ __global__ __launch_bounds__(256) void pack_weights_tiled_kernel(const float* __
   }
 }
 
-// max_tiles: the largest ceil(cout/32)·ceil(cin/32) over the segments (0 → the element-wise kernel)
+// total_tiles: Σ ceil(cout/32)·ceil(cin/32) over the segments (0 → the element-wise kernel)
 template <class P>
 static int pack_weights(const float* arena, int64_t ldw, const void* segs_dev, int nseg, typename P::T* dst,
-                        int64_t dst_ld, int C, int max_tiles, int max_taps, hipStream_t stream) {
-  if (max_tiles > 0 && max_taps <= PK_MAXTAPS && max_tiles <= 65535)
-    hipLaunchKernelGGL(pack_weights_tiled_kernel<P>, dim3(max_tiles, C, nseg), dim3(256), 0, stream, arena, ldw,
-                       (const PackSeg*)segs_dev, dst, dst_ld);
+                        int64_t dst_ld, int C, int total_tiles, int max_taps, hipStream_t stream) {
+  if (total_tiles > 0 && max_taps <= PK_MAXTAPS && total_tiles <= (1 << 30))
+    hipLaunchKernelGGL(pack_weights_tiled_kernel<P>, dim3(total_tiles, C), dim3(256), 0, stream, arena, ldw,
+                       (const PackSeg*)segs_dev, nseg, dst, dst_ld);
   else
     hipLaunchKernelGGL(pack_weights_kernel<P>, dim3(16, C, nseg), dim3(256), 0, stream, arena, ldw,
                        (const PackSeg*)segs_dev, nseg, dst, dst_ld);
@@ -172,7 +182,11 @@ enum { AOP_ACT = 0, AOP_DY = 1 };
 // MODE_BWD2: backward-data of a 1×1 / stride-2 / pad-0 convolution (the downsample shortcut): iterates
 // over the dy pixels (a quarter of the dx grid), writes dx(2i, 2j) = Wᵀ·dy(i, j) and zeros at the three
 // other pixels of each 2×2 cell — the generic MODE_BWD runs MFMAs over those zero pixels (4× the work).
-enum { MODE_FWD = 0, MODE_BWD = 1, MODE_BWD2 = 2 };
+// MODE_BWDS2 (K-streamed kernel only): backward-data of a 3×3 / stride-2 / pad-1 convolution split into the
+// four parity classes of dx pixels: dx(i, j) only receives taps kh ≡ (i + pad), kw ≡ (j + pad) (mod 2), so
+// each class runs a GEMM over its 1, 2, 2 or 4 taps (2.25 on average) instead of 9 taps of which 3/4
+// are zero — grid.z carries (N-tile, class).
+enum { MODE_FWD = 0, MODE_BWD = 1, MODE_BWD2 = 2, MODE_BWDS2 = 3 };
 
 struct ConvArgs {        // activations / packed weights are P::T (bf16 | fp32)
   const void* src;       // A source activations / g
@@ -499,21 +513,29 @@ __global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
   const int full = total / 8 * 8;
   if (lin < full) lin = (lin % 8) * (full / 8) + lin / 8;
   const int bx = lin % gx;
-  const int bz = (lin / gx) % gz;
+  const int bzz = (lin / gx) % gz;
   const int c = lin / (gx * gz);
+  constexpr bool S2 = MODE == MODE_BWDS2;
+  const int bz = S2 ? bzz >> 2 : bzz;
+  // stride-2 parity class: dx rows i ≡ r0, cols j ≡ c0 (mod 2); taps kh = qh + 2t (t < nth), kw = qw + 2u
+  const int qh = (bzz >> 1) & 1, qw = bzz & 1;
+  const int r0 = S2 ? (qh + a.pad) & 1 : 0, c0 = S2 ? (qw + a.pad) & 1 : 0;
+  const int nth = S2 ? (a.KH - qh + 1) / 2 : 1, ntw = S2 ? (a.KW - qw + 1) / 2 : 1;
+  const int Hc = S2 ? (a.Ho - r0 + 1) / 2 : 0, Wc = S2 ? (a.Wo - c0 + 1) / 2 : 0;
   const int NO = a.nout_total;
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int wm = wid / WN, wn = wid % WN;
   const int ch_base = bz * CK::BN;
   const int ch_w = ch_base + wn * 64;
-  const int K = a.KH * a.KW * a.KC;
+  const int K = S2 ? nth * ntw * a.KC : a.KH * a.KW * a.KC;
+  const int Kp = S2 ? (K + 31) / 32 * 32 : a.Kp;
   const int Mo = a.Nb * a.Ho * a.Wo;
-  const int HWi = MODE == MODE_BWD2 ? a.Hs * a.Ws : a.Ho * a.Wo;
-  const int M = MODE == MODE_BWD2 ? a.Nb * HWi : Mo;
+  const int HWi = MODE == MODE_BWD2 ? a.Hs * a.Ws : (S2 ? Hc * Wc : a.Ho * a.Wo);
+  const int M = (MODE == MODE_BWD2 || S2) ? a.Nb * HWi : Mo;
   const int Mv = a.nimg ? min(M, a.nimg[c] * HWi) : M;
   const int m0 = bx * CK::BM;
-  if (m0 >= Mv) return;   // uniform: whole workgroup idle
+  if (m0 >= Mv) return;   // uniform: whole workgroup idle (also: classes smaller than the grid)
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* al = reinterpret_cast<T*>(smem);                                               // [BM][LD]
@@ -542,7 +564,7 @@ __global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
   // this thread's staging slots: column chunk `col` of rows row0 + RPI·j
   const int col = threadIdx.x % CK::CPR;
   const int row0 = threadIdx.x / CK::CPR;
-  const int IW = MODE == MODE_BWD2 ? a.Ws : a.Wo;
+  const int IW = MODE == MODE_BWD2 ? a.Ws : (S2 ? Wc : a.Wo);
   int rn[CK::NA], rhw[CK::NA];   // image index, (h << 16 | w) of the row's iteration pixel; rn < 0: invalid
 #pragma unroll
   for (int j = 0; j < CK::NA; ++j) {
@@ -569,7 +591,8 @@ __global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
     const int k = kbase + col * V;
     const bool kval = k < K;
     const int tap = kval ? k / a.KC : 0, ci = kval ? k % a.KC : 0;
-    const int kh = tap / a.KW, kw = tap % a.KW;
+    const int kh = S2 ? qh + 2 * (tap / ntw) : tap / a.KW, kw = S2 ? qw + 2 * (tap % ntw) : tap % a.KW;
+    const int kcol = S2 ? (kh * a.KW + kw) * a.KC + ci : k;   // column of the packed weights
     aval = 0;
 #pragma unroll
     for (int j = 0; j < CK::NA; ++j) {
@@ -585,6 +608,10 @@ __global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
           ih = ph * a.stride - a.pad + kh;
           iw = pw * a.stride - a.pad + kw;
           ok = ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws;
+        } else if (S2) {   // dx (2ph + r0, 2pw + c0): the parity makes (i + pad − kh) even by construction
+          ih = (2 * ph + r0 + a.pad - kh) >> 1;
+          iw = (2 * pw + c0 + a.pad - kw) >> 1;
+          ok = 2 * ph + r0 + a.pad - kh >= 0 && 2 * pw + c0 + a.pad - kw >= 0 && ih < a.Hs && iw < a.Ws;
         } else {
           const int th = ph + a.pad - kh, tw = pw + a.pad - kw;
           ok = th >= 0 && tw >= 0 && (th % a.stride) == 0 && (tw % a.stride) == 0;
@@ -602,7 +629,7 @@ __global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
     }
 #pragma unroll
     for (int j = 0; j < CK::NB; ++j)
-      rb[j] = kval ? *reinterpret_cast<const uint4*>(wsrc + (int64_t)(row0 + CK::RPI * j) * a.ldk + k)
+      rb[j] = kval ? *reinterpret_cast<const uint4*>(wsrc + (int64_t)(row0 + CK::RPI * j) * a.ldk + kcol)
                    : make_uint4(0, 0, 0, 0);
   };
   auto put = [&](int kbase) {
@@ -639,12 +666,12 @@ __global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
   const T* my_b = wl + (wn * 64 + (lane & 15)) * LD + 8 * (lane >> 4);
   __syncthreads();   // prologue vectors visible to put()
   fetch(0);
-  for (int kbase = 0; kbase < a.Kp; kbase += KB) {
-    const int kn = min(KB, a.Kp - kbase);   // multiple of 32
+  for (int kbase = 0; kbase < Kp; kbase += KB) {
+    const int kn = min(KB, Kp - kbase);     // multiple of 32
     if (kbase) __syncthreads();             // previous chunk fully consumed
     put(kbase);
     __syncthreads();
-    if (kbase + KB < a.Kp) fetch(kbase + KB);
+    if (kbase + KB < Kp) fetch(kbase + KB);
     for (int k0 = 0; k0 < kn; k0 += 32) {
       frag_t af[TM];
 #pragma unroll
@@ -694,6 +721,11 @@ __global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
         const int ch0 = my_cg * V;
         const uint4 dv = *reinterpret_cast<const uint4*>(my_stage + row * NOUT + ch0);
         int64_t goff = ((int64_t)(tile * 16 + row)) * NO + ch_w + ch0;
+        if (S2) {   // class pixel (n, a, b) → dx (2a + r0, 2b + c0)
+          const int pm = tile * 16 + row;
+          const int n_ = pm / HWi, r_ = pm % HWi;
+          goff = (((int64_t)n_ * a.Ho + 2 * (r_ / Wc) + r0) * a.Wo + 2 * (r_ % Wc) + c0) * NO + ch_w + ch0;
+        }
         if (MODE == MODE_BWD2) {
           const int pm = tile * 16 + row;
           const int n_ = pm / HWi, r_ = pm % HWi;
@@ -791,7 +823,7 @@ static int convk_min_k() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("FEDML_AMD_CONVK_MIN_K");
-    v = e ? atoi(e) : 1024;
+    v = e ? atoi(e) : 256;   // measured: ResNet-18 preset +9 %, ResNet-56 headline neutral
   }
   return v;
 }
@@ -801,13 +833,15 @@ static int launch_convk_t(ConvArgs a, int nout, int C, hipStream_t stream) {
   using CK = ConvK<P, TM, WN>;
   a.nout_total = nout;
   if (nout % CK::BN != 0) return -2;
-  const int M = MODE == MODE_BWD2 ? a.Nb * a.Hs * a.Ws : a.Nb * a.Ho * a.Wo;
+  // MODE_BWDS2: the largest parity class sets grid.x; grid.z = N-tiles × 4 classes
+  const int M = MODE == MODE_BWD2 ? a.Nb * a.Hs * a.Ws
+                                  : (MODE == MODE_BWDS2 ? a.Nb * ((a.Ho + 1) / 2) * ((a.Wo + 1) / 2) : a.Nb * a.Ho * a.Wo);
   const int gx = (M + CK::BM - 1) / CK::BM;
   const size_t smem = CK::smem(a.KC);
   if (smem > 160 * 1024) return -5;
   auto kern = convk_gemm_kernel<P, TM, WN, AOP, PRO, MODE, EPI>;
   if (smem > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-  hipLaunchKernelGGL(kern, dim3(gx, C, nout / CK::BN), dim3(256), smem, stream, a);
+  hipLaunchKernelGGL(kern, dim3(gx, C, nout / CK::BN * (MODE == MODE_BWDS2 ? 4 : 1)), dim3(256), smem, stream, a);
   return (int)hipGetLastError();
 }
 
@@ -821,7 +855,7 @@ static int launch_convk(ConvArgs a, int nout, int C, hipStream_t s) {
     force = e ? atoi(e) : -1;
   }
   if (nout % 64 != 0) return -2;
-  const int M = MODE == MODE_BWD2 ? a.Nb * a.Hs * a.Ws : a.Nb * a.Ho * a.Wo;
+  const int M = MODE == MODE_BWD2 ? a.Nb * a.Hs * a.Ws : a.Nb * a.Ho * a.Wo;   // (BWDS2: all 4 classes)
   const int64_t wgs1 = (int64_t)((M + 63) / 64) * C * (nout / 64);   // workgroups of a 64 × 64 tile
   int pick = force;
   if (pick < 0) pick = nout % 128 == 0 ? 0 : (wgs1 >= 4096 ? 1 : (wgs1 >= 1024 ? 2 : 3));
@@ -900,6 +934,15 @@ static int conv_bwd_data(const void* g, const void* yv, const float* alpha, cons
   a.stats = stats; a.NS = 3;  // backward statistics are always laid out [C][Ch][3]
   a.Nb = Nb; a.Hs = Hy; a.Ws = Wy; a.KC = Cout; a.Ho = Hx; a.Wo = Wx; a.KH = KH; a.KW = KW; a.stride = stride;
   a.pad = pad; a.ldk = ldk2; a.Kp = (KH * KW * Cout + 31) / 32 * 32; a.tiles_per_wave = tiles_per_wave;
+  // 3×3 / stride-2 / pad-1 (ResNet-18 stage entries): parity-class GEMMs over the valid taps only
+  if (KH == 3 && KW == 3 && stride == 2 && pad == 1 && Cin % 64 == 0 && Cout % 64 == 0) {
+    switch (epi) {
+      case EPI_STORE: return launch_convk<P, AOP_DY, PRO_NONE, MODE_BWDS2, EPI_STORE>(a, Cin, C, stream);
+      case EPI_MASK: return launch_convk<P, AOP_DY, PRO_NONE, MODE_BWDS2, EPI_MASK>(a, Cin, C, stream);
+      case EPI_BLOCK: return launch_convk<P, AOP_DY, PRO_NONE, MODE_BWDS2, EPI_BLOCK>(a, Cin, C, stream);
+      default: return -4;
+    }
+  }
   switch (epi) {
     case EPI_STORE:
       if (KH == 1 && KW == 1 && stride == 2 && pad == 0 && Hx == 2 * Hy && Wx == 2 * Wy)

@@ -210,6 +210,41 @@ __global__ __launch_bounds__(256) void conv_wgrad_tr_kernel(
 __global__ void wgrad_scatter_kernel(float* __restrict__ dw, float* __restrict__ garena, int64_t ldw, int64_t woff,
                                      int Cout, int Cin, int taps, int cin_src);
 
+// GEMM-layout dW row [tap·Cin + ci] of one (client, co) → OIHW row [ci][tap] (+=), through LDS so both
+// the read and the write are contiguous (the element-wise scatter writes with a stride of `taps`), and
+// the scratch row is cleared for the next layer. One workgroup per (co, client).
+__global__ __launch_bounds__(256) void wgrad_scatter_rows_kernel(float* __restrict__ dw, float* __restrict__ garena,
+                                                                 int64_t ldw, int64_t woff, int Cout, int Cin,
+                                                                 int taps, int cin_src) {
+  extern __shared__ float row[];
+  const int co = blockIdx.x, c = blockIdx.y;
+  const int K = taps * Cin;
+  float* d = dw + ((int64_t)c * Cout + co) * K;
+  for (int i = threadIdx.x; i < K; i += 256) {
+    row[i] = d[i];
+    d[i] = 0.f;
+  }
+  __syncthreads();
+  float* gw = garena + (int64_t)c * ldw + woff + (int64_t)co * cin_src * taps;
+  for (int i = threadIdx.x; i < cin_src * taps; i += 256) {
+    const int ci = i / taps, tap = i - ci * taps;
+    gw[i] += row[tap * Cin + ci];
+  }
+}
+
+static int wgrad_scatter_rows(float* dw, float* garena, int64_t ldw, int64_t woff, int C, int Cout, int Cin, int taps,
+                              int cin_src, hipStream_t stream) {
+  const size_t smem = (size_t)taps * Cin * 4;
+  if (smem > 64 * 1024 || Cout > 65535 || C > 65535) {
+    hipLaunchKernelGGL(wgrad_scatter_kernel, dim3(fa_grid((int64_t)Cout * taps * Cin, 256, 64), C), dim3(256), 0,
+                       stream, dw, garena, ldw, woff, Cout, Cin, taps, cin_src);
+  } else {
+    hipLaunchKernelGGL(wgrad_scatter_rows_kernel, dim3(Cout, C), dim3(256), smem, stream, dw, garena, ldw, woff, Cout,
+                       Cin, taps, cin_src);
+  }
+  return (int)hipGetLastError();
+}
+
 // ---- wide layers (Cout ≥ 128: ResNet-18 stages 2-4) ----
 // One workgroup owns a 128 (co) × 128 (k) dW tile of one client and reduces it over a pixel chunk;
 // its 4 waves form a 2 × 2 grid of 64 × 64 sub-tiles (4 × 4 MFMA tiles each), so per 32-pixel K step
@@ -250,53 +285,64 @@ __global__ __launch_bounds__(256) void wgrad_wide_kernel(
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* dyL = reinterpret_cast<T*>(smem);                 // [PT][LD]
   T* aL = dyL + PT * LD;                               // [PT][LD]
-  float* vv = reinterpret_cast<float*>(aL + PT * LD);  // α β γ [TS], s t [Cin]
-  for (int i = threadIdx.x; i < TS; i += 256) {
-    vv[i] = alpha[(int64_t)c * Cout + co_lo + i];
-    vv[TS + i] = beta[(int64_t)c * Cout + co_lo + i];
-    vv[2 * TS + i] = gamma[(int64_t)c * Cout + co_lo + i];
-  }
-  if (PRO)
-    for (int i = threadIdx.x; i < Cin; i += 256) {
-      vv[3 * TS + i] = ps[(int64_t)c * Cin + i];
-      vv[3 * TS + Cin + i] = pt[(int64_t)c * Cin + i];
-    }
 
-  const T* gc = g + (int64_t)c * M * Cout;
-  const T* yc = yv + (int64_t)c * M * Cout;
-  const T* xc = x + (int64_t)c * Nb * H * W * Cin;
+  // Each thread always stages the same 16-B column chunk (channels col..col+V-1 of dy and k-columns
+  // k_lo+col.. of im2col) for rows pp0 + RPI·it: its folded-BN coefficients, tap and prologue
+  // scale/shift are loop invariants kept in registers; per row only the pixel is decoded (float-
+  // reciprocal divmod — the runtime integer divisions made this loop VALU-bound).
   constexpr int CPR = TS / V;   // chunks per staged row
+  constexpr int RPI = 256 / CPR;
+  const int col = (threadIdx.x % CPR) * V;
+  const int pp0 = threadIdx.x / CPR;
+  float ca[V], cb[V], cc[V], cs[V], ct[V];
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    ca[j] = alpha[(int64_t)c * Cout + co_lo + col + j];
+    cb[j] = beta[(int64_t)c * Cout + co_lo + col + j];
+    cc[j] = gamma[(int64_t)c * Cout + co_lo + col + j];
+  }
+  const bool kval = col < kn;
+  const int k0 = k_lo + (kval ? col : 0);
+  const int tap = k0 / Cin, ci0 = k0 % Cin;
+  const int kh = tap / KW, kw = tap % KW;
+#pragma unroll
+  for (int j = 0; j < V; ++j) {
+    cs[j] = PRO ? ps[(int64_t)c * Cin + ci0 + j] : 1.f;
+    ct[j] = PRO ? pt[(int64_t)c * Cin + ci0 + j] : 0.f;
+  }
+  const int HWo = Ho * Wo;
+  const float inv_hw = 1.f / (float)HWo, inv_w = 1.f / (float)Wo;
+  auto fdiv = [](int a, int b, float inv_b) {   // exact for 0 ≤ a < 2^22
+    int q = (int)((float)a * inv_b);
+    const int r = a - q * b;
+    return q + (r >= b) - (r < 0);
+  };
+
+  const T* gc = g + (int64_t)c * M * Cout + co_lo + col;
+  const T* yc = yv + (int64_t)c * M * Cout + co_lo + col;
+  const T* xc = x + (int64_t)c * Nb * H * W * Cin + ci0;
   uint4 rg[NI], ry[NI], rx[NI];
-  uint32_t dvalid = 0;
+  uint32_t dvalid = 0, avalid = 0;
   auto load_sub = [&](int p0) {
     dvalid = 0;
+    avalid = 0;
 #pragma unroll
     for (int it = 0; it < NI; ++it) {
-      const int i = threadIdx.x + it * 256;
-      const int pp = i / CPR, col = (i % CPR) * V;
-      const int p = p0 + pp;
+      const int p = p0 + pp0 + RPI * it;
       rg[it] = make_uint4(0, 0, 0, 0);
       ry[it] = make_uint4(0, 0, 0, 0);
       rx[it] = make_uint4(0, 0, 0, 0);
       if (p < p_end) {
         dvalid |= 1u << it;
-        rg[it] = *reinterpret_cast<const uint4*>(gc + (int64_t)p * Cout + co_lo + col);
-        ry[it] = *reinterpret_cast<const uint4*>(yc + (int64_t)p * Cout + co_lo + col);
-        if (col < kn) {
-          const int k0 = k_lo + col;
-          const int tap = k0 / Cin, ci0 = k0 % Cin;
-          const int n = p / (Ho * Wo), r = p % (Ho * Wo);
-          const int ih = (r / Wo) * stride - pad + tap / KW, iw = (r % Wo) * stride - pad + tap % KW;
+        rg[it] = *reinterpret_cast<const uint4*>(gc + (int64_t)p * Cout);
+        ry[it] = *reinterpret_cast<const uint4*>(yc + (int64_t)p * Cout);
+        if (kval) {
+          const int n = fdiv(p, HWo, inv_hw), r = p - n * HWo;
+          const int oh = fdiv(r, Wo, inv_w), ow = r - oh * Wo;
+          const int ih = oh * stride - pad + kh, iw = ow * stride - pad + kw;
           if (ih >= 0 && ih < H && iw >= 0 && iw < W) {
-            uint4 v = *reinterpret_cast<const uint4*>(xc + (((int64_t)n * H + ih) * W + iw) * Cin + ci0);
-            if (PRO) {
-              float f[V];
-              P::unpack(v, f);
-#pragma unroll
-              for (int j = 0; j < V; ++j) f[j] = fmaxf(f[j] * vv[3 * TS + ci0 + j] + vv[3 * TS + Cin + ci0 + j], 0.f);
-              v = P::pack(f);
-            }
-            rx[it] = v;   // out-of-image taps stay 0 (zero padding, not relu(shift))
+            rx[it] = *reinterpret_cast<const uint4*>(xc + (((int64_t)n * H + ih) * W + iw) * Cin);
+            avalid |= 1u << it;
           }
         }
       }
@@ -305,17 +351,23 @@ __global__ __launch_bounds__(256) void wgrad_wide_kernel(
   auto store_sub = [&]() {
 #pragma unroll
     for (int it = 0; it < NI; ++it) {
-      const int i = threadIdx.x + it * 256;
-      const int pp = i / CPR, col = (i % CPR) * V;
+      const int pp = pp0 + RPI * it;
       float gf[V], yf[V], d[V];
       P::unpack(rg[it], gf);
       P::unpack(ry[it], yf);
       const bool live = (dvalid >> it) & 1u;   // pixels past the chunk: dy = 0 (not γ)
 #pragma unroll
-      for (int j = 0; j < V; ++j)
-        d[j] = live ? vv[col + j] * gf[j] + vv[TS + col + j] * yf[j] + vv[2 * TS + col + j] : 0.f;
+      for (int j = 0; j < V; ++j) d[j] = live ? ca[j] * gf[j] + cb[j] * yf[j] + cc[j] : 0.f;
       P::st_chunk(dyL + pp * LD + col, P::pack(d));
-      P::st_chunk(aL + pp * LD + col, rx[it]);
+      uint4 v = rx[it];   // out-of-image taps / past-K columns stay 0 (zero padding, not relu(shift))
+      if (PRO && ((avalid >> it) & 1u)) {
+        float f[V];
+        P::unpack(v, f);
+#pragma unroll
+        for (int j = 0; j < V; ++j) f[j] = fmaxf(f[j] * cs[j] + ct[j], 0.f);
+        v = P::pack(f);
+      }
+      P::st_chunk(aL + pp * LD + col, v);
     }
   };
 
@@ -359,7 +411,7 @@ __global__ __launch_bounds__(256) void wgrad_wide_kernel(
         const int co = co_lo + (wm * 4 + i) * 16 + 4 * (lane >> 4) + r;
         if (direct) {
           if (ci < cin_src) garena[(int64_t)c * ldw + woff + ((int64_t)co * cin_src + ci) * taps + tap] += acc[i][j][r];
-        } else {
+        } else {   // several pixel chunks per tile: row-contiguous atomics into the GEMM-layout scratch
           atomicAdd(&dw[((int64_t)c * Cout + co) * K + k], acc[i][j][r]);
         }
       }
@@ -383,15 +435,13 @@ static int wgrad_wide(const typename P::T* g, const typename P::T* yv, const flo
   int ppw = ((M + gx - 1) / gx + PT - 1) / PT * PT;
   gx = (M + ppw - 1) / ppw;
   const int direct = gx == 1;
-  const size_t smem = (size_t)2 * PT * P::pitch_tr(128) * P::ES + (size_t)(3 * 128 + 2 * Cin) * 4;
+  const size_t smem = (size_t)2 * PT * P::pitch_tr(128) * P::ES;
   auto kern = wgrad_wide_kernel<P>;
   if (smem > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   hipLaunchKernelGGL(kern, dim3(gx, C, nks * (Cout / 128)), dim3(256), smem, stream, g, yv, alpha, beta, gamma, x,
                      ps, pt, dw, garena, ldw, woff, cin_src, Nb, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ppw,
                      nimg, direct);
-  if (!direct)
-    hipLaunchKernelGGL(wgrad_scatter_kernel, dim3(fa_grid((int64_t)Cout * K, 256, 64), C), dim3(256), 0, stream, dw,
-                       garena, ldw, woff, Cout, Cin, KH * KW, cin_src);
+  if (!direct) return wgrad_scatter_rows(dw, garena, ldw, woff, C, Cout, Cin, KH * KW, cin_src, stream);
   return (int)hipGetLastError();
 }
 
@@ -474,9 +524,7 @@ static int conv_wgrad(const typename P::T* g, const typename P::T* yv, const flo
   if (tpw <= 4) by_d(std::integral_constant<int, 4>{});
   else if (tpw <= 8) by_d(std::integral_constant<int, 8>{});
   else by_d(std::integral_constant<int, 16>{});
-  hipLaunchKernelGGL(wgrad_scatter_kernel, dim3(fa_grid((int64_t)Cout * K, 256, 64), C), dim3(256), 0, stream, dw,
-                     garena, ldw, woff, Cout, Cin, KH * KW, cin_src);
-  return (int)hipGetLastError();
+  return wgrad_scatter_rows(dw, garena, ldw, woff, C, Cout, Cin, KH * KW, cin_src, stream);
 }
 
 FA_EXPORT int fa_conv_wgrad(const uint16_t* g, const uint16_t* yv, const float* alpha, const float* beta,

@@ -37,8 +37,8 @@ class PackSeg(ctypes.Structure):
 
 
 def pack_weights(arena, segs_dev, nseg, dst, dst_ld, C, max_tiles=0, max_taps=0):
-    """OIHW fp32 arena rows → packed forward/backward GEMM layouts. ``max_tiles`` = the largest
-    ceil(cout/32)·ceil(cin/32) over the segments selects the LDS-tiled kernel (0: element-wise)."""
+    """OIHW fp32 arena rows → packed forward/backward GEMM layouts. ``max_tiles`` = Σ over the segments
+    of ceil(cout/32)·ceil(cin/32) selects the LDS-tiled kernel (0: element-wise)."""
     rc = _fnp("fa_pack_weights", dst)(_p(arena), _i64(arena.stride(0)), _p(segs_dev), _i(nseg), _p(dst), _i64(dst_ld),
                                 _i(C), _i(max_tiles), _i(max_taps), _stream(arena))
     _check(rc, "fa_pack_weights")

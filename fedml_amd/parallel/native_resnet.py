@@ -210,7 +210,7 @@ class NativeResNetStep:
         raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
         self._segs = raw.to(dev)
         self._nseg = len(segs)
-        self._pack_tiles = max(-(-cv.cout // 32) * -(-cv.cin_pad // 32) for cv in self._all_convs())
+        self._pack_tiles = sum(-(-cv.cout // 32) * -(-cv.cin_pad // 32) for cv in self._all_convs())
         self._pack_taps = max(cv.k * cv.k for cv in self._all_convs())
         # activations (storage precision) and per-BN vectors
         bf = self.dtype
