@@ -115,11 +115,15 @@ __global__ __launch_bounds__(256) void pack_weights_tiled_kernel(const float* __
   }
   __syncthreads();
   T* df = dst + (int64_t)c * dst_ld + s.dst_f;
-  // Wf[co][tap·cin + ci]: ci fastest
-  for (int i = threadIdx.x; i < tco * taps * tci; i += 256) {
-    const int ci = i % tci, rt = i / tci;
+  // Wf[co][tap·cin + ci]: ci fastest, 4 consecutive elements per store (8 B bf16 / 16 B fp32 — single
+  // 2-byte stores made this kernel store-issue-bound); cin, cout are multiples of 8 and 16
+  const int tci4 = tci / 4, tco4 = tco / 4;
+  for (int i = threadIdx.x; i < tco * taps * tci4; i += 256) {
+    const int ci = (i % tci4) * 4, rt = i / tci4;
     const int tap = rt % taps, r = rt / taps;
-    df[(int64_t)(co0 + r) * s.ldk + tap * s.cin + ci0 + ci] = P::from_f(tile[r][ci * taps + tap]);
+    float f[4] = {tile[r][ci * taps + tap], tile[r][(ci + 1) * taps + tap], tile[r][(ci + 2) * taps + tap],
+                  tile[r][(ci + 3) * taps + tap]};
+    P::store4(df + (int64_t)(co0 + r) * s.ldk + tap * s.cin + ci0 + ci, f);
   }
   if (ci0 == 0) {   // zero the K padding of these rows
     const int kp = s.ldk - taps * s.cin;
@@ -128,11 +132,13 @@ __global__ __launch_bounds__(256) void pack_weights_tiled_kernel(const float* __
   }
   if (s.dst_b >= 0) {
     T* db = dst + (int64_t)c * dst_ld + s.dst_b;
-    // Wb[ci][tap·cout + co]: co fastest
-    for (int i = threadIdx.x; i < tci * taps * tco; i += 256) {
-      const int r = i % tco, ct = i / tco;
+    // Wb[ci][tap·cout + co]: co fastest, 4 per store
+    for (int i = threadIdx.x; i < tci * taps * tco4; i += 256) {
+      const int r = (i % tco4) * 4, ct = i / tco4;
       const int tap = ct % taps, ci = ct / taps;
-      db[(int64_t)(ci0 + ci) * s.ldk2 + tap * s.cout + co0 + r] = P::from_f(tile[r][ci * taps + tap]);
+      const int q = ci * taps + tap;
+      float f[4] = {tile[r][q], tile[r + 1][q], tile[r + 2][q], tile[r + 3][q]};
+      P::store4(db + (int64_t)(ci0 + ci) * s.ldk2 + tap * s.cout + co0 + r, f);
     }
     if (co0 == 0) {
       const int kp = s.ldk2 - taps * s.cout;
