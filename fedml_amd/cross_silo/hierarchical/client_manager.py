@@ -33,6 +33,7 @@ class ClientMasterManager(FedMLClientManager):
                 self.trainer.sync_model()
 
     def handle_message_init(self, msg):
+        self.note_global(msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS))
         self.trainer.update_model(msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS))
         silo = int(msg.get(MyMessage.MSG_ARG_KEY_CLIENT_INDEX))
         self.round_idx = int(msg.get(MyMessage.MSG_ARG_KEY_ROUND_INDEX, 0))
@@ -41,6 +42,7 @@ class ClientMasterManager(FedMLClientManager):
         self._train_and_send()
 
     def handle_message_receive_model_from_server(self, msg):
+        self.note_global(msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS))
         self.trainer.update_model(msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS))
         silo = int(msg.get(MyMessage.MSG_ARG_KEY_CLIENT_INDEX))
         self.round_idx = int(msg.get(MyMessage.MSG_ARG_KEY_ROUND_INDEX, self.round_idx + 1))

@@ -4,6 +4,7 @@ the group is independent of any other torch.distributed world; backend RCCL (``n
 gloo on CPU."""
 import datetime
 import logging
+import os
 
 import torch
 import torch.distributed as dist
@@ -14,7 +15,8 @@ class ProcessGroupManager:
                  timeout_s=1800):
         self.rank, self.world_size = int(rank), int(world_size)
         use_gpu = torch.cuda.is_available() if only_gpu is None else bool(only_gpu)
-        backend = "nccl" if use_gpu else "gloo"
+        # FEDML_AMD_DIST_BACKEND=gloo: rehearsal with several silo processes sharing one GPU
+        backend = os.environ.get("FEDML_AMD_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
         if not dist.is_initialized():
             dist.init_process_group(backend=backend, init_method=f"tcp://{master_address}:{int(master_port)}",
                                     rank=self.rank, world_size=self.world_size,

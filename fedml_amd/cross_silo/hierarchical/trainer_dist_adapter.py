@@ -27,8 +27,13 @@ class TrainerDistAdapter:
                                           int(getattr(args, "pg_master_port", 29700)),
                                           only_gpu=self.device.type == "cuda")
         model = model.to(self.device)
+        # silo_local_clients > 1: the silo trains that many local clients per round on the client-batched
+        # engine, client-parallel over the silo's processes (silo_batched.py) instead of one DDP replica
+        self.n_local = int(getattr(args, "silo_local_clients", 1) or 1)
+        self.silo_trainers = {}
+        self._pending = None
         self.ddp = FlatDDP(model, self.device, bucket_mb=float(getattr(args, "ddp_bucket_mb", 64.0))) \
-            if self.n_proc > 1 else None
+            if self.n_proc > 1 and self.n_local <= 1 else None
         self.model = model
         self.trainer = model_trainer or create_model_trainer(model, args)
         self.trainer.model = self.ddp if self.ddp is not None else model
@@ -48,6 +53,13 @@ class TrainerDistAdapter:
 
     def update_dataset(self, client_index):
         self.client_index = int(client_index)
+        if self.n_local > 1:
+            if self.client_index not in self.silo_trainers:   # collective: every silo process builds it
+                from .silo_batched import SiloBatchedTrainer
+                self.silo_trainers[self.client_index] = SiloBatchedTrainer(
+                    self.args, self.device, self.model, self.train_data_local_dict[self.client_index], self.n_local)
+            self.local_sample_number = self.train_data_local_num_dict[self.client_index]
+            return
         self.train_local = self._shard(self.train_data_local_dict[self.client_index])
         self.local_sample_number = self.train_data_local_num_dict[self.client_index]
         self.trainer.set_id(self.client_index)
@@ -55,12 +67,14 @@ class TrainerDistAdapter:
     def update_model(self, params):
         if params is not None:
             self.model.load_state_dict(params)
+            self._pending = params
 
     def get_model_params(self):
         return {k: v.detach().cpu().clone() for k, v in self.model.state_dict().items()}
 
     def sync_model(self):
-        """Collective: every silo rank leaves with rank 0's parameters and buffers."""
+        """Collective: every silo rank leaves with rank 0's parameters and buffers (batched silos
+        broadcast inside ``train``, once their engine exists)."""
         if self.ddp is None:
             return
         dist.broadcast(self.ddp.flat, 0)
@@ -69,6 +83,14 @@ class TrainerDistAdapter:
 
     def train(self, round_idx=None):
         self.args.round_idx = round_idx
+        if self.n_local > 1:
+            st = self.silo_trainers[self.client_index]
+            if self.rank_in_silo == 0 and self._pending is not None:
+                st.load_global(self._pending)
+            st.sync()
+            state = st.train(int(round_idx or 0))
+            self.model.load_state_dict(state)
+            return state, self.local_sample_number
         if self.ddp is not None:
             dist.barrier()
         self.trainer.train(self.train_local, self.device, self.args)

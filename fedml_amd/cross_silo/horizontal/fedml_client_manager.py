@@ -30,6 +30,17 @@ class FedMLClientManager(ClientManager):
         self._stop_stats = threading.Event()
         self.final_model = None
         self.faults = FaultInjector(args)
+        # compressed uploads on the WAN path (cross_silo/wan_codec.py): int8 Δ + error feedback
+        wc = str(getattr(args, "wan_compression", "") or "").lower()
+        self.wan = None
+        if wc:
+            from ..wan_codec import WanEncoder
+            self.wan = WanEncoder(wc)
+
+    def note_global(self, params):
+        """The round's global model (the reference point of a compressed upload)."""
+        if self.wan is not None and params is not None:
+            self.wan.note_global(params)
 
     def run(self):
         inject_connection_ready(self)
@@ -57,12 +68,14 @@ class FedMLClientManager(ClientManager):
     def handle_message_init(self, msg):
         MLOpsMetrics.get_instance().report_client_training_status(self.client_real_id,
                                                                   MyMessage.MSG_MLOPS_CLIENT_STATUS_TRAINING)
+        self.note_global(msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS))
         self.trainer.update_model(msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS))
         self.trainer.update_dataset(int(msg.get(MyMessage.MSG_ARG_KEY_CLIENT_INDEX)))
         self.round_idx = int(msg.get(MyMessage.MSG_ARG_KEY_ROUND_INDEX, 0))
         self.__train()
 
     def handle_message_receive_model_from_server(self, msg):
+        self.note_global(msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS))
         self.trainer.update_model(msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS))
         self.trainer.update_dataset(int(msg.get(MyMessage.MSG_ARG_KEY_CLIENT_INDEX)))
         self.round_idx = int(msg.get(MyMessage.MSG_ARG_KEY_ROUND_INDEX, self.round_idx + 1))
@@ -81,6 +94,8 @@ class FedMLClientManager(ClientManager):
     def send_model_to_server(self, receive_id, weights, local_sample_num):
         MLOpsProfilerEvent.get_instance().log_event_started("comm_c2s", event_value=str(self.round_idx))
         m = Message(MyMessage.MSG_TYPE_C2S_SEND_MODEL_TO_SERVER, self.client_real_id, receive_id)
+        if self.wan is not None and self.wan.ref is not None:
+            weights = self.wan.encode(weights, seed=self.round_idx * 4099 + int(self.client_real_id))
         m.add_params(MyMessage.MSG_ARG_KEY_MODEL_PARAMS, weights)
         m.add_params(MyMessage.MSG_ARG_KEY_NUM_SAMPLES, local_sample_num)
         m.add_params(MyMessage.MSG_ARG_KEY_ROUND_INDEX, self.round_idx)

@@ -152,8 +152,12 @@ class FedMLServerManager(ServerManager):
             return
         prof = MLOpsProfilerEvent.get_instance()
         prof.log_event_ended("comm_c2s", event_value=str(self.round_idx), event_edge_id=sender)
-        self.aggregator.add_local_trained_result(self._selected.index(sender),
-                                                 msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS),
+        params = msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS)
+        from ..wan_codec import decode, is_encoded, payload_bytes
+        self.wan_bytes = getattr(self, "wan_bytes", 0) + payload_bytes(params)
+        if is_encoded(params):   # compressed silo update: w_global + deq(Δ) (cross_silo/wan_codec.py)
+            params = decode(params, self.aggregator.get_global_model_params())
+        self.aggregator.add_local_trained_result(self._selected.index(sender), params,
                                                  msg.get(MyMessage.MSG_ARG_KEY_NUM_SAMPLES))
         if not self.aggregator.check_whether_all_receive():
             return

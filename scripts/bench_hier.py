@@ -1,0 +1,135 @@
+#!/usr/bin/env python3
+"""BASELINE config 5: cross-silo hierarchical FedAvg, ViT-B/16, 8 silos × 4 local clients, data
+parallelism inside each silo — as real processes: one server + S silos × P processes, TCP between the
+server and the silo masters, an RCCL (or gloo) process group inside each silo, and each silo training
+its local clients on the client-batched transformer engine (cross_silo/hierarchical/silo_batched.py).
+
+    python scripts/bench_hier.py --silos 8 --local-clients 4 --procs-per-silo 1 --rounds 3 --warmup 1
+
+Silo processes are spread over the visible GPUs (process i → GPU i mod ngpus); with fewer GPUs than
+processes inside one silo the silo group must use gloo (FEDML_AMD_DIST_BACKEND=gloo is set then).
+Metric: FL rounds/s measured by the server (round-completion timestamps after the warmup rounds).
+Data: synthetic ILSVRC2012-shaped images, random-init weights."""
+import argparse
+import json
+import os
+import socket
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def worker(a):
+    import torch
+    sys.path.insert(0, ROOT)
+    import fedml_amd
+    from fedml_amd.arguments import Arguments
+    cfg = {"training_type": "cross_silo", "scenario": "hierarchical", "dataset": a.dataset, "model": a.model,
+           "client_num_in_total": a.silos, "client_num_per_round": a.silos, "comm_round": a.rounds + a.warmup,
+           "epochs": 1, "batch_size": a.batch_size, "learning_rate": a.lr, "client_optimizer": "adamw",
+           "weight_decay": 0.01, "frequency_of_the_test": 0, "backend": "TCP", "federated_optimizer": "FedAvg",
+           "worker_num": a.silos + 1, "client_id_list": str(list(range(1, a.silos + 1))), "sys_perf_interval": 0,
+           "synthetic_samples_per_client": a.samples_per_client * a.local_clients, "rank": a.silo,
+           "n_proc_in_silo": a.procs_per_silo, "proc_rank_in_silo": a.rank_in_silo, "pg_master_port": a.pg_port,
+           "silo_local_clients": a.local_clients, "compute_dtype": a.dtype,
+           "using_gpu": torch.cuda.is_available(), "gpu_id": 0,
+           "wan_compression": a.wan_compression, "random_seed": 0}
+    args = fedml_amd.init(Arguments.from_dict({"x": cfg}))
+    dev, ds, m = fedml_amd._prepare(args)
+    from fedml_amd.cross_silo.hierarchical import Client, Server
+    if a.role == "server":
+        srv = Server(args, dev, ds, m)
+        srv.run()
+        json.dump({"round_times": srv.manager.round_times,
+                   "wan_bytes": getattr(srv.manager, "wan_bytes", None)}, open(a.out, "w"))
+    else:
+        Client(args, dev, ds, m).run()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--silos", type=int, default=8)
+    p.add_argument("--local-clients", type=int, default=4)
+    p.add_argument("--procs-per-silo", type=int, default=1)
+    p.add_argument("--rounds", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--model", default="vit_b16")
+    p.add_argument("--dataset", default="ILSVRC2012")
+    p.add_argument("--samples-per-client", type=int, default=32)
+    p.add_argument("--batch-size", type=int, default=16)
+    p.add_argument("--lr", type=float, default=1e-4)
+    p.add_argument("--dtype", default="bf16")
+    p.add_argument("--wan-compression", default="", help="'' (fp32 state dicts, the reference) | int8")
+    p.add_argument("--timeout", type=float, default=900)
+    # worker-internal
+    p.add_argument("--role", default="")
+    p.add_argument("--silo", type=int, default=0)
+    p.add_argument("--rank-in-silo", type=int, default=0)
+    p.add_argument("--pg-port", type=int, default=0)
+    p.add_argument("--out", default="")
+    a = p.parse_args()
+    if a.role:
+        return worker(a)
+    import torch
+    ngpu = max(1, torch.cuda.device_count())
+    out = os.path.join(ROOT, "gpurun_out", "bench_hier_server.json")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    env = dict(os.environ, PYTHONPATH=ROOT, FEDML_TCP_BASE_PORT=str(_free_port()), HSA_ENABLE_IPC_MODE_LEGACY="0",
+               OMP_NUM_THREADS="2")
+    if a.procs_per_silo > ngpu:
+        env["FEDML_AMD_DIST_BACKEND"] = "gloo"
+    base = [sys.executable, os.path.abspath(__file__)] + [x for x in sys.argv[1:]]
+    procs = []
+    e = dict(env, HIP_VISIBLE_DEVICES="0")
+    procs.append(subprocess.Popen(base + ["--role", "server", "--out", out], env=e))
+    i = 0
+    for s in range(1, a.silos + 1):
+        port = _free_port()
+        for r in range(a.procs_per_silo):
+            e = dict(env, HIP_VISIBLE_DEVICES=str(i % ngpu))
+            procs.append(subprocess.Popen(base + ["--role", "silo", "--silo", str(s), "--rank-in-silo", str(r),
+                                                  "--pg-port", str(port)], env=e))
+            i += 1
+    t0 = time.time()
+    codes = []
+    for pr in procs:
+        try:
+            codes.append(pr.wait(timeout=max(1.0, a.timeout - (time.time() - t0))))
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise SystemExit("bench_hier: timed out")
+    if any(codes):
+        raise SystemExit(f"bench_hier: worker exit codes {codes}")
+    res = json.load(open(out))
+    rt = res["round_times"][a.warmup:]
+    t = sum(rt)
+    line = {"metric": f"FL rounds/sec (hierarchical cross-silo FedAvg, {a.silos} silos x {a.local_clients} local clients,"
+                      f" {a.model})",
+            "value": round(len(rt) / t, 4), "unit": "rounds/s", "n_gpus": ngpu, "steps": len(rt), "warmup": a.warmup,
+            "ms_per_step": round(1000 * t / len(rt), 1), "higher_is_better": True, "scaling": "strong",
+            "vs_baseline": None, "dtype": a.dtype if torch.cuda.is_available() else "fp32",
+            "data": f"synthetic ({a.dataset}-shaped), random-init weights",
+            "config": {"model": a.model, "silos": a.silos, "local_clients_per_silo": a.local_clients,
+                       "procs_per_silo": a.procs_per_silo, "samples_per_client": a.samples_per_client,
+                       "local_batch": a.batch_size, "wan_payload": a.wan_compression or "fp32 state_dict",
+                       "parallelism": f"server + {a.silos} silos x {a.procs_per_silo} procs (TCP WAN, "
+                                      f"{env.get('FEDML_AMD_DIST_BACKEND', 'RCCL')} in-silo)"},
+            "round_times_s": [round(x, 3) for x in res["round_times"]], "wan_bytes": res.get("wan_bytes")}
+    print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()
