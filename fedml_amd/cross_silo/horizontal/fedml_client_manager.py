@@ -11,6 +11,8 @@ import platform
 import threading
 import time
 
+import torch
+
 from ...core.distributed import ClientManager, Message
 from ...core.fault import FaultInjector
 from ...core.mlops import MLOpsMetrics, MLOpsProfilerEvent
@@ -35,7 +37,8 @@ class FedMLClientManager(ClientManager):
         self.wan = None
         if wc:
             from ..wan_codec import WanEncoder
-            self.wan = WanEncoder(wc)
+            dev = getattr(trainer, "device", None)   # the silo's GPU: quantisation runs as the HIP kernel
+            self.wan = WanEncoder(wc, device=dev if dev is not None and torch.device(dev).type == "cuda" else None)
 
     def note_global(self, params):
         """The round's global model (the reference point of a compressed upload)."""

@@ -17,6 +17,8 @@ import logging
 import threading
 import time
 
+import torch
+
 from ...core.distributed import Message, ServerManager
 from ...core.mlops import MLOpsMetrics, MLOpsProfilerEvent
 from ..message_define import MyMessage
@@ -156,7 +158,8 @@ class FedMLServerManager(ServerManager):
         from ..wan_codec import decode, is_encoded, payload_bytes
         self.wan_bytes = getattr(self, "wan_bytes", 0) + payload_bytes(params)
         if is_encoded(params):   # compressed silo update: w_global + deq(Δ) (cross_silo/wan_codec.py)
-            params = decode(params, self.aggregator.get_global_model_params())
+            params = decode(params, self.aggregator.get_global_model_params(),
+                            device="cuda" if torch.cuda.is_available() else None)
         self.aggregator.add_local_trained_result(self._selected.index(sender), params,
                                                  msg.get(MyMessage.MSG_ARG_KEY_NUM_SAMPLES))
         if not self.aggregator.check_whether_all_receive():
