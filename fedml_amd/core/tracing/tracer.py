@@ -28,6 +28,7 @@ class Tracer:
         self._names = {}
         self._rev = []
         self._events = collections.deque(maxlen=capacity)
+        self._gpu_pending = []   # (name, start event, end event) awaiting resolution
         self._roctx = None
         try:
             import ctypes
@@ -84,6 +85,37 @@ class Tracer:
             yield
         finally:
             self.end(name)
+
+    @contextlib.contextmanager
+    def gpu_span(self, name: str, device=None):
+        """Host span + GPU time of the enclosed work: HIP events recorded on the current stream at entry
+        and exit (no synchronisation here). Host spans only time the ENQUEUE of asynchronous GPU work;
+        ``gpu_times()`` after the caller's own synchronize resolves what the GPU actually spent."""
+        import torch
+        use = self.enabled and torch.cuda.is_available() and (device is None or torch.device(device).type == "cuda")
+        if not use:
+            with self.span(name):
+                yield
+            return
+        st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        st.record()
+        self.begin(name)
+        try:
+            yield
+        finally:
+            en.record()
+            self.end(name)
+            self._gpu_pending.append((name, st, en))
+
+    def gpu_times(self, clear: bool = True):
+        """name → GPU milliseconds (summed) of the resolved ``gpu_span``s; blocks on their end events."""
+        out = collections.defaultdict(float)
+        for name, st, en in self._gpu_pending:
+            en.synchronize()
+            out[name] += float(st.elapsed_time(en))
+        if clear:
+            self._gpu_pending = []
+        return dict(out)
 
     def events(self):
         """List of (ts_ns, name, phase, tid)."""

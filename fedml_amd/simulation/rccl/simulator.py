@@ -127,9 +127,9 @@ class RCCLSimulator:
         if self.residual is not None:
             with tr.span("round.residual_migrate"):
                 self.residual.migrate(self.round_owner)
-        with tr.span("round.broadcast_local"):
+        with tr.gpu_span("round.broadcast_local", self.device):
             self.engine.load_global(self.global_flat)
-        with tr.span("round.local_train"):
+        with tr.gpu_span("round.local_train", self.device):
             # data order / augmentation keyed by (seed, round, client): identical for any world size and
             # exactly reproducible on resume from the round index alone
             rng_key = (int(getattr(args, "random_seed", 0)) * 1000003 + int(round_idx) * 7919) & 0x7FFFFFFF
@@ -139,7 +139,7 @@ class RCCLSimulator:
                 self.engine.train(self.store, slots, int(args.epochs), int(args.batch_size),
                                   float(args.learning_rate), generator=self.gen,
                                   shuffle=bool(getattr(args, "shuffle", True)), valid_slots=valid, rng_key=rng_key)
-        with tr.span("round.aggregate"):
+        with tr.gpu_span("round.aggregate", self.device):
             w = torch.where(valid, self.store.counts[slots].to(torch.float32), torch.zeros(self.C, device=self.device))
             if self.faults.active:
                 # lost uploads (dropout / missed deadline, core.fault): survivors are re-weighted
@@ -230,6 +230,8 @@ class RCCLSimulator:
             dt = time.perf_counter() - t0
             self.round_times.append(dt)
             rec = {"round_time_s": dt, "train_loss": float(self.engine.last_loss)}
+            # GPU time per phase (HIP events, resolved after the round's synchronize)
+            rec.update({f"gpu_ms/{k}": round(v, 3) for k, v in tracer().gpu_times().items()})
             if freq > 0 and (self.round_idx % freq == 0 or r == n - 1):
                 rec.update(self.evaluate())
             self.history[self.round_idx] = rec
