@@ -33,7 +33,15 @@ def mapping_processes_to_gpu_device_from_yaml_file(process_id, worker_number, gp
         raise ValueError(f"gpu_mapping '{gpu_util_key}' lists {len(table)} processes but worker_number={worker_number}")
     host, gpu = table[process_id]
     n_local = torch.cuda.device_count()
-    gpu = gpu % max(1, n_local)
+    if gpu >= n_local:
+        # a mis-configured mapping must not silently double-book another GPU (it used to wrap modulo
+        # the device count); FEDML_AMD_GPU_MAPPING_WRAP=1 keeps the wrap for rehearsals on smaller boxes
+        import os
+        if os.environ.get("FEDML_AMD_GPU_MAPPING_WRAP", "0") != "1":
+            raise ValueError(f"gpu_mapping '{gpu_util_key}': process {process_id} → GPU {gpu} on host {host}, "
+                             f"but only {n_local} GPU(s) are visible here")
+        logging.warning("gpu_mapping: GPU %d not present (%d visible) — wrapping for a rehearsal", gpu, n_local)
+        gpu = gpu % max(1, n_local)
     logging.info("process %d (host %s / %s) → cuda:%d", process_id, host, socket.gethostname(), gpu)
     if set_device:
         torch.cuda.set_device(gpu)
