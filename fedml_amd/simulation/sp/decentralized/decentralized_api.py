@@ -9,6 +9,12 @@ like the reference: worker j pushes ``W[j,i]·x_j`` to i). PushSum additionally 
 The reference hands every client the SAME model object (so its "workers" share parameters);
 here each worker really has its own. ``mode: LOCAL`` trains without communication.
 Regret = average loss over workers and iterations so far (reference ``cal_regret``).
+
+Multi-GPU (one process per GPU, ``torch.distributed`` initialised — RCCL over xGMI): the N workers
+are sharded over the ranks; each rank computes its workers' gradients and local steps, ONE
+``all_gather`` of the gossip rows per iteration replaces the reference's per-neighbour sends
+(``client_dsgd.py:104-122``), and each rank mixes only its own receiver rows ``X_own ← W[:, own]ᵀ X``
+on the MFMA kernel. The result equals the single-process run (tests/test_decentralized_dist.py).
 """
 import logging
 
@@ -18,6 +24,7 @@ from torch.func import functional_call, grad, vmap
 
 from ....core.distributed.topology import AsymmetricTopologyManager, SymmetricTopologyManager
 from .... import ops
+from ....parallel import comm
 
 
 def _streams_from_dataset(dataset, n_clients):
@@ -66,6 +73,12 @@ class DecentralizedFLAPI:
         self.omega = torch.ones(self.N, 1, device=self.device)
         self.z = self.x.clone()                              # de-biased model used for the loss
         self.regret_history = []
+        # rank sharding of the workers (world 1: all rows local)
+        self.rank, self.world = comm.rank(), comm.world_size()
+        self.per = -(-self.N // self.world)
+        if self.world > 1:   # one topology for all ranks (the generators draw random edges)
+            comm.broadcast_flat(self.mix, 0)
+        self.lo, self.hi = min(self.N, self.rank * self.per), min(self.N, (self.rank + 1) * self.per)
         out_dim = None
         with torch.no_grad():
             out_dim = self.model(self.X[0, :1]).shape[-1]
@@ -86,7 +99,50 @@ class DecentralizedFLAPI:
                                                             y.float().reshape(-1))
         return torch.nn.functional.cross_entropy(out, y.long().reshape(-1))
 
+    def _gather_rows(self, own):
+        """[hi − lo, D] own rows → [N, D] all workers' rows (one all_gather, padded shards)."""
+        buf = torch.zeros(self.per, own.shape[1], dtype=own.dtype, device=own.device)
+        buf[:own.shape[0]] = own
+        parts = comm.all_gather_flat(buf.reshape(-1))
+        return torch.cat([q.view(self.per, -1) for q in parts])[:self.N]
+
+    def _train_sharded(self):
+        """The same iteration on this rank's workers lo:hi, gossip over all_gather."""
+        loss_fn = vmap(self._loss)
+        grad_fn = vmap(grad(self._loss))
+        lo, hi = self.lo, self.hi
+        mix_own = self.mix[lo:hi].contiguous()          # receiver rows of this rank
+        x, z, om = self.x[lo:hi].clone(), self.z[lo:hi].clone(), self.omega[lo:hi].clone()
+        per_iter = []
+        for t in range(self.T * self.epoch):
+            it = t % self.T
+            xb, yb = self.X[lo:hi, it], self.Y[lo:hi, it]
+            per_iter.append(loss_fn(z, xb, yb).double().sum())
+            g = grad_fn(z, xb, yb)
+            if self.wd:
+                g = g + self.wd * z
+            if self.mode == "LOCAL":
+                z = z - self.lr * g
+                x = z
+                continue
+            x = x - self.lr * g
+            xa = self._gather_rows(x)
+            x = ops.subset_aggregate(mix_own, xa) if xa.is_cuda else mix_own @ xa
+            if self.mode == "PUSHSUM":
+                om = mix_own @ self._gather_rows(om)
+                z = x / om
+            else:
+                z = x
+        losses = torch.stack(per_iter).to(torch.float64)
+        comm.all_reduce_flat(losses)
+        cum = torch.cumsum(losses, 0).cpu()
+        self.regret_history = (cum / (self.N * torch.arange(1, len(per_iter) + 1))).tolist()
+        self.z = self._gather_rows(z)
+        return {"regret": self.regret_history, "params": self.z}
+
     def train(self):
+        if self.world > 1:
+            return self._train_sharded()
         loss_fn = vmap(self._loss)
         grad_fn = vmap(grad(self._loss))
         per_iter = []
