@@ -1,6 +1,8 @@
 """FedNAS local search trainer (reference: `mpi_p2p_mp/fednas/FedNASTrainer.py`): on each
-client, alternate a first-order DARTS architecture step (Adam on the alphas, validation
-split) with an SGD weight step (train split); in ``stage == "train"`` only weights move.
+client, alternate a DARTS architecture step (Adam on the alphas from the validation split —
+first order, or the unrolled second-order gradient with ``unrolled: true``, Architect in
+``models/cv/darts_architect.py``) with an SGD weight step (train split); in ``stage == "train"``
+only weights move.
 The model is ``models.cv.darts.Network``; alphas live in the state dict so the FedAvg
 aggregator averages weights and architecture together."""
 import logging
@@ -26,8 +28,11 @@ class ModelTrainerNAS(ClientTrainer):
         w_opt = torch.optim.SGD(model.weight_parameters(), lr=float(args.learning_rate),
                                 momentum=float(getattr(args, "momentum", 0.9) or 0.9),
                                 weight_decay=float(getattr(args, "weight_decay", 3e-4) or 3e-4))
-        a_opt = torch.optim.Adam(model.arch_parameters(), lr=float(getattr(args, "arch_learning_rate", 3e-4)),
-                                 betas=(0.5, 0.999), weight_decay=float(getattr(args, "arch_weight_decay", 1e-3)))
+        from ..models.cv.darts_architect import Architect
+        if getattr(self, "_architect", None) is None or self._architect.model is not model:
+            self._architect = Architect(model, args)   # keeps its Adam state across rounds, like the reference
+        unrolled = bool(getattr(args, "unrolled", False))
+        eta = float(args.learning_rate)
         search = str(getattr(args, "stage", "search")) == "search"
         batches = list(train_data)
         # reference splits each local shard into train / validation halves for the bilevel step
@@ -37,11 +42,9 @@ class ModelTrainerNAS(ClientTrainer):
         for _ in range(int(args.epochs)):
             for i, (x, y) in enumerate(trn):
                 x, y = x.to(device), y.to(device)
-                if search:
+                if search:   # first-order or unrolled second-order α step (models/cv/darts_architect.py)
                     vx, vy = val[i % len(val)]
-                    a_opt.zero_grad(set_to_none=True)
-                    crit(model(vx.to(device)), vy.to(device)).backward()
-                    a_opt.step()
+                    self._architect.step(x, y, vx.to(device), vy.to(device), eta, w_opt, unrolled=unrolled)
                 w_opt.zero_grad(set_to_none=True)
                 loss = crit(model(x), y)
                 loss.backward()

@@ -1,0 +1,43 @@
+"""Second-order (unrolled) DARTS architecture gradient (reference model/cv/darts/architect.py): the
+finite-difference Hessian-vector form equals the exact autograd second-order gradient of
+L_val(w − η(∇_w L_train(w, α) + λw), α) with respect to α. The reference's step r = 1e-2 is coarse
+on a tiny random ReLU/BN net (measured: the central difference only converges below r ≈ 1e-5 here),
+so the algebra is checked in fp64 at r = 1e-6; the default stays the reference's 1e-2."""
+import torch
+from torch.func import functional_call
+
+from fedml_amd.arguments import Arguments
+from fedml_amd.models.cv.darts import Network
+from fedml_amd.models.cv.darts_architect import Architect
+
+
+def test_unrolled_gradient_matches_exact_second_order():
+    torch.manual_seed(0)
+    torch.set_default_dtype(torch.float64)
+    try:
+        m = Network(C=4, num_classes=3, layers=3, steps=2)   # normal + reduction cells
+        args = Arguments.from_dict({"x": {"momentum": 0.9, "weight_decay": 3e-4, "arch_hvp_r": 1e-6}})
+        arch = Architect(m, args)
+        assert Architect(m, Arguments.from_dict({"x": {}})).r == 1e-2
+        xt, yt = torch.randn(4, 3, 8, 8), torch.randint(0, 3, (4,))
+        xv, yv = torch.randn(4, 3, 8, 8), torch.randint(0, 3, (4,))
+        eta = 0.05
+        got = [g.clone() for g in arch.unrolled_grads(xt, yt, xv, yv, eta)]
+        W, A = arch._split()
+        bufs = {n: b.clone() for n, b in m.named_buffers()}
+
+        def loss(Wd, Ad, x, y):
+            return torch.nn.functional.cross_entropy(functional_call(m, {**Wd, **Ad, **bufs}, (x,)), y)
+        Ad = {n: p.detach().requires_grad_(True) for n, p in A.items()}
+        Wd = {n: p.detach().requires_grad_(True) for n, p in W.items()}
+        gW = torch.autograd.grad(loss(Wd, Ad, xt, yt), list(Wd.values()), create_graph=True, allow_unused=True)
+        gW = [torch.zeros_like(p) if g is None else g for p, g in zip(Wd.values(), gW)]
+        Wu = {n: Wd[n] - eta * (g + 3e-4 * Wd[n]) for n, g in zip(Wd, gW)}
+        exact = torch.autograd.grad(loss(Wu, Ad, xv, yv), list(Ad.values()))
+        first = torch.autograd.grad(loss({n: p.detach() for n, p in W.items()}, Ad, xv, yv), list(Ad.values()))
+        for g, e, f in zip(got, exact, first):
+            rel = float((g - e).norm() / e.norm())
+            assert rel < 1e-3, rel
+            assert float((f - e).norm() / e.norm()) > 10 * rel   # the second-order term is not negligible here
+    finally:
+        torch.set_default_dtype(torch.float32)
