@@ -44,6 +44,14 @@ def create(args, output_dim):
         if ds in ("femnist", "fed_emnist"):
             return CNN_DropOut(False)
         return CNN_DropOut(output_dim == 10)
+    if name in ("deeplabv3_plus", "deeplab"):   # FedSeg (reference mpi_p2p_mp/fedseg): DeepLabV3+ backbones
+        from .cv.segmentation import DeepLabV3PlusNet
+        return DeepLabV3PlusNet(output_dim, str(getattr(args, "backbone", "resnet101")),
+                                int(getattr(args, "outstride", getattr(args, "output_stride", 16)) or 16),
+                                bool(getattr(args, "backbone_freezed", False)))
+    if name == "unet":
+        from .cv.segmentation import UNet
+        return UNet(output_dim)
     if name == "cnn_original":
         return CNN_OriginalFedAvg(output_dim == 10)
     if name in ("resnet18_gn",):

@@ -133,23 +133,41 @@ class Saver:
 
 
 class ModelTrainerSeg(ClientTrainer):
+    """``backbone_freezed`` (reference MyModelTrainer.py:12-25): only ``encoder_decoder`` trains and travels;
+    otherwise backbone at 1× and head at 10× the learning rate when the model exposes the split."""
+
+    def _frozen(self):
+        return bool(getattr(self.args, "backbone_freezed", False)) and hasattr(self.model, "encoder_decoder")
+
+    def _payload_module(self):
+        return self.model.encoder_decoder if self._frozen() else self.model
+
     def get_model_params(self):
-        return {k: v.detach().cpu().clone() for k, v in self.model.state_dict().items()}
+        return {k: v.detach().cpu().clone() for k, v in self._payload_module().state_dict().items()}
 
     def set_model_params(self, model_parameters):
-        self.model.load_state_dict(model_parameters)
+        self._payload_module().load_state_dict(model_parameters)
 
     def train(self, train_data, device, args=None):
         args = args or self.args
         model = self.model.to(device)
         model.train()
         crit = SegmentationLosses().build_loss(str(getattr(args, "loss_type", "ce")))
-        opt = torch.optim.SGD(model.parameters(), lr=float(args.learning_rate),
-                              momentum=float(getattr(args, "momentum", 0.9) or 0.9),
-                              weight_decay=float(getattr(args, "weight_decay", 5e-4) or 5e-4),
-                              nesterov=bool(getattr(args, "nesterov", False)))
-        sched = LR_Scheduler(str(getattr(args, "lr_scheduler", "poly")), float(args.learning_rate),
-                             int(args.epochs), max(1, len(train_data)))
+        lr = float(args.learning_rate)
+        kw = dict(momentum=float(getattr(args, "momentum", 0.9) or 0.9),
+                  weight_decay=float(getattr(args, "weight_decay", 5e-4) or 5e-4),
+                  nesterov=bool(getattr(args, "nesterov", False)))
+        if self._frozen():   # head only, at 10× (the scheduler scales group 0 → keep base lr × 10 there)
+            for p in model.backbone.parameters():
+                p.requires_grad_(False)
+            opt = torch.optim.SGD([p for p in model.parameters() if p.requires_grad], lr=lr * 10, **kw)
+            lr = lr * 10
+        elif hasattr(model, "get_1x_lr_params"):
+            opt = torch.optim.SGD([{"params": model.get_1x_lr_params(), "lr": lr},
+                                   {"params": model.get_10x_lr_params(), "lr": lr * 10}], **kw)
+        else:
+            opt = torch.optim.SGD(model.parameters(), lr=lr, **kw)
+        sched = LR_Scheduler(str(getattr(args, "lr_scheduler", "poly")), lr, int(args.epochs), max(1, len(train_data)))
         losses = []
         for ep in range(int(args.epochs)):
             for i, (x, y) in enumerate(train_data):

@@ -181,3 +181,36 @@ def test_secagg_dropout_recovery():
     # a single masked upload reveals nothing close to the input
     single = cl[0].masked_input(xs[0], sa.pks)
     assert not torch.allclose(single.double() / 2 ** 20, xs[0].double(), atol=1.0)
+
+
+@pytest.mark.parametrize("backbone,os_", [("mobilenet", 16), ("resnet50", 8)])
+def test_deeplabv3_plus_backbones(backbone, os_):
+    """DeepLabV3+ with the reference FedSeg backbones: full-resolution logits, the 1×/10× parameter
+    split covers every trainable parameter, output stride by dilation (same spatial cost as stride)."""
+    from fedml_amd.models.cv.segmentation import DeepLabV3PlusNet
+    torch.manual_seed(0)
+    m = DeepLabV3PlusNet(5, backbone, os_)
+    x = torch.randn(2, 3, 64, 64)
+    assert m(x).shape == (2, 5, 64, 64)
+    high, low = m.backbone(x)
+    assert high.shape[-1] == 64 // os_ and low.shape[-1] == 16
+    n1, n10 = len(m.get_1x_lr_params()), len(m.get_10x_lr_params())
+    assert n1 + n10 == len([p for p in m.parameters() if p.requires_grad])
+
+
+def test_fedseg_deeplab_frozen_backbone():
+    """backbone_freezed (reference MyModelTrainer.py:12-25): only encoder_decoder trains and travels."""
+    from fedml_amd.data.segmentation import load_synthetic_segmentation
+    from fedml_amd.models.cv.segmentation import DeepLabV3PlusNet
+    from fedml_amd.simulation.mp.fedseg import FedML_FedSeg_distributed
+    ds, ncls = load_synthetic_segmentation(4, samples_per_client=4, n_classes=3, hw=32, batch_size=2)
+    a = _args("FedSeg", learning_rate=0.01, comm_round=1, backbone_freezed=True, client_num_in_total=4,
+              client_num_per_round=4)
+    torch.manual_seed(0)
+    m = DeepLabV3PlusNet(ncls, "mobilenet", 16, backbone_freezed=True)
+    bb0 = {k: v.clone() for k, v in m.backbone.state_dict().items()}
+    res = run_message_passing(FedML_FedSeg_distributed, a, torch.device("cpu"), ds, m)
+    g = res["global_model"]
+    assert all(not k.startswith("backbone.") for k in g) and any(k.startswith("aspp.") for k in g)
+    assert all(torch.equal(v, m.backbone.state_dict()[k]) for k, v in bb0.items() if v.is_floating_point()
+               and "running" not in k)
