@@ -72,6 +72,8 @@ def create(args, output_dim):
         return MobileNetV3(model_mode=getattr(args, "model_mode", "LARGE"), num_classes=output_dim)
     if name == "efficientnet":
         return EfficientNet(num_classes=output_dim)
+    if name.startswith("efficientnet-b"):   # compound-scaled variants (efficientnet_utils.py)
+        return EfficientNet.from_name(name, output_dim, stem_stride=int(getattr(args, "stem_stride", 2)))
     if name.startswith("vgg"):
         return VGG(name, output_dim)
     if name in ("distilbert", "distilbert-base-uncased"):

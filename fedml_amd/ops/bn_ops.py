@@ -59,33 +59,34 @@ class _BNAct(torch.autograd.Function):
             residual = residual.contiguous(memory_format=_CL)
         C = x.shape[1]
         M = x.numel() // C
-        acc = torch.zeros(4 * C, dtype=torch.float32, device=x.device)   # fwd Σx, Σx² | bwd Σg, Σg(x-μ)
+        acc = torch.zeros(2 * C, dtype=torch.float32, device=x.device)   # fwd Σ(x−K), Σ(x−K)²
         save = torch.empty(2 * C, dtype=torch.float32, device=x.device)  # mean, invstd
         y = torch.empty_like(x, memory_format=_CL)
         rc = _fn("fa_bnc_fwd")(_p(x), _p(residual), _p(y), _i64(M), _c.c_int(C), _p(acc), _p(weight), _p(bias),
                                _f(eps), _f(momentum), _p(rmean), _p(rvar), _p(save), _c.c_int(int(relu)),
                                _stream(x))
         _check(rc, "fa_bnc_fwd")
-        ctx.save_for_backward(x, y if relu else None, weight, save, acc)
+        ctx.save_for_backward(x, y if relu else None, weight, save)
         ctx.relu, ctx.has_res, ctx.M, ctx.has_b = relu, residual is not None, M, bias is not None
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, weight, save, acc = ctx.saved_tensors
+        x, y, weight, save = ctx.saved_tensors
         dy = dy.contiguous(memory_format=_CL)
         if dy.data_ptr() % 16:
             dy = dy.clone(memory_format=_CL)
         C, M = x.shape[1], ctx.M
-        # the backward sums are accumulated atomically into acc[2C:]: zero them on EVERY backward (a second
-        # backward through a retained graph must not add onto the first one's sums)
-        acc[2 * C:].zero_()
+        # the backward sums are accumulated atomically: a fresh zeroed buffer on EVERY backward (a second
+        # backward through a retained graph must not add onto the first one's sums, and a saved tensor must
+        # not be modified in place)
+        bacc = torch.zeros(2 * C, dtype=torch.float32, device=x.device)
         dx = torch.empty_like(x, memory_format=_CL)
         dres = torch.empty_like(x, memory_format=_CL) if (ctx.has_res and ctx.relu) else None
         dw = torch.empty(C, dtype=torch.float32, device=x.device) if weight is not None else None
         db = torch.empty(C, dtype=torch.float32, device=x.device) if ctx.has_b else None
         rc = _fn("fa_bnc_bwd")(_p(dy), _p(x), _p(y), _p(dres), _p(dx), _i64(M), _c.c_int(C), _p(save),
-                               _c.c_void_p(acc.data_ptr() + 2 * C * 4), _p(weight), _p(dw), _p(db), _stream(x))
+                               _p(bacc), _p(weight), _p(dw), _p(db), _stream(x))
         _check(rc, "fa_bnc_bwd")
         if ctx.has_res and not ctx.relu:
             dres = dy
