@@ -102,6 +102,16 @@ class RCCLSimulator:
         self.dropped_clients: List[int] = []
         self.history: Dict[int, dict] = {}
         self.round_idx = 0
+        # elastic: survive a dead peer by rebuilding the communicator from the survivors (parallel/elastic.py)
+        self.elastic = bool(getattr(args, "elastic", False)) and comm.is_dist()
+        if self.elastic:
+            if self.compression:
+                raise ValueError("elastic re-init does not support compressed updates (residual rows of a dead "
+                                 "rank are lost)")
+            from ...parallel import elastic
+            elastic.setup(self.rank, self.world, str(torch.distributed.get_backend()),
+                          int(getattr(args, "elastic_timeout_s", 60) or 60))
+        self.world_changes: List[tuple] = []
 
     # ---------------------------------------------------------------------------------------------
     def assignment(self, round_idx: int):
@@ -224,7 +234,7 @@ class RCCLSimulator:
         freq = int(getattr(self.args, "frequency_of_the_test", 0) or 0)
         for r in range(n):
             t0 = time.perf_counter()
-            self.run_round(self.round_idx)
+            self._run_round_elastic(self.round_idx)
             if self.device.type == "cuda":
                 torch.cuda.synchronize(self.device)
             dt = time.perf_counter() - t0
@@ -243,6 +253,25 @@ class RCCLSimulator:
                 self.save_checkpoint(ck)
             self.round_idx += 1
         return self.global_model_state()
+
+    def _run_round_elastic(self, round_idx):
+        if not self.elastic:
+            return self.run_round(round_idx)
+        while True:
+            try:
+                return self.run_round(round_idx)
+            except (RuntimeError, torch.distributed.DistBackendError) as e:
+                from ...parallel import elastic
+                logging.warning("round %d: collective failed (%s) — re-initialising the communicator", round_idx,
+                                str(e).splitlines()[0][:200])
+                old = self.world
+                self.rank, self.world = elastic.reinit(float(getattr(self.args, "elastic_settle_s", 3.0) or 3.0))
+                self.world_changes.append((round_idx, old, self.world))
+                self.C = math.ceil(self.K / self.world)
+                if self.C != self.engine.C:   # more clients per rank now: a wider client stack
+                    self.engine.close()
+                    self.engine = ClientBatchEngine(self.model, self.C, self.device, self.args, self.compute_dtype)
+                comm.broadcast_flat(self.global_flat, 0)   # every survivor restarts the round from rank 0's model
 
     # ---------------------------------------------------------------------------------------------
     def global_model_state(self):

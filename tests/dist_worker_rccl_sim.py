@@ -23,6 +23,8 @@ def run(rank, world, port, out_path, model_name, clients, counts_seed, shuffle=F
         "epochs": 1, "batch_size": 8, "client_optimizer": "sgd", "learning_rate": 0.05, "frequency_of_the_test": 0,
         "random_seed": 0, "shuffle": shuffle, "data_augmentation": augment and ds == "cifar10",
         "compression": os.environ.get("FEDML_TEST_COMPRESSION", ""),
+        "elastic": os.environ.get("FEDML_TEST_ELASTIC", "0") == "1", "elastic_timeout_s": 30,
+        "elastic_settle_s": 2.0,
         "allreduce_bucket_mb": float(os.environ.get("FEDML_TEST_BUCKET_MB", "32")),
         "client_num_per_round": int(os.environ.get("FEDML_TEST_PER_ROUND", clients))}})
     spec = get_spec(ds)
@@ -36,7 +38,19 @@ def run(rank, world, port, out_path, model_name, clients, counts_seed, shuffle=F
     counts = [int(v) for v in torch.randint(8, 24, (clients,), generator=g)]
     store = DeviceClientStore.synthetic_on_device(spec, counts, torch.device("cpu"), seed=0)
     sim = RCCLSimulator(args, torch.device("cpu"), None, model, store=store)
+    die = os.environ.get("FEDML_TEST_DIE")   # "rank:round" — that rank's process vanishes before the round
+    if die:
+        dr, dround = (int(v) for v in die.split(":"))
+        orig = sim.run_round
+
+        def run_round(ri):
+            if rank == dr and ri == dround:
+                os._exit(0)
+            return orig(ri)
+        sim.run_round = run_round
     sim.run(int(os.environ.get("FEDML_TEST_ROUNDS", "2")))
+    if die and rank == 0:
+        assert sim.world_changes and sim.world_changes[0][1:] == (world, world - 1), sim.world_changes
     if rank == 0:
         torch.save(sim.global_flat.clone(), out_path)
     comm.destroy()

@@ -67,3 +67,20 @@ def test_bucketed_aggregation_matches_single_rank(tmp_path):
     w1 = _launch(1, str(tmp_path / "w1.pt"), "lr", 7, True)
     w2 = _launch(2, str(tmp_path / "w2.pt"), "lr", 7, True, FEDML_TEST_BUCKET_MB="0.01")
     assert float((w1 - w2).norm() / w1.norm()) < 1e-5
+
+
+def test_elastic_reinit_after_rank_death(tmp_path):
+    """A rank dies before round 1 (of 3): the survivors' all-reduce fails, they rebuild the communicator
+    from the survivors (parallel/elastic.py), re-pack the clients and redo the round — the final model
+    equals the single-rank run (world-size invariance)."""
+    env = dict(FEDML_TEST_ELASTIC="1", FEDML_TEST_ROUNDS="3")
+    w1 = _launch(1, str(tmp_path / "w1.pt"), "lr", 7, True, **env)
+    port = _free_port()
+    out = str(tmp_path / "w3.pt")
+    e = dict(os.environ, PYTHONPATH=os.path.dirname(HERE), OMP_NUM_THREADS="2", FEDML_TEST_DIE="2:1", **env)
+    procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker_rccl_sim.py"), str(r), "3", str(port),
+                               out, "lr", "7", "3", "1", "0"], env=e) for r in range(3)]
+    codes = [p.wait(timeout=300) for p in procs]
+    assert codes == [0, 0, 0], codes
+    w3 = torch.load(out, weights_only=True)
+    assert float((w1 - w3).norm() / w1.norm()) < 1e-5
