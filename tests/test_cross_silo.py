@@ -242,3 +242,12 @@ def test_wan_codec_roundtrip_and_error_feedback():
     assert err < 0.01 * 4 / 127 * 2          # within one int8 step of the block scale
     # the quantisation error is carried: Δ + residual reproduces the true update exactly
     assert torch.allclose(dec["w"] - g["w"] + enc.residual[:1000], local["w"] - g["w"], atol=1e-6)
+
+
+def test_multinode_silo_commands():
+    from fedml_amd.cross_silo.hierarchical.dist_trainer_launcher import launch_silo_multinode
+    cmds = launch_silo_multinode("client.py", ["localhost", "node2"], 4, "10.0.0.1", 29700, ["--cf", "c.yaml"],
+                                 workdir="/srv/run", dry_run=True)
+    assert cmds[0][1:4] == ["-m", "torch.distributed.run", "--nnodes=2"] and "--node-rank=0" in cmds[0]
+    assert cmds[1][0] == "ssh" and "--node-rank=1" in cmds[1][-1] and "cd /srv/run" in cmds[1][-1]
+    assert "--rdzv-endpoint=10.0.0.1:29700" in cmds[0] and cmds[0][-2:] == ["--cf", "c.yaml"]
