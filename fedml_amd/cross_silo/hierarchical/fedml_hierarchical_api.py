@@ -17,7 +17,7 @@ def init_client(args, device, comm, rank, size, model, dataset, model_trainer=No
     (train_num, _, _, _, num_dict, train_local, test_local, _) = dataset[:8]
     adapter = TrainerDistAdapter(args, device, rank, model, train_num, num_dict, train_local, test_local,
                                  model_trainer)
-    if int(getattr(args, "proc_rank_in_silo", 0) or 0) == 0:
+    if adapter.rank_in_silo == 0:
         return ClientMasterManager(args, adapter, comm, rank, size, _backend(args, comm))
     return ClientSlaveManager(args, adapter)
 

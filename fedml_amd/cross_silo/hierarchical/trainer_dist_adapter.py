@@ -5,6 +5,8 @@ backward, see ``distributed.ddp``) and trains on its shard of the silo's data; t
 is unchanged — gradient averaging completes automatically at the end of each backward. The
 master broadcasts the global model to the silo with ONE flat-buffer broadcast (the reference uses
 ``broadcast_object_list`` of a pickled state dict)."""
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -20,7 +22,9 @@ class TrainerDistAdapter:
         self.args = args
         self.device = torch.device(device) if device is not None else torch.device("cpu")
         self.n_proc = int(getattr(args, "n_proc_in_silo", 1) or 1)
-        self.rank_in_silo = int(getattr(args, "proc_rank_in_silo", 0) or 0)
+        # explicit --proc_rank_in_silo, else torchrun's RANK (multi-node silos, dist_trainer_launcher.py)
+        pr = getattr(args, "proc_rank_in_silo", None)
+        self.rank_in_silo = int(pr) if pr not in (None, "") else int(os.environ.get("RANK", "0"))
         self.pg = None
         if self.n_proc > 1:
             self.pg = ProcessGroupManager(self.rank_in_silo, self.n_proc, getattr(args, "pg_master_address", "127.0.0.1"),
