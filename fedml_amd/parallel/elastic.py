@@ -46,11 +46,17 @@ def reinit(settle_s: float = 3.0):
     _STATE["gen"] += 1
     g = _STATE["gen"]
     idx = int(st.add(f"elastic/{g}/arrived", 1)) - 1
-    time.sleep(settle_s)
-    world = int(st.add(f"elastic/{g}/arrived", 0))
     if idx == 0:
-        st.set(f"elastic/{g}/world", str(world))
-    world = int(st.get(f"elastic/{g}/world"))   # everyone agrees with the first arrival's count
+        # the first survivor closes the generation once nobody new has checked in for settle_s (peers detect
+        # the failure at different times — a loaded machine spreads that by seconds)
+        last, quiet = 1, 0.0
+        while quiet < settle_s:
+            time.sleep(0.2)
+            n = int(st.add(f"elastic/{g}/arrived", 0))
+            quiet = 0.0 if n != last else quiet + 0.2
+            last = n
+        st.set(f"elastic/{g}/world", str(last))
+    world = int(st.get(f"elastic/{g}/world"))   # blocks until the generation is closed
     if idx >= world:
         raise RuntimeError("elastic: arrived after the new world was fixed")
     pg_store = dist.PrefixStore(f"elastic/{g}/pg", st)

@@ -24,7 +24,7 @@ def run(rank, world, port, out_path, model_name, clients, counts_seed, shuffle=F
         "random_seed": 0, "shuffle": shuffle, "data_augmentation": augment and ds == "cifar10",
         "compression": os.environ.get("FEDML_TEST_COMPRESSION", ""),
         "elastic": os.environ.get("FEDML_TEST_ELASTIC", "0") == "1", "elastic_timeout_s": 30,
-        "elastic_settle_s": 2.0,
+        "elastic_settle_s": 4.0,
         "allreduce_bucket_mb": float(os.environ.get("FEDML_TEST_BUCKET_MB", "32")),
         "client_num_per_round": int(os.environ.get("FEDML_TEST_PER_ROUND", clients))}})
     spec = get_spec(ds)
