@@ -175,6 +175,52 @@ FA_EXPORT int fa_block_out_f32(const float* y, const float* s, const float* t, c
   return block_out<F32>(y, s, t, r, rs, rt, out, C, per_client, Ch, nimg, per_img, stream);
 }
 
+// ---- materialised BN backward operand: dy = α·g + β·y + γ (per client and channel), valid images only.
+// The wide-layer backward kernels then stream ONE tensor instead of two (g, y) and skip the transform —
+// the weight-gradient kernel re-reads dy once per K-tile (36× for a 512-channel 3×3 layer).
+template <class P>
+__global__ __launch_bounds__(256) void dy_apply_kernel(const typename P::T* __restrict__ g,
+                                                       const typename P::T* __restrict__ y, const float* __restrict__ a,
+                                                       const float* __restrict__ b, const float* __restrict__ cg_,
+                                                       typename P::T* __restrict__ out, int nvec, int cg,
+                                                       const int* __restrict__ nimg, int vec_per_img) {
+  constexpr int V = P::VEC;
+  const int c = blockIdx.y;
+  const int v = blockIdx.x * 256 + threadIdx.x;
+  if (v >= (nimg ? min(nvec, nimg[c] * vec_per_img) : nvec)) return;
+  const int64_t base = (int64_t)c * nvec * V + (int64_t)v * V;
+  const int64_t co = (int64_t)c * cg * V + (v % cg) * V;
+  float f[V], h[V];
+  P::unpack(*reinterpret_cast<const uint4*>(g + base), f);
+  P::unpack(*reinterpret_cast<const uint4*>(y + base), h);
+#pragma unroll
+  for (int j = 0; j < V; ++j) f[j] = a[co + j] * f[j] + b[co + j] * h[j] + cg_[co + j];
+  *reinterpret_cast<uint4*>(out + base) = P::pack(f);
+}
+
+template <class P>
+static int dy_apply(const void* g, const void* y, const float* a, const float* b, const float* cc, void* out, int C,
+                    int64_t per_client, int Ch, const int* nimg, int per_img, hipStream_t stream) {
+  using T = typename P::T;
+  constexpr int V = P::VEC;
+  if (Ch % V != 0 || per_client / V > INT32_MAX) return -3;
+  const int nvec = (int)(per_client / V);
+  hipLaunchKernelGGL(dy_apply_kernel<P>, dim3((nvec + 255) / 256, C), dim3(256), 0, stream, (const T*)g, (const T*)y,
+                     a, b, cc, (T*)out, nvec, Ch / V, nimg, per_img / V);
+  return (int)hipGetLastError();
+}
+
+FA_EXPORT int fa_dy_apply(const uint16_t* g, const uint16_t* y, const float* a, const float* b, const float* c,
+                          uint16_t* out, int C, int64_t per_client, int Ch, const int* nimg, int per_img,
+                          hipStream_t stream) {
+  return dy_apply<BF16>(g, y, a, b, c, out, C, per_client, Ch, nimg, per_img, stream);
+}
+FA_EXPORT int fa_dy_apply_f32(const float* g, const float* y, const float* a, const float* b, const float* c,
+                              float* out, int C, int64_t per_client, int Ch, const int* nimg, int per_img,
+                              hipStream_t stream) {
+  return dy_apply<F32>(g, y, a, b, c, out, C, per_client, Ch, nimg, per_img, stream);
+}
+
 // ---- global average pool (forward): pooled[c][n][ch] = mean_hw out[c][n][hw][ch] (fp32 out)
 // Padding images (n ≥ nimg[c], N images per client) get zero rows: the head reads them (with zero loss
 // weight) and must see finite values.

@@ -926,6 +926,29 @@ static int conv_fwd(const void* x, const void* wpk, int64_t wpk_ld, const float*
   return dispatch_nt<P, AOP_ACT, PRO_NONE, MODE_FWD, EPI_FWD>(Cout, a, C, stream);
 }
 
+template <class P, int AOP>
+static int conv_bwd_data_dispatch(const ConvArgs& a, int epi, int C, int Cin, int Cout, int KH, int KW, int stride,
+                                  int pad, int Hx, int Wx, int Hy, int Wy, hipStream_t stream) {
+  // 3×3 / stride-2 / pad-1 (ResNet-18 stage entries): parity-class GEMMs over the valid taps only
+  if (KH == 3 && KW == 3 && stride == 2 && pad == 1 && Cin % 64 == 0 && Cout % 64 == 0) {
+    switch (epi) {
+      case EPI_STORE: return launch_convk<P, AOP, PRO_NONE, MODE_BWDS2, EPI_STORE>(a, Cin, C, stream);
+      case EPI_MASK: return launch_convk<P, AOP, PRO_NONE, MODE_BWDS2, EPI_MASK>(a, Cin, C, stream);
+      case EPI_BLOCK: return launch_convk<P, AOP, PRO_NONE, MODE_BWDS2, EPI_BLOCK>(a, Cin, C, stream);
+      default: return -4;
+    }
+  }
+  switch (epi) {
+    case EPI_STORE:
+      if (KH == 1 && KW == 1 && stride == 2 && pad == 0 && Hx == 2 * Hy && Wx == 2 * Wy)
+        return dispatch_nt<P, AOP, PRO_NONE, MODE_BWD2, EPI_STORE>(Cin, a, C, stream);
+      return dispatch_nt<P, AOP, PRO_NONE, MODE_BWD, EPI_STORE>(Cin, a, C, stream);
+    case EPI_MASK: return dispatch_nt<P, AOP, PRO_NONE, MODE_BWD, EPI_MASK>(Cin, a, C, stream);
+    case EPI_BLOCK: return dispatch_nt<P, AOP, PRO_NONE, MODE_BWD, EPI_BLOCK>(Cin, a, C, stream);
+    default: return -4;
+  }
+}
+
 template <class P>
 static int conv_bwd_data(const void* g, const void* yv, const float* alpha, const float* beta, const float* gamma,
                          const void* wpk_b, int64_t wpk_ld, void* dx, int epi, const void* e_x, const float* e_s,
@@ -940,24 +963,9 @@ static int conv_bwd_data(const void* g, const void* yv, const float* alpha, cons
   a.stats = stats; a.NS = 3;  // backward statistics are always laid out [C][Ch][3]
   a.Nb = Nb; a.Hs = Hy; a.Ws = Wy; a.KC = Cout; a.Ho = Hx; a.Wo = Wx; a.KH = KH; a.KW = KW; a.stride = stride;
   a.pad = pad; a.ldk = ldk2; a.Kp = (KH * KW * Cout + 31) / 32 * 32; a.tiles_per_wave = tiles_per_wave;
-  // 3×3 / stride-2 / pad-1 (ResNet-18 stage entries): parity-class GEMMs over the valid taps only
-  if (KH == 3 && KW == 3 && stride == 2 && pad == 1 && Cin % 64 == 0 && Cout % 64 == 0) {
-    switch (epi) {
-      case EPI_STORE: return launch_convk<P, AOP_DY, PRO_NONE, MODE_BWDS2, EPI_STORE>(a, Cin, C, stream);
-      case EPI_MASK: return launch_convk<P, AOP_DY, PRO_NONE, MODE_BWDS2, EPI_MASK>(a, Cin, C, stream);
-      case EPI_BLOCK: return launch_convk<P, AOP_DY, PRO_NONE, MODE_BWDS2, EPI_BLOCK>(a, Cin, C, stream);
-      default: return -4;
-    }
-  }
-  switch (epi) {
-    case EPI_STORE:
-      if (KH == 1 && KW == 1 && stride == 2 && pad == 0 && Hx == 2 * Hy && Wx == 2 * Wy)
-        return dispatch_nt<P, AOP_DY, PRO_NONE, MODE_BWD2, EPI_STORE>(Cin, a, C, stream);
-      return dispatch_nt<P, AOP_DY, PRO_NONE, MODE_BWD, EPI_STORE>(Cin, a, C, stream);
-    case EPI_MASK: return dispatch_nt<P, AOP_DY, PRO_NONE, MODE_BWD, EPI_MASK>(Cin, a, C, stream);
-    case EPI_BLOCK: return dispatch_nt<P, AOP_DY, PRO_NONE, MODE_BWD, EPI_BLOCK>(Cin, a, C, stream);
-    default: return -4;
-  }
+  // yv == null: `g` already holds the materialised dy (dy_apply), the operand is loaded as is
+  if (!yv) return conv_bwd_data_dispatch<P, AOP_ACT>(a, epi, C, Cin, Cout, KH, KW, stride, pad, Hx, Wx, Hy, Wy, stream);
+  return conv_bwd_data_dispatch<P, AOP_DY>(a, epi, C, Cin, Cout, KH, KW, stride, pad, Hx, Wx, Hy, Wy, stream);
 }
 
 // forward: y = conv(pro(x)) − K, stats[c][co][2] += (Σy, Σy²) of the stored y; K = pivot[c][co] (null: 0).

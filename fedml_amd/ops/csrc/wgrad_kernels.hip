@@ -295,11 +295,12 @@ __global__ __launch_bounds__(256) void wgrad_wide_kernel(
   const int col = (threadIdx.x % CPR) * V;
   const int pp0 = threadIdx.x / CPR;
   float ca[V], cb[V], cc[V], cs[V], ct[V];
+  const bool DYM = yv == nullptr;   // g holds the materialised dy (dy_apply): no transform, no y stream
 #pragma unroll
   for (int j = 0; j < V; ++j) {
-    ca[j] = alpha[(int64_t)c * Cout + co_lo + col + j];
-    cb[j] = beta[(int64_t)c * Cout + co_lo + col + j];
-    cc[j] = gamma[(int64_t)c * Cout + co_lo + col + j];
+    ca[j] = DYM ? 1.f : alpha[(int64_t)c * Cout + co_lo + col + j];
+    cb[j] = DYM ? 0.f : beta[(int64_t)c * Cout + co_lo + col + j];
+    cc[j] = DYM ? 0.f : gamma[(int64_t)c * Cout + co_lo + col + j];
   }
   const bool kval = col < kn;
   const int k0 = k_lo + (kval ? col : 0);
@@ -319,7 +320,7 @@ __global__ __launch_bounds__(256) void wgrad_wide_kernel(
   };
 
   const T* gc = g + (int64_t)c * M * Cout + co_lo + col;
-  const T* yc = yv + (int64_t)c * M * Cout + co_lo + col;
+  const T* yc = DYM ? gc : yv + (int64_t)c * M * Cout + co_lo + col;
   const T* xc = x + (int64_t)c * Nb * H * W * Cin + ci0;
   uint4 rg[NI], ry[NI], rx[NI];
   uint32_t dvalid = 0, avalid = 0;
@@ -335,7 +336,7 @@ __global__ __launch_bounds__(256) void wgrad_wide_kernel(
       if (p < p_end) {
         dvalid |= 1u << it;
         rg[it] = *reinterpret_cast<const uint4*>(gc + (int64_t)p * Cout);
-        ry[it] = *reinterpret_cast<const uint4*>(yc + (int64_t)p * Cout);
+        if (!DYM) ry[it] = *reinterpret_cast<const uint4*>(yc + (int64_t)p * Cout);
         if (kval) {
           const int n = fdiv(p, HWo, inv_hw), r = p - n * HWo;
           const int oh = fdiv(r, Wo, inv_w), ow = r - oh * Wo;
@@ -352,13 +353,17 @@ __global__ __launch_bounds__(256) void wgrad_wide_kernel(
 #pragma unroll
     for (int it = 0; it < NI; ++it) {
       const int pp = pp0 + RPI * it;
-      float gf[V], yf[V], d[V];
-      P::unpack(rg[it], gf);
-      P::unpack(ry[it], yf);
       const bool live = (dvalid >> it) & 1u;   // pixels past the chunk: dy = 0 (not γ)
+      if (DYM) {
+        P::st_chunk(dyL + pp * LD + col, rg[it]);   // zero-filled when not live
+      } else {
+        float gf[V], yf[V], d[V];
+        P::unpack(rg[it], gf);
+        P::unpack(ry[it], yf);
 #pragma unroll
-      for (int j = 0; j < V; ++j) d[j] = live ? ca[j] * gf[j] + cb[j] * yf[j] + cc[j] : 0.f;
-      P::st_chunk(dyL + pp * LD + col, P::pack(d));
+        for (int j = 0; j < V; ++j) d[j] = live ? ca[j] * gf[j] + cb[j] * yf[j] + cc[j] : 0.f;
+        P::st_chunk(dyL + pp * LD + col, P::pack(d));
+      }
       uint4 v = rx[it];   // out-of-image taps / past-K columns stay 0 (zero padding, not relu(shift))
       if (PRO && ((avalid >> it) & 1u)) {
         float f[V];
@@ -484,6 +489,7 @@ static int conv_wgrad(const typename P::T* g, const typename P::T* yv, const flo
       return wgrad_wide<P>(g, yv, alpha, beta, gamma, x, ps, pt, garena, ldw, woff, C, Nb, H, W, Cin, Ho, Wo, Cout, KH,
                            KW, stride, pad, cin_src, dw, nimg, stream);
   }
+  if (!yv) return -7;   // a materialised dy is only consumed by the wide kernel
   const int co_slice = Cout > 256 ? 128 : Cout;   // wide layers: 128-channel dy slices
   if (Cout % co_slice != 0) return -3;
   const int K = KH * KW * Cin;

@@ -204,6 +204,13 @@ def block_out(y, s, t, r, rs, rt, out, C, per_client, Ch, nimg=None, per_img=0):
     _check(rc, "fa_block_out")
 
 
+def dy_apply(g, y, alpha, beta, gamma, out, C, per_client, Ch, nimg=None, per_img=0):
+    """out = α·g + β·y + γ (the folded BN backward operand, materialised) over the valid images."""
+    rc = _fnp("fa_dy_apply", g)(_p(g), _p(y), _p(alpha), _p(beta), _p(gamma), _p(out), _i(C), _i64(per_client), _i(Ch),
+                            _p(nimg), _i(per_img), _stream(g))
+    _check(rc, "fa_dy_apply")
+
+
 def avgpool(x, pooled, CN, HW, Ch, nimg=None, N=1):
     rc = _fnp("fa_avgpool", x)(_p(x), _p(pooled), _i(CN), _i(HW), _i(Ch), _p(nimg), _i(N), _stream(x))
     _check(rc, "fa_avgpool")

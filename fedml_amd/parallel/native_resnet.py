@@ -151,6 +151,7 @@ class NativeResNetStep:
         self.use_c3 = os.environ.get("FEDML_AMD_CONV3X3", "1") != "0"
         self.use_c1 = os.environ.get("FEDML_AMD_CONV1X1", "1") != "0"
         self.use_c1f = os.environ.get("FEDML_AMD_C1_FUSED", "1") != "0"
+        self.use_dym = os.environ.get("FEDML_AMD_DY_MATERIALIZE", "1") != "0"
         self.dump = None   # debug: list collecting (name, tensor clone) of every backward gradient buffer
         self._nimg = None
 
@@ -232,6 +233,9 @@ class NativeResNetStep:
         # gradient scratch: block-output g (kept until the block's conv0 is done), two ping-pong
         # buffers for the inner chain, one for the shortcut gradient
         self.gbuf = [torch.zeros(C * N * maxel, dtype=bf, device=dev) for _ in range(4)]
+        # materialised dy of the wide layers (one tensor for their bwd-data AND weight-gradient kernels)
+        self.dybuf = torch.zeros(C * N * maxel, dtype=bf, device=dev) if any(
+            self._dym(cv) for cv in self._all_convs()) else None
         # per-BN vectors: scale, shift, mean, rstd, alpha, beta, gamma, pivot   + stats
         # (pivot: the per-channel shift K the producing conv subtracts from its stored output — the
         # previous step's batch mean — so activations and BN sums stay centred; see bn_fwd_finalize)
@@ -278,7 +282,7 @@ class NativeResNetStep:
 
     # Every geometry keeps its own buffers alive: a captured HIP graph of one batch size must stay
     # valid while another batch size (the ragged last step of an epoch) is being run.
-    _STATE_ATTRS = ("x_in", "stem_y", "stem_out", "gbuf", "bn_vec", "stats", "stat_views", "pooled", "dw_scratch",
+    _STATE_ATTRS = ("x_in", "stem_y", "stem_out", "gbuf", "dybuf", "bn_vec", "stats", "stat_views", "pooled", "dw_scratch",
                     "dw_c3", "c3_segs", "c3_nseg", "c3_maxn", "_c3_off",
                     "packed", "packed_ld", "_segs", "_nseg", "_pack_tiles", "_pack_taps", "final_hw", "geom")
 
@@ -320,12 +324,33 @@ class NativeResNetStep:
         if self.dump is not None:
             self.dump.append((name, t.reshape(-1)[:n].clone()))
 
+    def _dym(self, cv: ConvSpec):
+        """Wide layers whose weight gradient runs on the 128×128 kernel (wgrad_kernels.hip wgrad_wide): their
+        folded BN backward operand is materialised once (dy_apply) and read by both backward kernels."""
+        if not self.use_dym or cv is self.stem[0] or self._c3(cv):
+            return False
+        K = cv.k * cv.k * cv.cin_pad
+        return cv.cout % 128 == 0 and (K >= 256 or cv.cout > 256) and not (
+            self.use_c1 and cv.cin == cv.cin_pad and nn_ops.conv1x1_wgrad_supported(cv.cin, cv.cout, cv.k, cv.stride,
+                                                                                    cv.pad))
+
+    def _dy(self, cv, g, y, v, N):
+        """(operand, y, α, β, γ) for the backward kernels of ``cv``: the materialised dy for wide layers."""
+        if not self._dym(cv):
+            return g, y, v[4], v[5], v[6]
+        nn_ops.dy_apply(g, y, v[4], v[5], v[6], self.dybuf, self.C, N * cv.Ho * cv.Wo * cv.cout, cv.cout,
+                        nimg=self._nimg, per_img=cv.Ho * cv.Wo * cv.cout)
+        return self.dybuf, None, None, None, None
+
     def _c3(self, cv: ConvSpec):
         return self.use_c3 and nn_ops.conv3x3_supported(cv.cin_pad, cv.cout, cv.k, cv.stride, cv.pad, cv.H, cv.W)
 
     def _wgrad(self, cv: ConvSpec, g, y, vec, x, pro_vec, garena, N):
-        """Weight gradient of conv ``cv`` (dy from (g, y, α β γ), x the conv input with an optional
-        BN+ReLU prologue) accumulated into the arena: tiled 3×3 / 1×1 kernels when they apply."""
+        """Weight gradient of conv ``cv`` (dy from (g, y, α β γ) — ``vec`` indexable with [4..6] or an
+        (α, β, γ) triple; y None: g is the materialised dy —, x the conv input with an optional BN+ReLU
+        prologue) accumulated into the arena: tiled 3×3 / 1×1 kernels when they apply."""
+        if isinstance(vec, tuple):
+            vec = (None, None, None, None) + vec
         C = self.C
         ps = pro_vec[0] if pro_vec is not None else None
         pt = pro_vec[1] if pro_vec is not None else None
@@ -509,7 +534,8 @@ class NativeResNetStep:
                     g_j = out_g
                     self._dump(f"{cv.key}.dx", out_g, C * N * cv.H * cv.W * cv.cin)
                     continue
-                self._wgrad(cv, g_j, b.ys[j], v, b.ys[j - 1], pv, garena, N)
+                dg, dyv, al, be, ga = self._dy(cv, g_j, b.ys[j], v, N)
+                self._wgrad(cv, dg, dyv, (al, be, ga), b.ys[j - 1], pv, garena, N)
                 if self._c3(cv):
                     nn_ops.conv3x3_bwd_data(g_j, b.ys[j], v[4], v[5], v[6], self.packed.view(-1)[cv.off_b:],
                                             self.packed_ld, out_g, b.ys[j - 1], pv[0], pv[1],
@@ -519,7 +545,7 @@ class NativeResNetStep:
                     g_j = out_g
                     self._dump(f"{cv.key}.dx", out_g, C * N * cv.H * cv.W * cv.cin)
                     continue
-                nn_ops.conv_bwd_data(g_j, b.ys[j], v[4], v[5], v[6], self.packed.view(-1)[cv.off_b:],
+                nn_ops.conv_bwd_data(dg, dyv, al, be, ga, self.packed.view(-1)[cv.off_b:],
                                      self.packed_ld, out_g, nn_ops.EPI_MASK, b.ys[j - 1], pv[0], pv[1], None, None,
                                      None, self.stat_views[b.bns[j - 1].key][1], C, N, cv.Ho, cv.Wo, cv.cout,
                                      cv.cin_pad, cv.k, cv.k, cv.stride, cv.pad, cv.H, cv.W, cv.ldk2,
@@ -532,8 +558,9 @@ class NativeResNetStep:
             if b.ds_conv is not None:
                 d = b.ds_conv
                 vd = self.bn_vec[b.ds_bn.key]
-                self._wgrad(d, gpre, b.yd, vd, b.act_in, None, garena, N)
-                nn_ops.conv_bwd_data(gpre, b.yd, vd[4], vd[5], vd[6], self.packed.view(-1)[d.off_b:], self.packed_ld,
+                dg, dyv, al, be, ga = self._dy(d, gpre, b.yd, vd, N)
+                self._wgrad(d, dg, dyv, (al, be, ga), b.act_in, None, garena, N)
+                nn_ops.conv_bwd_data(dg, dyv, al, be, ga, self.packed.view(-1)[d.off_b:], self.packed_ld,
                                      gadd, nn_ops.EPI_STORE, None, None, None, None, None, None, self.stats, C, N,
                                      d.Ho, d.Wo, d.cout, d.cin_pad, d.k, d.k, d.stride, d.pad, d.H, d.W, d.ldk2,
                                      self._tiles_per_wave(N * d.H * d.W), nimg=self._nimg)
@@ -544,8 +571,10 @@ class NativeResNetStep:
             cv0, bn0 = b.convs[0], b.bns[0]
             v = self.bn_vec[bn0.key]
             fused0 = self._c1f(cv0, nn_ops.EPI_BLOCK)
+            dg0, dyv0, al0, be0, ga0 = (g_j, b.ys[0], v[4], v[5], v[6]) if fused0 else \
+                self._dy(cv0, g_j, b.ys[0], v, N)
             if not fused0:
-                self._wgrad(cv0, g_j, b.ys[0], v, b.act_in, None, garena, N)
+                self._wgrad(cv0, dg0, dyv0, (al0, be0, ga0), b.act_in, None, garena, N)
             if prev_block is not None:
                 ey1, ey2 = prev_block.ys[-1], prev_block.yd
                 pstats = self.stat_views[prev_block.bns[-1].key][1]
@@ -566,7 +595,7 @@ class NativeResNetStep:
                 gpre = out_buf
                 self._dump(f"{cv0.key}.dx", out_buf, C * N * cv0.H * cv0.W * cv0.cin)
                 continue
-            nn_ops.conv_bwd_data(g_j, b.ys[0], v[4], v[5], v[6], self.packed.view(-1)[cv0.off_b:], self.packed_ld,
+            nn_ops.conv_bwd_data(dg0, dyv0, al0, be0, ga0, self.packed.view(-1)[cv0.off_b:], self.packed_ld,
                                  out_buf, nn_ops.EPI_BLOCK, b.act_in, None, None, shortcut, ey1, ey2, pstats, C, N,
                                  cv0.Ho, cv0.Wo, cv0.cout, cv0.cin_pad, cv0.k, cv0.k, cv0.stride, cv0.pad, cv0.H,
                                  cv0.W, cv0.ldk2, self._tiles_per_wave(N * cv0.H * cv0.W), nimg=self._nimg)
