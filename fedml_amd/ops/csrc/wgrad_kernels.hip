@@ -482,7 +482,7 @@ static int conv_wgrad(const typename P::T* g, const typename P::T* yv, const flo
     static int mode = -1;
     if (mode < 0) {
       const char* e = getenv("FEDML_AMD_WGRAD_WIDE");
-      mode = e ? atoi(e) : 1;
+      mode = e ? atoi(e) : 2;   // measured: +1.8 % on the fp32 headline (downsample convs)
     }
     const int K = KH * KW * Cin;
     if (Cout % 128 == 0 && ((mode == 1 && (K >= 256 || Cout > 256)) || mode == 2))

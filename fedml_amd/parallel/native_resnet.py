@@ -152,6 +152,7 @@ class NativeResNetStep:
         self.use_c1 = os.environ.get("FEDML_AMD_CONV1X1", "1") != "0"
         self.use_c1f = os.environ.get("FEDML_AMD_C1_FUSED", "1") != "0"
         self.use_dym = os.environ.get("FEDML_AMD_DY_MATERIALIZE", "1") != "0"
+        self.use_s2k = os.environ.get("FEDML_AMD_C3S2_CONVK", "1") == "1"   # measured +2 % (fp32 headline)
         self.dump = None   # debug: list collecting (name, tensor clone) of every backward gradient buffer
         self._nimg = None
 
@@ -329,8 +330,7 @@ class NativeResNetStep:
         folded BN backward operand is materialised once (dy_apply) and read by both backward kernels."""
         if not self.use_dym or cv is self.stem[0] or self._c3(cv):
             return False
-        K = cv.k * cv.k * cv.cin_pad
-        return cv.cout % 128 == 0 and (K >= 256 or cv.cout > 256) and not (
+        return cv.cout % 128 == 0 and not (
             self.use_c1 and cv.cin == cv.cin_pad and nn_ops.conv1x1_wgrad_supported(cv.cin, cv.cout, cv.k, cv.stride,
                                                                                     cv.pad))
 
@@ -341,6 +341,11 @@ class NativeResNetStep:
         nn_ops.dy_apply(g, y, v[4], v[5], v[6], self.dybuf, self.C, N * cv.Ho * cv.Wo * cv.cout, cv.cout,
                         nimg=self._nimg, per_img=cv.Ho * cv.Wo * cv.cout)
         return self.dybuf, None, None, None, None
+
+    def _s2k(self, cv: ConvSpec):
+        """Stride-2 3×3 backward-data with ≥ 64 channels: the parity-class GEMMs of the K-streamed kernel
+        (conv_kernels.hip MODE_BWDS2) instead of the 3×3 tile kernel, which runs all 9 taps."""
+        return self.use_s2k and cv.k == 3 and cv.stride == 2 and cv.cin_pad % 64 == 0 and cv.cout % 64 == 0
 
     def _c3(self, cv: ConvSpec):
         return self.use_c3 and nn_ops.conv3x3_supported(cv.cin_pad, cv.cout, cv.k, cv.stride, cv.pad, cv.H, cv.W)
@@ -536,7 +541,7 @@ class NativeResNetStep:
                     continue
                 dg, dyv, al, be, ga = self._dy(cv, g_j, b.ys[j], v, N)
                 self._wgrad(cv, dg, dyv, (al, be, ga), b.ys[j - 1], pv, garena, N)
-                if self._c3(cv):
+                if self._c3(cv) and not self._s2k(cv):
                     nn_ops.conv3x3_bwd_data(g_j, b.ys[j], v[4], v[5], v[6], self.packed.view(-1)[cv.off_b:],
                                             self.packed_ld, out_g, b.ys[j - 1], pv[0], pv[1],
                                             self.stat_views[b.bns[j - 1].key][1], C, N, cv.H, cv.W, cv.cout,
