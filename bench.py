@@ -38,6 +38,8 @@ def parse():
     p.add_argument("--model", default="resnet56")
     p.add_argument("--dataset", default="cifar100")
     p.add_argument("--dtype", default="fp32", help="fp32 (the reference's training precision) | bf16")
+    p.add_argument("--fp32-mma", default="exact", help="fp32 conv products: exact (v_mfma_f32_16x16x4_f32) | "
+                   "bf16x3 (split-bf16 matrix cores, ~16-bit products, fp32 storage/accumulation)")
     p.add_argument("--lr", type=float, default=0.001)
     p.add_argument("--profile-rounds", type=int, default=0)
     p.add_argument("--optimizer", default="FedAvg", help="FedAvg | FedOpt (server Adam)")
@@ -91,6 +93,7 @@ def main():
         "client_num_per_round": a.clients, "comm_round": a.steps, "epochs": a.epochs,
         "batch_size": a.batch_size, "client_optimizer": a.client_optimizer, "learning_rate": a.lr, "weight_decay": 0.001,
         "frequency_of_the_test": 0, "compute_dtype": a.dtype if use_gpu else "fp32", "random_seed": 0,
+        "fp32_mma": a.fp32_mma,
     }})
     torch.manual_seed(0)
     model = create(args, spec.num_classes)
@@ -160,6 +163,7 @@ def main():
                             and a.clients == DEFAULT_CLIENTS.get(a.preset) and a.partition == "homo"
                             and a.dtype == "fp32" else None),
             "dtype": a.dtype if use_gpu else "fp32",
+            "fp32_mma": (a.fp32_mma if use_gpu and a.dtype == "fp32" else None),
             "data": f"synthetic ({a.dataset}-shaped {tuple(spec.shape)}, class-conditional), random-init weights",
             "config": {"model": a.model, "dataset": a.dataset, "clients": a.clients,
                        "samples_per_client": a.samples_per_client, "global_batch": a.batch_size * a.clients,

@@ -103,7 +103,11 @@ FA_EXPORT int fa_bn_bwd_finalize(const float* bstats, int NS, int q_gy, int C, i
 // ---- fused block output: out = relu(y·s + t + R), R = yd·sd + td (downsample) | x (identity) | 0
 // One 16-B vector (P::VEC channels) per thread (no grid-stride loop, no 64-bit modulo); the
 // per-channel vectors are read as float4 (L1-resident). Streams 3 tensors: HBM-bound by construction.
-template <class P, int RES>  // RES 0: no residual, 1: identity, 2: downsample-BN residual
+// UNR 16-B vectors per thread, 256 apart (coalesced), all loads issued before any math: ≥ 3 streams × UNR
+// outstanding 16-B requests per lane keep HBM busy (one vector per thread reached ~2.6 TB/s on MI355X).
+constexpr int kEwUnr = 4;
+
+template <class P, int RES>
 __global__ __launch_bounds__(256) void block_out_kernel(const typename P::T* __restrict__ y, const float* __restrict__ s,
                                                         const float* __restrict__ t,
                                                         const typename P::T* __restrict__ r,
@@ -112,31 +116,44 @@ __global__ __launch_bounds__(256) void block_out_kernel(const typename P::T* __r
                                                         const int* __restrict__ nimg, int vec_per_img) {
   constexpr int V = P::VEC;
   const int c = blockIdx.y;
-  const int v = blockIdx.x * 256 + threadIdx.x;
-  if (v >= (nimg ? min(nvec, nimg[c] * vec_per_img) : nvec)) return;   // valid images of client c only
-  const int64_t base = (int64_t)c * nvec * V + (int64_t)v * V;
-  const int ch0 = (v % cg) * V;
-  const int64_t co = (int64_t)c * cg * V + ch0;
-  const uint4 yv = *reinterpret_cast<const uint4*>(y + base);
-  uint4 rv = make_uint4(0, 0, 0, 0);
-  if (RES) rv = *reinterpret_cast<const uint4*>(r + base);
-  float f[V], g[V];
-  P::unpack(yv, f);
+  const int lim = nimg ? min(nvec, nimg[c] * vec_per_img) : nvec;   // valid images of client c only
+  const int v0 = blockIdx.x * (256 * kEwUnr) + threadIdx.x;
+  if (v0 >= lim) return;
+  const int64_t cbase = (int64_t)c * nvec * V;
+  uint4 yv[kEwUnr], rv[kEwUnr];
 #pragma unroll
-  for (int j = 0; j < V; ++j) f[j] = f[j] * s[co + j] + t[co + j];
-  if (RES) {
-    P::unpack(rv, g);
-    if (RES == 2) {
-#pragma unroll
-      for (int j = 0; j < V; ++j) f[j] += g[j] * rs[co + j] + rt[co + j];
-    } else {
-#pragma unroll
-      for (int j = 0; j < V; ++j) f[j] += g[j];
+  for (int u = 0; u < kEwUnr; ++u) {
+    const int v = v0 + u * 256;
+    yv[u] = make_uint4(0, 0, 0, 0);
+    rv[u] = make_uint4(0, 0, 0, 0);
+    if (v < lim) {
+      yv[u] = *reinterpret_cast<const uint4*>(y + cbase + (int64_t)v * V);
+      if (RES) rv[u] = *reinterpret_cast<const uint4*>(r + cbase + (int64_t)v * V);
     }
   }
 #pragma unroll
-  for (int j = 0; j < V; ++j) f[j] = fmaxf(f[j], 0.f);
-  *reinterpret_cast<uint4*>(out + base) = P::pack(f);
+  for (int u = 0; u < kEwUnr; ++u) {
+    const int v = v0 + u * 256;
+    if (v >= lim) break;
+    const int64_t co = (int64_t)c * cg * V + (v % cg) * V;
+    float f[V], g[V];
+    P::unpack(yv[u], f);
+#pragma unroll
+    for (int j = 0; j < V; ++j) f[j] = f[j] * s[co + j] + t[co + j];
+    if (RES) {
+      P::unpack(rv[u], g);
+      if (RES == 2) {
+#pragma unroll
+        for (int j = 0; j < V; ++j) f[j] += g[j] * rs[co + j] + rt[co + j];
+      } else {
+#pragma unroll
+        for (int j = 0; j < V; ++j) f[j] += g[j];
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < V; ++j) f[j] = fmaxf(f[j], 0.f);
+    *reinterpret_cast<uint4*>(out + cbase + (int64_t)v * V) = P::pack(f);
+  }
 }
 
 template <class P>
@@ -145,9 +162,9 @@ static int block_out(const void* y, const float* s, const float* t, const void* 
                      hipStream_t stream) {
   using T = typename P::T;
   constexpr int V = P::VEC;
-  if (Ch % V != 0 || per_client / V > INT32_MAX) return -3;
+  if (Ch % V != 0 || per_client / V > INT32_MAX - 256 * kEwUnr) return -3;
   const int nvec = (int)(per_client / V);
-  dim3 grid((nvec + 255) / 256, C);
+  dim3 grid((nvec + 256 * kEwUnr - 1) / (256 * kEwUnr), C);
   const T* y_ = (const T*)y;
   const T* r_ = (const T*)r;
   T* o_ = (T*)out;
@@ -186,16 +203,32 @@ __global__ __launch_bounds__(256) void dy_apply_kernel(const typename P::T* __re
                                                        const int* __restrict__ nimg, int vec_per_img) {
   constexpr int V = P::VEC;
   const int c = blockIdx.y;
-  const int v = blockIdx.x * 256 + threadIdx.x;
-  if (v >= (nimg ? min(nvec, nimg[c] * vec_per_img) : nvec)) return;
-  const int64_t base = (int64_t)c * nvec * V + (int64_t)v * V;
-  const int64_t co = (int64_t)c * cg * V + (v % cg) * V;
-  float f[V], h[V];
-  P::unpack(*reinterpret_cast<const uint4*>(g + base), f);
-  P::unpack(*reinterpret_cast<const uint4*>(y + base), h);
+  const int lim = nimg ? min(nvec, nimg[c] * vec_per_img) : nvec;
+  const int v0 = blockIdx.x * (256 * kEwUnr) + threadIdx.x;
+  if (v0 >= lim) return;
+  const int64_t cbase = (int64_t)c * nvec * V;
+  uint4 gv[kEwUnr], yv[kEwUnr];
 #pragma unroll
-  for (int j = 0; j < V; ++j) f[j] = a[co + j] * f[j] + b[co + j] * h[j] + cg_[co + j];
-  *reinterpret_cast<uint4*>(out + base) = P::pack(f);
+  for (int u = 0; u < kEwUnr; ++u) {
+    const int v = v0 + u * 256;
+    gv[u] = yv[u] = make_uint4(0, 0, 0, 0);
+    if (v < lim) {
+      gv[u] = *reinterpret_cast<const uint4*>(g + cbase + (int64_t)v * V);
+      yv[u] = *reinterpret_cast<const uint4*>(y + cbase + (int64_t)v * V);
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kEwUnr; ++u) {
+    const int v = v0 + u * 256;
+    if (v >= lim) break;
+    const int64_t co = (int64_t)c * cg * V + (v % cg) * V;
+    float f[V], h[V];
+    P::unpack(gv[u], f);
+    P::unpack(yv[u], h);
+#pragma unroll
+    for (int j = 0; j < V; ++j) f[j] = a[co + j] * f[j] + b[co + j] * h[j] + cg_[co + j];
+    *reinterpret_cast<uint4*>(out + cbase + (int64_t)v * V) = P::pack(f);
+  }
 }
 
 template <class P>
@@ -203,10 +236,10 @@ static int dy_apply(const void* g, const void* y, const float* a, const float* b
                     int64_t per_client, int Ch, const int* nimg, int per_img, hipStream_t stream) {
   using T = typename P::T;
   constexpr int V = P::VEC;
-  if (Ch % V != 0 || per_client / V > INT32_MAX) return -3;
+  if (Ch % V != 0 || per_client / V > INT32_MAX - 256 * kEwUnr) return -3;
   const int nvec = (int)(per_client / V);
-  hipLaunchKernelGGL(dy_apply_kernel<P>, dim3((nvec + 255) / 256, C), dim3(256), 0, stream, (const T*)g, (const T*)y,
-                     a, b, cc, (T*)out, nvec, Ch / V, nimg, per_img / V);
+  hipLaunchKernelGGL(dy_apply_kernel<P>, dim3((nvec + 256 * kEwUnr - 1) / (256 * kEwUnr), C), dim3(256), 0, stream,
+                     (const T*)g, (const T*)y, a, b, cc, (T*)out, nvec, Ch / V, nimg, per_img / V);
   return (int)hipGetLastError();
 }
 

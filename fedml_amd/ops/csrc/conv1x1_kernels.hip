@@ -16,6 +16,7 @@ namespace c1 {
 
 using prec::BF16;
 using prec::F32;
+using prec::F32X3;
 
 // WM × WN waves tile the (COUT/16) × (CIN/16) output tiles; WK = 4/(WM·WN) waves split the pixels.
 template <class P, int CIN, int COUT, int PRO, int WM, int WN, int PT>
@@ -253,8 +254,8 @@ FA_EXPORT int fa_conv1x1_wgrad_f32(const float* g, const float* yv, const float*
                                    const float* gamma, const float* x, const float* ps, const float* pt, float* garena,
                                    int64_t ldw, int64_t woff, int C, int M, int Cin, int Cout, int pix_per_wg,
                                    const int* nimg, int hw, hipStream_t stream) {
-  return conv1x1_wgrad<c1::F32>(g, yv, alpha, beta, gamma, x, ps, pt, garena, ldw, woff, C, M, Cin, Cout, pix_per_wg,
-                                nimg, hw, stream);
+  FA_F32_DISPATCH(c1, conv1x1_wgrad<PX>(g, yv, alpha, beta, gamma, x, ps, pt, garena, ldw, woff, C, M, Cin, Cout, pix_per_wg,
+                                nimg, hw, stream));
 }
 
 // ============================================================================================
@@ -278,6 +279,7 @@ FA_EXPORT int fa_conv1x1_wgrad_f32(const float* g, const float* yv, const float*
 namespace c1f {
 using prec::BF16;
 using prec::F32;
+using prec::F32X3;
 
 struct Args {             // activations are P::T (bf16 | fp32)
   const void* g;          // [C][M][CO]
@@ -727,7 +729,7 @@ FA_EXPORT int fa_conv1x1_bwd_fused_f32(const float* g, const float* y, const flo
                                        const float* e_y2, float* out, float* stats, int NS, float* garena,
                                        int64_t ldw, int64_t woff, int C, int M, int Cin, int Cout, int epi,
                                        int pix_per_wg, float* part, const int* nimg, int hw, hipStream_t stream) {
-  return c1f::bwd_fused<c1f::F32>(g, y, alpha, beta, gamma, wb, wb_ld, ldk2, e_x, e_s, e_t, e_add, e_y1, e_y2, out,
+  FA_F32_DISPATCH(c1f, c1f::bwd_fused<PX>(g, y, alpha, beta, gamma, wb, wb_ld, ldk2, e_x, e_s, e_t, e_add, e_y1, e_y2, out,
                                   stats, NS, garena, ldw, woff, C, M, Cin, Cout, epi, pix_per_wg, part, nimg, hw,
-                                  stream);
+                                  stream));
 }

@@ -31,6 +31,7 @@ namespace c3 {
 
 using prec::BF16;
 using prec::F32;
+using prec::F32X3;
 
 enum { XF_NONE = 0, XF_BNRELU = 1, XF_DY = 2 };
 enum { EPI_FWD = 0, EPI_MASK = 2 };
@@ -870,8 +871,8 @@ FA_EXPORT int fa_conv3x3_fwd_f32(const float* x, const float* wpk, int64_t wpk_l
                                  const float* pshift, float* y, float* stats, int C, int N, int H, int W, int Cin,
                                  int Cout, int ldk, int stride, const float* pivot, const int* nimg,
                                  hipStream_t stream) {
-  return c3::conv3x3_fwd<c3::F32>(x, wpk, wpk_ld, pscale, pshift, y, stats, C, N, H, W, Cin, Cout, ldk, stride,
-                                  pivot, nimg, stream);
+  FA_F32_DISPATCH(c3, c3::conv3x3_fwd<PX>(x, wpk, wpk_ld, pscale, pshift, y, stats, C, N, H, W, Cin, Cout, ldk, stride,
+                                  pivot, nimg, stream));
 }
 
 // backward-data 3×3 / pad 1 / stride 1|2 with the ReLU-mask epilogue (EPI_MASK of the generic kernel):
@@ -890,8 +891,8 @@ FA_EXPORT int fa_conv3x3_bwd_data_f32(const float* g, const float* yv, const flo
                                       const float* e_x, const float* e_s, const float* e_t, float* stats, int C, int N,
                                       int Hx, int Wx, int Cout, int Cin, int ldk2, int stride, const int* nimg,
                                       hipStream_t stream) {
-  return c3::conv3x3_bwd_data<c3::F32>(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, dx, e_x, e_s, e_t, stats, C, N, Hx,
-                                       Wx, Cout, Cin, ldk2, stride, nimg, stream);
+  FA_F32_DISPATCH(c3, c3::conv3x3_bwd_data<PX>(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, dx, e_x, e_s, e_t, stats, C, N, Hx,
+                                       Wx, Cout, Cin, ldk2, stride, nimg, stream));
 }
 
 // weight gradient 3×3 / pad 1 / stride 1|2 into the GEMM-layout scratch `dw` [C][Cout][9·Cin] (zero
@@ -908,6 +909,6 @@ FA_EXPORT int fa_conv3x3_wgrad_f32(const float* g, const float* yv, const float*
                                    const float* gamma, const float* x, const float* ps, const float* pt, float* dw,
                                    int C, int N, int H, int W, int Cin, int Cout, int stride, const int* nimg,
                                    hipStream_t stream) {
-  return c3::conv3x3_wgrad<c3::F32>(g, yv, alpha, beta, gamma, x, ps, pt, dw, C, N, H, W, Cin, Cout, stride, nimg,
-                                    stream);
+  FA_F32_DISPATCH(c3, c3::conv3x3_wgrad<PX>(g, yv, alpha, beta, gamma, x, ps, pt, dw, C, N, H, W, Cin, Cout, stride, nimg,
+                                    stream));
 }

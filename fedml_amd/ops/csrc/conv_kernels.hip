@@ -24,6 +24,7 @@
 
 using prec::BF16;
 using prec::F32;
+using prec::F32X3;
 
 enum { PRO_NONE = 0, PRO_BNRELU = 1 };
 enum { EPI_FWD = 0, EPI_STORE = 1, EPI_MASK = 2, EPI_BLOCK = 3 };
@@ -981,8 +982,8 @@ FA_EXPORT int fa_conv_fwd_f32(const float* x, const float* wpk, int64_t wpk_ld, 
                               const float* pshift, float* y, float* stats, int C, int Nb, int H, int W, int Cin,
                               int Cout, int KH, int KW, int stride, int pad, int Ho, int Wo, int ldk,
                               int tiles_per_wave, const float* pivot, const int* nimg, hipStream_t stream) {
-  return conv_fwd<F32>(x, wpk, wpk_ld, pscale, pshift, y, stats, C, Nb, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo,
-                       ldk, tiles_per_wave, pivot, nimg, stream);
+  FA_F32_DISPATCH(prec, conv_fwd<PX>(x, wpk, wpk_ld, pscale, pshift, y, stats, C, Nb, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo,
+                       ldk, tiles_per_wave, pivot, nimg, stream));
 }
 
 // backward-data: dx = convᵀ(α·g + β·y + γ) with epilogue
@@ -1005,7 +1006,15 @@ FA_EXPORT int fa_conv_bwd_data_f32(const float* g, const float* yv, const float*
                                    const float* e_y1, const float* e_y2, float* stats, int C, int Nb, int Hy,
                                    int Wy, int Cout, int Cin, int KH, int KW, int stride, int pad, int Hx, int Wx,
                                    int ldk2, int tiles_per_wave, const int* nimg, hipStream_t stream) {
-  return conv_bwd_data<F32>(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, dx, epi, e_x, e_s, e_t, e_add, e_y1, e_y2,
+  FA_F32_DISPATCH(prec, conv_bwd_data<PX>(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, dx, epi, e_x, e_s, e_t, e_add, e_y1, e_y2,
                             stats, C, Nb, Hy, Wy, Cout, Cin, KH, KW, stride, pad, Hx, Wx, ldk2, tiles_per_wave, nimg,
-                            stream);
+                            stream));
+}
+
+// fp32 matrix-core mode of every `_f32` conv launcher (prec.h): 0 exact v_mfma_f32_16x16x4_f32,
+// 1 split-bf16 (three v_mfma_f32_16x16x32_bf16 per fragment). Returns the previous mode.
+FA_EXPORT int fa_set_f32_mma_mode(int mode) {
+  const int prev = prec::f32_mma_mode();
+  prec::f32_mma_mode() = mode ? 1 : 0;
+  return prev;
 }

@@ -171,4 +171,58 @@ struct F32 {
   static constexpr int pitch_tr(int ch) { return ch + 2; }
 };
 
+// fp32 storage, products on the bf16 matrix cores as a three-term split (Ootomo & Yokota style):
+//   a = a_hi + a_lo,  a_hi = bf16(a),  a_lo = bf16(a − a_hi)     (same for b)
+//   a·b ≈ a_lo·b_hi + a_hi·b_lo + a_hi·b_hi                         (a_lo·b_lo, ~2⁻¹⁸ relative, dropped)
+// Each product keeps ~16 significant bits (relative error ≲ 2⁻¹⁶ ≈ 1.5e-5 per product, fp32 accumulation):
+// ~8 bits more than TF32 — what cuDNN uses for "fp32" convolutions by default (torch.backends.cudnn.allow_tf32)
+// — and 3 v_mfma_f32_16x16x32_bf16 instead of 8 v_mfma_f32_16x16x4_f32 per 8-element fragment
+// (≈ 5× the matrix throughput). Storage, epilogues, statistics and everything outside the MFMA stay fp32.
+// The split is done once per fragment load, so operand reuse across the wave's tile amortises it.
+struct F32X3 : F32 {
+  struct frag_t {
+    bf16x8v hi, lo;
+  };
+  static __device__ __forceinline__ frag_t split(const f32x8v& f) {
+    frag_t s;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const __bf16 h = (__bf16)f[j];
+      s.hi[j] = h;
+      s.lo[j] = (__bf16)(f[j] - (float)h);
+    }
+    return s;
+  }
+  static __device__ __forceinline__ frag_t frag(const T* p) { return split(F32::frag(p)); }
+  static __device__ __forceinline__ frag_t frag_px(const T* a, int step) { return split(F32::frag_px(a, step)); }
+  static __device__ __forceinline__ frag_t frag_tr(const T* tile, int ld, int row0, int col0, int lane) {
+    return split(F32::frag_tr(tile, ld, row0, col0, lane));
+  }
+  static __device__ __forceinline__ frag_t frag_a8(const T* p) { return split(F32::frag_a8(p)); }
+  static __device__ __forceinline__ frag_t frag8(const float* f) { return split(F32::frag8(f)); }
+  static __device__ __forceinline__ f32x4 mma(const frag_t& a, const frag_t& b, f32x4 c) {
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.lo, b.hi, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.lo, c, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.hi, c, 0, 0, 0);
+  }
+};
+
+// fp32 matrix-core mode of the `_f32` entry points: 0 = exact (F32), 1 = split bf16 (F32X3). One flag per
+// process (inline function → a single COMDAT object across the kernel translation units).
+inline int& f32_mma_mode() {
+  static int mode = 0;
+  return mode;
+}
+
 }  // namespace prec
+
+// dispatch an `_f32` launcher body on the fp32 matrix-core mode: EXPR uses the policy name PX
+#define FA_F32_DISPATCH(NS, EXPR)                   \
+  do {                                              \
+    if (prec::f32_mma_mode() == 1) {                \
+      using PX = NS::F32X3;                         \
+      return EXPR;                                  \
+    }                                               \
+    using PX = NS::F32;                             \
+    return EXPR;                                    \
+  } while (0)

@@ -20,6 +20,7 @@
 
 using prec::BF16;
 using prec::F32;
+using prec::F32X3;
 
 // One workgroup = (client c, pixel chunk, K-slice z). The K-slice keeps the per-wave output
 // tile count ≤ 16 (≤ 64 accumulator registers) and means each workgroup only stages the im2col
@@ -546,8 +547,8 @@ FA_EXPORT int fa_conv_wgrad_f32(const float* g, const float* yv, const float* al
                                 int64_t ldw, int64_t woff, int C, int Nb, int H, int W, int Cin, int Ho, int Wo,
                                 int Cout, int KH, int KW, int stride, int pad, int pix_per_wg, int cin_src, float* dw,
                                 const int* nimg, hipStream_t stream) {
-  return conv_wgrad<F32>(g, yv, alpha, beta, gamma, x, ps, pt, garena, ldw, woff, C, Nb, H, W, Cin, Ho, Wo, Cout, KH,
-                         KW, stride, pad, pix_per_wg, cin_src, dw, nimg, stream);
+  FA_F32_DISPATCH(prec, conv_wgrad<PX>(g, yv, alpha, beta, gamma, x, ps, pt, garena, ldw, woff, C, Nb, H, W, Cin, Ho, Wo, Cout, KH,
+                         KW, stride, pad, pix_per_wg, cin_src, dw, nimg, stream));
 }
 
 // scatter a GEMM-layout dW scratch [C][Cout][taps·Cin] into the OIHW arena (+=) and clear it

@@ -30,6 +30,21 @@ def _fnp(name, t):
     return _fn(name)
 
 
+F32_MMA_MODES = {"exact": 0, "bf16x3": 1}
+
+
+def set_f32_mma_mode(mode: str) -> str:
+    """Matrix-core mode of the fp32 (``_f32``) conv launchers, process-wide (``csrc/prec.h``):
+    ``exact`` — v_mfma_f32_16x16x4_f32 (bit-faithful fp32 products); ``bf16x3`` — each fp32 operand split
+    into bf16 hi + lo and multiplied with three v_mfma_f32_16x16x32_bf16 (≈16-bit products, fp32 storage and
+    accumulation; more precise than the TF32 convolutions cuDNN runs for fp32 by default). Returns the
+    previous mode. Kernels captured into a HIP graph keep the mode they were captured with."""
+    if mode not in F32_MMA_MODES:
+        raise ValueError(f"fp32_mma {mode!r}: expected one of {sorted(F32_MMA_MODES)}")
+    prev = int(_fn("fa_set_f32_mma_mode")(_i(F32_MMA_MODES[mode])))
+    return {v: k for k, v in F32_MMA_MODES.items()}[prev]
+
+
 class PackSeg(ctypes.Structure):
     _fields_ = [("src_off", ctypes.c_int64), ("dst_f", ctypes.c_int64), ("dst_b", ctypes.c_int64),
                 ("cout", ctypes.c_int), ("cin", ctypes.c_int), ("kh", ctypes.c_int), ("kw", ctypes.c_int),

@@ -161,6 +161,10 @@ class ClientBatchEngine:
             from ...parallel.native_resnet import NativeResNetStep, UnsupportedNative
             # the native kernels run at the requested precision: fp32 (compute_dtype None / fp32, the
             # reference's) or bf16; any other dtype keeps the torch path, which honours it
+            self.fp32_mma = str(getattr(args, "fp32_mma", "exact") or "exact")
+            if (self.compute_dtype or torch.float32) == torch.float32:
+                from ...ops import nn_ops
+                nn_ops.set_f32_mma_mode(self.fp32_mma)
             try:
                 self.native_step = NativeResNetStep(model, self.layout, self.C, self.device,
                                                     dtype=self.compute_dtype or torch.float32)

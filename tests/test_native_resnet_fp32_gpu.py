@@ -17,8 +17,30 @@ DEV = "cuda"
 F32 = torch.float32
 
 
+# Every test runs under both fp32 matrix-core modes (csrc/prec.h): exact v_mfma_f32_16x16x4_f32 products,
+# and the split-bf16 mode (three bf16 MFMAs per fragment, ~2^-16 relative per product). Kernel checks
+# stated as "< 1e-5" hold at 1e-5 for exact and at 1e-4 for bf16x3 (TOL scales every relative error).
+# Whole-step / multi-round checks are dominated by ReLU-mask flips at the threshold (see
+# test_native_step_f32_matches_reference); ~2^-16 products flip more of them than exact fp32 does, so
+# those bounds are 3x wider under bf16x3 (bf16 storage is at 2-4e-1 on the same checks).
+TOL = {"exact": 1.0, "bf16x3": 10.0}
+STEP_TOL = {"exact": 1.0, "bf16x3": 3.0}
+_mode = ["exact"]
+
+
+@pytest.fixture(autouse=True, params=["exact", "bf16x3"])
+def f32_mma(request):
+    from fedml_amd.ops import nn_ops
+    _mode[0] = request.param
+    nn_ops.set_f32_mma_mode(request.param)
+    yield request.param
+    nn_ops.set_f32_mma_mode("exact")
+    _mode[0] = "exact"
+
+
 def rel(a, b):
-    return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
+    err = float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
+    return err / TOL[_mode[0]]
 
 
 @pytest.mark.parametrize("ch,hw,stride", [(16, 32, 1), (32, 16, 1), (64, 8, 1), (32, 32, 2), (64, 16, 2), (32, 16, 2),
@@ -240,7 +262,7 @@ def test_native_step_f32_matches_reference(builder, hw):
     torch.cuda.synchronize()
     assert step.packed.dtype == F32 and step.x_in.dtype == F32
     ref_loss, ref64 = _reference_grads(model, layout, flat.cpu().double(), x.cpu(), y.cpu(), torch.float64, "cpu")
-    assert abs(loss - ref_loss) / ref_loss < 1e-5, (loss, ref_loss)
+    assert abs(loss - ref_loss) / ref_loss < 1e-5 * TOL[_mode[0]], (loss, ref_loss)
     bad = []
     for s in layout.slots:
         if not s.trainable:
@@ -248,7 +270,7 @@ def test_native_step_f32_matches_reference(builder, hw):
         sl = slice(s.offset, s.offset + s.numel)
         r = ref64[:, sl]
         err = float((garena[:, sl].double() - r).norm() / r.norm().clamp_min(1e-30))
-        if err > 1e-2:
+        if err > 1e-2 * STEP_TOL[_mode[0]]:
             bad.append((s.key, err))
     assert not bad, bad[:8]
     s = layout.slot("bn1.running_mean")
@@ -287,7 +309,7 @@ def _reference_fedavg(model, x, y, K, n, bs, lr, rounds, device=DEV):
 
 
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
-def test_fedavg_resnet56_loss_curve_tracks_fp32_torch(dtype):
+def test_fedavg_resnet56_loss_curve_tracks_fp32_torch(dtype, f32_mma):
     """10 FedAvg rounds of ResNet-56 / CIFAR-100-shaped synthetic data through the RCCL simulator (native
     HIP step, HIP graphs, on-GPU aggregation) against the reference's fp32 training loop run by PyTorch on
     the GPU. Training amplifies last-bit differences (ReLU masks at the threshold, see above), so the
@@ -298,6 +320,8 @@ def test_fedavg_resnet56_loss_curve_tracks_fp32_torch(dtype):
     from fedml_amd.data.synthetic import get_spec
     from fedml_amd.simulation.rccl.client_store import DeviceClientStore
     from fedml_amd.simulation.rccl.simulator import RCCLSimulator
+    if dtype == "bf16" and f32_mma != "exact":
+        pytest.skip("the fp32 matrix-core mode does not apply to bf16 storage")
     torch.manual_seed(0)
     K, n, bs, lr, rounds = 4, 64, 32, 0.02, 10
     spec = get_spec("cifar100")
@@ -308,7 +332,7 @@ def test_fedavg_resnet56_loss_curve_tracks_fp32_torch(dtype):
         "training_type": "simulation", "backend": "RCCL", "federated_optimizer": "FedAvg", "dataset": "cifar100",
         "model": "resnet56", "client_num_in_total": K, "client_num_per_round": K, "comm_round": rounds,
         "epochs": 1, "batch_size": bs, "client_optimizer": "sgd", "learning_rate": lr, "shuffle": False,
-        "frequency_of_the_test": 0, "compute_dtype": dtype, "random_seed": 0}})
+        "frequency_of_the_test": 0, "compute_dtype": dtype, "random_seed": 0, "fp32_mma": f32_mma}})
     sim = RCCLSimulator(args, torch.device(DEV), None, copy.deepcopy(model), store=store)
     assert sim.engine.native_step is not None
     assert sim.engine.native_step.dtype == (F32 if dtype == "fp32" else torch.bfloat16)
@@ -319,7 +343,7 @@ def test_fedavg_resnet56_loss_curve_tracks_fp32_torch(dtype):
     if dtype == "fp32":
         cpu = _reference_fedavg(model, store.x_all, store.y_all, K, n, bs, lr, rounds, device="cpu")
         spread = max(abs(a - b) / b for a, b in zip(cpu, ref))
-        assert dev < max(3 * spread, 5e-3), (dev, spread, list(zip(got, ref, cpu)))
+        assert dev < max(3 * spread, 5e-3) * STEP_TOL[f32_mma], (dev, spread, list(zip(got, ref, cpu)))
     else:
         assert dev < 0.05, (dev, list(zip(got, ref)))
     assert got[-1] < got[0] - 0.1      # it learns
@@ -366,11 +390,11 @@ def test_native_step_heterogeneous_counts(dtype, tol):
             if s.key in sd:
                 r = sd[s.key].reshape(-1)
                 err = float((g[s.offset:s.offset + s.numel].cpu().double() - r).norm() / r.norm().clamp_min(1e-30))
-                assert err < tol, (c, s.key, err)
+                assert err < tol * (STEP_TOL[_mode[0]] if dtype == torch.float32 else 1.0), (c, s.key, err)
         rm = layout.slot("bn1.running_mean")
         assert torch.allclose(arena[c, rm.offset:rm.offset + rm.numel].cpu().double(),
                               m.bn1.running_mean, rtol=1e-3 if dtype == torch.float32 else 5e-2, atol=1e-4)
-    assert abs(loss - ref_loss) / ref_loss < (1e-5 if dtype == torch.float32 else 2e-2)
+    assert abs(loss - ref_loss) / ref_loss < (1e-5 * TOL[_mode[0]] if dtype == torch.float32 else 2e-2)
 
 
 def test_engine_heterogeneous_partition_stays_native():
