@@ -20,6 +20,7 @@ from fedml_amd.ops import nn_ops
 from fedml_amd.parallel.native_resnet import NativeResNetStep
 
 REC = []
+ES = [2]           # bytes per activation element (bf16 2, fp32 4)
 ENABLED = [False]
 
 
@@ -41,21 +42,21 @@ def _wrap(name, cost):
 
 def c_fwd(x, wpk, ld, ps, pt, y, st, C, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, ldk, tpw):
     return (f"{KH}x{KW} {Cin}->{Cout} s{stride} @{H}" + (" +bnrelu" if ps is not None else ""),
-            C * N * (H * W * Cin + Ho * Wo * Cout) * 2, 2 * C * N * Ho * Wo * Cout * KH * KW * Cin)
+            C * N * (H * W * Cin + Ho * Wo * Cout) * ES[0], 2 * C * N * Ho * Wo * Cout * KH * KW * Cin)
 
 
 def c_bwd(g, y, al, be, ga, wpk, ld, dx, epi, ex, es, et, eadd, ey1, ey2, st, C, N, Hy, Wy, Cout, Cin, KH, KW, stride,
           pad, Hx, Wx, ldk2, tpw):
     extra = {1: 0, 2: 1, 3: 3 + (ey2 is not None)}[epi]
     return (f"{KH}x{KW} {Cin}<-{Cout} s{stride} @{Hx} epi{epi}",
-            C * N * (2 * Hy * Wy * Cout + (1 + extra) * Hx * Wx * Cin) * 2,
+            C * N * (2 * Hy * Wy * Cout + (1 + extra) * Hx * Wx * Cin) * ES[0],
             2 * C * N * Hx * Wx * Cin * KH * KW * Cout)
 
 
 def c_wgrad(g, y, al, be, ga, x, ps, pt, garena, woff, C, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ppw, cs,
             scratch):
     return (f"{KH}x{KW} {Cin}->{Cout} s{stride} @{H}" + (" +bnrelu" if ps is not None else ""),
-            C * N * (2 * Ho * Wo * Cout + H * W * Cin) * 2, 2 * C * N * Ho * Wo * Cout * KH * KW * Cin)
+            C * N * (2 * Ho * Wo * Cout + H * W * Cin) * ES[0], 2 * C * N * Ho * Wo * Cout * KH * KW * Cin)
 
 
 def c3_fwd(x, wpk, ld, ps, pt, y, st, C, N, H, W, Cin, Cout, ldk, stride=1):
@@ -73,18 +74,18 @@ def c3_wgrad(g, y, al, be, ga, x, ps, pt, garena, woff, C, N, H, W, Cin, Cout, c
 
 
 def c1_wgrad(g, y, al, be, ga, x, ps, pt, garena, woff, C, M, Cin, Cout, ppw):
-    return (f"1x1 {Cin}->{Cout} M{M}" + (" +bnrelu" if ps is not None else ""), C * M * (2 * Cout + Cin) * 2,
+    return (f"1x1 {Cin}->{Cout} M{M}" + (" +bnrelu" if ps is not None else ""), C * M * (2 * Cout + Cin) * ES[0],
             2 * C * M * Cout * Cin)
 
 
 def c1_fused(g, y, al, be, ga, wpk, ld, ldk2, ex, es, et, eadd, ey1, ey2, out, st, garena, woff, C, M, Cin, Cout,
              epi, ppw):
     extra = 0 if epi == 2 else 2 + (ey2 is not None)
-    return (f"1x1 {Cin}<-{Cout} M{M} epi{epi}", C * M * (2 * Cout + (2 + extra) * Cin) * 2, 4 * C * M * Cout * Cin)
+    return (f"1x1 {Cin}<-{Cout} M{M} epi{epi}", C * M * (2 * Cout + (2 + extra) * Cin) * ES[0], 4 * C * M * Cout * Cin)
 
 
 def c_block(y, s, t, r, rs, rt, out, C, per, Ch):
-    return (f"ch{Ch} n{per // Ch}" + (" ds" if rs is not None else ""), C * per * 2 * (3 if r is not None else 2), 0)
+    return (f"ch{Ch} n{per // Ch}" + (" ds" if rs is not None else ""), C * per * ES[0] * (3 if r is not None else 2), 0)
 
 
 def c_other(*a):
@@ -97,7 +98,12 @@ def main():
     ap.add_argument("--N", type=int, default=64)
     ap.add_argument("--model", default="resnet56")
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--dtype", default="bf16", help="bf16 | fp32")
+    ap.add_argument("--fp32-mma", default="exact", help="exact | bf16x3")
     a = ap.parse_args()
+    dtype = {"bf16": torch.bfloat16, "fp32": torch.float32}[a.dtype]
+    ES[0] = 2 if dtype == torch.bfloat16 else 4
+    nn_ops.set_f32_mma_mode(a.fp32_mma)
     _wrap("conv_fwd", c_fwd)
     _wrap("conv_bwd_data", c_bwd)
     _wrap("conv_wgrad", c_wgrad)
@@ -120,7 +126,7 @@ def main():
     y = torch.randint(0, 100, (a.C, a.N), device=dev)
     rs = torch.full((a.C, a.N), 1.0 / a.N, device=dev)
     act = torch.ones(a.C, device=dev)
-    step = NativeResNetStep(model, layout, a.C, dev)
+    step = NativeResNetStep(model, layout, a.C, dev, dtype=dtype)
     for _ in range(2):
         step.step(arena, garena, x, y, rs, act)
     torch.cuda.synchronize()
@@ -144,7 +150,7 @@ def main():
         d[3] += fl
     rows = sorted(agg.items(), key=lambda kv: -kv[1][1])
     by_op = collections.Counter()
-    print(f"step time {total_ms:.2f} ms  (C={a.C}, N={a.N}, {a.model}); per-step numbers below")
+    print(f"step time {total_ms:.2f} ms  (C={a.C}, N={a.N}, {a.model}, {a.dtype}, fp32_mma {a.fp32_mma}); per-step")
     print(f"{'op':16s} {'geometry':34s} {'calls':>5s} {'ms':>8s} {'us/call':>8s} {'GB/s':>7s} {'TF/s':>6s}")
     for (name, label), (n, ms, nb, fl) in rows:
         ms_s = ms / a.steps
