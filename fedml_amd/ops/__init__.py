@@ -16,6 +16,7 @@ from .fl_ops import (
     sgd_step,
     adam_step,
     fedopt_step,
+    fednova_server_step,
     client_sqnorm,
     norm_diff_clip_,
     gaussian_noise_,

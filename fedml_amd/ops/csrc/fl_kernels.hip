@@ -321,6 +321,41 @@ FA_EXPORT int fa_fedopt_step(const float* X, int64_t ldx, int C, const float* w,
 }
 
 // =====================================================================================
+// K11  FedNova server step (`single_process/fednova/fednova_trainer.py` aggregate, Wang et al. 2020) on
+//      the all-reduced coefficient-weighted client sum wsum = Σ_i coef_i·w_i, coef_i = τ_eff·p_i / a_i,
+//      S = Σ_i coef_i (device scalar: no host sync):
+//        cum = S·g − wsum                 (τ_eff · Σ p_i (g − w_i)/a_i, the normalised cumulative update)
+//        gmf = 0:  g ← g − cum
+//        gmf > 0:  buf ← first ? cum/lr : gmf·buf + cum/lr;   g ← g − lr·buf   (server momentum)
+//      one pass over P instead of the reference's per-tensor loops.
+// =====================================================================================
+__global__ __launch_bounds__(256) void fednova_server_kernel(float* __restrict__ glob, const float* __restrict__ wsum,
+                                                             const float* __restrict__ S_ptr, float* __restrict__ buf,
+                                                             int64_t P, float gmf, float lr, int first) {
+  const float S = *S_ptr;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += stride) {
+    const float g = glob[i];
+    const float cum = S * g - wsum[i];
+    if (gmf != 0.f) {
+      const float b = first ? cum / lr : gmf * buf[i] + cum / lr;
+      buf[i] = b;
+      glob[i] = g - lr * b;
+    } else {
+      glob[i] = g - cum;
+    }
+  }
+}
+
+FA_EXPORT int fa_fednova_server_step(float* glob, const float* wsum, const float* S, float* buf, int64_t P, float gmf,
+                                     float lr, int first, hipStream_t stream) {
+  if (gmf != 0.f && (!buf || lr == 0.f)) return -1;
+  hipLaunchKernelGGL(fednova_server_kernel, dim3(fa_grid(P, 256, 2048)), dim3(256), 0, stream, glob, wsum, S, buf, P,
+                     gmf, lr, first);
+  return (int)hipGetLastError();
+}
+
+// =====================================================================================
 // K9  Robust aggregation (`core/robustness/robust_aggregation.py`)
 //   per-client squared L2 norm of (X_c - G) restricted to a mask of "weight" coordinates
 //   (BN running stats excluded, `is_weight_param`), deterministic two-level reduction:

@@ -196,6 +196,30 @@ _FEDOPT_IDS = {"sgd": 0, "fedavgm": 0, "adam": 1, "fedadam": 1, "yogi": 2, "fedy
                "fedadagrad": 3}
 
 
+def fednova_server_step(glob, wsum, S, buf=None, gmf=0.0, lr=1.0, first=False):
+    """FedNova server update in place on ``glob`` (flat fp32 [P]) from the all-reduced coefficient-weighted
+    client sum ``wsum`` [P] and ``S`` = Σ coef (a 1-element device tensor): cum = S·glob − wsum; glob −= cum,
+    or with server momentum ``gmf``: buf = (first ? 0 : gmf·buf) + cum/lr, glob −= lr·buf (csrc K11)."""
+    P = glob.numel()
+    if gmf and buf is None:
+        raise ValueError("fednova_server_step: gmf > 0 needs a momentum buffer")
+    if use_native(glob):
+        rc = _fn("fa_fednova_server_step")(_p(glob), _p(wsum), _p(S), _p(buf), _i64(P), _f(gmf), _f(lr),
+                                           _c.c_int(int(bool(first))), _stream(glob))
+        _check(rc, "fa_fednova_server_step")
+        return glob
+    cum = S.view(()) * glob - wsum
+    if gmf:
+        if first:
+            buf.copy_(cum / lr)
+        else:
+            buf.mul_(gmf).add_(cum, alpha=1.0 / lr)
+        glob.sub_(lr * buf)
+    else:
+        glob.sub_(cum)
+    return glob
+
+
 def fedopt_step(stack, w, glob, opt="sgd", lr=1.0, beta1=0.9, beta2=0.99, eps=1e-3, momentum=0.0, nesterov=False,
                 state1=None, state2=None, step=1, first_step=False):
     """Fused FedOpt server update: avg = Σ w_c stack_c; g = glob − avg; glob ← ServerOpt(glob, g)."""

@@ -101,7 +101,7 @@ class ClientBatchEngine:
         self.weight_decay = float(getattr(args, "weight_decay", 0.0) or 0.0)
         self.sgd_wd = bool(getattr(args, "sgd_weight_decay", False))
         self.mu = float(getattr(args, "fedprox_mu", getattr(args, "mu", 0.0)) or 0.0) if \
-            str(getattr(args, "federated_optimizer", "")) == "FedProx" else 0.0
+            str(getattr(args, "federated_optimizer", "")) in ("FedProx", "FedNova") else 0.0
         self.mom = self.layout.alloc_stack(self.C, self.device) if (opt == "sgd" and self.momentum) else None
         if opt != "sgd":
             self.m1 = self.layout.alloc_stack(self.C, self.device)

@@ -45,6 +45,23 @@ def _dtype(name):
     return table[name]
 
 
+def fednova_normalizer(tau: int, lr: float, momentum: float = 0.0, mu: float = 0.0):
+    """(a_i, τ_eff_i / p_i) of a client after ``tau`` local SGD steps — the counters of the FedNova local
+    optimizer (``trainers/fednova.py``, reference ``single_process/fednova/fednova.py:110-140``): with
+    momentum ρ each step adds the geometric counter 1 + ρ + … ; a proximal term μ damps the running sum by
+    (1 − lr·μ) per step; plain SGD counts steps. τ_eff_i is τ·p_i under a proximal term, else a_i·p_i."""
+    vec, counter, etamu = 0.0, 0.0, lr * mu
+    for _ in range(int(tau)):
+        if momentum:
+            counter = counter * momentum + 1.0
+            vec += counter
+        if etamu:
+            vec = vec * (1.0 - etamu) + 1.0
+        if not momentum and not etamu:
+            vec += 1.0
+    return vec, (float(tau) if mu else vec)
+
+
 class RCCLSimulator:
     def __init__(self, args, device, dataset, model, store: Optional[DeviceClientStore] = None, model_trainer=None):
         """``model_trainer`` (reference ``fedml.run_simulation(..., model_trainer)``): a functional trainer
@@ -88,6 +105,13 @@ class RCCLSimulator:
         self.server_opt = None
         if str(args.federated_optimizer) == "FedOpt":
             self.server_opt = _ServerOptState(args, self.layout.size, self.device)
+        # FedNova: normalised averaging (coefficients from each client's local step count) + optional server
+        # momentum gmf, applied by the fused K11 kernel on the all-reduced weighted sum
+        self.fednova = str(args.federated_optimizer) == "FedNova"
+        self.nova_gmf = float(getattr(args, "gmf", 0.0) or 0.0) if self.fednova else 0.0
+        self.nova_buf = torch.zeros(self.layout.size, dtype=torch.float32, device=self.device) \
+            if self.nova_gmf else None
+        self.nova_first = True
         self.round_times: List[float] = []
         # aggregation bucket (elements) for the pipelined weighted-sum + all-reduce of large models
         self.bucket_elems = max(256, int(float(getattr(args, "allreduce_bucket_mb", 32) or 32) * (1 << 20) / 4))
@@ -126,7 +150,7 @@ class RCCLSimulator:
         tr = tracer()
         args = self.args
         with tr.span("round.assign"):
-            _, mine = self.assignment(round_idx)
+            ids, mine = self.assignment(round_idx)
             slots = torch.full((self.C,), 0, dtype=torch.int64)
             valid = torch.zeros(self.C, dtype=torch.bool)
             for i, cid in enumerate(mine):
@@ -134,6 +158,9 @@ class RCCLSimulator:
                 valid[i] = True
             slots = slots.to(self.device)
             valid = valid.to(self.device)
+        if self.fednova and (self.compression or self.server_opt is not None or self.user_trainer is not None):
+            raise ValueError("FedNova on the RCCL simulator: compressed updates, a server optimizer or a user "
+                             "ClientTrainer are not supported")
         if self.residual is not None:
             with tr.span("round.residual_migrate"):
                 self.residual.migrate(self.round_owner)
@@ -150,7 +177,11 @@ class RCCLSimulator:
                                   float(args.learning_rate), generator=self.gen,
                                   shuffle=bool(getattr(args, "shuffle", True)), valid_slots=valid, rng_key=rng_key)
         with tr.gpu_span("round.aggregate", self.device):
-            w = torch.where(valid, self.store.counts[slots].to(torch.float32), torch.zeros(self.C, device=self.device))
+            if self.fednova:
+                w = self._fednova_coefficients(ids, mine)
+            else:
+                w = torch.where(valid, self.store.counts[slots].to(torch.float32),
+                                torch.zeros(self.C, device=self.device))
             if self.faults.active:
                 # lost uploads (dropout / missed deadline, core.fault): survivors are re-weighted
                 alive = self.faults.survivors(round_idx, mine)
@@ -184,6 +215,14 @@ class RCCLSimulator:
             else:
                 self.engine.partial_sum(w, out=self.partial)
                 comm.all_reduce_flat(self.partial)
+            if self.fednova:
+                # normalised update g − (S·g − Σ coef_i w_i) (+ server momentum), one fused pass
+                P = self.layout.size
+                ops.fednova_server_step(self.global_flat, self.partial[:P], self.partial[P:P + 1], self.nova_buf,
+                                        self.nova_gmf, float(args.learning_rate), self.nova_first)
+                self.nova_first = False
+                self._post_aggregate()
+                return
             total = self.partial[self.layout.size:self.layout.size + 1]
             avg = self.partial[:self.layout.size] / total.clamp_min(1e-12)
             if self.faults.active:   # every upload lost: the global model stays as it was
@@ -193,6 +232,25 @@ class RCCLSimulator:
             else:
                 self.global_flat.copy_(avg)
             self._post_aggregate()
+
+    def _fednova_coefficients(self, ids, mine):
+        """FedNova weights of this rank's slots: coef_i = τ_eff·p_i / a_i with p_i = n_i / Σn over the round's
+        sampled clients (all ranks — every rank computes the same host-side numbers, no communication) and
+        a_i from the client's local step count τ_i = epochs·⌈n_i / batch⌉ (``fednova_normalizer``)."""
+        a = self.args
+        lr, bs, ep = float(a.learning_rate), int(a.batch_size), int(a.epochs)
+        mom = self.engine.momentum if self.engine.optimizer == "sgd" else 0.0
+        mu = self.engine.mu
+        n_all = {int(c): int(self.sample_counts[int(c)]) for c in ids}
+        total = float(sum(n_all.values())) or 1.0
+        norm = {c: fednova_normalizer(ep * math.ceil(n / bs), lr, mom, mu) for c, n in n_all.items()}
+        tau_eff = sum((n_all[c] / total) * norm[c][1] for c in n_all)
+        coef = torch.zeros(self.C, dtype=torch.float32)
+        for i, cid in enumerate(mine):
+            a_i = norm[int(cid)][0]
+            if a_i > 0:
+                coef[i] = tau_eff * (n_all[int(cid)] / total) / a_i
+        return coef.to(self.device)
 
     def _train_user_trainer(self, mine):
         """Compatibility path for a non-functional ``ClientTrainer`` (reference client.py:27-47 call
@@ -325,6 +383,8 @@ class RCCLSimulator:
             clients = {"gen": self.gen.get_state()}
             if dense is not None:
                 clients["residual"] = dense.detach().cpu()
+            if self.nova_buf is not None and not self.nova_first:
+                clients["fednova_buf"] = self.nova_buf.detach().cpu()
             save_round_checkpoint(directory, self.round_idx, self.global_model_state(), self.args,
                                   server_opt=self.server_opt.state_dict() if self.server_opt else None,
                                   clients=clients)
@@ -336,6 +396,9 @@ class RCCLSimulator:
         if self.server_opt is not None and ck.get("server_opt") is not None:
             self.server_opt.load_state_dict(ck["server_opt"])
         cl = ck.get("clients") or {}
+        if cl.get("fednova_buf") is not None and self.nova_buf is not None:
+            self.nova_buf.copy_(cl["fednova_buf"].to(self.device))
+            self.nova_first = False
         if cl.get("gen") is not None and self.world == 1:
             self.gen.set_state(cl["gen"])
         if cl.get("residual") is not None and self.residual is not None:

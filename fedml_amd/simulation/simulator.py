@@ -106,7 +106,8 @@ class SimulatorRCCL:
     def __init__(self, args, device, dataset, model, model_trainer=None):
         from .rccl.simulator import RCCLSimulator
         if args.federated_optimizer not in (FedML_FEDERATED_OPTIMIZER_FEDAVG, FedML_FEDERATED_OPTIMIZER_FEDOPT,
-                                            FedML_FEDERATED_OPTIMIZER_FEDPROX, FedML_FEDERATED_OPTIMIZER_FEDAVG_ROBUST):
+                                            FedML_FEDERATED_OPTIMIZER_FEDPROX, FedML_FEDERATED_OPTIMIZER_FEDAVG_ROBUST,
+                                            FedML_FEDERATED_OPTIMIZER_FEDNOVA):
             logging.warning("RCCL simulator runs FedAvg-family optimizers; %s falls back to the SP simulator",
                             args.federated_optimizer)
             self.simulator = SimulatorSingleProcess(args, device, dataset, model, model_trainer)

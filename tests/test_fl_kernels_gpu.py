@@ -256,3 +256,23 @@ def test_adamw_writes_bf16_shadow():
     assert torch.equal(p, ref)
     assert torch.equal(shadow[0], p[0].to(torch.bfloat16)) and torch.equal(shadow[2], p[2].to(torch.bfloat16))
     assert (shadow[1] == 7.0).all()
+
+
+@pytest.mark.parametrize("gmf", [0.0, 0.5])
+def test_fednova_server_step(gmf):
+    """K11 fused FedNova server step against its fp32 torch reference (two rounds: momentum init + update)."""
+    torch.manual_seed(0)
+    P = 100_003
+    g = torch.randn(P, device=DEV)
+    buf = torch.zeros(P, device=DEV) if gmf else None
+    g_ref = g.cpu().clone()
+    buf_ref = torch.zeros(P) if gmf else None
+    for first in (True, False):
+        wsum = torch.randn(P, device=DEV)
+        S = torch.tensor([1.3], device=DEV)
+        ops.fednova_server_step(g, wsum, S, buf, gmf, 0.05, first)
+        ops.fednova_server_step(g_ref, wsum.cpu(), S.cpu(), buf_ref, gmf, 0.05, first)
+        torch.cuda.synchronize()
+        assert torch.allclose(g.cpu(), g_ref, rtol=1e-5, atol=1e-5)
+        if gmf:
+            assert torch.allclose(buf.cpu(), buf_ref, rtol=1e-5, atol=1e-4)
