@@ -64,6 +64,9 @@ def init(args=None, argv=None):
     MLOpsMetrics.get_instance(args)
     logging.info("args = %s", args.to_dict() if hasattr(args, "to_dict") else vars(args))
     _seed_everything(int(getattr(args, "random_seed", 0)))
+    if bool(getattr(args, "deterministic", False)):
+        from .utils import determinism
+        determinism.enable(args)
 
     if getattr(args, "enable_wandb", False):
         try:

@@ -17,8 +17,15 @@ _FORCE_TORCH = os.environ.get("FEDML_AMD_FORCE_TORCH", "0") == "1"
 _SIGS = {}
 
 
+_SC = None   # stream-ordering checker (core/tracing/stream_check.py) when installed
+
+
 def _p(t):
-    return None if t is None else _c.c_void_p(t.data_ptr())
+    if t is None:
+        return None
+    if _SC is not None and t.is_cuda:
+        _SC.pending(t)
+    return _c.c_void_p(t.data_ptr())
 
 
 def _stream(t):
@@ -46,6 +53,8 @@ _KERNEL_SYNC = os.environ.get("FEDML_AMD_KERNEL_SYNC", "0") == "1"
 
 
 def _check(rc, name):
+    if _SC is not None:
+        _SC.flush(name)
     if rc != 0:
         raise RuntimeError(f"{name} failed with HIP error {rc}")
     if _KERNEL_SYNC:

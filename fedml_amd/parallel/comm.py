@@ -32,6 +32,8 @@ def init_process_group(backend: Optional[str] = None, timeout_s: int = 1800, dev
         backend = os.environ.get("FEDML_AMD_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29500")
+    from ..utils import determinism
+    determinism.apply_env()     # deterministic mode: fixed RCCL algorithm / protocol
     kw = {}
     if backend == "nccl" and device is not None:
         kw["device_id"] = torch.device(device)

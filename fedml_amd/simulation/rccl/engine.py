@@ -156,8 +156,14 @@ class ClientBatchEngine:
         self.use_graphs = self.device.type == "cuda" and os.environ.get("FEDML_AMD_HIP_GRAPHS", "1") != "0"
         self.native = None
         self.native_step = None
+        from ...utils import determinism
+        self.deterministic = determinism.enabled(args)
+        if self.deterministic:
+            determinism.enable(args)
+        # deterministic mode: the native step's fp32-atomic BN statistics / split-K weight gradients are
+        # not bitwise reproducible, so it runs the batched torch path instead (utils/determinism.py)
         if self.device.type == "cuda" and not self.sequential and self.loss_name == "ce" and \
-                os.environ.get("FEDML_AMD_NATIVE_CONV", "1") != "0":
+                not self.deterministic and os.environ.get("FEDML_AMD_NATIVE_CONV", "1") != "0":
             from ...parallel.native_resnet import NativeResNetStep, UnsupportedNative
             # the native kernels run at the requested precision: fp32 (compute_dtype None / fp32, the
             # reference's) or bf16; any other dtype keeps the torch path, which honours it

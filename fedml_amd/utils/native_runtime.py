@@ -7,6 +7,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _PKG = os.path.dirname(_HERE)
 _SRC = os.path.join(_PKG, "csrc", "runtime.cpp")
+_SRCS = [_SRC, os.path.join(_PKG, "csrc", "stream_check.cpp")]
 _LIB = os.path.join(_PKG, "_native", "libfedml_runtime.so")
 _lock = threading.Lock()
 _lib = None
@@ -15,8 +16,8 @@ _tried = False
 
 def build_runtime(force: bool = False) -> str:
     os.makedirs(os.path.dirname(_LIB), exist_ok=True)
-    if force or not os.path.exists(_LIB) or os.path.getmtime(_LIB) < os.path.getmtime(_SRC):
-        cmd = ["g++", "-O3", "-std=c++17", "-shared", "-fPIC", "-pthread", _SRC, "-o", _LIB]
+    if force or not os.path.exists(_LIB) or os.path.getmtime(_LIB) < max(os.path.getmtime(f) for f in _SRCS):
+        cmd = ["g++", "-O3", "-std=c++17", "-shared", "-fPIC", "-pthread", *_SRCS, "-o", _LIB]
         subprocess.check_call(cmd)
     return _LIB
 
@@ -29,7 +30,7 @@ def runtime_lib():
             return _lib
         _tried = True
         try:
-            if not os.path.exists(_LIB) or os.path.getmtime(_LIB) < os.path.getmtime(_SRC):
+            if not os.path.exists(_LIB) or os.path.getmtime(_LIB) < max(os.path.getmtime(f) for f in _SRCS):
                 build_runtime()
             lib = ctypes.CDLL(_LIB)
         except Exception:
@@ -46,5 +47,16 @@ def runtime_lib():
         lib.fr_schedule.restype = c.c_double
         lib.fr_layout.argtypes = [c.c_int32, c.c_void_p, c.c_int32, c.c_int32, c.c_void_p]
         lib.fr_layout.restype = c.c_int64
+        lib.fr_sc_access.argtypes = [c.c_int64, c.c_int64, c.c_int32, c.c_int32, c.c_int32]
+        lib.fr_sc_wait.argtypes = [c.c_int32, c.c_int32]
+        lib.fr_sc_sync.argtypes = [c.c_int32]
+        lib.fr_sc_wait_epoch.argtypes = [c.c_int32, c.c_int32, c.c_int64]
+        lib.fr_sc_epoch.argtypes = [c.c_int32]
+        lib.fr_sc_epoch.restype = c.c_int64
+        lib.fr_sc_release.argtypes = [c.c_int64, c.c_int64]
+        lib.fr_sc_hazard_count.restype = c.c_int64
+        lib.fr_sc_access_count.restype = c.c_int64
+        lib.fr_sc_hazards.argtypes = [c.c_void_p, c.c_void_p, c.c_int64]
+        lib.fr_sc_hazards.restype = c.c_int64
         _lib = lib
         return _lib

@@ -16,6 +16,12 @@ int64_t fr_trace_copy(int64_t* ts, int32_t* ids, int32_t* phase, int64_t* tid, i
 double fr_schedule(int32_t n, const double* workloads, const double* mem_per_wl, int32_t m, const double* speed,
                    const double* memory, int32_t mode, int64_t node_budget, int32_t* out_assign);
 int64_t fr_layout(int32_t n, const int64_t* numel, int32_t elem_bytes, int32_t align, int64_t* out_offsets);
+void fr_sc_reset();
+void fr_sc_access(int64_t addr, int64_t nbytes, int32_t stream, int32_t write, int32_t tag);
+void fr_sc_wait(int32_t dst, int32_t src);
+void fr_sc_sync(int32_t stream);
+int64_t fr_sc_hazard_count();
+int64_t fr_sc_access_count();
 }
 
 #define CHECK(c)                                              \
@@ -81,6 +87,21 @@ int main() {
     end = off[i] + numel[i];
   }
   CHECK(total >= end);
+  // 4. stream checker fed from 8 host threads (each its own stream and buffers; a final unordered
+  //    cross-stream write per thread must be reported exactly once per thread)
+  fr_sc_reset();
+  {
+    std::vector<std::thread> sc;
+    for (int t = 0; t < 8; ++t)
+      sc.emplace_back([t] {
+        for (int i = 0; i < 2000; ++i) fr_sc_access(0x100000 * (t + 1) + 64 * (i % 50), 64, t, i & 1, 0);
+      });
+    for (auto& x : sc) x.join();
+  }
+  CHECK(fr_sc_hazard_count() == 0);
+  CHECK(fr_sc_access_count() == 8 * 2000);
+  for (int t = 0; t < 8; ++t) fr_sc_access(0x100000 * (t + 1), 64, 100 + t, 1, 1);
+  CHECK(fr_sc_hazard_count() == 8);
   std::printf("runtime stress ok: %lld trace events, 50 schedules, layout total %lld\n", (long long)n,
               (long long)total);
   return 0;

@@ -10,7 +10,8 @@ import pytest
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = [os.path.join(HERE, "native", "runtime_stress.cpp"),
-       os.path.join(os.path.dirname(HERE), "fedml_amd", "csrc", "runtime.cpp")]
+       os.path.join(os.path.dirname(HERE), "fedml_amd", "csrc", "runtime.cpp"),
+       os.path.join(os.path.dirname(HERE), "fedml_amd", "csrc", "stream_check.cpp")]
 
 
 @pytest.mark.parametrize("san", ["thread", "address,undefined"])
