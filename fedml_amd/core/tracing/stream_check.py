@@ -11,7 +11,8 @@
 * ``hazards()`` lists every access that touched a buffer whose last write (or, for a write, a read since)
   came from another stream with no ordering in between (RAW / WAW / WAR). ``assert_clean()`` raises on any.
 
-It is a debug tool (host bookkeeping per launch); captured graphs are checked at capture time.
+It is a debug tool (host bookkeeping per launch). Launches inside a HIP-graph capture are logged with the
+graph and checked on the replaying stream at every ``replay()``.
 """
 import ctypes
 import os
@@ -36,6 +37,10 @@ class StreamChecker:
         self._tag_names: List[str] = []
         self._pending = threading.local()
         self._event_epochs: Dict[int, tuple] = {}
+        # graph capture: launches are recorded into the graph's log (nothing executes yet) and reported on
+        # the replaying stream at each replay — the work's real position in stream order
+        self._capturing = None
+        self._graph_log: Dict[int, list] = {}
 
     # ---- identities ------------------------------------------------------------------------------
     def sid(self, stream) -> int:
@@ -93,8 +98,16 @@ class StreamChecker:
         if not lst:
             return
         self._pending.lst = []
+        if self._capturing is not None:
+            self._graph_log.setdefault(self._capturing, []).extend(
+                (t.data_ptr(), _span_bytes(t), name) for t in lst)
+            return
         for t in lst:
             self.tensor(t, write=True, tag=name)
+
+    def replay(self, graph, stream):
+        for addr, nb, name in self._graph_log.get(id(graph), ()):
+            self.access(addr, nb, stream, True, name)
 
     def discard(self):
         self._pending.lst = []
@@ -172,6 +185,23 @@ def install() -> StreamChecker:
 
         S.wait_stream, S.wait_event, E.record, S.synchronize = wait_stream, wait_event, record, ssync
         torch.cuda.synchronize = dsync
+        G = torch.cuda.CUDAGraph
+        _ORIG.update(cbegin=G.capture_begin, cend=G.capture_end, replay=G.replay)
+
+        def capture_begin(self, *a, **k):
+            chk._graph_log[id(self)] = []
+            chk._capturing = id(self)
+            return _ORIG["cbegin"](self, *a, **k)
+
+        def capture_end(self):
+            chk._capturing = None
+            return _ORIG["cend"](self)
+
+        def replay(self):
+            chk.replay(self, torch.cuda.current_stream())
+            return _ORIG["replay"](self)
+
+        G.capture_begin, G.capture_end, G.replay = capture_begin, capture_end, replay
     _CHECKER = chk
     return chk
 
@@ -186,6 +216,8 @@ def uninstall():
         S, E = torch.cuda.Stream, torch.cuda.Event
         S.wait_stream, S.wait_event, E.record = _ORIG["wait_stream"], _ORIG["wait_event"], _ORIG["record"]
         S.synchronize, torch.cuda.synchronize = _ORIG["ssync"], _ORIG["dsync"]
+        G = torch.cuda.CUDAGraph
+        G.capture_begin, G.capture_end, G.replay = _ORIG["cbegin"], _ORIG["cend"], _ORIG["replay"]
         _ORIG.clear()
     _CHECKER = None
 
