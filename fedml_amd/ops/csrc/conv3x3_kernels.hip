@@ -20,6 +20,7 @@
 // Every kernel is instantiated for bf16 and fp32 storage (prec.h); the fp32 instances are the
 // reference-precision path (exact fp32 MFMA products, fp32 activations).
 #include "prec.h"
+#include <algorithm>
 
 #include <cstdlib>
 
@@ -800,10 +801,14 @@ static int conv3x3_wgrad(const void* g, const void* yv, const float* alpha, cons
   // bf16 256: +2/+3/+6 % rounds/s at 50/25/13 clients per GPU, neutral at 100 (fewer fp32 atomics per
   // client); fp32 2048: the MFMA work per workgroup dominates the atomics (wgrad 0.72 → 0.54 ms at 16×32²,
   // profiles/r2_c3_sweep_fp32.txt)
-  static const int wgs = [] {
+  // fp32 scales with the clients on this GPU (~20 workgroups per client, 256..2048): at 13 clients (the
+  // 8-GPU share of the headline) 2048 workgroups spend the kernel on atomics — 256 cuts wgrad 2.16 → 1.67
+  // ms/step, while 100 clients still want 2048 (scripts/gpu_c3w_small_c.sh)
+  static const int wgs_env = [] {
     const char* e = getenv("FEDML_AMD_C3W_WGS");
-    return e ? atoi(e) : (P::kF32 ? 2048 : 256);
+    return e ? atoi(e) : 0;
   }();
+  const int wgs = wgs_env > 0 ? wgs_env : (P::kF32 ? std::min(2048, std::max(256, 20 * C)) : 256);
   const int CGX = Cin / P::VEC, CGD = Cout / P::VEC;
   constexpr int XMAX = P::kF32 ? 16 : 8;   // x-tile 16-B chunks per thread (fp32: twice the chunks per pixel)
   Plan p = make_plan(N, Ho, Wo, C, tpx, wgs);
