@@ -118,7 +118,13 @@ class ClientBatchEngine:
             self.interp = None
             self.sequential = True
             self.tf = None
-            if os.environ.get("FEDML_AMD_BATCHED_TRANSFORMER", "1") != "0":
+            # the client-batched transformer kernels compute in bf16 (fp32 masters); an fp32 run on the GPU
+            # keeps the per-client torch path, which honours fp32, instead of silently downgrading
+            tf_dtype_ok = self.device.type != "cuda" or compute_dtype == torch.bfloat16
+            if not tf_dtype_ok:
+                logging.warning("virtual-client engine: client-batched transformer kernels are bf16; compute_dtype "
+                                "%s runs the sequential per-client torch path", compute_dtype or "fp32")
+            if os.environ.get("FEDML_AMD_BATCHED_TRANSFORMER", "1") != "0" and tf_dtype_ok:
                 try:
                     self.tf = BatchedTransformer(model, self.C)
                     logging.info("virtual-client engine: client-batched transformer path (%s)", self.tf.kind)
