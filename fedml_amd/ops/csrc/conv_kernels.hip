@@ -663,10 +663,10 @@ __global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
           v = ra[j];
         }
       }
-      *reinterpret_cast<uint4*>(al + (row0 + CK::RPI * j) * LD + col * V) = v;
+      P::st_tile(al + (row0 + CK::RPI * j) * LD + col * V, col, v);
     }
 #pragma unroll
-    for (int j = 0; j < CK::NB; ++j) *reinterpret_cast<uint4*>(wl + (row0 + CK::RPI * j) * LD + col * V) = rb[j];
+    for (int j = 0; j < CK::NB; ++j) P::st_tile(wl + (row0 + CK::RPI * j) * LD + col * V, col, rb[j]);
   };
 
   const T* my_a = al + (wm * 16 * TM + (lane & 15)) * LD + 8 * (lane >> 4);
@@ -682,10 +682,10 @@ __global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
     for (int k0 = 0; k0 < kn; k0 += 32) {
       frag_t af[TM];
 #pragma unroll
-      for (int t = 0; t < TM; ++t) af[t] = P::frag(my_a + t * 16 * LD + k0);
+      for (int t = 0; t < TM; ++t) af[t] = P::frag_tile(my_a + t * 16 * LD + k0);
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
-        const frag_t bv = P::frag(my_b + nt * 16 * LD + k0);
+        const frag_t bv = P::frag_tile(my_b + nt * 16 * LD + k0);
 #pragma unroll
         for (int t = 0; t < TM; ++t) acc[t][nt] = P::mma(af[t], bv, acc[t][nt]);
       }

@@ -99,6 +99,10 @@ struct BF16 {
   static __device__ __forceinline__ f32x4 mma(const frag_t& a, const frag_t& b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
   }
+  // row-tile staging pair (K-streamed kernels): chunk `col` (16 B, K offset col·VEC from an 8-element-aligned
+  // row start) into the LDS tile, and the 8-element row fragment back out — identity layouts here
+  static __device__ __forceinline__ void st_tile(T* p, int, uint4 v) { *reinterpret_cast<uint4*>(p) = v; }
+  static __device__ __forceinline__ frag_t frag_tile(const T* p) { return frag(p); }
   // LDS row pitch (elements) of a [rows][ch] tile: 16-B aligned, bank-spread for the bf16 reads
   static constexpr int pitch(int ch) { return ch + 8; }
   // pitch of tiles read with frag_tr
@@ -166,6 +170,8 @@ struct F32 {
     for (int j = 0; j < 8; ++j) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], c, 0, 0, 0);
     return c;
   }
+  static __device__ __forceinline__ void st_tile(T* p, int, uint4 v) { *reinterpret_cast<uint4*>(p) = v; }
+  static __device__ __forceinline__ frag_t frag_tile(const T* p) { return frag(p); }
   static constexpr int pitch(int ch) { return ch + 4; }
   // ≡ 2 (mod 4) dwords: rows 8 apart (lane groups g and g + 1 of one frag_px read) are 16 banks apart
   static constexpr int pitch_tr(int ch) { return ch + 2; }
@@ -200,6 +206,28 @@ struct F32X3 : F32 {
   }
   static __device__ __forceinline__ frag_t frag_a8(const T* p) { return split(F32::frag_a8(p)); }
   static __device__ __forceinline__ frag_t frag8(const float* f) { return split(F32::frag8(f)); }
+  // pre-split row tiles: each 8-element K group (32 B, two chunks) is stored as [hi 0-7 | lo 0-7] bf16, so
+  // a fragment is two ds_read_b128 with no conversion; the split happens once per element at staging
+  // instead of once per fragment use
+  static __device__ __forceinline__ void st_tile(T* p, int col, uint4 v) {
+    char* g = reinterpret_cast<char*>(p - 4 * (col & 1)) + 8 * (col & 1);
+    const float f[4] = {__uint_as_float(v.x), __uint_as_float(v.y), __uint_as_float(v.z), __uint_as_float(v.w)};
+    uint16_t h[4], l[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const __bf16 b = (__bf16)f[j];
+      h[j] = __builtin_bit_cast(uint16_t, b);
+      l[j] = __builtin_bit_cast(uint16_t, (__bf16)(f[j] - (float)b));
+    }
+    *reinterpret_cast<uint2*>(g) = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
+    *reinterpret_cast<uint2*>(g + 16) = make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
+  }
+  static __device__ __forceinline__ frag_t frag_tile(const T* p) {
+    frag_t s;
+    s.hi = *reinterpret_cast<const bf16x8v*>(p);
+    s.lo = *reinterpret_cast<const bf16x8v*>(reinterpret_cast<const char*>(p) + 16);
+    return s;
+  }
   static __device__ __forceinline__ f32x4 mma(const frag_t& a, const frag_t& b, f32x4 c) {
     c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.lo, b.hi, c, 0, 0, 0);
     c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.lo, c, 0, 0, 0);
