@@ -682,10 +682,13 @@ template <class P, int KC, int NOUT_WG, int XF, int BWD, int EPI, int ST>
 static int launch_gemm(Args a, int nout, int C, int target_px, hipStream_t stream) {
   constexpr int MTW = NOUT_WG >= 64 ? 2 : 4;
   constexpr int CG = KC / P::VEC;
-  static const int wgs = [] {   // FEDML_AMD_C3G_WGS: workgroup target of the fwd / bwd-data kernels
+  static const int wgs_env = [] {   // FEDML_AMD_C3G_WGS: workgroup target of the fwd / bwd-data kernels
     const char* e = getenv("FEDML_AMD_C3G_WGS");
-    return e ? atoi(e) : 2048;
+    return e ? atoi(e) : 0;
   }();
+  // fp32: ~40 workgroups per client (512..2048): the 13-client share wants 512 (fwd 1.72 → 1.52, bwd-data
+  // 1.86 → 1.61 ms/step), 100 clients keep 2048 (scripts/gpu_c3g_small_c.sh)
+  const int wgs = wgs_env > 0 ? wgs_env : (P::kF32 ? std::min(2048, std::max(512, 40 * C)) : 2048);
   Plan p = make_plan(a.N, a.H, a.W, C, target_px, wgs);
   {  // a unit's tile must fit the loader's register budget (≤ 12 16-B chunks per thread)
     const bool f2 = !BWD && ST == 2;
