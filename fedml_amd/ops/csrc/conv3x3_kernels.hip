@@ -726,9 +726,25 @@ static int px_override() {
   return v;
 }
 
+// tuning override of the fp32 64-channel output slice per workgroup: FEDML_AMD_C3_N64=32 (default 16)
+static int n64_override() {
+  static const int v = [] {
+    const char* e = getenv("FEDML_AMD_C3_N64");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 template <class P, int XF, int BWD, int EPI, int ST>
 static int dispatch_gemm(int kc, int nout, const Args& a, int C, hipStream_t s) {
   if (kc != nout) return -2;
+  if constexpr (P::kF32) {
+    if (kc == 64 && n64_override() == 32) {
+      const int r = launch_gemm<P, 64, 32, XF, BWD, EPI, ST>(
+          a, nout, C, px_override() > 0 ? px_override() : (ST == 2 ? (BWD ? 256 : 64) : 128), s);
+      if (r != -5) return r;   // -5: the 32-channel fp32 weight slice does not fit LDS with this unit
+    }
+  }
   // fp32: half the output channels per workgroup on the 64-channel layers (the fp32 weight slice of
   // 32 channels alone would take 75 KB of LDS)
   constexpr int N64 = P::kF32 ? 16 : 32;
