@@ -18,7 +18,9 @@ def run(rank, world, port, out_path, model_name, clients, counts_seed, shuffle=F
     ds = "mnist" if model_name == "lr" else "cifar10"
     model_arg = "resnet56" if model_name == "resnet_shallow" else model_name
     args = Arguments.from_dict({"x": {
-        "training_type": "simulation", "backend": "RCCL", "federated_optimizer": "FedAvg", "dataset": ds,
+        "training_type": "simulation", "backend": "RCCL",
+        "federated_optimizer": os.environ.get("FEDML_TEST_OPTIMIZER", "FedAvg"), "dataset": ds,
+        "momentum": float(os.environ.get("FEDML_TEST_MOMENTUM", "0")), "gmf": float(os.environ.get("FEDML_TEST_GMF", "0")),
         "model": model_arg, "client_num_in_total": clients, "comm_round": 2,
         "epochs": 1, "batch_size": 8, "client_optimizer": "sgd", "learning_rate": 0.05, "frequency_of_the_test": 0,
         "random_seed": 0, "shuffle": shuffle, "data_augmentation": augment and ds == "cifar10",

@@ -61,6 +61,15 @@ def test_compressed_partial_participation_world_size_invariance(tmp_path, method
     assert float((w1 - w2).norm() / w1.norm()) < 1e-4
 
 
+def test_fednova_world_size_invariance(tmp_path):
+    """FedNova (unequal client sizes → unequal local steps, momentum + server momentum): every rank computes the
+    same normalising coefficients host-side, so 2 ranks equal 1 rank."""
+    env = dict(FEDML_TEST_OPTIMIZER="FedNova", FEDML_TEST_MOMENTUM="0.5", FEDML_TEST_GMF="0.5")
+    w1 = _launch(1, str(tmp_path / "w1.pt"), "lr", 7, True, **env)
+    w2 = _launch(2, str(tmp_path / "w2.pt"), "lr", 7, True, **env)
+    assert torch.allclose(w1, w2, atol=1e-5), float((w1 - w2).abs().max())
+
+
 def test_bucketed_aggregation_matches_single_rank(tmp_path):
     """The pipelined per-bucket weighted sum + async all-reduce (large-model path; here 0.01 MB buckets
     over the 7,850-parameter LR model → 3 buckets) equals the single-rank aggregate."""
