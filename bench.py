@@ -55,9 +55,9 @@ def parse():
                                     batch_size=64, lr=0.001),
         "distilbert_fedopt_32": dict(model="distilbert", dataset="text_cls", clients=32, samples_per_client=64,
                                      batch_size=16, lr=5e-5, optimizer="FedOpt", compression="int8",
-                                     client_optimizer="adamw", dtype="bf16"),
+                                     client_optimizer="adamw"),
         "vit_b16_32": dict(model="vit_b16", dataset="ILSVRC2012", clients=32, samples_per_client=32, batch_size=16,
-                           lr=1e-4, client_optimizer="adamw", dtype="bf16"),
+                           lr=1e-4, client_optimizer="adamw"),
     }
     pre, _ = p.parse_known_args()
     if pre.preset:   # a preset changes the defaults; flags given on the command line still win

@@ -10,23 +10,12 @@
 // MFMA 16x16x32 bf16 operand maps (gfx950): lane l holds A[row l&15][k 8(l>>4)..+7],
 // B[k 8(l>>4)..+7][col l&15]; C/D: col = l&15, row = 4(l>>4) + reg.
 #include "common.h"
+#include "dropout.h"
 
 typedef __bf16 bf16x8_mf __attribute__((ext_vector_type(8)));
 
 namespace {
 
-__device__ __forceinline__ uint32_t fmix32(uint32_t h) {
-  h ^= h >> 16;
-  h *= 0x85ebca6bu;
-  h ^= h >> 13;
-  h *= 0xc2b2ae35u;
-  h ^= h >> 16;
-  return h;
-}
-// dropout keep test shared by forward and backward (and mirrored in ops/transformer_ops.py)
-__device__ __forceinline__ bool drop_keep(uint32_t seed, uint32_t a, uint32_t b, uint32_t thr) {
-  return fmix32(fmix32(a ^ seed) + b * 0x9E3779B1u) >= thr;
-}
 
 __device__ __forceinline__ void unpack8(const uint4 u, float* f) {
   const uint32_t w[4] = {u.x, u.y, u.z, u.w};
@@ -69,7 +58,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const uint16_t* __restrict_
       unpack8(*(const uint4*)(h + (size_t)row * d + col), x[v]);
       if (thr) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) x[v][j] = drop_keep(seed, (uint32_t)row, (uint32_t)(col + j), thr) ? x[v][j] * dscale : 0.f;
+        for (int j = 0; j < 8; ++j) x[v][j] = fa_drop::keep(seed, (uint32_t)row, (uint32_t)(col + j), thr) ? x[v][j] * dscale : 0.f;
       }
       if (res) {
         float r8[8];
@@ -185,7 +174,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
           if (thr) {
 #pragma unroll
             for (int j = 0; j < 8; ++j)
-              o[j] = drop_keep(seed, (uint32_t)row, (uint32_t)(col + j), thr) ? o[j] * dscale : 0.f;
+              o[j] = fa_drop::keep(seed, (uint32_t)row, (uint32_t)(col + j), thr) ? o[j] * dscale : 0.f;
           }
           *(uint4*)(dh + row * d + col) = pack8(o);
         }
@@ -356,7 +345,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
       for (int r = 0; r < 4; ++r) {
         float p = m[r] == -INFINITY ? 0.f : exp2f(sc[nb][r] - m[r]);
         l[r] += p;
-        if (thr) p = drop_keep(seed, bh * 65536u + (uint32_t)(qbase + r), (uint32_t)key, thr) ? p * dscale : 0.f;
+        if (thr) p = fa_drop::keep(seed, bh * 65536u + (uint32_t)(qbase + r), (uint32_t)key, thr) ? p * dscale : 0.f;
         P[(4 * (lane >> 4) + r) * VST + key] = f32_to_bf16(p);
       }
     }
@@ -472,7 +461,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const uint16_t* __rest
       for (int r = 0; r < 4; ++r) {
         const float p = valid ? exp2f(s[r] * c2 - L[r]) : 0.f;
         float g = dp[r];
-        if (thr) g = drop_keep(seed, bh * 65536u + (uint32_t)(qbase + r), (uint32_t)key, thr) ? g * dscale : 0.f;
+        if (thr) g = fa_drop::keep(seed, bh * 65536u + (uint32_t)(qbase + r), (uint32_t)key, thr) ? g * dscale : 0.f;
         dS[(4 * (lane >> 4) + r) * KST + nb * 16 + (lane & 15)] = f32_to_bf16(p * (g - Dr[r]));
       }
     }
@@ -563,7 +552,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const uint16_t* __res
         const float p = valid ? exp2f(st[r] * c2 - Lq) : 0.f;
         float pd = p, g = dpt[r];
         if (thr) {
-          const bool kp = drop_keep(seed, bh * 65536u + (uint32_t)qq, (uint32_t)(kbase + r), thr);
+          const bool kp = fa_drop::keep(seed, bh * 65536u + (uint32_t)qq, (uint32_t)(kbase + r), thr);
           pd = kp ? p * dscale : 0.f;
           g = kp ? g * dscale : 0.f;
         }

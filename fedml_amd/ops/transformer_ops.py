@@ -6,9 +6,11 @@
 * :func:`attention` — softmax(q·kᵀ/√64 + key mask)·v per (row-group, head) for S ≤ 256 and head
   dim 64, with attention-probability dropout; q/k/v/o are token-major ``[CB·S, H·64]``.
 
-CUDA tensors run the kernels (bf16 in/out, fp32 statistics); CPU tensors run the plain-PyTorch
-fp32 reference of the same math — the same hash-based dropout mask included — which is also the
-oracle of ``tests/test_transformer_kernels_gpu.py``.
+CUDA tensors run the kernels at the tensor's storage precision: bf16 (``csrc/transformer_kernels.hip``,
+``bgemm_kernels.hip``) or fp32 — the reference's training precision — (``csrc/tf_f32_kernels.hip``:
+exact ``v_mfma_f32_16x16x4_f32`` products, or split-bf16 ones under ``fp32_mma: bf16x3``), fp32
+statistics either way. CPU tensors run the plain-PyTorch fp32 reference of the same math — the same
+hash-based dropout mask included — which is also the oracle of ``tests/test_transformer_kernels_gpu.py``.
 """
 import ctypes as _c
 import math
@@ -18,6 +20,14 @@ import torch
 from .fl_ops import _check, _f, _fn, _i64, _p, _stream, use_native
 
 _M32 = 0xFFFFFFFF
+
+
+def _sfx(t: torch.Tensor) -> str:
+    """Kernel-name suffix of a storage dtype: fp32 tensors run the ``_f32`` kernels."""
+    if t.dtype == torch.float32:
+        return "_f32"
+    assert t.dtype == torch.bfloat16, f"transformer kernels take bf16 or fp32, got {t.dtype}"
+    return ""
 
 
 def _thr(p: float) -> int:
@@ -41,22 +51,28 @@ def dropout_keep(seed: int, a: torch.Tensor, b: torch.Tensor, p: float) -> torch
 
 
 # ------------------------------------------------------------------------------------------- LN
+def _ct(t):
+    """Compute dtype of the references: fp32, or fp64 for fp64 inputs (the kernels' numerics oracle)."""
+    return torch.float64 if t.dtype == torch.float64 else torch.float32
+
+
 def _ln_ref(h, res, gamma, beta, eps, p, seed, rpc):
     R, d = h.shape
-    x = h.float()
+    ct = _ct(h)
+    x = h.to(ct)
     if p > 0:
         keep = dropout_keep(seed, torch.arange(R, device=h.device).view(R, 1),
                             torch.arange(d, device=h.device).view(1, d), p)
         x = torch.where(keep, x / (1.0 - p), torch.zeros_like(x))
     if res is not None:
-        x = x + res.float()
+        x = x + res.to(ct)
     if (res is not None or p > 0) and h.dtype == torch.bfloat16:
         x = x.to(torch.bfloat16).float()
     C = R // rpc
     xc = x.view(C, rpc, d)
     mu = xc.mean(-1, keepdim=True)
     var = ((xc - mu) ** 2).mean(-1, keepdim=True)
-    y = (xc - mu) * torch.rsqrt(var + eps) * gamma.view(C, 1, d).float() + beta.view(C, 1, d).float()
+    y = (xc - mu) * torch.rsqrt(var + eps) * gamma.view(C, 1, d).to(ct) + beta.view(C, 1, d).to(ct)
     return y.view(R, d).to(h.dtype)
 
 
@@ -71,10 +87,11 @@ class _LayerNorm(torch.autograd.Function):
         rstd = torch.empty(R, dtype=torch.float32, device=h.device)
         g = gamma.detach().float().contiguous()
         b = beta.detach().float().contiguous()
-        rc = _fn("fa_ln_fwd")(_p(h), _p(res), _c.c_int(R), _c.c_int(d), _c.c_int(rpc), _p(g), _p(b), _f(eps),
-                              _c.c_uint32(_thr(p)), _f(1.0 / (1.0 - p) if p > 0 else 1.0), _c.c_uint32(seed & _M32),
-                              _p(y), _p(xsum), _p(mean), _p(rstd), _p(seed_dev), _stream(h))
-        _check(rc, "fa_ln_fwd")
+        name = "fa_ln_fwd" + _sfx(h)
+        rc = _fn(name)(_p(h), _p(res), _c.c_int(R), _c.c_int(d), _c.c_int(rpc), _p(g), _p(b), _f(eps),
+                       _c.c_uint32(_thr(p)), _f(1.0 / (1.0 - p) if p > 0 else 1.0), _c.c_uint32(seed & _M32),
+                       _p(y), _p(xsum), _p(mean), _p(rstd), _p(seed_dev), _stream(h))
+        _check(rc, name)
         ctx.save_for_backward(xsum if fused else h, mean, rstd, g)
         ctx.cfg = (p, seed, rpc, res is not None, fused, gamma.dtype)
         ctx.seed_dev = seed_dev
@@ -87,15 +104,16 @@ class _LayerNorm(torch.autograd.Function):
         seed_dev = ctx.seed_dev
         R, d = x.shape
         C = R // rpc
-        dy = dy.contiguous()
+        dy = dy.to(x.dtype).contiguous()
         dres = torch.empty_like(x) if has_res else None
         dh = torch.empty_like(x)
         dg = torch.zeros(C, d, dtype=torch.float32, device=x.device)
         db = torch.zeros(C, d, dtype=torch.float32, device=x.device)
-        rc = _fn("fa_ln_bwd")(_p(dy), _p(x), _p(mean), _p(rstd), _c.c_int(C), _c.c_int(rpc), _c.c_int(d), _p(g),
-                              _p(dres), _p(dh), _c.c_uint32(_thr(p)), _f(1.0 / (1.0 - p) if p > 0 else 1.0),
-                              _c.c_uint32(seed & _M32), _p(dg), _p(db), _p(seed_dev), _stream(x))
-        _check(rc, "fa_ln_bwd")
+        name = "fa_ln_bwd" + _sfx(x)
+        rc = _fn(name)(_p(dy), _p(x), _p(mean), _p(rstd), _c.c_int(C), _c.c_int(rpc), _c.c_int(d), _p(g),
+                       _p(dres), _p(dh), _c.c_uint32(_thr(p)), _f(1.0 / (1.0 - p) if p > 0 else 1.0),
+                       _c.c_uint32(seed & _M32), _p(dg), _p(db), _p(seed_dev), _stream(x))
+        _check(rc, name)
         return dh, dres, dg.to(gdt), db.to(gdt), None, None, None, None, None
 
 
@@ -106,7 +124,8 @@ def layer_norm(h: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: fl
     seed + counter·1000003, so a captured HIP graph draws new dropout masks on every replay."""
     assert h.dim() == 2 and h.shape[0] % rows_per_client == 0
     if use_native(h):
-        assert h.dtype == torch.bfloat16 and h.is_contiguous() and (res is None or res.is_contiguous())
+        _sfx(h)
+        assert h.is_contiguous() and (res is None or (res.is_contiguous() and res.dtype == h.dtype))
         return _LayerNorm.apply(h, res, gamma, beta, float(eps), float(p), int(seed), int(rows_per_client), seed_dev)
     return _ln_ref(h, res, gamma, beta, eps, p, seed, rows_per_client)
 
@@ -116,22 +135,24 @@ class _Gelu(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x):
         y = torch.empty_like(x)
-        _check(_fn("fa_gelu_fwd")(_p(x), _p(y), _i64(x.numel()), _stream(x)), "fa_gelu_fwd")
+        name = "fa_gelu_fwd" + _sfx(x)
+        _check(_fn(name)(_p(x), _p(y), _i64(x.numel()), _stream(x)), name)
         ctx.save_for_backward(x)
         return y
 
     @staticmethod
     def backward(ctx, gy):
         (x,) = ctx.saved_tensors
-        gy = gy.contiguous()
+        gy = gy.to(x.dtype).contiguous()
         gx = torch.empty_like(x)
-        _check(_fn("fa_gelu_bwd")(_p(x), _p(gy), _p(gx), _i64(x.numel()), _stream(x)), "fa_gelu_bwd")
+        name = "fa_gelu_bwd" + _sfx(x)
+        _check(_fn(name)(_p(x), _p(gy), _p(gx), _i64(x.numel()), _stream(x)), name)
         return gx
 
 
 def gelu(x: torch.Tensor) -> torch.Tensor:
     if use_native(x):
-        assert x.dtype == torch.bfloat16 and x.is_contiguous() and x.numel() % 8 == 0
+        assert x.is_contiguous() and x.numel() % (8 if _sfx(x) == "" else 4) == 0
         return _Gelu.apply(x)
     return torch.nn.functional.gelu(x.float()).to(x.dtype)
 
@@ -140,9 +161,10 @@ def gelu(x: torch.Tensor) -> torch.Tensor:
 def _attn_ref(q, k, v, kmask, S, H, p, seed):
     T, dm = q.shape
     CB = T // S
-    qh = q.float().view(CB, S, H, 64).transpose(1, 2)
-    kh = k.float().view(CB, S, H, 64).transpose(1, 2)
-    vh = v.float().view(CB, S, H, 64).transpose(1, 2)
+    ct = _ct(q)
+    qh = q.to(ct).view(CB, S, H, 64).transpose(1, 2)
+    kh = k.to(ct).view(CB, S, H, 64).transpose(1, 2)
+    vh = v.to(ct).view(CB, S, H, 64).transpose(1, 2)
     s = qh @ kh.transpose(-1, -2) / math.sqrt(64.0)
     if kmask is not None:
         s = s.masked_fill(~kmask.view(CB, 1, 1, S).bool(), float("-inf"))
@@ -165,12 +187,13 @@ class _Attention(torch.autograd.Function):
         o = torch.empty(T, dm, dtype=q.dtype, device=q.device)
         lse = torch.empty(CB, H, S, dtype=torch.float32, device=q.device)
         scale = 1.0 / math.sqrt(64.0)
-        rc = _fn("fa_attn_fwd")(_p(q), _c.c_int(q.stride(0)), _p(k), _c.c_int(k.stride(0)), _p(v),
-                                _c.c_int(v.stride(0)), _p(o), _c.c_int(dm), _p(kmask), _p(lse), _c.c_int(CB),
-                                _c.c_int(S), _c.c_int(H), _f(scale), _c.c_uint32(_thr(p)),
-                                _f(1.0 / (1.0 - p) if p > 0 else 1.0), _c.c_uint32(seed & _M32), _p(seed_dev),
-                                _stream(q))
-        _check(rc, "fa_attn_fwd")
+        name = "fa_attn_fwd" + _sfx(q)
+        rc = _fn(name)(_p(q), _c.c_int(q.stride(0)), _p(k), _c.c_int(k.stride(0)), _p(v),
+                       _c.c_int(v.stride(0)), _p(o), _c.c_int(dm), _p(kmask), _p(lse), _c.c_int(CB),
+                       _c.c_int(S), _c.c_int(H), _f(scale), _c.c_uint32(_thr(p)),
+                       _f(1.0 / (1.0 - p) if p > 0 else 1.0), _c.c_uint32(seed & _M32), _p(seed_dev),
+                       _stream(q))
+        _check(rc, name)
         ctx.save_for_backward(q, k, v, o, lse, kmask)
         ctx.cfg = (S, H, p, seed)
         ctx.seed_dev = seed_dev
@@ -182,18 +205,19 @@ class _Attention(torch.autograd.Function):
         S, H, p, seed = ctx.cfg
         T, dm = q.shape
         CB = T // S
-        do = do.contiguous()
+        do = do.to(q.dtype).contiguous()
         dq = torch.empty(T, dm, dtype=q.dtype, device=q.device)
         dk = torch.empty_like(dq)
         dv = torch.empty_like(dq)
         D = torch.empty(CB, H, S, dtype=torch.float32, device=q.device)
-        rc = _fn("fa_attn_bwd")(_p(q), _c.c_int(q.stride(0)), _p(k), _c.c_int(k.stride(0)), _p(v),
-                                _c.c_int(v.stride(0)), _p(o), _c.c_int(dm), _p(do), _c.c_int(dm), _p(kmask), _p(lse),
-                                _p(D), _p(dq), _c.c_int(dm), _p(dk), _c.c_int(dm), _p(dv), _c.c_int(dm),
-                                _c.c_int(CB), _c.c_int(S), _c.c_int(H), _f(1.0 / math.sqrt(64.0)),
-                                _c.c_uint32(_thr(p)), _f(1.0 / (1.0 - p) if p > 0 else 1.0),
-                                _c.c_uint32(seed & _M32), _p(ctx.seed_dev), _stream(q))
-        _check(rc, "fa_attn_bwd")
+        name = "fa_attn_bwd" + _sfx(q)
+        rc = _fn(name)(_p(q), _c.c_int(q.stride(0)), _p(k), _c.c_int(k.stride(0)), _p(v),
+                       _c.c_int(v.stride(0)), _p(o), _c.c_int(dm), _p(do), _c.c_int(dm), _p(kmask), _p(lse),
+                       _p(D), _p(dq), _c.c_int(dm), _p(dk), _c.c_int(dm), _p(dv), _c.c_int(dm),
+                       _c.c_int(CB), _c.c_int(S), _c.c_int(H), _f(1.0 / math.sqrt(64.0)),
+                       _c.c_uint32(_thr(p)), _f(1.0 / (1.0 - p) if p > 0 else 1.0),
+                       _c.c_uint32(seed & _M32), _p(ctx.seed_dev), _stream(q))
+        _check(rc, name)
         return dq, dk, dv, None, None, None, None, None, None
 
 
@@ -204,9 +228,10 @@ def attention(q, k, v, S: int, H: int, kmask: torch.Tensor = None, p: float = 0.
     ``seed_dev`` as in :func:`layer_norm`."""
     assert q.dim() == 2 and q.shape[1] == H * 64 and q.shape[0] % S == 0
     if use_native(q):
-        assert S <= 256 and q.dtype == torch.bfloat16
+        vec = 8 if _sfx(q) == "" else 4
+        assert S <= 256
         for t in (q, k, v):
-            assert t.stride(1) == 1 and t.stride(0) % 8 == 0
+            assert t.dtype == q.dtype and t.stride(1) == 1 and t.stride(0) % vec == 0
         km = None if kmask is None else kmask.to(torch.uint8).contiguous()
         return _Attention.apply(q, k, v, km, int(S), int(H), float(p), int(seed), seed_dev)
     return _attn_ref(q, k, v, kmask, S, H, p, seed)
@@ -228,8 +253,11 @@ def _segments(views):
     return base, cs, (_c.c_int64 * 4)(*(off + [0] * (4 - len(off)))), (_c.c_int * 5)(*(lo + [0] * (5 - len(lo))))
 
 
-def native_linear_ok(M: int, N: int, K: int, nseg: int = 1) -> bool:
-    """Shapes the batched-GEMM kernels take (16-byte vectors along every contiguous dim)."""
+def native_linear_ok(M: int, N: int, K: int, nseg: int = 1, dtype=torch.bfloat16) -> bool:
+    """Shapes the batched-GEMM kernels take: bf16 needs 16-byte vectors along every contiguous dim;
+    the fp32 kernels take any shape (an element-wise staging variant covers unaligned ones)."""
+    if dtype == torch.float32:
+        return 1 <= nseg <= 4 and M > 0 and N > 0 and K > 0
     return K % 8 == 0 and N % 8 == 0 and 1 <= nseg <= 4 and M > 0
 
 
@@ -253,13 +281,19 @@ class _ClientLinear(torch.autograd.Function):
             assert list(blo) == list(lo)
         else:
             bb, bcs, boff = None, 0, None
-        y = torch.empty(C, M, N, dtype=torch.bfloat16, device=x.device)
+        y = torch.empty(C, M, N, dtype=x.dtype, device=x.device)
         y2 = torch.empty_like(y) if gelu else None
-        rc = _fn("fa_bgemm_fwd")(_p(x), _i64(M * K), _c.c_int(K), _p(wb), _c.c_int(wh), _i64(wcs), woff, _p(bb),
-                                 _i64(bcs), boff,
-                                 lo, _c.c_int(len(ws)), _p(y), _i64(M * N), _c.c_int(N), _p(y2), _c.c_int(C),
-                                 _c.c_int(M), _c.c_int(N), _c.c_int(K), _stream(x))
-        _check(rc, "fa_bgemm_fwd")
+        if x.dtype == torch.float32:    # fp32 activations: the fp32 kernels read the fp32 arena
+            assert wh == 0
+            rc = _fn("fa_bgemm_fwd_f32")(_p(x), _i64(M * K), _c.c_int(K), _p(wb), _i64(wcs), woff, _p(bb),
+                                         _i64(bcs), boff, lo, _c.c_int(len(ws)), _p(y), _i64(M * N), _c.c_int(N),
+                                         _p(y2), _c.c_int(C), _c.c_int(M), _c.c_int(N), _c.c_int(K), _stream(x))
+        else:
+            rc = _fn("fa_bgemm_fwd")(_p(x), _i64(M * K), _c.c_int(K), _p(wb), _c.c_int(wh), _i64(wcs), woff, _p(bb),
+                                     _i64(bcs), boff,
+                                     lo, _c.c_int(len(ws)), _p(y), _i64(M * N), _c.c_int(N), _p(y2), _c.c_int(C),
+                                     _c.c_int(M), _c.c_int(N), _c.c_int(K), _stream(x))
+        _check(rc, "fa_bgemm_fwd" + _sfx(x))
         ctx.save_for_backward(x, y if gelu else None)
         ctx.ws, ctx.bs, ctx.gelu, ctx.wsrc = ws, bs, gelu, wsrc
         return y2 if gelu else y
@@ -270,20 +304,27 @@ class _ClientLinear(torch.autograd.Function):
         ws, bs = ctx.ws, ctx.bs
         C, M, K = x.shape
         N = sum(w.shape[1] for w in ws)
-        g = g.contiguous()
+        g = g.to(x.dtype).contiguous()
+        sfx = _sfx(x)
         if ctx.gelu:
             gp = torch.empty_like(pre)
-            _check(_fn("fa_gelu_bwd")(_p(pre), _p(g), _p(gp), _i64(pre.numel()), _stream(pre)), "fa_gelu_bwd")
+            _check(_fn("fa_gelu_bwd" + sfx)(_p(pre), _p(g), _p(gp), _i64(pre.numel()), _stream(pre)),
+                   "fa_gelu_bwd" + sfx)
             g = gp
         dx = None
         if ctx.needs_input_grad[0]:
             wb, wcs, woff, lo = _segments(ctx.wsrc)
             wh = 1 if ctx.wsrc[0].dtype == torch.bfloat16 else 0
             dx = torch.empty_like(x)
-            rc = _fn("fa_bgemm_dgrad")(_p(g), _i64(M * N), _c.c_int(N), _p(wb), _c.c_int(wh), _i64(wcs), woff, lo,
-                                       _c.c_int(len(ws)), _p(dx), _i64(M * K), _c.c_int(K), _c.c_int(C), _c.c_int(M),
-                                       _c.c_int(N), _c.c_int(K), _stream(x))
-            _check(rc, "fa_bgemm_dgrad")
+            if sfx:
+                rc = _fn("fa_bgemm_dgrad_f32")(_p(g), _i64(M * N), _c.c_int(N), _p(wb), _i64(wcs), woff, lo,
+                                               _c.c_int(len(ws)), _p(dx), _i64(M * K), _c.c_int(K), _c.c_int(C),
+                                               _c.c_int(M), _c.c_int(N), _c.c_int(K), _stream(x))
+            else:
+                rc = _fn("fa_bgemm_dgrad")(_p(g), _i64(M * N), _c.c_int(N), _p(wb), _c.c_int(wh), _i64(wcs), woff, lo,
+                                           _c.c_int(len(ws)), _p(dx), _i64(M * K), _c.c_int(K), _c.c_int(C),
+                                           _c.c_int(M), _c.c_int(N), _c.c_int(K), _stream(x))
+            _check(rc, "fa_bgemm_dgrad" + sfx)
         # weight gradients: into the arena views when the engine pre-assigned them, else returned
         own = all(w.is_leaf and w.grad is not None for w in ws)
         if own:
@@ -298,10 +339,10 @@ class _ClientLinear(torch.autograd.Function):
                 out_w.append(v.view_as(w))
                 r += w.shape[1]
         gb, gcs, goff, glo = _segments(gviews)
-        rc = _fn("fa_bgemm_wgrad")(_p(g), _i64(M * N), _c.c_int(N), _p(x), _i64(M * K), _c.c_int(K), _p(gb), _i64(gcs),
+        rc = _fn("fa_bgemm_wgrad" + sfx)(_p(g), _i64(M * N), _c.c_int(N), _p(x), _i64(M * K), _c.c_int(K), _p(gb), _i64(gcs),
                                    goff, glo, _c.c_int(len(ws)), _c.c_int(C), _c.c_int(M), _c.c_int(N), _c.c_int(K),
                                    _stream(x))
-        _check(rc, "fa_bgemm_wgrad")
+        _check(rc, "fa_bgemm_wgrad" + sfx)
         out_b = []
         if bs:
             # column sums of g straight into the gradient arena (or a dense [C, N] when not owned)
@@ -317,9 +358,9 @@ class _ClientLinear(torch.autograd.Function):
                     out_b.append(dense_b[:, r:r + b.shape[1]])
                     r += b.shape[1]
             bb, bcs, boff, blo = _segments(bviews)
-            rc = _fn("fa_bias_grad")(_p(g), _i64(M * N), _c.c_int(N), _p(bb), _i64(bcs), boff, blo,
+            rc = _fn("fa_bias_grad" + sfx)(_p(g), _i64(M * N), _c.c_int(N), _p(bb), _i64(bcs), boff, blo,
                                      _c.c_int(len(bs)), _c.c_int(C), _c.c_int(M), _c.c_int(N), _stream(x))
-            _check(rc, "fa_bias_grad")
+            _check(rc, "fa_bias_grad" + sfx)
         return (dx, None, None, None, *out_w, *out_b)
 
 
@@ -328,15 +369,15 @@ def client_linear(x: torch.Tensor, weights, biases=None, gelu: bool = False, sha
     [C, n_i, K] fp32 arena views (concatenated along the output dim), ``biases`` the matching
     [C, n_i] views or None; ``gelu`` fuses the exact-erf GELU into the epilogue. ``shadows``: the
     same slots of a bf16 copy of the arena (current for this step) — the GEMMs then read bf16
-    weights; gradients always land in the fp32 arena. CUDA → the batched MFMA GEMM kernels (bf16
-    in/out); CPU → the fp32 PyTorch reference."""
+    weights; gradients always land in the fp32 arena. CUDA → the batched MFMA GEMM kernels at the
+    activation dtype (bf16, or fp32 through ``tf_f32_kernels.hip``); CPU → the fp32 PyTorch reference."""
     weights = list(weights)
     biases = list(biases) if biases else []
     C, M, K = x.shape
     N = sum(w.shape[1] for w in weights)
-    if use_native(x) and native_linear_ok(M, N, K, len(weights)):
-        assert x.dtype == torch.bfloat16
-        sh = tuple(shadows) if shadows else None
+    if use_native(x) and native_linear_ok(M, N, K, len(weights), x.dtype):
+        _sfx(x)
+        sh = tuple(shadows) if shadows and x.dtype == torch.bfloat16 else None
         if sh is not None:
             assert len(sh) == len(weights) and all(t.shape == w.shape for t, w in zip(sh, weights))
         return _ClientLinear.apply(x.contiguous(), bool(gelu), len(weights), sh, *weights, *biases)

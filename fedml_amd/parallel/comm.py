@@ -18,8 +18,15 @@ import torch.distributed as dist
 _COMM_STREAMS = {}
 
 
-def init_process_group(backend: Optional[str] = None, timeout_s: int = 1800, device=None):
-    """Idempotent init from torchrun env (RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT)."""
+def init_process_group(backend: Optional[str] = None, timeout_s: int = 1800, device=None, args=None):
+    """Idempotent init from torchrun env (RANK/WORLD_SIZE/MASTER_ADDR/MASTER_PORT).
+
+    ``args`` (the run config) is read before the group exists: ``deterministic`` pins the RCCL algorithm and
+    protocol; ``elastic`` makes a dead peer surface as an exception in the survivors instead of a hang —
+    the group gets the ``elastic_timeout_s`` timeout, and under RCCL every collective wait blocks with that
+    timeout (``TORCH_NCCL_BLOCKING_WAIT``) while the watchdog aborts the broken communicator without
+    tearing the process down (``TORCH_NCCL_ASYNC_ERROR_HANDLING=2``, clean-up only) — the simulator then
+    rebuilds the group from the survivors (``parallel.elastic``)."""
     if dist.is_initialized():
         return dist.get_rank(), dist.get_world_size()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -33,7 +40,12 @@ def init_process_group(backend: Optional[str] = None, timeout_s: int = 1800, dev
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29500")
     from ..utils import determinism
-    determinism.apply_env()     # deterministic mode: fixed RCCL algorithm / protocol
+    determinism.apply_env(args)     # deterministic mode: fixed RCCL algorithm / protocol
+    if args is not None and bool(getattr(args, "elastic", False)):
+        timeout_s = int(getattr(args, "elastic_timeout_s", 60) or 60)
+        if backend == "nccl":
+            os.environ["TORCH_NCCL_BLOCKING_WAIT"] = "1"
+            os.environ["TORCH_NCCL_ASYNC_ERROR_HANDLING"] = "2"
     kw = {}
     if backend == "nccl" and device is not None:
         kw["device_id"] = torch.device(device)

@@ -102,6 +102,13 @@ class ClientBatchEngine:
         self.sgd_wd = bool(getattr(args, "sgd_weight_decay", False))
         self.mu = float(getattr(args, "fedprox_mu", getattr(args, "mu", 0.0)) or 0.0) if \
             str(getattr(args, "federated_optimizer", "")) in ("FedProx", "FedNova") else 0.0
+        if str(getattr(args, "federated_optimizer", "")) == "FedNova":
+            # the FedNova local optimizer always applies its weight decay (reference client.py:83-91
+            # FedNova(..., weight_decay=args.wd)); the fused SGD kernel's order — d = g + wd·w + μ(w − w0),
+            # buf = ρ·buf + d — is the reference step's, whose in-place `d_p.add_(mu, …)` on the aliased
+            # momentum buffer puts the proximal term into the buffer (fednova.py:129-142)
+            self.weight_decay = float(getattr(args, "wd", getattr(args, "weight_decay", 0.0)) or 0.0)
+            self.sgd_wd = True
         self.mom = self.layout.alloc_stack(self.C, self.device) if (opt == "sgd" and self.momentum) else None
         if opt != "sgd":
             self.m1 = self.layout.alloc_stack(self.C, self.device)
@@ -118,16 +125,18 @@ class ClientBatchEngine:
             self.interp = None
             self.sequential = True
             self.tf = None
-            # the client-batched transformer kernels compute in bf16 (fp32 masters); an fp32 run on the GPU
-            # keeps the per-client torch path, which honours fp32, instead of silently downgrading
-            tf_dtype_ok = self.device.type != "cuda" or compute_dtype == torch.bfloat16
-            if not tf_dtype_ok:
-                logging.warning("virtual-client engine: client-batched transformer kernels are bf16; compute_dtype "
-                                "%s runs the sequential per-client torch path", compute_dtype or "fp32")
+            # the client-batched transformer kernels run at the requested precision: fp32 (compute_dtype
+            # None / fp32, the reference's: csrc/tf_f32_kernels.hip, products per `fp32_mma`) or bf16
+            tf_dtype_ok = self.device.type != "cuda" or (compute_dtype or torch.float32) in (torch.float32,
+                                                                                           torch.bfloat16)
             if os.environ.get("FEDML_AMD_BATCHED_TRANSFORMER", "1") != "0" and tf_dtype_ok:
                 try:
                     self.tf = BatchedTransformer(model, self.C)
-                    logging.info("virtual-client engine: client-batched transformer path (%s)", self.tf.kind)
+                    logging.info("virtual-client engine: client-batched transformer path (%s, %s)", self.tf.kind,
+                                 compute_dtype or torch.float32)
+                    if self.device.type == "cuda" and (compute_dtype or torch.float32) == torch.float32:
+                        from ...ops import nn_ops
+                        nn_ops.set_f32_mma_mode(str(getattr(args, "fp32_mma", "exact") or "exact"))
                 except UnsupportedTransformer:
                     pass
             if self.tf is None:
@@ -732,7 +741,8 @@ class ClientBatchEngine:
         """Like ``partial_sum`` but each client's update Δ_c = w_c − w_global travels compressed:
         block-256 int8 (stochastic rounding) / fp8-e4m3 quantisation, or exact top-k sparsification,
         all with per-client error feedback (``residual``: per-client rows indexed by client id —
-        ``residuals.ShardedResiduals`` or a [K_total, P] tensor). int8 / fp8 run as ONE launch over the
+        ``residuals.ShardedResiduals`` or a [K_total, P] tensor; id −1 marks a padding slot, which has no
+        row). int8 / fp8 run as ONE launch over the
         [C, P] stack with the decompression fused into the accumulation (``ops.compress_accumulate``);
         top-k selects per client. Returns (out, uploaded_bytes); ``n_upload`` = clients with a non-zero
         weight (host-known; avoids a device sync for the byte count)."""
@@ -740,9 +750,10 @@ class ClientBatchEngine:
             out = torch.empty(self.P + 1, dtype=torch.float32, device=self.device)
         acc = out[:self.P]
         w = weights.to(torch.float32)
-        ids = torch.as_tensor([int(c) for c in client_ids], dtype=torch.int64)
+        # padding slots (a rank hosting fewer than C clients) carry client id -1: no residual row, weight 0
+        ids = torch.as_tensor([max(0, int(c)) for c in client_ids], dtype=torch.int64)
         if method in ("int8", "fp8"):
-            rows = [residual[int(c)] for c in client_ids] if residual is not None else None
+            rows = [residual[int(c)] if int(c) >= 0 else None for c in client_ids] if residual is not None else None
             ops.compress_accumulate(self.params, global_flat, rows, w, ids.to(self.device, non_blocking=True),
                                     method, seed, acc)
             out[self.P:].copy_(w.sum().view(1))
@@ -757,7 +768,7 @@ class ClientBatchEngine:
         nbytes = 0
         k = max(1, int(self.P * ratio))
         for c, wc in enumerate(w_host):
-            if wc == 0.0:
+            if wc == 0.0 or int(client_ids[c]) < 0:
                 continue
             r = residual[int(client_ids[c])]
             torch.sub(self.params[c], global_flat, out=delta)

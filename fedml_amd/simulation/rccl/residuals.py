@@ -25,11 +25,14 @@ class ShardedResiduals:
         self.owner: Dict[int, int] = {}
 
     def __getitem__(self, cid: int) -> torch.Tensor:
+        """This rank's row of client ``cid`` (zeros on first use). Ownership is never changed here: only
+        ``migrate`` (the same call on every rank) assigns owners, so all ranks keep the same owner map."""
         cid = int(cid)
+        if cid < 0:
+            raise KeyError(f"client id {cid}: padding slots have no residual row")
         row = self.rows.get(cid)
         if row is None:
             row = self.rows[cid] = torch.zeros(self.P, dtype=torch.float32, device=self.device)
-            self.owner[cid] = self.rank
         return row
 
     def nbytes(self) -> int:

@@ -62,6 +62,19 @@ def fednova_normalizer(tau: int, lr: float, momentum: float = 0.0, mu: float = 0
     return vec, (float(tau) if mu else vec)
 
 
+_PEER_FAILURE_MARKERS = ("connection closed", "connection reset", "connection refused", "broken pipe", "peer",
+                         "gloo", "nccl", "rccl", "timed out", "timeout", "socket", "communicator")
+
+
+def _is_peer_failure(e: BaseException) -> bool:
+    """A collective that failed because another rank died or became unreachable (what elastic re-init
+    can repair), as opposed to a local error."""
+    if isinstance(e, torch.distributed.DistBackendError):
+        return True
+    msg = str(e).lower()
+    return any(m in msg for m in _PEER_FAILURE_MARKERS)
+
+
 class RCCLSimulator:
     def __init__(self, args, device, dataset, model, store: Optional[DeviceClientStore] = None, model_trainer=None):
         """``model_trainer`` (reference ``fedml.run_simulation(..., model_trainer)``): a functional trainer
@@ -78,7 +91,11 @@ class RCCLSimulator:
             else:
                 self.user_trainer = model_trainer
         self.device = torch.device(device)
-        self.rank, self.world = comm.init_process_group(device=self.device if self.device.type == "cuda" else None)
+        from ...utils import determinism
+        if determinism.enabled(args):
+            determinism.enable(args)     # before the process group: the RCCL env must precede the communicator
+        self.rank, self.world = comm.init_process_group(device=self.device if self.device.type == "cuda" else None,
+                                                        args=args)
         self.model = model.to(self.device)
         self.dataset = dataset
         self.K_total = int(args.client_num_in_total)
@@ -112,6 +129,9 @@ class RCCLSimulator:
         self.nova_buf = torch.zeros(self.layout.size, dtype=torch.float32, device=self.device) \
             if self.nova_gmf else None
         self.nova_first = True
+        # the reference re-creates its global momentum buffer every round (fednova_trainer.py:80), so gmf
+        # reduces to w −= cum_grad; `fednova_gmf_persist: true` keeps the buffer across rounds instead
+        self.nova_persist = bool(getattr(args, "fednova_gmf_persist", False))
         self.round_times: List[float] = []
         # aggregation bucket (elements) for the pipelined weighted-sum + all-reduce of large models
         self.bucket_elems = max(256, int(float(getattr(args, "allreduce_bucket_mb", 32) or 32) * (1 << 20) / 4))
@@ -179,6 +199,8 @@ class RCCLSimulator:
         with tr.gpu_span("round.aggregate", self.device):
             if self.fednova:
                 w = self._fednova_coefficients(ids, mine)
+                if not self.nova_persist:
+                    self.nova_first = True
             else:
                 w = torch.where(valid, self.store.counts[slots].to(torch.float32),
                                 torch.zeros(self.C, device=self.device))
@@ -191,7 +213,7 @@ class RCCLSimulator:
                 w = w * keep.to(self.device)
             self._robust_preaggregate(w)
             if self.compression:
-                ids = list(mine) + [0] * (self.C - len(mine))
+                ids = list(mine) + [-1] * (self.C - len(mine))     # -1: padding slot (no residual row)
                 n_up = len(mine) if not self.faults.active else int(keep.sum())
                 _, nb = self.engine.compressed_partial_sum(w, self.global_flat, ids, self.residual, self.compression,
                                                            self.compress_ratio, round_idx, out=self.partial,
@@ -315,11 +337,16 @@ class RCCLSimulator:
     def _run_round_elastic(self, round_idx):
         if not self.elastic:
             return self.run_round(round_idx)
+        max_reinit = int(getattr(self.args, "elastic_max_reinit", 3) or 3)
         while True:
             try:
                 return self.run_round(round_idx)
             except (RuntimeError, torch.distributed.DistBackendError) as e:
                 from ...parallel import elastic
+                # only a failed collective (a dead / unreachable peer) is retried, at most max_reinit times
+                # per run; a local error (kernel fault, OOM, shape bug) would recur on every retry
+                if not _is_peer_failure(e) or len(self.world_changes) >= max_reinit:
+                    raise
                 logging.warning("round %d: collective failed (%s) — re-initialising the communicator", round_idx,
                                 str(e).splitlines()[0][:200])
                 old = self.world
@@ -383,7 +410,7 @@ class RCCLSimulator:
             clients = {"gen": self.gen.get_state()}
             if dense is not None:
                 clients["residual"] = dense.detach().cpu()
-            if self.nova_buf is not None and not self.nova_first:
+            if self.nova_buf is not None and not self.nova_first and self.nova_persist:
                 clients["fednova_buf"] = self.nova_buf.detach().cpu()
             save_round_checkpoint(directory, self.round_idx, self.global_model_state(), self.args,
                                   server_opt=self.server_opt.state_dict() if self.server_opt else None,

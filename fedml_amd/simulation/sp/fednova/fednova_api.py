@@ -34,6 +34,9 @@ class FedNovaAPI(FedAvgAPI):
                 ratios.append(ratio)
                 a_vec.append(self.model_trainer.a_i)
                 taus.append(self.model_trainer.tau_eff_i)
+            # the reference starts every round with an empty global momentum buffer (fednova_trainer.py:80)
+            if not bool(getattr(self.args, "fednova_gmf_persist", False)):
+                self.momentum_buf = None
             w_global, self.momentum_buf = fednova_aggregate(
                 w_global, w_locals, ratios, a_vec, taus, gmf=float(getattr(self.args, "gmf", 0.0) or 0.0),
                 lr=float(self.args.learning_rate), momentum_buf=self.momentum_buf)

@@ -44,7 +44,13 @@ class FedNovaOptimizer(torch.optim.Optimizer):
                         buf.mul_(g["momentum"]).add_(d, alpha=1 - g["dampening"])
                     d = d.add(buf, alpha=g["momentum"]) if g["nesterov"] else buf
                 if self.mu:
-                    d = d.add(p - st["old_init"], alpha=self.mu)
+                    prox = p.detach() - st["old_init"]
+                    if g["momentum"] and not g["nesterov"]:
+                        # the reference adds in place (fednova.py:140 `d_p.add_(self.mu, …)`) and d_p IS the
+                        # momentum buffer here, so the proximal term accumulates in the buffer
+                        buf.add_(prox, alpha=self.mu)
+                    else:
+                        d = d.add(prox, alpha=self.mu)
                 if "cum_grad" not in st:
                     st["cum_grad"] = d.detach().clone().mul_(lr)
                 else:

@@ -28,9 +28,9 @@ def enabled(args=None) -> bool:
     return _ENABLED[0]
 
 
-def apply_env():
+def apply_env(args=None):
     """Collective-library settings that fix the reduction order (call before the process group exists)."""
-    if enabled():
+    if enabled(args):
         os.environ["NCCL_ALGO"] = "Ring"
         os.environ["NCCL_PROTO"] = "Simple"
 

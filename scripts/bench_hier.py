@@ -70,7 +70,7 @@ def main():
     p.add_argument("--samples-per-client", type=int, default=32)
     p.add_argument("--batch-size", type=int, default=16)
     p.add_argument("--lr", type=float, default=1e-4)
-    p.add_argument("--dtype", default="bf16")
+    p.add_argument("--dtype", default="fp32", help="fp32 (the reference's precision) | bf16")
     p.add_argument("--wan-compression", default="", help="'' (fp32 state dicts, the reference) | int8")
     p.add_argument("--timeout", type=float, default=900)
     # worker-internal

@@ -28,7 +28,9 @@ def _flat(sd):
     return torch.cat([v.detach().float().reshape(-1) for k, v in sorted(sd.items()) if v.is_floating_point()])
 
 
-@pytest.mark.parametrize("kw", [{}, {"momentum": 0.9}, {"gmf": 0.5}, {"mu": 0.01}])
+@pytest.mark.parametrize("kw", [{}, {"momentum": 0.9}, {"gmf": 0.5}, {"mu": 0.01},
+                                {"momentum": 0.5, "mu": 0.01, "wd": 0.001},
+                                {"gmf": 0.5, "fednova_gmf_persist": True}])
 def test_fednova_rccl_equals_sp(kw):
     from fedml_amd.simulation.rccl.simulator import RCCLSimulator
     from fedml_amd.simulation.sp.fednova.fednova_api import FedNovaAPI
@@ -63,3 +65,39 @@ def test_fednova_normalizer_matches_local_optimizer():
             opt.step()
         a, t = fednova_normalizer(7, 0.1, mom, mu)
         assert abs(a - opt.local_normalizing_vec) < 1e-9 and abs(t - opt.tau_eff()) < 1e-9, (mom, mu)
+
+
+def test_fednova_gmf_resets_each_round_like_reference():
+    """The reference re-creates its global momentum buffer at the start of every round
+    (fednova_trainer.py:80): buf = cum_grad / lr, then w −= lr·buf, i.e. w −= cum_grad — so any gmf gives
+    the gmf = 0 trajectory. Pinned on both simulators; the persistent variant (opt-in) differs."""
+    from fedml_amd.simulation.rccl.simulator import RCCLSimulator
+    args = _args(backend="RCCL")
+    dataset, k = load(args)
+    torch.manual_seed(0)
+    model = fedml_amd.models.create(args, k)
+    out = {}
+    for name, kw in {"g0": {}, "g5": {"gmf": 0.5}, "g5p": {"gmf": 0.5, "fednova_gmf_persist": True}}.items():
+        sim = RCCLSimulator(_args(backend="RCCL", **kw), torch.device("cpu"), dataset, copy.deepcopy(model))
+        sim.run(3)
+        out[name] = _flat(sim.global_model_state())
+    assert torch.allclose(out["g0"], out["g5"], atol=1e-6)
+    assert not torch.allclose(out["g0"], out["g5p"], atol=1e-4)
+
+
+def test_fednova_prox_enters_momentum_buffer_like_reference():
+    """Reference step (fednova.py:129-142): d_p = buf after the momentum update, then d_p.add_(mu, w − w0)
+    in place — the proximal term accumulates in the buffer. Hand-computed two steps."""
+    from fedml_amd.trainers.fednova import FedNovaOptimizer
+    p = torch.nn.Parameter(torch.tensor([1.0]))
+    opt = FedNovaOptimizer([p], lr=0.1, momentum=0.5, mu=0.2)
+    w0, lr, rho, mu = 1.0, 0.1, 0.5, 0.2
+    g1, g2 = 2.0, 3.0
+    p.grad = torch.tensor([g1]); opt.step()
+    buf = g1 + mu * (1.0 - w0)
+    w = 1.0 - lr * buf
+    p.grad = torch.tensor([g2]); opt.step()
+    buf = rho * buf + g2 + mu * (w - w0)
+    w = w - lr * buf
+    assert abs(float(p) - w) < 1e-6
+    assert abs(float(opt.state[p]["momentum_buffer"]) - buf) < 1e-6

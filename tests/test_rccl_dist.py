@@ -49,12 +49,13 @@ def test_rccl_sim_world_size_invariance_4_ranks(tmp_path):
     assert float((w1 - w4).norm() / w1.norm()) < 1e-5
 
 
-@pytest.mark.parametrize("method", ["int8", "topk"])
-def test_compressed_partial_participation_world_size_invariance(tmp_path, method):
-    """Compressed updates with error feedback and 4 of 9 clients per round: clients move between ranks
-    from round to round, so their residual rows migrate point-to-point (residuals.ShardedResiduals); the
-    4-round result equals the single-rank run."""
-    env = dict(FEDML_TEST_COMPRESSION=method, FEDML_TEST_PER_ROUND="4", FEDML_TEST_ROUNDS="4")
+@pytest.mark.parametrize("method,per_round", [("int8", 4), ("topk", 4), ("int8", 5), ("fp8", 5), ("topk", 5)])
+def test_compressed_partial_participation_world_size_invariance(tmp_path, method, per_round):
+    """Compressed updates with error feedback and 4 (or 5) of 9 clients per round: clients move between
+    ranks from round to round, so their residual rows migrate point-to-point (residuals.ShardedResiduals);
+    the 4-round result equals the single-rank run. With 5 per round on 2 ranks one rank has a padding slot
+    every round: it must neither touch a residual row nor claim a client."""
+    env = dict(FEDML_TEST_COMPRESSION=method, FEDML_TEST_PER_ROUND=str(per_round), FEDML_TEST_ROUNDS="4")
     w1 = _launch(1, str(tmp_path / "w1.pt"), "lr", 9, True, **env)
     w2 = _launch(2, str(tmp_path / "w2.pt"), "lr", 9, True, **env)
     # fp32 summation order only (a lost or stale residual row moves the result by > 1e-2)
@@ -93,3 +94,25 @@ def test_elastic_reinit_after_rank_death(tmp_path):
     assert codes == [0, 0, 0], codes
     w3 = torch.load(out, weights_only=True)
     assert float((w1 - w3).norm() / w1.norm()) < 1e-5
+
+
+def test_elastic_retries_only_peer_failures():
+    """A local error (kernel fault, OOM, shape bug) is re-raised at once instead of re-initialising the
+    communicator in a loop; collective / transport failures are retried."""
+    from fedml_amd.simulation.rccl.simulator import _is_peer_failure
+    assert _is_peer_failure(RuntimeError("[gloo/transport/tcp/pair.cc:534] Connection closed by peer [127.0.0.1]"))
+    assert _is_peer_failure(torch.distributed.DistBackendError("NCCL communicator was aborted"))
+    assert _is_peer_failure(RuntimeError("Watchdog caught collective operation timeout"))
+    assert not _is_peer_failure(RuntimeError("fa_conv_fwd failed with HIP error 1"))
+    assert not _is_peer_failure(RuntimeError("HIP out of memory. Tried to allocate 2.00 GiB"))
+    assert not _is_peer_failure(RuntimeError("shape '[4, 3]' is invalid for input of size 10"))
+
+
+def test_residual_rows_do_not_claim_ownership():
+    from fedml_amd.simulation.rccl.residuals import ShardedResiduals
+    r = ShardedResiduals(8, "cpu", rank=1, world=2)
+    r.migrate({0: 0, 3: 1})
+    _ = r[3]
+    assert r.owner == {0: 0, 3: 1}
+    with pytest.raises(KeyError):
+        r[-1]

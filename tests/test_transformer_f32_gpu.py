@@ -1,0 +1,248 @@
+"""fp32 transformer kernels (``csrc/tf_f32_kernels.hip``) — the reference's training precision — against
+fp64 references of the same ops, forward and backward, under both fp32 matrix-core modes:
+
+* ``exact``  (v_mfma_f32_16x16x4_f32): the error must stay within a small multiple of what PyTorch's own
+  fp32 GPU result shows against the same fp64 reference (and under 1e-5 of the output scale);
+* ``bf16x3`` (split-bf16 products, ~2⁻¹⁶ per product): under 2e-4 of the output scale.
+
+Plus a whole local step of the client-batched fp32 DistilBERT / ViT engine against per-client fp64
+``nn.Module`` steps."""
+import copy
+import math
+
+import pytest
+import torch
+
+from fedml_amd.ops import nn_ops
+from fedml_amd.ops import transformer_ops as T
+
+pytestmark = pytest.mark.gpu
+dev = "cuda"
+MODES = ["exact", "bf16x3"]
+TOL = {"exact": 1e-5, "bf16x3": 2e-4}
+
+
+@pytest.fixture(params=MODES)
+def mode(request):
+    prev = nn_ops.set_f32_mma_mode(request.param)
+    yield request.param
+    nn_ops.set_f32_mma_mode(prev)
+
+
+def _rel(a, ref):
+    ref = ref.double()
+    return ((a.double() - ref).abs().max() / (ref.abs().max() + 1e-30)).item()
+
+
+def _check(native, torch32, ref64, mode, what):
+    e = _rel(native, ref64)
+    assert e <= TOL[mode], f"{what}: {e:.3g} > {TOL[mode]} (fp64 reference)"
+    if mode == "exact":
+        e32 = _rel(torch32, ref64)
+        assert e <= max(4.0 * e32, 2e-6), f"{what}: native {e:.3g} vs torch fp32 {e32:.3g} (fp64 reference)"
+
+
+def _arena_views(C, shapes, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    offs, o = [], 0
+    for s in shapes:
+        offs.append(o)
+        o += (math.prod(s) + 63) // 64 * 64
+    P = o + 64
+    params = (0.05 * torch.randn(C, P, generator=g)).to(dev)
+    grads = torch.zeros(C, P, device=dev)
+    views = []
+    for s, off in zip(shapes, offs):
+        n = math.prod(s)
+        v = params[:, off:off + n].view(C, *s).detach().requires_grad_(True)
+        v.grad = grads[:, off:off + n].view(C, *s)
+        views.append(v)
+    return views
+
+
+@pytest.mark.parametrize("C,M,K,ns,gelu", [(3, 200, 768, [768, 768, 768], False),
+                                           (2, 16, 72, [136], True),
+                                           (4, 130, 256, [1024], True),
+                                           (2, 300, 768, [3], False),      # classifier head: unaligned N
+                                           (2, 37, 30, [10], True)])       # unaligned K and N
+def test_client_linear_f32(mode, C, M, K, ns, gelu):
+    torch.manual_seed(0)
+    vs = _arena_views(C, [(n, K) for n in ns] + [(n,) for n in ns])
+    ws, bs = vs[:len(ns)], vs[len(ns):]
+    x = torch.randn(C, M, K, device=dev).requires_grad_(True)
+    y = T.client_linear(x, ws, bs, gelu=gelu)
+    assert y.dtype == torch.float32
+    gy = torch.randn_like(y)
+    y.backward(gy)
+
+    def ref(dt):
+        w = [t.detach().to(dt).requires_grad_(True) for t in ws]
+        b = [t.detach().to(dt).requires_grad_(True) for t in bs]
+        xr = x.detach().to(dt).requires_grad_(True)
+        yr = torch.bmm(xr, torch.cat(w, 1).transpose(1, 2)) + torch.cat(b, 1).unsqueeze(1)
+        if gelu:
+            yr = torch.nn.functional.gelu(yr)
+        yr.backward(gy.to(dt))
+        return yr, xr.grad, [t.grad for t in w], [t.grad for t in b]
+
+    y64, dx64, dw64, db64 = ref(torch.float64)
+    y32, dx32, dw32, db32 = ref(torch.float32)
+    _check(y, y32, y64, mode, "y")
+    _check(x.grad, dx32, dx64, mode, "dx")
+    for w, a, b in zip(ws, dw32, dw64):
+        _check(w.grad, a, b, mode, "dW")
+    for bb, a, b in zip(bs, db32, db64):
+        _check(bb.grad, a, b, mode, "db")
+
+
+@pytest.mark.parametrize("d,rpc,C,res,p", [(768, 40, 3, True, 0.1), (768, 33, 2, False, 0.0), (192, 17, 4, True, 0.0),
+                                           (1024, 8, 2, False, 0.2)])
+def test_layer_norm_f32(d, rpc, C, res, p):
+    torch.manual_seed(0)
+    R = rpc * C
+    h = (torch.randn(R, d, device=dev) * 2 + 0.5).requires_grad_(True)
+    r = torch.randn(R, d, device=dev).requires_grad_(True) if res else None
+    g = (1 + 0.1 * torch.randn(C, d, device=dev)).requires_grad_(True)
+    b = (0.1 * torch.randn(C, d, device=dev)).requires_grad_(True)
+    y = T.layer_norm(h, g, b, 1e-12, rpc, res=r, p=p, seed=1234)
+    assert y.dtype == torch.float32
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    outs = {}
+    for dt in (torch.float64, torch.float32):
+        h2 = h.detach().to(dt).requires_grad_(True)
+        r2 = r.detach().to(dt).requires_grad_(True) if res else None
+        g2 = g.detach().to(dt).requires_grad_(True)
+        b2 = b.detach().to(dt).requires_grad_(True)
+        y2 = T._ln_ref(h2, r2, g2, b2, 1e-12, p, 1234, rpc)
+        y2.backward(gy.to(dt))
+        outs[dt] = (y2, h2.grad, r2.grad if res else None, g2.grad, b2.grad)
+    got = (y, h.grad, r.grad if res else None, g.grad, b.grad)
+    for name, a, t32, t64 in zip(("y", "dh", "dres", "dgamma", "dbeta"), got, outs[torch.float32],
+                                 outs[torch.float64]):
+        if a is not None:
+            _check(a, t32, t64, "exact", name)
+
+
+def test_gelu_f32():
+    torch.manual_seed(0)
+    x = (torch.randn(4096, 96, device=dev) * 3).requires_grad_(True)
+    y = T.gelu(x)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+    x2 = x.detach().double().requires_grad_(True)
+    y2 = torch.nn.functional.gelu(x2)
+    y2.backward(gy.double())
+    assert _rel(y, y2) < 2e-6
+    assert _rel(x.grad, x2.grad) < 2e-6
+
+
+@pytest.mark.parametrize("S,H,CB,mask,p", [(197, 3, 4, False, 0.0), (128, 2, 3, True, 0.0), (128, 2, 3, True, 0.1),
+                                           (64, 1, 2, False, 0.0), (250, 2, 2, True, 0.0), (37, 2, 5, True, 0.1),
+                                           (150, 1, 2, False, 0.0)])
+def test_attention_f32(mode, S, H, CB, mask, p):
+    torch.manual_seed(0)
+    dm = 64 * H
+    qkv = torch.randn(CB * S, 3 * dm, device=dev).requires_grad_(True)
+    q, k, v = qkv[:, :dm], qkv[:, dm:2 * dm], qkv[:, 2 * dm:]
+    km = None
+    if mask:
+        km = torch.rand(CB, S, device=dev) > 0.3
+        km[:, 0] = True
+    o = T.attention(q, k, v, S, H, kmask=km, p=p, seed=77)
+    assert o.dtype == torch.float32
+    go = torch.randn_like(o)
+    o.backward(go)
+    res = {}
+    for dt in (torch.float64, torch.float32):
+        q2 = qkv.detach().to(dt).requires_grad_(True)
+        o2 = T._attn_ref(q2[:, :dm], q2[:, dm:2 * dm], q2[:, 2 * dm:], km, S, H, p, 77)
+        o2.backward(go.to(dt))
+        res[dt] = (o2, q2.grad)
+    _check(o, res[torch.float32][0], res[torch.float64][0], mode, "o")
+    _check(qkv.grad, res[torch.float32][1], res[torch.float64][1], mode, "dqkv")
+
+
+def test_attention_f32_fully_masked_row_is_zero():
+    S, H, CB = 64, 1, 2
+    q = torch.randn(CB * S, 64, device=dev)
+    km = torch.ones(CB, S, dtype=torch.bool, device=dev)
+    km[1] = False
+    o = T.attention(q, q, q, S, H, kmask=km)
+    assert torch.isfinite(o).all()
+    assert o[S:].abs().max().item() == 0.0
+
+
+def _tiny(kind):
+    from fedml_amd.models.transformer.distilbert import distilbert
+    from fedml_amd.models.transformer.vit import vit_tiny
+    if kind == "distilbert":
+        m = distilbert(3, vocab=211, dim=128, n_layers=2, n_heads=2, hidden=256, max_pos=64)
+    else:
+        m = vit_tiny(num_classes=7, img_size=32, patch=4, depth=2)
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.Dropout):
+            mod.p = 0.0
+    if hasattr(m, "layer"):
+        for blk in m.layer:
+            blk.attention.dropout = 0.0
+    if hasattr(m, "blocks"):
+        for blk in m.blocks:
+            blk.attn.dropout = 0.0
+    return m
+
+
+@pytest.mark.parametrize("kind", ["distilbert", "vit"])
+def test_engine_fp32_transformer_step_vs_fp64(mode, kind):
+    """One fp32 local SGD step of the client-batched engine (BatchedTransformer on the fp32 kernels)
+    against per-client fp64 nn.Module steps; bounded by the fp32-vs-fp64 spread of PyTorch's own fp32
+    GPU step of the same modules (exact mode) or 2e-4 of the update scale (bf16x3)."""
+    from fedml_amd.arguments import Arguments
+    from fedml_amd.simulation.rccl.client_store import DeviceClientStore
+    from fedml_amd.simulation.rccl.engine import ClientBatchEngine
+    torch.manual_seed(0)
+    model = _tiny(kind)
+    C, n = 2, 8
+    if kind == "distilbert":
+        x = torch.randint(1, 211, (C * n, 48), device=dev)
+        x[:, -5:] = 0
+        y = torch.randint(0, 3, (C * n,), device=dev)
+    else:
+        x = torch.randn(C * n, 3, 32, 32, device=dev)
+        y = torch.randint(0, 7, (C * n,), device=dev)
+    lr = 0.5
+    args = Arguments.from_dict({"x": {"client_optimizer": "sgd", "learning_rate": lr, "fp32_mma": mode}})
+    eng = ClientBatchEngine(copy.deepcopy(model).to(dev), C, dev, args, compute_dtype=None)
+    assert eng.tf is not None, "fp32 must run the client-batched transformer path"
+    eng.tf.p_attn = eng.tf.p_hidden = eng.tf.p_emb = eng.tf.p_cls = 0.0
+    init = eng.layout.flatten(model.state_dict(), device=dev)
+    eng.load_global(init)
+    store = DeviceClientStore(x, y, [0, n], [n, n])
+    eng.train(store, torch.arange(C, device=dev), 1, n, lr, shuffle=False)
+    torch.cuda.synchronize()
+    got = eng.params.clone()
+    eng.close()
+
+    def step(dt):
+        rows = []
+        for c in range(C):
+            m = copy.deepcopy(model).to(dev).to(dt).train()
+            xc = x[c * n:(c + 1) * n]
+            out = m(xc if kind == "distilbert" else xc.to(dt))
+            loss = torch.nn.functional.cross_entropy(out, y[c * n:(c + 1) * n])
+            loss.backward()
+            with torch.no_grad():
+                for prm in m.parameters():
+                    prm -= lr * prm.grad
+            rows.append(eng.layout.flatten({k: v.double() for k, v in m.state_dict().items()}, device=dev))
+        return torch.stack(rows)
+
+    p64 = step(torch.float64)
+    p32 = step(torch.float32).double()
+    d64 = p64 - init.double()
+    e_nat = ((got.double() - p64).abs().max() / d64.abs().max()).item()
+    e_t32 = ((p32 - p64).abs().max() / d64.abs().max()).item()
+    if mode == "exact":
+        assert e_nat <= max(8.0 * e_t32, 1e-5), f"native {e_nat:.3g} vs torch fp32 {e_t32:.3g}"
+    else:
+        assert e_nat <= max(8.0 * e_t32, 2e-3), f"native {e_nat:.3g} vs torch fp32 {e_t32:.3g}"
