@@ -10,6 +10,7 @@ import logging
 
 from .cv.cnn import CNN_DropOut, CNN_OriginalFedAvg
 from .cv.darts import Network as DartsNetwork
+from .cv.darts import Network_GumbelSoftmax, NetworkCIFAR
 from .cv.efficientnet import EfficientNet
 from .cv.mnist_gan import MNISTGAN
 from .cv.mobilenet import mobilenet
@@ -84,8 +85,16 @@ def create(args, output_dim):
         return vit_tiny(num_classes=output_dim)
     if name == "gan":
         return MNISTGAN(int(getattr(args, "nz", 100)))
-    if name == "darts":
-        return DartsNetwork(int(getattr(args, "init_channels", 8)), output_dim, int(getattr(args, "layers", 3)))
+    if name in ("darts", "darts_gdas", "gdas"):
+        # FedNAS (reference fednas main): `stage: search` → the supernet (DARTS, or GDAS with
+        # `search_method: gdas`); `stage: train` → the genotype network named by `arch` (default FedNAS_V1)
+        C, L = int(getattr(args, "init_channels", 16)), int(getattr(args, "layers", 8))
+        if str(getattr(args, "stage", "search")) == "train":
+            return NetworkCIFAR(C, output_dim, L, bool(getattr(args, "auxiliary", False)),
+                                getattr(args, "arch", "FedNAS_V1") or "FedNAS_V1")
+        if name != "darts" or str(getattr(args, "search_method", "darts")).lower() == "gdas":
+            return Network_GumbelSoftmax(C, output_dim, L, tau=float(getattr(args, "tau_max", 5.0) or 5.0))
+        return DartsNetwork(C, output_dim, L)
     if name == "resnet56_gkt":
         return resnet8_56(output_dim), resnet56_server(output_dim)
     logging.warning("unknown model %s → LogisticRegression fallback (reference behaviour)", name)

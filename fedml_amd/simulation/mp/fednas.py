@@ -1,6 +1,10 @@
-"""FedNAS over message passing (reference: `mpi_p2p_mp/fednas/*`): clients run DARTS search
-(weights + architecture alphas) on their shard; the server averages both and records the
-derived genotype each round. ``args.stage`` = ``search`` | ``train``."""
+"""FedNAS over message passing (reference: `mpi_p2p_mp/fednas/*`). ``args.stage``:
+
+* ``search`` — clients run DARTS (or GDAS) search (weights + architecture alphas) on their shard; the
+  server averages both (FedNASAggregator.__aggregate_weight / __aggregate_alpha) and records the derived
+  genotype each round;
+* ``train`` — the genotype-built ``NetworkCIFAR`` (``models/cv/darts/eval_net.py``) trains its weights
+  only; the server averages weights (FedNASAggregator.aggregate :66-74)."""
 import logging
 
 from ...trainers.nas import ModelTrainerNAS
@@ -11,7 +15,7 @@ class FedNASAggregator(FedAVGAggregator):
     def aggregate(self):
         averaged = super().aggregate()
         model = self.trainer.model
-        if hasattr(model, "genotype"):
+        if hasattr(model, "arch_parameters"):
             g = model.genotype()
             self.genotypes = getattr(self, "genotypes", []) + [g]
             logging.info("FedNAS genotype: %s", g)
@@ -25,5 +29,6 @@ def FedML_FedNAS_distributed(args, process_id, worker_number, comm, device, data
     out = run_fl(args, process_id, worker_number, comm, device, dataset, model, model_trainer,
                  aggregator_cls=FedNASAggregator, preprocessed_sampling_lists=preprocessed_sampling_lists)
     if out is not None:
-        out["genotype"] = model_trainer.model.genotype()
+        m = model_trainer.model
+        out["genotype"] = m.genotype() if hasattr(m, "arch_parameters") else getattr(m, "genotype_used", None)
     return out

@@ -1,10 +1,14 @@
-"""FedNAS local search trainer (reference: `mpi_p2p_mp/fednas/FedNASTrainer.py`): on each
-client, alternate a DARTS architecture step (Adam on the alphas from the validation split —
-first order, or the unrolled second-order gradient with ``unrolled: true``, Architect in
-``models/cv/darts_architect.py``) with an SGD weight step (train split); in ``stage == "train"``
-only weights move.
-The model is ``models.cv.darts.Network``; alphas live in the state dict so the FedAvg
-aggregator averages weights and architecture together."""
+"""FedNAS local trainer (reference: `mpi_p2p_mp/fednas/FedNASTrainer.py`).
+
+``stage: search`` (``search()``, :43-165): on each client, alternate a DARTS architecture step (Adam on the
+alphas from the validation split — first order, or the unrolled second-order gradient with
+``unrolled: true``, Architect in ``models/cv/darts_architect.py``) with an SGD weight step (train split).
+The model is ``models.cv.darts.Network`` (or the GDAS ``Network_GumbelSoftmax``); alphas live in the state
+dict so the FedAvg aggregator averages weights and architecture together.
+
+``stage: train`` (``train()``, :167-246): the genotype-built ``NetworkCIFAR`` trains its weights only — SGD
+with cosine annealing over the local epochs (to ``learning_rate_min``), the auxiliary head's loss added
+with ``auxiliary_weight``, drop-path probability ramped over the epochs, gradient clipping."""
 import logging
 
 import torch
@@ -24,6 +28,8 @@ class ModelTrainerNAS(ClientTrainer):
         args = args or self.args
         model = self.model.to(device)
         model.train()
+        if str(getattr(args, "stage", "search")) == "train" and not hasattr(model, "arch_parameters"):
+            return self._train_eval_net(model, train_data, device, args)
         crit = nn.CrossEntropyLoss()
         w_opt = torch.optim.SGD(model.weight_parameters(), lr=float(args.learning_rate),
                                 momentum=float(getattr(args, "momentum", 0.9) or 0.9),
@@ -56,6 +62,36 @@ class ModelTrainerNAS(ClientTrainer):
         logging.debug("client %s genotype %s", self.id, model.genotype())
         return getattr(self, "last_loss", None)
 
+    def _train_eval_net(self, model, train_data, device, args):
+        """``stage: train`` on the genotype network (FedNASTrainer.train / local_train)."""
+        crit = nn.CrossEntropyLoss()
+        epochs = int(args.epochs)
+        opt = torch.optim.SGD(model.parameters(), lr=float(args.learning_rate),
+                              momentum=float(getattr(args, "momentum", 0.9) or 0.9),
+                              weight_decay=float(getattr(args, "weight_decay", 3e-4) or 3e-4))
+        sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, float(epochs),
+                                                           eta_min=float(getattr(args, "learning_rate_min", 0.001)))
+        aux_w = float(getattr(args, "auxiliary_weight", 0.4))
+        dpp = float(getattr(args, "drop_path_prob", 0.2))
+        losses = []
+        for ep in range(epochs):
+            model.drop_path_prob = dpp * ep / max(1, epochs)
+            for x, y in train_data:
+                x, y = x.to(device), y.to(device)
+                opt.zero_grad(set_to_none=True)
+                logits, aux = model(x)
+                loss = crit(logits, y)
+                if aux is not None:
+                    loss = loss + aux_w * crit(aux, y)
+                loss.backward()
+                nn.utils.clip_grad_norm_(model.parameters(), float(getattr(args, "grad_clip", 5.0)))
+                opt.step()
+                losses.append(loss.detach())
+            sched.step()
+        if losses:
+            self.last_loss = float(torch.stack(losses).mean())
+        return getattr(self, "last_loss", None)
+
     @torch.no_grad()
     def test(self, test_data, device, args=None):
         model = self.model.to(device)
@@ -65,6 +101,8 @@ class ModelTrainerNAS(ClientTrainer):
         for x, y in test_data:
             x, y = x.to(device), y.to(device)
             out = model(x)
+            if isinstance(out, tuple):   # NetworkCIFAR: (logits, auxiliary logits)
+                out = out[0]
             loss += float(nn.functional.cross_entropy(out, y, reduction="sum"))
             correct += int((out.argmax(1) == y).sum())
             total += y.numel()

@@ -9,6 +9,8 @@ def run(rank, world, port, out_path, model_name, clients, counts_seed, shuffle=F
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
                        "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
     torch.set_num_threads(2)
+    # FEDML_TEST_DEVICE=cuda: every rank on cuda:0 (a multi-rank rehearsal on a one-GPU box, gloo collectives)
+    dev = torch.device("cuda:0" if os.environ.get("FEDML_TEST_DEVICE") == "cuda" else "cpu")
     from fedml_amd.arguments import Arguments
     from fedml_amd.data.synthetic import get_spec
     from fedml_amd.models import create
@@ -38,8 +40,12 @@ def run(rank, world, port, out_path, model_name, clients, counts_seed, shuffle=F
         model = create(args, spec.num_classes)
     g = torch.Generator().manual_seed(counts_seed)
     counts = [int(v) for v in torch.randint(8, 24, (clients,), generator=g)]
-    store = DeviceClientStore.synthetic_on_device(spec, counts, torch.device("cpu"), seed=0)
-    sim = RCCLSimulator(args, torch.device("cpu"), None, model, store=store)
+    store = DeviceClientStore.synthetic_on_device(spec, counts, dev, seed=0)
+    sim = RCCLSimulator(args, dev, None, model, store=store)
+    if dev.type == "cuda" and model_name == "resnet_shallow":
+        # the headline engine: native HIP ResNet step (fp32), HIP-graph replays
+        assert sim.engine.native_step is not None and sim.engine.native_step.dtype == torch.float32, rank
+        assert sim.engine.use_graphs
     die = os.environ.get("FEDML_TEST_DIE")   # "rank:round" — that rank's process vanishes before the round
     if die:
         dr, dround = (int(v) for v in die.split(":"))
@@ -53,8 +59,10 @@ def run(rank, world, port, out_path, model_name, clients, counts_seed, shuffle=F
     sim.run(int(os.environ.get("FEDML_TEST_ROUNDS", "2")))
     if die and rank == 0:
         assert sim.world_changes and sim.world_changes[0][1:] == (world, world - 1), sim.world_changes
+    if dev.type == "cuda":
+        assert sim.engine._graphs, "native step never replayed from a HIP graph"
     if rank == 0:
-        torch.save(sim.global_flat.clone(), out_path)
+        torch.save(sim.global_flat.detach().cpu().clone(), out_path)
     comm.destroy()
 
 

@@ -15,7 +15,7 @@ def test_unrolled_gradient_matches_exact_second_order():
     torch.manual_seed(0)
     torch.set_default_dtype(torch.float64)
     try:
-        m = Network(C=4, num_classes=3, layers=3, steps=2)   # normal + reduction cells
+        m = Network(C=4, num_classes=3, layers=3, steps=2, multiplier=2)   # normal + reduction cells
         args = Arguments.from_dict({"x": {"momentum": 0.9, "weight_decay": 3e-4, "arch_hvp_r": 1e-6}})
         arch = Architect(m, args)
         assert Architect(m, Arguments.from_dict({"x": {}})).r == 1e-2

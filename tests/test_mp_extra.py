@@ -110,6 +110,65 @@ def test_fednas_search():
     assert len(res["genotype"].normal) == 4
 
 
+def test_fednas_gdas_search():
+    from fedml_amd.models.cv.darts import Network_GumbelSoftmax
+    from fedml_amd.simulation.mp.fednas import FedML_FedNAS_distributed
+    a = _args("FedNAS", comm_round=1, learning_rate=0.025, frequency_of_the_test=0, stage="search")
+    ds = _image_dataset(n_clients=6, n=16, hw=8)
+    m = Network_GumbelSoftmax(C=4, num_classes=10, layers=2, steps=2, multiplier=2)
+    alphas0 = m.alphas_reduce.detach().clone()
+    res = run_message_passing(FedML_FedNAS_distributed, a, torch.device("cpu"), ds, m)
+    assert not torch.equal(res["global_model"]["alphas_reduce"], alphas0)
+    g, n_cnn, r_cnn = res["genotype"]
+    assert len(g.normal) == 4 and 0 <= n_cnn <= 4 and 0 <= r_cnn <= 4
+
+
+def test_fednas_train_stage_on_genotype_network():
+    """stage: train (FedNASTrainer.train / FedNASAggregator.aggregate): the genotype-built NetworkCIFAR with its
+    auxiliary head trains weights only; the server averages weights and keeps the genotype."""
+    from fedml_amd.models.cv.darts import FedNAS_V1, NetworkCIFAR
+    from fedml_amd.simulation.mp.fednas import FedML_FedNAS_distributed
+    a = _args("FedNAS", comm_round=2, learning_rate=0.025, frequency_of_the_test=1, stage="train", epochs=2,
+              auxiliary=True, auxiliary_weight=0.4, drop_path_prob=0.2, learning_rate_min=0.001,
+              client_num_in_total=4, client_num_per_round=2)
+    ds = _image_dataset(n_clients=4, n=8, hw=32)
+    m = NetworkCIFAR(4, 10, 3, True, "FedNAS_V1")
+    before = {k: v.clone() for k, v in m.state_dict().items()}
+    res = run_message_passing(FedML_FedNAS_distributed, a, torch.device("cpu"), ds, m)
+    assert res["genotype"] == FedNAS_V1
+    moved = [k for k in before if before[k].is_floating_point() and not torch.equal(before[k], res["global_model"][k])]
+    assert any(k.startswith("auxiliary_head.") for k in moved) and any(k.startswith("cells.") for k in moved)
+    assert not any("alphas" in k for k in res["global_model"])
+
+
+def test_darts_search_space_is_the_reference_one():
+    """8 primitives, 4-step cells with multiplier 4 by default (reference genotypes.py:5-14,
+    model_search.py:209); the GDAS net runs only the sampled op per edge."""
+    import torch.nn.functional as F
+    from fedml_amd.models.cv.darts import PRIMITIVES, Network, Network_GumbelSoftmax
+    assert PRIMITIVES == ["none", "max_pool_3x3", "avg_pool_3x3", "skip_connect", "sep_conv_3x3", "sep_conv_5x5",
+                          "dil_conv_3x3", "dil_conv_5x5"]
+    m = Network(C=4, num_classes=5, layers=3)
+    assert m.alphas_normal.shape == (14, 8) and m._steps == 4 and m._multiplier == 4
+    assert m(torch.randn(2, 3, 16, 16)).shape == (2, 5)
+    assert len(m.genotype().normal) == 8
+    g = Network_GumbelSoftmax(C=4, num_classes=5, layers=3)
+    calls = []
+    for mod in g.modules():
+        if isinstance(mod, torch.nn.Conv2d) and mod.groups > 1:
+            mod.register_forward_hook(lambda *_: calls.append(1))
+    g(torch.randn(2, 3, 16, 16))
+    dense = []
+    for mod in m.modules():
+        if isinstance(mod, torch.nn.Conv2d) and mod.groups > 1:
+            mod.register_forward_hook(lambda *_: dense.append(1))
+    m(torch.randn(2, 3, 16, 16))
+    assert len(calls) < len(dense) / 2        # one op per edge instead of all eight
+    loss = F.cross_entropy(g(torch.randn(2, 3, 16, 16)), torch.tensor([0, 1]))
+    loss.backward()
+    assert g.alphas_normal.grad is not None and g.alphas_normal.grad.abs().sum() > 0   # straight-through
+
+
 def test_fedseg():
     from fedml_amd.data.segmentation import load_synthetic_segmentation
     from fedml_amd.models.cv.segmentation import UNet
