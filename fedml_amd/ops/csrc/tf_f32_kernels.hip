@@ -50,12 +50,16 @@ struct Segs {        // row segments of an operand (≤ 4 arena slots); one segm
   int n;
 };
 
+// Constant-index selects only: a runtime index into the by-value kernel-argument struct would be lowered to
+// a global load of the kernarg segment plus an s_waitcnt vmcnt(0) — which also waits for every prefetch
+// load in flight, serialising the K loop.
 __device__ __forceinline__ int64_t seg_row(const Segs& s, int r, int rowlen) {
-  int i = 0;
-#pragma unroll
-  for (int t = 1; t < 4; ++t)
-    if (t < s.n && r >= s.lo[t]) i = t;
-  return s.off[i] + (int64_t)(r - s.lo[i]) * rowlen;
+  int64_t off = s.off[0];
+  int lo = s.lo[0];
+  if (s.n > 1 && r >= s.lo[1]) { off = s.off[1]; lo = s.lo[1]; }
+  if (s.n > 2 && r >= s.lo[2]) { off = s.off[2]; lo = s.lo[2]; }
+  if (s.n > 3 && r >= s.lo[3]) { off = s.off[3]; lo = s.lo[3]; }
+  return off + (int64_t)(r - lo) * rowlen;
 }
 
 struct Args {

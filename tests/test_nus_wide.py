@@ -38,3 +38,26 @@ def test_two_and_three_party_parsing(tmp_path):
     assert np.array_equal(np.r_[y[:, 0], y_t[:, 0]], expect)
     (a, b, c, y3), _ = NUS_WIDE_load_three_party_data(str(tmp_path), ["sky", "water", "person"])
     assert b.shape[1] == 3 and c.shape[1] == 3 and len(a) == len(y3) == int(0.8 * n)
+
+
+def test_lending_club_two_and_three_party(tmp_path):
+    """Lending Club VFL parties (reference data/lending_club_loan/lending_club_dataset.py:187-287) from a
+    synthetic loan.csv with the dataset's columns: 2018 loans only, bad-loan target, standardised features,
+    feature-group party split, 80/20 train/test, processed CSV cached."""
+    import numpy as np
+    from fedml_amd.data import lending_club as lc
+    lc.write_synthetic_loan_csv(str(tmp_path / "loan.csv"), n=300)
+    d = str(tmp_path) + "/"
+    train, test = lc.loan_load_two_party_data(d)
+    assert (tmp_path / "processed_loan.csv").exists()
+    Xa, Xb, y = train
+    n2018 = len(lc.prepare_data(str(tmp_path / "loan.csv")))
+    assert Xa.shape == (int(0.8 * n2018), len(lc.QUALIFICATION + lc.LOAN))
+    assert Xb.shape[1] == len(lc.DEBT + lc.REPAYMENT + lc.MULTI_ACC + lc.MAL_BEHAVIOR)
+    assert y.shape == (Xa.shape[0], 1) and set(np.unique(y)) <= {0.0, 1.0} and not np.isnan(y).any()
+    full = np.concatenate([Xa, test[0]])
+    assert np.allclose(full.mean(0), 0, atol=1e-9) and np.allclose(full.std(0)[full.std(0) > 0], 1, atol=1e-9)
+    tr3, te3 = lc.loan_load_three_party_data(d)
+    assert len(tr3) == 4 and tr3[1].shape[1] == len(lc.DEBT + lc.REPAYMENT)
+    assert tr3[2].shape[1] == len(lc.MULTI_ACC + lc.MAL_BEHAVIOR)
+    assert np.allclose(tr3[0], Xa, rtol=1e-12, atol=1e-12)
