@@ -27,6 +27,7 @@ from .fl_ops import (
     quantize_fp8,
     dequantize_fp8_axpy,
     topk_abs,
+    topk_compress_accumulate,
     scatter_axpy,
     softmax_xent_fwd_bwd,
     FusedCrossEntropy,

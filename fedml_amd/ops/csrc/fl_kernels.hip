@@ -6,6 +6,8 @@
 // is [P]. All are launched on the caller's HIP stream (graph-capturable: no
 // allocation, no sync, no host-side scalars that change between replays unless
 // passed by device pointer).
+#include <algorithm>
+
 #include "common.h"
 
 // =====================================================================================
@@ -823,6 +825,165 @@ FA_EXPORT int fa_topk_abs(const float* x, int64_t n, int64_t k, uint32_t* state,
     hipLaunchKernelGGL(topk_select_kernel, dim3(1), dim3(64), 0, stream, hist, pass, state);
   }
   hipLaunchKernelGGL(topk_compact_kernel, dim3(grid), dim3(256), 0, stream, x, n, state, idx, val, residual, k);
+  return (int)hipGetLastError();
+}
+
+// ---- batched top-k with error feedback over the [C, P] client stack (8 launches for any C) ----
+// Client c's update Δ_c = params_c − glob + r_c keeps its k largest |Δ_c| entries; the rest becomes its new
+// residual r_c. The same 3-pass radix select as topk_abs, but every pass runs all clients in ONE grid
+// (blockIdx.y = client, per-client histogram and state), Δ_c is recomputed from the arenas in each pass
+// (reading params + residual costs less than writing and re-reading a [C, P] scratch), and the final pass
+// applies the selection and accumulates acc = Σ_c w_c·(glob + topk(Δ_c)) with one thread per element
+// looping over the clients — no atomics on acc, no per-client host loop.
+// state[c][0] prefix bits, [1] k left inside the prefix, [3] tie cursor.
+__global__ __launch_bounds__(256) void topkb_init_kernel(uint32_t* __restrict__ state, uint32_t* __restrict__ hist,
+                                                         int C, uint32_t k) {
+  const int c = blockIdx.x;
+  for (int b = threadIdx.x; b < 2048; b += blockDim.x) hist[(int64_t)c * 2048 + b] = 0;
+  if (threadIdx.x < 8) state[c * 8 + threadIdx.x] = (threadIdx.x == 1) ? k : 0u;
+}
+
+__device__ __forceinline__ float4 topkb_delta(const float* __restrict__ pc, const float* __restrict__ glob,
+                                              const float* __restrict__ res, int64_t i) {
+  const float4 p = *reinterpret_cast<const float4*>(pc + i);
+  const float4 g = *reinterpret_cast<const float4*>(glob + i);
+  float4 v = make_float4(p.x - g.x, p.y - g.y, p.z - g.z, p.w - g.w);
+  if (res) {
+    const float4 r = *reinterpret_cast<const float4*>(res + i);
+    v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
+  }
+  return v;
+}
+
+// grid (blocks per client, C); n % 4 == 0, rows 16-byte aligned
+__global__ __launch_bounds__(256) void topkb_hist_kernel(const float* __restrict__ params, int64_t ldp,
+                                                         const float* __restrict__ glob,
+                                                         const uint64_t* __restrict__ rows,
+                                                         const float* __restrict__ weights, int64_t n, int pass,
+                                                         const uint32_t* __restrict__ state,
+                                                         uint32_t* __restrict__ hist) {
+  const int c = blockIdx.y;
+  if (weights[c] == 0.f) return;   // block-uniform: padding / dropped slots
+  __shared__ uint32_t h[2048];
+  const TopkPass ps = kTopkPasses[pass];
+  const int nb = 1 << ps.bits;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x) h[b] = 0;
+  __syncthreads();
+  const uint32_t prefix = state[c * 8];
+  const int hi_shift = ps.shift + ps.bits;
+  const float* pc = params + (int64_t)c * ldp;
+  const float* res = reinterpret_cast<const float*>(rows ? rows[c] : 0ull);
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n;
+       i += (int64_t)gridDim.x * blockDim.x * 4) {
+    const float4 v = topkb_delta(pc, glob, res, i);
+    const float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint32_t a = __float_as_uint(e[j]) & 0x7fffffffu;
+      if (hi_shift < 31 && (a >> hi_shift) != (prefix >> hi_shift)) continue;
+      atomicAdd(&h[(a >> ps.shift) & (nb - 1)], 1u);
+    }
+  }
+  __syncthreads();
+  uint32_t* hc = hist + (int64_t)c * 2048;
+  for (int b = threadIdx.x; b < nb; b += blockDim.x)
+    if (h[b]) atomicAdd(&hc[b], h[b]);
+}
+
+// one wave per client: lane l owns 32 bins counted from the top, a wave prefix sum finds the lane holding
+// the k-th element, that lane walks its bins; the histogram is cleared for the next pass
+__global__ __launch_bounds__(64) void topkb_select_kernel(uint32_t* __restrict__ hist, int pass,
+                                                          uint32_t* __restrict__ state,
+                                                          const float* __restrict__ weights) {
+  const int c = blockIdx.x;
+  if (weights[c] == 0.f) return;
+  const TopkPass ps = kTopkPasses[pass];
+  const int nb = 1 << ps.bits;
+  const int per = nb / 64;   // 32 (11-bit passes) or 8 (9-bit pass)
+  uint32_t* hc = hist + (int64_t)c * 2048;
+  const int lane = threadIdx.x;
+  const int top = nb - 1 - lane * per;   // this lane's bins: top, top-1, …, top-per+1
+  uint32_t mine = 0;
+  for (int j = 0; j < per; ++j) mine += hc[top - j];
+  uint32_t incl = mine;   // inclusive scan from lane 0 (the highest bins)
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  const uint32_t k = state[c * 8 + 1];
+  const uint64_t hit = __ballot(incl >= k);
+  const int owner = hit ? __ffsll((long long)hit) - 1 : 63;
+  if (lane == owner) {
+    uint32_t cum = incl - mine;
+    int digit = top - per + 1;
+    for (int j = 0; j < per; ++j) {
+      const uint32_t hb = hc[top - j];
+      if (cum + hb >= k) {
+        digit = top - j;
+        break;
+      }
+      cum += hb;
+    }
+    state[c * 8] |= ((uint32_t)digit << ps.shift);
+    state[c * 8 + 1] = k - cum;
+  }
+  __syncthreads();
+  for (int b = lane; b < nb; b += 64) hc[b] = 0;
+}
+
+// one thread per 4 elements, looping over the clients: take |Δ| > T_c and the first `ties` entries equal
+// to T_c; acc = wsum·glob + Σ w_c·taken Δ_c; residual ← untaken Δ_c (0 where taken)
+__global__ __launch_bounds__(256) void topkb_apply_kernel(const float* __restrict__ params, int64_t ldp, int C,
+                                                          const float* __restrict__ glob,
+                                                          const uint64_t* __restrict__ rows,
+                                                          const float* __restrict__ weights, int64_t n,
+                                                          uint32_t* __restrict__ state, float* __restrict__ acc) {
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n;
+       i += (int64_t)gridDim.x * blockDim.x * 4) {
+    const float4 g = *reinterpret_cast<const float4*>(glob + i);
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    float wsum = 0.f;
+    for (int c = 0; c < C; ++c) {
+      const float w = weights[c];
+      if (w == 0.f) continue;
+      wsum += w;
+      float* res = reinterpret_cast<float*>(rows ? rows[c] : 0ull);
+      const float4 v4 = topkb_delta(params + (int64_t)c * ldp, glob, res, i);
+      const uint32_t T = state[c * 8], ties = state[c * 8 + 1];
+      float e[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t bits = __float_as_uint(e[j]) & 0x7fffffffu;
+        bool take = bits > T;
+        if (!take && bits == T) take = atomicAdd(&state[c * 8 + 3], 1u) < ties;
+        if (take) {
+          a[j] += w * e[j];
+          e[j] = 0.f;
+        }
+      }
+      if (res) *reinterpret_cast<float4*>(res + i) = make_float4(e[0], e[1], e[2], e[3]);
+    }
+    *reinterpret_cast<float4*>(acc + i) =
+        make_float4(a[0] + wsum * g.x, a[1] + wsum * g.y, a[2] + wsum * g.z, a[3] + wsum * g.w);
+  }
+}
+
+// state: C·8 uint32, hist: C·2048 uint32 scratch; rows: C residual-row pointers (0 = none) or null
+FA_EXPORT int fa_topk_compress_accumulate(const float* params, int64_t ldp, int C, const float* glob,
+                                          const uint64_t* rows, const float* weights, int64_t n, int64_t k,
+                                          uint32_t* state, uint32_t* hist, float* acc, hipStream_t stream) {
+  if (C <= 0 || C > 65535 || n <= 0 || (n & 3) || (ldp & 3) || k <= 0 || k > n || k > 0xffffffffll)
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(topkb_init_kernel, dim3(C), dim3(256), 0, stream, state, hist, C, (uint32_t)k);
+  const int per_client = (int)std::max<int64_t>(1, std::min<int64_t>((n / 4 + 255) / 256, std::max(1, 4096 / C)));
+  for (int pass = 0; pass < 3; ++pass) {
+    hipLaunchKernelGGL(topkb_hist_kernel, dim3(per_client, C), dim3(256), 0, stream, params, ldp, glob, rows,
+                       weights, n, pass, state, hist);
+    hipLaunchKernelGGL(topkb_select_kernel, dim3(C), dim3(64), 0, stream, hist, pass, state, weights);
+  }
+  hipLaunchKernelGGL(topkb_apply_kernel, dim3(fa_grid(n / 4, 256, 8192)), dim3(256), 0, stream, params, ldp, C, glob,
+                     rows, weights, n, state, acc);
   return (int)hipGetLastError();
 }
 

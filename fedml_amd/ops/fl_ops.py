@@ -445,6 +445,7 @@ def dequantize_fp8_axpy(q, scales, w, acc):
 
 class _TopkScratch:
     cache = {}
+    batched = {}   # (device, C) → (state [C·8], hist [C·2048]) of topk_compress_accumulate
 
     @classmethod
     def get(cls, device):
@@ -476,6 +477,43 @@ def topk_abs(x, k, residual=None):
         r[i] = 0.0
         residual.copy_(r.view_as(residual))
     return i.to(torch.int32), val
+
+
+def topk_compress_accumulate(params, glob, residual_rows, weights, k, out):
+    """All C clients of the [C, P] stack in one batched radix select (8 launches for any C): client c's
+    update Δ_c = params[c] − glob + r_c keeps its k largest |Δ_c| entries (exact, ties cut by count), the rest
+    becomes its new residual r_c (``residual_rows``: list of C fp32 [P] rows or None entries, or None), and
+    out = Σ_c w_c·(glob + topk(Δ_c)). Slots with w_c = 0 are skipped (their rows untouched). ``weights``
+    stays on the device."""
+    C, P = params.shape[0], glob.numel()
+    k = int(min(max(int(k), 1), P))
+    if use_native(params) and P % 4 == 0 and params.stride(0) % 4 == 0:
+        key = (str(params.device), C)
+        sc = _TopkScratch.batched.get(key)
+        if sc is None:
+            sc = _TopkScratch.batched[key] = (torch.zeros(C * 8, dtype=torch.int32, device=params.device),
+                                              torch.zeros(C * 2048, dtype=torch.int32, device=params.device))
+        rows = torch.tensor([r.data_ptr() if r is not None else 0 for r in residual_rows]
+                            if residual_rows is not None else [0] * C, dtype=torch.int64).to(params.device,
+                                                                                             non_blocking=True)
+        rc = _fn("fa_topk_compress_accumulate")(_p(params), _i64(params.stride(0)), _c.c_int(C), _p(glob), _p(rows),
+                                                _p(weights.to(torch.float32).contiguous()), _i64(P), _i64(k),
+                                                _p(sc[0]), _p(sc[1]), _p(out), _stream(params))
+        _check(rc, "fa_topk_compress_accumulate")
+        return out
+    w_host = weights.to(torch.float32).tolist()
+    acc = torch.zeros(P, dtype=torch.float32, device=params.device)
+    for c, wc in enumerate(w_host):
+        if wc == 0.0:
+            continue
+        r = residual_rows[c] if residual_rows is not None else None
+        d = params[c].to(torch.float32) - glob
+        if r is not None:
+            d = d + r
+        idx, val = topk_abs(d, k, residual=r)
+        acc.index_add_(0, idx.long(), wc * val)
+    out.copy_(acc + float(sum(w_host)) * glob)
+    return out
 
 
 def scatter_axpy(idx, val, w, acc):

@@ -240,18 +240,3 @@ def head_bwd(dpool, out, y3, yd, gpre, stats, C, N, HW, Ch, NS, nimg=None):
 def nchw_to_nhwc_pad(x, y, CN, Cin, HW, Cpad):
     rc = _fnp("fa_nchw_to_nhwc_pad", y)(_p(x), _p(y), _i64(CN), _i(Cin), _i(HW), _i(Cpad), _stream(x))
     _check(rc, "fa_nchw_to_nhwc_pad")
-
-
-class NativeBatchedOps:
-    """Marker object handed to the fx interpreter; the native executor is model-level instead."""
-
-    def __init__(self, C, compute_dtype):
-        _native.lib(required=True)
-        self.C = C
-        self.compute_dtype = compute_dtype
-
-    def supports_conv(self, m, x):
-        return False
-
-    def conv2d(self, x, w, b, C, m):  # pragma: no cover - not used (model-level executor)
-        raise NotImplementedError

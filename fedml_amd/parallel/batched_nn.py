@@ -143,10 +143,17 @@ def bgroup_norm(x, C, groups, weight, bias, eps):
 
 
 def blinear(x, w, b, C):
-    """x [B, C·in] (or [B, ..., C·in] for sequence inputs); w [C, out, in]; b [C, out] → [B, C·out]."""
+    """x [B, C·in] (or [B, ..., C·in] for sequence inputs); w [C, out, in]; b [C, out] → [B, C·out].
+    fp32 on the GPU: the hand-written client-batched GEMM (``ops.transformer_ops.client_linear``, exact
+    fp32 matrix-core products; weight/bias gradients straight into the gradient-arena views); otherwise
+    one strided-batched library GEMM."""
     lead = x.shape[:-1]
     fin = x.shape[-1] // C
     xx = x.reshape(-1, C, fin).transpose(0, 1)           # [C, N, in]
+    if x.is_cuda and x.dtype == torch.float32 and w.dtype == torch.float32 and xx.shape[1] > 0:
+        from ..ops.transformer_ops import client_linear
+        y = client_linear(xx.contiguous(), [w], [b] if b is not None else None)
+        return y.transpose(0, 1).reshape(*lead, C * w.shape[1])
     if b is not None:
         y = torch.baddbmm(b.unsqueeze(1), xx, w.transpose(1, 2))
     else:
@@ -164,7 +171,6 @@ class BatchedInterpreter:
         self.layout = layout
         self.C = C
         self.modules = dict(self.gm.named_modules())
-        self.native = None  # set by the engine: ops.nn_ops-backed fast path
         self.deferred = []  # BN running-stat updates, applied after backward by ``flush_deferred``
         for n in self.gm.graph.nodes:
             if n.op == "call_function" and n.target in (torch.cat, torch.stack):
@@ -220,15 +226,12 @@ class BatchedInterpreter:
     def _call_module(self, name, m, args, params, training, sample_mask, active):
         x = args[0]
         C = self.C
-        nat = self.native
         if isinstance(m, nn.Conv2d):
             w = params[f"{name}.weight"]
             b = params.get(f"{name}.bias")
             if w.dtype != x.dtype:
                 w = w.to(x.dtype)
                 b = b.to(x.dtype) if b is not None else None
-            if nat is not None and nat.supports_conv(m, x):
-                return nat.conv2d(x, w, b, C, m)
             return bconv2d(x, w, b, C, m.stride, m.padding, m.dilation, m.groups)
         if isinstance(m, nn.BatchNorm2d):
             rm = params.get(f"{name}.running_mean")

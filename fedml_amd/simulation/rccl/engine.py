@@ -169,7 +169,6 @@ class ClientBatchEngine:
         self.clip_grad_norm = float(cg) if cg not in (None, "", 0, 0.0) else None
         _LIVE_ENGINES.add(self)
         self.use_graphs = self.device.type == "cuda" and os.environ.get("FEDML_AMD_HIP_GRAPHS", "1") != "0"
-        self.native = None
         self.native_step = None
         from ...utils import determinism
         self.deterministic = determinism.enabled(args)
@@ -762,24 +761,14 @@ class ClientBatchEngine:
             return out, nb
         if method != "topk":
             raise ValueError(f"unknown compression {method}")
-        acc.zero_()
-        w_host = w.tolist()     # top-k: one host read of the C weights per round
-        delta = torch.empty(self.P, dtype=torch.float32, device=self.device)
-        nbytes = 0
+        # top-k: every client's exact radix select in one batched grid, the sparse updates accumulated in
+        # the same pass (ops.topk_compress_accumulate: 8 launches for any C, no host loop, no sync)
         k = max(1, int(self.P * ratio))
-        for c, wc in enumerate(w_host):
-            if wc == 0.0 or int(client_ids[c]) < 0:
-                continue
-            r = residual[int(client_ids[c])]
-            torch.sub(self.params[c], global_flat, out=delta)
-            delta.add_(r)
-            idx, val = ops.topk_abs(delta, k, residual=r)
-            ops.scatter_axpy(idx, val, wc, acc)
-            nbytes += k * 8
-        total = float(sum(w_host))
-        acc.add_(global_flat, alpha=total)
-        out[self.P:].fill_(total)
-        return out, nbytes
+        rows = [residual[int(c)] if int(c) >= 0 else None for c in client_ids] if residual is not None else None
+        ops.topk_compress_accumulate(self.params, global_flat, rows, w, k, acc)
+        out[self.P:].copy_(w.sum().view(1))
+        n = n_upload if n_upload is not None else int((w != 0).sum())
+        return out, k * 8 * n
 
     @torch.no_grad()
     def evaluate(self, store, slots, batch_size: int = 256):

@@ -170,6 +170,41 @@ def test_topk_exact(n, k):
     assert torch.allclose((acc + r).cpu(), x)
 
 
+@pytest.mark.parametrize("C,P,k,ties", [(5, 40000, 400, False), (3, 4096, 1, False), (4, 20000, 2000, True),
+                                         (32, 8192, 81, False)])
+def test_topk_compress_accumulate_batched(C, P, k, ties):
+    """Every client's exact top-k with error feedback in one batched radix select + fused accumulation,
+    against the per-client torch reference (same Δ = w − g + r, same k, weight-0 slot untouched)."""
+    g = torch.Generator().manual_seed(0)
+    params = torch.randn(C, P, generator=g)
+    glob = torch.randn(P, generator=g)
+    res = [torch.randn(P, generator=g) * 0.1 for _ in range(C)]
+    if ties:   # many exact duplicates of |Δ| around the threshold
+        params = (params * 4).round() / 4
+        glob = (glob * 4).round() / 4
+        res = [torch.zeros(P) for _ in range(C)]
+    w = torch.rand(C, generator=g) + 0.5
+    w[1 % C] = 0.0 if C > 1 else w[0]
+    out = torch.empty(P, device=DEV)
+    rows_d = [r.to(DEV) for r in res]
+    ops.topk_compress_accumulate(params.to(DEV), glob.to(DEV), rows_d, w.to(DEV), k, out)
+    out, rows_d = out.cpu(), [r.cpu() for r in rows_d]
+    ref = glob * float(w.sum())
+    for c in range(C):
+        d = params[c] - glob + res[c]
+        if w[c] == 0:
+            assert torch.equal(rows_d[c], res[c])       # skipped slot: row untouched
+            continue
+        taken = rows_d[c] == 0
+        taken &= d != 0
+        assert int(taken.sum()) == k, (c, int(taken.sum()))
+        thr = torch.topk(d.abs(), k).values.min()
+        assert (d[taken].abs() >= thr).all() and (d[~taken].abs() <= thr).all()
+        assert torch.equal(rows_d[c][~taken], d[~taken])     # residual = untaken Δ
+        ref = ref + w[c] * torch.where(taken, d, torch.zeros_like(d))
+    assert torch.allclose(out, ref, atol=1e-5, rtol=1e-5)
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 def test_softmax_xent(dtype):
     R, K = 1000, 100
