@@ -1,13 +1,17 @@
 """Pickle-free wire format for Messages.
 
-    frame := magic(4) | header_len(u32) | header JSON (utf-8) | blob_0 | blob_1 | ...
+    frame := magic(4) | header_len(u32) | header JSON (utf-8, space-padded) | blob_0 | blob_1 | ...
 
 The header is the message dict where every tensor / ndarray is replaced by
 ``{"__t__": i, "dtype": ..., "shape": [...], "off": byte_offset, "nbytes": n}`` pointing
-into the blob area; dicts/lists nest. state_dicts therefore cost one memcpy per tensor
-(or one for a flat arena buffer), instead of the reference's pickle of a dict of tensors
-(`mpi_send_thread.py:27`, `grpc_comm_manager.py:68`) — and nothing executable is ever
-deserialised.
+into the blob area; dicts/lists nest. Nothing executable is ever deserialised (the reference pickles a
+dict of tensors: `mpi_send_thread.py:27`, `grpc_comm_manager.py:68`).
+
+Copies: ``encode_segments`` returns the frame as a list of buffers — the header plus a zero-copy view of
+every CPU tensor (a device tensor costs its one device→host copy) — which the TCP transport writes
+with one ``sendall`` per segment (no concatenation); ``decode`` of a writable buffer (the transport's
+receive ``bytearray``) returns tensors that VIEW the frame (no per-tensor copy). Blobs start on 16-byte
+boundaries of the frame, so every view is aligned.
 """
 import json
 import struct
@@ -29,30 +33,38 @@ def _dtype_name(t: torch.Tensor) -> str:
     return str(t.dtype).replace("torch.", "")
 
 
+_ALIGN = 16
+
+
+def _add_blob(blobs, offset, raw) -> int:
+    """Append ``raw`` (bytes-like) at the next 16-byte boundary of the blob area; returns its offset."""
+    pad = -offset[0] % _ALIGN
+    if pad:
+        blobs.append(bytes(pad))
+        offset[0] += pad
+    at = offset[0]
+    blobs.append(raw)
+    offset[0] += len(raw)
+    return at
+
+
 def encode_obj(obj, blobs, offset):
     if isinstance(obj, torch.Tensor):
         t = obj.detach()
         if t.device.type != "cpu":
             t = t.cpu()
         t = t.contiguous()
-        if t.dtype == torch.bfloat16:
-            raw = t.view(torch.int16).numpy().tobytes()
-        else:
-            raw = t.numpy().tobytes()
-        desc = {"__t__": "torch", "dtype": _dtype_name(t), "shape": list(t.shape), "off": offset[0],
-                "nbytes": len(raw)}
-        blobs.append(raw)
-        offset[0] += len(raw)
-        return desc
+        a = t.view(torch.int16).numpy() if t.dtype == torch.bfloat16 else t.numpy()
+        raw = memoryview(a.reshape(-1)).cast("B")      # a view: the tensor's own bytes
+        off = _add_blob(blobs, offset, raw)
+        return {"__t__": "torch", "dtype": _dtype_name(t), "shape": list(t.shape), "off": off, "nbytes": len(raw)}
     if isinstance(obj, np.ndarray):
         a = np.ascontiguousarray(obj)
         if a.dtype == object:
             raise TypeError("object arrays are not serialisable (no pickle)")
-        raw = a.tobytes()
-        desc = {"__t__": "numpy", "dtype": a.dtype.str, "shape": list(a.shape), "off": offset[0], "nbytes": len(raw)}
-        blobs.append(raw)
-        offset[0] += len(raw)
-        return desc
+        raw = memoryview(a.reshape(-1)).cast("B")
+        off = _add_blob(blobs, offset, raw)
+        return {"__t__": "numpy", "dtype": a.dtype.str, "shape": list(a.shape), "off": off, "nbytes": len(raw)}
     if isinstance(obj, dict):
         kind = "od" if isinstance(obj, OrderedDict) else "d"
         return {"__d__": kind, "items": [[encode_obj(k, blobs, offset), encode_obj(v, blobs, offset)]
@@ -64,10 +76,8 @@ def encode_obj(obj, blobs, offset):
     if isinstance(obj, (np.floating,)):
         return float(obj)
     if isinstance(obj, bytes):
-        desc = {"__t__": "bytes", "off": offset[0], "nbytes": len(obj)}
-        blobs.append(obj)
-        offset[0] += len(obj)
-        return desc
+        off = _add_blob(blobs, offset, obj)
+        return {"__t__": "bytes", "off": off, "nbytes": len(obj)}
     if obj is None or isinstance(obj, (int, float, str, bool)):
         return obj
     raise TypeError(f"cannot serialise {type(obj).__name__} (no pickle on the wire)")
@@ -80,15 +90,18 @@ def decode_obj(obj, blob: memoryview):
             raw = blob[obj["off"]:obj["off"] + obj["nbytes"]]
             if kind == "bytes":
                 return bytes(raw)
+            writable = not raw.readonly   # views of a writable frame; a read-only frame is copied
             if kind == "numpy":
-                return np.frombuffer(raw, dtype=np.dtype(obj["dtype"])).reshape(obj["shape"]).copy()
+                arr = np.frombuffer(raw, dtype=np.dtype(obj["dtype"])).reshape(obj["shape"])
+                return arr if writable else arr.copy()
             dt = _TORCH_DTYPES[obj["dtype"]]
+            if obj["nbytes"] == 0:
+                return torch.empty(obj["shape"], dtype=dt)
             if dt == torch.bfloat16:
-                arr = np.frombuffer(raw, dtype=np.int16).copy()
-                return torch.from_numpy(arr).view(torch.bfloat16).reshape(obj["shape"])
-            npdt = torch.empty(0, dtype=dt).numpy().dtype
-            arr = np.frombuffer(raw, dtype=npdt).copy()
-            return torch.from_numpy(arr).reshape(obj["shape"])
+                t = torch.frombuffer(raw if writable else bytearray(raw), dtype=torch.int16).view(torch.bfloat16)
+            else:
+                t = torch.frombuffer(raw if writable else bytearray(raw), dtype=dt)
+            return t.reshape(obj["shape"])
         if "__d__" in obj:
             d = OrderedDict() if obj["__d__"] == "od" else {}
             for k, v in obj["items"]:
@@ -101,10 +114,18 @@ def decode_obj(obj, blob: memoryview):
     return obj
 
 
-def encode(obj) -> bytes:
+def encode_segments(obj):
+    """The frame as [head, blob views...] (see the module docstring) and its total length."""
     blobs = []
     header = json.dumps(encode_obj(obj, blobs, [0])).encode("utf-8")
-    return MAGIC + struct.pack("<I", len(header)) + header + b"".join(blobs)
+    header += b" " * (-(8 + len(header)) % _ALIGN)     # the blob area starts on a 16-byte boundary
+    segs = [MAGIC + struct.pack("<I", len(header)) + header] + blobs
+    return segs, sum(len(b) for b in segs)
+
+
+def encode(obj) -> bytes:
+    segs, _ = encode_segments(obj)
+    return b"".join(segs)
 
 
 def decode(buf) -> object:
@@ -118,6 +139,10 @@ def decode(buf) -> object:
 
 def encode_message(msg) -> bytes:
     return encode(msg.get_params())
+
+
+def encode_message_segments(msg):
+    return encode_segments(msg.get_params())
 
 
 def decode_message(buf):

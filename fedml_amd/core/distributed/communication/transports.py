@@ -22,7 +22,7 @@ from typing import Dict, Optional, Tuple
 
 from .base_com_manager import QueueCommManager
 from .message import Message
-from .serialization import decode_message, encode_message
+from .serialization import decode_message, encode_message, encode_message_segments
 
 
 # ------------------------------------------------------------------------------------------------
@@ -81,7 +81,7 @@ def _recv_exact(sock, n):
         if k == 0:
             raise ConnectionError("peer closed")
         got += k
-    return bytes(buf)
+    return buf   # decoded in place: the message's tensors view this buffer
 
 
 class TCPCommManager(QueueCommManager):
@@ -141,14 +141,16 @@ class TCPCommManager(QueueCommManager):
 
     def send_message(self, msg: Message):
         dst = int(msg.get_receiver_id())
-        buf = encode_message(msg)
+        segs, n = encode_message_segments(msg)
         with self._send_locks[dst]:
             if dst == self.rank:
-                self.deliver(decode_message(buf))
+                self.deliver(decode_message(bytearray(b"".join(segs))))
                 return
             c = self._conn(dst)
-            c.sendall(struct.pack("<Q", len(buf)) + buf)
-        self.bytes_sent += len(buf)
+            c.sendall(struct.pack("<Q", n) + segs[0])
+            for b in segs[1:]:        # tensor bytes straight from the tensors (no frame concatenation)
+                c.sendall(b)
+        self.bytes_sent += n
 
     def stop_receive_message(self):
         super().stop_receive_message()

@@ -33,8 +33,9 @@ class ClientMasterManager(FedMLClientManager):
                 self.trainer.sync_model()
 
     def handle_message_init(self, msg):
-        self.note_global(msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS))
-        self.trainer.update_model(msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS))
+        params = self.resolve_payload(msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS))
+        self.note_global(params)
+        self.trainer.update_model(params)
         silo = int(msg.get(MyMessage.MSG_ARG_KEY_CLIENT_INDEX))
         self.round_idx = int(msg.get(MyMessage.MSG_ARG_KEY_ROUND_INDEX, 0))
         self._sync_silo(False, silo)
@@ -42,8 +43,9 @@ class ClientMasterManager(FedMLClientManager):
         self._train_and_send()
 
     def handle_message_receive_model_from_server(self, msg):
-        self.note_global(msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS))
-        self.trainer.update_model(msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS))
+        params = self.resolve_payload(msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS))
+        self.note_global(params)
+        self.trainer.update_model(params)
         silo = int(msg.get(MyMessage.MSG_ARG_KEY_CLIENT_INDEX))
         self.round_idx = int(msg.get(MyMessage.MSG_ARG_KEY_ROUND_INDEX, self.round_idx + 1))
         self._sync_silo(False, silo)
@@ -56,7 +58,8 @@ class ClientMasterManager(FedMLClientManager):
         self.trainer.cleanup_pg()
 
     def _train_and_send(self):
-        weights, n = self.trainer.train(self.round_idx)
+        # device plane: keep the silo average on the GPU (no state-dict round trip through the host)
+        weights, n = self.trainer.train(self.round_idx, flat=self.mailbox is not None)
         self.send_model_to_server(0, weights, n)
 
 

@@ -54,8 +54,12 @@ class SiloBatchedTrainer:
         logging.info("silo: %d local clients (%s samples), %d of them on this process", self.n_local, counts,
                      len(self.sim.assignment(0)[1]))
 
-    def load_global(self, state_dict):
-        self.sim.global_flat.copy_(self.sim.layout.flatten(state_dict, device=self.device))
+    def load_global(self, params):
+        """A state dict, or the flat global model (device tensor, e.g. the device plane's shared buffer)."""
+        if torch.is_tensor(params):
+            self.sim.global_flat.copy_(params.reshape(-1))
+            return
+        self.sim.global_flat.copy_(self.sim.layout.flatten(params, device=self.device))
 
     def sync(self):
         """Collective over the silo: every process leaves with the master's global model."""

@@ -68,13 +68,34 @@ class TrainerDistAdapter:
         self.local_sample_number = self.train_data_local_num_dict[self.client_index]
         self.trainer.set_id(self.client_index)
 
+    def _layout(self):
+        if getattr(self, "_flat_layout", None) is None:
+            from ...core.arena import ParamLayout
+            self._flat_layout = ParamLayout.from_module(self.model)
+        return self._flat_layout
+
     def update_model(self, params):
-        if params is not None:
-            self.model.load_state_dict(params)
-            self._pending = params
+        """A state dict, or the flat global model (a device tensor of the device data plane)."""
+        if params is None:
+            return
+        if torch.is_tensor(params):
+            if self.n_local > 1:       # batched silo: the flat model goes straight into its engine
+                self._pending = params
+                return
+            params = self._layout().unflatten(params.to(self.device))
+        self.model.load_state_dict(params)
+        self._pending = params
 
     def get_model_params(self):
+        if self.n_local > 1 and self.client_index in self.silo_trainers and torch.is_tensor(self._pending):
+            return self.silo_trainers[self.client_index].sim.global_model_state()
         return {k: v.detach().cpu().clone() for k, v in self.model.state_dict().items()}
+
+    def flat_params(self):
+        """This silo's model as a flat fp32 device tensor (the device plane's upload)."""
+        if self.n_local > 1 and self.client_index in self.silo_trainers:
+            return self.silo_trainers[self.client_index].sim.global_flat
+        return self._layout().flatten(self.model.state_dict(), device=self.device)
 
     def sync_model(self):
         """Collective: every silo rank leaves with rank 0's parameters and buffers (batched silos
@@ -85,13 +106,19 @@ class TrainerDistAdapter:
         for b in self.model.buffers():
             dist.broadcast(b, 0)
 
-    def train(self, round_idx=None):
+    def train(self, round_idx=None, flat=False):
+        """``flat``: return the batched silo's average as its flat device tensor (device data plane)
+        instead of a host state dict."""
         self.args.round_idx = round_idx
         if self.n_local > 1:
             st = self.silo_trainers[self.client_index]
             if self.rank_in_silo == 0 and self._pending is not None:
                 st.load_global(self._pending)
             st.sync()
+            if flat:
+                st.sim.run_round(int(round_idx or 0))
+                st.last_loss = st.sim.engine.last_loss
+                return st.sim.global_flat, self.local_sample_number
             state = st.train(int(round_idx or 0))
             self.model.load_state_dict(state)
             return state, self.local_sample_number

@@ -9,9 +9,11 @@ import logging
 import time
 
 import numpy as np
+import torch
 
 from ...core.arena import fedavg_state_dicts
 from ...core.mlops import MLOpsMetrics
+from ...ops import weighted_sum
 from ...simulation.common import client_sampling, summarize_metrics
 
 
@@ -32,11 +34,17 @@ class FedMLAggregator:
         self.model_dict, self.sample_num_dict = {}, {}
         self.flag_client_model_uploaded_dict = {i: False for i in range(client_num)}
         self.history = []
+        self.flat_layout = None      # set by the server manager on the same-node device plane
+        self._flat_global = None     # newest aggregate as a flat device tensor (state dict made lazily)
 
     def get_global_model_params(self):
+        if self._flat_global is not None:
+            self.aggregator.set_model_params(self.flat_layout.unflatten(self._flat_global))
+            self._flat_global = None
         return self.aggregator.get_model_params()
 
     def set_global_model_params(self, model_parameters):
+        self._flat_global = None
         self.aggregator.set_model_params(model_parameters)
 
     def add_local_trained_result(self, index, model_params, sample_num):
@@ -53,6 +61,19 @@ class FedMLAggregator:
 
     def aggregate(self):
         t0 = time.time()
+        if self.model_dict and all(torch.is_tensor(v) for v in self.model_dict.values()):
+            # flat device uploads (device mailbox slots): one FedAvg kernel over the stacked rows; the
+            # result stays a flat device tensor (the state-dict hooks do not apply on this plane)
+            idx = sorted(self.model_dict)
+            counts = [float(self.sample_num_dict[i]) for i in idx]
+            stack = torch.stack([self.model_dict[i] for i in idx])
+            w = torch.tensor([c / sum(counts) for c in counts], dtype=torch.float32, device=stack.device)
+            avg = weighted_sum(stack, w)
+            self._flat_global = avg
+            self.model_dict.clear()
+            self.sample_num_dict.clear()
+            logging.info("aggregate (device plane) time cost: %.3f s", time.time() - t0)
+            return avg
         w_locals = [(self.sample_num_dict[i], self.model_dict[i]) for i in sorted(self.model_dict)]
         hook = getattr(self.aggregator, "on_before_aggregation", None)
         if callable(hook):
@@ -91,6 +112,8 @@ class FedMLAggregator:
             return None
         if self.test_global is None:
             return None
+        if self._flat_global is not None:   # device-plane aggregate: materialise the model for the test
+            self.get_global_model_params()
         m = self.aggregator.test(self.test_global, self.device, self.args)
         acc, loss = summarize_metrics([m])
         stats = {"round": round_idx, "Test/Acc": acc, "Test/Loss": loss}

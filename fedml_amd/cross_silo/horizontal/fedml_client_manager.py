@@ -29,6 +29,7 @@ class FedMLClientManager(ClientManager):
         self.client_real_ids = parse_client_ids(args, client_num - 1)
         self.client_real_id = self.client_real_ids[self.get_sender_id() - 1]
         self.has_sent_online_msg = False
+        self.mailbox = None
         self._stop_stats = threading.Event()
         self.final_model = None
         self.faults = FaultInjector(args)
@@ -42,8 +43,18 @@ class FedMLClientManager(ClientManager):
 
     def note_global(self, params):
         """The round's global model (the reference point of a compressed upload)."""
-        if self.wan is not None and params is not None:
+        if self.wan is not None and params is not None and not torch.is_tensor(params):
             self.wan.note_global(params)
+
+    def resolve_payload(self, params):
+        """A device-plane marker (``cross_silo/device_mailbox.py``) → the global model as a flat device
+        tensor read from the server's shared buffer; any other payload passes through."""
+        from ..device_mailbox import SiloMailbox, is_marker
+        if not is_marker(params):
+            return params
+        if params["__devmail__"] == "init":
+            self.mailbox = SiloMailbox(params["desc"], int(params["slot"]))
+        return self.mailbox.glob
 
     def run(self):
         inject_connection_ready(self)
@@ -71,24 +82,26 @@ class FedMLClientManager(ClientManager):
     def handle_message_init(self, msg):
         MLOpsMetrics.get_instance().report_client_training_status(self.client_real_id,
                                                                   MyMessage.MSG_MLOPS_CLIENT_STATUS_TRAINING)
-        self.note_global(msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS))
-        self.trainer.update_model(msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS))
+        params = self.resolve_payload(msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS))
+        self.note_global(params)
+        self.trainer.update_model(params)
         self.trainer.update_dataset(int(msg.get(MyMessage.MSG_ARG_KEY_CLIENT_INDEX)))
         self.round_idx = int(msg.get(MyMessage.MSG_ARG_KEY_ROUND_INDEX, 0))
         self.__train()
 
     def handle_message_receive_model_from_server(self, msg):
-        self.note_global(msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS))
-        self.trainer.update_model(msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS))
+        params = self.resolve_payload(msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS))
+        self.note_global(params)
+        self.trainer.update_model(params)
         self.trainer.update_dataset(int(msg.get(MyMessage.MSG_ARG_KEY_CLIENT_INDEX)))
         self.round_idx = int(msg.get(MyMessage.MSG_ARG_KEY_ROUND_INDEX, self.round_idx + 1))
         self.__train()
 
     def handle_finish(self, msg):
-        params = msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS)
+        params = self.resolve_payload(msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS))
         if params is not None:
             self.trainer.update_model(params)
-            self.final_model = params
+            self.final_model = self.trainer.get_model_params() if torch.is_tensor(params) else params
         MLOpsMetrics.get_instance().report_client_training_status(self.client_real_id,
                                                                   MyMessage.MSG_MLOPS_CLIENT_STATUS_FINISHED)
         self._stop_stats.set()
@@ -97,7 +110,19 @@ class FedMLClientManager(ClientManager):
     def send_model_to_server(self, receive_id, weights, local_sample_num):
         MLOpsProfilerEvent.get_instance().log_event_started("comm_c2s", event_value=str(self.round_idx))
         m = Message(MyMessage.MSG_TYPE_C2S_SEND_MODEL_TO_SERVER, self.client_real_id, receive_id)
-        if self.wan is not None and self.wan.ref is not None:
+        if getattr(self, "mailbox", None) is not None:
+            # device plane: the upload goes into this silo's shared slot; the message only points at it
+            from ..device_mailbox import marker
+            if torch.is_tensor(weights):
+                flat = weights
+            elif hasattr(self.trainer, "flat_params"):
+                flat = self.trainer.flat_params()
+            else:
+                from ...core.arena import ParamLayout
+                flat = ParamLayout(weights).flatten(weights, device=self.mailbox.glob.device)
+            self.mailbox.write_upload(flat, float(local_sample_num))
+            weights = marker("slot", slot=self.mailbox.slot)
+        elif self.wan is not None and self.wan.ref is not None:
             weights = self.wan.encode(weights, seed=self.round_idx * 4099 + int(self.client_real_id))
         m.add_params(MyMessage.MSG_ARG_KEY_MODEL_PARAMS, weights)
         m.add_params(MyMessage.MSG_ARG_KEY_NUM_SAMPLES, local_sample_num)

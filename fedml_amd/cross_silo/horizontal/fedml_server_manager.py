@@ -7,6 +7,10 @@ the selected clients, aggregate (flat-arena kernel), test, report round info, se
 ``S2C_SYNC_MODEL_TO_CLIENT``. After ``comm_round`` rounds the server stops (clients stop after
 the final sync, as in the reference, and additionally on ``S2C_FINISH``).
 
+Same-node device data plane (``silo_transport: device``; ``cross_silo/device_mailbox.py``): the model
+payloads stay in HBM — the server publishes the global model into a HIP-IPC-shared buffer and aggregates
+the silos' uploads straight from shared slots; the messages carry markers only.
+
 Deadline rounds (not in the reference, which waits for every client forever): with
 ``round_timeout`` (seconds) the server closes a round when the deadline passes and aggregates the
 uploads that arrived (at least ``min_clients_per_round``, default 1), re-weighted by their sample
@@ -62,6 +66,11 @@ class FedMLServerManager(ServerManager):
         self.min_clients = max(1, int(getattr(args, "min_clients_per_round", 1) or 1))
         self._timer = None
         self.partial_rounds = []     # (round, #arrived, #selected) of rounds closed by the deadline
+        self.device_payload = str(getattr(args, "silo_transport", "") or "").lower() == "device"
+        if self.device_payload and not torch.cuda.is_available():
+            raise ValueError("silo_transport: device needs the GPU (HIP IPC buffers)")
+        self.mailbox = None
+        self._slot_of = {cid: i for i, cid in enumerate(self.client_real_ids)}
 
     def run(self):
         inject_connection_ready(self)
@@ -127,6 +136,14 @@ class FedMLServerManager(ServerManager):
         silos = self.aggregator.data_silo_selection(self.round_idx, int(self.args.client_num_in_total), len(ids))
         return ids, silos
 
+    def _open_mailbox(self, g):
+        from ...core.arena import ParamLayout
+        from ..device_mailbox import ServerMailbox
+        layout = ParamLayout(g)
+        self.mailbox = ServerMailbox(layout.size, len(self.client_real_ids), torch.device("cuda"))
+        self.mailbox.publish(layout.flatten(g, device=self.mailbox.glob.device))
+        self.aggregator.flat_layout = layout
+
     def send_init_msg(self):
         self.start_running_time = time.time()
         self._t0 = time.time()
@@ -134,8 +151,13 @@ class FedMLServerManager(ServerManager):
         ids, silos = self._selection()
         self._selected = ids
         self.aggregator.flag_client_model_uploaded_dict = {i: False for i in range(len(ids))}
+        if self.device_payload:
+            from ..device_mailbox import marker
+            self._open_mailbox(g)
+            desc = self.mailbox.descriptor()
         for cid, silo in zip(ids, silos):
-            self._send(MyMessage.MSG_TYPE_S2C_INIT_CONFIG, cid, g, silo)
+            payload = marker("init", desc=desc, slot=self._slot_of[cid]) if self.device_payload else g
+            self._send(MyMessage.MSG_TYPE_S2C_INIT_CONFIG, cid, payload, silo)
         MLOpsProfilerEvent.get_instance().log_event_started("server.wait", event_value=str(self.round_idx))
         self._arm_deadline()
 
@@ -155,8 +177,12 @@ class FedMLServerManager(ServerManager):
         prof = MLOpsProfilerEvent.get_instance()
         prof.log_event_ended("comm_c2s", event_value=str(self.round_idx), event_edge_id=sender)
         params = msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS)
+        from ..device_mailbox import is_marker
         from ..wan_codec import decode, is_encoded, payload_bytes
-        self.wan_bytes = getattr(self, "wan_bytes", 0) + payload_bytes(params)
+        if is_marker(params):    # same-node device plane: the upload sits in the sender's shared slot
+            params, _ = self.mailbox.upload(int(params["slot"]))
+        else:
+            self.wan_bytes = getattr(self, "wan_bytes", 0) + payload_bytes(params)
         if is_encoded(params):   # compressed silo update: w_global + deq(Δ) (cross_silo/wan_codec.py)
             params = decode(params, self.aggregator.get_global_model_params(),
                             device="cuda" if torch.cuda.is_available() else None)
@@ -186,6 +212,11 @@ class FedMLServerManager(ServerManager):
             {"run_id": getattr(self.args, "run_id", "0"), "round_index": self.round_idx,
              "total_rounds": self.round_num, "running_time": round(now - self.start_running_time, 4)})
         self.round_idx += 1
+        if self.device_payload:
+            self.mailbox.publish(g if torch.is_tensor(g) else self.aggregator.flat_layout.flatten(
+                g, device=self.mailbox.glob.device))
+            from ..device_mailbox import marker
+            g = marker("global")
         if self.round_idx == self.round_num:
             # final sync lets clients see the final model; then everyone stops
             for cid in self.client_real_ids:

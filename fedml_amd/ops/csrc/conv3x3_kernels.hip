@@ -677,10 +677,16 @@ static size_t gemm_smem(int kc, int nout, int ldk, const Plan& p, int TR, int TW
          (size_t)p.S * TR * TW * P::pitch(kc) * P::ES;
 }
 
+template <class P, int KC, int NOUT_WG, int XF, int BWD, int EPI, int MTW, int ST>
+static auto gemm_variant(int need) {
+  return need <= 4 ? conv3x3_gemm_kernel<P, KC, NOUT_WG, XF, BWD, EPI, MTW, ST, 4>
+       : need <= 8 ? conv3x3_gemm_kernel<P, KC, NOUT_WG, XF, BWD, EPI, MTW, ST, 8>
+                   : conv3x3_gemm_kernel<P, KC, NOUT_WG, XF, BWD, EPI, MTW, ST, 12>;
+}
+
 // NOUT_WG output channels per workgroup (blockIdx.z slices the layer's NOUT)
 template <class P, int KC, int NOUT_WG, int XF, int BWD, int EPI, int ST>
 static int launch_gemm(Args a, int nout, int C, int target_px, hipStream_t stream) {
-  constexpr int MTW = NOUT_WG >= 64 ? 2 : 4;
   constexpr int CG = KC / P::VEC;
   static const int wgs_env = [] {   // FEDML_AMD_C3G_WGS: workgroup target of the fwd / bwd-data kernels
     const char* e = getenv("FEDML_AMD_C3G_WGS");
@@ -707,11 +713,15 @@ static int launch_gemm(Args a, int nout, int C, int target_px, hipStream_t strea
   if (smem > 160 * 1024) return -5;
   a.fd_trtw = make_fdiv(TR * TW); a.fd_tw = make_fdiv(TW); a.fd_rw = make_fdiv(p.R * a.W); a.fd_w = make_fdiv(a.W);
   const int need = (p.S * TR * TW * CG + 255) / 256;  // 16-B chunks per thread per unit
-  auto kern = need <= 2 ? conv3x3_gemm_kernel<P, KC, NOUT_WG, XF, BWD, EPI, MTW, ST, 2>
-            : need <= 4 ? conv3x3_gemm_kernel<P, KC, NOUT_WG, XF, BWD, EPI, MTW, ST, 4>
-            : need <= 8 ? conv3x3_gemm_kernel<P, KC, NOUT_WG, XF, BWD, EPI, MTW, ST, 8>
-                        : conv3x3_gemm_kernel<P, KC, NOUT_WG, XF, BWD, EPI, MTW, ST, 12>;
   if (need > 12) return -7;
+  // 16-pixel tiles per wave: as many as keep all 4 waves busy on one unit. A unit of ONE 8×8 image (the
+  // 64-channel fp32 layers: two would not fit the loader's registers) has 4 tiles, so MTW = 4 used to run
+  // it on a single wave while three waited at the barrier.
+  const int ntile = p.S * p.R * a.W / 16;
+  auto kern = gemm_variant<P, KC, NOUT_WG, XF, BWD, EPI, 1, ST>(need);
+  if (ntile >= 8) kern = gemm_variant<P, KC, NOUT_WG, XF, BWD, EPI, 2, ST>(need);
+  if constexpr (NOUT_WG < 64)
+    if (ntile >= 16) kern = gemm_variant<P, KC, NOUT_WG, XF, BWD, EPI, 4, ST>(need);
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   hipLaunchKernelGGL(kern, dim3(p.gx, C, nout / NOUT_WG), dim3(256), smem, stream, a);
   return (int)hipGetLastError();

@@ -6,8 +6,12 @@ its local clients on the client-batched transformer engine (cross_silo/hierarchi
 
     python scripts/bench_hier.py --silos 8 --local-clients 4 --procs-per-silo 1 --rounds 3 --warmup 1
 
-Silo processes are spread over the visible GPUs (process i → GPU i mod ngpus); with fewer GPUs than
-processes inside one silo the silo group must use gloo (FEDML_AMD_DIST_BACKEND=gloo is set then).
+Silo processes are spread over the GPUs (process i → GPU i mod ngpus, every process sees every GPU so
+the device data plane's IPC buffers open anywhere on the node); with fewer GPUs than processes inside one
+silo the silo group must use gloo (FEDML_AMD_DIST_BACKEND=gloo is set then).
+``--silo-transport device`` keeps the server↔silo-master model payloads in HBM (HIP-IPC mailbox,
+cross_silo/device_mailbox.py; the TCP messages carry markers); the default is the reference's network
+payload (fp32 state dicts, or ``--wan-compression int8``).
 Metric: FL rounds/s measured by the server (round-completion timestamps after the warmup rounds).
 Data: synthetic ILSVRC2012-shaped images, random-init weights."""
 import argparse
@@ -42,8 +46,8 @@ def worker(a):
            "synthetic_samples_per_client": a.samples_per_client * a.local_clients, "rank": a.silo,
            "n_proc_in_silo": a.procs_per_silo, "proc_rank_in_silo": a.rank_in_silo, "pg_master_port": a.pg_port,
            "silo_local_clients": a.local_clients, "compute_dtype": a.dtype,
-           "using_gpu": torch.cuda.is_available(), "gpu_id": 0,
-           "wan_compression": a.wan_compression, "random_seed": 0}
+           "using_gpu": torch.cuda.is_available(), "gpu_id": a.gpu, "rank_in_node": a.gpu,
+           "wan_compression": a.wan_compression, "silo_transport": a.silo_transport, "random_seed": 0}
     args = fedml_amd.init(Arguments.from_dict({"x": cfg}))
     dev, ds, m = fedml_amd._prepare(args)
     from fedml_amd.cross_silo.hierarchical import Client, Server
@@ -72,6 +76,7 @@ def main():
     p.add_argument("--lr", type=float, default=1e-4)
     p.add_argument("--dtype", default="fp32", help="fp32 (the reference's precision) | bf16")
     p.add_argument("--wan-compression", default="", help="'' (fp32 state dicts, the reference) | int8")
+    p.add_argument("--silo-transport", default="", help="'' (network payloads) | device (same-node HBM plane)")
     p.add_argument("--timeout", type=float, default=900)
     # worker-internal
     p.add_argument("--role", default="")
@@ -79,6 +84,7 @@ def main():
     p.add_argument("--rank-in-silo", type=int, default=0)
     p.add_argument("--pg-port", type=int, default=0)
     p.add_argument("--out", default="")
+    p.add_argument("--gpu", type=int, default=0)
     a = p.parse_args()
     if a.role:
         return worker(a)
@@ -92,15 +98,13 @@ def main():
         env["FEDML_AMD_DIST_BACKEND"] = "gloo"
     base = [sys.executable, os.path.abspath(__file__)] + [x for x in sys.argv[1:]]
     procs = []
-    e = dict(env, HIP_VISIBLE_DEVICES="0")
-    procs.append(subprocess.Popen(base + ["--role", "server", "--out", out], env=e))
+    procs.append(subprocess.Popen(base + ["--role", "server", "--out", out, "--gpu", "0"], env=env))
     i = 0
     for s in range(1, a.silos + 1):
         port = _free_port()
         for r in range(a.procs_per_silo):
-            e = dict(env, HIP_VISIBLE_DEVICES=str(i % ngpu))
             procs.append(subprocess.Popen(base + ["--role", "silo", "--silo", str(s), "--rank-in-silo", str(r),
-                                                  "--pg-port", str(port)], env=e))
+                                                  "--pg-port", str(port), "--gpu", str(i % ngpu)], env=env))
             i += 1
     t0 = time.time()
     codes = []
@@ -124,8 +128,10 @@ def main():
             "data": f"synthetic ({a.dataset}-shaped), random-init weights",
             "config": {"model": a.model, "silos": a.silos, "local_clients_per_silo": a.local_clients,
                        "procs_per_silo": a.procs_per_silo, "samples_per_client": a.samples_per_client,
-                       "local_batch": a.batch_size, "wan_payload": a.wan_compression or "fp32 state_dict",
-                       "parallelism": f"server + {a.silos} silos x {a.procs_per_silo} procs (TCP WAN, "
+                       "local_batch": a.batch_size,
+                       "wan_payload": ("device mailbox (HIP IPC, same node)" if a.silo_transport == "device"
+                                       else a.wan_compression or "fp32 state_dict"),
+                       "parallelism": f"server + {a.silos} silos x {a.procs_per_silo} procs (TCP control, "
                                       f"{env.get('FEDML_AMD_DIST_BACKEND', 'RCCL')} in-silo)"},
             "round_times_s": [round(x, 3) for x in res["round_times"]], "wan_bytes": res.get("wan_bytes")}
     print(json.dumps(line), flush=True)

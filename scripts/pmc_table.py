@@ -49,11 +49,8 @@ def main():
             seen[name] += ns
             vd = vals.get(did, {})
             for c, v in vd.items():
-                if c == "GRBM_GUI_ACTIVE" and "GRBM_GUI_ACTIVE" in agg[name] and "SQ_VALU_MFMA_BUSY_CYCLES" not in vd:
-                    continue   # one pass's GRBM_GUI_ACTIVE is enough (the passes ran the same dispatches)
-                if c == "GRBM_GUI_ACTIVE" and "SQ_VALU_MFMA_BUSY_CYCLES" in vd:
-                    agg[name]["GRBM_GUI_ACTIVE_mfma"] += v
-                    continue
+                if c == "GRBM_GUI_ACTIVE":   # kept per pass: the MFMA ratio uses its own pass's cycles
+                    c = "GRBM_GUI_ACTIVE_mfma" if "SQ_VALU_MFMA_BUSY_CYCLES" in vd else "GRBM_GUI_ACTIVE@" + d
                 agg[name][c] += v
             agg[name]["_calls_" + d] += 1
         for name, ns in seen.items():
@@ -70,9 +67,9 @@ def main():
         wr = a.get("WRITE_SIZE", float("nan")) * 1024 / 1e9
         tbs = (rd + (wr if wr == wr else 0)) / (ms / 1e3) / 1e3 if ms > 0 and rd == rd else float("nan")
         mf = a.get("SQ_VALU_MFMA_BUSY_CYCLES")
-        gui = a.get("GRBM_GUI_ACTIVE_mfma", a.get("GRBM_GUI_ACTIVE"))
+        gui = a.get("GRBM_GUI_ACTIVE_mfma") or next((a[k] for k in a if k.startswith("GRBM_GUI_ACTIVE@")), None)
         mfp = 100 * mf / (gui / 8 * 1024) if mf is not None and gui else float("nan")
-        clk = (a.get("GRBM_GUI_ACTIVE", 0) / 8) / (ms * 1e-3) / 1e9 if ms > 0 and a.get("GRBM_GUI_ACTIVE") else float("nan")
+        clk = (gui / 8) / (ms * 1e-3) / 1e9 if ms > 0 and gui else float("nan")
         lc, la = a.get("SQ_LDS_BANK_CONFLICT"), a.get("SQ_LDS_IDX_ACTIVE")
         lcp = 100 * lc / la if lc is not None and la else float("nan")
         lines.append(f"{name:70s} {int(a.get('_calls', 0)):6d} {ms:8.1f} {100 * ms * 1e6 / tot:5.1f} {rd:7.2f} "

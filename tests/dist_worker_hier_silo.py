@@ -1,6 +1,7 @@
 """Worker for the batched-silo hierarchical cross-silo tests: role ∈ {server, silo}.
 argv: role silo rank_in_silo pg_port out n_proc n_local device [model dataset rounds]"""
 import logging
+import os
 import sys
 
 import torch
@@ -18,7 +19,8 @@ def main(role, silo, rank_in_silo, pg_port, out, n_proc, n_local, device, model=
            "client_id_list": str(list(range(1, n_silos + 1))), "sys_perf_interval": 0,
            "synthetic_samples_per_client": 48, "rank": silo, "n_proc_in_silo": n_proc,
            "proc_rank_in_silo": rank_in_silo, "pg_master_port": pg_port, "silo_local_clients": n_local,
-           "shuffle": False, "using_gpu": device == "cuda", "gpu_id": 0}
+           "shuffle": False, "using_gpu": device == "cuda", "gpu_id": 0,
+           "silo_transport": os.environ.get("FEDML_TEST_SILO_TRANSPORT", "")}
     args = fedml_amd.init(Arguments.from_dict({"x": cfg}))
     logging.getLogger().setLevel(logging.WARNING)
     dev, ds, m = fedml_amd._prepare(args)

@@ -20,9 +20,11 @@ F32 = torch.float32
 # Every test runs under both fp32 matrix-core modes (csrc/prec.h): exact v_mfma_f32_16x16x4_f32 products,
 # and the split-bf16 mode (three bf16 MFMAs per fragment, ~2^-16 relative per product). Kernel checks
 # stated as "< 1e-5" hold at 1e-5 for exact and at 1e-4 for bf16x3 (TOL scales every relative error).
-# Whole-step / multi-round checks are dominated by ReLU-mask flips at the threshold (see
-# test_native_step_f32_matches_reference); ~2^-16 products flip more of them than exact fp32 does, so
-# those bounds are 3x wider under bf16x3 (bf16 storage is at 2-4e-1 on the same checks).
+# The whole-step check derives its bound from measured spreads at the mode's product precision (see
+# test_native_step_f32_matches_reference). The 10-round loss curve is bounded by the CPU-vs-GPU PyTorch
+# fp32 spread; split-bf16 products (~2^-16) drift further from it than exact fp32 — measured: 10-round
+# deviation 1.11e-2 against an exact-mode bound of 9.4e-3 (3 x the 3.1e-3 spread), i.e. 1.18x — so that
+# one bound is 3x under bf16x3 (bf16 storage sits at 2-4e-1 on the same checks).
 TOL = {"exact": 1.0, "bf16x3": 10.0}
 STEP_TOL = {"exact": 1.0, "bf16x3": 3.0}
 _mode = ["exact"]
@@ -238,13 +240,15 @@ def _reference_grads(model, layout, flat, x, y, dtype=torch.float32, device=DEV)
 def test_native_step_f32_matches_reference(builder, hw):
     """The fp32 native step against an fp64 reference (CPU), next to PyTorch's own fp32 GPU step.
 
-    Tolerance: fp32 gradients agree with fp64 to ~1e-6 except where a ReLU pre-activation sits within
-    fp32 rounding of 0 — its mask (and that element's gradient, |g| not ~eps·|g|) then depends on the
-    last bit of the BN scale/shift, which follows the fp32-atomic order of the statistics sums. A flip
-    moves every upstream gradient of this tiny random-init net by ~1e-3 (measured:
-    scripts/dbg_dump_runs.py — one element of one data-gradient differs between runs, nothing else);
-    PyTorch fp32 flips the same way against fp64 on other seeds. So: per slot ≤ 1e-2 (one flip measured
-    up to 5.7e-3 on the [2, 2, 2] net; bf16 autocast is at 2-4e-1 here), and the loss to 1e-5."""
+    Tolerance, measured rather than chosen: fp32 gradients agree with fp64 to ~1e-6 except where a ReLU
+    pre-activation sits within rounding of 0 — its mask (and that element's gradient, |g| not ~eps·|g|)
+    then depends on the last bit of the BN scale/shift, which follows the order of the statistics sums.
+    One flip moves every upstream gradient of these tiny random-init nets by 1e-3..1e-2. So the test
+    measures, on the same inputs, how far the fp64 gradients move under perturbations at the precision of
+    the mode's products (inputs and weights × (1 ± u), u = 2^-24 for exact fp32, 2^-16 for the split-bf16
+    mode; 3 draws) and how far PyTorch's own fp32 GPU step is from fp64; the native step must stay within
+    3× the larger of the two (floor 1e-5), per parameter slot. The bulk of the slots must in addition sit
+    at fp32 accuracy: the median slot error ≤ 10 × PyTorch fp32's median (floor 1e-6)."""
     torch.manual_seed(0)
     model = builder()
     layout = ParamLayout.from_module(model)
@@ -261,18 +265,38 @@ def test_native_step_f32_matches_reference(builder, hw):
     loss = float(step.step(arena, garena, x, y, row_scale, active))
     torch.cuda.synchronize()
     assert step.packed.dtype == F32 and step.x_in.dtype == F32
-    ref_loss, ref64 = _reference_grads(model, layout, flat.cpu().double(), x.cpu(), y.cpu(), torch.float64, "cpu")
+    flat64, x64 = flat.cpu().double(), x.cpu().double()
+    ref_loss, ref64 = _reference_grads(model, layout, flat64, x64, y.cpu(), torch.float64, "cpu")
     assert abs(loss - ref_loss) / ref_loss < 1e-5 * TOL[_mode[0]], (loss, ref_loss)
-    bad = []
+    _, t32 = _reference_grads(model, layout, flat, x, y, torch.float32, DEV)
+    u = 2.0 ** -24 if _mode[0] == "exact" else 2.0 ** -16
+    pert = []
+    for r in range(3):
+        g = torch.Generator().manual_seed(1000 + r)
+        fp = flat64 * (1 + u * (2 * torch.rand(flat64.shape, generator=g, dtype=torch.float64) - 1))
+        xp = x64 * (1 + u * (2 * torch.rand(x64.shape, generator=g, dtype=torch.float64) - 1))
+        pert.append(_reference_grads(model, layout, fp, xp, y.cpu(), torch.float64, "cpu")[1])
+
+    def err(g, sl, r):
+        return float((g[:, sl].double().cpu() - r).norm() / r.norm().clamp_min(1e-30))
+
+    e_nat, e_t32, e_pert = [], [], []
     for s in layout.slots:
         if not s.trainable:
             continue
         sl = slice(s.offset, s.offset + s.numel)
-        r = ref64[:, sl]
-        err = float((garena[:, sl].double() - r).norm() / r.norm().clamp_min(1e-30))
-        if err > 1e-2 * STEP_TOL[_mode[0]]:
-            bad.append((s.key, err))
-    assert not bad, bad[:8]
+        r = ref64[:, sl].cpu()
+        e_nat.append((s.key, err(garena, sl, r)))
+        e_t32.append(err(t32, sl, r))
+        e_pert.append(max(err(p, sl, r) for p in pert))
+    bound = max(3 * max(max(e_t32), max(e_pert)), 1e-5)
+    bad = [(k, e) for k, e in e_nat if e > bound]
+    print(f"[{_mode[0]}] native max {max(e for _, e in e_nat):.2e} median "
+          f"{sorted(e for _, e in e_nat)[len(e_nat) // 2]:.2e}; torch fp32 max {max(e_t32):.2e} median "
+          f"{sorted(e_t32)[len(e_t32) // 2]:.2e}; perturbed fp64 max {max(e_pert):.2e} -> bound {bound:.2e}")
+    assert not bad, (bound, bad[:8])
+    med = sorted(e for _, e in e_nat)[len(e_nat) // 2]
+    assert med <= max(10 * sorted(e_t32)[len(e_t32) // 2], 1e-6) * TOL[_mode[0]], med
     s = layout.slot("bn1.running_mean")
     m = copy.deepcopy(model).to(DEV)
     m.train()
