@@ -22,6 +22,9 @@
 // of one row: 8-byte bf16 / 16-byte fp32 epilogue accesses, bias as one float4.
 #include "common.h"
 #include <cstdlib>
+#include "detacc.h"
+
+FA_DET_EXPORT(bgemm)
 
 namespace bg {
 
@@ -348,8 +351,8 @@ __global__ __launch_bounds__(256) void bias_grad_kernel(const uint16_t* __restri
     a1 += bf16_to_f32((uint16_t)(v >> 16));
   }
   float* o = out + (int64_t)c * o_cs;
-  atomicAdd(o + seg_row(seg, n, 1), a0);
-  atomicAdd(o + seg_row(seg, n + 1, 1), a1);
+  fa_acc_add(o + seg_row(seg, n, 1), a0);
+  fa_acc_add(o + seg_row(seg, n + 1, 1), a1);
 }
 
 template <int A_TR, int B_TR, int B_F32, int EPI>

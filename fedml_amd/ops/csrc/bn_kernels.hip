@@ -3,6 +3,9 @@
 // activations [C][N][H][W][Ch] bf16 | fp32 (`_f32` entry points); vectors [C][Ch] fp32; parameters/grads in the client-stacked
 // fp32 arenas [C][ldw] addressed by offset.
 #include "prec.h"
+#include "detacc.h"
+
+FA_DET_EXPORT(bn)
 
 using prec::BF16;
 using prec::F32;
@@ -309,14 +312,48 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const float* __restrict__
       gpre[i] = gb;
       const float gr = P::to_f(gb);
       a0 += gr;
-      a1 += gr * P::to_f(y3[i]);
+      if (y3) a1 += gr * P::to_f(y3[i]);   // null: a recomputed-y last conv gets Σg·y from its Gram pass
       if (yd) a2 += gr * P::to_f(yd[i]);
     }
     float* st = stats + ((int64_t)c * Ch + ch) * NS;
-    atomicAdd(st + 0, a0);
-    atomicAdd(st + 1, a1);
-    if (yd && NS > 2) atomicAdd(st + 2, a2);
+    fa_acc_add(st + 0, a0);
+    fa_acc_add(st + 1, a1);
+    if (yd && NS > 2) fa_acc_add(st + 2, a2);
   }
+}
+
+// Σ_p g·(y − K) of a recomputed-y 1×1 convolution's BN from the Gram product G = gᵀ·act(x) (its output y =
+// act(x)·Wᵀ is never stored): stats[c][o][1] = Σ_i W[c][o][i]·G[c][o][i] − K[c][o]·stats[c][o][0]; the consumed
+// G row is cleared for the next use. One wave per (output channel, client); CI ≤ 256.
+__global__ __launch_bounds__(256) void gy_from_gram_kernel(const float* __restrict__ arena, int64_t ldw, int64_t woff,
+                                                           float* __restrict__ G, int64_t ldg,
+                                                           const float* __restrict__ pivot, float* __restrict__ stats,
+                                                           int NS, int CO, int CI) {
+  const int c = blockIdx.y;
+  const int o = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (o >= CO) return;
+  const float* w = arena + (int64_t)c * ldw + woff + (int64_t)o * CI;
+  float* gr = G + (int64_t)c * ldg + (int64_t)o * CI;
+  float s = 0.f;
+  for (int i = lane; i < CI; i += 64) {
+    s += w[i] * gr[i];
+    gr[i] = 0.f;
+  }
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) {
+    float* st = stats + ((int64_t)c * CO + o) * NS;
+    st[1] = s - (pivot ? pivot[(int64_t)c * CO + o] : 0.f) * st[0];
+  }
+}
+
+FA_EXPORT int fa_gy_from_gram(const float* arena, int64_t ldw, int64_t woff, float* G, int64_t ldg, const float* pivot,
+                              float* stats, int NS, int C, int CO, int CI, hipStream_t stream) {
+  if (CI > 4096 || NS < 2) return -3;
+  hipLaunchKernelGGL(gy_from_gram_kernel, dim3((CO + 3) / 4, C), dim3(256), 0, stream, arena, ldw, woff, G, ldg, pivot,
+                     stats, NS, CO, CI);
+  return (int)hipGetLastError();
 }
 
 FA_EXPORT int fa_head_bwd(const float* dpool, const uint16_t* out, const uint16_t* y3, const uint16_t* yd,

@@ -11,6 +11,9 @@
 // layout [co][ci] IS the OIHW layout, so the partial sums go straight into the gradient arena
 // with fp32 atomics — no scratch / scatter pass.
 #include "prec.h"
+#include "detacc.h"
+
+FA_DET_EXPORT(conv1x1)
 
 namespace c1 {
 
@@ -48,11 +51,13 @@ __global__ __launch_bounds__(256) void conv1x1_wgrad_kernel(const typename P::T*
   T* dyL = reinterpret_cast<T*>(vv + 3 * COUT + 2 * CIN);                  // [PT][LDD]
   T* xL = dyL + PT * LDD;                                                  // [PT][LDX]
 
-  for (int i = threadIdx.x; i < COUT; i += 256) {
-    vv[i] = alpha[(int64_t)c * COUT + i];
-    vv[COUT + i] = beta[(int64_t)c * COUT + i];
-    vv[2 * COUT + i] = gamma[(int64_t)c * COUT + i];
-  }
+  const bool raw = yv == nullptr;   // dy = g as stored (e.g. Gᵀ·act(x) of a recomputed-y bottleneck)
+  if (!raw)
+    for (int i = threadIdx.x; i < COUT; i += 256) {
+      vv[i] = alpha[(int64_t)c * COUT + i];
+      vv[COUT + i] = beta[(int64_t)c * COUT + i];
+      vv[2 * COUT + i] = gamma[(int64_t)c * COUT + i];
+    }
   if (PRO)
     for (int i = threadIdx.x; i < CIN; i += 256) {
       vv[3 * COUT + i] = ps[(int64_t)c * CIN + i];
@@ -60,7 +65,7 @@ __global__ __launch_bounds__(256) void conv1x1_wgrad_kernel(const typename P::T*
     }
 
   const T* gc = g + (int64_t)c * M * COUT;
-  const T* yc = yv + (int64_t)c * M * COUT;
+  const T* yc = raw ? nullptr : yv + (int64_t)c * M * COUT;
   const T* xc = x + (int64_t)c * M * CIN;
   const int p_begin = blockIdx.x * pix_per_wg;
   const int p_end = min(nimg ? min(M, nimg[c] * hw) : M, p_begin + pix_per_wg);   // valid pixels of client c
@@ -78,7 +83,7 @@ __global__ __launch_bounds__(256) void conv1x1_wgrad_kernel(const typename P::T*
         if (p < p_end) {
           const int64_t off = (int64_t)p * COUT + (i % (COUT / V)) * V;
           rg[it] = *reinterpret_cast<const uint4*>(gc + off);
-          ry[it] = *reinterpret_cast<const uint4*>(yc + off);
+          if (!raw) ry[it] = *reinterpret_cast<const uint4*>(yc + off);
         }
       }
     }
@@ -104,7 +109,7 @@ __global__ __launch_bounds__(256) void conv1x1_wgrad_kernel(const typename P::T*
         const bool live = p0 + pp < p_end;
 #pragma unroll
         for (int j = 0; j < V; ++j)
-          gf[j] = live ? vv[co0 + j] * gf[j] + vv[COUT + co0 + j] * yf[j] + vv[2 * COUT + co0 + j] : 0.f;
+          gf[j] = !live ? 0.f : raw ? gf[j] : vv[co0 + j] * gf[j] + vv[COUT + co0 + j] * yf[j] + vv[2 * COUT + co0 + j];
         P::st_chunk(dyL + pp * LDD + co0, P::pack(gf));
       }
     }
@@ -187,7 +192,7 @@ __global__ __launch_bounds__(256) void conv1x1_wgrad_kernel(const typename P::T*
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int co = (mgrp * MTW + m) * 16 + 4 * g4 + i;
-          atomicAdd(&gw[(int64_t)co * CIN + ci], acc[m][n][i]);
+          fa_acc_add(&gw[(int64_t)co * CIN + ci], acc[m][n][i]);
         }
       }
   }
@@ -304,6 +309,7 @@ struct Args {             // activations are P::T (bf16 | fp32)
   float* part;            // optional [C][G][CO·CI + 3·CI] per-workgroup partials (no atomics)
   const int* nimg;        // per-client valid images (null: all) and pixels per image
   int hw;
+  const float* pivot;     // RY: [C][CO] shift K of the conv's forward output (y − K is what α, β, γ assume)
 };
 
 enum { EPI_MASK = 2, EPI_BLOCK = 3 };
@@ -312,7 +318,11 @@ enum { EPI_MASK = 2, EPI_BLOCK = 3 };
 // over NW waves, so the 64/256-channel layers use 8 waves to stay off the 256-VGPR cliff.
 // LDS: dyL is read both ways (pixel fragments for dW, row fragments for dx), so it takes the
 // frag_tr pitch and its row fragments are read 8-B aligned (P::frag_a8).
-template <class P, int CI, int CO, int EPI, int WM, int WN, int PT, int NW>
+// RY (recomputed y, EPI_MASK, fp32 storage): the conv's forward output y is not stored — it is recomputed
+// per stage from the staged act(e_x) tile (the conv input) and the weights already in LDS (wL holds Wᵀ:
+// read transposed it is W), as y − K straight into the dy tile, which is then turned into dy in place.
+// This replaces a 4·planes-channel read of y with MFMA work on data the kernel holds anyway.
+template <class P, int CI, int CO, int EPI, int WM, int WN, int PT, int NW, bool RY = false>
 __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
   using T = typename P::T;
   using frag_t = typename P::frag_t;
@@ -321,7 +331,9 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
   constexpr int WK = NW / (WM * WN);
   constexpr int MTW = CO / 16 / WM, NTW = CI / 16 / WN;  // weight-gradient tiles per wave
   constexpr int KP = (CO + 31) / 32 * 32;            // dx GEMM depth (zero-padded to the MFMA K)
-  constexpr int LDD = P::pitch_tr(KP), LDX = P::pitch_tr(CI), LDS_ = P::pitch(CI), LDW = KP + 8;
+  // RY with CI < 32: the recompute GEMM's K is padded to 32 with zero columns of act(x) and zero rows of W
+  constexpr int KCI = RY ? (CI + 31) / 32 * 32 : CI;
+  constexpr int LDD = P::pitch_tr(KP), LDX = P::pitch_tr(KCI), LDS_ = P::pitch(CI), LDW = KP + 8;
   constexpr int DCH = PT * CO / V, XCH = PT * CI / V;
   constexpr int DI = (DCH + NT - 1) / NT, XI = (XCH + NT - 1) / NT;
   constexpr int MT = PT / 16;                       // dx row tiles per stage
@@ -345,8 +357,8 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* vv = reinterpret_cast<float*>(smem);                            // α β γ [CO], s t [CI]
-  T* wL = reinterpret_cast<T*>(vv + 3 * CO + 2 * CI);                    // [CI][LDW]
-  T* sL = wL + CI * LDW;                                                 // [PT][LDS_] dx staging
+  T* wL = reinterpret_cast<T*>(vv + 3 * CO + 2 * CI + (RY ? CO : 0));    // [CI][LDW]
+  T* sL = wL + KCI * LDW;                                                // [PT][LDS_] dx staging
   T* dyL = sL + PT * LDS_;                                               // [PT][LDD]
   T* xL = dyL + PT * LDD;                                                // [PT][LDX]  act(e_x)
 
@@ -360,6 +372,9 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
       vv[3 * CO + i] = a.e_s[(int64_t)c * CI + i];
       vv[3 * CO + CI + i] = a.e_t[(int64_t)c * CI + i];
     }
+  float* pivL = vv + 3 * CO + 2 * CI;   // RY: [CO] (the weight tile below starts after it)
+  if (RY)
+    for (int i = threadIdx.x; i < CO; i += NT) pivL[i] = a.pivot ? a.pivot[(int64_t)c * CO + i] : 0.f;
   {
     const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.wb) + (int64_t)c * a.wb_ld);
     uint4* dst = reinterpret_cast<uint4*>(wL);
@@ -367,6 +382,10 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
   }
   if (KP > CO)  // zero K-padding columns of the dy tile (never rewritten by the stage stores)
     for (int i = threadIdx.x; i < PT * (KP - CO); i += NT) dyL[(i / (KP - CO)) * LDD + CO + i % (KP - CO)] = 0;
+  if (KCI > CI) {   // RY, CI < 32: zero K padding of the recompute operands (never rewritten either)
+    for (int i = threadIdx.x; i < (KCI - CI) * LDW; i += NT) wL[CI * LDW + i] = 0;
+    for (int i = threadIdx.x; i < PT * (KCI - CI); i += NT) xL[(i / (KCI - CI)) * LDX + CI + i % (KCI - CI)] = 0;
+  }
 
   const int M = a.M;
   const int Mc = a.nimg ? min(M, a.nimg[c] * a.hw) : M;   // this client's valid pixels
@@ -382,6 +401,7 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
   const int p_end = min(Mc, p_begin + a.pix_per_wg);
   const int ci0 = (threadIdx.x % CGX) * V;  // this thread's channel chunk in every e_x-shaped pass
   const bool has_y2 = BLK && e_y2 != nullptr;
+  const bool has_y1 = BLK && e_y1 != nullptr;   // null: the previous BN's Σg·y comes from elsewhere
 
   // registers: next stage (r*) and current stage (e*) — every operand is fetched one stage ahead
   uint4 rg[DI], ry[DI], rx[XI], ra[XI], r1[XI], r2[XI];
@@ -397,7 +417,7 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
         if (p < p_end) {
           const int64_t off = (int64_t)p * CO + (i % (CO / V)) * V;
           rg[it] = *reinterpret_cast<const uint4*>(gc + off);
-          ry[it] = *reinterpret_cast<const uint4*>(yc + off);
+          if (!RY) ry[it] = *reinterpret_cast<const uint4*>(yc + off);
         }
       }
     }
@@ -411,13 +431,13 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
         rx[it] = *reinterpret_cast<const uint4*>(e_x + off);
         if (BLK) {
           ra[it] = *reinterpret_cast<const uint4*>(e_add + off);
-          r1[it] = *reinterpret_cast<const uint4*>(e_y1 + off);
+          if (has_y1) r1[it] = *reinterpret_cast<const uint4*>(e_y1 + off);
           if (has_y2) r2[it] = *reinterpret_cast<const uint4*>(e_y2 + off);
         }
       }
     }
   };
-  auto store = [&](int p0) {
+  auto form_dy = [&](int p0) {
 #pragma unroll
     for (int it = 0; it < DI; ++it) {
       const int i = threadIdx.x + it * NT;
@@ -425,7 +445,13 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
         const int pp = i / (CO / V), co0 = (i % (CO / V)) * V;
         float gf[V], yf[V];
         P::unpack(rg[it], gf);
-        P::unpack(ry[it], yf);
+        if (RY) {   // y − K recomputed into this very chunk of the dy tile (8-B aligned rows)
+          const uint2 lo = reinterpret_cast<const uint2*>(dyL + pp * LDD + co0)[0];
+          const uint2 hi = reinterpret_cast<const uint2*>(dyL + pp * LDD + co0)[1];
+          P::unpack(make_uint4(lo.x, lo.y, hi.x, hi.y), yf);
+        } else {
+          P::unpack(ry[it], yf);
+        }
         const bool live = p0 + pp < p_end;
 #pragma unroll
         for (int j = 0; j < V; ++j)
@@ -433,6 +459,27 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
         P::st_chunk(dyL + pp * LDD + co0, P::pack(gf));
       }
     }
+  };
+  // RY: y − K = act(x) · Wᵀ − K for the stage's PT pixels, one 16 × 16 tile per wave iteration
+  auto recompute_y = [&]() {
+    constexpr int NCT = CO / 16;
+#pragma unroll 1
+    for (int t = wid; t < (PT / 16) * NCT; t += NW) {
+      const int mt = t / NCT, nt = t % NCT;
+      f32x4 yacc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k0 = 0; k0 < KCI; k0 += 32) {
+        const frag_t af = P::frag_a8(xL + (mt * 16 + (lane & 15)) * LDX + k0 + 8 * g4);
+        const frag_t bw = P::frag_tr(wL, LDW, k0, nt * 16, lane);
+        yacc = P::mma(af, bw, yacc);
+      }
+      const int col = nt * 16 + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dyL[(mt * 16 + 4 * g4 + i) * LDD + col] = P::from_f(yacc[i] - pivL[col]);
+    }
+  };
+  auto store = [&](int p0) {
+    if (!RY) form_dy(p0);
 #pragma unroll
     for (int it = 0; it < XI; ++it) {
       const int i = threadIdx.x + it * NT;
@@ -450,6 +497,12 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
         }
         P::st_chunk(xL + pp * LDX + ci0, v);
       }
+    }
+    if (RY) {
+      __syncthreads();   // act(x) staged
+      recompute_y();
+      __syncthreads();   // y − K staged
+      form_dy(p0);
     }
   };
 
@@ -572,7 +625,7 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
     if (mypart) {
       mypart[(int64_t)CO * CI + i] = v;
     } else if (p_begin < p_end && (i % 3 < 2 || has_y2)) {
-      atomicAdd(a.stats + (int64_t)c * CI * a.NS + (i / 3) * a.NS + i % 3, v);
+      fa_acc_add(a.stats + (int64_t)c * CI * a.NS + (i / 3) * a.NS + i % 3, v);
     }
   }
 
@@ -614,7 +667,7 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
           if (mypart)
             mypart[(int64_t)co * CI + ci] = acc[m][n][i];
           else if (p_begin < p_end)
-            atomicAdd(&gw[(int64_t)co * CI + ci], acc[m][n][i]);
+            fa_acc_add(&gw[(int64_t)co * CI + ci], acc[m][n][i]);
         }
       }
   }
@@ -649,14 +702,15 @@ __global__ __launch_bounds__(256) void partial_reduce_kernel(const float* __rest
   }
 }
 
-template <class P, int CI, int CO, int EPI, int WM, int WN, int PT, int NW>
+template <class P, int CI, int CO, int EPI, int WM, int WN, int PT, int NW, bool RY = false>
 static int launch(const Args& a, int C, hipStream_t stream) {
   constexpr int WK = NW / (WM * WN);
   constexpr int KP = (CO + 31) / 32 * 32;
-  const size_t vv = (size_t)(3 * CO + 2 * CI) * 4;
-  const size_t wl = (size_t)CI * (KP + 8) * P::ES;
+  constexpr int KCI = RY ? (CI + 31) / 32 * 32 : CI;
+  const size_t vv = (size_t)(3 * CO + 2 * CI + (RY ? CO : 0)) * 4;
+  const size_t wl = (size_t)KCI * (KP + 8) * P::ES;
   const size_t stage = (size_t)PT * P::pitch(CI) * P::ES;
-  const size_t tiles = (size_t)PT * (P::pitch_tr(KP) + P::pitch_tr(CI)) * P::ES;
+  const size_t tiles = (size_t)PT * (P::pitch_tr(KP) + P::pitch_tr(KCI)) * P::ES;
   const size_t red = (size_t)(WK - 1) * (WM * WN) * (CO / 16 / WM) * (CI / 16 / WN) * 256 * 4;
   const size_t sred = (size_t)NW * CI * 3 * 4;
   size_t region = stage + tiles;   // the reduction buffers reuse the stage + tile region
@@ -665,7 +719,7 @@ static int launch(const Args& a, int C, hipStream_t stream) {
   const size_t smem = vv + wl + region;
   if (smem > 160 * 1024) return -5;
   if (a.NS < 2 || (EPI == EPI_BLOCK && a.e_y2 && a.NS < 3)) return -4;
-  auto kern = conv1x1_bwd_kernel<P, CI, CO, EPI, WM, WN, PT, NW>;
+  auto kern = conv1x1_bwd_kernel<P, CI, CO, EPI, WM, WN, PT, NW, RY>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   const int gx = (a.M + a.pix_per_wg - 1) / a.pix_per_wg;
   hipLaunchKernelGGL(kern, dim3(gx, C), dim3(64 * NW), smem, stream, a);
@@ -682,14 +736,20 @@ static int bwd_fused(const void* g, const void* y, const float* alpha, const flo
                      const void* wb, int64_t wb_ld, int ldk2, const void* e_x, const float* e_s, const float* e_t,
                      const void* e_add, const void* e_y1, const void* e_y2, void* out, float* stats, int NS,
                      float* garena, int64_t ldw, int64_t woff, int C, int M, int Cin, int Cout, int epi,
-                     int pix_per_wg, float* part, const int* nimg, int hw, hipStream_t stream) {
+                     int pix_per_wg, float* part, const int* nimg, int hw, const float* pivot, hipStream_t stream) {
   if (ldk2 != (Cout + 31) / 32 * 32 + 8 || pix_per_wg <= 0) return -3;
   if (epi == EPI_MASK && (!e_s || !e_t)) return -4;
-  if (epi == EPI_BLOCK && (!e_add || !e_y1)) return -4;
+  if (epi == EPI_BLOCK && !e_add) return -4;
+  // y == null: recompute y from the staged input (EPI_MASK, fp32 storage only)
+  if (!y && (epi != EPI_MASK || !P::kF32)) return -4;
   Args a{g, y, alpha, beta, gamma, wb, wb_ld, e_x, e_s, e_t, e_add, e_y1, e_y2, out, stats, NS, garena, ldw,
-         woff, M, pix_per_wg, part, nimg, hw};
-#define C1F(CI, CO, E, WM, WN, PT, NW) \
-  if (Cin == CI && Cout == CO && epi == E) return launch<P, CI, CO, E, WM, WN, PT, NW>(a, C, stream);
+         woff, M, pix_per_wg, part, nimg, hw, pivot};
+#define C1F(CI, CO, E, WM, WN, PT, NW)                                              \
+  if (Cin == CI && Cout == CO && epi == E) {                                       \
+    if constexpr (E == EPI_MASK && P::kF32)                                        \
+      if (!y) return launch<P, CI, CO, E, WM, WN, PT, NW, true>(a, C, stream);     \
+    return launch<P, CI, CO, E, WM, WN, PT, NW>(a, C, stream);                     \
+  }
   // conv2 of a bottleneck (planes → 4·planes): mask epilogue, BN-ReLU prologue on the wgrad operand
   C1F(16, 64, 2, 2, 1, 64, 4)
   C1F(32, 128, 2, 4, 1, 64, 4)
@@ -721,7 +781,7 @@ FA_EXPORT int fa_conv1x1_bwd_fused(const uint16_t* g, const uint16_t* y, const f
                                    float* part, const int* nimg, int hw, hipStream_t stream) {
   return c1f::bwd_fused<c1f::BF16>(g, y, alpha, beta, gamma, wb, wb_ld, ldk2, e_x, e_s, e_t, e_add, e_y1, e_y2, out,
                                    stats, NS, garena, ldw, woff, C, M, Cin, Cout, epi, pix_per_wg, part, nimg, hw,
-                                   stream);
+                                   nullptr, stream);
 }
 FA_EXPORT int fa_conv1x1_bwd_fused_f32(const float* g, const float* y, const float* alpha, const float* beta,
                                        const float* gamma, const float* wb, int64_t wb_ld, int ldk2, const float* e_x,
@@ -731,5 +791,16 @@ FA_EXPORT int fa_conv1x1_bwd_fused_f32(const float* g, const float* y, const flo
                                        int pix_per_wg, float* part, const int* nimg, int hw, hipStream_t stream) {
   FA_F32_DISPATCH(c1f, c1f::bwd_fused<PX>(g, y, alpha, beta, gamma, wb, wb_ld, ldk2, e_x, e_s, e_t, e_add, e_y1, e_y2, out,
                                   stats, NS, garena, ldw, woff, C, M, Cin, Cout, epi, pix_per_wg, part, nimg, hw,
-                                  stream));
+                                  nullptr, stream));
+}
+// recomputed-y variant (EPI_MASK): `y` is not read — y − pivot is rebuilt from e_x and the weights
+FA_EXPORT int fa_conv1x1_bwd_fused_ry_f32(const float* g, const float* alpha, const float* beta, const float* gamma,
+                                          const float* pivot, const float* wb, int64_t wb_ld, int ldk2,
+                                          const float* e_x, const float* e_s, const float* e_t, float* out,
+                                          float* stats, int NS, float* garena, int64_t ldw, int64_t woff, int C, int M,
+                                          int Cin, int Cout, int pix_per_wg, float* part, const int* nimg, int hw,
+                                          hipStream_t stream) {
+  FA_F32_DISPATCH(c1f, c1f::bwd_fused<PX>(g, nullptr, alpha, beta, gamma, wb, wb_ld, ldk2, e_x, e_s, e_t, nullptr,
+                                  nullptr, nullptr, out, stats, NS, garena, ldw, woff, C, M, Cin, Cout, c1f::EPI_MASK,
+                                  pix_per_wg, part, nimg, hw, pivot, stream));
 }

@@ -20,9 +20,12 @@
 // Every kernel is instantiated for bf16 and fp32 storage (prec.h); the fp32 instances are the
 // reference-precision path (exact fp32 MFMA products, fp32 activations).
 #include "prec.h"
+#include "detacc.h"
 #include <algorithm>
 
 #include <cstdlib>
+
+FA_DET_EXPORT(conv3x3)
 
 #ifndef TAP_UNROLL
 #define TAP_UNROLL 3
@@ -466,7 +469,7 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
     const int ch = i / 2, q = i % 2;
     const float s = red[(0 * NOUT + ch) * 2 + q] + red[(1 * NOUT + ch) * 2 + q] + red[(2 * NOUT + ch) * 2 + q] +
                     red[(3 * NOUT + ch) * 2 + q];
-    atomicAdd(&a.stats[((int64_t)c * NO + ch_base + ch) * a.NS + q], s);
+    fa_acc_add(&a.stats[((int64_t)c * NO + ch_base + ch) * a.NS + q], s);
   }
 }
 
@@ -635,7 +638,7 @@ __global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WArgs a) {
 #pragma unroll
         for (int m = 0; m < MT; ++m)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) atomicAdd(&dwc[(int64_t)(m * 16 + 4 * g + i) * K + k], acc[m][t][i]);
+          for (int i = 0; i < 4; ++i) fa_acc_add(&dwc[(int64_t)(m * 16 + 4 * g + i) * K + k], acc[m][t][i]);
       }
     }
   }

@@ -21,13 +21,19 @@
 // MFMA: v_mfma_f32_16x16x32_bf16. Lane l holds A[row l&15][k 8(l>>4)..+7], B[k 8(l>>4)..+7][col l&15];
 // D: col = l&15, row = 4(l>>4) + i.
 #include "prec.h"
+#include "detacc.h"
+
+FA_DET_EXPORT(conv)
 
 using prec::BF16;
 using prec::F32;
 using prec::F32X3;
 
 enum { PRO_NONE = 0, PRO_BNRELU = 1 };
-enum { EPI_FWD = 0, EPI_STORE = 1, EPI_MASK = 2, EPI_BLOCK = 3 };
+// EPI_BOUT (conv_gemm_kernel only): the bottleneck block output straight from the last conv's accumulators,
+//   out = relu((acc − K)·e_s + e_t + r),  r = e_add (identity shortcut) | e_add·e_rs + e_rt (downsample BN)
+// — the conv's output y itself is never stored (its BN statistics come from a stats-only EPI_FWD pass)
+enum { EPI_FWD = 0, EPI_STORE = 1, EPI_MASK = 2, EPI_BLOCK = 3, EPI_BOUT = 4 };
 
 // =====================================================================================
 // Weight packing: fp32 OIHW (client-stacked arena, stride ldw) → bf16 | fp32 GEMM layouts.
@@ -212,7 +218,9 @@ struct ConvArgs {        // activations / packed weights are P::T (bf16 | fp32)
   const void* e_y1;      // EPI_BLOCK: previous block's bn3 input (Σg·y)
   const void* e_y2;      // EPI_BLOCK: previous block's downsample-bn input (optional)
   float* stats;          // [C][NOUT][NS]
-  const float* pivot;    // EPI_FWD: per-(client, channel) shift subtracted from the stored output (or null)
+  const float* pivot;    // EPI_FWD / EPI_BOUT: per-(client, channel) shift subtracted from the output (or null)
+  const float* e_rs;     // EPI_BOUT: downsample-BN scale / shift of the shortcut (null: identity shortcut)
+  const float* e_rt;
   const int* nimg;       // per-client valid images (null: all Nb) — heterogeneous client batches
   int NS;
   int Nb, Hs, Ws, KC;    // source geometry (KC = channels of the A source = GEMM K per tap)
@@ -273,7 +281,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
   const int64_t src_client = (int64_t)c * a.Nb * a.Hs * a.Ws * a.KC;
   const T* src = reinterpret_cast<const T*>(a.src) + src_client;
   const T* src2 = (AOP == AOP_DY) ? reinterpret_cast<const T*>(a.src2) + src_client : nullptr;
-  T* out = reinterpret_cast<T*>(a.out) + (int64_t)c * Mo * NO;
+  T* out = a.out ? reinterpret_cast<T*>(a.out) + (int64_t)c * Mo * NO : nullptr;   // null: statistics only (EPI_FWD)
   const T* e_x = reinterpret_cast<const T*>(a.e_x);
   const T* e_add = reinterpret_cast<const T*>(a.e_add);
   const T* e_y1 = reinterpret_cast<const T*>(a.e_y1);
@@ -286,6 +294,19 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
 #pragma unroll
   for (int j = 0; j < V; ++j) { st0[j] = 0.f; st1[j] = 0.f; st2[j] = 0.f; }
   const int my_cg = lane % CG;
+  constexpr int NPASS = (16 + ROWS_PER_PASS - 1) / ROWS_PER_PASS;
+  // EPI_BOUT: this lane's BN3 / shortcut-BN vectors (its channel chunk is fixed for the whole kernel)
+  float bs[V], bt[V], brs[V], brt[V];
+  if (EPI == EPI_BOUT) {
+    const int64_t vo = (int64_t)c * NO + ch_base + my_cg * V;
+#pragma unroll
+    for (int j = 0; j < V; ++j) {
+      bs[j] = a.e_s[vo + j];
+      bt[j] = a.e_t[vo + j];
+      brs[j] = a.e_rs ? a.e_rs[vo + j] : 0.f;
+      brt[j] = a.e_rs ? a.e_rt[vo + j] : 0.f;
+    }
+  }
 
   const int tiles_total = (Mv + 15) / 16;
   const int tile0 = (blockIdx.x * 4 + wid) * a.tiles_per_wave;
@@ -303,6 +324,19 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
     f32x4 acc[NT];
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[nt] = {0.f, 0.f, 0.f, 0.f};
+    // EPI_BOUT: the shortcut rows of this tile's epilogue, in flight during the K loop
+    uint4 rres[EPI == EPI_BOUT ? NPASS : 1];
+    if (EPI == EPI_BOUT) {
+      const int rv = min(16, Mv - tile * 16);
+#pragma unroll
+      for (int pass = 0; pass < NPASS; ++pass) {
+        const int row = pass * ROWS_PER_PASS + lane / CG;
+        rres[pass] = make_uint4(0, 0, 0, 0);
+        if (lane / CG < ROWS_PER_PASS && row < rv)
+          rres[pass] = *reinterpret_cast<const uint4*>(e_add + (int64_t)c * Mo * NO +
+                                                       (int64_t)(tile * 16 + row) * NO + ch_base + my_cg * V);
+      }
+    }
 
     for (int k0 = 0; k0 < a.Kp; k0 += 32) {
       const int k = k0 + 8 * (lane >> 4);
@@ -352,7 +386,8 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
     // ---- stage the 16 × NOUT tile (storage precision) in LDS; forward outputs as y − K (pivot) ----
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) {
-      const float k = (EPI == EPI_FWD && a.pivot) ? a.pivot[(int64_t)c * NO + ch_base + nt * 16 + (lane & 15)] : 0.f;
+      const float k = ((EPI == EPI_FWD || EPI == EPI_BOUT) && a.pivot)
+                          ? a.pivot[(int64_t)c * NO + ch_base + nt * 16 + (lane & 15)] : 0.f;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int row = 4 * (lane >> 4) + i;
@@ -381,8 +416,19 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
           *reinterpret_cast<uint4*>(out + goff + (int64_t)a.Wo * NO) = z;
           *reinterpret_cast<uint4*>(out + goff + (int64_t)(a.Wo + 1) * NO) = z;
         }
-        if (EPI == EPI_FWD || EPI == EPI_STORE) {
-          *reinterpret_cast<uint4*>(out + goff) = dv;
+        if (EPI == EPI_BOUT) {
+          float f[V], r[V];
+          P::unpack(dv, f);
+          P::unpack(rres[EPI == EPI_BOUT ? pass : 0], r);
+#pragma unroll
+          for (int j = 0; j < V; ++j) {
+            f[j] = f[j] * bs[j] + bt[j];   // same operation order as block_out_kernel
+            f[j] += a.e_rs ? r[j] * brs[j] + brt[j] : r[j];
+            f[j] = fmaxf(f[j], 0.f);
+          }
+          *reinterpret_cast<uint4*>(out + goff) = P::pack(f);
+        } else if (EPI == EPI_FWD || EPI == EPI_STORE) {
+          if (EPI == EPI_STORE || out) *reinterpret_cast<uint4*>(out + goff) = dv;
           if (EPI == EPI_FWD) {
             float f[V];
             P::unpack(dv, f);
@@ -415,10 +461,14 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
 #pragma unroll
             for (int j = 0; j < V; ++j) { st0[j] += gr[j]; st1[j] += gr[j] * xv[j]; }
           } else {
-            float y1[V];
-            P::unpack(*reinterpret_cast<const uint4*>(e_y1 + eoff), y1);
 #pragma unroll
-            for (int j = 0; j < V; ++j) { st0[j] += gr[j]; st1[j] += gr[j] * y1[j]; }
+            for (int j = 0; j < V; ++j) st0[j] += gr[j];
+            if (e_y1) {   // null: the previous BN's Σg·y comes from elsewhere (recomputed-y bottlenecks)
+              float y1[V];
+              P::unpack(*reinterpret_cast<const uint4*>(e_y1 + eoff), y1);
+#pragma unroll
+              for (int j = 0; j < V; ++j) st1[j] += gr[j] * y1[j];
+            }
             if (e_y2) {
               float y2[V];
               P::unpack(*reinterpret_cast<const uint4*>(e_y2 + eoff), y2);
@@ -433,7 +483,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
   }
 
   // ---- statistics: reduce lanes sharing a channel group, then waves, then one atomic ----
-  if (EPI != EPI_STORE) {
+  if (EPI != EPI_STORE && EPI != EPI_BOUT) {
 #pragma unroll
     for (int o = CG; o < 64; o <<= 1) {
 #pragma unroll
@@ -457,7 +507,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
       const int ch = i / a.NS, q = i % a.NS;
       const float s = red[(0 * NOUT + ch) * 3 + q] + red[(1 * NOUT + ch) * 3 + q] + red[(2 * NOUT + ch) * 3 + q] +
                       red[(3 * NOUT + ch) * 3 + q];
-      atomicAdd(&a.stats[((int64_t)c * NO + ch_base + ch) * a.NS + q], s);
+      fa_acc_add(&a.stats[((int64_t)c * NO + ch_base + ch) * a.NS + q], s);
     }
   }
 }
@@ -777,10 +827,14 @@ __global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
 #pragma unroll
             for (int j = 0; j < V; ++j) { st0[j] += gr[j]; st1[j] += gr[j] * xv[j]; }
           } else {
-            float y1[V];
-            P::unpack(*reinterpret_cast<const uint4*>(e_y1 + eoff), y1);
 #pragma unroll
-            for (int j = 0; j < V; ++j) { st0[j] += gr[j]; st1[j] += gr[j] * y1[j]; }
+            for (int j = 0; j < V; ++j) st0[j] += gr[j];
+            if (e_y1) {   // null: the previous BN's Σg·y comes from elsewhere (recomputed-y bottlenecks)
+              float y1[V];
+              P::unpack(*reinterpret_cast<const uint4*>(e_y1 + eoff), y1);
+#pragma unroll
+              for (int j = 0; j < V; ++j) st1[j] += gr[j] * y1[j];
+            }
             if (e_y2) {
               float y2[V];
               P::unpack(*reinterpret_cast<const uint4*>(e_y2 + eoff), y2);
@@ -820,7 +874,7 @@ __global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
       float s = 0.f;
 #pragma unroll
       for (int m_ = 0; m_ < CK::WM; ++m_) s += red[((m_ * WN + wn_) * NOUT + ch) * 3 + q];
-      atomicAdd(&a.stats[((int64_t)c * NO + ch_base + chb) * a.NS + q], s);
+      fa_acc_add(&a.stats[((int64_t)c * NO + ch_base + chb) * a.NS + q], s);
     }
   }
 }
@@ -927,6 +981,22 @@ static int conv_fwd(const void* x, const void* wpk, int64_t wpk_ld, const float*
   return dispatch_nt<P, AOP_ACT, PRO_NONE, MODE_FWD, EPI_FWD>(Cout, a, C, stream);
 }
 
+// bottleneck block output from the last 1×1 conv (EPI_BOUT): out = relu(BN(conv(relu(x·ps + pt)) − K) + shortcut)
+template <class P>
+static int conv_fwd_bout(const void* x, const void* wpk, int64_t wpk_ld, const float* pscale, const float* pshift,
+                         void* out, const float* s, const float* t, const float* pivot, const void* res, const float* rs,
+                         const float* rt, int C, int Nb, int H, int W, int Cin, int Cout, int ldk, int tiles_per_wave,
+                         const int* nimg, hipStream_t stream) {
+  if (Cin % 8 != 0 || Cout % 64 != 0 || !pscale || !s || !t || !res || (rs && !rt)) return -3;
+  ConvArgs a = {};
+  a.src = x; a.wpk = wpk; a.wpk_ld = wpk_ld; a.vec0 = pscale; a.vec1 = pshift; a.out = out; a.NS = 2;
+  a.e_s = s; a.e_t = t; a.pivot = pivot; a.e_add = res; a.e_rs = rs; a.e_rt = rt; a.nimg = nimg;
+  a.Nb = Nb; a.Hs = H; a.Ws = W; a.KC = Cin; a.Ho = H; a.Wo = W; a.KH = 1; a.KW = 1; a.stride = 1;
+  a.pad = 0; a.ldk = ldk; a.Kp = (Cin + 31) / 32 * 32; a.tiles_per_wave = tiles_per_wave;
+  if (conv_smem_bytes<P>(64, a.ldk, a.KC) > 160 * 1024) return -5;
+  return launch_conv<P, 4, AOP_ACT, PRO_BNRELU, MODE_FWD, EPI_BOUT>(a, Cout, C, stream);
+}
+
 template <class P, int AOP>
 static int conv_bwd_data_dispatch(const ConvArgs& a, int epi, int C, int Cin, int Cout, int KH, int KW, int stride,
                                   int pad, int Hx, int Wx, int Hy, int Wy, hipStream_t stream) {
@@ -984,6 +1054,14 @@ FA_EXPORT int fa_conv_fwd_f32(const float* x, const float* wpk, int64_t wpk_ld, 
                               int tiles_per_wave, const float* pivot, const int* nimg, hipStream_t stream) {
   FA_F32_DISPATCH(prec, conv_fwd<PX>(x, wpk, wpk_ld, pscale, pshift, y, stats, C, Nb, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo,
                        ldk, tiles_per_wave, pivot, nimg, stream));
+}
+
+FA_EXPORT int fa_conv_fwd_bout_f32(const float* x, const float* wpk, int64_t wpk_ld, const float* pscale,
+                                   const float* pshift, float* out, const float* s, const float* t, const float* pivot,
+                                   const float* res, const float* rs, const float* rt, int C, int Nb, int H, int W,
+                                   int Cin, int Cout, int ldk, int tiles_per_wave, const int* nimg, hipStream_t stream) {
+  FA_F32_DISPATCH(prec, conv_fwd_bout<PX>(x, wpk, wpk_ld, pscale, pshift, out, s, t, pivot, res, rs, rt, C, Nb, H, W,
+                                          Cin, Cout, ldk, tiles_per_wave, nimg, stream));
 }
 
 // backward-data: dx = convᵀ(α·g + β·y + γ) with epilogue

@@ -1,0 +1,33 @@
+// Flush of the deterministic fixed-point accumulators (detacc.h): dst[i] += round_f32(acc[i] · 2^-80),
+// acc[i] = 0. The 128-bit sum goes through fp64 (hi · 2^64 + lo, then · 2^-80) and rounds once more to
+// fp32 — a pure function of the integer sum, so the result is the same bits for any arrival order.
+#include "common.h"
+#include "detacc.h"
+
+__global__ __launch_bounds__(256) void det_flush_kernel(float* __restrict__ dst, unsigned long long* __restrict__ acc,
+                                                        int64_t n, const unsigned int* __restrict__ bad) {
+  const bool poisoned = bad != nullptr && *bad != 0u;
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const unsigned long long lo = acc[2 * i], hi = acc[2 * i + 1];
+    if (poisoned) {
+      dst[i] = __builtin_nanf("");
+    } else if ((lo | hi) != 0ull) {
+      const double d = (double)(long long)hi * 18446744073709551616.0 + (double)lo;
+      dst[i] += (float)(d * 8.271806125530277e-25);   // 2^-80
+    } else {
+      continue;
+    }
+    acc[2 * i] = 0ull;
+    acc[2 * i + 1] = 0ull;
+  }
+}
+
+extern "C" int fa_det_flush(float* dst, void* acc, int64_t n, unsigned int* bad, hipStream_t stream) {
+  if (n <= 0) return 0;
+  const int64_t blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(det_flush_kernel, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, stream, dst,
+                     (unsigned long long*)acc, n, bad);
+  return (int)hipGetLastError();
+}
+
+FA_DET_EXPORT(det)

@@ -27,6 +27,9 @@
 
 #include "prec.h"
 #include "dropout.h"
+#include "detacc.h"
+
+FA_DET_EXPORT(tf_f32)
 
 namespace tff {
 
@@ -458,8 +461,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
       sg += red[(w * 2 + 0) * d + i];
       sb += red[(w * 2 + 1) * d + i];
     }
-    atomicAdd(dgamma + (size_t)c * d + i, sg);
-    atomicAdd(dbeta + (size_t)c * d + i, sb);
+    fa_acc_add(dgamma + (size_t)c * d + i, sg);
+    fa_acc_add(dbeta + (size_t)c * d + i, sb);
   }
 }
 
@@ -499,7 +502,7 @@ __global__ __launch_bounds__(256) void bias_grad_kernel(const float* __restrict_
   const float* gp = g + (int64_t)c * g_bs + n;
   float a = 0.f;
   for (int m = m0; m < m1; ++m) a += gp[(int64_t)m * ldg];
-  atomicAdd(out + (int64_t)c * o_cs + seg_row(seg, n, 1), a);
+  fa_acc_add(out + (int64_t)c * o_cs + seg_row(seg, n, 1), a);
 }
 
 // =========================================================================================

@@ -11,6 +11,9 @@
 // B[k 8(l>>4)..+7][col l&15]; C/D: col = l&15, row = 4(l>>4) + reg.
 #include "common.h"
 #include "dropout.h"
+#include "detacc.h"
+
+FA_DET_EXPORT(transformer)
 
 typedef __bf16 bf16x8_mf __attribute__((ext_vector_type(8)));
 
@@ -200,8 +203,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
       sg += red[(w * 2 + 0) * d + i];
       sb += red[(w * 2 + 1) * d + i];
     }
-    atomicAdd(dgamma + (size_t)c * d + i, sg);
-    atomicAdd(dbeta + (size_t)c * d + i, sb);
+    fa_acc_add(dgamma + (size_t)c * d + i, sg);
+    fa_acc_add(dbeta + (size_t)c * d + i, sb);
   }
 }
 

@@ -14,9 +14,12 @@
 // tiles and keep them in registers for the whole chunk; the partial dW is added (fp32 atomics)
 // into the client-stacked gradient arena at the OIHW position of each element.
 #include "prec.h"
+#include "detacc.h"
 
 #include <stdlib.h>
 #include <type_traits>
+
+FA_DET_EXPORT(wgrad)
 
 using prec::BF16;
 using prec::F32;
@@ -201,7 +204,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_tr_kernel(
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int co = co_lo + mt * 16 + 4 * (lane >> 4) + i;
-          atomicAdd(&dwc[(int64_t)co * K + k], acc[t][i]);
+          fa_acc_add(&dwc[(int64_t)co * K + k], acc[t][i]);
         }
       }
     }
@@ -418,7 +421,7 @@ __global__ __launch_bounds__(256) void wgrad_wide_kernel(
         if (direct) {
           if (ci < cin_src) garena[(int64_t)c * ldw + woff + ((int64_t)co * cin_src + ci) * taps + tap] += acc[i][j][r];
         } else {   // several pixel chunks per tile: row-contiguous atomics into the GEMM-layout scratch
-          atomicAdd(&dw[((int64_t)c * Cout + co) * K + k], acc[i][j][r]);
+          fa_acc_add(&dw[((int64_t)c * Cout + co) * K + k], acc[i][j][r]);
         }
       }
     }
@@ -447,7 +450,10 @@ static int wgrad_wide(const typename P::T* g, const typename P::T* yv, const flo
   hipLaunchKernelGGL(kern, dim3(gx, C, nks * (Cout / 128)), dim3(256), smem, stream, g, yv, alpha, beta, gamma, x,
                      ps, pt, dw, garena, ldw, woff, cin_src, Nb, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ppw,
                      nimg, direct);
-  if (!direct) return wgrad_scatter_rows(dw, garena, ldw, woff, C, Cout, Cin, KH * KW, cin_src, stream);
+  if (!direct) {
+    fa_det_flush_if_registered(g_fa_det_host_wgrad, dw, (int64_t)C * Cout * K, stream);
+    return wgrad_scatter_rows(dw, garena, ldw, woff, C, Cout, Cin, KH * KW, cin_src, stream);
+  }
   return (int)hipGetLastError();
 }
 
@@ -531,6 +537,7 @@ static int conv_wgrad(const typename P::T* g, const typename P::T* yv, const flo
   if (tpw <= 4) by_d(std::integral_constant<int, 4>{});
   else if (tpw <= 8) by_d(std::integral_constant<int, 8>{});
   else by_d(std::integral_constant<int, 16>{});
+  fa_det_flush_if_registered(g_fa_det_host_wgrad, dw, (int64_t)C * Cout * K, stream);
   return wgrad_scatter_rows(dw, garena, ldw, woff, C, Cout, Cin, KH * KW, cin_src, stream);
 }
 

@@ -68,6 +68,27 @@ def conv_fwd(x, wpk, wpk_ld, pscale, pshift, y, stats, C, N, H, W, Cin, Cout, KH
     _check(rc, "fa_conv_fwd")
 
 
+def conv_fwd_bout(x, wpk, wpk_ld, pscale, pshift, out, s, t, pivot, res, rs, rt, C, N, H, W, Cin, Cout, ldk,
+                  tiles_per_wave, nimg=None):
+    """Bottleneck block output from its last 1×1 conv without storing that conv's output (fp32 storage):
+    out = relu((conv(relu(x·ps + pt)) − pivot)·s + t + r), r = res (identity) | res·rs + rt (downsample BN).
+    The BN statistics of the conv output come from :func:`conv_fwd` with ``y=None`` (same kernel, same bits)."""
+    if x.dtype != torch.float32:
+        raise ValueError("conv_fwd_bout: fp32 storage only")
+    rc = _fn("fa_conv_fwd_bout_f32")(_p(x), _p(wpk), _i64(wpk_ld), _p(pscale), _p(pshift), _p(out), _p(s), _p(t),
+                                     _p(pivot), _p(res), _p(rs), _p(rt), _i(C), _i(N), _i(H), _i(W), _i(Cin), _i(Cout),
+                                     _i(ldk), _i(tiles_per_wave), _p(nimg), _stream(x))
+    _check(rc, "fa_conv_fwd_bout_f32")
+
+
+def gy_from_gram(arena, woff, G, pivot, stats, C, Cout, Cin):
+    """stats[c, o, 1] = Σ_i W[c, o, i]·G[c, o, i] − pivot[c, o]·stats[c, o, 0] (= Σ_p g·(y − K) of a 1×1 conv whose
+    output y = act(x)·Wᵀ was not stored; G = gᵀ·act(x)); clears G."""
+    rc = _fn("fa_gy_from_gram")(_p(arena), _i64(arena.stride(0)), _i64(woff), _p(G), _i64(G.stride(0)), _p(pivot),
+                                _p(stats), _i(stats.shape[-1]), _i(C), _i(Cout), _i(Cin), _stream(G))
+    _check(rc, "fa_gy_from_gram")
+
+
 EPI_STORE, EPI_MASK, EPI_BLOCK = 1, 2, 3
 
 
@@ -175,6 +196,20 @@ def conv1x1_bwd_fused_scratch(C, M, Cin, Cout, pix_per_wg):
     """fp32 elements of the partial-sum scratch :func:`conv1x1_bwd_fused` needs for this shape."""
     G = -(-M // pix_per_wg)
     return C * G * (Cout * Cin + 3 * Cin)
+
+
+def conv1x1_bwd_fused_ry(g, alpha, beta, gamma, pivot, wpk_b, wpk_ld, ldk2, e_x, e_s, e_t, out, stats, garena, woff,
+                         C, M, Cin, Cout, pix_per_wg, part=None, nimg=None, hw=0):
+    """:func:`conv1x1_bwd_fused` (EPI_MASK) of a conv whose output y was not stored: y − pivot is recomputed
+    per pixel stage from the staged relu(e_x·e_s + e_t) and the weights in LDS (fp32 storage)."""
+    if part is not None and part.numel() < conv1x1_bwd_fused_scratch(C, M, Cin, Cout, pix_per_wg):
+        raise ValueError("conv1x1_bwd_fused_ry: partial-sum scratch too small")
+    rc = _fn("fa_conv1x1_bwd_fused_ry_f32")(_p(g), _p(alpha), _p(beta), _p(gamma), _p(pivot), _p(wpk_b), _i64(wpk_ld),
+                                            _i(ldk2), _p(e_x), _p(e_s), _p(e_t), _p(out), _p(stats),
+                                            _i(stats.shape[-1]), _p(garena), _i64(garena.stride(0)), _i64(woff), _i(C),
+                                            _i(M), _i(Cin), _i(Cout), _i(pix_per_wg), _p(part), _p(nimg), _i(hw),
+                                            _stream(g))
+    _check(rc, "fa_conv1x1_bwd_fused_ry_f32")
 
 
 def conv1x1_bwd_fused(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, ldk2, e_x, e_s, e_t, e_add, e_y1, e_y2, out, stats,

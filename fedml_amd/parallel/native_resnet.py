@@ -68,6 +68,7 @@ class BlockSpec:
     ys: list = field(default_factory=list)
     yd: Optional[torch.Tensor] = None
     out: Optional[torch.Tensor] = None
+    ry: bool = False     # recomputed-y bottleneck (NativeResNetStep._ry_ok): the last conv's output is not stored
 
 
 class UnsupportedNative(Exception):
@@ -153,8 +154,27 @@ class NativeResNetStep:
         self.use_c1f = os.environ.get("FEDML_AMD_C1_FUSED", "1") != "0"
         self.use_dym = os.environ.get("FEDML_AMD_DY_MATERIALIZE", "1") != "0"
         self.use_s2k = os.environ.get("FEDML_AMD_C3S2_CONVK", "1") == "1"   # measured +2 % (fp32 headline)
+        self.use_ry = os.environ.get("FEDML_AMD_RECOMPUTE_Y", "0") == "1" and dtype == torch.float32
         self.dump = None   # debug: list collecting (name, tensor clone) of every backward gradient buffer
         self._nimg = None
+        self.det = None    # DetAccumulator in deterministic mode (enable_deterministic)
+
+    def enable_deterministic(self):
+        """Bitwise-reproducible steps on the same kernels: every cross-workgroup fp32 atomic (BN statistics,
+        split weight gradients) accumulates in 128-bit fixed point and is rounded once, at a fixed point
+        of the step (ops/det_ops.py, csrc/detacc.h). Costs one flush launch per BN and one per step."""
+        from ..ops.det_ops import DetAccumulator
+        if self.det is None:
+            self.det = DetAccumulator(self.device)
+            self.det.activate()
+            if self.geom is not None:
+                for t in (self.stats, self.dw_scratch, self.dw_c3, self.gram):
+                    self.det.register(t)
+
+    def close(self):
+        if self.det is not None:
+            self.det.close()
+            self.det = None
 
     # ------------------------------------------------------------------ setup
     def _all_convs(self):
@@ -225,7 +245,9 @@ class NativeResNetStep:
         self.stem_out = act(st.Ho, st.Wo, st.cout)
         maxel = st.Ho * st.Wo * st.cout
         for b in self.blocks:
-            b.ys = [act(cv.Ho, cv.Wo, cv.cout) for cv in b.convs]
+            b.ry = self._ry_ok(b)
+            b.ys = [None if (b.ry and j == len(b.convs) - 1) else act(cv.Ho, cv.Wo, cv.cout)
+                    for j, cv in enumerate(b.convs)]
             b.yd = act(b.ds_conv.Ho, b.ds_conv.Wo, b.ds_conv.cout) if b.ds_conv is not None else None
             last = b.convs[-1]
             b.out = act(last.Ho, last.Wo, last.cout)
@@ -243,7 +265,9 @@ class NativeResNetStep:
         self.bn_vec = {}
         nstat = 0
         for bn in self._all_bns():
-            self.bn_vec[bn.key] = torch.zeros(8, C, bn.ch, dtype=torch.float32, device=dev)
+            # row 8: the pivot this step's forward subtracted (recomputed-y convs read it after
+            # bn_fwd_finalize has already moved row 7 on to the next step's pivot)
+            self.bn_vec[bn.key] = torch.zeros(9, C, bn.ch, dtype=torch.float32, device=dev)
             nstat += bn.ch * 5
         self.stats = torch.zeros(C * nstat, dtype=torch.float32, device=dev)
         self.stat_views = {}
@@ -270,21 +294,27 @@ class NativeResNetStep:
                 o3 += C * n
                 self.c3_maxn = max(self.c3_maxn, n)
         self.dw_c3 = torch.zeros(max(1, o3), dtype=torch.float32, device=dev)
+        # Gram scratch gᵀ·h2 of the recomputed-y bottlenecks ([C][4·planes·planes], kept zeroed by its consumer)
+        gmax = max([b.convs[-1].cout * b.convs[-1].cin for b in self.blocks if b.ry] or [0])
+        self.gram = torch.zeros(C, gmax, dtype=torch.float32, device=dev) if gmax else None
         self.c3_nseg = len(segs)
         raw = bytes((nn_ops.ScatterSeg * max(1, len(segs)))(*segs))
         self.c3_segs = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
         self.geom = (N, H, W)
+        if self.det is not None:
+            for t in (self.stats, self.dw_scratch, self.dw_c3, self.gram):
+                self.det.register(t)
         if os.environ.get("FEDML_AMD_POISON", "0") == "1":   # debug: uninitialised reads show up as NaN
             for t in [self.x_in, self.stem_y, self.stem_out, self.pooled] + list(self.gbuf):
                 t.fill_(float("nan"))
             for b in self.blocks:
-                for t in b.ys + [b.out] + ([b.yd] if b.yd is not None else []):
+                for t in [u for u in b.ys if u is not None] + [b.out] + ([b.yd] if b.yd is not None else []):
                     t.fill_(float("nan"))
 
     # Every geometry keeps its own buffers alive: a captured HIP graph of one batch size must stay
     # valid while another batch size (the ragged last step of an epoch) is being run.
     _STATE_ATTRS = ("x_in", "stem_y", "stem_out", "gbuf", "dybuf", "bn_vec", "stats", "stat_views", "pooled", "dw_scratch",
-                    "dw_c3", "c3_segs", "c3_nseg", "c3_maxn", "_c3_off",
+                    "dw_c3", "gram", "c3_segs", "c3_nseg", "c3_maxn", "_c3_off",
                     "packed", "packed_ld", "_segs", "_nseg", "_pack_tiles", "_pack_taps", "final_hw", "geom")
 
     def _snapshot(self):
@@ -374,6 +404,19 @@ class NativeResNetStep:
                           cv.cin_pad, cv.Ho, cv.Wo, cv.cout, cv.k, cv.k, cv.stride, cv.pad, self._pix_per_wg(M), cv.cin,
                           self.dw_scratch, nimg=self._nimg)
 
+    def _ry_ok(self, b) -> bool:
+        """Bottleneck whose last (1×1, planes → 4·planes) conv output y3 is never stored (fp32): its BN statistics
+        come from a stats-only pass, the block output straight from a second pass of the same GEMM (EPI_BOUT),
+        Σg·y3 of its BN backward from the Gram product gᵀ·h2 (h2 = the conv input), and the fused 1×1 backward
+        recomputes y3 per pixel stage. Per block and pixel that removes the 4·planes-wide y3 write and its three
+        reads (block output, next block's backward epilogue, BN backward) for one planes-wide Gram read."""
+        if not self.use_ry or len(b.convs) != 3:
+            return False
+        cv = b.convs[-1]
+        return (cv.k == 1 and cv.stride == 1 and cv.pad == 0 and cv.cin == cv.cin_pad and cv.cout % 64 == 0
+                and self._c1f(cv, nn_ops.EPI_MASK)
+                and nn_ops.conv1x1_wgrad_supported(cv.cin, cv.cout, cv.k, cv.stride, cv.pad))
+
     def _c1f(self, cv: ConvSpec, epi):
         return (self.use_c1f and cv.cin == cv.cin_pad
                 and nn_ops.conv1x1_bwd_fused_supported(cv.cin, cv.cout, cv.k, cv.stride, cv.pad, epi))
@@ -418,6 +461,8 @@ class NativeResNetStep:
     def _bn_fwd(self, bn, N, hw, arena, active, training=True):
         v = self.bn_vec[bn.key]
         fst = self.stat_views[bn.key][0]
+        if self.det is not None:
+            self.det.flush(fst)
         g, b, rm, rv, nbt = self._bn_offsets(bn)
         nn_ops.bn_fwd_finalize(fst, self.C, bn.ch, float(N * hw), arena, g, b, rm, rv, nbt, bn.momentum, bn.eps,
                                active, v[0], v[1], v[2], v[3], training, pivot=v[7], nimg=self._nimg, hw=hw)
@@ -425,6 +470,8 @@ class NativeResNetStep:
     def _bn_bwd(self, bn, q, N, hw, arena, garena):
         v = self.bn_vec[bn.key]
         bst = self.stat_views[bn.key][1]
+        if self.det is not None:
+            self.det.flush(bst)
         g, b = self.off[f"{bn.key}.weight"], self.off[f"{bn.key}.bias"]
         nn_ops.bn_bwd_finalize(bst, 3, q, self.C, bn.ch, float(N * hw), v[2], v[3], arena, garena, g, b, v[4], v[5],
                                v[6], nimg=self._nimg, hw=hw)
@@ -447,6 +494,8 @@ class NativeResNetStep:
             else:
                 self._setup(N, H, W)
                 self._states[(N, H, W)] = self._snapshot()
+        if self.det is not None:
+            self.det.register(garena)
         self.stats.zero_()
         nn_ops.pack_weights(arena, self._segs, self._nseg, self.packed, self.packed_ld, C, self._pack_tiles,
                             self._pack_taps)
@@ -468,6 +517,8 @@ class NativeResNetStep:
                 src = act_in if j == 0 else b.ys[j - 1]
                 pro = None if j == 0 else self.bn_vec[b.bns[j - 1].key]
                 self._fwd(cv, src, b.ys[j], pro, bn, N)
+                if b.ys[j] is None:     # recomputed-y conv: keep the pivot its later passes must subtract
+                    self.bn_vec[bn.key][8].copy_(self.bn_vec[bn.key][7])
                 self._bn_fwd(bn, N, cv.Ho * cv.Wo, arena, active)
             last, lbn = b.convs[-1], b.bns[-1]
             vl = self.bn_vec[lbn.key]
@@ -475,6 +526,14 @@ class NativeResNetStep:
                 d = b.ds_conv
                 self._fwd(d, act_in, b.yd, None, b.ds_bn, N)
                 self._bn_fwd(b.ds_bn, N, d.Ho * d.Wo, arena, active)
+            if b.ry:    # block output from a second pass of the last conv (its output y3 is never stored)
+                pv = self.bn_vec[b.bns[-2].key]
+                res, rs, rt = (b.yd, self.bn_vec[b.ds_bn.key][0], self.bn_vec[b.ds_bn.key][1]) \
+                    if b.ds_conv is not None else (act_in, None, None)
+                nn_ops.conv_fwd_bout(b.ys[-2], self.packed.view(-1)[last.off_f:], self.packed_ld, pv[0], pv[1], b.out,
+                                     vl[0], vl[1], vl[8], res, rs, rt, C, N, last.H, last.W, last.cin_pad, last.cout,
+                                     last.ldk, self._tiles_per_wave(N * last.Ho * last.Wo), nimg=self._nimg)
+            elif b.ds_conv is not None:
                 vd = self.bn_vec[b.ds_bn.key]
                 nn_ops.block_out(b.ys[-1], vl[0], vl[1], b.yd, vd[0], vd[1], b.out, C,
                                  N * last.Ho * last.Wo * last.cout, last.cout, nimg=self._nimg,
@@ -516,6 +575,17 @@ class NativeResNetStep:
             lbn = b.bns[-1]
             last = b.convs[-1]
             hw_last = last.Ho * last.Wo
+            if b.ry:    # Σg·(y3 − K) of BN3's backward from G = gᵀ·h2 (y3 = h2·W3ᵀ is not stored)
+                M3 = N * hw_last
+                pv = self.bn_vec[b.bns[-2].key]
+                nn_ops.conv1x1_wgrad(gpre, None, None, None, None, b.ys[-2], pv[0], pv[1], self.gram, 0, C, M3,
+                                     last.cin, last.cout, self._c1_pix_per_wg(M3), nimg=self._nimg, hw=hw_last)
+                bst = self.stat_views[lbn.key][1]
+                if self.det is not None:
+                    self.det.flush(self.gram)
+                    self.det.flush(bst)
+                nn_ops.gy_from_gram(arena, self.off[last.key], self.gram, self.bn_vec[lbn.key][8], bst, C, last.cout,
+                                    last.cin)
             self._bn_bwd(lbn, 1, N, hw_last, arena, garena)
             if b.ds_bn is not None:
                 # the shortcut BN sees the same g: its (Σg, Σg·yd) live in slots 0 and 2 of lbn's stats
@@ -529,6 +599,16 @@ class NativeResNetStep:
                 pv = self.bn_vec[b.bns[j - 1].key]
                 M = N * cv.Ho * cv.Wo
                 out_g = free[0] if g_j is not free[0] else free[1]
+                if b.ry and j == len(b.convs) - 1:
+                    nn_ops.conv1x1_bwd_fused_ry(g_j, v[4], v[5], v[6], v[8], self.packed.view(-1)[cv.off_b:],
+                                                self.packed_ld, cv.ldk2, b.ys[j - 1], pv[0], pv[1], out_g,
+                                                self.stat_views[b.bns[j - 1].key][1], garena, self.off[cv.key], C, M,
+                                                cv.cin, cv.cout, self._c1f_pix_per_wg(M), nimg=self._nimg,
+                                                hw=cv.Ho * cv.Wo)
+                    self._bn_bwd(b.bns[j - 1], 1, N, cv.H * cv.W, arena, garena)
+                    g_j = out_g
+                    self._dump(f"{cv.key}.dx", out_g, C * N * cv.H * cv.W * cv.cin)
+                    continue
                 if self._c1f(cv, nn_ops.EPI_MASK):
                     nn_ops.conv1x1_bwd_fused(g_j, b.ys[j], v[4], v[5], v[6], self.packed.view(-1)[cv.off_b:],
                                              self.packed_ld, cv.ldk2, b.ys[j - 1], pv[0], pv[1], None, None, None,
@@ -612,5 +692,9 @@ class NativeResNetStep:
         v = self.bn_vec[st_bn.key]
         self._wgrad(st_conv, gpre, self.stem_y, v, self.x_in, None, garena, N)
         if self.c3_nseg:
+            if self.det is not None:
+                self.det.flush(self.dw_c3)
             nn_ops.wgrad_scatter_multi(self.dw_c3, garena, self.c3_segs, self.c3_nseg, self.c3_maxn, C)
+        if self.det is not None:
+            self.det.flush(garena)
         return loss.detach()

@@ -174,10 +174,10 @@ class ClientBatchEngine:
         self.deterministic = determinism.enabled(args)
         if self.deterministic:
             determinism.enable(args)
-        # deterministic mode: the native step's fp32-atomic BN statistics / split-K weight gradients are
-        # not bitwise reproducible, so it runs the batched torch path instead (utils/determinism.py)
+        # deterministic mode keeps the native step: its cross-workgroup fp32 atomics (BN statistics, split
+        # weight gradients) switch to order-independent fixed-point accumulation (ops/det_ops.py)
         if self.device.type == "cuda" and not self.sequential and self.loss_name == "ce" and \
-                not self.deterministic and os.environ.get("FEDML_AMD_NATIVE_CONV", "1") != "0":
+                os.environ.get("FEDML_AMD_NATIVE_CONV", "1") != "0":
             from ...parallel.native_resnet import NativeResNetStep, UnsupportedNative
             # the native kernels run at the requested precision: fp32 (compute_dtype None / fp32, the
             # reference's) or bf16; any other dtype keeps the torch path, which honours it
@@ -188,6 +188,8 @@ class ClientBatchEngine:
             try:
                 self.native_step = NativeResNetStep(model, self.layout, self.C, self.device,
                                                     dtype=self.compute_dtype or torch.float32)
+                if self.deterministic:
+                    self.native_step.enable_deterministic()
                 logging.info("virtual-client engine: native HIP ResNet path (C=%d, %s)", self.C,
                              self.native_step.dtype)
             except UnsupportedNative as e:
@@ -434,19 +436,34 @@ class ClientBatchEngine:
         if self._graphs:
             torch.cuda.synchronize(self.device)
             self._graphs.clear()
+        if self.native_step is not None:
+            self.native_step.close()     # releases the deterministic-accumulation tables, if any
         if getattr(self, "_prev_benchmark", None) is not None:
             torch.backends.cudnn.benchmark = self._prev_benchmark
             self._prev_benchmark = None
 
+    def _counts_dev(self, b_c):
+        """(per-client batch sizes as fp32 ≥ 1, as int32) on the device, cached per batch pattern: an
+        epoch has a handful of patterns (full batches, the ragged last one), so steady-state steps make
+        no host tensors and no host→device copies for them."""
+        key = tuple(b_c)
+        ent = self._counts_cache.get(key) if hasattr(self, "_counts_cache") else None
+        if ent is None:
+            if not hasattr(self, "_counts_cache") or len(self._counts_cache) >= 64:
+                self._counts_cache = {}      # bounded: sampled / heterogeneous rounds vary the patterns
+            ent = self._counts_cache[key] = (
+                torch.tensor([max(1, b) for b in b_c], dtype=torch.float32, device=self.device),
+                torch.tensor(b_c, dtype=torch.int32, device=self.device))
+        return ent
+
     def _fill_static(self, st, x, y, mask, b_c, active):
         st["x"].copy_(x, non_blocking=True)
         st["y"].copy_(y, non_blocking=True)
-        bc = torch.tensor([max(1, b) for b in b_c], dtype=torch.float32).pin_memory() \
-            .to(self.device, non_blocking=True)
+        bc, nimg = self._counts_dev(b_c)
         torch.div(mask.to(torch.float32), bc.view(-1, 1), out=st["rs"])
         st["act"].copy_(active, non_blocking=True)
         if "nimg" in st:
-            st["nimg"].copy_(torch.tensor(b_c, dtype=torch.int32).pin_memory(), non_blocking=True)
+            st["nimg"].copy_(nimg, non_blocking=True)
 
     # ---------------------------------------------------------------- sequential per-client path
     def _seq_param_views(self):

@@ -242,13 +242,15 @@ def test_native_step_f32_matches_reference(builder, hw):
 
     Tolerance, measured rather than chosen: fp32 gradients agree with fp64 to ~1e-6 except where a ReLU
     pre-activation sits within rounding of 0 — its mask (and that element's gradient, |g| not ~eps·|g|)
-    then depends on the last bit of the BN scale/shift, which follows the order of the statistics sums.
-    One flip moves every upstream gradient of these tiny random-init nets by 1e-3..1e-2. So the test
-    measures, on the same inputs, how far the fp64 gradients move under perturbations at the precision of
-    the mode's products (inputs and weights × (1 ± u), u = 2^-24 for exact fp32, 2^-16 for the split-bf16
-    mode; 3 draws) and how far PyTorch's own fp32 GPU step is from fp64; the native step must stay within
-    3× the larger of the two (floor 1e-5), per parameter slot. The bulk of the slots must in addition sit
-    at fp32 accuracy: the median slot error ≤ 10 × PyTorch fp32's median (floor 1e-6)."""
+    then depends on the last bits of the BN scale/shift. One flip moves every upstream gradient of these
+    tiny random-init nets by 1e-4..1e-2; with ~10⁶ pre-activations per step a flip is a coin toss for ANY
+    fp32 implementation (measured: the native exact step flipped one mask on the [1,1,1] net, PyTorch fp32
+    did not on that seed; both flip on others). Two bounds, both measured on the same inputs:
+      * outliers: the fp64 step under input/weight perturbations × (1 ± u) — u = 2^-20 (16 fp32 ulps, enough
+        to flip a few masks per draw) for exact products, 2^-16 for the split-bf16 mode — 3 draws; the native
+        step stays within 3× the larger of that flip spread and PyTorch fp32's own error, per slot (floor 1e-5);
+      * bulk: the median slot error ≤ 10 × the median of PyTorch fp32 (exact products) or of the 2^-16
+        perturbed fp64 step (split-bf16 products) (floor 1e-6) — no systematic error."""
     torch.manual_seed(0)
     model = builder()
     layout = ParamLayout.from_module(model)
@@ -269,7 +271,7 @@ def test_native_step_f32_matches_reference(builder, hw):
     ref_loss, ref64 = _reference_grads(model, layout, flat64, x64, y.cpu(), torch.float64, "cpu")
     assert abs(loss - ref_loss) / ref_loss < 1e-5 * TOL[_mode[0]], (loss, ref_loss)
     _, t32 = _reference_grads(model, layout, flat, x, y, torch.float32, DEV)
-    u = 2.0 ** -24 if _mode[0] == "exact" else 2.0 ** -16
+    u = 2.0 ** -20 if _mode[0] == "exact" else 2.0 ** -16
     pert = []
     for r in range(3):
         g = torch.Generator().manual_seed(1000 + r)
@@ -296,7 +298,10 @@ def test_native_step_f32_matches_reference(builder, hw):
           f"{sorted(e_t32)[len(e_t32) // 2]:.2e}; perturbed fp64 max {max(e_pert):.2e} -> bound {bound:.2e}")
     assert not bad, (bound, bad[:8])
     med = sorted(e for _, e in e_nat)[len(e_nat) // 2]
-    assert med <= max(10 * sorted(e_t32)[len(e_t32) // 2], 1e-6) * TOL[_mode[0]], med
+    # bulk yardstick at the mode's product precision: PyTorch fp32 for exact products; the fp64 step perturbed
+    # at 2^-16 for split-bf16 products (~2^-16 relative each, so that is the noise they are entitled to)
+    ref_med = sorted(e_t32)[len(e_t32) // 2] if _mode[0] == "exact" else sorted(e_pert)[len(e_pert) // 2]
+    assert med <= max(10 * ref_med, 1e-6), (med, ref_med)
     s = layout.slot("bn1.running_mean")
     m = copy.deepcopy(model).to(DEV)
     m.train()

@@ -1,0 +1,76 @@
+"""Recomputed-y bottlenecks (parallel/native_resnet.py ``_ry_ok``): the last 1×1 conv of a bottleneck never
+stores its output y3 — statistics from a stats-only pass, the block output from a second pass of the same
+GEMM (EPI_BOUT), Σg·y3 from the Gram product gᵀ·h2, and the fused 1×1 backward rebuilds y3 per pixel stage.
+
+Against the stored-y path on the same inputs, both in deterministic mode (order-independent statistics): the
+forward is the same kernel with the same tiling (block outputs bitwise equal), the backward masks come from
+the same forward values, and only the order of the Σg·y3 reduction differs — so gradients agree to fp32
+reduction noise (no ReLU-flip allowance needed)."""
+import pytest
+import torch
+
+from fedml_amd.core.arena import ParamLayout
+from fedml_amd.models.cv.resnet import Bottleneck, ResNet
+from fedml_amd.parallel.native_resnet import NativeResNetStep
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _run(monkeypatch, flag, model, layout, flat, x, y, counts):
+    monkeypatch.setenv("FEDML_AMD_RECOMPUTE_Y", flag)
+    C, N = x.shape[0], x.shape[1]
+    arena = flat.view(1, -1).repeat(C, 1).contiguous()
+    garena = torch.zeros_like(arena)
+    mask = torch.arange(N, device=DEV).view(1, -1) < torch.tensor(counts, device=DEV).view(-1, 1)
+    row_scale = mask.float() / torch.tensor([max(1, b) for b in counts], device=DEV).view(-1, 1)
+    active = torch.tensor([1.0 if b else 0.0 for b in counts], device=DEV)
+    nimg = torch.tensor(counts, dtype=torch.int32, device=DEV)
+    step = NativeResNetStep(model, layout, C, DEV, dtype=torch.float32)
+    # order-independent statistics: two separate runs see the same BN scale/shift bits (fp32 atomics would
+    # differ run to run in the last bit, and so would every activation downstream)
+    step.enable_deterministic()
+    try:
+        loss = float(step.step(arena, garena, x, y, row_scale, active, nimg=nimg))
+        torch.cuda.synchronize()
+    finally:
+        step.close()
+    outs = [b.out.clone() for b in step.blocks]
+    return loss, arena, garena, outs, step
+
+
+@pytest.mark.parametrize("mode", ["exact", "bf16x3"])
+@pytest.mark.parametrize("layers,hw,counts", [([1, 1, 1], 16, [16, 16, 16]), ([2, 2, 2], 32, [16, 11, 3, 0])])
+def test_recompute_y_matches_stored_y(monkeypatch, mode, layers, hw, counts):
+    from fedml_amd.ops import nn_ops
+    nn_ops.set_f32_mma_mode(mode)
+    try:
+        torch.manual_seed(0)
+        model = ResNet(Bottleneck, layers, 10)
+        layout = ParamLayout.from_module(model)
+        flat = layout.flatten(model.state_dict()).to(DEV)
+        C, N = len(counts), 16
+        x = torch.randn(C, N, 3, hw, hw, device=DEV)
+        y = torch.randint(0, 10, (C, N), device=DEV)
+        l0, a0, g0, o0, s0 = _run(monkeypatch, "0", model, layout, flat, x, y, counts)
+        l1, a1, g1, o1, s1 = _run(monkeypatch, "1", model, layout, flat, x, y, counts)
+    finally:
+        nn_ops.set_f32_mma_mode("exact")
+    assert not any(b.ry for b in s0.blocks)
+    assert all(b.ry and b.ys[-1] is None for b in s1.blocks)
+    for c, n in enumerate(counts):
+        for u, v in zip(o0, o1):      # block outputs of the valid images: same kernel, same tiling
+            assert torch.equal(u[c, :n], v[c, :n])
+    assert abs(l0 - l1) <= 1e-6 * abs(l0)
+    bad = []
+    for s in layout.slots:
+        sl = slice(s.offset, s.offset + s.numel)
+        if s.trainable:
+            r = g0[:, sl]
+            err = float((g1[:, sl] - r).norm() / r.norm().clamp_min(1e-30))
+            if err > 2e-5:
+                bad.append((s.key, err))
+        else:   # BN running statistics / counters: from the same forward statistics
+            assert torch.allclose(a1[:, sl], a0[:, sl], rtol=1e-6, atol=1e-7), s.key
+    assert not bad, bad[:8]
+    assert float(g1[counts.index(0)].abs().max()) == 0.0 if 0 in counts else True
