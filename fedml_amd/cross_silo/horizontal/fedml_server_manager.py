@@ -207,6 +207,7 @@ class FedMLServerManager(ServerManager):
             logging.exception("server-side test failed")
         now = time.time()
         self.round_times.append(now - self._t0)
+        logging.info("round %d complete in %.3f s", self.round_idx, now - self._t0)
         self._t0 = now
         MLOpsMetrics.get_instance().report_server_training_round_info(
             {"run_id": getattr(self.args, "run_id", "0"), "round_index": self.round_idx,

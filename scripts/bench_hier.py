@@ -34,6 +34,9 @@ def _free_port():
 
 
 def worker(a):
+    import faulthandler
+    # a stuck process prints where every thread is (and the run keeps producing output while it waits)
+    faulthandler.dump_traceback_later(a.stack_dump_s, repeat=True)
     import torch
     sys.path.insert(0, ROOT)
     import fedml_amd
@@ -78,6 +81,7 @@ def main():
     p.add_argument("--wan-compression", default="", help="'' (fp32 state dicts, the reference) | int8")
     p.add_argument("--silo-transport", default="", help="'' (network payloads) | device (same-node HBM plane)")
     p.add_argument("--timeout", type=float, default=900)
+    p.add_argument("--stack-dump-s", type=float, default=90, help="workers dump their Python stacks this often")
     # worker-internal
     p.add_argument("--role", default="")
     p.add_argument("--silo", type=int, default=0)
@@ -107,14 +111,18 @@ def main():
                                                   "--pg-port", str(port), "--gpu", str(i % ngpu)], env=env))
             i += 1
     t0 = time.time()
-    codes = []
-    for pr in procs:
-        try:
-            codes.append(pr.wait(timeout=max(1.0, a.timeout - (time.time() - t0))))
-        except subprocess.TimeoutExpired:
+    last = t0
+    while any(pr.poll() is None for pr in procs):
+        if time.time() - t0 > a.timeout:
             for q in procs:
                 q.kill()
             raise SystemExit("bench_hier: timed out")
+        if time.time() - last > 30:
+            last = time.time()
+            print(f"bench_hier: {last - t0:.0f} s, {sum(pr.poll() is None for pr in procs)} workers running",
+                  flush=True)
+        time.sleep(0.5)
+    codes = [pr.returncode for pr in procs]
     if any(codes):
         raise SystemExit(f"bench_hier: worker exit codes {codes}")
     res = json.load(open(out))
