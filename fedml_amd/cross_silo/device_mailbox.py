@@ -17,6 +17,12 @@ slots with the FedAvg kernel straight from the shared stack. Ordering is by mess
 synchronises its stream before it sends the message that tells the reader to look.
 
 Genuine WAN deployments keep the network transport (``silo_transport`` unset)."""
+import fcntl
+import logging
+import os
+import tempfile
+import time
+
 import torch
 
 KEY = "__devmail__"
@@ -63,8 +69,18 @@ class ServerMailbox:
 class SiloMailbox:
     def __init__(self, desc: dict, slot: int):
         self.P = int(desc["P"])
-        self.glob = _open(desc["glob"])
-        self.slots = _open(desc["slots"])
+        # one importer at a time on the node: the silo masters all receive the descriptor at once, and
+        # concurrent imports of the same dmabuf-backed IPC handles were seen to stall (8 silos; 2 were fine)
+        t0 = time.time()
+        with open(os.path.join(tempfile.gettempdir(), "fedml_amd_ipc_open.lock"), "a+") as lk:
+            fcntl.flock(lk, fcntl.LOCK_EX)
+            try:
+                self.glob = _open(desc["glob"])
+                self.slots = _open(desc["slots"])
+                torch.cuda.synchronize()
+            finally:
+                fcntl.flock(lk, fcntl.LOCK_UN)
+        logging.info("device mailbox opened in %.2f s (slot %d)", time.time() - t0, int(slot))
         self.slot = int(slot)
 
     def read_global(self, out: torch.Tensor):

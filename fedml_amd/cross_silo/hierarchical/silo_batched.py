@@ -39,8 +39,8 @@ class SiloBatchedTrainer:
         self.args = args
         self.device = torch.device(device)
         self.n_local = int(n_local)
-        offs, counts = split_local_clients(silo_data, self.n_local)
-        store = DeviceClientStore(silo_data.x.to(self.device), silo_data.y.to(self.device), offs, counts)
+        self._stores = {}
+        store, counts = self._store(None, silo_data)
         a = copy.copy(args)
         a.client_num_in_total = self.n_local
         a.client_num_per_round = self.n_local
@@ -53,6 +53,23 @@ class SiloBatchedTrainer:
         self.last_loss = None
         logging.info("silo: %d local clients (%s samples), %d of them on this process", self.n_local, counts,
                      len(self.sim.assignment(0)[1]))
+
+    def _store(self, key, silo_data: ClientData):
+        offs, counts = split_local_clients(silo_data, self.n_local)
+        st = DeviceClientStore(silo_data.x.to(self.device), silo_data.y.to(self.device), offs, counts)
+        self._stores[key] = st
+        return st, counts
+
+    def set_data(self, key, silo_data: ClientData):
+        """Train on another data shard from now on (the server assigns silos a data index per round): the
+        engine, its arenas and its captured graphs are kept — only the device data store changes (cached per
+        index)."""
+        st = self._stores.get(key)
+        if st is None:
+            st, _ = self._store(key, silo_data)
+        self.sim.store = st
+        self.sim.sample_counts = st.counts_host
+        self.num_samples = int(sum(st.counts_host))
 
     def load_global(self, params):
         """A state dict, or the flat global model (device tensor, e.g. the device plane's shared buffer)."""

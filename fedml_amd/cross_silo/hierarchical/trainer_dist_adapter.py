@@ -35,6 +35,7 @@ class TrainerDistAdapter:
         # engine, client-parallel over the silo's processes (silo_batched.py) instead of one DDP replica
         self.n_local = int(getattr(args, "silo_local_clients", 1) or 1)
         self.silo_trainers = {}
+        self.silo_trainer = None
         self._pending = None
         self.ddp = FlatDDP(model, self.device, bucket_mb=float(getattr(args, "ddp_bucket_mb", 64.0))) \
             if self.n_proc > 1 and self.n_local <= 1 else None
@@ -58,10 +59,17 @@ class TrainerDistAdapter:
     def update_dataset(self, client_index):
         self.client_index = int(client_index)
         if self.n_local > 1:
-            if self.client_index not in self.silo_trainers:   # collective: every silo process builds it
+            # ONE client-batched engine per silo process (collective: every silo process builds it); a new data
+            # index only swaps its device data store — an engine per index would hold S copies of the model,
+            # optimizer state and activations
+            data = self.train_data_local_dict[self.client_index]
+            if self.silo_trainer is None:
                 from .silo_batched import SiloBatchedTrainer
-                self.silo_trainers[self.client_index] = SiloBatchedTrainer(
-                    self.args, self.device, self.model, self.train_data_local_dict[self.client_index], self.n_local)
+                self.silo_trainer = SiloBatchedTrainer(self.args, self.device, self.model, data, self.n_local)
+                self.silo_trainer.set_data(self.client_index, data)
+            else:
+                self.silo_trainer.set_data(self.client_index, data)
+            self.silo_trainers[self.client_index] = self.silo_trainer
             self.local_sample_number = self.train_data_local_num_dict[self.client_index]
             return
         self.train_local = self._shard(self.train_data_local_dict[self.client_index])

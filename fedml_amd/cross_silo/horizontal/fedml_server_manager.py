@@ -59,6 +59,7 @@ class FedMLServerManager(ServerManager):
         self.client_online_mapping = {}
         self.start_running_time = 0.0
         self.round_times = []
+        self.test_times = []
         self._selected = []
         self._started = False
         to = getattr(args, "round_timeout", None)
@@ -201,14 +202,18 @@ class FedMLServerManager(ServerManager):
         prof.log_event_started("aggregate", event_value=str(self.round_idx))
         g = self.aggregator.aggregate()
         prof.log_event_ended("aggregate", event_value=str(self.round_idx))
+        if torch.is_tensor(g) and g.is_cuda:
+            torch.cuda.synchronize(g.device)
+        now = time.time()   # the round's training + aggregation; server-side evaluation is timed on its own
         try:
+            t_test = time.time()
             self.aggregator.test_on_server_for_all_clients(self.round_idx)
+            self.test_times.append(time.time() - t_test)
         except Exception:  # evaluation must never stall the federation (reference behaviour)
             logging.exception("server-side test failed")
-        now = time.time()
         self.round_times.append(now - self._t0)
         logging.info("round %d complete in %.3f s", self.round_idx, now - self._t0)
-        self._t0 = now
+        self._t0 = time.time()
         MLOpsMetrics.get_instance().report_server_training_round_info(
             {"run_id": getattr(self.args, "run_id", "0"), "round_index": self.round_idx,
              "total_rounds": self.round_num, "running_time": round(now - self.start_running_time, 4)})

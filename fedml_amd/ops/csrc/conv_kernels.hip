@@ -29,7 +29,11 @@ using prec::BF16;
 using prec::F32;
 using prec::F32X3;
 
-enum { PRO_NONE = 0, PRO_BNRELU = 1 };
+// PRO_BOUT (conv_gemm_kernel, 1×1 / stride 1 forward only): the previous block's output is formed in the operand
+//   load, a = relu(y·s + t + r) with r = src2 (identity shortcut) | src2·rs + rt (downsample BN) — the same
+//   operation order as block_out_kernel — and written once to `pro_out` by the blockIdx.z == 0 workgroups: the
+//   block output pass of that block (read y and r, write out, then this conv reads out again) disappears.
+enum { PRO_NONE = 0, PRO_BNRELU = 1, PRO_BOUT = 2 };
 // EPI_BOUT (conv_gemm_kernel only): the bottleneck block output straight from the last conv's accumulators,
 //   out = relu((acc − K)·e_s + e_t + r),  r = e_add (identity shortcut) | e_add·e_rs + e_rt (downsample BN)
 // — the conv's output y itself is never stored (its BN statistics come from a stats-only EPI_FWD pass)
@@ -208,7 +212,9 @@ struct ConvArgs {        // activations / packed weights are P::T (bf16 | fp32)
   int64_t wpk_ld;        // per-client stride of the packed weights (elements)
   const float* vec0;     // PRO scale  | α
   const float* vec1;     // PRO shift  | β
-  const float* vec2;     //            | γ
+  const float* vec2;     //            | γ       | PRO_BOUT: shortcut-BN scale (null: identity)
+  const float* vec3;     // PRO_BOUT: shortcut-BN shift
+  void* pro_out;         // PRO_BOUT: the formed block output [C][Nb][Hs][Ws][KC]
   void* out;             // [C][M][NOUT]
   // epilogue inputs
   const void* e_x;       // EPI_MASK: previous raw activation (mask + Σg·x); EPI_BLOCK: block input (mask)
@@ -256,7 +262,8 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
   float* v0 = reinterpret_cast<float*>(smem + (size_t)NOUT * a.ldk * P::ES);    // [KC]
   float* v1 = v0 + a.KC;
   float* v2 = v1 + a.KC;
-  float* red = v2 + a.KC;                                                         // [4][NOUT][3]
+  float* v3 = v2 + a.KC;
+  float* red = v3 + a.KC;                                                         // [4][NOUT][3]
   T* stage = reinterpret_cast<T*>(red + 4 * NOUT * 3);                           // [4][16][NOUT]
   T* my_stage = stage + wid * 16 * NOUT;
 
@@ -267,11 +274,12 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
     uint4* dst = reinterpret_cast<uint4*>(wl);
     const int n16 = NOUT * a.ldk / V;
     for (int i = threadIdx.x; i < n16; i += 256) dst[i] = src[i];
-    if (AOP == AOP_DY || PRO == PRO_BNRELU) {
+    if (AOP == AOP_DY || PRO != PRO_NONE) {
       for (int i = threadIdx.x; i < a.KC; i += 256) {
         v0[i] = a.vec0[(int64_t)c * a.KC + i];
         v1[i] = a.vec1[(int64_t)c * a.KC + i];
-        if (AOP == AOP_DY) v2[i] = a.vec2[(int64_t)c * a.KC + i];
+        if (AOP == AOP_DY || (PRO == PRO_BOUT && a.vec2)) v2[i] = a.vec2[(int64_t)c * a.KC + i];
+        if (PRO == PRO_BOUT && a.vec2) v3[i] = a.vec3[(int64_t)c * a.KC + i];
       }
     }
     for (int i = threadIdx.x; i < 4 * NOUT * 3; i += 256) red[i] = 0.f;
@@ -280,8 +288,9 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
 
   const int64_t src_client = (int64_t)c * a.Nb * a.Hs * a.Ws * a.KC;
   const T* src = reinterpret_cast<const T*>(a.src) + src_client;
-  const T* src2 = (AOP == AOP_DY) ? reinterpret_cast<const T*>(a.src2) + src_client : nullptr;
+  const T* src2 = (AOP == AOP_DY || PRO == PRO_BOUT) ? reinterpret_cast<const T*>(a.src2) + src_client : nullptr;
   T* out = a.out ? reinterpret_cast<T*>(a.out) + (int64_t)c * Mo * NO : nullptr;   // null: statistics only (EPI_FWD)
+  T* pro_out = (PRO == PRO_BOUT && blockIdx.z == 0) ? reinterpret_cast<T*>(a.pro_out) + src_client : nullptr;
   const T* e_x = reinterpret_cast<const T*>(a.e_x);
   const T* e_add = reinterpret_cast<const T*>(a.e_add);
   const T* e_y1 = reinterpret_cast<const T*>(a.e_y1);
@@ -367,6 +376,24 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
           if (AOP == AOP_ACT && PRO == PRO_BNRELU) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j] * v0[ci + j] + v1[ci + j], 0.f);
+          } else if (AOP == AOP_ACT && PRO == PRO_BOUT) {
+            float r[8];
+            P::load8(src2 + off, r);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) f[j] = f[j] * v0[ci + j] + v1[ci + j];
+            if (a.vec2) {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) f[j] += r[j] * v2[ci + j] + v3[ci + j];
+            } else {
+#pragma unroll
+              for (int j = 0; j < 8; ++j) f[j] += r[j];
+            }
+#pragma unroll
+            for (int j = 0; j < 8; ++j) f[j] = P::round(fmaxf(f[j], 0.f));   // the operand = the stored value
+            if (pro_out) {
+#pragma unroll
+              for (int q = 0; q < 8 / V; ++q) *reinterpret_cast<uint4*>(pro_out + off + q * V) = P::pack(f + q * V);
+            }
           } else if (AOP == AOP_DY) {
             float yv[8];
             P::load8(src2 + off, yv);
@@ -514,7 +541,7 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
 
 template <class P>
 static size_t conv_smem_bytes(int nout, int ldk, int kc) {
-  return (size_t)nout * ldk * P::ES + (size_t)3 * kc * 4 + (size_t)4 * nout * 3 * 4 + (size_t)4 * 16 * nout * P::ES;
+  return (size_t)nout * ldk * P::ES + (size_t)4 * kc * 4 + (size_t)4 * nout * 3 * 4 + (size_t)4 * 16 * nout * P::ES;
 }
 
 // =====================================================================================
@@ -981,6 +1008,23 @@ static int conv_fwd(const void* x, const void* wpk, int64_t wpk_ld, const float*
   return dispatch_nt<P, AOP_ACT, PRO_NONE, MODE_FWD, EPI_FWD>(Cout, a, C, stream);
 }
 
+// 1×1 / stride-1 forward whose operand is the previous block's output formed on the fly (PRO_BOUT), written to
+// `bout` on the way: bout = relu(yp·s + t + r), r = res | res·rs + rt;  y = conv(bout) − K, stats as conv_fwd
+template <class P>
+static int conv_fwd_pbout(const void* yp, const float* s, const float* t, const void* res, const float* rs,
+                          const float* rt, void* bout, const void* wpk, int64_t wpk_ld, void* y, float* stats, int C,
+                          int Nb, int H, int W, int Cin, int Cout, int ldk, int tiles_per_wave, const float* pivot,
+                          const int* nimg, hipStream_t stream) {
+  if (Cin % 8 != 0 || !s || !t || !res || !bout || (rs && !rt)) return -3;
+  ConvArgs a = {};
+  a.src = yp; a.src2 = res; a.vec0 = s; a.vec1 = t; a.vec2 = rs; a.vec3 = rt; a.pro_out = bout;
+  a.wpk = wpk; a.wpk_ld = wpk_ld; a.out = y; a.stats = stats; a.NS = 2; a.pivot = pivot; a.nimg = nimg;
+  a.Nb = Nb; a.Hs = H; a.Ws = W; a.KC = Cin; a.Ho = H; a.Wo = W; a.KH = 1; a.KW = 1; a.stride = 1;
+  a.pad = 0; a.ldk = ldk; a.Kp = (Cin + 31) / 32 * 32; a.tiles_per_wave = tiles_per_wave;
+  if (Cout % 64 == 0 && (Cout > 256 || Cin > convk_min_k())) return -5;   // the K-streamed kernel has no PRO_BOUT
+  return dispatch_nt<P, AOP_ACT, PRO_BOUT, MODE_FWD, EPI_FWD>(Cout, a, C, stream);
+}
+
 // bottleneck block output from the last 1×1 conv (EPI_BOUT): out = relu(BN(conv(relu(x·ps + pt)) − K) + shortcut)
 template <class P>
 static int conv_fwd_bout(const void* x, const void* wpk, int64_t wpk_ld, const float* pscale, const float* pshift,
@@ -1062,6 +1106,21 @@ FA_EXPORT int fa_conv_fwd_bout_f32(const float* x, const float* wpk, int64_t wpk
                                    int Cin, int Cout, int ldk, int tiles_per_wave, const int* nimg, hipStream_t stream) {
   FA_F32_DISPATCH(prec, conv_fwd_bout<PX>(x, wpk, wpk_ld, pscale, pshift, out, s, t, pivot, res, rs, rt, C, Nb, H, W,
                                           Cin, Cout, ldk, tiles_per_wave, nimg, stream));
+}
+
+FA_EXPORT int fa_conv_fwd_pbout(const uint16_t* yp, const float* s, const float* t, const uint16_t* res,
+                                const float* rs, const float* rt, uint16_t* bout, const uint16_t* wpk, int64_t wpk_ld,
+                                uint16_t* y, float* stats, int C, int Nb, int H, int W, int Cin, int Cout, int ldk,
+                                int tiles_per_wave, const float* pivot, const int* nimg, hipStream_t stream) {
+  return conv_fwd_pbout<BF16>(yp, s, t, res, rs, rt, bout, wpk, wpk_ld, y, stats, C, Nb, H, W, Cin, Cout, ldk,
+                              tiles_per_wave, pivot, nimg, stream);
+}
+FA_EXPORT int fa_conv_fwd_pbout_f32(const float* yp, const float* s, const float* t, const float* res,
+                                    const float* rs, const float* rt, float* bout, const float* wpk, int64_t wpk_ld,
+                                    float* y, float* stats, int C, int Nb, int H, int W, int Cin, int Cout, int ldk,
+                                    int tiles_per_wave, const float* pivot, const int* nimg, hipStream_t stream) {
+  FA_F32_DISPATCH(prec, conv_fwd_pbout<PX>(yp, s, t, res, rs, rt, bout, wpk, wpk_ld, y, stats, C, Nb, H, W, Cin, Cout,
+                                           ldk, tiles_per_wave, pivot, nimg, stream));
 }
 
 // backward-data: dx = convᵀ(α·g + β·y + γ) with epilogue

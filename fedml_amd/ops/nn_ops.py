@@ -8,6 +8,7 @@ Every conv / block launcher exists for two storage precisions (``csrc/prec.h``):
 chosen from the dtype of the activation tensor, so one orchestration drives both.
 """
 import ctypes
+import os
 
 import torch
 
@@ -66,6 +67,22 @@ def conv_fwd(x, wpk, wpk_ld, pscale, pshift, y, stats, C, N, H, W, Cin, Cout, KH
                             _i(H), _i(W), _i(Cin), _i(Cout), _i(KH), _i(KW), _i(stride), _i(pad), _i(Ho), _i(Wo),
                             _i(ldk), _i(tiles_per_wave), _p(pivot), _p(nimg), _stream(x))
     _check(rc, "fa_conv_fwd")
+
+
+def convk_min_k() -> int:
+    """K above which the wide-layer dispatch runs the K-streamed kernel (conv_kernels.hip convk_min_k)."""
+    return int(os.environ.get("FEDML_AMD_CONVK_MIN_K", "256") or 256)
+
+
+def conv_fwd_pbout(yp, s, t, res, rs, rt, bout, wpk, wpk_ld, y, stats, C, N, H, W, Cin, Cout, ldk, tiles_per_wave,
+                   pivot=None, nimg=None):
+    """1×1 / stride-1 forward whose operand is the previous block's output formed in the operand load and written
+    to ``bout`` once: bout = relu(yp·s + t + r), r = res (identity) | res·rs + rt (downsample BN) — bit-identical to
+    :func:`block_out` —; y = conv(bout) − pivot with its BN statistics, as :func:`conv_fwd`."""
+    rc = _fnp("fa_conv_fwd_pbout", yp)(_p(yp), _p(s), _p(t), _p(res), _p(rs), _p(rt), _p(bout), _p(wpk), _i64(wpk_ld),
+                                       _p(y), _p(stats), _i(C), _i(N), _i(H), _i(W), _i(Cin), _i(Cout), _i(ldk),
+                                       _i(tiles_per_wave), _p(pivot), _p(nimg), _stream(yp))
+    _check(rc, "fa_conv_fwd_pbout")
 
 
 def conv_fwd_bout(x, wpk, wpk_ld, pscale, pshift, out, s, t, pivot, res, rs, rt, C, N, H, W, Cin, Cout, ldk,

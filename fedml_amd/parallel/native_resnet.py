@@ -155,6 +155,7 @@ class NativeResNetStep:
         self.use_dym = os.environ.get("FEDML_AMD_DY_MATERIALIZE", "1") != "0"
         self.use_s2k = os.environ.get("FEDML_AMD_C3S2_CONVK", "1") == "1"   # measured +2 % (fp32 headline)
         self.use_ry = os.environ.get("FEDML_AMD_RECOMPUTE_Y", "0") == "1" and dtype == torch.float32
+        self.use_pbout = os.environ.get("FEDML_AMD_FUSE_BOUT", "1") != "0"
         self.dump = None   # debug: list collecting (name, tensor clone) of every backward gradient buffer
         self._nimg = None
         self.det = None    # DetAccumulator in deterministic mode (enable_deterministic)
@@ -417,6 +418,16 @@ class NativeResNetStep:
                 and self._c1f(cv, nn_ops.EPI_MASK)
                 and nn_ops.conv1x1_wgrad_supported(cv.cin, cv.cout, cv.k, cv.stride, cv.pad))
 
+    def _pbout_ok(self, b, nb) -> bool:
+        """Block ``b``'s output is formed in the operand load of the next block's first conv (conv_fwd_pbout: 1×1,
+        stride 1, identity shortcut in the next block — its only other reader is that block's output pass, which
+        then reads the stored output) instead of by its own block-output pass."""
+        if not self.use_pbout or nb is None or b.ry or nb.ds_conv is not None:
+            return False
+        cv = nb.convs[0]
+        return (cv.k == 1 and cv.stride == 1 and cv.pad == 0 and cv.cin == cv.cin_pad
+                and not (cv.cout % 64 == 0 and (cv.cout > 256 or cv.cin > nn_ops.convk_min_k())))
+
     def _c1f(self, cv: ConvSpec, epi):
         return (self.use_c1f and cv.cin == cv.cin_pad
                 and nn_ops.conv1x1_bwd_fused_supported(cv.cin, cv.cout, cv.k, cv.stride, cv.pad, epi))
@@ -510,13 +521,20 @@ class NativeResNetStep:
                          N * st_conv.Ho * st_conv.Wo * st_conv.cout, st_conv.cout, nimg=self._nimg,
                          per_img=st_conv.Ho * st_conv.Wo * st_conv.cout)
         act_in = self.stem_out
-        for b in self.blocks:
+        pend = None    # (yp, s, t, res, rs, rt, bout) of a block output formed by the next block's first conv
+        for bi, b in enumerate(self.blocks):
             b.act_in = act_in
-            prev = None
             for j, (cv, bn) in enumerate(zip(b.convs, b.bns)):
                 src = act_in if j == 0 else b.ys[j - 1]
                 pro = None if j == 0 else self.bn_vec[b.bns[j - 1].key]
-                self._fwd(cv, src, b.ys[j], pro, bn, N)
+                if j == 0 and pend is not None:
+                    nn_ops.conv_fwd_pbout(*pend, self.packed.view(-1)[cv.off_f:], self.packed_ld, b.ys[0],
+                                          self.stat_views[bn.key][0], C, N, cv.H, cv.W, cv.cin_pad, cv.cout, cv.ldk,
+                                          self._tiles_per_wave(N * cv.Ho * cv.Wo), pivot=self.bn_vec[bn.key][7],
+                                          nimg=self._nimg)
+                    pend = None
+                else:
+                    self._fwd(cv, src, b.ys[j], pro, bn, N)
                 if b.ys[j] is None:     # recomputed-y conv: keep the pivot its later passes must subtract
                     self.bn_vec[bn.key][8].copy_(self.bn_vec[bn.key][7])
                 self._bn_fwd(bn, N, cv.Ho * cv.Wo, arena, active)
@@ -526,7 +544,10 @@ class NativeResNetStep:
                 d = b.ds_conv
                 self._fwd(d, act_in, b.yd, None, b.ds_bn, N)
                 self._bn_fwd(b.ds_bn, N, d.Ho * d.Wo, arena, active)
-            if b.ry:    # block output from a second pass of the last conv (its output y3 is never stored)
+            if self._pbout_ok(b, self.blocks[bi + 1] if bi + 1 < len(self.blocks) else None):
+                vd = self.bn_vec[b.ds_bn.key] if b.ds_conv is not None else (None, None)
+                pend = (b.ys[-1], vl[0], vl[1], b.yd if b.ds_conv is not None else act_in, vd[0], vd[1], b.out)
+            elif b.ry:    # block output from a second pass of the last conv (its output y3 is never stored)
                 pv = self.bn_vec[b.bns[-2].key]
                 res, rs, rt = (b.yd, self.bn_vec[b.ds_bn.key][0], self.bn_vec[b.ds_bn.key][1]) \
                     if b.ds_conv is not None else (act_in, None, None)

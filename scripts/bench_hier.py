@@ -46,7 +46,8 @@ def worker(a):
            "epochs": 1, "batch_size": a.batch_size, "learning_rate": a.lr, "client_optimizer": "adamw",
            "weight_decay": 0.01, "frequency_of_the_test": 0, "backend": "TCP", "federated_optimizer": "FedAvg",
            "worker_num": a.silos + 1, "client_id_list": str(list(range(1, a.silos + 1))), "sys_perf_interval": 0,
-           "synthetic_samples_per_client": a.samples_per_client * a.local_clients, "rank": a.silo,
+           "synthetic_train_samples_per_client": a.samples_per_client * a.local_clients,
+           "synthetic_test_samples_per_client": 8, "partition_method": "homo", "rank": a.silo,
            "n_proc_in_silo": a.procs_per_silo, "proc_rank_in_silo": a.rank_in_silo, "pg_master_port": a.pg_port,
            "silo_local_clients": a.local_clients, "compute_dtype": a.dtype,
            "using_gpu": torch.cuda.is_available(), "gpu_id": a.gpu, "rank_in_node": a.gpu,

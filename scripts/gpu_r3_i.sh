@@ -5,8 +5,12 @@ cd "$(dirname "$0")/.."
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 mkdir -p gpurun_out
 R=$PWD
-timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_spectral_gpu.py -m gpu \
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_spectral_gpu.py tests/test_fused_block_out_gpu.py tests/test_recompute_y_gpu.py -m gpu \
   > gpurun_out/t_i.log 2>&1; rc=$?; tail -3 gpurun_out/t_i.log; [ $rc -eq 0 ] || exit $rc
+for fb in 1 0; do
+  FEDML_AMD_FUSE_BOUT=$fb timeout -k 10 300 python -u bench.py --steps 10 --warmup 2 > gpurun_out/b_head_fb$fb.log 2>&1; rc=$?
+  echo "fuse_bout=$fb"; grep '^{' gpurun_out/b_head_fb$fb.log | cut -c1-200; [ $rc -eq 0 ] || exit $rc
+done
 bash scripts/gpu_c3_pmc.sh || exit 1
 timeout -k 10 400 python -u bench.py --preset resnet18_cifar10_10 --steps 2 --warmup 1 > gpurun_out/b_r18_fp32.log 2>&1; rc=$?
 grep '^{' gpurun_out/b_r18_fp32.log | cut -c1-300; [ $rc -eq 0 ] || { tail -20 gpurun_out/b_r18_fp32.log; exit $rc; }

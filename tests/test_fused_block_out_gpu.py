@@ -1,0 +1,62 @@
+"""Block output formed in the next conv's operand load (conv_kernels.hip PRO_BOUT, native_resnet ``_pbout_ok``):
+a bottleneck's output relu(bn3(y3) + shortcut) is computed by the next block's first 1×1 conv while it loads
+its operand, and written once from there, instead of by a separate block-output pass that the conv then reads.
+
+The fused step must be bit-identical to the unfused one: same formula in the same operation order, the operand
+is the stored (rounded) value, and everything downstream is the same kernels. Both runs in deterministic mode
+(order-independent statistics), so any difference is the fusion's."""
+import pytest
+import torch
+
+from fedml_amd.core.arena import ParamLayout
+from fedml_amd.models.cv.resnet import Bottleneck, ResNet
+from fedml_amd.parallel.native_resnet import NativeResNetStep
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _run(monkeypatch, flag, model, layout, flat, x, y, counts, dtype):
+    monkeypatch.setenv("FEDML_AMD_FUSE_BOUT", flag)
+    C, N = x.shape[0], x.shape[1]
+    arena = flat.view(1, -1).repeat(C, 1).contiguous()
+    garena = torch.zeros_like(arena)
+    mask = torch.arange(N, device=DEV).view(1, -1) < torch.tensor(counts, device=DEV).view(-1, 1)
+    row_scale = mask.float() / torch.tensor([max(1, b) for b in counts], device=DEV).view(-1, 1)
+    active = torch.tensor([1.0 if b else 0.0 for b in counts], device=DEV)
+    nimg = torch.tensor(counts, dtype=torch.int32, device=DEV)
+    step = NativeResNetStep(model, layout, C, DEV, dtype=dtype)
+    step.enable_deterministic()
+    try:
+        losses = []
+        for _ in range(2):   # second step: BN running statistics / pivots moved by the first
+            garena.zero_()
+            losses.append(float(step.step(arena, garena, x, y, row_scale, active, nimg=nimg)))
+        torch.cuda.synchronize()
+    finally:
+        step.close()
+    return losses, arena, garena, [b.out.clone() for b in step.blocks], step
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("layers,hw,counts", [([2, 2, 2], 16, [16, 16, 16]), ([3, 2, 2], 32, [16, 11, 3, 0])])
+def test_fused_block_output_is_bit_identical(monkeypatch, dtype, layers, hw, counts):
+    torch.manual_seed(0)
+    model = ResNet(Bottleneck, layers, 10)
+    layout = ParamLayout.from_module(model)
+    flat = layout.flatten(model.state_dict()).to(DEV)
+    C, N = len(counts), 16
+    x = torch.randn(C, N, 3, hw, hw, device=DEV)
+    y = torch.randint(0, 10, (C, N), device=DEV)
+    l0, a0, g0, o0, s0 = _run(monkeypatch, "0", model, layout, flat, x, y, counts, dtype)
+    l1, a1, g1, o1, s1 = _run(monkeypatch, "1", model, layout, flat, x, y, counts, dtype)
+    nb = len(s1.blocks)
+    fused = [s1._pbout_ok(s1.blocks[i], s1.blocks[i + 1] if i + 1 < nb else None) for i in range(nb)]
+    assert sum(fused) == sum(layers) - 3 and not any(
+        s0._pbout_ok(s0.blocks[i], s0.blocks[i + 1] if i + 1 < nb else None) for i in range(nb))
+    for c, n in enumerate(counts):
+        for u, v in zip(o0, o1):
+            assert torch.equal(u[c, :n], v[c, :n])
+    assert l0 == l1
+    assert torch.equal(g0, g1)
+    assert torch.equal(a0, a1)
