@@ -75,9 +75,13 @@ def lib(required: bool = False):
         if _lib is None and _load_error is None:
             try:
                 import torch  # noqa: F401  (bind to torch's HIP runtime first)
-                if _stale():
-                    build()
-                _lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+                alt = os.environ.get("FEDML_AMD_LIB")   # A/B measurements: another build of the same library
+                if alt:
+                    _lib = ctypes.CDLL(alt, mode=ctypes.RTLD_GLOBAL)
+                else:
+                    if _stale():
+                        build()
+                    _lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
             except Exception as e:  # pragma: no cover - depends on toolchain
                 _load_error = e
         if _lib is None and required:

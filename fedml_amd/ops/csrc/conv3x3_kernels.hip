@@ -30,6 +30,14 @@ FA_DET_EXPORT(conv3x3)
 #ifndef TAP_UNROLL
 #define TAP_UNROLL 3
 #endif
+// Weight-gradient kernels with ≤ 8 prefetched x chunks per thread run ≥ 2 waves per SIMD: the fp32 instances
+// otherwise allocate 270-290 registers (VGPR + AGPR: loader prefetch registers, 20 accumulator tiles) and run ONE
+// wave per SIMD, so every barrier and exposed load stalls the matrix pipe. Measured (C=100 headline): 64-channel
+// wgrad 880 → 651 µs, 32-channel 590 → 444 µs. The forward / backward-data kernels and the 16-chunk wgrad variants
+// keep the compiler's choice: forced to 256 registers they spill (stage-2 backward-data 452 → 594 µs).
+#ifndef C3W_MIN_WAVES
+#define C3W_MIN_WAVES 2
+#endif
 
 namespace c3 {
 
@@ -496,7 +504,7 @@ struct WArgs {           // activations are P::T
 
 // WN waves split the column tiles of this z-slice, WK = 4/WN waves split the pixel K-steps.
 template <class P, int CIN, int COUT, int PRO, int WN, int TPW, int ST, int MAXC, int MAXD>
-__global__ __launch_bounds__(256) void conv3x3_wgrad_kernel(WArgs a) {
+__global__ __launch_bounds__(256, (MAXC <= 8 ? C3W_MIN_WAVES : 1)) void conv3x3_wgrad_kernel(WArgs a) {
   using T = typename P::T;
   using frag_t = typename P::frag_t;
   constexpr int WK = 4 / WN;

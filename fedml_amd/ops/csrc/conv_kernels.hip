@@ -319,17 +319,62 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
 
   const int tiles_total = (Mv + 15) / 16;
   const int tile0 = (blockIdx.x * 4 + wid) * a.tiles_per_wave;
-  for (int tt = 0; tt < a.tiles_per_wave; ++tt) {
-    const int tile = tile0 + tt;
-    if (tile >= tiles_total) break;
+  const int tile_end = min(tiles_total, tile0 + a.tiles_per_wave);
+  const int IW = MODE == MODE_BWD2 ? a.Ws : a.Wo;
+  // One-deep software pipeline over the wave's (tile, K-chunk) sequence: the raw global operand of the NEXT
+  // chunk — the next tile's first chunk at a tile's last one — is issued before this chunk's transform, MFMAs
+  // and (at a tile's end) epilogue, so its HBM latency hides behind them instead of stalling the wave.
+  constexpr bool TWO = AOP == AOP_DY || PRO == PRO_BOUT;   // second operand stream (y | shortcut)
+  int p_tile = tile0, p_k0 = 0, p_on = 0, p_oh = 0, p_ow = 0, p_ci = 0;
+  bool p_mvalid = false, p_ok = false;
+  int64_t p_off = 0;
+  float pf[8], pr[TWO ? 8 : 1];
+  auto coords = [&](int tile) {
     const int m = tile * 16 + (lane & 15);
-    const bool mvalid = m < Mv;
-    const int mm = mvalid ? m : 0;
-    const int IW = MODE == MODE_BWD2 ? a.Ws : a.Wo;
-    const int on = mm / HWi;
+    p_mvalid = m < Mv;
+    const int mm = p_mvalid ? m : 0;
+    p_on = mm / HWi;
     const int orem = mm % HWi;
-    const int oh = orem / IW, ow = orem % IW;
-
+    p_oh = orem / IW;
+    p_ow = orem % IW;
+  };
+  auto gather = [&]() {
+    p_ok = false;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) pf[j] = 0.f;
+    const int k = p_k0 + 8 * (lane >> 4);
+    if (p_tile >= tile_end || !p_mvalid || k >= K) return;
+    const int tap = k / a.KC, ci = k % a.KC;
+    const int kh = tap / a.KW, kw = tap % a.KW;
+    int ih, iw;
+    bool ok;
+    if (MODE == MODE_BWD2) {   // the iteration pixel IS the dy pixel
+      ih = p_oh;
+      iw = p_ow;
+      ok = true;
+    } else if (MODE == MODE_FWD) {
+      ih = p_oh * a.stride - a.pad + kh;
+      iw = p_ow * a.stride - a.pad + kw;
+      ok = ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws;
+    } else {
+      const int th = p_oh + a.pad - kh, tw = p_ow + a.pad - kw;
+      ok = th >= 0 && tw >= 0 && (th % a.stride) == 0 && (tw % a.stride) == 0;
+      ih = th / a.stride;
+      iw = tw / a.stride;
+      ok = ok && ih < a.Hs && iw < a.Ws;
+    }
+    if (!ok) return;
+    p_off = (((int64_t)p_on * a.Hs + ih) * a.Ws + iw) * a.KC + ci;
+    p_ci = ci;
+    p_ok = true;
+    P::load8(src + p_off, pf);
+    if (TWO) P::load8(src2 + p_off, pr);
+  };
+  if (tile0 < tile_end) {
+    coords(tile0);
+    gather();
+  }
+  for (int tile = tile0; tile < tile_end; ++tile) {
     f32x4 acc[NT];
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[nt] = {0.f, 0.f, 0.f, 0.f};
@@ -348,58 +393,45 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
     }
 
     for (int k0 = 0; k0 < a.Kp; k0 += 32) {
-      const int k = k0 + 8 * (lane >> 4);
-      float f[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      if (mvalid && k < K) {
-        const int tap = k / a.KC, ci = k % a.KC;
-        const int kh = tap / a.KW, kw = tap % a.KW;
-        int ih, iw;
-        bool ok;
-        if (MODE == MODE_BWD2) {   // the iteration pixel IS the dy pixel
-          ih = oh;
-          iw = ow;
-          ok = true;
-        } else if (MODE == MODE_FWD) {
-          ih = oh * a.stride - a.pad + kh;
-          iw = ow * a.stride - a.pad + kw;
-          ok = ih >= 0 && ih < a.Hs && iw >= 0 && iw < a.Ws;
-        } else {
-          const int th = oh + a.pad - kh, tw = ow + a.pad - kw;
-          ok = th >= 0 && tw >= 0 && (th % a.stride) == 0 && (tw % a.stride) == 0;
-          ih = th / a.stride;
-          iw = tw / a.stride;
-          ok = ok && ih < a.Hs && iw < a.Ws;
-        }
-        if (ok) {
-          const int64_t off = (((int64_t)on * a.Hs + ih) * a.Ws + iw) * a.KC + ci;
-          P::load8(src + off, f);
-          if (AOP == AOP_ACT && PRO == PRO_BNRELU) {
+      float f[8], r[TWO ? 8 : 1];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j] * v0[ci + j] + v1[ci + j], 0.f);
-          } else if (AOP == AOP_ACT && PRO == PRO_BOUT) {
-            float r[8];
-            P::load8(src2 + off, r);
+      for (int j = 0; j < 8; ++j) f[j] = pf[j];
+      if (TWO) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) f[j] = f[j] * v0[ci + j] + v1[ci + j];
-            if (a.vec2) {
+        for (int j = 0; j < 8; ++j) r[j] = pr[j];
+      }
+      const bool ok = p_ok;
+      const int ci = p_ci;
+      const int64_t off = p_off;
+      p_k0 += 32;   // advance the pipeline and issue the next chunk's loads
+      if (p_k0 >= a.Kp) {
+        p_k0 = 0;
+        if (++p_tile < tile_end) coords(p_tile);
+      }
+      gather();
+      if (ok) {
+        if (AOP == AOP_ACT && PRO == PRO_BNRELU) {
 #pragma unroll
-              for (int j = 0; j < 8; ++j) f[j] += r[j] * v2[ci + j] + v3[ci + j];
-            } else {
+          for (int j = 0; j < 8; ++j) f[j] = fmaxf(f[j] * v0[ci + j] + v1[ci + j], 0.f);
+        } else if (AOP == AOP_ACT && PRO == PRO_BOUT) {
 #pragma unroll
-              for (int j = 0; j < 8; ++j) f[j] += r[j];
-            }
+          for (int j = 0; j < 8; ++j) f[j] = f[j] * v0[ci + j] + v1[ci + j];
+          if (a.vec2) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j) f[j] = P::round(fmaxf(f[j], 0.f));   // the operand = the stored value
-            if (pro_out) {
+            for (int j = 0; j < 8; ++j) f[j] += r[j] * v2[ci + j] + v3[ci + j];
+          } else {
 #pragma unroll
-              for (int q = 0; q < 8 / V; ++q) *reinterpret_cast<uint4*>(pro_out + off + q * V) = P::pack(f + q * V);
-            }
-          } else if (AOP == AOP_DY) {
-            float yv[8];
-            P::load8(src2 + off, yv);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) f[j] = v0[ci + j] * f[j] + v1[ci + j] * yv[j] + v2[ci + j];
+            for (int j = 0; j < 8; ++j) f[j] += r[j];
           }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = P::round(fmaxf(f[j], 0.f));   // the operand = the stored value
+          if (pro_out) {
+#pragma unroll
+            for (int q = 0; q < 8 / V; ++q) *reinterpret_cast<uint4*>(pro_out + off + q * V) = P::pack(f + q * V);
+          }
+        } else if (AOP == AOP_DY) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) f[j] = v0[ci + j] * f[j] + v1[ci + j] * r[j] + v2[ci + j];
         }
       }
       const frag_t afrag = P::frag8(f);
