@@ -8,12 +8,15 @@ buffers through HIP IPC (``hipIpcGetMemHandle`` via torch's CUDA-IPC storage sha
 ``HSA_ENABLE_IPC_MODE_LEGACY=0``):
 
     glob  [P]           the current global model (flat fp32), written by the server after aggregation
-    slots [S, P + 1]    one row per silo: its uploaded flat model ‖ its sample count
+    slot_s [P + 1]      one buffer per silo: its uploaded flat model ‖ its sample count
 
 and the protocol messages (still on the TCP transport: handshake, round index, deadlines) carry only a
 marker. A silo master copies ``glob`` into its client engine device-to-device (peer access over xGMI
 when it sits on another GPU) and writes its silo average into its slot; the server aggregates the
-slots with the FedAvg kernel straight from the shared stack. Ordering is by message: a writer
+slots with one FedAvg kernel over their stack. Every buffer is its own allocation and a silo imports only the
+global buffer and its own slot: an import of one 2.75 GB allocation (8 ViT-B/16 slots in one tensor) never
+returned on this ROCm (scripts/ipc_probe.py: 2 x 344 MB imports in 0.22 s; 8 x 344 MB as one buffer hung, alone
+as well as concurrently). Ordering is by message: a writer
 synchronises its stream before it sends the message that tells the reader to look.
 
 Genuine WAN deployments keep the network transport (``silo_transport`` unset)."""
@@ -50,10 +53,10 @@ class ServerMailbox:
     def __init__(self, P: int, n_slots: int, device):
         self.P = int(P)
         self.glob = torch.zeros(self.P, dtype=torch.float32, device=device)
-        self.slots = torch.zeros(int(n_slots), self.P + 1, dtype=torch.float32, device=device)
+        self.slots = [torch.zeros(self.P + 1, dtype=torch.float32, device=device) for _ in range(int(n_slots))]
 
     def descriptor(self) -> dict:
-        return {"P": self.P, "glob": _share(self.glob), "slots": _share(self.slots)}
+        return {"P": self.P, "glob": _share(self.glob), "slots": [_share(t) for t in self.slots]}
 
     def publish(self, flat: torch.Tensor):
         """The next round's global model, visible to the silos once this returns."""
@@ -76,7 +79,7 @@ class SiloMailbox:
             fcntl.flock(lk, fcntl.LOCK_EX)
             try:
                 self.glob = _open(desc["glob"])
-                self.slots = _open(desc["slots"])
+                self.slot_buf = _open(desc["slots"][int(slot)])
                 torch.cuda.synchronize()
             finally:
                 fcntl.flock(lk, fcntl.LOCK_UN)
@@ -87,11 +90,11 @@ class SiloMailbox:
         out.reshape(-1).copy_(self.glob)
 
     def write_upload(self, flat: torch.Tensor, n_samples: float):
-        row = self.slots[self.slot]
+        row = self.slot_buf
         row[:self.P].copy_(flat.reshape(-1))
         row[self.P:].fill_(float(n_samples))
         torch.cuda.synchronize(flat.device)
-        torch.cuda.synchronize(self.slots.device)
+        torch.cuda.synchronize(self.slot_buf.device)
 
 
 def marker(kind: str, **kw) -> dict:
