@@ -747,6 +747,14 @@ static int px_override() {
   return v;
 }
 
+// per-channel-count unit override (tuning): FEDML_AMD_C3_PX16 / _PX32 / _PX64 (output pixels per LDS tile)
+static int px_override_kc(int kc) {
+  static const int v16 = [] { const char* e = getenv("FEDML_AMD_C3_PX16"); return e ? atoi(e) : 0; }();
+  static const int v32 = [] { const char* e = getenv("FEDML_AMD_C3_PX32"); return e ? atoi(e) : 0; }();
+  static const int v64 = [] { const char* e = getenv("FEDML_AMD_C3_PX64"); return e ? atoi(e) : 0; }();
+  return kc == 16 ? v16 : kc == 32 ? v32 : kc == 64 ? v64 : 0;
+}
+
 // tuning override of the fp32 64-channel output slice per workgroup: FEDML_AMD_C3_N64=32 (default 16)
 static int n64_override() {
   static const int v = [] {
@@ -781,9 +789,21 @@ static int dispatch_gemm(int kc, int nout, const Args& a, int C, hipStream_t s) 
   // unit sizes measured with FEDML_AMD_C3_PX sweeps (bf16: profiles/r1_c3_unit_sweep.txt; fp32:
   // profiles/r2_c3_sweep_fp32.txt — 256-px units for the fp32 backward, stride 2 included)
   constexpr int PX = ST == 2 ? ((P::kF32 && BWD) ? 256 : 128) : 256;
+  if (ST == 1 && px_override_kc(kc) > 0) {
+    const int o = px_override_kc(kc);
+    switch (kc) {
+      case 16: return launch_gemm<P, 16, 16, XF, BWD, EPI, ST>(a, nout, C, o, s);
+      case 32: return launch_gemm<P, 32, 32, XF, BWD, EPI, ST>(a, nout, C, o, s);
+      case 64: return launch_gemm<P, 64, N64, XF, BWD, EPI, ST>(a, nout, C, o, s);
+      default: return -2;
+    }
+  }
   switch (kc) {
     case 16: return launch_gemm<P, 16, 16, XF, BWD, EPI, ST>(a, nout, C, (BWD && ST == 1 && !P::kF32) ? 512 : PX, s);
-    case 32: return launch_gemm<P, 32, 32, XF, BWD, EPI, ST>(a, nout, C, PX, s);
+    // fp32 32-channel stride-1 layers: 64-px units (4 rows of 16²) — the loader then prefetches ≤ 8 chunks per
+    // thread and the kernel keeps 2 waves per SIMD (256-px units: 12 chunks, 272-290 registers, 1 wave);
+    // profiles/r3_c3_px_sweep.txt: fwd 0.416 → 0.361 ms, bwd 0.480 → 0.388 ms at C = 100
+    case 32: return launch_gemm<P, 32, 32, XF, BWD, EPI, ST>(a, nout, C, (P::kF32 && ST == 1) ? 64 : PX, s);
     case 64: return launch_gemm<P, 64, N64, XF, BWD, EPI, ST>(a, nout, C, ST == 2 ? ((P::kF32 && BWD) ? 256 : 64) : 128,
                                                                s);  // weights split over z
     default: return -2;
