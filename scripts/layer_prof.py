@@ -15,7 +15,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
 
 from fedml_amd.core.arena import ParamLayout
-from fedml_amd.models.cv.resnet import resnet56, resnet110
+from fedml_amd.models.cv.resnet import resnet18_cifar, resnet56, resnet110
 from fedml_amd.ops import nn_ops
 from fedml_amd.parallel.native_resnet import NativeResNetStep
 
@@ -43,6 +43,10 @@ def _wrap(name, cost):
 def c_fwd(x, wpk, ld, ps, pt, y, st, C, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, ldk, tpw):
     return (f"{KH}x{KW} {Cin}->{Cout} s{stride} @{H}" + (" +bnrelu" if ps is not None else ""),
             C * N * (H * W * Cin + Ho * Wo * Cout) * ES[0], 2 * C * N * Ho * Wo * Cout * KH * KW * Cin)
+
+
+def c_pbout(yp, s, t, res, rs, rt, bout, wpk, ld, y, st, C, N, H, W, Cin, Cout, ldk, tpw, **kw):
+    return (f"1x1 {Cin}->{Cout} @{H} +block-out", C * N * H * W * (3 * Cin + Cout) * ES[0], 2 * C * N * H * W * Cin * Cout)
 
 
 def c_bwd(g, y, al, be, ga, wpk, ld, dx, epi, ex, es, et, eadd, ey1, ey2, st, C, N, Hy, Wy, Cout, Cin, KH, KW, stride,
@@ -105,6 +109,7 @@ def main():
     ES[0] = 2 if dtype == torch.bfloat16 else 4
     nn_ops.set_f32_mma_mode(a.fp32_mma)
     _wrap("conv_fwd", c_fwd)
+    _wrap("conv_fwd_pbout", c_pbout)
     _wrap("conv_bwd_data", c_bwd)
     _wrap("conv_wgrad", c_wgrad)
     _wrap("block_out", c_block)
@@ -116,7 +121,7 @@ def main():
     for n in ("bn_fwd_finalize", "bn_bwd_finalize", "pack_weights", "avgpool", "head_bwd", "nchw_to_nhwc_pad"):
         _wrap(n, c_other)
     torch.manual_seed(0)
-    model = {"resnet56": resnet56, "resnet110": resnet110}[a.model](class_num=100)
+    model = {"resnet56": resnet56, "resnet110": resnet110, "resnet18": resnet18_cifar}[a.model](class_num=100)
     layout = ParamLayout.from_module(model)
     dev = "cuda"
     flat = layout.flatten(model.state_dict()).to(dev)

