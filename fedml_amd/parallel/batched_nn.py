@@ -27,6 +27,9 @@ import torch.fx as fx
 import torch.nn as nn
 import torch.nn.functional as F
 
+# FEDML_AMD_NATIVE_BCONV=0 keeps every client-batched convolution on torch (MIOpen grouped convolution), for A/B
+_NATIVE_BCONV = __import__("os").environ.get("FEDML_AMD_NATIVE_BCONV", "1") != "0"
+
 SUPPORTED_MODULES = (nn.Conv2d, nn.BatchNorm2d, nn.Linear, nn.ReLU, nn.Sigmoid, nn.Tanh, nn.MaxPool2d, nn.AvgPool2d,
                      nn.AdaptiveAvgPool2d, nn.Flatten, nn.Dropout, nn.Identity, nn.GroupNorm, nn.LeakyReLU)
 
@@ -229,6 +232,10 @@ class BatchedInterpreter:
         if isinstance(m, nn.Conv2d):
             w = params[f"{name}.weight"]
             b = params.get(f"{name}.bias")
+            if _NATIVE_BCONV and x.is_cuda:   # hand-written implicit GEMM (ops/bconv_ops.py) when it applies
+                from ..ops import bconv_ops
+                if bconv_ops.supported(m, x, w):
+                    return bconv_ops.bconv2d_native(x, w, b, C, m.stride, m.padding)
             if w.dtype != x.dtype:
                 w = w.to(x.dtype)
                 b = b.to(x.dtype) if b is not None else None

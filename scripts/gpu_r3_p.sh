@@ -16,3 +16,8 @@ b r18_fp32 --preset resnet18_cifar10_10 --steps 2 --warmup 1
 b r18_bf16 --preset resnet18_cifar10_10 --dtype bf16 --steps 3 --warmup 1
 b distil_fp32 --preset distilbert_fedopt_32 --dtype fp32 --steps 3 --warmup 1
 b vit_fp32 --preset vit_b16_32 --dtype fp32 --steps 3 --warmup 1
+
+for t in 2 3; do export FEDML_AMD_CONVK_TILE=$t; b r18_bf16_tile$t --preset resnet18_cifar10_10 --dtype bf16 --steps 3 --warmup 1; done; unset FEDML_AMD_CONVK_TILE
+for t in 2 3; do export FEDML_AMD_CONVK_TILE=$t; b r18_fp32_tile$t --preset resnet18_cifar10_10 --steps 2 --warmup 1; done; unset FEDML_AMD_CONVK_TILE
+timeout -k 10 300 python -u scripts/layer_prof.py --model resnet18 --C 10 --N 64 --dtype bf16 --steps 2 > gpurun_out/r18_bf16_layers.txt 2>&1 || exit 1
+head -40 gpurun_out/r18_bf16_layers.txt | cut -c1-130
