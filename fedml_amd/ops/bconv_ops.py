@@ -31,9 +31,31 @@ def supported(m, x, w) -> bool:
     if w.dtype != torch.float32 or w.dim() != 5 or not w[0].is_contiguous():
         return False
     k = m.kernel_size
-    return (m.groups == 1 and m.dilation == (1, 1) and k[0] == k[1] and m.stride[0] == m.stride[1]
-            and m.padding[0] == m.padding[1] and isinstance(m.padding, tuple) and m.out_channels % 16 == 0
-            and m.padding_mode == "zeros")
+    cout = m.out_channels   # the forward GEMM's N: the kernels' output slices are 16 / 32 / 64-multiples
+    if not (m.groups == 1 and m.dilation == (1, 1) and k[0] == k[1] and m.stride[0] == m.stride[1]
+            and m.padding[0] == m.padding[1] and isinstance(m.padding, tuple) and (cout in (16, 32) or cout % 64 == 0)
+            and m.padding_mode == "zeros"):
+        return False
+    # both GEMMs must have a kernel that takes them: the K-streamed kernel (64-multiple N and K > 256, or N > 256)
+    # or the resident-weight kernel, whose [N-slice][K] weight block must fit the LDS
+    es = 4 if x.dtype == torch.float32 else 2
+    cin_pad = _pad_channels(m.in_channels)
+    kk = k[0] * k[0]
+    return _gemm_ok(cout, kk * cin_pad, es) and _gemm_ok(cin_pad, kk * cout, es)
+
+
+def _gemm_ok(n, K, es):
+    if n % 64 == 0 and (n > 256 or K > 256):
+        return True
+    sl = n if n in (16, 32) else 16           # the narrowest slice the dispatch falls back to
+    ldk = _round_up(K, 32) + 8
+    return sl * ldk * es + 4 * 4 * 256 + 4 * sl * 3 * 4 + 4 * 16 * sl * es <= 160 * 1024
+
+
+def _pad_channels(cin):
+    """Input channels padded for the kernels: the backward-data GEMM's N (= the input channels) takes 16 / 32 /
+    64-multiples, the forward's K needs multiples of 8."""
+    return 16 if cin <= 16 else 32 if cin <= 32 else _round_up(cin, 64)
 
 
 class _Geom:
@@ -41,7 +63,7 @@ class _Geom:
     _cache = {}
 
     def __init__(self, C, cout, cin, k, device):
-        self.cin_pad = _round_up(cin, 8)
+        self.cin_pad = _pad_channels(cin)
         self.ldk = _round_up(k * k * self.cin_pad, 32) + 8
         self.ldk2 = _round_up(k * k * cout, 32) + 8
         self.off_b = _round_up(cout * self.ldk, 8)

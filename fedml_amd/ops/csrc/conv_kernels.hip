@@ -978,7 +978,10 @@ static int launch_convk(ConvArgs a, int nout, int C, hipStream_t s) {
   const int M = MODE == MODE_BWD2 ? a.Nb * a.Hs * a.Ws : a.Nb * a.Ho * a.Wo;   // (BWDS2: all 4 classes)
   const int64_t wgs1 = (int64_t)((M + 63) / 64) * C * (nout / 64);   // workgroups of a 64 × 64 tile
   int pick = force;
-  if (pick < 0) pick = nout % 128 == 0 ? 0 : (wgs1 >= 4096 ? 1 : (wgs1 >= 1024 ? 2 : 3));
+  // fp32 wide layers take 64 × 64 tiles too: the fp32 128 × 128 tile (operands twice the bytes, 16 accumulator
+  // tiles per wave) runs fewer waves per CU — ResNet-18 preset fp32 0.392 → 0.410 rounds/s, bf16 keeps 128 × 128
+  // (1.124 vs 1.055 rounds/s with 64 × 64; profiles/r3_bench_secondary_final.jsonl)
+  if (pick < 0) pick = nout % 128 == 0 ? (P::kF32 ? 3 : 0) : (wgs1 >= 4096 ? 1 : (wgs1 >= 1024 ? 2 : 3));
   switch (pick) {
     case 0: return launch_convk_t<P, 4, 2, AOP, PRO, MODE, EPI>(a, nout, C, s);
     case 1: return launch_convk_t<P, 4, 1, AOP, PRO, MODE, EPI>(a, nout, C, s);

@@ -19,4 +19,6 @@ def test_supported_rules():
     x = torch.zeros(2, 6, 8, 8)
     w = torch.zeros(3, 32, 2, 3, 3)
     assert not bconv_ops.supported(nn.Conv2d(2, 32, 3), x, w)          # CPU tensors: torch path
-    assert bconv_ops._round_up(27, 8) == 32
+    assert bconv_ops._gemm_ok(32, 9 * 16, 4) and bconv_ops._gemm_ok(64, 9 * 32, 4)
+    assert not bconv_ops._gemm_ok(32, 25 * 64, 4)                       # 32 x 1608 fp32 weights > LDS
+    assert [bconv_ops._pad_channels(c) for c in (1, 3, 16, 17, 32, 48, 64, 96)] == [16, 16, 16, 32, 32, 64, 64, 128]

@@ -15,10 +15,10 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-@pytest.mark.parametrize("cin,cout,k,s,p,hw,bias", [(1, 32, 5, 1, 2, 28, True), (32, 64, 5, 1, 2, 14, True),
+@pytest.mark.parametrize("cin,cout,k,s,p,hw,bias", [(1, 32, 5, 1, 2, 28, True), (32, 64, 3, 1, 0, 14, True),
                                                      (3, 64, 3, 1, 1, 32, False), (64, 128, 3, 2, 1, 16, True),
                                                      (64, 64, 1, 1, 0, 8, False), (16, 32, 1, 2, 0, 16, False),
-                                                     (128, 256, 3, 1, 1, 4, True)])
+                                                     (128, 256, 3, 1, 1, 4, True), (16, 32, 3, 1, 1, 12, True)])
 def test_native_bconv_matches_torch(cin, cout, k, s, p, hw, bias):
     torch.manual_seed(0)
     C, B = 3, 6
@@ -32,13 +32,15 @@ def test_native_bconv_matches_torch(cin, cout, k, s, p, hw, bias):
     m = nn.Conv2d(cin, cout, k, s, p, bias=bias)
     assert bconv_ops.supported(m, x, w)
     outs = []
+    gy = None
     for native in (True, False):
         xx = x.clone().requires_grad_(True)
         ww = w.detach().clone().requires_grad_(True) if not native else w.detach().requires_grad_(True)
         bb = b.detach().clone().requires_grad_(True) if b is not None else None
         y = bconv_ops.bconv2d_native(xx, ww, bb, C, (s, s), (p, p)) if native else \
             batched_nn.bconv2d(xx, ww, bb, C, (s, s), (p, p), (1, 1), 1)
-        gy = torch.randn_like(y)
+        if gy is None:
+            gy = torch.randn_like(y)   # one upstream gradient for both paths
         y.backward(gy)
         outs.append((y.detach(), xx.grad, ww.grad, bb.grad if bb is not None else None))
     for (a, ref), name in zip(zip(outs[0], outs[1]), ("y", "dx", "dw", "db")):
