@@ -68,7 +68,9 @@ __device__ __forceinline__ void add_fixed(unsigned long long* a, float v, unsign
 }
 }  // namespace fa_det
 
-static __device__ fa_det::Table g_fa_det;
+// __constant__: kernels never write it, so its loads are invariant across the atomics they guard — one load per
+// kernel instead of one load + wait per atomic call site (a __device__ table was reloaded after every atomic)
+static __constant__ fa_det::Table g_fa_det;
 
 // the deterministic branch: out of line (one copy per translation unit, not one per unrolled call site)
 __device__ __attribute__((noinline)) static void fa_acc_add_det(float* p, float v) {
