@@ -22,9 +22,13 @@ def test_native_engine_two_ranks_on_gpu_equals_one_rank(tmp_path):
     assert w1.shape == w2.shape and torch.isfinite(w1).all()
     rel = float((w1 - w2).norm() / w1.norm())
     if rel >= 1e-3:
-        # fp32 atomics make even two 1-rank runs differ; 3 rounds of small-batch BN training can amplify that
-        # (one box: 9.7e-3 once, < 1e-3 in six reruns). The 2-rank run must then be no further from the 1-rank
-        # run than a second 1-rank run is.
+        # fp32 atomics make even two runs of one configuration differ, and 3 rounds of small-batch BN training
+        # can amplify that (full-suite runs: 8.9e-3 / 9.7e-3 twice, isolated reruns < 1e-3 six times). World-size
+        # invariance then means: the 1-rank and 2-rank results are no further apart than two runs of the same
+        # configuration (1-rank twice, 2-rank twice — the 2-rank pair shares the GPU, whose timing varies). A
+        # systematic world-size error keeps each configuration's pair close and still fails.
         w1b = _launch(1, str(tmp_path / "w1b.pt"), "resnet_shallow", 5, True, True, **env)
-        noise = float((w1 - w1b).norm() / w1.norm())
-        assert rel < max(1e-3, 3 * noise), (rel, noise)
+        w2b = _launch(2, str(tmp_path / "w2b.pt"), "resnet_shallow", 5, True, True, **env)
+        n1 = float((w1 - w1b).norm() / w1.norm())
+        n2 = float((w2 - w2b).norm() / w2.norm())
+        assert rel < max(1e-3, 3 * n1, 3 * n2), (rel, n1, n2)
