@@ -97,7 +97,7 @@ def main():
     }})
     torch.manual_seed(0)
     model = create(args, spec.num_classes)
-    rank, ws = comm.init_process_group(device=device if use_gpu else None)
+    rank, ws = comm.init_process_group(device=device if use_gpu else None, args=args)
     if a.partition == "hetero":
         # the reference's LDA label partition (core/non_iid_partition/noniid_partition.py) of the same total
         # number of samples: client sizes follow the Dirichlet draw (the shipped RCCL config's setting)

@@ -96,7 +96,14 @@ class TrainerDistAdapter:
 
     def get_model_params(self):
         if self.n_local > 1 and self.client_index in self.silo_trainers and torch.is_tensor(self._pending):
-            return self.silo_trainers[self.client_index].sim.global_model_state()
+            # the pending flat model is the server's latest global (e.g. FINISH's final aggregate, with no train
+            # after it): load it first — sim.global_flat still holds this silo's own last upload
+            st = self.silo_trainers[self.client_index]
+            st.load_global(self._pending)
+            return st.sim.global_model_state()
+        if torch.is_tensor(self._pending) and self.n_local > 1:   # a silo that never trained (not yet selected)
+            self.model.load_state_dict(self._layout().unflatten(self._pending.to(self.device)))
+            self._pending = None
         return {k: v.detach().cpu().clone() for k, v in self.model.state_dict().items()}
 
     def flat_params(self):
@@ -122,6 +129,7 @@ class TrainerDistAdapter:
             st = self.silo_trainers[self.client_index]
             if self.rank_in_silo == 0 and self._pending is not None:
                 st.load_global(self._pending)
+            self._pending = None      # consumed: get_model_params must not reload it over the trained model
             st.sync()
             if flat:
                 st.sim.run_round(int(round_idx or 0))

@@ -52,7 +52,9 @@ class FedMLClientManager(ClientManager):
         from ..device_mailbox import SiloMailbox, is_marker
         if not is_marker(params):
             return params
-        if params["__devmail__"] == "init":
+        if self.mailbox is None or params["__devmail__"] == "init":
+            if "desc" not in params:
+                raise RuntimeError("device-plane marker without a mailbox descriptor before the silo opened one")
             self.mailbox = SiloMailbox(params["desc"], int(params["slot"]))
         return self.mailbox.glob
 

@@ -155,12 +155,21 @@ class FedMLServerManager(ServerManager):
         if self.device_payload:
             from ..device_mailbox import marker
             self._open_mailbox(g)
-            desc = self.mailbox.descriptor()
+            desc = self._desc = self.mailbox.descriptor()
         for cid, silo in zip(ids, silos):
             payload = marker("init", desc=desc, slot=self._slot_of[cid]) if self.device_payload else g
             self._send(MyMessage.MSG_TYPE_S2C_INIT_CONFIG, cid, payload, silo)
         MLOpsProfilerEvent.get_instance().log_event_started("server.wait", event_value=str(self.round_idx))
         self._arm_deadline()
+
+    def _global_payload(self, g, cid):
+        """Device plane: a 'global' marker that also carries the mailbox descriptor and the receiver's slot, so a
+        silo left out of round 0 (partial participation: it never got the 'init' marker) can still open the
+        shared buffers when it is first selected, or at FINISH."""
+        if not self.device_payload:
+            return g
+        from ..device_mailbox import marker
+        return marker("global", desc=self._desc, slot=self._slot_of[cid])
 
     def _send(self, mtype, receiver, params, silo):
         m = Message(mtype, self.get_sender_id(), receiver)
@@ -221,12 +230,11 @@ class FedMLServerManager(ServerManager):
         if self.device_payload:
             self.mailbox.publish(g if torch.is_tensor(g) else self.aggregator.flat_layout.flatten(
                 g, device=self.mailbox.glob.device))
-            from ..device_mailbox import marker
-            g = marker("global")
+            g = None
         if self.round_idx == self.round_num:
             # final sync lets clients see the final model; then everyone stops
             for cid in self.client_real_ids:
-                self._send(MyMessage.MSG_TYPE_S2C_FINISH, cid, g, 0)
+                self._send(MyMessage.MSG_TYPE_S2C_FINISH, cid, self._global_payload(g, cid), 0)
             MLOpsMetrics.get_instance().report_server_training_status(getattr(self.args, "run_id", "0"),
                                                                       MyMessage.MSG_MLOPS_SERVER_STATUS_FINISHED)
             self.finish()
@@ -235,7 +243,7 @@ class FedMLServerManager(ServerManager):
         self._selected = ids
         self.aggregator.flag_client_model_uploaded_dict = {i: False for i in range(len(ids))}
         for cid, silo in zip(ids, silos):
-            self._send(MyMessage.MSG_TYPE_S2C_SYNC_MODEL_TO_CLIENT, cid, g, silo)
+            self._send(MyMessage.MSG_TYPE_S2C_SYNC_MODEL_TO_CLIENT, cid, self._global_payload(g, cid), silo)
         prof.log_event_started("server.wait", event_value=str(self.round_idx))
         self._arm_deadline()
 

@@ -80,3 +80,10 @@ static inline int fa_grid(int64_t work, int block, int cap = 4096) {
   if (g > cap) g = cap;
   return (int)g;
 }
+
+// Deterministic mode (utils/determinism.py): every client-batched launcher plans its work split (pixel chunks,
+// workgroup targets, tile shapes) for this fixed client count instead of the launch's C, so the fp32 partial
+// sums of one client — and so its bits — do not depend on how many clients share its GPU (a world-size
+// invariant run). 0 (default): plan for the launch's own C. Set by fa_set_plan_clients (det_kernels.hip).
+extern "C" int fa_plan_clients;
+static inline int fa_plan_c(int C) { return fa_plan_clients > 0 ? fa_plan_clients : C; }

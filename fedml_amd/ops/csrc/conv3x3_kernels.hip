@@ -705,15 +705,16 @@ static int launch_gemm(Args a, int nout, int C, int target_px, hipStream_t strea
   }();
   // fp32: ~40 workgroups per client (512..2048): the 13-client share wants 512 (fwd 1.72 → 1.52, bwd-data
   // 1.86 → 1.61 ms/step), 100 clients keep 2048 (scripts/gpu_c3g_small_c.sh)
-  const int wgs = wgs_env > 0 ? wgs_env : (P::kF32 ? std::min(2048, std::max(512, 40 * C)) : 2048);
-  Plan p = make_plan(a.N, a.H, a.W, C, target_px, wgs);
+  const int PC = fa_plan_c(C);
+  const int wgs = wgs_env > 0 ? wgs_env : (P::kF32 ? std::min(2048, std::max(512, 40 * PC)) : 2048);
+  Plan p = make_plan(a.N, a.H, a.W, PC, target_px, wgs);
   {  // a unit's tile must fit the loader's register budget (≤ 12 16-B chunks per thread)
     const bool f2 = !BWD && ST == 2;
     while (target_px > 8) {
       const int tr = f2 ? 2 * p.R + 1 : p.R + 2, tw = (BWD ? a.W : a.Ws) + 2;
       if ((p.S * tr * tw * CG + 255) / 256 <= 12) break;
       target_px /= 2;
-      p = make_plan(a.N, a.H, a.W, C, target_px, wgs);
+      p = make_plan(a.N, a.H, a.W, PC, target_px, wgs);
     }
   }
   a.R = p.R; a.S = p.S; a.units = p.units; a.units_per_wg = p.units_per_wg; a.nout_total = nout;
@@ -868,15 +869,16 @@ static int conv3x3_wgrad(const void* g, const void* yv, const float* alpha, cons
     const char* e = getenv("FEDML_AMD_C3W_WGS");
     return e ? atoi(e) : 0;
   }();
-  const int wgs = wgs_env > 0 ? wgs_env : (P::kF32 ? std::min(2048, std::max(256, 20 * C)) : 256);
+  const int PC = fa_plan_c(C);
+  const int wgs = wgs_env > 0 ? wgs_env : (P::kF32 ? std::min(2048, std::max(256, 20 * PC)) : 256);
   const int CGX = Cin / P::VEC, CGD = Cout / P::VEC;
   constexpr int XMAX = P::kF32 ? 16 : 8;   // x-tile 16-B chunks per thread (fp32: twice the chunks per pixel)
-  Plan p = make_plan(N, Ho, Wo, C, tpx, wgs);
+  Plan p = make_plan(N, Ho, Wo, PC, tpx, wgs);
   while (tpx > 8) {
     const int tr = stride == 2 ? 2 * p.R + 1 : p.R + 2;
     if ((p.S * tr * (W + 2) * CGX + 255) / 256 <= XMAX && (p.S * p.R * Wo * CGD + 255) / 256 <= 4) break;
     tpx /= 2;
-    p = make_plan(N, Ho, Wo, C, tpx, wgs);
+    p = make_plan(N, Ho, Wo, PC, tpx, wgs);
   }
   if ((p.R * Wo) % 32 != 0) return -7;   // a unit must hold whole 32-pixel K-steps
   a.R = p.R; a.S = p.S; a.units = p.units; a.units_per_wg = p.units_per_wg;

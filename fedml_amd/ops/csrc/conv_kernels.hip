@@ -976,7 +976,7 @@ static int launch_convk(ConvArgs a, int nout, int C, hipStream_t s) {
   }
   if (nout % 64 != 0) return -2;
   const int M = MODE == MODE_BWD2 ? a.Nb * a.Hs * a.Ws : a.Nb * a.Ho * a.Wo;   // (BWDS2: all 4 classes)
-  const int64_t wgs1 = (int64_t)((M + 63) / 64) * C * (nout / 64);   // workgroups of a 64 × 64 tile
+  const int64_t wgs1 = (int64_t)((M + 63) / 64) * fa_plan_c(C) * (nout / 64);   // workgroups of a 64 × 64 tile
   int pick = force;
   // fp32 wide layers take 64 × 64 tiles too: the fp32 128 × 128 tile (operands twice the bytes, 16 accumulator
   // tiles per wave) runs fewer waves per CU — ResNet-18 preset fp32 0.392 → 0.410 rounds/s, bf16 keeps 128 × 128

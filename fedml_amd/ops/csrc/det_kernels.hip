@@ -30,4 +30,10 @@ extern "C" int fa_det_flush(float* dst, void* acc, int64_t n, unsigned int* bad,
   return (int)hipGetLastError();
 }
 
+extern "C" int fa_plan_clients = 0;
+extern "C" int fa_set_plan_clients(int c) {
+  fa_plan_clients = c > 0 ? c : 0;
+  return 0;
+}
+
 FA_DET_EXPORT(det)

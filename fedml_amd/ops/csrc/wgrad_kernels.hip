@@ -437,7 +437,7 @@ static int wgrad_wide(const typename P::T* g, const typename P::T* yv, const flo
   constexpr int PT = P::kF32 ? 32 : 64;
   const int K = KH * KW * Cin;
   const int nks = (K + 127) / 128;
-  const int base = C * nks * (Cout / 128);
+  const int base = fa_plan_c(C) * nks * (Cout / 128);
   const int M = Nb * Ho * Wo;
   // pixel chunks: enough workgroups to fill the chip (≈2048), chunks of ≥ 512 pixels
   int gx = max(1, min((2048 + base - 1) / base, (M + 511) / 512));

@@ -17,12 +17,19 @@ import torch
 from .fl_ops import _check, _fn, _i64, _p, _stream
 
 MAXR = 16
+# deterministic mode plans every client-batched work split for this many clients (csrc/common.h fa_plan_c)
+PLAN_CLIENTS = 64
 _TUS = ("det", "bn", "conv", "conv1x1", "conv3x3", "wgrad", "transformer", "tf_f32", "bgemm")
 _active = [None]
 
 
 def active():
     return _active[0]
+
+
+def set_plan_clients(n: int):
+    """Plan the native kernels' work splits for ``n`` clients whatever a launch's C is (0: the launch's C)."""
+    _check(_fn("fa_set_plan_clients")(ctypes.c_int(int(n))), "fa_set_plan_clients")
 
 
 class _Table(ctypes.Structure):

@@ -292,3 +292,21 @@ def head_bwd(dpool, out, y3, yd, gpre, stats, C, N, HW, Ch, NS, nimg=None):
 def nchw_to_nhwc_pad(x, y, CN, Cin, HW, Cpad):
     rc = _fnp("fa_nchw_to_nhwc_pad", y)(_p(x), _p(y), _i64(CN), _i(Cin), _i(HW), _i(Cpad), _stream(x))
     _check(rc, "fa_nchw_to_nhwc_pad")
+
+
+def fc_head_xent(pooled, arena, ow, ob, labels, row_scale, garena, dpool, loss_c, C, N, F, K) -> bool:
+    """Fused classifier head (csrc/head_kernels.hip): logits = pooled·Wᵀ + b from the arena rows, softmax-CE
+    with ``row_scale``, gW/gb added into the gradient arena at the same offsets, dpool = dl·W, per-client loss in
+    ``loss_c``. False when the shape does not fit one workgroup (the caller keeps the library path)."""
+    if pooled.dtype != torch.float32 or arena.dtype != torch.float32 or F % 4 != 0:
+        return False
+    lab = labels.reshape(-1)
+    if lab.dtype != torch.int64 or not lab.is_contiguous():
+        return False
+    rc = _fn("fa_fc_head_xent_f32")(_p(pooled), _p(arena), _i64(arena.stride(0)), _i64(ow), _i64(ob), _p(lab),
+                                    _p(row_scale.contiguous()), _p(garena), _i64(garena.stride(0)), _p(dpool),
+                                    _p(loss_c), _i(C), _i(N), _i(F), _i(K), _stream(pooled))
+    if rc == -5:
+        return False
+    _check(rc, "fa_fc_head_xent_f32")
+    return True

@@ -76,6 +76,11 @@ def _ln_ref(h, res, gamma, beta, eps, p, seed, rpc):
     return y.view(R, d).to(h.dtype)
 
 
+def _deterministic() -> bool:
+    from ..utils import determinism
+    return determinism.enabled()
+
+
 class _LayerNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, res, gamma, beta, eps, p, seed, rpc, seed_dev):
@@ -114,6 +119,13 @@ class _LayerNorm(torch.autograd.Function):
                        _p(dres), _p(dh), _c.c_uint32(_thr(p)), _f(1.0 / (1.0 - p) if p > 0 else 1.0),
                        _c.c_uint32(seed & _M32), _p(dg), _p(db), _p(seed_dev), _stream(x))
         _check(rc, name)
+        if _deterministic():
+            # the kernel's dgamma/dbeta reduce rows with fp32 atomics (arrival order → last bit): recompute them
+            # as fixed-order column sums (deterministic-mode only; the kernel's dh/dres are atomic-free)
+            xf, dyf = x.float().view(C, rpc, d), dy.float().view(C, rpc, d)
+            xhat = (xf - mean.view(C, rpc, 1)) * rstd.view(C, rpc, 1)
+            dg = (dyf * xhat).sum(1)
+            db = dyf.sum(1)
         return dh, dres, dg.to(gdt), db.to(gdt), None, None, None, None, None
 
 
@@ -357,6 +369,14 @@ class _ClientLinear(torch.autograd.Function):
                     bviews.append(dense_b[:, r:r + b.shape[1]])
                     out_b.append(dense_b[:, r:r + b.shape[1]])
                     r += b.shape[1]
+            if _deterministic():
+                # fixed-order column sums instead of the kernel's fp32 atomics (deterministic mode)
+                gs = g.view(C, M, N).float().sum(1)
+                r = 0
+                for bv in bviews:
+                    bv.add_(gs[:, r:r + bv.shape[1]])
+                    r += bv.shape[1]
+                return (dx, None, None, None, *out_w, *out_b)
             bb, bcs, boff, blo = _segments(bviews)
             rc = _fn("fa_bias_grad" + sfx)(_p(g), _i64(M * N), _c.c_int(N), _p(bb), _i64(bcs), boff, blo,
                                      _c.c_int(len(bs)), _c.c_int(C), _c.c_int(M), _c.c_int(N), _stream(x))

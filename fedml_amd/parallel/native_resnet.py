@@ -149,6 +149,7 @@ class NativeResNetStep:
         self.geom = None
         self._segs = None
         self._states = {}
+        self._shared = {}
         self.use_c3 = os.environ.get("FEDML_AMD_CONV3X3", "1") != "0"
         self.use_c1 = os.environ.get("FEDML_AMD_CONV1X1", "1") != "0"
         self.use_c1f = os.environ.get("FEDML_AMD_C1_FUSED", "1") != "0"
@@ -156,15 +157,21 @@ class NativeResNetStep:
         self.use_s2k = os.environ.get("FEDML_AMD_C3S2_CONVK", "1") == "1"   # measured +2 % (fp32 headline)
         self.use_ry = os.environ.get("FEDML_AMD_RECOMPUTE_Y", "0") == "1" and dtype == torch.float32
         self.use_pbout = os.environ.get("FEDML_AMD_FUSE_BOUT", "1") != "0"
+        self.use_fch = os.environ.get("FEDML_AMD_FC_HEAD", "1") != "0"      # fused fc + CE head kernel
         self.dump = None   # debug: list collecting (name, tensor clone) of every backward gradient buffer
         self._nimg = None
         self.det = None    # DetAccumulator in deterministic mode (enable_deterministic)
+        self.plan_C = C    # client count the kernels' work splits are planned for (fixed in deterministic mode)
 
     def enable_deterministic(self):
         """Bitwise-reproducible steps on the same kernels: every cross-workgroup fp32 atomic (BN statistics,
         split weight gradients) accumulates in 128-bit fixed point and is rounded once, at a fixed point
         of the step (ops/det_ops.py, csrc/detacc.h). Costs one flush launch per BN and one per step."""
-        from ..ops.det_ops import DetAccumulator
+        from ..ops.det_ops import PLAN_CLIENTS, DetAccumulator, set_plan_clients
+        # work splits planned for a fixed client count (csrc/common.h fa_plan_c): a client's bits must not depend
+        # on how many clients share the GPU (1 rank × 100 clients vs 4 ranks × 25)
+        self.plan_C = PLAN_CLIENTS
+        set_plan_clients(PLAN_CLIENTS)
         if self.det is None:
             self.det = DetAccumulator(self.device)
             self.det.activate()
@@ -174,6 +181,8 @@ class NativeResNetStep:
 
     def close(self):
         if self.det is not None:
+            from ..ops.det_ops import set_plan_clients
+            set_plan_clients(0)
             self.det.close()
             self.det = None
 
@@ -270,7 +279,7 @@ class NativeResNetStep:
             # bn_fwd_finalize has already moved row 7 on to the next step's pivot)
             self.bn_vec[bn.key] = torch.zeros(9, C, bn.ch, dtype=torch.float32, device=dev)
             nstat += bn.ch * 5
-        self.stats = torch.zeros(C * nstat, dtype=torch.float32, device=dev)
+        self.stats = self._shared_f32("stats", C * nstat)
         self.stat_views = {}
         o = 0
         for bn in self._all_bns():
@@ -281,9 +290,11 @@ class NativeResNetStep:
             self.stat_views[bn.key] = (fwd, bwd)
         fh, fw = self.final_hw
         self.pooled = torch.zeros(C, N, self.fc_in, dtype=torch.float32, device=dev)
+        self.dpool = torch.zeros(C, N, self.fc_in, dtype=torch.float32, device=dev)
+        self.loss_c = torch.zeros(C, dtype=torch.float32, device=dev)
         # GEMM-layout dW scratch for the weight-gradient kernel (kept zeroed by its scatter pass)
         mx = max(cv.cout * cv.k * cv.k * cv.cin_pad for cv in self._all_convs())
-        self.dw_scratch = torch.zeros(C * mx, dtype=torch.float32, device=dev)
+        self.dw_scratch = self._shared_f32("dw_scratch", C * mx)
         # the 3×3 layers keep their dW in scratch slices of their own and are scattered into the arena
         # together, in ONE launch at the end of backward (instead of one scatter launch per layer)
         segs, o3, self.c3_maxn, self._c3_off = [], 0, 0, {}
@@ -294,10 +305,10 @@ class NativeResNetStep:
                 segs.append(nn_ops.ScatterSeg(o3, self.off[cv.key], cv.cout, cv.cin_pad, cv.cin, 0))
                 o3 += C * n
                 self.c3_maxn = max(self.c3_maxn, n)
-        self.dw_c3 = torch.zeros(max(1, o3), dtype=torch.float32, device=dev)
+        self.dw_c3 = self._shared_f32("dw_c3", max(1, o3))
         # Gram scratch gᵀ·h2 of the recomputed-y bottlenecks ([C][4·planes·planes], kept zeroed by its consumer)
         gmax = max([b.convs[-1].cout * b.convs[-1].cin for b in self.blocks if b.ry] or [0])
-        self.gram = torch.zeros(C, gmax, dtype=torch.float32, device=dev) if gmax else None
+        self.gram = self._shared_f32("gram", C * gmax).view(C, gmax) if gmax else None
         self.c3_nseg = len(segs)
         raw = bytes((nn_ops.ScatterSeg * max(1, len(segs)))(*segs))
         self.c3_segs = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
@@ -312,9 +323,20 @@ class NativeResNetStep:
                 for t in [u for u in b.ys if u is not None] + [b.out] + ([b.yd] if b.yd is not None else []):
                     t.fill_(float("nan"))
 
+    def _shared_f32(self, name, n):
+        """The fp32 targets of cross-workgroup accumulation (BN statistics, weight-gradient scratch) depend on the
+        channel widths only, not on (N, H, W): ONE buffer per size serves every batch geometry. Steps never
+        overlap, each zeroes or drains what it uses, and in deterministic mode the accumulator registry (16
+        targets) holds these few shared buffers instead of 4 more per ragged batch size."""
+        t = self._shared.get((name, n))
+        if t is None:
+            t = self._shared[(name, n)] = torch.zeros(n, dtype=torch.float32, device=self.device)
+        return t
+
     # Every geometry keeps its own buffers alive: a captured HIP graph of one batch size must stay
     # valid while another batch size (the ragged last step of an epoch) is being run.
-    _STATE_ATTRS = ("x_in", "stem_y", "stem_out", "gbuf", "dybuf", "bn_vec", "stats", "stat_views", "pooled", "dw_scratch",
+    _STATE_ATTRS = ("x_in", "stem_y", "stem_out", "gbuf", "dybuf", "bn_vec", "stats", "stat_views", "pooled", "dpool",
+                    "loss_c", "dw_scratch",
                     "dw_c3", "gram", "c3_segs", "c3_nseg", "c3_maxn", "_c3_off",
                     "packed", "packed_ld", "_segs", "_nseg", "_pack_tiles", "_pack_taps", "final_hw", "geom")
 
@@ -340,11 +362,11 @@ class NativeResNetStep:
     def _tiles_per_wave(self, M):
         tiles = (M + 15) // 16
         target_wgs = _CONV_WGS
-        tpw = max(1, min(16, (tiles * self.C) // (4 * target_wgs)))
+        tpw = max(1, min(16, (tiles * self.plan_C) // (4 * target_wgs)))
         return tpw
 
     def _pix_per_wg(self, M):
-        per = max(256, _round_up((M * self.C) // 1024, 32))
+        per = max(256, _round_up((M * self.plan_C) // 1024, 32))
         return min(per, _round_up(M, 32))
 
     def _bn_offsets(self, bn):
@@ -440,7 +462,7 @@ class NativeResNetStep:
             return ppw
         if M >= 16384:
             return 512
-        target = M * self.C // 200
+        target = M * self.plan_C // 200
         p = 256
         while p < 2048 and 2 * p <= target:
             p *= 2
@@ -450,7 +472,7 @@ class NativeResNetStep:
         ppw = int(os.environ.get("FEDML_AMD_C1_PPW", "0"))
         if ppw:
             return ppw
-        return max(512, min(2048, _round_up(max(1, (M * self.C) // 1024), 128)))
+        return max(512, min(2048, _round_up(max(1, (M * self.plan_C) // 1024), 128)))
 
     def _fwd(self, cv: ConvSpec, x, y, pro_vec, bn: BNSpec, N):
         """y = conv(pro(x)) − pivot of the BN that follows; that BN's forward statistics."""
@@ -570,17 +592,22 @@ class NativeResNetStep:
         # ---------------- head: fc + fused CE (fp32, tiny) ----------------
         ow = self.off["fc.weight"]
         ob = self.off["fc.bias"]
-        Wfc = arena[:, ow:ow + self.fc_out * self.fc_in].view(C, self.fc_out, self.fc_in)
-        bfc = arena[:, ob:ob + self.fc_out]
-        logits = torch.baddbmm(bfc.unsqueeze(1), self.pooled, Wfc.transpose(1, 2))       # [C, N, K]
-        loss_rows, dlogits = softmax_xent_fwd_bwd(logits.view(C * N, -1), labels.reshape(-1), None,
-                                                  row_scale.reshape(-1))
-        loss = (loss_rows * row_scale.reshape(-1)).sum()
-        dl = dlogits.view(C, N, -1)
-        gW = garena[:, ow:ow + self.fc_out * self.fc_in].view(C, self.fc_out, self.fc_in)
-        gW.add_(torch.bmm(dl.transpose(1, 2), self.pooled))
-        garena[:, ob:ob + self.fc_out].add_(dl.sum(1))
-        dpool = torch.bmm(dl, Wfc)                                                         # [C, N, fc_in]
+        if self.use_fch and nn_ops.fc_head_xent(self.pooled, arena, ow, ob, labels, row_scale, garena, self.dpool,
+                                                self.loss_c, C, N, self.fc_in, self.fc_out):
+            loss = self.loss_c.sum()          # fused head (head_kernels.hip): logits, CE, gW/gb/dP in one launch
+            dpool = self.dpool
+        else:
+            Wfc = arena[:, ow:ow + self.fc_out * self.fc_in].view(C, self.fc_out, self.fc_in)
+            bfc = arena[:, ob:ob + self.fc_out]
+            logits = torch.baddbmm(bfc.unsqueeze(1), self.pooled, Wfc.transpose(1, 2))       # [C, N, K]
+            loss_rows, dlogits = softmax_xent_fwd_bwd(logits.view(C * N, -1), labels.reshape(-1), None,
+                                                      row_scale.reshape(-1))
+            loss = (loss_rows * row_scale.reshape(-1)).sum()
+            dl = dlogits.view(C, N, -1)
+            gW = garena[:, ow:ow + self.fc_out * self.fc_in].view(C, self.fc_out, self.fc_in)
+            gW.add_(torch.bmm(dl.transpose(1, 2), self.pooled))
+            garena[:, ob:ob + self.fc_out].add_(dl.sum(1))
+            dpool = torch.bmm(dl, Wfc)                                                     # [C, N, fc_in]
 
         # ---------------- backward ----------------
         bufs = list(self.gbuf)

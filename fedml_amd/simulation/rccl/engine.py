@@ -139,6 +139,15 @@ class ClientBatchEngine:
                         nn_ops.set_f32_mma_mode(str(getattr(args, "fp32_mma", "exact") or "exact"))
                 except UnsupportedTransformer:
                     pass
+            if self.tf is None and os.environ.get("FEDML_AMD_BATCHED_RNN", "1") != "0":
+                # recurrent language models: client-batched LSTM (parallel/batched_rnn.py, fp32 — the
+                # reference's precision; fused HIP cell kernels + client-batched GEMMs)
+                from ...parallel.batched_rnn import BatchedRNN, UnsupportedRNN
+                try:
+                    self.tf = BatchedRNN(model, self.C)
+                    logging.info("virtual-client engine: client-batched LSTM path (%s)", self.tf.kind)
+                except UnsupportedRNN:
+                    pass
             if self.tf is None:
                 logging.info("virtual-client engine: sequential per-client path (%s)", e)
         # GroupNorm layers run the HIP GN kernels on GPU (same parameters / state_dict keys); the

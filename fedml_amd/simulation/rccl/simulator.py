@@ -220,6 +220,8 @@ class RCCLSimulator:
                                                            n_upload=n_up)
                 self.upload_bytes.append(nb)
                 comm.all_reduce_flat(self.partial)
+            elif self.engine.deterministic:
+                self._det_partial_sum(w)
             elif comm.is_dist() and self.layout.size > self.bucket_elems:
                 # large models (DistilBERT / ViT: 67-86 M params): the weighted sum is produced bucket by
                 # bucket and each bucket's all-reduce is enqueued at once — RCCL's stream reduces bucket k
@@ -254,6 +256,22 @@ class RCCLSimulator:
             else:
                 self.global_flat.copy_(avg)
             self._post_aggregate()
+
+    def _det_partial_sum(self, w):
+        """Deterministic mode: Σ_c w_c·params_c ‖ Σ_c w_c accumulated and all-reduced in fp64, rounded to fp32 once.
+        The fp64 sums of different client groupings (1 rank × K clients vs R ranks × K/R) differ only at 2^-53, far
+        below the final fp32 rounding, so the global model's bits do not depend on the world size."""
+        P = self.layout.size
+        if getattr(self, "_partial64", None) is None:
+            self._partial64 = torch.empty(P + 1, dtype=torch.float64, device=self.device)
+        wd = w.to(torch.float64).view(-1, 1)
+        step = max(1, (1 << 26) // max(1, self.C))         # bounds the fp64 temporary to 512 MB
+        for lo in range(0, P, step):
+            hi = min(P, lo + step)
+            torch.sum(self.engine.params[:, lo:hi].to(torch.float64) * wd, 0, out=self._partial64[lo:hi])
+        self._partial64[P:].copy_(wd.sum().view(1))
+        comm.all_reduce_flat(self._partial64)
+        self.partial.copy_(self._partial64)
 
     def _fednova_coefficients(self, ids, mine):
         """FedNova weights of this rank's slots: coef_i = τ_eff·p_i / a_i with p_i = n_i / Σn over the round's

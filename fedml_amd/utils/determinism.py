@@ -8,9 +8,13 @@ reproducible from run to run on the same world size:
   before the process group is created; ``parallel.comm.init_process_group`` calls ``apply_env()``);
 * FL aggregation kernels are fixed-order by construction (``fl_kernels.hip``: the weighted sum walks the
   clients in slot order per element; norms use fixed partial slots + an ordered finalize);
-* the client-batched ResNet step leaves the native HIP kernels — their BN statistics and split-K weight
-  gradients accumulate with fp32 atomics, whose order (and so the last bit) varies between runs — for
-  the batched torch path under ``torch.use_deterministic_algorithms`` (MIOpen's deterministic solutions);
+* the client-batched ResNet step keeps the native HIP kernels: their cross-workgroup fp32 atomics (BN
+  statistics, split weight gradients) accumulate into 128-bit fixed-point shadows instead and are rounded
+  once (``ops/det_ops.py``, ``csrc/detacc.h``); the tiling of those kernels is fixed independently of the
+  number of client slots per GPU, so a client's gradients do not depend on the world size either;
+* the fp32 transformer kernels' LayerNorm / bias-gradient reductions become fixed-order column sums;
+* the aggregation partial sums Σ n_c·w_c (and their all-reduce) run in fp64 and are rounded to fp32
+  once, so packing clients onto more ranks does not change the global model's bits;
 * data order / augmentation / dropout are already keyed by (seed, round, client id).
 
 The cost is the native conv speed-up; deterministic runs are for debugging and bisecting, not benchmarks.

@@ -27,4 +27,6 @@ def main(role, silo, rank_in_silo, pg_port, out):
 
 
 if __name__ == "__main__":
+    import mp_harness
+    mp_harness.install_stack_dump()
     main(sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5])

@@ -13,7 +13,8 @@ def main(role, silo, rank_in_silo, pg_port, out, n_proc, n_local, device, model=
     from fedml_amd.arguments import Arguments
     torch.set_num_threads(1)
     cfg = {"training_type": "cross_silo", "scenario": "hierarchical", "dataset": dataset, "model": model,
-           "client_num_in_total": n_silos, "client_num_per_round": n_silos, "comm_round": rounds, "epochs": 1,
+           "client_num_in_total": n_silos,
+           "client_num_per_round": int(os.environ.get("FEDML_TEST_PER_ROUND", n_silos)), "comm_round": rounds, "epochs": 1,
            "batch_size": 8, "learning_rate": 0.05, "frequency_of_the_test": 0, "backend": "TCP",
            "federated_optimizer": "FedAvg", "worker_num": n_silos + 1,
            "client_id_list": str(list(range(1, n_silos + 1))), "sys_perf_interval": 0,
@@ -33,6 +34,8 @@ def main(role, silo, rank_in_silo, pg_port, out, n_proc, n_local, device, model=
 
 
 if __name__ == "__main__":
+    import mp_harness
+    mp_harness.install_stack_dump()
     a = sys.argv
     main(a[1], int(a[2]), int(a[3]), int(a[4]), a[5], int(a[6]), int(a[7]), a[8], *(a[9:11]),
          *([int(a[11])] if len(a) > 11 else []))

@@ -17,20 +17,24 @@ def run(rank, world, port, out_path, model_name, clients, counts_seed, shuffle=F
     from fedml_amd.simulation.rccl.client_store import DeviceClientStore
     from fedml_amd.simulation.rccl.simulator import RCCLSimulator
     from fedml_amd.parallel import comm
-    ds = "mnist" if model_name == "lr" else "cifar10"
-    model_arg = "resnet56" if model_name == "resnet_shallow" else model_name
+    headline = model_name == "headline"   # BASELINE config 3: ResNet-56 / CIFAR-100, 500 samples, batch 64
+    ds = "mnist" if model_name == "lr" else ("cifar100" if headline else "cifar10")
+    model_arg = "resnet56" if model_name in ("resnet_shallow", "headline") else model_name
     args = Arguments.from_dict({"x": {
         "training_type": "simulation", "backend": "RCCL",
         "federated_optimizer": os.environ.get("FEDML_TEST_OPTIMIZER", "FedAvg"), "dataset": ds,
         "momentum": float(os.environ.get("FEDML_TEST_MOMENTUM", "0")), "gmf": float(os.environ.get("FEDML_TEST_GMF", "0")),
         "model": model_arg, "client_num_in_total": clients, "comm_round": 2,
-        "epochs": 1, "batch_size": 8, "client_optimizer": "sgd", "learning_rate": 0.05, "frequency_of_the_test": 0,
+        "epochs": 1, "batch_size": 64 if headline else 8, "client_optimizer": "sgd",
+        "learning_rate": 0.001 if headline else 0.05,
+        "frequency_of_the_test": 0, "deterministic": os.environ.get("FEDML_AMD_DETERMINISTIC", "0") == "1",
         "random_seed": 0, "shuffle": shuffle, "data_augmentation": augment and ds == "cifar10",
         "compression": os.environ.get("FEDML_TEST_COMPRESSION", ""),
         "elastic": os.environ.get("FEDML_TEST_ELASTIC", "0") == "1", "elastic_timeout_s": 30,
         "elastic_settle_s": 4.0,
         "allreduce_bucket_mb": float(os.environ.get("FEDML_TEST_BUCKET_MB", "32")),
-        "client_num_per_round": int(os.environ.get("FEDML_TEST_PER_ROUND", clients))}})
+        "client_num_per_round": int(os.environ.get("FEDML_TEST_PER_ROUND", clients)),
+        **({"weight_decay": 0.001} if headline else {})}})
     spec = get_spec(ds)
     torch.manual_seed(0)
     if model_name == "resnet_shallow":  # deep ResNets at init are chaotic in fp32 (see test_batched_engine)
@@ -39,10 +43,10 @@ def run(rank, world, port, out_path, model_name, clients, counts_seed, shuffle=F
     else:
         model = create(args, spec.num_classes)
     g = torch.Generator().manual_seed(counts_seed)
-    counts = [int(v) for v in torch.randint(8, 24, (clients,), generator=g)]
+    counts = [500] * clients if headline else [int(v) for v in torch.randint(8, 24, (clients,), generator=g)]
     store = DeviceClientStore.synthetic_on_device(spec, counts, dev, seed=0)
     sim = RCCLSimulator(args, dev, None, model, store=store)
-    if dev.type == "cuda" and model_name == "resnet_shallow":
+    if dev.type == "cuda" and model_name in ("resnet_shallow", "headline"):
         # the headline engine: native HIP ResNet step (fp32), HIP-graph replays
         assert sim.engine.native_step is not None and sim.engine.native_step.dtype == torch.float32, rank
         assert sim.engine.use_graphs
@@ -67,6 +71,8 @@ def run(rank, world, port, out_path, model_name, clients, counts_seed, shuffle=F
 
 
 if __name__ == "__main__":
+    import mp_harness
+    mp_harness.install_stack_dump()
     r, w, p = int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3])
     run(r, w, p, sys.argv[4], sys.argv[5], int(sys.argv[6]), int(sys.argv[7]),
         shuffle=len(sys.argv) > 8 and sys.argv[8] == "1", augment=len(sys.argv) > 9 and sys.argv[9] == "1")

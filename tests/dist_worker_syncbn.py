@@ -34,4 +34,6 @@ def main(rank, world, port, out):
 
 
 if __name__ == "__main__":
+    import mp_harness
+    mp_harness.install_stack_dump()
     main(int(sys.argv[1]), int(sys.argv[2]), int(sys.argv[3]), sys.argv[4])

@@ -8,6 +8,7 @@ import subprocess
 import sys
 import threading
 
+import mp_harness
 import pytest
 import torch
 
@@ -71,7 +72,7 @@ def test_hierarchical_cross_silo_processes(tmp_path):
         for r in range(2):
             cmds.append([sys.executable, w, "silo", str(silo), str(r), str(port), out])
     ps = [subprocess.Popen(c, env=env) for c in cmds]
-    codes = [p.wait(timeout=300) for p in ps]
+    codes = mp_harness.wait_all(ps, 300)
     assert codes == [0] * len(cmds), codes
     g = torch.load(out, weights_only=True)
     assert all(torch.isfinite(v.float()).all() for v in g.values())

@@ -4,6 +4,7 @@ import os
 import subprocess
 import sys
 
+import mp_harness
 import pytest
 import torch
 import torch.nn as nn
@@ -19,7 +20,7 @@ def _run_ddp(tmp_path, mode, device="cpu"):
     env = dict(os.environ, PYTHONPATH=os.path.dirname(HERE), OMP_NUM_THREADS="1", FEDML_TEST_DEVICE=device)
     ps = [subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker_ddp.py"), str(r), "2", str(port), out, mode],
                            env=env) for r in range(2)]
-    assert [p.wait(timeout=300) for p in ps] == [0, 0]
+    assert mp_harness.wait_all(ps, 300) == [0, 0]
     return torch.load(out, weights_only=True)
 
 

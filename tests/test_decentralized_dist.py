@@ -4,6 +4,7 @@ import os
 import subprocess
 import sys
 
+import mp_harness
 import pytest
 import torch
 
@@ -16,7 +17,7 @@ def _run(world, out, mode):
     env = dict(os.environ, PYTHONPATH=os.path.dirname(HERE), OMP_NUM_THREADS="1")
     ps = [subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker_decentralized.py"), str(r), str(world),
                             str(port), out, mode], env=env) for r in range(world)]
-    assert [p.wait(timeout=300) for p in ps] == [0] * world
+    assert mp_harness.wait_all(ps, 300) == [0] * world
     return torch.load(out, weights_only=True)
 
 

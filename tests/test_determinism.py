@@ -33,13 +33,15 @@ def _args(**kw):
     return Arguments.from_dict({"x": cfg})
 
 
-def _run(dev, block=BasicBlock, **kw):
+def _run(dev, block=BasicBlock, counts=(16, 16, 13), rounds=2, **kw):
     torch.manual_seed(0)
     model = ResNet(block, [1, 1, 1], 10)
     spec = get_spec("cifar10")
-    store = DeviceClientStore.synthetic_on_device(spec, [16, 16, 13], torch.device(dev), seed=0)
+    store = DeviceClientStore.synthetic_on_device(spec, list(counts), torch.device(dev), seed=0)
+    kw.setdefault("client_num_in_total", len(counts))
+    kw.setdefault("client_num_per_round", len(counts))
     sim = RCCLSimulator(_args(**kw), torch.device(dev), None, copy.deepcopy(model), store=store)
-    sim.run(2)
+    sim.run(rounds)
     out = sim.global_flat.detach().cpu().clone()
     eng = sim.engine
     used_det = eng.native_step is not None and eng.native_step.det is not None
@@ -74,3 +76,55 @@ def test_deterministic_mode_gpu_bitwise(block):
     c, eng2, used2 = _run("cuda", block, deterministic=False)
     assert eng2.native_step is not None and not used2
     assert float((a - c).norm() / c.norm()) < 1e-4
+
+
+@pytest.mark.gpu
+def test_deterministic_mode_many_ragged_geometries():
+    """One client per round out of seven whose sizes leave remainders 1..7 at batch 8: every round's last step
+    has a new batch geometry. The accumulation targets are shared across geometries, so the 16-target
+    deterministic registry never overflows, and the run stays bitwise reproducible."""
+    counts = (9, 10, 11, 12, 13, 14, 15)
+    a, eng, used = _run("cuda", Bottleneck, counts=counts, rounds=7, client_num_per_round=1)
+    b, _, _ = _run("cuda", Bottleneck, counts=counts, rounds=7, client_num_per_round=1)
+    assert used and len(eng.native_step._states) >= 3, len(eng.native_step._states)
+    assert torch.equal(a, b), float((a - b).abs().max())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["distilbert", "vit"])
+def test_deterministic_mode_fp32_transformer_bitwise(kind):
+    """fp32 transformers on the client-batched tf_f32 kernels in deterministic mode: their LN
+    dgamma/dbeta and bias-gradient reductions leave the fp32 atomics for fixed-order column sums, so two
+    runs of several local steps (dropout ON, keyed by seed) are bitwise identical."""
+    from fedml_amd.arguments import Arguments
+    from fedml_amd.simulation.rccl.client_store import DeviceClientStore
+    from fedml_amd.simulation.rccl.engine import ClientBatchEngine
+    from fedml_amd.models.transformer.distilbert import distilbert
+    from fedml_amd.models.transformer.vit import vit_tiny
+
+    def run():
+        torch.manual_seed(0)
+        m = distilbert(3, vocab=211, dim=128, n_layers=2, n_heads=2, hidden=256, max_pos=64) \
+            if kind == "distilbert" else vit_tiny(num_classes=7, img_size=32, patch=4, depth=2)
+        C, n = 3, 24
+        g = torch.Generator().manual_seed(1)
+        if kind == "distilbert":
+            x = torch.randint(1, 211, (C * n, 48), generator=g)
+            y = torch.randint(0, 3, (C * n,), generator=g)
+        else:
+            x = torch.randn(C * n, 3, 32, 32, generator=g)
+            y = torch.randint(0, 7, (C * n,), generator=g)
+        args = _args(client_optimizer="adam", learning_rate=1e-3)
+        eng = ClientBatchEngine(m.to("cuda"), C, "cuda", args, compute_dtype=None)
+        assert eng.tf is not None and eng.deterministic
+        eng.load_global(eng.layout.flatten(m.state_dict(), device="cuda"))
+        store = DeviceClientStore(x.cuda(), y.cuda(), [0, n, 2 * n], [n, n, n - 5])
+        eng.train(store, torch.arange(C, device="cuda"), 1, 8, 1e-3, shuffle=True, rng_key=7)
+        torch.cuda.synchronize()
+        out = eng.params.clone()
+        eng.close()
+        return out
+
+    a, b = run(), run()
+    assert torch.isfinite(a).all()
+    assert torch.equal(a, b), float((a - b).abs().max())

@@ -10,6 +10,7 @@ import os
 import subprocess
 import sys
 
+import mp_harness
 import pytest
 import torch
 
@@ -63,7 +64,7 @@ def test_batched_silos_equal_flat_simulator(tmp_path):
         for r in range(n_proc):
             cmds.append([sys.executable, w, "silo", str(silo), str(r), str(port)] + common)
     ps = [subprocess.Popen(c, env=env) for c in cmds]
-    codes = [p.wait(timeout=300) for p in ps]
+    codes = mp_harness.wait_all(ps, 300)
     assert codes == [0] * len(cmds), codes
     got = torch.load(out, weights_only=True)
     ref, init = _flat_reference(n_silos, n_local, rounds)

@@ -214,22 +214,57 @@ def test_generic_conv_f32_kernels(cin, cout, k, stride, hw):
         assert rel(garena[c, 16:16 + cout * cin * k * k].view_as(rdw), rdw) < 1e-5
 
 
-def _reference_grads(model, layout, flat, x, y, dtype=torch.float32, device=DEV):
-    C = x.shape[0]
-    grads = torch.zeros(C, layout.size, device=DEV, dtype=torch.float64)
-    loss_sum = 0.0
-    for c in range(C):
-        m = copy.deepcopy(model).to(device=device, dtype=dtype)
-        m.load_state_dict({k: v.to(device) for k, v in layout.unflatten(flat).items()})
-        m.train()
-        loss = torch.nn.functional.cross_entropy(m(x[c].to(device=device, dtype=dtype)), y[c].to(device))
-        loss.backward()
-        loss_sum += float(loss.detach())
-        sd = {k: p.grad for k, p in m.named_parameters()}
-        for s in layout.slots:
-            if s.key in sd:
-                grads[c, s.offset:s.offset + s.numel] = sd[s.key].reshape(-1).to(DEV, torch.float64)
-    return loss_sum, grads
+def _native_masks(step, c):
+    """The ReLU masks client ``c``'s native forward used, NCHW bool, in network order: stem, then per block its
+    inner activations relu(y_j·s_j + t_j) (evaluated in fp64 — the product of two fp32 values and its sum with
+    a third keep their sign exactly) and its stored block output (> 0)."""
+    def inner(y, v):
+        return (y[c].double() * v[0, c].double() + v[1, c].double() > 0).permute(0, 3, 1, 2)
+    masks = [(step.stem_out[c] > 0).permute(0, 3, 1, 2)]
+    for b in step.blocks:
+        assert all(y is not None for y in b.ys), "recomputed-y blocks keep no activation to read the mask from"
+        for j in range(len(b.convs) - 1):
+            masks.append(inner(b.ys[j], step.bn_vec[b.bns[j].key]))
+        masks.append((b.out[c] > 0).permute(0, 3, 1, 2))
+    return masks
+
+
+def _masked_fp64_grads(step, layout, flat, x, y, masks):
+    """One client's fp64 step through the native step's own layer specs, every ReLU replaced by the given mask
+    (``masks`` in ``_native_masks`` order, None → the fp64 sign itself). Returns (loss, {key: grad}, flips):
+    flips = mask positions where the given mask disagrees with the fp64 pre-activation's sign."""
+    F = torch.nn.functional
+    sd = layout.unflatten(flat.double().cpu())
+    prm = {s.key: sd[s.key].double().requires_grad_(True) for s in layout.slots if s.trainable}
+    it = iter(masks) if masks is not None else None
+    flips = [0]
+
+    def relu(z):
+        if it is None:
+            return torch.relu(z)
+        m = next(it).cpu()
+        flips[0] += int(((z.detach() > 0) != m).sum())
+        return z * m.to(z.dtype)
+
+    def conv(cv, h):
+        return F.conv2d(h, prm[cv.key], stride=cv.stride, padding=cv.pad)
+
+    def bn(spec, h):
+        return F.batch_norm(h, None, None, prm[f"{spec.key}.weight"], prm[f"{spec.key}.bias"], True, 0.0, spec.eps)
+
+    h = relu(bn(step.stem[1], conv(step.stem[0], x.double())))
+    for b in step.blocks:
+        z = h
+        for j, (cv, sp) in enumerate(zip(b.convs, b.bns)):
+            z = bn(sp, conv(cv, z))
+            if j < len(b.convs) - 1:
+                z = relu(z)
+        sc = bn(b.ds_bn, conv(b.ds_conv, h)) if b.ds_conv is not None else h
+        h = relu(z + sc)
+    logits = F.linear(h.mean((2, 3)), prm["fc.weight"], prm["fc.bias"])
+    loss = F.cross_entropy(logits, y.cpu())
+    loss.backward()
+    return float(loss.detach()), {k: p.grad for k, p in prm.items()}, flips[0]
 
 
 @pytest.mark.parametrize("builder,hw", [
@@ -238,19 +273,17 @@ def _reference_grads(model, layout, flat, x, y, dtype=torch.float32, device=DEV)
     (lambda: ResNet(Bottleneck, [2, 2, 2], 100), 32),
 ])
 def test_native_step_f32_matches_reference(builder, hw):
-    """The fp32 native step against an fp64 reference (CPU), next to PyTorch's own fp32 GPU step.
+    """The fp32 native step (deterministic mode: bit-reproducible) against an fp64 step that uses the native
+    step's OWN ReLU masks.
 
-    Tolerance, measured rather than chosen: fp32 gradients agree with fp64 to ~1e-6 except where a ReLU
-    pre-activation sits within rounding of 0 — its mask (and that element's gradient, |g| not ~eps·|g|)
-    then depends on the last bits of the BN scale/shift. One flip moves every upstream gradient of these
-    tiny random-init nets by 1e-4..1e-2; with ~10⁶ pre-activations per step a flip is a coin toss for ANY
-    fp32 implementation (measured: the native exact step flipped one mask on the [1,1,1] net, PyTorch fp32
-    did not on that seed; both flip on others). Two bounds, both measured on the same inputs:
-      * outliers: the fp64 step under input/weight perturbations × (1 ± u) — u = 2^-20 (16 fp32 ulps, enough
-        to flip a few masks per draw) for exact products, 2^-16 for the split-bf16 mode — 3 draws; the native
-        step stays within 3× the larger of that flip spread and PyTorch fp32's own error, per slot (floor 1e-5);
-      * bulk: the median slot error ≤ 10 × the median of PyTorch fp32 (exact products) or of the 2^-16
-        perturbed fp64 step (split-bf16 products) (floor 1e-6) — no systematic error."""
+    A ReLU pre-activation within rounding of 0 makes its mask — and every upstream gradient — depend on the
+    last bits of the BN scale/shift: one such flip moves gradients of these random-init nets by 1e-4..1e-2
+    for ANY fp32 implementation (round 3: the driver's box saw native median 2.6e-3 vs fp64 on
+    ``Bottleneck,[2,2,2]``). Reading the masks back from the native activations (stored pre-BN outputs and
+    BN scale/shift, block outputs) and forcing them on the fp64 step removes that discontinuity, so the
+    comparison is a plain fp32-vs-fp64 rounding bound on every slot. The number of masks the native step
+    set differently from fp64's own signs is reported and must stay a vanishing fraction (only elements
+    at the threshold can flip); a kernel bug shows up as a large per-slot error, not as flips."""
     torch.manual_seed(0)
     model = builder()
     layout = ParamLayout.from_module(model)
@@ -263,45 +296,37 @@ def test_native_step_f32_matches_reference(builder, hw):
     row_scale = torch.full((C, N), 1.0 / N, device=DEV)
     active = torch.ones(C, device=DEV)
     step = NativeResNetStep(model, layout, C, DEV, dtype=F32)
-    assert step.dtype == F32
-    loss = float(step.step(arena, garena, x, y, row_scale, active))
-    torch.cuda.synchronize()
-    assert step.packed.dtype == F32 and step.x_in.dtype == F32
-    flat64, x64 = flat.cpu().double(), x.cpu().double()
-    ref_loss, ref64 = _reference_grads(model, layout, flat64, x64, y.cpu(), torch.float64, "cpu")
+    step.enable_deterministic()
+    try:
+        assert step.dtype == F32
+        loss = float(step.step(arena, garena, x, y, row_scale, active))
+        torch.cuda.synchronize()
+        assert step.packed.dtype == F32 and step.x_in.dtype == F32
+        ref_loss, worst, flips, n_mask, errs = 0.0, 0.0, 0, 0, []
+        for c in range(C):
+            masks = _native_masks(step, c)
+            n_mask += sum(int(m.numel()) for m in masks)
+            lc, gref, fl = _masked_fp64_grads(step, layout, flat, x[c].cpu(), y[c], masks)
+            ref_loss += lc
+            flips += fl
+            for s in layout.slots:
+                if s.key not in gref:
+                    continue
+                r = gref[s.key].reshape(-1)
+                e = float((garena[c, s.offset:s.offset + s.numel].double().cpu() - r).norm()
+                          / r.norm().clamp_min(1e-30))
+                errs.append((e, c, s.key))
+    finally:
+        step.close()
+    errs.sort(reverse=True)
+    med = errs[len(errs) // 2][0]
+    print(f"[{_mode[0]}] masked-fp64 slot error max {errs[0][0]:.2e} ({errs[0][2]}) median {med:.2e}; "
+          f"native masks differing from fp64 signs: {flips} of {n_mask}")
     assert abs(loss - ref_loss) / ref_loss < 1e-5 * TOL[_mode[0]], (loss, ref_loss)
-    _, t32 = _reference_grads(model, layout, flat, x, y, torch.float32, DEV)
-    u = 2.0 ** -20 if _mode[0] == "exact" else 2.0 ** -16
-    pert = []
-    for r in range(3):
-        g = torch.Generator().manual_seed(1000 + r)
-        fp = flat64 * (1 + u * (2 * torch.rand(flat64.shape, generator=g, dtype=torch.float64) - 1))
-        xp = x64 * (1 + u * (2 * torch.rand(x64.shape, generator=g, dtype=torch.float64) - 1))
-        pert.append(_reference_grads(model, layout, fp, xp, y.cpu(), torch.float64, "cpu")[1])
-
-    def err(g, sl, r):
-        return float((g[:, sl].double().cpu() - r).norm() / r.norm().clamp_min(1e-30))
-
-    e_nat, e_t32, e_pert = [], [], []
-    for s in layout.slots:
-        if not s.trainable:
-            continue
-        sl = slice(s.offset, s.offset + s.numel)
-        r = ref64[:, sl].cpu()
-        e_nat.append((s.key, err(garena, sl, r)))
-        e_t32.append(err(t32, sl, r))
-        e_pert.append(max(err(p, sl, r) for p in pert))
-    bound = max(3 * max(max(e_t32), max(e_pert)), 1e-5)
-    bad = [(k, e) for k, e in e_nat if e > bound]
-    print(f"[{_mode[0]}] native max {max(e for _, e in e_nat):.2e} median "
-          f"{sorted(e for _, e in e_nat)[len(e_nat) // 2]:.2e}; torch fp32 max {max(e_t32):.2e} median "
-          f"{sorted(e_t32)[len(e_t32) // 2]:.2e}; perturbed fp64 max {max(e_pert):.2e} -> bound {bound:.2e}")
-    assert not bad, (bound, bad[:8])
-    med = sorted(e for _, e in e_nat)[len(e_nat) // 2]
-    # bulk yardstick at the mode's product precision: PyTorch fp32 for exact products; the fp64 step perturbed
-    # at 2^-16 for split-bf16 products (~2^-16 relative each, so that is the noise they are entitled to)
-    ref_med = sorted(e_t32)[len(e_t32) // 2] if _mode[0] == "exact" else sorted(e_pert)[len(e_pert) // 2]
-    assert med <= max(10 * ref_med, 1e-6), (med, ref_med)
+    assert flips <= max(8, n_mask // 100000), (flips, n_mask)
+    # fp32 storage, fp32 accumulation: per-slot relative error a few fp32 ulps times the depth's growth
+    assert errs[0][0] < 1e-4 * TOL[_mode[0]], errs[:8]
+    assert med < 1e-5 * TOL[_mode[0]], med
     s = layout.slot("bn1.running_mean")
     m = copy.deepcopy(model).to(DEV)
     m.train()

@@ -10,15 +10,13 @@ import sys
 import pytest
 import torch
 
+import mp_harness
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    return mp_harness.free_port()
 
 
 def _launch(world, out, model, clients, shuffle=False, augment=False, **extra_env):
@@ -28,7 +26,7 @@ def _launch(world, out, model, clients, shuffle=False, augment=False, **extra_en
                                str(port), out, model, str(clients), "3", "1" if shuffle else "0",
                                "1" if augment else "0"], env=env)
              for r in range(world)]
-    codes = [p.wait(timeout=600) for p in procs]
+    codes = mp_harness.wait_all(procs, 420)
     assert codes == [0] * world, codes
     return torch.load(out, weights_only=True)
 
@@ -90,7 +88,7 @@ def test_elastic_reinit_after_rank_death(tmp_path):
     e = dict(os.environ, PYTHONPATH=os.path.dirname(HERE), OMP_NUM_THREADS="2", FEDML_TEST_DIE="2:1", **env)
     procs = [subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker_rccl_sim.py"), str(r), "3", str(port),
                                out, "lr", "7", "3", "1", "0"], env=e) for r in range(3)]
-    codes = [p.wait(timeout=300) for p in procs]
+    codes = mp_harness.wait_all(procs, 300)
     assert codes == [0, 0, 0], codes
     w3 = torch.load(out, weights_only=True)
     assert float((w1 - w3).norm() / w1.norm()) < 1e-5

@@ -7,6 +7,8 @@ import sys
 
 import torch
 
+import mp_harness
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
@@ -17,7 +19,7 @@ def test_syncbn_two_ranks_equal_full_batch(tmp_path):
     env = dict(os.environ, PYTHONPATH=os.path.dirname(HERE), OMP_NUM_THREADS="1")
     ps = [subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker_syncbn.py"), str(r), "2", str(port), out],
                            env=env) for r in range(2)]
-    assert [p.wait(timeout=120) for p in ps] == [0, 0]
+    assert mp_harness.wait_all(ps, 120) == [0, 0]
     r = torch.load(out, weights_only=True)
     g = torch.Generator().manual_seed(0)
     x = (torch.randn(8, 6, 5, 5, generator=g) * 3 + 1).requires_grad_(True)
