@@ -48,6 +48,7 @@ def parse():
     p.add_argument("--client-optimizer", default="sgd")
     p.add_argument("--partition", default="homo", help="homo (equal IID shards, the headline) | hetero (LDA)")
     p.add_argument("--partition-alpha", type=float, default=0.5, help="Dirichlet concentration of --partition hetero")
+    p.add_argument("--client-exec", default="auto", help="auto | batched | sequential (non-native conv nets)")
     p.add_argument("--preset", default="", help="resnet18_cifar10_10 | distilbert_fedopt_32 | vit_b16_32 "
                                                 "(other BASELINE.json configs; the default is the headline)")
     presets = {
@@ -58,6 +59,12 @@ def parse():
                                      client_optimizer="adamw"),
         "vit_b16_32": dict(model="vit_b16", dataset="ILSVRC2012", clients=32, samples_per_client=32, batch_size=16,
                            lr=1e-4, client_optimizer="adamw"),
+        # reference BENCHMARK_MPI.md:104: MobileNet / CIFAR-10, 10 clients, bs 64, SGD lr 0.001, wd 0.001
+        "mobilenet_cifar10_10": dict(model="mobilenet", dataset="cifar10", clients=10, samples_per_client=5000,
+                                     batch_size=64, lr=0.001),
+        # reference BENCHMARK_MPI.md:52: RNN_OriginalFedAvg / Shakespeare (LEAF), 10 clients per round, bs 4
+        "rnn_shakespeare_10": dict(model="rnn", dataset="shakespeare", clients=10, samples_per_client=2000,
+                                   batch_size=4, lr=1.47),
     }
     pre, _ = p.parse_known_args()
     if pre.preset:   # a preset changes the defaults; flags given on the command line still win
@@ -93,7 +100,7 @@ def main():
         "client_num_per_round": a.clients, "comm_round": a.steps, "epochs": a.epochs,
         "batch_size": a.batch_size, "client_optimizer": a.client_optimizer, "learning_rate": a.lr, "weight_decay": 0.001,
         "frequency_of_the_test": 0, "compute_dtype": a.dtype if use_gpu else "fp32", "random_seed": 0,
-        "fp32_mma": a.fp32_mma,
+        "fp32_mma": a.fp32_mma, "client_exec": a.client_exec,
     }})
     torch.manual_seed(0)
     model = create(args, spec.num_classes)

@@ -61,6 +61,13 @@ class FedMLAggregator:
 
     def aggregate(self):
         t0 = time.time()
+        hooked = callable(getattr(self.aggregator, "on_before_aggregation", None)) or \
+            callable(getattr(self.aggregator, "on_after_aggregation", None))
+        if hooked and self.model_dict and all(torch.is_tensor(v) for v in self.model_dict.values()):
+            # a user aggregator with aggregation hooks (robust aggregation, DP noise) sees state dicts on the
+            # device plane too: the flat slot rows are unflattened (device-side views, no host copy)
+            for i in list(self.model_dict):
+                self.model_dict[i] = self.flat_layout.unflatten(self.model_dict[i], clone=False)
         if self.model_dict and all(torch.is_tensor(v) for v in self.model_dict.values()):
             # flat device uploads (device mailbox slots): one FedAvg kernel over the stacked rows; the
             # result stays a flat device tensor (the state-dict hooks do not apply on this plane)

@@ -24,6 +24,19 @@ def _round_up(v, m):
     return (v + m - 1) // m * m
 
 
+def supported_module(m, elem_bytes: int = 4) -> bool:
+    """The layer shape alone (no tensors): a groups-1 convolution both native GEMMs take."""
+    k = m.kernel_size
+    cout = m.out_channels
+    if not (m.groups == 1 and m.dilation == (1, 1) and k[0] == k[1] and m.stride[0] == m.stride[1]
+            and isinstance(m.padding, tuple) and m.padding[0] == m.padding[1] and (cout in (16, 32) or cout % 64 == 0)
+            and m.padding_mode == "zeros"):
+        return False
+    cin_pad = _pad_channels(m.in_channels)
+    kk = k[0] * k[0]
+    return _gemm_ok(cout, kk * cin_pad, elem_bytes) and _gemm_ok(cin_pad, kk * cout, elem_bytes)
+
+
 def supported(m, x, w) -> bool:
     """nn.Conv2d ``m`` on activations ``x`` [B, C·Cin, H, W] with the client-stacked weight view ``w``."""
     if not (x.is_cuda and x.dim() == 4 and x.dtype in (torch.float32, torch.bfloat16)):

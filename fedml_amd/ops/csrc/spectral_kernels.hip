@@ -83,7 +83,9 @@ __global__ __launch_bounds__(256) void spec_fft2_kernel(const float* __restrict_
 // running[c][i] (CHW elements): mean over the B planes of channel c, then the EMA (mode 0: keep, 1: EMA,
 // 2: replace — the reference's first call, when the running amplitude is still all zeros)
 __global__ __launch_bounds__(256) void spec_amp_update_kernel(const float* __restrict__ amp, float* __restrict__ run,
-                                                              int B, int C, int HW, float momentum, int mode) {
+                                                              int B, int C, int HW, float momentum, int mode,
+                                                              const unsigned char* __restrict__ first) {
+  if (first) mode = *first ? 2 : 1;   // the reference's `np.sum(running_amp) == 0`, decided on the device
   const int64_t n = (int64_t)C * HW;
   for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
     float s = 0.f;
@@ -152,6 +154,120 @@ __global__ __launch_bounds__(256) void spec_mix_ifft2_kernel(const float2* __res
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------------------------
+// Power-of-two planes up to 512 × 512 (HS-FedAvg's 3 × 512 × 512 amplitude, hs_fedavg/fedavg_api.py:135): a
+// radix-2 Stockham FFT in LDS, applied separably — a row pass (whole rows in LDS, several per workgroup) and a
+// column pass (a 16-column × H tile in LDS, padded leading dimension against bank conflicts, coalesced 128-B row
+// segments on both sides). Forward: rows (real in) → columns (F out, |F| fused). Inverse with the band mix:
+// columns (mix applied while loading F) → rows (real part × 1/HW out). O(HW·log HW) per plane instead of the
+// DFT's O(HW·(H+W)).
+constexpr int kMaxN = 512;
+
+__device__ __forceinline__ void twiddles_half(float2* tw, int n, float sign) {   // tw[k] = e^{sign·2πi·k/n}, k < n/2
+  for (int k = threadIdx.x; k < (n >> 1); k += blockDim.x) {
+    double sn, cs;
+    sincospi(2.0 * k / n, &sn, &cs);
+    tw[k] = make_float2((float)cs, (float)(sign * sn));
+  }
+}
+
+// nfft independent length-N (= 2^lg) transforms at x + f·ld; y is scratch of the same shape. Stockham autosort:
+// no bit reversal, the result (natural order) is in the returned buffer. Every stage ends with a barrier.
+__device__ float2* stockham(float2* x, float2* y, const float2* tw, int lg, int nfft, int ld) {
+  const int half = 1 << (lg - 1);
+  for (int ls = 0; ls < lg; ++ls) {                 // s = 2^ls, current length n = N / s, m = n / 2
+    const int s = 1 << ls, m = half >> ls;
+    for (int i = threadIdx.x; i < nfft * half; i += blockDim.x) {
+      const int f = i >> (lg - 1);
+      const int r = i & (half - 1);                 // r = p·s + q
+      const int p = r >> ls, q = r & (s - 1);
+      const float2* xf = x + f * ld;
+      float2* yf = y + f * ld;
+      const float2 a0 = xf[q + s * p], a1 = xf[q + s * (p + m)];
+      const float2 w = tw[p * s];
+      const float dx = a0.x - a1.x, dy = a0.y - a1.y;
+      yf[q + 2 * s * p] = make_float2(a0.x + a1.x, a0.y + a1.y);
+      yf[q + 2 * s * p + s] = make_float2(dx * w.x - dy * w.y, dx * w.y + dy * w.x);
+    }
+    __syncthreads();
+    float2* t = x;
+    x = y;
+    y = t;
+  }
+  return x;
+}
+
+// R rows of length W = 2^lg per workgroup. In: real (xr) or complex (xc). Out: complex (out) or the real part
+// (out_r), times `scale`.
+__global__ __launch_bounds__(256) void fft_rows_kernel(const float* __restrict__ xr, const float2* __restrict__ xc,
+                                                       float2* __restrict__ out, float* __restrict__ out_r,
+                                                       int64_t rows, int lg, int R, float sign, float scale) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int W = 1 << lg;
+  float2* tw = reinterpret_cast<float2*>(smem);
+  float2* A = tw + kMaxN / 2;
+  float2* Bf = A + R * W;
+  const int64_t r0 = (int64_t)blockIdx.x * R;
+  const int nr = (int)min((int64_t)R, rows - r0);
+  for (int i = threadIdx.x; i < nr * W; i += blockDim.x) {
+    const int64_t g = r0 * W + i;
+    A[i] = xr ? make_float2(xr[g], 0.f) : xc[g];
+  }
+  twiddles_half(tw, W, sign);
+  __syncthreads();
+  const float2* res = stockham(A, Bf, tw, lg, nr, W);
+  for (int i = threadIdx.x; i < nr * W; i += blockDim.x) {
+    const int64_t g = r0 * W + i;
+    const float2 v = res[i];
+    if (out_r) out_r[g] = v.x * scale;
+    else out[g] = make_float2(v.x * scale, v.y * scale);
+  }
+}
+
+constexpr int kColTile = 16;
+
+// a kColTile-column tile of one plane [H = 2^lg][W]: column transforms in LDS (leading dim H + 1). `trg` non-null:
+// inverse pass of the band mix — inside the band the loaded F is rescaled to amplitude trg[c] (F = 0: trg + 0i).
+// `amp_out` non-null: |F| of the result as well.
+__global__ __launch_bounds__(256) void fft_cols_kernel(const float2* __restrict__ in, float2* __restrict__ out,
+                                                       float* __restrict__ amp_out, const float* __restrict__ amp_in,
+                                                       const float* __restrict__ trg, int C, int band, int lg, int W,
+                                                       float sign) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int H = 1 << lg, ld = H + 1;
+  const int tc = min(kColTile, W);
+  float2* tw = reinterpret_cast<float2*>(smem);
+  float2* A = tw + kMaxN / 2;
+  float2* Bf = A + tc * ld;
+  const int64_t plane = blockIdx.y;
+  const int c0 = blockIdx.x * tc;
+  const int64_t base = plane * (int64_t)H * W;
+  const float* tp = trg ? trg + (int64_t)(plane % C) * H * W : nullptr;
+  for (int i = threadIdx.x; i < tc * H; i += blockDim.x) {
+    const int h = i / tc, cc = i - h * tc;
+    const int64_t g = base + (int64_t)h * W + c0 + cc;
+    float2 v = in[g];
+    if (tp) {
+      const int u = h, vv = c0 + cc;
+      if (min(u, H - u) <= band && min(vv, W - vv) <= band) {
+        const float a = amp_in[g], A_ = tp[(int64_t)h * W + c0 + cc];
+        v = a > 0.f ? make_float2(v.x * (A_ / a), v.y * (A_ / a)) : make_float2(A_, 0.f);
+      }
+    }
+    A[cc * ld + h] = v;
+  }
+  twiddles_half(tw, H, sign);
+  __syncthreads();
+  const float2* res = stockham(A, Bf, tw, lg, tc, ld);
+  for (int i = threadIdx.x; i < tc * H; i += blockDim.x) {
+    const int h = i / tc, cc = i - h * tc;
+    const int64_t g = base + (int64_t)h * W + c0 + cc;
+    const float2 v = res[cc * ld + h];
+    out[g] = v;
+    if (amp_out) amp_out[g] = sqrtf(v.x * v.x + v.y * v.y);
+  }
+}
 }  // namespace spec
 
 // x [B][C][H][W] fp32 → F [B][C][H][W] complex (float2), amp = |F|. H, W ≤ 64.
@@ -168,7 +284,7 @@ FA_EXPORT int fa_spec_amp_update(const float* amp, float* running, int B, int C,
                                  hipStream_t stream) {
   if (mode == 0) return 0;
   hipLaunchKernelGGL(spec::spec_amp_update_kernel, dim3(fa_grid((int64_t)C * HW, 256, 1024)), dim3(256), 0, stream,
-                     amp, running, B, C, HW, momentum, mode);
+                     amp, running, B, C, HW, momentum, mode, nullptr);
   return (int)hipGetLastError();
 }
 
@@ -181,5 +297,65 @@ FA_EXPORT int fa_spec_mix_ifft2(const void* F, const float* amp, const float* tr
                             (int)smem);
   hipLaunchKernelGGL(spec::spec_mix_ifft2_kernel, dim3((unsigned)planes), dim3(256), smem, stream,
                      reinterpret_cast<const float2*>(F), amp, trg, out, C, H, W, band);
+  return (int)hipGetLastError();
+}
+
+static int spec_lg(int n) {
+  int lg = 0;
+  while ((1 << lg) < n) ++lg;
+  return (1 << lg) == n && n >= 2 && n <= spec::kMaxN ? lg : -1;
+}
+
+static int spec_rows(const float* xr, const float2* xc, float2* out, float* out_r, int64_t rows, int W, float sign,
+                     float scale, hipStream_t stream) {
+  const int lg = spec_lg(W);
+  if (lg < 0) return -2;
+  const int R = max(1, 2048 / W);
+  const size_t smem = (size_t)(spec::kMaxN / 2 + 2 * R * W) * sizeof(float2);
+  if (smem > 64 * 1024)
+    (void)hipFuncSetAttribute((const void*)spec::fft_rows_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  hipLaunchKernelGGL(spec::fft_rows_kernel, dim3((unsigned)((rows + R - 1) / R)), dim3(256), smem, stream, xr, xc, out,
+                     out_r, rows, lg, R, sign, scale);
+  return (int)hipGetLastError();
+}
+
+static int spec_cols(const float2* in, float2* out, float* amp_out, const float* amp_in, const float* trg, int C,
+                     int band, int64_t planes, int H, int W, float sign, hipStream_t stream) {
+  const int lg = spec_lg(H);
+  if (lg < 0 || spec_lg(W) < 0) return -2;
+  const int tc = min(spec::kColTile, W);
+  const size_t smem = (size_t)(spec::kMaxN / 2 + 2 * tc * (H + 1)) * sizeof(float2);
+  if (smem > 160 * 1024) return -5;
+  (void)hipFuncSetAttribute((const void*)spec::fft_cols_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  hipLaunchKernelGGL(spec::fft_cols_kernel, dim3((unsigned)(W / tc), (unsigned)planes), dim3(256), smem, stream, in,
+                     out, amp_out, amp_in, trg, C, band, lg, W, sign);
+  return (int)hipGetLastError();
+}
+
+// Power-of-two planes (2..512 per side): x [planes][H][W] fp32 → F complex + |F|; `tmp` complex scratch of the
+// same size (the row pass's output).
+FA_EXPORT int fa_spec_fft2_pow2(const float* x, void* F, float* amp, void* tmp, int64_t planes, int H, int W,
+                                hipStream_t stream) {
+  int rc = spec_rows(x, nullptr, reinterpret_cast<float2*>(tmp), nullptr, planes * H, W, -1.f, 1.f, stream);
+  if (rc) return rc;
+  return spec_cols(reinterpret_cast<const float2*>(tmp), reinterpret_cast<float2*>(F), amp, nullptr, nullptr, 1, 0,
+                   planes, H, W, -1.f, stream);
+}
+
+// out = Re ifft2(F with amplitude ← trg inside the band), power-of-two planes; tmp: complex scratch
+FA_EXPORT int fa_spec_mix_ifft2_pow2(const void* F, const float* amp, const float* trg, float* out, void* tmp,
+                                     int64_t planes, int C, int H, int W, int band, hipStream_t stream) {
+  int rc = spec_cols(reinterpret_cast<const float2*>(F), reinterpret_cast<float2*>(tmp), nullptr, amp, trg, C, band,
+                     planes, H, W, 1.f, stream);
+  if (rc) return rc;
+  return spec_rows(nullptr, reinterpret_cast<const float2*>(tmp), nullptr, out, planes * H, W, 1.f,
+                   1.f / ((float)H * (float)W), stream);
+}
+
+// mode 3: EMA, or replace when Σ running == 0 (`flag` = that test, evaluated on the device: no host sync)
+FA_EXPORT int fa_spec_amp_update_auto(const float* amp, float* running, const unsigned char* first, int B, int C,
+                                      int HW, float momentum, hipStream_t stream) {
+  hipLaunchKernelGGL(spec::spec_amp_update_kernel, dim3(fa_grid((int64_t)C * HW, 256, 1024)), dim3(256), 0, stream,
+                     amp, running, B, C, HW, momentum, 1, first);
   return (int)hipGetLastError();
 }

@@ -2,7 +2,9 @@
 `hs_fedavg/hs_fft.py:8-84`, numpy per image on the CPU).
 
 Batched on device. On the GPU the whole transform is the hand-written K12 kernels
-(``csrc/spectral_kernels.hip``): a per-plane LDS 2-D DFT that also writes |F|, the batch-mean amplitude
+(``csrc/spectral_kernels.hip``): a radix-2 Stockham FFT in LDS (row pass + column pass) for power-of-two planes
+up to 512 × 512 — the reference's 3 × 512 × 512 amplitude —, a per-plane LDS 2-D DFT for other sizes ≤ 64; the
+forward pass also writes |F|, the batch-mean amplitude
 + running-amplitude EMA in fixed order (deterministic), and the band mix + inverse DFT — three launches per
 batch. On the CPU (and as the GPU tests' oracle) the same op runs on ``torch.fft``. The band mask (the centred
 ``(2b+1)²`` low-frequency box, ``b = ⌊min(H,W)·L⌋``) is applied in unshifted coordinates (no fftshift round
@@ -11,6 +13,7 @@ trips). For the reference default ``L = 0`` only the DC term changes, which has 
 """
 import ctypes
 import math
+import os
 
 import torch
 
@@ -30,22 +33,43 @@ def extract_amp(x: torch.Tensor) -> torch.Tensor:
     return torch.fft.fft2(x.float(), dim=(-2, -1)).abs()
 
 
+def _pow2(n):
+    return 2 <= n <= 512 and n & (n - 1) == 0
+
+
+def _fft_path(H, W) -> bool:
+    """Power-of-two planes above 64 px (and any power-of-two size under FEDML_AMD_SPEC_FFT=1): the radix-2
+    Stockham FFT kernels; otherwise the LDS DFT (any size ≤ 64)."""
+    if not (_pow2(H) and _pow2(W)):
+        return False
+    return max(H, W) > 64 or os.environ.get("FEDML_AMD_SPEC_FFT", "0") == "1"
+
+
 def _native_ok(x):
-    return fl_ops.use_native(x) and x.shape[-1] <= 64 and x.shape[-2] <= 64
+    H, W = x.shape[-2], x.shape[-1]
+    return fl_ops.use_native(x) and ((H <= 64 and W <= 64) or _fft_path(H, W))
 
 
-def _native_amp(xf, running_amp, momentum, fix_amp, init):
-    """(F, |F|) of every plane and the running amplitude updated in place (K12 kernels)."""
+def _native_amp(xf, running_amp, momentum, fix_amp):
+    """(F, |F|) of every plane and the running amplitude updated in place (K12 kernels). The reference's
+    first-call test (``np.sum(running_amp) == 0`` → replace instead of EMA) is evaluated on the device."""
     B, C, H, W = xf.shape
     F = torch.empty(B, C, H, W, 2, device=xf.device)
     amp = torch.empty(B, C, H, W, device=xf.device)
     s = fl_ops._stream(xf)
-    fl_ops._check(fl_ops._fn("fa_spec_fft2")(fl_ops._p(xf), fl_ops._p(F), fl_ops._p(amp), fl_ops._i64(B * C),
-                                             ctypes.c_int(H), ctypes.c_int(W), s), "fa_spec_fft2")
-    mode = 0 if fix_amp else (2 if init else 1)
-    fl_ops._check(fl_ops._fn("fa_spec_amp_update")(fl_ops._p(amp), fl_ops._p(running_amp), ctypes.c_int(B),
-                                                   ctypes.c_int(C), ctypes.c_int(H * W), fl_ops._f(momentum),
-                                                   ctypes.c_int(mode), s), "fa_spec_amp_update")
+    if _fft_path(H, W):
+        tmp = torch.empty_like(F)
+        fl_ops._check(fl_ops._fn("fa_spec_fft2_pow2")(fl_ops._p(xf), fl_ops._p(F), fl_ops._p(amp), fl_ops._p(tmp),
+                                                      fl_ops._i64(B * C), ctypes.c_int(H), ctypes.c_int(W), s),
+                      "fa_spec_fft2_pow2")
+    else:
+        fl_ops._check(fl_ops._fn("fa_spec_fft2")(fl_ops._p(xf), fl_ops._p(F), fl_ops._p(amp), fl_ops._i64(B * C),
+                                                 ctypes.c_int(H), ctypes.c_int(W), s), "fa_spec_fft2")
+    if not fix_amp:
+        first = (running_amp.sum() == 0).to(torch.uint8)
+        fl_ops._check(fl_ops._fn("fa_spec_amp_update_auto")(fl_ops._p(amp), fl_ops._p(running_amp), fl_ops._p(first),
+                                                            ctypes.c_int(B), ctypes.c_int(C), ctypes.c_int(H * W),
+                                                            fl_ops._f(momentum), s), "fa_spec_amp_update_auto")
     return F, amp
 
 
@@ -60,8 +84,7 @@ def amplitude_normalize(x: torch.Tensor, running_amp: torch.Tensor = None, momen
     running_amp = running_amp.to(device=x.device, dtype=torch.float32)
     if _native_ok(xf) and running_amp.shape == (C, H, W):
         running_amp = running_amp.clone().contiguous()
-        init = not fix_amp and float(running_amp.abs().sum()) == 0.0
-        F, amp = _native_amp(xf, running_amp, momentum, fix_amp, init)
+        F, amp = _native_amp(xf, running_amp, momentum, fix_amp)
         if L == 0.0:
             s = xf.sum(dim=(-2, -1), keepdim=True)
             sign = torch.where(s < 0, -1.0, 1.0)
@@ -69,10 +92,17 @@ def amplitude_normalize(x: torch.Tensor, running_amp: torch.Tensor = None, momen
         else:
             out = torch.empty_like(xf)
             b = int(math.floor(min(H, W) * L))
-            fl_ops._check(fl_ops._fn("fa_spec_mix_ifft2")(fl_ops._p(F), fl_ops._p(amp), fl_ops._p(running_amp),
-                                                          fl_ops._p(out), fl_ops._i64(B * C), ctypes.c_int(C),
-                                                          ctypes.c_int(H), ctypes.c_int(W), ctypes.c_int(b),
-                                                          fl_ops._stream(xf)), "fa_spec_mix_ifft2")
+            if _fft_path(H, W):
+                tmp = torch.empty_like(F)
+                fl_ops._check(fl_ops._fn("fa_spec_mix_ifft2_pow2")(
+                    fl_ops._p(F), fl_ops._p(amp), fl_ops._p(running_amp), fl_ops._p(out), fl_ops._p(tmp),
+                    fl_ops._i64(B * C), ctypes.c_int(C), ctypes.c_int(H), ctypes.c_int(W), ctypes.c_int(b),
+                    fl_ops._stream(xf)), "fa_spec_mix_ifft2_pow2")
+            else:
+                fl_ops._check(fl_ops._fn("fa_spec_mix_ifft2")(fl_ops._p(F), fl_ops._p(amp), fl_ops._p(running_amp),
+                                                              fl_ops._p(out), fl_ops._i64(B * C), ctypes.c_int(C),
+                                                              ctypes.c_int(H), ctypes.c_int(W), ctypes.c_int(b),
+                                                              fl_ops._stream(xf)), "fa_spec_mix_ifft2")
         return out.to(x.dtype), running_amp
     F = torch.fft.fft2(xf, dim=(-2, -1))
     if not fix_amp:

@@ -178,6 +178,17 @@ class BatchedInterpreter:
         for n in self.gm.graph.nodes:
             if n.op == "call_function" and n.target in (torch.cat, torch.stack):
                 raise UnsupportedForBatching("channel concatenation is not client-stackable")
+        # BN → ReLU pairs (the BN output feeds only the ReLU): the native plane BN applies the ReLU in its own
+        # pass and the ReLU node becomes an identity (ops/plane_ops.py)
+        self.bn_relu = {}
+        for n in self.gm.graph.nodes:
+            if n.op == "call_module" and isinstance(self.modules[n.target], nn.BatchNorm2d) and len(n.users) == 1:
+                u = next(iter(n.users))
+                is_relu = (u.op == "call_module" and isinstance(self.modules[u.target], nn.ReLU)) or \
+                    (u.op == "call_function" and u.target in (F.relu, torch.relu)) or \
+                    (u.op == "call_method" and u.target == "relu")
+                if is_relu and len(u.args) >= 1 and u.args[0] is n:
+                    self.bn_relu[n.name] = u.name
 
     def flush_deferred(self):
         for upd in self.deferred:
@@ -200,9 +211,13 @@ class BatchedInterpreter:
         if dtype is not None and h.is_floating_point():
             h = h.to(dtype)
         env = {}
+        fused_relu = set()      # ReLU nodes already applied by the preceding native plane BN
         for node in self.gm.graph.nodes:
             if node.op == "placeholder":
                 env[node.name] = h
+                continue
+            if node.name in fused_relu:
+                env[node.name] = env[node.args[0].name]
                 continue
             if node.op == "output":
                 out = env[node.args[0].name] if isinstance(node.args[0], fx.Node) else node.args[0]
@@ -215,8 +230,14 @@ class BatchedInterpreter:
             args = fx.node.map_arg(node.args, lambda n: env[n.name])
             kwargs = fx.node.map_arg(node.kwargs, lambda n: env[n.name])
             if node.op == "call_module":
-                env[node.name] = self._call_module(node.target, self.modules[node.target], args, params, training,
-                                                   sample_mask, active)
+                relu_next = self.bn_relu.get(node.name)
+                out = self._call_module(node.target, self.modules[node.target], args, params, training,
+                                        sample_mask, active, fuse_relu=relu_next is not None)
+                if isinstance(out, tuple):      # (y, relu applied)
+                    out, applied = out
+                    if applied:
+                        fused_relu.add(relu_next)
+                env[node.name] = out
             elif node.op == "call_function":
                 env[node.name] = self._call_function(node.target, args, kwargs)
             elif node.op == "call_method":
@@ -226,16 +247,18 @@ class BatchedInterpreter:
         raise RuntimeError("graph has no output")
 
     # ---- node handlers ---------------------------------------------------------------------------
-    def _call_module(self, name, m, args, params, training, sample_mask, active):
+    def _call_module(self, name, m, args, params, training, sample_mask, active, fuse_relu=False):
         x = args[0]
         C = self.C
         if isinstance(m, nn.Conv2d):
             w = params[f"{name}.weight"]
             b = params.get(f"{name}.bias")
             if _NATIVE_BCONV and x.is_cuda:   # hand-written implicit GEMM (ops/bconv_ops.py) when it applies
-                from ..ops import bconv_ops
+                from ..ops import bconv_ops, plane_ops
                 if bconv_ops.supported(m, x, w):
                     return bconv_ops.bconv2d_native(x, w, b, C, m.stride, m.padding)
+                if b is None and plane_ops.supported_dw(m, x, w):     # depthwise: plane kernels, no MIOpen
+                    return plane_ops.depthwise_conv2d(x, w, C, m.stride[0])
             if w.dtype != x.dtype:
                 w = w.to(x.dtype)
                 b = b.to(x.dtype) if b is not None else None
@@ -248,6 +271,15 @@ class BatchedInterpreter:
             b = params.get(f"{name}.bias")
             use_batch = training or not m.track_running_stats
             mom = m.momentum if m.momentum is not None else 0.1
+            if _NATIVE_BCONV and use_batch and sample_mask is None and m.momentum is not None:
+                from ..ops import plane_ops
+                if plane_ops.plane_supported(x, w, C) and (w is None) == (b is None):
+                    # per-(client, channel) statistics + affine (+ the next ReLU) on the plane kernels
+                    y, (mean, var_b, n) = plane_ops.plane_batch_norm(x, w, b, C, m.eps, relu=fuse_relu)
+                    if rm is not None and training:
+                        self.deferred.append((rm, rv, nbt, mean, var_b,
+                                              torch.full((C, 1), n, device=x.device), mom, active))
+                    return y, fuse_relu
             return bbatch_norm(x, C, w, b, rm, rv, use_batch, mom, m.eps, sample_mask, active, nbt,
                                deferred=self.deferred if training else None)
         if isinstance(m, nn.GroupNorm):

@@ -84,6 +84,17 @@ def _is_wide_convnet(model: torch.nn.Module, min_channels: int = 128) -> bool:
     return total > 0 and wide >= 0.5 * total
 
 
+def _native_depthwise_net(model: torch.nn.Module) -> bool:
+    """A depthwise-separable conv net (MobileNet family) whose every convolution the native client-batched
+    kernels take (plane depthwise kernels, implicit-GEMM groups-1 convolutions): the batched program then runs
+    without MIOpen, instead of one client after another."""
+    from ...ops import bconv_ops, plane_ops
+    from ...parallel import batched_nn
+    convs = [m for m in model.modules() if isinstance(m, torch.nn.Conv2d)]
+    return (batched_nn._NATIVE_BCONV and any(plane_ops.depthwise_module(m) for m in convs)
+            and all(plane_ops.depthwise_module(m) or bconv_ops.supported_module(m) for m in convs))
+
+
 class ClientBatchEngine:
     def __init__(self, model: torch.nn.Module, C: int, device, args, compute_dtype: Optional[torch.dtype] = None):
         self.C = int(C)
@@ -212,7 +223,8 @@ class ClientBatchEngine:
         self._seq_capture = (self.device.type == "cuda" and _is_wide_convnet(model)
                              and not any(isinstance(m, torch.nn.RNNBase) for m in model.modules()))
         if not self.sequential and self.native_step is None and self.tf is None and (
-                mode == "sequential" or (mode == "auto" and self.device.type == "cuda" and _is_wide_convnet(model))):
+                mode == "sequential" or (mode == "auto" and self.device.type == "cuda" and _is_wide_convnet(model)
+                                         and not _native_depthwise_net(model))):
             logging.info("virtual-client engine: per-client sequential execution (wide conv net)")
             self.sequential = True
             # MIOpen picks convolution solutions by heuristics unless a find-db entry exists; on a fresh
@@ -282,6 +294,12 @@ class ClientBatchEngine:
         for ep in range(int(epochs)):
             order = store.epoch_order(slots, n_max, generator, shuffle,
                                       key=None if rng_key is None else rng_key * 1009 + ep)
+            # deterministic mode on the native step: every step runs the full batch geometry (the ragged tail
+            # is padding rows, skipped by the kernels via nimg) — a client's kernel work split then does not
+            # depend on the OTHER clients packed with it (their remainders set the tail's padded size)
+            fixed_geom = self.deterministic and self.native_step is not None
+            if fixed_geom and order.shape[1] < steps_per_epoch * batch_size:
+                order = torch.cat([order, order.new_full((C, steps_per_epoch * batch_size - order.shape[1]), -1)], 1)
             for s in range(steps_per_epoch):
                 lo = s * batch_size
                 b_c = [max(0, min(batch_size, n - lo)) for n in counts_h]
@@ -293,7 +311,7 @@ class ClientBatchEngine:
                 # than C, exhausted partitions) are masked by ``active`` and zero row scales, so they do
                 # not break uniformity: the fast native / graph-captured paths stay in use
                 uniform = all(b == bmax for b in b_c if b > 0)
-                idx = order[:, lo:lo + bmax]
+                idx = order[:, lo:lo + (batch_size if fixed_geom else bmax)]
                 x, y, mask = store.gather(idx)
                 if self.augment and x.dim() == 5:
                     self._aug_calls += 1

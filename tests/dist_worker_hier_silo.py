@@ -38,4 +38,4 @@ if __name__ == "__main__":
     mp_harness.install_stack_dump()
     a = sys.argv
     main(a[1], int(a[2]), int(a[3]), int(a[4]), a[5], int(a[6]), int(a[7]), a[8], *(a[9:11]),
-         *([int(a[11])] if len(a) > 11 else []))
+         *[int(v) for v in a[11:13]])

@@ -25,7 +25,11 @@ def test_fc_head_xent_matches_fp64(C, N, F, K):
     labels[-1, N // 2:] = -1
     dpool = torch.empty(C, N, F, device=DEV)
     loss_c = torch.empty(C, device=DEV)
-    assert nn_ops.fc_head_xent(pooled, arena, ow, ob, labels, rs, garena, dpool, loss_c, C, N, F, K)
+    fits = (N * (F + 4) + N * K) * 4 <= 160 * 1024
+    assert nn_ops.fc_head_xent(pooled, arena, ow, ob, labels, rs, garena, dpool, loss_c, C, N, F, K) == fits
+    if not fits:      # too large for one workgroup's LDS: the caller keeps the library path, nothing written
+        assert torch.equal(garena, g0)
+        return
     torch.cuda.synchronize()
     for c in range(C):
         W = arena[c, ow:ow + K * F].view(K, F).double().requires_grad_(True)

@@ -29,3 +29,54 @@ def test_native_fft_kernel_is_the_path_taken():
     from fedml_amd.ops import _native
     assert spectral._native_ok(torch.zeros(1, 1, 32, 32, device="cuda"))
     assert _native.lib(required=True).fa_spec_fft2 is not None
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,L,force", [((2, 3, 512, 512), 0.0, False), ((2, 3, 512, 512), 0.01, False),
+                                            ((3, 2, 128, 64), 0.1, False), ((4, 3, 32, 32), 0.25, True),
+                                            ((2, 1, 8, 16), 0.25, True)])
+def test_stockham_fft_path_matches_torch_fft(shape, L, force, monkeypatch):
+    """The radix-2 Stockham FFT kernels (power-of-two planes up to the reference's 3 × 512 × 512) against
+    torch.fft: the running amplitude (first call replaces, then EMA — decided on the device) and the mixed
+    images (band mix + inverse FFT for L > 0, the closed-form DC update for L = 0)."""
+    if force:
+        monkeypatch.setenv("FEDML_AMD_SPEC_FFT", "1")
+    assert spectral._fft_path(shape[-2], shape[-1])
+    torch.manual_seed(0)
+    run_d, run_c = None, None
+    for call in range(2):
+        x = torch.rand(*shape) * 2 - 0.5
+        out_c, run_c = spectral.amplitude_normalize(x, run_c, 0.1, False, L)
+        out_d, run_d = spectral.amplitude_normalize(x.cuda(), run_d, 0.1, False, L)
+        torch.cuda.synchronize()
+        e_amp = float((run_d.cpu() - run_c).norm() / run_c.norm())
+        e_out = float((out_d.cpu() - out_c).norm() / out_c.norm())
+        assert e_amp < 1e-5 and e_out < 1e-5, (call, e_amp, e_out)
+
+
+@pytest.mark.gpu
+def test_stockham_fft_timing_512(capsys):
+    """Throughput line for the reference's working size (32 images × 3 × 512 × 512, L = 0.01): the forward
+    FFT + amplitude EMA + band mix + inverse FFT, against torch.fft (rocFFT) on the same device."""
+    x = torch.rand(32, 3, 512, 512, device="cuda")
+    run = None
+    for _ in range(2):
+        _, run = spectral.amplitude_normalize(x, run, 0.1, False, 0.01)
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+    ev[0].record()
+    for _ in range(5):
+        _, run = spectral.amplitude_normalize(x, run, 0.1, False, 0.01)
+    ev[1].record()
+    mask = spectral._band_mask(512, 512, 0.01, "cuda")
+    ev[2].record()
+    for _ in range(5):
+        F = torch.fft.fft2(x)
+        amp = torch.where(mask, run[None], F.abs())
+        torch.fft.ifft2(torch.polar(amp, F.angle())).real
+    ev[3].record()
+    torch.cuda.synchronize()
+    ms_nat, ms_t = ev[0].elapsed_time(ev[1]) / 5, ev[2].elapsed_time(ev[3]) / 5
+    with capsys.disabled():
+        print(f"\n[K12 512x512] native {ms_nat:.2f} ms/batch, torch.fft {ms_t:.2f} ms/batch (32x3 planes)")
+    assert ms_nat > 0
