@@ -12,6 +12,7 @@
 // with fp32 atomics — no scratch / scatter pass.
 #include "prec.h"
 #include "detacc.h"
+#include "bnlazy.h"
 
 FA_DET_EXPORT(conv1x1)
 
@@ -32,7 +33,7 @@ __global__ __launch_bounds__(256) void conv1x1_wgrad_kernel(const typename P::T*
                                                             const float* __restrict__ ps, const float* __restrict__ pt,
                                                             float* __restrict__ garena, int64_t ldw, int64_t woff,
                                                             int M, int pix_per_wg, const int* __restrict__ nimg,
-                                                            int hw) {
+                                                            int hw, const BnLazy* __restrict__ lz) {
   using T = typename P::T;
   using frag_t = typename P::frag_t;
   constexpr int V = P::VEC;
@@ -54,9 +55,13 @@ __global__ __launch_bounds__(256) void conv1x1_wgrad_kernel(const typename P::T*
   const bool raw = yv == nullptr;   // dy = g as stored (e.g. Gᵀ·act(x) of a recomputed-y bottleneck)
   if (!raw)
     for (int i = threadIdx.x; i < COUT; i += 256) {
-      vv[i] = alpha[(int64_t)c * COUT + i];
-      vv[COUT + i] = beta[(int64_t)c * COUT + i];
-      vv[2 * COUT + i] = gamma[(int64_t)c * COUT + i];
+      if (lz) {
+        bn_lazy_bwd(lz, c, i, blockIdx.x == 0, vv[i], vv[COUT + i], vv[2 * COUT + i]);
+      } else {
+        vv[i] = alpha[(int64_t)c * COUT + i];
+        vv[COUT + i] = beta[(int64_t)c * COUT + i];
+        vv[2 * COUT + i] = gamma[(int64_t)c * COUT + i];
+      }
     }
   if (PRO)
     for (int i = threadIdx.x; i < CIN; i += 256) {
@@ -216,7 +221,7 @@ static int launch(const void* g_, const void* yv_, const float* al, const float*
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   const int gx = (M + pix_per_wg - 1) / pix_per_wg;
   hipLaunchKernelGGL(kern, dim3(gx, C), dim3(256), smem, stream, g, yv, al, be, ga, x, ps, pt, garena, ldw, woff, M,
-                     pix_per_wg, nimg, hw);
+                     pix_per_wg, nimg, hw, fa_take_lazy(0));
   return (int)hipGetLastError();
 }
 
@@ -310,6 +315,7 @@ struct Args {             // activations are P::T (bf16 | fp32)
   const int* nimg;        // per-client valid images (null: all) and pixels per image
   int hw;
   const float* pivot;     // RY: [C][CO] shift K of the conv's forward output (y − K is what α, β, γ assume)
+  const BnLazy* lz;       // deferred backward finalisation of this conv's BN (α, β, γ; bnlazy.h) or null
 };
 
 enum { EPI_MASK = 2, EPI_BLOCK = 3 };
@@ -363,9 +369,13 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
   T* xL = dyL + PT * LDD;                                                // [PT][LDX]  act(e_x)
 
   for (int i = threadIdx.x; i < CO; i += NT) {
-    vv[i] = a.alpha[(int64_t)c * CO + i];
-    vv[CO + i] = a.beta[(int64_t)c * CO + i];
-    vv[2 * CO + i] = a.gamma[(int64_t)c * CO + i];
+    if (a.lz) {
+      bn_lazy_bwd(a.lz, c, i, blockIdx.x == 0, vv[i], vv[CO + i], vv[2 * CO + i]);
+    } else {
+      vv[i] = a.alpha[(int64_t)c * CO + i];
+      vv[CO + i] = a.beta[(int64_t)c * CO + i];
+      vv[2 * CO + i] = a.gamma[(int64_t)c * CO + i];
+    }
   }
   if (PRO)
     for (int i = threadIdx.x; i < CI; i += NT) {
@@ -743,7 +753,7 @@ static int bwd_fused(const void* g, const void* y, const float* alpha, const flo
   // y == null: recompute y from the staged input (EPI_MASK, fp32 storage only)
   if (!y && (epi != EPI_MASK || !P::kF32)) return -4;
   Args a{g, y, alpha, beta, gamma, wb, wb_ld, e_x, e_s, e_t, e_add, e_y1, e_y2, out, stats, NS, garena, ldw,
-         woff, M, pix_per_wg, part, nimg, hw, pivot};
+         woff, M, pix_per_wg, part, nimg, hw, pivot, fa_take_lazy(0)};
 #define C1F(CI, CO, E, WM, WN, PT, NW)                                              \
   if (Cin == CI && Cout == CO && epi == E) {                                       \
     if constexpr (E == EPI_MASK && P::kF32)                                        \

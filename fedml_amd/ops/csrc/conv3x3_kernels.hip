@@ -21,6 +21,7 @@
 // reference-precision path (exact fp32 MFMA products, fp32 activations).
 #include "prec.h"
 #include "detacc.h"
+#include "bnlazy.h"
 #include <algorithm>
 
 #include <cstdlib>
@@ -245,6 +246,7 @@ struct Args {              // tensors are P::T (bf16 | fp32) unless noted
   int R, S, units, units_per_wg;  // stage geometry (see unit_geom) and work split
   int nout_total;                 // output channels of the layer (a workgroup computes NOUT of them)
   FastDiv fd_trtw, fd_tw, fd_rw, fd_w;  // ÷ TR·TW, ÷ TW (tile), ÷ R·W, ÷ W (output unit)
+  const BnLazy* lz0;              // XF_BNRELU: deferred finalisation of the prologue BN (bnlazy.h) or null
 };
 
 // MTW 16-pixel tiles per wave share every B fragment read.
@@ -299,8 +301,12 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
     for (int i = threadIdx.x; i < n16; i += 256) d[i] = s[i];
     if (XF != XF_NONE)
       for (int i = threadIdx.x; i < KC; i += 256) {
-        v0[i] = a.vec0[(int64_t)c * KC + i];
-        v1[i] = a.vec1[(int64_t)c * KC + i];
+        if (XF == XF_BNRELU && a.lz0) {
+          bn_lazy_fwd(a.lz0, c, i, blockIdx.x == 0 && blockIdx.z == 0, v0[i], v1[i]);
+        } else {
+          v0[i] = a.vec0[(int64_t)c * KC + i];
+          v1[i] = a.vec1[(int64_t)c * KC + i];
+        }
         if (XF == XF_DY) v2[i] = a.vec2[(int64_t)c * KC + i];
       }
     if (EPI == EPI_MASK)
@@ -495,6 +501,7 @@ struct WArgs {           // activations are P::T
   const float* pt;
   float* dw;              // GEMM-layout scratch [C][COUT][9·CIN]
   const int* nimg;        // per-client valid images (null: all N)
+  const BnLazy* lz0;      // deferred backward finalisation of the BN whose α/β/γ this kernel reads (or null)
   int N, H, W;            // dy (output) geometry
   int Hs, Ws;             // x (input) geometry
   int R, S, units, units_per_wg;
@@ -532,9 +539,13 @@ __global__ __launch_bounds__(256, (MAXC <= 8 ? C3W_MIN_WAVES : 1)) void conv3x3_
   T* xt = dyL + (size_t)a.S * a.R * W * LDD;                           // [S][TR][TW][LDX]
 
   for (int i = threadIdx.x; i < COUT; i += 256) {
-    vv[i] = a.alpha[(int64_t)c * COUT + i];
-    vv[COUT + i] = a.beta[(int64_t)c * COUT + i];
-    vv[2 * COUT + i] = a.gamma[(int64_t)c * COUT + i];
+    if (a.lz0) {
+      bn_lazy_bwd(a.lz0, c, i, blockIdx.x == 0 && blockIdx.z == 0, vv[i], vv[COUT + i], vv[2 * COUT + i]);
+    } else {
+      vv[i] = a.alpha[(int64_t)c * COUT + i];
+      vv[COUT + i] = a.beta[(int64_t)c * COUT + i];
+      vv[2 * COUT + i] = a.gamma[(int64_t)c * COUT + i];
+    }
   }
   if (PRO)
     for (int i = threadIdx.x; i < CIN; i += 256) {
@@ -818,7 +829,7 @@ static int conv3x3_fwd(const void* x, const void* wpk, int64_t wpk_ld, const flo
   if ((stride != 1 && stride != 2) || H % stride || W % stride || (W / stride) % 8 != 0) return -3;
   Args a = {};
   a.src = x; a.wpk = wpk; a.wpk_ld = wpk_ld; a.vec0 = pscale; a.vec1 = pshift; a.out = y; a.stats = stats; a.NS = 2;
-  a.pivot = pivot; a.nimg = nimg;
+  a.pivot = pivot; a.nimg = nimg; a.lz0 = fa_take_lazy(0);
   a.N = N; a.H = H / stride; a.W = W / stride; a.Hs = H; a.Ws = W; a.ldk = ldk;
   if (stride == 2) {
     if (pscale) return dispatch_gemm<P, XF_BNRELU, 0, EPI_FWD, 2>(Cin, Cout, a, C, stream);
@@ -851,6 +862,7 @@ static int conv3x3_wgrad(const void* g, const void* yv, const float* alpha, cons
   if (Wo % 8 != 0 || (Ho * Wo) % 32 != 0) return -3;
   WArgs a = {};
   a.g = g; a.yv = yv; a.alpha = alpha; a.beta = beta; a.gamma = gamma; a.x = x; a.ps = ps; a.pt = pt; a.dw = dw;
+  a.lz0 = fa_take_lazy(0);
   a.nimg = nimg;
   a.N = N; a.H = Ho; a.W = Wo; a.Hs = H; a.Ws = W;
   // units sized so one unit's operands fit the loaders' register budget (x tile ≤ 8, dy ≤ 4 chunks/thread)

@@ -22,6 +22,7 @@
 // D: col = l&15, row = 4(l>>4) + i.
 #include "prec.h"
 #include "detacc.h"
+#include "bnlazy.h"
 
 FA_DET_EXPORT(conv)
 
@@ -236,6 +237,8 @@ struct ConvArgs {        // activations / packed weights are P::T (bf16 | fp32)
   int Kp;                // K rounded to 32
   int tiles_per_wave;
   int nout_total;        // output channels of the layer; a workgroup computes NOUT of them (blockIdx.z)
+  const BnLazy* lz0;     // PRO: deferred finalisation of the prologue BN (vec0/vec1; bnlazy.h) or null
+  const BnLazy* lz1;     // PRO_BOUT: ... of the shortcut BN (vec2/vec3)
 };
 
 template <class P, int NT, int AOP, int PRO, int MODE, int EPI>
@@ -276,10 +279,18 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
     for (int i = threadIdx.x; i < n16; i += 256) dst[i] = src[i];
     if (AOP == AOP_DY || PRO != PRO_NONE) {
       for (int i = threadIdx.x; i < a.KC; i += 256) {
-        v0[i] = a.vec0[(int64_t)c * a.KC + i];
-        v1[i] = a.vec1[(int64_t)c * a.KC + i];
-        if (AOP == AOP_DY || (PRO == PRO_BOUT && a.vec2)) v2[i] = a.vec2[(int64_t)c * a.KC + i];
-        if (PRO == PRO_BOUT && a.vec2) v3[i] = a.vec3[(int64_t)c * a.KC + i];
+        if (PRO != PRO_NONE && a.lz0) {
+          bn_lazy_fwd(a.lz0, c, i, blockIdx.x == 0 && blockIdx.z == 0, v0[i], v1[i]);
+        } else {
+          v0[i] = a.vec0[(int64_t)c * a.KC + i];
+          v1[i] = a.vec1[(int64_t)c * a.KC + i];
+        }
+        if (PRO == PRO_BOUT && a.vec2 && a.lz1) {
+          bn_lazy_fwd(a.lz1, c, i, blockIdx.x == 0 && blockIdx.z == 0, v2[i], v3[i]);
+        } else {
+          if (AOP == AOP_DY || (PRO == PRO_BOUT && a.vec2)) v2[i] = a.vec2[(int64_t)c * a.KC + i];
+          if (PRO == PRO_BOUT && a.vec2) v3[i] = a.vec3[(int64_t)c * a.KC + i];
+        }
       }
     }
     for (int i = threadIdx.x; i < 4 * NOUT * 3; i += 256) red[i] = 0.f;
@@ -664,8 +675,12 @@ __global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
 
   if (DY || PRO == PRO_BNRELU) {
     for (int i = threadIdx.x; i < a.KC; i += 256) {
-      v0[i] = a.vec0[(int64_t)c * a.KC + i];
-      v1[i] = a.vec1[(int64_t)c * a.KC + i];
+      if (!DY && a.lz0) {
+        bn_lazy_fwd(a.lz0, c, i, bx == 0 && bzz == 0, v0[i], v1[i]);
+      } else {
+        v0[i] = a.vec0[(int64_t)c * a.KC + i];
+        v1[i] = a.vec1[(int64_t)c * a.KC + i];
+      }
       if (DY) v2[i] = a.vec2[(int64_t)c * a.KC + i];
     }
   }
@@ -1038,6 +1053,8 @@ static int conv_fwd(const void* x, const void* wpk, int64_t wpk_ld, const float*
   a.pivot = pivot; a.nimg = nimg;
   a.Nb = Nb; a.Hs = H; a.Ws = W; a.KC = Cin; a.Ho = Ho; a.Wo = Wo; a.KH = KH; a.KW = KW; a.stride = stride;
   a.pad = pad; a.ldk = ldk; a.Kp = (KH * KW * Cin + 31) / 32 * 32; a.tiles_per_wave = tiles_per_wave;
+  a.lz0 = fa_take_lazy(0);
+  a.lz1 = fa_take_lazy(1);
   if (pscale)
     return dispatch_nt<P, AOP_ACT, PRO_BNRELU, MODE_FWD, EPI_FWD>(Cout, a, C, stream);
   return dispatch_nt<P, AOP_ACT, PRO_NONE, MODE_FWD, EPI_FWD>(Cout, a, C, stream);
@@ -1056,6 +1073,8 @@ static int conv_fwd_pbout(const void* yp, const float* s, const float* t, const 
   a.wpk = wpk; a.wpk_ld = wpk_ld; a.out = y; a.stats = stats; a.NS = 2; a.pivot = pivot; a.nimg = nimg;
   a.Nb = Nb; a.Hs = H; a.Ws = W; a.KC = Cin; a.Ho = H; a.Wo = W; a.KH = 1; a.KW = 1; a.stride = 1;
   a.pad = 0; a.ldk = ldk; a.Kp = (Cin + 31) / 32 * 32; a.tiles_per_wave = tiles_per_wave;
+  a.lz0 = fa_take_lazy(0);
+  a.lz1 = fa_take_lazy(1);
   if (Cout % 64 == 0 && (Cout > 256 || Cin > convk_min_k())) return -5;   // the K-streamed kernel has no PRO_BOUT
   return dispatch_nt<P, AOP_ACT, PRO_BOUT, MODE_FWD, EPI_FWD>(Cout, a, C, stream);
 }

@@ -3,6 +3,7 @@
 // fp32 — a pure function of the integer sum, so the result is the same bits for any arrival order.
 #include "common.h"
 #include "detacc.h"
+#include "bnlazy.h"
 
 __global__ __launch_bounds__(256) void det_flush_kernel(float* __restrict__ dst, unsigned long long* __restrict__ acc,
                                                         int64_t n, const unsigned int* __restrict__ bad) {
@@ -31,6 +32,20 @@ extern "C" int fa_det_flush(float* dst, void* acc, int64_t n, unsigned int* bad,
 }
 
 extern "C" int fa_plan_clients = 0;
+
+// deferred BatchNorm finalisation (bnlazy.h): descriptors for the next consumer launch (slot 0: the vectors the
+// kernel reads as scale/shift or α/β/γ; slot 1: a second BN — the downsample branch of a block-output prologue)
+static const void* g_lazy[2] = {nullptr, nullptr};
+extern "C" int fa_set_lazy(const void* d0, const void* d1) {
+  g_lazy[0] = d0;
+  g_lazy[1] = d1;
+  return 0;
+}
+extern "C" const BnLazy* fa_take_lazy(int slot) {
+  const void* d = g_lazy[slot];
+  g_lazy[slot] = nullptr;
+  return reinterpret_cast<const BnLazy*>(d);
+}
 extern "C" int fa_set_plan_clients(int c) {
   fa_plan_clients = c > 0 ? c : 0;
   return 0;

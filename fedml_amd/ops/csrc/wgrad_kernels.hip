@@ -15,6 +15,7 @@
 // into the client-stacked gradient arena at the OIHW position of each element.
 #include "prec.h"
 #include "detacc.h"
+#include "bnlazy.h"
 
 #include <stdlib.h>
 #include <type_traits>
@@ -37,7 +38,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_tr_kernel(
     const float* __restrict__ beta, const float* __restrict__ gamma, const typename P::T* __restrict__ x,
     const float* __restrict__ ps, const float* __restrict__ pt, float* __restrict__ dw, int Nb, int H, int W,
     int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int pix_per_wg, int nt_per_z,
-    const int* __restrict__ nimg, int co_slice) {
+    const int* __restrict__ nimg, int co_slice, const BnLazy* __restrict__ lz) {
   using T = typename P::T;
   const bool PRO = ps != nullptr;   // runtime flag: halves the instantiations (uniform branch)
   using frag_t = typename P::frag_t;
@@ -71,9 +72,13 @@ __global__ __launch_bounds__(256) void conv_wgrad_tr_kernel(
   float* vv = reinterpret_cast<float*>(aL + PT * lda);  // α β γ [Cs] (this slice), s t [Cin]
 
   for (int i = threadIdx.x; i < Cs; i += 256) {
-    vv[i] = alpha[(int64_t)c * Cout + co_lo + i];
-    vv[Cs + i] = beta[(int64_t)c * Cout + co_lo + i];
-    vv[2 * Cs + i] = gamma[(int64_t)c * Cout + co_lo + i];
+    if (lz) {   // one writer per output-channel slice: the first pixel chunk of its first K-slice
+      bn_lazy_bwd(lz, c, co_lo + i, blockIdx.x == 0 && (int)blockIdx.z < nco, vv[i], vv[Cs + i], vv[2 * Cs + i]);
+    } else {
+      vv[i] = alpha[(int64_t)c * Cout + co_lo + i];
+      vv[Cs + i] = beta[(int64_t)c * Cout + co_lo + i];
+      vv[2 * Cs + i] = gamma[(int64_t)c * Cout + co_lo + i];
+    }
   }
   if (PRO)
     for (int i = threadIdx.x; i < Cin; i += 256) {
@@ -484,6 +489,7 @@ static int conv_wgrad(const typename P::T* g, const typename P::T* yv, const flo
   constexpr int V = P::VEC;
   constexpr int PT = P::kF32 ? 32 : 64;
   if (Cin % 8 != 0 || Cout % 16 != 0) return -3;
+  const BnLazy* lz = fa_take_lazy(0);   // deferred BN finalisation: the tiled kernel only (not wgrad_wide)
   {
     // FEDML_AMD_WGRAD_WIDE: 0 off, 1 (default) wide layers with K ≥ 256 or Cout > 256, 2 every Cout % 128 == 0
     static int mode = -1;
@@ -492,9 +498,11 @@ static int conv_wgrad(const typename P::T* g, const typename P::T* yv, const flo
       mode = e ? atoi(e) : 2;   // measured: +1.8 % on the fp32 headline (downsample convs)
     }
     const int K = KH * KW * Cin;
-    if (Cout % 128 == 0 && ((mode == 1 && (K >= 256 || Cout > 256)) || mode == 2))
+    if (Cout % 128 == 0 && ((mode == 1 && (K >= 256 || Cout > 256)) || mode == 2)) {
+      if (lz) return -9;
       return wgrad_wide<P>(g, yv, alpha, beta, gamma, x, ps, pt, garena, ldw, woff, C, Nb, H, W, Cin, Ho, Wo, Cout, KH,
                            KW, stride, pad, cin_src, dw, nimg, stream);
+    }
   }
   if (!yv) return -7;   // a materialised dy is only consumed by the wide kernel
   const int co_slice = Cout > 256 ? 128 : Cout;   // wide layers: 128-channel dy slices
@@ -520,7 +528,7 @@ static int conv_wgrad(const typename P::T* g, const typename P::T* yv, const flo
   auto go = [&](auto kern) {
     if (smem > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     hipLaunchKernelGGL(kern, grid, dim3(256), smem, stream, g, yv, alpha, beta, gamma, x, ps, pt, dw, Nb, H, W, Cin,
-                       Ho, Wo, Cout, KH, KW, stride, pad, pix_per_wg, nt_per_z, nimg, co_slice);
+                       Ho, Wo, Cout, KH, KW, stride, pad, pix_per_wg, nt_per_z, nimg, co_slice, lz);
   };
   // instantiated register budgets: dy chunks/thread D ∈ {2, 8}, A chunks/thread ∈ {2, 4, 8, 16}
   auto by_a = [&](auto tpw_c, auto d_c) {

@@ -22,6 +22,27 @@ def _i(v):
     return _c.c_int(int(v))
 
 
+class BnLazy(ctypes.Structure):
+    """csrc/bnlazy.h ``BnLazy``: a deferred BatchNorm finalisation, computed by the consumer kernel's prologue."""
+    _fields_ = [("kind", ctypes.c_int), ("Ch", ctypes.c_int), ("NS", ctypes.c_int), ("q_gy", ctypes.c_int),
+                ("hw", ctypes.c_int), ("update_running", ctypes.c_int), ("n", ctypes.c_float),
+                ("momentum", ctypes.c_float), ("eps", ctypes.c_float), ("stats", ctypes.c_void_p),
+                ("arena", ctypes.c_void_p), ("garena", ctypes.c_void_p), ("ldw", ctypes.c_int64),
+                ("off_gamma", ctypes.c_int64), ("off_beta", ctypes.c_int64), ("off_rm", ctypes.c_int64),
+                ("off_rv", ctypes.c_int64), ("off_nbt", ctypes.c_int64), ("active", ctypes.c_void_p),
+                ("nimg", ctypes.c_void_p), ("r0", ctypes.c_void_p), ("r1", ctypes.c_void_p), ("r2", ctypes.c_void_p),
+                ("r3", ctypes.c_void_p), ("pivot", ctypes.c_void_p), ("mean_in", ctypes.c_void_p),
+                ("rstd_in", ctypes.c_void_p)]
+
+
+def _set_lazy(lazy):
+    """Hand the next consumer launch its deferred BN descriptors (device pointers; the launcher takes and clears
+    them). Called immediately before that launch."""
+    if lazy is None or (lazy[0] is None and lazy[1] is None):
+        return
+    _check(_fn("fa_set_lazy")(ctypes.c_void_p(lazy[0]), ctypes.c_void_p(lazy[1])), "fa_set_lazy")
+
+
 def _fnp(name, t):
     """Kernel entry point for the storage precision of activation tensor ``t``."""
     if t.dtype == torch.float32:
@@ -61,8 +82,9 @@ def pack_weights(arena, segs_dev, nseg, dst, dst_ld, C, max_tiles=0, max_taps=0)
 
 
 def conv_fwd(x, wpk, wpk_ld, pscale, pshift, y, stats, C, N, H, W, Cin, Cout, KH, KW, stride, pad, Ho, Wo, ldk,
-             tiles_per_wave, pivot=None, nimg=None):
+             tiles_per_wave, pivot=None, nimg=None, lazy=None):
     """y = conv(pro(x)) − pivot (per client and output channel; None → 0), BN statistics of y."""
+    _set_lazy(lazy)
     rc = _fnp("fa_conv_fwd", x)(_p(x), _p(wpk), _i64(wpk_ld), _p(pscale), _p(pshift), _p(y), _p(stats), _i(C), _i(N),
                             _i(H), _i(W), _i(Cin), _i(Cout), _i(KH), _i(KW), _i(stride), _i(pad), _i(Ho), _i(Wo),
                             _i(ldk), _i(tiles_per_wave), _p(pivot), _p(nimg), _stream(x))
@@ -75,10 +97,11 @@ def convk_min_k() -> int:
 
 
 def conv_fwd_pbout(yp, s, t, res, rs, rt, bout, wpk, wpk_ld, y, stats, C, N, H, W, Cin, Cout, ldk, tiles_per_wave,
-                   pivot=None, nimg=None):
+                   pivot=None, nimg=None, lazy=None):
     """1×1 / stride-1 forward whose operand is the previous block's output formed in the operand load and written
     to ``bout`` once: bout = relu(yp·s + t + r), r = res (identity) | res·rs + rt (downsample BN) — bit-identical to
     :func:`block_out` —; y = conv(bout) − pivot with its BN statistics, as :func:`conv_fwd`."""
+    _set_lazy(lazy)
     rc = _fnp("fa_conv_fwd_pbout", yp)(_p(yp), _p(s), _p(t), _p(res), _p(rs), _p(rt), _p(bout), _p(wpk), _i64(wpk_ld),
                                        _p(y), _p(stats), _i(C), _i(N), _i(H), _i(W), _i(Cin), _i(Cout), _i(ldk),
                                        _i(tiles_per_wave), _p(pivot), _p(nimg), _stream(yp))
@@ -119,8 +142,9 @@ def conv_bwd_data(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, dx, epi, e_x, e_s, e
 
 
 def conv_wgrad(g, yv, alpha, beta, gamma, x, ps, pt, garena, woff, C, N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
-               pad, pix_per_wg, cin_src, dw_scratch, nimg=None):
+               pad, pix_per_wg, cin_src, dw_scratch, nimg=None, lazy=None):
     """``dw_scratch``: ≥ C·Cout·KH·KW·Cin fp32, zero on entry; the kernel leaves it zeroed."""
+    _set_lazy(lazy)
     rc = _fnp("fa_conv_wgrad", g)(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(x), _p(ps), _p(pt), _p(garena),
                               _i64(garena.stride(0)), _i64(woff), _i(C), _i(N), _i(H), _i(W), _i(Cin), _i(Ho), _i(Wo),
                               _i(Cout), _i(KH), _i(KW), _i(stride), _i(pad), _i(pix_per_wg), _i(cin_src),
@@ -140,7 +164,8 @@ def conv3x3_supported(cin, cout, k, stride, pad, H, W):
 
 
 def conv3x3_fwd(x, wpk, wpk_ld, pscale, pshift, y, stats, C, N, H, W, Cin, Cout, ldk, stride=1, pivot=None,
-                nimg=None):
+                nimg=None, lazy=None):
+    _set_lazy(lazy)
     rc = _fnp("fa_conv3x3_fwd", x)(_p(x), _p(wpk), _i64(wpk_ld), _p(pscale), _p(pshift), _p(y), _p(stats), _i(C), _i(N),
                                _i(H), _i(W), _i(Cin), _i(Cout), _i(ldk), _i(stride), _p(pivot), _p(nimg), _stream(x))
     _check(rc, "fa_conv3x3_fwd")
@@ -156,10 +181,11 @@ def conv3x3_bwd_data(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, dx, e_x, e_s, e_t
 
 
 def conv3x3_wgrad(g, yv, alpha, beta, gamma, x, ps, pt, garena, woff, C, N, H, W, Cin, Cout, cin_src, dw_scratch,
-                  stride=1, scatter=True, nimg=None):
+                  stride=1, scatter=True, nimg=None, lazy=None):
     """Weight gradient into the GEMM-layout scratch, then scattered (+=) into the OIHW arena
     (``scatter=False``: left in the scratch for :func:`wgrad_scatter_multi`). (H, W) = input (x)
     resolution."""
+    _set_lazy(lazy)
     rc = _fnp("fa_conv3x3_wgrad", g)(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(x), _p(ps), _p(pt),
                                  _p(dw_scratch), _i(C), _i(N), _i(H), _i(W), _i(Cin), _i(Cout), _i(stride), _p(nimg),
                                  _stream(g))
@@ -193,8 +219,10 @@ def conv1x1_wgrad_supported(cin, cout, k, stride, pad):
     return k == 1 and stride == 1 and pad == 0 and (cin, cout) in _C1_SHAPES
 
 
-def conv1x1_wgrad(g, yv, alpha, beta, gamma, x, ps, pt, garena, woff, C, M, Cin, Cout, pix_per_wg, nimg=None, hw=0):
+def conv1x1_wgrad(g, yv, alpha, beta, gamma, x, ps, pt, garena, woff, C, M, Cin, Cout, pix_per_wg, nimg=None, hw=0,
+                  lazy=None):
     """dW += Σ_p dyᵀ·act(x) straight into the OIHW arena rows (stride garena.stride(0))."""
+    _set_lazy(lazy)
     rc = _fnp("fa_conv1x1_wgrad", g)(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(x), _p(ps), _p(pt), _p(garena),
                                  _i64(garena.stride(0)), _i64(woff), _i(C), _i(M), _i(Cin), _i(Cout), _i(pix_per_wg),
                                  _p(nimg), _i(hw), _stream(g))
@@ -216,11 +244,12 @@ def conv1x1_bwd_fused_scratch(C, M, Cin, Cout, pix_per_wg):
 
 
 def conv1x1_bwd_fused_ry(g, alpha, beta, gamma, pivot, wpk_b, wpk_ld, ldk2, e_x, e_s, e_t, out, stats, garena, woff,
-                         C, M, Cin, Cout, pix_per_wg, part=None, nimg=None, hw=0):
+                         C, M, Cin, Cout, pix_per_wg, part=None, nimg=None, hw=0, lazy=None):
     """:func:`conv1x1_bwd_fused` (EPI_MASK) of a conv whose output y was not stored: y − pivot is recomputed
     per pixel stage from the staged relu(e_x·e_s + e_t) and the weights in LDS (fp32 storage)."""
     if part is not None and part.numel() < conv1x1_bwd_fused_scratch(C, M, Cin, Cout, pix_per_wg):
         raise ValueError("conv1x1_bwd_fused_ry: partial-sum scratch too small")
+    _set_lazy(lazy)
     rc = _fn("fa_conv1x1_bwd_fused_ry_f32")(_p(g), _p(alpha), _p(beta), _p(gamma), _p(pivot), _p(wpk_b), _i64(wpk_ld),
                                             _i(ldk2), _p(e_x), _p(e_s), _p(e_t), _p(out), _p(stats),
                                             _i(stats.shape[-1]), _p(garena), _i64(garena.stride(0)), _i64(woff), _i(C),
@@ -230,13 +259,14 @@ def conv1x1_bwd_fused_ry(g, alpha, beta, gamma, pivot, wpk_b, wpk_ld, ldk2, e_x,
 
 
 def conv1x1_bwd_fused(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, ldk2, e_x, e_s, e_t, e_add, e_y1, e_y2, out, stats,
-                      garena, woff, C, M, Cin, Cout, epi, pix_per_wg, part=None, nimg=None, hw=0):
+                      garena, woff, C, M, Cin, Cout, epi, pix_per_wg, part=None, nimg=None, hw=0, lazy=None):
     """Data gradient (with the EPI_MASK / EPI_BLOCK epilogue of :func:`conv_bwd_data`) AND weight
     gradient (+= into the OIHW arena rows) of a 1×1 / stride-1 conv from one pass over g, y, e_x.
     ``stats`` is [C, Cin, NS] (NS = its last dim). ``part``: optional fp32 scratch of
     :func:`conv1x1_bwd_fused_scratch` elements → deterministic two-pass reduction, no atomics."""
     if part is not None and part.numel() < conv1x1_bwd_fused_scratch(C, M, Cin, Cout, pix_per_wg):
         raise ValueError("conv1x1_bwd_fused: partial-sum scratch too small")
+    _set_lazy(lazy)
     rc = _fnp("fa_conv1x1_bwd_fused", g)(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(wpk_b), _i64(wpk_ld),
                                      _i(ldk2), _p(e_x), _p(e_s), _p(e_t), _p(e_add), _p(e_y1), _p(e_y2), _p(out),
                                      _p(stats), _i(stats.shape[-1]), _p(garena), _i64(garena.stride(0)), _i64(woff),

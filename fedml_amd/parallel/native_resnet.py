@@ -158,6 +158,10 @@ class NativeResNetStep:
         self.use_ry = os.environ.get("FEDML_AMD_RECOMPUTE_Y", "0") == "1" and dtype == torch.float32
         self.use_pbout = os.environ.get("FEDML_AMD_FUSE_BOUT", "1") != "0"
         self.use_fch = os.environ.get("FEDML_AMD_FC_HEAD", "1") != "0"      # fused fc + CE head kernel
+        # deferred BN finalisation (csrc/bnlazy.h): the first consumer kernel folds the statistics itself
+        self.use_lazy = os.environ.get("FEDML_AMD_BN_LAZY", "1") != "0"
+        self._pending = {}       # (bn key, "f" | "b") → explicit finalisation closure, while deferred
+        self._lz_key = None
         self.dump = None   # debug: list collecting (name, tensor clone) of every backward gradient buffer
         self._nimg = None
         self.det = None    # DetAccumulator in deterministic mode (enable_deterministic)
@@ -312,6 +316,17 @@ class NativeResNetStep:
         self.c3_nseg = len(segs)
         raw = bytes((nn_ops.ScatterSeg * max(1, len(segs)))(*segs))
         self.c3_segs = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(dev)
+        # per-BN: pixels per image of its producing conv, and the Σg·y slot of its backward statistics
+        self._bn_hw = {self.stem[1].key: st.Ho * st.Wo}
+        self._bn_q = {self.stem[1].key: 1}
+        for b in self.blocks:
+            for cv, bn in zip(b.convs, b.bns):
+                self._bn_hw[bn.key] = cv.Ho * cv.Wo
+                self._bn_q[bn.key] = 1
+            if b.ds_conv is not None:
+                self._bn_hw[b.ds_bn.key] = b.ds_conv.Ho * b.ds_conv.Wo
+                self._bn_q[b.ds_bn.key] = 2
+        self._lz_dev, self._lz_key, self._lz_slot = None, None, {}
         self.geom = (N, H, W)
         if self.det is not None:
             for t in (self.stats, self.dw_scratch, self.dw_c3, self.gram):
@@ -336,7 +351,7 @@ class NativeResNetStep:
     # Every geometry keeps its own buffers alive: a captured HIP graph of one batch size must stay
     # valid while another batch size (the ragged last step of an epoch) is being run.
     _STATE_ATTRS = ("x_in", "stem_y", "stem_out", "gbuf", "dybuf", "bn_vec", "stats", "stat_views", "pooled", "dpool",
-                    "loss_c", "dw_scratch",
+                    "loss_c", "dw_scratch", "_lz_dev", "_lz_key", "_lz_slot", "_bn_hw", "_bn_q",
                     "dw_c3", "gram", "c3_segs", "c3_nseg", "c3_maxn", "_c3_off",
                     "packed", "packed_ld", "_segs", "_nseg", "_pack_tiles", "_pack_taps", "final_hw", "geom")
 
@@ -387,10 +402,11 @@ class NativeResNetStep:
             self.use_c1 and cv.cin == cv.cin_pad and nn_ops.conv1x1_wgrad_supported(cv.cin, cv.cout, cv.k, cv.stride,
                                                                                     cv.pad))
 
-    def _dy(self, cv, g, y, v, N):
+    def _dy(self, cv, g, y, v, N, bn_key=None):
         """(operand, y, α, β, γ) for the backward kernels of ``cv``: the materialised dy for wide layers."""
         if not self._dym(cv):
             return g, y, v[4], v[5], v[6]
+        self._flush(bn_key, "b")
         nn_ops.dy_apply(g, y, v[4], v[5], v[6], self.dybuf, self.C, N * cv.Ho * cv.Wo * cv.cout, cv.cout,
                         nimg=self._nimg, per_img=cv.Ho * cv.Wo * cv.cout)
         return self.dybuf, None, None, None, None
@@ -403,7 +419,7 @@ class NativeResNetStep:
     def _c3(self, cv: ConvSpec):
         return self.use_c3 and nn_ops.conv3x3_supported(cv.cin_pad, cv.cout, cv.k, cv.stride, cv.pad, cv.H, cv.W)
 
-    def _wgrad(self, cv: ConvSpec, g, y, vec, x, pro_vec, garena, N):
+    def _wgrad(self, cv: ConvSpec, g, y, vec, x, pro_vec, garena, N, bn_key=None):
         """Weight gradient of conv ``cv`` (dy from (g, y, α β γ) — ``vec`` indexable with [4..6] or an
         (α, β, γ) triple; y None: g is the materialised dy —, x the conv input with an optional BN+ReLU
         prologue) accumulated into the arena: tiled 3×3 / 1×1 kernels when they apply."""
@@ -412,20 +428,26 @@ class NativeResNetStep:
         C = self.C
         ps = pro_vec[0] if pro_vec is not None else None
         pt = pro_vec[1] if pro_vec is not None else None
+        lz = (self._take(bn_key, "b"), None) if y is not None else None   # y None: materialised dy, no BN
         if self._c3(cv):
             nn_ops.conv3x3_wgrad(g, y, vec[4], vec[5], vec[6], x, ps, pt, garena, self.off[cv.key], C, N, cv.H, cv.W,
                                  cv.cin_pad, cv.cout, cv.cin, self.dw_c3[self._c3_off[cv.key]:], cv.stride,
-                                 scatter=False, nimg=self._nimg)   # scattered with the other 3×3 layers at the end
+                                 scatter=False, nimg=self._nimg, lazy=lz)   # scattered with the other 3×3 layers
             return
         M = N * cv.Ho * cv.Wo
         if self.use_c1 and cv.cin == cv.cin_pad and nn_ops.conv1x1_wgrad_supported(cv.cin, cv.cout, cv.k, cv.stride,
                                                                                   cv.pad):
             nn_ops.conv1x1_wgrad(g, y, vec[4], vec[5], vec[6], x, ps, pt, garena, self.off[cv.key], C, M, cv.cin,
-                                 cv.cout, self._c1_pix_per_wg(M), nimg=self._nimg, hw=cv.Ho * cv.Wo)
+                                 cv.cout, self._c1_pix_per_wg(M), nimg=self._nimg, hw=cv.Ho * cv.Wo, lazy=lz)
             return
+        if lz is not None and lz[0] is not None and cv.cout % 128 == 0:
+            # the wide weight-gradient kernel (Cout % 128 == 0) takes no deferred descriptor: finalise explicitly
+            self._pending[(bn_key, "b")] = self._pending_closure
+            self._flush(bn_key, "b")
+            lz = None
         nn_ops.conv_wgrad(g, y, vec[4], vec[5], vec[6], x, ps, pt, garena, self.off[cv.key], C, N, cv.H, cv.W,
                           cv.cin_pad, cv.Ho, cv.Wo, cv.cout, cv.k, cv.k, cv.stride, cv.pad, self._pix_per_wg(M), cv.cin,
-                          self.dw_scratch, nimg=self._nimg)
+                          self.dw_scratch, nimg=self._nimg, lazy=lz)
 
     def _ry_ok(self, b) -> bool:
         """Bottleneck whose last (1×1, planes → 4·planes) conv output y3 is never stored (fp32): its BN statistics
@@ -474,9 +496,10 @@ class NativeResNetStep:
             return ppw
         return max(512, min(2048, _round_up(max(1, (M * self.plan_C) // 1024), 128)))
 
-    def _fwd(self, cv: ConvSpec, x, y, pro_vec, bn: BNSpec, N):
+    def _fwd(self, cv: ConvSpec, x, y, pro_vec, bn: BNSpec, N, pro_key=None):
         """y = conv(pro(x)) − pivot of the BN that follows; that BN's forward statistics."""
         M = N * cv.Ho * cv.Wo
+        lz = (self._take(pro_key, "f"), None) if pro_vec is not None else None
         stats = self.stat_views[bn.key][0]
         pivot = self.bn_vec[bn.key][7]
         # the strided 64-channel forward stays on the generic kernel (measured faster: tiny 8×8 outputs)
@@ -484,30 +507,110 @@ class NativeResNetStep:
             nn_ops.conv3x3_fwd(x, self.packed.view(-1)[cv.off_f:], self.packed_ld,
                                pro_vec[0] if pro_vec is not None else None,
                                pro_vec[1] if pro_vec is not None else None, y, stats, self.C, N, cv.H, cv.W,
-                               cv.cin_pad, cv.cout, cv.ldk, cv.stride, pivot=pivot, nimg=self._nimg)
+                               cv.cin_pad, cv.cout, cv.ldk, cv.stride, pivot=pivot, nimg=self._nimg, lazy=lz)
             return
         nn_ops.conv_fwd(x, self.packed.view(-1)[cv.off_f:], self.packed_ld, pro_vec[0] if pro_vec is not None else None,
                         pro_vec[1] if pro_vec is not None else None, y, stats, self.C, N, cv.H, cv.W, cv.cin_pad,
                         cv.cout, cv.k, cv.k, cv.stride, cv.pad, cv.Ho, cv.Wo, cv.ldk, self._tiles_per_wave(M),
-                        pivot=pivot, nimg=self._nimg)
+                        pivot=pivot, nimg=self._nimg, lazy=lz)
 
     def _bn_fwd(self, bn, N, hw, arena, active, training=True):
         v = self.bn_vec[bn.key]
         fst = self.stat_views[bn.key][0]
-        if self.det is not None:
-            self.det.flush(fst)
         g, b, rm, rv, nbt = self._bn_offsets(bn)
-        nn_ops.bn_fwd_finalize(fst, self.C, bn.ch, float(N * hw), arena, g, b, rm, rv, nbt, bn.momentum, bn.eps,
-                               active, v[0], v[1], v[2], v[3], training, pivot=v[7], nimg=self._nimg, hw=hw)
+
+        def explicit():
+            if self.det is not None:
+                self.det.flush(fst)
+            nn_ops.bn_fwd_finalize(fst, self.C, bn.ch, float(N * hw), arena, g, b, rm, rv, nbt, bn.momentum, bn.eps,
+                                   active, v[0], v[1], v[2], v[3], training, pivot=v[7], nimg=self._nimg, hw=hw)
+        self._defer((bn.key, "f"), explicit)
 
     def _bn_bwd(self, bn, q, N, hw, arena, garena):
         v = self.bn_vec[bn.key]
         bst = self.stat_views[bn.key][1]
-        if self.det is not None:
-            self.det.flush(bst)
         g, b = self.off[f"{bn.key}.weight"], self.off[f"{bn.key}.bias"]
-        nn_ops.bn_bwd_finalize(bst, 3, q, self.C, bn.ch, float(N * hw), v[2], v[3], arena, garena, g, b, v[4], v[5],
-                               v[6], nimg=self._nimg, hw=hw)
+
+        def explicit():
+            if self.det is not None:
+                self.det.flush(bst)
+            nn_ops.bn_bwd_finalize(bst, 3, q, self.C, bn.ch, float(N * hw), v[2], v[3], arena, garena, g, b, v[4],
+                                   v[5], v[6], nimg=self._nimg, hw=hw)
+        self._defer((bn.key, "b"), explicit)
+
+    # ------------------------------------------------------------------ deferred BN finalisation
+    def _lazy_on(self):
+        return self.use_lazy and self.det is None
+
+    def _defer(self, key, explicit):
+        """Explicit finalisation now, or (lazy mode) left to the first consumer kernel of the BN's vectors."""
+        if not self._lazy_on():
+            explicit()
+            return
+        if key in self._pending:      # a BN finalised twice without a consumer in between: keep the order
+            self._pending.pop(key)()
+        self._pending[key] = explicit
+
+    def _take(self, bn_key, kind):
+        """Device pointer of the pending BN's descriptor for the consumer about to launch (None: nothing pending,
+        the consumer reads the finalised rows)."""
+        key = (bn_key, kind)
+        if bn_key is None or key not in self._pending:
+            return None
+        self._pending_closure = self._pending.pop(key)
+        return self._lz_dev.data_ptr() + self._lz_slot[key] * ctypes.sizeof(nn_ops.BnLazy)
+
+    def _flush(self, bn_key, kind):
+        key = (bn_key, kind)
+        if bn_key is not None and key in self._pending:
+            self._pending.pop(key)()
+
+    def _flush_all(self):
+        for key in list(self._pending):
+            self._pending.pop(key)()
+
+    def _lz_prepare(self, arena, garena, active, N):
+        """Descriptors of every BN (forward + backward) for this geometry and these buffers, uploaded only when
+        they change (a captured graph replays with the same buffers, so its capture never uploads)."""
+        nimg = self._nimg
+        key = (self.geom, arena.data_ptr(), garena.data_ptr(), active.data_ptr() if active is not None else 0,
+               nimg.data_ptr() if nimg is not None else 0, arena.stride(0))
+        if self._lz_key == key:
+            return
+        bns = list(self._all_bns())
+        arr = (nn_ops.BnLazy * (2 * len(bns)))()
+        self._lz_slot = {}
+        hw_of = self._bn_hw
+        for i, bn in enumerate(bns):
+            v = self.bn_vec[bn.key]
+            fst, bst = self.stat_views[bn.key]
+            g, b, rm, rv, nbt = self._bn_offsets(bn)
+            hw = hw_of[bn.key]
+            common = dict(Ch=bn.ch, hw=hw, n=float(N * hw), arena=arena.data_ptr(), garena=garena.data_ptr(),
+                          ldw=arena.stride(0), off_gamma=g, off_beta=b,
+                          nimg=nimg.data_ptr() if nimg is not None else None)
+            f = arr[2 * i]
+            for k, val in dict(common, kind=0, NS=2, q_gy=0, update_running=1, momentum=bn.momentum, eps=bn.eps,
+                               stats=fst.data_ptr(), off_rm=rm, off_rv=rv, off_nbt=nbt,
+                               active=active.data_ptr() if active is not None else None, r0=v[0].data_ptr(),
+                               r1=v[1].data_ptr(), r2=v[2].data_ptr(), r3=v[3].data_ptr(),
+                               pivot=v[7].data_ptr()).items():
+                setattr(f, k, val)
+            bd = arr[2 * i + 1]
+            for k, val in dict(common, kind=1, NS=3, q_gy=self._bn_q[bn.key],
+                               update_running=0, momentum=0.0, eps=bn.eps, stats=bst.data_ptr(), off_rm=-1, off_rv=-1,
+                               off_nbt=-1, r0=v[4].data_ptr(), r1=v[5].data_ptr(), r2=v[6].data_ptr(),
+                               mean_in=v[2].data_ptr(), rstd_in=v[3].data_ptr()).items():
+                setattr(bd, k, val)
+            self._lz_slot[(bn.key, "f")] = 2 * i
+            self._lz_slot[(bn.key, "b")] = 2 * i + 1
+        raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+        if self._lz_dev is None or self._lz_dev.numel() != raw.numel():
+            self._lz_dev = torch.empty(raw.numel(), dtype=torch.uint8, device=self.device)   # per geometry
+        if torch.cuda.is_current_stream_capturing():
+            raise RuntimeError("deferred-BN descriptors changed during graph capture")
+        self._lz_dev.copy_(raw)
+        self._lz_key = key
 
     # ------------------------------------------------------------------ step
     def step(self, arena, garena, x, labels, row_scale, active, nimg=None):
@@ -530,6 +633,10 @@ class NativeResNetStep:
         if self.det is not None:
             self.det.register(garena)
         self.stats.zero_()
+        self._pending.clear()
+        nn_ops._set_lazy((0, 0))        # no descriptor left over from an aborted launch
+        if self._lazy_on():
+            self._lz_prepare(arena, garena, active, N)
         nn_ops.pack_weights(arena, self._segs, self._nseg, self.packed, self.packed_ld, C, self._pack_tiles,
                             self._pack_taps)
         st_conv, st_bn = self.stem
@@ -539,24 +646,27 @@ class NativeResNetStep:
         self._fwd(st_conv, self.x_in, self.stem_y, None, st_bn, N)
         self._bn_fwd(st_bn, N, st_conv.Ho * st_conv.Wo, arena, active)
         v0 = self.bn_vec[st_bn.key]
+        self._flush(st_bn.key, "f")          # block_out reads the finalised rows
         nn_ops.block_out(self.stem_y, v0[0], v0[1], None, None, None, self.stem_out, C,
                          N * st_conv.Ho * st_conv.Wo * st_conv.cout, st_conv.cout, nimg=self._nimg,
                          per_img=st_conv.Ho * st_conv.Wo * st_conv.cout)
         act_in = self.stem_out
         pend = None    # (yp, s, t, res, rs, rt, bout) of a block output formed by the next block's first conv
+        pend_keys = (None, None)   # its BNs (deferred finalisation: taken by that conv)
         for bi, b in enumerate(self.blocks):
             b.act_in = act_in
             for j, (cv, bn) in enumerate(zip(b.convs, b.bns)):
                 src = act_in if j == 0 else b.ys[j - 1]
                 pro = None if j == 0 else self.bn_vec[b.bns[j - 1].key]
                 if j == 0 and pend is not None:
+                    lz = (self._take(pend_keys[0], "f"), self._take(pend_keys[1], "f"))
                     nn_ops.conv_fwd_pbout(*pend, self.packed.view(-1)[cv.off_f:], self.packed_ld, b.ys[0],
                                           self.stat_views[bn.key][0], C, N, cv.H, cv.W, cv.cin_pad, cv.cout, cv.ldk,
                                           self._tiles_per_wave(N * cv.Ho * cv.Wo), pivot=self.bn_vec[bn.key][7],
-                                          nimg=self._nimg)
+                                          nimg=self._nimg, lazy=lz)
                     pend = None
                 else:
-                    self._fwd(cv, src, b.ys[j], pro, bn, N)
+                    self._fwd(cv, src, b.ys[j], pro, bn, N, pro_key=None if j == 0 else b.bns[j - 1].key)
                 if b.ys[j] is None:     # recomputed-y conv: keep the pivot its later passes must subtract
                     self.bn_vec[bn.key][8].copy_(self.bn_vec[bn.key][7])
                 self._bn_fwd(bn, N, cv.Ho * cv.Wo, arena, active)
@@ -569,7 +679,10 @@ class NativeResNetStep:
             if self._pbout_ok(b, self.blocks[bi + 1] if bi + 1 < len(self.blocks) else None):
                 vd = self.bn_vec[b.ds_bn.key] if b.ds_conv is not None else (None, None)
                 pend = (b.ys[-1], vl[0], vl[1], b.yd if b.ds_conv is not None else act_in, vd[0], vd[1], b.out)
+                pend_keys = (lbn.key, b.ds_bn.key if b.ds_conv is not None else None)
             elif b.ry:    # block output from a second pass of the last conv (its output y3 is never stored)
+                for k in (b.bns[-2].key, lbn.key, b.ds_bn.key if b.ds_conv is not None else None):
+                    self._flush(k, "f")
                 pv = self.bn_vec[b.bns[-2].key]
                 res, rs, rt = (b.yd, self.bn_vec[b.ds_bn.key][0], self.bn_vec[b.ds_bn.key][1]) \
                     if b.ds_conv is not None else (act_in, None, None)
@@ -578,14 +691,18 @@ class NativeResNetStep:
                                      last.ldk, self._tiles_per_wave(N * last.Ho * last.Wo), nimg=self._nimg)
             elif b.ds_conv is not None:
                 vd = self.bn_vec[b.ds_bn.key]
+                self._flush(lbn.key, "f")
+                self._flush(b.ds_bn.key, "f")
                 nn_ops.block_out(b.ys[-1], vl[0], vl[1], b.yd, vd[0], vd[1], b.out, C,
                                  N * last.Ho * last.Wo * last.cout, last.cout, nimg=self._nimg,
                                  per_img=last.Ho * last.Wo * last.cout)
             else:
+                self._flush(lbn.key, "f")
                 nn_ops.block_out(b.ys[-1], vl[0], vl[1], act_in, None, None, b.out, C,
                                  N * last.Ho * last.Wo * last.cout, last.cout, nimg=self._nimg,
                                  per_img=last.Ho * last.Wo * last.cout)
             act_in = b.out
+        self._flush_all()       # every forward BN has been folded (by its consumer or explicitly)
         fh, fw = self.final_hw
         chl = self.blocks[-1].convs[-1].cout
         nn_ops.avgpool(act_in, self.pooled, C * N, fh * fw, chl, nimg=self._nimg, N=N)
@@ -652,7 +769,7 @@ class NativeResNetStep:
                                                 self.packed_ld, cv.ldk2, b.ys[j - 1], pv[0], pv[1], out_g,
                                                 self.stat_views[b.bns[j - 1].key][1], garena, self.off[cv.key], C, M,
                                                 cv.cin, cv.cout, self._c1f_pix_per_wg(M), nimg=self._nimg,
-                                                hw=cv.Ho * cv.Wo)
+                                                hw=cv.Ho * cv.Wo, lazy=(self._take(bn.key, "b"), None))
                     self._bn_bwd(b.bns[j - 1], 1, N, cv.H * cv.W, arena, garena)
                     g_j = out_g
                     self._dump(f"{cv.key}.dx", out_g, C * N * cv.H * cv.W * cv.cin)
@@ -662,13 +779,14 @@ class NativeResNetStep:
                                              self.packed_ld, cv.ldk2, b.ys[j - 1], pv[0], pv[1], None, None, None,
                                              out_g, self.stat_views[b.bns[j - 1].key][1], garena, self.off[cv.key], C,
                                              M, cv.cin, cv.cout, nn_ops.EPI_MASK, self._c1f_pix_per_wg(M),
-                                             nimg=self._nimg, hw=cv.Ho * cv.Wo)
+                                             nimg=self._nimg, hw=cv.Ho * cv.Wo, lazy=(self._take(bn.key, "b"), None))
                     self._bn_bwd(b.bns[j - 1], 1, N, cv.H * cv.W, arena, garena)
                     g_j = out_g
                     self._dump(f"{cv.key}.dx", out_g, C * N * cv.H * cv.W * cv.cin)
                     continue
-                dg, dyv, al, be, ga = self._dy(cv, g_j, b.ys[j], v, N)
-                self._wgrad(cv, dg, dyv, (al, be, ga), b.ys[j - 1], pv, garena, N)
+                dg, dyv, al, be, ga = self._dy(cv, g_j, b.ys[j], v, N, bn_key=bn.key)
+                self._wgrad(cv, dg, dyv, (al, be, ga), b.ys[j - 1], pv, garena, N, bn_key=bn.key)
+                self._flush(bn.key, "b")
                 if self._c3(cv) and not self._s2k(cv):
                     nn_ops.conv3x3_bwd_data(g_j, b.ys[j], v[4], v[5], v[6], self.packed.view(-1)[cv.off_b:],
                                             self.packed_ld, out_g, b.ys[j - 1], pv[0], pv[1],
@@ -691,8 +809,9 @@ class NativeResNetStep:
             if b.ds_conv is not None:
                 d = b.ds_conv
                 vd = self.bn_vec[b.ds_bn.key]
-                dg, dyv, al, be, ga = self._dy(d, gpre, b.yd, vd, N)
-                self._wgrad(d, dg, dyv, (al, be, ga), b.act_in, None, garena, N)
+                dg, dyv, al, be, ga = self._dy(d, gpre, b.yd, vd, N, bn_key=b.ds_bn.key)
+                self._wgrad(d, dg, dyv, (al, be, ga), b.act_in, None, garena, N, bn_key=b.ds_bn.key)
+                self._flush(b.ds_bn.key, "b")
                 nn_ops.conv_bwd_data(dg, dyv, al, be, ga, self.packed.view(-1)[d.off_b:], self.packed_ld,
                                      gadd, nn_ops.EPI_STORE, None, None, None, None, None, None, self.stats, C, N,
                                      d.Ho, d.Wo, d.cout, d.cin_pad, d.k, d.k, d.stride, d.pad, d.H, d.W, d.ldk2,
@@ -705,9 +824,10 @@ class NativeResNetStep:
             v = self.bn_vec[bn0.key]
             fused0 = self._c1f(cv0, nn_ops.EPI_BLOCK)
             dg0, dyv0, al0, be0, ga0 = (g_j, b.ys[0], v[4], v[5], v[6]) if fused0 else \
-                self._dy(cv0, g_j, b.ys[0], v, N)
+                self._dy(cv0, g_j, b.ys[0], v, N, bn_key=bn0.key)
             if not fused0:
-                self._wgrad(cv0, dg0, dyv0, (al0, be0, ga0), b.act_in, None, garena, N)
+                self._wgrad(cv0, dg0, dyv0, (al0, be0, ga0), b.act_in, None, garena, N, bn_key=bn0.key)
+                self._flush(bn0.key, "b")
             if prev_block is not None:
                 ey1, ey2 = prev_block.ys[-1], prev_block.yd
                 pstats = self.stat_views[prev_block.bns[-1].key][1]
@@ -724,7 +844,7 @@ class NativeResNetStep:
                                          self.packed_ld, cv0.ldk2, b.act_in, None, None, shortcut, ey1, ey2, out_buf,
                                          pstats, garena, self.off[cv0.key], C, M0, cv0.cin, cv0.cout,
                                          nn_ops.EPI_BLOCK, self._c1f_pix_per_wg(M0), nimg=self._nimg,
-                                         hw=cv0.H * cv0.W)
+                                         hw=cv0.H * cv0.W, lazy=(self._take(bn0.key, "b"), None))
                 gpre = out_buf
                 self._dump(f"{cv0.key}.dx", out_buf, C * N * cv0.H * cv0.W * cv0.cin)
                 continue
@@ -738,7 +858,8 @@ class NativeResNetStep:
         # stem backward: bn0 bwd then weight grad only
         self._bn_bwd(st_bn, 1, N, st_conv.Ho * st_conv.Wo, arena, garena)
         v = self.bn_vec[st_bn.key]
-        self._wgrad(st_conv, gpre, self.stem_y, v, self.x_in, None, garena, N)
+        self._wgrad(st_conv, gpre, self.stem_y, v, self.x_in, None, garena, N, bn_key=st_bn.key)
+        self._flush_all()
         if self.c3_nseg:
             if self.det is not None:
                 self.det.flush(self.dw_c3)
