@@ -4,6 +4,7 @@
 // fp32 arenas [C][ldw] addressed by offset.
 #include "prec.h"
 #include "detacc.h"
+#include "bnlazy.h"
 
 FA_DET_EXPORT(bn)
 
@@ -32,24 +33,20 @@ __global__ void bn_fwd_finalize_kernel(const float* __restrict__ stats, int Ch, 
   if (n <= 0.f) return;                       // client without data this step: nothing to normalise
   float* pa = arena + (int64_t)c * ldw;
   const int64_t v = (int64_t)c * Ch + ch;
-  const float s1 = stats[v * 2 + 0];
-  const float s2 = stats[v * 2 + 1];
-  const float mean = s1 / n;
-  const float var = fmaxf(s2 / n - mean * mean, 0.f);
-  const float rstd = rsqrtf(var + eps);
   const float g = off_gamma >= 0 ? pa[off_gamma + ch] : 1.f;
   const float b = off_beta >= 0 ? pa[off_beta + ch] : 0.f;
+  const BnFwdFold f = bn_fold_fwd(stats[v * 2 + 0], stats[v * 2 + 1], n, eps, g, b);   // shared with bnlazy.h
   const float k = pivot ? pivot[v] : 0.f;
-  const float true_mean = mean + k;
-  scale[v] = g * rstd;
-  shift[v] = b - mean * g * rstd;
-  mean_out[v] = mean;
-  rstd_out[v] = rstd;
+  const float true_mean = __fadd_rn(f.mean, k);
+  scale[v] = f.scale;
+  shift[v] = f.shift;
+  mean_out[v] = f.mean;
+  rstd_out[v] = f.rstd;
   const bool on = active ? active[c] > 0.f : true;
   if (pivot && on) pivot[v] = true_mean;
   if (update_running && on) {
-    if (off_rm >= 0) pa[off_rm + ch] = (1.f - momentum) * pa[off_rm + ch] + momentum * true_mean;
-    if (off_rv >= 0) pa[off_rv + ch] = (1.f - momentum) * pa[off_rv + ch] + momentum * var * n / fmaxf(n - 1.f, 1.f);
+    if (off_rm >= 0) pa[off_rm + ch] = bn_running_update(pa[off_rm + ch], momentum, true_mean);
+    if (off_rv >= 0) pa[off_rv + ch] = bn_running_update(pa[off_rv + ch], momentum, bn_unbiased(f.var, n));
     if (off_nbt >= 0 && ch == 0) pa[off_nbt] += 1.f;
   }
 }
@@ -79,19 +76,13 @@ __global__ void bn_bwd_finalize_kernel(const float* __restrict__ bstats, int NS,
   if (nimg) n = (float)nimg[c] * (float)hw;
   if (n <= 0.f) return;
   const int64_t v = (int64_t)c * Ch + ch;
-  const float sg = bstats[v * NS + 0];
-  const float sgy = bstats[v * NS + q_gy];
-  const float mu = mean[v], r = rstd[v];
-  const float dbeta = sg;
-  const float dgamma = r * (sgy - mu * sg);
   const float g = off_gamma >= 0 ? arena[(int64_t)c * ldw + off_gamma + ch] : 1.f;
-  if (off_gamma >= 0) garena[(int64_t)c * ldw + off_gamma + ch] += dgamma;
-  if (off_beta >= 0) garena[(int64_t)c * ldw + off_beta + ch] += dbeta;
-  const float a = g * r;
-  const float b = -g * r * r * dgamma / n;
-  alpha[v] = a;
-  beta_c[v] = b;
-  gamma_c[v] = -a * dbeta / n - b * mu;
+  const BnBwdFold f = bn_fold_bwd(bstats[v * NS + 0], bstats[v * NS + q_gy], mean[v], rstd[v], g, n);
+  if (off_gamma >= 0) garena[(int64_t)c * ldw + off_gamma + ch] += f.dgamma;
+  if (off_beta >= 0) garena[(int64_t)c * ldw + off_beta + ch] += f.dbeta;
+  alpha[v] = f.a;
+  beta_c[v] = f.b;
+  gamma_c[v] = f.c;
 }
 
 FA_EXPORT int fa_bn_bwd_finalize(const float* bstats, int NS, int q_gy, int C, int Ch, float n, const float* mean,

@@ -39,6 +39,40 @@ struct BnLazy {
 
 extern "C" const BnLazy* fa_take_lazy(int slot);   // host side: the descriptor set for this launch (or null)
 
+// The folding arithmetic shared by the explicit finalize kernels (bn_kernels.hip) and the deferred path, written
+// with explicitly rounded operations so that no FMA contraction can differ between the kernels it is inlined
+// into: both paths produce the same bits.
+struct BnFwdFold {
+  float mean, var, rstd, scale, shift;
+};
+__device__ __forceinline__ BnFwdFold bn_fold_fwd(float s1, float s2, float n, float eps, float g, float b) {
+  BnFwdFold f;
+  f.mean = __fdiv_rn(s1, n);
+  f.var = fmaxf(__fsub_rn(__fdiv_rn(s2, n), __fmul_rn(f.mean, f.mean)), 0.f);
+  f.rstd = rsqrtf(__fadd_rn(f.var, eps));
+  f.scale = __fmul_rn(g, f.rstd);
+  f.shift = __fsub_rn(b, __fmul_rn(__fmul_rn(f.mean, g), f.rstd));
+  return f;
+}
+struct BnBwdFold {
+  float dgamma, dbeta, a, b, c;
+};
+__device__ __forceinline__ BnBwdFold bn_fold_bwd(float sg, float sgy, float mu, float r, float g, float n) {
+  BnBwdFold f;
+  f.dbeta = sg;
+  f.dgamma = __fmul_rn(r, __fsub_rn(sgy, __fmul_rn(mu, sg)));
+  f.a = __fmul_rn(g, r);
+  f.b = __fdiv_rn(__fmul_rn(__fmul_rn(__fmul_rn(-g, r), r), f.dgamma), n);
+  f.c = __fsub_rn(__fdiv_rn(__fmul_rn(-f.a, f.dbeta), n), __fmul_rn(f.b, mu));
+  return f;
+}
+__device__ __forceinline__ float bn_running_update(float old, float mom, float v) {
+  return __fadd_rn(__fmul_rn(__fsub_rn(1.f, mom), old), __fmul_rn(mom, v));
+}
+__device__ __forceinline__ float bn_unbiased(float var, float n) {
+  return __fdiv_rn(__fmul_rn(var, n), fmaxf(__fsub_rn(n, 1.f), 1.f));
+}
+
 // forward: (scale, shift) of client c, channel ch — bn_fwd_finalize_kernel's arithmetic
 __device__ __forceinline__ void bn_lazy_fwd(const BnLazy* L, int c, int ch, bool writer, float& s_out, float& t_out) {
   float n = L->n;
@@ -51,29 +85,24 @@ __device__ __forceinline__ void bn_lazy_fwd(const BnLazy* L, int c, int ch, bool
   const int Ch = L->Ch;
   float* pa = L->arena + (int64_t)c * L->ldw;
   const int64_t v = (int64_t)c * Ch + ch;
-  const float s1 = L->stats[v * 2 + 0];
-  const float s2 = L->stats[v * 2 + 1];
-  const float mean = s1 / n;
-  const float var = fmaxf(s2 / n - mean * mean, 0.f);
-  const float rstd = rsqrtf(var + L->eps);
   const float g = L->off_gamma >= 0 ? pa[L->off_gamma + ch] : 1.f;
   const float b = L->off_beta >= 0 ? pa[L->off_beta + ch] : 0.f;
-  s_out = g * rstd;
-  t_out = b - mean * g * rstd;
+  const BnFwdFold f = bn_fold_fwd(L->stats[v * 2 + 0], L->stats[v * 2 + 1], n, L->eps, g, b);
+  s_out = f.scale;
+  t_out = f.shift;
   if (!writer) return;
   const float k = L->pivot ? L->pivot[v] : 0.f;
-  const float true_mean = mean + k;
+  const float true_mean = __fadd_rn(f.mean, k);
   L->r0[v] = s_out;
   L->r1[v] = t_out;
-  L->r2[v] = mean;
-  L->r3[v] = rstd;
+  L->r2[v] = f.mean;
+  L->r3[v] = f.rstd;
   const bool on = L->active ? L->active[c] > 0.f : true;
   if (L->pivot && on) L->pivot[v] = true_mean;
   if (L->update_running && on) {
     const float mom = L->momentum;
-    if (L->off_rm >= 0) pa[L->off_rm + ch] = (1.f - mom) * pa[L->off_rm + ch] + mom * true_mean;
-    if (L->off_rv >= 0)
-      pa[L->off_rv + ch] = (1.f - mom) * pa[L->off_rv + ch] + mom * var * n / fmaxf(n - 1.f, 1.f);
+    if (L->off_rm >= 0) pa[L->off_rm + ch] = bn_running_update(pa[L->off_rm + ch], mom, true_mean);
+    if (L->off_rv >= 0) pa[L->off_rv + ch] = bn_running_update(pa[L->off_rv + ch], mom, bn_unbiased(f.var, n));
     if (L->off_nbt >= 0 && ch == 0) pa[L->off_nbt] += 1.f;
   }
 }
@@ -88,20 +117,15 @@ __device__ __forceinline__ void bn_lazy_bwd(const BnLazy* L, int c, int ch, bool
     return;
   }
   const int64_t v = (int64_t)c * L->Ch + ch;
-  const float sg = L->stats[v * L->NS + 0];
-  const float sgy = L->stats[v * L->NS + L->q_gy];
-  const float mu = L->mean_in[v], r = L->rstd_in[v];
-  const float dbeta = sg;
-  const float dgamma = r * (sgy - mu * sg);
   const float g = L->off_gamma >= 0 ? L->arena[(int64_t)c * L->ldw + L->off_gamma + ch] : 1.f;
-  const float a = g * r;
-  const float b = -g * r * r * dgamma / n;
-  a_out = a;
-  b_out = b;
-  g_out = -a * dbeta / n - b * mu;
+  const BnBwdFold f = bn_fold_bwd(L->stats[v * L->NS + 0], L->stats[v * L->NS + L->q_gy], L->mean_in[v],
+                                  L->rstd_in[v], g, n);
+  a_out = f.a;
+  b_out = f.b;
+  g_out = f.c;
   if (!writer) return;
-  if (L->off_gamma >= 0) L->garena[(int64_t)c * L->ldw + L->off_gamma + ch] += dgamma;
-  if (L->off_beta >= 0) L->garena[(int64_t)c * L->ldw + L->off_beta + ch] += dbeta;
+  if (L->off_gamma >= 0) L->garena[(int64_t)c * L->ldw + L->off_gamma + ch] += f.dgamma;
+  if (L->off_beta >= 0) L->garena[(int64_t)c * L->ldw + L->off_beta + ch] += f.dbeta;
   L->r0[v] = a_out;
   L->r1[v] = b_out;
   L->r2[v] = g_out;

@@ -312,7 +312,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ h
                                                      const float* __restrict__ beta, float eps, uint32_t thr,
                                                      float dscale, uint32_t seed, float* __restrict__ y,
                                                      float* __restrict__ xsum, float* __restrict__ mean_out,
-                                                     float* __restrict__ rstd_out, const uint32_t* __restrict__ seedp) {
+                                                     float* __restrict__ rstd_out, const uint32_t* __restrict__ seedp,
+                                                     int64_t gcs) {
   if (seedp) seed += *seedp * 1000003u;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -358,8 +359,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const float* __restrict__ h
     }
   }
   const float rstd = rsqrtf(wave_sum(q) / (float)d + eps);
-  const float* g = gamma + (size_t)c * d;
-  const float* b = beta + (size_t)c * d;
+  const float* g = gamma + (int64_t)c * gcs;   // per-client γ/β rows: the arena views (client stride gcs)
+  const float* b = beta + (int64_t)c * gcs;
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int col = (v * 64 + lane) * 4;
@@ -385,12 +386,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
                                                      int rpc, int d, const float* __restrict__ gamma,
                                                      float* __restrict__ dx, float* __restrict__ dh, uint32_t thr,
                                                      float dscale, uint32_t seed, float* __restrict__ dgamma,
-                                                     float* __restrict__ dbeta, const uint32_t* __restrict__ seedp) {
+                                                     float* __restrict__ dbeta, const uint32_t* __restrict__ seedp,
+                                                     int64_t gcs, int64_t dgcs) {
   if (seedp) seed += *seedp * 1000003u;
   extern __shared__ float red[];   // [4][2][d]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int c = blockIdx.y;
-  const float* g = gamma + (size_t)c * d;
+  const float* g = gamma + (int64_t)c * gcs;
   float ag[NV][4], ab[NV][4];
 #pragma unroll
   for (int v = 0; v < NV; ++v)
@@ -461,8 +463,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
       sg += red[(w * 2 + 0) * d + i];
       sb += red[(w * 2 + 1) * d + i];
     }
-    fa_acc_add(dgamma + (size_t)c * d + i, sg);
-    fa_acc_add(dbeta + (size_t)c * d + i, sb);
+    fa_acc_add(dgamma + (int64_t)c * dgcs + i, sg);   // straight into the gradient arena rows when dgcs = ld
+    fa_acc_add(dbeta + (int64_t)c * dgcs + i, sb);
   }
 }
 
@@ -953,13 +955,14 @@ FA_EXPORT int fa_bias_grad_f32(const float* dy, int64_t dy_bs, int lddy, float* 
 
 FA_EXPORT int fa_ln_fwd_f32(const float* h, const float* res, int R, int d, int rows_per_client, const float* gamma,
                             const float* beta, float eps, uint32_t thr, float dscale, uint32_t seed, float* y,
-                            float* xsum, float* mean, float* rstd, const uint32_t* seedp, hipStream_t stream) {
+                            float* xsum, float* mean, float* rstd, const uint32_t* seedp, int64_t gcs,
+                            hipStream_t stream) {
   using namespace tff;
-  if (d % 4 != 0 || d > 2048 || R <= 0) return (int)hipErrorInvalidValue;
+  if (d % 4 != 0 || d > 2048 || R <= 0 || gcs % 4 != 0) return (int)hipErrorInvalidValue;
   const dim3 grid((R + 3) / 4);
 #define TFF_LNF(NV) \
   hipLaunchKernelGGL(ln_fwd_kernel<NV>, grid, dim3(256), 0, stream, h, res, R, d, rows_per_client, gamma, beta, eps, \
-                     thr, dscale, seed, y, xsum, mean, rstd, seedp)
+                     thr, dscale, seed, y, xsum, mean, rstd, seedp, gcs)
   if (d <= 256) TFF_LNF(1);
   else if (d <= 512) TFF_LNF(2);
   else if (d <= 768) TFF_LNF(3);
@@ -972,9 +975,9 @@ FA_EXPORT int fa_ln_fwd_f32(const float* h, const float* res, int R, int d, int 
 FA_EXPORT int fa_ln_bwd_f32(const float* dy, const float* x, const float* mean, const float* rstd, int C,
                             int rows_per_client, int d, const float* gamma, float* dx, float* dh, uint32_t thr,
                             float dscale, uint32_t seed, float* dgamma, float* dbeta, const uint32_t* seedp,
-                            hipStream_t stream) {
+                            int64_t gcs, int64_t dgcs, hipStream_t stream) {
   using namespace tff;
-  if (d % 4 != 0 || d > 2048 || C <= 0 || C > 65535) return (int)hipErrorInvalidValue;
+  if (d % 4 != 0 || d > 2048 || C <= 0 || C > 65535 || gcs % 4 != 0) return (int)hipErrorInvalidValue;
   int bpc = (rows_per_client + 31) / 32;   // ≥ 8 rows per wave
   if (bpc < 1) bpc = 1;
   if (bpc > 1024) bpc = 1024;
@@ -982,7 +985,7 @@ FA_EXPORT int fa_ln_bwd_f32(const float* dy, const float* x, const float* mean, 
   const size_t sm = 8 * (size_t)d * sizeof(float);
 #define TFF_LNB(NV) \
   hipLaunchKernelGGL(ln_bwd_kernel<NV>, grid, dim3(256), sm, stream, dy, x, mean, rstd, rows_per_client, d, gamma, dx, \
-                     dh, thr, dscale, seed, dgamma, dbeta, seedp)
+                     dh, thr, dscale, seed, dgamma, dbeta, seedp, gcs, dgcs)
   if (d <= 256) TFF_LNB(1);
   else if (d <= 512) TFF_LNB(2);
   else if (d <= 768) TFF_LNB(3);

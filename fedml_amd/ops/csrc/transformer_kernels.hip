@@ -46,7 +46,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const uint16_t* __restrict_
                                                      float dscale, uint32_t seed, uint16_t* __restrict__ y,
                                                      uint16_t* __restrict__ xsum, float* __restrict__ mean_out,
                                                      float* __restrict__ rstd_out,
-                                                     const uint32_t* __restrict__ seedp) {
+                                                     const uint32_t* __restrict__ seedp, int64_t gcs) {
   if (seedp) seed += *seedp * 1000003u;   // device step counter (graph-captured steps)
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -95,8 +95,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const uint16_t* __restrict_
     }
   }
   const float rstd = rsqrtf(wave_sum(q) / (float)d + eps);
-  const float* g = gamma + (size_t)c * d;
-  const float* b = beta + (size_t)c * d;
+  const float* g = gamma + (int64_t)c * gcs;
+  const float* b = beta + (int64_t)c * gcs;
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
     const int col = (v * 64 + lane) * 8;
@@ -127,12 +127,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
                                                      uint16_t* __restrict__ dx, uint16_t* __restrict__ dh,
                                                      uint32_t thr, float dscale, uint32_t seed,
                                                      float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                     const uint32_t* __restrict__ seedp) {
+                                                     const uint32_t* __restrict__ seedp, int64_t gcs, int64_t dgcs) {
   if (seedp) seed += *seedp * 1000003u;
   extern __shared__ float red[];  // [4][2][d]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int c = blockIdx.y;
-  const float* g = gamma + (size_t)c * d;
+  const float* g = gamma + (int64_t)c * gcs;
   float ag[NV][8], ab[NV][8];
 #pragma unroll
   for (int v = 0; v < NV; ++v)
@@ -203,8 +203,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
       sg += red[(w * 2 + 0) * d + i];
       sb += red[(w * 2 + 1) * d + i];
     }
-    fa_acc_add(dgamma + (size_t)c * d + i, sg);
-    fa_acc_add(dbeta + (size_t)c * d + i, sb);
+    fa_acc_add(dgamma + (int64_t)c * dgcs + i, sg);
+    fa_acc_add(dbeta + (int64_t)c * dgcs + i, sb);
   }
 }
 
@@ -591,21 +591,21 @@ template <int NV>
 int launch_ln_fwd(const uint16_t* h, const uint16_t* res, int R, int d, int rpc, const float* g, const float* b,
                   float eps, uint32_t thr, float dscale, uint32_t seed, const uint32_t* seedp, uint16_t* y,
                   uint16_t* xsum, float* mean,
-                  float* rstd, hipStream_t st) {
+                  float* rstd, int64_t gcs, hipStream_t st) {
   hipLaunchKernelGGL(ln_fwd_kernel<NV>, dim3((R + 3) / 4), dim3(256), 0, st, h, res, R, d, rpc, g, b, eps, thr,
-                     dscale, seed, y, xsum, mean, rstd, seedp);
+                     dscale, seed, y, xsum, mean, rstd, seedp, gcs);
   return (int)hipGetLastError();
 }
 template <int NV>
 int launch_ln_bwd(const uint16_t* dy, const uint16_t* x, const float* mean, const float* rstd, int C, int rpc, int d,
                   const float* g, uint16_t* dx, uint16_t* dh, uint32_t thr, float dscale, uint32_t seed,
                   const uint32_t* seedp, float* dg,
-                  float* db, hipStream_t st) {
+                  float* db, int64_t gcs, int64_t dgcs, hipStream_t st) {
   int bpc = (rpc + 31) / 32;  // ≥8 rows per wave
   if (bpc < 1) bpc = 1;
   if (bpc > 1024) bpc = 1024;
   hipLaunchKernelGGL(ln_bwd_kernel<NV>, dim3(bpc, C), dim3(256), 8 * d * sizeof(float), st, dy, x, mean, rstd, rpc,
-                     d, g, dx, dh, thr, dscale, seed, dg, db, seedp);
+                     d, g, dx, dh, thr, dscale, seed, dg, db, seedp, gcs, dgcs);
   return (int)hipGetLastError();
 }
 
@@ -622,28 +622,29 @@ int launch_attn_fwd(const uint16_t* q, int ldq, const uint16_t* k, int ldk, cons
 
 FA_EXPORT int fa_ln_fwd(const void* h, const void* res, int R, int d, int rows_per_client, const float* gamma,
                         const float* beta, float eps, uint32_t thr, float dscale, uint32_t seed, void* y, void* xsum,
-                        float* mean, float* rstd, const uint32_t* seedp, hipStream_t stream) {
-  if (d % 8 != 0 || d > 2048) return (int)hipErrorInvalidValue;
+                        float* mean, float* rstd, const uint32_t* seedp, int64_t gcs, hipStream_t stream) {
+  if (d % 8 != 0 || d > 2048 || gcs % 4 != 0) return (int)hipErrorInvalidValue;
   auto H = (const uint16_t*)h;
   auto Rs = (const uint16_t*)res;
   auto Y = (uint16_t*)y;
   auto X = (uint16_t*)xsum;
-  if (d <= 512) return launch_ln_fwd<1>(H, Rs, R, d, rows_per_client, gamma, beta, eps, thr, dscale, seed, seedp, Y, X, mean, rstd, stream);
-  if (d <= 1024) return launch_ln_fwd<2>(H, Rs, R, d, rows_per_client, gamma, beta, eps, thr, dscale, seed, seedp, Y, X, mean, rstd, stream);
-  return launch_ln_fwd<4>(H, Rs, R, d, rows_per_client, gamma, beta, eps, thr, dscale, seed, seedp, Y, X, mean, rstd, stream);
+  if (d <= 512) return launch_ln_fwd<1>(H, Rs, R, d, rows_per_client, gamma, beta, eps, thr, dscale, seed, seedp, Y, X, mean, rstd, gcs, stream);
+  if (d <= 1024) return launch_ln_fwd<2>(H, Rs, R, d, rows_per_client, gamma, beta, eps, thr, dscale, seed, seedp, Y, X, mean, rstd, gcs, stream);
+  return launch_ln_fwd<4>(H, Rs, R, d, rows_per_client, gamma, beta, eps, thr, dscale, seed, seedp, Y, X, mean, rstd, gcs, stream);
 }
 
 FA_EXPORT int fa_ln_bwd(const void* dy, const void* x, const float* mean, const float* rstd, int C,
                         int rows_per_client, int d, const float* gamma, void* dx, void* dh, uint32_t thr, float dscale,
-                        uint32_t seed, float* dgamma, float* dbeta, const uint32_t* seedp, hipStream_t stream) {
-  if (d % 8 != 0 || d > 2048) return (int)hipErrorInvalidValue;
+                        uint32_t seed, float* dgamma, float* dbeta, const uint32_t* seedp, int64_t gcs,
+                        int64_t dgcs, hipStream_t stream) {
+  if (d % 8 != 0 || d > 2048 || gcs % 4 != 0) return (int)hipErrorInvalidValue;
   auto DY = (const uint16_t*)dy;
   auto X = (const uint16_t*)x;
   auto DX = (uint16_t*)dx;
   auto DH = (uint16_t*)dh;
-  if (d <= 512) return launch_ln_bwd<1>(DY, X, mean, rstd, C, rows_per_client, d, gamma, DX, DH, thr, dscale, seed, seedp, dgamma, dbeta, stream);
-  if (d <= 1024) return launch_ln_bwd<2>(DY, X, mean, rstd, C, rows_per_client, d, gamma, DX, DH, thr, dscale, seed, seedp, dgamma, dbeta, stream);
-  return launch_ln_bwd<4>(DY, X, mean, rstd, C, rows_per_client, d, gamma, DX, DH, thr, dscale, seed, seedp, dgamma, dbeta, stream);
+  if (d <= 512) return launch_ln_bwd<1>(DY, X, mean, rstd, C, rows_per_client, d, gamma, DX, DH, thr, dscale, seed, seedp, dgamma, dbeta, gcs, dgcs, stream);
+  if (d <= 1024) return launch_ln_bwd<2>(DY, X, mean, rstd, C, rows_per_client, d, gamma, DX, DH, thr, dscale, seed, seedp, dgamma, dbeta, gcs, dgcs, stream);
+  return launch_ln_bwd<4>(DY, X, mean, rstd, C, rows_per_client, d, gamma, DX, DH, thr, dscale, seed, seedp, dgamma, dbeta, gcs, dgcs, stream);
 }
 
 FA_EXPORT int fa_gelu_fwd(const void* x, void* y, int64_t n, hipStream_t stream) {

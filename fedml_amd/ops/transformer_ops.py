@@ -76,6 +76,17 @@ def _ln_ref(h, res, gamma, beta, eps, p, seed, rpc):
     return y.view(R, d).to(h.dtype)
 
 
+def _client_rows(gamma, beta):
+    """(γ, β, client stride) for the LN kernels: per-client fp32 rows read in place when they are arena views
+    (contiguous rows, a common 16-B aligned client stride), else a dense [C, d] copy."""
+    if (gamma.dtype == torch.float32 and beta.dtype == torch.float32 and gamma.dim() == 2 and gamma[0].is_contiguous()
+            and beta[0].is_contiguous() and gamma.stride(0) == beta.stride(0) and gamma.stride(0) % 4 == 0
+            and gamma.data_ptr() % 16 == 0 and beta.data_ptr() % 16 == 0):
+        return gamma.detach(), beta.detach(), gamma.stride(0)
+    g = gamma.detach().float().contiguous()
+    return g, beta.detach().float().contiguous(), g.shape[-1]
+
+
 def _deterministic() -> bool:
     from ..utils import determinism
     return determinism.enabled()
@@ -90,36 +101,48 @@ class _LayerNorm(torch.autograd.Function):
         xsum = torch.empty_like(h) if fused else None
         mean = torch.empty(R, dtype=torch.float32, device=h.device)
         rstd = torch.empty(R, dtype=torch.float32, device=h.device)
-        g = gamma.detach().float().contiguous()
-        b = beta.detach().float().contiguous()
+        g, b, gcs = _client_rows(gamma, beta)
         name = "fa_ln_fwd" + _sfx(h)
         rc = _fn(name)(_p(h), _p(res), _c.c_int(R), _c.c_int(d), _c.c_int(rpc), _p(g), _p(b), _f(eps),
                        _c.c_uint32(_thr(p)), _f(1.0 / (1.0 - p) if p > 0 else 1.0), _c.c_uint32(seed & _M32),
-                       _p(y), _p(xsum), _p(mean), _p(rstd), _p(seed_dev), _stream(h))
+                       _p(y), _p(xsum), _p(mean), _p(rstd), _p(seed_dev), _i64(gcs), _stream(h))
         _check(rc, name)
         ctx.save_for_backward(xsum if fused else h, mean, rstd, g)
-        ctx.cfg = (p, seed, rpc, res is not None, fused, gamma.dtype)
+        ctx.cfg = (p, seed, rpc, res is not None, fused, gamma.dtype, gcs)
         ctx.seed_dev = seed_dev
+        # γ/β leaves with pre-assigned gradient-arena views: the backward kernel accumulates dγ/dβ into them
+        ctx.own = (gamma, beta) if (gamma.is_leaf and beta.is_leaf and gamma.grad is not None and beta.grad is not None
+                                    and gamma.grad.stride() == gamma.stride() and beta.grad.stride() == beta.stride()
+                                    and gamma.grad.stride(0) == beta.grad.stride(0)) else None
         return y
 
     @staticmethod
     def backward(ctx, dy):
         x, mean, rstd, g = ctx.saved_tensors
-        p, seed, rpc, has_res, fused, gdt = ctx.cfg
+        p, seed, rpc, has_res, fused, gdt, gcs = ctx.cfg
         seed_dev = ctx.seed_dev
         R, d = x.shape
         C = R // rpc
         dy = dy.to(x.dtype).contiguous()
         dres = torch.empty_like(x) if has_res else None
         dh = torch.empty_like(x)
-        dg = torch.zeros(C, d, dtype=torch.float32, device=x.device)
-        db = torch.zeros(C, d, dtype=torch.float32, device=x.device)
+        det = _deterministic()
+        own = ctx.own is not None and not det
+        if own:      # dγ/dβ atomically into the gradient arena rows (zeroed by the engine each step): no fill, no add
+            dg, db = ctx.own[0].grad, ctx.own[1].grad
+            dgcs = dg.stride(0)
+        else:
+            dg = torch.zeros(C, d, dtype=torch.float32, device=x.device)
+            db = torch.zeros(C, d, dtype=torch.float32, device=x.device)
+            dgcs = d
         name = "fa_ln_bwd" + _sfx(x)
         rc = _fn(name)(_p(dy), _p(x), _p(mean), _p(rstd), _c.c_int(C), _c.c_int(rpc), _c.c_int(d), _p(g),
                        _p(dres), _p(dh), _c.c_uint32(_thr(p)), _f(1.0 / (1.0 - p) if p > 0 else 1.0),
-                       _c.c_uint32(seed & _M32), _p(dg), _p(db), _p(seed_dev), _stream(x))
+                       _c.c_uint32(seed & _M32), _p(dg), _p(db), _p(seed_dev), _i64(gcs), _i64(dgcs), _stream(x))
         _check(rc, name)
-        if _deterministic():
+        if own:
+            return dh, dres, None, None, None, None, None, None, None
+        if det:
             # the kernel's dgamma/dbeta reduce rows with fp32 atomics (arrival order → last bit): recompute them
             # as fixed-order column sums (deterministic-mode only; the kernel's dh/dres are atomic-free)
             xf, dyf = x.float().view(C, rpc, d), dy.float().view(C, rpc, d)

@@ -170,10 +170,13 @@ class ClientBatchEngine:
         self._seq_bufs = None
         self._shadow = None            # bf16 copy of the params arena (transformer GEMM operand)
         self._shadow_stale = True
-        # opt-in: the eager transformer step is GPU-bound already (host launches run ahead), so the
-        # captured step measured the same rounds/s (scripts/gpu_tf_graph_ab.sh)
-        self._tf_capture = self.tf is not None and self.device.type == "cuda" and \
-            os.environ.get("FEDML_AMD_TF_GRAPHS", "0") == "1"
+        # transformers: opt-in (the eager step is GPU-bound already — host launches run ahead —, the captured step
+        # measured the same rounds/s, scripts/gpu_tf_graph_ab.sh); the batched LSTM is launch-bound (two launches
+        # per time step and direction): captured by default, 0.18 → 0.35 rounds/s on the Shakespeare preset
+        # (profiles/r4_bench_rnn_batched_vs_seq.jsonl)
+        from ...parallel.batched_rnn import BatchedRNN as _BRNN
+        tf_graphs = os.environ.get("FEDML_AMD_TF_GRAPHS", "1" if isinstance(self.tf, _BRNN) else "0") == "1"
+        self._tf_capture = self.tf is not None and self.device.type == "cuda" and tf_graphs
         self._active_cache = {}
         self._graphs = {}
         # task loss of the reference trainer this engine stands in for (core/alg_frame/functional.py):

@@ -81,6 +81,9 @@ def main():
     p.add_argument("--dtype", default="fp32", help="fp32 (the reference's precision) | bf16")
     p.add_argument("--wan-compression", default="", help="'' (fp32 state dicts, the reference) | int8")
     p.add_argument("--silo-transport", default="", help="'' (network payloads) | device (same-node HBM plane)")
+    p.add_argument("--server-cpu", action="store_true",
+                   help="server process without the GPU (network payloads only): 8 silos x 2 processes then stay "
+                        "within 16 GPU processes on a one-GPU box")
     p.add_argument("--timeout", type=float, default=900)
     p.add_argument("--stack-dump-s", type=float, default=90, help="workers dump their Python stacks this often")
     # worker-internal
@@ -103,7 +106,10 @@ def main():
         env["FEDML_AMD_DIST_BACKEND"] = "gloo"
     base = [sys.executable, os.path.abspath(__file__)] + [x for x in sys.argv[1:]]
     procs = []
-    procs.append(subprocess.Popen(base + ["--role", "server", "--out", out, "--gpu", "0"], env=env))
+    if a.server_cpu and a.silo_transport == "device":
+        raise SystemExit("bench_hier: the device data plane needs the server on the GPU")
+    senv = dict(env, HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="") if a.server_cpu else env
+    procs.append(subprocess.Popen(base + ["--role", "server", "--out", out, "--gpu", "0"], env=senv))
     i = 0
     for s in range(1, a.silos + 1):
         port = _free_port()

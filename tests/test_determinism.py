@@ -95,13 +95,15 @@ def test_deterministic_native_step_many_geometries():
         step = NativeResNetStep(model, layout, C, "cuda")
         step.enable_deterministic()
         outs = []
+        arena = flat.view(1, -1).repeat(C, 1).contiguous()     # one engine's arenas (their shape has no N)
+        garena = torch.zeros_like(arena)
         try:
             for N in (8, 7, 6, 5, 4, 3):      # the step's BN pivots carry over: the sequence is the unit
                 x = torch.randn(C, N, 3, 16, 16, device="cuda")
                 y = torch.randint(0, 10, (C, N), device="cuda")
                 rs = torch.full((C, N), 1.0 / N, device="cuda")
-                arena = flat.view(1, -1).repeat(C, 1).contiguous()
-                garena = torch.zeros_like(arena)
+                arena.copy_(flat.view(1, -1).expand(C, -1))
+                garena.zero_()
                 step.step(arena, garena, x, y, rs, torch.ones(C, device="cuda"))
                 outs.append(garena.clone())
             assert len(step._states) == 6 and len(step.det.targets) <= 8, len(step.det.targets)
