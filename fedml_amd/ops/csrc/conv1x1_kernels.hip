@@ -339,7 +339,11 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
   constexpr int KP = (CO + 31) / 32 * 32;            // dx GEMM depth (zero-padded to the MFMA K)
   // RY with CI < 32: the recompute GEMM's K is padded to 32 with zero columns of act(x) and zero rows of W
   constexpr int KCI = RY ? (CI + 31) / 32 * 32 : CI;
-  constexpr int LDD = P::pitch_tr(KP), LDX = P::pitch_tr(KCI), LDS_ = P::pitch(CI), LDW = KP + 8;
+  // weight tile pitch: the packed global rows are KP + 8 long; in LDS the fp32 rows take KP + 4 (≡ 4 mod 8 dwords:
+  // the 16 rows of a ds_read_b128 fragment read land on 16 distinct 4-bank groups — at KP + 8 rows r and r + 8
+  // shared banks, a 2-way conflict on every dgrad B fragment); bf16 rows keep KP + 8 (already ≡ 4 mod 8 dwords)
+  constexpr int LDWG = KP + 8, LDW = P::kF32 ? KP + 4 : KP + 8;
+  constexpr int LDD = P::pitch_tr(KP), LDX = P::pitch_tr(KCI), LDS_ = P::pitch(CI);
   constexpr int DCH = PT * CO / V, XCH = PT * CI / V;
   constexpr int DI = (DCH + NT - 1) / NT, XI = (XCH + NT - 1) / NT;
   constexpr int MT = PT / 16;                       // dx row tiles per stage
@@ -388,7 +392,15 @@ __global__ __launch_bounds__(64 * NW) void conv1x1_bwd_kernel(Args a) {
   {
     const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.wb) + (int64_t)c * a.wb_ld);
     uint4* dst = reinterpret_cast<uint4*>(wL);
-    for (int i = threadIdx.x; i < CI * LDW / V; i += NT) dst[i] = src[i];
+    if (LDW == LDWG) {
+      for (int i = threadIdx.x; i < CI * LDW / V; i += NT) dst[i] = src[i];
+    } else {      // re-pitched rows (K padding columns are never read: fragments stop at KP)
+      constexpr int RC = KP / V;   // 16-B chunks per row
+      for (int i = threadIdx.x; i < CI * RC; i += NT) {
+        const int r = i / RC, q = i - r * RC;
+        dst[r * (LDW / V) + q] = src[r * (LDWG / V) + q];
+      }
+    }
   }
   if (KP > CO)  // zero K-padding columns of the dy tile (never rewritten by the stage stores)
     for (int i = threadIdx.x; i < PT * (KP - CO); i += NT) dyL[(i / (KP - CO)) * LDD + CO + i % (KP - CO)] = 0;

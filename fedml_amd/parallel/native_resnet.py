@@ -442,8 +442,7 @@ class NativeResNetStep:
             return
         if lz is not None and lz[0] is not None and cv.cout % 128 == 0:
             # the wide weight-gradient kernel (Cout % 128 == 0) takes no deferred descriptor: finalise explicitly
-            self._pending[(bn_key, "b")] = self._pending_closure
-            self._flush(bn_key, "b")
+            self._pending_closure()          # (its statistics are already flushed in deterministic mode)
             lz = None
         nn_ops.conv_wgrad(g, y, vec[4], vec[5], vec[6], x, ps, pt, garena, self.off[cv.key], C, N, cv.H, cv.W,
                           cv.cin_pad, cv.Ho, cv.Wo, cv.cout, cv.k, cv.k, cv.stride, cv.pad, self._pix_per_wg(M), cv.cin,
@@ -524,7 +523,7 @@ class NativeResNetStep:
                 self.det.flush(fst)
             nn_ops.bn_fwd_finalize(fst, self.C, bn.ch, float(N * hw), arena, g, b, rm, rv, nbt, bn.momentum, bn.eps,
                                    active, v[0], v[1], v[2], v[3], training, pivot=v[7], nimg=self._nimg, hw=hw)
-        self._defer((bn.key, "f"), explicit)
+        self._defer((bn.key, "f"), explicit, fst)
 
     def _bn_bwd(self, bn, q, N, hw, arena, garena):
         v = self.bn_vec[bn.key]
@@ -536,20 +535,22 @@ class NativeResNetStep:
                 self.det.flush(bst)
             nn_ops.bn_bwd_finalize(bst, 3, q, self.C, bn.ch, float(N * hw), v[2], v[3], arena, garena, g, b, v[4],
                                    v[5], v[6], nimg=self._nimg, hw=hw)
-        self._defer((bn.key, "b"), explicit)
+        self._defer((bn.key, "b"), explicit, bst)
 
     # ------------------------------------------------------------------ deferred BN finalisation
     def _lazy_on(self):
-        return self.use_lazy and self.det is None
+        # deterministic mode keeps the explicit finalisation (FEDML_AMD_BN_LAZY_DET=1 defers there too, flushing
+        # the statistics' fixed-point shadow right before the consumer: under investigation, gradients differ)
+        return self.use_lazy and (self.det is None or os.environ.get("FEDML_AMD_BN_LAZY_DET", "0") == "1")
 
-    def _defer(self, key, explicit):
+    def _defer(self, key, explicit, stats):
         """Explicit finalisation now, or (lazy mode) left to the first consumer kernel of the BN's vectors."""
         if not self._lazy_on():
             explicit()
             return
         if key in self._pending:      # a BN finalised twice without a consumer in between: keep the order
-            self._pending.pop(key)()
-        self._pending[key] = explicit
+            self._pending.pop(key)[0]()
+        self._pending[key] = (explicit, stats)
 
     def _take(self, bn_key, kind):
         """Device pointer of the pending BN's descriptor for the consumer about to launch (None: nothing pending,
@@ -557,17 +558,20 @@ class NativeResNetStep:
         key = (bn_key, kind)
         if bn_key is None or key not in self._pending:
             return None
-        self._pending_closure = self._pending.pop(key)
+        explicit, stats = self._pending.pop(key)
+        self._pending_closure = explicit
+        if self.det is not None:
+            self.det.flush(stats)
         return self._lz_dev.data_ptr() + self._lz_slot[key] * ctypes.sizeof(nn_ops.BnLazy)
 
     def _flush(self, bn_key, kind):
         key = (bn_key, kind)
         if bn_key is not None and key in self._pending:
-            self._pending.pop(key)()
+            self._pending.pop(key)[0]()
 
     def _flush_all(self):
         for key in list(self._pending):
-            self._pending.pop(key)()
+            self._pending.pop(key)[0]()
 
     def _lz_prepare(self, arena, garena, active, N):
         """Descriptors of every BN (forward + backward) for this geometry and these buffers, uploaded only when

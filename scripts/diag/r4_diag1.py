@@ -75,9 +75,11 @@ def resnet_geometry():
     xs = torch.randn(C, 8, 3, 16, 16, device="cuda")
     ys = torch.randint(0, 10, (C, 8), device="cuda")
 
-    def run(N, nv, lazy):
+    def run(N, nv, lazy, det=False):
         step = NativeResNetStep(model, layout, C, "cuda")
         step.use_lazy = lazy
+        if det:
+            step.enable_deterministic()
         arena = flat.view(1, -1).repeat(C, 1).contiguous()
         garena = torch.zeros_like(arena)
         x = xs[:, :N].contiguous()
@@ -86,8 +88,13 @@ def resnet_geometry():
         nimg = torch.full((C,), nv, dtype=torch.int32, device="cuda")
         loss = step.step(arena, garena, x, y, rs.contiguous(), torch.ones(C, device="cuda"), nimg=nimg)
         torch.cuda.synchronize()
+        step.close()
         return float(loss), garena, arena
 
+    _, gd1, ad1 = run(5, 5, True, det=True)
+    _, gd0, ad0 = run(5, 5, False, det=True)
+    print(f"resnet deterministic lazy-vs-explicit: grad bitwise {torch.equal(gd1, gd0)} arena bitwise "
+          f"{torch.equal(ad1, ad0)} (rel {rel(gd1, gd0):.3e})")
     l5, g5, a5 = run(5, 5, True)
     l8, g8, a8 = run(8, 5, True)
     l5e, g5e, a5e = run(5, 5, False)
@@ -99,4 +106,3 @@ def resnet_geometry():
 
 if __name__ == "__main__":
     resnet_geometry()
-    mobilenet_grads()

@@ -272,9 +272,11 @@ def _masked_fp64_grads(step, layout, flat, x, y, masks):
     (lambda: ResNet(BasicBlock, [2, 1, 1], 10), 16),
     (lambda: ResNet(Bottleneck, [2, 2, 2], 100), 32),
 ])
-def test_native_step_f32_matches_reference(builder, hw):
-    """The fp32 native step (deterministic mode: bit-reproducible) against an fp64 step that uses the native
-    step's OWN ReLU masks.
+@pytest.mark.parametrize("det", [False, True], ids=["lazy_bn", "det_explicit_bn"])
+def test_native_step_f32_matches_reference(builder, hw, det):
+    """The fp32 native step against an fp64 step that uses the native step's OWN ReLU masks — both in the
+    production configuration (deferred BN finalisation folded into the consumer kernels, fp32 atomics) and in
+    deterministic mode (fixed-point cross-workgroup sums, explicit BN finalisation).
 
     A ReLU pre-activation within rounding of 0 makes its mask — and every upstream gradient — depend on the
     last bits of the BN scale/shift: one such flip moves gradients of these random-init nets by 1e-4..1e-2
@@ -296,7 +298,9 @@ def test_native_step_f32_matches_reference(builder, hw):
     row_scale = torch.full((C, N), 1.0 / N, device=DEV)
     active = torch.ones(C, device=DEV)
     step = NativeResNetStep(model, layout, C, DEV, dtype=F32)
-    step.enable_deterministic()
+    if det:
+        step.enable_deterministic()
+    assert step._lazy_on() == (not det)
     try:
         assert step.dtype == F32
         loss = float(step.step(arena, garena, x, y, row_scale, active))

@@ -67,37 +67,87 @@ def test_plane_batch_norm_matches_torch(relu, HW, B):
     assert _rel(g.grad, gr.grad) < 1e-4 and _rel(b.grad, br.grad) < 1e-5
 
 
-def test_mobilenet_round_native_equals_torch_engine(monkeypatch):
-    """One local epoch of 10 MobileNet / CIFAR-10 clients: the native path (plane depthwise + plane BN/ReLU +
-    implicit-GEMM pointwise / stem convolutions, no MIOpen convolution) equals the engine on PyTorch ops."""
-    from fedml_amd.arguments import Arguments
+def test_mobilenet_step_native_within_fp32_envelope():
+    """One MobileNet / CIFAR-10 step of 2 clients in the batched interpreter on the native kernels (plane
+    depthwise + plane BN/ReLU + implicit-GEMM pointwise / stem convolutions: no MIOpen) and on PyTorch ops,
+    both against a per-client fp64 nn.Module step. MobileNet at init sits on ReLU thresholds, so ANY fp32
+    implementation's gradients move by ~1e-2 on some slots (mask flips; measured: PyTorch fp32 max 8.3e-3,
+    median 3.9e-3). The native step must stay within 3× PyTorch fp32's own error on the same inputs (max and
+    median over slots) and its logits within 1e-4 of fp64."""
+    import copy
+    from fedml_amd.core.arena import ParamLayout
     from fedml_amd.models.cv.mobilenet import mobilenet
     from fedml_amd.parallel import batched_nn
+    torch.manual_seed(0)
+    model = mobilenet(10).to(DEV)
+    C, B = 2, 16
+    layout = ParamLayout.from_module(model)
+    x = torch.randn(C, B, 3, 32, 32, device=DEV)
+    y = torch.randint(0, 10, (C, B), device=DEV)
+    flat = layout.flatten(model.state_dict(), device=DEV)
+
+    def run(native):
+        saved = batched_nn._NATIVE_BCONV
+        batched_nn._NATIVE_BCONV = native
+        try:
+            params = layout.alloc_stack(C, DEV)
+            grads = layout.alloc_stack(C, DEV)
+            params.copy_(flat.view(1, -1).expand(C, -1))
+            views = {}
+            for s in layout.slots:
+                v = params[:, s.offset:s.offset + s.numel].view(C, *s.shape)
+                if s.trainable:
+                    v = v.detach().requires_grad_(True)
+                    v.grad = grads[:, s.offset:s.offset + s.numel].view(C, *s.shape)
+                views[s.key] = v
+            out = batched_nn.BatchedInterpreter(model, layout, C).run(views, x, training=True)
+            sum(F.cross_entropy(out[c], y[c]) for c in range(C)).backward()
+            torch.cuda.synchronize()
+            return out.detach(), grads.clone()
+        finally:
+            batched_nn._NATIVE_BCONV = saved
+
+    o_nat, g_nat = run(True)
+    o_t32, g_t32 = run(False)
+    ref = torch.zeros(C, layout.size, dtype=torch.float64, device=DEV)
+    o64 = []
+    for c in range(C):
+        m = copy.deepcopy(model).double().train()
+        out = m(x[c].double())
+        o64.append(out.detach())
+        F.cross_entropy(out, y[c]).backward()
+        for k, p in m.named_parameters():
+            sl = layout.slot(k)
+            ref[c, sl.offset:sl.offset + sl.numel] = p.grad.reshape(-1)
+    assert _rel(o_nat, torch.stack(o64)) < 1e-4
+    e_nat, e_t32 = [], []
+    for sl in layout.slots:
+        if sl.trainable:
+            r = slice(sl.offset, sl.offset + sl.numel)
+            e_nat.append(_rel(g_nat[:, r], ref[:, r]))
+            e_t32.append(_rel(g_t32[:, r], ref[:, r]))
+    med = lambda v: sorted(v)[len(v) // 2]   # noqa: E731
+    assert max(e_nat) <= 3 * max(e_t32) + 1e-5, (max(e_nat), max(e_t32))
+    assert med(e_nat) <= 3 * med(e_t32) + 1e-6, (med(e_nat), med(e_t32))
+
+
+def test_mobilenet_engine_round_runs_native_and_learns(monkeypatch):
+    """The engine's default (auto) path for MobileNet is the batched interpreter on the native kernels, and a
+    few rounds on a learnable synthetic task lower the loss."""
+    from fedml_amd.arguments import Arguments
+    from fedml_amd.models.cv.mobilenet import mobilenet
     from fedml_amd.simulation.rccl.client_store import DeviceClientStore
     from fedml_amd.simulation.rccl.engine import ClientBatchEngine
     torch.manual_seed(0)
     model = mobilenet(10)
-    K, n, bs = 10, 32, 16
-    store = DeviceClientStore(torch.randn(K * n, 3, 32, 32, device=DEV), torch.randint(0, 10, (K * n,), device=DEV),
-                              [c * n for c in range(K)], [n] * K)
-    args = Arguments.from_dict({"x": {"client_optimizer": "sgd", "learning_rate": 0.01, "weight_decay": 0.001,
-                                      "client_exec": "batched"}})
-
-    def run(native):
-        monkeypatch.setattr(batched_nn, "_NATIVE_BCONV", native)
-        eng = ClientBatchEngine(copy.deepcopy(model).to(DEV), K, DEV, args, compute_dtype=None)
-        assert eng.interp is not None and not eng.sequential
-        eng.load_global(eng.layout.flatten(model.state_dict(), device=DEV))
-        eng.train(store, torch.arange(K, device=DEV), 1, bs, 0.01, shuffle=False)
-        torch.cuda.synchronize()
-        out = eng.params.clone()
-        eng.close()
-        return out
-
-    from fedml_amd.core.arena import ParamLayout
-    init = ParamLayout.from_module(model).flatten(model.state_dict(), device=DEV)
-    nat, ref = run(True), run(False)
-    assert torch.isfinite(nat).all()
-    # relative to the round's update (the parameters themselves are much larger than one epoch's change)
-    err = float((nat - ref).double().norm() / (ref - init).double().norm())
-    assert err < 1e-3, err
+    K, n, bs = 4, 32, 16
+    yl = torch.randint(0, 10, (K * n,), device=DEV)
+    xs = torch.randn(K * n, 3, 32, 32, device=DEV) * 0.5 + yl.view(-1, 1, 1, 1).float() / 5
+    store = DeviceClientStore(xs, yl, [c * n for c in range(K)], [n] * K)
+    args = Arguments.from_dict({"x": {"client_optimizer": "sgd", "learning_rate": 0.05}})
+    eng = ClientBatchEngine(model.to(DEV), K, DEV, args, compute_dtype=None)
+    assert eng.interp is not None and not eng.sequential
+    eng.load_global(eng.layout.flatten(model.state_dict(), device=DEV))
+    losses = [float(eng.train(store, torch.arange(K, device=DEV), 1, bs, 0.05, shuffle=False)) for _ in range(4)]
+    eng.close()
+    assert losses[-1] < losses[0], losses
