@@ -539,9 +539,9 @@ class NativeResNetStep:
 
     # ------------------------------------------------------------------ deferred BN finalisation
     def _lazy_on(self):
-        # deterministic mode keeps the explicit finalisation (FEDML_AMD_BN_LAZY_DET=1 defers there too, flushing
-        # the statistics' fixed-point shadow right before the consumer: under investigation, gradients differ)
-        return self.use_lazy and (self.det is None or os.environ.get("FEDML_AMD_BN_LAZY_DET", "0") == "1")
+        # deterministic mode defers too (FEDML_AMD_BN_LAZY_DET=0: explicit there): the statistics' fixed-point
+        # shadow is rounded into them right before the consumer that folds them
+        return self.use_lazy and (self.det is None or os.environ.get("FEDML_AMD_BN_LAZY_DET", "1") != "0")
 
     def _defer(self, key, explicit, stats):
         """Explicit finalisation now, or (lazy mode) left to the first consumer kernel of the BN's vectors."""
@@ -758,6 +758,10 @@ class NativeResNetStep:
             self._bn_bwd(lbn, 1, N, hw_last, arena, garena)
             if b.ds_bn is not None:
                 # the shortcut BN sees the same g: its (Σg, Σg·yd) live in slots 0 and 2 of lbn's stats
+                # (deterministic mode: round lbn's fixed-point shadow into them first — with deferred
+                # finalisation nothing has flushed it yet)
+                if self.det is not None:
+                    self.det.flush(self.stat_views[lbn.key][1])
                 self.stat_views[b.ds_bn.key][1].copy_(self.stat_views[lbn.key][1])
                 self._bn_bwd(b.ds_bn, 2, N, b.ds_conv.Ho * b.ds_conv.Wo, arena, garena)
             free = [t for t in bufs if t is not gpre]           # three buffers besides gpre

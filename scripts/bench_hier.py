@@ -41,6 +41,12 @@ def worker(a):
     sys.path.insert(0, ROOT)
     import fedml_amd
     from fedml_amd.arguments import Arguments
+    # --server-cpu: the server never initialises HIP — torch.cuda.is_available() alone opens the device (one more
+    # GPU process), so the probes the framework makes answer "no GPU" without asking the runtime
+    if a.role == "server" and a.server_cpu:
+        torch.cuda.is_available = lambda: False
+        torch.cuda.device_count = lambda: 0
+    use_gpu = torch.cuda.is_available()
     cfg = {"training_type": "cross_silo", "scenario": "hierarchical", "dataset": a.dataset, "model": a.model,
            "client_num_in_total": a.silos, "client_num_per_round": a.silos, "comm_round": a.rounds + a.warmup,
            "epochs": 1, "batch_size": a.batch_size, "learning_rate": a.lr, "client_optimizer": "adamw",
@@ -50,7 +56,7 @@ def worker(a):
            "synthetic_test_samples_per_client": 8, "partition_method": "homo", "rank": a.silo,
            "n_proc_in_silo": a.procs_per_silo, "proc_rank_in_silo": a.rank_in_silo, "pg_master_port": a.pg_port,
            "silo_local_clients": a.local_clients, "compute_dtype": a.dtype,
-           "using_gpu": torch.cuda.is_available(), "gpu_id": a.gpu, "rank_in_node": a.gpu,
+           "using_gpu": use_gpu, "gpu_id": a.gpu, "rank_in_node": a.gpu,
            "wan_compression": a.wan_compression, "silo_transport": a.silo_transport, "random_seed": 0}
     args = fedml_amd.init(Arguments.from_dict({"x": cfg}))
     dev, ds, m = fedml_amd._prepare(args)
@@ -62,7 +68,7 @@ def worker(a):
                    "wan_bytes": getattr(srv.manager, "wan_bytes", None)}, open(a.out, "w"))
     else:
         Client(args, dev, ds, m).run()
-        if torch.cuda.is_available():
+        if use_gpu:
             torch.cuda.synchronize()
 
 
@@ -96,8 +102,10 @@ def main():
     a = p.parse_args()
     if a.role:
         return worker(a)
-    import torch
-    ngpu = max(1, torch.cuda.device_count())
+    # GPU count from a short-lived child: this launcher process must not hold the device (the box allows 16 GPU
+    # processes; 8 silos x 2 processes use all of them)
+    ngpu = max(1, int(subprocess.check_output([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                                              text=True).strip().splitlines()[-1]))
     out = os.path.join(ROOT, "gpurun_out", "bench_hier_server.json")
     os.makedirs(os.path.dirname(out), exist_ok=True)
     env = dict(os.environ, PYTHONPATH=ROOT, FEDML_TCP_BASE_PORT=str(_free_port()), HSA_ENABLE_IPC_MODE_LEGACY="0",
@@ -139,7 +147,7 @@ def main():
                       f" {a.model})",
             "value": round(len(rt) / t, 4), "unit": "rounds/s", "n_gpus": ngpu, "steps": len(rt), "warmup": a.warmup,
             "ms_per_step": round(1000 * t / len(rt), 1), "higher_is_better": True, "scaling": "strong",
-            "vs_baseline": None, "dtype": a.dtype if torch.cuda.is_available() else "fp32",
+            "vs_baseline": None, "dtype": a.dtype,
             "data": f"synthetic ({a.dataset}-shaped), random-init weights",
             "config": {"model": a.model, "silos": a.silos, "local_clients_per_silo": a.local_clients,
                        "procs_per_silo": a.procs_per_silo, "samples_per_client": a.samples_per_client,
