@@ -20,6 +20,7 @@
 //               straight into the client-stacked gradient arena (OIHW positions, stride ldw).
 // MFMA: v_mfma_f32_16x16x32_bf16. Lane l holds A[row l&15][k 8(l>>4)..+7], B[k 8(l>>4)..+7][col l&15];
 // D: col = l&15, row = 4(l>>4) + i.
+#include "lds_swz.h"
 #include "prec.h"
 #include "detacc.h"
 #include "bnlazy.h"
@@ -261,8 +262,10 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
   if ((int)(blockIdx.x * 4 * a.tiles_per_wave) * 16 >= Mv) return;   // uniform: whole workgroup idle
 
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  T* wl = reinterpret_cast<T*>(smem);                                            // [NOUT][ldk]
-  float* v0 = reinterpret_cast<float*>(smem + (size_t)NOUT * a.ldk * P::ES);    // [KC]
+  // fp32: the weight slice is staged as the bank-conflict-free swizzled image of lds_swz.h
+  const int wl_ld = P::kF32 ? lswz::pitch(a.Kp) : a.ldk;
+  T* wl = reinterpret_cast<T*>(smem);                                            // [NOUT][wl_ld]
+  float* v0 = reinterpret_cast<float*>(smem + (size_t)NOUT * wl_ld * P::ES);    // [KC]
   float* v1 = v0 + a.KC;
   float* v2 = v1 + a.KC;
   float* v3 = v2 + a.KC;
@@ -272,11 +275,16 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
 
   // ---- stage packed weights (16-B copies) and per-channel vectors ----
   {
-    const uint4* src = reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.wpk) + (int64_t)c * a.wpk_ld +
-                                                      (int64_t)ch_base * a.ldk);
-    uint4* dst = reinterpret_cast<uint4*>(wl);
-    const int n16 = NOUT * a.ldk / V;
-    for (int i = threadIdx.x; i < n16; i += 256) dst[i] = src[i];
+    const T* wsrc = reinterpret_cast<const T*>(a.wpk) + (int64_t)c * a.wpk_ld + (int64_t)ch_base * a.ldk;
+    if constexpr (P::kF32) {
+      lswz::stage(reinterpret_cast<float*>(wl), reinterpret_cast<const float*>(wsrc), a.ldk, NOUT, a.Kp, threadIdx.x,
+                  256);
+    } else {
+      const uint4* src = reinterpret_cast<const uint4*>(wsrc);
+      uint4* dst = reinterpret_cast<uint4*>(wl);
+      const int n16 = NOUT * a.ldk / V;
+      for (int i = threadIdx.x; i < n16; i += 256) dst[i] = src[i];
+    }
     if (AOP == AOP_DY || PRO != PRO_NONE) {
       for (int i = threadIdx.x; i < a.KC; i += 256) {
         if (PRO != PRO_NONE && a.lz0) {
@@ -448,7 +456,14 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
       const frag_t afrag = P::frag8(f);
 #pragma unroll
       for (int nt = 0; nt < NT; ++nt) {
-        const frag_t bv = P::frag(wl + (nt * 16 + (lane & 15)) * a.ldk + k0 + 8 * (lane >> 4));
+        frag_t bv;
+        if constexpr (P::kF32) {
+          float wf[8];
+          lswz::load8(reinterpret_cast<const float*>(wl), a.Kp, nt * 16 + (lane & 15), k0 + 8 * (lane >> 4), wf);
+          bv = P::frag8(wf);
+        } else {
+          bv = P::frag(wl + (nt * 16 + (lane & 15)) * a.ldk + k0 + 8 * (lane >> 4));
+        }
         acc[nt] = P::mma(afrag, bv, acc[nt]);
       }
     }
@@ -583,7 +598,8 @@ __global__ __launch_bounds__(256) void conv_gemm_kernel(ConvArgs a) {
 }
 
 template <class P>
-static size_t conv_smem_bytes(int nout, int ldk, int kc) {
+static size_t conv_smem_bytes(int nout, int ldk, int kc, int Kp) {
+  if (P::kF32) ldk = lswz::pitch(Kp);   // the swizzled weight image (lds_swz.h)
   return (size_t)nout * ldk * P::ES + (size_t)4 * kc * 4 + (size_t)4 * nout * 3 * 4 + (size_t)4 * 16 * nout * P::ES;
 }
 
@@ -1012,7 +1028,7 @@ static int launch_conv(ConvArgs a, int nout, int C, hipStream_t stream) {
   const int tiles = (M + 15) / 16;
   const int per_wg = 4 * a.tiles_per_wave;
   const int gx = (tiles + per_wg - 1) / per_wg;
-  const size_t smem = conv_smem_bytes<P>(NT * 16, a.ldk, a.KC);
+  const size_t smem = conv_smem_bytes<P>(NT * 16, a.ldk, a.KC, a.Kp);
   if (smem > 160 * 1024) return -5;
   auto kern = conv_gemm_kernel<P, NT, AOP, PRO, MODE, EPI>;
   if (smem > 64 * 1024) hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
@@ -1035,8 +1051,10 @@ static int dispatch_nt(int nout, const ConvArgs& a, int C, hipStream_t s) {
     case 128:
     case 256:
       // 64-channel slices; narrower when the packed-weight slice would not fit the LDS (fp32, K ≥ 576)
-      if (conv_smem_bytes<P>(64, a.ldk, a.KC) <= 160 * 1024) return launch_conv<P, 4, AOP, PRO, MODE, EPI>(a, nout, C, s);
-      if (conv_smem_bytes<P>(32, a.ldk, a.KC) <= 160 * 1024) return launch_conv<P, 2, AOP, PRO, MODE, EPI>(a, nout, C, s);
+      if (conv_smem_bytes<P>(64, a.ldk, a.KC, a.Kp) <= 160 * 1024)
+        return launch_conv<P, 4, AOP, PRO, MODE, EPI>(a, nout, C, s);
+      if (conv_smem_bytes<P>(32, a.ldk, a.KC, a.Kp) <= 160 * 1024)
+        return launch_conv<P, 2, AOP, PRO, MODE, EPI>(a, nout, C, s);
       return launch_conv<P, 1, AOP, PRO, MODE, EPI>(a, nout, C, s);
     default: return -2;
   }
@@ -1091,7 +1109,7 @@ static int conv_fwd_bout(const void* x, const void* wpk, int64_t wpk_ld, const f
   a.e_s = s; a.e_t = t; a.pivot = pivot; a.e_add = res; a.e_rs = rs; a.e_rt = rt; a.nimg = nimg;
   a.Nb = Nb; a.Hs = H; a.Ws = W; a.KC = Cin; a.Ho = H; a.Wo = W; a.KH = 1; a.KW = 1; a.stride = 1;
   a.pad = 0; a.ldk = ldk; a.Kp = (Cin + 31) / 32 * 32; a.tiles_per_wave = tiles_per_wave;
-  if (conv_smem_bytes<P>(64, a.ldk, a.KC) > 160 * 1024) return -5;
+  if (conv_smem_bytes<P>(64, a.ldk, a.KC, a.Kp) > 160 * 1024) return -5;
   return launch_conv<P, 4, AOP_ACT, PRO_BNRELU, MODE_FWD, EPI_BOUT>(a, Cout, C, stream);
 }
 

@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Which PyTorch ops launch the non-native ("at::native") kernels of a bench preset: runs bench.py's
+configuration with the timed rounds under torch.profiler (HIP graphs off, so every kernel is attributed to
+the op that launched it) and prints the ops by self device time.
+
+    FEDML_AMD_HIP_GRAPHS=0 python scripts/torch_op_prof.py --preset distilbert_fedopt_32 [--rows 40]
+"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--preset", default="distilbert_fedopt_32")
+    ap.add_argument("--rows", type=int, default=40)
+    a, rest = ap.parse_known_args()
+    import torch
+    import bench
+    from fedml_amd.simulation.rccl import simulator as S
+    orig = S.RCCLSimulator.run
+    state = {"n": 0}
+
+    def run(self, n):
+        state["n"] += 1
+        if state["n"] == 1:        # warmup round (bench --warmup 1)
+            return orig(self, n)
+        acts = [torch.profiler.ProfilerActivity.CPU, torch.profiler.ProfilerActivity.CUDA]
+        with torch.profiler.profile(activities=acts) as prof:
+            r = orig(self, n)
+            torch.cuda.synchronize()
+        print(prof.key_averages().table(sort_by="self_cuda_time_total", row_limit=a.rows, max_name_column_width=60),
+              flush=True)
+        return r
+
+    S.RCCLSimulator.run = run
+    sys.argv = ["bench.py", "--preset", a.preset, "--steps", "1", "--warmup", "1"] + rest
+    bench.main()
+
+
+if __name__ == "__main__":
+    main()
