@@ -102,9 +102,11 @@ __global__ __launch_bounds__(256) void dw_bwd_data_kernel(const T* __restrict__ 
 
 // one workgroup per stacked channel: dw[cc][tap] = Σ_b Σ_(oy,ox) dy·x (fixed per-thread order + fixed tree)
 template <typename T, int K, int S>
+// dw: dense [CC][K·K] (ocs = 0) or, ocs > 0, accumulated (+=) into client c = cc / Ch's gradient-arena rows
+// [Ch][K·K] at dw + c·ocs (single writer per element: no atomics, deterministic)
 __global__ __launch_bounds__(256) void dw_wgrad_kernel(const T* __restrict__ dy, const T* __restrict__ x,
                                                        float* __restrict__ dw, int B, int CC, int H, int W, int Ho,
-                                                       int Wo) {
+                                                       int Wo, int Ch, int64_t ocs) {
   constexpr int P = K / 2, KK = K * K;
   __shared__ float red[4][KK];
   const int cc = blockIdx.x;
@@ -136,8 +138,13 @@ __global__ __launch_bounds__(256) void dw_wgrad_kernel(const T* __restrict__ dy,
     if (lane == 0) red[wv][t] = s;
   }
   __syncthreads();
-  for (int t = threadIdx.x; t < KK; t += 256)
-    dw[(int64_t)cc * KK + t] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+  for (int t = threadIdx.x; t < KK; t += 256) {
+    const float v = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+    if (ocs > 0)
+      dw[(int64_t)(cc / Ch) * ocs + (int64_t)(cc % Ch) * KK + t] += v;
+    else
+      dw[(int64_t)cc * KK + t] = v;
+  }
 }
 
 // ---- BatchNorm over planes: channel cc's elements are B planes of HW at stride CC·HW ----
@@ -150,9 +157,21 @@ __device__ __forceinline__ float block_sum4(float v, float* sh) {
   return (sh[0] + sh[1]) + (sh[2] + sh[3]);
 }
 
+// running statistics of the BN's arena rows (client stride rcs), updated like torch's training-mode BN
+// (momentum, unbiased variance, num_batches_tracked) for active clients; null rm: no update
+struct PbnRun {
+  float* rm;
+  float* rv;
+  float* nbt;
+  int64_t rcs;
+  float momentum;
+  const float* active;
+  int Ch;
+};
+
 template <typename T>
 __global__ __launch_bounds__(256) void pbn_stats_kernel(const T* __restrict__ x, float* __restrict__ mean,
-                                                        float* __restrict__ var, int B, int CC, int HW) {
+                                                        float* __restrict__ var, int B, int CC, int HW, PbnRun run) {
   __shared__ float sh[4];
   const int cc = blockIdx.x;
   const float k = ld<T>(x + (int64_t)cc * HW);      // shift: the channel's first element (cancellation guard)
@@ -168,8 +187,19 @@ __global__ __launch_bounds__(256) void pbn_stats_kernel(const T* __restrict__ x,
   const float S2 = block_sum4(s2, sh);
   if (threadIdx.x == 0) {
     const float m = S / n;
-    mean[cc] = k + m;
-    var[cc] = fmaxf(S2 / n - m * m, 0.f);
+    const float mu = k + m, v = fmaxf(S2 / n - m * m, 0.f);
+    mean[cc] = mu;
+    var[cc] = v;
+    if (run.rm) {
+      const int c = cc / run.Ch, ch = cc - c * run.Ch;
+      if (!run.active || run.active[c] > 0.f) {
+        const int64_t o = (int64_t)c * run.rcs + ch;
+        const float mom = run.momentum;
+        run.rm[o] = (1.f - mom) * run.rm[o] + mom * mu;
+        run.rv[o] = (1.f - mom) * run.rv[o] + mom * (v * (n / fmaxf(n - 1.f, 1.f)));
+        if (run.nbt && ch == 0) run.nbt[(int64_t)c * run.rcs] += 1.f;
+      }
+    }
   }
 }
 
@@ -205,7 +235,8 @@ __global__ __launch_bounds__(256) void pbn_bwd_red_kernel(const T* __restrict__ 
                                                           const float* __restrict__ g, const float* __restrict__ bb,
                                                           int64_t pcs, const float* __restrict__ mean,
                                                           const float* __restrict__ var, float eps, int relu,
-                                                          float* __restrict__ red, int B, int CC, int Ch, int HW) {
+                                                          float* __restrict__ red, int B, int CC, int Ch, int HW,
+                                                          float* __restrict__ dg, float* __restrict__ db, int64_t dcs) {
   __shared__ float sh[4];
   const int cc = blockIdx.x;
   float s, t;
@@ -226,6 +257,10 @@ __global__ __launch_bounds__(256) void pbn_bwd_red_kernel(const T* __restrict__ 
   if (threadIdx.x == 0) {
     red[2 * cc] = A;
     red[2 * cc + 1] = Cs;
+    // dγ = Σg'·x̂ = rs·Σg'(x − μ), dβ = Σg' straight into the gradient arena rows (single writer per element)
+    const int64_t o = (int64_t)(cc / Ch) * dcs + cc % Ch;
+    if (dg) dg[o] += Cs * rsqrtf(var[cc] + eps);
+    if (db) db[o] += A;
   }
 }
 
@@ -266,7 +301,7 @@ int dw_dispatch(int op, const void* a, const void* b, const float* w, int64_t wc
                          (const T*)a, w, wcs, (T*)out, B, CC, Ch, H, W, Ho, Wo);                                   \
     else                                                                                                           \
       hipLaunchKernelGGL((dw_wgrad_kernel<T, KK_, SS_>), dim3(CC), dim3(256), 0, st, (const T*)a, (const T*)b,     \
-                         (float*)out, B, CC, H, W, Ho, Wo);                                                        \
+                         (float*)out, B, CC, H, W, Ho, Wo, Ch, wcs);                                               \
     return (int)hipGetLastError();                                                                                 \
   }
   DW_CASE(3, 1) DW_CASE(3, 2) DW_CASE(5, 1) DW_CASE(5, 2) DW_CASE(7, 1) DW_CASE(7, 2)
@@ -276,8 +311,10 @@ int dw_dispatch(int op, const void* a, const void* b, const float* w, int64_t wc
 
 }  // namespace pk
 
-// op 0: y = dw_fwd(x=a); 1: dx = dw_bwd_data(dy=a); 2: dw [CC][K·K] = dw_wgrad(dy=a, x=b). w: fp32 arena view of
-// client 0's [Ch][1][K][K] rows, client stride wcs. Pad = K/2 (the reference's depthwise layers). is_bf16: T.
+// op 0: y = dw_fwd(x=a); 1: dx = dw_bwd_data(dy=a); 2: dw [CC][K·K] = dw_wgrad(dy=a, x=b), or with wcs > 0
+// dw += into client-strided gradient-arena rows (out = client 0's [Ch][1][K][K] grad rows, client stride wcs).
+// w: fp32 arena view of client 0's [Ch][1][K][K] rows, client stride wcs. Pad = K/2 (the reference's depthwise
+// layers). is_bf16: T.
 FA_EXPORT int fa_dwconv(int op, int is_bf16, const void* a, const void* b, const float* w, int64_t wcs, void* out,
                         int B, int CC, int Ch, int H, int W, int Ho, int Wo, int K, int S, hipStream_t stream) {
   if (is_bf16) return pk::dw_dispatch<uint16_t>(op, a, b, w, wcs, out, B, CC, Ch, H, W, Ho, Wo, K, S, stream);
@@ -285,19 +322,43 @@ FA_EXPORT int fa_dwconv(int op, int is_bf16, const void* a, const void* b, const
 }
 
 // op 0: stats (mean, var) of x; 1: y = act(x·s + t); 2: bwd reduce of (gy, x) into red [CC][2]; 3: dx.
+// ext (optional, may be null): op 0 — running-statistics update {rm, rv, nbt, rcs, momentum, active, Ch};
+// op 2 — dγ / dβ accumulated into the gradient arena {dg, db, dcs}
+struct PbnExt {
+  float* rm;
+  float* rv;
+  float* nbt;
+  int64_t rcs;
+  float momentum;
+  const float* active;
+  float* dg;
+  float* db;
+  int64_t dcs;
+};
+
 FA_EXPORT int fa_plane_bn(int op, int is_bf16, const void* x, const void* gy, void* out, const float* g,
                           const float* bb, int64_t pcs, float* mean, float* var, float eps, int relu, float* red, int B,
-                          int CC, int Ch, int HW, hipStream_t stream) {
+                          int CC, int Ch, int HW, const PbnExt* ext, hipStream_t stream) {
   const int64_t n = (int64_t)B * CC * HW;
   const unsigned grid = (unsigned)fa_grid(n, 256, 16384);
+  pk::PbnRun run = {nullptr, nullptr, nullptr, 0, 0.f, nullptr, Ch};
+  float* dg = nullptr;
+  float* db = nullptr;
+  int64_t dcs = 0;
+  if (ext) {
+    run.rm = ext->rm; run.rv = ext->rv; run.nbt = ext->nbt; run.rcs = ext->rcs; run.momentum = ext->momentum;
+    run.active = ext->active;
+    dg = ext->dg; db = ext->db; dcs = ext->dcs;
+  }
 #define PBN(T)                                                                                                     \
   switch (op) {                                                                                                    \
     case 0: hipLaunchKernelGGL(pk::pbn_stats_kernel<T>, dim3(CC), dim3(256), 0, stream, (const T*)x, mean, var, B, \
-                               CC, HW); break;                                                                    \
+                               CC, HW, run); break;                                                               \
     case 1: hipLaunchKernelGGL(pk::pbn_apply_kernel<T>, dim3(grid), dim3(256), 0, stream, (const T*)x, (T*)out, g, \
                                bb, pcs, mean, var, eps, relu, B, CC, Ch, HW); break;                              \
     case 2: hipLaunchKernelGGL(pk::pbn_bwd_red_kernel<T>, dim3(CC), dim3(256), 0, stream, (const T*)gy,           \
-                               (const T*)x, g, bb, pcs, mean, var, eps, relu, red, B, CC, Ch, HW); break;         \
+                               (const T*)x, g, bb, pcs, mean, var, eps, relu, red, B, CC, Ch, HW, dg, db, dcs);   \
+      break;                                                                                                       \
     case 3: hipLaunchKernelGGL(pk::pbn_dx_kernel<T>, dim3(grid), dim3(256), 0, stream, (const T*)gy, (const T*)x,  \
                                (T*)out, g, bb, pcs, mean, var, eps, relu, red, B, CC, Ch, HW); break;             \
     default: return -2;                                                                                            \

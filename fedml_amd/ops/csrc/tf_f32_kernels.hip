@@ -81,6 +81,9 @@ struct Args {
   int64_t bias_bs;
   Segs biasseg;
   float* C2;         // GELU: gelu(D + b); Cp keeps the pre-activation for the backward
+  const float* R;    // STORE: optional residual addend [C][M][ldr] (D = A·Bᵀ + b + R: a pre-LN block's x + f(x))
+  int64_t r_bs;
+  int ldr;
   int M, N, K;
   int tiles_m, tiles_n, nclients;
 };
@@ -92,7 +95,8 @@ __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + er
 //   TR = 1: storage rows k [k0, k0+32) (segmented) × logical cols [r0, r0+128)
 // VEC = 1: every row start and extent is a multiple of 4 floats (one float4 per chunk); VEC = 0:
 // element-wise loads with bounds on every element.
-template <int TR, int VEC>
+// CHECK = 0: the tile lies inside the operand (interior blocks, K % 32 == 0) — unpredicated loads.
+template <int TR, int VEC, int CHECK = 1>
 __device__ __forceinline__ void load_tile(float4 (&r)[4], const float* __restrict__ base, const Segs& sg, int ld,
                                           int rows, int K, int r0, int k0, int tid) {
 #pragma unroll
@@ -110,6 +114,10 @@ __device__ __forceinline__ void load_tile(float4 (&r)[4], const float* __restric
       col = r0 + 4 * (v & 31);
       rok = srow < K;
       lim = rows;
+    }
+    if (!CHECK) {
+      r[i] = *reinterpret_cast<const float4*>(base + seg_row(sg, srow, ld) + col);
+      continue;
     }
     float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
     if (rok) {
@@ -143,6 +151,45 @@ template <class P, int TR>
 __device__ __forceinline__ typename P::frag_t frag_of(const float* tile, int row0, int lane) {
   if (TR) return P::frag_tr(tile, LDT, 0, row0, lane);
   return P::frag_tile(tile + (row0 + (lane & 15)) * LDR + 8 * (lane >> 4));
+}
+
+template <class P, int A_TR, int B_TR, int VEC, int CHECK>
+__device__ __forceinline__ void gemm_mainloop(f32x4 (&acc)[4][4], const float* A, const Segs& aseg, const float* B,
+                                              const Args& p, int m0, int n0, int nk, float* SA0, float* SB0, int tid,
+                                              int lane, int wm, int wn) {
+  float4 ra[4], rb[4];
+  load_tile<A_TR, VEC, CHECK>(ra, A, aseg, p.lda, p.M, p.K, m0, 0, tid);
+  load_tile<B_TR, VEC, CHECK>(rb, B, p.bseg, p.ldb, p.N, p.K, n0, 0, tid);
+  store_tile<P, A_TR>(SA0, ra, tid);
+  store_tile<P, B_TR>(SB0, rb, tid);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) {   // the next K-step's global reads fly under this step's MFMAs
+      load_tile<A_TR, VEC, CHECK>(ra, A, aseg, p.lda, p.M, p.K, m0, (kt + 1) * BK, tid);
+      load_tile<B_TR, VEC, CHECK>(rb, B, p.bseg, p.ldb, p.N, p.K, n0, (kt + 1) * BK, tid);
+    }
+    const float* ta = SA0 + cur * TILE;
+    const float* tb = SB0 + cur * TILE;
+    typename P::frag_t bfr[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) bfr[j] = frag_of<P, B_TR>(tb, wn + 16 * j, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const typename P::frag_t af = frag_of<P, A_TR>(ta, wm + 16 * i, lane);
+      // operands swapped: the MFMA computes the transposed tile, so a lane owns 4 consecutive
+      // output columns n of one row m (16-byte epilogue accesses)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = P::mma(bfr[j], af, acc[i][j]);
+    }
+    if (more) {
+      store_tile<P, A_TR>(SA0 + (cur ^ 1) * TILE, ra, tid);
+      store_tile<P, B_TR>(SB0 + (cur ^ 1) * TILE, rb, tid);
+    }
+    __syncthreads();
+  }
 }
 
 template <class P, int A_TR, int B_TR, int EPI, int VEC>
@@ -180,40 +227,12 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args p) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  float4 ra[4], rb[4];
   const int nk = (p.K + BK - 1) / BK;
-  load_tile<A_TR, VEC>(ra, A, aseg, p.lda, p.M, p.K, m0, 0, tid);
-  load_tile<B_TR, VEC>(rb, B, p.bseg, p.ldb, p.N, p.K, n0, 0, tid);
-  store_tile<P, A_TR>(SA0, ra, tid);
-  store_tile<P, B_TR>(SB0, rb, tid);
-  __syncthreads();
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    const bool more = kt + 1 < nk;
-    if (more) {   // the next K-step's global reads fly under this step's MFMAs
-      load_tile<A_TR, VEC>(ra, A, aseg, p.lda, p.M, p.K, m0, (kt + 1) * BK, tid);
-      load_tile<B_TR, VEC>(rb, B, p.bseg, p.ldb, p.N, p.K, n0, (kt + 1) * BK, tid);
-    }
-    const float* ta = SA0 + cur * TILE;
-    const float* tb = SB0 + cur * TILE;
-    typename P::frag_t bfr[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) bfr[j] = frag_of<P, B_TR>(tb, wn + 16 * j, lane);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const typename P::frag_t af = frag_of<P, A_TR>(ta, wm + 16 * i, lane);
-      // operands swapped: the MFMA computes the transposed tile, so a lane owns 4 consecutive
-      // output columns n of one row m (16-byte epilogue accesses)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = P::mma(bfr[j], af, acc[i][j]);
-    }
-    if (more) {
-      store_tile<P, A_TR>(SA0 + (cur ^ 1) * TILE, ra, tid);
-      store_tile<P, B_TR>(SB0 + (cur ^ 1) * TILE, rb, tid);
-    }
-    __syncthreads();
-  }
+  // interior blocks (the vast majority) stage their tiles with unpredicated vector loads
+  if (VEC && m0 + BM <= p.M && n0 + BN <= p.N && (p.K % BK) == 0)
+    gemm_mainloop<P, A_TR, B_TR, VEC, 0>(acc, A, aseg, B, p, m0, n0, nk, SA0, SB0, tid, lane, wm, wn);
+  else
+    gemm_mainloop<P, A_TR, B_TR, VEC, 1>(acc, A, aseg, B, p, m0, n0, nk, SA0, SB0, tid, lane, wm, wn);
 
   // epilogue: lane owns row m = m0 + wm + 16i + (lane & 15), cols n .. n+3, n = n0 + wn + 16j + 4(lane >> 4)
 #pragma unroll
@@ -246,6 +265,17 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args p) {
 #pragma unroll
             for (int r = 0; r < 4; ++r)
               if (n + r < p.N) v[r] += bp[seg_row(p.biasseg, n + r, 1)];
+          }
+        }
+        if (EPI == EPI_STORE && p.R) {
+          const float* rp = p.R + (int64_t)c * p.r_bs + (int64_t)m * p.ldr + n;
+          if (VEC) {
+            const float4 r4 = *reinterpret_cast<const float4*>(rp);
+            v[0] += r4.x; v[1] += r4.y; v[2] += r4.z; v[3] += r4.w;
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (n + r < p.N) v[r] += rp[r];
           }
         }
         const int64_t o = (int64_t)c * p.c_bs + (int64_t)m * p.ldc + n;
@@ -387,7 +417,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
                                                      float* __restrict__ dx, float* __restrict__ dh, uint32_t thr,
                                                      float dscale, uint32_t seed, float* __restrict__ dgamma,
                                                      float* __restrict__ dbeta, const uint32_t* __restrict__ seedp,
-                                                     int64_t gcs, int64_t dgcs) {
+                                                     int64_t gcs, int64_t dgcs, const float* __restrict__ dadd) {
   if (seedp) seed += *seedp * 1000003u;
   extern __shared__ float red[];   // [4][2][d]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -438,6 +468,10 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const float* __restrict__ d
 #pragma unroll
             for (int j = 0; j < 4; ++j)
               o[j] = fa_drop::keep(seed, (uint32_t)row, (uint32_t)(col + j), thr) ? o[j] * dscale : 0.f;
+          }
+          if (dadd) {   // the other consumer's gradient of the LN input (pre-LN residual stream)
+            const float4 a4 = *reinterpret_cast<const float4*>(dadd + row * d + col);
+            o[0] += a4.x; o[1] += a4.y; o[2] += a4.z; o[3] += a4.w;
           }
           *reinterpret_cast<float4*>(dh + row * d + col) = make_float4(o[0], o[1], o[2], o[3]);
         }
@@ -491,20 +525,48 @@ __global__ __launch_bounds__(256) void gelu_bwd_kernel(const float* __restrict__
   }
 }
 
-// db[c][n] += Σ_m g[c][m][n]: each thread owns one column of a 128-row chunk (coalesced rows),
-// one fp32 atomic per thread into the (segmented) gradient arena
+// db[c][n] += Σ_m g[c][m][n]: each thread owns one column (VEC = 4: four, as float4) of a row chunk, with
+// independent partial sums so several row loads are in flight (a one-accumulator chain left the kernel
+// latency-bound: 96 % of wave time waiting on memory); one fp32 atomic per column into the gradient arena
+template <int VEC>
 __global__ __launch_bounds__(256) void bias_grad_kernel(const float* __restrict__ g, int64_t g_bs, int ldg,
                                                         float* __restrict__ out, int64_t o_cs, Segs seg, int M, int N,
                                                         int rows_per_block) {
   const int c = blockIdx.z;
-  const int n = blockIdx.x * 256 + threadIdx.x;
+  const int n = (blockIdx.x * 256 + threadIdx.x) * VEC;
   if (n >= N) return;
   const int m0 = blockIdx.y * rows_per_block;
   const int m1 = min(M, m0 + rows_per_block);
   const float* gp = g + (int64_t)c * g_bs + n;
-  float a = 0.f;
-  for (int m = m0; m < m1; ++m) a += gp[(int64_t)m * ldg];
-  fa_acc_add(out + (int64_t)c * o_cs + seg_row(seg, n, 1), a);
+  float a[4][VEC];
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int j = 0; j < VEC; ++j) a[u][j] = 0.f;
+  int m = m0;
+  for (; m + 4 <= m1; m += 4) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (VEC == 4) {
+        const float4 v = *reinterpret_cast<const float4*>(gp + (int64_t)(m + u) * ldg);
+        a[u][0] += v.x; a[u][1] += v.y; a[u][2] += v.z; a[u][3] += v.w;
+      } else {
+        a[u][0] += gp[(int64_t)(m + u) * ldg];
+      }
+    }
+  }
+  for (; m < m1; ++m) {
+    if (VEC == 4) {
+      const float4 v = *reinterpret_cast<const float4*>(gp + (int64_t)m * ldg);
+      a[0][0] += v.x; a[0][1] += v.y; a[0][2] += v.z; a[0][3] += v.w;
+    } else {
+      a[0][0] += gp[(int64_t)m * ldg];
+    }
+  }
+  // columns n .. n+3 share a segment (segment bounds are multiples of 4 on the VEC path)
+  float* o = out + (int64_t)c * o_cs + seg_row(seg, n, 1);
+#pragma unroll
+  for (int j = 0; j < VEC; ++j) fa_acc_add(o + j, (a[0][j] + a[1][j]) + (a[2][j] + a[3][j]));
 }
 
 // =========================================================================================
@@ -904,6 +966,28 @@ FA_EXPORT int fa_bgemm_fwd_f32(const float* x, int64_t x_bs, int ldx, const floa
   FA_F32_DISPATCH(tff, (launch_gemm<PX, 0, 0, EPI_STORE>(a, vec, stream)));
 }
 
+// y[c] = x[c] · W[c]ᵀ + b[c] + res[c]   (no GELU; res [C][M][ldr], may alias nothing it reads)
+FA_EXPORT int fa_bgemm_fwd_res_f32(const float* x, int64_t x_bs, int ldx, const float* w_base, int64_t w_cs,
+                                   const int64_t* w_off, const float* b_base, int64_t b_cs, const int64_t* b_off,
+                                   const int* seg_lo, int nseg, float* y, int64_t y_bs, int ldy, const float* res,
+                                   int64_t r_bs, int ldr, int C, int M, int N, int K, hipStream_t stream) {
+  using namespace tff;
+  if (nseg < 1 || nseg > 4 || C <= 0 || M <= 0 || N <= 0 || K <= 0 || !res) return (int)hipErrorInvalidValue;
+  Args a{};
+  a.A = x; a.a_bs = x_bs; a.lda = ldx;
+  a.B = w_base; a.b_bs = w_cs; a.ldb = K;
+  fill_segs(a.bseg, w_off, seg_lo, nseg);
+  a.Cp = y; a.c_bs = y_bs; a.ldc = ldy;
+  a.bias = b_base; a.bias_bs = b_cs;
+  fill_segs(a.biasseg, b_off, seg_lo, nseg);
+  a.R = res; a.r_bs = r_bs; a.ldr = ldr;
+  a.M = M; a.N = N; a.K = K;
+  a.tiles_m = (M + BM - 1) / BM; a.tiles_n = (N + BN - 1) / BN; a.nclients = C;
+  const bool vec = al4({x_bs, ldx, K, w_cs, b_cs, y_bs, ldy, N, r_bs, ldr}) && segs_al4(a.bseg) &&
+                   (!b_base || segs_al4(a.biasseg)) && al16({x, w_base, b_base, y, res});
+  FA_F32_DISPATCH(tff, (launch_gemm<PX, 0, 0, EPI_STORE>(a, vec, stream)));
+}
+
 // dx[c] = dy[c] · W[c]    dy [M][N], W [N][K] arena segments (rows n = the reduction index), dx [M][K]
 FA_EXPORT int fa_bgemm_dgrad_f32(const float* dy, int64_t dy_bs, int lddy, const float* w_base, int64_t w_cs,
                                  const int64_t* w_off, const int* seg_lo, int nseg, float* dx, int64_t dx_bs, int lddx,
@@ -919,6 +1003,25 @@ FA_EXPORT int fa_bgemm_dgrad_f32(const float* dy, int64_t dy_bs, int lddy, const
   a.tiles_m = (M + BM - 1) / BM; a.tiles_n = (K + BN - 1) / BN; a.nclients = C;
   const bool vec = al4({dy_bs, lddy, N, w_cs, K, dx_bs, lddx}) && segs_al4(a.bseg) && al16({dy, w_base, dx});
   FA_F32_DISPATCH(tff, (launch_gemm<PX, 0, 1, EPI_STORE>(a, vec, stream)));
+}
+
+// dx[c] += dy[c] · W[c]   (accumulating form: the residual-stream gradient the caller already holds in dx —
+// a post-LN block's input feeds both the next LayerNorm's residual and this linear)
+FA_EXPORT int fa_bgemm_dgrad_acc_f32(const float* dy, int64_t dy_bs, int lddy, const float* w_base, int64_t w_cs,
+                                     const int64_t* w_off, const int* seg_lo, int nseg, float* dx, int64_t dx_bs,
+                                     int lddx, int C, int M, int N, int K, hipStream_t stream) {
+  using namespace tff;
+  if (nseg < 1 || nseg > 4 || C <= 0 || M <= 0 || N <= 0 || K <= 0) return (int)hipErrorInvalidValue;
+  Args a{};
+  a.A = dy; a.a_bs = dy_bs; a.lda = lddy;
+  a.B = w_base; a.b_bs = w_cs; a.ldb = K;
+  fill_segs(a.bseg, w_off, seg_lo, nseg);
+  a.Cp = dx; a.c_bs = dx_bs; a.ldc = lddx;
+  fill_segs(a.cseg, nullptr, nullptr, 1);   // one plain [M][lddx] matrix per client
+  a.M = M; a.N = K; a.K = N;
+  a.tiles_m = (M + BM - 1) / BM; a.tiles_n = (K + BN - 1) / BN; a.nclients = C;
+  const bool vec = al4({dy_bs, lddy, N, w_cs, K, dx_bs, lddx}) && segs_al4(a.bseg) && al16({dy, w_base, dx});
+  FA_F32_DISPATCH(tff, (launch_gemm<PX, 0, 1, EPI_ACC>(a, vec, stream)));
 }
 
 // dW[c] += dy[c]ᵀ · x[c]    dy [T][N], x [T][K]; dW [N][K] gradient-arena segments (rows n)
@@ -948,8 +1051,13 @@ FA_EXPORT int fa_bias_grad_f32(const float* dy, int64_t dy_bs, int lddy, float* 
   Segs sg;
   fill_segs(sg, o_off, seg_lo, nseg);
   const int rpb = 128;
-  dim3 grid((unsigned)((N + 255) / 256), (unsigned)((M + rpb - 1) / rpb), (unsigned)C);
-  hipLaunchKernelGGL(bias_grad_kernel, grid, dim3(256), 0, stream, dy, dy_bs, lddy, o_base, o_cs, sg, M, N, rpb);
+  const bool vec = al4({dy_bs, lddy, N}) && segs_al4(sg) && al16({dy});
+  const int cols = vec ? N / 4 : N;
+  dim3 grid((unsigned)((cols + 255) / 256), (unsigned)((M + rpb - 1) / rpb), (unsigned)C);
+  if (vec)
+    hipLaunchKernelGGL(bias_grad_kernel<4>, grid, dim3(256), 0, stream, dy, dy_bs, lddy, o_base, o_cs, sg, M, N, rpb);
+  else
+    hipLaunchKernelGGL(bias_grad_kernel<1>, grid, dim3(256), 0, stream, dy, dy_bs, lddy, o_base, o_cs, sg, M, N, rpb);
   return (int)hipGetLastError();
 }
 
@@ -972,10 +1080,24 @@ FA_EXPORT int fa_ln_fwd_f32(const float* h, const float* res, int R, int d, int 
   return (int)hipGetLastError();
 }
 
+// dadd (optional): added to dh (the gradient of the LN input h) — the residual stream's other gradient
+FA_EXPORT int fa_ln_bwd_add_f32(const float* dy, const float* x, const float* mean, const float* rstd, int C,
+                                int rows_per_client, int d, const float* gamma, float* dx, float* dh, uint32_t thr,
+                                float dscale, uint32_t seed, float* dgamma, float* dbeta, const uint32_t* seedp,
+                                int64_t gcs, int64_t dgcs, const float* dadd, hipStream_t stream);
+
 FA_EXPORT int fa_ln_bwd_f32(const float* dy, const float* x, const float* mean, const float* rstd, int C,
                             int rows_per_client, int d, const float* gamma, float* dx, float* dh, uint32_t thr,
                             float dscale, uint32_t seed, float* dgamma, float* dbeta, const uint32_t* seedp,
                             int64_t gcs, int64_t dgcs, hipStream_t stream) {
+  return fa_ln_bwd_add_f32(dy, x, mean, rstd, C, rows_per_client, d, gamma, dx, dh, thr, dscale, seed, dgamma, dbeta,
+                           seedp, gcs, dgcs, nullptr, stream);
+}
+
+FA_EXPORT int fa_ln_bwd_add_f32(const float* dy, const float* x, const float* mean, const float* rstd, int C,
+                                int rows_per_client, int d, const float* gamma, float* dx, float* dh, uint32_t thr,
+                                float dscale, uint32_t seed, float* dgamma, float* dbeta, const uint32_t* seedp,
+                                int64_t gcs, int64_t dgcs, const float* dadd, hipStream_t stream) {
   using namespace tff;
   if (d % 4 != 0 || d > 2048 || C <= 0 || C > 65535 || gcs % 4 != 0) return (int)hipErrorInvalidValue;
   int bpc = (rows_per_client + 31) / 32;   // ≥ 8 rows per wave
@@ -985,7 +1107,7 @@ FA_EXPORT int fa_ln_bwd_f32(const float* dy, const float* x, const float* mean, 
   const size_t sm = 8 * (size_t)d * sizeof(float);
 #define TFF_LNB(NV) \
   hipLaunchKernelGGL(ln_bwd_kernel<NV>, grid, dim3(256), sm, stream, dy, x, mean, rstd, rows_per_client, d, gamma, dx, \
-                     dh, thr, dscale, seed, dgamma, dbeta, seedp, gcs, dgcs)
+                     dh, thr, dscale, seed, dgamma, dbeta, seedp, gcs, dgcs, dadd)
   if (d <= 256) TFF_LNB(1);
   else if (d <= 512) TFF_LNB(2);
   else if (d <= 768) TFF_LNB(3);

@@ -92,9 +92,29 @@ def _deterministic() -> bool:
     return determinism.enabled()
 
 
+class ResLink:
+    """Hand-off of a residual-stream gradient between the two consumers of one activation, so autograd never
+    has to add their two gradients in a separate pass (fp32 native path):
+
+    * post-LN block (``x1 = LN(res = x, h = f(x))``): the LayerNorm's backward — which runs first — leaves dres
+      in ``g`` and returns nothing for ``res``; the linear that reads ``x`` accumulates its data gradient into
+      that buffer (``dx += dy·W`` in the GEMM epilogue) and returns it as the gradient of ``x``.
+    * pre-LN block (``x' = x + f(LN(x))``, the add fused as ``res`` of the output linear): the output linear's
+      backward leaves dres (= its incoming gradient) in ``g`` and returns nothing for ``res``; the LayerNorm that
+      reads ``x`` adds it to its input gradient in the same kernel.
+
+    Autograd runs the producer of the hand-off first in both patterns; should a consumer ever run first it
+    ``closes`` the link, and the producer then returns its gradient the ordinary way (never lost)."""
+    __slots__ = ("g", "closed")
+
+    def __init__(self):
+        self.g = None
+        self.closed = False
+
+
 class _LayerNorm(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, h, res, gamma, beta, eps, p, seed, rpc, seed_dev):
+    def forward(ctx, h, res, gamma, beta, eps, p, seed, rpc, seed_dev, link=None, in_link=None):
         R, d = h.shape
         y = torch.empty_like(h)
         fused = res is not None or p > 0
@@ -110,6 +130,8 @@ class _LayerNorm(torch.autograd.Function):
         ctx.save_for_backward(xsum if fused else h, mean, rstd, g)
         ctx.cfg = (p, seed, rpc, res is not None, fused, gamma.dtype, gcs)
         ctx.seed_dev = seed_dev
+        ctx.link = link if res is not None and h.dtype == torch.float32 else None    # post-LN: dres → link.g
+        ctx.in_link = in_link if h.dtype == torch.float32 else None                 # pre-LN: dh += link.g
         # γ/β leaves with pre-assigned gradient-arena views: the backward kernel accumulates dγ/dβ into them
         ctx.own = (gamma, beta) if (gamma.is_leaf and beta.is_leaf and gamma.grad is not None and beta.grad is not None
                                     and gamma.grad.stride() == gamma.stride() and beta.grad.stride() == beta.stride()
@@ -136,12 +158,29 @@ class _LayerNorm(torch.autograd.Function):
             db = torch.zeros(C, d, dtype=torch.float32, device=x.device)
             dgcs = d
         name = "fa_ln_bwd" + _sfx(x)
-        rc = _fn(name)(_p(dy), _p(x), _p(mean), _p(rstd), _c.c_int(C), _c.c_int(rpc), _c.c_int(d), _p(g),
-                       _p(dres), _p(dh), _c.c_uint32(_thr(p)), _f(1.0 / (1.0 - p) if p > 0 else 1.0),
-                       _c.c_uint32(seed & _M32), _p(dg), _p(db), _p(seed_dev), _i64(gcs), _i64(dgcs), _stream(x))
+        dadd = None
+        if ctx.in_link is not None:
+            if ctx.in_link.g is not None:
+                dadd = ctx.in_link.g.reshape(R, d).to(x.dtype).contiguous()
+                ctx.in_link.g = None
+            else:
+                ctx.in_link.closed = True
+        if dadd is not None:
+            name = "fa_ln_bwd_add_f32"
+            rc = _fn(name)(_p(dy), _p(x), _p(mean), _p(rstd), _c.c_int(C), _c.c_int(rpc), _c.c_int(d), _p(g),
+                           _p(dres), _p(dh), _c.c_uint32(_thr(p)), _f(1.0 / (1.0 - p) if p > 0 else 1.0),
+                           _c.c_uint32(seed & _M32), _p(dg), _p(db), _p(seed_dev), _i64(gcs), _i64(dgcs), _p(dadd),
+                           _stream(x))
+        else:
+            rc = _fn(name)(_p(dy), _p(x), _p(mean), _p(rstd), _c.c_int(C), _c.c_int(rpc), _c.c_int(d), _p(g),
+                           _p(dres), _p(dh), _c.c_uint32(_thr(p)), _f(1.0 / (1.0 - p) if p > 0 else 1.0),
+                           _c.c_uint32(seed & _M32), _p(dg), _p(db), _p(seed_dev), _i64(gcs), _i64(dgcs), _stream(x))
         _check(rc, name)
+        if ctx.link is not None and dres is not None and not ctx.link.closed:   # its other consumer adds into it
+            ctx.link.g = dres
+            dres = None
         if own:
-            return dh, dres, None, None, None, None, None, None, None
+            return dh, dres, None, None, None, None, None, None, None, None, None
         if det:
             # the kernel's dgamma/dbeta reduce rows with fp32 atomics (arrival order → last bit): recompute them
             # as fixed-order column sums (deterministic-mode only; the kernel's dh/dres are atomic-free)
@@ -149,19 +188,22 @@ class _LayerNorm(torch.autograd.Function):
             xhat = (xf - mean.view(C, rpc, 1)) * rstd.view(C, rpc, 1)
             dg = (dyf * xhat).sum(1)
             db = dyf.sum(1)
-        return dh, dres, dg.to(gdt), db.to(gdt), None, None, None, None, None
+        return dh, dres, dg.to(gdt), db.to(gdt), None, None, None, None, None, None, None
 
 
 def layer_norm(h: torch.Tensor, gamma: torch.Tensor, beta: torch.Tensor, eps: float, rows_per_client: int,
-               res: torch.Tensor = None, p: float = 0.0, seed: int = 0, seed_dev: torch.Tensor = None) -> torch.Tensor:
+               res: torch.Tensor = None, p: float = 0.0, seed: int = 0, seed_dev: torch.Tensor = None,
+               res_link: "ResLink" = None, in_link: "ResLink" = None) -> torch.Tensor:
     """LN(res + dropout_p(h)) over the last dim of 2-D ``h`` [R, d]; gamma/beta ``[C, d]``.
     ``seed_dev`` (GPU): a [1] uint32/int32 device step counter — the kernels then use
-    seed + counter·1000003, so a captured HIP graph draws new dropout masks on every replay."""
+    seed + counter·1000003, so a captured HIP graph draws new dropout masks on every replay.
+    ``res_link`` / ``in_link``: :class:`ResLink` hand-offs of the residual-stream gradient (fp32 native path)."""
     assert h.dim() == 2 and h.shape[0] % rows_per_client == 0
     if use_native(h):
         _sfx(h)
         assert h.is_contiguous() and (res is None or (res.is_contiguous() and res.dtype == h.dtype))
-        return _LayerNorm.apply(h, res, gamma, beta, float(eps), float(p), int(seed), int(rows_per_client), seed_dev)
+        return _LayerNorm.apply(h, res, gamma, beta, float(eps), float(p), int(seed), int(rows_per_client), seed_dev,
+                                res_link, in_link)
     return _ln_ref(h, res, gamma, beta, eps, p, seed, rows_per_client)
 
 
@@ -256,6 +298,52 @@ class _Attention(torch.autograd.Function):
         return dq, dk, dv, None, None, None, None, None, None
 
 
+class _AttentionQKV(torch.autograd.Function):
+    """Attention over the fused q/k/v projection output ``qkv`` [T, 3·dm] taken whole: the backward kernels write
+    dq / dk / dv straight into the column slices of ONE gradient buffer — three separate slice gradients would
+    make autograd zero a [T, 3·dm] buffer and copy each slice into it."""
+
+    @staticmethod
+    def forward(ctx, qkv, kmask, S, H, p, seed, seed_dev):
+        dm = qkv.shape[1] // 3
+        q, k, v = qkv[:, :dm], qkv[:, dm:2 * dm], qkv[:, 2 * dm:]
+        o = _Attention.forward(ctx, q, k, v, kmask, S, H, p, seed, seed_dev)
+        return o
+
+    @staticmethod
+    def backward(ctx, do):
+        q, k, v, o, lse, kmask = ctx.saved_tensors
+        S, H, p, seed = ctx.cfg
+        T, dm = q.shape
+        CB = T // S
+        do = do.to(q.dtype).contiguous()
+        dqkv = torch.empty(T, 3 * dm, dtype=q.dtype, device=q.device)
+        D = torch.empty(CB, H, S, dtype=torch.float32, device=q.device)
+        ld = 3 * dm
+        name = "fa_attn_bwd" + _sfx(q)
+        rc = _fn(name)(_p(q), _c.c_int(q.stride(0)), _p(k), _c.c_int(k.stride(0)), _p(v),
+                       _c.c_int(v.stride(0)), _p(o), _c.c_int(dm), _p(do), _c.c_int(dm), _p(kmask), _p(lse),
+                       _p(D), _p(dqkv), _c.c_int(ld), _p(dqkv[:, dm:]), _c.c_int(ld), _p(dqkv[:, 2 * dm:]),
+                       _c.c_int(ld), _c.c_int(CB), _c.c_int(S), _c.c_int(H), _f(1.0 / math.sqrt(64.0)),
+                       _c.c_uint32(_thr(p)), _f(1.0 / (1.0 - p) if p > 0 else 1.0),
+                       _c.c_uint32(seed & _M32), _p(ctx.seed_dev), _stream(q))
+        _check(rc, name)
+        return dqkv, None, None, None, None, None, None
+
+
+def attention_qkv(qkv, S: int, H: int, kmask: torch.Tensor = None, p: float = 0.0, seed: int = 0,
+                  seed_dev: torch.Tensor = None):
+    """:func:`attention` over the fused projection output ``qkv`` [CB·S, 3·H·64] (q | k | v column blocks)."""
+    dm = qkv.shape[1] // 3
+    if use_native(qkv) and qkv.is_contiguous():
+        vec = 8 if _sfx(qkv) == "" else 4
+        assert S <= 256 and dm == H * 64 and qkv.shape[0] % S == 0 and (3 * dm) % vec == 0
+        km = None if kmask is None else kmask.to(torch.uint8).contiguous()
+        return _AttentionQKV.apply(qkv, km, int(S), int(H), float(p), int(seed), seed_dev)
+    return attention(qkv[:, :dm], qkv[:, dm:2 * dm], qkv[:, 2 * dm:], S, H, kmask=kmask, p=p, seed=seed,
+                     seed_dev=seed_dev)
+
+
 def attention(q, k, v, S: int, H: int, kmask: torch.Tensor = None, p: float = 0.0, seed: int = 0,
               seed_dev: torch.Tensor = None):
     """Multi-head self-attention over token-major ``[CB·S, H·64]`` q/k/v (row stride may exceed
@@ -302,8 +390,10 @@ class _ClientLinear(torch.autograd.Function):
     (the leaves' pre-assigned ``.grad`` views) — no dense per-step weight copies either way."""
 
     @staticmethod
-    def forward(ctx, x, gelu, n_w, shadows, *params):
+    def forward(ctx, x, gelu, n_w, shadows, res, links, *params):
         ws, bs = params[:n_w], params[n_w:]
+        # links = (dx_link, res_link) (ResLink | None each; fp32 native only)
+        ctx.dx_link, ctx.res_link = links if (links is not None and x.dtype == torch.float32) else (None, None)
         C, M, K = x.shape
         N = sum(w.shape[1] for w in ws)
         # bf16 shadow of the weights (refreshed once per step by the engine) when given: half the
@@ -318,7 +408,14 @@ class _ClientLinear(torch.autograd.Function):
             bb, bcs, boff = None, 0, None
         y = torch.empty(C, M, N, dtype=x.dtype, device=x.device)
         y2 = torch.empty_like(y) if gelu else None
-        if x.dtype == torch.float32:    # fp32 activations: the fp32 kernels read the fp32 arena
+        fused_res = res is not None and x.dtype == torch.float32 and not gelu
+        if fused_res:                   # y = x·Wᵀ + b + res in the GEMM epilogue (pre-LN residual stream)
+            assert wh == 0 and res.shape == (C, M, N) and res.dtype == torch.float32 and res.is_contiguous()
+            rc = _fn("fa_bgemm_fwd_res_f32")(_p(x), _i64(M * K), _c.c_int(K), _p(wb), _i64(wcs), woff, _p(bb),
+                                             _i64(bcs), boff, lo, _c.c_int(len(ws)), _p(y), _i64(M * N), _c.c_int(N),
+                                             _p(res), _i64(M * N), _c.c_int(N), _c.c_int(C), _c.c_int(M),
+                                             _c.c_int(N), _c.c_int(K), _stream(x))
+        elif x.dtype == torch.float32:    # fp32 activations: the fp32 kernels read the fp32 arena
             assert wh == 0
             rc = _fn("fa_bgemm_fwd_f32")(_p(x), _i64(M * K), _c.c_int(K), _p(wb), _i64(wcs), woff, _p(bb),
                                          _i64(bcs), boff, lo, _c.c_int(len(ws)), _p(y), _i64(M * N), _c.c_int(N),
@@ -329,8 +426,11 @@ class _ClientLinear(torch.autograd.Function):
                                      lo, _c.c_int(len(ws)), _p(y), _i64(M * N), _c.c_int(N), _p(y2), _c.c_int(C),
                                      _c.c_int(M), _c.c_int(N), _c.c_int(K), _stream(x))
         _check(rc, "fa_bgemm_fwd" + _sfx(x))
+        if res is not None and not fused_res:
+            y = y + res.to(y.dtype)
         ctx.save_for_backward(x, y if gelu else None)
         ctx.ws, ctx.bs, ctx.gelu, ctx.wsrc = ws, bs, gelu, wsrc
+        ctx.has_res = res is not None
         return y2 if gelu else y
 
     @staticmethod
@@ -339,6 +439,10 @@ class _ClientLinear(torch.autograd.Function):
         ws, bs = ctx.ws, ctx.bs
         C, M, K = x.shape
         N = sum(w.shape[1] for w in ws)
+        g_res = g if ctx.has_res and ctx.needs_input_grad[4] else None   # y = … + res: dres = dy
+        if g_res is not None and ctx.res_link is not None and not ctx.res_link.closed:   # the LN adds it to its dh
+            ctx.res_link.g = g_res
+            g_res = None
         g = g.to(x.dtype).contiguous()
         sfx = _sfx(x)
         if ctx.gelu:
@@ -350,16 +454,31 @@ class _ClientLinear(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             wb, wcs, woff, lo = _segments(ctx.wsrc)
             wh = 1 if ctx.wsrc[0].dtype == torch.bfloat16 else 0
-            dx = torch.empty_like(x)
-            if sfx:
+            link = ctx.dx_link
+            acc = sfx and link is not None and link.g is not None
+            if link is not None and not acc:
+                link.closed = True
+            if acc:   # x's other consumer (a post-LN residual) left its gradient: add ours into it
+                dx = link.g.view(C, M, K)
+                link.g = None
+                assert dx.dtype == torch.float32 and dx.is_contiguous()
+                rc = _fn("fa_bgemm_dgrad_acc_f32")(_p(g), _i64(M * N), _c.c_int(N), _p(wb), _i64(wcs), woff, lo,
+                                                   _c.c_int(len(ws)), _p(dx), _i64(M * K), _c.c_int(K), _c.c_int(C),
+                                                   _c.c_int(M), _c.c_int(N), _c.c_int(K), _stream(x))
+            elif sfx:
+                dx = torch.empty_like(x)
                 rc = _fn("fa_bgemm_dgrad_f32")(_p(g), _i64(M * N), _c.c_int(N), _p(wb), _i64(wcs), woff, lo,
                                                _c.c_int(len(ws)), _p(dx), _i64(M * K), _c.c_int(K), _c.c_int(C),
                                                _c.c_int(M), _c.c_int(N), _c.c_int(K), _stream(x))
             else:
+                dx = torch.empty_like(x)
                 rc = _fn("fa_bgemm_dgrad")(_p(g), _i64(M * N), _c.c_int(N), _p(wb), _c.c_int(wh), _i64(wcs), woff, lo,
                                            _c.c_int(len(ws)), _p(dx), _i64(M * K), _c.c_int(K), _c.c_int(C),
                                            _c.c_int(M), _c.c_int(N), _c.c_int(K), _stream(x))
             _check(rc, "fa_bgemm_dgrad" + sfx)
+            if not acc and link is not None and link.g is not None:   # (not reached: links are fp32-only)
+                dx = dx + link.g.view(C, M, K).to(dx.dtype)
+                link.g = None
         # weight gradients: into the arena views when the engine pre-assigned them, else returned
         own = all(w.is_leaf and w.grad is not None for w in ws)
         if own:
@@ -399,21 +518,26 @@ class _ClientLinear(torch.autograd.Function):
                 for bv in bviews:
                     bv.add_(gs[:, r:r + bv.shape[1]])
                     r += bv.shape[1]
-                return (dx, None, None, None, *out_w, *out_b)
+                return (dx, None, None, None, g_res, None, *out_w, *out_b)
             bb, bcs, boff, blo = _segments(bviews)
             rc = _fn("fa_bias_grad" + sfx)(_p(g), _i64(M * N), _c.c_int(N), _p(bb), _i64(bcs), boff, blo,
                                      _c.c_int(len(bs)), _c.c_int(C), _c.c_int(M), _c.c_int(N), _stream(x))
             _check(rc, "fa_bias_grad" + sfx)
-        return (dx, None, None, None, *out_w, *out_b)
+        return (dx, None, None, None, g_res, None, *out_w, *out_b)
 
 
-def client_linear(x: torch.Tensor, weights, biases=None, gelu: bool = False, shadows=None) -> torch.Tensor:
+def client_linear(x: torch.Tensor, weights, biases=None, gelu: bool = False, shadows=None,
+                  res: torch.Tensor = None, dx_link: "ResLink" = None, res_link: "ResLink" = None) -> torch.Tensor:
     """Per-client linear over client-stacked activations ``x`` [C, M, K]: ``weights`` is a list of
     [C, n_i, K] fp32 arena views (concatenated along the output dim), ``biases`` the matching
     [C, n_i] views or None; ``gelu`` fuses the exact-erf GELU into the epilogue. ``shadows``: the
     same slots of a bf16 copy of the arena (current for this step) — the GEMMs then read bf16
     weights; gradients always land in the fp32 arena. CUDA → the batched MFMA GEMM kernels at the
-    activation dtype (bf16, or fp32 through ``tf_f32_kernels.hip``); CPU → the fp32 PyTorch reference."""
+    activation dtype (bf16, or fp32 through ``tf_f32_kernels.hip``); CPU → the fp32 PyTorch reference.
+    ``res`` [C, M, N] (no GELU): the result is ``res + linear(x)`` — at fp32 added in the GEMM epilogue (the residual
+    stream of a pre-LN block without a separate add pass). ``dx_link`` / ``res_link``: :class:`ResLink`
+    hand-offs of the residual-stream gradient (fp32 native path)."""
+    assert res is None or not gelu
     weights = list(weights)
     biases = list(biases) if biases else []
     C, M, K = x.shape
@@ -423,11 +547,14 @@ def client_linear(x: torch.Tensor, weights, biases=None, gelu: bool = False, sha
         sh = tuple(shadows) if shadows and x.dtype == torch.bfloat16 else None
         if sh is not None:
             assert len(sh) == len(weights) and all(t.shape == w.shape for t, w in zip(sh, weights))
-        return _ClientLinear.apply(x.contiguous(), bool(gelu), len(weights), sh, *weights, *biases)
+        r = res.contiguous() if res is not None else None
+        links = (dx_link, res_link) if (dx_link is not None or res_link is not None) else None
+        return _ClientLinear.apply(x.contiguous(), bool(gelu), len(weights), sh, r, links, *weights, *biases)
     w = torch.cat([t.reshape(C, t.shape[1], K) for t in weights], 1)
     y = torch.bmm(x.float(), w.float().transpose(1, 2))
     if biases:
         y = y + torch.cat(list(biases), 1).float().unsqueeze(1)
     if gelu:
         y = torch.nn.functional.gelu(y.to(x.dtype).float())
-    return y.to(x.dtype)
+    y = y.to(x.dtype)
+    return y if res is None else res + y

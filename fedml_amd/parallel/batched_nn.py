@@ -274,9 +274,15 @@ class BatchedInterpreter:
             if _NATIVE_BCONV and use_batch and sample_mask is None and m.momentum is not None:
                 from ..ops import plane_ops
                 if plane_ops.plane_supported(x, w, C) and (w is None) == (b is None):
-                    # per-(client, channel) statistics + affine (+ the next ReLU) on the plane kernels
-                    y, (mean, var_b, n) = plane_ops.plane_batch_norm(x, w, b, C, m.eps, relu=fuse_relu)
-                    if rm is not None and training:
+                    # per-(client, channel) statistics + affine (+ the next ReLU) on the plane kernels; the
+                    # statistics kernel also updates the running statistics in the arena (no deferred pass)
+                    run = None
+                    if rm is not None and training and rm.dtype == torch.float32 and rm.stride() == rv.stride() \
+                            and rm[0].is_contiguous() and (nbt is None or (nbt.dtype == torch.float32
+                                                                           and nbt.stride(0) == rm.stride(0))):
+                        run = (rm, rv, nbt, mom, active)
+                    y, (mean, var_b, n) = plane_ops.plane_batch_norm(x, w, b, C, m.eps, relu=fuse_relu, running=run)
+                    if rm is not None and training and run is None:
                         self.deferred.append((rm, rv, nbt, mean, var_b,
                                               torch.full((C, 1), n, device=x.device), mom, active))
                     return y, fuse_relu

@@ -105,11 +105,11 @@ class BatchedTransformer:
         self._sh = None
 
     # -------------------------------------------------------------------------------- helpers
-    def _lin(self, v, x, key, dt, weights=None, gelu=False):
+    def _lin(self, v, x, key, dt, weights=None, gelu=False, res=None, dx_link=None, res_link=None):
         """x [C, T, in] → [C, T, out] with per-client W [C, out, in] and bias [C, out] read straight
         from the fp32 arena views (``ops.transformer_ops.client_linear``: one batched MFMA GEMM per
         linear, weight gradients accumulated into the gradient arena; ``gelu`` fuses the
-        activation into the GEMM epilogue)."""
+        activation into the GEMM epilogue; ``res``: returns res + linear(x), the add in the epilogue)."""
         sh = None
         if weights is None:
             ws, bs = [v[key + ".weight"]], [v[key + ".bias"]]
@@ -117,27 +117,32 @@ class BatchedTransformer:
                 sh = [self._sh[key + ".weight"]]
         else:
             ws, bs, sh = weights
-        return T.client_linear(_bf(x, dt), ws, bs, gelu=gelu, shadows=sh)
+        return T.client_linear(_bf(x, dt), ws, bs, gelu=gelu, shadows=sh, res=res, dx_link=dx_link, res_link=res_link)
 
-    def _qkv(self, v, x, pre, dt):
+    def _qkv(self, v, x, pre, dt, dx_link=None):
         names = ("q_lin", "k_lin", "v_lin")
         sh = None if self._sh is None else [self._sh[f"{pre}.{n}.weight"] for n in names]
         return self._lin(v, x, None, dt, ([v[f"{pre}.{n}.weight"] for n in names],
-                                          [v[f"{pre}.{n}.bias"] for n in names], sh))
+                                          [v[f"{pre}.{n}.bias"] for n in names], sh), dx_link=dx_link)
 
-    def _ln(self, v, key, h, rows_per_client, res=None, p=0.0, seed=0, eps=None):
+    def _ln(self, v, key, h, rows_per_client, res=None, p=0.0, seed=0, eps=None, res_link=None, in_link=None):
         d = h.shape[-1]
         y = T.layer_norm(h.reshape(-1, d), v[key + ".weight"], v[key + ".bias"], self.eps if eps is None else eps,
                          rows_per_client, res=None if res is None else res.reshape(-1, d), p=p, seed=seed,
-                         seed_dev=self._seed_dev if h.is_cuda else None)
+                         seed_dev=self._seed_dev if h.is_cuda else None, res_link=res_link, in_link=in_link)
         return y.view(h.shape)
 
-    def _attn(self, v, x, pre, S, kmask, training, dt, seed):
+    @staticmethod
+    def _link(x, dt):
+        """A residual-gradient hand-off (ops.transformer_ops.ResLink) on the fp32 native path, else None."""
+        return T.ResLink() if (x.is_cuda and dt == torch.float32) else None
+
+    def _attn(self, v, x, pre, S, kmask, training, dt, seed, res=None, dx_link=None, res_link=None):
         C, Tk, d = x.shape
-        qkv = self._qkv(v, x, pre, dt).view(C * Tk, 3 * d)
-        a = T.attention(qkv[:, :d], qkv[:, d:2 * d], qkv[:, 2 * d:], S, self.heads, kmask=kmask,
-                        p=self.p_attn if training else 0.0, seed=seed, seed_dev=self._seed_dev if x.is_cuda else None)
-        return self._lin(v, a.view(C, Tk, d), pre + ".out_lin", dt)
+        qkv = self._qkv(v, x, pre, dt, dx_link=dx_link).view(C * Tk, 3 * d)
+        a = T.attention_qkv(qkv, S, self.heads, kmask=kmask, p=self.p_attn if training else 0.0, seed=seed,
+                            seed_dev=self._seed_dev if x.is_cuda else None)
+        return self._lin(v, a.view(C, Tk, d), pre + ".out_lin", dt, res=res, res_link=res_link)
 
     # -------------------------------------------------------------------------------- forward
     def forward(self, v: Dict[str, torch.Tensor], x: torch.Tensor, training: bool = True,
@@ -173,13 +178,16 @@ class BatchedTransformer:
         kmask = (ids != 0).reshape(C * B, S)
         for i in range(self.n_layers):
             pre = f"layer.{i}"
-            sa = self._attn(v, x, pre + ".attention", S, kmask, training, dt, base + 10 * i + 1)
+            # post-LN: x feeds the q/k/v GEMM and the LayerNorm's residual; the LN hands its residual gradient
+            # to the GEMM, which adds its data gradient in place (ResLink): no separate gradient add
+            l1, l2 = self._link(x, dt), self._link(x, dt)
+            sa = self._attn(v, x, pre + ".attention", S, kmask, training, dt, base + 10 * i + 1, dx_link=l1)
             x = self._ln(v, pre + ".sa_layer_norm", sa.contiguous(), rows, res=x,
-                         p=self.p_hidden if training else 0.0, seed=base + 10 * i + 2)
-            f = self._lin(v, x, pre + ".ffn.lin1", dt, gelu=True)
+                         p=self.p_hidden if training else 0.0, seed=base + 10 * i + 2, res_link=l1)
+            f = self._lin(v, x, pre + ".ffn.lin1", dt, gelu=True, dx_link=l2)
             f = self._lin(v, f, pre + ".ffn.lin2", dt)
             x = self._ln(v, pre + ".output_layer_norm", f.contiguous(), rows, res=x,
-                         p=self.p_hidden if training else 0.0, seed=base + 10 * i + 3)
+                         p=self.p_hidden if training else 0.0, seed=base + 10 * i + 3, res_link=l2)
         cls = x.view(C, B, S, d)[:, :, 0]                                                      # [C, B, d]
         pooled = torch.relu(self._lin(v, cls, "pre_classifier", dt))
         if training and self.p_cls:
@@ -203,11 +211,14 @@ class BatchedTransformer:
         rows = B * S
         for i in range(self.n_layers):
             pre = f"blocks.{i}"
-            h = self._ln(v, pre + ".norm1", x, rows)
-            x = x + self._attn(v, h, pre + ".attn", S, None, training, dt, base + 10 * i + 1)
-            h = self._ln(v, pre + ".norm2", x, rows)
+            l1, l2 = self._link(x, dt), self._link(x, dt)
+            h = self._ln(v, pre + ".norm1", x, rows, in_link=l1)
+            # residual adds in the output projections' GEMM epilogues; their residual gradient goes to the
+            # LayerNorm that also reads x, which adds it in its own kernel (ResLink)
+            x = self._attn(v, h, pre + ".attn", S, None, training, dt, base + 10 * i + 1, res=x, res_link=l1)
+            h = self._ln(v, pre + ".norm2", x, rows, in_link=l2)
             f = self._lin(v, h, pre + ".mlp.lin1", dt, gelu=True)
-            x = x + self._lin(v, f, pre + ".mlp.lin2", dt)
+            x = self._lin(v, f, pre + ".mlp.lin2", dt, res=x, res_link=l2)
         cls_out = x.view(C, B, S, d)[:, :, 0].contiguous()
         y = self._ln(v, "norm", cls_out, B)
         return self._lin(v, y, "head", dt).float()

@@ -539,9 +539,11 @@ class NativeResNetStep:
 
     # ------------------------------------------------------------------ deferred BN finalisation
     def _lazy_on(self):
-        # deterministic mode defers too (FEDML_AMD_BN_LAZY_DET=0: explicit there): the statistics' fixed-point
-        # shadow is rounded into them right before the consumer that folds them
-        return self.use_lazy and (self.det is None or os.environ.get("FEDML_AMD_BN_LAZY_DET", "1") != "0")
+        # deterministic mode keeps the explicit finalisation by default. FEDML_AMD_BN_LAZY_DET=1 defers there too
+        # (the statistics' fixed-point shadow rounded in right before the consumer that folds them): bitwise equal
+        # to explicit on full batches (scripts/diag/r4_diag3.py), but a ragged multi-round run (padded fixed
+        # geometry, clients idle in a step) produced NaN weights (tests/test_rccl_dist_gpu.py) — not yet resolved
+        return self.use_lazy and (self.det is None or os.environ.get("FEDML_AMD_BN_LAZY_DET", "0") == "1")
 
     def _defer(self, key, explicit, stats):
         """Explicit finalisation now, or (lazy mode) left to the first consumer kernel of the BN's vectors."""

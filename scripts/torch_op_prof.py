@@ -17,6 +17,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--preset", default="distilbert_fedopt_32")
     ap.add_argument("--rows", type=int, default=40)
+    ap.add_argument("--stacks", default="aten::copy_,aten::fill_,aten::add_,aten::add,aten::zero_,aten::mul",
+                    help="ops whose Python call sites are printed (comma list; '' = none)")
     a, rest = ap.parse_known_args()
     import torch
     import bench
@@ -29,11 +31,22 @@ def main():
         if state["n"] == 1:        # warmup round (bench --warmup 1)
             return orig(self, n)
         acts = [torch.profiler.ProfilerActivity.CPU, torch.profiler.ProfilerActivity.CUDA]
-        with torch.profiler.profile(activities=acts) as prof:
+        with torch.profiler.profile(activities=acts, with_stack=bool(a.stacks)) as prof:
             r = orig(self, n)
             torch.cuda.synchronize()
         print(prof.key_averages().table(sort_by="self_cuda_time_total", row_limit=a.rows, max_name_column_width=60),
               flush=True)
+        if a.stacks:
+            want = set(a.stacks.split(","))
+            rows = [e for e in prof.key_averages(group_by_stack_n=8) if e.key in want]
+            def dev_us(e):
+                return getattr(e, "self_device_time_total", None) or getattr(e, "self_cuda_time_total", 0.0)
+
+            rows.sort(key=lambda e: -dev_us(e))
+            for e in rows[:25]:
+                print(f"== {e.key}  calls {e.count}  self device {dev_us(e) / 1e3:.2f} ms")
+                for fr in e.stack[:8]:
+                    print("     ", fr)
         return r
 
     S.RCCLSimulator.run = run

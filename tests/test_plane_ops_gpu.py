@@ -67,6 +67,64 @@ def test_plane_batch_norm_matches_torch(relu, HW, B):
     assert _rel(g.grad, gr.grad) < 1e-4 and _rel(b.grad, br.grad) < 1e-5
 
 
+def test_plane_bn_running_stats_and_arena_grads():
+    """The engine's layout: γ, β, running mean / var and num_batches_tracked are strided rows of one parameter
+    arena, γ/β gradients pre-assigned views of a gradient arena. The statistics kernel updates the running
+    statistics in place (momentum, unbiased variance, active clients only) and the backward reduction
+    accumulates dγ/dβ into the gradient arena (+=, autograd returns nothing for them)."""
+    torch.manual_seed(2)
+    C, Ch, B, HW, mom = 3, 16, 8, 6, 0.1
+    P_ = 4 * Ch + 5
+    arena = torch.rand(C, P_, device=DEV) + 0.5
+    garena = torch.randn(C, P_, device=DEV)          # non-zero: the kernels must add, not store
+    g0 = garena.clone()
+    g = arena[:, 0:Ch].detach().requires_grad_(True)
+    b = arena[:, Ch:2 * Ch].detach().requires_grad_(True)
+    g.grad = garena[:, 0:Ch]
+    b.grad = garena[:, Ch:2 * Ch]
+    rm, rv, nbt = arena[:, 2 * Ch:3 * Ch], arena[:, 3 * Ch:4 * Ch], arena[:, 4 * Ch]
+    rm0, rv0, nbt0 = rm.clone(), rv.clone(), nbt.clone()
+    active = torch.tensor([1.0, 0.0, 1.0], device=DEV)
+    x = (torch.randn(B, C * Ch, HW, HW, device=DEV) * 2 + 1).requires_grad_(True)
+    y, _ = plane_ops.plane_batch_norm(x, g, b, C, 1e-5, relu=True, running=(rm, rv, nbt, mom, active))
+    xr = x.detach().clone().requires_grad_(True)
+    gr, br = g.detach().clone().requires_grad_(True), b.detach().clone().requires_grad_(True)
+    rmr, rvr = rm0.reshape(-1).clone(), rv0.reshape(-1).clone()
+    yr = torch.relu(F.batch_norm(xr, rmr, rvr, gr.reshape(-1), br.reshape(-1), True, mom, 1e-5))
+    assert _rel(y, yr) < 2e-5
+    on = active.view(C, 1) > 0
+    assert _rel(rm, torch.where(on, rmr.view(C, Ch), rm0)) < 1e-5
+    assert _rel(rv, torch.where(on, rvr.view(C, Ch), rv0)) < 1e-5
+    assert torch.equal(nbt, nbt0 + active)
+    gy = torch.randn_like(yr)
+    (y * gy).sum().backward()
+    (yr * gy).sum().backward()
+    assert _rel(x.grad, xr.grad) < 1e-4
+    assert _rel(garena[:, 0:Ch] - g0[:, 0:Ch], gr.grad) < 1e-4
+    assert _rel(garena[:, Ch:2 * Ch] - g0[:, Ch:2 * Ch], br.grad) < 1e-5
+    assert torch.equal(garena[:, 2 * Ch:], g0[:, 2 * Ch:])
+
+
+def test_depthwise_wgrad_accumulates_into_arena():
+    torch.manual_seed(3)
+    C, Ch, B, K, H = 2, 8, 4, 3, 10
+    P_ = Ch * K * K + 3
+    arena = torch.randn(C, P_, device=DEV) * 0.3
+    garena = torch.randn(C, P_, device=DEV)
+    g0 = garena.clone()
+    w = arena[:, 3:].view(C, Ch, 1, K, K).detach().requires_grad_(True)
+    w.grad = garena[:, 3:].view(C, Ch, 1, K, K)
+    wref = w.detach().clone().reshape(C * Ch, 1, K, K).requires_grad_(True)
+    x = torch.randn(B, C * Ch, H, H, device=DEV)
+    y = plane_ops.depthwise_conv2d(x, w, C, 1)
+    yr = F.conv2d(x, wref, padding=K // 2, groups=C * Ch)
+    gy = torch.randn_like(yr)
+    (y * gy).sum().backward()
+    (yr * gy).sum().backward()
+    assert _rel((garena[:, 3:] - g0[:, 3:]).reshape(C * Ch, 1, K, K), wref.grad) < 2e-5
+    assert torch.equal(garena[:, :3], g0[:, :3])
+
+
 def test_mobilenet_step_native_within_fp32_envelope():
     """One MobileNet / CIFAR-10 step of 2 clients in the batched interpreter on the native kernels (plane
     depthwise + plane BN/ReLU + implicit-GEMM pointwise / stem convolutions: no MIOpen) and on PyTorch ops,

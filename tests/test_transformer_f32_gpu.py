@@ -95,6 +95,33 @@ def test_client_linear_f32(mode, C, M, K, ns, gelu):
         _check(bb.grad, a, b, mode, "db")
 
 
+@pytest.mark.parametrize("C,M,K,N", [(3, 200, 768, 768), (2, 37, 30, 10), (2, 256, 128, 384)])
+def test_client_linear_f32_residual_epilogue(mode, C, M, K, N):
+    """y = res + x·Wᵀ + b with the residual added in the GEMM epilogue; dres = dy."""
+    torch.manual_seed(1)
+    w, b = _arena_views(C, [(N, K), (N,)], seed=1)
+    x = torch.randn(C, M, K, device=dev).requires_grad_(True)
+    r = torch.randn(C, M, N, device=dev).requires_grad_(True)
+    y = T.client_linear(x, [w], [b], res=r)
+    gy = torch.randn_like(y)
+    y.backward(gy)
+
+    def ref(dt):
+        wr, br = w.detach().to(dt).requires_grad_(True), b.detach().to(dt).requires_grad_(True)
+        xr, rr = x.detach().to(dt).requires_grad_(True), r.detach().to(dt).requires_grad_(True)
+        yr = rr + torch.bmm(xr, wr.transpose(1, 2)) + br.unsqueeze(1)
+        yr.backward(gy.to(dt))
+        return yr, xr.grad, rr.grad, wr.grad, br.grad
+
+    y64, dx64, dr64, dw64, db64 = ref(torch.float64)
+    y32, dx32, dr32, dw32, db32 = ref(torch.float32)
+    _check(y, y32, y64, mode, "y")
+    _check(x.grad, dx32, dx64, mode, "dx")
+    assert torch.equal(r.grad, gy)
+    _check(w.grad, dw32, dw64, mode, "dW")
+    _check(b.grad, db32, db64, mode, "db")
+
+
 @pytest.mark.parametrize("d,rpc,C,res,p", [(768, 40, 3, True, 0.1), (768, 33, 2, False, 0.0), (192, 17, 4, True, 0.0),
                                            (1024, 8, 2, False, 0.2)])
 def test_layer_norm_f32(d, rpc, C, res, p):
@@ -161,6 +188,27 @@ def test_attention_f32(mode, S, H, CB, mask, p):
         res[dt] = (o2, q2.grad)
     _check(o, res[torch.float32][0], res[torch.float64][0], mode, "o")
     _check(qkv.grad, res[torch.float32][1], res[torch.float64][1], mode, "dqkv")
+
+
+@pytest.mark.parametrize("S,H,CB,mask,p", [(197, 3, 4, False, 0.0), (128, 2, 3, True, 0.1), (37, 2, 5, True, 0.1)])
+def test_attention_qkv_packed_equals_sliced(S, H, CB, mask, p):
+    """The fused-qkv form (one gradient buffer, dq/dk/dv written into its column blocks) gives the same bits as
+    attention over the three column slices."""
+    torch.manual_seed(4)
+    dm = 64 * H
+    base = torch.randn(CB * S, 3 * dm, device=dev)
+    km = None
+    if mask:
+        km = torch.rand(CB, S, device=dev) > 0.3
+        km[:, 0] = True
+    go = torch.randn(CB * S, dm, device=dev)
+    a = base.clone().requires_grad_(True)
+    o1 = T.attention(a[:, :dm], a[:, dm:2 * dm], a[:, 2 * dm:], S, H, kmask=km, p=p, seed=5)
+    o1.backward(go)
+    b = base.clone().requires_grad_(True)
+    o2 = T.attention_qkv(b, S, H, kmask=km, p=p, seed=5)
+    o2.backward(go)
+    assert torch.equal(o1, o2) and torch.equal(a.grad, b.grad)
 
 
 def test_attention_f32_fully_masked_row_is_zero():
