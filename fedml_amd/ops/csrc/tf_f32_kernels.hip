@@ -619,6 +619,10 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const float* __restric
   const int q0 = blockIdx.x * 64, h = blockIdx.y, cb = blockIdx.z;
   const size_t tok0 = (size_t)cb * S;
   const int qr = q0 + 16 * w + (lane & 15);   // A-operand row of this lane
+  // wave-uniform skips of work that only touches padding (S not a multiple of 64, e.g. ViT's 197 tokens):
+  // a wave whose 16 query rows are all ≥ S, and 16-key blocks / 32-key halves entirely ≥ S (their scores are
+  // −∞ and their probabilities 0: skipping them leaves every result bit unchanged)
+  const bool wrows = q0 + 16 * w < S;
   typename P::frag_t qf[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
@@ -634,9 +638,11 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const float* __restric
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      if (wrows && kc * 64 + nb * 16 < S) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
-        acc = P::mma(qf[t], P::frag(Ks + (nb * 16 + (lane & 15)) * AKP + 32 * t + 8 * g), acc);
+        for (int t = 0; t < 2; ++t)
+          acc = P::mma(qf[t], P::frag(Ks + (nb * 16 + (lane & 15)) * AKP + 32 * t + 8 * g), acc);
+      }
       const int key = kc * 64 + nb * 16 + (lane & 15);
       const bool valid = key < S && (kmask == nullptr || kmask[tok0 + key] != 0);
 #pragma unroll
@@ -676,12 +682,16 @@ __global__ __launch_bounds__(256, 2) void attn_fwd_kernel(const float* __restric
       }
     }
     __syncthreads();
+    if (wrows) {
 #pragma unroll
-    for (int db = 0; db < 4; ++db)
+      for (int kt = 0; kt < 2; ++kt) {
+        if (kc * 64 + 32 * kt >= S) continue;
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-        ao[db] = P::mma(P::frag(Pw + (lane & 15) * AKP + 32 * kt + 8 * g), P::frag_tr(Vs, AVP, 32 * kt, 16 * db, lane),
-                        ao[db]);
+        for (int db = 0; db < 4; ++db)
+          ao[db] = P::mma(P::frag(Pw + (lane & 15) * AKP + 32 * kt + 8 * g),
+                          P::frag_tr(Vs, AVP, 32 * kt, 16 * db, lane), ao[db]);
+      }
+    }
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -744,6 +754,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const float* __rest
   const size_t tok0 = (size_t)cb * S;
   const size_t bhS = ((size_t)cb * H + h) * S;
   const int qr = blockIdx.x * 64 + 16 * w + (lane & 15);
+  const bool wrows = blockIdx.x * 64 + 16 * w < S;   // wave-uniform padding skips, as in the forward
   typename P::frag_t qf[2], df[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -772,11 +783,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const float* __rest
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb) {
       f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+      if (wrows && k0 + nb * 16 < S) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int off = (nb * 16 + (lane & 15)) * AKP + 32 * t + 8 * g;
-        s = P::mma(qf[t], P::frag(Ks + off), s);
-        dp = P::mma(df[t], P::frag(Vs + off), dp);
+        for (int t = 0; t < 2; ++t) {
+          const int off = (nb * 16 + (lane & 15)) * AKP + 32 * t + 8 * g;
+          s = P::mma(qf[t], P::frag(Ks + off), s);
+          dp = P::mma(df[t], P::frag(Vs + off), dp);
+        }
       }
       const int key = k0 + nb * 16 + (lane & 15);
       const bool valid = key < S && (kmask == nullptr || kmask[tok0 + key] != 0);
@@ -789,12 +802,16 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dq_kernel(const float* __rest
       }
     }
     __syncthreads();
+    if (wrows) {
 #pragma unroll
-    for (int db = 0; db < 4; ++db)
+      for (int kt = 0; kt < 2; ++kt) {
+        if (k0 + 32 * kt >= S) continue;
 #pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-        acc[db] = P::mma(P::frag(dS + (lane & 15) * AKP + 32 * kt + 8 * g), P::frag_tr(Ks, AKP, 32 * kt, 16 * db, lane),
-                         acc[db]);
+        for (int db = 0; db < 4; ++db)
+          acc[db] = P::mma(P::frag(dS + (lane & 15) * AKP + 32 * kt + 8 * g),
+                           P::frag_tr(Ks, AKP, 32 * kt, 16 * db, lane), acc[db]);
+      }
+    }
   }
 #pragma unroll
   for (int db = 0; db < 4; ++db)
@@ -828,6 +845,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(const float* __res
   const size_t tok0 = (size_t)cb * S;
   const size_t bhS = ((size_t)cb * H + h) * S;
   const int kr = blockIdx.x * 64 + 16 * w + (lane & 15);
+  const bool wkeys = blockIdx.x * 64 + 16 * w < S;   // wave-uniform padding skips, as in the forward
   typename P::frag_t kf[2], vf[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -861,11 +879,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(const float* __res
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb) {
       f32x4 st = {0.f, 0.f, 0.f, 0.f}, dpt = {0.f, 0.f, 0.f, 0.f};
+      if (wkeys && q0 + nb * 16 < S) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int off = (nb * 16 + (lane & 15)) * AKP + 32 * t + 8 * g;
-        st = P::mma(kf[t], P::frag(Qs + off), st);
-        dpt = P::mma(vf[t], P::frag(dOs + off), dpt);
+        for (int t = 0; t < 2; ++t) {
+          const int off = (nb * 16 + (lane & 15)) * AKP + 32 * t + 8 * g;
+          st = P::mma(kf[t], P::frag(Qs + off), st);
+          dpt = P::mma(vf[t], P::frag(dOs + off), dpt);
+        }
       }
       const int ql = nb * 16 + (lane & 15);
       const int qq = q0 + ql;
@@ -885,14 +905,18 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_dkv_kernel(const float* __res
       }
     }
     __syncthreads();
-#pragma unroll
-    for (int db = 0; db < 4; ++db)
+    if (wkeys) {
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
+        if (q0 + 32 * kt >= S) continue;
         const int ao = (lane & 15) * AKP + 32 * kt + 8 * g;
-        adv[db] = P::mma(P::frag(Pw + ao), P::frag_tr(dOs, AKP, 32 * kt, 16 * db, lane), adv[db]);
-        adk[db] = P::mma(P::frag(dSw + ao), P::frag_tr(Qs, AKP, 32 * kt, 16 * db, lane), adk[db]);
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+          adv[db] = P::mma(P::frag(Pw + ao), P::frag_tr(dOs, AKP, 32 * kt, 16 * db, lane), adv[db]);
+          adk[db] = P::mma(P::frag(dSw + ao), P::frag_tr(Qs, AKP, 32 * kt, 16 * db, lane), adk[db]);
+        }
       }
+    }
   }
 #pragma unroll
   for (int db = 0; db < 4; ++db)

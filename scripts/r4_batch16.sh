@@ -1,0 +1,10 @@
+#!/bin/bash
+# fused-qkv attention: transformer tests, presets, glue attribution with call sites
+cd "$(dirname "$0")/.." && mkdir -p gpurun_out
+export TMPDIR=/tmp
+bash scripts/gpu_steps.sh \
+ "timeout -k 10 400 python -u -m pytest tests/test_transformer_f32_gpu.py tests/test_transformer_kernels_gpu.py tests/test_determinism.py tests/test_apis_gpu.py -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider -rf > gpurun_out/r4_t16.log 2>&1" \
+ "timeout -k 10 150 python -u bench.py --preset distilbert_fedopt_32 --steps 5 --warmup 2 > gpurun_out/r4_distil_b16.json 2>&1" \
+ "timeout -k 10 150 python -u bench.py --preset vit_b16_32 --steps 4 --warmup 2 > gpurun_out/r4_vit_b16.json 2>&1" \
+ "FEDML_AMD_HIP_GRAPHS=0 timeout -k 10 200 python -u scripts/torch_op_prof.py --preset distilbert_fedopt_32 > gpurun_out/r4_distil_ops2.txt 2>&1" \
+ "FEDML_AMD_HIP_GRAPHS=0 timeout -k 10 200 python -u scripts/torch_op_prof.py --preset vit_b16_32 > gpurun_out/r4_vit_ops2.txt 2>&1"
