@@ -45,7 +45,7 @@ constexpr int LDT = BM + 2;      // TR tile [32][130]: ≡ 2 (mod 4) → the two
 constexpr int TILE = BM * LDR;   // floats per operand image
 static_assert(BK * LDT <= TILE, "TR image must fit the tile slot");
 
-enum { EPI_STORE = 0, EPI_GELU = 1, EPI_ACC = 2 };
+enum { EPI_STORE = 0, EPI_GELU = 1, EPI_ACC = 2, EPI_DGELU = 3 };   // DGELU: D ⊙ gelu'(R) (a GELU's input grad)
 
 struct Segs {        // row segments of an operand (≤ 4 arena slots); one segment = a plain matrix
   int64_t off[4];    // element offset of segment s's first row, relative to the client base
@@ -89,6 +89,12 @@ struct Args {
 };
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_grad(float x, float g) {
+  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
+  return g * (cdf + x * pdf);
+}
+
 
 // Stage one operand tile into registers (4 float4 per thread):
 //   TR = 0: logical rows [r0, r0+128) × k [k0, k0+32) of storage S[row][k]          (row segmented)
@@ -265,6 +271,18 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args p) {
 #pragma unroll
             for (int r = 0; r < 4; ++r)
               if (n + r < p.N) v[r] += bp[seg_row(p.biasseg, n + r, 1)];
+          }
+        }
+        if (EPI == EPI_DGELU) {   // the data gradient of a GELU'd linear's output, through the GELU
+          const float* rp = p.R + (int64_t)c * p.r_bs + (int64_t)m * p.ldr + n;
+          if (VEC) {
+            const float4 x4 = *reinterpret_cast<const float4*>(rp);
+            v[0] = gelu_grad(x4.x, v[0]); v[1] = gelu_grad(x4.y, v[1]);
+            v[2] = gelu_grad(x4.z, v[2]); v[3] = gelu_grad(x4.w, v[3]);
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (n + r < p.N) v[r] = gelu_grad(rp[r], v[r]);
           }
         }
         if (EPI == EPI_STORE && p.R) {
@@ -507,12 +525,6 @@ __global__ __launch_bounds__(256) void gelu_fwd_kernel(const float* __restrict__
     const float4 v = reinterpret_cast<const float4*>(x)[i];
     reinterpret_cast<float4*>(y)[i] = make_float4(gelu_erf(v.x), gelu_erf(v.y), gelu_erf(v.z), gelu_erf(v.w));
   }
-}
-
-__device__ __forceinline__ float gelu_grad(float x, float g) {
-  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
-  const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
-  return g * (cdf + x * pdf);
 }
 
 __global__ __launch_bounds__(256) void gelu_bwd_kernel(const float* __restrict__ x, const float* __restrict__ gy,
@@ -1027,6 +1039,24 @@ FA_EXPORT int fa_bgemm_dgrad_f32(const float* dy, int64_t dy_bs, int lddy, const
   a.tiles_m = (M + BM - 1) / BM; a.tiles_n = (K + BN - 1) / BN; a.nclients = C;
   const bool vec = al4({dy_bs, lddy, N, w_cs, K, dx_bs, lddx}) && segs_al4(a.bseg) && al16({dy, w_base, dx});
   FA_F32_DISPATCH(tff, (launch_gemm<PX, 0, 1, EPI_STORE>(a, vec, stream)));
+}
+
+// dx[c] = (dy[c] · W[c]) ⊙ gelu'(pre[c])   pre [C][M][K] (the pre-activation of the GELU that produced x)
+FA_EXPORT int fa_bgemm_dgrad_dgelu_f32(const float* dy, int64_t dy_bs, int lddy, const float* w_base, int64_t w_cs,
+                                       const int64_t* w_off, const int* seg_lo, int nseg, float* dx, int64_t dx_bs,
+                                       int lddx, const float* pre, int C, int M, int N, int K, hipStream_t stream) {
+  using namespace tff;
+  if (nseg < 1 || nseg > 4 || C <= 0 || M <= 0 || N <= 0 || K <= 0 || !pre) return (int)hipErrorInvalidValue;
+  Args a{};
+  a.A = dy; a.a_bs = dy_bs; a.lda = lddy;
+  a.B = w_base; a.b_bs = w_cs; a.ldb = K;
+  fill_segs(a.bseg, w_off, seg_lo, nseg);
+  a.Cp = dx; a.c_bs = dx_bs; a.ldc = lddx;
+  a.R = pre; a.r_bs = dx_bs; a.ldr = lddx;
+  a.M = M; a.N = K; a.K = N;
+  a.tiles_m = (M + BM - 1) / BM; a.tiles_n = (K + BN - 1) / BN; a.nclients = C;
+  const bool vec = al4({dy_bs, lddy, N, w_cs, K, dx_bs, lddx}) && segs_al4(a.bseg) && al16({dy, w_base, dx, pre});
+  FA_F32_DISPATCH(tff, (launch_gemm<PX, 0, 1, EPI_DGELU>(a, vec, stream)));
 }
 
 // dx[c] += dy[c] · W[c]   (accumulating form: the residual-stream gradient the caller already holds in dx —

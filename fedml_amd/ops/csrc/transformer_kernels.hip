@@ -312,6 +312,9 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
   }
   for (int q0 = 0; q0 < S; q0 += 64) {
     const int qr = q0 + w * 16 + (lane & 15);  // A-operand row of this lane
+    // wave-uniform skips of padding-only work (query waves past S, 16-key blocks / 32-key halves past S):
+    // their scores are −∞ and probabilities 0, so every result bit is unchanged
+    const bool wrows = q0 + w * 16 < S;
     bf16x8_mf qf[2];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -321,10 +324,12 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
 #pragma unroll
     for (int nb = 0; nb < NB; ++nb) {
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      if (wrows && nb * 16 < S) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[t], lds8(Ks + (nb * 16 + (lane & 15)) * KST + 32 * t + 8 * (lane >> 4)),
-                                                       acc, 0, 0, 0);
+        for (int t = 0; t < 2; ++t)
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+              qf[t], lds8(Ks + (nb * 16 + (lane & 15)) * KST + 32 * t + 8 * (lane >> 4)), acc, 0, 0, 0);
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) acc[r] = kval[nb] ? acc[r] * c2 : -INFINITY;
       sc[nb] = acc;
@@ -363,8 +368,9 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
       f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int kt = 0; kt < SP / 32; ++kt)
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(P + (lane & 15) * VST + kt * 32 + 8 * (lane >> 4)),
-                                                       tr8(Vs, KST, kt * 32, db * 16, lane), acc, 0, 0, 0);
+        if (wrows && kt * 32 < S)
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(P + (lane & 15) * VST + kt * 32 + 8 * (lane >> 4)),
+                                                         tr8(Vs, KST, kt * 32, db * 16, lane), acc, 0, 0, 0);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int qrow = qbase + r;
@@ -424,6 +430,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const uint16_t* __rest
   const size_t tok0 = (size_t)cb * S;
   const size_t bhS = ((size_t)cb * H + h) * S;
   const int qr = blockIdx.x * 64 + w * 16 + (lane & 15);
+  const bool wrows = blockIdx.x * 64 + w * 16 < S;   // wave-uniform padding skips, as in the forward
   bf16x8_mf qf[2], df[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -452,11 +459,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const uint16_t* __rest
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb) {
       f32x4 s = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+      if (wrows && k0 + nb * 16 < S) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int off = (nb * 16 + (lane & 15)) * KST + 32 * t + 8 * (lane >> 4);
-        s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[t], lds8(Ks + off), s, 0, 0, 0);
-        dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(df[t], lds8(Vs + off), dp, 0, 0, 0);
+        for (int t = 0; t < 2; ++t) {
+          const int off = (nb * 16 + (lane & 15)) * KST + 32 * t + 8 * (lane >> 4);
+          s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qf[t], lds8(Ks + off), s, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(df[t], lds8(Vs + off), dp, 0, 0, 0);
+        }
       }
       const int key = k0 + nb * 16 + (lane & 15);
       const bool valid = key < S && (kmask == nullptr || kmask[tok0 + key] != 0);
@@ -473,8 +482,9 @@ __global__ __launch_bounds__(256) void attn_bwd_dq_kernel(const uint16_t* __rest
     for (int db = 0; db < 4; ++db)
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
-        acc[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(dS + (lane & 15) * KST + kt * 32 + 8 * (lane >> 4)),
-                                                          tr8(Ks, KST, kt * 32, db * 16, lane), acc[db], 0, 0, 0);
+        if (wrows && k0 + kt * 32 < S)
+          acc[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(dS + (lane & 15) * KST + kt * 32 + 8 * (lane >> 4)),
+                                                            tr8(Ks, KST, kt * 32, db * 16, lane), acc[db], 0, 0, 0);
   }
 #pragma unroll
   for (int db = 0; db < 4; ++db)
@@ -507,6 +517,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const uint16_t* __res
   const size_t tok0 = (size_t)cb * S;
   const size_t bhS = ((size_t)cb * H + h) * S;
   const int kr = blockIdx.x * 64 + w * 16 + (lane & 15);
+  const bool wkeys = blockIdx.x * 64 + w * 16 < S;   // wave-uniform padding skips, as in the forward
   bf16x8_mf kf[2], vf[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
@@ -540,11 +551,13 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const uint16_t* __res
 #pragma unroll
     for (int nb = 0; nb < 4; ++nb) {
       f32x4 st = {0.f, 0.f, 0.f, 0.f}, dpt = {0.f, 0.f, 0.f, 0.f};
+      if (wkeys && q0 + nb * 16 < S) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        const int off = (nb * 16 + (lane & 15)) * KST + 32 * t + 8 * (lane >> 4);
-        st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[t], lds8(Qs + off), st, 0, 0, 0);
-        dpt = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[t], lds8(dOs + off), dpt, 0, 0, 0);
+        for (int t = 0; t < 2; ++t) {
+          const int off = (nb * 16 + (lane & 15)) * KST + 32 * t + 8 * (lane >> 4);
+          st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[t], lds8(Qs + off), st, 0, 0, 0);
+          dpt = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf[t], lds8(dOs + off), dpt, 0, 0, 0);
+        }
       }
       const int ql = nb * 16 + (lane & 15);
       const int qq = q0 + ql;
@@ -568,6 +581,7 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const uint16_t* __res
     for (int db = 0; db < 4; ++db)
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
+        if (!wkeys || q0 + kt * 32 >= S) continue;
         const int ao = (lane & 15) * KST + kt * 32 + 8 * (lane >> 4);
         adv[db] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(Pw + ao), tr8(dOs, KST, kt * 32, db * 16, lane),
                                                           adv[db], 0, 0, 0);

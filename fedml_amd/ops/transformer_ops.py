@@ -112,6 +112,17 @@ class ResLink:
         self.closed = False
 
 
+class GeluLink:
+    """Hand-off between a GELU'd linear (``gelu=True``, the producer: its pre-activation) and the linear that
+    consumes its output: the consumer's data-gradient GEMM applies gelu'(pre) in its epilogue and the producer
+    then skips its separate GELU-backward pass (fp32 native path). The consumer's backward runs first."""
+    __slots__ = ("pre", "fused")
+
+    def __init__(self):
+        self.pre = None
+        self.fused = False
+
+
 class _LayerNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, h, res, gamma, beta, eps, p, seed, rpc, seed_dev, link=None, in_link=None):
@@ -392,8 +403,9 @@ class _ClientLinear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gelu, n_w, shadows, res, links, *params):
         ws, bs = params[:n_w], params[n_w:]
-        # links = (dx_link, res_link) (ResLink | None each; fp32 native only)
-        ctx.dx_link, ctx.res_link = links if (links is not None and x.dtype == torch.float32) else (None, None)
+        # links = (dx_link, res_link, gelu_out, gelu_in): ResLink / GeluLink | None each; fp32 native only
+        ctx.dx_link, ctx.res_link, ctx.gelu_out, ctx.gelu_in = \
+            links if (links is not None and x.dtype == torch.float32) else (None, None, None, None)
         C, M, K = x.shape
         N = sum(w.shape[1] for w in ws)
         # bf16 shadow of the weights (refreshed once per step by the engine) when given: half the
@@ -431,6 +443,8 @@ class _ClientLinear(torch.autograd.Function):
         ctx.save_for_backward(x, y if gelu else None)
         ctx.ws, ctx.bs, ctx.gelu, ctx.wsrc = ws, bs, gelu, wsrc
         ctx.has_res = res is not None
+        if gelu and ctx.gelu_out is not None:
+            ctx.gelu_out.pre = y            # the consumer's dgrad applies gelu'(pre)
         return y2 if gelu else y
 
     @staticmethod
@@ -445,7 +459,9 @@ class _ClientLinear(torch.autograd.Function):
             g_res = None
         g = g.to(x.dtype).contiguous()
         sfx = _sfx(x)
-        if ctx.gelu:
+        if ctx.gelu and ctx.gelu_out is not None and ctx.gelu_out.fused:
+            ctx.gelu_out.pre = None         # g is already the gradient through the GELU
+        elif ctx.gelu:
             gp = torch.empty_like(pre)
             _check(_fn("fa_gelu_bwd" + sfx)(_p(pre), _p(g), _p(gp), _i64(pre.numel()), _stream(pre)),
                    "fa_gelu_bwd" + sfx)
@@ -458,7 +474,17 @@ class _ClientLinear(torch.autograd.Function):
             acc = sfx and link is not None and link.g is not None
             if link is not None and not acc:
                 link.closed = True
-            if acc:   # x's other consumer (a post-LN residual) left its gradient: add ours into it
+            gl = ctx.gelu_in
+            dgelu = sfx and not acc and gl is not None and gl.pre is not None and gl.pre.shape == x.shape
+            if dgelu:   # x = gelu(pre) of the previous linear: return the gradient w.r.t. pre directly
+                dx = torch.empty_like(x)
+                rc = _fn("fa_bgemm_dgrad_dgelu_f32")(_p(g), _i64(M * N), _c.c_int(N), _p(wb), _i64(wcs), woff, lo,
+                                                     _c.c_int(len(ws)), _p(dx), _i64(M * K), _c.c_int(K),
+                                                     _p(gl.pre), _c.c_int(C), _c.c_int(M), _c.c_int(N), _c.c_int(K),
+                                                     _stream(x))
+                gl.fused = True
+                gl.pre = None
+            elif acc:   # x's other consumer (a post-LN residual) left its gradient: add ours into it
                 dx = link.g.view(C, M, K)
                 link.g = None
                 assert dx.dtype == torch.float32 and dx.is_contiguous()
@@ -527,7 +553,8 @@ class _ClientLinear(torch.autograd.Function):
 
 
 def client_linear(x: torch.Tensor, weights, biases=None, gelu: bool = False, shadows=None,
-                  res: torch.Tensor = None, dx_link: "ResLink" = None, res_link: "ResLink" = None) -> torch.Tensor:
+                  res: torch.Tensor = None, dx_link: "ResLink" = None, res_link: "ResLink" = None,
+                  gelu_out: "GeluLink" = None, gelu_in: "GeluLink" = None) -> torch.Tensor:
     """Per-client linear over client-stacked activations ``x`` [C, M, K]: ``weights`` is a list of
     [C, n_i, K] fp32 arena views (concatenated along the output dim), ``biases`` the matching
     [C, n_i] views or None; ``gelu`` fuses the exact-erf GELU into the epilogue. ``shadows``: the
@@ -536,7 +563,8 @@ def client_linear(x: torch.Tensor, weights, biases=None, gelu: bool = False, sha
     activation dtype (bf16, or fp32 through ``tf_f32_kernels.hip``); CPU → the fp32 PyTorch reference.
     ``res`` [C, M, N] (no GELU): the result is ``res + linear(x)`` — at fp32 added in the GEMM epilogue (the residual
     stream of a pre-LN block without a separate add pass). ``dx_link`` / ``res_link``: :class:`ResLink`
-    hand-offs of the residual-stream gradient (fp32 native path)."""
+    hand-offs of the residual-stream gradient; ``gelu_out`` (on a ``gelu=True`` linear) / ``gelu_in`` (on the
+    linear reading its output): :class:`GeluLink`, the GELU backward folded into the consumer's dgrad GEMM."""
     assert res is None or not gelu
     weights = list(weights)
     biases = list(biases) if biases else []
@@ -548,7 +576,8 @@ def client_linear(x: torch.Tensor, weights, biases=None, gelu: bool = False, sha
         if sh is not None:
             assert len(sh) == len(weights) and all(t.shape == w.shape for t, w in zip(sh, weights))
         r = res.contiguous() if res is not None else None
-        links = (dx_link, res_link) if (dx_link is not None or res_link is not None) else None
+        links = (dx_link, res_link, gelu_out, gelu_in) \
+            if any(t is not None for t in (dx_link, res_link, gelu_out, gelu_in)) else None
         return _ClientLinear.apply(x.contiguous(), bool(gelu), len(weights), sh, r, links, *weights, *biases)
     w = torch.cat([t.reshape(C, t.shape[1], K) for t in weights], 1)
     y = torch.bmm(x.float(), w.float().transpose(1, 2))

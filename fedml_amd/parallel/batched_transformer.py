@@ -105,7 +105,8 @@ class BatchedTransformer:
         self._sh = None
 
     # -------------------------------------------------------------------------------- helpers
-    def _lin(self, v, x, key, dt, weights=None, gelu=False, res=None, dx_link=None, res_link=None):
+    def _lin(self, v, x, key, dt, weights=None, gelu=False, res=None, dx_link=None, res_link=None, gelu_out=None,
+             gelu_in=None):
         """x [C, T, in] → [C, T, out] with per-client W [C, out, in] and bias [C, out] read straight
         from the fp32 arena views (``ops.transformer_ops.client_linear``: one batched MFMA GEMM per
         linear, weight gradients accumulated into the gradient arena; ``gelu`` fuses the
@@ -117,7 +118,8 @@ class BatchedTransformer:
                 sh = [self._sh[key + ".weight"]]
         else:
             ws, bs, sh = weights
-        return T.client_linear(_bf(x, dt), ws, bs, gelu=gelu, shadows=sh, res=res, dx_link=dx_link, res_link=res_link)
+        return T.client_linear(_bf(x, dt), ws, bs, gelu=gelu, shadows=sh, res=res, dx_link=dx_link, res_link=res_link,
+                               gelu_out=gelu_out, gelu_in=gelu_in)
 
     def _qkv(self, v, x, pre, dt, dx_link=None):
         names = ("q_lin", "k_lin", "v_lin")
@@ -136,6 +138,11 @@ class BatchedTransformer:
     def _link(x, dt):
         """A residual-gradient hand-off (ops.transformer_ops.ResLink) on the fp32 native path, else None."""
         return T.ResLink() if (x.is_cuda and dt == torch.float32) else None
+
+    @staticmethod
+    def _glink(x, dt):
+        """A GELU-backward hand-off (ops.transformer_ops.GeluLink) on the fp32 native path, else None."""
+        return T.GeluLink() if (x.is_cuda and dt == torch.float32) else None
 
     def _attn(self, v, x, pre, S, kmask, training, dt, seed, res=None, dx_link=None, res_link=None):
         C, Tk, d = x.shape
@@ -184,8 +191,9 @@ class BatchedTransformer:
             sa = self._attn(v, x, pre + ".attention", S, kmask, training, dt, base + 10 * i + 1, dx_link=l1)
             x = self._ln(v, pre + ".sa_layer_norm", sa.contiguous(), rows, res=x,
                          p=self.p_hidden if training else 0.0, seed=base + 10 * i + 2, res_link=l1)
-            f = self._lin(v, x, pre + ".ffn.lin1", dt, gelu=True, dx_link=l2)
-            f = self._lin(v, f, pre + ".ffn.lin2", dt)
+            gl = self._glink(x, dt)
+            f = self._lin(v, x, pre + ".ffn.lin1", dt, gelu=True, dx_link=l2, gelu_out=gl)
+            f = self._lin(v, f, pre + ".ffn.lin2", dt, gelu_in=gl)
             x = self._ln(v, pre + ".output_layer_norm", f.contiguous(), rows, res=x,
                          p=self.p_hidden if training else 0.0, seed=base + 10 * i + 3, res_link=l2)
         cls = x.view(C, B, S, d)[:, :, 0]                                                      # [C, B, d]
@@ -217,8 +225,9 @@ class BatchedTransformer:
             # LayerNorm that also reads x, which adds it in its own kernel (ResLink)
             x = self._attn(v, h, pre + ".attn", S, None, training, dt, base + 10 * i + 1, res=x, res_link=l1)
             h = self._ln(v, pre + ".norm2", x, rows, in_link=l2)
-            f = self._lin(v, h, pre + ".mlp.lin1", dt, gelu=True)
-            x = self._lin(v, f, pre + ".mlp.lin2", dt, res=x, res_link=l2)
+            gl = self._glink(x, dt)
+            f = self._lin(v, h, pre + ".mlp.lin1", dt, gelu=True, gelu_out=gl)
+            x = self._lin(v, f, pre + ".mlp.lin2", dt, res=x, res_link=l2, gelu_in=gl)
         cls_out = x.view(C, B, S, d)[:, :, 0].contiguous()
         y = self._ln(v, "norm", cls_out, B)
         return self._lin(v, y, "head", dt).float()

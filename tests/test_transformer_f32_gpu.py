@@ -122,6 +122,37 @@ def test_client_linear_f32_residual_epilogue(mode, C, M, K, N):
     _check(b.grad, db32, db64, mode, "db")
 
 
+def test_mlp_links_fold_gelu_backward_and_residual(mode):
+    """x → LN → lin1(GELU) → lin2 (+ x), with the GELU backward folded into lin2's dgrad (GeluLink) and the
+    residual gradient handed to the LN backward (ResLink): same gradients as the plain composition."""
+    torch.manual_seed(5)
+    C, M, d, hid = 2, 70, 128, 256
+    g1, b1, w1, bb1, w2, bb2 = _arena_views(C, [(d,), (d,), (hid, d), (hid,), (d, hid), (d,)], seed=5)
+    with torch.no_grad():
+        g1 += 1.0
+    x0 = torch.randn(C, M, d, device=dev)
+    gy = torch.randn(C, M, d, device=dev)
+    outs = []
+    for linked in (False, True):
+        for t in (g1, b1, w1, bb1, w2, bb2):
+            t.grad.zero_()
+        x = x0.clone().requires_grad_(True)
+        rl = T.ResLink() if linked else None
+        gl = T.GeluLink() if linked else None
+        h = T.layer_norm(x.reshape(-1, d), g1, b1, 1e-5, M, in_link=rl).view(C, M, d)
+        f = T.client_linear(h, [w1], [bb1], gelu=True, gelu_out=gl)
+        y = T.client_linear(f, [w2], [bb2], res=x, res_link=rl, gelu_in=gl)
+        y.backward(gy)
+        outs.append((y.detach(), x.grad.clone(), [t.grad.clone() for t in (g1, b1, w1, bb1, w2, bb2)]))
+        if linked:
+            assert gl.fused
+    (y0, dx0, gr0), (y1, dx1, gr1) = outs
+    assert torch.equal(y0, y1)
+    assert _rel(dx1, dx0) < 1e-6
+    for a, b in zip(gr1, gr0):
+        assert _rel(a, b) < 1e-6
+
+
 @pytest.mark.parametrize("d,rpc,C,res,p", [(768, 40, 3, True, 0.1), (768, 33, 2, False, 0.0), (192, 17, 4, True, 0.0),
                                            (1024, 8, 2, False, 0.2)])
 def test_layer_norm_f32(d, rpc, C, res, p):
