@@ -444,8 +444,13 @@ static int wgrad_wide(const typename P::T* g, const typename P::T* yv, const flo
   const int nks = (K + 127) / 128;
   const int base = fa_plan_c(C) * nks * (Cout / 128);
   const int M = Nb * Ho * Wo;
-  // pixel chunks: enough workgroups to fill the chip (≈2048), chunks of ≥ 512 pixels
-  int gx = max(1, min((2048 + base - 1) / base, (M + 511) / 512));
+  // pixel chunks: enough workgroups to fill the chip (≈2048 by default; FEDML_AMD_WGW_WGS), chunks of ≥ 512 pixels.
+  // One chunk (gx = 1) writes the gradient arena directly — no fp32-atomic scratch and no scatter pass.
+  static const int target = [] {
+    const char* e = getenv("FEDML_AMD_WGW_WGS");
+    return e ? atoi(e) : 2048;
+  }();
+  int gx = max(1, min((target + base - 1) / base, (M + 511) / 512));
   int ppw = ((M + gx - 1) / gx + PT - 1) / PT * PT;
   gx = (M + ppw - 1) / ppw;
   const int direct = gx == 1;

@@ -17,6 +17,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--preset", default="distilbert_fedopt_32")
     ap.add_argument("--rows", type=int, default=40)
+    ap.add_argument("--trace-dtoh", action="store_true")
     ap.add_argument("--stacks", default="aten::copy_,aten::fill_,aten::add_,aten::add,aten::zero_,aten::mul",
                     help="ops whose Python call sites are printed (comma list; '' = none)")
     a, rest = ap.parse_known_args()
@@ -50,6 +51,26 @@ def main():
         return r
 
     S.RCCLSimulator.run = run
+    if a.trace_dtoh:   # print the Python call site of every device→host copy above 1 MB
+        import traceback
+        seen = {}
+
+        def wrap(name):
+            orig_m = getattr(torch.Tensor, name)
+
+            def f(t, *args, **kw):
+                if t.is_cuda and t.numel() * t.element_size() > (1 << 20):
+                    dst = args[0] if args else kw.get("device", kw.get("dtype"))
+                    if name != "to" or (isinstance(dst, (str, torch.device)) and str(dst).startswith("cpu")):
+                        site = "".join(traceback.format_stack(limit=6)[:-1])
+                        seen[site] = seen.get(site, 0) + 1
+                        if seen[site] == 1:
+                            print(f"== DtoH via Tensor.{name}: {t.numel() * t.element_size() / 2**20:.1f} MB\n{site}",
+                                  flush=True)
+                return orig_m(t, *args, **kw)
+            setattr(torch.Tensor, name, f)
+        for n_ in ("cpu", "to", "numpy", "tolist", "item"):
+            wrap(n_)
     sys.argv = ["bench.py", "--preset", a.preset, "--steps", "1", "--warmup", "1"] + rest
     bench.main()
 
