@@ -81,6 +81,9 @@ struct Args {
   int64_t bias_bs;
   Segs biasseg;
   float* C2;         // GELU: gelu(D + b); Cp keeps the pre-activation for the backward
+  float* bg;         // ACC with A_TR (weight gradient): optional bias gradient += Σ_t A[t][m] (segmented rows)
+  int64_t bg_bs;
+  Segs bgseg;
   const float* R;    // STORE: optional residual addend [C][M][ldr] (D = A·Bᵀ + b + R: a pre-LN block's x + f(x))
   int64_t r_bs;
   int ldr;
@@ -159,12 +162,21 @@ __device__ __forceinline__ typename P::frag_t frag_of(const float* tile, int row
   return P::frag_tile(tile + (row0 + (lane & 15)) * LDR + 8 * (lane >> 4));
 }
 
-template <class P, int A_TR, int B_TR, int VEC, int CHECK>
+// BSUM (weight gradient, A_TR): also sum the staged A chunks of this thread (its 4 rows t of 4 columns m) —
+// the bias gradient Σ_t dy[t][m] comes out of the same operand reads
+template <class P, int A_TR, int B_TR, int VEC, int CHECK, int BSUM = 0>
 __device__ __forceinline__ void gemm_mainloop(f32x4 (&acc)[4][4], const float* A, const Segs& aseg, const float* B,
                                               const Args& p, int m0, int n0, int nk, float* SA0, float* SB0, int tid,
-                                              int lane, int wm, int wn) {
+                                              int lane, int wm, int wn, float4& bs) {
   float4 ra[4], rb[4];
+  auto bsum = [&]() {
+    if constexpr (BSUM != 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { bs.x += ra[i].x; bs.y += ra[i].y; bs.z += ra[i].z; bs.w += ra[i].w; }
+    }
+  };
   load_tile<A_TR, VEC, CHECK>(ra, A, aseg, p.lda, p.M, p.K, m0, 0, tid);
+  bsum();
   load_tile<B_TR, VEC, CHECK>(rb, B, p.bseg, p.ldb, p.N, p.K, n0, 0, tid);
   store_tile<P, A_TR>(SA0, ra, tid);
   store_tile<P, B_TR>(SB0, rb, tid);
@@ -176,6 +188,7 @@ __device__ __forceinline__ void gemm_mainloop(f32x4 (&acc)[4][4], const float* A
     if (more) {   // the next K-step's global reads fly under this step's MFMAs
       load_tile<A_TR, VEC, CHECK>(ra, A, aseg, p.lda, p.M, p.K, m0, (kt + 1) * BK, tid);
       load_tile<B_TR, VEC, CHECK>(rb, B, p.bseg, p.ldb, p.N, p.K, n0, (kt + 1) * BK, tid);
+      bsum();
     }
     const float* ta = SA0 + cur * TILE;
     const float* tb = SB0 + cur * TILE;
@@ -234,11 +247,46 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = (p.K + BK - 1) / BK;
+  float4 bs = make_float4(0.f, 0.f, 0.f, 0.f);
   // interior blocks (the vast majority) stage their tiles with unpredicated vector loads
-  if (VEC && m0 + BM <= p.M && n0 + BN <= p.N && (p.K % BK) == 0)
-    gemm_mainloop<P, A_TR, B_TR, VEC, 0>(acc, A, aseg, B, p, m0, n0, nk, SA0, SB0, tid, lane, wm, wn);
-  else
-    gemm_mainloop<P, A_TR, B_TR, VEC, 1>(acc, A, aseg, B, p, m0, n0, nk, SA0, SB0, tid, lane, wm, wn);
+  const bool interior = VEC && m0 + BM <= p.M && n0 + BN <= p.N && (p.K % BK) == 0;
+  if constexpr (EPI == EPI_ACC && A_TR == 1 && VEC == 1) {
+    // weight gradient with a fused bias gradient: the first column-block of every row-block sums its A operand
+    if (p.bg != nullptr && tn == 0) {
+      if (interior)
+        gemm_mainloop<P, A_TR, B_TR, VEC, 0, 1>(acc, A, aseg, B, p, m0, n0, nk, SA0, SB0, tid, lane, wm, wn, bs);
+      else
+        gemm_mainloop<P, A_TR, B_TR, VEC, 1, 1>(acc, A, aseg, B, p, m0, n0, nk, SA0, SB0, tid, lane, wm, wn, bs);
+      // the 8 threads holding the same 4 columns (tid & 31) combine through LDS (free after the main loop)
+      float4* red = reinterpret_cast<float4*>(smem);
+      red[tid] = bs;
+      __syncthreads();
+      if (tid < 32) {
+        float4 t4 = red[tid];
+#pragma unroll
+        for (int g8 = 1; g8 < NT / 32; ++g8) {
+          const float4 u = red[g8 * 32 + tid];
+          t4.x += u.x; t4.y += u.y; t4.z += u.z; t4.w += u.w;
+        }
+        const int m = m0 + 4 * tid;
+        if (m < p.M) {   // m .. m+3 in one segment (segment bounds are multiples of 4 on the VEC path)
+          float4* bp = reinterpret_cast<float4*>(p.bg + (int64_t)c * p.bg_bs + seg_row(p.bgseg, m, 1));
+          float4 o = *bp;
+          o.x += t4.x; o.y += t4.y; o.z += t4.z; o.w += t4.w;
+          *bp = o;
+        }
+      }
+    } else if (interior) {
+      gemm_mainloop<P, A_TR, B_TR, VEC, 0>(acc, A, aseg, B, p, m0, n0, nk, SA0, SB0, tid, lane, wm, wn, bs);
+    } else {
+      gemm_mainloop<P, A_TR, B_TR, VEC, 1>(acc, A, aseg, B, p, m0, n0, nk, SA0, SB0, tid, lane, wm, wn, bs);
+    }
+  } else {
+    if (interior)
+      gemm_mainloop<P, A_TR, B_TR, VEC, 0>(acc, A, aseg, B, p, m0, n0, nk, SA0, SB0, tid, lane, wm, wn, bs);
+    else
+      gemm_mainloop<P, A_TR, B_TR, VEC, 1>(acc, A, aseg, B, p, m0, n0, nk, SA0, SB0, tid, lane, wm, wn, bs);
+  }
 
   // epilogue: lane owns row m = m0 + wm + 16i + (lane & 15), cols n .. n+3, n = n0 + wn + 16j + 4(lane >> 4)
 #pragma unroll
@@ -1093,6 +1141,29 @@ FA_EXPORT int fa_bgemm_wgrad_f32(const float* dy, int64_t dy_bs, int lddy, const
   a.M = N; a.N = K; a.K = T;
   a.tiles_m = (N + BM - 1) / BM; a.tiles_n = (K + BN - 1) / BN; a.nclients = C;
   const bool vec = al4({dy_bs, lddy, N, x_bs, ldx, K, g_cs}) && segs_al4(a.cseg) && al16({dy, x, g_base});
+  FA_F32_DISPATCH(tff, (launch_gemm<PX, 1, 1, EPI_ACC>(a, vec, stream)));
+}
+
+// dW[c] += dy[c]ᵀ · x[c] and db[c] += Σ_t dy[c][t][:] in one pass over dy (bias segments share seg_lo)
+FA_EXPORT int fa_bgemm_wgrad_bias_f32(const float* dy, int64_t dy_bs, int lddy, const float* x, int64_t x_bs,
+                                      int ldx, float* g_base, int64_t g_cs, const int64_t* g_off, const int* seg_lo,
+                                      int nseg, float* b_base, int64_t b_cs, const int64_t* b_off, int C, int T, int N,
+                                      int K, hipStream_t stream) {
+  using namespace tff;
+  if (nseg < 1 || nseg > 4 || C <= 0 || T <= 0 || N <= 0 || K <= 0 || !b_base) return (int)hipErrorInvalidValue;
+  Args a{};
+  a.A = dy; a.a_bs = dy_bs; a.lda = lddy;
+  a.B = x; a.b_bs = x_bs; a.ldb = ldx;
+  fill_segs(a.bseg, nullptr, nullptr, 1);
+  a.Cp = g_base; a.c_bs = g_cs; a.ldc = K;
+  fill_segs(a.cseg, g_off, seg_lo, nseg);
+  a.bg = b_base; a.bg_bs = b_cs;
+  fill_segs(a.bgseg, b_off, seg_lo, nseg);
+  a.M = N; a.N = K; a.K = T;
+  a.tiles_m = (N + BM - 1) / BM; a.tiles_n = (K + BN - 1) / BN; a.nclients = C;
+  const bool vec = al4({dy_bs, lddy, N, x_bs, ldx, K, g_cs, b_cs}) && segs_al4(a.cseg) && segs_al4(a.bgseg) &&
+                   al16({dy, x, g_base, b_base});
+  if (!vec) return -2;   // the caller falls back to the separate bias reduction
   FA_F32_DISPATCH(tff, (launch_gemm<PX, 1, 1, EPI_ACC>(a, vec, stream)));
 }
 

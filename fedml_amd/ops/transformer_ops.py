@@ -519,12 +519,27 @@ class _ClientLinear(torch.autograd.Function):
                 out_w.append(v.view_as(w))
                 r += w.shape[1]
         gb, gcs, goff, glo = _segments(gviews)
-        rc = _fn("fa_bgemm_wgrad" + sfx)(_p(g), _i64(M * N), _c.c_int(N), _p(x), _i64(M * K), _c.c_int(K), _p(gb), _i64(gcs),
-                                   goff, glo, _c.c_int(len(ws)), _c.c_int(C), _c.c_int(M), _c.c_int(N), _c.c_int(K),
-                                   _stream(x))
+        # fp32, engine-owned bias slots, not deterministic: the bias gradient comes out of the weight-gradient GEMM's
+        # own reads of g (one pass instead of a separate column reduction)
+        fused_b = (sfx != "" and bs and all(b.is_leaf and b.grad is not None for b in bs) and not _deterministic())
+        rc = -1
+        if fused_b:
+            bb_, bcs_, boff_, blo_ = _segments([b.grad for b in bs])
+            if list(blo_) == list(glo):
+                rc = _fn("fa_bgemm_wgrad_bias_f32")(_p(g), _i64(M * N), _c.c_int(N), _p(x), _i64(M * K), _c.c_int(K),
+                                                   _p(gb), _i64(gcs), goff, glo, _c.c_int(len(ws)), _p(bb_),
+                                                   _i64(bcs_), boff_, _c.c_int(C), _c.c_int(M), _c.c_int(N),
+                                                   _c.c_int(K), _stream(x))
+            fused_b = rc == 0
+        if not fused_b:
+            rc = _fn("fa_bgemm_wgrad" + sfx)(_p(g), _i64(M * N), _c.c_int(N), _p(x), _i64(M * K), _c.c_int(K), _p(gb),
+                                             _i64(gcs), goff, glo, _c.c_int(len(ws)), _c.c_int(C), _c.c_int(M),
+                                             _c.c_int(N), _c.c_int(K), _stream(x))
         _check(rc, "fa_bgemm_wgrad" + sfx)
         out_b = []
-        if bs:
+        if bs and fused_b:
+            out_b = [None] * len(bs)
+        elif bs:
             # column sums of g straight into the gradient arena (or a dense [C, N] when not owned)
             own_b = all(b.is_leaf and b.grad is not None for b in bs)
             if own_b:

@@ -137,12 +137,12 @@ class BatchedTransformer:
     @staticmethod
     def _link(x, dt):
         """A residual-gradient hand-off (ops.transformer_ops.ResLink) on the fp32 native path, else None."""
-        return T.ResLink() if (x.is_cuda and dt == torch.float32) else None
+        return T.ResLink() if (x.is_cuda and (dt or x.dtype) == torch.float32) else None
 
     @staticmethod
     def _glink(x, dt):
         """A GELU-backward hand-off (ops.transformer_ops.GeluLink) on the fp32 native path, else None."""
-        return T.GeluLink() if (x.is_cuda and dt == torch.float32) else None
+        return T.GeluLink() if (x.is_cuda and (dt or x.dtype) == torch.float32) else None
 
     def _attn(self, v, x, pre, S, kmask, training, dt, seed, res=None, dx_link=None, res_link=None):
         C, Tk, d = x.shape
