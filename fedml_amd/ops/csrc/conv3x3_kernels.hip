@@ -47,7 +47,7 @@ using prec::F32;
 using prec::F32X3;
 
 enum { XF_NONE = 0, XF_BNRELU = 1, XF_DY = 2 };
-enum { EPI_FWD = 0, EPI_MASK = 2 };
+enum { EPI_FWD = 0, EPI_MASK = 2, EPI_BLOCK = 3 };
 
 // Exact n / d for 0 ≤ n < 2^26 by multiply-high (branch-free libdivide form; d ≥ 1): the tile
 // index math runs per 16-B chunk and per 16-pixel MFMA tile, where a runtime integer divide
@@ -233,7 +233,10 @@ struct Args {              // tensors are P::T (bf16 | fp32) unless noted
   const float* vec1;     // shift | β
   const float* vec2;     //       | γ
   void* out;             // [C][N][H][W][NOUT]
-  const void* e_x;       // EPI_MASK: previous raw activation [C][N][H][W][NOUT]
+  const void* e_x;       // EPI_MASK: previous raw activation [C][N][H][W][NOUT]; EPI_BLOCK: block input (mask)
+  const void* e_add;     // EPI_BLOCK: shortcut gradient added before the mask
+  const void* e_y1;      // EPI_BLOCK: previous block's last-BN input (Σg'·y1; null: not accumulated)
+  const void* e_y2;      // EPI_BLOCK: previous block's shortcut-BN input (Σg'·y2; null: none)
   const float* e_s;
   const float* e_t;
   float* stats;          // [C][NOUT][NS]
@@ -286,8 +289,8 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
   float* v0 = reinterpret_cast<float*>(smem + (size_t)NOUT * a.ldk * P::ES);     // [KC] ×3
   float* v1 = v0 + KC;
   float* v2 = v1 + KC;
-  float* red = v2 + KC;                                                           // [4][NOUT][2]
-  float* esL = red + 4 * NOUT * 2;                                                // [NOUT] ×2 (EPI_MASK)
+  float* red = v2 + KC;                                                           // [4][NOUT][3]
+  float* esL = red + 4 * NOUT * 3;                                                // [NOUT] ×2 (EPI_MASK)
   float* etL = esL + NOUT;
   T* tile = reinterpret_cast<T*>(etL + NOUT);                                     // [S][TR][TW][LD]
 
@@ -322,12 +325,16 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
   const T* src = reinterpret_cast<const T*>(a.src) + (int64_t)c * a.N * Hs * Ws * KC;
   const T* src2 = (XF == XF_DY) ? reinterpret_cast<const T*>(a.src2) + (int64_t)c * a.N * Hs * Ws * KC : nullptr;
   T* out = reinterpret_cast<T*>(a.out) + (int64_t)c * a.N * HW * NO;
-  const T* ex = (EPI == EPI_MASK) ? reinterpret_cast<const T*>(a.e_x) + (int64_t)c * a.N * HW * NO : nullptr;
+  const int64_t eo = (int64_t)c * a.N * HW * NO;
+  const T* ex = (EPI != EPI_FWD) ? reinterpret_cast<const T*>(a.e_x) + eo : nullptr;
+  const T* ea = (EPI == EPI_BLOCK) ? reinterpret_cast<const T*>(a.e_add) + eo : nullptr;
+  const T* ey1 = (EPI == EPI_BLOCK && a.e_y1) ? reinterpret_cast<const T*>(a.e_y1) + eo : nullptr;
+  const T* ey2 = (EPI == EPI_BLOCK && a.e_y2) ? reinterpret_cast<const T*>(a.e_y2) + eo : nullptr;
 
   // per-lane epilogue state: channels ch_base + nt·16 + 4g + i; forward outputs are stored as y − K with a
   // per-channel pivot K ≈ the batch mean (BatchNorm statistics and the folded backward then work on
   // values centred near 0: no E[y²] − mean² cancellation)
-  float st0[NT][4], st1[NT][4], piv[NT][4];
+  float st0[NT][4], st1[NT][4], st2[EPI == EPI_BLOCK ? NT : 1][4], piv[NT][4];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
@@ -339,6 +346,7 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
     for (int i = 0; i < 4; ++i) {
       st0[nt][i] = 0.f;
       st1[nt][i] = 0.f;
+      if (EPI == EPI_BLOCK) st2[EPI == EPI_BLOCK ? nt : 0][i] = 0.f;
     }
 
   // loop-invariant A-operand tap offsets of this lane (one per K-step)
@@ -440,6 +448,27 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
             P::store4(out + prow + nt * 16, f);   // f ← the stored (rounded) values
 #pragma unroll
             for (int i = 0; i < 4; ++i) { st0[nt][i] += f[i]; st1[nt][i] += f[i] * f[i]; }
+          } else if (EPI == EPI_BLOCK) {   // g' = (dx + shortcut gradient) · [block input > 0]
+            float xv[4], ev[4];
+            P::load4(ex + prow + nt * 16, xv);
+            P::load4(ea + prow + nt * 16, ev);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) f[i] = xv[i] > 0.f ? f[i] + ev[i] : 0.f;
+            P::store4(out + prow + nt * 16, f);   // f ← the stored (rounded) values
+#pragma unroll
+            for (int i = 0; i < 4; ++i) st0[nt][i] += f[i];
+            if (ey1) {
+              float y1[4];
+              P::load4(ey1 + prow + nt * 16, y1);
+#pragma unroll
+              for (int i = 0; i < 4; ++i) st1[nt][i] += f[i] * y1[i];
+            }
+            if (ey2) {
+              float y2[4];
+              P::load4(ey2 + prow + nt * 16, y2);
+#pragma unroll
+              for (int i = 0; i < 4; ++i) st2[EPI == EPI_BLOCK ? nt : 0][i] += f[i] * y2[i];
+            }
           } else {
             float xv[4];
             P::load4(ex + prow + nt * 16, xv);
@@ -467,22 +496,26 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
       for (int i = 0; i < 4; ++i) {
         st0[nt][i] += __shfl_xor(st0[nt][i], o, 64);
         st1[nt][i] += __shfl_xor(st1[nt][i], o, 64);
+        if (EPI == EPI_BLOCK) st2[EPI == EPI_BLOCK ? nt : 0][i] += __shfl_xor(st2[EPI == EPI_BLOCK ? nt : 0][i], o, 64);
       }
   }
+  constexpr int NQ = EPI == EPI_BLOCK ? 3 : 2;   // statistics columns written
   if ((lane & 15) == 0) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        red[(wid * NOUT + nt * 16 + 4 * g + i) * 2 + 0] = st0[nt][i];
-        red[(wid * NOUT + nt * 16 + 4 * g + i) * 2 + 1] = st1[nt][i];
+        red[(wid * NOUT + nt * 16 + 4 * g + i) * 3 + 0] = st0[nt][i];
+        red[(wid * NOUT + nt * 16 + 4 * g + i) * 3 + 1] = st1[nt][i];
+        if (EPI == EPI_BLOCK) red[(wid * NOUT + nt * 16 + 4 * g + i) * 3 + 2] = st2[EPI == EPI_BLOCK ? nt : 0][i];
       }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < NOUT * 2; i += 256) {
-    const int ch = i / 2, q = i % 2;
-    const float s = red[(0 * NOUT + ch) * 2 + q] + red[(1 * NOUT + ch) * 2 + q] + red[(2 * NOUT + ch) * 2 + q] +
-                    red[(3 * NOUT + ch) * 2 + q];
+  for (int i = threadIdx.x; i < NOUT * NQ; i += 256) {
+    const int ch = i / NQ, q = i % NQ;
+    if (EPI == EPI_BLOCK && q == 2 && !ey2) continue;
+    const float s = red[(0 * NOUT + ch) * 3 + q] + red[(1 * NOUT + ch) * 3 + q] + red[(2 * NOUT + ch) * 3 + q] +
+                    red[(3 * NOUT + ch) * 3 + q];
     fa_acc_add(&a.stats[((int64_t)c * NO + ch_base + ch) * a.NS + q], s);
   }
 }
@@ -695,7 +728,7 @@ static Plan make_plan(int N, int H, int W, int C, int target_px, int target_wgs)
 
 template <class P>
 static size_t gemm_smem(int kc, int nout, int ldk, const Plan& p, int TR, int TW) {
-  return (size_t)nout * ldk * P::ES + (size_t)3 * kc * 4 + (size_t)4 * nout * 2 * 4 + (size_t)2 * nout * 4 +
+  return (size_t)nout * ldk * P::ES + (size_t)3 * kc * 4 + (size_t)4 * nout * 3 * 4 + (size_t)2 * nout * 4 +
          (size_t)p.S * TR * TW * P::pitch(kc) * P::ES;
 }
 
@@ -843,12 +876,18 @@ template <class P>
 static int conv3x3_bwd_data(const void* g, const void* yv, const float* alpha, const float* beta, const float* gamma,
                             const void* wpk_b, int64_t wpk_ld, void* dx, const void* e_x, const float* e_s,
                             const float* e_t, float* stats, int C, int N, int Hx, int Wx, int Cout, int Cin, int ldk2,
-                            int stride, const int* nimg, hipStream_t stream) {
+                            int stride, const int* nimg, hipStream_t stream, const void* e_add = nullptr,
+                            const void* e_y1 = nullptr, const void* e_y2 = nullptr) {
   if ((stride != 1 && stride != 2) || Hx % stride || Wx % stride || Wx % 8 != 0) return -3;
   Args a = {};
   a.src = g; a.src2 = yv; a.wpk = wpk_b; a.wpk_ld = wpk_ld; a.vec0 = alpha; a.vec1 = beta; a.vec2 = gamma;
   a.out = dx; a.e_x = e_x; a.e_s = e_s; a.e_t = e_t; a.stats = stats; a.NS = 3; a.nimg = nimg;
+  a.e_add = e_add; a.e_y1 = e_y1; a.e_y2 = e_y2;
   a.N = N; a.H = Hx; a.W = Wx; a.Hs = Hx / stride; a.Ws = Wx / stride; a.ldk = ldk2;
+  if (e_add) {   // EPI_BLOCK (stride 1: the block's first conv keeps the channel count)
+    if (stride != 1) return -3;
+    return dispatch_gemm<P, XF_DY, 1, EPI_BLOCK, 1>(Cout, Cin, a, C, stream);
+  }
   if (stride == 2) return dispatch_gemm<P, XF_DY, 1, EPI_MASK, 2>(Cout, Cin, a, C, stream);
   return dispatch_gemm<P, XF_DY, 1, EPI_MASK, 1>(Cout, Cin, a, C, stream);
 }
@@ -972,6 +1011,28 @@ FA_EXPORT int fa_conv3x3_bwd_data_f32(const float* g, const float* yv, const flo
                                       hipStream_t stream) {
   FA_F32_DISPATCH(c3, c3::conv3x3_bwd_data<PX>(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, dx, e_x, e_s, e_t, stats, C, N, Hx,
                                        Wx, Cout, Cin, ldk2, stride, nimg, stream));
+}
+
+// backward-data 3×3 / pad 1 / stride 1 of a block's first conv with the block epilogue (EPI_BLOCK of the
+// generic kernel):  g' = (convᵀ(α·g + β·y + γ) + e_add) · [e_x > 0];  stats[c][ci][3] += (Σg', Σg'·e_y1, Σg'·e_y2)
+// (e_y1 / e_y2 null: that column is left alone)
+FA_EXPORT int fa_conv3x3_bwd_data_block(const uint16_t* g, const uint16_t* yv, const float* alpha, const float* beta,
+                                        const float* gamma, const uint16_t* wpk_b, int64_t wpk_ld, uint16_t* dx,
+                                        const uint16_t* e_x, const uint16_t* e_add, const uint16_t* e_y1,
+                                        const uint16_t* e_y2, float* stats, int C, int N, int Hx, int Wx, int Cout,
+                                        int Cin, int ldk2, const int* nimg, hipStream_t stream) {
+  if (!e_add) return -3;
+  return c3::conv3x3_bwd_data<c3::BF16>(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, dx, e_x, nullptr, nullptr, stats, C,
+                                        N, Hx, Wx, Cout, Cin, ldk2, 1, nimg, stream, e_add, e_y1, e_y2);
+}
+FA_EXPORT int fa_conv3x3_bwd_data_block_f32(const float* g, const float* yv, const float* alpha, const float* beta,
+                                            const float* gamma, const float* wpk_b, int64_t wpk_ld, float* dx,
+                                            const float* e_x, const float* e_add, const float* e_y1, const float* e_y2,
+                                            float* stats, int C, int N, int Hx, int Wx, int Cout, int Cin, int ldk2,
+                                            const int* nimg, hipStream_t stream) {
+  if (!e_add) return -3;
+  FA_F32_DISPATCH(c3, c3::conv3x3_bwd_data<PX>(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, dx, e_x, nullptr, nullptr, stats,
+                                       C, N, Hx, Wx, Cout, Cin, ldk2, 1, nimg, stream, e_add, e_y1, e_y2));
 }
 
 // weight gradient 3×3 / pad 1 / stride 1|2 into the GEMM-layout scratch `dw` [C][Cout][9·Cin] (zero

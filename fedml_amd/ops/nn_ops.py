@@ -180,6 +180,16 @@ def conv3x3_bwd_data(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, dx, e_x, e_s, e_t
     _check(rc, "fa_conv3x3_bwd_data")
 
 
+def conv3x3_bwd_data_block(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, dx, e_x, e_add, e_y1, e_y2, stats, C, N, H, W,
+                           Cout, Cin, ldk2, nimg=None):
+    """Stride-1 backward-data of a block's first 3×3 conv with the block epilogue:
+    dx' = (convᵀ(dy) + e_add)·[e_x > 0], stats (Σdx', Σdx'·e_y1, Σdx'·e_y2). (H, W) = dx resolution."""
+    rc = _fnp("fa_conv3x3_bwd_data_block", g)(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(wpk_b), _i64(wpk_ld),
+                                          _p(dx), _p(e_x), _p(e_add), _p(e_y1), _p(e_y2), _p(stats), _i(C), _i(N),
+                                          _i(H), _i(W), _i(Cout), _i(Cin), _i(ldk2), _p(nimg), _stream(g))
+    _check(rc, "fa_conv3x3_bwd_data_block")
+
+
 def conv3x3_wgrad(g, yv, alpha, beta, gamma, x, ps, pt, garena, woff, C, N, H, W, Cin, Cout, cin_src, dw_scratch,
                   stride=1, scatter=True, nimg=None, lazy=None):
     """Weight gradient into the GEMM-layout scratch, then scattered (+=) into the OIHW arena

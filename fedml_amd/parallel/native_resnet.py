@@ -154,6 +154,8 @@ class NativeResNetStep:
         self.use_c1 = os.environ.get("FEDML_AMD_CONV1X1", "1") != "0"
         self.use_c1f = os.environ.get("FEDML_AMD_C1_FUSED", "1") != "0"
         self.use_dym = os.environ.get("FEDML_AMD_DY_MATERIALIZE", "1") != "0"
+        # basic blocks' first-conv backward-data on the 3×3 tile kernel with the block epilogue (generic kernel: 0)
+        self.use_c3_block = os.environ.get("FEDML_AMD_C3_BLOCK", "1") != "0"
         self.use_s2k = os.environ.get("FEDML_AMD_C3S2_CONVK", "1") == "1"   # measured +2 % (fp32 headline)
         self.use_ry = os.environ.get("FEDML_AMD_RECOMPUTE_Y", "0") == "1" and dtype == torch.float32
         self.use_pbout = os.environ.get("FEDML_AMD_FUSE_BOUT", "1") != "0"
@@ -855,6 +857,13 @@ class NativeResNetStep:
                                          pstats, garena, self.off[cv0.key], C, M0, cv0.cin, cv0.cout,
                                          nn_ops.EPI_BLOCK, self._c1f_pix_per_wg(M0), nimg=self._nimg,
                                          hw=cv0.H * cv0.W, lazy=(self._take(bn0.key, "b"), None))
+                gpre = out_buf
+                self._dump(f"{cv0.key}.dx", out_buf, C * N * cv0.H * cv0.W * cv0.cin)
+                continue
+            if self._c3(cv0) and cv0.stride == 1 and dyv0 is not None and self.use_c3_block:
+                nn_ops.conv3x3_bwd_data_block(dg0, dyv0, al0, be0, ga0, self.packed.view(-1)[cv0.off_b:],
+                                              self.packed_ld, out_buf, b.act_in, shortcut, ey1, ey2, pstats, C, N,
+                                              cv0.H, cv0.W, cv0.cout, cv0.cin_pad, cv0.ldk2, nimg=self._nimg)
                 gpre = out_buf
                 self._dump(f"{cv0.key}.dx", out_buf, C * N * cv0.H * cv0.W * cv0.cin)
                 continue

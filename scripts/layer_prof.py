@@ -72,6 +72,11 @@ def c3_bwd(g, y, al, be, ga, wpk, ld, dx, ex, es, et, st, C, N, H, W, Cout, Cin,
                  Cout, Cin, 3, 3, stride, 1, H, W, ldk2, 0)
 
 
+def c3_bwd_block(g, y, al, be, ga, wpk, ld, dx, ex, ea, e1, e2, st, C, N, H, W, Cout, Cin, ldk2):
+    return c_bwd(g, y, al, be, ga, wpk, ld, dx, 3, ex, None, None, ea, e1, e2, st, C, N, H, W, Cout, Cin, 3, 3, 1, 1,
+                 H, W, ldk2, 0)
+
+
 def c3_wgrad(g, y, al, be, ga, x, ps, pt, garena, woff, C, N, H, W, Cin, Cout, cs, scratch, stride=1):
     return c_wgrad(g, y, al, be, ga, x, ps, pt, garena, woff, C, N, H, W, Cin, H // stride, W // stride, Cout, 3, 3,
                    stride, 1, 0, cs, scratch)
@@ -115,6 +120,7 @@ def main():
     _wrap("block_out", c_block)
     _wrap("conv3x3_fwd", c3_fwd)
     _wrap("conv3x3_bwd_data", c3_bwd)
+    _wrap("conv3x3_bwd_data_block", c3_bwd_block)
     _wrap("conv3x3_wgrad", c3_wgrad)
     _wrap("conv1x1_wgrad", c1_wgrad)
     _wrap("conv1x1_bwd_fused", c1_fused)

@@ -175,6 +175,59 @@ def test_conv3x3_kernels_vs_fp32_reference(ch, hw, stride):
         assert rel(garena[c, 16:16 + ch * ch * 9], ref.reshape(-1)) < 1e-4
 
 
+@pytest.mark.parametrize("ch,hw,N", [(16, 32, 8), (32, 16, 8), (64, 32, 4), (64, 8, 16)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("y2", [False, True])
+def test_conv3x3_bwd_data_block_epilogue(ch, hw, N, dtype, y2):
+    """3×3 tile kernel with the block epilogue (a basic block's first conv): dx' = (convᵀ(dy) + e_add)·[e_x > 0]
+    and the statistics (Σdx', Σdx'·y1, Σdx'·y2) against torch fp32 of the same operands, and against the
+    generic implicit-GEMM kernel's EPI_BLOCK."""
+    from fedml_amd.ops import nn_ops
+    torch.manual_seed(3)
+    C, dt = 3, dtype
+    K = 9 * ch
+    ldk = (K + 31) // 32 * 32 + 8
+    wpk = torch.zeros(C, ch, ldk, device=DEV)
+    wpk[:, :, :K] = torch.randn(C, ch, K, device=DEV) * 0.1
+    wpk = wpk.to(dt).contiguous()
+    wt_b = wpk[:, :, :K].float().view(C, ch, 3, 3, ch).permute(0, 4, 1, 2, 3)
+    g = torch.randn(C, N, hw, hw, ch, device=DEV).to(dt)
+    yv = torch.randn(C, N, hw, hw, ch, device=DEV).to(dt)
+    al, be = torch.rand(C, ch, device=DEV), torch.randn(C, ch, device=DEV) * 0.1
+    ga = torch.randn(C, ch, device=DEV) * 0.01
+    ex = torch.relu(torch.randn(C, N, hw, hw, ch, device=DEV)).to(dt)      # block input (post-ReLU)
+    ea = torch.randn(C, N, hw, hw, ch, device=DEV).to(dt)                  # shortcut gradient
+    e1 = torch.randn(C, N, hw, hw, ch, device=DEV).to(dt)
+    e2 = torch.randn(C, N, hw, hw, ch, device=DEV).to(dt) if y2 else None
+    dx = torch.zeros_like(ex)
+    st = torch.zeros(C, ch, 3, device=DEV)
+    nn_ops.conv3x3_bwd_data_block(g, yv, al, be, ga, wpk, ch * ldk, dx, ex, ea, e1, e2, st, C, N, hw, hw, ch, ch, ldk)
+    dxg = torch.zeros_like(ex)
+    stg = torch.zeros_like(st)
+    nn_ops.conv_bwd_data(g, yv, al, be, ga, wpk, ch * ldk, dxg, nn_ops.EPI_BLOCK, ex, None, None, ea, e1, e2, stg,
+                         C, N, hw, hw, ch, ch, 3, 3, 1, 1, hw, hw, ldk, 1)
+    torch.cuda.synchronize()
+
+    def rel(a, b):
+        return float((a.float() - b.float()).norm() / b.float().norm().clamp_min(1e-12))
+
+    tol = 1e-2 if dt == torch.bfloat16 else 1e-5
+    assert rel(dx, dxg) < (5e-3 if dt == torch.bfloat16 else 1e-5)
+    for c in range(C):
+        dy = (al[c] * g[c].float() + be[c] * yv[c].float() + ga[c]).to(dt).float().permute(0, 3, 1, 2)
+        ref = torch.nn.grad.conv2d_input((N, ch, hw, hw), wt_b[c], dy, padding=1).permute(0, 2, 3, 1)
+        ref = (ref + ea[c].float()) * (ex[c].float() > 0)
+        assert rel(dx[c], ref) < tol
+        d = dx[c].float()
+        assert rel(st[c, :, 0], d.sum((0, 1, 2))) < 1e-4
+        assert rel(st[c, :, 1], (d * e1[c].float()).sum((0, 1, 2))) < 1e-4
+        if y2:
+            assert rel(st[c, :, 2], (d * e2[c].float()).sum((0, 1, 2))) < 1e-4
+        else:
+            assert float(st[c, :, 2].abs().max()) == 0.0
+        assert rel(st[c], stg[c]) < (1e-2 if dt == torch.bfloat16 else 1e-5)
+
+
 @pytest.mark.parametrize("cin,cout,hw", [(16, 64, 32), (64, 16, 32), (32, 128, 16), (128, 32, 16), (64, 256, 8),
                                          (256, 64, 8), (64, 64, 8)])
 @pytest.mark.parametrize("pro", [False, True])
