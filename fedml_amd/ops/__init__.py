@@ -12,6 +12,9 @@ from . import _native
 from .fl_ops import (
     weighted_sum,
     weighted_average,
+    broadcast_rows_,
+    ZeroSegments,
+    complement_segments,
     subset_aggregate,
     sgd_step,
     adam_step,

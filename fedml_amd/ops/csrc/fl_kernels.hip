@@ -206,6 +206,9 @@ FA_EXPORT int fa_sgd_step(float* param, const void* grad, int grad_is_bf16, floa
 
 // torch.optim.Adam(amsgrad=…, weight_decay=… as L2) over a [C, P] stack. The step count
 // lives on the device (`step`, per client) so the launch is replayable from a hipGraph.
+// A client's first step (t ≤ 1) starts from zero moments without reading them — torch's state at step 1 — so
+// the per-round moment resets need no fill pass over the [C, P] buffers (and the first step reads 2–3 fewer
+// streams).
 template <typename G>
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ param, const G* __restrict__ grad,
                                                    float* __restrict__ m1, float* __restrict__ m2,
@@ -221,6 +224,7 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ param, co
   const float bc2 = 1.f - __powf(beta2, t);
   const float step_size = lr / bc1;
   const float bc2_sqrt = sqrtf(bc2);
+  const bool fresh = t <= 1.f;
   float* pc = param + (int64_t)c * ld;
   const G* gc = grad + (int64_t)c * ld;
   float* a = m1 + (int64_t)c * ld;
@@ -234,13 +238,17 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ param, co
       if (decoupled) p *= (1.f - lr * wd);
       else g += wd * p;
     }
-    float ma = beta1 * a[i] + (1.f - beta1) * g;
-    float mb = beta2 * b[i] + (1.f - beta2) * g * g;
+    float ma = (1.f - beta1) * g;
+    float mb = (1.f - beta2) * g * g;
+    if (!fresh) {
+      ma += beta1 * a[i];
+      mb += beta2 * b[i];
+    }
     a[i] = ma;
     b[i] = mb;
     float den;
     if (vm) {
-      float v = fmaxf(vm[i], mb);
+      float v = fresh ? mb : fmaxf(vm[i], mb);
       vm[i] = v;
       den = sqrtf(v) / bc2_sqrt + eps;
     } else {
@@ -263,6 +271,82 @@ FA_EXPORT int fa_adam_step(float* param, const void* grad, int grad_is_bf16, flo
   else
     hipLaunchKernelGGL(adam_kernel<float>, grid, dim3(256), 0, stream, param, (const float*)grad, m1, m2, vmax, step,
                        P, ld, lr, beta1, beta2, eps, wd, decoupled, active, (uint16_t*)shadow);
+  return (int)hipGetLastError();
+}
+
+// dst[c][:] = src[:] for every row c of a [C, P] stack (row stride ld): the global model into every client
+// slot. float4 stores when the rows are 16-B aligned; the source row stays in L2 across the C rows.
+__global__ __launch_bounds__(256) void broadcast_rows_kernel(float* __restrict__ dst, const float* __restrict__ src,
+                                                             int64_t P, int64_t ld, int vec) {
+  float* d = dst + (int64_t)blockIdx.y * ld;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (vec) {
+    const int64_t n4 = P / 4;
+    const float4* s4 = reinterpret_cast<const float4*>(src);
+    float4* d4 = reinterpret_cast<float4*>(d);
+    for (int64_t i = i0; i < n4; i += stride) d4[i] = s4[i];
+    for (int64_t i = n4 * 4 + i0; i < P; i += stride) d[i] = src[i];
+  } else {
+    for (int64_t i = i0; i < P; i += stride) d[i] = src[i];
+  }
+}
+
+// Zero columns [off, off + len) of every row of a [C, ld] fp32 stack for the nseg (off, len) pairs of `segs`
+// (device int64 table): the gradient-arena columns that are accumulated into (everything but the
+// first-touch weight-gradient rows) in one launch. grid = (chunks, C, nseg).
+__global__ __launch_bounds__(256) void zero_segments_kernel(float* __restrict__ base, int64_t ld,
+                                                            const int64_t* __restrict__ segs) {
+  const int64_t off = segs[2 * blockIdx.z], len = segs[2 * blockIdx.z + 1];
+  float* d = base + (int64_t)blockIdx.y * ld + off;
+  const int64_t head = min<int64_t>(len, (int64_t)((16 - ((uintptr_t)d & 15)) & 15) / 4);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i0 < head) d[i0] = 0.f;
+  const int64_t n4 = (len - head) / 4;
+  float4* d4 = reinterpret_cast<float4*>(d + head);
+  for (int64_t i = i0; i < n4; i += stride) d4[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int64_t i = head + 4 * n4 + i0; i < len; i += stride) d[i] = 0.f;
+}
+
+FA_EXPORT int fa_zero_segments(float* base, int64_t ld, int C, const int64_t* segs_dev, int nseg, int64_t max_len,
+                               hipStream_t stream) {
+  if (C <= 0 || nseg <= 0 || max_len <= 0) return 0;
+  if (nseg > 65535 || C > 65535) return (int)hipErrorInvalidValue;
+  dim3 grid(fa_grid((max_len + 3) / 4, 256, 512), C, nseg);
+  hipLaunchKernelGGL(zero_segments_kernel, grid, dim3(256), 0, stream, base, ld, segs_dev);
+  return (int)hipGetLastError();
+}
+
+// Embedding-table gradient of a client-stacked lookup: dst[c][ids[c][t]][:] += g[c][t][:] with fp32 atomics
+// (vector-memory global atomics), dst = client c's [V][d] table at base + c·ld. torch's accumulating
+// index_put_ on the strided arena view copies the whole [C, V, d] table out and back (2 × 3 GB per DistilBERT
+// step). One workgroup per token row; tokens of one client hitting the same row add in any order.
+__global__ __launch_bounds__(256) void embedding_grad_kernel(float* __restrict__ base, int64_t ld,
+                                                             const int64_t* __restrict__ ids, const float* __restrict__ g,
+                                                             int T, int V, int d) {
+  const int64_t row = blockIdx.x;            // c·T + t
+  const int c = (int)(row / T);
+  const int64_t id = ids[row];
+  if (id < 0 || id >= V) return;             // out-of-range ids contribute nothing (torch would raise earlier)
+  float* dst = base + (int64_t)c * ld + id * d;
+  const float* src = g + row * d;
+  for (int k = threadIdx.x; k < d; k += blockDim.x) atomicAdd(dst + k, src[k]);
+}
+
+FA_EXPORT int fa_embedding_grad_f32(float* base, int64_t ld, const int64_t* ids, const float* g, int C, int T, int V,
+                                    int d, hipStream_t stream) {
+  if (C <= 0 || T <= 0 || d <= 0) return 0;
+  hipLaunchKernelGGL(embedding_grad_kernel, dim3((unsigned)((int64_t)C * T)), dim3(d >= 256 ? 256 : 64), 0, stream,
+                     base, ld, ids, g, T, V, d);
+  return (int)hipGetLastError();
+}
+
+FA_EXPORT int fa_broadcast_rows(float* dst, const float* src, int C, int64_t P, int64_t ld, hipStream_t stream) {
+  if (C <= 0 || P <= 0) return 0;
+  const int vec = ((uintptr_t)dst % 16 == 0) && ((uintptr_t)src % 16 == 0) && (ld % 4 == 0);
+  dim3 grid(fa_grid(vec ? (P + 3) / 4 : P, 256, 1024), C);
+  hipLaunchKernelGGL(broadcast_rows_kernel, grid, dim3(256), 0, stream, dst, src, P, ld, vec);
   return (int)hipGetLastError();
 }
 

@@ -89,6 +89,8 @@ struct Args {
   int ldr;
   int M, N, K;
   int tiles_m, tiles_n, nclients;
+  int acc_store;     // ACC: the first (and only) writer of these gradient rows — store instead of +=, so the
+                     // arena rows need no zero fill (each element has exactly one producing tile: no split-K)
 };
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
@@ -271,9 +273,13 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args p) {
         const int m = m0 + 4 * tid;
         if (m < p.M) {   // m .. m+3 in one segment (segment bounds are multiples of 4 on the VEC path)
           float4* bp = reinterpret_cast<float4*>(p.bg + (int64_t)c * p.bg_bs + seg_row(p.bgseg, m, 1));
-          float4 o = *bp;
-          o.x += t4.x; o.y += t4.y; o.z += t4.z; o.w += t4.w;
-          *bp = o;
+          if (p.acc_store) {
+            *bp = t4;
+          } else {
+            float4 o = *bp;
+            o.x += t4.x; o.y += t4.y; o.z += t4.z; o.w += t4.w;
+            *bp = o;
+          }
         }
       }
     } else if (interior) {
@@ -301,13 +307,16 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args p) {
       if (EPI == EPI_ACC) {
         float* dst = p.Cp + (int64_t)c * p.c_bs + seg_row(p.cseg, m, p.ldc) + n;
         if (VEC) {
-          float4 o = *reinterpret_cast<float4*>(dst);
-          o.x += v[0]; o.y += v[1]; o.z += v[2]; o.w += v[3];
+          float4 o = make_float4(v[0], v[1], v[2], v[3]);
+          if (!p.acc_store) {
+            const float4 q = *reinterpret_cast<const float4*>(dst);
+            o.x += q.x; o.y += q.y; o.z += q.z; o.w += q.w;
+          }
           *reinterpret_cast<float4*>(dst) = o;
         } else {
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            if (n + r < p.N) dst[r] += v[r];
+            if (n + r < p.N) dst[r] = p.acc_store ? v[r] : dst[r] + v[r];
         }
       } else {
         if (p.bias) {
@@ -1127,9 +1136,18 @@ FA_EXPORT int fa_bgemm_dgrad_acc_f32(const float* dy, int64_t dy_bs, int lddy, c
 }
 
 // dW[c] += dy[c]ᵀ · x[c]    dy [T][N], x [T][K]; dW [N][K] gradient-arena segments (rows n)
+FA_EXPORT int fa_bgemm_wgrad_st_f32(const float* dy, int64_t dy_bs, int lddy, const float* x, int64_t x_bs, int ldx,
+                                    float* g_base, int64_t g_cs, const int64_t* g_off, const int* seg_lo, int nseg,
+                                    int C, int T, int N, int K, int store, hipStream_t stream);
 FA_EXPORT int fa_bgemm_wgrad_f32(const float* dy, int64_t dy_bs, int lddy, const float* x, int64_t x_bs, int ldx,
                                  float* g_base, int64_t g_cs, const int64_t* g_off, const int* seg_lo, int nseg, int C,
                                  int T, int N, int K, hipStream_t stream) {
+  return fa_bgemm_wgrad_st_f32(dy, dy_bs, lddy, x, x_bs, ldx, g_base, g_cs, g_off, seg_lo, nseg, C, T, N, K, 0, stream);
+}
+// store = 1: dW[c] = dy[c]ᵀ · x[c] (the rows' first writer: no zero fill needed), else dW[c] += …
+FA_EXPORT int fa_bgemm_wgrad_st_f32(const float* dy, int64_t dy_bs, int lddy, const float* x, int64_t x_bs, int ldx,
+                                    float* g_base, int64_t g_cs, const int64_t* g_off, const int* seg_lo, int nseg,
+                                    int C, int T, int N, int K, int store, hipStream_t stream) {
   using namespace tff;
   if (nseg < 1 || nseg > 4 || C <= 0 || T <= 0 || N <= 0 || K <= 0) return (int)hipErrorInvalidValue;
   Args a{};
@@ -1140,15 +1158,17 @@ FA_EXPORT int fa_bgemm_wgrad_f32(const float* dy, int64_t dy_bs, int lddy, const
   fill_segs(a.cseg, g_off, seg_lo, nseg);
   a.M = N; a.N = K; a.K = T;
   a.tiles_m = (N + BM - 1) / BM; a.tiles_n = (K + BN - 1) / BN; a.nclients = C;
+  a.acc_store = store;
   const bool vec = al4({dy_bs, lddy, N, x_bs, ldx, K, g_cs}) && segs_al4(a.cseg) && al16({dy, x, g_base});
   FA_F32_DISPATCH(tff, (launch_gemm<PX, 1, 1, EPI_ACC>(a, vec, stream)));
 }
 
-// dW[c] += dy[c]ᵀ · x[c] and db[c] += Σ_t dy[c][t][:] in one pass over dy (bias segments share seg_lo)
+// dW[c] += dy[c]ᵀ · x[c] and db[c] += Σ_t dy[c][t][:] in one pass over dy (bias segments share seg_lo);
+// store = 1: = instead of += for both (the rows' first writer)
 FA_EXPORT int fa_bgemm_wgrad_bias_f32(const float* dy, int64_t dy_bs, int lddy, const float* x, int64_t x_bs,
                                       int ldx, float* g_base, int64_t g_cs, const int64_t* g_off, const int* seg_lo,
                                       int nseg, float* b_base, int64_t b_cs, const int64_t* b_off, int C, int T, int N,
-                                      int K, hipStream_t stream) {
+                                      int K, int store, hipStream_t stream) {
   using namespace tff;
   if (nseg < 1 || nseg > 4 || C <= 0 || T <= 0 || N <= 0 || K <= 0 || !b_base) return (int)hipErrorInvalidValue;
   Args a{};
@@ -1161,6 +1181,7 @@ FA_EXPORT int fa_bgemm_wgrad_bias_f32(const float* dy, int64_t dy_bs, int lddy, 
   fill_segs(a.bgseg, b_off, seg_lo, nseg);
   a.M = N; a.N = K; a.K = T;
   a.tiles_m = (N + BM - 1) / BM; a.tiles_n = (K + BN - 1) / BN; a.nclients = C;
+  a.acc_store = store;
   const bool vec = al4({dy_bs, lddy, N, x_bs, ldx, K, g_cs, b_cs}) && segs_al4(a.cseg) && segs_al4(a.bgseg) &&
                    al16({dy, x, g_base, b_base});
   if (!vec) return -2;   // the caller falls back to the separate bias reduction

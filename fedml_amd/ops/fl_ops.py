@@ -99,6 +99,52 @@ def weighted_sum(stack: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None,
     return out
 
 
+def broadcast_rows_(dst: torch.Tensor, src: torch.Tensor) -> torch.Tensor:
+    """dst[c, :] = src for every row of the [C, P] fp32 stack ``dst`` (unit inner stride) — one vectorised
+    launch (torch's copy of an expanded source splits a > 2^31-element stack into dozens of strided launches)."""
+    C, P = dst.shape
+    if use_native(dst) and dst.dtype == torch.float32 and src.dtype == torch.float32 and dst.stride(1) == 1 \
+            and src.is_contiguous() and src.numel() == P:
+        _check(_fn("fa_broadcast_rows")(_p(dst), _p(src), _c.c_int(C), _i64(P), _i64(dst.stride(0)), _stream(dst)),
+               "fa_broadcast_rows")
+        return dst
+    dst.copy_(src.reshape(1, P).expand(C, P))
+    return dst
+
+
+class ZeroSegments:
+    """Column ranges [(off, len)] of a [C, P] fp32 stack zeroed by one launch (``fa_zero_segments``); the
+    table lives on the device (built once, replayable from a captured graph)."""
+
+    def __init__(self, segs, device):
+        self.segs = [(int(o), int(n)) for o, n in segs if n > 0]
+        flat = [v for seg in self.segs for v in seg]
+        self.table = torch.tensor(flat or [0, 0], dtype=torch.int64, device=device)
+        self.max_len = max((n for _, n in self.segs), default=0)
+
+    def __call__(self, stack: torch.Tensor):
+        if use_native(stack) and stack.dtype == torch.float32 and stack.stride(1) == 1:
+            _check(_fn("fa_zero_segments")(_p(stack), _i64(stack.stride(0)), _c.c_int(stack.shape[0]), _p(self.table),
+                                           _c.c_int(len(self.segs)), _i64(self.max_len), _stream(stack)),
+                   "fa_zero_segments")
+        else:
+            for o, n in self.segs:
+                stack[:, o:o + n].zero_()
+        return stack
+
+
+def complement_segments(P: int, taken):
+    """The column ranges of [0, P) not covered by ``taken`` [(off, len)]."""
+    out, pos = [], 0
+    for o, n in sorted(taken):
+        if o > pos:
+            out.append((pos, o - pos))
+        pos = max(pos, o + n)
+    if pos < P:
+        out.append((pos, P - pos))
+    return out
+
+
 def weighted_average(stack: torch.Tensor, counts) -> torch.Tensor:
     """FedAvg: Σ_c (n_c / Σn) · stack[c]."""
     w = torch.as_tensor(counts, dtype=torch.float64)
@@ -182,12 +228,15 @@ def adam_step(param, grad, exp_avg, exp_avg_sq, step, lr, beta1=0.9, beta2=0.999
             param.mul_(1 - lr * weight_decay)
         else:
             g = g + weight_decay * param
-    exp_avg.mul_(beta1).add_(g, alpha=1 - beta1)
-    exp_avg_sq.mul_(beta2).addcmul_(g, g, value=1 - beta2)
+    # first step (t ≤ 1): the moments start from zero whatever the buffers hold (the native kernel never reads
+    # them then; callers need not reset them between rounds)
+    fresh = t <= 1
+    exp_avg.copy_(torch.where(fresh, 0.0, exp_avg)).mul_(beta1).add_(g, alpha=1 - beta1)
+    exp_avg_sq.copy_(torch.where(fresh, 0.0, exp_avg_sq)).mul_(beta2).addcmul_(g, g, value=1 - beta2)
     bc1 = 1 - beta1 ** t
     bc2 = 1 - beta2 ** t
     if amsgrad:
-        torch.maximum(max_exp_avg_sq, exp_avg_sq, out=max_exp_avg_sq)
+        max_exp_avg_sq.copy_(torch.where(fresh, exp_avg_sq, torch.maximum(max_exp_avg_sq, exp_avg_sq)))
         den = max_exp_avg_sq.sqrt() / bc2.sqrt() + eps
     else:
         den = exp_avg_sq.sqrt() / bc2.sqrt() + eps

@@ -12,6 +12,7 @@ exact ``v_mfma_f32_16x16x4_f32`` products, or split-bf16 ones under ``fp32_mma: 
 statistics either way. CPU tensors run the plain-PyTorch fp32 reference of the same math — the same
 hash-based dropout mask included — which is also the oracle of ``tests/test_transformer_kernels_gpu.py``.
 """
+import contextlib
 import ctypes as _c
 import math
 
@@ -90,6 +91,54 @@ def _client_rows(gamma, beta):
 def _deterministic() -> bool:
     from ..utils import determinism
     return determinism.enabled()
+
+
+class _GradStoreState:
+    """First-touch weight gradients (fp32 ``tff`` path). ``record``: every weight-gradient GEMM notes the arena
+    rows it writes (one tuple per call: weights and fused bias); ``store``: a call whose rows are all in ``rows``
+    writes them with ``=`` instead of ``+=`` — the engine then zero-fills only the other columns of the gradient
+    arena (:func:`first_touch_rows`, engine ``_tf_graph_step``)."""
+    mode = None
+    calls = None
+    rows = frozenset()
+
+
+_GS = _GradStoreState()
+
+
+@contextlib.contextmanager
+def grad_store_record():
+    """Record the weight-gradient rows written inside the block (yields the list of per-call tuples of
+    (data_ptr, elements per client))."""
+    prev = (_GS.mode, _GS.calls)
+    _GS.mode, _GS.calls = "record", []
+    try:
+        yield _GS.calls
+    finally:
+        _GS.mode, _GS.calls = prev
+
+
+@contextlib.contextmanager
+def grad_store(rows):
+    """Weight-gradient GEMMs whose rows (data_ptr) are all in ``rows`` store instead of accumulating."""
+    prev = (_GS.mode, _GS.rows)
+    _GS.mode, _GS.rows = "store", frozenset(rows)
+    try:
+        yield
+    finally:
+        _GS.mode, _GS.rows = prev
+
+
+def first_touch_rows(calls):
+    """(data_ptr set, [(data_ptr, elements per client)]) of the recorded calls whose rows no other recorded
+    call writes — the rows a store-mode step may leave unzeroed."""
+    count = {}
+    for call in calls:
+        for ptr, _ in call:
+            count[ptr] = count.get(ptr, 0) + 1
+    ok = [call for call in calls if all(count[ptr] == 1 for ptr, _ in call)]
+    rows = [r for call in ok for r in call]
+    return {ptr for ptr, _ in rows}, rows
 
 
 class ResLink:
@@ -522,6 +571,11 @@ class _ClientLinear(torch.autograd.Function):
         # fp32, engine-owned bias slots, not deterministic: the bias gradient comes out of the weight-gradient GEMM's
         # own reads of g (one pass instead of a separate column reduction)
         fused_b = (sfx != "" and bs and all(b.is_leaf and b.grad is not None for b in bs) and not _deterministic())
+        rows_w = [(v.data_ptr(), v[0].numel()) for v in gviews] if own and sfx else []
+        rows_b = [(b.grad.data_ptr(), b.grad[0].numel()) for b in bs] if fused_b else []
+
+        def first_touch(rows):   # store mode: these rows are written by this call only (not zero-filled)
+            return int(_GS.mode == "store" and bool(rows) and all(ptr in _GS.rows for ptr, _ in rows))
         rc = -1
         if fused_b:
             bb_, bcs_, boff_, blo_ = _segments([b.grad for b in bs])
@@ -529,12 +583,22 @@ class _ClientLinear(torch.autograd.Function):
                 rc = _fn("fa_bgemm_wgrad_bias_f32")(_p(g), _i64(M * N), _c.c_int(N), _p(x), _i64(M * K), _c.c_int(K),
                                                    _p(gb), _i64(gcs), goff, glo, _c.c_int(len(ws)), _p(bb_),
                                                    _i64(bcs_), boff_, _c.c_int(C), _c.c_int(M), _c.c_int(N),
-                                                   _c.c_int(K), _stream(x))
+                                                   _c.c_int(K), _c.c_int(first_touch(rows_w + rows_b)), _stream(x))
             fused_b = rc == 0
-        if not fused_b:
-            rc = _fn("fa_bgemm_wgrad" + sfx)(_p(g), _i64(M * N), _c.c_int(N), _p(x), _i64(M * K), _c.c_int(K), _p(gb),
-                                             _i64(gcs), goff, glo, _c.c_int(len(ws)), _c.c_int(C), _c.c_int(M),
-                                             _c.c_int(N), _c.c_int(K), _stream(x))
+        if fused_b:
+            if _GS.mode == "record":
+                _GS.calls.append(tuple(rows_w + rows_b))
+        elif sfx:
+            rc = _fn("fa_bgemm_wgrad_st_f32")(_p(g), _i64(M * N), _c.c_int(N), _p(x), _i64(M * K), _c.c_int(K),
+                                              _p(gb), _i64(gcs), goff, glo, _c.c_int(len(ws)), _c.c_int(C),
+                                              _c.c_int(M), _c.c_int(N), _c.c_int(K), _c.c_int(first_touch(rows_w)),
+                                              _stream(x))
+            if _GS.mode == "record" and rows_w:
+                _GS.calls.append(tuple(rows_w))
+        else:
+            rc = _fn("fa_bgemm_wgrad")(_p(g), _i64(M * N), _c.c_int(N), _p(x), _i64(M * K), _c.c_int(K), _p(gb),
+                                       _i64(gcs), goff, glo, _c.c_int(len(ws)), _c.c_int(C), _c.c_int(M),
+                                       _c.c_int(N), _c.c_int(K), _stream(x))
         _check(rc, "fa_bgemm_wgrad" + sfx)
         out_b = []
         if bs and fused_b:

@@ -19,6 +19,7 @@ ViT naming), so the arena layout, aggregation and checkpoints are unchanged. The
 transformer models; CPU tensors run the same program through the ops'
 PyTorch references (the engine's tests compare it with per-client ``nn.Module`` forward passes).
 """
+import ctypes as _c
 from typing import Dict, Optional
 
 import torch
@@ -26,7 +27,9 @@ import torch.nn.functional as F
 
 from ..models.transformer.distilbert import DistilBertForSequenceClassification
 from ..models.transformer.vit import VisionTransformer
+from .. import ops
 from ..ops import transformer_ops as T
+from ..utils.determinism import enabled as _deterministic
 
 
 class UnsupportedTransformer(Exception):
@@ -56,7 +59,20 @@ class _ClientEmbedding(torch.autograd.Function):
         W = ctx.W
         idx = (cidx.expand_as(ids), ids)
         if W.grad is not None:
-            W.grad.index_put_(idx, g.to(W.grad.dtype), accumulate=True)
+            gw = W.grad
+            if (g.is_cuda and gw.dtype == torch.float32 and gw.stride(2) == 1 and gw.stride(1) == gw.shape[2]
+                    and not _deterministic() and ops.use_native(gw)):
+                # atomic scatter-add straight into the strided arena view (torch's accumulating index_put_ copies
+                # the whole [C, V, d] table out and back)
+                C, T = ids.shape
+                V, d = gw.shape[1], gw.shape[2]
+                gf = g.to(torch.float32).contiguous()
+                idc = ids.to(torch.int64).contiguous()
+                ops.fl_ops._check(ops.fl_ops._fn("fa_embedding_grad_f32")(
+                    ops.fl_ops._p(gw), ops.fl_ops._i64(gw.stride(0)), ops.fl_ops._p(idc), ops.fl_ops._p(gf),
+                    _c.c_int(C), _c.c_int(T), _c.c_int(V), _c.c_int(d), ops.fl_ops._stream(gf)), "fa_embedding_grad_f32")
+                return None, None
+            gw.index_put_(idx, g.to(gw.dtype), accumulate=True)
             return None, None
         out = torch.zeros(W.shape, dtype=g.dtype, device=g.device)
         out.index_put_(idx, g, accumulate=True)

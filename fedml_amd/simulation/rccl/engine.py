@@ -23,6 +23,7 @@ from typing import List, Optional
 import torch
 
 from ... import ops
+from ...ops import transformer_ops as T
 from ...core.arena import ParamLayout
 from ...parallel.batched_transformer import BatchedTransformer, UnsupportedTransformer
 from ...parallel.batched_nn import BatchedInterpreter, UnsupportedForBatching
@@ -179,6 +180,7 @@ class ClientBatchEngine:
         self._tf_capture = self.tf is not None and self.device.type == "cuda" and tf_graphs
         self._active_cache = {}
         self._graphs = {}
+        self._tf_plans = {}            # batch geometry → (first-touch rows, ZeroSegments | None)
         # task loss of the reference trainer this engine stands in for (core/alg_frame/functional.py):
         #   ce      my_model_trainer_classification.py  CrossEntropyLoss (per-client batch mean)
         #   nwp_ce  my_model_trainer_nwp.py             CrossEntropyLoss(ignore_index=0), logits [B, V, T]
@@ -258,7 +260,7 @@ class ClientBatchEngine:
     def load_global(self, flat: torch.Tensor):
         self._shadow_stale = True
         with torch.no_grad():
-            self.params.copy_(flat.view(1, -1).expand(self.C, -1))
+            ops.broadcast_rows_(self.params, flat.reshape(-1))
         if self.mu:
             self.global_ref = flat
 
@@ -286,10 +288,7 @@ class ClientBatchEngine:
         use_native_loss = self.device.type == "cuda"
         first = True
         if self.optimizer != "sgd":
-            self.m1.zero_()
-            self.m2.zero_()
-            if self.vmax is not None:
-                self.vmax.zero_()
+            # the moments need no reset: adam_step starts a client's first step (t = 1) from zero moments
             self.step_t.zero_()
         total_loss = torch.zeros((), device=self.device)
         n_steps = 0
@@ -355,7 +354,26 @@ class ClientBatchEngine:
         return self.last_loss
 
     def _step_loss(self, x, y, mask, b_c, active, sample_mask, use_native_loss):
+        """Zero the gradient arena and run one forward + backward. Client-batched transformers on the GPU: the
+        first step of a batch geometry records which gradient rows the fp32 weight-gradient GEMMs write (each by
+        one call); later steps of that geometry let those GEMMs store (first touch) and zero-fill only the other
+        columns (``_first_touch_plan``)."""
+        plan_key = ("tfplan", tuple(x.shape)) if (self.tf is not None and self.native_step is None and
+                                                  self.device.type == "cuda") else None
+        plan = self._tf_plans.get(plan_key) if plan_key is not None else None
+        if plan is not None and plan[1] is not None:
+            plan[1](self.grads)
+            with T.grad_store(plan[0]):
+                return self._step_loss_body(x, y, mask, b_c, active, sample_mask, use_native_loss)
         self.grads.zero_()
+        if plan_key is None or plan is not None:
+            return self._step_loss_body(x, y, mask, b_c, active, sample_mask, use_native_loss)
+        with T.grad_store_record() as calls:
+            loss = self._step_loss_body(x, y, mask, b_c, active, sample_mask, use_native_loss)
+        self._tf_plans[plan_key] = self._first_touch_plan(calls)
+        return loss
+
+    def _step_loss_body(self, x, y, mask, b_c, active, sample_mask, use_native_loss):
         if self.native_step is not None:
             bc = torch.tensor([max(1, b) for b in b_c], dtype=torch.float32, device=self.device)
             row_scale = mask.to(torch.float32) / bc.view(-1, 1)
@@ -687,8 +705,11 @@ class ClientBatchEngine:
         key = ("tf", tuple(x.shape), tuple(y.shape), float(lr), bool(first))
         ent = self._graphs.get(key)
         if ent is None:
+            # the eager warm-up plans (or uses) the first-touch weight gradients of this geometry (_step_loss):
+            # the captured step lets those GEMMs store and zero-fills only the other gradient columns
             loss = self._step_loss(x, y, mask, b_c, active, None, True)
             self._optimizer_step(lr, active, first)
+            rows, zero = self._tf_plans.get(("tfplan", tuple(x.shape)), (frozenset(), None))
             st = {"x": torch.empty_like(x), "y": torch.empty_like(y),
                   "rs": torch.empty(mask.shape, dtype=torch.float32, device=self.device),
                   "act": torch.empty_like(active)}
@@ -698,8 +719,13 @@ class ClientBatchEngine:
             g = torch.cuda.CUDAGraph()
             try:
                 with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
-                    self.grads.zero_()
-                    gl = self._tf_loss(st["x"], st["y"], st["rs"])
+                    if zero is None:
+                        self.grads.zero_()
+                        gl = self._tf_loss(st["x"], st["y"], st["rs"])
+                    else:
+                        zero(self.grads)
+                        with T.grad_store(rows):
+                            gl = self._tf_loss(st["x"], st["y"], st["rs"])
                     self._optimizer_step(lr, st["act"], first)
             except Exception as e:  # noqa: BLE001 - any capture problem: keep the eager step
                 logging.warning("transformer step capture failed (%s); running eagerly", e)
@@ -717,6 +743,24 @@ class ClientBatchEngine:
         g.replay()
         self._shadow_stale = self.optimizer == "sgd"
         return loss
+
+    def _first_touch_plan(self, calls):
+        """(rows, ZeroSegments | None) from the weight-gradient rows recorded in an eager step: ``rows`` are the
+        data_ptrs the captured step's GEMMs may store into, the zero op covers every other gradient column.
+        None when nothing qualifies, or FEDML_AMD_TF_FIRST_TOUCH=0 (full zero fill)."""
+        if not calls or os.environ.get("FEDML_AMD_TF_FIRST_TOUCH", "1") == "0" or self.grads.stride(1) != 1:
+            return frozenset(), None
+        ptrs, rows = T.first_touch_rows(calls)
+        base, es, ld = self.grads.data_ptr(), self.grads.element_size(), self.grads.stride(0)
+        taken = []
+        for ptr, n in rows:
+            off = (ptr - base) // es
+            if (ptr - base) % es or off < 0 or off + n > ld:
+                return frozenset(), None     # not a column range of this arena: keep the full fill
+            taken.append((off, n))
+        if not taken:
+            return frozenset(), None
+        return ptrs, ops.ZeroSegments(ops.complement_segments(self.grads.shape[1], taken), self.device)
 
     def _seq_graph_step(self, x, y, b_c, active, lr, first):
         """Per-client (wide conv net) local step as ONE HIP graph whose C client branches run on C

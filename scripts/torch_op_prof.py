@@ -18,6 +18,8 @@ def main():
     ap.add_argument("--preset", default="distilbert_fedopt_32")
     ap.add_argument("--rows", type=int, default=40)
     ap.add_argument("--trace-dtoh", action="store_true")
+    ap.add_argument("--trace-big", action="store_true")
+    ap.add_argument("--shapes", default="", help="ops whose input shapes are printed (comma list)")
     ap.add_argument("--stacks", default="aten::copy_,aten::fill_,aten::add_,aten::add,aten::zero_,aten::mul",
                     help="ops whose Python call sites are printed (comma list; '' = none)")
     a, rest = ap.parse_known_args()
@@ -32,11 +34,21 @@ def main():
         if state["n"] == 1:        # warmup round (bench --warmup 1)
             return orig(self, n)
         acts = [torch.profiler.ProfilerActivity.CPU, torch.profiler.ProfilerActivity.CUDA]
-        with torch.profiler.profile(activities=acts, with_stack=bool(a.stacks)) as prof:
+        with torch.profiler.profile(activities=acts, with_stack=bool(a.stacks), record_shapes=bool(a.shapes)) as prof:
             r = orig(self, n)
             torch.cuda.synchronize()
         print(prof.key_averages().table(sort_by="self_cuda_time_total", row_limit=a.rows, max_name_column_width=60),
               flush=True)
+        if a.shapes:   # the input shapes of the listed ops, by device time
+            want_s = set(a.shapes.split(","))
+            rows_s = [e for e in prof.key_averages(group_by_input_shape=True) if e.key in want_s]
+            def dev_t_(e):
+                return getattr(e, "self_device_time_total", 0.0) or getattr(e, "self_cuda_time_total", 0.0)
+
+            rows_s.sort(key=lambda e: -dev_t_(e))
+            for e in rows_s[:20]:
+                dev_t = dev_t_(e)
+                print(f"== {e.key} calls {e.count} self device {dev_t / 1e3:.2f} ms shapes {e.input_shapes}")
         if a.stacks:
             want = set(a.stacks.split(","))
             rows = [e for e in prof.key_averages(group_by_stack_n=8) if e.key in want]
@@ -71,6 +83,24 @@ def main():
             setattr(torch.Tensor, name, f)
         for n_ in ("cpu", "to", "numpy", "tolist", "item"):
             wrap(n_)
+    if a.trace_big:    # print the Python call site of every in-place copy_/fill_/zero_ on a tensor above 64 MB
+        import traceback
+        seen_b = {}
+
+        def wrap_b(name):
+            orig_m = getattr(torch.Tensor, name)
+
+            def f(t, *args, **kw):
+                if t.is_cuda and t.numel() * t.element_size() > (64 << 20):
+                    site = "".join(traceback.format_stack()[-8:-1])
+                    seen_b[site] = seen_b.get(site, 0) + 1
+                    if seen_b[site] == 1:
+                        print(f"== Tensor.{name} on {t.numel() * t.element_size() / 2**20:.0f} MB "
+                              f"(contiguous {t.is_contiguous()})\n{site}", flush=True)
+                return orig_m(t, *args, **kw)
+            setattr(torch.Tensor, name, f)
+        for n_ in ("copy_", "fill_", "zero_"):
+            wrap_b(n_)
     sys.argv = ["bench.py", "--preset", a.preset, "--steps", "1", "--warmup", "1"] + rest
     bench.main()
 
