@@ -750,7 +750,11 @@ static int launch_gemm(Args a, int nout, int C, int target_px, hipStream_t strea
   // fp32: ~40 workgroups per client (512..2048): the 13-client share wants 512 (fwd 1.72 → 1.52, bwd-data
   // 1.86 → 1.61 ms/step), 100 clients keep 2048 (scripts/gpu_c3g_small_c.sh)
   const int PC = fa_plan_c(C);
-  const int wgs = wgs_env > 0 ? wgs_env : (P::kF32 ? std::min(2048, std::max(512, 40 * PC)) : 2048);
+  int wgs = wgs_env > 0 ? wgs_env : (P::kF32 ? std::min(2048, std::max(512, 40 * PC)) : 2048);
+  // fp32 64-channel layers over many pixels (ResNet-18's 32² stage: 64 Ki pixels per client) want ~640 pixels
+  // per workgroup: 512 → 1024 workgroups at 10 clients, −0.2 ms/step (profiles/r4_c3_r18_fp32_sweep.txt)
+  if (P::kF32 && KC == 64 && wgs_env <= 0)
+    wgs = std::max(wgs, (int)std::min<int64_t>(2048, (int64_t)PC * a.N * a.H * a.W / 640));
   Plan p = make_plan(a.N, a.H, a.W, PC, target_px, wgs);
   {  // a unit's tile must fit the loader's register budget (≤ 12 16-B chunks per thread)
     const bool f2 = !BWD && ST == 2;
@@ -921,7 +925,11 @@ static int conv3x3_wgrad(const void* g, const void* yv, const float* alpha, cons
     return e ? atoi(e) : 0;
   }();
   const int PC = fa_plan_c(C);
-  const int wgs = wgs_env > 0 ? wgs_env : (P::kF32 ? std::min(2048, std::max(256, 20 * PC)) : 256);
+  int wgs = wgs_env > 0 ? wgs_env : (P::kF32 ? std::min(2048, std::max(256, 20 * PC)) : 256);
+  // fp32 64-channel layers over many pixels: ~640 pixels per workgroup (ResNet-18 at 10 clients: 256 → 1024
+  // workgroups, wgrad −0.6 ms/step; the 8² ResNet-56 layers keep the client-count rule; r4_c3_r18_fp32_sweep.txt)
+  if (P::kF32 && Cin == 64 && wgs_env <= 0)
+    wgs = std::max(wgs, (int)std::min<int64_t>(2048, (int64_t)PC * N * Ho * Wo / 640));
   const int CGX = Cin / P::VEC, CGD = Cout / P::VEC;
   constexpr int XMAX = P::kF32 ? 16 : 8;   // x-tile 16-B chunks per thread (fp32: twice the chunks per pixel)
   Plan p = make_plan(N, Ho, Wo, PC, tpx, wgs);
