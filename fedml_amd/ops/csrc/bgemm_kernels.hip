@@ -38,7 +38,9 @@ constexpr int LDT = BM + 16;   // TR tile [64 k][128 cols] row pitch (elements)
 constexpr int TILE_ELEMS = 128 * LDK;  // == 64 * LDT (18 KiB per operand tile)
 static_assert(128 * LDK == 64 * LDT, "tile images must be the same size");
 
-enum { EPI_BF16 = 0, EPI_GELU = 1, EPI_ACC32 = 2 };
+// EPI_DGELU: the data gradient of a GELU'd linear's output taken through the GELU, D ⊙ gelu'(R) (R = its bf16
+// pre-activation) — the consumer's dgrad absorbs the GELU backward pass
+enum { EPI_BF16 = 0, EPI_GELU = 1, EPI_ACC32 = 2, EPI_DGELU = 3 };
 
 struct Segs {        // row segments of an fp32 arena operand (≤ 4 slots)
   int64_t off[4];    // element offset of segment s's first row, relative to the base pointer
@@ -63,8 +65,14 @@ struct Args {
   Segs biasseg;
   uint16_t* C2;      // EPI_GELU: gelu(D + b) (C keeps the pre-activation for the backward)
   int64_t c2_bs;
+  const uint16_t* R; // EPI_BF16: optional residual addend [C][M][ldc] (D = A·Bᵀ + b + R); EPI_DGELU: pre-activation
+  int64_t r_bs;
+  float* bg;         // EPI_ACC32 (weight gradient): optional bias gradient Σ_t A[t][m] (segmented rows, tn == 0 blocks)
+  int64_t bg_bs;
+  Segs bgseg;
   int M, N, K;
   int tiles_m, tiles_n, nclients;
+  int acc_store;     // EPI_ACC32: the rows' first (only) writer — store instead of += (no zero fill of those rows)
 };
 
 // Constant-index selects only: a runtime index into the by-value kernel-argument struct would be lowered to
@@ -103,6 +111,11 @@ __device__ __forceinline__ bf16x8 tr_frag(const uint16_t* tile, int row0, int co
 }
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_grad(float x, float g) {
+  const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+  const float pdf = 0.3989422804014327f * __expf(-0.5f * x * x);
+  return g * (cdf + x * pdf);
+}
 
 // ---- staging of one bf16 operand tile (4 × 16-byte vectors per thread) ----
 // TR = 0: logical rows [r0, r0+128) × k [k0, k0+64) of storage S[row][k]  (pitch ld)
@@ -244,8 +257,26 @@ __global__ __launch_bounds__(NT, 3) void bgemm_kernel(const Args p) {
   uint4 rbh[4];
   float4 rbf[8];
   const int nk = (p.K + BK - 1) / BK;
+  // weight gradient with a fused bias gradient: the first column-block of every row-block sums its A (dy) tiles
+  // — thread tid's 4 staging vectors all hold columns 8·(tid & 15) .. +7 of the A tile (TR layout)
+  const bool bsum = EPI == EPI_ACC32 && A_TR == 1 && p.bg != nullptr && tn == 0;
+  float bs8[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bs8[e] = 0.f;
+  auto bias_acc = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t w[4] = {ra[i].x, ra[i].y, ra[i].z, ra[i].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        bs8[2 * e] += bf16_to_f32((uint16_t)(w[e] & 0xffff));
+        bs8[2 * e + 1] += bf16_to_f32((uint16_t)(w[e] >> 16));
+      }
+    }
+  };
 
   load_bf16<A_TR>(ra, A, p.lda, p.M, p.K, m0, 0, tid);
+  if (bsum) bias_acc();
   if (B_F32) load_f32<B_TR>(rbf, Bf, p.bseg, p.ldb, p.N, p.K, n0, 0, tid);
   else if (BSEG) load_bf16_seg<B_TR>(rbh, Bh, p.bseg, p.ldb, p.N, p.K, n0, 0, tid);
       else load_bf16<B_TR>(rbh, Bh, p.ldb, p.N, p.K, n0, 0, tid);
@@ -259,6 +290,7 @@ __global__ __launch_bounds__(NT, 3) void bgemm_kernel(const Args p) {
     const bool more = kt + 1 < nk;
     if (more) {   // next tile's global reads fly while this tile's MFMAs run
       load_bf16<A_TR>(ra, A, p.lda, p.M, p.K, m0, (kt + 1) * BK, tid);
+      if (bsum) bias_acc();
       if (B_F32) load_f32<B_TR>(rbf, Bf, p.bseg, p.ldb, p.N, p.K, n0, (kt + 1) * BK, tid);
       else if (BSEG) load_bf16_seg<B_TR>(rbh, Bh, p.bseg, p.ldb, p.N, p.K, n0, (kt + 1) * BK, tid);
       else load_bf16<B_TR>(rbh, Bh, p.ldb, p.N, p.K, n0, (kt + 1) * BK, tid);
@@ -290,6 +322,24 @@ __global__ __launch_bounds__(NT, 3) void bgemm_kernel(const Args p) {
     __syncthreads();
   }
 
+  if (EPI == EPI_ACC32 && A_TR == 1 && bsum) {
+    // the 16 threads holding the same 8 columns (tid & 15) combine through LDS (free after the K loop)
+    float* red = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[tid * 8 + e] = bs8[e];
+    __syncthreads();
+    if (tid < 128) {   // column m0 + tid: group tid >> 3, element tid & 7
+      float t = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) t += red[(r * 16 + (tid >> 3)) * 8 + (tid & 7)];
+      const int m = m0 + tid;
+      if (m < p.M) {
+        float* bp = p.bg + (int64_t)c * p.bg_bs + seg_row(p.bgseg, m, 1);
+        *bp = p.acc_store ? t : *bp + t;
+      }
+    }
+  }
+
   // epilogue: lane owns row m = m0 + wm + 16i + (lane & 15), cols n .. n+3, n = n0 + wn + 16j + 4(lane >> 4)
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -302,13 +352,28 @@ __global__ __launch_bounds__(NT, 3) void bgemm_kernel(const Args p) {
       f32x4 v = acc[i][j];
       if (EPI == EPI_ACC32) {
         float* dst = (float*)p.Cp + (int64_t)c * p.c_bs + seg_row(p.cseg, m, p.ldc) + n;
-        float4 o = *reinterpret_cast<float4*>(dst);
-        o.x += v[0]; o.y += v[1]; o.z += v[2]; o.w += v[3];
+        float4 o = make_float4(v[0], v[1], v[2], v[3]);
+        if (!p.acc_store) {
+          const float4 q = *reinterpret_cast<const float4*>(dst);
+          o.x += q.x; o.y += q.y; o.z += q.z; o.w += q.w;
+        }
         *reinterpret_cast<float4*>(dst) = o;
       } else {
         if (p.bias) {
           const float4 b = *reinterpret_cast<const float4*>(p.bias + (int64_t)c * p.bias_bs + seg_row(p.biasseg, n, 1));
           v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+        }
+        if (p.R) {   // EPI_BF16: residual addend; EPI_DGELU: the pre-activation of the GELU
+          const uint2 rr = *reinterpret_cast<const uint2*>(p.R + (int64_t)c * p.r_bs + (int64_t)m * p.ldc + n);
+          const float r4[4] = {bf16_to_f32((uint16_t)(rr.x & 0xffff)), bf16_to_f32((uint16_t)(rr.x >> 16)),
+                               bf16_to_f32((uint16_t)(rr.y & 0xffff)), bf16_to_f32((uint16_t)(rr.y >> 16))};
+          if (EPI == EPI_DGELU) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = gelu_grad(r4[e], v[e]);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += r4[e];
+          }
         }
         uint2 o;
         o.x = pk2(v[0], v[1]);
@@ -386,13 +451,26 @@ inline void fill_segs(Segs& s, const int64_t* off, const int* lo, int n) {
 //
 // y[c] = x[c] · W[c]ᵀ + b[c]   (W: fp32 arena segments, or — w_bf16 — the same segments of the arena's
 // bf16 shadow; b: fp32 arena segments; y bf16; gelu → y2 = gelu(y))
+FA_EXPORT int fa_bgemm_fwd_res(const void* x, int64_t x_bs, int ldx, const void* w_base, int w_bf16, int64_t w_cs,
+                               const int64_t* w_off, const float* b_base, int64_t b_cs, const int64_t* b_off,
+                               const int* seg_lo, int nseg, void* y, int64_t y_bs, int ldy, void* y2, const void* res,
+                               int C, int M, int N, int K, hipStream_t stream);
 FA_EXPORT int fa_bgemm_fwd(const void* x, int64_t x_bs, int ldx, const void* w_base, int w_bf16, int64_t w_cs,
                            const int64_t* w_off, const float* b_base, int64_t b_cs, const int64_t* b_off,
                            const int* seg_lo, int nseg, void* y, int64_t y_bs, int ldy, void* y2, int C, int M, int N,
                            int K, hipStream_t stream) {
+  return fa_bgemm_fwd_res(x, x_bs, ldx, w_base, w_bf16, w_cs, w_off, b_base, b_cs, b_off, seg_lo, nseg, y, y_bs, ldy,
+                          y2, nullptr, C, M, N, K, stream);
+}
+// res (no GELU): y = x·Wᵀ + b + res, res bf16 with y's layout (a pre-LN block's residual stream in the epilogue)
+FA_EXPORT int fa_bgemm_fwd_res(const void* x, int64_t x_bs, int ldx, const void* w_base, int w_bf16, int64_t w_cs,
+                               const int64_t* w_off, const float* b_base, int64_t b_cs, const int64_t* b_off,
+                               const int* seg_lo, int nseg, void* y, int64_t y_bs, int ldy, void* y2, const void* res,
+                               int C, int M, int N, int K, hipStream_t stream) {
   using namespace bg;
-  if (nseg < 1 || nseg > 4) return (int)hipErrorInvalidValue;
+  if (nseg < 1 || nseg > 4 || (res && y2)) return (int)hipErrorInvalidValue;
   Args a{};
+  a.R = (const uint16_t*)res; a.r_bs = y_bs;
   a.A = (const uint16_t*)x; a.a_bs = x_bs; a.lda = ldx;
   a.B = w_base; a.b_bs = w_cs; a.ldb = K;
   fill_segs(a.bseg, w_off, seg_lo, nseg);
@@ -407,12 +485,25 @@ FA_EXPORT int fa_bgemm_fwd(const void* x, int64_t x_bs, int ldx, const void* w_b
 }
 
 // dx[c] = dy[c] · W[c]      dy [M][N] bf16, W [N][K] fp32 arena segments (rows n), dx [M][K] bf16
+FA_EXPORT int fa_bgemm_dgrad_dgelu(const void* dy, int64_t dy_bs, int lddy, const void* w_base, int w_bf16,
+                                   int64_t w_cs, const int64_t* w_off, const int* seg_lo, int nseg, void* dx,
+                                   int64_t dx_bs, int lddx, const void* pre, int C, int M, int N, int K,
+                                   hipStream_t stream);
 FA_EXPORT int fa_bgemm_dgrad(const void* dy, int64_t dy_bs, int lddy, const void* w_base, int w_bf16, int64_t w_cs,
                              const int64_t* w_off, const int* seg_lo, int nseg, void* dx, int64_t dx_bs, int lddx, int C,
                              int M, int N, int K, hipStream_t stream) {
+  return fa_bgemm_dgrad_dgelu(dy, dy_bs, lddy, w_base, w_bf16, w_cs, w_off, seg_lo, nseg, dx, dx_bs, lddx, nullptr, C, M,
+                              N, K, stream);
+}
+// pre != null: dx = (dy · W) ⊙ gelu'(pre) — pre [C][M][lddx] bf16, the GELU input that produced this linear's x
+FA_EXPORT int fa_bgemm_dgrad_dgelu(const void* dy, int64_t dy_bs, int lddy, const void* w_base, int w_bf16,
+                                   int64_t w_cs, const int64_t* w_off, const int* seg_lo, int nseg, void* dx,
+                                   int64_t dx_bs, int lddx, const void* pre, int C, int M, int N, int K,
+                                   hipStream_t stream) {
   using namespace bg;
   if (nseg < 1 || nseg > 4) return (int)hipErrorInvalidValue;
   Args a{};
+  a.R = (const uint16_t*)pre; a.r_bs = dx_bs;
   // GEMM: D[m][k] = Σ_n dy(m, n) · W(n, k): reduction = n (storage rows of W → TR)
   a.A = (const uint16_t*)dy; a.a_bs = dy_bs; a.lda = lddy;
   a.B = w_base; a.b_bs = w_cs; a.ldb = K;
@@ -420,16 +511,33 @@ FA_EXPORT int fa_bgemm_dgrad(const void* dy, int64_t dy_bs, int lddy, const void
   a.Cp = dx; a.c_bs = dx_bs; a.ldc = lddx;
   a.M = M; a.N = K; a.K = N;
   a.tiles_m = (M + BM - 1) / BM; a.tiles_n = (K + BN - 1) / BN; a.nclients = C;
+  if (pre) return w_bf16 ? launch<0, 1, 0, EPI_DGELU>(a, stream) : launch<0, 1, 1, EPI_DGELU>(a, stream);
   return w_bf16 ? launch<0, 1, 0, EPI_BF16>(a, stream) : launch<0, 1, 1, EPI_BF16>(a, stream);
 }
 
+FA_EXPORT int fa_bgemm_wgrad_bias(const void* dy, int64_t dy_bs, int lddy, const void* x, int64_t x_bs, int ldx,
+                                  float* g_base, int64_t g_cs, const int64_t* g_off, const int* seg_lo, int nseg,
+                                  float* b_base, int64_t b_cs, const int64_t* b_off, int C, int T, int N, int K,
+                                  int store, hipStream_t stream);
 // dW[c] += dy[c]ᵀ · x[c]    dy [T][N], x [T][K] bf16; dW [N][K] fp32 gradient-arena segments (rows n)
 FA_EXPORT int fa_bgemm_wgrad(const void* dy, int64_t dy_bs, int lddy, const void* x, int64_t x_bs, int ldx,
                              float* g_base, int64_t g_cs, const int64_t* g_off, const int* seg_lo, int nseg, int C,
                              int T, int N, int K, hipStream_t stream) {
+  return fa_bgemm_wgrad_bias(dy, dy_bs, lddy, x, x_bs, ldx, g_base, g_cs, g_off, seg_lo, nseg, nullptr, 0, nullptr, C, T,
+                             N, K, 0, stream);
+}
+// b_base != null: also db[c] (+)= Σ_t dy[c][t][:] (bias segments share seg_lo) from the GEMM's own dy tiles;
+// store = 1: = instead of += for dW and db (the rows' first writer)
+FA_EXPORT int fa_bgemm_wgrad_bias(const void* dy, int64_t dy_bs, int lddy, const void* x, int64_t x_bs, int ldx,
+                                  float* g_base, int64_t g_cs, const int64_t* g_off, const int* seg_lo, int nseg,
+                                  float* b_base, int64_t b_cs, const int64_t* b_off, int C, int T, int N, int K,
+                                  int store, hipStream_t stream) {
   using namespace bg;
   if (nseg < 1 || nseg > 4) return (int)hipErrorInvalidValue;
   Args a{};
+  a.bg = b_base; a.bg_bs = b_cs;
+  if (b_base) fill_segs(a.bgseg, b_off, seg_lo, nseg);
+  a.acc_store = store;
   // GEMM: D[n][k] = Σ_t dy(t, n) · x(t, k): both operands have storage rows along t (TR)
   a.A = (const uint16_t*)dy; a.a_bs = dy_bs; a.lda = lddy;
   a.B = x; a.b_bs = x_bs; a.ldb = ldx;

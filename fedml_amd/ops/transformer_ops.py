@@ -452,9 +452,12 @@ class _ClientLinear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gelu, n_w, shadows, res, links, *params):
         ws, bs = params[:n_w], params[n_w:]
-        # links = (dx_link, res_link, gelu_out, gelu_in): ResLink / GeluLink | None each; fp32 native only
-        ctx.dx_link, ctx.res_link, ctx.gelu_out, ctx.gelu_in = \
-            links if (links is not None and x.dtype == torch.float32) else (None, None, None, None)
+        # links = (dx_link, res_link, gelu_out, gelu_in): ResLink / GeluLink | None each; ResLinks fp32 only,
+        # GeluLinks fp32 and bf16 (native kernels)
+        dl, rl, go, gi = links if links is not None else (None, None, None, None)
+        f32 = x.dtype == torch.float32
+        ctx.dx_link, ctx.res_link = (dl, rl) if f32 else (None, None)
+        ctx.gelu_out, ctx.gelu_in = (go, gi) if x.dtype in (torch.float32, torch.bfloat16) else (None, None)
         C, M, K = x.shape
         N = sum(w.shape[1] for w in ws)
         # bf16 shadow of the weights (refreshed once per step by the engine) when given: half the
@@ -470,7 +473,14 @@ class _ClientLinear(torch.autograd.Function):
         y = torch.empty(C, M, N, dtype=x.dtype, device=x.device)
         y2 = torch.empty_like(y) if gelu else None
         fused_res = res is not None and x.dtype == torch.float32 and not gelu
-        if fused_res:                   # y = x·Wᵀ + b + res in the GEMM epilogue (pre-LN residual stream)
+        fused_res16 = (res is not None and x.dtype == torch.bfloat16 and not gelu and res.dtype == torch.bfloat16
+                       and res.shape == (C, M, N) and res.is_contiguous())
+        if fused_res16:                 # bf16: the same residual epilogue
+            rc = _fn("fa_bgemm_fwd_res")(_p(x), _i64(M * K), _c.c_int(K), _p(wb), _c.c_int(wh), _i64(wcs), woff, _p(bb),
+                                         _i64(bcs), boff, lo, _c.c_int(len(ws)), _p(y), _i64(M * N), _c.c_int(N),
+                                         None, _p(res), _c.c_int(C), _c.c_int(M), _c.c_int(N), _c.c_int(K), _stream(x))
+            fused_res = True
+        elif fused_res:                 # y = x·Wᵀ + b + res in the GEMM epilogue (pre-LN residual stream)
             assert wh == 0 and res.shape == (C, M, N) and res.dtype == torch.float32 and res.is_contiguous()
             rc = _fn("fa_bgemm_fwd_res_f32")(_p(x), _i64(M * K), _c.c_int(K), _p(wb), _i64(wcs), woff, _p(bb),
                                              _i64(bcs), boff, lo, _c.c_int(len(ws)), _p(y), _i64(M * N), _c.c_int(N),
@@ -524,8 +534,17 @@ class _ClientLinear(torch.autograd.Function):
             if link is not None and not acc:
                 link.closed = True
             gl = ctx.gelu_in
-            dgelu = sfx and not acc and gl is not None and gl.pre is not None and gl.pre.shape == x.shape
-            if dgelu:   # x = gelu(pre) of the previous linear: return the gradient w.r.t. pre directly
+            dgelu = not acc and gl is not None and gl.pre is not None and gl.pre.shape == x.shape and \
+                gl.pre.dtype == x.dtype and gl.pre.is_contiguous()
+            if dgelu and not sfx:   # bf16: the same GELU backward in the dgrad epilogue
+                dx = torch.empty_like(x)
+                rc = _fn("fa_bgemm_dgrad_dgelu")(_p(g), _i64(M * N), _c.c_int(N), _p(wb), _c.c_int(wh), _i64(wcs),
+                                                 woff, lo, _c.c_int(len(ws)), _p(dx), _i64(M * K), _c.c_int(K),
+                                                 _p(gl.pre), _c.c_int(C), _c.c_int(M), _c.c_int(N), _c.c_int(K),
+                                                 _stream(x))
+                gl.fused = True
+                gl.pre = None
+            elif dgelu:   # x = gelu(pre) of the previous linear: return the gradient w.r.t. pre directly
                 dx = torch.empty_like(x)
                 rc = _fn("fa_bgemm_dgrad_dgelu_f32")(_p(g), _i64(M * N), _c.c_int(N), _p(wb), _i64(wcs), woff, lo,
                                                      _c.c_int(len(ws)), _p(dx), _i64(M * K), _c.c_int(K),
@@ -570,8 +589,8 @@ class _ClientLinear(torch.autograd.Function):
         gb, gcs, goff, glo = _segments(gviews)
         # fp32, engine-owned bias slots, not deterministic: the bias gradient comes out of the weight-gradient GEMM's
         # own reads of g (one pass instead of a separate column reduction)
-        fused_b = (sfx != "" and bs and all(b.is_leaf and b.grad is not None for b in bs) and not _deterministic())
-        rows_w = [(v.data_ptr(), v[0].numel()) for v in gviews] if own and sfx else []
+        fused_b = (bool(bs) and all(b.is_leaf and b.grad is not None for b in bs) and not _deterministic())
+        rows_w = [(v.data_ptr(), v[0].numel()) for v in gviews] if own else []
         rows_b = [(b.grad.data_ptr(), b.grad[0].numel()) for b in bs] if fused_b else []
 
         def first_touch(rows):   # store mode: these rows are written by this call only (not zero-filled)
@@ -580,7 +599,7 @@ class _ClientLinear(torch.autograd.Function):
         if fused_b:
             bb_, bcs_, boff_, blo_ = _segments([b.grad for b in bs])
             if list(blo_) == list(glo):
-                rc = _fn("fa_bgemm_wgrad_bias_f32")(_p(g), _i64(M * N), _c.c_int(N), _p(x), _i64(M * K), _c.c_int(K),
+                rc = _fn("fa_bgemm_wgrad_bias" + sfx)(_p(g), _i64(M * N), _c.c_int(N), _p(x), _i64(M * K), _c.c_int(K),
                                                    _p(gb), _i64(gcs), goff, glo, _c.c_int(len(ws)), _p(bb_),
                                                    _i64(bcs_), boff_, _c.c_int(C), _c.c_int(M), _c.c_int(N),
                                                    _c.c_int(K), _c.c_int(first_touch(rows_w + rows_b)), _stream(x))
@@ -596,9 +615,12 @@ class _ClientLinear(torch.autograd.Function):
             if _GS.mode == "record" and rows_w:
                 _GS.calls.append(tuple(rows_w))
         else:
-            rc = _fn("fa_bgemm_wgrad")(_p(g), _i64(M * N), _c.c_int(N), _p(x), _i64(M * K), _c.c_int(K), _p(gb),
-                                       _i64(gcs), goff, glo, _c.c_int(len(ws)), _c.c_int(C), _c.c_int(M),
-                                       _c.c_int(N), _c.c_int(K), _stream(x))
+            rc = _fn("fa_bgemm_wgrad_bias")(_p(g), _i64(M * N), _c.c_int(N), _p(x), _i64(M * K), _c.c_int(K), _p(gb),
+                                            _i64(gcs), goff, glo, _c.c_int(len(ws)), None, _i64(0), None,
+                                            _c.c_int(C), _c.c_int(M), _c.c_int(N), _c.c_int(K),
+                                            _c.c_int(first_touch(rows_w)), _stream(x))
+            if _GS.mode == "record" and rows_w:
+                _GS.calls.append(tuple(rows_w))
         _check(rc, "fa_bgemm_wgrad" + sfx)
         out_b = []
         if bs and fused_b:

@@ -157,8 +157,8 @@ class BatchedTransformer:
 
     @staticmethod
     def _glink(x, dt):
-        """A GELU-backward hand-off (ops.transformer_ops.GeluLink) on the fp32 native path, else None."""
-        return T.GeluLink() if (x.is_cuda and (dt or x.dtype) == torch.float32) else None
+        """A GELU-backward hand-off (ops.transformer_ops.GeluLink) on the fp32 / bf16 native paths, else None."""
+        return T.GeluLink() if (x.is_cuda and (dt or x.dtype) in (torch.float32, torch.bfloat16)) else None
 
     def _attn(self, v, x, pre, S, kmask, training, dt, seed, res=None, dx_link=None, res_link=None):
         C, Tk, d = x.shape

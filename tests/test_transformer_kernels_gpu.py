@@ -220,3 +220,38 @@ def test_transformer_graph_step_matches_eager(opt):
     init = eng.layout.flatten(model.state_dict(), device=dev)
     assert abs(l0 - l1) / abs(l0) < 1e-2
     assert float((p0 - p1).norm() / (p0 - init).norm()) < 2e-2
+
+
+@pytest.mark.parametrize("store", [False, True])
+def test_bf16_mlp_gelu_fold_residual_and_first_touch(store):
+    """bf16 x → lin1(GELU) → lin2 (+ x): the GELU backward folded into lin2's dgrad epilogue (GeluLink), the residual
+    added in lin2's epilogue, the bias gradients fused into the weight-gradient GEMMs and — ``store`` — the
+    first-touch store mode over garbage-filled gradient rows; against fp32 torch on the same bf16 operands."""
+    torch.manual_seed(7)
+    C, M, d, hid = 2, 96, 128, 256
+    (w1, b1, w2, b2), _ = _arena_views(C, [(hid, d), (hid,), (d, hid), (d,)], seed=7)
+    x = torch.randn(C, M, d, device=dev).to(torch.bfloat16).requires_grad_(True)
+    gy = torch.randn(C, M, d, device=dev).to(torch.bfloat16)
+    gl = T.GeluLink()
+    rows = [(t.grad.data_ptr(), t.grad[0].numel()) for t in (w1, b1, w2, b2)]
+    if store:
+        for t in (w1, b1, w2, b2):
+            t.grad.fill_(123.0)     # first-touch rows must be overwritten, not accumulated onto
+    ctx = T.grad_store({p for p, _ in rows}) if store else T.grad_store_record()
+    with ctx as calls:
+        f = T.client_linear(x, [w1], [b1], gelu=True, gelu_out=gl)
+        y = T.client_linear(f, [w2], [b2], res=x.detach(), gelu_in=gl)
+        y.backward(gy)
+    assert gl.fused
+    if not store:   # both weight-gradient calls recorded with their fused bias rows
+        assert sorted(r for call in calls for r in call) == sorted(rows)
+    w1r, b1r, w2r, b2r = [t.detach().to(torch.bfloat16).float().requires_grad_(True) for t in (w1, b1, w2, b2)]
+    x32 = x.detach().float().requires_grad_(True)
+    pre = torch.bmm(x32, w1r.transpose(1, 2)) + b1r.unsqueeze(1)
+    f32 = torch.nn.functional.gelu(pre)
+    y32 = torch.bmm(f32, w2r.transpose(1, 2)) + b2r.unsqueeze(1) + x32.detach()
+    y32.backward(gy.float())
+    _close(y, y32, 2e-2)
+    _close(x.grad, x32.grad, 3e-2)
+    for t, r in zip((w1, b1, w2, b2), (w1r, b1r, w2r, b2r)):
+        _close(t.grad, r.grad, 3e-2)
