@@ -495,6 +495,24 @@ FA_EXPORT int fa_bgemm_dgrad(const void* dy, int64_t dy_bs, int lddy, const void
   return fa_bgemm_dgrad_dgelu(dy, dy_bs, lddy, w_base, w_bf16, w_cs, w_off, seg_lo, nseg, dx, dx_bs, lddx, nullptr, C, M,
                               N, K, stream);
 }
+// dx = dy · W + add   (add bf16 with dx's layout; may alias dx — each element is read, then written, by one lane):
+// the residual-stream gradient of x's other consumer folded into this dgrad's epilogue
+FA_EXPORT int fa_bgemm_dgrad_add(const void* dy, int64_t dy_bs, int lddy, const void* w_base, int w_bf16,
+                                 int64_t w_cs, const int64_t* w_off, const int* seg_lo, int nseg, void* dx,
+                                 int64_t dx_bs, int lddx, const void* add, int C, int M, int N, int K,
+                                 hipStream_t stream) {
+  using namespace bg;
+  if (nseg < 1 || nseg > 4 || !add) return (int)hipErrorInvalidValue;
+  Args a{};
+  a.R = (const uint16_t*)add; a.r_bs = dx_bs;
+  a.A = (const uint16_t*)dy; a.a_bs = dy_bs; a.lda = lddy;
+  a.B = w_base; a.b_bs = w_cs; a.ldb = K;
+  fill_segs(a.bseg, w_off, seg_lo, nseg);
+  a.Cp = dx; a.c_bs = dx_bs; a.ldc = lddx;
+  a.M = M; a.N = K; a.K = N;
+  a.tiles_m = (M + BM - 1) / BM; a.tiles_n = (K + BN - 1) / BN; a.nclients = C;
+  return w_bf16 ? launch<0, 1, 0, EPI_BF16>(a, stream) : launch<0, 1, 1, EPI_BF16>(a, stream);
+}
 // pre != null: dx = (dy · W) ⊙ gelu'(pre) — pre [C][M][lddx] bf16, the GELU input that produced this linear's x
 FA_EXPORT int fa_bgemm_dgrad_dgelu(const void* dy, int64_t dy_bs, int lddy, const void* w_base, int w_bf16,
                                    int64_t w_cs, const int64_t* w_off, const int* seg_lo, int nseg, void* dx,

@@ -127,7 +127,8 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
                                                      uint16_t* __restrict__ dx, uint16_t* __restrict__ dh,
                                                      uint32_t thr, float dscale, uint32_t seed,
                                                      float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                     const uint32_t* __restrict__ seedp, int64_t gcs, int64_t dgcs) {
+                                                     const uint32_t* __restrict__ seedp, int64_t gcs, int64_t dgcs,
+                                                     const uint16_t* __restrict__ dadd) {
   if (seedp) seed += *seedp * 1000003u;
   extern __shared__ float red[];  // [4][2][d]
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -178,6 +179,12 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const uint16_t* __restrict_
 #pragma unroll
             for (int j = 0; j < 8; ++j)
               o[j] = fa_drop::keep(seed, (uint32_t)row, (uint32_t)(col + j), thr) ? o[j] * dscale : 0.f;
+          }
+          if (dadd) {   // the other consumer's gradient of the LN input (pre-LN residual stream)
+            float a8[8];
+            unpack8(*(const uint4*)(dadd + row * d + col), a8);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) o[j] += a8[j];
           }
           *(uint4*)(dh + row * d + col) = pack8(o);
         }
@@ -614,12 +621,12 @@ template <int NV>
 int launch_ln_bwd(const uint16_t* dy, const uint16_t* x, const float* mean, const float* rstd, int C, int rpc, int d,
                   const float* g, uint16_t* dx, uint16_t* dh, uint32_t thr, float dscale, uint32_t seed,
                   const uint32_t* seedp, float* dg,
-                  float* db, int64_t gcs, int64_t dgcs, hipStream_t st) {
+                  float* db, int64_t gcs, int64_t dgcs, hipStream_t st, const uint16_t* dadd = nullptr) {
   int bpc = (rpc + 31) / 32;  // ≥8 rows per wave
   if (bpc < 1) bpc = 1;
   if (bpc > 1024) bpc = 1024;
   hipLaunchKernelGGL(ln_bwd_kernel<NV>, dim3(bpc, C), dim3(256), 8 * d * sizeof(float), st, dy, x, mean, rstd, rpc,
-                     d, g, dx, dh, thr, dscale, seed, dg, db, seedp, gcs, dgcs);
+                     d, g, dx, dh, thr, dscale, seed, dg, db, seedp, gcs, dgcs, dadd);
   return (int)hipGetLastError();
 }
 
@@ -647,18 +654,31 @@ FA_EXPORT int fa_ln_fwd(const void* h, const void* res, int R, int d, int rows_p
   return launch_ln_fwd<4>(H, Rs, R, d, rows_per_client, gamma, beta, eps, thr, dscale, seed, seedp, Y, X, mean, rstd, gcs, stream);
 }
 
+FA_EXPORT int fa_ln_bwd_add(const void* dy, const void* x, const float* mean, const float* rstd, int C,
+                            int rows_per_client, int d, const float* gamma, void* dx, void* dh, uint32_t thr,
+                            float dscale, uint32_t seed, float* dgamma, float* dbeta, const uint32_t* seedp,
+                            int64_t gcs, int64_t dgcs, const void* dadd, hipStream_t stream);
 FA_EXPORT int fa_ln_bwd(const void* dy, const void* x, const float* mean, const float* rstd, int C,
                         int rows_per_client, int d, const float* gamma, void* dx, void* dh, uint32_t thr, float dscale,
                         uint32_t seed, float* dgamma, float* dbeta, const uint32_t* seedp, int64_t gcs,
                         int64_t dgcs, hipStream_t stream) {
+  return fa_ln_bwd_add(dy, x, mean, rstd, C, rows_per_client, d, gamma, dx, dh, thr, dscale, seed, dgamma, dbeta, seedp,
+                       gcs, dgcs, nullptr, stream);
+}
+// dadd (optional, bf16 like dh): added to dh — the residual stream's other gradient (pre-LN)
+FA_EXPORT int fa_ln_bwd_add(const void* dy, const void* x, const float* mean, const float* rstd, int C,
+                            int rows_per_client, int d, const float* gamma, void* dx, void* dh, uint32_t thr,
+                            float dscale, uint32_t seed, float* dgamma, float* dbeta, const uint32_t* seedp,
+                            int64_t gcs, int64_t dgcs, const void* dadd, hipStream_t stream) {
   if (d % 8 != 0 || d > 2048 || gcs % 4 != 0) return (int)hipErrorInvalidValue;
   auto DY = (const uint16_t*)dy;
   auto X = (const uint16_t*)x;
   auto DX = (uint16_t*)dx;
   auto DH = (uint16_t*)dh;
-  if (d <= 512) return launch_ln_bwd<1>(DY, X, mean, rstd, C, rows_per_client, d, gamma, DX, DH, thr, dscale, seed, seedp, dgamma, dbeta, gcs, dgcs, stream);
-  if (d <= 1024) return launch_ln_bwd<2>(DY, X, mean, rstd, C, rows_per_client, d, gamma, DX, DH, thr, dscale, seed, seedp, dgamma, dbeta, gcs, dgcs, stream);
-  return launch_ln_bwd<4>(DY, X, mean, rstd, C, rows_per_client, d, gamma, DX, DH, thr, dscale, seed, seedp, dgamma, dbeta, gcs, dgcs, stream);
+  auto DA = (const uint16_t*)dadd;
+  if (d <= 512) return launch_ln_bwd<1>(DY, X, mean, rstd, C, rows_per_client, d, gamma, DX, DH, thr, dscale, seed, seedp, dgamma, dbeta, gcs, dgcs, stream, DA);
+  if (d <= 1024) return launch_ln_bwd<2>(DY, X, mean, rstd, C, rows_per_client, d, gamma, DX, DH, thr, dscale, seed, seedp, dgamma, dbeta, gcs, dgcs, stream, DA);
+  return launch_ln_bwd<4>(DY, X, mean, rstd, C, rows_per_client, d, gamma, DX, DH, thr, dscale, seed, seedp, dgamma, dbeta, gcs, dgcs, stream, DA);
 }
 
 FA_EXPORT int fa_gelu_fwd(const void* x, void* y, int64_t n, hipStream_t stream) {

@@ -190,8 +190,9 @@ class _LayerNorm(torch.autograd.Function):
         ctx.save_for_backward(xsum if fused else h, mean, rstd, g)
         ctx.cfg = (p, seed, rpc, res is not None, fused, gamma.dtype, gcs)
         ctx.seed_dev = seed_dev
-        ctx.link = link if res is not None and h.dtype == torch.float32 else None    # post-LN: dres → link.g
-        ctx.in_link = in_link if h.dtype == torch.float32 else None                 # pre-LN: dh += link.g
+        ln16 = h.dtype in (torch.float32, torch.bfloat16)
+        ctx.link = link if res is not None and ln16 else None    # post-LN: dres → link.g
+        ctx.in_link = in_link if ln16 else None                  # pre-LN: dh += link.g
         # γ/β leaves with pre-assigned gradient-arena views: the backward kernel accumulates dγ/dβ into them
         ctx.own = (gamma, beta) if (gamma.is_leaf and beta.is_leaf and gamma.grad is not None and beta.grad is not None
                                     and gamma.grad.stride() == gamma.stride() and beta.grad.stride() == beta.stride()
@@ -226,7 +227,7 @@ class _LayerNorm(torch.autograd.Function):
             else:
                 ctx.in_link.closed = True
         if dadd is not None:
-            name = "fa_ln_bwd_add_f32"
+            name = "fa_ln_bwd_add" + _sfx(x)
             rc = _fn(name)(_p(dy), _p(x), _p(mean), _p(rstd), _c.c_int(C), _c.c_int(rpc), _c.c_int(d), _p(g),
                            _p(dres), _p(dh), _c.c_uint32(_thr(p)), _f(1.0 / (1.0 - p) if p > 0 else 1.0),
                            _c.c_uint32(seed & _M32), _p(dg), _p(db), _p(seed_dev), _i64(gcs), _i64(dgcs), _p(dadd),
@@ -452,11 +453,9 @@ class _ClientLinear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gelu, n_w, shadows, res, links, *params):
         ws, bs = params[:n_w], params[n_w:]
-        # links = (dx_link, res_link, gelu_out, gelu_in): ResLink / GeluLink | None each; ResLinks fp32 only,
-        # GeluLinks fp32 and bf16 (native kernels)
+        # links = (dx_link, res_link, gelu_out, gelu_in): ResLink / GeluLink | None each (fp32 / bf16 native kernels)
         dl, rl, go, gi = links if links is not None else (None, None, None, None)
-        f32 = x.dtype == torch.float32
-        ctx.dx_link, ctx.res_link = (dl, rl) if f32 else (None, None)
+        ctx.dx_link, ctx.res_link = (dl, rl) if x.dtype in (torch.float32, torch.bfloat16) else (None, None)
         ctx.gelu_out, ctx.gelu_in = (go, gi) if x.dtype in (torch.float32, torch.bfloat16) else (None, None)
         C, M, K = x.shape
         N = sum(w.shape[1] for w in ws)
@@ -530,7 +529,7 @@ class _ClientLinear(torch.autograd.Function):
             wb, wcs, woff, lo = _segments(ctx.wsrc)
             wh = 1 if ctx.wsrc[0].dtype == torch.bfloat16 else 0
             link = ctx.dx_link
-            acc = sfx and link is not None and link.g is not None
+            acc = link is not None and link.g is not None and link.g.dtype == x.dtype and link.g.is_contiguous()
             if link is not None and not acc:
                 link.closed = True
             gl = ctx.gelu_in
@@ -552,6 +551,12 @@ class _ClientLinear(torch.autograd.Function):
                                                      _stream(x))
                 gl.fused = True
                 gl.pre = None
+            elif acc and not sfx:   # bf16: dx = dy·W + (the other consumer's gradient), in the epilogue, in place
+                dx = link.g.view(C, M, K)
+                link.g = None
+                rc = _fn("fa_bgemm_dgrad_add")(_p(g), _i64(M * N), _c.c_int(N), _p(wb), _c.c_int(wh), _i64(wcs), woff,
+                                               lo, _c.c_int(len(ws)), _p(dx), _i64(M * K), _c.c_int(K), _p(dx),
+                                               _c.c_int(C), _c.c_int(M), _c.c_int(N), _c.c_int(K), _stream(x))
             elif acc:   # x's other consumer (a post-LN residual) left its gradient: add ours into it
                 dx = link.g.view(C, M, K)
                 link.g = None

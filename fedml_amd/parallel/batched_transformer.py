@@ -152,8 +152,8 @@ class BatchedTransformer:
 
     @staticmethod
     def _link(x, dt):
-        """A residual-gradient hand-off (ops.transformer_ops.ResLink) on the fp32 native path, else None."""
-        return T.ResLink() if (x.is_cuda and (dt or x.dtype) == torch.float32) else None
+        """A residual-gradient hand-off (ops.transformer_ops.ResLink) on the fp32 / bf16 native paths, else None."""
+        return T.ResLink() if (x.is_cuda and (dt or x.dtype) in (torch.float32, torch.bfloat16)) else None
 
     @staticmethod
     def _glink(x, dt):

@@ -7,4 +7,5 @@ bash scripts/gpu_steps.sh \
  "timeout -k 10 150 python -u bench.py --preset vit_b16_32 --dtype bf16 --steps 4 --warmup 2 > gpurun_out/r4_vit_bf16_b35.json 2>&1" \
  "timeout -k 10 150 python -u bench.py --preset distilbert_fedopt_32 --dtype bf16 --steps 5 --warmup 2 > gpurun_out/r4_distil_bf16_b35.json 2>&1" \
  "timeout -k 10 150 python -u bench.py --preset vit_b16_32 --steps 4 --warmup 2 > gpurun_out/r4_vit_b35.json 2>&1" \
+ "timeout -k 10 150 python -u bench.py --preset distilbert_fedopt_32 --steps 5 --warmup 2 > gpurun_out/r4_distil_b35.json 2>&1" \
  "timeout -k 10 300 python -u scripts/torch_op_prof.py --preset vit_b16_32 --dtype bf16 --stacks '' --shapes aten::copy_,aten::fill_,aten::add_,aten::add --rows 30 > gpurun_out/r4_vit_bf16_ops2.txt 2>&1"

@@ -255,3 +255,36 @@ def test_bf16_mlp_gelu_fold_residual_and_first_touch(store):
     _close(x.grad, x32.grad, 3e-2)
     for t, r in zip((w1, b1, w2, b2), (w1r, b1r, w2r, b2r)):
         _close(t.grad, r.grad, 3e-2)
+
+
+def test_bf16_residual_links_match_plain_composition():
+    """bf16 pre-LN block x → LN → lin1(GELU) → lin2 (+ x) with the residual-stream gradient handed to the LN backward
+    (ResLink, added in the bf16 LN kernel) and the GELU backward folded into lin2's dgrad — against the plain
+    composition (autograd adds), to bf16 rounding. (The post-LN hand-off, added in the consumer's dgrad epilogue,
+    runs in the bf16 DistilBERT checks of test_batched_transformer_gpu_vs_fp32_modules.)"""
+    torch.manual_seed(9)
+    C, M, d, hid = 2, 80, 128, 256
+    (g1, b1, w1, bb1, w2, bb2), _ = _arena_views(C, [(d,), (d,), (hid, d), (hid,), (d, hid), (d,)], seed=9)
+    with torch.no_grad():
+        g1 += 1.0
+    x0 = torch.randn(C, M, d, device=dev).to(torch.bfloat16)
+    gy = torch.randn(C, M, d, device=dev).to(torch.bfloat16)
+    outs = []
+    for linked in (False, True):
+        for t in (g1, b1, w1, bb1, w2, bb2):
+            t.grad.zero_()
+        x = x0.clone().requires_grad_(True)
+        rl = T.ResLink() if linked else None
+        gl = T.GeluLink() if linked else None
+        h = T.layer_norm(x.reshape(-1, d), g1, b1, 1e-5, M, in_link=rl).view(C, M, d)
+        f = T.client_linear(h, [w1], [bb1], gelu=True, gelu_out=gl)
+        y = T.client_linear(f, [w2], [bb2], res=x, res_link=rl, gelu_in=gl)
+        y.backward(gy)
+        outs.append((y.detach().float(), x.grad.float().clone(), [t.grad.clone() for t in (g1, b1, w1, bb1, w2, bb2)]))
+        if linked:
+            assert gl.fused
+    (y0, dx0, gr0), (y1, dx1, gr1) = outs
+    _close(y1, y0, 1e-2)
+    _close(dx1, dx0, 2e-2)
+    for a, b in zip(gr1, gr0):
+        _close(a, b, 2e-2)
