@@ -171,6 +171,15 @@ def main():
         print(f"{name:16s} {label:34s} {n // a.steps:5d} {ms_s:8.3f} {1000 * ms / n:8.1f} {gbs:7.0f} {tfs:6.1f}")
     print("-- by op:", ", ".join(f"{k} {v:.2f} ms" for k, v in by_op.most_common()))
     print(f"-- kernels {sum(by_op.values()):.2f} ms of {total_ms:.2f} ms step (rest = torch head/zeroing/launch gaps)")
+    # per-step budget: every kernel at the practical HBM ceiling or the matrix peak, whichever binds it
+    hbm = float(os.environ.get("FEDML_AMD_HBM_TBS", "6.3")) * 1e12
+    peak = (157.3e12 if a.fp32_mma == "exact" else 2.5e15 / 3) if a.dtype == "fp32" else 2.5e15
+    nb_step = sum(v[2] for v in agg.values()) / a.steps
+    fl_step = sum(v[3] for v in agg.values()) / a.steps
+    bound_ms = sum(max(v[2] / hbm, v[3] / peak) * 1e3 for v in agg.values()) / a.steps
+    print(f"-- budget: ideal {nb_step / 1e9:.2f} GB and {fl_step / 1e12:.3f} TFLOP per step; every kernel at "
+          f"{hbm / 1e12:.1f} TB/s or {peak / 1e12:.0f} TF/s (whichever binds): {bound_ms:.2f} ms "
+          f"= {100 * bound_ms / max(1e-9, sum(by_op.values())):.0f} % of the measured kernel time")
 
 
 if __name__ == "__main__":
