@@ -928,8 +928,10 @@ static int conv3x3_wgrad(const void* g, const void* yv, const float* alpha, cons
   int wgs = wgs_env > 0 ? wgs_env : (P::kF32 ? std::min(2048, std::max(256, 20 * PC)) : 256);
   // fp32 64-channel layers over many pixels: ~640 pixels per workgroup (ResNet-18 at 10 clients: 256 → 1024
   // workgroups, wgrad −0.6 ms/step; the 8² ResNet-56 layers keep the client-count rule; r4_c3_r18_fp32_sweep.txt)
+  // and at most 1024 (100 clients, 64 channels at 8²: 2000 → 1024 workgroups, 2.78 → 2.43 ms/step; the 16- and
+  // 32-channel layers keep 2000, profiles/r4_c3w_c100_sweep.txt)
   if (P::kF32 && Cin == 64 && wgs_env <= 0)
-    wgs = std::max(wgs, (int)std::min<int64_t>(2048, (int64_t)PC * N * Ho * Wo / 640));
+    wgs = std::max(std::min(wgs, 1024), (int)std::min<int64_t>(2048, (int64_t)PC * N * Ho * Wo / 640));
   const int CGX = Cin / P::VEC, CGD = Cout / P::VEC;
   constexpr int XMAX = P::kF32 ? 16 : 8;   // x-tile 16-B chunks per thread (fp32: twice the chunks per pixel)
   Plan p = make_plan(N, Ho, Wo, PC, tpx, wgs);
