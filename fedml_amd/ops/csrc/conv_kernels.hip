@@ -993,7 +993,10 @@ static int convk_min_k() {
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("FEDML_AMD_CONVK_MIN_K");
-    v = e ? atoi(e) : 256;   // measured: ResNet-18 preset +9 %, ResNet-56 headline neutral
+    // 256 → 128 (round 4): the 256 → 64 block-output 1×1 of the headline's 8² stage runs faster as the K-streamed
+    // GEMM plus a separate block-output pass than as the fused generic kernel — headline fp32 +0.8 %, 13-client share
+    // +1.4 %, MobileNet +2 %, ResNet-18 neutral (profiles/r4_bench_convk_min_k.jsonl); 256 in round 3: ResNet-18 +9 %
+    v = e ? atoi(e) : 128;
   }
   return v;
 }

@@ -93,7 +93,7 @@ def conv_fwd(x, wpk, wpk_ld, pscale, pshift, y, stats, C, N, H, W, Cin, Cout, KH
 
 def convk_min_k() -> int:
     """K above which the wide-layer dispatch runs the K-streamed kernel (conv_kernels.hip convk_min_k)."""
-    return int(os.environ.get("FEDML_AMD_CONVK_MIN_K", "256") or 256)
+    return int(os.environ.get("FEDML_AMD_CONVK_MIN_K", "128") or 128)
 
 
 def conv_fwd_pbout(yp, s, t, res, rs, rt, bout, wpk, wpk_ld, y, stats, C, N, H, W, Cin, Cout, ldk, tiles_per_wave,
