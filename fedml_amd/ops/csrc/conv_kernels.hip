@@ -123,7 +123,7 @@ __global__ __launch_bounds__(256) void pack_weights_tiled_kernel(const float* __
   // PK_U independent loads per thread are in flight before the first LDS write: one load → wait → write per
   // iteration left the kernel HBM-latency bound (36 round trips per thread for a full 3×3 tile; ResNet-18
   // bf16 0.47 ms per step at 1.4 TB/s)
-  constexpr int PK_U = 12;
+  constexpr int PK_U = 36;
   const int rowlen = tci * taps, n = tco * rowlen;
   for (int base = 0; base < n; base += 256 * PK_U) {
     float v[PK_U];
