@@ -650,7 +650,7 @@ struct ConvK {
   static constexpr int NB = BN / RPI;                                      // B chunks per thread
   static_assert(NA >= 1 && NB >= 1, "tile too small for the staging map");
   static_assert(4 * 16 * 64 <= (BM + BN) * LD, "epilogue staging must fit the operand tiles");
-  static size_t smem(int kc) { return (size_t)(BM + BN) * LD * P::ES + (size_t)3 * kc * 4 + (size_t)4 * 64 * 3 * 4; }
+  static size_t smem(int kc) { return (size_t)(BM + BN) * LD * P::ES + (size_t)4 * kc * 4 + (size_t)4 * 64 * 3 * 4; }
 };
 
 // wave (wm, wn) = (wid / WN, wid % WN) owns pixel rows [16·TM·wm, +16·TM) × channels [64·wn, +64) of the
@@ -705,10 +705,14 @@ __global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
   float* v0 = reinterpret_cast<float*>(wl + CK::BN * LD);                          // [KC]
   float* v1 = v0 + a.KC;
   float* v2 = v1 + a.KC;
-  float* red = v2 + a.KC;                                                           // [4 waves][64][3]
+  float* v3 = v2 + a.KC;                                                            // PRO_BOUT: shortcut-BN shift
+  float* red = v3 + a.KC;                                                           // [4 waves][64][3]
   T* my_stage = al + wid * 16 * NOUT;   // epilogue staging [4][16][64] reuses the operand tiles
-
-  if (DY || PRO == PRO_BNRELU) {
+  // PRO_BOUT (1×1 / stride 1): the operand is the previous block's output relu(y·s + t + r), r = src2 | src2·v2 + v3,
+  // formed at staging (same operation order as block_out_kernel) and written once to pro_out by the first
+  // N-tile's workgroups
+  constexpr bool BOUT = PRO == PRO_BOUT;
+  if (DY || PRO == PRO_BNRELU || BOUT) {
     for (int i = threadIdx.x; i < a.KC; i += 256) {
       if (!DY && a.lz0) {
         bn_lazy_fwd(a.lz0, c, i, bx == 0 && bzz == 0, v0[i], v1[i]);
@@ -717,13 +721,23 @@ __global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
         v1[i] = a.vec1[(int64_t)c * a.KC + i];
       }
       if (DY) v2[i] = a.vec2[(int64_t)c * a.KC + i];
+      if (BOUT && a.vec2) {
+        if (a.lz1) {
+          bn_lazy_fwd(a.lz1, c, i, bx == 0 && bzz == 0, v2[i], v3[i]);
+        } else {
+          v2[i] = a.vec2[(int64_t)c * a.KC + i];
+          v3[i] = a.vec3[(int64_t)c * a.KC + i];
+        }
+      }
     }
   }
   for (int i = threadIdx.x; i < 4 * NOUT * 3; i += 256) red[i] = 0.f;
 
   const int64_t src_client = (int64_t)c * a.Nb * a.Hs * a.Ws * a.KC;
   const T* src = reinterpret_cast<const T*>(a.src) + src_client;
-  const T* src2 = DY ? reinterpret_cast<const T*>(a.src2) + src_client : nullptr;
+  constexpr bool TWO = DY || BOUT;   // second operand stream (y | shortcut)
+  const T* src2 = TWO ? reinterpret_cast<const T*>(a.src2) + src_client : nullptr;
+  T* pro_out = (BOUT && bz == 0) ? reinterpret_cast<T*>(a.pro_out) + src_client : nullptr;
   T* out = reinterpret_cast<T*>(a.out) + (int64_t)c * Mo * NO;
   const T* wsrc = reinterpret_cast<const T*>(a.wpk) + (int64_t)c * a.wpk_ld + (int64_t)ch_base * a.ldk;
 
@@ -751,7 +765,8 @@ __global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
 #pragma unroll
     for (int nt = 0; nt < NT; ++nt) acc[t][nt] = {0.f, 0.f, 0.f, 0.f};
 
-  uint4 ra[CK::NA], ry[DY ? CK::NA : 1], rb[CK::NB];
+  uint4 ra[CK::NA], ry[TWO ? CK::NA : 1], rb[CK::NB];
+  int64_t aoff[BOUT ? CK::NA : 1];   // PRO_BOUT: the operand element's position (pro_out write)
   uint32_t aval = 0;
   auto fetch = [&](int kbase) {
     const int k = kbase + col * V;
@@ -763,7 +778,7 @@ __global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < CK::NA; ++j) {
       ra[j] = make_uint4(0, 0, 0, 0);
-      if (DY) ry[j] = make_uint4(0, 0, 0, 0);
+      if (TWO) ry[j] = make_uint4(0, 0, 0, 0);
       if (rn[j] >= 0 && kval) {
         const int ph = rhw[j] >> 16, pw = rhw[j] & 0xffff;
         int ih, iw;
@@ -788,7 +803,8 @@ __global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
         if (ok) {
           const int64_t off = (((int64_t)rn[j] * a.Hs + ih) * a.Ws + iw) * a.KC + ci;
           ra[j] = *reinterpret_cast<const uint4*>(src + off);
-          if (DY) ry[j] = *reinterpret_cast<const uint4*>(src2 + off);
+          if (TWO) ry[j] = *reinterpret_cast<const uint4*>(src2 + off);
+          if constexpr (BOUT) aoff[j] = off;
           aval |= 1u << j;
         }
       }
@@ -805,7 +821,19 @@ __global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
     for (int j = 0; j < CK::NA; ++j) {
       uint4 v = make_uint4(0, 0, 0, 0);   // out-of-image taps / padding rows: 0 (not the transform of 0)
       if ((aval >> j) & 1u) {
-        if (PRO == PRO_BNRELU || DY) {
+        if constexpr (BOUT) {
+          float f[V], r[V];
+          P::unpack(ra[j], f);
+          P::unpack(ry[j], r);
+#pragma unroll
+          for (int e = 0; e < V; ++e) {
+            f[e] = f[e] * v0[ci + e] + v1[ci + e];
+            f[e] += a.vec2 ? r[e] * v2[ci + e] + v3[ci + e] : r[e];
+            f[e] = P::round(fmaxf(f[e], 0.f));   // the operand = the stored value
+          }
+          v = P::pack(f);
+          if (pro_out) *reinterpret_cast<uint4*>(pro_out + aoff[j]) = v;
+        } else if (PRO == PRO_BNRELU || DY) {
           float f[V];
           P::unpack(ra[j], f);
           if (DY) {
@@ -1115,7 +1143,7 @@ static int conv_fwd_pbout(const void* yp, const float* s, const float* t, const 
   a.pad = 0; a.ldk = ldk; a.Kp = (Cin + 31) / 32 * 32; a.tiles_per_wave = tiles_per_wave;
   a.lz0 = fa_take_lazy(0);
   a.lz1 = fa_take_lazy(1);
-  if (Cout % 64 == 0 && (Cout > 256 || Cin > convk_min_k())) return -5;   // the K-streamed kernel has no PRO_BOUT
+  // wide layers: the K-streamed kernel forms the operand at its LDS staging (dispatch_nt routes them there)
   return dispatch_nt<P, AOP_ACT, PRO_BOUT, MODE_FWD, EPI_FWD>(Cout, a, C, stream);
 }
 

@@ -470,8 +470,7 @@ class NativeResNetStep:
         if not self.use_pbout or nb is None or b.ry or nb.ds_conv is not None:
             return False
         cv = nb.convs[0]
-        return (cv.k == 1 and cv.stride == 1 and cv.pad == 0 and cv.cin == cv.cin_pad
-                and not (cv.cout % 64 == 0 and (cv.cout > 256 or cv.cin > nn_ops.convk_min_k())))
+        return cv.k == 1 and cv.stride == 1 and cv.pad == 0 and cv.cin == cv.cin_pad
 
     def _c1f(self, cv: ConvSpec, epi):
         return (self.use_c1f and cv.cin == cv.cin_pad
