@@ -465,9 +465,10 @@ class NativeResNetStep:
 
     def _pbout_ok(self, b, nb) -> bool:
         """Block ``b``'s output is formed in the operand load of the next block's first conv (conv_fwd_pbout: 1×1,
-        stride 1, identity shortcut in the next block — its only other reader is that block's output pass, which
-        then reads the stored output) instead of by its own block-output pass."""
-        if not self.use_pbout or nb is None or b.ry or nb.ds_conv is not None:
+        stride 1) and written once from there instead of by its own block-output pass. Its other readers run after
+        that conv and read the stored output: the next block's output pass (identity shortcut) or its downsample
+        conv (stage transitions), and the backward (act_in)."""
+        if not self.use_pbout or nb is None or b.ry:
             return False
         cv = nb.convs[0]
         return cv.k == 1 and cv.stride == 1 and cv.pad == 0 and cv.cin == cv.cin_pad

@@ -52,9 +52,10 @@ def test_fused_block_output_is_bit_identical(monkeypatch, dtype, layers, hw, cou
     l1, a1, g1, o1, s1 = _run(monkeypatch, "1", model, layout, flat, x, y, counts, dtype)
     nb = len(s1.blocks)
     fused = [s1._pbout_ok(s1.blocks[i], s1.blocks[i + 1] if i + 1 < nb else None) for i in range(nb)]
-    # every block followed by an identity-shortcut block of its stage (the 64-plane stage's 256 → 64 conv forms
-    # its operand in the K-streamed kernel's staging, the others in the generic kernel's operand load)
-    assert sum(fused) == sum(layers) - 3 and not any(
+    # every block but the last (the 64-plane stage's 256 → 64 conv forms its operand in the K-streamed kernel's
+    # staging, the others in the generic kernel's operand load; at stage transitions the downsample conv then
+    # reads the stored output)
+    assert sum(fused) == sum(layers) - 1 and not any(
         s0._pbout_ok(s0.blocks[i], s0.blocks[i + 1] if i + 1 < nb else None) for i in range(nb))
     for c, n in enumerate(counts):
         for u, v in zip(o0, o1):
