@@ -130,8 +130,13 @@ def score_from_metrics(m: Dict[str, torch.Tensor], score: str = "acc", target_la
 class CoalitionValuer:
     """Caches coalition values v(mask) for one round's K local models."""
 
+    _METRICS = ("correct", "loss", "tp", "fp", "fn", "total")
+
     def __init__(self, evaluator: BatchedModelEvaluator, flats: torch.Tensor, sample_nums, valid_data,
-                 score="acc", target_label=None):
+                 score="acc", target_label=None, shard: bool = False):
+        """``shard``: every rank of the process group evaluates its share of each batch of new coalitions
+        (coalition i of the sorted batch on rank i mod W) and the scores are all-gathered — the coalition
+        evaluation spreads over the GPUs (all ranks must call ``ensure`` with the same masks)."""
         self.ev = evaluator
         self.flats = flats.to(evaluator.device)
         self.n = list(sample_nums)
@@ -142,19 +147,41 @@ class CoalitionValuer:
         self.v: Dict[int, float] = {0: 0.0}
         self.metrics: Dict[int, Dict[str, float]] = {}
         self.evaluations = 0
+        from ..parallel import comm
+        self._comm = comm
+        self.shard = bool(shard) and comm.is_dist()
 
     def ensure(self, masks: Sequence[int]):
         todo = sorted({m for m in masks if m not in self.v})
         if not todo:
             return
-        W = coalition_weights(todo, self.n).to(self.flats.device)
-        models = ops.subset_aggregate(W, self.flats)
-        m = self.ev.evaluate(models, self.data, self.target)
+        if self.shard:
+            m = self._sharded_metrics(todo)
+        else:
+            W = coalition_weights(todo, self.n).to(self.flats.device)
+            m = self.ev.evaluate(ops.subset_aggregate(W, self.flats), self.data, self.target)
         vals = score_from_metrics(m, self.score, self.target)
         for i, mask in enumerate(todo):
             self.v[mask] = float(vals[i])
             self.metrics[mask] = {k: float(t[i]) for k, t in m.items()}
         self.evaluations += len(todo)
+
+    def _sharded_metrics(self, todo):
+        comm = self._comm
+        R, r = comm.world_size(), comm.rank()
+        mine = todo[r::R]
+        per = -(-len(todo) // R)
+        packed = torch.zeros(per, len(self._METRICS), dtype=torch.float64, device=self.flats.device)
+        if mine:
+            W = coalition_weights(mine, self.n).to(self.flats.device)
+            m = self.ev.evaluate(ops.subset_aggregate(W, self.flats), self.data, self.target)
+            packed[:len(mine)] = torch.stack([m[k] for k in self._METRICS], 1).to(packed.device)
+        parts = comm.all_gather_flat(packed.view(-1))
+        out = torch.zeros(len(todo), len(self._METRICS), dtype=torch.float64)
+        for q, part in enumerate(parts):
+            n_q = len(todo[q::R])
+            out[q::R] = part.view(per, -1)[:n_q].cpu()
+        return {k: out[:, j].clone() for j, k in enumerate(self._METRICS)}
 
     def exact_reference_sv(self) -> List[float]:
         """The reference's exact estimator: for client i, average over every non-empty coalition

@@ -221,31 +221,35 @@ def adam_step(param, grad, exp_avg, exp_avg_sq, step, lr, beta1=0.9, beta2=0.999
                                  _f(weight_decay), _c.c_int(int(decoupled)), _p(active), _p(shadow), _stream(param))
         _check(rc, "fa_adam_step")
         return param
+    # Same contract as the HIP kernel: an inactive client (active[c] == 0) is skipped ENTIRELY — its
+    # parameters, moments, AMSGrad maximum and shadow row keep their values (no weight decay either).
+    on = (active.view(C, 1) != 0) if active is not None else torch.ones(C, 1, dtype=torch.bool, device=param.device)
     g = grad.to(torch.float32)
     t = step.view(C, 1).to(torch.float32)
+    p = param
     if weight_decay != 0.0:
         if decoupled:
-            param.mul_(1 - lr * weight_decay)
+            p = param * (1 - lr * weight_decay)
         else:
             g = g + weight_decay * param
     # first step (t ≤ 1): the moments start from zero whatever the buffers hold (the native kernel never reads
     # them then; callers need not reset them between rounds)
     fresh = t <= 1
-    exp_avg.copy_(torch.where(fresh, 0.0, exp_avg)).mul_(beta1).add_(g, alpha=1 - beta1)
-    exp_avg_sq.copy_(torch.where(fresh, 0.0, exp_avg_sq)).mul_(beta2).addcmul_(g, g, value=1 - beta2)
+    m1 = torch.where(fresh, 0.0, exp_avg) * beta1 + (1 - beta1) * g
+    m2 = torch.where(fresh, 0.0, exp_avg_sq) * beta2 + (1 - beta2) * g * g
     bc1 = 1 - beta1 ** t
     bc2 = 1 - beta2 ** t
     if amsgrad:
-        max_exp_avg_sq.copy_(torch.where(fresh, exp_avg_sq, torch.maximum(max_exp_avg_sq, exp_avg_sq)))
-        den = max_exp_avg_sq.sqrt() / bc2.sqrt() + eps
+        vm = torch.where(fresh, m2, torch.maximum(max_exp_avg_sq, m2))
+        den = vm.sqrt() / bc2.sqrt() + eps
+        max_exp_avg_sq.copy_(torch.where(on, vm, max_exp_avg_sq))
     else:
-        den = exp_avg_sq.sqrt() / bc2.sqrt() + eps
-    upd = (lr / bc1) * exp_avg / den
-    if active is not None:
-        upd = upd * active.view(C, 1)
-    param.sub_(upd)
+        den = m2.sqrt() / bc2.sqrt() + eps
+    exp_avg.copy_(torch.where(on, m1, exp_avg))
+    exp_avg_sq.copy_(torch.where(on, m2, exp_avg_sq))
+    param.copy_(torch.where(on, p - (lr / bc1) * m1 / den, param))
     if shadow is not None:
-        shadow.copy_(param.to(torch.bfloat16))
+        shadow.copy_(torch.where(on, param.to(torch.bfloat16), shadow))
     return param
 
 

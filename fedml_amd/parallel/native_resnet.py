@@ -18,6 +18,7 @@ Per block (k chained convs, last BN joins the residual):
             conv_0 bwd-data adds the shortcut gradient, applies the previous block's ReLU mask and
             produces the previous block's g and BN statistics in its epilogue.
 """
+import collections
 import ctypes
 import math
 import os
@@ -163,7 +164,11 @@ class NativeResNetStep:
         # deferred BN finalisation (csrc/bnlazy.h): the first consumer kernel folds the statistics itself
         self.use_lazy = os.environ.get("FEDML_AMD_BN_LAZY", "1") != "0"
         self._pending = {}       # (bn key, "f" | "b") → explicit finalisation closure, while deferred
-        self._lz_key = None
+        # deferred-BN descriptor buffers, one per distinct content (geometry + every pointer they embed); buffers a
+        # captured HIP graph baked in are pinned: never overwritten, never freed while this step object lives
+        self._lz_cache = collections.OrderedDict()
+        self._lz_pinned = set()
+        self._lz_dev, self._lz_key, self._lz_slot = None, None, {}
         self.dump = None   # debug: list collecting (name, tensor clone) of every backward gradient buffer
         self._nimg = None
         self.det = None    # DetAccumulator in deterministic mode (enable_deterministic)
@@ -328,7 +333,6 @@ class NativeResNetStep:
             if b.ds_conv is not None:
                 self._bn_hw[b.ds_bn.key] = b.ds_conv.Ho * b.ds_conv.Wo
                 self._bn_q[b.ds_bn.key] = 2
-        self._lz_dev, self._lz_key, self._lz_slot = None, None, {}
         self.geom = (N, H, W)
         if self.det is not None:
             for t in (self.stats, self.dw_scratch, self.dw_c3, self.gram):
@@ -352,8 +356,10 @@ class NativeResNetStep:
 
     # Every geometry keeps its own buffers alive: a captured HIP graph of one batch size must stay
     # valid while another batch size (the ragged last step of an epoch) is being run.
+    # (the deferred-BN descriptor buffers are NOT per geometry: ``_lz_cache`` holds one buffer per distinct
+    # descriptor content, see _lz_prepare)
     _STATE_ATTRS = ("x_in", "stem_y", "stem_out", "gbuf", "dybuf", "bn_vec", "stats", "stat_views", "pooled", "dpool",
-                    "loss_c", "dw_scratch", "_lz_dev", "_lz_key", "_lz_slot", "_bn_hw", "_bn_q",
+                    "loss_c", "dw_scratch", "_bn_hw", "_bn_q",
                     "dw_c3", "gram", "c3_segs", "c3_nseg", "c3_maxn", "_c3_off",
                     "packed", "packed_ld", "_segs", "_nseg", "_pack_tiles", "_pack_taps", "final_hw", "geom")
 
@@ -577,14 +583,33 @@ class NativeResNetStep:
         for key in list(self._pending):
             self._pending.pop(key)[0]()
 
+    _LZ_UNPINNED_MAX = 8
+
     def _lz_prepare(self, arena, garena, active, N):
-        """Descriptors of every BN (forward + backward) for this geometry and these buffers, uploaded only when
-        they change (a captured graph replays with the same buffers, so its capture never uploads)."""
+        """Descriptors of every BN (forward + backward) for this geometry and these buffers.
+
+        The descriptor content is a pure function of ``key`` (the geometry — whose per-BN vectors live as long as
+        this object — and every external pointer it embeds), so each distinct key gets its OWN device buffer,
+        uploaded once. A HIP graph captured with one buffer keeps replaying against exactly that content: another
+        graph's warm-up (different static ``active`` / ``nimg`` tensors), an eager step or a geometry switch never
+        rewrites or frees it (one shared per-geometry buffer was overwritten in place, so the first-step
+        graph folded BN with another graph's ``nimg`` / ``active``, and a geometry switch dropped the only
+        reference to a buffer older graphs still read). Buffers used while a capture is running are pinned; at most
+        ``_LZ_UNPINNED_MAX`` unpinned ones are kept (eager steps with fresh ``nimg`` tensors), least recent first
+        out — stream order makes releasing one safe (the caching allocator reuses it on this stream only)."""
         nimg = self._nimg
         key = (self.geom, arena.data_ptr(), garena.data_ptr(), active.data_ptr() if active is not None else 0,
                nimg.data_ptr() if nimg is not None else 0, arena.stride(0))
-        if self._lz_key == key:
+        capturing = torch.cuda.is_current_stream_capturing()
+        buf = self._lz_cache.get(key)
+        if buf is not None:
+            self._lz_cache.move_to_end(key)
+            self._lz_dev, self._lz_key = buf, key
+            if capturing:
+                self._lz_pinned.add(key)
             return
+        if capturing:
+            raise RuntimeError("deferred-BN descriptors changed during graph capture (no warm-up with these buffers)")
         bns = list(self._all_bns())
         arr = (nn_ops.BnLazy * (2 * len(bns)))()
         self._lz_slot = {}
@@ -613,12 +638,13 @@ class NativeResNetStep:
             self._lz_slot[(bn.key, "f")] = 2 * i
             self._lz_slot[(bn.key, "b")] = 2 * i + 1
         raw = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
-        if self._lz_dev is None or self._lz_dev.numel() != raw.numel():
-            self._lz_dev = torch.empty(raw.numel(), dtype=torch.uint8, device=self.device)   # per geometry
-        if torch.cuda.is_current_stream_capturing():
-            raise RuntimeError("deferred-BN descriptors changed during graph capture")
-        self._lz_dev.copy_(raw)
-        self._lz_key = key
+        buf = torch.empty(raw.numel(), dtype=torch.uint8, device=self.device)
+        buf.copy_(raw)
+        self._lz_cache[key] = buf
+        self._lz_dev, self._lz_key = buf, key
+        unpinned = [k for k in self._lz_cache if k not in self._lz_pinned]
+        for k in unpinned[:max(0, len(unpinned) - self._LZ_UNPINNED_MAX)]:
+            del self._lz_cache[k]
 
     # ------------------------------------------------------------------ step
     def step(self, arena, garena, x, labels, row_scale, active, nimg=None):

@@ -192,6 +192,14 @@ class ClientBatchEngine:
         # semantics, e.g. S-FedAvg's clip 1.0: simulation/sp/valuation_base.py)
         cg = getattr(args, "clip_grad_norm", None)
         self.clip_grad_norm = float(cg) if cg not in (None, "", 0, 0.0) else None
+        # per-client class weights of a weighted CE ([C, classes] fp32 on the device, set per round; S-FedAvg's
+        # class-balanced loss, reference s_fedavg/my_model_trainer_classification.py:27): a weighted mean
+        # Σ w[y_i]·CE_i / Σ w[y_i] is the plain CE head with row scales w[y_i] / Σ_batch w[y_j] — every executor
+        # (native head kernel, fused CE, sequential torch) takes it through ``_row_scale``
+        self.class_weight: Optional[torch.Tensor] = None
+        # per-step input transform x [C, B, ...] → x on the client-stacked batch, after the gather and the
+        # augmentation (HS-FedAvg's amplitude normalisation): ``hook(x, b_c)`` with b_c the valid rows per slot
+        self.input_hook = None
         _LIVE_ENGINES.add(self)
         self.use_graphs = self.device.type == "cuda" and os.environ.get("FEDML_AMD_HIP_GRAPHS", "1") != "0"
         self.native_step = None
@@ -324,6 +332,8 @@ class ClientBatchEngine:
                     x = ops.augment(x.reshape(-1, *x.shape[2:]), seed=aug_seed & 0x7FFFFFFF,
                                     sample_ids=idx.reshape(-1), pad=self.aug_pad,
                                     cutout=self.aug_cutout).view_as(x)
+                if self.input_hook is not None:
+                    x = self.input_hook(x, b_c)
                 key_a = tuple(active_list)
                 active = self._active_cache.get(key_a)
                 if active is None:   # cached: a fresh host→device tensor per step would sync the stream
@@ -375,8 +385,7 @@ class ClientBatchEngine:
 
     def _step_loss_body(self, x, y, mask, b_c, active, sample_mask, use_native_loss):
         if self.native_step is not None:
-            bc = torch.tensor([max(1, b) for b in b_c], dtype=torch.float32, device=self.device)
-            row_scale = mask.to(torch.float32) / bc.view(-1, 1)
+            row_scale = self._row_scale(mask, b_c, y)
             nimg = torch.tensor(b_c, dtype=torch.int32, device=self.device)
             return self.native_step.step(self.params, self.grads, x, y, row_scale, active, nimg=nimg)
         if self.tf is not None:
@@ -400,8 +409,7 @@ class ClientBatchEngine:
             if not logits.is_contiguous():
                 logits = logits.contiguous()
             labels = y.reshape(C * B)
-            bc = torch.tensor([max(1, b) for b in b_c], dtype=torch.float32, device=self.device)
-            row_scale = (mask.to(torch.float32) / bc.view(C, 1)).reshape(C * B)
+            row_scale = self._row_scale(mask, b_c, y).reshape(C * B)
             if use_native_loss:
                 loss = ops.FusedCrossEntropy.apply(logits, labels, row_scale, None)
             else:
@@ -504,11 +512,24 @@ class ClientBatchEngine:
                 torch.tensor(b_c, dtype=torch.int32, device=self.device))
         return ent
 
+    def _row_scale(self, mask, b_c, y, out=None):
+        """[C, B] loss weight of every row: 1 / (valid rows of the client) — the per-client batch mean — or, with
+        ``class_weight``, w_c[y] / Σ_valid w_c[y] (class-weighted CE mean, torch ``CrossEntropyLoss(weight=)``)."""
+        if self.class_weight is None:
+            bc, _ = self._counts_dev(b_c)
+            if out is None:
+                return mask.to(torch.float32) / bc.view(-1, 1)
+            return torch.div(mask.to(torch.float32), bc.view(-1, 1), out=out)
+        C = mask.shape[0]
+        wr = torch.gather(self.class_weight, 1, y.reshape(C, -1).long()) * mask.to(torch.float32)
+        rs = wr / wr.sum(1, keepdim=True).clamp_min(1e-30)
+        return rs if out is None else out.copy_(rs)
+
     def _fill_static(self, st, x, y, mask, b_c, active):
         st["x"].copy_(x, non_blocking=True)
         st["y"].copy_(y, non_blocking=True)
-        bc, nimg = self._counts_dev(b_c)
-        torch.div(mask.to(torch.float32), bc.view(-1, 1), out=st["rs"])
+        _, nimg = self._counts_dev(b_c)
+        self._row_scale(mask, b_c, y, out=st["rs"])
         st["act"].copy_(active, non_blocking=True)
         if "nimg" in st:
             st["nimg"].copy_(nimg, non_blocking=True)
@@ -655,7 +676,9 @@ class ClientBatchEngine:
                 if isinstance(out, tuple):
                     out = out[-1]
                 if self.loss_name == "ce":
-                    loss = torch.nn.functional.cross_entropy(out.float().reshape(b, -1), y[c, :b].reshape(b))
+                    loss = torch.nn.functional.cross_entropy(
+                        out.float().reshape(b, -1), y[c, :b].reshape(b),
+                        weight=self.class_weight[c] if self.class_weight is not None else None)
                 else:
                     loss = _task_loss(self.loss_name, out.unsqueeze(0), y[c:c + 1, :b], None)[0]
                 keys = list(pv.keys())

@@ -244,7 +244,7 @@ class RCCLSimulator:
                 self.upload_bytes.append(nb)
                 comm.all_reduce_flat(self.partial)
             elif self.engine.deterministic:
-                self._det_partial_sum(w)
+                self._det_partial_sum(w, normalize=not self.fednova)
             elif comm.is_dist() and self.layout.size > self.bucket_elems:
                 # large models (DistilBERT / ViT: 67-86 M params): the weighted sum is produced bucket by
                 # bucket and each bucket's all-reduce is enqueued at once — RCCL's stream reduces bucket k
@@ -280,10 +280,15 @@ class RCCLSimulator:
                 self.global_flat.copy_(avg)
             self._post_aggregate()
 
-    def _det_partial_sum(self, w):
+    def _det_partial_sum(self, w, normalize=True):
         """Deterministic mode: Σ_c w_c·params_c ‖ Σ_c w_c accumulated and all-reduced in fp64, rounded to fp32 once.
         The fp64 sums of different client groupings (1 rank × K clients vs R ranks × K/R) differ only at 2^-53, far
-        below the final fp32 rounding, so the global model's bits do not depend on the world size."""
+        below the final fp32 rounding, so the global model's bits do not depend on the world size (barring an fp64
+        sum that lands within 2^-53 of an fp32 rounding tie).
+
+        ``normalize``: the weighted MEAN is formed in fp64 too (one rounding to fp32 instead of rounding the sum and
+        then dividing in fp32); ``partial`` then holds avg ‖ 1 (‖ 0 when every weight is zero), so the caller's
+        ``partial[:P] / partial[P]`` is exact. FedNova (which needs the raw sums) passes False."""
         P = self.layout.size
         if getattr(self, "_partial64", None) is None:
             self._partial64 = torch.empty(P + 1, dtype=torch.float64, device=self.device)
@@ -294,7 +299,12 @@ class RCCLSimulator:
             torch.sum(self.engine.params[:, lo:hi].to(torch.float64) * wd, 0, out=self._partial64[lo:hi])
         self._partial64[P:].copy_(wd.sum().view(1))
         comm.all_reduce_flat(self._partial64)
-        self.partial.copy_(self._partial64)
+        if normalize:
+            tot = self._partial64[P:]
+            self.partial[:P].copy_(self._partial64[:P] / tot.clamp_min(1e-300))
+            self.partial[P:].copy_((tot > 0).to(torch.float32))
+        else:
+            self.partial.copy_(self._partial64)
 
     def _fednova_coefficients(self, ids, mine):
         """FedNova weights of this rank's slots: coef_i = τ_eff·p_i / a_i with p_i = n_i / Σn over the round's

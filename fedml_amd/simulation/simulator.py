@@ -105,7 +105,11 @@ class SimulatorMPI:
 class SimulatorRCCL:
     def __init__(self, args, device, dataset, model, model_trainer=None):
         from .rccl.simulator import RCCLSimulator
-        if args.federated_optimizer not in (FedML_FEDERATED_OPTIMIZER_FEDAVG, FedML_FEDERATED_OPTIMIZER_FEDOPT,
+        if args.federated_optimizer in (FedML_FEDERATED_OPTIMIZER_S_FEDAVG, FedML_FEDERATED_OPTIMIZER_HS_FEDAVG):
+            # Shapley-valued variants: batched local training + sharded coalition valuation (rccl/valued.py)
+            from .rccl.valued import ValuedRCCLSimulator
+            self.simulator = ValuedRCCLSimulator(args, device, dataset, model, model_trainer=model_trainer)
+        elif args.federated_optimizer not in (FedML_FEDERATED_OPTIMIZER_FEDAVG, FedML_FEDERATED_OPTIMIZER_FEDOPT,
                                             FedML_FEDERATED_OPTIMIZER_FEDPROX, FedML_FEDERATED_OPTIMIZER_FEDAVG_ROBUST,
                                             FedML_FEDERATED_OPTIMIZER_FEDNOVA):
             logging.warning("RCCL simulator runs FedAvg-family optimizers; %s falls back to the SP simulator",

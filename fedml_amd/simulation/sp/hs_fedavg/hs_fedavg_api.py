@@ -11,25 +11,15 @@ top-K by φ (uniform ``np.random.seed(round)`` sampling while all φ are equal).
 import logging
 import time
 
-import numpy as np
 import torch
 
 from ....ops.spectral import amplitude_normalize
-from ..valuation_base import ValuedFedAvgBase
+from ..valuation_base import ValuedFedAvgBase, hs_fedavg_sampling
 
 
 class HS_FedAvgAPI(ValuedFedAvgBase):
     def _client_sampling(self, round_idx, client_num_in_total, client_num_per_round, phi=None):
-        if client_num_in_total == client_num_per_round:
-            return list(range(client_num_in_total))
-        n = min(client_num_per_round, client_num_in_total)
-        if phi is None or len(set(phi)) == 1:
-            np.random.seed(round_idx)
-            return np.random.choice(range(client_num_in_total), n, replace=False).tolist()
-        # top-K by φ; ties broken randomly (the reference picks a random sort algorithm)
-        rng = np.random.RandomState(round_idx)
-        keys = np.lexsort((rng.random_sample(len(phi)), np.asarray(phi)))
-        return keys[-n:].tolist()
+        return hs_fedavg_sampling(round_idx, client_num_in_total, client_num_per_round, phi)
 
     def _client_train(self, client, w, amp_summary=None):
         state = {"amp": amp_summary.clone() if amp_summary is not None else None}

@@ -14,20 +14,12 @@ import time
 
 import numpy as np
 
-from ..valuation_base import ValuedFedAvgBase
+from ..valuation_base import ValuedFedAvgBase, s_fedavg_sampling
 
 
 class S_FedAvgAPI(ValuedFedAvgBase):
     def _client_sampling(self, round_idx, client_num_in_total, client_num_per_round, phi=None, sampling_filter=None):
-        if client_num_in_total == client_num_per_round:
-            return list(range(client_num_in_total))
-        n = min(client_num_per_round, client_num_in_total)
-        if sampling_filter == "exp" and phi is not None:
-            P = np.exp(np.asarray(phi, dtype=np.float64))
-        else:
-            P = np.ones(client_num_in_total)
-        P = P / (P.sum() + 1e-13)
-        return np.random.choice(range(client_num_in_total), size=n, replace=False, p=P).tolist()
+        return s_fedavg_sampling(round_idx, client_num_in_total, client_num_per_round, phi, sampling_filter)
 
     def train(self):
         K = int(self.args.client_num_in_total)

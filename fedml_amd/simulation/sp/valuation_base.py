@@ -24,19 +24,70 @@ def calc_class_weight(train_data, class_num):
                         dtype=torch.float32)
 
 
+def s_fedavg_sampling(round_idx, client_num_in_total, client_num_per_round, phi=None, sampling_filter=None):
+    """S-FedAvg client sampling (reference `s_fedavg/fedavg_api.py:435-477`): ``p ∝ exp(φ)`` when
+    ``sampling_filter == "exp"``, else uniform, drawn from numpy's global generator (seeded by ``fedml.init``);
+    every client when all of them take part."""
+    if client_num_in_total == client_num_per_round:
+        return list(range(client_num_in_total))
+    n = min(client_num_per_round, client_num_in_total)
+    if sampling_filter == "exp" and phi is not None:
+        P = np.exp(np.asarray(phi, dtype=np.float64))
+    else:
+        P = np.ones(client_num_in_total)
+    P = P / (P.sum() + 1e-13)
+    return np.random.choice(range(client_num_in_total), size=n, replace=False, p=P).tolist()
+
+
+def hs_fedavg_sampling(round_idx, client_num_in_total, client_num_per_round, phi=None):
+    """HS-FedAvg client selection (reference `hs_fedavg/fedavg_api.py:284-302`): the top-K clients by φ, ties
+    broken randomly (the reference picks a random sort algorithm); uniform ``np.random.seed(round)`` sampling
+    while every φ is equal."""
+    if client_num_in_total == client_num_per_round:
+        return list(range(client_num_in_total))
+    n = min(client_num_per_round, client_num_in_total)
+    if phi is None or len(set(phi)) == 1:
+        np.random.seed(round_idx)
+        return np.random.choice(range(client_num_in_total), n, replace=False).tolist()
+    rng = np.random.RandomState(round_idx)
+    keys = np.lexsort((rng.random_sample(len(phi)), np.asarray(phi)))
+    return keys[-n:].tolist()
+
+
+def valuation_config(args, dataset=None):
+    """(valid, alpha, beta, filter, approaching, score, target) from the reference's 15-tuple dataset or the
+    config (`s_fedavg/fedavg_api.py:29-45`)."""
+    ds = list(dataset) if dataset is not None else []
+    if len(ds) >= 15:
+        return tuple(ds[8:15])
+    return (getattr(args, "valid_data_in_aggregator", None),
+            float(getattr(args, "sv_alpha", getattr(args, "alpha", 0.5))),
+            float(getattr(args, "sv_beta", getattr(args, "beta", 0.5))),
+            getattr(args, "sampling_filter", "exp"),
+            bool(getattr(args, "sv_approaching", False)),
+            getattr(args, "score_method", "acc"),
+            ds[8] if len(ds) == 9 else getattr(args, "target_label", None))
+
+
+def validation_subset(test_global, n, seed, batch_size):
+    """The server-side validation set: a seeded random subset of the global test set, as (x, y) batches."""
+    xs, ys = [], []
+    for x, y in test_global:
+        xs.append(x)
+        ys.append(y)
+    if not xs:
+        return []
+    x, y = torch.cat(xs), torch.cat(ys)
+    g = torch.Generator().manual_seed(int(seed))
+    idx = torch.randperm(len(x), generator=g)[:n]
+    bs = int(batch_size)
+    return [(x[idx[i:i + bs]], y[idx[i:i + bs]]) for i in range(0, len(idx), bs)]
+
+
 class ValuedFedAvgBase(FedAvgAPI):
     def __init__(self, args, device, dataset, model, model_trainer=None):
         ds = list(dataset)
-        if len(ds) >= 15:  # reference 15-tuple
-            valid, alpha, beta, filt, approaching, score, target = ds[8:15]
-        else:
-            valid = getattr(args, "valid_data_in_aggregator", None)
-            alpha = float(getattr(args, "sv_alpha", getattr(args, "alpha", 0.5)))
-            beta = float(getattr(args, "sv_beta", getattr(args, "beta", 0.5)))
-            filt = getattr(args, "sampling_filter", "exp")
-            approaching = bool(getattr(args, "sv_approaching", False))
-            score = getattr(args, "score_method", "acc")
-            target = ds[8] if len(ds) == 9 else getattr(args, "target_label", None)
+        valid, alpha, beta, filt, approaching, score, target = valuation_config(args, ds)
         trainer = model_trainer or create_model_trainer(model, args)
         if hasattr(trainer, "clip_grad_norm"):
             trainer.clip_grad_norm = 1.0
@@ -54,17 +105,8 @@ class ValuedFedAvgBase(FedAvgAPI):
 
     def _validation_subset(self, n):
         """Random subset of the global test set as the server-side validation set."""
-        xs, ys = [], []
-        for x, y in self.test_global:
-            xs.append(x)
-            ys.append(y)
-        if not xs:
-            return []
-        x, y = torch.cat(xs), torch.cat(ys)
-        g = torch.Generator().manual_seed(int(getattr(self.args, "random_seed", 0) or 0))
-        idx = torch.randperm(len(x), generator=g)[:n]
-        bs = int(self.args.batch_size)
-        return [(x[idx[i:i + bs]], y[idx[i:i + bs]]) for i in range(0, len(idx), bs)]
+        return validation_subset(self.test_global, n, int(getattr(self.args, "random_seed", 0) or 0),
+                                 int(self.args.batch_size))
 
     def _train_clients(self, client_indexes, w_global, **kw):
         w_locals = []

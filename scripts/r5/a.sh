@@ -1,0 +1,8 @@
+#!/bin/bash
+# round 5, call A: descriptor-lifetime fix + headline / 13-client share benches
+cd "$(dirname "$0")/../.." && mkdir -p gpurun_out/r5a
+export TMPDIR=/tmp
+bash scripts/gpu_steps.sh \
+ "timeout -k 10 400 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_native_graph_lazy_gpu.py tests/test_optimizer_state_reset.py > gpurun_out/r5a/tests.txt 2>&1" \
+ "timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/r5a/bench.txt 2>&1" \
+ "timeout -k 10 300 python -u bench.py --steps 40 --warmup 5 --clients 13 > gpurun_out/r5a/bench_c13.txt 2>&1"

@@ -33,6 +33,35 @@ def test_adam_first_step_ignores_stale_moments_cpu():
     _check_fresh("cpu")
 
 
+def _check_inactive(dev):
+    """A client idle in a step (active 0, step counter still at 1) keeps every piece of its state — the HIP
+    kernel skips its row entirely; the CPU fallback must not reset its moments or decay its weights."""
+    torch.manual_seed(1)
+    C, P = 3, 517
+    for amsgrad in (False, True):
+        p = torch.randn(C, P, device=dev)
+        m1, m2 = torch.randn(C, P, device=dev), torch.rand(C, P, device=dev)
+        vm = torch.rand(C, P, device=dev) if amsgrad else None
+        sh = p.to(torch.bfloat16)
+        before = [t.clone() for t in (p, m1, m2) + ((vm,) if amsgrad else ())] + [sh.clone()]
+        act = torch.tensor([1.0, 0.0, 1.0], device=dev)
+        ops.adam_step(p, torch.randn(C, P, device=dev), m1, m2, torch.ones(C, device=dev), 1e-2, weight_decay=0.1,
+                      amsgrad=amsgrad, max_exp_avg_sq=vm, decoupled=True, active=act, shadow=sh)
+        after = [p, m1, m2] + ([vm] if amsgrad else []) + [sh]
+        for a, b in zip(before, after):
+            assert torch.equal(a[1], b[1])          # idle client: untouched
+            assert not torch.equal(a[0], b[0])      # active client: updated
+
+
+def test_adam_inactive_client_keeps_state_cpu():
+    _check_inactive("cpu")
+
+
+@pytest.mark.gpu
+def test_adam_inactive_client_keeps_state_gpu():
+    _check_inactive("cuda")
+
+
 def test_broadcast_rows_cpu():
     dst = torch.randn(4, 10)
     src = torch.randn(10)
