@@ -34,6 +34,8 @@ class ClientMasterManager(FedMLClientManager):
 
     def handle_message_init(self, msg):
         params = self.resolve_payload(msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS))
+        if self.plane_skip():       # RCCL plane, not selected this round: zeros into the reduce, no silo round
+            return
         self.note_global(params)
         self.trainer.update_model(params)
         silo = int(msg.get(MyMessage.MSG_ARG_KEY_CLIENT_INDEX))
@@ -44,6 +46,8 @@ class ClientMasterManager(FedMLClientManager):
 
     def handle_message_receive_model_from_server(self, msg):
         params = self.resolve_payload(msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS))
+        if self.plane_skip():
+            return
         self.note_global(params)
         self.trainer.update_model(params)
         silo = int(msg.get(MyMessage.MSG_ARG_KEY_CLIENT_INDEX))
@@ -59,7 +63,7 @@ class ClientMasterManager(FedMLClientManager):
 
     def _train_and_send(self):
         # device plane: keep the silo average on the GPU (no state-dict round trip through the host)
-        weights, n = self.trainer.train(self.round_idx, flat=self.mailbox is not None)
+        weights, n = self.trainer.train(self.round_idx, flat=self.mailbox is not None or self.plane is not None)
         self.send_model_to_server(0, weights, n)
 
 

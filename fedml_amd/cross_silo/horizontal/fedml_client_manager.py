@@ -30,6 +30,8 @@ class FedMLClientManager(ClientManager):
         self.client_real_id = self.client_real_ids[self.get_sender_id() - 1]
         self.has_sent_online_msg = False
         self.mailbox = None
+        self.plane = None            # RCCL data plane (cross_silo/fed_plane.py), opened by the first 'rccl' marker
+        self._plane_train = True
         self._stop_stats = threading.Event()
         self.final_model = None
         self.faults = FaultInjector(args)
@@ -52,11 +54,35 @@ class FedMLClientManager(ClientManager):
         from ..device_mailbox import SiloMailbox, is_marker
         if not is_marker(params):
             return params
+        if params["__devmail__"] == "rccl":
+            return self._plane_receive(params)
         if self.mailbox is None or params["__devmail__"] == "init":
             if "desc" not in params:
                 raise RuntimeError("device-plane marker without a mailbox descriptor before the silo opened one")
             self.mailbox = SiloMailbox(params["desc"], int(params["slot"]))
         return self.mailbox.glob
+
+    def _plane_device(self):
+        dev = getattr(self.trainer, "device", None)
+        return torch.device(dev) if dev is not None and torch.device(dev).type == "cuda" else torch.device("cpu")
+
+    def _plane_receive(self, mk):
+        """Join the round's broadcast: the global model lands in this master's flat device buffer."""
+        if self.plane is None:
+            from ..fed_plane import FederationPlane
+            rank = self.client_real_ids.index(self.client_real_id) + 1
+            self.plane = FederationPlane(rank, len(self.client_real_ids) + 1, int(mk["port"]), self._plane_device())
+            self._plane_buf = torch.zeros(int(mk["P"]), dtype=torch.float32, device=self._plane_device())
+        self.plane.broadcast(self._plane_buf)
+        self._plane_train = bool(mk.get("train", True))
+        return self._plane_buf
+
+    def plane_skip(self):
+        """RCCL plane, silo not selected this round: add zeros to the round's reduce and do nothing else."""
+        if self.plane is None or self._plane_train:
+            return False
+        self.plane.reduce(torch.zeros(self._plane_buf.numel() + 1, dtype=torch.float32, device=self._plane_buf.device))
+        return True
 
     def run(self):
         inject_connection_ready(self)
@@ -85,18 +111,22 @@ class FedMLClientManager(ClientManager):
         MLOpsMetrics.get_instance().report_client_training_status(self.client_real_id,
                                                                   MyMessage.MSG_MLOPS_CLIENT_STATUS_TRAINING)
         params = self.resolve_payload(msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS))
+        self.round_idx = int(msg.get(MyMessage.MSG_ARG_KEY_ROUND_INDEX, 0))
+        if self.plane_skip():
+            return
         self.note_global(params)
         self.trainer.update_model(params)
         self.trainer.update_dataset(int(msg.get(MyMessage.MSG_ARG_KEY_CLIENT_INDEX)))
-        self.round_idx = int(msg.get(MyMessage.MSG_ARG_KEY_ROUND_INDEX, 0))
         self.__train()
 
     def handle_message_receive_model_from_server(self, msg):
         params = self.resolve_payload(msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS))
+        self.round_idx = int(msg.get(MyMessage.MSG_ARG_KEY_ROUND_INDEX, self.round_idx + 1))
+        if self.plane_skip():
+            return
         self.note_global(params)
         self.trainer.update_model(params)
         self.trainer.update_dataset(int(msg.get(MyMessage.MSG_ARG_KEY_CLIENT_INDEX)))
-        self.round_idx = int(msg.get(MyMessage.MSG_ARG_KEY_ROUND_INDEX, self.round_idx + 1))
         self.__train()
 
     def handle_finish(self, msg):
@@ -112,7 +142,24 @@ class FedMLClientManager(ClientManager):
     def send_model_to_server(self, receive_id, weights, local_sample_num):
         MLOpsProfilerEvent.get_instance().log_event_started("comm_c2s", event_value=str(self.round_idx))
         m = Message(MyMessage.MSG_TYPE_C2S_SEND_MODEL_TO_SERVER, self.client_real_id, receive_id)
-        if getattr(self, "mailbox", None) is not None:
+        plane_buf = None
+        if self.plane is not None:
+            # RCCL plane: n·w ‖ n goes into the round's reduce right after this marker (the server enters the
+            # reduce once every selected silo's marker is in, so the marker must go first)
+            from ..device_mailbox import marker
+            if torch.is_tensor(weights):
+                flat = weights
+            elif hasattr(self.trainer, "flat_params"):
+                flat = self.trainer.flat_params()
+            else:
+                from ...core.arena import ParamLayout
+                flat = ParamLayout(weights).flatten(weights, device=self._plane_buf.device)
+            n = float(local_sample_num)
+            plane_buf = torch.empty(self._plane_buf.numel() + 1, dtype=torch.float32, device=self._plane_buf.device)
+            torch.mul(flat.reshape(-1).to(plane_buf.device), n, out=plane_buf[:-1])
+            plane_buf[-1:].fill_(n)
+            weights = marker("rccl")
+        elif getattr(self, "mailbox", None) is not None:
             # device plane: the upload goes into this silo's shared slot; the message only points at it
             from ..device_mailbox import marker
             if torch.is_tensor(weights):
@@ -130,6 +177,8 @@ class FedMLClientManager(ClientManager):
         m.add_params(MyMessage.MSG_ARG_KEY_NUM_SAMPLES, local_sample_num)
         m.add_params(MyMessage.MSG_ARG_KEY_ROUND_INDEX, self.round_idx)
         self.send_message(m)
+        if plane_buf is not None:
+            self.plane.reduce(plane_buf)
 
     def send_client_status(self, receive_id, status="ONLINE"):
         m = Message(MyMessage.MSG_TYPE_C2S_CLIENT_STATUS, self.client_real_id, receive_id)

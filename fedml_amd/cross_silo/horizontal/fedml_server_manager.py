@@ -72,6 +72,12 @@ class FedMLServerManager(ServerManager):
             raise ValueError("silo_transport: device needs the GPU (HIP IPC buffers)")
         self.mailbox = None
         self._slot_of = {cid: i for i, cid in enumerate(self.client_real_ids)}
+        # same-node RCCL data plane (cross_silo/fed_plane.py): one broadcast + one reduce per round
+        self.rccl_payload = str(getattr(args, "silo_transport", "") or "").lower() == "rccl"
+        if self.rccl_payload and self.round_timeout is not None:
+            raise ValueError("silo_transport: rccl does not support round_timeout (a missing silo stalls the collective)")
+        self.plane = None
+        self._plane_glob = None
 
     def run(self):
         inject_connection_ready(self)
@@ -152,6 +158,10 @@ class FedMLServerManager(ServerManager):
         ids, silos = self._selection()
         self._selected = ids
         self.aggregator.flag_client_model_uploaded_dict = {i: False for i in range(len(ids))}
+        if self.rccl_payload:
+            self._plane_round(MyMessage.MSG_TYPE_S2C_INIT_CONFIG, g, ids, silos)
+            MLOpsProfilerEvent.get_instance().log_event_started("server.wait", event_value=str(self.round_idx))
+            return
         if self.device_payload:
             from ..device_mailbox import marker
             self._open_mailbox(g)
@@ -161,6 +171,43 @@ class FedMLServerManager(ServerManager):
             self._send(MyMessage.MSG_TYPE_S2C_INIT_CONFIG, cid, payload, silo)
         MLOpsProfilerEvent.get_instance().log_event_started("server.wait", event_value=str(self.round_idx))
         self._arm_deadline()
+
+    # ---- RCCL data plane ------------------------------------------------------------------------
+    def _plane_round(self, mtype, g, ids, silos, final=False):
+        """Markers to EVERY silo (selected ones train on their data silo, the others only join the collectives),
+        then the global model as one broadcast. ``g``: state dict or flat device tensor."""
+        from ..device_mailbox import marker
+        from ..fed_plane import FederationPlane, plane_port
+        dev = torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
+        if self._plane_glob is None:
+            from ...core.arena import ParamLayout
+            layout = ParamLayout(g)
+            self.aggregator.flat_layout = layout
+            self._plane_glob = torch.zeros(layout.size, dtype=torch.float32, device=dev)
+        if torch.is_tensor(g):
+            self._plane_glob.copy_(g.reshape(-1))
+        else:
+            self.aggregator.flat_layout.flatten(g, out=self._plane_glob)
+        P = self._plane_glob.numel()
+        port = plane_port(self.args)
+        silo_of = dict(zip(ids, silos))
+        for cid in self.client_real_ids:
+            mk = marker("rccl", P=P, port=port, train=cid in silo_of and not final)
+            self._send(mtype if cid in silo_of or final else MyMessage.MSG_TYPE_S2C_SYNC_MODEL_TO_CLIENT, cid, mk,
+                       silo_of.get(cid, 0))
+        if self.plane is None:
+            self.plane = FederationPlane(0, len(self.client_real_ids) + 1, port, dev)
+        self.plane.broadcast(self._plane_glob)
+
+    def _plane_aggregate(self):
+        """Σ n·w ‖ Σ n of the round's selected silos (the others add zeros) by one reduce; w = the new global."""
+        acc = torch.zeros(self._plane_glob.numel() + 1, dtype=torch.float32, device=self._plane_glob.device)
+        self.plane.reduce(acc)
+        avg = acc[:-1] / acc[-1:].clamp_min(1e-30)
+        self.aggregator.model_dict.clear()
+        self.aggregator.sample_num_dict.clear()
+        self.aggregator._flat_global = avg
+        return avg
 
     def _global_payload(self, g, cid):
         """Device plane: a 'global' marker that also carries the mailbox descriptor and the receiver's slot, so a
@@ -189,7 +236,9 @@ class FedMLServerManager(ServerManager):
         params = msg.get(MyMessage.MSG_ARG_KEY_MODEL_PARAMS)
         from ..device_mailbox import is_marker
         from ..wan_codec import decode, is_encoded, payload_bytes
-        if is_marker(params):    # same-node device plane: the upload sits in the sender's shared slot
+        if is_marker(params) and params.get("__devmail__") == "rccl":
+            params = None        # RCCL plane: the upload arrives in the round's reduce, the marker only counts it
+        elif is_marker(params):    # same-node device plane: the upload sits in the sender's shared slot
             params, _ = self.mailbox.upload(int(params["slot"]))
         else:
             self.wan_bytes = getattr(self, "wan_bytes", 0) + payload_bytes(params)
@@ -209,7 +258,7 @@ class FedMLServerManager(ServerManager):
         prof = MLOpsProfilerEvent.get_instance()
         prof.log_event_ended("server.wait", event_value=str(self.round_idx))
         prof.log_event_started("aggregate", event_value=str(self.round_idx))
-        g = self.aggregator.aggregate()
+        g = self._plane_aggregate() if self.rccl_payload else self.aggregator.aggregate()
         prof.log_event_ended("aggregate", event_value=str(self.round_idx))
         if torch.is_tensor(g) and g.is_cuda:
             torch.cuda.synchronize(g.device)
@@ -231,6 +280,20 @@ class FedMLServerManager(ServerManager):
             self.mailbox.publish(g if torch.is_tensor(g) else self.aggregator.flat_layout.flatten(
                 g, device=self.mailbox.glob.device))
             g = None
+        if self.rccl_payload:
+            final = self.round_idx == self.round_num
+            ids, silos = ([], []) if final else self._selection()
+            self._selected = ids
+            self.aggregator.flag_client_model_uploaded_dict = {i: False for i in range(len(ids))}
+            self._plane_round(MyMessage.MSG_TYPE_S2C_FINISH if final else MyMessage.MSG_TYPE_S2C_SYNC_MODEL_TO_CLIENT,
+                              g, ids, silos, final=final)
+            if final:
+                MLOpsMetrics.get_instance().report_server_training_status(
+                    getattr(self.args, "run_id", "0"), MyMessage.MSG_MLOPS_SERVER_STATUS_FINISHED)
+                self.finish()
+            else:
+                prof.log_event_started("server.wait", event_value=str(self.round_idx))
+            return
         if self.round_idx == self.round_num:
             # final sync lets clients see the final model; then everyone stops
             for cid in self.client_real_ids:

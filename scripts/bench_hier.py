@@ -57,7 +57,8 @@ def worker(a):
            "n_proc_in_silo": a.procs_per_silo, "proc_rank_in_silo": a.rank_in_silo, "pg_master_port": a.pg_port,
            "silo_local_clients": a.local_clients, "compute_dtype": a.dtype,
            "using_gpu": use_gpu, "gpu_id": a.gpu, "rank_in_node": a.gpu,
-           "wan_compression": a.wan_compression, "silo_transport": a.silo_transport, "random_seed": 0}
+           "wan_compression": a.wan_compression, "silo_transport": a.silo_transport, "random_seed": 0,
+           "fed_plane_port": int(os.environ.get("FEDML_AMD_PLANE_PORT", "0"))}
     args = fedml_amd.init(Arguments.from_dict({"x": cfg}))
     dev, ds, m = fedml_amd._prepare(args)
     from fedml_amd.cross_silo.hierarchical import Client, Server
@@ -86,7 +87,8 @@ def main():
     p.add_argument("--lr", type=float, default=1e-4)
     p.add_argument("--dtype", default="fp32", help="fp32 (the reference's precision) | bf16")
     p.add_argument("--wan-compression", default="", help="'' (fp32 state dicts, the reference) | int8")
-    p.add_argument("--silo-transport", default="", help="'' (network payloads) | device (same-node HBM plane)")
+    p.add_argument("--silo-transport", default="", help="'' (network payloads) | device (same-node HBM plane) | "
+                                                        "rccl (server + silo masters in one communicator)")
     p.add_argument("--server-cpu", action="store_true",
                    help="server process without the GPU (network payloads only): 8 silos x 2 processes then stay "
                         "within 16 GPU processes on a one-GPU box")
@@ -112,6 +114,10 @@ def main():
                OMP_NUM_THREADS="2")
     if a.procs_per_silo > ngpu:
         env["FEDML_AMD_DIST_BACKEND"] = "gloo"
+    if a.silo_transport == "rccl":
+        env["FEDML_AMD_PLANE_PORT"] = str(_free_port())
+        if a.silos + 1 > ngpu:      # RCCL: one GPU per rank of the server + silo-master communicator
+            env["FEDML_AMD_PLANE_BACKEND"] = "gloo"
     base = [sys.executable, os.path.abspath(__file__)] + [x for x in sys.argv[1:]]
     procs = []
     if a.server_cpu and a.silo_transport == "device":
@@ -152,7 +158,9 @@ def main():
             "config": {"model": a.model, "silos": a.silos, "local_clients_per_silo": a.local_clients,
                        "procs_per_silo": a.procs_per_silo, "samples_per_client": a.samples_per_client,
                        "local_batch": a.batch_size,
-                       "wan_payload": ("device mailbox (HIP IPC, same node)" if a.silo_transport == "device"
+                       "wan_payload": ("device mailbox (HIP IPC, same node)" if a.silo_transport == "device" else
+                                       f"{env.get('FEDML_AMD_PLANE_BACKEND', 'RCCL')} broadcast + reduce (server + silo "
+                                       f"masters communicator)" if a.silo_transport == "rccl"
                                        else a.wan_compression or "fp32 state_dict"),
                        "parallelism": f"server + {a.silos} silos x {a.procs_per_silo} procs (TCP control, "
                                       f"{env.get('FEDML_AMD_DIST_BACKEND', 'RCCL')} in-silo)"},

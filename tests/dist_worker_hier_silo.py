@@ -21,7 +21,8 @@ def main(role, silo, rank_in_silo, pg_port, out, n_proc, n_local, device, model=
            "synthetic_samples_per_client": 48, "rank": silo, "n_proc_in_silo": n_proc,
            "proc_rank_in_silo": rank_in_silo, "pg_master_port": pg_port, "silo_local_clients": n_local,
            "shuffle": False, "using_gpu": device == "cuda", "gpu_id": 0,
-           "silo_transport": os.environ.get("FEDML_TEST_SILO_TRANSPORT", "")}
+           "silo_transport": os.environ.get("FEDML_TEST_SILO_TRANSPORT", ""),
+           "fed_plane_port": int(os.environ.get("FEDML_TEST_PLANE_PORT", "0"))}
     args = fedml_amd.init(Arguments.from_dict({"x": cfg}))
     logging.getLogger().setLevel(logging.WARNING)
     dev, ds, m = fedml_amd._prepare(args)

@@ -19,7 +19,7 @@ def main(rank, world, port, out):
     cfg = {"training_type": "simulation", "dataset": "mnist", "model": "lr", "client_num_in_total": 8,
            "client_num_per_round": 5, "comm_round": 3, "epochs": 1, "batch_size": 16, "learning_rate": 0.1,
            "frequency_of_the_test": 0, "backend": "RCCL", "federated_optimizer": "S-FedAvg",
-           "synthetic_samples_per_client": 64, "partition_method": "hetero", "valid_samples": 200,
+           "synthetic_train_samples_per_client": 64, "partition_method": "hetero", "valid_samples": 200,
            "shuffle": True, "random_seed": 0}
     a = fedml_amd.init(Arguments.from_dict({"x": cfg}))
     logging.getLogger().setLevel(logging.WARNING)

@@ -23,7 +23,7 @@ def _setup(opt, **kw):
     cfg = {"training_type": "simulation", "dataset": "mnist", "model": "lr", "client_num_in_total": 8,
            "client_num_per_round": 4, "comm_round": 3, "epochs": 1, "batch_size": 16, "learning_rate": 0.1,
            "frequency_of_the_test": 0, "backend": "single_process", "federated_optimizer": opt,
-           "synthetic_samples_per_client": 64, "partition_method": "hetero", "valid_samples": 200,
+           "synthetic_train_samples_per_client": 64, "partition_method": "hetero", "valid_samples": 200,
            "shuffle": False, "random_seed": 0}
     cfg.update(kw)
     a = fedml_amd.init(Arguments.from_dict({"x": cfg}))
@@ -58,7 +58,7 @@ def _rccl(opt, **kw):
 
 @pytest.mark.parametrize("opt,kw", [("S-FedAvg", {}), ("S-FedAvg", {"sv_approaching": True}),
                                     ("HS-FedAvg", {"dataset": "cifar10", "model": "lr",
-                                                   "synthetic_samples_per_client": 24, "valid_samples": 64})])
+                                                   "synthetic_train_samples_per_client": 24, "valid_samples": 64})])
 def test_valued_rccl_reproduces_sp(opt, kw):
     sp, sampled, w_sp = _sp(opt, **kw)
     rc, w_rc = _rccl(opt, **kw)
