@@ -35,6 +35,8 @@ class BatchedModelEvaluator:
         self.compute_dtype = compute_dtype
         self._interps = {}
         self._batched_ok = True
+        self._native = {}            # chunk size → NativeResNetStep used for inference (GPU, CIFAR ResNets)
+        self._native_ok = self.device.type == "cuda"
 
     def flatten(self, state_dict) -> torch.Tensor:
         return self.layout.flatten(state_dict, device=self.device)
@@ -63,8 +65,34 @@ class BatchedModelEvaluator:
         res["total"] = torch.full((S,), float(total), dtype=torch.float64)
         return res
 
+    def _native_step(self, c):
+        """The native HIP ResNet forward for ``c`` models at once (``NativeResNetStep.forward_eval``: the training
+        kernels with BatchNorm folded from each model's running statistics), or None for other models."""
+        if not self._native_ok:
+            return None
+        st = self._native.get(c)
+        if st is None:
+            from ..parallel.native_resnet import NativeResNetStep, UnsupportedNative
+            try:
+                st = NativeResNetStep(self.model, self.layout, c, self.device,
+                                      dtype=self.compute_dtype or torch.float32)
+            except UnsupportedNative as e:
+                logging.info("coalition evaluation: no native inference (%s)", e)
+                self._native_ok = False
+                return None
+            self._native[c] = st
+        return st
+
     def _run_chunk(self, chunk, batches):
         c = chunk.shape[0]
+        cm = max(c, self.max_models)
+        st = self._native_step(cm)
+        if st is not None:
+            # one native step (one set of buffers) for every chunk: a short last chunk is padded with copies of
+            # its first model, whose outputs are dropped
+            arena = chunk if c == cm else torch.cat([chunk, chunk[:1].expand(cm - c, -1)])
+            arena = arena.contiguous()
+            return [st.forward_eval(arena, x.unsqueeze(0).expand(cm, *x.shape))[:c].float() for x, _ in batches]
         if self._batched_ok:
             try:
                 interp = self._interp(c)

@@ -62,6 +62,32 @@ FA_EXPORT int fa_bn_fwd_finalize(const float* stats, int C, int Ch, float n, flo
   return (int)hipGetLastError();
 }
 
+// ---- inference folding (eval mode: the running statistics, no batch statistics): scale = γ·rsqrt(rv + ε),
+// shift = β − rm·scale per (client, channel) — the vectors every consumer kernel's BN prologue / block-output pass
+// reads. Used by the native batched inference of many models at once (coalition valuation, core/valuation.py).
+__global__ void bn_eval_fold_kernel(int Ch, const float* __restrict__ arena, int64_t ldw, int64_t off_gamma,
+                                    int64_t off_beta, int64_t off_rm, int64_t off_rv, float eps,
+                                    float* __restrict__ scale, float* __restrict__ shift) {
+  const int c = blockIdx.y;
+  const int ch = blockIdx.x * blockDim.x + threadIdx.x;
+  if (ch >= Ch) return;
+  const float* pa = arena + (int64_t)c * ldw;
+  const float g = off_gamma >= 0 ? pa[off_gamma + ch] : 1.f;
+  const float b = off_beta >= 0 ? pa[off_beta + ch] : 0.f;
+  const float s = g * rsqrtf(pa[off_rv + ch] + eps);
+  scale[(int64_t)c * Ch + ch] = s;
+  shift[(int64_t)c * Ch + ch] = b - pa[off_rm + ch] * s;
+}
+
+FA_EXPORT int fa_bn_eval_fold(int C, int Ch, const float* arena, int64_t ldw, int64_t off_gamma, int64_t off_beta,
+                              int64_t off_rm, int64_t off_rv, float eps, float* scale, float* shift,
+                              hipStream_t stream) {
+  if (off_rm < 0 || off_rv < 0) return -3;
+  hipLaunchKernelGGL(bn_eval_fold_kernel, dim3((Ch + 63) / 64, C), dim3(64), 0, stream, Ch, arena, ldw, off_gamma,
+                     off_beta, off_rm, off_rv, eps, scale, shift);
+  return (int)hipGetLastError();
+}
+
 // ---- backward finalisation: (Σg, Σg·y) → dγ, dβ into the gradient arena and the folded
 // coefficients of dy = α·g + β·y + γc consumed by the conv backward kernels.
 __global__ void bn_bwd_finalize_kernel(const float* __restrict__ bstats, int NS, int q_gy, int Ch, float n,

@@ -296,6 +296,13 @@ def bn_fwd_finalize(stats, C, Ch, n, arena, off_gamma, off_beta, off_rm, off_rv,
     _check(rc, "fa_bn_fwd_finalize")
 
 
+def bn_eval_fold(C, Ch, arena, off_gamma, off_beta, off_rm, off_rv, eps, scale, shift):
+    """Inference BatchNorm as the per-(client, channel) scale / shift of the consumer kernels (running stats)."""
+    rc = _fn("fa_bn_eval_fold")(_i(C), _i(Ch), _p(arena), _i64(arena.stride(0)), _i64(off_gamma), _i64(off_beta),
+                                _i64(off_rm), _i64(off_rv), _f(eps), _p(scale), _p(shift), _stream(arena))
+    _check(rc, "fa_bn_eval_fold")
+
+
 def bn_bwd_finalize(bstats, NS, q_gy, C, Ch, n, mean, rstd, arena, garena, off_gamma, off_beta, alpha, beta_c,
                     gamma_c, nimg=None, hw=0):
     rc = _fn("fa_bn_bwd_finalize")(_p(bstats), _i(NS), _i(q_gy), _i(C), _i(Ch), _f(n), _p(mean), _p(rstd),

@@ -525,6 +525,9 @@ class NativeResNetStep:
         v = self.bn_vec[bn.key]
         fst = self.stat_views[bn.key][0]
         g, b, rm, rv, nbt = self._bn_offsets(bn)
+        if not getattr(self, "_training", True):      # inference: running statistics, folded at once
+            nn_ops.bn_eval_fold(self.C, bn.ch, arena, g, b, rm, rv, bn.eps, v[0], v[1])
+            return
 
         def explicit():
             if self.det is not None:
@@ -657,13 +660,7 @@ class NativeResNetStep:
         the padding rows never enter a statistic or a gradient (their ``row_scale`` must be 0)."""
         C, N = x.shape[0], x.shape[1]
         self._nimg = nimg
-        H, W = x.shape[3], x.shape[4]
-        if self.geom != (N, H, W):
-            if (N, H, W) in self._states:
-                self._restore(self._states[(N, H, W)])
-            else:
-                self._setup(N, H, W)
-                self._states[(N, H, W)] = self._snapshot()
+        self._geometry(N, x.shape[3], x.shape[4])
         if self.det is not None:
             self.det.register(garena)
         self.stats.zero_()
@@ -671,75 +668,10 @@ class NativeResNetStep:
         nn_ops._set_lazy((0, 0))        # no descriptor left over from an aborted launch
         if self._lazy_on():
             self._lz_prepare(arena, garena, active, N)
-        nn_ops.pack_weights(arena, self._segs, self._nseg, self.packed, self.packed_ld, C, self._pack_tiles,
-                            self._pack_taps)
         st_conv, st_bn = self.stem
-        nn_ops.nchw_to_nhwc_pad(x.contiguous(), self.x_in, C * N, st_conv.cin, H * W, st_conv.cin_pad)
-
-        # ---------------- forward ----------------
-        self._fwd(st_conv, self.x_in, self.stem_y, None, st_bn, N)
-        self._bn_fwd(st_bn, N, st_conv.Ho * st_conv.Wo, arena, active)
-        v0 = self.bn_vec[st_bn.key]
-        self._flush(st_bn.key, "f")          # block_out reads the finalised rows
-        nn_ops.block_out(self.stem_y, v0[0], v0[1], None, None, None, self.stem_out, C,
-                         N * st_conv.Ho * st_conv.Wo * st_conv.cout, st_conv.cout, nimg=self._nimg,
-                         per_img=st_conv.Ho * st_conv.Wo * st_conv.cout)
-        act_in = self.stem_out
-        pend = None    # (yp, s, t, res, rs, rt, bout) of a block output formed by the next block's first conv
-        pend_keys = (None, None)   # its BNs (deferred finalisation: taken by that conv)
-        for bi, b in enumerate(self.blocks):
-            b.act_in = act_in
-            for j, (cv, bn) in enumerate(zip(b.convs, b.bns)):
-                src = act_in if j == 0 else b.ys[j - 1]
-                pro = None if j == 0 else self.bn_vec[b.bns[j - 1].key]
-                if j == 0 and pend is not None:
-                    lz = (self._take(pend_keys[0], "f"), self._take(pend_keys[1], "f"))
-                    nn_ops.conv_fwd_pbout(*pend, self.packed.view(-1)[cv.off_f:], self.packed_ld, b.ys[0],
-                                          self.stat_views[bn.key][0], C, N, cv.H, cv.W, cv.cin_pad, cv.cout, cv.ldk,
-                                          self._tiles_per_wave(N * cv.Ho * cv.Wo), pivot=self.bn_vec[bn.key][7],
-                                          nimg=self._nimg, lazy=lz)
-                    pend = None
-                else:
-                    self._fwd(cv, src, b.ys[j], pro, bn, N, pro_key=None if j == 0 else b.bns[j - 1].key)
-                if b.ys[j] is None:     # recomputed-y conv: keep the pivot its later passes must subtract
-                    self.bn_vec[bn.key][8].copy_(self.bn_vec[bn.key][7])
-                self._bn_fwd(bn, N, cv.Ho * cv.Wo, arena, active)
-            last, lbn = b.convs[-1], b.bns[-1]
-            vl = self.bn_vec[lbn.key]
-            if b.ds_conv is not None:
-                d = b.ds_conv
-                self._fwd(d, act_in, b.yd, None, b.ds_bn, N)
-                self._bn_fwd(b.ds_bn, N, d.Ho * d.Wo, arena, active)
-            if self._pbout_ok(b, self.blocks[bi + 1] if bi + 1 < len(self.blocks) else None):
-                vd = self.bn_vec[b.ds_bn.key] if b.ds_conv is not None else (None, None)
-                pend = (b.ys[-1], vl[0], vl[1], b.yd if b.ds_conv is not None else act_in, vd[0], vd[1], b.out)
-                pend_keys = (lbn.key, b.ds_bn.key if b.ds_conv is not None else None)
-            elif b.ry:    # block output from a second pass of the last conv (its output y3 is never stored)
-                for k in (b.bns[-2].key, lbn.key, b.ds_bn.key if b.ds_conv is not None else None):
-                    self._flush(k, "f")
-                pv = self.bn_vec[b.bns[-2].key]
-                res, rs, rt = (b.yd, self.bn_vec[b.ds_bn.key][0], self.bn_vec[b.ds_bn.key][1]) \
-                    if b.ds_conv is not None else (act_in, None, None)
-                nn_ops.conv_fwd_bout(b.ys[-2], self.packed.view(-1)[last.off_f:], self.packed_ld, pv[0], pv[1], b.out,
-                                     vl[0], vl[1], vl[8], res, rs, rt, C, N, last.H, last.W, last.cin_pad, last.cout,
-                                     last.ldk, self._tiles_per_wave(N * last.Ho * last.Wo), nimg=self._nimg)
-            elif b.ds_conv is not None:
-                vd = self.bn_vec[b.ds_bn.key]
-                self._flush(lbn.key, "f")
-                self._flush(b.ds_bn.key, "f")
-                nn_ops.block_out(b.ys[-1], vl[0], vl[1], b.yd, vd[0], vd[1], b.out, C,
-                                 N * last.Ho * last.Wo * last.cout, last.cout, nimg=self._nimg,
-                                 per_img=last.Ho * last.Wo * last.cout)
-            else:
-                self._flush(lbn.key, "f")
-                nn_ops.block_out(b.ys[-1], vl[0], vl[1], act_in, None, None, b.out, C,
-                                 N * last.Ho * last.Wo * last.cout, last.cout, nimg=self._nimg,
-                                 per_img=last.Ho * last.Wo * last.cout)
-            act_in = b.out
-        self._flush_all()       # every forward BN has been folded (by its consumer or explicitly)
+        act_in = self._forward(arena, x, active, N, training=True)
         fh, fw = self.final_hw
         chl = self.blocks[-1].convs[-1].cout
-        nn_ops.avgpool(act_in, self.pooled, C * N, fh * fw, chl, nimg=self._nimg, N=N)
         # ---------------- head: fc + fused CE (fp32, tiny) ----------------
         ow = self.off["fc.weight"]
         ob = self.off["fc.bias"]
@@ -912,3 +844,113 @@ class NativeResNetStep:
         if self.det is not None:
             self.det.flush(garena)
         return loss.detach()
+
+    def _geometry(self, N, H, W):
+        if self.geom != (N, H, W):
+            if (N, H, W) in self._states:
+                self._restore(self._states[(N, H, W)])
+            else:
+                self._setup(N, H, W)
+                self._states[(N, H, W)] = self._snapshot()
+
+    @torch.no_grad()
+    def forward_eval(self, arena, x):
+        """Inference of C models at once: x [C, N, Cin, H, W] fp32 (each model's own batch; the same images
+        expanded for a model sweep) → logits [C, N, classes] fp32. BatchNorm in eval mode (running statistics of
+        each model's arena row, ``bn_eval_fold``), same kernels as the training forward. Zeroes this object's
+        pivots (stored outputs are then uncentred): give inference its own ``NativeResNetStep``."""
+        C, N = x.shape[0], x.shape[1]
+        if C != self.C:
+            raise ValueError(f"forward_eval: {C} models for a step built for {self.C}")
+        self._nimg = None
+        self._geometry(N, x.shape[3], x.shape[4])
+        if not getattr(self, "_eval_ready", False) or self._eval_geom != self.geom:
+            for v in self.bn_vec.values():
+                v[7:9].zero_()
+            self._eval_ready, self._eval_geom = True, self.geom
+        self._pending.clear()
+        self.stats.zero_()           # the forward kernels still accumulate (unused) batch statistics
+        nn_ops._set_lazy((0, 0))
+        self._forward(arena, x, None, N, training=False)
+        ow, ob = self.off["fc.weight"], self.off["fc.bias"]
+        Wfc = arena[:, ow:ow + self.fc_out * self.fc_in].view(C, self.fc_out, self.fc_in)
+        bfc = arena[:, ob:ob + self.fc_out]
+        return torch.baddbmm(bfc.unsqueeze(1), self.pooled, Wfc.transpose(1, 2))
+
+    def _forward(self, arena, x, active, N, training=True):
+        """Forward of every conv / BN / block output into this geometry's buffers; pooled features in
+        ``self.pooled``. Returns the last block's output. ``training=False``: BatchNorm from the running
+        statistics (no batch statistics are used or updated)."""
+        C = self.C
+        H, W = x.shape[3], x.shape[4]
+        self._training = training
+        nn_ops.pack_weights(arena, self._segs, self._nseg, self.packed, self.packed_ld, C, self._pack_tiles,
+                            self._pack_taps)
+        st_conv, st_bn = self.stem
+        nn_ops.nchw_to_nhwc_pad(x.contiguous(), self.x_in, C * N, st_conv.cin, H * W, st_conv.cin_pad)
+
+        # ---------------- forward ----------------
+        self._fwd(st_conv, self.x_in, self.stem_y, None, st_bn, N)
+        self._bn_fwd(st_bn, N, st_conv.Ho * st_conv.Wo, arena, active)
+        v0 = self.bn_vec[st_bn.key]
+        self._flush(st_bn.key, "f")          # block_out reads the finalised rows
+        nn_ops.block_out(self.stem_y, v0[0], v0[1], None, None, None, self.stem_out, C,
+                         N * st_conv.Ho * st_conv.Wo * st_conv.cout, st_conv.cout, nimg=self._nimg,
+                         per_img=st_conv.Ho * st_conv.Wo * st_conv.cout)
+        act_in = self.stem_out
+        pend = None    # (yp, s, t, res, rs, rt, bout) of a block output formed by the next block's first conv
+        pend_keys = (None, None)   # its BNs (deferred finalisation: taken by that conv)
+        for bi, b in enumerate(self.blocks):
+            b.act_in = act_in
+            for j, (cv, bn) in enumerate(zip(b.convs, b.bns)):
+                src = act_in if j == 0 else b.ys[j - 1]
+                pro = None if j == 0 else self.bn_vec[b.bns[j - 1].key]
+                if j == 0 and pend is not None:
+                    lz = (self._take(pend_keys[0], "f"), self._take(pend_keys[1], "f"))
+                    nn_ops.conv_fwd_pbout(*pend, self.packed.view(-1)[cv.off_f:], self.packed_ld, b.ys[0],
+                                          self.stat_views[bn.key][0], C, N, cv.H, cv.W, cv.cin_pad, cv.cout, cv.ldk,
+                                          self._tiles_per_wave(N * cv.Ho * cv.Wo), pivot=self.bn_vec[bn.key][7],
+                                          nimg=self._nimg, lazy=lz)
+                    pend = None
+                else:
+                    self._fwd(cv, src, b.ys[j], pro, bn, N, pro_key=None if j == 0 else b.bns[j - 1].key)
+                if b.ys[j] is None:     # recomputed-y conv: keep the pivot its later passes must subtract
+                    self.bn_vec[bn.key][8].copy_(self.bn_vec[bn.key][7])
+                self._bn_fwd(bn, N, cv.Ho * cv.Wo, arena, active)
+            last, lbn = b.convs[-1], b.bns[-1]
+            vl = self.bn_vec[lbn.key]
+            if b.ds_conv is not None:
+                d = b.ds_conv
+                self._fwd(d, act_in, b.yd, None, b.ds_bn, N)
+                self._bn_fwd(b.ds_bn, N, d.Ho * d.Wo, arena, active)
+            if self._pbout_ok(b, self.blocks[bi + 1] if bi + 1 < len(self.blocks) else None):
+                vd = self.bn_vec[b.ds_bn.key] if b.ds_conv is not None else (None, None)
+                pend = (b.ys[-1], vl[0], vl[1], b.yd if b.ds_conv is not None else act_in, vd[0], vd[1], b.out)
+                pend_keys = (lbn.key, b.ds_bn.key if b.ds_conv is not None else None)
+            elif b.ry:    # block output from a second pass of the last conv (its output y3 is never stored)
+                for k in (b.bns[-2].key, lbn.key, b.ds_bn.key if b.ds_conv is not None else None):
+                    self._flush(k, "f")
+                pv = self.bn_vec[b.bns[-2].key]
+                res, rs, rt = (b.yd, self.bn_vec[b.ds_bn.key][0], self.bn_vec[b.ds_bn.key][1]) \
+                    if b.ds_conv is not None else (act_in, None, None)
+                nn_ops.conv_fwd_bout(b.ys[-2], self.packed.view(-1)[last.off_f:], self.packed_ld, pv[0], pv[1], b.out,
+                                     vl[0], vl[1], vl[8], res, rs, rt, C, N, last.H, last.W, last.cin_pad, last.cout,
+                                     last.ldk, self._tiles_per_wave(N * last.Ho * last.Wo), nimg=self._nimg)
+            elif b.ds_conv is not None:
+                vd = self.bn_vec[b.ds_bn.key]
+                self._flush(lbn.key, "f")
+                self._flush(b.ds_bn.key, "f")
+                nn_ops.block_out(b.ys[-1], vl[0], vl[1], b.yd, vd[0], vd[1], b.out, C,
+                                 N * last.Ho * last.Wo * last.cout, last.cout, nimg=self._nimg,
+                                 per_img=last.Ho * last.Wo * last.cout)
+            else:
+                self._flush(lbn.key, "f")
+                nn_ops.block_out(b.ys[-1], vl[0], vl[1], act_in, None, None, b.out, C,
+                                 N * last.Ho * last.Wo * last.cout, last.cout, nimg=self._nimg,
+                                 per_img=last.Ho * last.Wo * last.cout)
+            act_in = b.out
+        self._flush_all()       # every forward BN has been folded (by its consumer or explicitly)
+        fh, fw = self.final_hw
+        chl = self.blocks[-1].convs[-1].cout
+        nn_ops.avgpool(act_in, self.pooled, C * N, fh * fw, chl, nimg=self._nimg, N=N)
+        return act_in

@@ -255,6 +255,17 @@ class ClientBatchEngine:
         self.aug_cutout = int(getattr(args, "cutout_length", 16))
         self._aug_calls = 0
 
+    @property
+    def executor(self) -> str:
+        """Which executor trains the clients: native (HIP ResNet step) | transformer | lstm (client-batched
+        kernels) | batched (client-batched interpreter) | sequential (one client after another)."""
+        if self.native_step is not None:
+            return "native"
+        if self.tf is not None:
+            from ...parallel.batched_rnn import BatchedRNN
+            return "lstm" if isinstance(self.tf, BatchedRNN) else "transformer"
+        return "sequential" if self.sequential else "batched"
+
     # ------------------------------------------------------------------------------------------
     def _build_views(self):
         self.views = {}

@@ -61,7 +61,7 @@ def _run(graphs: bool, lazy: bool, det: bool = False, momentum: float = 0.9):
 def test_graphs_lazy_bn_multi_round_match_eager_explicit():
     ref, ng0, _ = _run(graphs=False, lazy=False)
     got, ng, (ncache, npinned) = _run(graphs=True, lazy=True)
-    assert ng0 == 0 and ng >= 4            # first/later step × full/ragged geometries were captured
+    assert ng0 == 0 and ng >= 3            # first/later step of the full geometry + the ragged tail, captured
     assert npinned >= 2 and ncache >= npinned
     assert torch.isfinite(got).all()
     rel = float((got - ref).norm() / ref.norm())

@@ -48,3 +48,38 @@ def test_s_fedavg_native_engine_tracks_sp_resnet56():
             num += float((w_rc[key].float().cpu() - v.float().cpu()).norm() ** 2)
             den += float(v.float().norm() ** 2)
     assert (num / den) ** 0.5 < 2e-2, (num / den) ** 0.5
+
+
+@pytest.mark.parametrize("depth", [56, 18])
+def test_native_forward_eval_matches_torch_eval(depth):
+    """``NativeResNetStep.forward_eval``: C models' logits in one native forward (BatchNorm from each model's running
+    statistics) against each model's own torch fp32 eval-mode forward."""
+    import copy as _copy
+    from fedml_amd.core.arena import ParamLayout
+    from fedml_amd.models.cv.resnet import ResNet18Cifar, resnet56
+    from fedml_amd.parallel.native_resnet import NativeResNetStep
+    torch.manual_seed(0)
+    base = resnet56(100) if depth == 56 else ResNet18Cifar(10)
+    layout = ParamLayout.from_module(base)
+    models = []
+    for i in range(3):
+        m = _copy.deepcopy(base)
+        with torch.no_grad():
+            for name, b in m.named_buffers():
+                if "running_mean" in name:
+                    b.normal_(0, 0.1)
+                elif "running_var" in name:
+                    b.uniform_(0.5, 2.0)
+            for p in m.parameters():
+                p.add_(torch.randn_like(p) * 0.01)
+        models.append(m.cuda().eval())
+    arena = torch.stack([layout.flatten(m.state_dict(), device="cuda") for m in models])
+    x = torch.randn(3, 20, 3, 32, 32, device="cuda")
+    st = NativeResNetStep(base, layout, 3, "cuda")
+    got = st.forward_eval(arena, x)
+    torch.backends.cudnn.allow_tf32 = False
+    for i, m in enumerate(models):
+        with torch.no_grad():
+            ref = m(x[i])
+        err = float((got[i] - ref).norm() / ref.norm())
+        assert err < 1e-4, (i, err)
