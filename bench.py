@@ -62,6 +62,10 @@ def parse():
         # reference BENCHMARK_MPI.md:104: MobileNet / CIFAR-10, 10 clients, bs 64, SGD lr 0.001, wd 0.001
         "mobilenet_cifar10_10": dict(model="mobilenet", dataset="cifar10", clients=10, samples_per_client=5000,
                                      batch_size=64, lr=0.001),
+        # reference BENCHMARK_MPI.md:51: ResNet-18 + GroupNorm / fed_CIFAR-100 (24x24 crops), 10 clients per round of
+        # 100 samples, bs 20, SGD lr 0.1 (native GroupNorm step: parallel/native_resnet_gn.py)
+        "resnet18_gn_fed_cifar100_10": dict(model="resnet18_gn", dataset="fed_cifar100", clients=10,
+                                            samples_per_client=100, batch_size=20, lr=0.1),
         # reference BENCHMARK_MPI.md:52: RNN_OriginalFedAvg / Shakespeare (LEAF), 10 clients per round, bs 4
         "rnn_shakespeare_10": dict(model="rnn", dataset="shakespeare", clients=10, samples_per_client=2000,
                                    batch_size=4, lr=1.47),

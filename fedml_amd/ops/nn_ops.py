@@ -357,3 +357,39 @@ def fc_head_xent(pooled, arena, ow, ob, labels, row_scale, garena, dpool, loss_c
         return False
     _check(rc, "fa_fc_head_xent_f32")
     return True
+
+
+# ---- NHWC GroupNorm / max-pool of the native ResNet-GN step (csrc/gnh_kernels.hip) ----
+def gnh_fwd(x, res, out, ms, arena, off_g, off_b, C, N, HW, Ch, G, eps, relu, nimg=None):
+    """out = act(GN(x)·γ + β [+ res]) per (client, image); mean / rstd per group into ``ms`` [C, N, G, 2]."""
+    rc = _fn("fa_gnh_fwd")(_i(x.dtype == torch.bfloat16), _p(x), _p(res), _p(out), _p(ms), _p(arena),
+                           _i64(arena.stride(0)), _i64(off_g), _i64(off_b), _p(nimg), _i(C), _i(N), _i(HW), _i(Ch),
+                           _i(G), _f(eps), _i(int(relu)), _stream(x))
+    _check(rc, "fa_gnh_fwd")
+
+
+def gnh_bwd(x, go, act, dx, ms, pscr, arena, off_g, C, N, HW, Ch, G, nimg=None):
+    """dx of a GroupNorm (upstream ``go`` masked by ``act > 0`` when ``act`` is given); per-image dγ / dβ partials
+    into ``pscr`` [C, N, 2, Ch] (added into the gradient arena by ``gnh_param_reduce``)."""
+    rc = _fn("fa_gnh_bwd")(_i(x.dtype == torch.bfloat16), _p(x), _p(go), _p(act), _p(dx), _p(ms), _p(pscr),
+                           _p(arena), _i64(arena.stride(0)), _i64(off_g), _p(nimg), _i(C), _i(N), _i(HW), _i(Ch),
+                           _i(G), _stream(x))
+    _check(rc, "fa_gnh_bwd")
+
+
+def gnh_param_reduce(pscr, garena, off_g, off_b, C, N, Ch, nimg=None):
+    rc = _fn("fa_gnh_param_reduce")(_p(pscr), _p(garena), _i64(garena.stride(0)), _i64(off_g), _i64(off_b), _i(C),
+                                    _i(N), _i(Ch), _p(nimg), _stream(garena))
+    _check(rc, "fa_gnh_param_reduce")
+
+
+def maxpool_fwd(x, y, idx, C, N, H, W, Ch, Ho, Wo, k, s, p, nimg=None):
+    rc = _fn("fa_maxpool_fwd")(_i(x.dtype == torch.bfloat16), _p(x), _p(y), _p(idx), _i(C), _i(N), _i(H), _i(W),
+                               _i(Ch), _i(Ho), _i(Wo), _i(k), _i(s), _i(p), _p(nimg), _stream(x))
+    _check(rc, "fa_maxpool_fwd")
+
+
+def maxpool_bwd(gy, idx, gx, C, N, H, W, Ch, Ho, Wo, k, s, p, nimg=None):
+    rc = _fn("fa_maxpool_bwd")(_i(gy.dtype == torch.bfloat16), _p(gy), _p(idx), _p(gx), _i(C), _i(N), _i(H), _i(W),
+                               _i(Ch), _i(Ho), _i(Wo), _i(k), _i(s), _i(p), _p(nimg), _stream(gy))
+    _check(rc, "fa_maxpool_bwd")

@@ -226,7 +226,17 @@ class ClientBatchEngine:
                 logging.info("virtual-client engine: native HIP ResNet path (C=%d, %s)", self.C,
                              self.native_step.dtype)
             except UnsupportedNative as e:
-                logging.info("virtual-client engine: torch batched path (%s)", e)
+                # GroupNorm ResNets (ResNet-18/34-GN): explicit NHWC GroupNorm passes between the same native convs
+                from ...parallel.native_resnet_gn import NativeGNResNetStep
+                try:
+                    self.native_step = NativeGNResNetStep(model, self.layout, self.C, self.device,
+                                                          dtype=self.compute_dtype or torch.float32)
+                    if self.deterministic:
+                        self.native_step.enable_deterministic()
+                    logging.info("virtual-client engine: native HIP ResNet-GN path (C=%d, %s)", self.C,
+                                 self.native_step.dtype)
+                except UnsupportedNative as e2:
+                    logging.info("virtual-client engine: torch batched path (%s; %s)", e, e2)
         # Client-stacked grouped convolutions only pay while each client's conv is too small to fill
         # the GPU on its own (ResNet-56: 16-64 channels). Wide conv nets (ResNet-18: 64-512 channels)
         # run faster as one full-width library conv per client than as one C-group grouped conv.

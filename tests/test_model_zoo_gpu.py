@@ -25,7 +25,7 @@ pytestmark = pytest.mark.gpu
 # family, dataset, executor the engine must pick
 CASES = [("lr", "mnist", "batched"), ("cnn", "femnist", "batched"), ("cnn_original", "femnist", "batched"),
          ("rnn", "shakespeare", "lstm"), ("mobilenet", "cifar10", "batched"), ("mobilenet_v3", "cifar10", "batched"),
-         ("vgg11", "cifar10", "sequential"), ("resnet18_gn", "fed_cifar100", "sequential"),
+         ("vgg11", "cifar10", "sequential"), ("resnet18_gn", "fed_cifar100", "native"),
          ("resnet110", "cifar10", "native"), ("efficientnet", "cifar10", "batched"),
          ("distilbert", "sst2", "transformer")]
 COUNTS = [16, 16, 16]
