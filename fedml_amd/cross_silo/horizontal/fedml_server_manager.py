@@ -178,7 +178,8 @@ class FedMLServerManager(ServerManager):
         then the global model as one broadcast. ``g``: state dict or flat device tensor."""
         from ..device_mailbox import marker
         from ..fed_plane import FederationPlane, plane_port
-        dev = torch.device("cuda") if torch.cuda.is_available() else torch.device("cpu")
+        use_gpu = torch.cuda.is_available() and bool(getattr(self.args, "using_gpu", True))
+        dev = torch.device("cuda") if use_gpu else torch.device("cpu")   # same device kind as the silo masters
         if self._plane_glob is None:
             from ...core.arena import ParamLayout
             layout = ParamLayout(g)

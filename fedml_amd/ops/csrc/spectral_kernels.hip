@@ -157,38 +157,102 @@ __global__ __launch_bounds__(256) void spec_mix_ifft2_kernel(const float2* __res
 
 // ---------------------------------------------------------------------------------------------------------------
 // Power-of-two planes up to 512 × 512 (HS-FedAvg's 3 × 512 × 512 amplitude, hs_fedavg/fedavg_api.py:135): a
-// radix-2 Stockham FFT in LDS, applied separably — a row pass (whole rows in LDS, several per workgroup) and a
+// radix-8 Stockham FFT in LDS (in-register 8-point butterflies), applied separably — a row pass (whole rows in LDS, several per workgroup) and a
 // column pass (a 16-column × H tile in LDS, padded leading dimension against bank conflicts, coalesced 128-B row
 // segments on both sides). Forward: rows (real in) → columns (F out, |F| fused). Inverse with the band mix:
 // columns (mix applied while loading F) → rows (real part × 1/HW out). O(HW·log HW) per plane instead of the
 // DFT's O(HW·(H+W)).
 constexpr int kMaxN = 512;
 
-__device__ __forceinline__ void twiddles_half(float2* tw, int n, float sign) {   // tw[k] = e^{sign·2πi·k/n}, k < n/2
-  for (int k = threadIdx.x; k < (n >> 1); k += blockDim.x) {
+// tw[k] = e^{sign·2πi·k/n}, k < n (double-precision table, as accurate as rocFFT's fp32 plan)
+__device__ __forceinline__ void twiddles_full(float2* tw, int n, float sign) {
+  for (int k = threadIdx.x; k < n; k += blockDim.x) {
     double sn, cs;
     sincospi(2.0 * k / n, &sn, &cs);
     tw[k] = make_float2((float)cs, (float)(sign * sn));
   }
 }
 
-// nfft independent length-N (= 2^lg) transforms at x + f·ld; y is scratch of the same shape. Stockham autosort:
-// no bit reversal, the result (natural order) is in the returned buffer. Every stage ends with a barrier.
-__device__ float2* stockham(float2* x, float2* y, const float2* tw, int lg, int nfft, int ld) {
-  const int half = 1 << (lg - 1);
-  for (int ls = 0; ls < lg; ++ls) {                 // s = 2^ls, current length n = N / s, m = n / 2
-    const int s = 1 << ls, m = half >> ls;
-    for (int i = threadIdx.x; i < nfft * half; i += blockDim.x) {
-      const int f = i >> (lg - 1);
-      const int r = i & (half - 1);                 // r = p·s + q
-      const int p = r >> ls, q = r & (s - 1);
-      const float2* xf = x + f * ld;
-      float2* yf = y + f * ld;
-      const float2 a0 = xf[q + s * p], a1 = xf[q + s * (p + m)];
-      const float2 w = tw[p * s];
-      const float dx = a0.x - a1.x, dy = a0.y - a1.y;
-      yf[q + 2 * s * p] = make_float2(a0.x + a1.x, a0.y + a1.y);
-      yf[q + 2 * s * p + s] = make_float2(dx * w.x - dy * w.y, dx * w.y + dy * w.x);
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 w) {
+  return make_float2(a.x * w.x - a.y * w.y, a.x * w.y + a.y * w.x);
+}
+// a · e^{sign·iπ/2}
+__device__ __forceinline__ float2 cmul_i(float2 a, float sign) { return make_float2(-sign * a.y, sign * a.x); }
+
+// In-register DFT of R ∈ {2, 4, 8} points: a[k] ← Σ_j a[j]·e^{sign·2πi·jk/R} (decimation in frequency)
+template <int R>
+__device__ __forceinline__ void dft_small(float2 (&a)[R], float sign) {
+  if (R == 2) {
+    const float2 t = a[0];
+    a[0] = cadd(t, a[1]);
+    a[1] = csub(t, a[1]);
+  } else if (R == 4) {
+    const float2 d0 = cadd(a[0], a[2]), d2 = csub(a[0], a[2]);
+    const float2 d1 = cadd(a[1], a[3]), d3 = cmul_i(csub(a[1], a[3]), sign);
+    a[0] = cadd(d0, d1);
+    a[2] = csub(d0, d1);
+    a[1] = cadd(d2, d3);
+    a[3] = csub(d2, d3);
+  } else {
+    const float h = 0.70710678118654752f;
+    float2 e[4] = {cadd(a[0], a[4]), cadd(a[1], a[5]), cadd(a[2], a[6]), cadd(a[3], a[7])};
+    float2 o[4] = {csub(a[0], a[4]), cmul(csub(a[1], a[5]), make_float2(h, sign * h)),
+                   cmul_i(csub(a[2], a[6]), sign), cmul(csub(a[3], a[7]), make_float2(-h, sign * h))};
+    dft_small<4>(e, sign);
+    dft_small<4>(o, sign);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      a[2 * k] = e[k];
+      a[2 * k + 1] = o[k];
+    }
+  }
+}
+
+// One radix-R Stockham (autosort) stage of nfft length-N transforms in LDS (transform f at x + f·ld): current
+// stride s, sub-length n = N/s, m = n/R. Task (p, q): inputs x[q + s(p + jm)], j < R; outputs
+// y[q + s(Rp + k)] = DFT_R(inputs)[k] · e^{sign·2πi·pk/n} — the twiddle is tw[p·k·s] of the length-N table.
+template <int R>
+__device__ __forceinline__ void stockham_stage(const float2* __restrict__ x, float2* __restrict__ y,
+                                               const float2* __restrict__ tw, int lgN, int ls, int nfft, int ld,
+                                               float sign) {
+  const int N = 1 << lgN, s = 1 << ls;
+  const int lgR = R == 8 ? 3 : R == 4 ? 2 : 1;
+  const int m = N >> (ls + lgR);
+  const int tasks = N >> lgR;
+  for (int i = threadIdx.x; i < nfft * tasks; i += blockDim.x) {
+    const int f = i >> (lgN - lgR);
+    const int r = i & (tasks - 1);
+    const int p = r >> ls, q = r & (s - 1);
+    const float2* xf = x + f * ld + q + s * p;
+    float2 a[R];
+#pragma unroll
+    for (int j = 0; j < R; ++j) a[j] = xf[s * m * j];
+    dft_small<R>(a, sign);
+    float2* yf = y + f * ld + q + s * R * p;
+    yf[0] = a[0];
+#pragma unroll
+    for (int k = 1; k < R; ++k) yf[s * k] = cmul(a[k], tw[p * k * s]);
+  }
+}
+
+// nfft independent length-2^lg transforms at x + f·ld (y: scratch of the same shape), radix-8 stages (then one
+// radix-4 or radix-2 stage for the remainder): 3 passes over LDS for a 512-point transform instead of radix-2's 9.
+// Natural-order result in the returned buffer; every stage ends with a barrier.
+__device__ float2* stockham(float2* x, float2* y, const float2* tw, int lg, int nfft, int ld, float sign) {
+  int ls = 0;
+  while (ls < lg) {
+    const int left = lg - ls;
+    if (left >= 3) {
+      stockham_stage<8>(x, y, tw, lg, ls, nfft, ld, sign);
+      ls += 3;
+    } else if (left == 2) {
+      stockham_stage<4>(x, y, tw, lg, ls, nfft, ld, sign);
+      ls += 2;
+    } else {
+      stockham_stage<2>(x, y, tw, lg, ls, nfft, ld, sign);
+      ls += 1;
     }
     __syncthreads();
     float2* t = x;
@@ -206,7 +270,7 @@ __global__ __launch_bounds__(256) void fft_rows_kernel(const float* __restrict__
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int W = 1 << lg;
   float2* tw = reinterpret_cast<float2*>(smem);
-  float2* A = tw + kMaxN / 2;
+  float2* A = tw + kMaxN;
   float2* Bf = A + R * W;
   const int64_t r0 = (int64_t)blockIdx.x * R;
   const int nr = (int)min((int64_t)R, rows - r0);
@@ -214,9 +278,9 @@ __global__ __launch_bounds__(256) void fft_rows_kernel(const float* __restrict__
     const int64_t g = r0 * W + i;
     A[i] = xr ? make_float2(xr[g], 0.f) : xc[g];
   }
-  twiddles_half(tw, W, sign);
+  twiddles_full(tw, W, sign);
   __syncthreads();
-  const float2* res = stockham(A, Bf, tw, lg, nr, W);
+  const float2* res = stockham(A, Bf, tw, lg, nr, W, sign);
   for (int i = threadIdx.x; i < nr * W; i += blockDim.x) {
     const int64_t g = r0 * W + i;
     const float2 v = res[i];
@@ -238,7 +302,7 @@ __global__ __launch_bounds__(256) void fft_cols_kernel(const float2* __restrict_
   const int H = 1 << lg, ld = H + 1;
   const int tc = min(kColTile, W);
   float2* tw = reinterpret_cast<float2*>(smem);
-  float2* A = tw + kMaxN / 2;
+  float2* A = tw + kMaxN;
   float2* Bf = A + tc * ld;
   const int64_t plane = blockIdx.y;
   const int c0 = blockIdx.x * tc;
@@ -257,9 +321,9 @@ __global__ __launch_bounds__(256) void fft_cols_kernel(const float2* __restrict_
     }
     A[cc * ld + h] = v;
   }
-  twiddles_half(tw, H, sign);
+  twiddles_full(tw, H, sign);
   __syncthreads();
-  const float2* res = stockham(A, Bf, tw, lg, tc, ld);
+  const float2* res = stockham(A, Bf, tw, lg, tc, ld, sign);
   for (int i = threadIdx.x; i < tc * H; i += blockDim.x) {
     const int h = i / tc, cc = i - h * tc;
     const int64_t g = base + (int64_t)h * W + c0 + cc;
@@ -311,7 +375,7 @@ static int spec_rows(const float* xr, const float2* xc, float2* out, float* out_
   const int lg = spec_lg(W);
   if (lg < 0) return -2;
   const int R = max(1, 2048 / W);
-  const size_t smem = (size_t)(spec::kMaxN / 2 + 2 * R * W) * sizeof(float2);
+  const size_t smem = (size_t)(spec::kMaxN + 2 * R * W) * sizeof(float2);
   if (smem > 64 * 1024)
     (void)hipFuncSetAttribute((const void*)spec::fft_rows_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   hipLaunchKernelGGL(spec::fft_rows_kernel, dim3((unsigned)((rows + R - 1) / R)), dim3(256), smem, stream, xr, xc, out,
@@ -324,7 +388,7 @@ static int spec_cols(const float2* in, float2* out, float* amp_out, const float*
   const int lg = spec_lg(H);
   if (lg < 0 || spec_lg(W) < 0) return -2;
   const int tc = min(spec::kColTile, W);
-  const size_t smem = (size_t)(spec::kMaxN / 2 + 2 * tc * (H + 1)) * sizeof(float2);
+  const size_t smem = (size_t)(spec::kMaxN + 2 * tc * (H + 1)) * sizeof(float2);
   if (smem > 160 * 1024) return -5;
   (void)hipFuncSetAttribute((const void*)spec::fft_cols_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   hipLaunchKernelGGL(spec::fft_cols_kernel, dim3((unsigned)(W / tc), (unsigned)planes), dim3(256), smem, stream, in,

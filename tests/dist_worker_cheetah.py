@@ -45,7 +45,8 @@ def main(rank, world, port, out, model, replicas, epochs):
     x, y, xt, yt = data(model)
     bs = 4
     ds = [len(x), len(xt), ClientData(x, y, bs), ClientData(xt, yt, bs), None, None, None, 5]
-    args = Arguments.from_dict({"x": {"client_optimizer": "sgd", "learning_rate": 0.05, "momentum": 0.9,
+    args = Arguments.from_dict({"x": {"client_optimizer": "sgd",
+                                      "learning_rate": float(os.environ.get("FEDML_TEST_LR", "0.05")), "momentum": 0.9,
                                       "weight_decay": 1e-3, "batch_size": bs, "epochs": epochs, "shuffle": True,
                                       "random_seed": 3, "replicas_per_gpu": replicas, "frequency_of_the_test": 1,
                                       "cheetah_exec": "native" if model != "mlp" else "auto"}})

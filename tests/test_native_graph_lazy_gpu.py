@@ -60,14 +60,17 @@ def _run(graphs: bool, lazy: bool, det: bool = False, momentum: float = 0.9):
 
 def test_graphs_lazy_bn_multi_round_match_eager_explicit():
     ref, ng0, _ = _run(graphs=False, lazy=False)
+    ref2, _, _ = _run(graphs=False, lazy=False)
     got, ng, (ncache, npinned) = _run(graphs=True, lazy=True)
+    spread = float((ref2 - ref).norm() / ref.norm())      # run-to-run spread of the fp32-atomic eager path
     assert ng0 == 0 and ng >= 3            # first/later step of the full geometry + the ragged tail, captured
     assert npinned >= 2 and ncache >= npinned
     assert torch.isfinite(got).all()
     rel = float((got - ref).norm() / ref.norm())
-    # fp32 atomics only (order of BN-statistic / weight-gradient sums): measured ~1e-6; a BN folded with another
-    # step's nimg / active moves whole clients' updates (> 1e-2)
-    assert rel < 1e-4, rel
+    # fp32 atomics only (order of BN-statistic / weight-gradient sums, amplified over 3 rounds × 2 epochs at momentum
+    # 0.9): measured 8.4e-4 on the driver's box; a BN folded with another step's nimg / active moves whole clients'
+    # first steps (rel > 1e-2). The bit-exact check of the same schedule is the deterministic test below.
+    assert rel < max(10 * spread, 3e-3), (rel, spread)
 
 
 def test_graphs_lazy_vs_explicit_deterministic_bitwise(monkeypatch):
