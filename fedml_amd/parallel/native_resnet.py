@@ -159,6 +159,9 @@ class NativeResNetStep:
         self.use_c3_block = os.environ.get("FEDML_AMD_C3_BLOCK", "1") != "0"
         self.use_s2k = os.environ.get("FEDML_AMD_C3S2_CONVK", "1") == "1"   # measured +2 % (fp32 headline)
         self.use_ry = os.environ.get("FEDML_AMD_RECOMPUTE_Y", "0") == "1" and dtype == torch.float32
+        # recompute y3 in the last 1×1 conv's BACKWARD only (y3 still stored for the forward consumers and the next
+        # block's BN3 statistics): the fused backward reads the planes-wide conv input instead of the 4·planes-wide y3
+        self.use_ry_bwd = os.environ.get("FEDML_AMD_RY_BWD", "0") == "1" and dtype == torch.float32
         self.use_pbout = os.environ.get("FEDML_AMD_FUSE_BOUT", "1") != "0"
         self.use_fch = os.environ.get("FEDML_AMD_FC_HEAD", "1") != "0"      # fused fc + CE head kernel
         # deferred BN finalisation (csrc/bnlazy.h): the first consumer kernel folds the statistics itself
@@ -267,6 +270,7 @@ class NativeResNetStep:
         maxel = st.Ho * st.Wo * st.cout
         for b in self.blocks:
             b.ry = self._ry_ok(b)
+            b.ryb = not b.ry and self.use_ry_bwd and self._ry_ok(b, shape_only=True)
             b.ys = [None if (b.ry and j == len(b.convs) - 1) else act(cv.Ho, cv.Wo, cv.cout)
                     for j, cv in enumerate(b.convs)]
             b.yd = act(b.ds_conv.Ho, b.ds_conv.Wo, b.ds_conv.cout) if b.ds_conv is not None else None
@@ -456,13 +460,13 @@ class NativeResNetStep:
                           cv.cin_pad, cv.Ho, cv.Wo, cv.cout, cv.k, cv.k, cv.stride, cv.pad, self._pix_per_wg(M), cv.cin,
                           self.dw_scratch, nimg=self._nimg, lazy=lz)
 
-    def _ry_ok(self, b) -> bool:
+    def _ry_ok(self, b, shape_only=False) -> bool:
         """Bottleneck whose last (1×1, planes → 4·planes) conv output y3 is never stored (fp32): its BN statistics
         come from a stats-only pass, the block output straight from a second pass of the same GEMM (EPI_BOUT),
         Σg·y3 of its BN backward from the Gram product gᵀ·h2 (h2 = the conv input), and the fused 1×1 backward
         recomputes y3 per pixel stage. Per block and pixel that removes the 4·planes-wide y3 write and its three
         reads (block output, next block's backward epilogue, BN backward) for one planes-wide Gram read."""
-        if not self.use_ry or len(b.convs) != 3:
+        if not (self.use_ry or shape_only) or len(b.convs) != 3:
             return False
         cv = b.convs[-1]
         return (cv.k == 1 and cv.stride == 1 and cv.pad == 0 and cv.cin == cv.cin_pad and cv.cout % 64 == 0
@@ -734,7 +738,7 @@ class NativeResNetStep:
                 pv = self.bn_vec[b.bns[j - 1].key]
                 M = N * cv.Ho * cv.Wo
                 out_g = free[0] if g_j is not free[0] else free[1]
-                if b.ry and j == len(b.convs) - 1:
+                if (b.ry or b.ryb) and j == len(b.convs) - 1:
                     nn_ops.conv1x1_bwd_fused_ry(g_j, v[4], v[5], v[6], v[8], self.packed.view(-1)[cv.off_b:],
                                                 self.packed_ld, cv.ldk2, b.ys[j - 1], pv[0], pv[1], out_g,
                                                 self.stat_views[b.bns[j - 1].key][1], garena, self.off[cv.key], C, M,
@@ -914,7 +918,8 @@ class NativeResNetStep:
                     pend = None
                 else:
                     self._fwd(cv, src, b.ys[j], pro, bn, N, pro_key=None if j == 0 else b.bns[j - 1].key)
-                if b.ys[j] is None:     # recomputed-y conv: keep the pivot its later passes must subtract
+                if b.ys[j] is None or (b.ryb and j == len(b.convs) - 1):
+                    # recomputed-y conv: keep the pivot its later passes must subtract
                     self.bn_vec[bn.key][8].copy_(self.bn_vec[bn.key][7])
                 self._bn_fwd(bn, N, cv.Ho * cv.Wo, arena, active)
             last, lbn = b.convs[-1], b.bns[-1]

@@ -202,6 +202,8 @@ class NativeGNResNetStep:
         self.stats = torch.zeros(C * max(maxco, maxch) * 3, dtype=torch.float32, device=dev)
         mx = max(cv.cout * cv.k * cv.k * cv.cin_pad for cv in self._all_convs())
         self.dw_scratch = torch.zeros(C * mx, dtype=torch.float32, device=dev)
+        self._ones = torch.ones(C, maxco, dtype=torch.float32, device=dev)
+        self._zeros = torch.zeros(C, maxco, dtype=torch.float32, device=dev)
         self.pooled = torch.zeros(C, N, self.fc_in, dtype=torch.float32, device=dev)
         self.dpool = torch.zeros(C, N, self.fc_in, dtype=torch.float32, device=dev)
         self.loss_c = torch.zeros(C, dtype=torch.float32, device=dev)
@@ -209,7 +211,8 @@ class NativeGNResNetStep:
         if self.det is not None:
             self.det.register(self.dw_scratch)
 
-    _STATE = ("x_in", "y0", "a0", "p0", "idx0", "gbuf", "ms", "pscr", "stats", "dw_scratch", "pooled", "dpool",
+    _STATE = ("x_in", "y0", "a0", "p0", "idx0", "gbuf", "ms", "pscr", "stats", "dw_scratch", "_ones", "_zeros",
+              "pooled", "dpool",
               "loss_c", "packed", "packed_ld", "_segs", "_nseg", "_pack_tiles", "_pack_taps", "final_hw", "pool_hw",
               "geom")
 
@@ -269,7 +272,10 @@ class NativeGNResNetStep:
         nn_ops.gnh_param_reduce(self.pscr, garena, g, b, self.C, N, n.ch, nimg=self._nimg)
 
     def _wgrad(self, cv, dy, x, garena, N):
-        nn_ops.conv_wgrad(dy, None, None, None, None, x, None, None, garena, self.off[cv.key], self.C, N, cv.H, cv.W,
+        # the tiled weight-gradient kernel consumes dy in its folded-BN form α·g + β·y + γ: a materialised dy is
+        # that form with α = 1, β = γ = 0 (y = dy itself, finite)
+        one, zero = self._ones[:, :cv.cout].contiguous(), self._zeros[:, :cv.cout].contiguous()
+        nn_ops.conv_wgrad(dy, dy, one, zero, zero, x, None, None, garena, self.off[cv.key], self.C, N, cv.H, cv.W,
                           cv.cin_pad, cv.Ho, cv.Wo, cv.cout, cv.k, cv.k, cv.stride, cv.pad,
                           self._ppw(N * cv.Ho * cv.Wo), cv.cin, self.dw_scratch, nimg=self._nimg)
 

@@ -44,8 +44,12 @@ def main():
     agg = collections.defaultdict(lambda: [0, 0.0, None])
     for r in rows:
         name = col(r, "Kernel_Name", "KernelName")
-        grid = int(col(r, "Grid_Size", "Grid_Size_X", default=0) or 0)
-        wg = int(col(r, "Workgroup_Size", "Workgroup_Size_X", default=256) or 256)
+        if "Grid_Size_X" in r:     # rocprofv3: 3-D grid and workgroup in work-items
+            grid = math.prod(int(col(r, "Grid_Size_" + d, default=1) or 1) for d in "XYZ")
+            wg = math.prod(int(col(r, "Workgroup_Size_" + d, default=1) or 1) for d in "XYZ")
+        else:
+            grid = int(col(r, "Grid_Size", default=0) or 0)
+            wg = int(col(r, "Workgroup_Size", default=256) or 256)
         vgpr = int(col(r, "VGPR_Count", "Arch_VGPR_Count", default=0) or 0)
         agpr = int(col(r, "Accum_VGPR_Count", default=0) or 0)
         lds = int(col(r, "LDS_Block_Size", "Lds_Size", "LDS_Size", default=0) or 0)

@@ -74,3 +74,30 @@ def test_recompute_y_matches_stored_y(monkeypatch, mode, layers, hw, counts):
             assert torch.allclose(a1[:, sl], a0[:, sl], rtol=1e-6, atol=1e-7), s.key
     assert not bad, bad[:8]
     assert float(g1[counts.index(0)].abs().max()) == 0.0 if 0 in counts else True
+
+
+@pytest.mark.parametrize("layers,hw,counts", [([1, 1, 1], 16, [16, 16, 16]), ([2, 2, 2], 32, [16, 11, 3, 0])])
+def test_backward_only_recompute_matches_stored_y(monkeypatch, layers, hw, counts):
+    """FEDML_AMD_RY_BWD: y3 stays stored for the forward and the next block's statistics; only the last 1×1 conv's
+    fused backward rebuilds y3 − K from its (planes-wide) input instead of reading the stored y3."""
+    torch.manual_seed(0)
+    model = ResNet(Bottleneck, layers, 10)
+    layout = ParamLayout.from_module(model)
+    flat = layout.flatten(model.state_dict()).to(DEV)
+    C, N = len(counts), 16
+    x = torch.randn(C, N, 3, hw, hw, device=DEV)
+    y = torch.randint(0, 10, (C, N), device=DEV)
+    l0, a0, g0, o0, s0 = _run(monkeypatch, "0", model, layout, flat, x, y, counts)
+    monkeypatch.setenv("FEDML_AMD_RY_BWD", "1")
+    l1, a1, g1, o1, s1 = _run(monkeypatch, "0", model, layout, flat, x, y, counts)
+    assert all(b.ryb and b.ys[-1] is not None for b in s1.blocks)
+    assert abs(l0 - l1) <= 1e-6 * abs(l0)
+    bad = []
+    for s in layout.slots:
+        if s.trainable:
+            sl = slice(s.offset, s.offset + s.numel)
+            r = g0[:, sl]
+            err = float((g1[:, sl] - r).norm() / r.norm().clamp_min(1e-30))
+            if err > 2e-5:
+                bad.append((s.key, err))
+    assert not bad, bad[:8]
