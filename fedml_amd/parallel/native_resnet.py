@@ -164,6 +164,13 @@ class NativeResNetStep:
         self.use_ry_bwd = os.environ.get("FEDML_AMD_RY_BWD", "0") == "1" and dtype == torch.float32
         self.use_pbout = os.environ.get("FEDML_AMD_FUSE_BOUT", "1") != "0"
         self.use_fch = os.environ.get("FEDML_AMD_FC_HEAD", "1") != "0"      # fused fc + CE head kernel
+        # 3×3 weight gradients on a second HIP stream: they are off the backward's critical path (dW of layer L is
+        # needed only by the optimizer), so they fill the CUs the small-grid backward-data kernels of L-1, L-2 leave
+        # idle (13 clients per GPU: those run at 0.25-0.5 workgroup waves). Not in deterministic mode.
+        self.use_side = os.environ.get("FEDML_AMD_SIDE_WGRAD", "1") != "0"
+        # (created here, never inside a graph capture)
+        self._side = torch.cuda.Stream(device=self.device) if (self.use_side and self.device.type == "cuda") else None
+        self._side_reads = {}    # data_ptr of a gradient buffer a side-stream kernel still reads → its done event
         # deferred BN finalisation (csrc/bnlazy.h): the first consumer kernel folds the statistics itself
         self.use_lazy = os.environ.get("FEDML_AMD_BN_LAZY", "1") != "0"
         self._pending = {}       # (bn key, "f" | "b") → explicit finalisation closure, while deferred
@@ -440,6 +447,21 @@ class NativeResNetStep:
         C = self.C
         ps = pro_vec[0] if pro_vec is not None else None
         pt = pro_vec[1] if pro_vec is not None else None
+        if self._c3(cv) and self._side_on():
+            # the main stream's backward-data reads the folded rows: finalise explicitly, then fork
+            self._flush(bn_key, "b")
+            main = torch.cuda.current_stream(self.device)
+            fork = torch.cuda.Event()
+            fork.record(main)
+            self._side.wait_event(fork)
+            with torch.cuda.stream(self._side):
+                nn_ops.conv3x3_wgrad(g, y, vec[4], vec[5], vec[6], x, ps, pt, garena, self.off[cv.key], C, N, cv.H,
+                                     cv.W, cv.cin_pad, cv.cout, cv.cin, self.dw_c3[self._c3_off[cv.key]:], cv.stride,
+                                     scatter=False, nimg=self._nimg)
+            done = torch.cuda.Event()
+            done.record(self._side)
+            self._side_reads[g.data_ptr()] = done     # activations (y, x) are not written in the backward
+            return
         lz = (self._take(bn_key, "b"), None) if y is not None else None   # y None: materialised dy, no BN
         if self._c3(cv):
             nn_ops.conv3x3_wgrad(g, y, vec[4], vec[5], vec[6], x, ps, pt, garena, self.off[cv.key], C, N, cv.H, cv.W,
@@ -459,6 +481,28 @@ class NativeResNetStep:
         nn_ops.conv_wgrad(g, y, vec[4], vec[5], vec[6], x, ps, pt, garena, self.off[cv.key], C, N, cv.H, cv.W,
                           cv.cin_pad, cv.Ho, cv.Wo, cv.cout, cv.k, cv.k, cv.stride, cv.pad, self._pix_per_wg(M), cv.cin,
                           self.dw_scratch, nimg=self._nimg, lazy=lz)
+
+    def _side_on(self):
+        return self._side is not None and self.det is None
+
+    def _claim(self, buf):
+        """``buf`` is about to be written on the main stream: wait for the side-stream kernel still reading it."""
+        ev = self._side_reads.pop(buf.data_ptr(), None)
+        if ev is not None:
+            torch.cuda.current_stream(self.device).wait_event(ev)
+        return buf
+
+    def _pick(self, cands):
+        """First candidate buffer no side-stream kernel is reading (else the first: claimed by the caller)."""
+        for t in cands:
+            if t.data_ptr() not in self._side_reads:
+                return t
+        return cands[0]
+
+    def _side_join(self):
+        if self._side is not None:
+            torch.cuda.current_stream(self.device).wait_stream(self._side)
+        self._side_reads.clear()
 
     def _ry_ok(self, b, shape_only=False) -> bool:
         """Bottleneck whose last (1×1, planes → 4·planes) conv output y3 is never stored (fp32): its BN statistics
@@ -737,7 +781,7 @@ class NativeResNetStep:
                 v = self.bn_vec[bn.key]
                 pv = self.bn_vec[b.bns[j - 1].key]
                 M = N * cv.Ho * cv.Wo
-                out_g = free[0] if g_j is not free[0] else free[1]
+                out_g = self._claim(self._pick([t for t in free[:2] if t is not g_j]))
                 if (b.ry or b.ryb) and j == len(b.convs) - 1:
                     nn_ops.conv1x1_bwd_fused_ry(g_j, v[4], v[5], v[6], v[8], self.packed.view(-1)[cv.off_b:],
                                                 self.packed_ld, cv.ldk2, b.ys[j - 1], pv[0], pv[1], out_g,
@@ -781,6 +825,7 @@ class NativeResNetStep:
             # shortcut gradient D into free[2] (downsample) or the block's own gpre (identity)
             gadd = free[2]
             if b.ds_conv is not None:
+                self._claim(gadd)
                 d = b.ds_conv
                 vd = self.bn_vec[b.ds_bn.key]
                 dg, dyv, al, be, ga = self._dy(d, gpre, b.yd, vd, N, bn_key=b.ds_bn.key)
@@ -811,7 +856,7 @@ class NativeResNetStep:
             # output buffer must differ from g_j and the shortcut source (gpre itself is free again once
             # the downsample path has consumed it)
             busy = {id(g_j), id(shortcut)}
-            out_buf = next(t for t in bufs if id(t) not in busy)
+            out_buf = self._claim(self._pick([t for t in bufs if id(t) not in busy]))
             if fused0:
                 M0 = N * cv0.H * cv0.W
                 nn_ops.conv1x1_bwd_fused(g_j, b.ys[0], v[4], v[5], v[6], self.packed.view(-1)[cv0.off_b:],
@@ -841,6 +886,7 @@ class NativeResNetStep:
         v = self.bn_vec[st_bn.key]
         self._wgrad(st_conv, gpre, self.stem_y, v, self.x_in, None, garena, N, bn_key=st_bn.key)
         self._flush_all()
+        self._side_join()
         if self.c3_nseg:
             if self.det is not None:
                 self.det.flush(self.dw_c3)

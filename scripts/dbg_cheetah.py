@@ -18,6 +18,8 @@ def main():
     x, y, xt, yt = W.data("resnet56")
     ds = [len(x), len(xt), ClientData(x, y, 4), ClientData(xt, yt, 4), None, None, None, 100]
     lr = float(sys.argv[1]) if len(sys.argv) > 1 else 0.002
+    if len(sys.argv) > 2 and sys.argv[2] == "fp32":
+        torch.backends.cuda.matmul.allow_tf32 = torch.backends.cudnn.allow_tf32 = False
     args = Arguments.from_dict({"x": {"client_optimizer": "sgd", "learning_rate": lr, "momentum": 0.0,
                                       "weight_decay": 0.0, "batch_size": 4, "epochs": 1, "shuffle": True,
                                       "random_seed": 3, "replicas_per_gpu": 1, "cheetah_exec": "native"}})

@@ -39,6 +39,9 @@ def test_native_single_replica_tracks_torch_sgd(tmp_path):
                  timeout=300)
     assert got["native"]
     x, y, _, _ = W.data("resnet56")
+    # plain fp32 on the torch side: TF32-style reduced-precision convs / GEMMs (allowed by default) alone move a
+    # batch-4 BatchNorm ResNet-56's gradients by ~3 % (scripts/dbg_cheetah.py)
+    torch.backends.cuda.matmul.allow_tf32 = torch.backends.cudnn.allow_tf32 = False
     model = W.make_model("resnet56").cuda()
     init = {k: v.detach().clone() for k, v in model.state_dict().items()}
     opt = torch.optim.SGD(model.parameters(), lr=0.002, momentum=0.9, weight_decay=1e-3)

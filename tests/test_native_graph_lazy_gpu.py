@@ -33,7 +33,7 @@ def _store():
                              torch.randint(0, 10, (n,), generator=g).to(DEV), offs, COUNTS)
 
 
-def _run(graphs: bool, lazy: bool, det: bool = False, momentum: float = 0.9):
+def _run(graphs: bool, lazy: bool, det: bool = False, momentum: float = 0.9, side: bool = True):
     torch.manual_seed(0)
     model = ResNet(Bottleneck, [1, 1, 1], 10)
     args = Arguments.from_dict({"x": {"client_optimizer": "sgd", "learning_rate": 0.02, "momentum": momentum,
@@ -42,6 +42,9 @@ def _run(graphs: bool, lazy: bool, det: bool = False, momentum: float = 0.9):
     assert eng.native_step is not None
     eng.use_graphs = graphs
     eng.native_step.use_lazy = lazy
+    if not side:
+        eng.native_step._side = None
+    assert (eng.native_step._side is not None) == side
     store = _store()
     glob = eng.layout.flatten(model.state_dict(), device=DEV)
     for r, slots in enumerate(ROUND_SLOTS):
@@ -85,3 +88,16 @@ def test_graphs_lazy_vs_explicit_deterministic_bitwise(monkeypatch):
         determinism.disable()
     assert torch.isfinite(a).all()
     assert torch.equal(a, b), float((a - b).norm() / a.norm())
+
+
+def test_side_stream_weight_gradients_match_single_stream():
+    """3×3 weight gradients forked onto a second stream (joined before the scatter; the main stream waits for a
+    side kernel before overwriting a gradient buffer it reads) — captured graphs across rounds and geometries must
+    agree with the single-stream schedule up to the fp32-atomic spread."""
+    ref, _, _ = _run(graphs=True, lazy=True, side=False)
+    ref2, _, _ = _run(graphs=True, lazy=True, side=False)
+    got, _, _ = _run(graphs=True, lazy=True, side=True)
+    spread = float((ref2 - ref).norm() / ref.norm())
+    rel = float((got - ref).norm() / ref.norm())
+    assert torch.isfinite(got).all()
+    assert rel < max(10 * spread, 3e-3), (rel, spread)

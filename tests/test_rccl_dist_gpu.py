@@ -32,3 +32,16 @@ def test_headline_config_four_ranks_equals_one_rank(tmp_path):
     w4 = _launch(4, str(tmp_path / "w4.pt"), "headline", 100, True, False, **env)
     assert w1.shape == w4.shape and torch.isfinite(w1).all()
     assert torch.equal(w1, w4), float((w1 - w4).norm() / w1.norm())
+
+
+def test_headline_config_eight_ranks_ragged_packing_equals_one_rank(tmp_path):
+    """The 8-GPU packing of the headline: 100 clients over 8 ranks is 13/13/13/13/12/12/12/12 (`pack_clients_to_gpus`),
+    so half the ranks run a ragged client count — still bitwise equal to 1 rank × 100 clients."""
+    from fedml_amd.core.schedule.scheduler import pack_clients_to_gpus
+    sizes = sorted(len(p) for p in pack_clients_to_gpus([500] * 100, 8))
+    assert sizes == [12] * 4 + [13] * 4, sizes
+    env = dict(_ENV, FEDML_TEST_ROUNDS="2")
+    w1 = _launch(1, str(tmp_path / "w1.pt"), "headline", 100, True, False, **env)
+    w8 = _launch(8, str(tmp_path / "w8.pt"), "headline", 100, True, False, **env)
+    assert w1.shape == w8.shape and torch.isfinite(w1).all()
+    assert torch.equal(w1, w8), float((w1 - w8).norm() / w1.norm())
