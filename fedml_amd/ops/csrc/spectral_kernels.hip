@@ -157,9 +157,9 @@ __global__ __launch_bounds__(256) void spec_mix_ifft2_kernel(const float2* __res
 
 // ---------------------------------------------------------------------------------------------------------------
 // Power-of-two planes up to 512 × 512 (HS-FedAvg's 3 × 512 × 512 amplitude, hs_fedavg/fedavg_api.py:135): a
-// radix-8 Stockham FFT in LDS (in-register 8-point butterflies), applied separably — a row pass (whole rows in LDS, several per workgroup) and a
-// column pass (a 16-column × H tile in LDS, padded leading dimension against bank conflicts, coalesced 128-B row
-// segments on both sides). Forward: rows (real in) → columns (F out, |F| fused). Inverse with the band mix:
+// radix-8 Stockham FFT in LDS (in-register 8-point butterflies, in place through registers, bank-padded indices),
+// applied separably — a row pass (whole rows in LDS, several per workgroup) and a column pass (a 16-column × H tile
+// in LDS, coalesced 128-B row segments on both sides). Forward: rows (real in) → columns (F out, |F| fused). Inverse with the band mix:
 // columns (mix applied while loading F) → rows (real part × 1/HW out). O(HW·log HW) per plane instead of the
 // DFT's O(HW·(H+W)).
 constexpr int kMaxN = 512;
@@ -210,56 +210,77 @@ __device__ __forceinline__ void dft_small(float2 (&a)[R], float sign) {
   }
 }
 
-// One radix-R Stockham (autosort) stage of nfft length-N transforms in LDS (transform f at x + f·ld): current
-// stride s, sub-length n = N/s, m = n/R. Task (p, q): inputs x[q + s(p + jm)], j < R; outputs
-// y[q + s(Rp + k)] = DFT_R(inputs)[k] · e^{sign·2πi·pk/n} — the twiddle is tw[p·k·s] of the length-N table.
-template <int R>
-__device__ __forceinline__ void stockham_stage(const float2* __restrict__ x, float2* __restrict__ y,
-                                               const float2* __restrict__ tw, int lgN, int ls, int nfft, int ld,
-                                               float sign) {
+// Transform-local LDS index with one float2 of padding per 8: the radix-8 stages' strided accesses (output stride
+// R·s) land on distinct banks (a 512-point stage 1 writes 8p + k → 9p + k: 18-float lane stride, 32 lanes on 64
+// distinct banks) instead of 4-16-way conflicts.
+__device__ __forceinline__ int lpad(int i) { return i + (i >> 3); }
+// LDS leading dimension of one transform: N + N/8 padded to ≡ 2 (mod 32) float2, so the 16 transforms of a column
+// tile written by one half-wave (consecutive columns) also fall on distinct banks
+__host__ __device__ __forceinline__ int lds_ld(int n) { return ((n + n / 8 + 29) / 32) * 32 + 2; }
+
+// One radix-R Stockham (autosort) stage of nfft length-N transforms IN PLACE in LDS (transform f at x + f·ld,
+// padded indices): current stride s, sub-length n = N/s, m = n/R. Task (p, q): inputs x[q + s(p + jm)], j < R;
+// outputs y[q + s(Rp + k)] = DFT_R(inputs)[k] · e^{sign·2πi·pk/n} — the twiddle is tw[p·k·s] of the length-N
+// table. Every thread loads all its tasks' inputs into registers, the workgroup synchronises, then the outputs
+// overwrite the same buffer: one LDS buffer instead of a ping-pong pair (twice the workgroups per CU).
+// MAXT = the tasks a thread may own (nfft·N/R ≤ MAXT·blockDim).
+template <int R, int MAXT>
+__device__ __forceinline__ void stockham_stage_ip(float2* __restrict__ x, const float2* __restrict__ tw, int lgN,
+                                                  int ls, int nfft, int ld, float sign) {
   const int N = 1 << lgN, s = 1 << ls;
   const int lgR = R == 8 ? 3 : R == 4 ? 2 : 1;
   const int m = N >> (ls + lgR);
   const int tasks = N >> lgR;
-  for (int i = threadIdx.x; i < nfft * tasks; i += blockDim.x) {
-    const int f = i >> (lgN - lgR);
-    const int r = i & (tasks - 1);
-    const int p = r >> ls, q = r & (s - 1);
-    const float2* xf = x + f * ld + q + s * p;
-    float2 a[R];
+  const int total = nfft * tasks;
+  float2 a[MAXT][R];
 #pragma unroll
-    for (int j = 0; j < R; ++j) a[j] = xf[s * m * j];
-    dft_small<R>(a, sign);
-    float2* yf = y + f * ld + q + s * R * p;
-    yf[0] = a[0];
+  for (int t = 0; t < MAXT; ++t) {
+    const int i = threadIdx.x + t * blockDim.x;
+    if (i < total) {
+      const int f = i >> (lgN - lgR);
+      const int r = i & (tasks - 1);
+      const int p = r >> ls, q = r & (s - 1);
+      const float2* xf = x + f * ld;
 #pragma unroll
-    for (int k = 1; k < R; ++k) yf[s * k] = cmul(a[k], tw[p * k * s]);
+      for (int j = 0; j < R; ++j) a[t][j] = xf[lpad(q + s * (p + j * m))];
+    }
   }
+  __syncthreads();
+#pragma unroll
+  for (int t = 0; t < MAXT; ++t) {
+    const int i = threadIdx.x + t * blockDim.x;
+    if (i < total) {
+      const int f = i >> (lgN - lgR);
+      const int r = i & (tasks - 1);
+      const int p = r >> ls, q = r & (s - 1);
+      dft_small<R>(a[t], sign);
+      float2* yf = x + f * ld;
+      yf[lpad(q + s * R * p)] = a[t][0];
+#pragma unroll
+      for (int k = 1; k < R; ++k) yf[lpad(q + s * (R * p + k))] = cmul(a[t][k], tw[p * k * s]);
+    }
+  }
+  __syncthreads();
 }
 
-// nfft independent length-2^lg transforms at x + f·ld (y: scratch of the same shape), radix-8 stages (then one
-// radix-4 or radix-2 stage for the remainder): 3 passes over LDS for a 512-point transform instead of radix-2's 9.
-// Natural-order result in the returned buffer; every stage ends with a barrier.
-__device__ float2* stockham(float2* x, float2* y, const float2* tw, int lg, int nfft, int ld, float sign) {
+// nfft independent length-2^lg transforms at x + f·ld (padded indices), in place, natural order out: radix-8 stages
+// then one radix-4 or radix-2 stage for the remainder (a 512-point transform: 3 LDS passes). nfft·2^lg ≤ 8192 with
+// 256 threads (every stage holds 32 points per thread in registers).
+__device__ void stockham(float2* x, const float2* tw, int lg, int nfft, int ld, float sign) {
   int ls = 0;
   while (ls < lg) {
     const int left = lg - ls;
     if (left >= 3) {
-      stockham_stage<8>(x, y, tw, lg, ls, nfft, ld, sign);
+      stockham_stage_ip<8, 4>(x, tw, lg, ls, nfft, ld, sign);
       ls += 3;
     } else if (left == 2) {
-      stockham_stage<4>(x, y, tw, lg, ls, nfft, ld, sign);
+      stockham_stage_ip<4, 8>(x, tw, lg, ls, nfft, ld, sign);
       ls += 2;
     } else {
-      stockham_stage<2>(x, y, tw, lg, ls, nfft, ld, sign);
+      stockham_stage_ip<2, 16>(x, tw, lg, ls, nfft, ld, sign);
       ls += 1;
     }
-    __syncthreads();
-    float2* t = x;
-    x = y;
-    y = t;
   }
-  return x;
 }
 
 // R rows of length W = 2^lg per workgroup. In: real (xr) or complex (xc). Out: complex (out) or the real part
@@ -268,22 +289,23 @@ __global__ __launch_bounds__(256) void fft_rows_kernel(const float* __restrict__
                                                        float2* __restrict__ out, float* __restrict__ out_r,
                                                        int64_t rows, int lg, int R, float sign, float scale) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int W = 1 << lg;
+  const int W = 1 << lg, ld = lds_ld(W);
   float2* tw = reinterpret_cast<float2*>(smem);
   float2* A = tw + kMaxN;
-  float2* Bf = A + R * W;
   const int64_t r0 = (int64_t)blockIdx.x * R;
   const int nr = (int)min((int64_t)R, rows - r0);
   for (int i = threadIdx.x; i < nr * W; i += blockDim.x) {
     const int64_t g = r0 * W + i;
-    A[i] = xr ? make_float2(xr[g], 0.f) : xc[g];
+    const int rr = i >> lg, w = i & (W - 1);
+    A[rr * ld + lpad(w)] = xr ? make_float2(xr[g], 0.f) : xc[g];
   }
   twiddles_full(tw, W, sign);
   __syncthreads();
-  const float2* res = stockham(A, Bf, tw, lg, nr, W, sign);
+  stockham(A, tw, lg, nr, ld, sign);
   for (int i = threadIdx.x; i < nr * W; i += blockDim.x) {
     const int64_t g = r0 * W + i;
-    const float2 v = res[i];
+    const int rr = i >> lg, w = i & (W - 1);
+    const float2 v = A[rr * ld + lpad(w)];
     if (out_r) out_r[g] = v.x * scale;
     else out[g] = make_float2(v.x * scale, v.y * scale);
   }
@@ -291,19 +313,18 @@ __global__ __launch_bounds__(256) void fft_rows_kernel(const float* __restrict__
 
 constexpr int kColTile = 16;
 
-// a kColTile-column tile of one plane [H = 2^lg][W]: column transforms in LDS (leading dim H + 1). `trg` non-null:
-// inverse pass of the band mix — inside the band the loaded F is rescaled to amplitude trg[c] (F = 0: trg + 0i).
-// `amp_out` non-null: |F| of the result as well.
+// a kColTile-column tile of one plane [H = 2^lg][W]: column transforms in LDS (transform per column, padded). `trg`
+// non-null: inverse pass of the band mix — inside the band the loaded F is rescaled to amplitude trg[c] (F = 0:
+// trg + 0i). `amp_out` non-null: |F| of the result as well.
 __global__ __launch_bounds__(256) void fft_cols_kernel(const float2* __restrict__ in, float2* __restrict__ out,
                                                        float* __restrict__ amp_out, const float* __restrict__ amp_in,
                                                        const float* __restrict__ trg, int C, int band, int lg, int W,
                                                        float sign) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int H = 1 << lg, ld = H + 1;
+  const int H = 1 << lg, ld = lds_ld(H);
   const int tc = min(kColTile, W);
   float2* tw = reinterpret_cast<float2*>(smem);
   float2* A = tw + kMaxN;
-  float2* Bf = A + tc * ld;
   const int64_t plane = blockIdx.y;
   const int c0 = blockIdx.x * tc;
   const int64_t base = plane * (int64_t)H * W;
@@ -319,15 +340,15 @@ __global__ __launch_bounds__(256) void fft_cols_kernel(const float2* __restrict_
         v = a > 0.f ? make_float2(v.x * (A_ / a), v.y * (A_ / a)) : make_float2(A_, 0.f);
       }
     }
-    A[cc * ld + h] = v;
+    A[cc * ld + lpad(h)] = v;
   }
   twiddles_full(tw, H, sign);
   __syncthreads();
-  const float2* res = stockham(A, Bf, tw, lg, tc, ld, sign);
+  stockham(A, tw, lg, tc, ld, sign);
   for (int i = threadIdx.x; i < tc * H; i += blockDim.x) {
     const int h = i / tc, cc = i - h * tc;
     const int64_t g = base + (int64_t)h * W + c0 + cc;
-    const float2 v = res[cc * ld + h];
+    const float2 v = A[cc * ld + lpad(h)];
     out[g] = v;
     if (amp_out) amp_out[g] = sqrtf(v.x * v.x + v.y * v.y);
   }
@@ -375,7 +396,7 @@ static int spec_rows(const float* xr, const float2* xc, float2* out, float* out_
   const int lg = spec_lg(W);
   if (lg < 0) return -2;
   const int R = max(1, 2048 / W);
-  const size_t smem = (size_t)(spec::kMaxN + 2 * R * W) * sizeof(float2);
+  const size_t smem = (size_t)(spec::kMaxN + R * spec::lds_ld(W)) * sizeof(float2);
   if (smem > 64 * 1024)
     (void)hipFuncSetAttribute((const void*)spec::fft_rows_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   hipLaunchKernelGGL(spec::fft_rows_kernel, dim3((unsigned)((rows + R - 1) / R)), dim3(256), smem, stream, xr, xc, out,
@@ -388,7 +409,7 @@ static int spec_cols(const float2* in, float2* out, float* amp_out, const float*
   const int lg = spec_lg(H);
   if (lg < 0 || spec_lg(W) < 0) return -2;
   const int tc = min(spec::kColTile, W);
-  const size_t smem = (size_t)(spec::kMaxN + 2 * tc * (H + 1)) * sizeof(float2);
+  const size_t smem = (size_t)(spec::kMaxN + tc * spec::lds_ld(H)) * sizeof(float2);
   if (smem > 160 * 1024) return -5;
   (void)hipFuncSetAttribute((const void*)spec::fft_cols_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   hipLaunchKernelGGL(spec::fft_cols_kernel, dim3((unsigned)(W / tc), (unsigned)planes), dim3(256), smem, stream, in,

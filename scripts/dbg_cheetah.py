@@ -38,6 +38,19 @@ def main():
         g = tr.grads[0, s.offset:s.offset + s.numel]
         r = p.grad.reshape(-1)
         rows.append((float((g - r).norm() / r.norm().clamp_min(1e-30)), name, float(r.norm())))
+    # the same step in fp64 on the CPU: how far plain fp32 torch itself is from exact arithmetic
+    m64 = W.make_model("resnet56").double()
+    out64 = m64(x[sel].double())
+    l64 = nn.functional.cross_entropy(out64, y[sel])
+    l64.backward()
+    g32 = torch.cat([p.grad.reshape(-1).cpu().double() for p in model.parameters()])
+    g64 = torch.cat([p.grad.reshape(-1) for p in m64.parameters()])
+    gn = torch.cat([tr.grads[0, tr.layout.slot(n).offset:tr.layout.slot(n).offset + p.numel()].cpu().double()
+                    for n, p in model.named_parameters()])
+    print("loss torch32 %.7f torch64 %.7f" % (float(loss), float(l64)))
+    print("whole-gradient rel err: torch32 vs fp64 %.3e | native vs fp64 %.3e | native vs torch32 %.3e" % (
+        float((g32 - g64).norm() / g64.norm()), float((gn - g64).norm() / g64.norm()),
+        float((gn - g32).norm() / g32.norm())))
     rows.sort(reverse=True)
     print("native step grads vs torch (rel err, name, |g|):")
     for r in rows[:12]:
