@@ -420,6 +420,213 @@ __global__ __launch_bounds__(256) void bias_grad_kernel(const uint16_t* __restri
   fa_acc_add(o + seg_row(seg, n + 1, 1), a1);
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Large-tile variant for bf16 B operands (the arena's bf16 shadow / activations): 256 × 256 × 64 block tile, 4 waves
+// of 128 × 128 (8 × 8 MFMA 16x16x32 accumulators per wave, 256 accumulator registers — AGPRs at one wave per SIMD),
+// double-buffered LDS (2 × 2 × 36 KiB), register-staged prefetch of the next K-step under the current one's MFMAs.
+// Per K-step a block moves 64 KiB through L2 for 8.4 MFLOP — half the L2 bytes per flop of the 128 × 128 tile,
+// whose ViT shapes were L2-bandwidth bound (~470 TF/s, profiles/r4_vit_bf16_op_attribution.txt).
+constexpr int BB = 256;                 // block tile rows = cols
+constexpr int LDT2 = BB + 16;           // TR tile [64 k][256 cols] row pitch (elements)
+constexpr int TILE2 = BB * LDK;         // ≥ 64 · LDT2: one operand image (36 KiB)
+static_assert(BB * LDK >= 64 * LDT2, "tile image size");
+
+template <int TR>
+__device__ __forceinline__ void load2(uint4 (&r)[8], const uint16_t* __restrict__ S, const Segs& sg, bool seg, int ld,
+                                      int rows, int K, int r0, int k0, int tid) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int v = tid + NT * i;
+    int row, col;
+    bool ok;
+    if (!TR) {
+      row = r0 + (v >> 3);
+      col = k0 + 8 * (v & 7);
+      ok = row < rows && col < K;
+    } else {
+      row = k0 + (v >> 5);
+      col = r0 + 8 * (v & 31);
+      ok = row < K && col < rows;
+    }
+    const int64_t off = seg ? seg_row(sg, row, ld) : (int64_t)row * ld;
+    r[i] = ok ? *reinterpret_cast<const uint4*>(S + off + col) : make_uint4(0, 0, 0, 0);
+  }
+}
+
+template <int TR>
+__device__ __forceinline__ void store2(uint16_t* tile, const uint4 (&r)[8], int tid) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int v = tid + NT * i;
+    const int off = TR ? (v >> 5) * LDT2 + 8 * (v & 31) : (v >> 3) * LDK + 8 * (v & 7);
+    *reinterpret_cast<uint4*>(tile + off) = r[i];
+  }
+}
+
+__device__ __forceinline__ bf16x8 tr_frag2(const uint16_t* tile, int row0, int col0, int lane) {
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const uint16_t* a0 = tile + (row0 + 8 * g + q) * LDT2 + col0 + 4 * p;
+  const v4i16 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a0));
+  const v4i16 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a0 + 4 * LDT2));
+  union {
+    short s[8];
+    bf16x8 b;
+  } u;
+  u.s[0] = r0[0]; u.s[1] = r0[1]; u.s[2] = r0[2]; u.s[3] = r0[3];
+  u.s[4] = r1[0]; u.s[5] = r1[1]; u.s[6] = r1[2]; u.s[7] = r1[3];
+  return u.b;
+}
+
+template <int A_TR, int B_TR, int EPI, int BSEG>
+__global__ __launch_bounds__(NT, 1) void bgemm_big_kernel(const Args p) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+#define SA2(b) (smem + (b) * TILE2)
+#define SB2(b) (smem + (2 + (b)) * TILE2)
+  const int total = p.tiles_m * p.tiles_n * p.nclients;
+  int L = blockIdx.x;
+  if ((total & 7) == 0) L = (L & 7) * (total >> 3) + (L >> 3);   // contiguous tile ranges per XCD
+  const int tn = L % p.tiles_n;
+  const int tm = (L / p.tiles_n) % p.tiles_m;
+  const int c = L / (p.tiles_n * p.tiles_m);
+  const int m0 = tm * BB, n0 = tn * BB;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = (wid >> 1) * 128, wn = (wid & 1) * 128;
+  const uint16_t* A = p.A + (int64_t)c * p.a_bs;
+  const uint16_t* B = (const uint16_t*)p.B + (int64_t)c * p.b_bs + (BSEG ? 0 : p.bseg.off[0]);
+
+  f32x4 acc[8][8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  uint4 ra[8];
+  const int nk = (p.K + BK - 1) / BK;
+  const bool bsum = EPI == EPI_ACC32 && A_TR == 1 && p.bg != nullptr && tn == 0;
+  float bs8[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bs8[e] = 0.f;
+  auto bias_acc = [&]() {   // A (dy) in TR layout: all 8 staging vectors hold columns 8·(tid & 31) .. +7
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t w[4] = {ra[i].x, ra[i].y, ra[i].z, ra[i].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        bs8[2 * e] += bf16_to_f32((uint16_t)(w[e] & 0xffff));
+        bs8[2 * e + 1] += bf16_to_f32((uint16_t)(w[e] >> 16));
+      }
+    }
+  };
+  load2<A_TR>(ra, A, p.bseg, false, p.lda, p.M, p.K, m0, 0, tid);
+  if (bsum) bias_acc();
+  store2<A_TR>(SA2(0), ra, tid);
+  load2<B_TR>(ra, B, p.bseg, BSEG, p.ldb, p.N, p.K, n0, 0, tid);
+  store2<B_TR>(SB2(0), ra, tid);
+  __syncthreads();
+
+  // the next K-step streams through ONE 8-vector staging set: A's loads fly under the first half of this step's
+  // MFMAs and land in the free LDS buffer, then B's under the second half (32 staging registers, not 64)
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) load2<A_TR>(ra, A, p.bseg, false, p.lda, p.M, p.K, m0, (kt + 1) * BK, tid);
+    const uint16_t* ta = SA2(cur);
+    const uint16_t* tb = SB2(cur);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      if (kk == 1 && more) {
+        if (bsum) bias_acc();
+        store2<A_TR>(SA2(cur ^ 1), ra, tid);
+        load2<B_TR>(ra, B, p.bseg, BSEG, p.ldb, p.N, p.K, n0, (kt + 1) * BK, tid);
+      }
+      bf16x8 af[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+        af[i] = A_TR ? tr_frag2(ta, kk * 32, wm + 16 * i, lane)
+                     : row_frag(ta, wm + 16 * i + (lane & 15), kk * 32 + 8 * (lane >> 4));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const bf16x8 bfr = B_TR ? tr_frag2(tb, kk * 32, wn + 16 * j, lane)
+                                : row_frag(tb, wn + 16 * j + (lane & 15), kk * 32 + 8 * (lane >> 4));
+#pragma unroll
+        for (int i = 0; i < 8; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr, af[i], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (more) store2<B_TR>(SB2(cur ^ 1), ra, tid);
+    __syncthreads();
+  }
+
+  if (EPI == EPI_ACC32 && A_TR == 1 && bsum) {
+    float* red = reinterpret_cast<float*>(smem);   // 8 threads per column group (tid >> 5) combine through LDS
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[tid * 8 + e] = bs8[e];
+    __syncthreads();
+    {   // column m0 + tid: group tid >> 3, element tid & 7
+      float t = 0.f;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) t += red[(r * 32 + (tid >> 3)) * 8 + (tid & 7)];
+      const int m = m0 + tid;
+      if (m < p.M) {
+        float* bp = p.bg + (int64_t)c * p.bg_bs + seg_row(p.bgseg, m, 1);
+        *bp = p.acc_store ? t : *bp + t;
+      }
+    }
+  }
+
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wm + 16 * i + (lane & 15);
+    if (m >= p.M) continue;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int n = n0 + wn + 16 * j + 4 * (lane >> 4);
+      if (n >= p.N) continue;
+      f32x4 v = acc[i][j];
+      if (EPI == EPI_ACC32) {
+        float* dst = (float*)p.Cp + (int64_t)c * p.c_bs + seg_row(p.cseg, m, p.ldc) + n;
+        float4 o = make_float4(v[0], v[1], v[2], v[3]);
+        if (!p.acc_store) {
+          const float4 q = *reinterpret_cast<const float4*>(dst);
+          o.x += q.x; o.y += q.y; o.z += q.z; o.w += q.w;
+        }
+        *reinterpret_cast<float4*>(dst) = o;
+      } else {
+        if (p.bias) {
+          const float4 b = *reinterpret_cast<const float4*>(p.bias + (int64_t)c * p.bias_bs + seg_row(p.biasseg, n, 1));
+          v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+        }
+        if (p.R) {
+          const uint2 rr = *reinterpret_cast<const uint2*>(p.R + (int64_t)c * p.r_bs + (int64_t)m * p.ldc + n);
+          const float r4[4] = {bf16_to_f32((uint16_t)(rr.x & 0xffff)), bf16_to_f32((uint16_t)(rr.x >> 16)),
+                               bf16_to_f32((uint16_t)(rr.y & 0xffff)), bf16_to_f32((uint16_t)(rr.y >> 16))};
+          if (EPI == EPI_DGELU) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = gelu_grad(r4[e], v[e]);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += r4[e];
+          }
+        }
+        uint2 o;
+        o.x = pk2(v[0], v[1]);
+        o.y = pk2(v[2], v[3]);
+        *reinterpret_cast<uint2*>((uint16_t*)p.Cp + (int64_t)c * p.c_bs + (int64_t)m * p.ldc + n) = o;
+        if (EPI == EPI_GELU) {
+          float r[4];
+          r[0] = bf16_to_f32((uint16_t)(o.x & 0xffff)); r[1] = bf16_to_f32((uint16_t)(o.x >> 16));
+          r[2] = bf16_to_f32((uint16_t)(o.y & 0xffff)); r[3] = bf16_to_f32((uint16_t)(o.y >> 16));
+          uint2 g;
+          g.x = pk2(gelu_erf(r[0]), gelu_erf(r[1]));
+          g.y = pk2(gelu_erf(r[2]), gelu_erf(r[3]));
+          *reinterpret_cast<uint2*>(p.C2 + (int64_t)c * p.c2_bs + (int64_t)m * p.ldc + n) = g;
+        }
+      }
+    }
+  }
+#undef SA2
+#undef SB2
+}
+
 template <int A_TR, int B_TR, int B_F32, int EPI>
 int launch(const Args& a, hipStream_t st) {
   const int64_t blocks = (int64_t)a.tiles_m * a.tiles_n * a.nclients;
@@ -428,8 +635,25 @@ int launch(const Args& a, hipStream_t st) {
     const char* e = getenv("FEDML_AMD_BGEMM_DB");
     return e ? atoi(e) : 0;
   }();
-  const size_t smem = (db ? 4 : 2) * TILE_ELEMS * sizeof(uint16_t);   // 72 KiB (2 blocks/CU) | 36 KiB (3)
   const bool seg = !B_F32 && a.bseg.n > 1;
+  // bf16 B and enough 256 × 256 tiles to cover the CUs: the large-tile kernel (FEDML_AMD_BGEMM_BIG=0: never)
+  // (read per launch — tests force it per case; a captured graph replays without this host code)
+  const char* big_env = getenv("FEDML_AMD_BGEMM_BIG");
+  const int big = big_env ? atoi(big_env) : 1;
+  if (!B_F32 && big) {
+    Args b = a;
+    b.tiles_m = (a.M + BB - 1) / BB;
+    b.tiles_n = (a.N + BB - 1) / BB;
+    const int64_t nb = (int64_t)b.tiles_m * b.tiles_n * b.nclients;
+    if (nb >= 256 || big == 2) {
+      auto kern = seg ? bgemm_big_kernel<A_TR, B_TR, EPI, 1> : bgemm_big_kernel<A_TR, B_TR, EPI, 0>;
+      const size_t smem2 = 4 * TILE2 * sizeof(uint16_t);   // 144 KiB: one block per CU
+      (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem2);
+      hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(NT), smem2, st, b);
+      return (int)hipGetLastError();
+    }
+  }
+  const size_t smem = (db ? 4 : 2) * TILE_ELEMS * sizeof(uint16_t);   // 72 KiB (2 blocks/CU) | 36 KiB (3)
   auto kern = db ? (seg ? bgemm_kernel<A_TR, B_TR, B_F32, EPI, 1, 1> : bgemm_kernel<A_TR, B_TR, B_F32, EPI, 0, 1>)
                  : (seg ? bgemm_kernel<A_TR, B_TR, B_F32, EPI, 1, 0> : bgemm_kernel<A_TR, B_TR, B_F32, EPI, 0, 0>);
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);

@@ -156,6 +156,21 @@ def _arena_views(C, shapes, seed=0):
                                                (4, 130, 256, [1024], True, True),
                                                (2, 2048, 768, [3072], False, True)])
 def test_client_linear_fwd_bwd(C, M, K, ns, gelu, own, shadow):
+    _linear_case(C, M, K, ns, gelu, own, shadow)
+
+
+@pytest.mark.parametrize("C,M,K,ns,gelu,own", [(3, 200, 768, [768, 768, 768], False, True),
+                                               (2, 300, 768, [3072], True, True),
+                                               (2, 520, 3072, [768], False, False)])
+def test_client_linear_large_tile_kernel(monkeypatch, C, M, K, ns, gelu, own):
+    """bf16-shadow GEMMs forced onto the 256 × 256 tile kernel (FEDML_AMD_BGEMM_BIG=2; by default it takes grids of
+    ≥ 256 such tiles): forward (+GELU, segmented q/k/v rows), data gradient, weight gradient with the fused bias sum,
+    ragged row / reduction extents."""
+    monkeypatch.setenv("FEDML_AMD_BGEMM_BIG", "2")
+    _linear_case(C, M, K, ns, gelu, own, True)
+
+
+def _linear_case(C, M, K, ns, gelu, own, shadow):
     torch.manual_seed(0)
     vs, shs = _arena_views(C, [(n, K) for n in ns] + [(n,) for n in ns])
     ws, bs = vs[:len(ns)], vs[len(ns):]
