@@ -523,7 +523,22 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
 // ---------------------------------------------------------------------------------------------
 // weight gradient
 // ---------------------------------------------------------------------------------------------
+// per-layer operands of a multi-layer weight-gradient launch (conv3x3_wgrad_multi): same geometry, own tensors
+struct WPtrs {
+  const void* g;
+  const void* yv;
+  const float* alpha;
+  const float* beta;
+  const float* gamma;
+  const void* x;
+  const float* ps;
+  const float* pt;
+  float* dw;
+};
+
 struct WArgs {           // activations are P::T
+  const WPtrs* tab;       // multi-layer launch: nl layers × C clients along blockIdx.y (null: one layer, these below)
+  int nl;
   const void* g;          // [C][N][H][W][COUT]
   const void* yv;
   const float* alpha;
@@ -551,7 +566,14 @@ __global__ __launch_bounds__(256, (MAXC <= 8 ? C3W_MIN_WAVES : 1)) void conv3x3_
   constexpr int MT = COUT / 16;
   constexpr int LDX = P::pitch_tr(CIN), LDD = P::pitch_tr(COUT);
   constexpr int K = 9 * CIN;
-  const int c = blockIdx.y;
+  int c = blockIdx.y;
+  if (a.tab) {   // layer l = blockIdx.y / C (uniform: scalar loads of its operand pointers)
+    const int Cc = gridDim.y / a.nl, l = c / Cc;
+    c -= l * Cc;
+    const WPtrs q = a.tab[l];
+    a.g = q.g; a.yv = q.yv; a.alpha = q.alpha; a.beta = q.beta; a.gamma = q.gamma;
+    a.x = q.x; a.ps = q.ps; a.pt = q.pt; a.dw = q.dw;
+  }
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int g = lane >> 4;
@@ -899,13 +921,16 @@ static int conv3x3_bwd_data(const void* g, const void* yv, const float* alpha, c
 template <class P>
 static int conv3x3_wgrad(const void* g, const void* yv, const float* alpha, const float* beta, const float* gamma,
                          const void* x, const float* ps, const float* pt, float* dw, int C, int N, int H, int W,
-                         int Cin, int Cout, int stride, const int* nimg, hipStream_t stream) {
+                         int Cin, int Cout, int stride, const int* nimg, hipStream_t stream,
+                         const WPtrs* tab = nullptr, int nl = 1, int has_ps = 0) {
   if ((stride != 1 && stride != 2) || H % stride || W % stride || Cin != Cout) return -3;
   const int Ho = H / stride, Wo = W / stride;
   if (Wo % 8 != 0 || (Ho * Wo) % 32 != 0) return -3;
   WArgs a = {};
   a.g = g; a.yv = yv; a.alpha = alpha; a.beta = beta; a.gamma = gamma; a.x = x; a.ps = ps; a.pt = pt; a.dw = dw;
-  a.lz0 = fa_take_lazy(0);
+  a.tab = tab; a.nl = nl;
+  a.lz0 = tab ? nullptr : fa_take_lazy(0);
+  if (tab) ps = has_ps ? reinterpret_cast<const float*>(tab) : nullptr;   // selects the prologue variant below
   a.nimg = nimg;
   a.N = N; a.H = Ho; a.W = Wo; a.Hs = H; a.Ws = W;
   // units sized so one unit's operands fit the loaders' register budget (x tile ≤ 8, dy ≤ 4 chunks/thread)
@@ -965,7 +990,7 @@ static int conv3x3_wgrad(const void* g, const void* yv, const float* alpha, cons
     const size_t smem = smem_base > red + vv ? smem_base : red + vv;                                           \
     if (smem > 160 * 1024) return -5;                                                                          \
     (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);       \
-    hipLaunchKernelGGL(kern, dim3(p.gx, C, NZ), dim3(256), smem, stream, a);                                   \
+    hipLaunchKernelGGL(kern, dim3(p.gx, C * nl, NZ), dim3(256), smem, stream, a);                              \
     return (int)hipGetLastError();                                                                             \
   }
 #define W3_ALL(ST)                                                                                             \
@@ -1054,6 +1079,16 @@ FA_EXPORT int fa_conv3x3_wgrad(const uint16_t* g, const uint16_t* yv, const floa
                                hipStream_t stream) {
   return c3::conv3x3_wgrad<c3::BF16>(g, yv, alpha, beta, gamma, x, ps, pt, dw, C, N, H, W, Cin, Cout, stride, nimg,
                                      stream);
+}
+// the same weight gradient for nl layers of one geometry in ONE launch (`tab`: device table of nl WPtrs; has_ps:
+// every layer has the BN + ReLU prologue on x): nl × the workgroups of one layer — the small-grid layers of a
+// 13-client share fill the GPU together
+FA_EXPORT int fa_conv3x3_wgrad_multi_f32(const void* tab, int nl, int has_ps, int C, int N, int H, int W, int Cin,
+                                         int Cout, int stride, const int* nimg, hipStream_t stream) {
+  if (!tab || nl < 1 || nl > 64) return -3;
+  const c3::WPtrs* t = reinterpret_cast<const c3::WPtrs*>(tab);
+  FA_F32_DISPATCH(c3, c3::conv3x3_wgrad<PX>(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                            nullptr, C, N, H, W, Cin, Cout, stride, nimg, stream, t, nl, has_ps));
 }
 FA_EXPORT int fa_conv3x3_wgrad_f32(const float* g, const float* yv, const float* alpha, const float* beta,
                                    const float* gamma, const float* x, const float* ps, const float* pt, float* dw,

@@ -207,6 +207,15 @@ def conv3x3_wgrad(g, yv, alpha, beta, gamma, x, ps, pt, garena, woff, C, N, H, W
     _check(rc, "fa_wgrad_scatter")
 
 
+def conv3x3_wgrad_multi(tab, nl, has_ps, C, N, H, W, Cin, Cout, stride, like, nimg=None):
+    """:func:`conv3x3_wgrad` (scatter=False) of ``nl`` layers of one geometry in one launch: ``tab`` int64 device
+    tensor [nl, 9] of per-layer pointers (g, yv, α, β, γ, x, ps, pt, dw scratch); fp32 only. ``like``: any device
+    tensor (the stream's device)."""
+    rc = _fn("fa_conv3x3_wgrad_multi_f32")(_p(tab), _i(nl), _i(int(has_ps)), _i(C), _i(N), _i(H), _i(W), _i(Cin),
+                                           _i(Cout), _i(stride), _p(nimg), _stream(like))
+    _check(rc, "fa_conv3x3_wgrad_multi")
+
+
 class ScatterSeg(ctypes.Structure):
     _fields_ = [("src_off", ctypes.c_int64), ("woff", ctypes.c_int64), ("cout", ctypes.c_int), ("cin", ctypes.c_int),
                 ("cin_src", ctypes.c_int), ("pad_", ctypes.c_int)]

@@ -171,6 +171,11 @@ class NativeResNetStep:
         # (created here, never inside a graph capture)
         self._side = torch.cuda.Stream(device=self.device) if (self.use_side and self.device.type == "cuda") else None
         self._side_reads = {}    # data_ptr of a gradient buffer a side-stream kernel still reads → its done event
+        # the stride-1 middle 3×3 convs of a stage's bottlenecks get their own dy buffer, and their weight gradients
+        # run as ONE multi-layer launch per stage (conv3x3_wgrad_multi): at 13 clients per GPU each layer alone fills
+        # 0.25-0.4 of the GPU's workgroup slots
+        self.use_wgrad_batch = os.environ.get("FEDML_AMD_C3W_BATCH", "1") != "0" and dtype == torch.float32
+        self._wb_tabs = {}       # (geometry, layer keys) → device table of per-layer operand pointers
         # deferred BN finalisation (csrc/bnlazy.h): the first consumer kernel folds the statistics itself
         self.use_lazy = os.environ.get("FEDML_AMD_BN_LAZY", "1") != "0"
         self._pending = {}       # (bn key, "f" | "b") → explicit finalisation closure, while deferred
@@ -283,6 +288,10 @@ class NativeResNetStep:
             b.yd = act(b.ds_conv.Ho, b.ds_conv.Wo, b.ds_conv.cout) if b.ds_conv is not None else None
             last = b.convs[-1]
             b.out = act(last.Ho, last.Wo, last.cout)
+            mid = b.convs[1] if len(b.convs) == 3 else None
+            b.wb = (mid is not None and self.use_wgrad_batch and mid.stride == 1 and self._c3(mid)
+                    and not self._s2k(mid))
+            b.g3 = act(mid.Ho, mid.Wo, mid.cout) if b.wb else None
             for cv in b.convs + ([b.ds_conv] if b.ds_conv else []):
                 maxel = max(maxel, cv.H * cv.W * cv.cin_pad, cv.Ho * cv.Wo * cv.cout)
         # gradient scratch: block-output g (kept until the block's conv0 is done), two ping-pong
@@ -376,14 +385,14 @@ class NativeResNetStep:
 
     def _snapshot(self):
         st = {k: getattr(self, k) for k in self._STATE_ATTRS}
-        st["blocks"] = [(b.ys, b.yd, b.out) for b in self.blocks]
+        st["blocks"] = [(b.ys, b.yd, b.out, b.wb, b.g3) for b in self.blocks]
         return st
 
     def _restore(self, st):
         for k in self._STATE_ATTRS:
             setattr(self, k, st[k])
-        for b, (ys, yd, out) in zip(self.blocks, st["blocks"]):
-            b.ys, b.yd, b.out = ys, yd, out
+        for b, (ys, yd, out, wb, g3) in zip(self.blocks, st["blocks"]):
+            b.ys, b.yd, b.out, b.wb, b.g3 = ys, yd, out, wb, g3
 
     def _all_bns(self):
         yield self.stem[1]
@@ -498,6 +507,28 @@ class NativeResNetStep:
             if t.data_ptr() not in self._side_reads:
                 return t
         return cands[0]
+
+    def _wb_flush(self, pend, garena, N):
+        """One multi-layer weight-gradient launch for the pending stride-1 middle 3×3 convs of a stage (each with
+        its own dy buffer ``b.g3``; their BN backward rows were finalised explicitly)."""
+        if not pend:
+            return
+        cv0 = pend[0][0]
+        key = (self.geom, tuple(cv.key for cv, _ in pend), garena.data_ptr())
+        tab = self._wb_tabs.get(key)
+        if tab is None:
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("native step: a new batched weight-gradient table while capturing a graph")
+            rows = []
+            for cv, b in pend:
+                v, pv = self.bn_vec[b.bns[1].key], self.bn_vec[b.bns[0].key]
+                dw = self.dw_c3[self._c3_off[cv.key]:]
+                rows.append([b.g3.data_ptr(), b.ys[1].data_ptr(), v[4].data_ptr(), v[5].data_ptr(), v[6].data_ptr(),
+                             b.ys[0].data_ptr(), pv[0].data_ptr(), pv[1].data_ptr(), dw.data_ptr()])
+            tab = self._wb_tabs[key] = torch.tensor(rows, dtype=torch.int64).to(self.device)
+        nn_ops.conv3x3_wgrad_multi(tab, len(pend), True, self.C, N, cv0.H, cv0.W, cv0.cin_pad, cv0.cout, 1,
+                                   self.dw_c3, nimg=self._nimg)
+        pend.clear()
 
     def _side_join(self):
         if self._side is not None:
@@ -748,9 +779,13 @@ class NativeResNetStep:
                         fh * fw, chl, 3, nimg=self._nimg)
         # head_bwd wrote (Σg, Σg·y_last, Σg·yd) into the last BN's bwd stats; the downsample BN needs
         # (Σg, Σg·yd) → copy slots into its own stats buffer below (same g)
+        wb_pend = []      # (conv, block) of the stage's batched 3×3 weight gradients
         for bi in range(len(self.blocks) - 1, -1, -1):
             b = self.blocks[bi]
             prev_block = self.blocks[bi - 1] if bi > 0 else None
+            if wb_pend and (not b.wb or (b.convs[1].H, b.convs[1].cin_pad) != (wb_pend[0][0].H,
+                                                                               wb_pend[0][0].cin_pad)):
+                self._wb_flush(wb_pend, garena, N)
             lbn = b.bns[-1]
             last = b.convs[-1]
             hw_last = last.Ho * last.Wo
@@ -781,7 +816,10 @@ class NativeResNetStep:
                 v = self.bn_vec[bn.key]
                 pv = self.bn_vec[b.bns[j - 1].key]
                 M = N * cv.Ho * cv.Wo
-                out_g = self._claim(self._pick([t for t in free[:2] if t is not g_j]))
+                if b.wb and j == len(b.convs) - 1:
+                    out_g = b.g3      # the middle conv's dy, kept for the stage's batched weight gradient
+                else:
+                    out_g = self._claim(self._pick([t for t in free[:2] if t is not g_j]))
                 if (b.ry or b.ryb) and j == len(b.convs) - 1:
                     nn_ops.conv1x1_bwd_fused_ry(g_j, v[4], v[5], v[6], v[8], self.packed.view(-1)[cv.off_b:],
                                                 self.packed_ld, cv.ldk2, b.ys[j - 1], pv[0], pv[1], out_g,
@@ -803,7 +841,11 @@ class NativeResNetStep:
                     self._dump(f"{cv.key}.dx", out_g, C * N * cv.H * cv.W * cv.cin)
                     continue
                 dg, dyv, al, be, ga = self._dy(cv, g_j, b.ys[j], v, N, bn_key=bn.key)
-                self._wgrad(cv, dg, dyv, (al, be, ga), b.ys[j - 1], pv, garena, N, bn_key=bn.key)
+                if b.wb and j == 1:
+                    self._flush(bn.key, "b")          # explicit: the batched launch and the dgrad read the rows
+                    wb_pend.append((cv, b))
+                else:
+                    self._wgrad(cv, dg, dyv, (al, be, ga), b.ys[j - 1], pv, garena, N, bn_key=bn.key)
                 self._flush(bn.key, "b")
                 if self._c3(cv) and not self._s2k(cv):
                     nn_ops.conv3x3_bwd_data(g_j, b.ys[j], v[4], v[5], v[6], self.packed.view(-1)[cv.off_b:],
@@ -885,6 +927,7 @@ class NativeResNetStep:
         self._bn_bwd(st_bn, 1, N, st_conv.Ho * st_conv.Wo, arena, garena)
         v = self.bn_vec[st_bn.key]
         self._wgrad(st_conv, gpre, self.stem_y, v, self.x_in, None, garena, N, bn_key=st_bn.key)
+        self._wb_flush(wb_pend, garena, N)
         self._flush_all()
         self._side_join()
         if self.c3_nseg:

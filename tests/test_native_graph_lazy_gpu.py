@@ -33,9 +33,9 @@ def _store():
                              torch.randint(0, 10, (n,), generator=g).to(DEV), offs, COUNTS)
 
 
-def _run(graphs: bool, lazy: bool, det: bool = False, momentum: float = 0.9, side: bool = True):
+def _run(graphs: bool, lazy: bool, det: bool = False, momentum: float = 0.9, side: bool = True, layers=(1, 1, 1)):
     torch.manual_seed(0)
-    model = ResNet(Bottleneck, [1, 1, 1], 10)
+    model = ResNet(Bottleneck, list(layers), 10)
     args = Arguments.from_dict({"x": {"client_optimizer": "sgd", "learning_rate": 0.02, "momentum": momentum,
                                       "deterministic": det}})
     eng = ClientBatchEngine(copy.deepcopy(model).to(DEV), 4, DEV, args, compute_dtype=None)
@@ -101,3 +101,19 @@ def test_side_stream_weight_gradients_match_single_stream():
     rel = float((got - ref).norm() / ref.norm())
     assert torch.isfinite(got).all()
     assert rel < max(10 * spread, 3e-3), (rel, spread)
+
+
+def test_batched_middle_conv_weight_gradients_bitwise(monkeypatch):
+    """FEDML_AMD_C3W_BATCH: a stage's stride-1 middle 3×3 weight gradients as ONE multi-layer launch (own dy buffer
+    per block) — the same per-layer work split and fixed-point sums, so deterministic mode must match the per-layer
+    launches bit for bit, across rounds, ragged geometries and graph replays."""
+    from fedml_amd.utils import determinism
+    try:
+        monkeypatch.setenv("FEDML_AMD_C3W_BATCH", "0")
+        a, _, _ = _run(graphs=True, lazy=False, det=True, layers=(3, 2, 2))
+        monkeypatch.setenv("FEDML_AMD_C3W_BATCH", "1")
+        b, _, _ = _run(graphs=True, lazy=False, det=True, layers=(3, 2, 2))
+    finally:
+        determinism.disable()
+    assert torch.isfinite(a).all()
+    assert torch.equal(a, b), float((a - b).norm() / a.norm())
