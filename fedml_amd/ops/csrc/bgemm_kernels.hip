@@ -73,6 +73,7 @@ struct Args {
   int M, N, K;
   int tiles_m, tiles_n, nclients;
   int acc_store;     // EPI_ACC32: the rows' first (only) writer — store instead of += (no zero fill of those rows)
+  int64_t a_bytes, b_bytes;   // LDS-DMA kernel: per-client operand extents its buffer descriptors bound
 };
 
 // Constant-index selects only: a runtime index into the by-value kernel-argument struct would be lowered to
@@ -421,53 +422,31 @@ __global__ __launch_bounds__(256) void bias_grad_kernel(const uint16_t* __restri
 }
 
 // ---------------------------------------------------------------------------------------------------------------
-// Large-tile variant for bf16 B operands (the arena's bf16 shadow / activations): 256 × 256 × 64 block tile, 4 waves
-// of 128 × 128 (8 × 8 MFMA 16x16x32 accumulators per wave, 256 accumulator registers — AGPRs at one wave per SIMD),
-// double-buffered LDS (2 × 2 × 36 KiB), register-staged prefetch of the next K-step under the current one's MFMAs.
-// Per K-step a block moves 64 KiB through L2 for 8.4 MFLOP — half the L2 bytes per flop of the 128 × 128 tile,
-// whose ViT shapes were L2-bandwidth bound (~470 TF/s, profiles/r4_vit_bf16_op_attribution.txt).
-constexpr int BB = 256;                 // block tile rows = cols
-constexpr int LDT2 = BB + 16;           // TR tile [64 k][256 cols] row pitch (elements)
-constexpr int TILE2 = BB * LDK;         // ≥ 64 · LDT2: one operand image (36 KiB)
-static_assert(BB * LDK >= 64 * LDT2, "tile image size");
+// LDS-DMA variant for bf16 operands (activations, the arena's bf16 shadow): the same 128 × 128 × 64 block tile and
+// wave layout, but the tiles travel global → LDS by `buffer_load_dwordx4 … lds` (no staging registers, no
+// ds_write pass). The LDS image is lane-linear per wave instruction, so bank spreading is an XOR swizzle of the
+// SOURCE address: K-major [128 rows][64 k] images put 16-B chunk q of row r at q ^ ((r >> 1) & 7) (ds_read_b128
+// conflict-free), TR [64 k][128 cols] images put 32-B chunk h of row r at h ^ ((r & 3) | ((r >> 1) & 4))
+// (ds_read_b64_tr_b16 conflict-free). Buffer descriptors bound each client's operand: reads past it return 0, which
+// zero-fills the reduction tail of the weight gradient (T % 64) and every ragged row for free.
+// DB = 1: two images per operand (64 KiB), next K-step's DMA in flight under this one's MFMAs;
+// DB = 0: one image (32 KiB, more blocks per CU), load → wait → compute.
+constexpr int GIMG = 128 * 64;   // elements of one operand image (16 KiB)
 
-template <int TR>
-__device__ __forceinline__ void load2(uint4 (&r)[8], const uint16_t* __restrict__ S, const Segs& sg, bool seg, int ld,
-                                      int rows, int K, int r0, int k0, int tid) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int v = tid + NT * i;
-    int row, col;
-    bool ok;
-    if (!TR) {
-      row = r0 + (v >> 3);
-      col = k0 + 8 * (v & 7);
-      ok = row < rows && col < K;
-    } else {
-      row = k0 + (v >> 5);
-      col = r0 + 8 * (v & 31);
-      ok = row < K && col < rows;
-    }
-    const int64_t off = seg ? seg_row(sg, row, ld) : (int64_t)row * ld;
-    r[i] = ok ? *reinterpret_cast<const uint4*>(S + off + col) : make_uint4(0, 0, 0, 0);
-  }
+__device__ __forceinline__ int swz_nt(int r, int q) { return q ^ ((r >> 1) & 7); }
+__device__ __forceinline__ int swz_tr(int r, int h) { return h ^ ((r & 3) | ((r >> 1) & 4)); }
+
+__device__ __forceinline__ bf16x8 row_frag_s(const uint16_t* tile, int row, int q) {
+  return *reinterpret_cast<const bf16x8*>(tile + row * 64 + 8 * swz_nt(row, q));
 }
 
-template <int TR>
-__device__ __forceinline__ void store2(uint16_t* tile, const uint4 (&r)[8], int tid) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const int v = tid + NT * i;
-    const int off = TR ? (v >> 5) * LDT2 + 8 * (v & 31) : (v >> 3) * LDK + 8 * (v & 7);
-    *reinterpret_cast<uint4*>(tile + off) = r[i];
-  }
-}
-
-__device__ __forceinline__ bf16x8 tr_frag2(const uint16_t* tile, int row0, int col0, int lane) {
+__device__ __forceinline__ bf16x8 tr_frag_s(const uint16_t* tile, int row0, int col0, int lane) {
   const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
-  const uint16_t* a0 = tile + (row0 + 8 * g + q) * LDT2 + col0 + 4 * p;
+  const int r = row0 + 8 * g + q, h = col0 >> 4;
+  const uint16_t* a0 = tile + r * 128 + 16 * swz_tr(r, h) + 4 * p;
+  const uint16_t* a1 = tile + (r + 4) * 128 + 16 * swz_tr(r + 4, h) + 4 * p;
   const v4i16 r0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a0));
-  const v4i16 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a0 + 4 * LDT2));
+  const v4i16 r1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16*)(a1));
   union {
     short s[8];
     bf16x8 b;
@@ -477,108 +456,150 @@ __device__ __forceinline__ bf16x8 tr_frag2(const uint16_t* tile, int row0, int c
   return u.b;
 }
 
-template <int A_TR, int B_TR, int EPI, int BSEG>
-__global__ __launch_bounds__(NT, 1) void bgemm_big_kernel(const Args p) {
+// per-lane byte offsets (relative to the K-step's first reduction row / column) of the 4 DMA instructions a wave
+// issues for one operand image; instruction i of wave w fills LDS bytes [(4w + i)·1 KiB, +1 KiB)
+template <int TR>
+__device__ __forceinline__ void dma_offsets(uint32_t (&vo)[4], const Segs& sg, bool seg, int ld, int r0, int wid,
+                                            int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int P = (wid * 4 + i) * 1024 + lane * 16;
+    if (!TR) {   // image row r = logical row r0 + r (an output row / col), stored chunk → source chunk
+      const int r = P >> 7;
+      const int q = ((P >> 4) & 7) ^ ((r >> 1) & 7);
+      const int64_t row = seg ? seg_row(sg, r0 + r, ld) : (int64_t)(r0 + r) * ld;
+      vo[i] = (uint32_t)((row + 8 * q) * 2);
+    } else {     // image row r = reduction row k0 + r, cols r0 .. r0 + 127
+      const int r = P >> 8;
+      const int h = ((P >> 5) & 7) ^ ((r & 3) | ((r >> 1) & 4));
+      const int col = r0 + 16 * h + 8 * ((P >> 4) & 1);
+      vo[i] = (uint32_t)(((int64_t)r * ld + col) * 2);
+    }
+  }
+}
+
+template <int A_TR, int B_TR, int EPI, int BSEG, int DB>
+__global__ __launch_bounds__(NT, 2) void bgemm_dma_kernel(const Args p) {
   extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
-#define SA2(b) (smem + (b) * TILE2)
-#define SB2(b) (smem + (2 + (b)) * TILE2)
+  // [A img 0][B img 0]([A img 1][B img 1])
   const int total = p.tiles_m * p.tiles_n * p.nclients;
   int L = blockIdx.x;
-  if ((total & 7) == 0) L = (L & 7) * (total >> 3) + (L >> 3);   // contiguous tile ranges per XCD
+  {   // contiguous tile ranges per XCD (bijective for any total)
+    const int q = total >> 3, r = total & 7, x = L & 7;
+    L = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (L >> 3);
+  }
   const int tn = L % p.tiles_n;
   const int tm = (L / p.tiles_n) % p.tiles_m;
   const int c = L / (p.tiles_n * p.tiles_m);
-  const int m0 = tm * BB, n0 = tn * BB;
+  const int m0 = tm * BM, n0 = tn * BN;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = (wid >> 1) * 128, wn = (wid & 1) * 128;
-  const uint16_t* A = p.A + (int64_t)c * p.a_bs;
-  const uint16_t* B = (const uint16_t*)p.B + (int64_t)c * p.b_bs + (BSEG ? 0 : p.bseg.off[0]);
+  const int wm = (wid >> 1) * 64, wn = (wid & 1) * 64;
 
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // descriptors from PROVABLY wave-uniform inputs (readfirstlane), else hipcc wraps every buffer op in a waterfall
+  // loop (cdna_hip_programming.md T20)
+  auto rsrc = [](const void* base, int64_t bytes) {
+    const uint64_t a = (uint64_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const int nb = __builtin_amdgcn_readfirstlane((int)bytes);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, nb, 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t ra = rsrc(p.A + (int64_t)c * p.a_bs, p.a_bytes);
+  const __amdgpu_buffer_rsrc_t rb = rsrc((const uint16_t*)p.B + (int64_t)c * p.b_bs, p.b_bytes);
+  uint32_t voa[4], vob[4];
+  dma_offsets<A_TR>(voa, p.bseg, false, p.lda, m0, wid, lane);
+  dma_offsets<B_TR>(vob, p.bseg, BSEG && !B_TR, p.ldb, n0, wid, lane);
 
-  uint4 ra[8];
-  const int nk = (p.K + BK - 1) / BK;
-  const bool bsum = EPI == EPI_ACC32 && A_TR == 1 && p.bg != nullptr && tn == 0;
-  float bs8[8];
+  auto issue = [&](int kt, int buf) {
+    const int k0 = kt * BK;
+    // uniform advance of the K-step: along the row (K-major) or down the rows (TR; a segmented TR operand's 64
+    // reduction rows sit inside one segment — the host checks the boundaries)
+    const uint32_t sa = __builtin_amdgcn_readfirstlane(A_TR ? (uint32_t)((int64_t)k0 * p.lda * 2) : (uint32_t)(k0 * 2));
+    const uint32_t sb = __builtin_amdgcn_readfirstlane(
+        B_TR ? (uint32_t)((BSEG ? seg_row(p.bseg, k0, p.ldb) : (int64_t)k0 * p.ldb) * 2) : (uint32_t)(k0 * 2));
+    uint16_t* ia = smem + (DB ? buf : 0) * 2 * GIMG;
+    uint16_t* ib = ia + GIMG;
 #pragma unroll
-  for (int e = 0; e < 8; ++e) bs8[e] = 0.f;
-  auto bias_acc = [&]() {   // A (dy) in TR layout: all 8 staging vectors hold columns 8·(tid & 31) .. +7
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint32_t w[4] = {ra[i].x, ra[i].y, ra[i].z, ra[i].w};
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        bs8[2 * e] += bf16_to_f32((uint16_t)(w[e] & 0xffff));
-        bs8[2 * e + 1] += bf16_to_f32((uint16_t)(w[e] >> 16));
-      }
+    for (int i = 0; i < 4; ++i) {
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(ra, (__attribute__((address_space(3))) void*)(ia + (wid * 4 + i) * 512),
+                                               16, voa[i], sa, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb, (__attribute__((address_space(3))) void*)(ib + (wid * 4 + i) * 512),
+                                               16, vob[i], sb, 0, 0);
     }
   };
-  load2<A_TR>(ra, A, p.bseg, false, p.lda, p.M, p.K, m0, 0, tid);
-  if (bsum) bias_acc();
-  store2<A_TR>(SA2(0), ra, tid);
-  load2<B_TR>(ra, B, p.bseg, BSEG, p.ldb, p.N, p.K, n0, 0, tid);
-  store2<B_TR>(SB2(0), ra, tid);
-  __syncthreads();
 
-  // the next K-step streams through ONE 8-vector staging set: A's loads fly under the first half of this step's
-  // MFMAs and land in the free LDS buffer, then B's under the second half (32 staging registers, not 64)
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = (p.K + BK - 1) / BK;
+  // weight gradient with a fused bias gradient: the first column-block of every row-block sums its A (dy) images
+  const bool bsum = EPI == EPI_ACC32 && A_TR == 1 && p.bg != nullptr && tn == 0;
+  float bs = 0.f;
+
+  if (DB) {
+    issue(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    const bool more = kt + 1 < nk;
-    if (more) load2<A_TR>(ra, A, p.bseg, false, p.lda, p.M, p.K, m0, (kt + 1) * BK, tid);
-    const uint16_t* ta = SA2(cur);
-    const uint16_t* tb = SB2(cur);
+    const int cur = DB ? (kt & 1) : 0;
+    if (DB) {
+      if (kt + 1 < nk) issue(kt + 1, cur ^ 1);
+    } else {
+      issue(kt, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    const uint16_t* ta = smem + cur * 2 * GIMG;
+    const uint16_t* tb = ta + GIMG;
+    if (bsum) {   // column tid & 127 of the dy image, rows 32·(tid >> 7) .. +31
+      const int col = tid & 127;
+#pragma unroll 8
+      for (int r = 32 * (tid >> 7); r < 32 * (tid >> 7) + 32; ++r)
+        bs += bf16_to_f32(ta[r * 128 + 16 * swz_tr(r, col >> 4) + (col & 15)]);
+    }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      if (kk == 1 && more) {
-        if (bsum) bias_acc();
-        store2<A_TR>(SA2(cur ^ 1), ra, tid);
-        load2<B_TR>(ra, B, p.bseg, BSEG, p.ldb, p.N, p.K, n0, (kt + 1) * BK, tid);
-      }
-      bf16x8 af[8];
+      bf16x8 af[4], bfr[4];
 #pragma unroll
-      for (int i = 0; i < 8; ++i)
-        af[i] = A_TR ? tr_frag2(ta, kk * 32, wm + 16 * i, lane)
-                     : row_frag(ta, wm + 16 * i + (lane & 15), kk * 32 + 8 * (lane >> 4));
+      for (int i = 0; i < 4; ++i)
+        af[i] = A_TR ? tr_frag_s(ta, kk * 32, wm + 16 * i, lane)
+                     : row_frag_s(ta, wm + 16 * i + (lane & 15), kk * 4 + (lane >> 4));
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const bf16x8 bfr = B_TR ? tr_frag2(tb, kk * 32, wn + 16 * j, lane)
-                                : row_frag(tb, wn + 16 * j + (lane & 15), kk * 32 + 8 * (lane >> 4));
+      for (int j = 0; j < 4; ++j)
+        bfr[j] = B_TR ? tr_frag_s(tb, kk * 32, wn + 16 * j, lane)
+                      : row_frag_s(tb, wn + 16 * j + (lane & 15), kk * 4 + (lane >> 4));
 #pragma unroll
-        for (int i = 0; i < 8; ++i) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr, af[i], acc[i][j], 0, 0, 0);
-      }
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
-    if (more) store2<B_TR>(SB2(cur ^ 1), ra, tid);
-    __syncthreads();
+    if (DB) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next image has landed (this wave's part)
+    __syncthreads();    // ... every wave's part; and nobody reads the image the next DMA overwrites
   }
 
   if (EPI == EPI_ACC32 && A_TR == 1 && bsum) {
-    float* red = reinterpret_cast<float*>(smem);   // 8 threads per column group (tid >> 5) combine through LDS
-#pragma unroll
-    for (int e = 0; e < 8; ++e) red[tid * 8 + e] = bs8[e];
+    float* red = reinterpret_cast<float*>(smem);
+    red[tid] = bs;
     __syncthreads();
-    {   // column m0 + tid: group tid >> 3, element tid & 7
-      float t = 0.f;
-#pragma unroll
-      for (int r = 0; r < 8; ++r) t += red[(r * 32 + (tid >> 3)) * 8 + (tid & 7)];
+    if (tid < 128) {
       const int m = m0 + tid;
       if (m < p.M) {
         float* bp = p.bg + (int64_t)c * p.bg_bs + seg_row(p.bgseg, m, 1);
+        const float t = red[tid] + red[tid + 128];
         *bp = p.acc_store ? t : *bp + t;
       }
     }
   }
 
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
+  for (int i = 0; i < 4; ++i) {
     const int m = m0 + wm + 16 * i + (lane & 15);
     if (m >= p.M) continue;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < 4; ++j) {
       const int n = n0 + wn + 16 * j + 4 * (lane >> 4);
       if (n >= p.N) continue;
       f32x4 v = acc[i][j];
@@ -623,8 +644,17 @@ __global__ __launch_bounds__(NT, 1) void bgemm_big_kernel(const Args p) {
       }
     }
   }
-#undef SA2
-#undef SB2
+}
+
+// operand extent (bytes from the client's base) the DMA descriptors bound: rows × ld of a plain matrix, or the end
+// of the last segment row
+inline int64_t seg_extent(const Segs& s, int rows, int ld) {
+  int64_t e = 0;
+  for (int i = 0; i < s.n; ++i) {
+    const int lo = s.lo[i], hi = (i + 1 < s.n) ? s.lo[i + 1] : rows;
+    e = std::max<int64_t>(e, s.off[i] + (int64_t)(hi - lo) * ld);
+  }
+  return e * 2;
 }
 
 template <int A_TR, int B_TR, int B_F32, int EPI>
@@ -636,20 +666,25 @@ int launch(const Args& a, hipStream_t st) {
     return e ? atoi(e) : 0;
   }();
   const bool seg = !B_F32 && a.bseg.n > 1;
-  // bf16 B and enough 256 × 256 tiles to cover the CUs: the large-tile kernel (FEDML_AMD_BGEMM_BIG=0: never)
-  // (read per launch — tests force it per case; a captured graph replays without this host code)
-  const char* big_env = getenv("FEDML_AMD_BGEMM_BIG");
-  const int big = big_env ? atoi(big_env) : 1;
-  if (!B_F32 && big) {
+  // bf16 operands: the LDS-DMA kernel (FEDML_AMD_BGEMM_DMA=0: never; 1: double-buffered; 2: single image)
+  const char* dma_env = getenv("FEDML_AMD_BGEMM_DMA");
+  const int dma = dma_env ? atoi(dma_env) : 1;
+  if (!B_F32 && dma) {
     Args b = a;
-    b.tiles_m = (a.M + BB - 1) / BB;
-    b.tiles_n = (a.N + BB - 1) / BB;
-    const int64_t nb = (int64_t)b.tiles_m * b.tiles_n * b.nclients;
-    if (nb >= 256 || big == 2) {
-      auto kern = seg ? bgemm_big_kernel<A_TR, B_TR, EPI, 1> : bgemm_big_kernel<A_TR, B_TR, EPI, 0>;
-      const size_t smem2 = 4 * TILE2 * sizeof(uint16_t);   // 144 KiB: one block per CU
+    // A: [M][lda] (K-major) or [K][lda] (TR); B: [N][ldb] / segments (K-major) or [K][ldb] / segments (TR)
+    b.a_bytes = (int64_t)(A_TR ? a.K : a.M) * a.lda * 2;
+    const int brows = B_TR ? a.K : a.N;
+    b.b_bytes = seg_extent(a.bseg, brows, a.ldb);
+    bool ok = b.a_bytes < (1ll << 31) && b.b_bytes < (1ll << 31);
+    if (B_TR && seg)   // a K-step's 64 reduction rows must not straddle a segment boundary
+      for (int i = 1; i < a.bseg.n; ++i) ok = ok && (a.bseg.lo[i] % BK == 0);
+    if (ok) {
+      auto pick = [&](auto k1, auto k0) { return dma == 2 ? k0 : k1; };
+      auto kern = seg ? pick(bgemm_dma_kernel<A_TR, B_TR, EPI, 1, 1>, bgemm_dma_kernel<A_TR, B_TR, EPI, 1, 0>)
+                      : pick(bgemm_dma_kernel<A_TR, B_TR, EPI, 0, 1>, bgemm_dma_kernel<A_TR, B_TR, EPI, 0, 0>);
+      const size_t smem2 = (dma == 2 ? 2 : 4) * GIMG * sizeof(uint16_t);
       (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem2);
-      hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(NT), smem2, st, b);
+      hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(NT), smem2, st, b);
       return (int)hipGetLastError();
     }
   }

@@ -159,14 +159,15 @@ def test_client_linear_fwd_bwd(C, M, K, ns, gelu, own, shadow):
     _linear_case(C, M, K, ns, gelu, own, shadow)
 
 
+@pytest.mark.parametrize("dma", ["0", "1", "2"])
 @pytest.mark.parametrize("C,M,K,ns,gelu,own", [(3, 200, 768, [768, 768, 768], False, True),
                                                (2, 300, 768, [3072], True, True),
                                                (2, 520, 3072, [768], False, False)])
-def test_client_linear_large_tile_kernel(monkeypatch, C, M, K, ns, gelu, own):
-    """bf16-shadow GEMMs forced onto the 256 × 256 tile kernel (FEDML_AMD_BGEMM_BIG=2; by default it takes grids of
-    ≥ 256 such tiles): forward (+GELU, segmented q/k/v rows), data gradient, weight gradient with the fused bias sum,
-    ragged row / reduction extents."""
-    monkeypatch.setenv("FEDML_AMD_BGEMM_BIG", "2")
+def test_client_linear_dma_kernel(monkeypatch, dma, C, M, K, ns, gelu, own):
+    """bf16-shadow GEMMs on the LDS-DMA kernel (FEDML_AMD_BGEMM_DMA 1: double-buffered images, 2: one image) and on
+    the register-staged kernel (0): forward (+GELU, segmented q/k/v rows), data gradient (segmented TR weight rows),
+    weight gradient with the fused bias sum; ragged row and reduction extents (zero-filled by the descriptors)."""
+    monkeypatch.setenv("FEDML_AMD_BGEMM_DMA", dma)
     _linear_case(C, M, K, ns, gelu, own, True)
 
 
