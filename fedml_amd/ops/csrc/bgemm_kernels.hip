@@ -666,9 +666,11 @@ int launch(const Args& a, hipStream_t st) {
     return e ? atoi(e) : 0;
   }();
   const bool seg = !B_F32 && a.bseg.n > 1;
-  // bf16 operands: the LDS-DMA kernel (FEDML_AMD_BGEMM_DMA=0: never; 1: double-buffered; 2: single image)
+  // bf16 operands: the LDS-DMA kernel (FEDML_AMD_BGEMM_DMA=0: never; 1: double-buffered; 2: single image, default)
+  // (single image measured faster: ViT-B/16 bf16 3.84 vs 3.50 rounds/s double-buffered, 3.71 register-staged;
+  // profiles/r5_bgemm_dma_micro.txt)
   const char* dma_env = getenv("FEDML_AMD_BGEMM_DMA");
-  const int dma = dma_env ? atoi(dma_env) : 1;
+  const int dma = dma_env ? atoi(dma_env) : 2;
   if (!B_F32 && dma) {
     Args b = a;
     // A: [M][lda] (K-major) or [K][lda] (TR); B: [N][ldb] / segments (K-major) or [K][ldb] / segments (TR)
@@ -676,6 +678,8 @@ int launch(const Args& a, hipStream_t st) {
     const int brows = B_TR ? a.K : a.N;
     b.b_bytes = seg_extent(a.bseg, brows, a.ldb);
     bool ok = b.a_bytes < (1ll << 31) && b.b_bytes < (1ll << 31);
+    // a K-major operand's reduction runs along its rows: a K tail would read the next row, not zeros
+    if ((!A_TR || !B_TR) && a.K % BK != 0) ok = false;
     if (B_TR && seg)   // a K-step's 64 reduction rows must not straddle a segment boundary
       for (int i = 1; i < a.bseg.n; ++i) ok = ok && (a.bseg.lo[i] % BK == 0);
     if (ok) {

@@ -1,4 +1,4 @@
-// Fused classifier head of the client-batched ResNet step (fp32, one workgroup per client):
+// Fused classifier head of the client-batched ResNet step (fp32, one 1024-thread workgroup per client):
 //
 //   Z  = P·Wᵀ + b                        logits            P [N][F] pooled features, W [K][F], b [K] (arena)
 //   dl = rs·(softmax(Z) − onehot(y))     CE backward       rs = the row's scale (1/batch, 0 for padding rows)
@@ -13,7 +13,10 @@
 
 namespace fch {
 
-__global__ __launch_bounds__(256) void fc_head_xent_kernel(const float* __restrict__ pooled,
+constexpr int kThreads = 1024;   // 16 waves: the phases are latency-bound chains of W / LDS reads (one block per
+                                 // client: 13 per GPU at the 8-GPU headline share), 4× the 256-thread block's waves
+
+__global__ __launch_bounds__(kThreads) void fc_head_xent_kernel(const float* __restrict__ pooled,
                                                            const float* __restrict__ arena, int64_t lda, int64_t ow,
                                                            int64_t ob, const int64_t* __restrict__ labels,
                                                            const float* __restrict__ row_scale,
@@ -25,21 +28,21 @@ __global__ __launch_bounds__(256) void fc_head_xent_kernel(const float* __restri
   const int FP = F + 4;                 // padded row: float4 reads of 64 rows hit distinct bank groups
   float* P = sm;                        // [N][FP]
   float* Z = sm + (size_t)N * FP;       // [N][K]: logits, then dl
-  __shared__ float red[4];
+  __shared__ float red[kThreads / 64];
   const int c = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const float* Pg = pooled + (int64_t)c * N * F;
   const float* W = arena + (int64_t)c * lda + ow;
   const float* b = arena + (int64_t)c * lda + ob;
   const int F4 = F >> 2;
-  for (int i = tid; i < N * F4; i += 256) {
+  for (int i = tid; i < N * F4; i += kThreads) {
     const int n = i / F4, f = (i - n * F4) * 4;
     *reinterpret_cast<float4*>(P + n * FP + f) = *reinterpret_cast<const float4*>(Pg + (int64_t)n * F + f);
   }
   __syncthreads();
   // logits: a thread owns 4 consecutive classes of one row; lanes run over rows (W loads are wave-uniform)
   const int K4 = (K + 3) >> 2;
-  for (int i = tid; i < N * K4; i += 256) {
+  for (int i = tid; i < N * K4; i += kThreads) {
     const int kq = i / N, n = i - kq * N, k0 = kq * 4;
     float acc0 = 0.f, acc1 = 0.f, acc2 = 0.f, acc3 = 0.f;
     const float* pr = P + n * FP;
@@ -67,7 +70,7 @@ __global__ __launch_bounds__(256) void fc_head_xent_kernel(const float* __restri
   __syncthreads();
   // softmax cross-entropy, one wave per row; Z becomes dl in place
   float lsum = 0.f;
-  for (int n = wv; n < N; n += 4) {
+  for (int n = wv; n < N; n += kThreads / 64) {
     float* zr = Z + n * K;
     const float rs = row_scale[(int64_t)c * N + n];
     const int64_t lbl = labels[(int64_t)c * N + n];
@@ -88,10 +91,14 @@ __global__ __launch_bounds__(256) void fc_head_xent_kernel(const float* __restri
   }
   if (lane == 0) red[wv] = lsum;
   __syncthreads();
-  if (tid == 0) loss_c[c] = (red[0] + red[1]) + (red[2] + red[3]);
+  if (tid == 0) {   // fixed order
+    float t = 0.f;
+    for (int w = 0; w < kThreads / 64; ++w) t += red[w];
+    loss_c[c] = t;
+  }
   // gW += dlᵀ·P: a thread owns (class k, 4 features); lanes run over features
   float* gW = garena + (int64_t)c * ldg + ow;
-  for (int i = tid; i < K * F4; i += 256) {
+  for (int i = tid; i < K * F4; i += kThreads) {
     const int k = i / F4, f = (i - k * F4) * 4;
     float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
     for (int n = 0; n < N; ++n) {
@@ -103,14 +110,14 @@ __global__ __launch_bounds__(256) void fc_head_xent_kernel(const float* __restri
     g[0] += a0; g[1] += a1; g[2] += a2; g[3] += a3;
   }
   float* gb = garena + (int64_t)c * ldg + ob;
-  for (int k = tid; k < K; k += 256) {
+  for (int k = tid; k < K; k += kThreads) {
     float s = 0.f;
     for (int n = 0; n < N; ++n) s += Z[n * K + k];
     gb[k] += s;
   }
   // dP = dl·W: a thread owns (row n, 4 features)
   float* dp = dpool + (int64_t)c * N * F;
-  for (int i = tid; i < N * F4; i += 256) {
+  for (int i = tid; i < N * F4; i += kThreads) {
     const int n = i / F4, f = (i - n * F4) * 4;
     float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
     const float* zr = Z + n * K;
@@ -141,7 +148,7 @@ FA_EXPORT int fa_fc_head_xent_f32(const float* pooled, const float* arena, int64
   if (smem > 64 * 1024)
     (void)hipFuncSetAttribute((const void*)fch::fc_head_xent_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                               (int)smem);
-  hipLaunchKernelGGL(fch::fc_head_xent_kernel, dim3(C), dim3(256), smem, stream, pooled, arena, lda, ow, ob, labels,
+  hipLaunchKernelGGL(fch::fc_head_xent_kernel, dim3(C), dim3(fch::kThreads), smem, stream, pooled, arena, lda, ow, ob, labels,
                      row_scale, garena, ldg, dpool, loss_c, N, F, K);
   return (int)hipGetLastError();
 }

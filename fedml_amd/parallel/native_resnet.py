@@ -176,6 +176,9 @@ class NativeResNetStep:
         # 0.25-0.4 of the GPU's workgroup slots
         self.use_wgrad_batch = os.environ.get("FEDML_AMD_C3W_BATCH", "1") != "0" and dtype == torch.float32
         self._wb_tabs = {}       # (geometry, layer keys) → device table of per-layer operand pointers
+        # fused 1×1 backward: per-workgroup weight-gradient / statistics partials + a reduce pass instead of fp32
+        # atomics on the Cout·Cin addresses (FEDML_AMD_C1F_PART=1; not in deterministic mode)
+        self.use_c1f_part = os.environ.get("FEDML_AMD_C1F_PART", "0") == "1"
         # deferred BN finalisation (csrc/bnlazy.h): the first consumer kernel folds the statistics itself
         self.use_lazy = os.environ.get("FEDML_AMD_BN_LAZY", "1") != "0"
         self._pending = {}       # (bn key, "f" | "b") → explicit finalisation closure, while deferred
@@ -337,6 +340,13 @@ class NativeResNetStep:
                 o3 += C * n
                 self.c3_maxn = max(self.c3_maxn, n)
         self.dw_c3 = self._shared_f32("dw_c3", max(1, o3))
+        npart = 0
+        if self.use_c1f_part:
+            for cv in self._all_convs():
+                if cv.k == 1 and self._c1f(cv, nn_ops.EPI_MASK) or self._c1f(cv, nn_ops.EPI_BLOCK):
+                    M = N * cv.H * cv.W
+                    npart = max(npart, nn_ops.conv1x1_bwd_fused_scratch(C, M, cv.cin, cv.cout, self._c1f_pix_per_wg(M)))
+        self.c1f_part = self._shared_f32("c1f_part", npart) if npart else None
         # Gram scratch gᵀ·h2 of the recomputed-y bottlenecks ([C][4·planes·planes], kept zeroed by its consumer)
         gmax = max([b.convs[-1].cout * b.convs[-1].cin for b in self.blocks if b.ry] or [0])
         self.gram = self._shared_f32("gram", C * gmax).view(C, gmax) if gmax else None
@@ -380,7 +390,7 @@ class NativeResNetStep:
     # descriptor content, see _lz_prepare)
     _STATE_ATTRS = ("x_in", "stem_y", "stem_out", "gbuf", "dybuf", "bn_vec", "stats", "stat_views", "pooled", "dpool",
                     "loss_c", "dw_scratch", "_bn_hw", "_bn_q",
-                    "dw_c3", "gram", "c3_segs", "c3_nseg", "c3_maxn", "_c3_off",
+                    "dw_c3", "c1f_part", "gram", "c3_segs", "c3_nseg", "c3_maxn", "_c3_off",
                     "packed", "packed_ld", "_segs", "_nseg", "_pack_tiles", "_pack_taps", "final_hw", "geom")
 
     def _snapshot(self):
@@ -490,6 +500,9 @@ class NativeResNetStep:
         nn_ops.conv_wgrad(g, y, vec[4], vec[5], vec[6], x, ps, pt, garena, self.off[cv.key], C, N, cv.H, cv.W,
                           cv.cin_pad, cv.Ho, cv.Wo, cv.cout, cv.k, cv.k, cv.stride, cv.pad, self._pix_per_wg(M), cv.cin,
                           self.dw_scratch, nimg=self._nimg, lazy=lz)
+
+    def _part(self):
+        return self.c1f_part if (self.c1f_part is not None and self.det is None) else None
 
     def _side_on(self):
         return self._side is not None and self.det is None
@@ -824,8 +837,9 @@ class NativeResNetStep:
                     nn_ops.conv1x1_bwd_fused_ry(g_j, v[4], v[5], v[6], v[8], self.packed.view(-1)[cv.off_b:],
                                                 self.packed_ld, cv.ldk2, b.ys[j - 1], pv[0], pv[1], out_g,
                                                 self.stat_views[b.bns[j - 1].key][1], garena, self.off[cv.key], C, M,
-                                                cv.cin, cv.cout, self._c1f_pix_per_wg(M), nimg=self._nimg,
-                                                hw=cv.Ho * cv.Wo, lazy=(self._take(bn.key, "b"), None))
+                                                cv.cin, cv.cout, self._c1f_pix_per_wg(M), part=self._part(),
+                                                nimg=self._nimg, hw=cv.Ho * cv.Wo,
+                                                lazy=(self._take(bn.key, "b"), None))
                     self._bn_bwd(b.bns[j - 1], 1, N, cv.H * cv.W, arena, garena)
                     g_j = out_g
                     self._dump(f"{cv.key}.dx", out_g, C * N * cv.H * cv.W * cv.cin)
@@ -835,7 +849,8 @@ class NativeResNetStep:
                                              self.packed_ld, cv.ldk2, b.ys[j - 1], pv[0], pv[1], None, None, None,
                                              out_g, self.stat_views[b.bns[j - 1].key][1], garena, self.off[cv.key], C,
                                              M, cv.cin, cv.cout, nn_ops.EPI_MASK, self._c1f_pix_per_wg(M),
-                                             nimg=self._nimg, hw=cv.Ho * cv.Wo, lazy=(self._take(bn.key, "b"), None))
+                                             part=self._part(), nimg=self._nimg, hw=cv.Ho * cv.Wo,
+                                             lazy=(self._take(bn.key, "b"), None))
                     self._bn_bwd(b.bns[j - 1], 1, N, cv.H * cv.W, arena, garena)
                     g_j = out_g
                     self._dump(f"{cv.key}.dx", out_g, C * N * cv.H * cv.W * cv.cin)
@@ -904,8 +919,8 @@ class NativeResNetStep:
                 nn_ops.conv1x1_bwd_fused(g_j, b.ys[0], v[4], v[5], v[6], self.packed.view(-1)[cv0.off_b:],
                                          self.packed_ld, cv0.ldk2, b.act_in, None, None, shortcut, ey1, ey2, out_buf,
                                          pstats, garena, self.off[cv0.key], C, M0, cv0.cin, cv0.cout,
-                                         nn_ops.EPI_BLOCK, self._c1f_pix_per_wg(M0), nimg=self._nimg,
-                                         hw=cv0.H * cv0.W, lazy=(self._take(bn0.key, "b"), None))
+                                         nn_ops.EPI_BLOCK, self._c1f_pix_per_wg(M0), part=self._part(),
+                                         nimg=self._nimg, hw=cv0.H * cv0.W, lazy=(self._take(bn0.key, "b"), None))
                 gpre = out_buf
                 self._dump(f"{cv0.key}.dx", out_buf, C * N * cv0.H * cv0.W * cv0.cin)
                 continue
