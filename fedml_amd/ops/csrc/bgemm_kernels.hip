@@ -646,6 +646,202 @@ __global__ __launch_bounds__(NT, 2) void bgemm_dma_kernel(const Args p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// 256 × 256 × 64 block tile on the same LDS-DMA images: 8 waves (2 along M × 4 along N, 128 × 64 outputs and 128
+// accumulator registers each — two waves per SIMD), the block's A and B tiles as two 128-wide half images each
+// (the 128 × 128 kernel's swizzled layouts), two buffers (128 KiB). The next K-step's four half images are DMA'd
+// one per quadrant phase under this K-step's MFMAs; one counted wait + raw barrier per K-step. Half the L2 bytes
+// per MFMA of the 128 × 128 tile. (cdna_hip_programming.md §5: 256² tiles with the prefetch in flight across the
+// barrier.)
+template <int A_TR, int B_TR, int EPI, int BSEG>
+__global__ __launch_bounds__(512, 1) void bgemm_dma256_kernel(const Args p) {
+  extern __shared__ __attribute__((aligned(16))) uint16_t smem[];
+  // buffer b: [A0][A1][B0][B1] images at smem + b·4·GIMG
+  const int total = p.tiles_m * p.tiles_n * p.nclients;
+  int L = blockIdx.x;
+  {
+    const int q = total >> 3, r = total & 7, x = L & 7;
+    L = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (L >> 3);
+  }
+  const int tn = L % p.tiles_n;
+  const int tm = (L / p.tiles_n) % p.tiles_m;
+  const int c = L / (p.tiles_n * p.tiles_m);
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;   // rows wr·128 (A half wr), cols wc·64 (B half wc >> 1)
+
+  auto rsrc = [](const void* base, int64_t bytes) {
+    const uint64_t a = (uint64_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const int nb = __builtin_amdgcn_readfirstlane((int)bytes);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, nb, 0x00020000);
+  };
+  const __amdgpu_buffer_rsrc_t ra = rsrc(p.A + (int64_t)c * p.a_bs, p.a_bytes);
+  const __amdgpu_buffer_rsrc_t rb = rsrc((const uint16_t*)p.B + (int64_t)c * p.b_bs, p.b_bytes);
+  // per-lane offsets: half image h (0, 1: A halves; 2, 3: B halves), instruction i of this wave (2 per wave)
+  uint32_t vo[4][2];
+#pragma unroll
+  for (int h = 0; h < 4; ++h)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int P = (wid * 2 + i) * 1024 + lane * 16;
+      const bool isA = h < 2;
+      const int TR = isA ? A_TR : B_TR;
+      const int ld = isA ? p.lda : p.ldb;
+      const int r0 = (isA ? m0 : n0) + (h & 1) * 128;
+      if (!TR) {
+        const int r = P >> 7;
+        const int q = ((P >> 4) & 7) ^ ((r >> 1) & 7);
+        const int64_t row = (!isA && BSEG) ? seg_row(p.bseg, r0 + r, ld) : (int64_t)(r0 + r) * ld;
+        vo[h][i] = (uint32_t)((row + 8 * q) * 2);
+      } else {
+        const int r = P >> 8;
+        const int hh = ((P >> 5) & 7) ^ ((r & 3) | ((r >> 1) & 4));
+        const int col = r0 + 16 * hh + 8 * ((P >> 4) & 1);
+        vo[h][i] = (uint32_t)(((int64_t)r * ld + col) * 2);
+      }
+    }
+  auto issue_half = [&](int kt, int buf, int h) {
+    const int k0 = kt * BK;
+    uint32_t so;
+    if (h < 2) so = A_TR ? (uint32_t)((int64_t)k0 * p.lda * 2) : (uint32_t)(k0 * 2);
+    else so = B_TR ? (uint32_t)((BSEG ? seg_row(p.bseg, k0, p.ldb) : (int64_t)k0 * p.ldb) * 2) : (uint32_t)(k0 * 2);
+    so = __builtin_amdgcn_readfirstlane(so);
+    uint16_t* img = smem + (buf * 4 + h) * GIMG;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(h < 2 ? ra : rb,
+                                               (__attribute__((address_space(3))) void*)(img + (wid * 2 + i) * 512),
+                                               16, vo[h][i], so, 0, 0);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nk = (p.K + BK - 1) / BK;
+  const bool bsum = EPI == EPI_ACC32 && A_TR == 1 && p.bg != nullptr && tn == 0;
+  float bs = 0.f;
+
+#pragma unroll
+  for (int h = 0; h < 4; ++h) issue_half(0, 0, h);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < nk;
+    const uint16_t* ta = smem + (cur * 4 + wr) * GIMG;
+    const uint16_t* tb = smem + (cur * 4 + 2 + (wc >> 1)) * GIMG;
+    const int cb = (wc & 1) * 64;     // this wave's columns inside its B half image
+    if (bsum) {   // column tid & 255 of the block's dy (A half (tid & 255) >> 7), rows 32·(tid >> 8) .. +31
+      const int col = tid & 127;
+      const uint16_t* th = smem + (cur * 4 + ((tid >> 7) & 1)) * GIMG;
+#pragma unroll 8
+      for (int r = 32 * (tid >> 8); r < 32 * (tid >> 8) + 32; ++r)
+        bs += bf16_to_f32(th[r * 128 + 16 * swz_tr(r, col >> 4) + (col & 15)]);
+    }
+    bf16x8 af[4][2];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {     // quadrant (qm, qn): rows qm·64, cols qn·32 of the wave's 128 × 64 tile
+      const int qm = q >> 1, qn = (q == 1 || q == 2) ? 1 : 0;
+      if (more) issue_half(kt + 1, cur ^ 1, q);
+      if (q == 0 || q == 2) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk)
+            af[i][kk] = A_TR ? tr_frag_s(ta, kk * 32, qm * 64 + 16 * i, lane)
+                             : row_frag_s(ta, qm * 64 + 16 * i + (lane & 15), kk * 4 + (lane >> 4));
+      }
+      bf16x8 bfr[2][2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          bfr[j][kk] = B_TR ? tr_frag_s(tb, kk * 32, cb + qn * 32 + 16 * j, lane)
+                            : row_frag_s(tb, cb + qn * 32 + 16 * j + (lane & 15), kk * 4 + (lane >> 4));
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[qm * 4 + i][qn * 2 + j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], af[i][kk], acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // this wave's DMA of the next K-step landed
+    __builtin_amdgcn_s_barrier();                                  // ... every wave's; nobody reads buf cur again
+  }
+
+  if (EPI == EPI_ACC32 && A_TR == 1 && bsum) {
+    float* red = reinterpret_cast<float*>(smem);
+    red[tid] = bs;
+    __syncthreads();
+    if (tid < 256) {
+      const int m = m0 + tid;
+      if (m < p.M) {
+        float* bp = p.bg + (int64_t)c * p.bg_bs + seg_row(p.bgseg, m, 1);
+        const float t = red[tid] + red[tid + 256];
+        *bp = p.acc_store ? t : *bp + t;
+      }
+    }
+  }
+
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + wr * 128 + 16 * i + (lane & 15);
+    if (m >= p.M) continue;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int n = n0 + wc * 64 + 16 * j + 4 * (lane >> 4);
+      if (n >= p.N) continue;
+      f32x4 v = acc[i][j];
+      if (EPI == EPI_ACC32) {
+        float* dst = (float*)p.Cp + (int64_t)c * p.c_bs + seg_row(p.cseg, m, p.ldc) + n;
+        float4 o = make_float4(v[0], v[1], v[2], v[3]);
+        if (!p.acc_store) {
+          const float4 q = *reinterpret_cast<const float4*>(dst);
+          o.x += q.x; o.y += q.y; o.z += q.z; o.w += q.w;
+        }
+        *reinterpret_cast<float4*>(dst) = o;
+      } else {
+        if (p.bias) {
+          const float4 b = *reinterpret_cast<const float4*>(p.bias + (int64_t)c * p.bias_bs + seg_row(p.biasseg, n, 1));
+          v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
+        }
+        if (p.R) {
+          const uint2 rr = *reinterpret_cast<const uint2*>(p.R + (int64_t)c * p.r_bs + (int64_t)m * p.ldc + n);
+          const float r4[4] = {bf16_to_f32((uint16_t)(rr.x & 0xffff)), bf16_to_f32((uint16_t)(rr.x >> 16)),
+                               bf16_to_f32((uint16_t)(rr.y & 0xffff)), bf16_to_f32((uint16_t)(rr.y >> 16))};
+          if (EPI == EPI_DGELU) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = gelu_grad(r4[e], v[e]);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += r4[e];
+          }
+        }
+        uint2 o;
+        o.x = pk2(v[0], v[1]);
+        o.y = pk2(v[2], v[3]);
+        *reinterpret_cast<uint2*>((uint16_t*)p.Cp + (int64_t)c * p.c_bs + (int64_t)m * p.ldc + n) = o;
+        if (EPI == EPI_GELU) {
+          float r[4];
+          r[0] = bf16_to_f32((uint16_t)(o.x & 0xffff)); r[1] = bf16_to_f32((uint16_t)(o.x >> 16));
+          r[2] = bf16_to_f32((uint16_t)(o.y & 0xffff)); r[3] = bf16_to_f32((uint16_t)(o.y >> 16));
+          uint2 g;
+          g.x = pk2(gelu_erf(r[0]), gelu_erf(r[1]));
+          g.y = pk2(gelu_erf(r[2]), gelu_erf(r[3]));
+          *reinterpret_cast<uint2*>(p.C2 + (int64_t)c * p.c2_bs + (int64_t)m * p.ldc + n) = g;
+        }
+      }
+    }
+  }
+}
+
 // operand extent (bytes from the client's base) the DMA descriptors bound: rows × ld of a plain matrix, or the end
 // of the last segment row
 inline int64_t seg_extent(const Segs& s, int rows, int ld) {
@@ -682,6 +878,25 @@ int launch(const Args& a, hipStream_t st) {
     if ((!A_TR || !B_TR) && a.K % BK != 0) ok = false;
     if (B_TR && seg)   // a K-step's 64 reduction rows must not straddle a segment boundary
       for (int i = 1; i < a.bseg.n; ++i) ok = ok && (a.bseg.lo[i] % BK == 0);
+    // FEDML_AMD_BGEMM_256=1: the 256 × 256 tile when it still gives ≥ 256 blocks (one per CU)
+    const char* e256 = getenv("FEDML_AMD_BGEMM_256");
+    const int t256 = e256 ? atoi(e256) : 0;
+    if (ok && t256) {
+      Args b2 = b;
+      b2.tiles_m = (a.M + 255) / 256;
+      b2.tiles_n = (a.N + 255) / 256;
+      const int64_t nb = (int64_t)b2.tiles_m * b2.tiles_n * b2.nclients;
+      // 1: K-major operands only (a transposing ds_read_b64_tr_b16 after an in-flight LDS-DMA gets a conservative
+      // vmcnt(0) from hipcc, which serialises the phase pipeline); 2: every layout, any grid (tests)
+      const bool ok2 = t256 == 2 || (nb >= 256 && !A_TR && !B_TR);
+      if (ok2) {
+        auto kern = seg ? bgemm_dma256_kernel<A_TR, B_TR, EPI, 1> : bgemm_dma256_kernel<A_TR, B_TR, EPI, 0>;
+        const size_t smem3 = 8 * GIMG * sizeof(uint16_t);   // 128 KiB
+        (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem3);
+        hipLaunchKernelGGL(kern, dim3((unsigned)nb), dim3(512), smem3, st, b2);
+        return (int)hipGetLastError();
+      }
+    }
     if (ok) {
       auto pick = [&](auto k1, auto k0) { return dma == 2 ? k0 : k1; };
       auto kern = seg ? pick(bgemm_dma_kernel<A_TR, B_TR, EPI, 1, 1>, bgemm_dma_kernel<A_TR, B_TR, EPI, 1, 0>)
