@@ -264,24 +264,32 @@ __device__ __forceinline__ void stockham_stage_ip(float2* __restrict__ x, const 
 }
 
 // nfft independent length-2^lg transforms at x + f·ld (padded indices), in place, natural order out: radix-8 stages
-// then one radix-4 or radix-2 stage for the remainder (a 512-point transform: 3 LDS passes). nfft·2^lg ≤ 8192 with
-// 256 threads (every stage holds 32 points per thread in registers).
+// then one radix-4 or radix-2 stage for the remainder (a 512-point transform: 3 LDS passes). PPT = the points a
+// thread holds in registers per stage: nfft·2^lg ≤ PPT·blockDim (sized per kernel — a 32-point worst case for every
+// kernel cost 248 VGPRs, two waves per SIMD).
+template <int PPT>
 __device__ void stockham(float2* x, const float2* tw, int lg, int nfft, int ld, float sign) {
   int ls = 0;
   while (ls < lg) {
     const int left = lg - ls;
     if (left >= 3) {
-      stockham_stage_ip<8, 4>(x, tw, lg, ls, nfft, ld, sign);
+      stockham_stage_ip<8, (PPT + 7) / 8>(x, tw, lg, ls, nfft, ld, sign);
       ls += 3;
     } else if (left == 2) {
-      stockham_stage_ip<4, 8>(x, tw, lg, ls, nfft, ld, sign);
+      stockham_stage_ip<4, (PPT + 3) / 4>(x, tw, lg, ls, nfft, ld, sign);
       ls += 2;
     } else {
-      stockham_stage_ip<2, 16>(x, tw, lg, ls, nfft, ld, sign);
+      stockham_stage_ip<2, (PPT + 1) / 2>(x, tw, lg, ls, nfft, ld, sign);
       ls += 1;
     }
   }
 }
+
+constexpr int kRowPoints = 2048;   // points per row-pass workgroup (R = 2048 / W rows)
+constexpr int kColTile = 16;
+// 512 threads: two column-tile workgroups fill a CU's LDS, so the waves that hide the strided global traffic come from
+// a wider workgroup (16 per CU instead of 8)
+constexpr int kColThreads = 512;
 
 // R rows of length W = 2^lg per workgroup. In: real (xr) or complex (xc). Out: complex (out) or the real part
 // (out_r), times `scale`.
@@ -301,7 +309,7 @@ __global__ __launch_bounds__(256) void fft_rows_kernel(const float* __restrict__
   }
   twiddles_full(tw, W, sign);
   __syncthreads();
-  stockham(A, tw, lg, nr, ld, sign);
+  stockham<kRowPoints / 256>(A, tw, lg, nr, ld, sign);
   for (int i = threadIdx.x; i < nr * W; i += blockDim.x) {
     const int64_t g = r0 * W + i;
     const int rr = i >> lg, w = i & (W - 1);
@@ -311,12 +319,11 @@ __global__ __launch_bounds__(256) void fft_rows_kernel(const float* __restrict__
   }
 }
 
-constexpr int kColTile = 16;
 
 // a kColTile-column tile of one plane [H = 2^lg][W]: column transforms in LDS (transform per column, padded). `trg`
 // non-null: inverse pass of the band mix — inside the band the loaded F is rescaled to amplitude trg[c] (F = 0:
 // trg + 0i). `amp_out` non-null: |F| of the result as well.
-__global__ __launch_bounds__(256) void fft_cols_kernel(const float2* __restrict__ in, float2* __restrict__ out,
+__global__ __launch_bounds__(kColThreads) void fft_cols_kernel(const float2* __restrict__ in, float2* __restrict__ out,
                                                        float* __restrict__ amp_out, const float* __restrict__ amp_in,
                                                        const float* __restrict__ trg, int C, int band, int lg, int W,
                                                        float sign) {
@@ -344,7 +351,7 @@ __global__ __launch_bounds__(256) void fft_cols_kernel(const float2* __restrict_
   }
   twiddles_full(tw, H, sign);
   __syncthreads();
-  stockham(A, tw, lg, tc, ld, sign);
+  stockham<kColTile * kMaxN / kColThreads>(A, tw, lg, tc, ld, sign);
   for (int i = threadIdx.x; i < tc * H; i += blockDim.x) {
     const int h = i / tc, cc = i - h * tc;
     const int64_t g = base + (int64_t)h * W + c0 + cc;
@@ -395,7 +402,7 @@ static int spec_rows(const float* xr, const float2* xc, float2* out, float* out_
                      float scale, hipStream_t stream) {
   const int lg = spec_lg(W);
   if (lg < 0) return -2;
-  const int R = max(1, 2048 / W);
+  const int R = max(1, spec::kRowPoints / W);
   const size_t smem = (size_t)(spec::kMaxN + R * spec::lds_ld(W)) * sizeof(float2);
   if (smem > 64 * 1024)
     (void)hipFuncSetAttribute((const void*)spec::fft_rows_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
@@ -412,7 +419,8 @@ static int spec_cols(const float2* in, float2* out, float* amp_out, const float*
   const size_t smem = (size_t)(spec::kMaxN + tc * spec::lds_ld(H)) * sizeof(float2);
   if (smem > 160 * 1024) return -5;
   (void)hipFuncSetAttribute((const void*)spec::fft_cols_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-  hipLaunchKernelGGL(spec::fft_cols_kernel, dim3((unsigned)(W / tc), (unsigned)planes), dim3(256), smem, stream, in,
+  hipLaunchKernelGGL(spec::fft_cols_kernel, dim3((unsigned)(W / tc), (unsigned)planes), dim3(spec::kColThreads), smem,
+                     stream, in,
                      out, amp_out, amp_in, trg, C, band, lg, W, sign);
   return (int)hipGetLastError();
 }
