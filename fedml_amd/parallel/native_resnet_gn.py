@@ -170,11 +170,21 @@ class NativeGNResNetStep:
                          cv.cin))
         self.packed_ld = _round_up(off, 64)
         self.packed = torch.zeros(C, self.packed_ld, dtype=dt, device=dev)
-        arr = (nn_ops.PackSeg * len(segs))(*[nn_ops.PackSeg(*s) for s in segs])
-        self._segs = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(dev)
-        self._nseg = len(segs)
-        self._pack_tiles = sum(-(-cv.cout // 32) * -(-cv.cin_pad // 32) for cv in self._all_convs())
-        self._pack_taps = max(cv.k * cv.k for cv in self._all_convs())
+        # the tiled packing kernel takes ≤ 9 taps: the 7×7 stem gets its own (element-wise) launch — packing every
+        # layer element-wise was a quarter of the step (profiles/r5_resnet18_gn_kernel_stats.txt)
+        convs = list(self._all_convs())
+        small = [i for i, cv in enumerate(convs) if cv.k * cv.k <= 9]
+        big = [i for i, cv in enumerate(convs) if cv.k * cv.k > 9]
+
+        def table(ix):
+            arr = (nn_ops.PackSeg * max(1, len(ix)))(*[nn_ops.PackSeg(*segs[i]) for i in ix])
+            return torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(dev), len(ix)
+
+        self._segs, self._nseg = table(small)
+        self._segs_big, self._nseg_big = table(big)
+        self._pack_tiles = sum(-(-convs[i].cout // 32) * -(-convs[i].cin_pad // 32) for i in small)
+        self._pack_taps = max([convs[i].k ** 2 for i in small] or [1])
+        self._pack_taps_big = max([convs[i].k ** 2 for i in big] or [1])
 
         def act(hh, ww, ch):       # zero-initialised: padding images are never written
             return torch.zeros(C, N, hh, ww, ch, dtype=dt, device=dev)
@@ -213,7 +223,8 @@ class NativeGNResNetStep:
 
     _STATE = ("x_in", "y0", "a0", "p0", "idx0", "gbuf", "ms", "pscr", "stats", "dw_scratch", "_ones", "_zeros",
               "pooled", "dpool",
-              "loss_c", "packed", "packed_ld", "_segs", "_nseg", "_pack_tiles", "_pack_taps", "final_hw", "pool_hw",
+              "loss_c", "packed", "packed_ld", "_segs", "_nseg", "_segs_big", "_nseg_big", "_pack_tiles", "_pack_taps",
+              "_pack_taps_big", "final_hw", "pool_hw",
               "geom")
 
     def _geometry(self, N, H, W):
@@ -294,8 +305,12 @@ class NativeGNResNetStep:
             self.det.register(garena)
         nn_ops._set_lazy((0, 0))
         self.stats.zero_()        # the conv kernels' (unused) BatchNorm-statistics epilogue target
-        nn_ops.pack_weights(arena, self._segs, self._nseg, self.packed, self.packed_ld, C, self._pack_tiles,
-                            self._pack_taps)
+        if self._nseg:
+            nn_ops.pack_weights(arena, self._segs, self._nseg, self.packed, self.packed_ld, C, self._pack_tiles,
+                                self._pack_taps)
+        if self._nseg_big:
+            nn_ops.pack_weights(arena, self._segs_big, self._nseg_big, self.packed, self.packed_ld, C, 0,
+                                self._pack_taps_big)
         st, sgn, (pk, ps, pp) = self.stem
         nn_ops.nchw_to_nhwc_pad(x.contiguous(), self.x_in, C * N, st.cin, H * W, st.cin_pad)
         # ---------------- forward ----------------
