@@ -650,7 +650,7 @@ __global__ __launch_bounds__(NT, 2) void bgemm_dma_kernel(const Args p) {
 // 256 × 256 × 64 block tile on the same LDS-DMA images: 8 waves (2 along M × 4 along N, 128 × 64 outputs and 128
 // accumulator registers each — two waves per SIMD), the block's A and B tiles as two 128-wide half images each
 // (the 128 × 128 kernel's swizzled layouts), two buffers (128 KiB). The next K-step's four half images are DMA'd
-// one per quadrant phase under this K-step's MFMAs; one counted wait + raw barrier per K-step. Half the L2 bytes
+// at the start of this K-step, under its four quadrant phases of MFMAs; one wait + raw barrier per K-step. Half the L2 bytes
 // per MFMA of the 128 × 128 tile. (cdna_hip_programming.md §5: 256² tiles with the prefetch in flight across the
 // barrier.)
 template <int A_TR, int B_TR, int EPI, int BSEG>
@@ -744,10 +744,13 @@ __global__ __launch_bounds__(512, 1) void bgemm_dma256_kernel(const Args p) {
         bs += bf16_to_f32(th[r * 128 + 16 * swz_tr(r, col >> 4) + (col & 15)]);
     }
     bf16x8 af[4][2];
+    if (more) {   // the whole next K-step in flight from the start of this one (the most lead time 2 buffers give)
+#pragma unroll
+      for (int h = 0; h < 4; ++h) issue_half(kt + 1, cur ^ 1, h);
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {     // quadrant (qm, qn): rows qm·64, cols qn·32 of the wave's 128 × 64 tile
       const int qm = q >> 1, qn = (q == 1 || q == 2) ? 1 : 0;
-      if (more) issue_half(kt + 1, cur ^ 1, q);
       if (q == 0 || q == 2) {
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -763,6 +766,7 @@ __global__ __launch_bounds__(512, 1) void bgemm_dma256_kernel(const Args p) {
         for (int kk = 0; kk < 2; ++kk)
           bfr[j][kk] = B_TR ? tr_frag_s(tb, kk * 32, cb + qn * 32 + 16 * j, lane)
                             : row_frag_s(tb, cb + qn * 32 + 16 * j + (lane & 15), kk * 4 + (lane >> 4));
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
@@ -771,6 +775,7 @@ __global__ __launch_bounds__(512, 1) void bgemm_dma256_kernel(const Args p) {
           for (int j = 0; j < 2; ++j)
             acc[qm * 4 + i][qn * 2 + j] =
                 __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], af[i][kk], acc[qm * 4 + i][qn * 2 + j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
     }
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");   // this wave's DMA of the next K-step landed
     __builtin_amdgcn_s_barrier();                                  // ... every wave's; nobody reads buf cur again

@@ -171,6 +171,7 @@ class NativeResNetStep:
         # (created here, never inside a graph capture)
         self._side = torch.cuda.Stream(device=self.device) if (self.use_side and self.device.type == "cuda") else None
         self._side_reads = {}    # data_ptr of a gradient buffer a side-stream kernel still reads → its done event
+        self._side_forked = False
         # the stride-1 middle 3×3 convs of a stage's bottlenecks get their own dy buffer, and their weight gradients
         # run as ONE multi-layer launch per stage (conv3x3_wgrad_multi): at 13 clients per GPU each layer alone fills
         # 0.25-0.4 of the GPU's workgroup slots
@@ -480,6 +481,7 @@ class NativeResNetStep:
             done = torch.cuda.Event()
             done.record(self._side)
             self._side_reads[g.data_ptr()] = done     # activations (y, x) are not written in the backward
+            self._side_forked = True
             return
         lz = (self._take(bn_key, "b"), None) if y is not None else None   # y None: materialised dy, no BN
         if self._c3(cv):
@@ -544,8 +546,11 @@ class NativeResNetStep:
         pend.clear()
 
     def _side_join(self):
-        if self._side is not None:
+        """Join the side stream into the main one — only after this step forked work onto it (in deterministic mode
+        or without 3×3 layers nothing was forked, and a capturing stream must not wait on an uncaptured one)."""
+        if self._side is not None and self._side_forked:
             torch.cuda.current_stream(self.device).wait_stream(self._side)
+        self._side_forked = False
         self._side_reads.clear()
 
     def _ry_ok(self, b, shape_only=False) -> bool:

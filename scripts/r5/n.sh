@@ -1,0 +1,7 @@
+#!/bin/bash
+# round 5, call N: which side of the multi-rank deterministic comparison varies run to run?
+cd "$(dirname "$0")/../.." && mkdir -p gpurun_out/r5n
+export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
+bash scripts/gpu_steps.sh \
+ "timeout -k 10 500 python -u scripts/det_repro.py --model headline --clients 100 --worlds 1,8 --repeats 3 --rounds 2 > gpurun_out/r5n/headline.txt 2>&1" \
+ "timeout -k 10 400 python -u scripts/det_repro.py --model resnet_shallow --clients 5 --worlds 1,2 --repeats 3 --rounds 3 --augment 1 > gpurun_out/r5n/shallow.txt 2>&1"
