@@ -39,6 +39,30 @@ _global_comm_backend = None
 os.environ.setdefault("KMP_DUPLICATE_LIB_OK", "True")
 
 
+def _miopen_dirs():
+    """MIOpen keeps its run-time compiled kernels and perf database under $HOME; on boxes where that is absent or
+    read-only its compiles can fail ("Empty code object path") and the failed kernel later faults. Give it a
+    per-user directory under the temp dir unless the caller chose one (must happen before MIOpen initialises)."""
+    import getpass
+    import tempfile
+    try:
+        user = getpass.getuser()
+    except Exception:   # no passwd entry for the uid
+        user = str(os.getuid())
+    base = os.path.join(tempfile.gettempdir(), f"miopen-{user}")
+    for var, sub in (("MIOPEN_USER_DB_PATH", "db"), ("MIOPEN_CUSTOM_CACHE_DIR", "cache")):
+        if not os.environ.get(var):
+            path = os.path.join(base, sub)
+            try:
+                os.makedirs(path, exist_ok=True)
+                os.environ[var] = path
+            except OSError:
+                pass
+
+
+_miopen_dirs()
+
+
 def _seed_everything(seed: int):
     import torch
     random.seed(seed)

@@ -251,9 +251,11 @@ class ClientBatchEngine:
             logging.info("virtual-client engine: per-client sequential execution (wide conv net)")
             self.sequential = True
             # MIOpen picks convolution solutions by heuristics unless a find-db entry exists; on a fresh
-            # machine that costs ~40 % of the round. Benchmark mode runs Find once per shape during the
-            # first (eager, uncaptured) step of each geometry; the captured graphs then replay the winners.
-            if os.environ.get("FEDML_AMD_MIOPEN_FIND", "1") != "0":
+            # machine that costs ~40 % of the round. Benchmark mode (FEDML_AMD_MIOPEN_FIND=1) runs Find once per
+            # shape during the first (eager, uncaptured) step of each geometry; the captured graphs then replay the
+            # winners. Off by default: Find compiles candidate solvers at run time, and on the test boxes a failed
+            # compile ("Empty code object path") surfaced as an illegal memory access (MobileNet-v3, round 5).
+            if os.environ.get("FEDML_AMD_MIOPEN_FIND", "0") == "1":
                 self._prev_benchmark = torch.backends.cudnn.benchmark   # restored by close()
                 torch.backends.cudnn.benchmark = True
         self._build_views()
