@@ -4,8 +4,8 @@
 ``install()`` (or ``FEDML_AMD_STREAM_CHECK=1`` at import of ``fedml_amd``) turns it on for the process:
 
 * every native kernel launch (``ops`` layer) reports the tensors it was handed as accesses on the
-  stream it was launched on — conservatively as writes, since the C ABI does not say which operands
-  are read-only;
+  stream it was launched on — as writes, unless the wrapper passed the operand through ``_pr`` (read-only
+  by the kernel's contract; the convolution / BatchNorm wrappers mark their inputs so);
 * ``torch.cuda.Stream.wait_stream`` / ``wait_event``, ``Event.record`` and ``synchronize`` report the
   orderings the program establishes;
 * ``hazards()`` lists every access that touched a buffer whose last write (or, for a write, a read since)
@@ -87,11 +87,11 @@ class StreamChecker:
         self._event_epochs.clear()
 
     # ---- ops-layer hook: operands collected by ``_p`` are flushed by ``_check`` ----------------------
-    def pending(self, t: torch.Tensor):
+    def pending(self, t: torch.Tensor, write: bool = True):
         lst = getattr(self._pending, "lst", None)
         if lst is None:
             lst = self._pending.lst = []
-        lst.append(t)
+        lst.append((t, write))
 
     def flush(self, name: str):
         lst = getattr(self._pending, "lst", None)
@@ -100,14 +100,14 @@ class StreamChecker:
         self._pending.lst = []
         if self._capturing is not None:
             self._graph_log.setdefault(self._capturing, []).extend(
-                (t.data_ptr(), _span_bytes(t), name) for t in lst)
+                (t.data_ptr(), _span_bytes(t), name, w) for t, w in lst)
             return
-        for t in lst:
-            self.tensor(t, write=True, tag=name)
+        for t, w in lst:
+            self.tensor(t, write=w, tag=name)
 
     def replay(self, graph, stream):
-        for addr, nb, name in self._graph_log.get(id(graph), ()):
-            self.access(addr, nb, stream, True, name)
+        for addr, nb, name, w in self._graph_log.get(id(graph), ()):
+            self.access(addr, nb, stream, w, name)
 
     def discard(self):
         self._pending.lst = []

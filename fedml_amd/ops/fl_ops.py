@@ -28,6 +28,15 @@ def _p(t):
     return _c.c_void_p(t.data_ptr())
 
 
+def _pr(t):
+    """:func:`_p` for an operand the kernel only READS (the stream checker records a read, not a write)."""
+    if t is None:
+        return None
+    if _SC is not None and t.is_cuda:
+        _SC.pending(t, write=False)
+    return _c.c_void_p(t.data_ptr())
+
+
 def _stream(t):
     return _c.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
 

@@ -13,7 +13,7 @@ import os
 import torch
 
 from . import _native
-from .fl_ops import _check, _f, _fn, _i64, _p, _stream
+from .fl_ops import _check, _f, _fn, _i64, _p, _pr, _stream
 
 _c = ctypes
 
@@ -85,9 +85,9 @@ def conv_fwd(x, wpk, wpk_ld, pscale, pshift, y, stats, C, N, H, W, Cin, Cout, KH
              tiles_per_wave, pivot=None, nimg=None, lazy=None):
     """y = conv(pro(x)) − pivot (per client and output channel; None → 0), BN statistics of y."""
     _set_lazy(lazy)
-    rc = _fnp("fa_conv_fwd", x)(_p(x), _p(wpk), _i64(wpk_ld), _p(pscale), _p(pshift), _p(y), _p(stats), _i(C), _i(N),
+    rc = _fnp("fa_conv_fwd", x)(_pr(x), _pr(wpk), _i64(wpk_ld), _pr(pscale), _pr(pshift), _p(y), _p(stats), _i(C), _i(N),
                             _i(H), _i(W), _i(Cin), _i(Cout), _i(KH), _i(KW), _i(stride), _i(pad), _i(Ho), _i(Wo),
-                            _i(ldk), _i(tiles_per_wave), _p(pivot), _p(nimg), _stream(x))
+                            _i(ldk), _i(tiles_per_wave), _pr(pivot), _pr(nimg), _stream(x))
     _check(rc, "fa_conv_fwd")
 
 
@@ -102,9 +102,9 @@ def conv_fwd_pbout(yp, s, t, res, rs, rt, bout, wpk, wpk_ld, y, stats, C, N, H, 
     to ``bout`` once: bout = relu(yp·s + t + r), r = res (identity) | res·rs + rt (downsample BN) — bit-identical to
     :func:`block_out` —; y = conv(bout) − pivot with its BN statistics, as :func:`conv_fwd`."""
     _set_lazy(lazy)
-    rc = _fnp("fa_conv_fwd_pbout", yp)(_p(yp), _p(s), _p(t), _p(res), _p(rs), _p(rt), _p(bout), _p(wpk), _i64(wpk_ld),
+    rc = _fnp("fa_conv_fwd_pbout", yp)(_pr(yp), _pr(s), _pr(t), _pr(res), _pr(rs), _pr(rt), _p(bout), _pr(wpk), _i64(wpk_ld),
                                        _p(y), _p(stats), _i(C), _i(N), _i(H), _i(W), _i(Cin), _i(Cout), _i(ldk),
-                                       _i(tiles_per_wave), _p(pivot), _p(nimg), _stream(yp))
+                                       _i(tiles_per_wave), _pr(pivot), _pr(nimg), _stream(yp))
     _check(rc, "fa_conv_fwd_pbout")
 
 
@@ -115,9 +115,9 @@ def conv_fwd_bout(x, wpk, wpk_ld, pscale, pshift, out, s, t, pivot, res, rs, rt,
     The BN statistics of the conv output come from :func:`conv_fwd` with ``y=None`` (same kernel, same bits)."""
     if x.dtype != torch.float32:
         raise ValueError("conv_fwd_bout: fp32 storage only")
-    rc = _fn("fa_conv_fwd_bout_f32")(_p(x), _p(wpk), _i64(wpk_ld), _p(pscale), _p(pshift), _p(out), _p(s), _p(t),
-                                     _p(pivot), _p(res), _p(rs), _p(rt), _i(C), _i(N), _i(H), _i(W), _i(Cin), _i(Cout),
-                                     _i(ldk), _i(tiles_per_wave), _p(nimg), _stream(x))
+    rc = _fn("fa_conv_fwd_bout_f32")(_pr(x), _pr(wpk), _i64(wpk_ld), _pr(pscale), _pr(pshift), _p(out), _pr(s), _pr(t),
+                                     _pr(pivot), _pr(res), _pr(rs), _pr(rt), _i(C), _i(N), _i(H), _i(W), _i(Cin), _i(Cout),
+                                     _i(ldk), _i(tiles_per_wave), _pr(nimg), _stream(x))
     _check(rc, "fa_conv_fwd_bout_f32")
 
 
@@ -134,10 +134,10 @@ EPI_STORE, EPI_MASK, EPI_BLOCK = 1, 2, 3
 
 def conv_bwd_data(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, dx, epi, e_x, e_s, e_t, e_add, e_y1, e_y2, stats, C, N,
                   Hy, Wy, Cout, Cin, KH, KW, stride, pad, Hx, Wx, ldk2, tiles_per_wave, nimg=None):
-    rc = _fnp("fa_conv_bwd_data", g)(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(wpk_b), _i64(wpk_ld), _p(dx),
-                                 _i(epi), _p(e_x), _p(e_s), _p(e_t), _p(e_add), _p(e_y1), _p(e_y2), _p(stats), _i(C),
+    rc = _fnp("fa_conv_bwd_data", g)(_pr(g), _pr(yv), _pr(alpha), _pr(beta), _pr(gamma), _pr(wpk_b), _i64(wpk_ld), _p(dx),
+                                 _i(epi), _pr(e_x), _pr(e_s), _pr(e_t), _pr(e_add), _pr(e_y1), _pr(e_y2), _p(stats), _i(C),
                                  _i(N), _i(Hy), _i(Wy), _i(Cout), _i(Cin), _i(KH), _i(KW), _i(stride), _i(pad),
-                                 _i(Hx), _i(Wx), _i(ldk2), _i(tiles_per_wave), _p(nimg), _stream(g))
+                                 _i(Hx), _i(Wx), _i(ldk2), _i(tiles_per_wave), _pr(nimg), _stream(g))
     _check(rc, "fa_conv_bwd_data")
 
 
@@ -145,10 +145,10 @@ def conv_wgrad(g, yv, alpha, beta, gamma, x, ps, pt, garena, woff, C, N, H, W, C
                pad, pix_per_wg, cin_src, dw_scratch, nimg=None, lazy=None):
     """``dw_scratch``: ≥ C·Cout·KH·KW·Cin fp32, zero on entry; the kernel leaves it zeroed."""
     _set_lazy(lazy)
-    rc = _fnp("fa_conv_wgrad", g)(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(x), _p(ps), _p(pt), _p(garena),
+    rc = _fnp("fa_conv_wgrad", g)(_pr(g), _pr(yv), _pr(alpha), _pr(beta), _pr(gamma), _pr(x), _pr(ps), _pr(pt), _p(garena),
                               _i64(garena.stride(0)), _i64(woff), _i(C), _i(N), _i(H), _i(W), _i(Cin), _i(Ho), _i(Wo),
                               _i(Cout), _i(KH), _i(KW), _i(stride), _i(pad), _i(pix_per_wg), _i(cin_src),
-                              _p(dw_scratch), _p(nimg), _stream(g))
+                              _p(dw_scratch), _pr(nimg), _stream(g))
     _check(rc, "fa_conv_wgrad")
 
 
@@ -166,17 +166,17 @@ def conv3x3_supported(cin, cout, k, stride, pad, H, W):
 def conv3x3_fwd(x, wpk, wpk_ld, pscale, pshift, y, stats, C, N, H, W, Cin, Cout, ldk, stride=1, pivot=None,
                 nimg=None, lazy=None):
     _set_lazy(lazy)
-    rc = _fnp("fa_conv3x3_fwd", x)(_p(x), _p(wpk), _i64(wpk_ld), _p(pscale), _p(pshift), _p(y), _p(stats), _i(C), _i(N),
-                               _i(H), _i(W), _i(Cin), _i(Cout), _i(ldk), _i(stride), _p(pivot), _p(nimg), _stream(x))
+    rc = _fnp("fa_conv3x3_fwd", x)(_pr(x), _pr(wpk), _i64(wpk_ld), _pr(pscale), _pr(pshift), _p(y), _p(stats), _i(C), _i(N),
+                               _i(H), _i(W), _i(Cin), _i(Cout), _i(ldk), _i(stride), _pr(pivot), _pr(nimg), _stream(x))
     _check(rc, "fa_conv3x3_fwd")
 
 
 def conv3x3_bwd_data(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, dx, e_x, e_s, e_t, stats, C, N, H, W, Cout, Cin,
                      ldk2, stride=1, nimg=None):
     """(H, W) = dx (input) resolution."""
-    rc = _fnp("fa_conv3x3_bwd_data", g)(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(wpk_b), _i64(wpk_ld), _p(dx),
-                                    _p(e_x), _p(e_s), _p(e_t), _p(stats), _i(C), _i(N), _i(H), _i(W), _i(Cout), _i(Cin),
-                                    _i(ldk2), _i(stride), _p(nimg), _stream(g))
+    rc = _fnp("fa_conv3x3_bwd_data", g)(_pr(g), _pr(yv), _pr(alpha), _pr(beta), _pr(gamma), _pr(wpk_b), _i64(wpk_ld), _p(dx),
+                                    _pr(e_x), _pr(e_s), _pr(e_t), _p(stats), _i(C), _i(N), _i(H), _i(W), _i(Cout), _i(Cin),
+                                    _i(ldk2), _i(stride), _pr(nimg), _stream(g))
     _check(rc, "fa_conv3x3_bwd_data")
 
 
@@ -184,9 +184,9 @@ def conv3x3_bwd_data_block(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, dx, e_x, e_
                            Cout, Cin, ldk2, nimg=None):
     """Stride-1 backward-data of a block's first 3×3 conv with the block epilogue:
     dx' = (convᵀ(dy) + e_add)·[e_x > 0], stats (Σdx', Σdx'·e_y1, Σdx'·e_y2). (H, W) = dx resolution."""
-    rc = _fnp("fa_conv3x3_bwd_data_block", g)(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(wpk_b), _i64(wpk_ld),
-                                          _p(dx), _p(e_x), _p(e_add), _p(e_y1), _p(e_y2), _p(stats), _i(C), _i(N),
-                                          _i(H), _i(W), _i(Cout), _i(Cin), _i(ldk2), _p(nimg), _stream(g))
+    rc = _fnp("fa_conv3x3_bwd_data_block", g)(_pr(g), _pr(yv), _pr(alpha), _pr(beta), _pr(gamma), _pr(wpk_b), _i64(wpk_ld),
+                                          _p(dx), _pr(e_x), _pr(e_add), _pr(e_y1), _pr(e_y2), _p(stats), _i(C), _i(N),
+                                          _i(H), _i(W), _i(Cout), _i(Cin), _i(ldk2), _pr(nimg), _stream(g))
     _check(rc, "fa_conv3x3_bwd_data_block")
 
 
@@ -196,8 +196,8 @@ def conv3x3_wgrad(g, yv, alpha, beta, gamma, x, ps, pt, garena, woff, C, N, H, W
     (``scatter=False``: left in the scratch for :func:`wgrad_scatter_multi`). (H, W) = input (x)
     resolution."""
     _set_lazy(lazy)
-    rc = _fnp("fa_conv3x3_wgrad", g)(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(x), _p(ps), _p(pt),
-                                 _p(dw_scratch), _i(C), _i(N), _i(H), _i(W), _i(Cin), _i(Cout), _i(stride), _p(nimg),
+    rc = _fnp("fa_conv3x3_wgrad", g)(_pr(g), _pr(yv), _pr(alpha), _pr(beta), _pr(gamma), _pr(x), _pr(ps), _pr(pt),
+                                 _p(dw_scratch), _i(C), _i(N), _i(H), _i(W), _i(Cin), _i(Cout), _i(stride), _pr(nimg),
                                  _stream(g))
     _check(rc, "fa_conv3x3_wgrad")
     if not scatter:
@@ -207,12 +207,17 @@ def conv3x3_wgrad(g, yv, alpha, beta, gamma, x, ps, pt, garena, woff, C, N, H, W
     _check(rc, "fa_wgrad_scatter")
 
 
-def conv3x3_wgrad_multi(tab, nl, has_ps, C, N, H, W, Cin, Cout, stride, like, nimg=None):
+def conv3x3_wgrad_multi(tab, nl, has_ps, C, N, H, W, Cin, Cout, stride, like, nimg=None, reads=(), writes=()):
     """:func:`conv3x3_wgrad` (scatter=False) of ``nl`` layers of one geometry in one launch: ``tab`` int64 device
     tensor [nl, 9] of per-layer pointers (g, yv, α, β, γ, x, ps, pt, dw scratch); fp32 only. ``like``: any device
-    tensor (the stream's device)."""
-    rc = _fn("fa_conv3x3_wgrad_multi_f32")(_p(tab), _i(nl), _i(int(has_ps)), _i(C), _i(N), _i(H), _i(W), _i(Cin),
-                                           _i(Cout), _i(stride), _p(nimg), _stream(like))
+    tensor (the stream's device). ``reads`` / ``writes``: the tensors behind the table's pointers (reported to the
+    stream-ordering checker, which cannot see through the table)."""
+    for t in reads:
+        _pr(t)
+    for t in writes:
+        _p(t)
+    rc = _fn("fa_conv3x3_wgrad_multi_f32")(_pr(tab), _i(nl), _i(int(has_ps)), _i(C), _i(N), _i(H), _i(W), _i(Cin),
+                                           _i(Cout), _i(stride), _pr(nimg), _stream(like))
     _check(rc, "fa_conv3x3_wgrad_multi")
 
 
@@ -242,9 +247,9 @@ def conv1x1_wgrad(g, yv, alpha, beta, gamma, x, ps, pt, garena, woff, C, M, Cin,
                   lazy=None):
     """dW += Σ_p dyᵀ·act(x) straight into the OIHW arena rows (stride garena.stride(0))."""
     _set_lazy(lazy)
-    rc = _fnp("fa_conv1x1_wgrad", g)(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(x), _p(ps), _p(pt), _p(garena),
+    rc = _fnp("fa_conv1x1_wgrad", g)(_pr(g), _pr(yv), _pr(alpha), _pr(beta), _pr(gamma), _pr(x), _pr(ps), _pr(pt), _p(garena),
                                  _i64(garena.stride(0)), _i64(woff), _i(C), _i(M), _i(Cin), _i(Cout), _i(pix_per_wg),
-                                 _p(nimg), _i(hw), _stream(g))
+                                 _pr(nimg), _i(hw), _stream(g))
     _check(rc, "fa_conv1x1_wgrad")
 
 
@@ -269,10 +274,10 @@ def conv1x1_bwd_fused_ry(g, alpha, beta, gamma, pivot, wpk_b, wpk_ld, ldk2, e_x,
     if part is not None and part.numel() < conv1x1_bwd_fused_scratch(C, M, Cin, Cout, pix_per_wg):
         raise ValueError("conv1x1_bwd_fused_ry: partial-sum scratch too small")
     _set_lazy(lazy)
-    rc = _fn("fa_conv1x1_bwd_fused_ry_f32")(_p(g), _p(alpha), _p(beta), _p(gamma), _p(pivot), _p(wpk_b), _i64(wpk_ld),
-                                            _i(ldk2), _p(e_x), _p(e_s), _p(e_t), _p(out), _p(stats),
+    rc = _fn("fa_conv1x1_bwd_fused_ry_f32")(_pr(g), _pr(alpha), _pr(beta), _pr(gamma), _pr(pivot), _pr(wpk_b), _i64(wpk_ld),
+                                            _i(ldk2), _pr(e_x), _pr(e_s), _pr(e_t), _p(out), _p(stats),
                                             _i(stats.shape[-1]), _p(garena), _i64(garena.stride(0)), _i64(woff), _i(C),
-                                            _i(M), _i(Cin), _i(Cout), _i(pix_per_wg), _p(part), _p(nimg), _i(hw),
+                                            _i(M), _i(Cin), _i(Cout), _i(pix_per_wg), _p(part), _pr(nimg), _i(hw),
                                             _stream(g))
     _check(rc, "fa_conv1x1_bwd_fused_ry_f32")
 
@@ -286,11 +291,11 @@ def conv1x1_bwd_fused(g, yv, alpha, beta, gamma, wpk_b, wpk_ld, ldk2, e_x, e_s, 
     if part is not None and part.numel() < conv1x1_bwd_fused_scratch(C, M, Cin, Cout, pix_per_wg):
         raise ValueError("conv1x1_bwd_fused: partial-sum scratch too small")
     _set_lazy(lazy)
-    rc = _fnp("fa_conv1x1_bwd_fused", g)(_p(g), _p(yv), _p(alpha), _p(beta), _p(gamma), _p(wpk_b), _i64(wpk_ld),
-                                     _i(ldk2), _p(e_x), _p(e_s), _p(e_t), _p(e_add), _p(e_y1), _p(e_y2), _p(out),
+    rc = _fnp("fa_conv1x1_bwd_fused", g)(_pr(g), _pr(yv), _pr(alpha), _pr(beta), _pr(gamma), _pr(wpk_b), _i64(wpk_ld),
+                                     _i(ldk2), _pr(e_x), _pr(e_s), _pr(e_t), _pr(e_add), _pr(e_y1), _pr(e_y2), _p(out),
                                      _p(stats), _i(stats.shape[-1]), _p(garena), _i64(garena.stride(0)), _i64(woff),
                                      _i(C), _i(M), _i(Cin), _i(Cout), _i(epi), _i(pix_per_wg), _p(part),
-                                     _p(nimg), _i(hw), _stream(g))
+                                     _pr(nimg), _i(hw), _stream(g))
     _check(rc, "fa_conv1x1_bwd_fused")
 
 

@@ -476,8 +476,8 @@ class NativeResNetStep:
             self._side.wait_event(fork)
             with torch.cuda.stream(self._side):
                 nn_ops.conv3x3_wgrad(g, y, vec[4], vec[5], vec[6], x, ps, pt, garena, self.off[cv.key], C, N, cv.H,
-                                     cv.W, cv.cin_pad, cv.cout, cv.cin, self.dw_c3[self._c3_off[cv.key]:], cv.stride,
-                                     scatter=False, nimg=self._nimg)
+                                     cv.W, cv.cin_pad, cv.cout, cv.cin, self._c3_dw(cv), cv.stride, scatter=False,
+                                     nimg=self._nimg)
             done = torch.cuda.Event()
             done.record(self._side)
             self._side_reads[g.data_ptr()] = done     # activations (y, x) are not written in the backward
@@ -486,7 +486,7 @@ class NativeResNetStep:
         lz = (self._take(bn_key, "b"), None) if y is not None else None   # y None: materialised dy, no BN
         if self._c3(cv):
             nn_ops.conv3x3_wgrad(g, y, vec[4], vec[5], vec[6], x, ps, pt, garena, self.off[cv.key], C, N, cv.H, cv.W,
-                                 cv.cin_pad, cv.cout, cv.cin, self.dw_c3[self._c3_off[cv.key]:], cv.stride,
+                                 cv.cin_pad, cv.cout, cv.cin, self._c3_dw(cv), cv.stride,
                                  scatter=False, nimg=self._nimg, lazy=lz)   # scattered with the other 3×3 layers
             return
         M = N * cv.Ho * cv.Wo
@@ -502,6 +502,11 @@ class NativeResNetStep:
         nn_ops.conv_wgrad(g, y, vec[4], vec[5], vec[6], x, ps, pt, garena, self.off[cv.key], C, N, cv.H, cv.W,
                           cv.cin_pad, cv.Ho, cv.Wo, cv.cout, cv.k, cv.k, cv.stride, cv.pad, self._pix_per_wg(M), cv.cin,
                           self.dw_scratch, nimg=self._nimg, lazy=lz)
+
+    def _c3_dw(self, cv):
+        """This 3×3 layer's slice of the GEMM-layout weight-gradient scratch (exactly its C·Cout·9·Cin floats)."""
+        o = self._c3_off[cv.key]
+        return self.dw_c3[o:o + self.C * cv.cout * 9 * cv.cin_pad]
 
     def _part(self):
         return self.c1f_part if (self.c1f_part is not None and self.det is None) else None
@@ -537,12 +542,17 @@ class NativeResNetStep:
             rows = []
             for cv, b in pend:
                 v, pv = self.bn_vec[b.bns[1].key], self.bn_vec[b.bns[0].key]
-                dw = self.dw_c3[self._c3_off[cv.key]:]
+                dw = self._c3_dw(cv)
                 rows.append([b.g3.data_ptr(), b.ys[1].data_ptr(), v[4].data_ptr(), v[5].data_ptr(), v[6].data_ptr(),
                              b.ys[0].data_ptr(), pv[0].data_ptr(), pv[1].data_ptr(), dw.data_ptr()])
             tab = self._wb_tabs[key] = torch.tensor(rows, dtype=torch.int64).to(self.device)
+        reads, writes = [], []
+        for cv, b in pend:
+            v, pv = self.bn_vec[b.bns[1].key], self.bn_vec[b.bns[0].key]
+            reads += [b.g3, b.ys[1], v[4], v[5], v[6], b.ys[0], pv[0], pv[1]]
+            writes.append(self._c3_dw(cv))
         nn_ops.conv3x3_wgrad_multi(tab, len(pend), True, self.C, N, cv0.H, cv0.W, cv0.cin_pad, cv0.cout, 1,
-                                   self.dw_c3, nimg=self._nimg)
+                                   self.dw_c3, nimg=self._nimg, reads=reads, writes=writes)
         pend.clear()
 
     def _side_join(self):
