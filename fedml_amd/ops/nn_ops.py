@@ -305,8 +305,8 @@ def bn_fwd_finalize(stats, C, Ch, n, arena, off_gamma, off_beta, off_rm, off_rv,
     batch's true mean (the next step's pivot)."""
     rc = _fn("fa_bn_fwd_finalize")(_p(stats), _i(C), _i(Ch), _f(n), _p(arena), _i64(arena.stride(0)),
                                    _i64(off_gamma), _i64(off_beta), _i64(off_rm), _i64(off_rv), _i64(off_nbt),
-                                   _f(momentum), _f(eps), _p(active), _p(scale), _p(shift), _p(mean), _p(rstd),
-                                   _i(int(update_running)), _p(pivot), _p(nimg), _i(hw), _stream(stats))
+                                   _f(momentum), _f(eps), _pr(active), _p(scale), _p(shift), _p(mean), _p(rstd),
+                                   _i(int(update_running)), _p(pivot), _pr(nimg), _i(hw), _stream(stats))
     _check(rc, "fa_bn_fwd_finalize")
 
 
@@ -319,34 +319,34 @@ def bn_eval_fold(C, Ch, arena, off_gamma, off_beta, off_rm, off_rv, eps, scale, 
 
 def bn_bwd_finalize(bstats, NS, q_gy, C, Ch, n, mean, rstd, arena, garena, off_gamma, off_beta, alpha, beta_c,
                     gamma_c, nimg=None, hw=0):
-    rc = _fn("fa_bn_bwd_finalize")(_p(bstats), _i(NS), _i(q_gy), _i(C), _i(Ch), _f(n), _p(mean), _p(rstd),
-                                   _p(arena), _p(garena), _i64(arena.stride(0)), _i64(off_gamma), _i64(off_beta),
-                                   _p(alpha), _p(beta_c), _p(gamma_c), _p(nimg), _i(hw), _stream(bstats))
+    rc = _fn("fa_bn_bwd_finalize")(_pr(bstats), _i(NS), _i(q_gy), _i(C), _i(Ch), _f(n), _pr(mean), _pr(rstd),
+                                   _pr(arena), _p(garena), _i64(arena.stride(0)), _i64(off_gamma), _i64(off_beta),
+                                   _p(alpha), _p(beta_c), _p(gamma_c), _pr(nimg), _i(hw), _stream(bstats))
     _check(rc, "fa_bn_bwd_finalize")
 
 
 def block_out(y, s, t, r, rs, rt, out, C, per_client, Ch, nimg=None, per_img=0):
     """out = relu(y·s + t + R) over the first nimg[c] images (per_img elements each) of every client."""
     rc = _fnp("fa_block_out", y)(_p(y), _p(s), _p(t), _p(r), _p(rs), _p(rt), _p(out), _i(C), _i64(per_client), _i(Ch),
-                             _p(nimg), _i(per_img), _stream(y))
+                             _pr(nimg), _i(per_img), _stream(y))
     _check(rc, "fa_block_out")
 
 
 def dy_apply(g, y, alpha, beta, gamma, out, C, per_client, Ch, nimg=None, per_img=0):
     """out = α·g + β·y + γ (the folded BN backward operand, materialised) over the valid images."""
     rc = _fnp("fa_dy_apply", g)(_p(g), _p(y), _p(alpha), _p(beta), _p(gamma), _p(out), _i(C), _i64(per_client), _i(Ch),
-                            _p(nimg), _i(per_img), _stream(g))
+                            _pr(nimg), _i(per_img), _stream(g))
     _check(rc, "fa_dy_apply")
 
 
 def avgpool(x, pooled, CN, HW, Ch, nimg=None, N=1):
-    rc = _fnp("fa_avgpool", x)(_p(x), _p(pooled), _i(CN), _i(HW), _i(Ch), _p(nimg), _i(N), _stream(x))
+    rc = _fnp("fa_avgpool", x)(_p(x), _p(pooled), _i(CN), _i(HW), _i(Ch), _pr(nimg), _i(N), _stream(x))
     _check(rc, "fa_avgpool")
 
 
 def head_bwd(dpool, out, y3, yd, gpre, stats, C, N, HW, Ch, NS, nimg=None):
     rc = _fnp("fa_head_bwd", out)(_p(dpool), _p(out), _p(y3), _p(yd), _p(gpre), _p(stats), _i(C), _i(N), _i(HW), _i(Ch),
-                            _i(NS), _p(nimg), _stream(out))
+                            _i(NS), _pr(nimg), _stream(out))
     _check(rc, "fa_head_bwd")
 
 
@@ -377,7 +377,7 @@ def fc_head_xent(pooled, arena, ow, ob, labels, row_scale, garena, dpool, loss_c
 def gnh_fwd(x, res, out, ms, arena, off_g, off_b, C, N, HW, Ch, G, eps, relu, nimg=None):
     """out = act(GN(x)·γ + β [+ res]) per (client, image); mean / rstd per group into ``ms`` [C, N, G, 2]."""
     rc = _fn("fa_gnh_fwd")(_i(x.dtype == torch.bfloat16), _p(x), _p(res), _p(out), _p(ms), _p(arena),
-                           _i64(arena.stride(0)), _i64(off_g), _i64(off_b), _p(nimg), _i(C), _i(N), _i(HW), _i(Ch),
+                           _i64(arena.stride(0)), _i64(off_g), _i64(off_b), _pr(nimg), _i(C), _i(N), _i(HW), _i(Ch),
                            _i(G), _f(eps), _i(int(relu)), _stream(x))
     _check(rc, "fa_gnh_fwd")
 
@@ -386,24 +386,24 @@ def gnh_bwd(x, go, act, dx, ms, pscr, arena, off_g, C, N, HW, Ch, G, nimg=None):
     """dx of a GroupNorm (upstream ``go`` masked by ``act > 0`` when ``act`` is given); per-image dγ / dβ partials
     into ``pscr`` [C, N, 2, Ch] (added into the gradient arena by ``gnh_param_reduce``)."""
     rc = _fn("fa_gnh_bwd")(_i(x.dtype == torch.bfloat16), _p(x), _p(go), _p(act), _p(dx), _p(ms), _p(pscr),
-                           _p(arena), _i64(arena.stride(0)), _i64(off_g), _p(nimg), _i(C), _i(N), _i(HW), _i(Ch),
+                           _p(arena), _i64(arena.stride(0)), _i64(off_g), _pr(nimg), _i(C), _i(N), _i(HW), _i(Ch),
                            _i(G), _stream(x))
     _check(rc, "fa_gnh_bwd")
 
 
 def gnh_param_reduce(pscr, garena, off_g, off_b, C, N, Ch, nimg=None):
     rc = _fn("fa_gnh_param_reduce")(_p(pscr), _p(garena), _i64(garena.stride(0)), _i64(off_g), _i64(off_b), _i(C),
-                                    _i(N), _i(Ch), _p(nimg), _stream(garena))
+                                    _i(N), _i(Ch), _pr(nimg), _stream(garena))
     _check(rc, "fa_gnh_param_reduce")
 
 
 def maxpool_fwd(x, y, idx, C, N, H, W, Ch, Ho, Wo, k, s, p, nimg=None):
     rc = _fn("fa_maxpool_fwd")(_i(x.dtype == torch.bfloat16), _p(x), _p(y), _p(idx), _i(C), _i(N), _i(H), _i(W),
-                               _i(Ch), _i(Ho), _i(Wo), _i(k), _i(s), _i(p), _p(nimg), _stream(x))
+                               _i(Ch), _i(Ho), _i(Wo), _i(k), _i(s), _i(p), _pr(nimg), _stream(x))
     _check(rc, "fa_maxpool_fwd")
 
 
 def maxpool_bwd(gy, idx, gx, C, N, H, W, Ch, Ho, Wo, k, s, p, nimg=None):
     rc = _fn("fa_maxpool_bwd")(_i(gy.dtype == torch.bfloat16), _p(gy), _p(idx), _p(gx), _i(C), _i(N), _i(H), _i(W),
-                               _i(Ch), _i(Ho), _i(Wo), _i(k), _i(s), _i(p), _p(nimg), _stream(gy))
+                               _i(Ch), _i(Ho), _i(Wo), _i(k), _i(s), _i(p), _pr(nimg), _stream(gy))
     _check(rc, "fa_maxpool_bwd")
