@@ -74,6 +74,7 @@ struct Args {
   int tiles_m, tiles_n, nclients;
   int acc_store;     // EPI_ACC32: the rows' first (only) writer — store instead of += (no zero fill of those rows)
   int64_t a_bytes, b_bytes;   // LDS-DMA kernel: per-client operand extents its buffer descriptors bound
+  int stage_epi;              // LDS-DMA kernel: bf16 epilogue staged through LDS (16-B row-contiguous stores)
 };
 
 // Constant-index selects only: a runtime index into the by-value kernel-argument struct would be lowered to
@@ -432,6 +433,7 @@ __global__ __launch_bounds__(256) void bias_grad_kernel(const uint16_t* __restri
 // DB = 1: two images per operand (64 KiB), next K-step's DMA in flight under this one's MFMAs;
 // DB = 0: one image (32 KiB, more blocks per CU), load → wait → compute.
 constexpr int GIMG = 128 * 64;   // elements of one operand image (16 KiB)
+constexpr int kStgLd = 128 + 4;  // fp32 epilogue staging row pitch (16-B rows, 4-bank shift per row)
 
 __device__ __forceinline__ int swz_nt(int r, int q) { return q ^ ((r >> 1) & 7); }
 __device__ __forceinline__ int swz_tr(int r, int h) { return h ^ ((r & 3) | ((r >> 1) & 4)); }
@@ -592,6 +594,72 @@ __global__ __launch_bounds__(NT, 2) void bgemm_dma_kernel(const Args p) {
         *bp = p.acc_store ? t : *bp + t;
       }
     }
+  }
+
+  if (EPI != EPI_ACC32 && p.stage_epi) {
+    // bf16 outputs through LDS: each 64-row half of the tile is staged in fp32 by the two waves that own it, then
+    // written by all 256 threads as 16-B chunks of whole 256-B rows (the MFMA layout stores 32-B row pieces)
+    float* stg = reinterpret_cast<float*>(smem);   // [64][kStgLd] fp32
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if ((wm >> 6) == h) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const f32x4 v = acc[i][j];
+            *reinterpret_cast<float4*>(stg + (16 * i + (lane & 15)) * kStgLd + wn + 16 * j + 4 * (lane >> 4)) =
+                make_float4(v[0], v[1], v[2], v[3]);
+          }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const int q = tid + NT * t, row = q >> 4, col = 8 * (q & 15);
+        const int m = m0 + 64 * h + row, n = n0 + col;
+        if (m < p.M && n < p.N) {
+          const float4 a0 = *reinterpret_cast<const float4*>(stg + row * kStgLd + col);
+          const float4 a1 = *reinterpret_cast<const float4*>(stg + row * kStgLd + col + 4);
+          float v[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+          if (p.bias) {
+            const float* bp = p.bias + (int64_t)c * p.bias_bs + seg_row(p.biasseg, n, 1);
+            const float4 b0 = *reinterpret_cast<const float4*>(bp), b1 = *reinterpret_cast<const float4*>(bp + 4);
+            v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w;
+            v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+          }
+          if (p.R) {
+            const uint4 rr = *reinterpret_cast<const uint4*>(p.R + (int64_t)c * p.r_bs + (int64_t)m * p.ldc + n);
+            const uint32_t w4[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float lo = bf16_to_f32((uint16_t)(w4[e] & 0xffff)), hi = bf16_to_f32((uint16_t)(w4[e] >> 16));
+              if (EPI == EPI_DGELU) {
+                v[2 * e] = gelu_grad(lo, v[2 * e]);
+                v[2 * e + 1] = gelu_grad(hi, v[2 * e + 1]);
+              } else {
+                v[2 * e] += lo;
+                v[2 * e + 1] += hi;
+              }
+            }
+          }
+          uint4 o;
+          o.x = pk2(v[0], v[1]); o.y = pk2(v[2], v[3]); o.z = pk2(v[4], v[5]); o.w = pk2(v[6], v[7]);
+          *reinterpret_cast<uint4*>((uint16_t*)p.Cp + (int64_t)c * p.c_bs + (int64_t)m * p.ldc + n) = o;
+          if (EPI == EPI_GELU) {   // GELU of the bf16-rounded pre-activation (what the backward recomputes from)
+            const uint32_t w4[4] = {o.x, o.y, o.z, o.w};
+            uint32_t g4[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              g4[e] = pk2(gelu_erf(bf16_to_f32((uint16_t)(w4[e] & 0xffff))),
+                          gelu_erf(bf16_to_f32((uint16_t)(w4[e] >> 16))));
+            *reinterpret_cast<uint4*>(p.C2 + (int64_t)c * p.c2_bs + (int64_t)m * p.ldc + n) =
+                make_uint4(g4[0], g4[1], g4[2], g4[3]);
+          }
+        }
+      }
+      __syncthreads();   // the staging rows are rewritten by the next half
+    }
+    return;
   }
 
 #pragma unroll
@@ -902,11 +970,18 @@ int launch(const Args& a, hipStream_t st) {
         return (int)hipGetLastError();
       }
     }
+    {   // staged epilogue: 16-B chunks need 8-element aligned rows / client strides / output columns
+      const char* se = getenv("FEDML_AMD_BGEMM_STAGE_EPI");
+      const bool want = se ? atoi(se) != 0 : true;
+      b.stage_epi = want && EPI != EPI_ACC32 && a.ldc % 8 == 0 && a.c_bs % 8 == 0 && a.N % 8 == 0 &&
+                    (!a.R || a.r_bs % 8 == 0) && (!a.C2 || a.c2_bs % 8 == 0);
+    }
     if (ok) {
       auto pick = [&](auto k1, auto k0) { return dma == 2 ? k0 : k1; };
       auto kern = seg ? pick(bgemm_dma_kernel<A_TR, B_TR, EPI, 1, 1>, bgemm_dma_kernel<A_TR, B_TR, EPI, 1, 0>)
                       : pick(bgemm_dma_kernel<A_TR, B_TR, EPI, 0, 1>, bgemm_dma_kernel<A_TR, B_TR, EPI, 0, 0>);
-      const size_t smem2 = (dma == 2 ? 2 : 4) * GIMG * sizeof(uint16_t);
+      const size_t smem2 = std::max<size_t>((dma == 2 ? 2 : 4) * GIMG * sizeof(uint16_t),
+                                            b.stage_epi ? 64 * kStgLd * sizeof(float) : 0);
       (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem2);
       hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(NT), smem2, st, b);
       return (int)hipGetLastError();

@@ -78,6 +78,8 @@ class UnsupportedNative(Exception):
 
 # workgroup target of the generic conv kernels (FEDML_AMD_CONV_WGS overrides, for tuning)
 _CONV_WGS = int(os.environ.get("FEDML_AMD_CONV_WGS", "1024"))   # scripts/gpu_conv_sweep.sh
+# workgroup target of the fused 1×1 backward on the small (8×8) stage (FEDML_AMD_C1F_WGS, for tuning)
+_C1F_WGS = int(os.environ.get("FEDML_AMD_C1F_WGS", "200"))
 
 def _round_up(v, m):
     return (v + m - 1) // m * m
@@ -598,7 +600,7 @@ class NativeResNetStep:
             return ppw
         if M >= 16384:
             return 512
-        target = M * self.plan_C // 200
+        target = M * self.plan_C // _C1F_WGS
         p = 256
         while p < 2048 and 2 * p <= target:
             p *= 2

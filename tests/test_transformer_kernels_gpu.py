@@ -159,16 +159,19 @@ def test_client_linear_fwd_bwd(C, M, K, ns, gelu, own, shadow):
     _linear_case(C, M, K, ns, gelu, own, shadow)
 
 
-@pytest.mark.parametrize("dma", ["0", "1", "2", "256"])
+@pytest.mark.parametrize("dma", ["0", "1", "2", "2u", "256"])
 @pytest.mark.parametrize("C,M,K,ns,gelu,own", [(3, 200, 768, [768, 768, 768], False, True),
                                                (2, 300, 768, [3072], True, True),
                                                (2, 520, 3072, [768], False, False)])
 def test_client_linear_dma_kernel(monkeypatch, dma, C, M, K, ns, gelu, own):
-    """bf16-shadow GEMMs on the LDS-DMA kernel (FEDML_AMD_BGEMM_DMA 1: double-buffered images, 2: one image) and on
-    the register-staged kernel (0): forward (+GELU, segmented q/k/v rows), data gradient (segmented TR weight rows),
+    """bf16-shadow GEMMs on the LDS-DMA kernel (FEDML_AMD_BGEMM_DMA 1: double-buffered images, 2: one image; the bf16
+    epilogue staged through LDS by default, "2u": stored from the MFMA layout) and on the register-staged kernel (0): forward (+GELU, segmented q/k/v rows), data gradient (segmented TR weight rows),
     weight gradient with the fused bias sum; ragged row and reduction extents (zero-filled by the descriptors)."""
     if dma == "256":     # the 256 × 256 DMA tile forced for every layout and grid
         monkeypatch.setenv("FEDML_AMD_BGEMM_256", "2")
+    elif dma == "2u":    # single image, epilogue stored straight from the MFMA layout (not staged through LDS)
+        monkeypatch.setenv("FEDML_AMD_BGEMM_DMA", "2")
+        monkeypatch.setenv("FEDML_AMD_BGEMM_STAGE_EPI", "0")
     else:
         monkeypatch.setenv("FEDML_AMD_BGEMM_DMA", dma)
     _linear_case(C, M, K, ns, gelu, own, True)
