@@ -594,11 +594,13 @@ __global__ __launch_bounds__(NT, 2) void bgemm_dma_kernel(const Args p) {
         *bp = p.acc_store ? t : *bp + t;
       }
     }
+    __syncthreads();   // the reduction scratch is the epilogue staging area
   }
 
-  if (EPI != EPI_ACC32 && p.stage_epi) {
-    // bf16 outputs through LDS: each 64-row half of the tile is staged in fp32 by the two waves that own it, then
-    // written by all 256 threads as 16-B chunks of whole 256-B rows (the MFMA layout stores 32-B row pieces)
+  if (p.stage_epi) {
+    // outputs through LDS: each 64-row half of the tile is staged in fp32 by the two waves that own it, then
+    // written by all 256 threads as 16-B chunks of whole rows (the MFMA layout stores 32-B (bf16) / 64-B (fp32)
+    // row pieces)
     float* stg = reinterpret_cast<float*>(smem);   // [64][kStgLd] fp32
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -613,6 +615,24 @@ __global__ __launch_bounds__(NT, 2) void bgemm_dma_kernel(const Args p) {
           }
       }
       __syncthreads();
+      if (EPI == EPI_ACC32) {   // fp32 weight gradient rows of the arena: += (or = for the first writer)
+#pragma unroll
+        for (int t = 0; t < 8; ++t) {
+          const int q = tid + NT * t, row = q >> 5, col = 4 * (q & 31);
+          const int m = m0 + 64 * h + row, n = n0 + col;
+          if (m < p.M && n < p.N) {
+            float4 o = *reinterpret_cast<const float4*>(stg + row * kStgLd + col);
+            float* dst = (float*)p.Cp + (int64_t)c * p.c_bs + seg_row(p.cseg, m, p.ldc) + n;
+            if (!p.acc_store) {
+              const float4 q4 = *reinterpret_cast<const float4*>(dst);
+              o.x += q4.x; o.y += q4.y; o.z += q4.z; o.w += q4.w;
+            }
+            *reinterpret_cast<float4*>(dst) = o;
+          }
+        }
+        __syncthreads();
+        continue;
+      }
 #pragma unroll
       for (int t = 0; t < 4; ++t) {
         const int q = tid + NT * t, row = q >> 4, col = 8 * (q & 15);
@@ -973,8 +993,10 @@ int launch(const Args& a, hipStream_t st) {
     {   // staged epilogue: 16-B chunks need 8-element aligned rows / client strides / output columns
       const char* se = getenv("FEDML_AMD_BGEMM_STAGE_EPI");
       const bool want = se ? atoi(se) != 0 : true;
-      b.stage_epi = want && EPI != EPI_ACC32 && a.ldc % 8 == 0 && a.c_bs % 8 == 0 && a.N % 8 == 0 &&
-                    (!a.R || a.r_bs % 8 == 0) && (!a.C2 || a.c2_bs % 8 == 0);
+      b.stage_epi = want && (EPI == EPI_ACC32
+                                 ? (a.ldc % 4 == 0 && a.c_bs % 4 == 0 && a.N % 4 == 0)
+                                 : (a.ldc % 8 == 0 && a.c_bs % 8 == 0 && a.N % 8 == 0 && (!a.R || a.r_bs % 8 == 0) &&
+                                    (!a.C2 || a.c2_bs % 8 == 0)));
     }
     if (ok) {
       auto pick = [&](auto k1, auto k0) { return dma == 2 ? k0 : k1; };
