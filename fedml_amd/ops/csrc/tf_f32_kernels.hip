@@ -91,6 +91,7 @@ struct Args {
   int tiles_m, tiles_n, nclients;
   int acc_store;     // ACC: the first (and only) writer of these gradient rows — store instead of +=, so the
                      // arena rows need no zero fill (each element has exactly one producing tile: no split-K)
+  int stage_epi;     // VEC: epilogue through LDS, row-contiguous 16-B chunks (FEDML_AMD_TF_STAGE_EPI=0: off)
 };
 
 __device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.70710678118654752f)); }
@@ -294,6 +295,64 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(const Args p) {
       gemm_mainloop<P, A_TR, B_TR, VEC, 1>(acc, A, aseg, B, p, m0, n0, nk, SA0, SB0, tid, lane, wm, wn, bs);
   }
 
+  if (VEC && p.stage_epi) {
+    // the tile through LDS (free after the main loop; the bias-sum scratch above is consumed): each 64-row half
+    // staged by the two waves that own it, then written by all 256 threads as 16-B chunks of whole 512-B rows —
+    // the MFMA layout stores 64-B row pieces
+    constexpr int SLD = BN + 4;
+    float* stg = smem;   // [64][SLD]
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if ((wm >> 6) == h) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const f32x4 v = acc[i][j];
+            *reinterpret_cast<float4*>(stg + (16 * i + (lane & 15)) * SLD + wn + 16 * j + 4 * (lane >> 4)) =
+                make_float4(v[0], v[1], v[2], v[3]);
+          }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int q = tid + NT * t, row = q >> 5, col = 4 * (q & 31);
+        const int m = m0 + 64 * h + row, n = n0 + col;
+        if (m >= p.M || n >= p.N) continue;
+        float4 v = *reinterpret_cast<const float4*>(stg + row * SLD + col);
+        if (EPI == EPI_ACC) {
+          float* dst = p.Cp + (int64_t)c * p.c_bs + seg_row(p.cseg, m, p.ldc) + n;
+          if (!p.acc_store) {
+            const float4 q4 = *reinterpret_cast<const float4*>(dst);
+            v.x += q4.x; v.y += q4.y; v.z += q4.z; v.w += q4.w;
+          }
+          *reinterpret_cast<float4*>(dst) = v;
+          continue;
+        }
+        if (p.bias) {
+          const float4 b = *reinterpret_cast<const float4*>(p.bias + (int64_t)c * p.bias_bs + seg_row(p.biasseg, n, 1));
+          v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+        }
+        if (EPI == EPI_DGELU) {
+          const float4 x4 = *reinterpret_cast<const float4*>(p.R + (int64_t)c * p.r_bs + (int64_t)m * p.ldr + n);
+          v.x = gelu_grad(x4.x, v.x); v.y = gelu_grad(x4.y, v.y);
+          v.z = gelu_grad(x4.z, v.z); v.w = gelu_grad(x4.w, v.w);
+        }
+        if (EPI == EPI_STORE && p.R) {
+          const float4 r4 = *reinterpret_cast<const float4*>(p.R + (int64_t)c * p.r_bs + (int64_t)m * p.ldr + n);
+          v.x += r4.x; v.y += r4.y; v.z += r4.z; v.w += r4.w;
+        }
+        const int64_t o = (int64_t)c * p.c_bs + (int64_t)m * p.ldc + n;
+        *reinterpret_cast<float4*>(p.Cp + o) = v;
+        if (EPI == EPI_GELU)
+          *reinterpret_cast<float4*>(p.C2 + o) = make_float4(gelu_erf(v.x), gelu_erf(v.y), gelu_erf(v.z), gelu_erf(v.w));
+      }
+      __syncthreads();
+    }
+    return;
+  }
+
   // epilogue: lane owns row m = m0 + wm + 16i + (lane & 15), cols n .. n+3, n = n0 + wn + 16j + 4(lane >> 4)
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -376,10 +435,14 @@ template <class P, int A_TR, int B_TR, int EPI>
 int launch_gemm(const Args& a, bool vec, hipStream_t st) {
   const int64_t blocks = (int64_t)a.tiles_m * a.tiles_n * a.nclients;
   if (blocks <= 0 || blocks > 0x7fffffff) return (int)hipErrorInvalidValue;
-  const size_t smem = 4 * TILE * sizeof(float);   // 72 KiB: 2 blocks per CU
+  const size_t smem = 4 * TILE * sizeof(float);   // 72 KiB: 2 blocks per CU (≥ the 33 KiB epilogue staging)
+  static_assert(4 * TILE >= 64 * (BN + 4), "epilogue staging must fit the operand images");
   auto kern = vec ? gemm_kernel<P, A_TR, B_TR, EPI, 1> : gemm_kernel<P, A_TR, B_TR, EPI, 0>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(NT), smem, st, a);
+  Args b = a;
+  const char* se = getenv("FEDML_AMD_TF_STAGE_EPI");
+  b.stage_epi = se ? atoi(se) != 0 : 1;
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(NT), smem, st, b);
   return (int)hipGetLastError();
 }
 

@@ -416,3 +416,21 @@ def test_client_embedding_grad_into_strided_arena():
         view[c].index_add_(0, ids[c], g[c])
     assert torch.allclose(grads, ref, rtol=1e-5, atol=1e-5)
     assert torch.equal(grads[:, :7], before[:, :7]) and torch.equal(grads[:, 7 + V * d:], before[:, 7 + V * d:])
+
+
+@pytest.mark.parametrize("C,M,K,ns,gelu", [(3, 200, 768, [768, 768, 768], False), (4, 130, 256, [1024], True)])
+def test_staged_epilogue_bitwise_equals_direct_stores(monkeypatch, C, M, K, ns, gelu):
+    """FEDML_AMD_TF_STAGE_EPI: the fp32 GEMM epilogue through LDS (row-contiguous 16-B chunks) does the same per-element
+    arithmetic as the stores from the MFMA layout — forward, data and weight gradients must agree bit for bit."""
+    outs = []
+    for stage in ("0", "1"):
+        monkeypatch.setenv("FEDML_AMD_TF_STAGE_EPI", stage)
+        torch.manual_seed(0)
+        vs = _arena_views(C, [(n, K) for n in ns] + [(n,) for n in ns])
+        ws, bs = vs[:len(ns)], vs[len(ns):]
+        x = torch.randn(C, M, K, device=dev).requires_grad_(True)
+        y = T.client_linear(x, ws, bs, gelu=gelu)
+        y.backward(torch.ones_like(y))
+        outs.append([y.detach().clone(), x.grad.clone()] + [t.grad.clone() for t in vs])
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
