@@ -31,10 +31,14 @@ MSG_TYPE_CONNECTION_IS_READY = 0
 
 
 class InProcessBroker:
-    """Topic → subscriber callbacks, retained last-will messages, connection tracking."""
+    """Topic → subscriber callbacks, retained last-will messages, connection tracking. A message published to a
+    topic nobody has subscribed to YET is held and delivered to its first subscriber (a persistent-session broker's
+    behaviour): the peers of an in-process run start in threads, and a status message sent before the other side
+    subscribed was lost under load — a rare hang of the MQTT_S3 cross-silo test."""
 
     def __init__(self):
         self._subs: Dict[str, List[Callable]] = defaultdict(list)
+        self._held: Dict[str, List[bytes]] = defaultdict(list)
         self._wills: Dict[str, tuple] = {}
         self._lock = threading.Lock()
         self.published = 0
@@ -51,6 +55,9 @@ class InProcessBroker:
     def subscribe(self, topic: str, cb: Callable[[str, bytes], None]):
         with self._lock:
             self._subs[topic].append(cb)
+            held = self._held.pop(topic, [])
+        for payload in held:
+            cb(topic, payload)
 
     def unsubscribe_all(self, cb):
         with self._lock:
@@ -61,6 +68,8 @@ class InProcessBroker:
         with self._lock:
             cbs = list(self._subs.get(topic, ()))
             self.published += 1
+            if not cbs:
+                self._held[topic].append(payload)
         for cb in cbs:
             cb(topic, payload)
 
