@@ -73,7 +73,7 @@ class ValuedRCCLSimulator(RCCLSimulator):
                                       int(args.batch_size))
         self.valid = [(x.to(self.device), y.to(self.device)) for x, y in valid]
         self.evaluator = BatchedModelEvaluator(self.model, self.device,
-                                               max_models=int(getattr(args, "sv_batch_models", 32)),
+                                               max_models=int(getattr(args, "sv_batch_models", 128)),
                                                compute_dtype=self.compute_dtype)
         K = self.K_total
         self.phi = [1.0 / K] * K

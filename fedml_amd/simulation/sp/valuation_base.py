@@ -101,7 +101,7 @@ class ValuedFedAvgBase(FedAvgAPI):
         self.score = str(score)
         self.seed = int(getattr(args, "random_seed", 0) or 0)
         self.evaluator = BatchedModelEvaluator(self.model_trainer.model, device,
-                                               max_models=int(getattr(args, "sv_batch_models", 32)))
+                                               max_models=int(getattr(args, "sv_batch_models", 128)))
 
     def _validation_subset(self, n):
         """Random subset of the global test set as the server-side validation set."""

@@ -61,7 +61,7 @@ def main():
     p.add_argument("--lr", type=float, default=0.01)
     p.add_argument("--valid", type=int, default=500)
     p.add_argument("--rounds", type=int, default=2)
-    p.add_argument("--sv-batch", type=int, default=32)
+    p.add_argument("--sv-batch", type=int, default=128)
     p.add_argument("--mc", action="store_true", help="Monte-Carlo Shapley (sv_approaching) instead of exact")
     p.add_argument("--skip-sp", action="store_true")
     a = p.parse_args()
