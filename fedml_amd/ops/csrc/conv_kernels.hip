@@ -745,19 +745,50 @@ __global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
   const int col = threadIdx.x % CK::CPR;
   const int row0 = threadIdx.x / CK::CPR;
   const int IW = MODE == MODE_BWD2 ? a.Ws : (S2 ? Wc : a.Wo);
+  // Uniform-tap path (every ResNet-18 wide layer: KC % KB == 0): a K-chunk then lies inside ONE tap, so the
+  // tap, its pixel delta and the channel base are wave-uniform. Each staged row keeps its base element
+  // offset and a validity bit per tap (computed once), and a chunk's gather costs one add and one bit test
+  // per row — the generic decode below (two runtime divisions, bounds and 64-bit offsets per row and chunk)
+  // made this kernel VALU-issue-bound: ~420 VALU instructions per 32 MFMAs of a chunk (profiles/r5_convk_valu.txt).
+  const int ntap = S2 ? nth * ntw : a.KH * a.KW;
+  const bool UT = (a.KC % KB == 0) && ntap <= 32 && (MODE != MODE_BWD || a.stride == 1) &&
+                  (int64_t)a.Nb * a.Hs * a.Ws * a.KC < (1ll << 31);   // 32-bit element offsets
   int rn[CK::NA], rhw[CK::NA];   // image index, (h << 16 | w) of the row's iteration pixel; rn < 0: invalid
+  int rbase[CK::NA];             // UT: element offset of the row's tap-(0,0) source pixel + this thread's column
+  uint32_t rmask[CK::NA];        // UT: bit t = tap t of this row reads inside the image
 #pragma unroll
   for (int j = 0; j < CK::NA; ++j) {
     const int m = m0 + row0 + CK::RPI * j;
+    rbase[j] = 0;
+    rmask[j] = 0;
     if (m < Mv) {
       rn[j] = m / HWi;
       const int r = m % HWi;
-      rhw[j] = ((r / IW) << 16) | (r % IW);
+      const int ph = r / IW, pw = r % IW;
+      rhw[j] = (ph << 16) | pw;
+      if (UT) {
+        // source pixel of tap t = (h0 + dh(t), w0 + dw(t)), dh/dw as in tap_delta below
+        int h0, w0;
+        if (MODE == MODE_FWD) { h0 = ph * a.stride - a.pad; w0 = pw * a.stride - a.pad; }
+        else if (MODE == MODE_BWD) { h0 = ph + a.pad; w0 = pw + a.pad; }
+        else if (MODE == MODE_BWD2) { h0 = ph; w0 = pw; }
+        else { h0 = ph + ((r0 + a.pad - qh) >> 1); w0 = pw + ((c0 + a.pad - qw) >> 1); }
+        rbase[j] = ((rn[j] * a.Hs + h0) * a.Ws + w0) * a.KC + col * V;
+        for (int t = 0; t < ntap; ++t) {
+          const int tr = S2 ? t / ntw : t / a.KW, tc = S2 ? t % ntw : t % a.KW;
+          const int ih = MODE == MODE_FWD ? h0 + tr : h0 - tr, iw = MODE == MODE_FWD ? w0 + tc : w0 - tc;
+          if ((unsigned)ih < (unsigned)a.Hs && (unsigned)iw < (unsigned)a.Ws) rmask[j] |= 1u << t;
+        }
+      }
     } else {
       rn[j] = -1;
       rhw[j] = 0;
     }
   }
+  // UT chunk state (uniform): tap index and channel base of the chunk fetched last, advanced per fetch
+  int u_tap = 0, u_ci0 = 0, u_tr = 0, u_tc = 0;
+  const int u_tcn = S2 ? ntw : a.KW;   // taps per tap row
+  const int wrow = row0 * a.ldk + col * V;
 
   f32x4 acc[TM][NT];
 #pragma unroll
@@ -768,12 +799,46 @@ __global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
   uint4 ra[CK::NA], ry[TWO ? CK::NA : 1], rb[CK::NB];
   int64_t aoff[BOUT ? CK::NA : 1];   // PRO_BOUT: the operand element's position (pro_out write)
   uint32_t aval = 0;
+  int p_ci = 0;                      // channel of this thread's first element in the fetched chunk
   auto fetch = [&](int kbase) {
+    if (UT) {
+      if (kbase == 0) { u_tap = 0; u_ci0 = 0; u_tr = 0; u_tc = 0; }
+      const int dh = MODE == MODE_FWD ? u_tr : -u_tr, dw = MODE == MODE_FWD ? u_tc : -u_tc;
+      const int uoff = (dh * a.Ws + dw) * a.KC + u_ci0;
+      const int kh = S2 ? qh + 2 * u_tr : u_tr, kw = S2 ? qw + 2 * u_tc : u_tc;
+      const int kcol = (kh * a.KW + kw) * a.KC + u_ci0;   // column of the packed weights (chunk start)
+      p_ci = u_ci0 + col * V;
+      aval = 0;
+#pragma unroll
+      for (int j = 0; j < CK::NA; ++j) {
+        ra[j] = make_uint4(0, 0, 0, 0);
+        if (TWO) ry[j] = make_uint4(0, 0, 0, 0);
+        if ((rmask[j] >> u_tap) & 1u) {
+          const int off = rbase[j] + uoff;
+          ra[j] = *reinterpret_cast<const uint4*>(src + off);
+          if (TWO) ry[j] = *reinterpret_cast<const uint4*>(src2 + off);
+          if constexpr (BOUT) aoff[j] = off;
+          aval |= 1u << j;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < CK::NB; ++j)
+        rb[j] = *reinterpret_cast<const uint4*>(wsrc + kcol + (wrow + CK::RPI * j * a.ldk));
+      // advance to the next chunk: channel base, then tap (column, row)
+      u_ci0 += KB;
+      if (u_ci0 == a.KC) {
+        u_ci0 = 0;
+        ++u_tap;
+        if (++u_tc == u_tcn) { u_tc = 0; ++u_tr; }
+      }
+      return;
+    }
     const int k = kbase + col * V;
     const bool kval = k < K;
     const int tap = kval ? k / a.KC : 0, ci = kval ? k % a.KC : 0;
     const int kh = S2 ? qh + 2 * (tap / ntw) : tap / a.KW, kw = S2 ? qw + 2 * (tap % ntw) : tap % a.KW;
     const int kcol = S2 ? (kh * a.KW + kw) * a.KC + ci : k;   // column of the packed weights
+    p_ci = ci;
     aval = 0;
 #pragma unroll
     for (int j = 0; j < CK::NA; ++j) {
@@ -814,9 +879,19 @@ __global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
       rb[j] = kval ? *reinterpret_cast<const uint4*>(wsrc + (int64_t)(row0 + CK::RPI * j) * a.ldk + kcol)
                    : make_uint4(0, 0, 0, 0);
   };
-  auto put = [&](int kbase) {
-    const int k = kbase + col * V;
-    const int ci = k < K ? k % a.KC : 0;
+  auto put = [&](int) {
+    const int ci = p_ci;
+    // the chunk's per-channel coefficients, read from LDS once for all NA rows (the row loop's LDS stores
+    // otherwise make the compiler re-read them per row)
+    float c0v[(PRO == PRO_BNRELU || DY) ? V : 1], c1v[(PRO == PRO_BNRELU || DY) ? V : 1], c2v[DY ? V : 1];
+    if constexpr (PRO == PRO_BNRELU || DY) {
+#pragma unroll
+      for (int e = 0; e < V; ++e) {
+        c0v[e] = v0[ci + e];
+        c1v[e] = v1[ci + e];
+        if (DY) c2v[e] = v2[ci + e];
+      }
+    }
 #pragma unroll
     for (int j = 0; j < CK::NA; ++j) {
       uint4 v = make_uint4(0, 0, 0, 0);   // out-of-image taps / padding rows: 0 (not the transform of 0)
@@ -840,10 +915,10 @@ __global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
             float yv[V];
             P::unpack(ry[j], yv);
 #pragma unroll
-            for (int e = 0; e < V; ++e) f[e] = v0[ci + e] * f[e] + v1[ci + e] * yv[e] + v2[ci + e];
+            for (int e = 0; e < V; ++e) f[e] = c0v[e] * f[e] + c1v[e] * yv[e] + c2v[e];
           } else {
 #pragma unroll
-            for (int e = 0; e < V; ++e) f[e] = fmaxf(f[e] * v0[ci + e] + v1[ci + e], 0.f);
+            for (int e = 0; e < V; ++e) f[e] = fmaxf(f[e] * c0v[e] + c1v[e], 0.f);
           }
           v = P::pack(f);
         } else {

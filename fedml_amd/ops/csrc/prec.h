@@ -30,6 +30,8 @@ typedef __bf16 bf16x8v __attribute__((ext_vector_type(8)));
 typedef short v4i16v __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) v4i16v lds_v4i16v;
 typedef float f32x8v __attribute__((ext_vector_type(8)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
 
 struct BF16 {
   using T = uint16_t;
@@ -47,8 +49,11 @@ struct BF16 {
     f[4] = __uint_as_float(v.z << 16); f[5] = __uint_as_float(v.z & 0xffff0000u);
     f[6] = __uint_as_float(v.w << 16); f[7] = __uint_as_float(v.w & 0xffff0000u);
   }
+  // one v_cvt_pk_bf16_f32 for the pair (the same RNE conversion as two scalar casts, which the compiler
+  // emitted as two converts plus an OR)
   static __device__ __forceinline__ uint32_t pack2(float a, float b) {
-    return (uint32_t)f32_to_bf16(a) | ((uint32_t)f32_to_bf16(b) << 16);
+    const f32x2v v = {a, b};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v));
   }
   static __device__ __forceinline__ uint4 pack(const float* f) {
     return make_uint4(pack2(f[0], f[1]), pack2(f[2], f[3]), pack2(f[4], f[5]), pack2(f[6], f[7]));

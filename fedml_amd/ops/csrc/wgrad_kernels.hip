@@ -328,9 +328,32 @@ __global__ __launch_bounds__(256) void wgrad_wide_kernel(
     return q + (r >= b) - (r < 0);
   };
 
-  const T* gc = g + (int64_t)c * M * Cout + co_lo + col;
-  const T* yc = DYM ? gc : yv + (int64_t)c * M * Cout + co_lo + col;
-  const T* xc = x + (int64_t)c * Nb * H * W * Cin + ci0;
+  // buffer descriptors over this client's operands (wave-uniform inputs made provably uniform by readfirstlane,
+  // else hipcc wraps each buffer op in a waterfall loop): per-row 32-bit byte offsets, one VALU add each, and an
+  // offset past num_records loads zeros (rows past the chunk, out-of-image taps) without a branch
+  auto rsrc = [](const void* base, int64_t bytes) {
+    const uint64_t a = (uint64_t)base;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    const int nb = __builtin_amdgcn_readfirstlane((int)bytes);
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, nb, 0x00020000);
+  };
+  typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+  auto bl = [](__amdgpu_buffer_rsrc_t r, uint32_t off) {
+    const u32x4v v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 0);
+    return make_uint4(v.x, v.y, v.z, v.w);
+  };
+  constexpr uint32_t kOOB = 0x80000000u;   // ≥ every num_records (the launcher keeps them below 2^31 bytes)
+  const int64_t dy_bytes = (int64_t)M * Cout * (int64_t)sizeof(T);
+  const __amdgpu_buffer_rsrc_t sg = rsrc(g + (int64_t)c * M * Cout, dy_bytes);
+  const __amdgpu_buffer_rsrc_t sy = rsrc(DYM ? g + (int64_t)c * M * Cout : yv + (int64_t)c * M * Cout, dy_bytes);
+  const __amdgpu_buffer_rsrc_t sx = rsrc(x + (int64_t)c * Nb * H * W * Cin, (int64_t)Nb * H * W * Cin * (int64_t)sizeof(T));
+  // Per staged row: the pixel decoded by shifts when Ho·Wo and Wo are powers of two — the 64-bit offsets and
+  // float-reciprocal divisions cost ~60 VALU instructions per row, which made this kernel VALU-issue-bound
+  // (~380 VALU per 32 MFMAs of a sub-tile; profiles/r5_convk_valu.txt)
+  const int sh_w = (Wo & (Wo - 1)) == 0 ? __builtin_ctz(Wo) : -1;
+  const int sh_hw = (sh_w >= 0 && (HWo & (HWo - 1)) == 0) ? __builtin_ctz(HWo) : -1;
+  const int xh = kh - pad, xw = kw - pad;
   uint4 rg[NI], ry[NI], rx[NI];
   uint32_t dvalid = 0, avalid = 0;
   auto load_sub = [&](int p0) {
@@ -339,23 +362,28 @@ __global__ __launch_bounds__(256) void wgrad_wide_kernel(
 #pragma unroll
     for (int it = 0; it < NI; ++it) {
       const int p = p0 + pp0 + RPI * it;
-      rg[it] = make_uint4(0, 0, 0, 0);
-      ry[it] = make_uint4(0, 0, 0, 0);
-      rx[it] = make_uint4(0, 0, 0, 0);
-      if (p < p_end) {
-        dvalid |= 1u << it;
-        rg[it] = *reinterpret_cast<const uint4*>(gc + (int64_t)p * Cout);
-        if (!DYM) ry[it] = *reinterpret_cast<const uint4*>(yc + (int64_t)p * Cout);
-        if (kval) {
-          const int n = fdiv(p, HWo, inv_hw), r = p - n * HWo;
-          const int oh = fdiv(r, Wo, inv_w), ow = r - oh * Wo;
-          const int ih = oh * stride - pad + kh, iw = ow * stride - pad + kw;
-          if (ih >= 0 && ih < H && iw >= 0 && iw < W) {
-            rx[it] = *reinterpret_cast<const uint4*>(xc + (((int64_t)n * H + ih) * W + iw) * Cin);
-            avalid |= 1u << it;
-          }
-        }
+      if (DYM) ry[it] = make_uint4(0, 0, 0, 0);
+      const bool pv = p < p_end;
+      dvalid |= (uint32_t)pv << it;
+      const uint32_t go = pv ? (uint32_t)(p * Cout + co_lo + col) * (uint32_t)sizeof(T) : kOOB;
+      rg[it] = bl(sg, go);
+      if (!DYM) ry[it] = bl(sy, go);
+      int n, oh, ow;
+      if (sh_hw >= 0) {
+        n = p >> sh_hw;
+        const int r = p & (HWo - 1);
+        oh = r >> sh_w;
+        ow = r & (Wo - 1);
+      } else {
+        n = fdiv(p, HWo, inv_hw);
+        const int r = p - n * HWo;
+        oh = fdiv(r, Wo, inv_w);
+        ow = r - oh * Wo;
       }
+      const int ih = oh * stride + xh, iw = ow * stride + xw;
+      const bool ok = pv && kval && (unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W;
+      rx[it] = bl(sx, ok ? (uint32_t)(((n * H + ih) * W + iw) * Cin + ci0) * (uint32_t)sizeof(T) : kOOB);
+      avalid |= (uint32_t)ok << it;
     }
   };
   auto store_sub = [&]() {
@@ -444,6 +472,8 @@ static int wgrad_wide(const typename P::T* g, const typename P::T* yv, const flo
   const int nks = (K + 127) / 128;
   const int base = fa_plan_c(C) * nks * (Cout / 128);
   const int M = Nb * Ho * Wo;
+  // the kernel's buffer descriptors and per-row byte offsets are 32-bit
+  if ((int64_t)M * Cout * P::ES >= (1ll << 31) || (int64_t)Nb * H * W * Cin * P::ES >= (1ll << 31)) return -8;
   // pixel chunks: enough workgroups to fill the chip (FEDML_AMD_WGW_WGS; measured on ResNet-18 ×10: fp32 2048,
   // bf16 1024 — 1.257 → 1.282 rounds/s), chunks of ≥ 512 pixels. One chunk (gx = 1) writes the gradient arena
   // directly — no fp32-atomic scratch and no scatter pass.
