@@ -250,6 +250,7 @@ struct Args {              // tensors are P::T (bf16 | fp32) unless noted
   int nout_total;                 // output channels of the layer (a workgroup computes NOUT of them)
   FastDiv fd_trtw, fd_tw, fd_rw, fd_w;  // ÷ TR·TW, ÷ TW (tile), ÷ R·W, ÷ W (output unit)
   const BnLazy* lz0;              // XF_BNRELU: deferred finalisation of the prologue BN (bnlazy.h) or null
+  int xcd;                        // XCD-aware block order (FEDML_AMD_C3_XCD, default on)
 };
 
 // MTW 16-pixel tiles per wave share every B fragment read.
@@ -270,7 +271,20 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
   constexpr int LD = P::pitch(KC);
   constexpr int K = 9 * KC;
   constexpr int KSTEPS = (K + 31) / 32;
-  const int c = blockIdx.y;
+  // XCD-aware order: workgroups go round-robin over the 8 XCDs (linear id mod 8). Remap so each XCD runs a
+  // contiguous client-major run of (unit block, output slice) with the slice fastest: the NOUT/32 slices of one
+  // unit block — which stage the SAME input tile — then run back to back on one XCD and the later ones read the
+  // tile from that XCD's L2 instead of HBM
+  int bx = blockIdx.x, bz = blockIdx.z, c = blockIdx.y;
+  if (a.xcd) {
+    const int gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
+    const int total = gx * gy * gz, full = total / 8 * 8;
+    int lin = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    if (lin < full) lin = (lin % 8) * (full / 8) + lin / 8;
+    bz = lin % gz;
+    bx = (lin / gz) % gx;
+    c = lin / (gz * gx);
+  }
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int g = lane >> 4;
@@ -280,7 +294,7 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
   constexpr bool UPS = BWD && ST == 2;
   const int TW = (UPS ? W : Ws) + 2;             // tile width incl. halo
   const int Ne = client_images(a.nimg, c, a.N);
-  const int u_lo = blockIdx.x * a.units_per_wg;
+  const int u_lo = bx * a.units_per_wg;
   const int u_hi = min(client_units(Ne, H, a.R, a.S), u_lo + a.units_per_wg);
   if (u_lo >= u_hi) return;   // no valid images in this workgroup's units (uniform: whole workgroup)
 
@@ -294,7 +308,7 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
   float* etL = esL + NOUT;
   T* tile = reinterpret_cast<T*>(etL + NOUT);                                     // [S][TR][TW][LD]
 
-  const int ch_base = blockIdx.z * NOUT;  // output-channel slice of this workgroup
+  const int ch_base = bz * NOUT;  // output-channel slice of this workgroup
   const int NO = a.nout_total;
   {
     const uint4* s = reinterpret_cast<const uint4*>(reinterpret_cast<const T*>(a.wpk) + (int64_t)c * a.wpk_ld +
@@ -305,7 +319,7 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
     if (XF != XF_NONE)
       for (int i = threadIdx.x; i < KC; i += 256) {
         if (XF == XF_BNRELU && a.lz0) {
-          bn_lazy_fwd(a.lz0, c, i, blockIdx.x == 0 && blockIdx.z == 0, v0[i], v1[i]);
+          bn_lazy_fwd(a.lz0, c, i, bx == 0 && bz == 0, v0[i], v1[i]);
         } else {
           v0[i] = a.vec0[(int64_t)c * KC + i];
           v1[i] = a.vec1[(int64_t)c * KC + i];
@@ -555,6 +569,7 @@ struct WArgs {           // activations are P::T
   int R, S, units, units_per_wg;
   int nt_per_z;           // GEMM column tiles (16 wide) per blockIdx.z
   FastDiv fd_trtw, fd_tw, fd_rw, fd_w;
+  int xcd;                // XCD-aware block order (FEDML_AMD_C3_XCD, default on)
 };
 
 // WN waves split the column tiles of this z-slice, WK = 4/WN waves split the pixel K-steps.
@@ -566,8 +581,19 @@ __global__ __launch_bounds__(256, (MAXC <= 8 ? C3W_MIN_WAVES : 1)) void conv3x3_
   constexpr int MT = COUT / 16;
   constexpr int LDX = P::pitch_tr(CIN), LDD = P::pitch_tr(COUT);
   constexpr int K = 9 * CIN;
-  int c = blockIdx.y;
-  if (a.tab) {   // layer l = blockIdx.y / C (uniform: scalar loads of its operand pointers)
+  // XCD-aware order as in conv3x3_gemm_kernel: the column slices (z) of one pixel chunk stage the same dy and x
+  // tiles, so they run back to back on one XCD and share its L2
+  int bx = blockIdx.x, bz = blockIdx.z, c = blockIdx.y;
+  if (a.xcd) {
+    const int gx = gridDim.x, gy = gridDim.y, gz = gridDim.z;
+    const int total = gx * gy * gz, full = total / 8 * 8;
+    int lin = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+    if (lin < full) lin = (lin % 8) * (full / 8) + lin / 8;
+    bz = lin % gz;
+    bx = (lin / gz) % gx;
+    c = lin / (gz * gx);
+  }
+  if (a.tab) {   // layer l = (block row) / C (uniform: scalar loads of its operand pointers)
     const int Cc = gridDim.y / a.nl, l = c / Cc;
     c -= l * Cc;
     const WPtrs q = a.tab[l];
@@ -580,11 +606,11 @@ __global__ __launch_bounds__(256, (MAXC <= 8 ? C3W_MIN_WAVES : 1)) void conv3x3_
   const int kgrp = wid / WN, ngrp = wid % WN;
   const int H = a.H, W = a.W, HW = H * W;
   const int Hs = a.Hs, Ws = a.Ws, TW = Ws + 2;
-  const int nt_lo = blockIdx.z * a.nt_per_z;
+  const int nt_lo = bz * a.nt_per_z;
   const int nt_hi = min(K / 16, nt_lo + a.nt_per_z);
   const int my_nt0 = nt_lo + ngrp * TPW;  // this wave's column tiles [my_nt0, my_nt0 + TPW) ∩ [.., nt_hi)
   const int Ne = client_images(a.nimg, c, a.N);
-  const int u_lo = blockIdx.x * a.units_per_wg;
+  const int u_lo = bx * a.units_per_wg;
   const int u_hi = min(client_units(Ne, H, a.R, a.S), u_lo + a.units_per_wg);
   if (u_lo >= u_hi) return;   // nothing to add (uniform: whole workgroup)
 
@@ -595,7 +621,7 @@ __global__ __launch_bounds__(256, (MAXC <= 8 ? C3W_MIN_WAVES : 1)) void conv3x3_
 
   for (int i = threadIdx.x; i < COUT; i += 256) {
     if (a.lz0) {
-      bn_lazy_bwd(a.lz0, c, i, blockIdx.x == 0 && blockIdx.z == 0, vv[i], vv[COUT + i], vv[2 * COUT + i]);
+      bn_lazy_bwd(a.lz0, c, i, bx == 0 && bz == 0, vv[i], vv[COUT + i], vv[2 * COUT + i]);
     } else {
       vv[i] = a.alpha[(int64_t)c * COUT + i];
       vv[COUT + i] = a.beta[(int64_t)c * COUT + i];
@@ -754,6 +780,15 @@ static size_t gemm_smem(int kc, int nout, int ldk, const Plan& p, int TR, int TW
          (size_t)p.S * TR * TW * P::pitch(kc) * P::ES;
 }
 
+// FEDML_AMD_C3_XCD=0: hardware block order in the 3×3 tile kernels (A/B of the XCD-aware remap)
+static int c3_xcd() {
+  static const int v = [] {
+    const char* e = getenv("FEDML_AMD_C3_XCD");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
 template <class P, int KC, int NOUT_WG, int XF, int BWD, int EPI, int MTW, int ST>
 static auto gemm_variant(int need) {
   return need <= 4 ? conv3x3_gemm_kernel<P, KC, NOUT_WG, XF, BWD, EPI, MTW, ST, 4>
@@ -788,6 +823,7 @@ static int launch_gemm(Args a, int nout, int C, int target_px, hipStream_t strea
     }
   }
   a.R = p.R; a.S = p.S; a.units = p.units; a.units_per_wg = p.units_per_wg; a.nout_total = nout;
+  a.xcd = c3_xcd();
   const bool fwd2 = !BWD && ST == 2;
   const int TR = fwd2 ? 2 * p.R + 1 : p.R + 2;
   const int TW = (BWD ? a.W : a.Ws) + 2;
@@ -927,6 +963,7 @@ static int conv3x3_wgrad(const void* g, const void* yv, const float* alpha, cons
   const int Ho = H / stride, Wo = W / stride;
   if (Wo % 8 != 0 || (Ho * Wo) % 32 != 0) return -3;
   WArgs a = {};
+  a.xcd = c3_xcd();
   a.g = g; a.yv = yv; a.alpha = alpha; a.beta = beta; a.gamma = gamma; a.x = x; a.ps = ps; a.pt = pt; a.dw = dw;
   a.tab = tab; a.nl = nl;
   a.lz0 = tab ? nullptr : fa_take_lazy(0);
