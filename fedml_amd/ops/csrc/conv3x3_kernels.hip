@@ -690,15 +690,16 @@ __global__ __launch_bounds__(256, (MAXC <= 8 ? C3W_MIN_WAVES : 1)) void conv3x3_
       for (int m = 0; m < MT; ++m) af[m] = P::frag_px(drow + m * 16, LDD);
 #pragma unroll
       for (int t = 0; t < TPW; ++t) {
-        const int nt = my_nt0 + t;
-        if (nt < nt_hi) {
-          const int k0 = nt * 16;
-          const int tap = k0 / CIN, ci0 = k0 % CIN;
-          const int kh = tap / 3, kw = tap % 3;
-          const frag_t bf = P::frag_px(xrow + (kh * TW + kw) * LDX + ci0, ST * LDX);
+        // branch-free: a tile past the slice end recomputes its last tile (the epilogue discards it), so all
+        // TPW fragment reads issue ahead of the MFMAs — behind a per-tile branch each read's LDS latency was
+        // exposed before its 4 MFMAs (s_waitcnt lgkmcnt(0) per tile)
+        const int nt = min(my_nt0 + t, nt_hi - 1);
+        const int k0 = nt * 16;
+        const int tap = k0 / CIN, ci0 = k0 % CIN;
+        const int kh = tap / 3, kw = tap % 3;
+        const frag_t bf = P::frag_px(xrow + (kh * TW + kw) * LDX + ci0, ST * LDX);
 #pragma unroll
-          for (int m = 0; m < MT; ++m) acc[m][t] = P::mma(af[m], bf, acc[m][t]);
-        }
+        for (int m = 0; m < MT; ++m) acc[m][t] = P::mma(af[m], bf, acc[m][t]);
       }
     }
   }
