@@ -1098,8 +1098,10 @@ static int convk_min_k() {
     const char* e = getenv("FEDML_AMD_CONVK_MIN_K");
     // 256 → 128 (round 4): the 256 → 64 block-output 1×1 of the headline's 8² stage runs faster as the K-streamed
     // GEMM plus a separate block-output pass than as the fused generic kernel — headline fp32 +0.8 %, 13-client share
-    // +1.4 %, MobileNet +2 %, ResNet-18 neutral (profiles/r4_bench_convk_min_k.jsonl); 256 in round 3: ResNet-18 +9 %
-    v = e ? atoi(e) : 128;
+    // +1.4 %, MobileNet +2 %, ResNet-18 neutral (profiles/r4_bench_convk_min_k.jsonl); 256 in round 3: ResNet-18 +9 %.
+    // 128 → 32 (round 5, after the K-streamed kernel's uniform-tap gather): 13-client share 10.09 → 10.21 rounds/s
+    // over three alternating pairs, headline unchanged (profiles/r5_convk_min_k_ab.txt)
+    v = e ? atoi(e) : 32;
   }
   return v;
 }
