@@ -738,7 +738,8 @@ __global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
   constexpr bool TWO = DY || BOUT;   // second operand stream (y | shortcut)
   const T* src2 = TWO ? reinterpret_cast<const T*>(a.src2) + src_client : nullptr;
   T* pro_out = (BOUT && bz == 0) ? reinterpret_cast<T*>(a.pro_out) + src_client : nullptr;
-  T* out = reinterpret_cast<T*>(a.out) + (int64_t)c * Mo * NO;
+  // null: statistics only (EPI_FWD; the recomputed-y backward takes a conv's BN statistics from the same kernel)
+  T* out = a.out ? reinterpret_cast<T*>(a.out) + (int64_t)c * Mo * NO : nullptr;
   const T* wsrc = reinterpret_cast<const T*>(a.wpk) + (int64_t)c * a.wpk_ld + (int64_t)ch_base * a.ldk;
 
   // this thread's staging slots: column chunk `col` of rows row0 + RPI·j
@@ -1006,7 +1007,7 @@ __global__ __launch_bounds__(256) void convk_gemm_kernel(ConvArgs a) {
           *reinterpret_cast<uint4*>(out + goff + (int64_t)(a.Wo + 1) * NO) = z;
         }
         if (EPI == EPI_FWD || EPI == EPI_STORE) {
-          *reinterpret_cast<uint4*>(out + goff) = dv;
+          if (EPI == EPI_STORE || out) *reinterpret_cast<uint4*>(out + goff) = dv;
           if (EPI == EPI_FWD) {
             float f[V];
             P::unpack(dv, f);
