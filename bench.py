@@ -49,6 +49,9 @@ def parse():
     p.add_argument("--partition", default="homo", help="homo (equal IID shards, the headline) | hetero (LDA)")
     p.add_argument("--partition-alpha", type=float, default=0.5, help="Dirichlet concentration of --partition hetero")
     p.add_argument("--client-exec", default="auto", help="auto | batched | sequential (non-native conv nets)")
+    p.add_argument("--eval-every", type=int, default=0,
+                   help="evaluate every N rounds inside the timed region (fork metrics: Global/Acc|Loss|Recall on a "
+                        "synthetic 100-per-client test set + every client's train/test accuracy); 0 = no evaluation")
     p.add_argument("--preset", default="", help="resnet18_cifar10_10 | distilbert_fedopt_32 | vit_b16_32 "
                                                 "(other BASELINE.json configs; the default is the headline)")
     presets = {
@@ -103,7 +106,7 @@ def main():
         "dataset": a.dataset, "model": a.model, "client_num_in_total": a.clients,
         "client_num_per_round": a.clients, "comm_round": a.steps, "epochs": a.epochs,
         "batch_size": a.batch_size, "client_optimizer": a.client_optimizer, "learning_rate": a.lr, "weight_decay": 0.001,
-        "frequency_of_the_test": 0, "compute_dtype": a.dtype if use_gpu else "fp32", "random_seed": 0,
+        "frequency_of_the_test": a.eval_every, "target_label": 0, "compute_dtype": a.dtype if use_gpu else "fp32", "random_seed": 0,
         "fp32_mma": a.fp32_mma, "client_exec": a.client_exec,
     }})
     torch.manual_seed(0)
@@ -132,6 +135,15 @@ def main():
         store = DeviceClientStore.synthetic_on_device(spec, counts, device, seed=0,
                                                       dtype=torch.float32)
     sim = RCCLSimulator(args, device, None, model, store=store)
+    if a.eval_every > 0:
+        # evaluation data for the fork's metrics: a synthetic test split of 100 samples per client (the global
+        # test set is their union), resident on the device like the training store
+        from fedml_amd.data.client_data import ClientData
+        te = DeviceClientStore.synthetic_on_device(spec, [100] * a.clients, device, seed=1, dtype=torch.float32)
+        tl = {c: ClientData(te.x_all[100 * c:100 * (c + 1)], te.y_all[100 * c:100 * (c + 1)], 500)
+              for c in range(a.clients)}
+        sim.dataset = [sum(counts), 100 * a.clients, None, ClientData(te.x_all, te.y_all, 500),
+                       {c: counts[c] for c in range(a.clients)}, None, tl, spec.num_classes]
     for _ in range(a.warmup):
         sim.run(1)
     if use_gpu:
@@ -187,6 +199,12 @@ def main():
             "samples_per_s": round(a.clients * a.samples_per_client * a.epochs * a.steps / elapsed, 1),
             "final_train_loss": round(loss, 4),
         }
+        if a.eval_every > 0:
+            ev = [h for h in sim.history.values() if "eval_time_s" in h]
+            out["eval"] = {"every": a.eval_every, "evaluations": len(ev),
+                           "eval_ms_mean": round(1000.0 * sum(h["eval_time_s"] for h in ev) / max(1, len(ev)), 2),
+                           "Global/Acc": ev[-1].get("Global/Acc") if ev else None,
+                           "Train/Acc": ev[-1].get("Train/Acc") if ev else None}
         print(json.dumps(out), flush=True)
     sim.close()
     comm.destroy()

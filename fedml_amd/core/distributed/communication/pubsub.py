@@ -32,16 +32,23 @@ MSG_TYPE_CONNECTION_IS_READY = 0
 
 class InProcessBroker:
     """Topic → subscriber callbacks, retained last-will messages, connection tracking. A message published to a
-    topic nobody has subscribed to YET is held and delivered to its first subscriber (a persistent-session broker's
-    behaviour): the peers of an in-process run start in threads, and a status message sent before the other side
-    subscribed was lost under load — a rare hang of the MQTT_S3 cross-silo test."""
+    topic that has NEVER had a subscriber is held (at most ``max_held`` per topic, oldest dropped first) and
+    delivered to its first subscriber (a persistent-session broker's behaviour): the peers of an in-process run
+    start in threads, and a status message sent before the other side subscribed was lost under load — a rare hang
+    of the MQTT_S3 cross-silo test. Once a topic has had a subscriber, messages to it while nobody listens are
+    dropped (late FINISH / status messages of a stopped peer are not replayed to the next run on the same broker),
+    and ``forget(prefix)`` drops what is still held for a finished run. Held messages are replayed under the broker
+    lock, so a concurrent publish cannot overtake them."""
 
-    def __init__(self):
+    def __init__(self, max_held: int = 1024):
         self._subs: Dict[str, List[Callable]] = defaultdict(list)
         self._held: Dict[str, List[bytes]] = defaultdict(list)
+        self._seen = set()               # topics that have had a subscriber
         self._wills: Dict[str, tuple] = {}
-        self._lock = threading.Lock()
+        self._lock = threading.RLock()   # re-entrant: a replayed callback may publish from the same thread
+        self.max_held = int(max_held)
         self.published = 0
+        self.dropped = 0
 
     def connect(self, client_id: str, will_topic: Optional[str] = None, will_payload: Optional[bytes] = None):
         if will_topic:
@@ -55,21 +62,38 @@ class InProcessBroker:
     def subscribe(self, topic: str, cb: Callable[[str, bytes], None]):
         with self._lock:
             self._subs[topic].append(cb)
+            self._seen.add(topic)
             held = self._held.pop(topic, [])
-        for payload in held:
-            cb(topic, payload)
+            for payload in held:
+                cb(topic, payload)
 
     def unsubscribe_all(self, cb):
         with self._lock:
             for t in list(self._subs):
                 self._subs[t] = [c for c in self._subs[t] if c is not cb]
+                if not self._subs[t]:
+                    del self._subs[t]
+
+    def forget(self, prefix: str):
+        """Drop the held messages of every topic starting with ``prefix`` (a finished run's topics)."""
+        with self._lock:
+            for t in [t for t in self._held if t.startswith(prefix)]:
+                del self._held[t]
 
     def publish(self, topic: str, payload: bytes):
         with self._lock:
             cbs = list(self._subs.get(topic, ()))
             self.published += 1
             if not cbs:
-                self._held[topic].append(payload)
+                if topic in self._seen:
+                    self.dropped += 1
+                    return
+                q = self._held[topic]
+                q.append(payload)
+                if len(q) > self.max_held:
+                    del q[0]
+                    self.dropped += 1
+                return
         for cb in cbs:
             cb(topic, payload)
 
@@ -206,7 +230,8 @@ class MqttS3CommManager(QueueCommManager):
                 broker.subscribe(f"fedml_{run_id}_{c}", self._cb)
         else:
             broker.subscribe(f"fedml_{run_id}_0_{rank}", self._cb)
-        broker.subscribe("W/topic", self._on_will)
+        self._will_cb = self._on_will
+        broker.subscribe("W/topic", self._will_cb)
         # local CONNECTION_IS_READY (reference: `mqtt_s3_multi_clients_comm_manager.py:175-180`)
         ready = Message(MSG_TYPE_CONNECTION_IS_READY, rank, rank)
         self.deliver(ready)
@@ -257,7 +282,11 @@ class MqttS3CommManager(QueueCommManager):
     def stop_receive_message(self, clean: bool = True):
         super().stop_receive_message()
         self.broker.unsubscribe_all(self._cb)
+        self.broker.unsubscribe_all(self._will_cb)
         self.broker.disconnect(self.cid, clean=clean)
+        if self.rank == 0 and hasattr(self.broker, "forget"):
+            # the server ends the run: nothing still held for its topics may reach a later run on this broker
+            self.broker.forget(f"fedml_{self.run_id}_")
 
 
 class MqttS3StatusManager:

@@ -28,8 +28,8 @@ class FederationPlane:
         self.rank, self.size = int(rank), int(size)
         self.device = torch.device(device)
         timeout = datetime.timedelta(seconds=timeout_s)
-        store = dist.TCPStore(host, int(port), self.size, self.rank == 0, timeout)
-        store = dist.PrefixStore("fedml_amd_fed_plane", store)
+        self._tcp = dist.TCPStore(host, int(port), self.size, self.rank == 0, timeout)
+        store = dist.PrefixStore("fedml_amd_fed_plane", self._tcp)
         # RCCL needs one GPU per rank: with more plane ranks than GPUs (a one-GPU rehearsal, 8 silos + the server on
         # an 8-GPU node) the launcher picks gloo (FEDML_AMD_PLANE_BACKEND / FEDML_AMD_DIST_BACKEND)
         backend = (os.environ.get("FEDML_AMD_PLANE_BACKEND") or os.environ.get("FEDML_AMD_DIST_BACKEND")
@@ -66,8 +66,23 @@ class FederationPlane:
         return t
 
     def close(self):
-        self.pg = None
+        """Shut the communicator down and release the store (its TCP port) — called from the managers' finish()."""
+        pg, self.pg = self.pg, None
+        if pg is not None and hasattr(pg, "shutdown"):
+            try:
+                pg.shutdown()
+            except Exception as e:  # noqa: BLE001 - teardown is best effort
+                logging.debug("federation plane shutdown: %s", e)
+        self._tcp = None
 
 
 def plane_port(args) -> int:
-    return int(getattr(args, "fed_plane_port", 0) or 29650)
+    """``fed_plane_port`` if configured, else a free port picked on the server (the markers carry it to the silo
+    masters): concurrent cross-silo runs on one node, or a second run in the same process, never share a store."""
+    p = int(getattr(args, "fed_plane_port", 0) or 0)
+    if p:
+        return p
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return int(s.getsockname()[1])

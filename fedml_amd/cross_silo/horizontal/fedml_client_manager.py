@@ -77,6 +77,12 @@ class FedMLClientManager(ClientManager):
         self._plane_train = bool(mk.get("train", True))
         return self._plane_buf
 
+    def finish(self):
+        if self.plane is not None:      # release the RCCL plane's communicator and its store port
+            self.plane.close()
+            self.plane = None
+        super().finish()
+
     def plane_skip(self):
         """RCCL plane, silo not selected this round: add zeros to the round's reduce and do nothing else."""
         if self.plane is None or self._plane_train:

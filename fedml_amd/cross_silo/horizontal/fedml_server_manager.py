@@ -172,6 +172,12 @@ class FedMLServerManager(ServerManager):
         MLOpsProfilerEvent.get_instance().log_event_started("server.wait", event_value=str(self.round_idx))
         self._arm_deadline()
 
+    def finish(self):
+        if self.plane is not None:      # release the RCCL plane's communicator and its store port
+            self.plane.close()
+            self.plane = None
+        super().finish()
+
     # ---- RCCL data plane ------------------------------------------------------------------------
     def _plane_round(self, mtype, g, ids, silos, final=False):
         """Markers to EVERY silo (selected ones train on their data silo, the others only join the collectives),
@@ -190,7 +196,9 @@ class FedMLServerManager(ServerManager):
         else:
             self.aggregator.flat_layout.flatten(g, out=self._plane_glob)
         P = self._plane_glob.numel()
-        port = plane_port(self.args)
+        if getattr(self, "_plane_port", None) is None:
+            self._plane_port = plane_port(self.args)
+        port = self._plane_port
         silo_of = dict(zip(ids, silos))
         for cid in self.client_real_ids:
             mk = marker("rccl", P=P, port=port, train=cid in silo_of and not final)

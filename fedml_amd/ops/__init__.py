@@ -35,6 +35,7 @@ from .fl_ops import (
     softmax_xent_fwd_bwd,
     FusedCrossEntropy,
     confusion_matrix,
+    eval_stats,
     cast_bf16,
     mod_matmul,
     augment,

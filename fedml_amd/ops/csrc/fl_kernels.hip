@@ -1180,6 +1180,67 @@ FA_EXPORT int fa_confusion(const void* z, int is_bf16, const int64_t* y, int32_t
   return (int)hipGetLastError();
 }
 
+// K8b  Evaluation statistics of a logits block in one pass (one wave per row): argmax, the row's cross-entropy
+//      (log-sum-exp − z[y]) and, per group g = grp[row] (a client; null → group 0), the sums
+//      sums[g] = (correct, loss, rows) and optionally per-class counts cls[g] = (true positives[K], actual[K],
+//      predicted[K]) — what the fork's trainer test() derives per batch on the host
+//      (`my_model_trainer_classification.py:113-154`, `fedavg_api.py:143-177`). Rows with a label outside
+//      [0, K) or a negative group are padding and skipped.
+template <typename T>
+__global__ __launch_bounds__(256) void eval_stats_kernel(const T* __restrict__ z, const int64_t* __restrict__ y,
+                                                         const int32_t* __restrict__ grp, float* __restrict__ sums,
+                                                         int32_t* __restrict__ cls, int64_t R, int K) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= R) return;
+  const int64_t lbl = y[row];
+  const int g = grp != nullptr ? grp[row] : 0;
+  if (lbl < 0 || lbl >= K || g < 0) return;          // uniform per wave: the whole wave leaves
+  const T* zr = z + row * K;
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int j = lane; j < K; j += 64) {
+    const float v = load1<T>(zr + j);
+    if (v > best || (v == best && j < bi)) { best = v; bi = j; }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ov > best || (ov == best && oi < bi)) { best = ov; bi = oi; }
+  }
+  float se = 0.f;
+  for (int j = lane; j < K; j += 64) se += __expf(load1<T>(zr + j) - best);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) se += __shfl_xor(se, o, 64);
+  if (lane == 0) {
+    const float loss = __logf(se) + best - load1<T>(zr + lbl);
+    const int hit = bi == (int)lbl;
+    atomicAdd(&sums[3 * g + 0], (float)hit);
+    atomicAdd(&sums[3 * g + 1], loss);
+    atomicAdd(&sums[3 * g + 2], 1.f);
+    if (cls != nullptr) {
+      int32_t* c = cls + (int64_t)g * 3 * K;
+      if (hit) atomicAdd(&c[lbl], 1);
+      atomicAdd(&c[K + lbl], 1);
+      atomicAdd(&c[2 * K + bi], 1);
+    }
+  }
+}
+
+FA_EXPORT int fa_eval_stats(const void* z, int is_bf16, const int64_t* y, const int32_t* grp, float* sums,
+                            int32_t* cls, int64_t R, int K, hipStream_t stream) {
+  if (R <= 0) return 0;
+  const unsigned grid = (unsigned)((R + 3) / 4);
+  if (is_bf16)
+    hipLaunchKernelGGL(eval_stats_kernel<uint16_t>, dim3(grid), dim3(256), 0, stream, (const uint16_t*)z, y, grp, sums,
+                       cls, R, K);
+  else
+    hipLaunchKernelGGL(eval_stats_kernel<float>, dim3(grid), dim3(256), 0, stream, (const float*)z, y, grp, sums, cls,
+                       R, K);
+  return (int)hipGetLastError();
+}
+
 // misc: fp32 → bf16 cast of a flat buffer (weights for bf16 compute)
 __global__ __launch_bounds__(256) void cast_bf16_kernel(const float* __restrict__ x, uint16_t* __restrict__ y,
                                                         int64_t n) {

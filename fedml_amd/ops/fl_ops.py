@@ -653,6 +653,47 @@ def confusion_matrix(logits, labels, num_groups=1, rows_per_group=None):
     return torch.bincount(flat, minlength=num_groups * K * K).view(num_groups, K, K).to(torch.int32)
 
 
+def eval_stats(logits, labels, groups=None, num_groups=1, with_classes=False, sums=None, cls=None):
+    """Accumulate evaluation statistics of a logits block [R, K] into per-group buffers (K8b):
+    ``sums`` [G, 3] fp32 = (correct, Σ cross-entropy, rows) and, with ``with_classes``, ``cls`` [G, 3, K]
+    int32 = (true positives, actual, predicted) per class. ``groups`` [R] int32 group of each row (None: 0);
+    rows with a label outside [0, K) or a negative group are skipped. Returns (sums, cls)."""
+    R, K = logits.shape
+    dev = logits.device
+    if sums is None:
+        sums = torch.zeros(num_groups, 3, dtype=torch.float32, device=dev)
+    if with_classes and cls is None:
+        cls = torch.zeros(num_groups, 3, K, dtype=torch.int32, device=dev)
+    if R == 0:
+        return sums, cls
+    lab = labels.reshape(-1).to(torch.int64)
+    grp = None if groups is None else groups.reshape(-1).to(torch.int32)
+    if use_native(logits):
+        rc = _fn("fa_eval_stats")(_pr(logits.contiguous()), _c.c_int(logits.dtype == torch.bfloat16),
+                                  _pr(lab.contiguous()), _pr(None if grp is None else grp.contiguous()), _p(sums),
+                                  _p(cls if with_classes else None), _i64(R), _c.c_int(K), _stream(logits))
+        _check(rc, "fa_eval_stats")
+        return sums, cls
+    z = logits.to(torch.float32)
+    g = torch.zeros(R, dtype=torch.int64, device=dev) if grp is None else grp.to(torch.int64)
+    ok = (lab >= 0) & (lab < K) & (g >= 0)
+    z, lab, g = z[ok], lab[ok], g[ok]
+    pred = z.argmax(1)
+    loss = torch.nn.functional.cross_entropy(z, lab, reduction="none")
+    G = sums.shape[0]
+    sums[:, 0].add_(torch.bincount(g, weights=(pred == lab).to(torch.float32), minlength=G).to(sums.dtype))
+    sums[:, 1].add_(torch.bincount(g, weights=loss, minlength=G).to(sums.dtype))
+    sums[:, 2].add_(torch.bincount(g, minlength=G).to(sums.dtype))
+    if with_classes:
+        hit = (pred == lab).to(torch.int64)
+        c = cls.view(G, 3, K)
+        c[:, 0].add_(torch.bincount(g * K + lab, weights=hit.to(torch.float64), minlength=G * K).view(G, K)
+                     .to(torch.int32))
+        c[:, 1].add_(torch.bincount(g * K + lab, minlength=G * K).view(G, K).to(torch.int32))
+        c[:, 2].add_(torch.bincount(g * K + pred, minlength=G * K).view(G, K).to(torch.int32))
+    return sums, cls
+
+
 def cast_bf16(x, out=None):
     if use_native(x):
         out = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device) if out is None else out

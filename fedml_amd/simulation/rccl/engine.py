@@ -196,7 +196,11 @@ class ClientBatchEngine:
         # class-balanced loss, reference s_fedavg/my_model_trainer_classification.py:27): a weighted mean
         # Σ w[y_i]·CE_i / Σ w[y_i] is the plain CE head with row scales w[y_i] / Σ_batch w[y_j] — every executor
         # (native head kernel, fused CE, sequential torch) takes it through ``_row_scale``
-        self.class_weight: Optional[torch.Tensor] = None
+        # ``class_weight`` is a property over ONE persistent buffer: a captured per-client graph reads its address,
+        # so a new round's table is copied into it (rebinding the attribute would leave the graph reading a freed
+        # tensor)
+        self._cw: Optional[torch.Tensor] = None
+        self._cw_on = False
         # per-step input transform x [C, B, ...] → x on the client-stacked batch, after the gather and the
         # augmentation (HS-FedAvg's amplitude normalisation): ``hook(x, b_c)`` with b_c the valid rows per slot
         self.input_hook = None
@@ -266,6 +270,25 @@ class ClientBatchEngine:
         self.aug_pad = int(getattr(args, "augment_pad", 4))
         self.aug_cutout = int(getattr(args, "cutout_length", 16))
         self._aug_calls = 0
+
+    @property
+    def class_weight(self) -> Optional[torch.Tensor]:
+        return self._cw if self._cw_on else None
+
+    @class_weight.setter
+    def class_weight(self, w: Optional[torch.Tensor]):
+        if w is None:
+            self._cw_on = False
+            return
+        w = w.detach().to(self.device, torch.float32)
+        if self._cw is None or self._cw.shape != w.shape:
+            if self._cw is not None and any(k[0] == "seq" for k in self._graphs):
+                # graphs captured against the old buffer: drop them (re-captured on their next geometry)
+                torch.cuda.synchronize(self.device)
+                self._graphs = {k: v for k, v in self._graphs.items() if k[0] != "seq"}
+            self._cw = torch.empty_like(w)
+        self._cw.copy_(w)
+        self._cw_on = True
 
     @property
     def executor(self) -> str:
@@ -817,7 +840,7 @@ class ClientBatchEngine:
         the warm-up: library algorithm selection, allocator pools) and is captured right after
         (capture executes nothing), so every later occurrence — including the once-per-round first
         step and the ragged last batch — replays."""
-        key = ("seq", tuple(x.shape), tuple(y.shape), tuple(b_c), float(lr), bool(first))
+        key = ("seq", tuple(x.shape), tuple(y.shape), tuple(b_c), float(lr), bool(first), self._cw_on)
         ent = self._graphs.get(key)
         if ent is None:
             loss = self._seq_step_loss(x, y, b_c, zero=True)

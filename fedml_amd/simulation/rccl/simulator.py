@@ -373,12 +373,20 @@ class RCCLSimulator:
             rec = {"round_time_s": dt, "train_loss": float(self.engine.last_loss)}
             # GPU time per phase (HIP events, resolved after the round's synchronize)
             rec.update({f"gpu_ms/{k}": round(v, 3) for k, v in tracer().gpu_times().items()})
-            if freq > 0 and (self.round_idx % freq == 0 or r == n - 1):
+            # the SP simulator's schedule (reference fedavg_api.py:120-131): every ``frequency_of_the_test``-th
+            # round and the last one
+            last = self.round_idx == int(self.args.comm_round) - 1
+            if (freq > 0 and self.round_idx % freq == 0) or last:
+                t1 = time.perf_counter()
                 rec.update(self.evaluate())
+                if self.device.type == "cuda":
+                    torch.cuda.synchronize(self.device)
+                rec["eval_time_s"] = time.perf_counter() - t1
             self.history[self.round_idx] = rec
             if self.rank == 0:
-                logging.info("[RCCL-sim] round %d: %s", self.round_idx, rec)
-                MLOpsMetrics.get_instance().log(dict(rec, round=self.round_idx), step=self.round_idx)
+                from ..common import scalar_metrics
+                logging.info("[RCCL-sim] round %d: %s", self.round_idx, scalar_metrics(rec))
+                MLOpsMetrics.get_instance().log(dict(scalar_metrics(rec), round=self.round_idx), step=self.round_idx)
             ck = getattr(self.args, "checkpoint_dir", None)
             if ck and (self.round_idx + 1) % int(getattr(self.args, "checkpoint_every", 1) or 1) == 0:
                 self.save_checkpoint(ck)
@@ -416,10 +424,19 @@ class RCCLSimulator:
         return self.layout.unflatten(self.global_flat.detach().cpu())
 
     @torch.no_grad()
-    def evaluate(self):
-        """Global model on the (sharded) global test set; confusion counts all-reduced."""
+    def evaluate(self, local_tests: bool = True):
+        """The fork's per-round metrics of the global model (``evaluation.SimEvaluator``): ``Global/Acc``,
+        ``Global/Loss``, ``Global/Recall`` of ``target_label`` on the rank-sharded global test set and, with
+        ``local_tests``, ``_local_test_on_all_clients`` (every client's train and test data: federation accuracy /
+        loss and per-client accuracy, recall and precision), all from one flat statistics buffer and one
+        all-reduce. Task losses other than classification CE keep the global-test Acc / Loss below."""
         if self.dataset is None:
             return {}
+        if self.engine.loss_name == "ce":
+            if getattr(self, "_evaluator", None) is None:
+                from .evaluation import SimEvaluator
+                self._evaluator = SimEvaluator(self)
+            return self._evaluator.evaluate(self.global_flat, local_tests=local_tests)
         test = self.dataset[3]
         self.model.load_state_dict(self.layout.unflatten(self.global_flat))
         self.model.eval()

@@ -10,7 +10,7 @@ batched engine (native HIP ResNet step / batched interpreter / sequential execut
 pieces slotted in:
 
 * sampling: S-FedAvg draws ``p ∝ exp(φ)`` (``sampling_filter: exp``) from numpy's global generator, HS-FedAvg takes
-  the top-K by φ (same functions as the SP simulator, ``sp/valuation_base.py``) — every rank draws the same ids;
+  the top-K by φ (same functions as the SP simulator, ``sp/valuation_base.py``) — rank 0's draw is broadcast;
 * local training: per-client class-balanced CE as per-row loss scales (``engine.class_weight``, one [C, classes]
   table gathered per round from a device-side per-client label histogram) and the per-client gradient clip 1.0
   inside the (captured) optimizer step; HS-FedAvg normalises every client's batches toward its running Fourier
@@ -97,6 +97,12 @@ class ValuedRCCLSimulator(RCCLSimulator):
         else:
             ids = s_fedavg_sampling(round_idx, self.K_total, self.K, self.phi, self.sampling_filter)
         ids = [int(i) for i in ids]
+        if comm.is_dist():
+            # rank 0's draw is THE sample: a rank whose numpy state drifted (extra rank-local draws, another resume
+            # path) would otherwise pack different clients and desynchronise every later collective
+            t = torch.tensor(ids, dtype=torch.int64, device=self.device)
+            comm.broadcast_flat(t, 0)
+            ids = [int(i) for i in t.tolist()]
         packs = pack_clients_to_gpus([self.sample_counts[i] for i in ids], self.world)
         self.packs = [[ids[j] for j in pk] for pk in packs]
         mine = self.packs[self.rank]

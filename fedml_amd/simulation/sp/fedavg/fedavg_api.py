@@ -14,7 +14,7 @@ import time
 
 import torch
 
-from ...common import client_sampling, log_metrics, save_results, summarize_metrics
+from ...common import client_sampling, fork_local_test_stats, log_metrics, save_results
 from ....core.arena import fedavg_state_dicts
 from ....trainers import create_model_trainer
 from .client import Client
@@ -89,6 +89,7 @@ class FedAvgAPI:
             if last or (freq > 0 and round_idx % freq == 0):
                 acc, recall = self._validate_global_model(self.model_trainer.model, self.test_global, self.device)
                 rec["Global/Acc"], rec["Global/Recall"] = acc, recall
+                rec["Global/Loss"] = self._last_global_loss
             rec["round_time_s"] = time.time() - t0
         out = getattr(self.args, "results_path", None)
         if out:
@@ -105,15 +106,14 @@ class FedAvgAPI:
                                         self.train_data_local_num_dict[cid])
             train_m.append(client.local_test(False))
             test_m.append(client.local_test(True))
-        tr_acc, tr_loss = summarize_metrics(train_m)
-        te_acc, te_loss = summarize_metrics(test_m)
-        stats = {"Train/Acc": tr_acc, "Train/Loss": tr_loss, "Test/Acc": te_acc, "Test/Loss": te_loss}
+        stats = fork_local_test_stats(train_m, test_m)
         log_metrics(stats, round_idx)
         return stats
 
     def _validate_global_model(self, model, data, device):
         m = self.model_trainer.test(data, device, self.args)
         acc = m["test_correct"] / max(1, m["test_total"])
+        self._last_global_loss = m["test_loss"] / max(1, m["test_total"])
         recall = None
         if self.target_label is not None and "recall_per_class" in m:
             recall = m["recall_per_class"][int(self.target_label)]

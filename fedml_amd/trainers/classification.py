@@ -85,6 +85,9 @@ class ModelTrainerCLS(ClientTrainer, FunctionalTrainerMixin):
             metrics["recall_per_class"] = (tp / cm.sum(1).clamp_min(1)).tolist()
             metrics["precision_per_class"] = (tp / cm.sum(0).clamp_min(1)).tolist()
             metrics["confusion_matrix"] = cm
+            # the fork's per-class dicts over the classes present in the labels (simulation/common.class_rates)
+            from ..simulation.common import class_rates
+            metrics["test_recall"], metrics["test_precision"] = class_rates(tp, cm.sum(1), cm.sum(0))
         return metrics
 
     def test_on_the_server(self, train_data_local_dict, test_data_local_dict, device, args=None) -> bool:
