@@ -109,6 +109,10 @@ class SimulatorRCCL:
             # Shapley-valued variants: batched local training + sharded coalition valuation (rccl/valued.py)
             from .rccl.valued import ValuedRCCLSimulator
             self.simulator = ValuedRCCLSimulator(args, device, dataset, model, model_trainer=model_trainer)
+        elif args.federated_optimizer == FedML_FEDERATED_OPTIMIZER_HIERARCHICAL_FL:
+            # group rounds as per-group GEMM reductions + one all-reduce per group round (rccl/hierarchical.py)
+            from .rccl.hierarchical import HierarchicalRCCLSimulator
+            self.simulator = HierarchicalRCCLSimulator(args, device, dataset, model, model_trainer=model_trainer)
         elif args.federated_optimizer not in (FedML_FEDERATED_OPTIMIZER_FEDAVG, FedML_FEDERATED_OPTIMIZER_FEDOPT,
                                             FedML_FEDERATED_OPTIMIZER_FEDPROX, FedML_FEDERATED_OPTIMIZER_FEDAVG_ROBUST,
                                             FedML_FEDERATED_OPTIMIZER_FEDNOVA):
