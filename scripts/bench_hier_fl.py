@@ -62,6 +62,7 @@ def main():
     else:
         from fedml_amd.simulation.sp.hierarchical_fl.trainer import HierarchicalTrainer
         tr = HierarchicalTrainer(args, dev, dataset, copy.deepcopy(model))
+        tr._local_test_on_all_clients = lambda ge: {}     # no evaluation in either timed loop
         tr.global_rounds = 1
         tr.train()
         torch.cuda.synchronize()
