@@ -34,8 +34,67 @@ import torch
 import torch.nn as nn
 
 from .. import ops
+from ..ops import transformer_ops as T
 from ..parallel import comm
 from .ddp import FlatDDP, FlatOptimizer
+
+
+class GradBuckets:
+    """Bucketed, backward-overlapped gradient reduction of an [R, P] replica gradient arena: columns complete as the
+    backward's Functions report them (``ready``); every maximal run of complete columns at the top of the pending
+    range that reaches ``bucket_mb`` is averaged over the R local replicas into ``gsum`` (one ``weighted_sum``
+    launch on the compute stream, after the writes) and all-reduced asynchronously (RCCL's stream waits on the
+    compute stream's event, so the collective overlaps the rest of the backward). Backward writes gradients from
+    the last layer to the first, i.e. from high to low arena offsets, so the runs form as the backward proceeds.
+    ``finish`` issues the rest and yields each bucket's (lo, hi) as its all-reduce completes."""
+
+    def __init__(self, layout, grads, rep_w, gsum, group, bucket_mb):
+        self.grads, self.rep_w, self.gsum, self.group = grads, rep_w, gsum, group
+        self.P = layout.size
+        self.B = max(1024, int(bucket_mb * (1 << 20) / 4))
+        self.ld = grads.stride(0)
+        self.es = grads.element_size()
+        ts = sorted((s.offset, s.numel) for s in layout.slots if s.trainable)
+        self.lo_of = [o for o, _ in ts]                       # trainable slot starts, ascending
+        self.end_of = {o: o + n for o, n in ts}
+        self.launched_during_backward = 0
+
+    def begin(self):
+        self.done = set()
+        self.hi = self.P                # columns [hi, P) are launched
+        self.k = len(self.lo_of) - 1    # highest trainable slot not yet launched
+        self.works = []
+
+    def _launch(self, lo, hi):
+        if hi <= lo:
+            return
+        ops.weighted_sum(self.grads[:, lo:hi], self.rep_w, out=self.gsum[0, lo:hi])
+        self.works.append((lo, hi, comm.all_reduce_flat(self.gsum[0, lo:hi], group=self.group, async_op=True)))
+
+    def ready(self, views):
+        base = self.grads.data_ptr()
+        for v in views:
+            off = ((v.data_ptr() - base) // self.es) % self.ld
+            if off in self.end_of:
+                self.done.add(off)
+        # extend the complete run downward from the launched boundary; launch once it holds a bucket
+        lo = self.hi
+        k = self.k
+        while k >= 0 and self.lo_of[k] in self.done:
+            lo = self.lo_of[k]
+            k -= 1
+        if self.hi - lo >= self.B:
+            self._launch(lo, self.hi)
+            self.hi, self.k = lo, k
+            self.launched_during_backward += 1
+
+    def finish(self):
+        self._launch(0, self.hi)
+        self.hi = 0
+        for lo, hi, ws in self.works:
+            for w in ws:
+                w.wait()
+            yield lo, hi
 
 
 def shard_indices(n: int, replica: int, n_replicas: int, epoch: int = 0, shuffle: bool = False, seed: int = 0):
@@ -98,7 +157,7 @@ class CheetahTrainer:
         self.samples_seen = 0
         self.native = None
         mode = str(getattr(args, "cheetah_exec", "auto") or "auto")
-        if self.device.type == "cuda" and mode in ("auto", "native"):
+        if mode == "native" or (mode == "auto" and self.device.type == "cuda"):
             self._try_native(int(getattr(args, "replicas_per_gpu", 1) or 1), required=mode == "native")
         if self.native is None:
             self.R = 1
@@ -111,84 +170,100 @@ class CheetahTrainer:
 
     # ------------------------------------------------------------------ native executor
     def _try_native(self, R, required):
-        from ..core.arena import ParamLayout
-        from ..parallel.native_resnet import NativeResNetStep, UnsupportedNative
-        layout = ParamLayout.from_module(self.model)
-        try:
-            step = NativeResNetStep(self.model, layout, R, self.device, dtype=self.compute_dtype or torch.float32)
-        except UnsupportedNative as e:
+        """The client-batched engine of the FL simulator as the replica executor: R replicas are R client slots
+        (``ClientBatchEngine``: the native HIP ResNet step, or the client-batched transformer kernels for
+        DistilBERT / ViT). Anything else (its executor would be the torch interpreter) keeps ``FlatDDP``."""
+        from ..simulation.rccl.engine import ClientBatchEngine
+        eng = ClientBatchEngine(self.model, R, self.device, self.args, self.compute_dtype)
+        if eng.executor not in ("native", "transformer"):
+            eng.close()
             if required:
-                raise
-            logging.info("cheetah: torch executor (%s)", e)
+                from ..parallel.native_resnet import UnsupportedNative
+                raise UnsupportedNative(f"no native replica executor for this model ({eng.executor})")
+            logging.info("cheetah: torch executor (engine would run %s)", eng.executor)
             return
-        if self.compute_dtype is None:
-            from ..ops import nn_ops
-            nn_ops.set_f32_mma_mode(str(getattr(self.args, "fp32_mma", "exact") or "exact"))
-        if self.det:
-            step.enable_deterministic()
-        self.native, self.layout, self.R = step, layout, R
+        self.engine, self.native, self.layout, self.R = eng, eng.native_step or eng.tf, eng.layout, R
         dev = self.device
-        self.params = layout.alloc_stack(R, dev)
-        self.grads = layout.alloc_stack(R, dev)
+        layout = self.layout
+        self.params, self.grads = eng.params, eng.grads
         flat = layout.flatten(self.model.state_dict(), device=dev)
         comm.broadcast_flat(flat, 0, self.pg)               # every rank starts from rank 0's weights
-        ops.broadcast_rows_(self.params, flat)
-        self.gsum = torch.zeros(1, layout.size, dtype=torch.float32, device=dev)
+        eng.load_global(flat)
+        P = layout.size
+        self.gsum = torch.zeros(1, P, dtype=torch.float32, device=dev)
         self.tmask = layout.trainable_mask(dev).to(torch.bool)
-        self.bmask = ~self.tmask                             # BN running statistics / counters (+ alignment pad)
         self.wmask = self.tmask.to(torch.float32) if self.wd else None
-        self.mom = torch.zeros(1, layout.size, device=dev) if (self.opt_name == "sgd" and self.momentum) else None
+        self.mom = torch.zeros(1, P, device=dev) if (self.opt_name == "sgd" and self.momentum) else None
         if self.opt_name != "sgd":
-            self.m1 = torch.zeros(1, layout.size, device=dev)
-            self.m2 = torch.zeros(1, layout.size, device=dev)
-            self.vmax = torch.zeros(1, layout.size, device=dev) if self.opt_name == "adam" else None
+            self.m1 = torch.zeros(1, P, device=dev)
+            self.m2 = torch.zeros(1, P, device=dev)
+            self.vmax = torch.zeros(1, P, device=dev) if self.opt_name == "adam" else None
         self.t = 0
         self.rep_w = torch.full((R,), 1.0 / (R * self.world), dtype=torch.float32, device=dev)
         self.active = torch.ones(R, dtype=torch.float32, device=dev)
-        self._nimg = {}
         self.x_dev = self.train_data.x.to(dev, non_blocking=True)
         self.y_dev = self.train_data.y.to(dev, non_blocking=True)
+        self.buckets = GradBuckets(layout, self.grads, self.rep_w, self.gsum, self.pg,
+                                   float(getattr(self.args, "ddp_bucket_mb", 64.0) or 64.0))
+        # CPU / torch-accumulated gradients report completion through post-accumulate hooks; the native kernels
+        # report it themselves (transformer_ops grad_ready_listener)
+        self._hooks = [v.register_post_accumulate_grad_hook(lambda t: self.buckets.ready([t.grad]))
+                       for v in eng.views.values() if v.requires_grad]
 
     def _native_step(self, idx):
-        """idx [R, b] sample indices (one row per local replica)."""
+        """idx [R, b] sample indices (one row per local replica). Backward runs under the bucketer: each bucket of
+        gradient columns whose writes are all enqueued is averaged over the local replicas (``weighted_sum``) and
+        its all-reduce starts on RCCL's stream while the rest of the backward still runs; the optimizer then
+        updates each bucket as its all-reduce lands."""
         R, b = idx.shape
-        x = self.x_dev[idx.reshape(-1)].view(R, b, *self.x_dev.shape[1:]).float()
+        x = self.x_dev[idx.reshape(-1)].view(R, b, *self.x_dev.shape[1:])
+        if x.is_floating_point():
+            x = x.float()
         y = self.y_dev[idx.reshape(-1)].view(R, b).long()
-        nimg = self._nimg.get(b)
-        if nimg is None:
-            nimg = self._nimg[b] = (torch.full((R,), b, dtype=torch.int32, device=self.device),
-                                    torch.full((R, b), 1.0 / b, dtype=torch.float32, device=self.device))
-        self.grads.zero_()
-        loss = self.native.step(self.params, self.grads, x, y, nimg[1], self.active, nimg=nimg[0])
-        g = self.gsum[0]
-        ops.weighted_sum(self.grads, self.rep_w, out=g)                # mean over local replicas (÷ R·world)
-        # rank 0 contributes replica 0's BN running statistics in the buffer slots: after the SUM all-reduce every
-        # rank holds them (torch DDP broadcast_buffers) — one collective per step
-        g.copy_(torch.where(self.bmask, self.params[0] if self.rank == 0 else torch.zeros_like(g), g))
-        comm.all_reduce_flat(self.gsum, group=self.pg)
-        p0 = self.params[0:1]
-        p0.copy_(torch.where(self.bmask, self.gsum, p0))
-        self.gsum.masked_fill_(self.bmask.view(1, -1), 0.0)
+        mask = self._masks.get(b) if hasattr(self, "_masks") else None
+        if mask is None:
+            self._masks = getattr(self, "_masks", {})
+            mask = self._masks[b] = torch.ones(R, b, dtype=torch.bool, device=self.device)
+        eng = self.engine
+        self.buckets.begin()
+        with T.grad_ready_listener(self.buckets.ready):
+            loss = eng._step_loss(x, y, mask, [b] * R, self.active, None, self.device.type == "cuda")
         self.t += 1
+        for lo, hi in self.buckets.finish():
+            self._opt_slice(lo, hi)
+        ops.broadcast_rows_(self.params, self.params[0].clone() if self.R > 1 else self.params[0])
+        eng._shadow_stale = True
+        return loss / R
+
+    def _opt_slice(self, lo, hi):
+        """Fused optimizer on master row 0, columns [lo, hi) (BatchNorm statistics / counters have zero gradients
+        and no decay: they are left as replica 0 computed them)."""
+        p0, g = self.params[0:1, lo:hi], self.gsum[:, lo:hi]
+        wm = self.wmask[lo:hi].view(1, -1) if self.wd else None
         if self.opt_name == "sgd":
             if self.wd:
-                self.gsum.addcmul_(self.wmask.view(1, -1), p0, value=self.wd)     # no decay on BN statistics
-            ops.sgd_step(p0, self.gsum, self.lr, momentum=self.momentum, mom_buf=self.mom, first_step=self.t == 1)
+                g.addcmul_(wm, p0, value=self.wd)
+            ops.sgd_step(p0, g, self.lr, momentum=self.momentum,
+                         mom_buf=self.mom[:, lo:hi] if self.mom is not None else None, first_step=self.t == 1)
         else:
             decoupled = self.opt_name == "adamw"
             if self.wd and decoupled:
-                p0.sub_(self.wmask.view(1, -1) * p0, alpha=self.lr * self.wd)
+                p0.sub_(wm * p0, alpha=self.lr * self.wd)
             elif self.wd:
-                self.gsum.addcmul_(self.wmask.view(1, -1), p0, value=self.wd)
-            ops.adam_step(p0, self.gsum, self.m1, self.m2, torch.full((1,), float(self.t), device=self.device),
-                          self.lr, amsgrad=self.vmax is not None, max_exp_avg_sq=self.vmax)
-        ops.broadcast_rows_(self.params, p0[0].clone() if self.R > 1 else p0[0])
-        return loss / R
+                g.addcmul_(wm, p0, value=self.wd)
+            ops.adam_step(p0, g, self.m1[:, lo:hi], self.m2[:, lo:hi],
+                          torch.full((1,), float(self.t), device=self.device), self.lr, amsgrad=self.vmax is not None,
+                          max_exp_avg_sq=self.vmax[:, lo:hi] if self.vmax is not None else None)
 
     def _sync_module(self):
-        """Master weights → the torch module (evaluation, state_dict)."""
+        """Master weights → the torch module (evaluation, state_dict). Trainable weights are identical on every
+        rank; BatchNorm running statistics follow replica 0 of rank 0 (torch DDP's broadcast_buffers: rank 0's
+        replica-0 statistics are only ever updated by its own batches, so broadcasting them once here equals
+        broadcasting them before every forward)."""
         if self.native is not None:
-            self.model.load_state_dict(self.layout.unflatten(self.params[0]))
+            flat = self.params[0].clone()
+            comm.broadcast_flat(flat, 0, self.pg)
+            self.model.load_state_dict(self.layout.unflatten(flat))
 
     # ------------------------------------------------------------------ epochs
     def train_epoch(self, epoch):
@@ -259,4 +334,6 @@ class CheetahTrainer:
 
     def close(self):
         if self.native is not None:
-            self.native.close()
+            for h in self._hooks:
+                h.remove()
+            self.engine.close()

@@ -105,6 +105,26 @@ class _GradStoreState:
 
 _GS = _GradStoreState()
 
+# gradient-completion listener (the data-parallel bucketer of ``distributed/cheetah.py``): called with the gradient-arena
+# views a backward Function has finished writing — all of its kernels are enqueued on the current stream, so work
+# enqueued after the call sees the final values
+_READY = [None]
+
+
+@contextlib.contextmanager
+def grad_ready_listener(fn):
+    prev = _READY[0]
+    _READY[0] = fn
+    try:
+        yield
+    finally:
+        _READY[0] = prev
+
+
+def _notify(views):
+    if _READY[0] is not None and views:
+        _READY[0](views)
+
 
 @contextlib.contextmanager
 def grad_store_record():
@@ -241,6 +261,7 @@ class _LayerNorm(torch.autograd.Function):
             ctx.link.g = dres
             dres = None
         if own:
+            _notify([dg, db])
             return dh, dres, None, None, None, None, None, None, None, None, None
         if det:
             # the kernel's dgamma/dbeta reduce rows with fp32 atomics (arrival order → last bit): recompute them
@@ -650,11 +671,18 @@ class _ClientLinear(torch.autograd.Function):
                 for bv in bviews:
                     bv.add_(gs[:, r:r + bv.shape[1]])
                     r += bv.shape[1]
+                if own:
+                    _notify(list(gviews) + list(bviews))
                 return (dx, None, None, None, g_res, None, *out_w, *out_b)
             bb, bcs, boff, blo = _segments(bviews)
             rc = _fn("fa_bias_grad" + sfx)(_p(g), _i64(M * N), _c.c_int(N), _p(bb), _i64(bcs), boff, blo,
                                      _c.c_int(len(bs)), _c.c_int(C), _c.c_int(M), _c.c_int(N), _stream(x))
             _check(rc, "fa_bias_grad" + sfx)
+        if own:
+            done = list(gviews)
+            if bs and (fused_b or all(b.is_leaf and b.grad is not None for b in bs)):
+                done += [b.grad for b in bs]
+            _notify(done)
         return (dx, None, None, None, g_res, None, *out_w, *out_b)
 
 

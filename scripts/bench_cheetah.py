@@ -28,6 +28,7 @@ def main():
     p.add_argument("--lr", type=float, default=0.05)
     p.add_argument("--dtype", default="fp32")
     p.add_argument("--exec", default="auto", help="auto | native | torch")
+    p.add_argument("--optimizer", default="sgd", help="sgd | adam | adamw")
     a = p.parse_args()
     from fedml_amd.arguments import Arguments
     from fedml_amd.data.client_data import ClientData
@@ -40,11 +41,22 @@ def main():
         torch.cuda.set_device(dev)
     g = torch.Generator().manual_seed(0)
     y = torch.randint(0, a.classes, (a.samples,), generator=g)
-    x = torch.randn(a.samples, 3, 32, 32, generator=g) * 0.5 + (y.view(-1, 1, 1, 1).float() / a.classes - 0.5)
+    if a.model == "distilbert":     # token ids, sequence 128 (BASELINE config 4's text-classification shape)
+        x = torch.randint(1, 30522, (a.samples, 128), generator=g)
+    else:
+        hw = 224 if a.model == "vit_b16" else 32
+        x = torch.randn(a.samples, 3, hw, hw, generator=g) * 0.5 + (y.view(-1, 1, 1, 1).float() / a.classes - 0.5)
     ds = [a.samples, 0, ClientData(x, y, a.batch_size), None, None, None, None, a.classes]
     torch.manual_seed(0)
-    model = {"resnet56": resnet56, "resnet110": resnet110}[a.model](a.classes)
-    args = Arguments.from_dict({"x": {"client_optimizer": "sgd", "learning_rate": a.lr, "momentum": 0.9,
+    if a.model == "vit_b16":
+        from fedml_amd.models.transformer.vit import vit_b16
+        model = vit_b16(a.classes)
+    elif a.model == "distilbert":
+        from fedml_amd.models.transformer.distilbert import distilbert
+        model = distilbert(a.classes)
+    else:
+        model = {"resnet56": resnet56, "resnet110": resnet110}[a.model](a.classes)
+    args = Arguments.from_dict({"x": {"client_optimizer": a.optimizer, "learning_rate": a.lr, "momentum": 0.9,
                                       "weight_decay": 5e-4, "batch_size": a.batch_size, "epochs": a.epochs + 1,
                                       "shuffle": True, "random_seed": 0, "replicas_per_gpu": a.replicas,
                                       "cheetah_exec": a.exec, "compute_dtype": a.dtype}})
@@ -65,10 +77,12 @@ def main():
     n = tr.samples_seen - s0
     if tr.rank == 0:
         print(json.dumps({
-            "metric": f"Cheetah data-parallel training samples/s ({a.model}, CIFAR-{a.classes} shape)",
+            "metric": f"Cheetah data-parallel training samples/s ({a.model}, {tuple(x.shape[1:])} inputs, "
+                      f"{a.classes} classes)",
             "value": round(n / el, 1), "unit": "samples/s", "n_gpus": tr.world, "epochs": a.epochs,
             "ms_per_epoch": round(1000 * el / a.epochs, 1), "higher_is_better": True, "dtype": a.dtype,
-            "executor": "native (client-batched HIP step, C = replicas)" if tr.native is not None else "torch FlatDDP",
+            "executor": (f"native {tr.engine.executor} (client-batched HIP kernels, C = replicas)"
+                         if tr.native is not None else "torch FlatDDP"),
             "replicas_per_gpu": tr.R, "global_batch": a.batch_size * tr.R * tr.world,
             "data": "synthetic, random-init weights", "final_train_loss": round(float(loss), 4)}), flush=True)
     tr.close()

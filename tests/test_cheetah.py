@@ -70,3 +70,20 @@ def test_cheetah_matches_full_batch_single_process(tmp_path, world):
         assert err < 1e-5, (k, err)
     assert abs(got["eval"]["test_acc"] - acc) < 1e-6         # exact global evaluation (no padded test samples)
     assert got["samples"] == 2 * world * math.ceil(50 / world)
+
+
+def test_transformer_replica_executor_world_invariant(tmp_path):
+    """Data parallelism of a ViT through the client-batched transformer executor (``ClientBatchEngine`` replicas)
+    with gradients reduced in backward-overlapped buckets: 2 gloo ranks × 1 replica ≡ 1 rank × 2 replicas
+    bit for bit, buckets go out DURING the backward, and the result matches the torch FlatDDP executor."""
+    two = launch(2, str(tmp_path / "vit_w2.pt"), model="vit", replicas=1)
+    one = launch(1, str(tmp_path / "vit_w1.pt"), model="vit", replicas=2)
+    assert two["native"] and one["native"]
+    for k, v in one["state"].items():
+        assert torch.equal(v, two["state"][k]), k
+    assert one["overlapped"] > 0 and two["overlapped"] > 0
+    ddp = launch(2, str(tmp_path / "vit_ddp.pt"), model="vit", replicas=1, env={"FEDML_TEST_EXEC": "auto"})
+    assert not ddp["native"]
+    for k, v in ddp["state"].items():      # (absolute floor: the key bias has an exactly-zero true gradient)
+        err = float((one["state"][k] - v).norm() / max(1.0, float(v.norm())))
+        assert err < 1e-4, (k, err)

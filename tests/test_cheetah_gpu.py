@@ -70,3 +70,16 @@ def test_native_single_replica_tracks_torch_sgd(tmp_path):
 
     e_nat, e_t32 = err(got["state"]), err(t32)
     assert e_nat < max(2.0 * e_t32, 1e-3), (e_nat, e_t32)
+
+
+def test_native_transformer_dp_world_invariant(tmp_path):
+    """ViT data parallelism on the native fp32 transformer kernels (replicas = client slots of the batched
+    transformer executor) with backward-overlapped gradient buckets: 2 ranks × 1 replica ≡ 1 rank × 2 replicas bit
+    for bit (deterministic mode), and buckets were all-reduced while the backward was still being issued (the
+    kernels' completion notifications drive them)."""
+    a = launch(1, str(tmp_path / "v1.pt"), "vit_gpu", replicas=2, epochs=2, env=_ENV, timeout=400)
+    b = launch(2, str(tmp_path / "v2.pt"), "vit_gpu", replicas=1, epochs=2, env=_ENV, timeout=400)
+    assert a["native"] and b["native"]
+    for k, v in a["state"].items():
+        assert torch.equal(v, b["state"][k]), (k, float((v.float() - b["state"][k].float()).abs().max()))
+    assert a["overlapped"] > 0 and b["overlapped"] > 0
