@@ -83,13 +83,23 @@ class BatchedModelEvaluator:
             self._native[c] = st
         return st
 
+    def _bucket(self, c):
+        """Model-stack width of the native step for a chunk of ``c`` models: the next power of two ≥ max(8, c),
+        capped at ``max_models`` — small evaluations (the K singletons, a rank's shard of a sharded batch,
+        Monte-Carlo prefixes) do not run ``max_models`` models, and only a handful of widths (each with its own
+        native step and buffers) ever exist."""
+        b = 8
+        while b < c:
+            b *= 2
+        return max(c, min(b, self.max_models))
+
     def _run_chunk(self, chunk, batches):
         c = chunk.shape[0]
-        cm = max(c, self.max_models)
+        cm = self._bucket(c)
         st = self._native_step(cm)
         if st is not None:
-            # one native step (one set of buffers) for every chunk: a short last chunk is padded with copies of
-            # its first model, whose outputs are dropped
+            # one native step (one set of buffers) per width bucket: a chunk narrower than its bucket is padded with
+            # copies of its first model, whose outputs are dropped
             arena = chunk if c == cm else torch.cat([chunk, chunk[:1].expand(cm - c, -1)])
             arena = arena.contiguous()
             return [st.forward_eval(arena, x.unsqueeze(0).expand(cm, *x.shape))[:c].float() for x, _ in batches]

@@ -1,9 +1,15 @@
 """Silo-side data-parallel trainer (reference: `cross_silo/hierarchical/trainer_dist_adapter.py:40-141`).
 
-Every process of a silo holds a ``FlatDDP`` replica (bucketed RCCL all-reduce overlapped with
-backward, see ``distributed.ddp``) and trains on its shard of the silo's data; the model trainer
-is unchanged — gradient averaging completes automatically at the end of each backward. The
-master broadcasts the global model to the silo with ONE flat-buffer broadcast (the reference uses
+Every process of a silo holds one data-parallel replica and trains on its share of the silo's data:
+
+* GPU silos with a standard supervised trainer (``functional``) and a model the native kernels take (CIFAR ResNets,
+  DistilBERT, ViT): Cheetah's native replica executor (``distributed/cheetah.py``: the client-batched HIP step with
+  ``replicas_per_gpu`` replicas per process, gradients all-reduced in backward-overlapped buckets over the silo's
+  process group) — ``silo_dp_exec: auto | native | torch``;
+* otherwise a ``FlatDDP`` replica (bucketed RCCL all-reduce overlapped with the torch backward, see
+  ``distributed.ddp``) under the user's model trainer.
+
+The master broadcasts the global model to the silo with ONE flat-buffer broadcast (the reference uses
 ``broadcast_object_list`` of a pickled state dict)."""
 import os
 
@@ -37,10 +43,16 @@ class TrainerDistAdapter:
         self.silo_trainers = {}
         self.silo_trainer = None
         self._pending = None
-        self.ddp = FlatDDP(model, self.device, bucket_mb=float(getattr(args, "ddp_bucket_mb", 64.0))) \
-            if self.n_proc > 1 and self.n_local <= 1 else None
         self.model = model
         self.trainer = model_trainer or create_model_trainer(model, args)
+        mode = str(getattr(args, "silo_dp_exec", "auto") or "auto")
+        # native data parallelism: decided on the first train() (needs the silo's data); FlatDDP otherwise
+        self._native_dp = (self.n_proc > 1 and self.n_local <= 1 and self.device.type == "cuda"
+                           and getattr(self.trainer, "functional", False) and mode in ("auto", "native"))
+        self._native_required = mode == "native"
+        self.cheetah = None
+        self.ddp = FlatDDP(model, self.device, bucket_mb=float(getattr(args, "ddp_bucket_mb", 64.0))) \
+            if self.n_proc > 1 and self.n_local <= 1 else None
         self.trainer.model = self.ddp if self.ddp is not None else model
         self.client_rank = client_rank
         self.train_data_local_dict = train_data_local_dict
@@ -138,10 +150,42 @@ class TrainerDistAdapter:
             state = st.train(int(round_idx or 0))
             self.model.load_state_dict(state)
             return state, self.local_sample_number
+        if self._native_dp and self._train_native():
+            return self.get_model_params(), self.local_sample_number
         if self.ddp is not None:
             dist.barrier()
         self.trainer.train(self.train_local, self.device, self.args)
         return self.get_model_params(), self.local_sample_number
+
+    def _train_native(self) -> bool:
+        """One round of the silo's local training on Cheetah's native replica executor (all silo processes call
+        it): ``epochs`` DistributedSampler epochs over the silo's whole data index, a fresh optimizer state per
+        round (the reference's trainer builds its optimizer in every ``train`` call). False → FlatDDP instead."""
+        from ...data.client_data import concat_client_data
+        from ...distributed.cheetah import CheetahTrainer
+        data = self.train_data_local_dict[self.client_index]
+        if isinstance(data, (list, tuple)):          # load_cross_silo's per-process shards: the silo's whole index
+            data = concat_client_data(list(data))
+        if self.cheetah is None:
+            import copy
+            a = copy.copy(self.args)
+            a.cheetah_exec = "native" if self._native_required else "auto"
+            a.frequency_of_the_test = 10 ** 9
+            ds = [len(data.x), 0, data, None, None, None, None, 0]
+            ct = CheetahTrainer(a, self.device, self.model, ds)
+            if ct.native is None:                    # model the native kernels do not take: FlatDDP from now on
+                ct.close()
+                self._native_dp = False
+                return False
+            self.cheetah = ct
+        else:
+            self.cheetah.set_data(data)
+            self.cheetah.load_state(self.model.state_dict(), broadcast=False)     # sync_model() already did
+        for ep in range(int(self.args.epochs)):
+            loss = self.cheetah.train_epoch(ep + 1000 * int(getattr(self.args, "round_idx", 0) or 0))
+        self.trainer.last_loss = float(loss)
+        self.model.load_state_dict(self.cheetah.state_dict())
+        return True
 
     def cleanup_pg(self):
         if self.pg is not None:

@@ -255,6 +255,28 @@ class CheetahTrainer:
                           torch.full((1,), float(self.t), device=self.device), self.lr, amsgrad=self.vmax is not None,
                           max_exp_avg_sq=self.vmax[:, lo:hi] if self.vmax is not None else None)
 
+    def set_data(self, train):
+        """Swap the training data (a ``ClientData``-like object; the silo adapter's next data index)."""
+        self.train_data = train
+        if self.native is not None:
+            self.x_dev = train.x.to(self.device, non_blocking=True)
+            self.y_dev = train.y.to(self.device, non_blocking=True)
+
+    def load_state(self, state_dict, broadcast: bool = True):
+        """New starting weights on every replica (a new FL round) with a fresh optimizer state. ``broadcast``:
+        take rank 0's (False when the caller's ranks already hold the same state, e.g. after the silo's own sync)."""
+        if self.native is None:
+            self.model.load_state_dict(state_dict)
+            return
+        flat = self.layout.flatten(state_dict, device=self.device)
+        if broadcast:
+            comm.broadcast_flat(flat, 0, self.pg)
+        self.engine.load_global(flat)
+        self.t = 0
+        for buf in (self.mom, getattr(self, "m1", None), getattr(self, "m2", None), getattr(self, "vmax", None)):
+            if buf is not None:
+                buf.zero_()
+
     def _sync_module(self):
         """Master weights → the torch module (evaluation, state_dict). Trainable weights are identical on every
         rank; BatchNorm running statistics follow replica 0 of rank 0 (torch DDP's broadcast_buffers: rank 0's
@@ -262,7 +284,14 @@ class CheetahTrainer:
         broadcasting them before every forward)."""
         if self.native is not None:
             flat = self.params[0].clone()
-            comm.broadcast_flat(flat, 0, self.pg)
+            if comm.is_dist():
+                # only the buffer columns differ between ranks (none for a transformer: no collective at all)
+                if getattr(self, "_bufcols", None) is None:
+                    self._bufcols = torch.nonzero(~self.tmask).view(-1)
+                if self._bufcols.numel():
+                    b = flat.index_select(0, self._bufcols)
+                    comm.broadcast_flat(b, 0, self.pg)
+                    flat.index_copy_(0, self._bufcols, b)
             self.model.load_state_dict(self.layout.unflatten(flat))
 
     # ------------------------------------------------------------------ epochs

@@ -27,10 +27,9 @@ def _round_up(v, m):
 def supported_module(m, elem_bytes: int = 4) -> bool:
     """The layer shape alone (no tensors): a groups-1 convolution both native GEMMs take."""
     k = m.kernel_size
-    cout = m.out_channels
+    cout = _pad_channels(m.out_channels)      # narrower / odd widths run zero-padded filters
     if not (m.groups == 1 and m.dilation == (1, 1) and k[0] == k[1] and m.stride[0] == m.stride[1]
-            and isinstance(m.padding, tuple) and m.padding[0] == m.padding[1] and (cout in (16, 32) or cout % 64 == 0)
-            and m.padding_mode == "zeros"):
+            and isinstance(m.padding, tuple) and m.padding[0] == m.padding[1] and m.padding_mode == "zeros"):
         return False
     cin_pad = _pad_channels(m.in_channels)
     kk = k[0] * k[0]
@@ -44,10 +43,10 @@ def supported(m, x, w) -> bool:
     if w.dtype != torch.float32 or w.dim() != 5 or not w[0].is_contiguous():
         return False
     k = m.kernel_size
-    cout = m.out_channels   # the forward GEMM's N: the kernels' output slices are 16 / 32 / 64-multiples
+    # the forward GEMM's N: the kernels' output slices are 16 / 32 / 64-multiples (other widths are zero-padded)
+    cout = _pad_channels(m.out_channels)
     if not (m.groups == 1 and m.dilation == (1, 1) and k[0] == k[1] and m.stride[0] == m.stride[1]
-            and m.padding[0] == m.padding[1] and isinstance(m.padding, tuple) and (cout in (16, 32) or cout % 64 == 0)
-            and m.padding_mode == "zeros"):
+            and m.padding[0] == m.padding[1] and isinstance(m.padding, tuple) and m.padding_mode == "zeros"):
         return False
     # both GEMMs must have a kernel that takes them: the K-streamed kernel (64-multiple N and K > 256, or N > 256)
     # or the resident-weight kernel, whose [N-slice][K] weight block must fit the LDS
@@ -77,14 +76,17 @@ class _Geom:
 
     def __init__(self, C, cout, cin, k, device):
         self.cin_pad = _pad_channels(cin)
+        # output channels padded the same way (16 / 32 / 64-multiples: the kernels' N slices); the padded filters
+        # are zero, their outputs dropped and their gradients never written back
+        self.cout_pad = _pad_channels(cout)
         self.ldk = _round_up(k * k * self.cin_pad, 32) + 8
-        self.ldk2 = _round_up(k * k * cout, 32) + 8
-        self.off_b = _round_up(cout * self.ldk, 8)
+        self.ldk2 = _round_up(k * k * self.cout_pad, 32) + 8
+        self.off_b = _round_up(self.cout_pad * self.ldk, 8)
         self.ld = _round_up(self.off_b + self.cin_pad * self.ldk2, 64)
-        seg = nn_ops.PackSeg(0, 0, self.off_b, cout, self.cin_pad, k, k, self.ldk, self.ldk2, cin)
+        seg = nn_ops.PackSeg(0, 0, self.off_b, self.cout_pad, self.cin_pad, k, k, self.ldk, self.ldk2, cin)
         raw = bytes((nn_ops.PackSeg * 1)(seg))
         self.segs = torch.frombuffer(bytearray(raw), dtype=torch.uint8).to(device)
-        self.tiles = -(-cout // 32) * -(-self.cin_pad // 32)
+        self.tiles = -(-self.cout_pad // 32) * -(-self.cin_pad // 32)
         self.taps = k * k
 
     @classmethod
@@ -134,12 +136,17 @@ class _NativeBConv2d(torch.autograd.Function):
         Wo = (W + 2 * pad - k) // stride + 1
         xn = _to_nhwc(x, C, cin, g.cin_pad)
         packed = torch.zeros(C, g.ld, dtype=dt, device=x.device)
+        cp = g.cout_pad
+        if cp != cout:       # zero filters up to the padded width (a small copy: these are the narrow layers)
+            wp = torch.zeros(C, cp, cin, k, k, dtype=torch.float32, device=x.device)
+            wp[:, :cout] = w
+            w = wp
         # the kernel reads client c's OIHW rows at w + c·w.stride(0) (the arena row stride): no copy
         nn_ops.pack_weights(w, g.segs, 1, packed, g.ld, C, g.tiles, g.taps)
-        y = torch.empty(C, B, Ho, Wo, cout, dtype=dt, device=x.device)
-        stats = torch.zeros(C, cout, 2, dtype=torch.float32, device=x.device)
+        y = torch.empty(C, B, Ho, Wo, cp, dtype=dt, device=x.device)
+        stats = torch.zeros(C, cp, 2, dtype=torch.float32, device=x.device)
         M = B * Ho * Wo
-        nn_ops.conv_fwd(xn, packed, g.ld, None, None, y, stats, C, B, H, W, g.cin_pad, cout, k, k, stride, pad, Ho,
+        nn_ops.conv_fwd(xn, packed, g.ld, None, None, y, stats, C, B, H, W, g.cin_pad, cp, k, k, stride, pad, Ho,
                         Wo, g.ldk, _tiles_per_wave(M, C))
         out = _from_nhwc(y, cout)
         if b is not None:
@@ -153,25 +160,26 @@ class _NativeBConv2d(torch.autograd.Function):
         xn, packed = ctx.saved_tensors
         C, B, H, W, Ho, Wo, cin, cout, k, stride, pad, g, has_b, wshape = ctx.geo
         dt = xn.dtype
-        gn = _to_nhwc(gy.to(dt).contiguous(), C, cout, cout)
+        cp = g.cout_pad
+        gn = _to_nhwc(gy.to(dt).contiguous(), C, cout, cp)      # zero gradients for the padded filters
         dx = None
         if ctx.needs_input_grad[0]:
             dxn = torch.empty(C, B, H, W, g.cin_pad, dtype=dt, device=gy.device)
             scratch = torch.zeros(C, g.cin_pad, 3, dtype=torch.float32, device=gy.device)
             nn_ops.conv_bwd_data(gn, None, None, None, None, packed.view(-1)[g.off_b:], g.ld, dxn, nn_ops.EPI_STORE,
-                                 None, None, None, None, None, None, scratch, C, B, Ho, Wo, cout, g.cin_pad, k, k,
+                                 None, None, None, None, None, None, scratch, C, B, Ho, Wo, cp, g.cin_pad, k, k,
                                  stride, pad, H, W, g.ldk2, _tiles_per_wave(B * H * W, C))
             dx = _from_nhwc(dxn, cin)
         dw = None
         if ctx.needs_input_grad[1]:
-            dw = torch.zeros(C, cout * cin * k * k, dtype=torch.float32, device=gy.device)
-            ones = torch.ones(C, cout, dtype=torch.float32, device=gy.device)
-            zeros = torch.zeros(C, cout, dtype=torch.float32, device=gy.device)
-            scratch = torch.zeros(C * cout * k * k * g.cin_pad, dtype=torch.float32, device=gy.device)
+            dw = torch.zeros(C, cp * cin * k * k, dtype=torch.float32, device=gy.device)
+            ones = torch.ones(C, cp, dtype=torch.float32, device=gy.device)
+            zeros = torch.zeros(C, cp, dtype=torch.float32, device=gy.device)
+            scratch = torch.zeros(C * cp * k * k * g.cin_pad, dtype=torch.float32, device=gy.device)
             M = B * Ho * Wo
-            nn_ops.conv_wgrad(gn, gn, ones, zeros, zeros, xn, None, None, dw, 0, C, B, H, W, g.cin_pad, Ho, Wo, cout, k,
+            nn_ops.conv_wgrad(gn, gn, ones, zeros, zeros, xn, None, None, dw, 0, C, B, H, W, g.cin_pad, Ho, Wo, cp, k,
                               k, stride, pad, _pix_per_wg(M, C), cin, scratch)
-            dw = dw.view(wshape)
+            dw = dw.view(C, cp, cin * k * k)[:, :cout].reshape(wshape) if cp != cout else dw.view(wshape)
         db = None
         if has_b and ctx.needs_input_grad[2]:
             db = gy.float().reshape(B, C, cout, Ho * Wo).sum(dim=(0, 3))

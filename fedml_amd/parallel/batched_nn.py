@@ -31,7 +31,8 @@ import torch.nn.functional as F
 _NATIVE_BCONV = __import__("os").environ.get("FEDML_AMD_NATIVE_BCONV", "1") != "0"
 
 SUPPORTED_MODULES = (nn.Conv2d, nn.BatchNorm2d, nn.Linear, nn.ReLU, nn.Sigmoid, nn.Tanh, nn.MaxPool2d, nn.AvgPool2d,
-                     nn.AdaptiveAvgPool2d, nn.Flatten, nn.Dropout, nn.Identity, nn.GroupNorm, nn.LeakyReLU)
+                     nn.AdaptiveAvgPool2d, nn.Flatten, nn.Dropout, nn.Identity, nn.GroupNorm, nn.LeakyReLU, nn.SiLU,
+                     nn.Hardswish, nn.Hardsigmoid, nn.ReLU6)
 
 
 class UnsupportedForBatching(Exception):
@@ -305,6 +306,14 @@ class BatchedInterpreter:
             return torch.sigmoid(x)
         if isinstance(m, nn.Tanh):
             return torch.tanh(x)
+        if isinstance(m, nn.SiLU):         # EfficientNet's swish
+            return F.silu(x)
+        if isinstance(m, nn.Hardswish):
+            return F.hardswish(x)
+        if isinstance(m, nn.Hardsigmoid):
+            return F.hardsigmoid(x)
+        if isinstance(m, nn.ReLU6):
+            return F.relu6(x)
         if isinstance(m, nn.MaxPool2d):
             return F.max_pool2d(x, m.kernel_size, m.stride, m.padding, m.dilation, m.ceil_mode)
         if isinstance(m, nn.AvgPool2d):
@@ -328,6 +337,14 @@ class BatchedInterpreter:
             return F.relu(args[0])
         if fn in (torch.sigmoid, F.sigmoid):
             return torch.sigmoid(args[0])
+        if fn in (operator.truediv, torch.div) and not torch.is_tensor(args[1]):
+            return args[0] / args[1]
+        if fn is operator.sub and not torch.is_tensor(args[1]):
+            return args[0] - args[1]
+        if fn in (F.relu6, F.hardtanh):    # MobileNetV3's h-swish / h-sigmoid: x·relu6(x + 3) / 6
+            return fn(*args, **kwargs)
+        if fn in (F.silu, F.hardswish, F.hardsigmoid):
+            return fn(*args, **kwargs)
         if fn is torch.flatten:
             return torch.flatten(*args, **kwargs)
         if fn is F.adaptive_avg_pool2d:

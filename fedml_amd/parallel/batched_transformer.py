@@ -29,6 +29,7 @@ from ..models.transformer.distilbert import DistilBertForSequenceClassification
 from ..models.transformer.vit import VisionTransformer
 from .. import ops
 from ..ops import transformer_ops as T
+from ..ops.transformer_ops import _notify as _notify_ready
 from ..utils.determinism import enabled as _deterministic
 
 
@@ -71,10 +72,10 @@ class _ClientEmbedding(torch.autograd.Function):
                 ops.fl_ops._check(ops.fl_ops._fn("fa_embedding_grad_f32")(
                     ops.fl_ops._p(gw), ops.fl_ops._i64(gw.stride(0)), ops.fl_ops._p(idc), ops.fl_ops._p(gf),
                     _c.c_int(C), _c.c_int(T), _c.c_int(V), _c.c_int(d), ops.fl_ops._stream(gf)), "fa_embedding_grad_f32")
-                T._notify([gw])
+                _notify_ready([gw])
                 return None, None
             gw.index_put_(idx, g.to(gw.dtype), accumulate=True)
-            T._notify([gw])
+            _notify_ready([gw])
             return None, None
         out = torch.zeros(W.shape, dtype=g.dtype, device=g.device)
         out.index_put_(idx, g, accumulate=True)

@@ -85,14 +85,14 @@ def _is_wide_convnet(model: torch.nn.Module, min_channels: int = 128) -> bool:
     return total > 0 and wide >= 0.5 * total
 
 
-def _native_depthwise_net(model: torch.nn.Module) -> bool:
-    """A depthwise-separable conv net (MobileNet family) whose every convolution the native client-batched
-    kernels take (plane depthwise kernels, implicit-GEMM groups-1 convolutions): the batched program then runs
-    without MIOpen, instead of one client after another."""
+def _native_batched_net(model: torch.nn.Module) -> bool:
+    """A conv net whose every convolution the native client-batched kernels take (plane depthwise kernels,
+    implicit-GEMM groups-1 convolutions with zero-padded channel widths): VGG, MobileNet / MobileNetV3,
+    EfficientNet. The batched program then runs without MIOpen, instead of one client after another."""
     from ...ops import bconv_ops, plane_ops
     from ...parallel import batched_nn
     convs = [m for m in model.modules() if isinstance(m, torch.nn.Conv2d)]
-    return (batched_nn._NATIVE_BCONV and any(plane_ops.depthwise_module(m) for m in convs)
+    return (batched_nn._NATIVE_BCONV and bool(convs)
             and all(plane_ops.depthwise_module(m) or bconv_ops.supported_module(m) for m in convs))
 
 
@@ -251,7 +251,7 @@ class ClientBatchEngine:
                              and not any(isinstance(m, torch.nn.RNNBase) for m in model.modules()))
         if not self.sequential and self.native_step is None and self.tf is None and (
                 mode == "sequential" or (mode == "auto" and self.device.type == "cuda" and _is_wide_convnet(model)
-                                         and not _native_depthwise_net(model))):
+                                         and not _native_batched_net(model))):
             logging.info("virtual-client engine: per-client sequential execution (wide conv net)")
             self.sequential = True
             # MIOpen picks convolution solutions by heuristics unless a find-db entry exists; on a fresh

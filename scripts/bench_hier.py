@@ -58,7 +58,7 @@ def worker(a):
            "silo_local_clients": a.local_clients, "compute_dtype": a.dtype,
            "using_gpu": use_gpu, "gpu_id": a.gpu, "rank_in_node": a.gpu,
            "wan_compression": a.wan_compression, "silo_transport": a.silo_transport, "random_seed": 0,
-           "fed_plane_port": int(os.environ.get("FEDML_AMD_PLANE_PORT", "0"))}
+           "fed_plane_port": int(os.environ.get("FEDML_AMD_PLANE_PORT", "0")), "silo_dp_exec": a.silo_dp_exec}
     args = fedml_amd.init(Arguments.from_dict({"x": cfg}))
     dev, ds, m = fedml_amd._prepare(args)
     from fedml_amd.cross_silo.hierarchical import Client, Server
@@ -92,6 +92,9 @@ def main():
     p.add_argument("--server-cpu", action="store_true",
                    help="server process without the GPU (network payloads only): 8 silos x 2 processes then stay "
                         "within 16 GPU processes on a one-GPU box")
+    p.add_argument("--silo-dp-exec", default="auto",
+                   help="data parallelism inside a silo with --local-clients 1: auto/native (Cheetah's native "
+                        "replica executor) | torch (FlatDDP)")
     p.add_argument("--timeout", type=float, default=900)
     p.add_argument("--stack-dump-s", type=float, default=90, help="workers dump their Python stacks this often")
     # worker-internal

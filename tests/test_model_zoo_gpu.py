@@ -23,11 +23,17 @@ from fedml_amd.simulation.rccl.simulator import RCCLSimulator
 pytestmark = pytest.mark.gpu
 
 # family, dataset, executor the engine must pick
+# (VGG, MobileNetV3 and EfficientNet run client-batched on the native kernels: zero-padded channel widths for the
+# narrow / squeeze-excite 1×1 convolutions, plane depthwise kernels, h-swish / swish in the interpreter)
 CASES = [("lr", "mnist", "batched"), ("cnn", "femnist", "batched"), ("cnn_original", "femnist", "batched"),
-         ("rnn", "shakespeare", "lstm"), ("mobilenet", "cifar10", "batched"), ("mobilenet_v3", "cifar10", "sequential"),
-         ("vgg11", "cifar10", "sequential"), ("resnet18_gn", "fed_cifar100", "native"),
-         ("resnet110", "cifar10", "native"), ("efficientnet", "cifar10", "sequential"),
+         ("rnn", "shakespeare", "lstm"), ("mobilenet", "cifar10", "batched"), ("mobilenet_v3", "cifar10", "batched"),
+         ("vgg11", "cifar10", "batched"), ("resnet18_gn", "fed_cifar100", "native"),
+         ("resnet110", "cifar10", "native"), ("efficientnet", "cifar10", "batched"),
          ("distilbert", "sst2", "transformer")]
+# the reference round of these families runs on MIOpen (cuDNN API) as a user's torch loop would; the others use
+# PyTorch's own GPU conv kernels (round 5: MIOpen's run-time compiles failed intermittently without writable cache
+# directories — fixed in fedml_amd/__init__.py — and surfaced as an illegal address)
+MIOPEN_REF = {"cnn", "vgg11"}
 COUNTS = [16, 16, 16]
 BS, LR = 8, 0.01
 BOUND_X = {"native": 30.0, "transformer": 30.0}
@@ -113,7 +119,7 @@ def test_model_family_fp32_round_matches_torch(model_name, dataset, executor):
         # intermittently on the test boxes ("Empty code object path" → illegal address), which is not what this
         # test measures
         prev_cudnn = torch.backends.cudnn.enabled
-        torch.backends.cudnn.enabled = False
+        torch.backends.cudnn.enabled = model_name in MIOPEN_REF
         try:
             ref_gpu = _torch_round(init, store, torch.device("cuda:0"))
         finally:

@@ -83,3 +83,62 @@ def test_native_forward_eval_matches_torch_eval(depth):
             ref = m(x[i])
         err = float((got[i] - ref).norm() / ref.norm())
         assert err < 1e-4, (i, err)
+
+
+def test_coalition_values_match_torch_per_coalition():
+    """The Shapley valuation's inputs, checked one coalition at a time: every coalition model of 5 clients (31
+    subset averages from the MFMA subset-aggregation kernel) is scored by the native batched evaluator and by a
+    plain torch fp32 eval of the same averaged state dict — correct counts within 2 flipped predictions per
+    coalition — and the exact Shapley values from both score tables rank the clients identically. The clients
+    differ in quality on purpose (client k's weights are the reference model plus noise growing with k), so the
+    coalition scores spread widely and a wrong evaluator (or an all-zero valuation) cannot pass."""
+    import copy as _copy
+    from fedml_amd.core.arena import ParamLayout
+    from fedml_amd.core.valuation import BatchedModelEvaluator, CoalitionValuer, coalition_weights
+    from fedml_amd.models.cv.resnet import resnet56
+    torch.manual_seed(0)
+    base = resnet56(10)
+    layout = ParamLayout.from_module(base)
+    dev = torch.device("cuda:0")
+    ref = _copy.deepcopy(base).to(dev).eval()
+    g = torch.Generator(device="cpu").manual_seed(1)
+    x = torch.randn(160, 3, 32, 32, generator=g)
+    with torch.no_grad(), torch.backends.cudnn.flags(enabled=False):
+        y_ref = ref(x.to(dev)).argmax(1).cpu()
+    y = torch.where(torch.rand(160, generator=g) < 0.8, y_ref, torch.randint(0, 10, (160,), generator=g))
+    flats = []
+    for k in range(5):
+        m = _copy.deepcopy(base)
+        with torch.no_grad():
+            for p in m.parameters():
+                p.add_(torch.randn(p.shape, generator=g) * (0.02 + 0.08 * k) * p.detach().abs().mean())
+        flats.append(layout.flatten(m.state_dict(), device=dev))
+    flats = torch.stack(flats)
+    n = [100, 80, 120, 90, 110]
+    valid = [(x[i:i + 40], y[i:i + 40]) for i in range(0, 160, 40)]
+    ev = BatchedModelEvaluator(base, dev, max_models=16)
+    valuer = CoalitionValuer(ev, flats, n, valid)
+    sv_native = valuer.exact_reference_sv()
+    masks = list(range(1, 32))
+    W = coalition_weights(masks, n).to(dev)
+    agg = W @ flats
+    torch_v = {0: 0.0}
+    spread = []
+    for i, mask in enumerate(masks):
+        mm = _copy.deepcopy(base).to(dev).eval()
+        mm.load_state_dict(layout.unflatten(agg[i]))
+        with torch.no_grad(), torch.backends.cudnn.flags(enabled=False):
+            correct = int((mm(x.to(dev)).argmax(1).cpu() == y).sum())
+        got = valuer.metrics[mask]["correct"]
+        assert abs(got - correct) <= 2, (mask, got, correct)
+        torch_v[mask] = correct / 160.0
+        spread.append(correct)
+    assert max(spread) - min(spread) >= 16, spread          # the coalitions really differ
+    K, full = 5, 31
+    sv_torch = []
+    for i in range(K):
+        bit = 1 << i
+        terms = [torch_v[S | bit] - torch_v[S] for S in range(1, full + 1) if not S & bit] + [torch_v[bit]]
+        sv_torch.append(sum(terms) / len(terms))
+    assert max(abs(a - b) for a, b in zip(sv_native, sv_torch)) <= 4 / 160.0, (sv_native, sv_torch)
+    assert list(np.argsort(sv_native)) == list(np.argsort(sv_torch)), (sv_native, sv_torch)
