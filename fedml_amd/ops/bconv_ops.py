@@ -65,9 +65,13 @@ def _gemm_ok(n, K, es):
 
 
 def _pad_channels(cin):
-    """Input channels padded for the kernels: the backward-data GEMM's N (= the input channels) takes 16 / 32 /
-    64-multiples, the forward's K needs multiples of 8."""
-    return 16 if cin <= 16 else 32 if cin <= 32 else _round_up(cin, 64)
+    """Channel widths padded for the kernels (input channels: the backward-data GEMM's N; output channels: the
+    forward GEMM's N): the resident-weight dispatch takes 16 / 32 / 64 / 128 / 256, the K-streamed kernel any
+    64-multiple above 256 (a 192-wide N has no kernel)."""
+    for w in (16, 32, 64, 128, 256):
+        if cin <= w:
+            return w
+    return _round_up(cin, 64)
 
 
 class _Geom:

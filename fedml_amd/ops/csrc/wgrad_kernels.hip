@@ -547,7 +547,9 @@ static int conv_wgrad(const typename P::T* g, const typename P::T* yv, const flo
   const int K = KH * KW * Cin;
   const int NT2 = (K + 15) / 16;
   const int MT = co_slice / 16;
-  const int nt_per_z = max(1, min(NT2, 64 / MT));   // ≤ 64 tiles per workgroup → ≤ 16 per wave
+  // ≤ 64 tiles per workgroup → ≤ 16 per wave; ≤ 32 column tiles so the A staging fits the largest instantiation
+  // (a 16-wide output slice over a long K — squeeze-excite / narrow 1×1 layers — would otherwise ask for 22+)
+  const int nt_per_z = max(1, min(min(NT2, 64 / MT), 256 * V / PT));
   const int nz = (NT2 + nt_per_z - 1) / nt_per_z * (Cout / co_slice);
   const int tpw = (MT * nt_per_z + 3) / 4;
   const int M = Nb * Ho * Wo;

@@ -121,6 +121,15 @@ def grad_ready_listener(fn):
         _READY[0] = prev
 
 
+def client_sum(t: torch.Tensor, dim: int) -> torch.Tensor:
+    """Σ over ``dim`` (> 0) of a client-stacked [C, ...] tensor. Deterministic mode: one reduction per client, so a
+    client's bits never depend on how many clients share the launch (torch picks its reduction split from the
+    whole tensor's shape) — R ranks × 1 replica then equal 1 rank × R replicas bit for bit."""
+    if not _deterministic():
+        return t.sum(dim)
+    return torch.stack([t[c].sum(dim - 1) for c in range(t.shape[0])])
+
+
 def _notify(views):
     if _READY[0] is not None and views:
         _READY[0](views)
@@ -268,8 +277,8 @@ class _LayerNorm(torch.autograd.Function):
             # as fixed-order column sums (deterministic-mode only; the kernel's dh/dres are atomic-free)
             xf, dyf = x.float().view(C, rpc, d), dy.float().view(C, rpc, d)
             xhat = (xf - mean.view(C, rpc, 1)) * rstd.view(C, rpc, 1)
-            dg = (dyf * xhat).sum(1)
-            db = dyf.sum(1)
+            dg = client_sum(dyf * xhat, 1)
+            db = client_sum(dyf, 1)
         return dh, dres, dg.to(gdt), db.to(gdt), None, None, None, None, None, None, None
 
 
@@ -666,7 +675,7 @@ class _ClientLinear(torch.autograd.Function):
                     r += b.shape[1]
             if _deterministic():
                 # fixed-order column sums instead of the kernel's fp32 atomics (deterministic mode)
-                gs = g.view(C, M, N).float().sum(1)
+                gs = client_sum(g.view(C, M, N).float(), 1)
                 r = 0
                 for bv in bviews:
                     bv.add_(gs[:, r:r + bv.shape[1]])

@@ -82,6 +82,19 @@ class _ClientEmbedding(torch.autograd.Function):
         return out, None
 
 
+class _BcastB(torch.autograd.Function):
+    """Per-client table t [C, ...] broadcast over the batch → [C, B, ...] (CLS token, position embeddings); the
+    backward's batch sum goes through ``client_sum`` (per-client reductions in deterministic mode)."""
+
+    @staticmethod
+    def forward(ctx, t, B):
+        return t.unsqueeze(1).expand(t.shape[0], B, *t.shape[1:])
+
+    @staticmethod
+    def backward(ctx, g):
+        return T.client_sum(g, 1), None
+
+
 class BatchedTransformer:
     """Batched forward of a DistilBERT / ViT over a client-stacked parameter dict.
 
@@ -196,7 +209,7 @@ class BatchedTransformer:
         d = self.dim
         we = _ClientEmbedding.apply(v["embeddings.word_embeddings.weight"], ids.reshape(C, B * S))  # [C, BS, d]
         pe = v["embeddings.position_embeddings.weight"][:, :S]                                  # [C, S, d]
-        h = _bf((we.view(C, B, S, d) + pe.unsqueeze(1)).view(C, B * S, d), dt).contiguous()
+        h = _bf((we.view(C, B, S, d) + _BcastB.apply(pe, B)).view(C, B * S, d), dt).contiguous()
         rows = B * S
         x = self._ln(v, "embeddings.LayerNorm", h, rows, eps=self.emb_eps)
         if training and self.p_emb:
@@ -232,9 +245,10 @@ class BatchedTransformer:
         pw = v["patch_embed.proj.weight"].reshape(C, d, ch * p * p)
         psh = None if self._sh is None else [self._sh["patch_embed.proj.weight"].reshape(C, d, ch * p * p)]
         tok = self._lin(v, patches, None, dt, ([pw], [v["patch_embed.proj.bias"]], psh)).view(C, B, gh * gw, d)
-        cls = _bf(v["cls_token"], dt).view(C, 1, 1, d).expand(C, B, 1, d)
+        cls = _BcastB.apply(_bf(v["cls_token"], dt).view(C, 1, d), B)                                # [C, B, 1, d]
         S = gh * gw + 1
-        x = (torch.cat([cls, tok], 2) + _bf(v["pos_embed"], dt).view(C, 1, S, d)).reshape(C, B * S, d).contiguous()
+        x = (torch.cat([cls, tok], 2) + _BcastB.apply(_bf(v["pos_embed"], dt).view(C, S, d), B)).reshape(
+            C, B * S, d).contiguous()
         rows = B * S
         for i in range(self.n_layers):
             pre = f"blocks.{i}"

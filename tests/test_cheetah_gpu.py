@@ -80,6 +80,7 @@ def test_native_transformer_dp_world_invariant(tmp_path):
     a = launch(1, str(tmp_path / "v1.pt"), "vit_gpu", replicas=2, epochs=2, env=_ENV, timeout=400)
     b = launch(2, str(tmp_path / "v2.pt"), "vit_gpu", replicas=1, epochs=2, env=_ENV, timeout=400)
     assert a["native"] and b["native"]
-    for k, v in a["state"].items():
-        assert torch.equal(v, b["state"][k]), (k, float((v.float() - b["state"][k].float()).abs().max()))
+    diff = {k: float((v.float() - b["state"][k].float()).abs().max()) for k, v in a["state"].items()
+            if not torch.equal(v, b["state"][k])}
+    assert not diff, diff
     assert a["overlapped"] > 0 and b["overlapped"] > 0

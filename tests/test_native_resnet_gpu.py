@@ -355,7 +355,8 @@ def test_multistream_graph_seq_step_matches_eager(momentum, monkeypatch):
                               [i * n for i in range(C)], [n] * C)
     outs = []
     for graphs in (False, True):
-        args = Arguments.from_dict({"x": {"client_optimizer": "sgd", "learning_rate": 1e-3, "momentum": momentum}})
+        args = Arguments.from_dict({"x": {"client_optimizer": "sgd", "learning_rate": 1e-3, "momentum": momentum,
+                                          "client_exec": "sequential"}})
         eng = ClientBatchEngine(copy.deepcopy(model).to(DEV), C, DEV, args, compute_dtype=None)
         assert eng.sequential and eng.tf is None
         eng.use_graphs = graphs
@@ -419,7 +420,8 @@ def test_conv_weight_shadow_matches_autocast_path(monkeypatch):
     outs = []
     for shadow in ("0", "1"):
         monkeypatch.setenv("FEDML_AMD_SEQ_CONV_SHADOW", shadow)
-        args = Arguments.from_dict({"x": {"client_optimizer": "sgd", "learning_rate": 1e-3}})
+        args = Arguments.from_dict({"x": {"client_optimizer": "sgd", "learning_rate": 1e-3,
+                                          "client_exec": "sequential"}})
         eng = ClientBatchEngine(copy.deepcopy(model).to(DEV), C, DEV, args, compute_dtype=torch.bfloat16)
         eng.load_global(eng.layout.flatten(model.state_dict(), device=DEV))
         loss = float(eng.train(store, torch.arange(C, device=DEV), 1, 32, 1e-3, shuffle=False))
