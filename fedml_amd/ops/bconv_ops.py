@@ -27,7 +27,7 @@ def _round_up(v, m):
 def supported_module(m, elem_bytes: int = 4) -> bool:
     """The layer shape alone (no tensors): a groups-1 convolution both native GEMMs take."""
     k = m.kernel_size
-    cout = _pad_channels(m.out_channels)      # narrower / odd widths run zero-padded filters
+    cout = _pad_cout(m.out_channels)      # narrower / odd widths run zero-padded filters
     if not (m.groups == 1 and m.dilation == (1, 1) and k[0] == k[1] and m.stride[0] == m.stride[1]
             and isinstance(m.padding, tuple) and m.padding[0] == m.padding[1] and m.padding_mode == "zeros"):
         return False
@@ -44,7 +44,7 @@ def supported(m, x, w) -> bool:
         return False
     k = m.kernel_size
     # the forward GEMM's N: the kernels' output slices are 16 / 32 / 64-multiples (other widths are zero-padded)
-    cout = _pad_channels(m.out_channels)
+    cout = _pad_cout(m.out_channels)
     if not (m.groups == 1 and m.dilation == (1, 1) and k[0] == k[1] and m.stride[0] == m.stride[1]
             and m.padding[0] == m.padding[1] and isinstance(m.padding, tuple) and m.padding_mode == "zeros"):
         return False
@@ -62,6 +62,12 @@ def _gemm_ok(n, K, es):
     sl = n if n in (16, 32) else 16           # the narrowest slice the dispatch falls back to
     ldk = _round_up(K, 32) + 8
     return sl * ldk * es + 4 * 4 * 256 + 4 * sl * 3 * 4 + 4 * 16 * sl * es <= 160 * 1024
+
+
+def _pad_cout(cout):
+    """Output widths: as ``_pad_channels``, but 128-multiples above 256 (the weight-gradient kernel slices wide
+    layers into 128-channel dy slices)."""
+    return _pad_channels(cout) if cout <= 256 else _round_up(cout, 128)
 
 
 def _pad_channels(cin):
@@ -82,7 +88,7 @@ class _Geom:
         self.cin_pad = _pad_channels(cin)
         # output channels padded the same way (16 / 32 / 64-multiples: the kernels' N slices); the padded filters
         # are zero, their outputs dropped and their gradients never written back
-        self.cout_pad = _pad_channels(cout)
+        self.cout_pad = _pad_cout(cout)
         self.ldk = _round_up(k * k * self.cin_pad, 32) + 8
         self.ldk2 = _round_up(k * k * self.cout_pad, 32) + 8
         self.off_b = _round_up(self.cout_pad * self.ldk, 8)
@@ -141,6 +147,7 @@ class _NativeBConv2d(torch.autograd.Function):
         xn = _to_nhwc(x, C, cin, g.cin_pad)
         packed = torch.zeros(C, g.ld, dtype=dt, device=x.device)
         cp = g.cout_pad
+        wshape = w.shape
         if cp != cout:       # zero filters up to the padded width (a small copy: these are the narrow layers)
             wp = torch.zeros(C, cp, cin, k, k, dtype=torch.float32, device=x.device)
             wp[:, :cout] = w
@@ -156,7 +163,7 @@ class _NativeBConv2d(torch.autograd.Function):
         if b is not None:
             out = out + b.reshape(1, C * cout, 1, 1).to(dt)
         ctx.save_for_backward(xn, packed)
-        ctx.geo = (C, B, H, W, Ho, Wo, cin, cout, k, stride, pad, g, b is not None, w.shape)
+        ctx.geo = (C, B, H, W, Ho, Wo, cin, cout, k, stride, pad, g, b is not None, wshape)
         return out
 
     @staticmethod

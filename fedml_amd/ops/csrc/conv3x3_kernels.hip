@@ -25,7 +25,6 @@
 #include <algorithm>
 
 #include <cstdlib>
-#include <type_traits>
 
 FA_DET_EXPORT(conv3x3)
 
@@ -49,30 +48,6 @@ using prec::F32X3;
 
 enum { XF_NONE = 0, XF_BNRELU = 1, XF_DY = 2 };
 enum { EPI_FWD = 0, EPI_MASK = 2, EPI_BLOCK = 3 };
-
-// C3_PIPE=0 builds the previous (unpipelined) K loop of the tile kernels, for A/B runs (FEDML_AMD_LIB)
-#ifndef C3_PIPE
-#define C3_PIPE 1
-#endif
-#define NKS_PIPE(KC) (9 * ((KC) / 32))
-
-// acc[mt][nt] += w · a[mt] for every mt. Exact fp32 (8 v_mfma_f32_16x16x4_f32 per 8-element fragment): the
-// fragment's 8 products go j-outer / tile-inner, so consecutive MFMAs feed different accumulators and the
-// 40-cycle dependent latency hides behind the 32-cycle issue of the other chains (same per-accumulator k order,
-// bitwise the same results). Other policies: one call per tile.
-template <class P, int M, int N>
-__device__ __forceinline__ void mma_cols(const typename P::frag_t& w, const typename P::frag_t (&a)[M],
-                                         f32x4 (&acc)[M][N], int nt) {
-  if constexpr (std::is_same<typename P::frag_t, prec::f32x8v>::value) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int mt = 0; mt < M; ++mt) acc[mt][nt] = __builtin_amdgcn_mfma_f32_16x16x4f32(w[j], a[mt][j], acc[mt][nt], 0, 0, 0);
-  } else {
-#pragma unroll
-    for (int mt = 0; mt < M; ++mt) acc[mt][nt] = P::mma(w, a[mt], acc[mt][nt]);
-  }
-}
 
 // Exact n / d for 0 ≤ n < 2^26 by multiply-high (branch-free libdivide form; d ≥ 1): the tile
 // index math runs per 16-B chunk and per 16-pixel MFMA tile, where a runtime integer divide
@@ -439,38 +414,7 @@ __global__ __launch_bounds__(256) void conv3x3_gemm_kernel(Args a) {
       for (int mt = 0; mt < MTW; ++mt)
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) acc[mt][nt] = {0.f, 0.f, 0.f, 0.f};
-      if constexpr (C3_PIPE && (KC < 32 || NKS_PIPE(KC) <= 18)) {
-        // software-pipelined K loop: the A fragments of K-step ks + 1 are read from LDS while the MFMAs of step
-        // ks run (double-buffered registers), and the MFMAs of one fragment interleave across the MTW×NT
-        // independent accumulators (exact fp32: 8 v_mfma_f32_16x16x4_f32 per fragment, 40-cycle dependent
-        // latency vs a 32-cycle issue). The naive form read each fragment right before its 8 MFMAs on one
-        // accumulator chain, exposing the LDS latency and the chain latency every K-step.
-        constexpr int NKS = KC >= 32 ? 9 * (KC / 32) : KSTEPS;
-        auto aoff = [&](int ks) -> int {
-          if constexpr (KC >= 32) {
-            const int tap = ks / (KC / 32), cc = ks % (KC / 32);
-            const int kh = tap / 3, kw = tap - 3 * (tap / 3);
-            return (BWD ? ((2 - kh) * TW + (2 - kw)) : (kh * TW + kw)) * LD + 8 * g + cc * 32;
-          } else {
-            return toff[ks];
-          }
-        };
-        frag_t af[2][MTW];
-#pragma unroll
-        for (int mt = 0; mt < MTW; ++mt) af[0][mt] = P::frag(tile + base[mt] + aoff(0));
-#pragma unroll
-        for (int ks = 0; ks < NKS; ++ks) {
-          if (ks + 1 < NKS) {
-#pragma unroll
-            for (int mt = 0; mt < MTW; ++mt) af[(ks + 1) & 1][mt] = P::frag(tile + base[mt] + aoff(ks + 1));
-          }
-#pragma unroll
-          for (int nt = 0; nt < NT; ++nt) {
-            const frag_t bw = P::frag(wrow + nt * 16 * a.ldk + ks * 32);
-            mma_cols<P, MTW, NT>(bw, af[ks & 1], acc, nt);
-          }
-        }
-      } else if constexpr (KC >= 32) {
+      if constexpr (KC >= 32) {
         // one tap per group of KC/32 K-steps: the tap offset is wave-uniform (scalar ALU)
 #pragma unroll TAP_UNROLL
         for (int tap = 0; tap < 9; ++tap) {

@@ -165,6 +165,8 @@ class NativeResNetStep:
         # block's BN3 statistics): the fused backward reads the planes-wide conv input instead of the 4·planes-wide y3
         self.use_ry_bwd = os.environ.get("FEDML_AMD_RY_BWD", "0") == "1" and dtype == torch.float32
         self.use_pbout = os.environ.get("FEDML_AMD_FUSE_BOUT", "1") != "0"
+        # inference (forward_eval): stride-1 bottlenecks of stages 1-2 as one fused kernel (infer_kernels.hip)
+        self.use_fused_eval = os.environ.get("FEDML_AMD_FUSED_EVAL", "1") != "0"
         self.use_fch = os.environ.get("FEDML_AMD_FC_HEAD", "1") != "0"      # fused fc + CE head kernel
         # 3×3 weight gradients on a second HIP stream: they are off the backward's critical path (dW of layer L is
         # needed only by the optimizer), so they fill the CUs the small-grid backward-data kernels of L-1, L-2 leave
@@ -578,12 +580,27 @@ class NativeResNetStep:
                 and self._c1f(cv, nn_ops.EPI_MASK)
                 and nn_ops.conv1x1_wgrad_supported(cv.cin, cv.cout, cv.k, cv.stride, cv.pad))
 
+    def _fused_eval_ok(self, b) -> bool:
+        """Inference (forward_eval) runs this block as ONE fused kernel (nn_ops.bneck_eval): fp32, a stride-1
+        bottleneck without downsample of mid width 16 at 32² or 32 at 16² (CIFAR ResNet-56/110 stages 1-2).
+        FEDML_AMD_FUSED_EVAL=0 keeps the training kernels for inference too."""
+        if b is None or getattr(self, "_training", True) or self.dtype != torch.float32 or not self.use_fused_eval:
+            return False
+        if b.ds_conv is not None or len(b.convs) != 3:
+            return False
+        c1, c2, c3 = b.convs
+        cm = c2.cout
+        return (c1.k == 1 and c1.stride == 1 and c2.k == 3 and c2.stride == 1 and c2.pad == 1 and c3.k == 1
+                and c3.stride == 1 and c1.cin == 4 * cm and c1.cin_pad == c1.cin and c1.cout == cm
+                and c2.cin == cm and c2.cin_pad == cm and c3.cin == cm and c3.cin_pad == cm and c3.cout == 4 * cm
+                and c1.H == c1.W and (cm, c1.H) in ((16, 32), (32, 16)))
+
     def _pbout_ok(self, b, nb) -> bool:
         """Block ``b``'s output is formed in the operand load of the next block's first conv (conv_fwd_pbout: 1×1,
         stride 1) and written once from there instead of by its own block-output pass. Its other readers run after
         that conv and read the stored output: the next block's output pass (identity shortcut) or its downsample
         conv (stage transitions), and the backward (act_in)."""
-        if not self.use_pbout or nb is None or b.ry:
+        if not self.use_pbout or nb is None or b.ry or self._fused_eval_ok(nb):
             return False
         cv = nb.convs[0]
         return cv.k == 1 and cv.stride == 1 and cv.pad == 0 and cv.cin == cv.cin_pad
@@ -1027,6 +1044,17 @@ class NativeResNetStep:
         pend_keys = (None, None)   # its BNs (deferred finalisation: taken by that conv)
         for bi, b in enumerate(self.blocks):
             b.act_in = act_in
+            if pend is None and self._fused_eval_ok(b):
+                # inference: the whole bottleneck in one kernel, BN folded from the running statistics
+                for bn in b.bns:
+                    self._bn_fwd(bn, N, 0, arena, active)
+                vec = [(self.bn_vec[bn.key][0], self.bn_vec[bn.key][1]) for bn in b.bns]
+                pk = self.packed.view(-1)
+                c1 = b.convs[0]
+                if nn_ops.bneck_eval(act_in, b.out, pk, self.packed_ld, [(cv.off_f, cv.ldk) for cv in b.convs], vec,
+                                     C, N, c1.H, c1.W, b.convs[1].cout):
+                    act_in = b.out
+                    continue
             for j, (cv, bn) in enumerate(zip(b.convs, b.bns)):
                 src = act_in if j == 0 else b.ys[j - 1]
                 pro = None if j == 0 else self.bn_vec[b.bns[j - 1].key]

@@ -1,0 +1,59 @@
+"""The fused inference bottleneck (``ops/csrc/infer_kernels.hip``, one kernel per stride-1 bottleneck of stages 1-2)
+against the unfused inference forward of the same native step (the training kernels with BatchNorm folded) and
+against torch fp32 eval — for several models at once with their own running statistics."""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _models(base, C, seed):
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    for _ in range(C):
+        m = copy.deepcopy(base)
+        with torch.no_grad():
+            for name, b in m.named_buffers():
+                if "running_mean" in name:
+                    b.copy_(torch.randn(b.shape, generator=g) * 0.1)
+                elif "running_var" in name:
+                    b.copy_(torch.rand(b.shape, generator=g) * 1.5 + 0.5)
+            for p in m.parameters():
+                p.add_(torch.randn(p.shape, generator=g) * 0.02)
+        out.append(m.cuda().eval())
+    return out
+
+
+@pytest.mark.parametrize("depth,C,N", [(56, 5, 20), (110, 3, 7)])
+def test_fused_eval_matches_unfused_and_torch(depth, C, N):
+    from fedml_amd.core.arena import ParamLayout
+    from fedml_amd.models.cv.resnet import resnet56, resnet110
+    from fedml_amd.parallel.native_resnet import NativeResNetStep
+    torch.manual_seed(0)
+    base = resnet56(100) if depth == 56 else resnet110(10)
+    layout = ParamLayout.from_module(base)
+    models = _models(base, C, depth)
+    arena = torch.stack([layout.flatten(m.state_dict(), device="cuda") for m in models])
+    x = torch.randn(C, N, 3, 32, 32, device="cuda")
+    fused = NativeResNetStep(base, layout, C, "cuda")
+    assert fused.use_fused_eval
+    got = fused.forward_eval(arena, x)
+    assert sum(fused._fused_eval_ok(b) for b in fused.blocks) == (10 if depth == 56 else 22)
+    plain = NativeResNetStep(base, layout, C, "cuda")
+    plain.use_fused_eval = False
+    ref_native = plain.forward_eval(arena, x)
+    torch.cuda.synchronize()
+    err = float((got - ref_native).norm() / ref_native.norm())
+    assert err < 2e-5, err
+    prev = torch.backends.cudnn.allow_tf32
+    torch.backends.cudnn.allow_tf32 = False
+    try:
+        for i, m in enumerate(models):
+            with torch.no_grad():
+                ref = m(x[i])
+            e = float((got[i] - ref).norm() / ref.norm())
+            assert e < 1e-4, (i, e)
+    finally:
+        torch.backends.cudnn.allow_tf32 = prev
