@@ -84,9 +84,21 @@ def comm_stream(device) -> Optional[torch.cuda.Stream]:
     return _COMM_STREAMS[key]
 
 
+def _host_staged(buf: torch.Tensor, group=None) -> bool:
+    """gloo on device tensors (multi-rank rehearsals on a box with fewer GPUs than ranks): the collective runs on
+    a host copy — ``.cpu()`` orders it after every kernel that produced the buffer and the copy back is ordered
+    before every later kernel on this stream, with no reliance on gloo's internal device-stream handoff."""
+    return buf.is_cuda and str(dist.get_backend(group)) == "gloo"
+
+
 def all_reduce_flat(buf: torch.Tensor, group=None, bucket_bytes: int = 64 << 20, async_op: bool = False):
     """SUM all-reduce of a flat buffer in ≤ ``bucket_bytes`` slices (one slice for FL-sized models)."""
     if not is_dist():
+        return [] if async_op else buf
+    if _host_staged(buf, group):
+        h = buf.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+        buf.copy_(h)
         return [] if async_op else buf
     n = buf.numel()
     per = max(1, bucket_bytes // buf.element_size())
@@ -102,19 +114,34 @@ def all_reduce_flat(buf: torch.Tensor, group=None, bucket_bytes: int = 64 << 20,
 
 def broadcast_flat(buf: torch.Tensor, src: int = 0, group=None):
     if is_dist():
-        dist.broadcast(buf, src=src, group=group)
+        if _host_staged(buf, group):
+            h = buf.cpu()
+            dist.broadcast(h, src=src, group=group)
+            buf.copy_(h)
+        else:
+            dist.broadcast(buf, src=src, group=group)
     return buf
 
 
 def reduce_flat(buf: torch.Tensor, dst: int = 0, group=None):
     if is_dist():
-        dist.reduce(buf, dst=dst, op=dist.ReduceOp.SUM, group=group)
+        if _host_staged(buf, group):
+            h = buf.cpu()
+            dist.reduce(h, dst=dst, op=dist.ReduceOp.SUM, group=group)
+            buf.copy_(h)
+        else:
+            dist.reduce(buf, dst=dst, op=dist.ReduceOp.SUM, group=group)
     return buf
 
 
 def all_gather_flat(buf: torch.Tensor, group=None) -> List[torch.Tensor]:
     if not is_dist():
         return [buf]
+    if _host_staged(buf, group):
+        h = buf.cpu()
+        out = [torch.empty_like(h) for _ in range(world_size())]
+        dist.all_gather(out, h, group=group)
+        return [o.to(buf.device) for o in out]
     out = [torch.empty_like(buf) for _ in range(world_size())]
     dist.all_gather(out, buf, group=group)
     return out

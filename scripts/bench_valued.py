@@ -49,6 +49,56 @@ def timed(run_round, rounds, dev):
     return time.perf_counter() - t0
 
 
+def ref_style_valuation(sim, a, dev):
+    """The reference's coalition evaluation (`s_fedavg/fedavg_api.py:267-296`), timed on N coalitions of the round's
+    trained client models: ``copy.deepcopy(model_trainer)``, the reference's ``_aggregate`` (a Python loop over
+    state-dict keys and clients), ``set_model_params``, then a pass over the validation batches. The validation
+    pass uses this repo's trainer ``test`` (on-device confusion counts) instead of the reference's per-batch
+    ``.cpu()`` bookkeeping, which only makes the baseline faster."""
+    import copy
+    import itertools
+    from fedml_amd.trainers import create_model_trainer
+    K = len(sim.results["sampled"][max(sim.results["sampled"])])
+    ids = sim.results["sampled"][max(sim.results["sampled"])]
+    stack = sim._gather_models(ids)
+    w_locals = [(sim.sample_counts[c], {k: v.to(dev) for k, v in sim.layout.unflatten(stack[i]).items()})
+                for i, c in enumerate(ids)]
+    trainer = create_model_trainer(copy.deepcopy(sim.model), sim.args)
+
+    def aggregate(wl):            # reference _aggregate: mutates and returns the first dict
+        total = sum(n for n, _ in wl)
+        n0, avg = wl[0]
+        for k in avg.keys():
+            for i, (n, p) in enumerate(wl):
+                w = n / total
+                avg[k] = p[k] * w if i == 0 else avg[k] + p[k] * w
+        return avg
+
+    combos = [c for r in range(1, K) for c in itertools.combinations(range(K), r)]
+    valid = sim.valid
+
+    def one(cset):
+        tmp = copy.deepcopy(trainer)
+        part = [(n, dict(p)) for n, p in (w_locals[i] for i in cset)]
+        tmp.set_model_params(aggregate(part))
+        return tmp.test(valid, dev, sim.args)
+
+    for c in combos[:2]:
+        one(c)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for c in combos[:a.ref_sample]:
+        one(c)
+    torch.cuda.synchronize(dev)
+    per = (time.perf_counter() - t0) / a.ref_sample
+    n_eval = K * (2 * (2 ** (K - 1) - 1) + 1)
+    return {"metric": "reference-style coalition valuation (deepcopy + Python aggregate + validation pass)",
+            "per_evaluation_ms": round(1000 * per, 2), "evaluations_timed": a.ref_sample,
+            "reference_evaluations_per_round": n_eval,
+            "valuation_s_per_round_extrapolated": round(per * n_eval, 1),
+            "note": "measured per-evaluation cost x the reference's evaluation count; not a full-round run"}
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--opt", default="S-FedAvg")
@@ -64,6 +114,10 @@ def main():
     p.add_argument("--sv-batch", type=int, default=128)
     p.add_argument("--mc", action="store_true", help="Monte-Carlo Shapley (sv_approaching) instead of exact")
     p.add_argument("--skip-sp", action="store_true")
+    p.add_argument("--ref-sample", type=int, default=0,
+                   help="time N coalition evaluations done the reference's way (deepcopy of the trainer, state-dict "
+                        "aggregation in Python, a validation pass per coalition model) and extrapolate to the "
+                        "reference's K·(2·(2^(K-1)−1)+1) evaluations per round")
     a = p.parse_args()
     out = {}
     # ---- RCCL engine
@@ -87,6 +141,8 @@ def main():
                       "dtype": "fp32", "gpus": 1}}
     print(json.dumps(rec), flush=True)
     out["rccl"] = res
+    if a.ref_sample > 0:
+        print(json.dumps(ref_style_valuation(sim, a, dev)), flush=True)
     sim.close()
     del sim
     if a.skip_sp:
