@@ -14,13 +14,18 @@ replicas × b samples is one global batch of Q·b consecutive samples of the pad
 
 Two executors:
 
-* native (GPU, CIFAR ResNets that ``parallel.native_resnet.parse_resnet`` accepts): ``replicas_per_gpu`` = R
-  data-parallel replicas of the model run as ONE client-batched native HIP step (``NativeResNetStep`` with
-  C = R — the same kernels as the FL engine; per-replica BatchNorm, like per-rank BN under DDP). The R replica
-  gradients are averaged on the device (``weighted_sum`` kernel), all-reduced across ranks as one flat buffer,
-  and one fused optimizer kernel updates the master row, which is then broadcast to the R rows. BatchNorm running
-  statistics follow replica 0 of rank 0 (torch DDP's ``broadcast_buffers``): they ride in the buffer slots of the
-  same all-reduce (rank 0 contributes them, the other ranks zeros) — one collective per step.
+* native (GPU): ``replicas_per_gpu`` = R data-parallel replicas of the model are R client slots of the FL simulator's
+  client-batched engine (``ClientBatchEngine``): the native HIP ResNet step for CIFAR ResNets, the client-batched
+  transformer kernels for DistilBERT / ViT (auto picks them at bf16; fp32 transformers go to torch unless
+  ``cheetah_exec: native``). Per-replica BatchNorm, like per-rank BN under DDP. Gradients leave the backward in
+  buckets (``GradBuckets``): the kernels report which gradient-arena columns they finished
+  (``transformer_ops.grad_ready_listener``; torch-accumulated leaves through post-accumulate hooks), and each complete
+  run of columns is averaged over the local replicas (``weighted_sum`` kernel) and all-reduced asynchronously while
+  the rest of the backward is still being issued; the fused optimizer then updates master row 0 bucket by bucket as
+  the all-reduces land, and one broadcast launch copies it to the R rows. BatchNorm running statistics follow
+  replica 0 of rank 0 (torch DDP's ``broadcast_buffers``): rank 0's replica-0 statistics are only ever updated by its
+  own batches, so they are broadcast once when the module is synchronised (evaluation, ``state_dict``), never per
+  step.
 * torch (anything else, CPU): ``FlatDDP`` — bucketed all-reduce overlapped with backward — and the fused flat
   optimizer; bf16 autocast when ``compute_dtype: bf16``.
 
@@ -175,6 +180,13 @@ class CheetahTrainer:
         DistilBERT / ViT). Anything else (its executor would be the torch interpreter) keeps ``FlatDDP``."""
         from ..simulation.rccl.engine import ClientBatchEngine
         eng = ClientBatchEngine(self.model, R, self.device, self.args, self.compute_dtype)
+        if eng.executor == "transformer" and self.compute_dtype is None and not required:
+            # fp32 transformers: the client-batched fp32 GEMMs trail hipBLASLt's fp32 GEMMs on one GPU (ViT-B/16 595
+            # vs 804, DistilBERT 2121 vs 2717 samples/s, profiles/r6_bench_lines.txt); bf16 is the native win
+            # (2266 vs 1722, 7650 vs 6199). cheetah_exec: native forces the native executor anyway.
+            eng.close()
+            logging.info("cheetah: torch executor for an fp32 transformer (cheetah_exec: native overrides)")
+            return
         if eng.executor not in ("native", "transformer"):
             eng.close()
             if required:

@@ -21,6 +21,7 @@
 #include "common.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace infer {
 
@@ -68,8 +69,8 @@ struct Geo {
   static constexpr int FLOATS = CM * LW1 + CM * LW2 + CIN * LW3 + 4 * CM + 2 * CIN + (R + 2) * TW * LM + P2 * LM;
 };
 
-template <int CM, int HW, int R>
-__global__ __launch_bounds__(256) void bneck_eval_kernel(BArgs a) {
+template <int CM, int HW, int R, int NW>
+__global__ __launch_bounds__(64 * NW) void bneck_eval_kernel(BArgs a) {
   using G = Geo<CM, HW, R>;
   constexpr int CIN = G::CIN, H = G::H, W = G::W, TW = G::TW, LM = G::LM;
   constexpr int LW1 = G::LW1, LW2 = G::LW2, LW3 = G::LW3;
@@ -88,30 +89,30 @@ __global__ __launch_bounds__(256) void bneck_eval_kernel(BArgs a) {
   const int u_hi = min(units, u_lo + a.units_per_wg);
   {
     const float* pk = a.wpk + (int64_t)c * a.wpk_ld;
-    for (int i = tid; i < CM * CIN; i += 256) {
+    for (int i = tid; i < CM * CIN; i += 64 * NW) {
       const int n = i / CIN, k = i - n * CIN;
       w1[n * LW1 + k] = pk[a.off1 + (int64_t)n * a.ldk1 + k];
     }
-    for (int i = tid; i < CM * 9 * CM; i += 256) {
+    for (int i = tid; i < CM * 9 * CM; i += 64 * NW) {
       const int n = i / (9 * CM), k = i - n * (9 * CM);
       w2[n * LW2 + k] = pk[a.off2 + (int64_t)n * a.ldk2 + k];
     }
-    for (int i = tid; i < CIN * CM; i += 256) {
+    for (int i = tid; i < CIN * CM; i += 64 * NW) {
       const int n = i / CM, k = i - n * CM;
       w3[n * LW3 + k] = pk[a.off3 + (int64_t)n * a.ldk3 + k];
     }
-    for (int i = tid; i < CM; i += 256) {
+    for (int i = tid; i < CM; i += 64 * NW) {
       vs[i] = a.s1[(int64_t)c * CM + i];
       vs[CM + i] = a.t1[(int64_t)c * CM + i];
       vs[2 * CM + i] = a.s2[(int64_t)c * CM + i];
       vs[3 * CM + i] = a.t2[(int64_t)c * CM + i];
     }
-    for (int i = tid; i < CIN; i += 256) {
+    for (int i = tid; i < CIN; i += 64 * NW) {
       vs[4 * CM + i] = a.s3[(int64_t)c * CIN + i];
       vs[4 * CM + CIN + i] = a.t3[(int64_t)c * CIN + i];
     }
     // the zero halo columns of m1 (conv1 never writes them)
-    for (int i = tid; i < (R + 2) * 2 * CM; i += 256) {
+    for (int i = tid; i < (R + 2) * 2 * CM; i += 64 * NW) {
       const int r = i / (2 * CM), side = (i / CM) & 1, ch = i % CM;
       m1[(r * TW + (side ? W + 1 : 0)) * LM + ch] = 0.f;
     }
@@ -131,7 +132,7 @@ __global__ __launch_bounds__(256) void bneck_eval_kernel(BArgs a) {
     float* yout = a.out + img;
 
     // ---- conv1 + bn1 + relu: rows r0−1 .. r0+R → m1 ----
-    for (int t = wid; t < (G::P1 / 16) * (CM / 16); t += 4) {
+    for (int t = wid; t < (G::P1 / 16) * (CM / 16); t += NW) {
       const int pt = t / (CM / 16), nt = t - pt * (CM / 16);
       const int p = pt * 16 + l16, pr = p / W, pc = p - pr * W;
       const int row = r0 - 1 + pr;
@@ -156,14 +157,14 @@ __global__ __launch_bounds__(256) void bneck_eval_kernel(BArgs a) {
     __syncthreads();
 
     // ---- conv2 (3×3) + bn2 + relu → m2: two tiles per wave iteration (T2 is a multiple of 8) ----
-    static_assert(((G::P2 / 16) * (CM / 16)) % 8 == 0, "conv2 tiles");
-    for (int t = wid; t < (G::P2 / 16) * (CM / 16); t += 8) {
+    static_assert(((G::P2 / 16) * (CM / 16)) % (2 * NW) == 0, "conv2 tiles");
+    for (int t = wid; t < (G::P2 / 16) * (CM / 16); t += 2 * NW) {
       int p[2], ch[2];
       const float* wr[2];
       const float* mp[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int th = t + 4 * h;
+        const int th = t + NW * h;
         const int pt = th / (CM / 16), nt = th - pt * (CM / 16);
         p[h] = pt * 16 + l16;
         const int pr = p[h] / W, pc = p[h] - pr * W;
@@ -198,15 +199,15 @@ __global__ __launch_bounds__(256) void bneck_eval_kernel(BArgs a) {
     __syncthreads();
 
     // ---- conv3 (1×1) + bn3 + residual + relu → y: two tiles per wave iteration ----
-    static_assert(((G::P2 / 16) * (CIN / 16)) % 8 == 0, "conv3 tiles");
-    for (int t = wid; t < (G::P2 / 16) * (CIN / 16); t += 8) {
+    static_assert(((G::P2 / 16) * (CIN / 16)) % (2 * NW) == 0, "conv3 tiles");
+    for (int t = wid; t < (G::P2 / 16) * (CIN / 16); t += 2 * NW) {
       int p[2], ch[2];
       const float* wr[2];
       const float* mp[2];
       float4 res[2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int th = t + 4 * h;
+        const int th = t + NW * h;
         const int pt = th / (CIN / 16), nt = th - pt * (CIN / 16);
         p[h] = pt * 16 + l16;
         wr[h] = w3 + (nt * 16 + l16) * LW3 + 4 * g;
@@ -238,7 +239,7 @@ __global__ __launch_bounds__(256) void bneck_eval_kernel(BArgs a) {
   }
 }
 
-template <int CM, int HW, int R>
+template <int CM, int HW, int R, int NW>
 static int launch(BArgs a, int C, hipStream_t stream) {
   using G = Geo<CM, HW, R>;
   const size_t smem = (size_t)G::FLOATS * 4;
@@ -249,9 +250,9 @@ static int launch(BArgs a, int C, hipStream_t stream) {
   const int per_model = std::max(1, std::min(units, (1024 + C - 1) / C));
   a.units_per_wg = (units + per_model - 1) / per_model;
   const int gx = (units + a.units_per_wg - 1) / a.units_per_wg;
-  auto kern = bneck_eval_kernel<CM, HW, R>;
+  auto kern = bneck_eval_kernel<CM, HW, R, NW>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
-  hipLaunchKernelGGL(kern, dim3(gx, C), dim3(256), smem, stream, a);
+  hipLaunchKernelGGL(kern, dim3(gx, C), dim3(64 * NW), smem, stream, a);
   return (int)hipGetLastError();
 }
 
@@ -266,7 +267,15 @@ FA_EXPORT int fa_bneck_eval_f32(const float* x, float* out, const float* wpk, in
                                 int W, int cm, hipStream_t stream) {
   if (C <= 0 || N <= 0 || H != W || C > 65535) return (int)hipErrorInvalidValue;
   infer::BArgs a = {x, out, wpk, wpk_ld, off1, off2, off3, ldk1, ldk2, ldk3, s1, t1, s2, t2, s3, t3, N, 1};
-  if (cm == 16 && H == 32) return infer::launch<16, 32, 8>(a, C, stream);
-  if (cm == 32 && H == 16) return infer::launch<32, 16, 8>(a, C, stream);
+  // 8 waves per workgroup: two per SIMD share the staged weights (the 32-wide stage's 73 KB of weights leave room
+  // for one workgroup per CU), so one wave's LDS / HBM waits overlap the other's MFMAs
+  static const int variant = [] {
+    const char* e = getenv("FEDML_AMD_BNECK_EVAL_VARIANT");
+    return e ? atoi(e) : 1;
+  }();
+  if (cm == 16 && H == 32)
+    return variant == 0 ? infer::launch<16, 32, 8, 4>(a, C, stream) : infer::launch<16, 32, 16, 8>(a, C, stream);
+  if (cm == 32 && H == 16)
+    return variant == 0 ? infer::launch<32, 16, 8, 4>(a, C, stream) : infer::launch<32, 16, 8, 8>(a, C, stream);
   return -2;
 }
