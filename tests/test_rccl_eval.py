@@ -101,3 +101,26 @@ def test_eval_stats_cpu_matches_direct_counts():
             assert cls[c, 1, k] == int((m & (y == k)).sum())
             assert cls[c, 2, k] == int((m & (pred == k)).sum())
     assert np.isfinite(sums.numpy()).all()
+
+
+def test_eval_metrics_world_invariant(tmp_path):
+    """The evaluation's shards (global test rows split by rank, clients c ≡ rank mod world) and its one all-reduce
+    give the same per-round metric record on 1 and 2 gloo ranks (full-batch training: the same global models)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    import mp_harness
+    here = os.path.dirname(os.path.abspath(__file__))
+    out = {}
+    for world in (1, 2):
+        port = mp_harness.free_port()
+        path = str(tmp_path / f"h{world}.json")
+        env = dict(os.environ, PYTHONPATH=os.path.dirname(here), OMP_NUM_THREADS="1")
+        ps = [subprocess.Popen([sys.executable, os.path.join(here, "dist_worker_eval.py"), str(r), str(world),
+                                str(port), path], env=env) for r in range(world)]
+        assert mp_harness.wait_all(ps, 300) == [0] * world
+        out[world] = json.load(open(path))
+    assert set(out[1]) == set(out[2]) and len(out[1]) == 3
+    for r in out[1]:
+        _close(out[1][r], out[2][r], 1e-5)
