@@ -434,3 +434,41 @@ def test_conv_weight_shadow_matches_autocast_path(monkeypatch):
     init = ParamLayout.from_module(model).flatten(model.state_dict(), device=DEV)
     assert abs(l0 - l1) / abs(l0) < 1e-2
     assert float((p0 - p1).norm() / (p0 - init).norm()) < 5e-2
+
+
+def test_seq_graph_reads_the_rounds_class_weights(monkeypatch):
+    """S-FedAvg's class-balanced CE on the captured per-client path: the class-weight table changes
+    every round; the captured graph must read THIS round's table (one persistent engine buffer, refilled in place),
+    so three rounds with different tables give the same parameters replayed as run eagerly."""
+    from fedml_amd.arguments import Arguments
+    from fedml_amd.models.cv.resnet import resnet18_cifar
+    from fedml_amd.simulation.rccl.client_store import DeviceClientStore
+    from fedml_amd.simulation.rccl.engine import ClientBatchEngine
+    monkeypatch.setenv("FEDML_AMD_NATIVE_CONV", "0")
+    torch.manual_seed(0)
+    model = resnet18_cifar(10)
+    C, n = 2, 64
+    store = DeviceClientStore(torch.randn(C * n, 3, 16, 16, device=DEV), torch.randint(0, 10, (C * n,), device=DEV),
+                              [i * n for i in range(C)], [n] * C)
+    g = torch.Generator().manual_seed(3)
+    tables = [torch.rand(C, 10, generator=g) * 3 + 0.1 for _ in range(3)]
+    outs = []
+    for graphs in (False, True):
+        args = Arguments.from_dict({"x": {"client_optimizer": "sgd", "learning_rate": 1e-3,
+                                          "client_exec": "sequential"}})
+        eng = ClientBatchEngine(copy.deepcopy(model).to(DEV), C, DEV, args, compute_dtype=None)
+        assert eng.sequential and eng.tf is None
+        eng.use_graphs = graphs
+        eng.load_global(eng.layout.flatten(model.state_dict(), device=DEV))
+        losses = []
+        for t in tables:
+            eng.class_weight = t.to(DEV)          # a fresh tensor each round, as ValuedRCCLSimulator.run_round does
+            losses.append(float(eng.train(store, torch.arange(C, device=DEV), 1, 32, 1e-3, shuffle=False)))
+        torch.cuda.synchronize()
+        outs.append((losses, eng.params.clone()))
+        eng.close()
+    (l0, p0), (l1, p1) = outs
+    init = ParamLayout.from_module(model).flatten(model.state_dict(), device=DEV)
+    for a, b in zip(l0, l1):
+        assert abs(a - b) / abs(a) < 1e-3, (l0, l1)
+    assert float((p0 - p1).norm() / (p0 - init).norm()) < 1e-3
