@@ -12,7 +12,8 @@
 //   y  = relu(s3·(m2 ⊛ W3) + t3 + x)                                                        → HBM
 //
 // reading x once (plus its L2-resident residual re-read) and writing y once. The model's three packed weight
-// matrices stay in LDS for all the units of that model the workgroup processes.
+// matrices stay in LDS (bneck_eval_kernel) or, by default, in each wave's registers (bneck_eval_rw_kernel) for all
+// the units of that model the workgroup processes.
 //
 // MFMA operand convention (K16 fragments): in one K-step of 16, lane group g = lane>>4 holds k = 4g..4g+3 as a
 // float4 and MFMA j (0..3) consumes element j — A = weights (row = output channel lane&15), B = activations
@@ -239,6 +240,272 @@ __global__ __launch_bounds__(64 * NW) void bneck_eval_kernel(BArgs a) {
   }
 }
 
+// ---- register-resident weights (variant 3) ----
+// Every wave keeps ONE output-channel tile per conv for the whole kernel (conv1 / conv2: nt = wave mod CM/16, conv3:
+// nt = wave mod CIN/16), so the three A-fragment sets live in VGPRs — loaded once from the packed weights, no LDS
+// weight reads in the MFMA loops (half the LDS traffic of conv2, none in conv1 / conv3) and no 73 KB weight stage
+// in LDS. conv1's x tiles are software-pipelined one tile ahead (the last tile of a unit prefetches the next unit's
+// first, in flight across conv2 / conv3); its K is split over two accumulators so the MFMA chain never waits on
+// itself.
+//
+// BAND (the memory-bound 32×32 stage): the unit's whole input band (R+2 rows × W × CIN) is staged in LDS from
+// registers that were loaded during the PREVIOUS unit — HBM reads spread over the whole unit instead of bursting in
+// conv1, ~80 KB in flight per CU — and the residual comes from the band too (x is read from HBM exactly once).
+template <int CM, int HW, int R, bool BAND, bool PIPE>
+struct GeoR {
+  static constexpr int CIN = 4 * CM, H = HW, W = HW, BANDS = H / R, TW = W + 2;
+  static constexpr int P1 = (R + 2) * W, P2 = R * W, PT1 = P1 / 16, PT2 = P2 / 16;
+  static constexpr int NT1 = CM / 16, NT3 = CIN / 16, LM = CM + 4, LX = CIN + 4;
+  static constexpr int NF4 = P1 * CIN / 4;   // band float4s
+  static constexpr int M1F = (R + 2) * TW * LM, M2F = P2 * LM, NB = PIPE ? 2 : 1;   // m1 / m2 floats; buffers
+  static constexpr int FLOATS = 4 * CM + 2 * CIN + NB * (M1F + M2F) + (BAND ? P1 * LX : 0);
+};
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+
+// NW = 8: one workgroup per CU; NW = 4 (smaller R): two per CU, so one workgroup's barrier waits overlap the
+// other's MFMAs. conv3 gives a wave NT3/NW channel tiles when the waves are fewer than CIN/16.
+template <int CM, int HW, int R, bool BAND, bool PIPE, int NW>
+__global__ __launch_bounds__(64 * NW, 2) void bneck_eval_rw_kernel(BArgs a) {   // ≥ 2 waves per SIMD
+  using G = GeoR<CM, HW, R, BAND, PIPE>;
+  static_assert(!(BAND && PIPE), "the band is read by conv1 and conv3 of one unit");
+  constexpr int CIN = G::CIN, H = G::H, W = G::W, TW = G::TW, LM = G::LM, NT1 = G::NT1, NT3 = G::NT3;
+  constexpr int NTW3 = NT3 > NW ? NT3 / NW : 1;   // conv3 channel tiles per wave
+  constexpr int PS1 = NW / NT1, PS3 = NT3 >= NW ? 1 : NW / NT3;   // pixel-tile strides of conv1/conv2 and conv3
+  constexpr int PF = (G::NF4 + 64 * NW - 1) / (64 * NW);          // BAND float4s per thread
+  static_assert(NW % NT1 == 0 && (NW % NT3 == 0 || NT3 % NW == 0), "wave split");
+  static_assert(G::PT2 % (2 * PS1) == 0 && G::PT2 % (2 * PS3) == 0, "two pixel tiles per wave iteration");
+  static_assert((CIN / 16) % 2 == 0, "conv1 K split");
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* vs = sm;                          // s1 t1 s2 t2 [CM], s3 t3 [CIN]
+  float* m1 = vs + 4 * CM + 2 * CIN;       // [NB][R+2][TW][LM]
+  float* m2 = m1 + G::NB * G::M1F;         // [NB][P2][LM]
+  float* xb = m2 + G::NB * G::M2F;         // BAND: [P1][LX]
+  constexpr int LX = G::LX;
+  const int c = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4, l16 = lane & 15;
+  const int units = a.N * G::BANDS;
+  const int u_lo = blockIdx.x * a.units_per_wg;
+  if (u_lo >= units) return;   // uniform: whole workgroup
+  const int u_hi = min(units, u_lo + a.units_per_wg);
+  const int nt1 = wid % NT1, pg1 = wid / NT1, nt3 = wid % NT3, pg3 = NT3 >= NW ? 0 : wid / NT3;
+
+  const float* pk = a.wpk + (int64_t)c * a.wpk_ld;
+  float4 a1[CIN / 16], a2[9 * NT1], a3[NTW3][NT1];
+  {
+    const float* w1 = pk + a.off1 + (int64_t)(nt1 * 16 + l16) * a.ldk1 + 4 * g;
+    const float* w2 = pk + a.off2 + (int64_t)(nt1 * 16 + l16) * a.ldk2 + 4 * g;
+    const float* w3 = pk + a.off3 + (int64_t)(nt3 * 16 + l16) * a.ldk3 + 4 * g;   // + NW·16 rows per extra tile
+#pragma unroll
+    for (int ks = 0; ks < CIN / 16; ++ks) a1[ks] = ld4(w1 + 16 * ks);
+#pragma unroll
+    for (int j = 0; j < 9 * NT1; ++j) a2[j] = ld4(w2 + (j / NT1) * CM + 16 * (j % NT1));
+#pragma unroll
+    for (int j = 0; j < NTW3; ++j)
+#pragma unroll
+      for (int ks = 0; ks < NT1; ++ks) a3[j][ks] = ld4(w3 + (int64_t)j * NW * 16 * a.ldk3 + 16 * ks);
+  }
+  for (int i = tid; i < CM; i += 64 * NW) {
+    vs[i] = a.s1[(int64_t)c * CM + i];
+    vs[CM + i] = a.t1[(int64_t)c * CM + i];
+    vs[2 * CM + i] = a.s2[(int64_t)c * CM + i];
+    vs[3 * CM + i] = a.t2[(int64_t)c * CM + i];
+  }
+  for (int i = tid; i < CIN; i += 64 * NW) {
+    vs[4 * CM + i] = a.s3[(int64_t)c * CIN + i];
+    vs[4 * CM + CIN + i] = a.t3[(int64_t)c * CIN + i];
+  }
+  for (int i = tid; i < G::NB * (R + 2) * 2 * CM; i += 64 * NW) {   // m1's zero halo columns (never written)
+    const int b = i / ((R + 2) * 2 * CM), r = (i / (2 * CM)) % (R + 2), side = (i / CM) & 1, ch = i % CM;
+    m1[b * G::M1F + (r * TW + (side ? W + 1 : 0)) * LM + ch] = 0.f;
+  }
+  const float* s1 = vs;
+  const float* t1 = vs + CM;
+  const float* s2 = vs + 2 * CM;
+  const float* t2 = vs + 3 * CM;
+  const float* s3 = vs + 4 * CM;
+  const float* t3 = vs + 4 * CM + CIN;
+
+  // x tile `pt` of unit u (rows r0−1 .. r0+R; rows outside the image read a clamped in-image row — conv1 zeroes
+  // their outputs, so only the address has to be valid)
+  float4 bx[CIN / 16];
+  float4 pf[BAND ? PF : 1];
+  // BAND: thread tid holds float4s f = tid + 512·i of the band (pixel f / (CIN/4), channels 4·(f mod CIN/4)):
+  // consecutive threads read consecutive 16 B of HBM. Rows outside the image are not loaded (conv1 zeroes them).
+  auto load_band = [&](int u) {
+    const int n = u / G::BANDS, r0 = (u - n * G::BANDS) * R;
+    const float* xi = a.x + ((int64_t)c * a.N + n) * H * W * CIN;
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      const int f = tid + 64 * NW * i, q = f / (CIN / 4), row = r0 - 1 + q / W;
+      if (f < G::NF4 && row >= 0 && row < H)
+        pf[i] = ld4(xi + ((int64_t)row * W + q % W) * CIN + 4 * (f % (CIN / 4)));
+    }
+  };
+  auto store_band = [&]() {
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      const int f = tid + 64 * NW * i;
+      if (f < G::NF4) *reinterpret_cast<float4*>(xb + (f / (CIN / 4)) * LX + 4 * (f % (CIN / 4))) = pf[i];
+    }
+  };
+  auto load_x = [&](int u, int pt) {
+    const int n = u / G::BANDS, r0 = (u - n * G::BANDS) * R;
+    const int p = pt * 16 + l16, pr = p / W, pc = p - pr * W;
+    const int row = min(max(r0 - 1 + pr, 0), H - 1);
+    const float* xp = a.x + (((int64_t)c * a.N + n) * H * W + (int64_t)row * W + pc) * CIN + 4 * g;
+#pragma unroll
+    for (int ks = 0; ks < CIN / 16; ++ks) bx[ks] = ld4(xp + 16 * ks);
+  };
+  // ---- conv1 + bn1 + relu: unit u → m1b ----
+  auto conv1 = [&](int u, float* m1b) {
+    const int n = u / G::BANDS, r0 = (u - n * G::BANDS) * R;
+    for (int pt = pg1; pt < G::PT1; pt += PS1) {
+      float4 cur[CIN / 16];
+      if constexpr (BAND) {
+        const float* xp = xb + (pt * 16 + l16) * LX + 4 * g;
+#pragma unroll
+        for (int ks = 0; ks < CIN / 16; ++ks) cur[ks] = ld4(xp + 16 * ks);
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < CIN / 16; ++ks) cur[ks] = bx[ks];
+        if (pt + PS1 < G::PT1) load_x(u, pt + PS1);
+        else if (u + 1 < u_hi) load_x(u + 1, pg1);
+      }
+      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < CIN / 16; ks += 2) mma4x2(a1[ks], cur[ks], acc0, a1[ks + 1], cur[ks + 1], acc1);
+      const int p = pt * 16 + l16, pr = p / W, pc = p - pr * W;
+      const int row = r0 - 1 + pr;
+      const bool inside = row >= 0 && row < H;
+      const int ch = nt1 * 16 + 4 * g;
+      float4 v;
+      v.x = inside ? fmaxf((acc0[0] + acc1[0]) * s1[ch] + t1[ch], 0.f) : 0.f;
+      v.y = inside ? fmaxf((acc0[1] + acc1[1]) * s1[ch + 1] + t1[ch + 1], 0.f) : 0.f;
+      v.z = inside ? fmaxf((acc0[2] + acc1[2]) * s1[ch + 2] + t1[ch + 2], 0.f) : 0.f;
+      v.w = inside ? fmaxf((acc0[3] + acc1[3]) * s1[ch + 3] + t1[ch + 3], 0.f) : 0.f;
+      *reinterpret_cast<float4*>(m1b + (pr * TW + pc + 1) * LM + ch) = v;
+    }
+  };
+
+  // ---- conv2 (3×3) + bn2 + relu: m1b → m2b, pixel tiles pt and pt + PS1 per iteration ----
+  auto conv2 = [&](const float* m1b, float* m2b) {
+    for (int pt = pg1; pt < G::PT2; pt += 2 * PS1) {
+      const float* mp[2];
+      int p[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        p[h] = (pt + h * PS1) * 16 + l16;
+        const int pr = p[h] / W, pc = p[h] - pr * W;
+        mp[h] = m1b + (pr * TW + pc) * LM + 4 * g;
+      }
+      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int mo = ((tap / 3) * TW + tap % 3) * LM;
+#pragma unroll
+        for (int cc = 0; cc < NT1; ++cc)
+          mma4x2(a2[tap * NT1 + cc], ld4(mp[0] + mo + 16 * cc), acc0, a2[tap * NT1 + cc], ld4(mp[1] + mo + 16 * cc),
+                 acc1);
+      }
+      const int c0 = nt1 * 16 + 4 * g;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 acc = h ? acc1 : acc0;
+        float4 v;
+        v.x = fmaxf(acc[0] * s2[c0] + t2[c0], 0.f);
+        v.y = fmaxf(acc[1] * s2[c0 + 1] + t2[c0 + 1], 0.f);
+        v.z = fmaxf(acc[2] * s2[c0 + 2] + t2[c0 + 2], 0.f);
+        v.w = fmaxf(acc[3] * s2[c0 + 3] + t2[c0 + 3], 0.f);
+        *reinterpret_cast<float4*>(m2b + p[h] * LM + c0) = v;
+      }
+    }
+  };
+
+  // ---- conv3 (1×1) + bn3 + residual + relu: m2b → y of unit u, pixel tiles pt and pt + PS3 per iteration ----
+  auto conv3 = [&](int u, const float* m2b) {
+    const int n = u / G::BANDS, r0 = (u - n * G::BANDS) * R;
+    const int64_t img = ((int64_t)c * a.N + n) * H * W * CIN + (int64_t)r0 * W * CIN;
+#pragma unroll
+    for (int j = 0; j < NTW3; ++j) {
+      const int c0 = (nt3 + j * NW) * 16 + 4 * g;
+      for (int pt = pg3; pt < G::PT2; pt += 2 * PS3) {
+        int p[2];
+        float4 res[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          p[h] = (pt + h * PS3) * 16 + l16;
+          res[h] = BAND ? ld4(xb + (W + p[h]) * LX + c0)             // the band's centre rows
+                        : ld4(a.x + img + (int64_t)p[h] * CIN + c0);   // early: hides under the MFMAs
+        }
+        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < NT1; ++ks)
+          mma4x2(a3[j][ks], ld4(m2b + p[0] * LM + 16 * ks + 4 * g), acc0, a3[j][ks],
+                 ld4(m2b + p[1] * LM + 16 * ks + 4 * g), acc1);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f32x4 acc = h ? acc1 : acc0;
+          float4 v;
+          v.x = fmaxf(acc[0] * s3[c0] + t3[c0] + res[h].x, 0.f);
+          v.y = fmaxf(acc[1] * s3[c0 + 1] + t3[c0 + 1] + res[h].y, 0.f);
+          v.z = fmaxf(acc[2] * s3[c0 + 2] + t3[c0 + 2] + res[h].z, 0.f);
+          v.w = fmaxf(acc[3] * s3[c0 + 3] + t3[c0 + 3] + res[h].w, 0.f);
+          *reinterpret_cast<float4*>(a.out + img + (int64_t)p[h] * CIN + c0) = v;
+        }
+      }
+    }
+  };
+
+  if constexpr (BAND) load_band(u_lo);
+  else if (pg1 < G::PT1) load_x(u_lo, pg1);
+  __syncthreads();
+
+  if constexpr (PIPE) {
+    // interval k: conv1 of unit k, conv2 of unit k−1, conv3 of unit k−2 (m1 / m2 double-buffered): one barrier per
+    // unit, and every interval carries a whole bottleneck's work, so the waves stay balanced between barriers
+    const int nu = u_hi - u_lo;
+    for (int k = 0; k < nu + 2; ++k) {
+      if (k < nu) conv1(u_lo + k, m1 + (k & 1) * G::M1F);
+      if (k >= 1 && k - 1 < nu) conv2(m1 + ((k - 1) & 1) * G::M1F, m2 + ((k - 1) & 1) * G::M2F);
+      if (k >= 2) conv3(u_lo + k - 2, m2 + (k & 1) * G::M2F);
+      __syncthreads();
+    }
+  } else {
+    for (int u = u_lo; u < u_hi; ++u) {
+      if constexpr (BAND) {
+        store_band();
+        __syncthreads();
+        if (u + 1 < u_hi) load_band(u + 1);   // in flight for the whole unit
+      }
+      conv1(u, m1);
+      __syncthreads();
+      conv2(m1, m2);
+      __syncthreads();
+      conv3(u, m2);
+      __syncthreads();   // m1 / m2 are rewritten by the next unit
+    }
+  }
+}
+
+template <int CM, int HW, int R, bool BAND, bool PIPE, int NW>
+static int launch_rw(BArgs a, int C, hipStream_t stream) {
+  using G = GeoR<CM, HW, R, BAND, PIPE>;
+  const size_t smem = (size_t)G::FLOATS * 4;
+  if (smem > 160 * 1024) return -5;
+  const int units = a.N * G::BANDS;
+  // one 8-wave (two 4-wave) workgroups per CU (the weight fragments take ~60-120 VGPRs a wave): ~2 workgroups per
+  // CU over all models, each looping over a contiguous run of one model's units
+  const int target = NW == 4 ? 1024 : 512;
+  const int per_model = std::max(1, std::min(units, (target + C - 1) / C));
+  a.units_per_wg = (units + per_model - 1) / per_model;
+  const int gx = (units + a.units_per_wg - 1) / a.units_per_wg;
+  auto kern = bneck_eval_rw_kernel<CM, HW, R, BAND, PIPE, NW>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  hipLaunchKernelGGL(kern, dim3(gx, C), dim3(64 * NW), smem, stream, a);
+  return (int)hipGetLastError();
+}
+
 template <int CM, int HW, int R, int NW>
 static int launch(BArgs a, int C, hipStream_t stream) {
   using G = Geo<CM, HW, R>;
@@ -267,15 +534,39 @@ FA_EXPORT int fa_bneck_eval_f32(const float* x, float* out, const float* wpk, in
                                 int W, int cm, hipStream_t stream) {
   if (C <= 0 || N <= 0 || H != W || C > 65535) return (int)hipErrorInvalidValue;
   infer::BArgs a = {x, out, wpk, wpk_ld, off1, off2, off3, ldk1, ldk2, ldk3, s1, t1, s2, t2, s3, t3, N, 1};
-  // 8 waves per workgroup: two per SIMD share the staged weights (the 32-wide stage's 73 KB of weights leave room
-  // for one workgroup per CU), so one wave's LDS / HBM waits overlap the other's MFMAs
+  // FEDML_AMD_BNECK_EVAL_VARIANT (A/B of the tilings; ms per 128-model × 64-image ResNet-56 forward on MI355X,
+  // profiles/r6_fused_eval_variants.txt): 0 = LDS-resident weights, 4 waves, R = 8 (27.9); 1 = 8 waves, R = 16 / 8
+  // (26.4); 2 = 8 waves, R = 8 / 16 (26.0); 3 = register-resident weights, R = 16 (25.3); 4 = same, R = 8 (25.4);
+  // 5 (default) = 3 with the stage-1 input band staged in LDS one unit ahead (24.4); 6 = 4-wave workgroups, R = 4
+  // band (25.6); 7 = three-stage unit pipeline, one barrier per unit (26.5)
   static const int variant = [] {
     const char* e = getenv("FEDML_AMD_BNECK_EVAL_VARIANT");
-    return e ? atoi(e) : 1;
+    return e ? atoi(e) : 5;
   }();
-  if (cm == 16 && H == 32)
-    return variant == 0 ? infer::launch<16, 32, 8, 4>(a, C, stream) : infer::launch<16, 32, 16, 8>(a, C, stream);
-  if (cm == 32 && H == 16)
-    return variant == 0 ? infer::launch<32, 16, 8, 4>(a, C, stream) : infer::launch<32, 16, 8, 8>(a, C, stream);
+  if (variant >= 3 && ((off1 | off2 | off3 | ldk1 | ldk2 | ldk3 | wpk_ld) & 3) == 0 &&
+      (reinterpret_cast<uintptr_t>(wpk) & 15) == 0) {   // float4 weight-fragment loads
+    if (cm == 16 && H == 32) {
+      if (variant == 3) return infer::launch_rw<16, 32, 16, false, false, 8>(a, C, stream);
+      if (variant == 4) return infer::launch_rw<16, 32, 8, false, false, 8>(a, C, stream);
+      if (variant == 6) return infer::launch_rw<16, 32, 4, true, false, 4>(a, C, stream);
+      if (variant == 7) return infer::launch_rw<16, 32, 8, false, true, 8>(a, C, stream);
+      return infer::launch_rw<16, 32, 8, true, false, 8>(a, C, stream);
+    }
+    if (cm == 32 && H == 16) {
+      if (variant == 4) return infer::launch_rw<32, 16, 8, false, false, 8>(a, C, stream);
+      if (variant >= 6) return infer::launch_rw<32, 16, 8, false, true, 8>(a, C, stream);
+      return infer::launch_rw<32, 16, 16, false, false, 8>(a, C, stream);
+    }
+  }
+  if (cm == 16 && H == 32) {
+    if (variant == 0) return infer::launch<16, 32, 8, 4>(a, C, stream);
+    if (variant == 2) return infer::launch<16, 32, 8, 8>(a, C, stream);
+    return infer::launch<16, 32, 16, 8>(a, C, stream);
+  }
+  if (cm == 32 && H == 16) {
+    if (variant == 0) return infer::launch<32, 16, 8, 4>(a, C, stream);
+    if (variant == 2) return infer::launch<32, 16, 16, 8>(a, C, stream);
+    return infer::launch<32, 16, 8, 8>(a, C, stream);
+  }
   return -2;
 }
