@@ -523,11 +523,416 @@ static int launch(BArgs a, int C, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
+// ---- stage-entry bottleneck with a downsample shortcut (register-resident weights) ----
+// y = relu(s3·(m2 ⊛ W3) + t3 + sd·(x ⊛_S Wd) + td), m2 = relu(bn2(conv2_S(relu(bn1(x ⊛ W1))))): the first block of a
+// stage (reference model/cv/resnet.py:113-121 — stride S on the 3×3, a 1×1 stride-S projection shortcut). x has CX
+// channels at HW², y has CO = 4·CM at (HW/S)². A unit is a band of R output rows; conv1 runs on the S·(R−1)+3 input
+// rows the band's 3×3 windows touch. The projection's operands are the x pixels conv1 just read (L2-resident).
+template <int CX, int CM, int HW, int S, int R>
+struct GeoD {
+  static constexpr int CO = 4 * CM, H = HW, W = HW, HO = HW / S, WO = HW / S, BANDS = HO / R, TW = W + 2;
+  static constexpr int RI = S * (R - 1) + 3, P1 = RI * W, P2 = R * WO, PT1 = P1 / 16, PT2 = P2 / 16;
+  static constexpr int NT1 = CM / 16, NT3 = CO / 16, KX = CX / 16, LM = CM + 4;
+  static constexpr int M1F = RI * TW * LM, M2F = P2 * LM;
+  static constexpr int FLOATS = 4 * CM + 4 * CO + M1F + M2F;
+};
+
+struct DArgs {
+  BArgs b;
+  int64_t offd;
+  int ldkd;
+  const float *sd, *td;   // folded shortcut BatchNorm [C][CO]
+};
+
+template <int CX, int CM, int HW, int S, int R>
+__global__ __launch_bounds__(512, 2) void bneck_ds_eval_kernel(DArgs d) {
+  using G = GeoD<CX, CM, HW, S, R>;
+  constexpr int NW = 8, CO = G::CO, H = G::H, W = G::W, WO = G::WO, TW = G::TW, LM = G::LM;
+  constexpr int NT1 = G::NT1, NT3 = G::NT3, KX = G::KX;
+  constexpr int NTW3 = NT3 > NW ? NT3 / NW : 1;
+  constexpr int PS1 = NW / NT1, PS3 = NT3 >= NW ? 1 : NW / NT3;
+  static_assert(CX % 16 == 0 && G::P1 % 16 == 0 && G::P2 % 16 == 0 && HW % S == 0 && G::HO % R == 0, "geometry");
+  static_assert(NW % NT1 == 0 && (NW % NT3 == 0 || NT3 % NW == 0), "wave split");
+  static_assert(G::PT2 % (2 * PS1) == 0 && G::PT2 % (2 * PS3) == 0, "two pixel tiles per wave iteration");
+  const BArgs& a = d.b;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* vs = sm;                          // s1 t1 s2 t2 [CM], s3 t3 sd td [CO]
+  float* m1 = vs + 4 * CM + 4 * CO;        // [RI][TW][LM]
+  float* m2 = m1 + G::M1F;                 // [P2][LM]
+  const int c = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4, l16 = lane & 15;
+  const int units = a.N * G::BANDS;
+  const int u_lo = blockIdx.x * a.units_per_wg;
+  if (u_lo >= units) return;   // uniform: whole workgroup
+  const int u_hi = min(units, u_lo + a.units_per_wg);
+  const int nt1 = wid % NT1, pg1 = wid / NT1, nt3 = wid % NT3, pg3 = NT3 >= NW ? 0 : wid / NT3;
+
+  const float* pk = a.wpk + (int64_t)c * a.wpk_ld;
+  float4 a1[KX], a2[9 * NT1], a3[NTW3][NT1], ad[NTW3][KX];
+  {
+    const float* w1 = pk + a.off1 + (int64_t)(nt1 * 16 + l16) * a.ldk1 + 4 * g;
+    const float* w2 = pk + a.off2 + (int64_t)(nt1 * 16 + l16) * a.ldk2 + 4 * g;
+    const float* w3 = pk + a.off3 + (int64_t)(nt3 * 16 + l16) * a.ldk3 + 4 * g;
+    const float* wd = pk + d.offd + (int64_t)(nt3 * 16 + l16) * d.ldkd + 4 * g;
+#pragma unroll
+    for (int ks = 0; ks < KX; ++ks) a1[ks] = ld4(w1 + 16 * ks);
+#pragma unroll
+    for (int j = 0; j < 9 * NT1; ++j) a2[j] = ld4(w2 + (j / NT1) * CM + 16 * (j % NT1));
+#pragma unroll
+    for (int j = 0; j < NTW3; ++j) {
+#pragma unroll
+      for (int ks = 0; ks < NT1; ++ks) a3[j][ks] = ld4(w3 + (int64_t)j * NW * 16 * a.ldk3 + 16 * ks);
+#pragma unroll
+      for (int ks = 0; ks < KX; ++ks) ad[j][ks] = ld4(wd + (int64_t)j * NW * 16 * d.ldkd + 16 * ks);
+    }
+  }
+  for (int i = tid; i < CM; i += 64 * NW) {
+    vs[i] = a.s1[(int64_t)c * CM + i];
+    vs[CM + i] = a.t1[(int64_t)c * CM + i];
+    vs[2 * CM + i] = a.s2[(int64_t)c * CM + i];
+    vs[3 * CM + i] = a.t2[(int64_t)c * CM + i];
+  }
+  for (int i = tid; i < CO; i += 64 * NW) {
+    vs[4 * CM + i] = a.s3[(int64_t)c * CO + i];
+    vs[4 * CM + CO + i] = a.t3[(int64_t)c * CO + i];
+    vs[4 * CM + 2 * CO + i] = d.sd[(int64_t)c * CO + i];
+    vs[4 * CM + 3 * CO + i] = d.td[(int64_t)c * CO + i];
+  }
+  for (int i = tid; i < G::RI * 2 * CM; i += 64 * NW) {   // m1's zero halo columns (conv1 never writes them)
+    const int r = i / (2 * CM), side = (i / CM) & 1, ch = i % CM;
+    m1[(r * TW + (side ? W + 1 : 0)) * LM + ch] = 0.f;
+  }
+  const float* s1 = vs;
+  const float* t1 = vs + CM;
+  const float* s2 = vs + 2 * CM;
+  const float* t2 = vs + 3 * CM;
+  const float* s3 = vs + 4 * CM;
+  const float* t3 = vs + 4 * CM + CO;
+  const float* sdv = vs + 4 * CM + 2 * CO;
+  const float* tdv = vs + 4 * CM + 3 * CO;
+
+  float4 bx[KX];
+  auto load_x = [&](int u, int pt) {   // conv1 input tile pt of unit u (a clamped in-image row outside the image)
+    const int n = u / G::BANDS, r0 = (u - n * G::BANDS) * R;
+    const int p = pt * 16 + l16, pr = p / W, pc = p - pr * W;
+    const int row = min(max(S * r0 - 1 + pr, 0), H - 1);
+    const float* xp = a.x + (((int64_t)c * a.N + n) * H * W + (int64_t)row * W + pc) * CX + 4 * g;
+#pragma unroll
+    for (int ks = 0; ks < KX; ++ks) bx[ks] = ld4(xp + 16 * ks);
+  };
+  if (pg1 < G::PT1) load_x(u_lo, pg1);
+  __syncthreads();
+
+  for (int u = u_lo; u < u_hi; ++u) {
+    const int n = u / G::BANDS, r0 = (u - n * G::BANDS) * R;
+    const float* xi = a.x + ((int64_t)c * a.N + n) * H * W * CX;
+    float* yo = a.out + (((int64_t)c * a.N + n) * G::HO + r0) * WO * CO;
+
+    // ---- conv1 + bn1 + relu on input rows S·r0−1 .. S·(r0+R−1)+1 → m1 ----
+    for (int pt = pg1; pt < G::PT1; pt += PS1) {
+      float4 cur[KX];
+#pragma unroll
+      for (int ks = 0; ks < KX; ++ks) cur[ks] = bx[ks];
+      if (pt + PS1 < G::PT1) load_x(u, pt + PS1);
+      else if (u + 1 < u_hi) load_x(u + 1, pg1);
+      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (KX % 2 == 0) {
+#pragma unroll
+        for (int ks = 0; ks < KX; ks += 2) mma4x2(a1[ks], cur[ks], acc0, a1[ks + 1], cur[ks + 1], acc1);
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < KX; ++ks) acc0 = mma4(a1[ks], cur[ks], acc0);
+      }
+      const int p = pt * 16 + l16, pr = p / W, pc = p - pr * W;
+      const int row = S * r0 - 1 + pr;
+      const bool inside = row >= 0 && row < H;
+      const int ch = nt1 * 16 + 4 * g;
+      float4 v;
+      v.x = inside ? fmaxf((acc0[0] + acc1[0]) * s1[ch] + t1[ch], 0.f) : 0.f;
+      v.y = inside ? fmaxf((acc0[1] + acc1[1]) * s1[ch + 1] + t1[ch + 1], 0.f) : 0.f;
+      v.z = inside ? fmaxf((acc0[2] + acc1[2]) * s1[ch + 2] + t1[ch + 2], 0.f) : 0.f;
+      v.w = inside ? fmaxf((acc0[3] + acc1[3]) * s1[ch + 3] + t1[ch + 3], 0.f) : 0.f;
+      *reinterpret_cast<float4*>(m1 + (pr * TW + pc + 1) * LM + ch) = v;
+    }
+    __syncthreads();
+
+    // ---- conv2 (3×3, stride S) + bn2 + relu → m2 ----
+    for (int pt = pg1; pt < G::PT2; pt += 2 * PS1) {
+      const float* mp[2];
+      int q[2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        q[h] = (pt + h * PS1) * 16 + l16;
+        const int orow = q[h] / WO, ocol = q[h] - orow * WO;
+        mp[h] = m1 + (S * orow * TW + S * ocol) * LM + 4 * g;
+      }
+      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int mo = ((tap / 3) * TW + tap % 3) * LM;
+#pragma unroll
+        for (int cc = 0; cc < NT1; ++cc)
+          mma4x2(a2[tap * NT1 + cc], ld4(mp[0] + mo + 16 * cc), acc0, a2[tap * NT1 + cc], ld4(mp[1] + mo + 16 * cc),
+                 acc1);
+      }
+      const int c0 = nt1 * 16 + 4 * g;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const f32x4 acc = h ? acc1 : acc0;
+        float4 v;
+        v.x = fmaxf(acc[0] * s2[c0] + t2[c0], 0.f);
+        v.y = fmaxf(acc[1] * s2[c0 + 1] + t2[c0 + 1], 0.f);
+        v.z = fmaxf(acc[2] * s2[c0 + 2] + t2[c0 + 2], 0.f);
+        v.w = fmaxf(acc[3] * s2[c0 + 3] + t2[c0 + 3], 0.f);
+        *reinterpret_cast<float4*>(m2 + q[h] * LM + c0) = v;
+      }
+    }
+    __syncthreads();
+
+    // ---- conv3 + bn3 and the stride-S projection + bn_d, summed, relu → y ----
+#pragma unroll
+    for (int j = 0; j < NTW3; ++j) {
+      const int c0 = (nt3 + j * NW) * 16 + 4 * g;
+      for (int pt = pg3; pt < G::PT2; pt += 2 * PS3) {
+        int q[2];
+        float4 xs[2][KX];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          q[h] = (pt + h * PS3) * 16 + l16;
+          const int orow = q[h] / WO, ocol = q[h] - orow * WO;
+          const float* xp = xi + ((int64_t)S * (r0 + orow) * W + S * ocol) * CX + 4 * g;
+#pragma unroll
+          for (int ks = 0; ks < KX; ++ks) xs[h][ks] = ld4(xp + 16 * ks);   // early: hides under conv3's MFMAs
+        }
+        f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+        f32x4 dac0 = {0.f, 0.f, 0.f, 0.f}, dac1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < NT1; ++ks)
+          mma4x2(a3[j][ks], ld4(m2 + q[0] * LM + 16 * ks + 4 * g), acc0, a3[j][ks],
+                 ld4(m2 + q[1] * LM + 16 * ks + 4 * g), acc1);
+#pragma unroll
+        for (int ks = 0; ks < KX; ++ks) mma4x2(ad[j][ks], xs[0][ks], dac0, ad[j][ks], xs[1][ks], dac1);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const f32x4 acc = h ? acc1 : acc0;
+          const f32x4 dac = h ? dac1 : dac0;
+          float4 v;
+          v.x = fmaxf(acc[0] * s3[c0] + t3[c0] + dac[0] * sdv[c0] + tdv[c0], 0.f);
+          v.y = fmaxf(acc[1] * s3[c0 + 1] + t3[c0 + 1] + dac[1] * sdv[c0 + 1] + tdv[c0 + 1], 0.f);
+          v.z = fmaxf(acc[2] * s3[c0 + 2] + t3[c0 + 2] + dac[2] * sdv[c0 + 2] + tdv[c0 + 2], 0.f);
+          v.w = fmaxf(acc[3] * s3[c0 + 3] + t3[c0 + 3] + dac[3] * sdv[c0 + 3] + tdv[c0 + 3], 0.f);
+          *reinterpret_cast<float4*>(yo + (int64_t)q[h] * CO + c0) = v;
+        }
+      }
+    }
+    __syncthreads();   // m1 / m2 are rewritten by the next unit
+  }
+}
+
+template <int CX, int CM, int HW, int S, int R>
+static int launch_ds(DArgs d, int C, hipStream_t stream) {
+  using G = GeoD<CX, CM, HW, S, R>;
+  const size_t smem = (size_t)G::FLOATS * 4;
+  if (smem > 160 * 1024) return -5;
+  const int units = d.b.N * G::BANDS;
+  const int per_model = std::max(1, std::min(units, (512 + C - 1) / C));
+  d.b.units_per_wg = (units + per_model - 1) / per_model;
+  const int gx = (units + d.b.units_per_wg - 1) / d.b.units_per_wg;
+  auto kern = bneck_ds_eval_kernel<CX, CM, HW, S, R>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  hipLaunchKernelGGL(kern, dim3(gx, C), dim3(512), smem, stream, d);
+  return (int)hipGetLastError();
+}
+
+// ---- stage-3 bottleneck (64-wide, 8×8): one wave per SIMD, every weight in registers ----
+// The 64-wide stage's weights (W1 64×256, W2 64×576, W3 256×64: 272 KB fp32) fit neither LDS nor the 2-waves-per-SIMD
+// register budget, but split over FOUR waves (wave w owns conv1 / conv2 output tile w and conv3 output tiles
+// w + 4j) they are 68 float4 = 272 VGPRs a wave: one 4-wave workgroup per CU, one wave per SIMD with the 512-entry
+// register file. A unit is one 8×8 image: its x (64 px × 256 ch, 64 KB) is staged in LDS from registers loaded
+// during the PREVIOUS image, so HBM reads overlap the MFMAs and the residual comes from LDS; four pixel tiles per
+// wave give four independent accumulator chains (the 40-cycle MFMA dependency hides behind the other three).
+template <int CM>
+struct Geo3 {
+  static constexpr int CIN = 4 * CM, HW = 8, P = HW * HW, TW = HW + 2, NT1 = CM / 16, NT3 = CIN / 16;
+  static constexpr int LX = CIN + 4, LM = CM + 4;
+  static constexpr int XF = P * LX, M1F = TW * TW * LM, M2F = P * LM;
+  static constexpr int FLOATS = 4 * CM + 2 * CIN + XF + M1F + M2F;
+  static constexpr int PF = P * CIN / 4 / 256;   // x float4s per thread
+};
+
+template <int CM>
+__global__ __launch_bounds__(256, 1) void bneck3_eval_kernel(BArgs a) {
+  using G = Geo3<CM>;
+  constexpr int CIN = G::CIN, HW = G::HW, P = G::P, TW = G::TW, LX = G::LX, LM = G::LM;
+  constexpr int NW = 4, NT1 = G::NT1, NTW3 = G::NT3 / NW, PT = P / 16;
+  static_assert(NT1 == NW && G::NT3 % NW == 0 && PT == 4 && (P * CIN / 4) % 256 == 0, "one tile a wave");
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* vs = sm;                          // s1 t1 s2 t2 [CM], s3 t3 [CIN]
+  float* xs = vs + 4 * CM + 2 * CIN;       // [P][LX]
+  float* m1 = xs + G::XF;                  // [TW][TW][LM], zero ring
+  float* m2 = m1 + G::M1F;                 // [P][LM]
+  const int c = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4, l16 = lane & 15;
+  const int u_lo = blockIdx.x * a.units_per_wg;
+  if (u_lo >= a.N) return;   // uniform: whole workgroup
+  const int u_hi = min(a.N, u_lo + a.units_per_wg);
+
+  const float* pk = a.wpk + (int64_t)c * a.wpk_ld;
+  float4 a1[CIN / 16], a2[9 * NT1], a3[NTW3][NT1];
+  {
+    const float* w1 = pk + a.off1 + (int64_t)(wid * 16 + l16) * a.ldk1 + 4 * g;
+    const float* w2 = pk + a.off2 + (int64_t)(wid * 16 + l16) * a.ldk2 + 4 * g;
+    const float* w3 = pk + a.off3 + (int64_t)(wid * 16 + l16) * a.ldk3 + 4 * g;
+#pragma unroll
+    for (int ks = 0; ks < CIN / 16; ++ks) a1[ks] = ld4(w1 + 16 * ks);
+#pragma unroll
+    for (int j = 0; j < 9 * NT1; ++j) a2[j] = ld4(w2 + (j / NT1) * CM + 16 * (j % NT1));
+#pragma unroll
+    for (int j = 0; j < NTW3; ++j)
+#pragma unroll
+      for (int ks = 0; ks < NT1; ++ks) a3[j][ks] = ld4(w3 + (int64_t)j * NW * 16 * a.ldk3 + 16 * ks);
+  }
+  for (int i = tid; i < CM; i += 256) {
+    vs[i] = a.s1[(int64_t)c * CM + i];
+    vs[CM + i] = a.t1[(int64_t)c * CM + i];
+    vs[2 * CM + i] = a.s2[(int64_t)c * CM + i];
+    vs[3 * CM + i] = a.t2[(int64_t)c * CM + i];
+  }
+  for (int i = tid; i < CIN; i += 256) {
+    vs[4 * CM + i] = a.s3[(int64_t)c * CIN + i];
+    vs[4 * CM + CIN + i] = a.t3[(int64_t)c * CIN + i];
+  }
+  for (int i = tid; i < G::M1F; i += 256) m1[i] = 0.f;   // the zero ring (conv1 rewrites the interior)
+  const float* s1 = vs;
+  const float* t1 = vs + CM;
+  const float* s2 = vs + 2 * CM;
+  const float* t2 = vs + 3 * CM;
+  const float* s3 = vs + 4 * CM;
+  const float* t3 = vs + 4 * CM + CIN;
+
+  float4 pf[G::PF];   // float4 f = tid + 256·i of an image: pixel f / (CIN/4), channels 4·(f mod CIN/4)
+  auto load_img = [&](int n) {
+    const float* xi = a.x + ((int64_t)c * a.N + n) * P * CIN;
+#pragma unroll
+    for (int i = 0; i < G::PF; ++i) pf[i] = ld4(xi + 4 * (int64_t)(tid + 256 * i));
+  };
+  load_img(u_lo);
+  __syncthreads();
+
+  for (int n = u_lo; n < u_hi; ++n) {
+#pragma unroll
+    for (int i = 0; i < G::PF; ++i) {
+      const int f = tid + 256 * i;
+      *reinterpret_cast<float4*>(xs + (f / (CIN / 4)) * LX + 4 * (f % (CIN / 4))) = pf[i];
+    }
+    __syncthreads();
+    if (n + 1 < u_hi) load_img(n + 1);   // in flight for the whole image
+
+    // ---- conv1 + bn1 + relu → m1 interior: output tile `wid`, all four pixel tiles ----
+    {
+      f32x4 acc[PT];
+#pragma unroll
+      for (int t = 0; t < PT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const float* xp = xs + l16 * LX + 4 * g;
+#pragma unroll
+      for (int ks = 0; ks < CIN / 16; ++ks)
+#pragma unroll
+        for (int t = 0; t < PT; ++t) acc[t] = mma4(a1[ks], ld4(xp + 16 * t * LX + 16 * ks), acc[t]);
+      const int ch = wid * 16 + 4 * g;
+#pragma unroll
+      for (int t = 0; t < PT; ++t) {
+        const int p = 16 * t + l16, r = p / HW, col = p % HW;
+        float4 v;
+        v.x = fmaxf(acc[t][0] * s1[ch] + t1[ch], 0.f);
+        v.y = fmaxf(acc[t][1] * s1[ch + 1] + t1[ch + 1], 0.f);
+        v.z = fmaxf(acc[t][2] * s1[ch + 2] + t1[ch + 2], 0.f);
+        v.w = fmaxf(acc[t][3] * s1[ch + 3] + t1[ch + 3], 0.f);
+        *reinterpret_cast<float4*>(m1 + ((r + 1) * TW + col + 1) * LM + ch) = v;
+      }
+    }
+    __syncthreads();
+
+    // ---- conv2 (3×3) + bn2 + relu → m2 ----
+    {
+      f32x4 acc[PT];
+#pragma unroll
+      for (int t = 0; t < PT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const float* mp[PT];
+#pragma unroll
+      for (int t = 0; t < PT; ++t) {
+        const int p = 16 * t + l16, r = p / HW, col = p % HW;
+        mp[t] = m1 + (r * TW + col) * LM + 4 * g;
+      }
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int mo = ((tap / 3) * TW + tap % 3) * LM;
+#pragma unroll
+        for (int cc = 0; cc < NT1; ++cc)
+#pragma unroll
+          for (int t = 0; t < PT; ++t) acc[t] = mma4(a2[tap * NT1 + cc], ld4(mp[t] + mo + 16 * cc), acc[t]);
+      }
+      const int ch = wid * 16 + 4 * g;
+#pragma unroll
+      for (int t = 0; t < PT; ++t) {
+        float4 v;
+        v.x = fmaxf(acc[t][0] * s2[ch] + t2[ch], 0.f);
+        v.y = fmaxf(acc[t][1] * s2[ch + 1] + t2[ch + 1], 0.f);
+        v.z = fmaxf(acc[t][2] * s2[ch + 2] + t2[ch + 2], 0.f);
+        v.w = fmaxf(acc[t][3] * s2[ch + 3] + t2[ch + 3], 0.f);
+        *reinterpret_cast<float4*>(m2 + (16 * t + l16) * LM + ch) = v;
+      }
+    }
+    __syncthreads();
+
+    // ---- conv3 + bn3 + residual (from the staged x) + relu → y: output tiles wid + 4j ----
+    float* yo = a.out + ((int64_t)c * a.N + n) * P * CIN;
+#pragma unroll
+    for (int j = 0; j < NTW3; ++j) {
+      const int c0 = (wid + NW * j) * 16 + 4 * g;
+      f32x4 acc[PT];
+#pragma unroll
+      for (int t = 0; t < PT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < NT1; ++ks)
+#pragma unroll
+        for (int t = 0; t < PT; ++t)
+          acc[t] = mma4(a3[j][ks], ld4(m2 + (16 * t + l16) * LM + 16 * ks + 4 * g), acc[t]);
+#pragma unroll
+      for (int t = 0; t < PT; ++t) {
+        const int p = 16 * t + l16;
+        const float4 res = ld4(xs + p * LX + c0);
+        float4 v;
+        v.x = fmaxf(acc[t][0] * s3[c0] + t3[c0] + res.x, 0.f);
+        v.y = fmaxf(acc[t][1] * s3[c0 + 1] + t3[c0 + 1] + res.y, 0.f);
+        v.z = fmaxf(acc[t][2] * s3[c0 + 2] + t3[c0 + 2] + res.z, 0.f);
+        v.w = fmaxf(acc[t][3] * s3[c0 + 3] + t3[c0 + 3] + res.w, 0.f);
+        *reinterpret_cast<float4*>(yo + (int64_t)p * CIN + c0) = v;
+      }
+    }
+    __syncthreads();   // xs / m1 / m2 are rewritten by the next image
+  }
+}
+
+template <int CM>
+static int launch3(BArgs a, int C, hipStream_t stream) {
+  using G = Geo3<CM>;
+  const size_t smem = (size_t)G::FLOATS * 4;
+  if (smem > 160 * 1024) return -5;
+  // one workgroup per CU: ~512 workgroups over all models, each looping over a contiguous run of one model's images
+  const int per_model = std::max(1, std::min(a.N, (512 + C - 1) / C));
+  a.units_per_wg = (a.N + per_model - 1) / per_model;
+  const int gx = (a.N + a.units_per_wg - 1) / a.units_per_wg;
+  auto kern = bneck3_eval_kernel<CM>;
+  (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  hipLaunchKernelGGL(kern, dim3(gx, C), dim3(256), smem, stream, a);
+  return (int)hipGetLastError();
+}
+
 }  // namespace infer
 
 // y = relu(bn3(conv3(relu(bn2(conv2(relu(bn1(conv1(x)))))))) + x) for a stride-1, downsample-free bottleneck of
-// C models at once; mid width cm ∈ {16, 32} at hw = 32 / 16 (the ResNet-56/110 CIFAR stages 1 and 2). Returns -2
-// for a geometry without an instantiation (the caller keeps the unfused forward).
+// C models at once; mid width cm ∈ {16, 32, 64} at hw = 32 / 16 / 8 (the ResNet-56/110 CIFAR stages 1-3). Returns
+// -2 for a geometry without an instantiation (the caller keeps the unfused forward).
 FA_EXPORT int fa_bneck_eval_f32(const float* x, float* out, const float* wpk, int64_t wpk_ld, int64_t off1, int ldk1,
                                 int64_t off2, int ldk2, int64_t off3, int ldk3, const float* s1, const float* t1,
                                 const float* s2, const float* t2, const float* s3, const float* t3, int C, int N, int H,
@@ -552,6 +957,7 @@ FA_EXPORT int fa_bneck_eval_f32(const float* x, float* out, const float* wpk, in
       if (variant == 7) return infer::launch_rw<16, 32, 8, false, true, 8>(a, C, stream);
       return infer::launch_rw<16, 32, 8, true, false, 8>(a, C, stream);
     }
+    if (cm == 64 && H == 8 && variant != 8) return infer::launch3<64>(a, C, stream);
     if (cm == 32 && H == 16) {
       if (variant == 4) return infer::launch_rw<32, 16, 8, false, false, 8>(a, C, stream);
       if (variant >= 6) return infer::launch_rw<32, 16, 8, false, true, 8>(a, C, stream);
@@ -568,5 +974,25 @@ FA_EXPORT int fa_bneck_eval_f32(const float* x, float* out, const float* wpk, in
     if (variant == 2) return infer::launch<32, 16, 16, 8>(a, C, stream);
     return infer::launch<32, 16, 8, 8>(a, C, stream);
   }
+  return -2;
+}
+
+// The stage-entry bottleneck (projection shortcut, stride on the 3×3) of C models at once: x [C][N][H][W][cx] →
+// out [C][N][H/stride][W/stride][4·cm]. Instantiated for the CIFAR ResNet-56/110 stage-1 (cx 16, cm 16, 32², stride
+// 1) and stage-2 (cx 64, cm 32, 32², stride 2) entries; -2 for any other geometry (the caller keeps the unfused
+// forward — the stage-3 entry's 64-wide weights do not fit the register-resident scheme).
+FA_EXPORT int fa_bneck_ds_eval_f32(const float* x, float* out, const float* wpk, int64_t wpk_ld, int64_t off1, int ldk1,
+                                   int64_t off2, int ldk2, int64_t off3, int ldk3, int64_t offd, int ldkd,
+                                   const float* s1, const float* t1, const float* s2, const float* t2, const float* s3,
+                                   const float* t3, const float* sd, const float* td, int C, int N, int H, int W,
+                                   int cx, int cm, int stride, hipStream_t stream) {
+  if (C <= 0 || N <= 0 || H != W || C > 65535) return (int)hipErrorInvalidValue;
+  if (((off1 | off2 | off3 | offd | ldk1 | ldk2 | ldk3 | ldkd | wpk_ld) & 3) != 0 ||
+      (reinterpret_cast<uintptr_t>(wpk) & 15) != 0)
+    return -2;
+  infer::DArgs d = {{x, out, wpk, wpk_ld, off1, off2, off3, ldk1, ldk2, ldk3, s1, t1, s2, t2, s3, t3, N, 1}, offd, ldkd,
+                    sd, td};
+  if (cx == 16 && cm == 16 && H == 32 && stride == 1) return infer::launch_ds<16, 16, 32, 1, 8>(d, C, stream);
+  if (cx == 64 && cm == 32 && H == 32 && stride == 2) return infer::launch_ds<64, 32, 32, 2, 8>(d, C, stream);
   return -2;
 }

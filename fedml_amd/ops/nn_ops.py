@@ -342,6 +342,23 @@ def bneck_eval(x, out, wpk, wpk_ld, convs, vecs, C, N, H, W, cm):
     return True
 
 
+def bneck_ds_eval(x, out, wpk, wpk_ld, convs, vecs, C, N, H, W, cx, cm, stride):
+    """Inference stage-entry bottleneck as ONE kernel (ops/csrc/infer_kernels.hip): out = relu(bn3(conv3(m2)) +
+    bn_d(conv_d(x))) with m2 = relu(bn2(conv2_stride(relu(bn1(conv1(x)))))) — the projection-shortcut first block of
+    a stage. ``convs``: (off_f, ldk) of conv1, conv2, conv3 and the shortcut conv; ``vecs``: the (scale, shift)
+    [C, ch] pairs of bn1, bn2, bn3, bn_d. Returns False when no instantiation takes the geometry."""
+    (o1, l1), (o2, l2), (o3, l3), (od, ld) = convs
+    (s1, t1), (s2, t2), (s3, t3), (sd, td) = vecs
+    rc = _fn("fa_bneck_ds_eval_f32")(_pr(x), _p(out), _pr(wpk), _i64(wpk_ld), _i64(o1), _i(l1), _i64(o2), _i(l2),
+                                     _i64(o3), _i(l3), _i64(od), _i(ld), _pr(s1), _pr(t1), _pr(s2), _pr(t2), _pr(s3),
+                                     _pr(t3), _pr(sd), _pr(td), _i(C), _i(N), _i(H), _i(W), _i(cx), _i(cm), _i(stride),
+                                     _stream(x))
+    if rc == -2:
+        return False
+    _check(rc, "fa_bneck_ds_eval_f32")
+    return True
+
+
 def block_out(y, s, t, r, rs, rt, out, C, per_client, Ch, nimg=None, per_img=0):
     """out = relu(y·s + t + R) over the first nimg[c] images (per_img elements each) of every client."""
     rc = _fnp("fa_block_out", y)(_p(y), _p(s), _p(t), _p(r), _p(rs), _p(rt), _p(out), _i(C), _i64(per_client), _i(Ch),

@@ -582,7 +582,8 @@ class NativeResNetStep:
 
     def _fused_eval_ok(self, b) -> bool:
         """Inference (forward_eval) runs this block as ONE fused kernel (nn_ops.bneck_eval): fp32, a stride-1
-        bottleneck without downsample of mid width 16 at 32² or 32 at 16² (CIFAR ResNet-56/110 stages 1-2).
+        bottleneck without downsample of mid width 16 at 32², 32 at 16² or 64 at 8² (CIFAR ResNet-56/110 stages
+        1-3).
         FEDML_AMD_FUSED_EVAL=0 keeps the training kernels for inference too."""
         if b is None or getattr(self, "_training", True) or self.dtype != torch.float32 or not self.use_fused_eval:
             return False
@@ -593,14 +594,30 @@ class NativeResNetStep:
         return (c1.k == 1 and c1.stride == 1 and c2.k == 3 and c2.stride == 1 and c2.pad == 1 and c3.k == 1
                 and c3.stride == 1 and c1.cin == 4 * cm and c1.cin_pad == c1.cin and c1.cout == cm
                 and c2.cin == cm and c2.cin_pad == cm and c3.cin == cm and c3.cin_pad == cm and c3.cout == 4 * cm
-                and c1.H == c1.W and (cm, c1.H) in ((16, 32), (32, 16)))
+                and c1.H == c1.W and (cm, c1.H) in ((16, 32), (32, 16), (64, 8)))
+
+    def _fused_ds_eval_ok(self, b) -> bool:
+        """Inference runs this stage-entry block (projection shortcut, stride on the 3×3) as ONE fused kernel
+        (nn_ops.bneck_ds_eval): the CIFAR ResNet-56/110 stage-1 and stage-2 entries."""
+        if b is None or getattr(self, "_training", True) or self.dtype != torch.float32 or not self.use_fused_eval:
+            return False
+        if b.ds_conv is None or len(b.convs) != 3:
+            return False
+        c1, c2, c3 = b.convs
+        d = b.ds_conv
+        cm, cx = c2.cout, c1.cin
+        return (c1.k == 1 and c1.stride == 1 and c2.k == 3 and c2.pad == 1 and c3.k == 1 and c3.stride == 1
+                and d.k == 1 and d.pad == 0 and d.stride == c2.stride and c1.cin_pad == cx and d.cin == cx
+                and d.cin_pad == cx and c1.cout == cm and c2.cin_pad == cm and c3.cin_pad == cm
+                and c3.cout == 4 * cm and d.cout == 4 * cm and c1.H == c1.W
+                and (cx, cm, c1.H, c2.stride) in ((16, 16, 32, 1), (64, 32, 32, 2)))
 
     def _pbout_ok(self, b, nb) -> bool:
         """Block ``b``'s output is formed in the operand load of the next block's first conv (conv_fwd_pbout: 1×1,
         stride 1) and written once from there instead of by its own block-output pass. Its other readers run after
         that conv and read the stored output: the next block's output pass (identity shortcut) or its downsample
         conv (stage transitions), and the backward (act_in)."""
-        if not self.use_pbout or nb is None or b.ry or self._fused_eval_ok(nb):
+        if not self.use_pbout or nb is None or b.ry or self._fused_eval_ok(nb) or self._fused_ds_eval_ok(nb):
             return False
         cv = nb.convs[0]
         return cv.k == 1 and cv.stride == 1 and cv.pad == 0 and cv.cin == cv.cin_pad
@@ -1053,6 +1070,17 @@ class NativeResNetStep:
                 c1 = b.convs[0]
                 if nn_ops.bneck_eval(act_in, b.out, pk, self.packed_ld, [(cv.off_f, cv.ldk) for cv in b.convs], vec,
                                      C, N, c1.H, c1.W, b.convs[1].cout):
+                    act_in = b.out
+                    continue
+            if pend is None and self._fused_ds_eval_ok(b):
+                bns = list(b.bns) + [b.ds_bn]
+                for bn in bns:
+                    self._bn_fwd(bn, N, 0, arena, active)
+                vec = [(self.bn_vec[bn.key][0], self.bn_vec[bn.key][1]) for bn in bns]
+                c1, c2 = b.convs[0], b.convs[1]
+                if nn_ops.bneck_ds_eval(act_in, b.out, self.packed.view(-1), self.packed_ld,
+                                        [(cv.off_f, cv.ldk) for cv in list(b.convs) + [b.ds_conv]], vec, C, N, c1.H,
+                                        c1.W, c1.cin, c2.cout, c2.stride):
                     act_in = b.out
                     continue
             for j, (cv, bn) in enumerate(zip(b.convs, b.bns)):

@@ -38,7 +38,7 @@ def main():
     ms = 1000 * (time.perf_counter() - t0) / a.iters
     print(json.dumps({"metric": "forward_eval ms per call", "value": round(ms, 3), "models": a.models,
                       "images": a.images, "depth": a.depth, "fused": os.environ.get("FEDML_AMD_FUSED_EVAL", "1"),
-                      "variant": os.environ.get("FEDML_AMD_BNECK_EVAL_VARIANT", "1"),
+                      "variant": os.environ.get("FEDML_AMD_BNECK_EVAL_VARIANT", "5"),
                       "us_per_image": round(1000 * ms / (a.models * a.images), 3)}), flush=True)
 
 

@@ -1,4 +1,5 @@
-"""The fused inference bottleneck (``ops/csrc/infer_kernels.hip``, one kernel per stride-1 bottleneck of stages 1-2)
+"""The fused inference bottlenecks (``ops/csrc/infer_kernels.hip``: one kernel per stride-1 bottleneck of stages 1-3
+and per stage-1 / stage-2 entry block with its projection shortcut)
 against the unfused inference forward of the same native step (the training kernels with BatchNorm folded) and
 against torch fp32 eval — for several models at once with their own running statistics."""
 import copy
@@ -40,7 +41,8 @@ def test_fused_eval_matches_unfused_and_torch(depth, C, N):
     fused = NativeResNetStep(base, layout, C, "cuda")
     assert fused.use_fused_eval
     got = fused.forward_eval(arena, x)
-    assert sum(fused._fused_eval_ok(b) for b in fused.blocks) == (10 if depth == 56 else 22)
+    assert sum(fused._fused_eval_ok(b) for b in fused.blocks) == (15 if depth == 56 else 33)   # stages 1-3
+    assert sum(fused._fused_ds_eval_ok(b) for b in fused.blocks) == 2     # the stage-1 and stage-2 entries
     plain = NativeResNetStep(base, layout, C, "cuda")
     plain.use_fused_eval = False
     ref_native = plain.forward_eval(arena, x)
