@@ -928,6 +928,59 @@ static int launch3(BArgs a, int C, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
+// ---- stem: NCHW image → 3×3 conv (≤ 4 input channels, 16 outputs) → BN → ReLU → NHWC ----
+// Replaces the layout pass, the stem conv (a 16-output GEMM that cannot fill a tile) and the BN/ReLU pass of the
+// training path with one memory-bound kernel. A workgroup takes a band of 8 rows of one 32-wide image: the input
+// rows (+1 halo row above and below, zero columns left and right) are staged in LDS as [row][col][4 channels];
+// MFMA K-step t is tap t (lane group g = input channel g, the 4th channel zero), so each 16-pixel × 16-channel
+// tile is 9 MFMAs, four tiles per wave interleaved.
+__global__ __launch_bounds__(256) void stem_eval_kernel(const float* __restrict__ x, float* __restrict__ out,
+                                                        const float* __restrict__ wpk, int64_t wpk_ld, int64_t off,
+                                                        int ldk, int cin_pad, const float* __restrict__ s,
+                                                        const float* __restrict__ t, int N, int H, int cin) {
+  constexpr int W = 32, R = 8, TW = W + 2, CO = 16, PT = R * W / 16 / 4;   // 4 pixel tiles a wave
+  __shared__ __attribute__((aligned(16))) float xs[(R + 2) * TW * 4];
+  const int c = blockIdx.y;
+  const int bands = H / R;
+  const int n = blockIdx.x / bands, r0 = (blockIdx.x - n * bands) * R;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4, l16 = lane & 15;
+  const float* xi = x + ((int64_t)c * N + n) * cin * H * W;
+  for (int i = tid; i < (R + 2) * TW * 4; i += 256) {
+    const int ch = i & 3, col = (i >> 2) % TW - 1, row = r0 - 1 + (i >> 2) / TW;
+    xs[i] = (ch < cin && col >= 0 && col < W && row >= 0 && row < H) ? xi[((int64_t)ch * H + row) * W + col] : 0.f;
+  }
+  float a[9];
+  const float* wp = wpk + (int64_t)c * wpk_ld + off + (int64_t)l16 * ldk + g;
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) a[tap] = g < cin ? wp[tap * cin_pad] : 0.f;
+  __syncthreads();
+  f32x4 acc[PT];
+#pragma unroll
+  for (int q = 0; q < PT; ++q) acc[q] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const int kh = tap / 3, kw = tap % 3;
+#pragma unroll
+    for (int q = 0; q < PT; ++q) {
+      const int p = (wid * PT + q) * 16 + l16, pr = p / W, pc = p % W;
+      acc[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[tap], xs[((pr + kh) * TW + pc + kw) * 4 + g], acc[q], 0, 0, 0);
+    }
+  }
+  const float* sv = s + (int64_t)c * CO + 4 * g;
+  const float* tv = t + (int64_t)c * CO + 4 * g;
+  float* yo = out + (((int64_t)c * N + n) * H + r0) * W * CO + 4 * g;
+#pragma unroll
+  for (int q = 0; q < PT; ++q) {
+    const int p = (wid * PT + q) * 16 + l16;
+    float4 v;
+    v.x = fmaxf(acc[q][0] * sv[0] + tv[0], 0.f);
+    v.y = fmaxf(acc[q][1] * sv[1] + tv[1], 0.f);
+    v.z = fmaxf(acc[q][2] * sv[2] + tv[2], 0.f);
+    v.w = fmaxf(acc[q][3] * sv[3] + tv[3], 0.f);
+    *reinterpret_cast<float4*>(yo + (int64_t)p * CO) = v;
+  }
+}
+
 }  // namespace infer
 
 // y = relu(bn3(conv3(relu(bn2(conv2(relu(bn1(conv1(x)))))))) + x) for a stride-1, downsample-free bottleneck of
@@ -995,4 +1048,17 @@ FA_EXPORT int fa_bneck_ds_eval_f32(const float* x, float* out, const float* wpk,
   if (cx == 16 && cm == 16 && H == 32 && stride == 1) return infer::launch_ds<16, 16, 32, 1, 8>(d, C, stream);
   if (cx == 64 && cm == 32 && H == 32 && stride == 2) return infer::launch_ds<64, 32, 32, 2, 8>(d, C, stream);
   return -2;
+}
+
+// relu(bn(conv3×3(x))) of the CIFAR stem for C models at once: x [C][N][cin][H][32] fp32 (NCHW, cin ≤ 4) →
+// out [C][N][H][32][16] (NHWC), BN folded (s, t [C][16]); weights from the packed forward layout (k = tap·cin_pad +
+// ci). -2 for any other geometry (the caller keeps the layout pass + conv + block-output path).
+FA_EXPORT int fa_stem_eval_f32(const float* x, float* out, const float* wpk, int64_t wpk_ld, int64_t off, int ldk,
+                               int cin_pad, const float* s, const float* t, int C, int N, int cin, int H, int W,
+                               int cout, hipStream_t stream) {
+  if (C <= 0 || N <= 0 || C > 65535) return (int)hipErrorInvalidValue;
+  if (W != 32 || H % 8 != 0 || cin > 4 || cin < 1 || cout != 16 || cin_pad < cin) return -2;
+  hipLaunchKernelGGL(infer::stem_eval_kernel, dim3(N * (H / 8), C), dim3(256), 0, stream, x, out, wpk, wpk_ld, off,
+                     ldk, cin_pad, s, t, N, H, cin);
+  return (int)hipGetLastError();
 }

@@ -342,6 +342,17 @@ def bneck_eval(x, out, wpk, wpk_ld, convs, vecs, C, N, H, W, cm):
     return True
 
 
+def stem_eval(x, out, wpk, wpk_ld, off, ldk, cin_pad, s, t, C, N, cin, H, W, cout):
+    """Inference stem as ONE kernel (ops/csrc/infer_kernels.hip): out (NHWC) = relu(bn(conv3×3(x))) straight from
+    the NCHW fp32 images x [C, N, cin, H, W] (cin ≤ 4, 16 outputs, W = 32). Returns False for other geometries."""
+    rc = _fn("fa_stem_eval_f32")(_pr(x), _p(out), _pr(wpk), _i64(wpk_ld), _i64(off), _i(ldk), _i(cin_pad), _pr(s),
+                                 _pr(t), _i(C), _i(N), _i(cin), _i(H), _i(W), _i(cout), _stream(x))
+    if rc == -2:
+        return False
+    _check(rc, "fa_stem_eval_f32")
+    return True
+
+
 def bneck_ds_eval(x, out, wpk, wpk_ld, convs, vecs, C, N, H, W, cx, cm, stride):
     """Inference stage-entry bottleneck as ONE kernel (ops/csrc/infer_kernels.hip): out = relu(bn3(conv3(m2)) +
     bn_d(conv_d(x))) with m2 = relu(bn2(conv2_stride(relu(bn1(conv1(x)))))) — the projection-shortcut first block of

@@ -596,6 +596,14 @@ class NativeResNetStep:
                 and c2.cin == cm and c2.cin_pad == cm and c3.cin == cm and c3.cin_pad == cm and c3.cout == 4 * cm
                 and c1.H == c1.W and (cm, c1.H) in ((16, 32), (32, 16), (64, 8)))
 
+    def _fused_stem_ok(self) -> bool:
+        """Inference runs the CIFAR stem (3×3, stride 1, ≤ 4 → 16 channels, 32-wide images) as one kernel."""
+        if getattr(self, "_training", True) or self.dtype != torch.float32 or not self.use_fused_eval:
+            return False
+        cv = self.stem[0]
+        return (cv.k == 3 and cv.stride == 1 and cv.pad == 1 and cv.cin <= 4 and cv.cout == 16 and cv.W == 32
+                and cv.H % 8 == 0)
+
     def _fused_ds_eval_ok(self, b) -> bool:
         """Inference runs this stage-entry block (projection shortcut, stride on the 3×3) as ONE fused kernel
         (nn_ops.bneck_ds_eval): the CIFAR ResNet-56/110 stage-1 and stage-2 entries."""
@@ -1046,16 +1054,25 @@ class NativeResNetStep:
         nn_ops.pack_weights(arena, self._segs, self._nseg, self.packed, self.packed_ld, C, self._pack_tiles,
                             self._pack_taps)
         st_conv, st_bn = self.stem
-        nn_ops.nchw_to_nhwc_pad(x.contiguous(), self.x_in, C * N, st_conv.cin, H * W, st_conv.cin_pad)
-
-        # ---------------- forward ----------------
-        self._fwd(st_conv, self.x_in, self.stem_y, None, st_bn, N)
-        self._bn_fwd(st_bn, N, st_conv.Ho * st_conv.Wo, arena, active)
-        v0 = self.bn_vec[st_bn.key]
-        self._flush(st_bn.key, "f")          # block_out reads the finalised rows
-        nn_ops.block_out(self.stem_y, v0[0], v0[1], None, None, None, self.stem_out, C,
-                         N * st_conv.Ho * st_conv.Wo * st_conv.cout, st_conv.cout, nimg=self._nimg,
-                         per_img=st_conv.Ho * st_conv.Wo * st_conv.cout)
+        x = x.contiguous()
+        fused_stem = False
+        if self._fused_stem_ok():
+            # inference: layout pass + stem conv + BN/ReLU as one kernel from the NCHW images
+            self._bn_fwd(st_bn, N, 0, arena, active)
+            v0 = self.bn_vec[st_bn.key]
+            fused_stem = nn_ops.stem_eval(x, self.stem_out, self.packed.view(-1), self.packed_ld, st_conv.off_f,
+                                          st_conv.ldk, st_conv.cin_pad, v0[0], v0[1], C, N, st_conv.cin, H, W,
+                                          st_conv.cout)
+        if not fused_stem:
+            nn_ops.nchw_to_nhwc_pad(x, self.x_in, C * N, st_conv.cin, H * W, st_conv.cin_pad)
+            # ---------------- forward ----------------
+            self._fwd(st_conv, self.x_in, self.stem_y, None, st_bn, N)
+            self._bn_fwd(st_bn, N, st_conv.Ho * st_conv.Wo, arena, active)
+            v0 = self.bn_vec[st_bn.key]
+            self._flush(st_bn.key, "f")          # block_out reads the finalised rows
+            nn_ops.block_out(self.stem_y, v0[0], v0[1], None, None, None, self.stem_out, C,
+                             N * st_conv.Ho * st_conv.Wo * st_conv.cout, st_conv.cout, nimg=self._nimg,
+                             per_img=st_conv.Ho * st_conv.Wo * st_conv.cout)
         act_in = self.stem_out
         pend = None    # (yp, s, t, res, rs, rt, bout) of a block output formed by the next block's first conv
         pend_keys = (None, None)   # its BNs (deferred finalisation: taken by that conv)
