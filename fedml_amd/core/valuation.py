@@ -102,7 +102,9 @@ class BatchedModelEvaluator:
             # copies of its first model, whose outputs are dropped
             arena = chunk if c == cm else torch.cat([chunk, chunk[:1].expand(cm - c, -1)])
             arena = arena.contiguous()
-            return [st.forward_eval(arena, x.unsqueeze(0).expand(cm, *x.shape))[:c].float() for x, _ in batches]
+            token = object()   # the batches after the first reuse this chunk's packed weights and folded BNs
+            return [st.forward_eval(arena, x.unsqueeze(0).expand(cm, *x.shape), models_token=token)[:c].float()
+                    for x, _ in batches]
         if self._batched_ok:
             try:
                 interp = self._interp(c)

@@ -265,8 +265,8 @@ __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast
 
 // NW = 8: one workgroup per CU; NW = 4 (smaller R): two per CU, so one workgroup's barrier waits overlap the
 // other's MFMAs. conv3 gives a wave NT3/NW channel tiles when the waves are fewer than CIN/16.
-template <int CM, int HW, int R, bool BAND, bool PIPE, int NW>
-__global__ __launch_bounds__(64 * NW, 2) void bneck_eval_rw_kernel(BArgs a) {   // ≥ 2 waves per SIMD
+template <int CM, int HW, int R, bool BAND, bool PIPE, int NW, int Q2>
+__global__ __launch_bounds__(64 * NW, NW == 4 && !BAND ? 3 : 2) void bneck_eval_rw_kernel(BArgs a) {   // waves per SIMD
   using G = GeoR<CM, HW, R, BAND, PIPE>;
   static_assert(!(BAND && PIPE), "the band is read by conv1 and conv3 of one unit");
   constexpr int CIN = G::CIN, H = G::H, W = G::W, TW = G::TW, LM = G::LM, NT1 = G::NT1, NT3 = G::NT3;
@@ -274,8 +274,8 @@ __global__ __launch_bounds__(64 * NW, 2) void bneck_eval_rw_kernel(BArgs a) {   
   constexpr int PS1 = NW / NT1, PS3 = NT3 >= NW ? 1 : NW / NT3;   // pixel-tile strides of conv1/conv2 and conv3
   constexpr int PF = (G::NF4 + 64 * NW - 1) / (64 * NW);          // BAND float4s per thread
   static_assert(NW % NT1 == 0 && (NW % NT3 == 0 || NT3 % NW == 0), "wave split");
-  static_assert(G::PT2 % (2 * PS1) == 0 && G::PT2 % (2 * PS3) == 0, "two pixel tiles per wave iteration");
-  static_assert((CIN / 16) % 2 == 0, "conv1 K split");
+  static_assert(G::PT2 % (Q2 * PS1) == 0 && G::PT2 % (2 * PS3) == 0, "Q2 / two pixel tiles per wave iteration");
+  static_assert((CIN / 16) % 2 == 0 && Q2 % 2 == 0, "conv1 K split; conv2 chains in pairs");
   extern __shared__ __attribute__((aligned(16))) float sm[];
   float* vs = sm;                          // s1 t1 s2 t2 [CM], s3 t3 [CIN]
   float* m1 = vs + 4 * CM + 2 * CIN;       // [NB][R+2][TW][LM]
@@ -390,33 +390,36 @@ __global__ __launch_bounds__(64 * NW, 2) void bneck_eval_rw_kernel(BArgs a) {   
 
   // ---- conv2 (3×3) + bn2 + relu: m1b → m2b, pixel tiles pt and pt + PS1 per iteration ----
   auto conv2 = [&](const float* m1b, float* m2b) {
-    for (int pt = pg1; pt < G::PT2; pt += 2 * PS1) {
-      const float* mp[2];
-      int p[2];
+    for (int pt = pg1; pt < G::PT2; pt += Q2 * PS1) {
+      const float* mp[Q2];
+      int p[Q2];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
+      for (int h = 0; h < Q2; ++h) {
         p[h] = (pt + h * PS1) * 16 + l16;
         const int pr = p[h] / W, pc = p[h] - pr * W;
         mp[h] = m1b + (pr * TW + pc) * LM + 4 * g;
       }
-      f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      f32x4 acc[Q2];
+#pragma unroll
+      for (int h = 0; h < Q2; ++h) acc[h] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         const int mo = ((tap / 3) * TW + tap % 3) * LM;
 #pragma unroll
         for (int cc = 0; cc < NT1; ++cc)
-          mma4x2(a2[tap * NT1 + cc], ld4(mp[0] + mo + 16 * cc), acc0, a2[tap * NT1 + cc], ld4(mp[1] + mo + 16 * cc),
-                 acc1);
+#pragma unroll
+          for (int h = 0; h < Q2; h += 2)
+            mma4x2(a2[tap * NT1 + cc], ld4(mp[h] + mo + 16 * cc), acc[h], a2[tap * NT1 + cc],
+                   ld4(mp[h + 1] + mo + 16 * cc), acc[h + 1]);
       }
       const int c0 = nt1 * 16 + 4 * g;
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const f32x4 acc = h ? acc1 : acc0;
+      for (int h = 0; h < Q2; ++h) {
         float4 v;
-        v.x = fmaxf(acc[0] * s2[c0] + t2[c0], 0.f);
-        v.y = fmaxf(acc[1] * s2[c0 + 1] + t2[c0 + 1], 0.f);
-        v.z = fmaxf(acc[2] * s2[c0 + 2] + t2[c0 + 2], 0.f);
-        v.w = fmaxf(acc[3] * s2[c0 + 3] + t2[c0 + 3], 0.f);
+        v.x = fmaxf(acc[h][0] * s2[c0] + t2[c0], 0.f);
+        v.y = fmaxf(acc[h][1] * s2[c0 + 1] + t2[c0 + 1], 0.f);
+        v.z = fmaxf(acc[h][2] * s2[c0 + 2] + t2[c0 + 2], 0.f);
+        v.w = fmaxf(acc[h][3] * s2[c0 + 3] + t2[c0 + 3], 0.f);
         *reinterpret_cast<float4*>(m2b + p[h] * LM + c0) = v;
       }
     }
@@ -488,7 +491,7 @@ __global__ __launch_bounds__(64 * NW, 2) void bneck_eval_rw_kernel(BArgs a) {   
   }
 }
 
-template <int CM, int HW, int R, bool BAND, bool PIPE, int NW>
+template <int CM, int HW, int R, bool BAND, bool PIPE, int NW, int Q2 = 2>
 static int launch_rw(BArgs a, int C, hipStream_t stream) {
   using G = GeoR<CM, HW, R, BAND, PIPE>;
   const size_t smem = (size_t)G::FLOATS * 4;
@@ -500,7 +503,7 @@ static int launch_rw(BArgs a, int C, hipStream_t stream) {
   const int per_model = std::max(1, std::min(units, (target + C - 1) / C));
   a.units_per_wg = (units + per_model - 1) / per_model;
   const int gx = (units + a.units_per_wg - 1) / a.units_per_wg;
-  auto kern = bneck_eval_rw_kernel<CM, HW, R, BAND, PIPE, NW>;
+  auto kern = bneck_eval_rw_kernel<CM, HW, R, BAND, PIPE, NW, Q2>;
   (void)hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
   hipLaunchKernelGGL(kern, dim3(gx, C), dim3(64 * NW), smem, stream, a);
   return (int)hipGetLastError();
@@ -1008,12 +1011,14 @@ FA_EXPORT int fa_bneck_eval_f32(const float* x, float* out, const float* wpk, in
       if (variant == 4) return infer::launch_rw<16, 32, 8, false, false, 8>(a, C, stream);
       if (variant == 6) return infer::launch_rw<16, 32, 4, true, false, 4>(a, C, stream);
       if (variant == 7) return infer::launch_rw<16, 32, 8, false, true, 8>(a, C, stream);
+      if (variant == 9) return infer::launch_rw<16, 32, 8, false, false, 4>(a, C, stream);
       return infer::launch_rw<16, 32, 8, true, false, 8>(a, C, stream);
     }
     if (cm == 64 && H == 8 && variant != 8) return infer::launch3<64>(a, C, stream);
     if (cm == 32 && H == 16) {
       if (variant == 4) return infer::launch_rw<32, 16, 8, false, false, 8>(a, C, stream);
-      if (variant >= 6) return infer::launch_rw<32, 16, 8, false, true, 8>(a, C, stream);
+      if (variant == 10) return infer::launch_rw<32, 16, 16, false, false, 8, 4>(a, C, stream);
+      if (variant == 6 || variant == 7) return infer::launch_rw<32, 16, 8, false, true, 8>(a, C, stream);
       return infer::launch_rw<32, 16, 16, false, false, 8>(a, C, stream);
     }
   }

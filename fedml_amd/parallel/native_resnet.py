@@ -677,6 +677,8 @@ class NativeResNetStep:
         fst = self.stat_views[bn.key][0]
         g, b, rm, rv, nbt = self._bn_offsets(bn)
         if not getattr(self, "_training", True):      # inference: running statistics, folded at once
+            if getattr(self, "_eval_reuse", False):     # same models as this geometry's last call: folded already
+                return
             nn_ops.bn_eval_fold(self.C, bn.ch, arena, g, b, rm, rv, bn.eps, v[0], v[1])
             return
 
@@ -1021,11 +1023,13 @@ class NativeResNetStep:
                 self._states[(N, H, W)] = self._snapshot()
 
     @torch.no_grad()
-    def forward_eval(self, arena, x):
+    def forward_eval(self, arena, x, models_token=None):
         """Inference of C models at once: x [C, N, Cin, H, W] fp32 (each model's own batch; the same images
         expanded for a model sweep) → logits [C, N, classes] fp32. BatchNorm in eval mode (running statistics of
         each model's arena row, ``bn_eval_fold``), same kernels as the training forward. Zeroes this object's
-        pivots (stored outputs are then uncentred): give inference its own ``NativeResNetStep``."""
+        pivots (stored outputs are then uncentred): give inference its own ``NativeResNetStep``.
+        ``models_token``: a caller's name for the arena's CONTENTS — a later call of this geometry with the same
+        token skips the weight packing and the BatchNorm folds (several batches through one set of models)."""
         C, N = x.shape[0], x.shape[1]
         if C != self.C:
             raise ValueError(f"forward_eval: {C} models for a step built for {self.C}")
@@ -1038,7 +1042,13 @@ class NativeResNetStep:
         self._pending.clear()
         self.stats.zero_()           # the forward kernels still accumulate (unused) batch statistics
         nn_ops._set_lazy((0, 0))
-        self._forward(arena, x, None, N, training=False)
+        tokens = self.__dict__.setdefault("_eval_tokens", {})
+        self._eval_reuse = models_token is not None and tokens.get(self.geom) is models_token
+        try:
+            self._forward(arena, x, None, N, training=False)
+        finally:
+            self._eval_reuse = False
+        tokens[self.geom] = models_token
         ow, ob = self.off["fc.weight"], self.off["fc.bias"]
         Wfc = arena[:, ow:ow + self.fc_out * self.fc_in].view(C, self.fc_out, self.fc_in)
         bfc = arena[:, ob:ob + self.fc_out]
@@ -1051,8 +1061,11 @@ class NativeResNetStep:
         C = self.C
         H, W = x.shape[3], x.shape[4]
         self._training = training
-        nn_ops.pack_weights(arena, self._segs, self._nseg, self.packed, self.packed_ld, C, self._pack_tiles,
-                            self._pack_taps)
+        if training:
+            self.__dict__.get("_eval_tokens", {}).clear()   # the packed weights now hold the training models
+        if training or not getattr(self, "_eval_reuse", False):
+            nn_ops.pack_weights(arena, self._segs, self._nseg, self.packed, self.packed_ld, C, self._pack_tiles,
+                                self._pack_taps)
         st_conv, st_bn = self.stem
         x = x.contiguous()
         fused_stem = False

@@ -77,6 +77,7 @@ class SimEvaluator:
                 self._n_row = min(_N_MAX, max(8, 8 * math.ceil(n / (_ROWS * 8))))
             cap = _ROWS * self._n_row
             arena = flat.view(1, -1).expand(_ROWS, -1).contiguous()
+            token = object()   # one model for every chunk: packed weights and BN folds once per call
             for lo in range(0, n, cap):
                 hi = min(n, lo + cap)
                 sel = idx[lo:hi]
@@ -88,7 +89,8 @@ class SimEvaluator:
                     x = torch.cat([x, x.new_zeros((pad,) + tuple(x.shape[1:]))])
                     y = torch.cat([y, y.new_full((pad,), -1)])
                     g = torch.cat([g, g.new_full((pad,), -1)])
-                logits = st.forward_eval(arena, x.view(_ROWS, self._n_row, *x.shape[1:])).reshape(cap, -1)
+                logits = st.forward_eval(arena, x.view(_ROWS, self._n_row, *x.shape[1:]),
+                                         models_token=token).reshape(cap, -1)
                 ops.eval_stats(logits, y, g, sums=sums, cls=cls, with_classes=cls is not None)
             return
         model = self.sim.model
@@ -107,7 +109,10 @@ class SimEvaluator:
     def _global_data(self):
         if self._global is None:
             test = self.sim.dataset[3]
-            self._global = (test.x.to(self.device), test.y.to(self.device))
+            if test is None:            # no global test split: the Global/* metrics are None
+                self._global = (None, torch.zeros(0, dtype=torch.int64, device=self.device))
+            else:
+                self._global = (test.x.to(self.device), test.y.to(self.device))
         return self._global
 
     def _client_test_store(self):
@@ -179,7 +184,10 @@ class SimEvaluator:
                 test_m.append({"test_correct": float(tes[c, 0]), "test_loss": float(tes[c, 1]),
                                "test_total": int(tes[c, 2]), "test_recall": rec, "test_precision": prec})
             out.update(fork_local_test_stats(train_m, test_m))
-        tot = max(1.0, float(gs[2]))
+        if float(gs[2]) == 0:
+            out.update({"Global/Acc": None, "Global/Loss": None, "Global/Recall": None})
+            return out
+        tot = float(gs[2])
         out["Global/Acc"] = float(gs[0]) / tot
         out["Global/Loss"] = float(gs[1]) / tot
         recall: Optional[float] = None

@@ -59,3 +59,30 @@ def test_fused_eval_matches_unfused_and_torch(depth, C, N):
             assert e < 1e-4, (i, e)
     finally:
         torch.backends.cudnn.allow_tf32 = prev
+
+
+def test_models_token_reuses_packing_only_for_the_same_models():
+    """forward_eval(models_token=t): a second batch under the same token skips the weight packing and BN folds and
+    still matches a fresh step; a new token (other models, same geometry) re-packs."""
+    from fedml_amd.core.arena import ParamLayout
+    from fedml_amd.models.cv.resnet import resnet56
+    from fedml_amd.parallel.native_resnet import NativeResNetStep
+    torch.manual_seed(0)
+    base = resnet56(10)
+    layout = ParamLayout.from_module(base)
+    C, N = 4, 8
+    arena1 = torch.stack([layout.flatten(m.state_dict(), device="cuda") for m in _models(base, C, 1)])
+    arena2 = torch.stack([layout.flatten(m.state_dict(), device="cuda") for m in _models(base, C, 2)])
+    x1, x2 = torch.randn(2, C, N, 3, 32, 32, device="cuda").unbind(0)
+    st = NativeResNetStep(base, layout, C, "cuda")
+    t1, t2 = object(), object()
+    st.forward_eval(arena1, x1, models_token=t1)
+    got_a = st.forward_eval(arena1, x2, models_token=t1).clone()      # reuse
+    got_b = st.forward_eval(arena2, x2, models_token=t2).clone()      # new models → re-pack
+    fresh = NativeResNetStep(base, layout, C, "cuda")
+    ref_a = fresh.forward_eval(arena1, x2).clone()
+    ref_b = fresh.forward_eval(arena2, x2).clone()
+    torch.cuda.synchronize()
+    assert torch.equal(got_a, ref_a)
+    assert torch.equal(got_b, ref_b)
+    assert not torch.equal(ref_a, ref_b)
