@@ -931,6 +931,200 @@ static int launch3(BArgs a, int C, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
+// ---- stage-3 entry (16² × 128 → 8² × 256, stride-2 3×3, projection shortcut): one wave per SIMD ----
+// As bneck3_eval_kernel: wave w keeps ALL of conv1's weights (it takes four input rows for every output tile), conv2
+// output tile w and conv3 output tiles w + 4j in registers (32 + 36 + 16 = 84 float4 = 336 VGPRs); the projection's
+// fragments (32 float4 more would spill) are re-read from L2 per image, each tile's ahead of its conv3 MFMAs. A unit
+// is one image: conv1
+// reads x straight from global memory (L2 after the first wave) for the 16 input rows; wave 0 also copies the
+// stride-2 pixels' fragments to LDS, where conv3's shortcut operand is read from with m2.
+struct Geo3D {
+  static constexpr int CX = 128, CM = 64, CO = 256, H = 16, W = 16, HO = 8, WO = 8, TW = W + 2, RI = H + 1;
+  static constexpr int LM = CM + 4, LX = CX + 4, P1 = H * W, P2 = HO * WO;
+  static constexpr int M1F = RI * TW * LM, M2F = P2 * LM, XSF = P2 * LX;
+  static constexpr int FLOATS = 4 * CM + 4 * CO + M1F + M2F + XSF;
+};
+
+__global__ __launch_bounds__(256, 1) void bneck3_ds_eval_kernel(DArgs d) {
+  using G = Geo3D;
+  constexpr int CX = G::CX, CM = G::CM, CO = G::CO, W = G::W, WO = G::WO, TW = G::TW, LM = G::LM, LX = G::LX;
+  constexpr int NW = 4, KX = CX / 16, NT1 = CM / 16, NTW3 = CO / 16 / NW, PT1 = G::P1 / 16, PT2 = G::P2 / 16;
+  static_assert(NT1 == NW && PT2 == 4 && PT1 == 16, "one output tile a wave");
+  const BArgs& a = d.b;
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  float* vs = sm;                      // s1 t1 s2 t2 [CM], s3 t3 sd td [CO]
+  float* m1 = vs + 4 * CM + 4 * CO;    // [RI][TW][LM]: input row r ↦ r + 1, col c ↦ c + 1; row 0 / col 0 zero
+  float* m2 = m1 + G::M1F;             // [P2][LM]
+  float* xs = m2 + G::M2F;             // [P2][LX]: x at the stride-2 pixels (the shortcut's operand)
+  const int c = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6, g = lane >> 4, l16 = lane & 15;
+  const int u_lo = blockIdx.x * a.units_per_wg;
+  if (u_lo >= a.N) return;   // uniform: whole workgroup
+  const int u_hi = min(a.N, u_lo + a.units_per_wg);
+
+  const float* pk = a.wpk + (int64_t)c * a.wpk_ld;
+  float4 a1[NT1][KX], a2[9 * NT1], a3[NTW3][NT1];
+  const float* wd = pk + d.offd + (int64_t)(wid * 16 + l16) * d.ldkd + 4 * g;   // + NW·16 rows per tile j
+  {
+    const float* w1 = pk + a.off1 + (int64_t)l16 * a.ldk1 + 4 * g;
+    const float* w2 = pk + a.off2 + (int64_t)(wid * 16 + l16) * a.ldk2 + 4 * g;
+    const float* w3 = pk + a.off3 + (int64_t)(wid * 16 + l16) * a.ldk3 + 4 * g;
+#pragma unroll
+    for (int o = 0; o < NT1; ++o)
+#pragma unroll
+      for (int ks = 0; ks < KX; ++ks) a1[o][ks] = ld4(w1 + (int64_t)o * 16 * a.ldk1 + 16 * ks);
+#pragma unroll
+    for (int j = 0; j < 9 * NT1; ++j) a2[j] = ld4(w2 + (j / NT1) * CM + 16 * (j % NT1));
+#pragma unroll
+    for (int j = 0; j < NTW3; ++j)
+#pragma unroll
+      for (int ks = 0; ks < NT1; ++ks) a3[j][ks] = ld4(w3 + (int64_t)j * NW * 16 * a.ldk3 + 16 * ks);
+  }
+  for (int i = tid; i < CM; i += 256) {
+    vs[i] = a.s1[(int64_t)c * CM + i];
+    vs[CM + i] = a.t1[(int64_t)c * CM + i];
+    vs[2 * CM + i] = a.s2[(int64_t)c * CM + i];
+    vs[3 * CM + i] = a.t2[(int64_t)c * CM + i];
+  }
+  for (int i = tid; i < CO; i += 256) {
+    vs[4 * CM + i] = a.s3[(int64_t)c * CO + i];
+    vs[4 * CM + CO + i] = a.t3[(int64_t)c * CO + i];
+    vs[4 * CM + 2 * CO + i] = d.sd[(int64_t)c * CO + i];
+    vs[4 * CM + 3 * CO + i] = d.td[(int64_t)c * CO + i];
+  }
+  for (int i = tid; i < G::M1F; i += 256) m1[i] = 0.f;   // the zero row 0 / column 0 (conv1 writes the rest)
+  const float* s1 = vs;
+  const float* t1 = vs + CM;
+  const float* s2 = vs + 2 * CM;
+  const float* t2 = vs + 3 * CM;
+  const float* s3 = vs + 4 * CM;
+  const float* t3 = vs + 4 * CM + CO;
+  const float* sdv = vs + 4 * CM + 2 * CO;
+  const float* tdv = vs + 4 * CM + 3 * CO;
+  __syncthreads();
+
+  for (int n = u_lo; n < u_hi; ++n) {
+    const float* xi = a.x + ((int64_t)c * a.N + n) * G::P1 * CX;
+
+    // ---- conv1 + bn1 + relu over the 16 input rows → m1: wave w takes input rows 4w..4w+3 (pixel tile = row)
+    // for all four output tiles, so x is read once per workgroup and every B fragment feeds four MFMA chains; the
+    // stride-2 pixels' fragments are kept in LDS for the shortcut ----
+    {
+      f32x4 acc[NT1][4];
+#pragma unroll
+      for (int o = 0; o < NT1; ++o)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[o][q] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const float* xr = xi + (int64_t)(4 * wid * W + l16) * CX + 4 * g;
+#pragma unroll
+      for (int ks = 0; ks < KX; ++ks) {
+        float4 b[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) b[q] = ld4(xr + (int64_t)q * W * CX + 16 * ks);
+#pragma unroll
+        for (int o = 0; o < NT1; ++o)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc[o][q] = mma4(a1[o][ks], b[q], acc[o][q]);
+        if ((l16 & 1) == 0) {
+#pragma unroll
+          for (int q = 0; q < 4; q += 2)
+            *reinterpret_cast<float4*>(xs + ((2 * wid + q / 2) * WO + (l16 >> 1)) * LX + 16 * ks + 4 * g) = b[q];
+        }
+      }
+#pragma unroll
+      for (int o = 0; o < NT1; ++o) {
+        const int ch = o * 16 + 4 * g;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float4 v;
+          v.x = fmaxf(acc[o][q][0] * s1[ch] + t1[ch], 0.f);
+          v.y = fmaxf(acc[o][q][1] * s1[ch + 1] + t1[ch + 1], 0.f);
+          v.z = fmaxf(acc[o][q][2] * s1[ch + 2] + t1[ch + 2], 0.f);
+          v.w = fmaxf(acc[o][q][3] * s1[ch + 3] + t1[ch + 3], 0.f);
+          *reinterpret_cast<float4*>(m1 + ((4 * wid + q + 1) * TW + l16 + 1) * LM + ch) = v;
+        }
+      }
+    }
+    __syncthreads();
+
+    // ---- conv2 (3×3, stride 2) + bn2 + relu → m2 ----
+    {
+      const int ch1 = wid * 16 + 4 * g;
+      f32x4 acc[PT2];
+      const float* mp[PT2];
+#pragma unroll
+      for (int t = 0; t < PT2; ++t) {
+        acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int p = 16 * t + l16, orow = p / WO, ocol = p % WO;
+        mp[t] = m1 + (2 * orow * TW + 2 * ocol) * LM + 4 * g;
+      }
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int mo = ((tap / 3) * TW + tap % 3) * LM;
+#pragma unroll
+        for (int cc = 0; cc < NT1; ++cc)
+#pragma unroll
+          for (int t = 0; t < PT2; ++t) acc[t] = mma4(a2[tap * NT1 + cc], ld4(mp[t] + mo + 16 * cc), acc[t]);
+      }
+#pragma unroll
+      for (int t = 0; t < PT2; ++t) {
+        float4 v;
+        v.x = fmaxf(acc[t][0] * s2[ch1] + t2[ch1], 0.f);
+        v.y = fmaxf(acc[t][1] * s2[ch1 + 1] + t2[ch1 + 1], 0.f);
+        v.z = fmaxf(acc[t][2] * s2[ch1 + 2] + t2[ch1 + 2], 0.f);
+        v.w = fmaxf(acc[t][3] * s2[ch1 + 3] + t2[ch1 + 3], 0.f);
+        *reinterpret_cast<float4*>(m2 + (16 * t + l16) * LM + ch1) = v;
+      }
+    }
+    __syncthreads();
+
+    // ---- conv3 + bn3 + shortcut conv + bn_d, summed, relu → y ----
+    float* yo = a.out + ((int64_t)c * a.N + n) * G::P2 * CO;
+#pragma unroll
+    for (int j = 0; j < NTW3; ++j) {
+      const int c0 = (wid + NW * j) * 16 + 4 * g;
+      float4 adj[KX];   // issued before conv3's MFMAs, consumed after them
+      __builtin_amdgcn_sched_barrier(0);   // keep the next tile's fragment loads out of this one (register budget)
+#pragma unroll
+      for (int ks = 0; ks < KX; ++ks) adj[ks] = ld4(wd + (int64_t)j * NW * 16 * d.ldkd + 16 * ks);
+      f32x4 acc[PT2], dac[PT2];
+#pragma unroll
+      for (int t = 0; t < PT2; ++t) acc[t] = dac[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < NT1; ++ks)
+#pragma unroll
+        for (int t = 0; t < PT2; ++t)
+          acc[t] = mma4(a3[j][ks], ld4(m2 + (16 * t + l16) * LM + 16 * ks + 4 * g), acc[t]);
+#pragma unroll
+      for (int ks = 0; ks < KX; ++ks)
+#pragma unroll
+        for (int t = 0; t < PT2; ++t)
+          dac[t] = mma4(adj[ks], ld4(xs + (16 * t + l16) * LX + 16 * ks + 4 * g), dac[t]);
+#pragma unroll
+      for (int t = 0; t < PT2; ++t) {
+        float4 v;
+        v.x = fmaxf(acc[t][0] * s3[c0] + t3[c0] + dac[t][0] * sdv[c0] + tdv[c0], 0.f);
+        v.y = fmaxf(acc[t][1] * s3[c0 + 1] + t3[c0 + 1] + dac[t][1] * sdv[c0 + 1] + tdv[c0 + 1], 0.f);
+        v.z = fmaxf(acc[t][2] * s3[c0 + 2] + t3[c0 + 2] + dac[t][2] * sdv[c0 + 2] + tdv[c0 + 2], 0.f);
+        v.w = fmaxf(acc[t][3] * s3[c0 + 3] + t3[c0 + 3] + dac[t][3] * sdv[c0 + 3] + tdv[c0 + 3], 0.f);
+        *reinterpret_cast<float4*>(yo + (int64_t)(16 * t + l16) * CO + c0) = v;
+      }
+    }
+    __syncthreads();   // m1 / m2 / xs are rewritten by the next image
+  }
+}
+
+static int launch3_ds(DArgs d, int C, hipStream_t stream) {
+  const size_t smem = (size_t)Geo3D::FLOATS * 4;
+  if (smem > 160 * 1024) return -5;
+  const int per_model = std::max(1, std::min(d.b.N, (512 + C - 1) / C));
+  d.b.units_per_wg = (d.b.N + per_model - 1) / per_model;
+  const int gx = (d.b.N + d.b.units_per_wg - 1) / d.b.units_per_wg;
+  (void)hipFuncSetAttribute((const void*)bneck3_ds_eval_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+  hipLaunchKernelGGL(bneck3_ds_eval_kernel, dim3(gx, C), dim3(256), smem, stream, d);
+  return (int)hipGetLastError();
+}
+
 // ---- stem: NCHW image → 3×3 conv (≤ 4 input channels, 16 outputs) → BN → ReLU → NHWC ----
 // Replaces the layout pass, the stem conv (a 16-output GEMM that cannot fill a tile) and the BN/ReLU pass of the
 // training path with one memory-bound kernel. A workgroup takes a band of 8 rows of one 32-wide image: the input
@@ -1037,8 +1231,8 @@ FA_EXPORT int fa_bneck_eval_f32(const float* x, float* out, const float* wpk, in
 
 // The stage-entry bottleneck (projection shortcut, stride on the 3×3) of C models at once: x [C][N][H][W][cx] →
 // out [C][N][H/stride][W/stride][4·cm]. Instantiated for the CIFAR ResNet-56/110 stage-1 (cx 16, cm 16, 32², stride
-// 1) and stage-2 (cx 64, cm 32, 32², stride 2) entries; -2 for any other geometry (the caller keeps the unfused
-// forward — the stage-3 entry's 64-wide weights do not fit the register-resident scheme).
+// 1), stage-2 (cx 64, cm 32, 32², stride 2) and stage-3 (cx 128, cm 64, 16², stride 2) entries; -2 for any other
+// geometry (the caller keeps the unfused forward).
 FA_EXPORT int fa_bneck_ds_eval_f32(const float* x, float* out, const float* wpk, int64_t wpk_ld, int64_t off1, int ldk1,
                                    int64_t off2, int ldk2, int64_t off3, int ldk3, int64_t offd, int ldkd,
                                    const float* s1, const float* t1, const float* s2, const float* t2, const float* s3,
@@ -1052,6 +1246,7 @@ FA_EXPORT int fa_bneck_ds_eval_f32(const float* x, float* out, const float* wpk,
                     sd, td};
   if (cx == 16 && cm == 16 && H == 32 && stride == 1) return infer::launch_ds<16, 16, 32, 1, 8>(d, C, stream);
   if (cx == 64 && cm == 32 && H == 32 && stride == 2) return infer::launch_ds<64, 32, 32, 2, 8>(d, C, stream);
+  if (cx == 128 && cm == 64 && H == 16 && stride == 2) return infer::launch3_ds(d, C, stream);
   return -2;
 }
 

@@ -606,7 +606,7 @@ class NativeResNetStep:
 
     def _fused_ds_eval_ok(self, b) -> bool:
         """Inference runs this stage-entry block (projection shortcut, stride on the 3×3) as ONE fused kernel
-        (nn_ops.bneck_ds_eval): the CIFAR ResNet-56/110 stage-1 and stage-2 entries."""
+        (nn_ops.bneck_ds_eval): the CIFAR ResNet-56/110 stage-1, stage-2 and stage-3 entries."""
         if b is None or getattr(self, "_training", True) or self.dtype != torch.float32 or not self.use_fused_eval:
             return False
         if b.ds_conv is None or len(b.convs) != 3:
@@ -618,7 +618,7 @@ class NativeResNetStep:
                 and d.k == 1 and d.pad == 0 and d.stride == c2.stride and c1.cin_pad == cx and d.cin == cx
                 and d.cin_pad == cx and c1.cout == cm and c2.cin_pad == cm and c3.cin_pad == cm
                 and c3.cout == 4 * cm and d.cout == 4 * cm and c1.H == c1.W
-                and (cx, cm, c1.H, c2.stride) in ((16, 16, 32, 1), (64, 32, 32, 2)))
+                and (cx, cm, c1.H, c2.stride) in ((16, 16, 32, 1), (64, 32, 32, 2), (128, 64, 16, 2)))
 
     def _pbout_ok(self, b, nb) -> bool:
         """Block ``b``'s output is formed in the operand load of the next block's first conv (conv_fwd_pbout: 1×1,

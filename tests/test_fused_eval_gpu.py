@@ -1,5 +1,5 @@
 """The fused inference bottlenecks (``ops/csrc/infer_kernels.hip``: one kernel per stride-1 bottleneck of stages 1-3
-and per stage-1 / stage-2 entry block with its projection shortcut)
+and per stage-entry block with its projection shortcut, and the stem)
 against the unfused inference forward of the same native step (the training kernels with BatchNorm folded) and
 against torch fp32 eval — for several models at once with their own running statistics."""
 import copy
@@ -42,7 +42,7 @@ def test_fused_eval_matches_unfused_and_torch(depth, C, N):
     assert fused.use_fused_eval
     got = fused.forward_eval(arena, x)
     assert sum(fused._fused_eval_ok(b) for b in fused.blocks) == (15 if depth == 56 else 33)   # stages 1-3
-    assert sum(fused._fused_ds_eval_ok(b) for b in fused.blocks) == 2     # the stage-1 and stage-2 entries
+    assert sum(fused._fused_ds_eval_ok(b) for b in fused.blocks) == 3     # the three stage entries
     plain = NativeResNetStep(base, layout, C, "cuda")
     plain.use_fused_eval = False
     ref_native = plain.forward_eval(arena, x)
