@@ -35,6 +35,7 @@ struct BArgs {
   int ldk1, ldk2, ldk3;
   const float *s1, *t1, *s2, *t2, *s3, *t3;   // folded BatchNorm [C][CM] ×4, [C][CIN] ×2
   int N, units_per_wg;
+  float* pool;   // bneck3 only: non-null → write the global average pool [C][N][CIN] instead of y
 };
 
 __device__ __forceinline__ f32x4 mma4(const float4 a, const float4 b, f32x4 c) {
@@ -266,7 +267,7 @@ __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast
 // NW = 8: one workgroup per CU; NW = 4 (smaller R): two per CU, so one workgroup's barrier waits overlap the
 // other's MFMAs. conv3 gives a wave NT3/NW channel tiles when the waves are fewer than CIN/16.
 template <int CM, int HW, int R, bool BAND, bool PIPE, int NW, int Q2>
-__global__ __launch_bounds__(64 * NW, NW == 4 && !BAND ? 3 : 2) void bneck_eval_rw_kernel(BArgs a) {   // waves per SIMD
+__global__ __launch_bounds__(64 * NW, NW == 4 ? (BAND ? 1 : 3) : 2) void bneck_eval_rw_kernel(BArgs a) {   // waves per SIMD
   using G = GeoR<CM, HW, R, BAND, PIPE>;
   static_assert(!(BAND && PIPE), "the band is read by conv1 and conv3 of one unit");
   constexpr int CIN = G::CIN, H = G::H, W = G::W, TW = G::TW, LM = G::LM, NT1 = G::NT1, NT3 = G::NT3;
@@ -887,7 +888,9 @@ __global__ __launch_bounds__(256, 1) void bneck3_eval_kernel(BArgs a) {
     }
     __syncthreads();
 
-    // ---- conv3 + bn3 + residual (from the staged x) + relu → y: output tiles wid + 4j ----
+    // ---- conv3 + bn3 + residual (from the staged x) + relu → y: output tiles wid + 4j (the network's last block
+    // with a.pool: the 64-pixel average instead, summed over the four tiles in-lane and over the 16 pixel lanes
+    // by butterfly shuffles — y is never written and no pooling pass runs) ----
     float* yo = a.out + ((int64_t)c * a.N + n) * P * CIN;
 #pragma unroll
     for (int j = 0; j < NTW3; ++j) {
@@ -900,6 +903,7 @@ __global__ __launch_bounds__(256, 1) void bneck3_eval_kernel(BArgs a) {
 #pragma unroll
         for (int t = 0; t < PT; ++t)
           acc[t] = mma4(a3[j][ks], ld4(m2 + (16 * t + l16) * LM + 16 * ks + 4 * g), acc[t]);
+      float4 sum = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
       for (int t = 0; t < PT; ++t) {
         const int p = 16 * t + l16;
@@ -909,7 +913,28 @@ __global__ __launch_bounds__(256, 1) void bneck3_eval_kernel(BArgs a) {
         v.y = fmaxf(acc[t][1] * s3[c0 + 1] + t3[c0 + 1] + res.y, 0.f);
         v.z = fmaxf(acc[t][2] * s3[c0 + 2] + t3[c0 + 2] + res.z, 0.f);
         v.w = fmaxf(acc[t][3] * s3[c0 + 3] + t3[c0 + 3] + res.w, 0.f);
-        *reinterpret_cast<float4*>(yo + (int64_t)p * CIN + c0) = v;
+        if (a.pool) {
+          sum.x += v.x;
+          sum.y += v.y;
+          sum.z += v.z;
+          sum.w += v.w;
+        } else {
+          *reinterpret_cast<float4*>(yo + (int64_t)p * CIN + c0) = v;
+        }
+      }
+      if (a.pool) {   // uniform branch
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          sum.x += __shfl_xor(sum.x, o);
+          sum.y += __shfl_xor(sum.y, o);
+          sum.z += __shfl_xor(sum.z, o);
+          sum.w += __shfl_xor(sum.w, o);
+        }
+        if (l16 == 0) {
+          constexpr float inv = 1.f / P;
+          *reinterpret_cast<float4*>(a.pool + ((int64_t)c * a.N + n) * CIN + c0) =
+              make_float4(sum.x * inv, sum.y * inv, sum.z * inv, sum.w * inv);
+        }
       }
     }
     __syncthreads();   // xs / m1 / m2 are rewritten by the next image
@@ -1181,14 +1206,18 @@ __global__ __launch_bounds__(256) void stem_eval_kernel(const float* __restrict_
 }  // namespace infer
 
 // y = relu(bn3(conv3(relu(bn2(conv2(relu(bn1(conv1(x)))))))) + x) for a stride-1, downsample-free bottleneck of
-// C models at once; mid width cm ∈ {16, 32, 64} at hw = 32 / 16 / 8 (the ResNet-56/110 CIFAR stages 1-3). Returns
-// -2 for a geometry without an instantiation (the caller keeps the unfused forward).
+// C models at once; mid width cm ∈ {16, 32, 64} at hw = 32 / 16 / 8 (the ResNet-56/110 CIFAR stages 1-3). pool
+// (cm 64 only; else null): write the global average pool of y [C][N][4·cm] instead of y. Returns -2 for a geometry
+// without an instantiation (the caller keeps the unfused forward).
 FA_EXPORT int fa_bneck_eval_f32(const float* x, float* out, const float* wpk, int64_t wpk_ld, int64_t off1, int ldk1,
                                 int64_t off2, int ldk2, int64_t off3, int ldk3, const float* s1, const float* t1,
                                 const float* s2, const float* t2, const float* s3, const float* t3, int C, int N, int H,
-                                int W, int cm, hipStream_t stream) {
+                                int W, int cm, float* pool, hipStream_t stream) {
   if (C <= 0 || N <= 0 || H != W || C > 65535) return (int)hipErrorInvalidValue;
-  infer::BArgs a = {x, out, wpk, wpk_ld, off1, off2, off3, ldk1, ldk2, ldk3, s1, t1, s2, t2, s3, t3, N, 1};
+  infer::BArgs a = {x, out, wpk, wpk_ld, off1, off2, off3, ldk1, ldk2, ldk3, s1, t1, s2, t2, s3, t3, N, 1, pool};
+  if (pool && !(cm == 64 && H == 8 && ((off1 | off2 | off3 | ldk1 | ldk2 | ldk3 | wpk_ld) & 3) == 0 &&
+                (reinterpret_cast<uintptr_t>(wpk) & 15) == 0))
+    return -2;   // the pooled epilogue exists in the stage-3 kernel only
   // FEDML_AMD_BNECK_EVAL_VARIANT (A/B of the tilings; ms per 128-model × 64-image ResNet-56 forward on MI355X,
   // profiles/r6_fused_eval_variants.txt): 0 = LDS-resident weights, 4 waves, R = 8 (27.9); 1 = 8 waves, R = 16 / 8
   // (26.4); 2 = 8 waves, R = 8 / 16 (26.0); 3 = register-resident weights, R = 16 (25.3); 4 = same, R = 8 (25.4);
@@ -1206,6 +1235,8 @@ FA_EXPORT int fa_bneck_eval_f32(const float* x, float* out, const float* wpk, in
       if (variant == 6) return infer::launch_rw<16, 32, 4, true, false, 4>(a, C, stream);
       if (variant == 7) return infer::launch_rw<16, 32, 8, false, true, 8>(a, C, stream);
       if (variant == 9) return infer::launch_rw<16, 32, 8, false, false, 4>(a, C, stream);
+      if (variant == 11) return infer::launch_rw<16, 32, 8, true, false, 4, 4>(a, C, stream);
+      if (variant == 12) return infer::launch_rw<16, 32, 8, false, false, 4, 4>(a, C, stream);
       return infer::launch_rw<16, 32, 8, true, false, 8>(a, C, stream);
     }
     if (cm == 64 && H == 8 && variant != 8) return infer::launch3<64>(a, C, stream);
@@ -1242,8 +1273,8 @@ FA_EXPORT int fa_bneck_ds_eval_f32(const float* x, float* out, const float* wpk,
   if (((off1 | off2 | off3 | offd | ldk1 | ldk2 | ldk3 | ldkd | wpk_ld) & 3) != 0 ||
       (reinterpret_cast<uintptr_t>(wpk) & 15) != 0)
     return -2;
-  infer::DArgs d = {{x, out, wpk, wpk_ld, off1, off2, off3, ldk1, ldk2, ldk3, s1, t1, s2, t2, s3, t3, N, 1}, offd, ldkd,
-                    sd, td};
+  infer::DArgs d = {{x, out, wpk, wpk_ld, off1, off2, off3, ldk1, ldk2, ldk3, s1, t1, s2, t2, s3, t3, N, 1, nullptr},
+                    offd, ldkd, sd, td};
   if (cx == 16 && cm == 16 && H == 32 && stride == 1) return infer::launch_ds<16, 16, 32, 1, 8>(d, C, stream);
   if (cx == 64 && cm == 32 && H == 32 && stride == 2) return infer::launch_ds<64, 32, 32, 2, 8>(d, C, stream);
   if (cx == 128 && cm == 64 && H == 16 && stride == 2) return infer::launch3_ds(d, C, stream);

@@ -325,17 +325,18 @@ def bn_bwd_finalize(bstats, NS, q_gy, C, Ch, n, mean, rstd, arena, garena, off_g
     _check(rc, "fa_bn_bwd_finalize")
 
 
-def bneck_eval(x, out, wpk, wpk_ld, convs, vecs, C, N, H, W, cm):
+def bneck_eval(x, out, wpk, wpk_ld, convs, vecs, C, N, H, W, cm, pool=None):
     """Inference bottleneck as ONE kernel (ops/csrc/infer_kernels.hip): out = relu(bn3(conv3(relu(bn2(conv2(relu(
     bn1(conv1(x)))))))) + x) for a stride-1, downsample-free block of C models, BN folded (``vecs``: the (scale,
     shift) [C, ch] pairs of bn1..bn3). ``convs``: ((off_f, ldk) of conv1, conv2, conv3) in the packed forward
     weights. fp32 storage. Returns False when no instantiation takes the geometry (the caller runs the unfused
-    forward)."""
+    forward). ``pool`` [C, N, 4·cm] (the 8×8 stage only): write the global average pool of the output there instead
+    of ``out``."""
     (o1, l1), (o2, l2), (o3, l3) = convs
     (s1, t1), (s2, t2), (s3, t3) = vecs
     rc = _fn("fa_bneck_eval_f32")(_pr(x), _p(out), _pr(wpk), _i64(wpk_ld), _i64(o1), _i(l1), _i64(o2), _i(l2), _i64(o3),
                                   _i(l3), _pr(s1), _pr(t1), _pr(s2), _pr(t2), _pr(s3), _pr(t3), _i(C), _i(N), _i(H), _i(W),
-                                  _i(cm), _stream(x))
+                                  _i(cm), _p(pool), _stream(x))
     if rc == -2:
         return False
     _check(rc, "fa_bneck_eval_f32")

@@ -1087,6 +1087,7 @@ class NativeResNetStep:
                              N * st_conv.Ho * st_conv.Wo * st_conv.cout, st_conv.cout, nimg=self._nimg,
                              per_img=st_conv.Ho * st_conv.Wo * st_conv.cout)
         act_in = self.stem_out
+        pooled = False  # inference: the last block wrote the average pool itself
         pend = None    # (yp, s, t, res, rs, rt, bout) of a block output formed by the next block's first conv
         pend_keys = (None, None)   # its BNs (deferred finalisation: taken by that conv)
         for bi, b in enumerate(self.blocks):
@@ -1098,9 +1099,12 @@ class NativeResNetStep:
                 vec = [(self.bn_vec[bn.key][0], self.bn_vec[bn.key][1]) for bn in b.bns]
                 pk = self.packed.view(-1)
                 c1 = b.convs[0]
+                last = bi == len(self.blocks) - 1 and c1.H == 8 and b.convs[-1].cout == self.fc_in
+                pool = self.pooled if last else None
                 if nn_ops.bneck_eval(act_in, b.out, pk, self.packed_ld, [(cv.off_f, cv.ldk) for cv in b.convs], vec,
-                                     C, N, c1.H, c1.W, b.convs[1].cout):
+                                     C, N, c1.H, c1.W, b.convs[1].cout, pool=pool):
                     act_in = b.out
+                    pooled = pool is not None
                     continue
             if pend is None and self._fused_ds_eval_ok(b):
                 bns = list(b.bns) + [b.ds_bn]
@@ -1164,5 +1168,6 @@ class NativeResNetStep:
         self._flush_all()       # every forward BN has been folded (by its consumer or explicitly)
         fh, fw = self.final_hw
         chl = self.blocks[-1].convs[-1].cout
-        nn_ops.avgpool(act_in, self.pooled, C * N, fh * fw, chl, nimg=self._nimg, N=N)
+        if not pooled:
+            nn_ops.avgpool(act_in, self.pooled, C * N, fh * fw, chl, nimg=self._nimg, N=N)
         return act_in
