@@ -36,6 +36,7 @@ class BatchedModelEvaluator:
         self._interps = {}
         self._batched_ok = True
         self._native = {}            # chunk size → NativeResNetStep used for inference (GPU, CIFAR ResNets)
+        self.native_images = 512     # images per model per native call (batches merged up to this)
         self._native_ok = self.device.type == "cuda"
 
     def flatten(self, state_dict) -> torch.Tensor:
@@ -75,7 +76,7 @@ class BatchedModelEvaluator:
             from ..parallel.native_resnet import NativeResNetStep, UnsupportedNative
             try:
                 st = NativeResNetStep(self.model, self.layout, c, self.device,
-                                      dtype=self.compute_dtype or torch.float32)
+                                      dtype=self.compute_dtype or torch.float32, eval_only=True)
             except UnsupportedNative as e:
                 logging.info("coalition evaluation: no native inference (%s)", e)
                 self._native_ok = False
@@ -102,9 +103,22 @@ class BatchedModelEvaluator:
             # copies of its first model, whose outputs are dropped
             arena = chunk if c == cm else torch.cat([chunk, chunk[:1].expand(cm - c, -1)])
             arena = arena.contiguous()
-            token = object()   # the batches after the first reuse this chunk's packed weights and folded BNs
-            return [st.forward_eval(arena, x.unsqueeze(0).expand(cm, *x.shape), models_token=token)[:c].float()
-                    for x, _ in batches]
+            token = object()   # the calls after the first reuse this chunk's packed weights and folded BNs
+            # consecutive batches run as one call of up to native_images images per model (an eval-only step
+            # stores two activation buffers, so larger calls fit); the logits are split back per batch
+            outs = []
+            cap = self.native_images if getattr(st, "lean", False) else 0
+            i = 0
+            while i < len(batches):
+                j, n = i + 1, batches[i][0].shape[0]
+                while j < len(batches) and n + batches[j][0].shape[0] <= cap:
+                    n += batches[j][0].shape[0]
+                    j += 1
+                x = batches[i][0] if j == i + 1 else torch.cat([b[0] for b in batches[i:j]])
+                z = st.forward_eval(arena, x.unsqueeze(0).expand(cm, *x.shape), models_token=token)[:c].float()
+                outs.extend(z.split([b[0].shape[0] for b in batches[i:j]], dim=1))
+                i = j
+            return outs
         if self._batched_ok:
             try:
                 interp = self._interp(c)

@@ -138,7 +138,13 @@ def parse_resnet(model: nn.Module):
 class NativeResNetStep:
     """Owns the activation / statistics buffers for one (C, N, H, W) geometry."""
 
-    def __init__(self, model: nn.Module, layout, C: int, device, dtype: torch.dtype = torch.float32):
+    def __init__(self, model: nn.Module, layout, C: int, device, dtype: torch.dtype = torch.float32,
+                 eval_only: bool = False):
+        """``eval_only``: this step only ever runs ``forward_eval`` (the valuation / evaluation steps). When every
+        block has a fused inference kernel, each geometry then holds two ping-pong activation buffers instead of
+        the training step's per-layer activations and gradient scratch (~16× less memory: larger batches per
+        call)."""
+        self.eval_only = bool(eval_only)
         if dtype not in (torch.float32, torch.bfloat16):
             raise UnsupportedNative(f"storage dtype {dtype} (native kernels: float32 | bfloat16)")
         self.dtype = dtype
@@ -284,11 +290,25 @@ class NativeResNetStep:
         def act(hh, ww, ch):   # zero-initialised: padding images (heterogeneous batches) are never written
             return torch.zeros(C, N, hh, ww, ch, dtype=bf, device=dev)
 
-        self.x_in = act(H, W, st.cin_pad)
-        self.stem_y = act(st.Ho, st.Wo, st.cout)
-        self.stem_out = act(st.Ho, st.Wo, st.cout)
+        self.lean = self._lean_ok()
+        if self.lean:
+            # eval_only + every kernel fused: block i writes ping-pong buffer i mod 2, nothing else is stored
+            big = max(b.convs[-1].Ho * b.convs[-1].Wo * b.convs[-1].cout for b in self.blocks)
+            pp = [torch.zeros(C * N * big, dtype=bf, device=dev) for _ in range(2)]
+            self.x_in = self.stem_y = None
+            self.stem_out = act(st.Ho, st.Wo, st.cout)
+            for i, b in enumerate(self.blocks):
+                last = b.convs[-1]
+                b.ry, b.ryb, b.wb = False, False, False
+                b.ys, b.yd, b.g3 = [None] * len(b.convs), None, None
+                b.out = pp[i % 2][:C * N * last.Ho * last.Wo * last.cout].view(C, N, last.Ho, last.Wo, last.cout)
+            self.gbuf, self.dybuf = [], None
+        else:
+            self.x_in = act(H, W, st.cin_pad)
+            self.stem_y = act(st.Ho, st.Wo, st.cout)
+            self.stem_out = act(st.Ho, st.Wo, st.cout)
         maxel = st.Ho * st.Wo * st.cout
-        for b in self.blocks:
+        for b in ([] if self.lean else self.blocks):
             b.ry = self._ry_ok(b)
             b.ryb = not b.ry and self.use_ry_bwd and self._ry_ok(b, shape_only=True)
             b.ys = [None if (b.ry and j == len(b.convs) - 1) else act(cv.Ho, cv.Wo, cv.cout)
@@ -302,12 +322,13 @@ class NativeResNetStep:
             b.g3 = act(mid.Ho, mid.Wo, mid.cout) if b.wb else None
             for cv in b.convs + ([b.ds_conv] if b.ds_conv else []):
                 maxel = max(maxel, cv.H * cv.W * cv.cin_pad, cv.Ho * cv.Wo * cv.cout)
-        # gradient scratch: block-output g (kept until the block's conv0 is done), two ping-pong
-        # buffers for the inner chain, one for the shortcut gradient
-        self.gbuf = [torch.zeros(C * N * maxel, dtype=bf, device=dev) for _ in range(4)]
-        # materialised dy of the wide layers (one tensor for their bwd-data AND weight-gradient kernels)
-        self.dybuf = torch.zeros(C * N * maxel, dtype=bf, device=dev) if any(
-            self._dym(cv) for cv in self._all_convs()) else None
+        if not self.lean:
+            # gradient scratch: block-output g (kept until the block's conv0 is done), two ping-pong
+            # buffers for the inner chain, one for the shortcut gradient
+            self.gbuf = [torch.zeros(C * N * maxel, dtype=bf, device=dev) for _ in range(4)]
+            # materialised dy of the wide layers (one tensor for their bwd-data AND weight-gradient kernels)
+            self.dybuf = torch.zeros(C * N * maxel, dtype=bf, device=dev) if any(
+                self._dym(cv) for cv in self._all_convs()) else None
         # per-BN vectors: scale, shift, mean, rstd, alpha, beta, gamma, pivot   + stats
         # (pivot: the per-channel shift K the producing conv subtracts from its stored output — the
         # previous step's batch mean — so activations and BN sums stay centred; see bn_fwd_finalize)
@@ -329,7 +350,7 @@ class NativeResNetStep:
             self.stat_views[bn.key] = (fwd, bwd)
         fh, fw = self.final_hw
         self.pooled = torch.zeros(C, N, self.fc_in, dtype=torch.float32, device=dev)
-        self.dpool = torch.zeros(C, N, self.fc_in, dtype=torch.float32, device=dev)
+        self.dpool = None if self.lean else torch.zeros(C, N, self.fc_in, dtype=torch.float32, device=dev)
         self.loss_c = torch.zeros(C, dtype=torch.float32, device=dev)
         # GEMM-layout dW scratch for the weight-gradient kernel (kept zeroed by its scatter pass)
         mx = max(cv.cout * cv.k * cv.k * cv.cin_pad for cv in self._all_convs())
@@ -373,7 +394,7 @@ class NativeResNetStep:
             for t in (self.stats, self.dw_scratch, self.dw_c3, self.gram):
                 self.det.register(t)
         if os.environ.get("FEDML_AMD_POISON", "0") == "1":   # debug: uninitialised reads show up as NaN
-            for t in [self.x_in, self.stem_y, self.stem_out, self.pooled] + list(self.gbuf):
+            for t in [u for u in (self.x_in, self.stem_y, self.stem_out, self.pooled) if u is not None] + list(self.gbuf):
                 t.fill_(float("nan"))
             for b in self.blocks:
                 for t in [u for u in b.ys if u is not None] + [b.out] + ([b.yd] if b.yd is not None else []):
@@ -396,7 +417,7 @@ class NativeResNetStep:
     _STATE_ATTRS = ("x_in", "stem_y", "stem_out", "gbuf", "dybuf", "bn_vec", "stats", "stat_views", "pooled", "dpool",
                     "loss_c", "dw_scratch", "_bn_hw", "_bn_q",
                     "dw_c3", "c1f_part", "gram", "c3_segs", "c3_nseg", "c3_maxn", "_c3_off",
-                    "packed", "packed_ld", "_segs", "_nseg", "_pack_tiles", "_pack_taps", "final_hw", "geom")
+                    "packed", "packed_ld", "_segs", "_nseg", "_pack_tiles", "_pack_taps", "final_hw", "geom", "lean")
 
     def _snapshot(self):
         st = {k: getattr(self, k) for k in self._STATE_ATTRS}
@@ -579,6 +600,21 @@ class NativeResNetStep:
         return (cv.k == 1 and cv.stride == 1 and cv.pad == 0 and cv.cin == cv.cin_pad and cv.cout % 64 == 0
                 and self._c1f(cv, nn_ops.EPI_MASK)
                 and nn_ops.conv1x1_wgrad_supported(cv.cin, cv.cout, cv.k, cv.stride, cv.pad))
+
+    def _lean_ok(self) -> bool:
+        """eval_only step whose whole forward is fused kernels (stem, every block, the pooled last block)."""
+        if not self.eval_only:
+            return False
+        prev = self.__dict__.get("_training")
+        self._training = False
+        try:
+            return (self._fused_stem_ok() and self.blocks[-1].convs[0].H == 8
+                    and all(self._fused_eval_ok(b) or self._fused_ds_eval_ok(b) for b in self.blocks))
+        finally:
+            if prev is None:
+                del self._training
+            else:
+                self._training = prev
 
     def _fused_eval_ok(self, b) -> bool:
         """Inference (forward_eval) runs this block as ONE fused kernel (nn_ops.bneck_eval): fp32, a stride-1
@@ -811,6 +847,8 @@ class NativeResNetStep:
         nimg[c] of its N rows (heterogeneous partitions, exhausted clients: 0). Every kernel restricts its
         pixel range to them (grids of idle clients exit at once), BatchNorm normalises over them, and
         the padding rows never enter a statistic or a gradient (their ``row_scale`` must be 0)."""
+        if self.eval_only:
+            raise RuntimeError("NativeResNetStep(eval_only=True) runs forward_eval only")
         C, N = x.shape[0], x.shape[1]
         self._nimg = nimg
         self._geometry(N, x.shape[3], x.shape[4])
@@ -1077,6 +1115,8 @@ class NativeResNetStep:
                                           st_conv.ldk, st_conv.cin_pad, v0[0], v0[1], C, N, st_conv.cin, H, W,
                                           st_conv.cout)
         if not fused_stem:
+            if getattr(self, "lean", False):
+                raise RuntimeError("eval-only native step: the fused stem kernel declined the geometry")
             nn_ops.nchw_to_nhwc_pad(x, self.x_in, C * N, st_conv.cin, H * W, st_conv.cin_pad)
             # ---------------- forward ----------------
             self._fwd(st_conv, self.x_in, self.stem_y, None, st_bn, N)
@@ -1117,6 +1157,8 @@ class NativeResNetStep:
                                         c1.W, c1.cin, c2.cout, c2.stride):
                     act_in = b.out
                     continue
+            if getattr(self, "lean", False):
+                raise RuntimeError(f"eval-only native step: no fused inference kernel took block {bi}")
             for j, (cv, bn) in enumerate(zip(b.convs, b.bns)):
                 src = act_in if j == 0 else b.ys[j - 1]
                 pro = None if j == 0 else self.bn_vec[b.bns[j - 1].key]

@@ -62,7 +62,8 @@ class SimEvaluator:
             from ...parallel.native_resnet import NativeResNetStep
             st = self.sim.engine.native_step
             if type(st) is NativeResNetStep:
-                self._native = NativeResNetStep(self.sim.model, self.sim.layout, _ROWS, self.device, dtype=st.dtype)
+                self._native = NativeResNetStep(self.sim.model, self.sim.layout, _ROWS, self.device, dtype=st.dtype,
+                                                eval_only=True)
         return self._native or None
 
     def _accumulate(self, flat, x_all, y_all, idx, groups, sums, cls):

@@ -27,7 +27,7 @@ def main():
     flat = layout.flatten(base.state_dict(), device="cuda")
     arena = (flat.view(1, -1) + 0.01 * torch.randn(a.models, flat.numel(), device="cuda")).contiguous()
     x = torch.randn(a.models, a.images, 3, 32, 32, device="cuda")
-    st = NativeResNetStep(base, layout, a.models, "cuda")
+    st = NativeResNetStep(base, layout, a.models, "cuda", eval_only=True)
     for _ in range(2):
         st.forward_eval(arena, x)
     torch.cuda.synchronize()

@@ -43,6 +43,9 @@ def test_fused_eval_matches_unfused_and_torch(depth, C, N):
     got = fused.forward_eval(arena, x)
     assert sum(fused._fused_eval_ok(b) for b in fused.blocks) == (15 if depth == 56 else 33)   # stages 1-3
     assert sum(fused._fused_ds_eval_ok(b) for b in fused.blocks) == 3     # the three stage entries
+    lean = NativeResNetStep(base, layout, C, "cuda", eval_only=True)    # two activation buffers per geometry
+    got_lean = lean.forward_eval(arena, x)
+    assert lean.lean and torch.equal(got_lean, got)
     plain = NativeResNetStep(base, layout, C, "cuda")
     plain.use_fused_eval = False
     ref_native = plain.forward_eval(arena, x)
