@@ -10,6 +10,7 @@
 // MFMA 16x16x32 bf16 operand maps (gfx950): lane l holds A[row l&15][k 8(l>>4)..+7],
 // B[k 8(l>>4)..+7][col l&15]; C/D: col = l&15, row = 4(l>>4) + reg.
 #include "common.h"
+#include <cstdlib>
 #include "dropout.h"
 #include "detacc.h"
 
@@ -397,6 +398,113 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const uint16_t* __restric
   }
 }
 
+// Forward with the probabilities kept in registers: the scores are computed transposed, Sᵀ = K·Qᵀ
+// (mfma_16x16x32: A = K rows, B = Q rows), so a lane holds ONE query (its column) and keys 4g … 4g+3 of every
+// 16-key block in its 4 accumulators. The softmax of a query is then an in-lane max / sum over its 4·NB scores
+// plus two cross-group shuffles, and the bf16 probabilities of a block ARE the B operand of the 16×16×16 MFMA
+// (B[k = 4g + j][col]) for Oᵀ = Vᵀ·Pᵀ — no LDS round trip for P. Vᵀ's A fragment (A[row = dim][k = 4g + j]) is one
+// ds_read_b64_tr_b16 of the row-major V image (16-lane group g: rows 4g … 4g+3 of the key block). K and V of the
+// (sequence, head) stay in LDS for all its query chunks; 64 KB at S ≤ 224, two workgroups per CU. Same
+// results as attn_fwd_kernel up to the order of the fp32 sums (the backward kernels are shared).
+template <int SP>
+__global__ __launch_bounds__(256, 2) void attn_fwd_rp_kernel(const uint16_t* __restrict__ q, int ldq,
+                                                          const uint16_t* __restrict__ k, int ldk,
+                                                          const uint16_t* __restrict__ v, int ldv,
+                                                          uint16_t* __restrict__ o, int ldo,
+                                                          const uint8_t* __restrict__ kmask, float* __restrict__ lse2,
+                                                          int S, int H, float scale, uint32_t thr, float dscale,
+                                                          uint32_t seed, const uint32_t* __restrict__ seedp) {
+  if (seedp) seed += *seedp * 1000003u;
+  constexpr int NB = SP / 16;
+  static_assert(NB <= 16, "key-validity bits");
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[SP * KST];
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[SP * KST];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, i16 = lane & 15;
+  const int h = blockIdx.x, cb = blockIdx.y;
+  const size_t tok0 = (size_t)cb * S;
+  stage_rows(Ks, k + tok0 * ldk + h * 64, ldk, 0, SP, S);
+  stage_rows(Vs, v + tok0 * ldv + h * 64, ldv, 0, SP, S);
+  const float c2 = scale * kLog2e;
+  const uint32_t bh = (uint32_t)(cb * H + h);
+  uint64_t kv = 0;   // bit 4·nb + r: key nb·16 + 4g + r exists and is not masked
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int key = nb * 16 + 4 * g + r;
+      if (key < S && (kmask == nullptr || kmask[tok0 + key] != 0)) kv |= 1ull << (4 * nb + r);
+    }
+  // V^T fragment address of this lane inside a 16-key block (lane 4q + p of its group: row 4g + q, cols 4p..4p+3)
+  const int vrow = 4 * g + (i16 >> 2), vcol = 4 * (i16 & 3);
+  __syncthreads();
+  for (int q0 = 0; q0 < S; q0 += 64) {
+    const int qr = q0 + w * 16 + i16;          // this lane's query (the B / C column)
+    const bool wrows = q0 + w * 16 < S;        // wave-uniform: whole 16-query tile past S → skip its MFMAs
+    bf16x8_mf qf[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) qf[t] = qr < S ? g8(q + (tok0 + qr) * ldq + h * 64 + 32 * t + 8 * g) : zero8();
+    f32x4 sc[NB];
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      if (wrows && nb * 16 < S) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(Ks + (nb * 16 + i16) * KST + 32 * t + 8 * g), qf[t], acc,
+                                                         0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r] = ((kv >> (4 * nb + r)) & 1) ? acc[r] * c2 : -INFINITY;
+      sc[nb] = acc;
+    }
+    float m = -INFINITY;
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) m = fmaxf(m, sc[nb][r]);
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float l = 0.f;
+    v4i16_t pt[NB];
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float p = m == -INFINITY ? 0.f : exp2f(sc[nb][r] - m);
+        l += p;
+        if (thr) p = fa_drop::keep(seed, bh * 65536u + (uint32_t)qr, (uint32_t)(nb * 16 + 4 * g + r), thr) ? p * dscale : 0.f;
+        pt[nb][r] = (short)f32_to_bf16(p);
+      }
+    l += __shfl_xor(l, 16, 64);
+    l += __shfl_xor(l, 32, 64);
+    f32x4 oacc[4];
+#pragma unroll
+    for (int db = 0; db < 4; ++db) oacc[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int nb = 0; nb < NB; ++nb) {
+      if (wrows && nb * 16 < S) {   // wave-uniform (the transposing read needs every lane active)
+#pragma unroll
+        for (int db = 0; db < 4; ++db) {
+          const v4i16_t va =
+              __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16_t*)(Vs + (nb * 16 + vrow) * KST + db * 16 + vcol));
+          oacc[db] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(va, pt[nb], oacc[db], 0, 0, 0);
+        }
+      }
+    }
+    if (qr < S) {
+      const float inv = l > 0.f ? 1.f / l : 0.f;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        uint2 ov;
+        ov.x = (uint32_t)f32_to_bf16(oacc[db][0] * inv) | ((uint32_t)f32_to_bf16(oacc[db][1] * inv) << 16);
+        ov.y = (uint32_t)f32_to_bf16(oacc[db][2] * inv) | ((uint32_t)f32_to_bf16(oacc[db][3] * inv) << 16);
+        *reinterpret_cast<uint2*>(o + (tok0 + qr) * ldo + h * 64 + db * 16 + 4 * g) = ov;
+      }
+      if (g == 0) lse2[((size_t)cb * H + h) * S + qr] = l > 0.f ? m + log2f(l) : INFINITY;
+    }
+  }
+}
+
 // D[cb,h,q] = Σ_dim dO·O  (one thread per (token, head))
 __global__ __launch_bounds__(256) void attn_bwd_prep_kernel(const uint16_t* __restrict__ o, int ldo,
                                                             const uint16_t* __restrict__ dout, int lddo,
@@ -634,8 +742,17 @@ template <int SP>
 int launch_attn_fwd(const uint16_t* q, int ldq, const uint16_t* k, int ldk, const uint16_t* v, int ldv, uint16_t* o,
                     int ldo, const uint8_t* kmask, float* lse2, int CB, int S, int H, float scale, uint32_t thr,
                     float dscale, uint32_t seed, const uint32_t* seedp, hipStream_t st) {
-  hipLaunchKernelGGL(attn_fwd_kernel<SP>, dim3(H, CB), dim3(256), 0, st, q, ldq, k, ldk, v, ldv, o,
-                     ldo, kmask, lse2, S, H, scale, thr, dscale, seed, seedp);
+  // FEDML_AMD_ATTN_RP=0: the LDS-staged-probability forward (A/B)
+  static const bool rp = [] {
+    const char* e = getenv("FEDML_AMD_ATTN_RP");
+    return !(e && e[0] == '0');
+  }();
+  if (rp)
+    hipLaunchKernelGGL(attn_fwd_rp_kernel<SP>, dim3(H, CB), dim3(256), 0, st, q, ldq, k, ldk, v, ldv, o,
+                       ldo, kmask, lse2, S, H, scale, thr, dscale, seed, seedp);
+  else
+    hipLaunchKernelGGL(attn_fwd_kernel<SP>, dim3(H, CB), dim3(256), 0, st, q, ldq, k, ldk, v, ldv, o,
+                       ldo, kmask, lse2, S, H, scale, thr, dscale, seed, seedp);
   return (int)hipGetLastError();
 }
 
