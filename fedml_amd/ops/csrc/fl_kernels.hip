@@ -231,6 +231,57 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ param, co
   float* b = m2 + (int64_t)c * ld;
   float* vm = vmax ? vmax + (int64_t)c * ld : nullptr;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  // 16-B vectors (4 elements a thread) when every row is 16-B aligned: ≈ 30 B of HBM traffic per element, so the
+  // step is a pure stream
+  const bool vec = (P & 3) == 0 && (ld & 3) == 0 && ((reinterpret_cast<uintptr_t>(pc) | reinterpret_cast<uintptr_t>(a) |
+                                                      reinterpret_cast<uintptr_t>(b)) & 15) == 0 &&
+                   (reinterpret_cast<uintptr_t>(gc) & (4 * sizeof(G) - 1)) == 0 && vm == nullptr;
+  if (vec) {
+    for (int64_t i = 4 * ((int64_t)blockIdx.x * blockDim.x + threadIdx.x); i < P; i += 4 * stride) {
+      float pv[4], gv[4], av[4] = {0.f, 0.f, 0.f, 0.f}, bv[4] = {0.f, 0.f, 0.f, 0.f};
+      *reinterpret_cast<float4*>(pv) = *reinterpret_cast<const float4*>(pc + i);
+      if constexpr (sizeof(G) == 4) {
+        *reinterpret_cast<float4*>(gv) = *reinterpret_cast<const float4*>(gc + i);
+      } else {
+        const uint2 r = *reinterpret_cast<const uint2*>(gc + i);
+        gv[0] = bf16_to_f32((uint16_t)(r.x & 0xffff));
+        gv[1] = bf16_to_f32((uint16_t)(r.x >> 16));
+        gv[2] = bf16_to_f32((uint16_t)(r.y & 0xffff));
+        gv[3] = bf16_to_f32((uint16_t)(r.y >> 16));
+      }
+      if (!fresh) {
+        *reinterpret_cast<float4*>(av) = *reinterpret_cast<const float4*>(a + i);
+        *reinterpret_cast<float4*>(bv) = *reinterpret_cast<const float4*>(b + i);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float pj = pv[e], g = gv[e];
+        if (wd != 0.f) {
+          if (decoupled) pj *= (1.f - lr * wd);
+          else g += wd * pj;
+        }
+        float ma = (1.f - beta1) * g;
+        float mb = (1.f - beta2) * g * g;
+        if (!fresh) {
+          ma += beta1 * av[e];
+          mb += beta2 * bv[e];
+        }
+        av[e] = ma;
+        bv[e] = mb;
+        pv[e] = pj - step_size * ma / (sqrtf(mb) / bc2_sqrt + eps);
+      }
+      *reinterpret_cast<float4*>(a + i) = *reinterpret_cast<const float4*>(av);
+      *reinterpret_cast<float4*>(b + i) = *reinterpret_cast<const float4*>(bv);
+      *reinterpret_cast<float4*>(pc + i) = *reinterpret_cast<const float4*>(pv);
+      if (shadow) {
+        uint2 o;
+        o.x = (uint32_t)f32_to_bf16(pv[0]) | ((uint32_t)f32_to_bf16(pv[1]) << 16);
+        o.y = (uint32_t)f32_to_bf16(pv[2]) | ((uint32_t)f32_to_bf16(pv[3]) << 16);
+        *reinterpret_cast<uint2*>(shadow + (int64_t)c * ld + i) = o;
+      }
+    }
+    return;
+  }
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < P; i += stride) {
     float p = pc[i];
     float g = load1<G>(gc + i);

@@ -11,6 +11,7 @@
 // B[k 8(l>>4)..+7][col l&15]; C/D: col = l&15, row = 4(l>>4) + reg.
 #include "common.h"
 #include <cstdlib>
+#include <type_traits>
 #include "dropout.h"
 #include "detacc.h"
 
@@ -716,6 +717,184 @@ __global__ __launch_bounds__(256) void attn_bwd_dkv_kernel(const uint16_t* __res
     }
 }
 
+// Backward with the probabilities in registers (the orientation trick of attn_fwd_rp_kernel).
+// dQ: scores and dP transposed (Sᵀ = K·Qᵀ, dPᵀ = V·dOᵀ: lane = one query, keys 4g … 4g+3 of a 16-key block), so
+// dSᵀ = Pᵀ ∘ (dPᵀ − D) is the B operand of dQᵀ = Kᵀ·dSᵀ (16×16×16; Kᵀ by a transposing read) — no dS staging.
+template <int CH>
+__global__ __launch_bounds__(256) void attn_bwd_dq_rp_kernel(const uint16_t* __restrict__ q, int ldq,
+                                                             const uint16_t* __restrict__ k, int ldk,
+                                                             const uint16_t* __restrict__ v, int ldv,
+                                                             const uint16_t* __restrict__ dout, int lddo,
+                                                             const uint8_t* __restrict__ kmask,
+                                                             const float* __restrict__ lse2, const float* __restrict__ D,
+                                                             uint16_t* __restrict__ dq, int lddq, int S, int H,
+                                                             float scale, uint32_t thr, float dscale, uint32_t seed,
+                                                             const uint32_t* __restrict__ seedp) {
+  if (seedp) seed += *seedp * 1000003u;
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[CH * KST];   // CH keys at a time (CH ≥ S: staged once)
+  __shared__ __attribute__((aligned(16))) uint16_t Vs[CH * KST];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, i16 = lane & 15;
+  const int h = blockIdx.y, cb = blockIdx.z;
+  const size_t tok0 = (size_t)cb * S;
+  const size_t bhS = ((size_t)cb * H + h) * S;
+  const int qr = blockIdx.x * 64 + w * 16 + i16;     // this lane's query
+  const bool wrows = blockIdx.x * 64 + w * 16 < S;   // wave-uniform
+  bf16x8_mf qf[2], df[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    qf[t] = qr < S ? g8(q + (tok0 + qr) * ldq + h * 64 + 32 * t + 8 * g) : zero8();
+    df[t] = qr < S ? g8(dout + (tok0 + qr) * lddo + h * 64 + 32 * t + 8 * g) : zero8();
+  }
+  const float L = qr < S ? lse2[bhS + qr] : INFINITY;
+  const float Dq = qr < S ? D[bhS + qr] : 0.f;
+  const float c2 = scale * kLog2e;
+  const uint32_t bh = (uint32_t)(cb * H + h);
+  const int trow = 4 * g + (i16 >> 2), tcol = 4 * (i16 & 3);   // transposing-read address of this lane
+  f32x4 acc[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) acc[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < S; k0 += CH) {
+    __syncthreads();
+    stage_rows(Ks, k + tok0 * ldk + h * 64, ldk, k0, CH, S);
+    stage_rows(Vs, v + tok0 * ldv + h * 64, ldv, k0, CH, S);
+    __syncthreads();
+#pragma unroll
+    for (int nb = 0; nb < CH / 16; ++nb) {
+      if (!wrows || k0 + nb * 16 >= S) continue;   // wave-uniform
+      f32x4 st = {0.f, 0.f, 0.f, 0.f}, dpt = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int off = (nb * 16 + i16) * KST + 32 * t + 8 * g;
+        st = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(Ks + off), qf[t], st, 0, 0, 0);
+        dpt = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(Vs + off), df[t], dpt, 0, 0, 0);
+      }
+      v4i16_t ds;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int key = k0 + nb * 16 + 4 * g + r;
+        const bool valid = key < S && (kmask == nullptr || kmask[tok0 + key] != 0);
+        const float p = valid ? exp2f(st[r] * c2 - L) : 0.f;
+        float gg = dpt[r];
+        if (thr) gg = fa_drop::keep(seed, bh * 65536u + (uint32_t)qr, (uint32_t)key, thr) ? gg * dscale : 0.f;
+        ds[r] = (short)f32_to_bf16(p * (gg - Dq));
+      }
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        const v4i16_t ka =
+            __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16_t*)(Ks + (nb * 16 + trow) * KST + db * 16 + tcol));
+        acc[db] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ka, ds, acc[db], 0, 0, 0);
+      }
+    }
+  }
+  if (qr < S) {
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      uint2 ov;
+      ov.x = (uint32_t)f32_to_bf16(acc[db][0] * scale) | ((uint32_t)f32_to_bf16(acc[db][1] * scale) << 16);
+      ov.y = (uint32_t)f32_to_bf16(acc[db][2] * scale) | ((uint32_t)f32_to_bf16(acc[db][3] * scale) << 16);
+      *reinterpret_cast<uint2*>(dq + (tok0 + qr) * lddq + h * 64 + db * 16 + 4 * g) = ov;
+    }
+  }
+}
+
+// dK, dV: scores in the natural orientation (S = Q·Kᵀ, dP = dO·Vᵀ: lane = one key, queries 4g … 4g+3 of a
+// 16-query block), so P and dS = P ∘ (dP − D) are the B operands of dVᵀ = dOᵀ·P and dKᵀ = Qᵀ·dS (16×16×16; dOᵀ and
+// Qᵀ by transposing reads of the staged row-major tiles) — no P / dS staging.
+template <int CH>
+__global__ __launch_bounds__(256) void attn_bwd_dkv_rp_kernel(const uint16_t* __restrict__ q, int ldq,
+                                                              const uint16_t* __restrict__ k, int ldk,
+                                                              const uint16_t* __restrict__ v, int ldv,
+                                                              const uint16_t* __restrict__ dout, int lddo,
+                                                              const uint8_t* __restrict__ kmask,
+                                                              const float* __restrict__ lse2,
+                                                              const float* __restrict__ D, uint16_t* __restrict__ dk,
+                                                              int lddk, uint16_t* __restrict__ dv, int lddv, int S,
+                                                              int H, float scale, uint32_t thr, float dscale,
+                                                              uint32_t seed, const uint32_t* __restrict__ seedp) {
+  if (seedp) seed += *seedp * 1000003u;
+  __shared__ __attribute__((aligned(16))) uint16_t Qs[CH * KST];   // CH queries at a time (CH ≥ S: staged once)
+  __shared__ __attribute__((aligned(16))) uint16_t dOs[CH * KST];
+  __shared__ __attribute__((aligned(16))) float Ls[CH], Dsh[CH];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, g = lane >> 4, i16 = lane & 15;
+  const int h = blockIdx.y, cb = blockIdx.z;
+  const size_t tok0 = (size_t)cb * S;
+  const size_t bhS = ((size_t)cb * H + h) * S;
+  const int kr = blockIdx.x * 64 + w * 16 + i16;     // this lane's key
+  const bool wkeys = blockIdx.x * 64 + w * 16 < S;   // wave-uniform
+  bf16x8_mf kf[2], vf[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    kf[t] = kr < S ? g8(k + (tok0 + kr) * ldk + h * 64 + 32 * t + 8 * g) : zero8();
+    vf[t] = kr < S ? g8(v + (tok0 + kr) * ldv + h * 64 + 32 * t + 8 * g) : zero8();
+  }
+  const bool kvalid = kr < S && (kmask == nullptr || kmask[tok0 + kr] != 0);
+  const float c2 = scale * kLog2e;
+  const uint32_t bh = (uint32_t)(cb * H + h);
+  const int trow = 4 * g + (i16 >> 2), tcol = 4 * (i16 & 3);
+  f32x4 adk[4], adv[4];
+#pragma unroll
+  for (int db = 0; db < 4; ++db) adk[db] = adv[db] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int q0 = 0; q0 < S; q0 += CH) {
+    __syncthreads();
+    stage_rows(Qs, q + tok0 * ldq + h * 64, ldq, q0, CH, S);
+    stage_rows(dOs, dout + tok0 * lddo + h * 64, lddo, q0, CH, S);
+    for (int i = threadIdx.x; i < CH; i += 256) {
+      Ls[i] = q0 + i < S ? lse2[bhS + q0 + i] : INFINITY;
+      Dsh[i] = q0 + i < S ? D[bhS + q0 + i] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int nb = 0; nb < CH / 16; ++nb) {
+      if (!wkeys || q0 + nb * 16 >= S) continue;   // wave-uniform
+      f32x4 s_ = {0.f, 0.f, 0.f, 0.f}, dp = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int off = (nb * 16 + i16) * KST + 32 * t + 8 * g;
+        s_ = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(Qs + off), kf[t], s_, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(lds8(dOs + off), vf[t], dp, 0, 0, 0);
+      }
+      const float4 Lq = *reinterpret_cast<const float4*>(Ls + nb * 16 + 4 * g);
+      const float4 Dq = *reinterpret_cast<const float4*>(Dsh + nb * 16 + 4 * g);
+      const float Lr[4] = {Lq.x, Lq.y, Lq.z, Lq.w}, Dr[4] = {Dq.x, Dq.y, Dq.z, Dq.w};
+      v4i16_t pp, dss;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int qq = q0 + nb * 16 + 4 * g + r;
+        const bool valid = kvalid && qq < S;
+        const float p = valid ? exp2f(s_[r] * c2 - Lr[r]) : 0.f;
+        float pd = p, gg = dp[r];
+        if (thr) {
+          const bool kp = fa_drop::keep(seed, bh * 65536u + (uint32_t)qq, (uint32_t)kr, thr);
+          pd = kp ? p * dscale : 0.f;
+          gg = kp ? gg * dscale : 0.f;
+        }
+        pp[r] = (short)f32_to_bf16(pd);
+        dss[r] = (short)f32_to_bf16(p * (gg - Dr[r]));
+      }
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        const int ao = (nb * 16 + trow) * KST + db * 16 + tcol;
+        const v4i16_t oa = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16_t*)(dOs + ao));
+        const v4i16_t qa = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4i16_t*)(Qs + ao));
+        adv[db] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(oa, pp, adv[db], 0, 0, 0);
+        adk[db] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(qa, dss, adk[db], 0, 0, 0);
+      }
+    }
+  }
+  if (kr < S) {
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      uint2 kv2, vv2;
+      kv2.x = (uint32_t)f32_to_bf16(adk[db][0] * scale) | ((uint32_t)f32_to_bf16(adk[db][1] * scale) << 16);
+      kv2.y = (uint32_t)f32_to_bf16(adk[db][2] * scale) | ((uint32_t)f32_to_bf16(adk[db][3] * scale) << 16);
+      vv2.x = (uint32_t)f32_to_bf16(adv[db][0]) | ((uint32_t)f32_to_bf16(adv[db][1]) << 16);
+      vv2.y = (uint32_t)f32_to_bf16(adv[db][2]) | ((uint32_t)f32_to_bf16(adv[db][3]) << 16);
+      *reinterpret_cast<uint2*>(dk + (tok0 + kr) * lddk + h * 64 + db * 16 + 4 * g) = kv2;
+      *reinterpret_cast<uint2*>(dv + (tok0 + kr) * lddv + h * 64 + db * 16 + 4 * g) = vv2;
+    }
+  }
+}
+
 template <int NV>
 int launch_ln_fwd(const uint16_t* h, const uint16_t* res, int R, int d, int rpc, const float* g, const float* b,
                   float eps, uint32_t thr, float dscale, uint32_t seed, const uint32_t* seedp, uint16_t* y,
@@ -838,11 +1017,32 @@ FA_EXPORT int fa_attn_bwd(const void* q, int ldq, const void* k, int ldk, const 
   hipLaunchKernelGGL(attn_bwd_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream,
                      (const uint16_t*)o, ldo, (const uint16_t*)dout, lddo, Dbuf, CB * S, S, H);
   const dim3 grid((S + 63) / 64, H, CB);
-  hipLaunchKernelGGL(attn_bwd_dq_kernel, grid, dim3(256), 0, stream, (const uint16_t*)q, ldq, (const uint16_t*)k, ldk,
-                     (const uint16_t*)v, ldv, (const uint16_t*)dout, lddo, kmask, lse2, Dbuf, (uint16_t*)dq, lddq, S, H,
-                     scale, thr, dscale, seed, seedp);
-  hipLaunchKernelGGL(attn_bwd_dkv_kernel, grid, dim3(256), 0, stream, (const uint16_t*)q, ldq, (const uint16_t*)k,
-                     ldk, (const uint16_t*)v, ldv, (const uint16_t*)dout, lddo, kmask, lse2, Dbuf, (uint16_t*)dk, lddk,
-                     (uint16_t*)dv, lddv, S, H, scale, thr, dscale, seed, seedp);
+  static const bool rp = [] {   // FEDML_AMD_ATTN_RP=0: the LDS-staged dS / P kernels (A/B)
+    const char* e = getenv("FEDML_AMD_ATTN_RP");
+    return !(e && e[0] == '0');
+  }();
+  auto Q = (const uint16_t*)q;
+  auto K = (const uint16_t*)k;
+  auto V = (const uint16_t*)v;
+  auto DO = (const uint16_t*)dout;
+  if (rp) {   // S ≤ 128: the whole sequence staged once per workgroup; longer: 64-row chunks (more workgroups per
+             // CU — measured faster at S = 197, slower at 128; profiles/r6_attention_rp.txt)
+    auto go = [&](auto sp) {
+      constexpr int SP = decltype(sp)::value;
+      hipLaunchKernelGGL(attn_bwd_dq_rp_kernel<SP>, grid, dim3(256), 0, stream, Q, ldq, K, ldk, V, ldv, DO, lddo,
+                         kmask, lse2, Dbuf, (uint16_t*)dq, lddq, S, H, scale, thr, dscale, seed, seedp);
+      hipLaunchKernelGGL(attn_bwd_dkv_rp_kernel<SP>, grid, dim3(256), 0, stream, Q, ldq, K, ldk, V, ldv, DO, lddo,
+                         kmask, lse2, Dbuf, (uint16_t*)dk, lddk, (uint16_t*)dv, lddv, S, H, scale, thr, dscale, seed,
+                         seedp);
+    };
+    if (S <= 64) go(std::integral_constant<int, 64>{});
+    else if (S <= 128) go(std::integral_constant<int, 128>{});
+    else go(std::integral_constant<int, 64>{});
+    return (int)hipGetLastError();
+  }
+  hipLaunchKernelGGL(attn_bwd_dq_kernel, grid, dim3(256), 0, stream, Q, ldq, K, ldk, V, ldv, DO, lddo, kmask, lse2,
+                     Dbuf, (uint16_t*)dq, lddq, S, H, scale, thr, dscale, seed, seedp);
+  hipLaunchKernelGGL(attn_bwd_dkv_kernel, grid, dim3(256), 0, stream, Q, ldq, K, ldk, V, ldv, DO, lddo, kmask, lse2,
+                     Dbuf, (uint16_t*)dk, lddk, (uint16_t*)dv, lddv, S, H, scale, thr, dscale, seed, seedp);
   return (int)hipGetLastError();
 }

@@ -63,9 +63,10 @@ def test_sgd_step(momentum, mu, grad_dtype):
             assert torch.allclose(mg.cpu(), mc, atol=1e-5, rtol=1e-5)
 
 
+@pytest.mark.parametrize("P", [2049, 2048])   # scalar path; 16-B vector path
 @pytest.mark.parametrize("amsgrad,decoupled", [(False, False), (True, False), (False, True)])
-def test_adam_step(amsgrad, decoupled):
-    C, P = 3, 2049
+def test_adam_step(amsgrad, decoupled, P):
+    C = 3
     p = torch.randn(C, P)
     g = torch.randn(C, P)
     st = [torch.rand(C, P), torch.rand(C, P), torch.rand(C, P)]
