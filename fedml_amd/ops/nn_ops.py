@@ -67,6 +67,14 @@ def set_f32_mma_mode(mode: str) -> str:
     return {v: k for k, v in F32_MMA_MODES.items()}[prev]
 
 
+def set_expand_kernel(on: bool) -> bool:
+    """Route fp32 1×1 / stride-1 planes → 4·planes forwards (the bottleneck's last conv) to the dedicated expand
+    kernel (``conv_kernels.hip`` c1x, the default; env FEDML_AMD_C1X) or to the generic implicit GEMM. Returns the
+    previous setting (-1 → not yet read from the environment: reported as on)."""
+    prev = int(_fn("fa_set_c1x")(_i(1 if on else 0)))
+    return prev != 0
+
+
 class PackSeg(ctypes.Structure):
     _fields_ = [("src_off", ctypes.c_int64), ("dst_f", ctypes.c_int64), ("dst_b", ctypes.c_int64),
                 ("cout", ctypes.c_int), ("cin", ctypes.c_int), ("kh", ctypes.c_int), ("kw", ctypes.c_int),

@@ -1,0 +1,21 @@
+#!/bin/bash
+# round 6, call B2: dedicated fp32 1x1 expand forward (c1x) — kernel test, native fp32 step tests, headline and
+# 13-client A/B against the generic kernel (FEDML_AMD_C1X=0)
+cd "$(dirname "$0")/../.." && O=gpurun_out/r6b2 && mkdir -p $O
+export TMPDIR=/tmp HSA_ENABLE_IPC_MODE_LEGACY=0
+( while true; do date > $O/heartbeat; sleep 30; done ) &
+HB=$!
+bash scripts/gpu_steps.sh \
+ "timeout -k 10 300 python -u -m pytest tests/test_conv1x1_expand_gpu.py -x -v --timeout 200 --timeout-method thread -p no:cacheprovider > $O/t_c1x.txt 2>&1" \
+ "timeout -k 10 600 python -u -m pytest tests/test_native_resnet_fp32_gpu.py tests/test_recompute_y_gpu.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $O/t_fp32.txt 2>&1" \
+ "timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/head1.txt 2>&1" \
+ "FEDML_AMD_C1X=0 timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/head0.txt 2>&1" \
+ "timeout -k 10 300 python -u bench.py --clients 13 --steps 20 --warmup 5 > $O/c13_1.txt 2>&1" \
+ "FEDML_AMD_C1X=0 timeout -k 10 300 python -u bench.py --clients 13 --steps 20 --warmup 5 > $O/c13_0.txt 2>&1" \
+ "FEDML_AMD_SIDE_WGRAD=0 FEDML_AMD_C3W_BATCH=0 timeout -k 10 300 python -u scripts/layer_prof.py --model resnet56 --C 100 --N 64 --dtype fp32 > $O/lp100.txt 2>&1"
+rc=$?
+kill $HB
+for f in t_c1x t_fp32; do echo "$f: $(grep -E 'passed|failed' $O/$f.txt | tail -1)"; done
+for f in head1 head0 c13_1 c13_0; do echo "$f: $(tail -1 $O/$f.txt | cut -c1-150)"; done
+grep -E 'conv_fwd  ' $O/lp100.txt | head; tail -3 $O/lp100.txt
+exit $rc
