@@ -1538,7 +1538,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1_pbout_f32_kernel(ConvArgs a, i
 }
 
 static int g_enable = -1;   // FEDML_AMD_C1X (default on); fa_set_c1x overrides
-static int nt_stores() {     // FEDML_AMD_C1X_NT: non-temporal output stores (A/B)
+static int nt_stores() {     // FEDML_AMD_C1X_NT: non-temporal output stores (measured slower: off; profiles/r6_c1x_ab.txt)
   static int v = -1;
   if (v < 0) {
     const char* e = getenv("FEDML_AMD_C1X_NT");
