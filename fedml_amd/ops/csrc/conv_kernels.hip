@@ -1538,6 +1538,25 @@ __global__ __launch_bounds__(256, 2) void conv1x1_pbout_f32_kernel(ConvArgs a, i
 }
 
 static int g_enable = -1;   // FEDML_AMD_C1X (default on); fa_set_c1x overrides
+// launch sizing (tuning): total workgroup target and the minimum pixels per wave, which bounds how often a wave
+// refills its weight slice (16 KB per wave at 64 input channels) for few clients
+static int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
+static int wg_target() {
+  static int v = -1;
+  if (v < 0) v = std::max(64, env_int("FEDML_AMD_C1X_WGS", 2048));
+  return v;
+}
+// expand: ≥ 128 px per wave (13 clients, 8² stage: 41 → 34 µs per call); block-output-forming: no minimum (its
+// 8² stage measured 63 → 80 µs at 128) — profiles/r6_c1x_sizing.txt
+static int min_px_per_wave(bool expand) {
+  static int v[2] = {-1, -1};
+  if (v[expand] < 0) v[expand] = std::max(16, env_int(expand ? "FEDML_AMD_C1X_MINPX" : "FEDML_AMD_C1X_PB_MINPX",
+                                                      expand ? 128 : 16));
+  return v[expand];
+}
 static int nt_stores() {     // FEDML_AMD_C1X_NT: non-temporal output stores (measured slower: off; profiles/r6_c1x_ab.txt)
   static int v = -1;
   if (v < 0) {
@@ -1555,8 +1574,8 @@ static int launch_t(const ConvArgs& a, int C, hipStream_t stream) {
   const int groups = (M + 16 * U - 1) / (16 * U);
   // ≈ 2048 workgroups over the launch (8 per CU), ≥ 2 pixel groups per wave
   const int pc = fa_plan_c(C);
-  const int wgs_target = std::max(1, (2048 + pc - 1) / pc);
-  const int gpw = std::max(2, (groups + wgs_target * R - 1) / (wgs_target * R));
+  const int wgs_target = std::max(1, (wg_target() + pc - 1) / pc);
+  const int gpw = std::max(std::max(2, min_px_per_wave(true) / (16 * U)), (groups + wgs_target * R - 1) / (wgs_target * R));
   const int gx = (groups + R * gpw - 1) / (R * gpw);
   hipLaunchKernelGGL((conv1x1_expand_f32_kernel<CIN, S, PRO, U>), dim3(gx, C), dim3(256), 0, stream, a, gpw,
                      nt_stores());
@@ -1575,7 +1594,8 @@ static int try_launch(const ConvArgs& a, int Cin, int Cout, int KH, int KW, int 
   // generic kernel: both must sum in the same order, so it stays there
   if (!g_enable || !std::is_same<P, prec::F32>::value || !a.out) return 0;
   if (KH != 1 || KW != 1 || stride != 1 || pad != 0 || a.Ho != a.Hs || a.Wo != a.Ws || Cout != 4 * Cin) return 0;
-  if (a.ldk % 4 != 0 || a.wpk_ld % 4 != 0) return 0;
+  // whole 16-pixel tiles per image: a tile never straddles the valid / padding boundary of a ragged client
+  if (a.ldk % 4 != 0 || a.wpk_ld % 4 != 0 || (a.Ho * a.Wo) % 16 != 0) return 0;
   switch ((Cin << 1) | (bnrelu ? 1 : 0)) {
     case (16 << 1) | 1: *rc = launch_t<16, 1, PRO_BNRELU>(a, C, stream); return 1;
     case (32 << 1) | 1: *rc = launch_t<32, 2, PRO_BNRELU>(a, C, stream); return 1;
@@ -1591,8 +1611,8 @@ template <int CIN, int COUT>
 static int launch_pbout_t(const ConvArgs& a, int C, hipStream_t stream) {
   const int tiles = a.Nb * a.Ho * a.Wo / 16;
   const int pc = fa_plan_c(C);
-  const int wgs_target = std::max(1, (2048 + pc - 1) / pc);
-  const int gpw = std::max(1, (tiles + wgs_target * 4 - 1) / (wgs_target * 4));
+  const int wgs_target = std::max(1, (wg_target() + pc - 1) / pc);
+  const int gpw = std::max(min_px_per_wave(false) / 16, (tiles + wgs_target * 4 - 1) / (wgs_target * 4));
   const int gx = (tiles + 4 * gpw - 1) / (4 * gpw);
   hipLaunchKernelGGL((conv1x1_pbout_f32_kernel<CIN, COUT>), dim3(gx, C), dim3(256), 0, stream, a, gpw, nt_stores());
   return (int)hipGetLastError();

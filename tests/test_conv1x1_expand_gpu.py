@@ -14,7 +14,8 @@ def rel(a, b):
 
 @pytest.mark.parametrize("cin,hw,bnrelu,pivot,ragged", [(16, 32, True, True, False), (32, 16, True, False, True),
                                                          (64, 8, True, True, True), (16, 32, False, False, False),
-                                                         (64, 8, False, True, False)])
+                                                         (64, 8, False, True, False),
+                                                         (16, 7, True, True, True)])   # 49 px: generic fallback
 def test_expand_kernel_matches_torch_and_generic(cin, hw, bnrelu, pivot, ragged):
     from fedml_amd.ops import nn_ops
     torch.manual_seed(11)
