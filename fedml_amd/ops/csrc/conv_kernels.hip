@@ -1377,7 +1377,9 @@ __global__ __launch_bounds__(256, 2) void conv1x1_expand_f32_kernel(ConvArgs a, 
 // output once and feeds the transposed MFMA (D[channel][pixel]) from registers; the weights
 // [COUT][CIN] sit in LDS (pitch CIN + 4: the 16 rows a ds_read_b128 touches start in different banks), the BN
 // vectors too. The operands stream in 64-channel chunks (8 16-B loads per lane), one chunk ahead.
-template <int CIN, int COUT>
+// BOUT = false: the plain 1×1 forward of the same shapes (operand = the stored block output as is, nothing written
+// but y): the unfused path's conv then sums in exactly the fused kernel's order — both paths give the same bits
+template <int CIN, int COUT, bool BOUT>
 __global__ __launch_bounds__(256, 2) void conv1x1_pbout_f32_kernel(ConvArgs a, int gpw, int nts) {
   constexpr int KB = CIN / 16, NT = COUT / 16, LDW = CIN + 4;
   const int c = blockIdx.y;
@@ -1391,8 +1393,8 @@ __global__ __launch_bounds__(256, 2) void conv1x1_pbout_f32_kernel(ConvArgs a, i
   __shared__ __attribute__((aligned(16))) float wl[COUT * LDW];
   __shared__ __attribute__((aligned(16))) float vs[CIN], vt[CIN], vrs[CIN], vrt[CIN];
   __shared__ float red[4][COUT][2];
-  const bool ds = a.vec2 != nullptr;   // downsample-BN shortcut
-  for (int i = threadIdx.x; i < CIN; i += 256) {
+  const bool ds = BOUT && a.vec2 != nullptr;   // downsample-BN shortcut
+  for (int i = threadIdx.x; i < (BOUT ? CIN : 0); i += 256) {
     float s_, t_;
     if (a.lz0) {
       bn_lazy_fwd(a.lz0, c, i, blockIdx.x == 0, s_, t_);
@@ -1436,8 +1438,8 @@ __global__ __launch_bounds__(256, 2) void conv1x1_pbout_f32_kernel(ConvArgs a, i
 
   const int64_t cin_off = (int64_t)c * M * CIN;
   const float* ysrc = reinterpret_cast<const float*>(a.src) + cin_off;
-  const float* rsrc = reinterpret_cast<const float*>(a.src2) + cin_off;
-  float* bout = reinterpret_cast<float*>(a.pro_out) + cin_off;
+  const float* rsrc = BOUT ? reinterpret_cast<const float*>(a.src2) + cin_off : nullptr;
+  float* bout = BOUT ? reinterpret_cast<float*>(a.pro_out) + cin_off : nullptr;
   float* out = reinterpret_cast<float*>(a.out) + (int64_t)c * M * COUT;
   const int tbeg = ((int)blockIdx.x * 4 + wid) * gpw;
   const int tend = min(tiles, tbeg + gpw);
@@ -1449,7 +1451,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1_pbout_f32_kernel(ConvArgs a, i
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       py[k] = *reinterpret_cast<const float4*>(ysrc + px * CIN + 64 * q + 16 * k + 4 * g);
-      pr[k] = *reinterpret_cast<const float4*>(rsrc + px * CIN + 64 * q + 16 * k + 4 * g);
+      if (BOUT) pr[k] = *reinterpret_cast<const float4*>(rsrc + px * CIN + 64 * q + 16 * k + 4 * g);
     }
   };
   if (tbeg < tend) load(tbeg, 0);
@@ -1466,15 +1468,16 @@ __global__ __launch_bounds__(256, 2) void conv1x1_pbout_f32_kernel(ConvArgs a, i
     for (int q = 0; q < NQ; ++q) {
       float4 yv[4], rv[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) { yv[k] = py[k]; rv[k] = pr[k]; }
+      for (int k = 0; k < 4; ++k) { yv[k] = py[k]; rv[k] = BOUT ? pr[k] : py[k]; }
       if (q + 1 < NQ) load(tile, q + 1);
       else if (tile + 1 < tend) load(tile + 1, 0);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         const int ci = 64 * q + 16 * k + 4 * g;
         const int cl = 64 * q + 16 * k + lo;   // == ci
-        const float4 s4 = *reinterpret_cast<const float4*>(vs + cl), t4 = *reinterpret_cast<const float4*>(vt + cl);
         float f[4] = {yv[k].x, yv[k].y, yv[k].z, yv[k].w};
+        if (BOUT) {
+        const float4 s4 = *reinterpret_cast<const float4*>(vs + cl), t4 = *reinterpret_cast<const float4*>(vt + cl);
         const float r[4] = {rv[k].x, rv[k].y, rv[k].z, rv[k].w};
         const float sv[4] = {s4.x, s4.y, s4.z, s4.w}, tv[4] = {t4.x, t4.y, t4.z, t4.w};
 #pragma unroll
@@ -1491,6 +1494,7 @@ __global__ __launch_bounds__(256, 2) void conv1x1_pbout_f32_kernel(ConvArgs a, i
 #pragma unroll
         for (int j = 0; j < 4; ++j) f[j] = fmaxf(f[j], 0.f);
         st4(bout + px * CIN + ci, make_float4(f[0], f[1], f[2], f[3]), nts);
+        }
 #pragma unroll
         for (int nt = 0; nt < NT; ++nt) {
           const float4 w4 = *reinterpret_cast<const float4*>(wl + (16 * nt + px_l) * LDW + cl);
@@ -1607,14 +1611,15 @@ static int try_launch(const ConvArgs& a, int Cin, int Cout, int KH, int KW, int 
   }
 }
 
-template <int CIN, int COUT>
+template <int CIN, int COUT, bool BOUT = true>
 static int launch_pbout_t(const ConvArgs& a, int C, hipStream_t stream) {
   const int tiles = a.Nb * a.Ho * a.Wo / 16;
   const int pc = fa_plan_c(C);
   const int wgs_target = std::max(1, (wg_target() + pc - 1) / pc);
   const int gpw = std::max(min_px_per_wave(false) / 16, (tiles + wgs_target * 4 - 1) / (wgs_target * 4));
   const int gx = (tiles + 4 * gpw - 1) / (4 * gpw);
-  hipLaunchKernelGGL((conv1x1_pbout_f32_kernel<CIN, COUT>), dim3(gx, C), dim3(256), 0, stream, a, gpw, nt_stores());
+  hipLaunchKernelGGL((conv1x1_pbout_f32_kernel<CIN, COUT, BOUT>), dim3(gx, C), dim3(256), 0, stream, a, gpw,
+                     nt_stores());
   return (int)hipGetLastError();
 }
 
@@ -1636,6 +1641,25 @@ static int try_pbout(const ConvArgs& a, int Cin, int Cout, int C, hipStream_t st
     case 128032: *rc = launch_pbout_t<128, 32>(a, C, stream); return 1;
     case 256064: *rc = launch_pbout_t<256, 64>(a, C, stream); return 1;
     case 128064: *rc = launch_pbout_t<128, 64>(a, C, stream); return 1;
+    default: return 0;
+  }
+}
+
+// the plain (PRO_NONE) 1×1 / stride-1 forward of the block-output-forming shapes: same kernel, same sums
+template <class P>
+static int try_plain_reduce(const ConvArgs& a, int Cin, int Cout, int KH, int KW, int stride, int pad, int C,
+                            hipStream_t stream, int* rc) {
+  if (g_enable < 0) {
+    const char* e = getenv("FEDML_AMD_C1X");
+    g_enable = e ? (atoi(e) != 0) : 1;
+  }
+  if (!g_enable || !std::is_same<P, prec::F32>::value || !a.out) return 0;
+  if (KH != 1 || KW != 1 || stride != 1 || pad != 0 || a.Ho != a.Hs || a.Wo != a.Ws) return 0;
+  if (a.ldk % 4 != 0 || a.wpk_ld % 4 != 0 || (a.Ho * a.Wo) % 16 != 0) return 0;
+  switch (Cin * 1000 + Cout) {
+    case 128032: *rc = launch_pbout_t<128, 32, false>(a, C, stream); return 1;
+    case 256064: *rc = launch_pbout_t<256, 64, false>(a, C, stream); return 1;
+    case 128064: *rc = launch_pbout_t<128, 64, false>(a, C, stream); return 1;
     default: return 0;
   }
 }
@@ -1664,6 +1688,7 @@ static int conv_fwd(const void* x, const void* wpk, int64_t wpk_ld, const float*
   a.lz1 = fa_take_lazy(1);
   int rc = 0;
   if (c1x::try_launch<P>(a, Cin, Cout, KH, KW, stride, pad, C, pscale != nullptr, stream, &rc)) return rc;
+  if (!pscale && c1x::try_plain_reduce<P>(a, Cin, Cout, KH, KW, stride, pad, C, stream, &rc)) return rc;
   if (pscale)
     return dispatch_nt<P, AOP_ACT, PRO_BNRELU, MODE_FWD, EPI_FWD>(Cout, a, C, stream);
   return dispatch_nt<P, AOP_ACT, PRO_NONE, MODE_FWD, EPI_FWD>(Cout, a, C, stream);

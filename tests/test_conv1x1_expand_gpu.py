@@ -115,3 +115,29 @@ def test_pbout_kernel_matches_torch_and_generic(monkeypatch, cin, cout, hw, ds, 
                 assert bool((y[c, n:] == 7.0).all()) and bool((bout[c, n:] == 5.0).all()), (on, c)
     assert torch.equal(outs[True][0], outs[False][0])
     assert rel(outs[True][1], outs[False][1]) < 1e-5
+
+
+@pytest.mark.parametrize("cin,cout,hw", [(128, 32, 16), (256, 64, 8), (128, 64, 16)])
+def test_plain_reduce_matches_pbout_bitwise(cin, cout, hw):
+    """The plain 1×1 forward of the block-output-forming shapes (operand = the stored block output) runs the same
+    c1x kernel without the prologue, so unfused (block_out pass + conv) and fused paths produce the same bits."""
+    from fedml_amd.ops import nn_ops
+    torch.manual_seed(9)
+    C, N = 2, 4
+    ldk = (cin + 31) // 32 * 32 + 8
+    wf = torch.zeros(C, cout, ldk, device=DEV)
+    wf[:, :, :cin] = torch.randn(C, cout, cin, device=DEV) * 0.1
+    yp, res = torch.randn(C, N, hw, hw, cin, device=DEV), torch.randn(C, N, hw, hw, cin, device=DEV)
+    s, t = torch.rand(C, cin, device=DEV) + 0.5, torch.randn(C, cin, device=DEV) * 0.3
+    piv = torch.randn(C, cout, device=DEV) * 0.1
+    bout = torch.empty(C, N, hw, hw, cin, device=DEV)
+    y1, st1 = torch.empty(C, N, hw, hw, cout, device=DEV), torch.zeros(C, cout, 2, device=DEV)
+    nn_ops.conv_fwd_pbout(yp, s, t, res, None, None, bout, wf, cout * ldk, y1, st1, C, N, hw, hw, cin, cout, ldk, 1,
+                          pivot=piv)
+    y2, st2 = torch.empty_like(y1), torch.zeros_like(st1)
+    nn_ops.conv_fwd(bout, wf, cout * ldk, None, None, y2, st2, C, N, hw, hw, cin, cout, 1, 1, 1, 0, hw, hw, ldk, 1,
+                    pivot=piv)
+    torch.cuda.synchronize()
+    assert torch.equal(y1, y2)
+    ref = (bout.reshape(C, -1, cin) @ wf[:, :, :cin].transpose(1, 2)).reshape_as(y1) - piv.view(C, 1, 1, 1, cout)
+    assert rel(y2, ref) < 1e-5
