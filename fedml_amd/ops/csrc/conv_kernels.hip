@@ -1375,13 +1375,15 @@ __global__ __launch_bounds__(256, 2) void conv1x1_expand_f32_kernel(ConvArgs a, 
 // 4-channel pieces of y and the shortcut r for every 16-channel input block, forms a = relu(y·s + t + r)
 // (r → r·rs + rt behind a downsample BN; block_out_kernel's operation order, so the same bits), writes the block
 // output once and feeds the transposed MFMA (D[channel][pixel]) from registers; the weights
-// [COUT][CIN] sit in LDS (pitch CIN + 4: the 16 rows a ds_read_b128 touches start in different banks), the BN
+// [COUT][CIN] sit in LDS (pitch CIN + 8, bank-conflict free), the BN
 // vectors too. The operands stream in 64-channel chunks (8 16-B loads per lane), one chunk ahead.
 // BOUT = false: the plain 1×1 forward of the same shapes (operand = the stored block output as is, nothing written
 // but y): the unfused path's conv then sums in exactly the fused kernel's order — both paths give the same bits
 template <int CIN, int COUT, bool BOUT>
 __global__ __launch_bounds__(256, 2) void conv1x1_pbout_f32_kernel(ConvArgs a, int gpw, int nts) {
-  constexpr int KB = CIN / 16, NT = COUT / 16, LDW = CIN + 4;
+  // LDW ≡ 8 (mod 64) dwords: the 16 rows × 4 lane groups of a ds_read_b128 fragment read (row px_l, column 4·g)
+  // land on 16 distinct 4-bank slots (CIN + 4 measured 56–64 % bank-conflict cycles)
+  constexpr int KB = CIN / 16, NT = COUT / 16, LDW = CIN + 8;
   const int c = blockIdx.y;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int g = lane >> 4, px_l = lane & 15;
