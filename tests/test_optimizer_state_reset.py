@@ -75,7 +75,7 @@ def test_adam_first_step_ignores_stale_moments_gpu():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("C,P,ld", [(3, 1001, 1001), (5, 4096, 4100), (2, 7, 9)])
+@pytest.mark.parametrize("C,P,ld", [(3, 1001, 1001), (5, 4096, 4100), (2, 7, 9), (19, 5000, 5004), (17, 333, 333)])
 def test_broadcast_rows_gpu(C, P, ld):
     buf = torch.randn(C, ld, device="cuda")
     dst = buf[:, :P]
