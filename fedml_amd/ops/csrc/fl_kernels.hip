@@ -329,10 +329,10 @@ FA_EXPORT int fa_adam_step(float* param, const void* grad, int grad_is_bf16, flo
 // slot. float4 stores when the rows are 16-B aligned; the source row stays in L2 across the C rows.
 // blockIdx.y takes BR_ROWS destination rows: each source vector is read once per BR_ROWS rows (a 32-client
 // transformer arena: 1.4 instead of 11 GB of source reads, the source row being larger than the MALL)
-constexpr int BR_ROWS = 8;
+// (FEDML_AMD_BCAST_ROWS overrides the 8, for A/B runs)
 __global__ __launch_bounds__(256) void broadcast_rows_kernel(float* __restrict__ dst, const float* __restrict__ src,
-                                                             int64_t P, int64_t ld, int vec, int C) {
-  const int r0 = blockIdx.y * BR_ROWS, nr = min(BR_ROWS, C - r0);
+                                                             int64_t P, int64_t ld, int vec, int C, int rows) {
+  const int r0 = blockIdx.y * rows, nr = min(rows, C - r0);
   float* d = dst + (int64_t)r0 * ld;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -407,8 +407,13 @@ FA_EXPORT int fa_embedding_grad_f32(float* base, int64_t ld, const int64_t* ids,
 FA_EXPORT int fa_broadcast_rows(float* dst, const float* src, int C, int64_t P, int64_t ld, hipStream_t stream) {
   if (C <= 0 || P <= 0) return 0;
   const int vec = ((uintptr_t)dst % 16 == 0) && ((uintptr_t)src % 16 == 0) && (ld % 4 == 0);
-  dim3 grid(fa_grid(vec ? (P + 3) / 4 : P, 256, 1024), (C + BR_ROWS - 1) / BR_ROWS);
-  hipLaunchKernelGGL(broadcast_rows_kernel, grid, dim3(256), 0, stream, dst, src, P, ld, vec, C);
+  static int rows = -1;
+  if (rows < 0) {
+    const char* e = getenv("FEDML_AMD_BCAST_ROWS");
+    rows = e && atoi(e) > 0 ? atoi(e) : 8;
+  }
+  dim3 grid(fa_grid(vec ? (P + 3) / 4 : P, 256, 1024), (C + rows - 1) / rows);
+  hipLaunchKernelGGL(broadcast_rows_kernel, grid, dim3(256), 0, stream, dst, src, P, ld, vec, C, rows);
   return (int)hipGetLastError();
 }
 
@@ -823,10 +828,22 @@ __global__ __launch_bounds__(256) void compress_accumulate_kernel(
     float* res = reinterpret_cast<float*>(residual_rows ? residual_rows[c] : 0ull);
     const float* pc = params + (int64_t)c * ldp;
     float v[4];
+    // 16-B accesses when this lane's 4 values are in range and the rows are 16-B aligned (one load per operand
+    // instead of four: the kernel is a stream over [C, P] params + residuals)
+    const bool vec = base + 3 < n && (((uintptr_t)(pc + base) | (uintptr_t)(res ? res + base : pc + base)) & 15) == 0;
+    if (vec) {
+      const float4 p4 = *reinterpret_cast<const float4*>(pc + base);
+      const float4 r4 = res ? *reinterpret_cast<const float4*>(res + base) : make_float4(0.f, 0.f, 0.f, 0.f);
+      v[0] = p4.x - g[0] + r4.x;
+      v[1] = p4.y - g[1] + r4.y;
+      v[2] = p4.z - g[2] + r4.z;
+      v[3] = p4.w - g[3] + r4.w;
+    } else {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int64_t i = base + j;
-      v[j] = (i < n) ? pc[i] - g[j] + (res ? res[i] : 0.f) : 0.f;
+      for (int j = 0; j < 4; ++j) {
+        const int64_t i = base + j;
+        v[j] = (i < n) ? pc[i] - g[j] + (res ? res[i] : 0.f) : 0.f;
+      }
     }
     float amax = fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3])));
     amax = wave_max(amax);
@@ -855,11 +872,15 @@ __global__ __launch_bounds__(256) void compress_accumulate_kernel(
       back[2] = __builtin_amdgcn_cvt_f32_fp8(pk, 2) * scale;
       back[3] = __builtin_amdgcn_cvt_f32_fp8(pk, 3) * scale;
     }
+    if (vec && res) {
+      *reinterpret_cast<float4*>(res + base) = make_float4(v[0] - back[0], v[1] - back[1], v[2] - back[2], v[3] - back[3]);
+    } else if (res) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      if (res && base + j < n) res[base + j] = v[j] - back[j];
-      a[j] += w * back[j];
+      for (int j = 0; j < 4; ++j)
+        if (base + j < n) res[base + j] = v[j] - back[j];
     }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) a[j] += w * back[j];
   }
 #pragma unroll
   for (int j = 0; j < 4; ++j)

@@ -315,6 +315,15 @@ class ClientBatchEngine:
         self._shadow_stale = True
         with torch.no_grad():
             ops.broadcast_rows_(self.params, flat.reshape(-1))
+            sh = self._shadow
+            if (sh is not None and sh.is_cuda and flat.is_cuda and flat.dtype == torch.float32
+                    and sh.shape[1] % 2 == 0 and sh.is_contiguous()
+                    and os.environ.get("FEDML_AMD_SHADOW_REFILL", "1") != "0"):
+                # the bf16 weight shadow straight from the global row: one cast of P values and a broadcast of the
+                # bf16 rows (read as fp32 pairs) instead of re-casting the whole [C, P] fp32 stack at the first step
+                row = ops.cast_bf16(flat.reshape(-1).contiguous())
+                ops.broadcast_rows_(sh.view(torch.float32), row.view(torch.float32))
+                self._shadow_stale = False
         if self.mu:
             self.global_ref = flat
 

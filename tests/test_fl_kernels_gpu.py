@@ -312,3 +312,33 @@ def test_fednova_server_step(gmf):
         assert torch.allclose(g.cpu(), g_ref, rtol=1e-5, atol=1e-5)
         if gmf:
             assert torch.allclose(buf.cpu(), buf_ref, rtol=1e-5, atol=1e-4)
+
+
+@pytest.mark.parametrize("method", ["int8", "fp8"])
+def test_compress_accumulate_vector_and_scalar_paths_agree(method):
+    """The fused compress + error-feedback + accumulate kernel takes 16-B accesses for aligned rows and scalar ones
+    otherwise: the same stack laid out with an odd row stride (scalar path for every row but the first) gives the
+    same aggregate and residual updates bit for bit, and the aggregate tracks the uncompressed weighted sum."""
+    torch.manual_seed(4)
+    C, P = 5, 5000
+    params = torch.randn(C, P, device=DEV)
+    glob = torch.randn(P, device=DEV)
+    w = torch.rand(C, device=DEV)
+    ids = torch.arange(10, 10 + C, device=DEV)
+    outs = []
+    for ld in (P, P + 1):
+        buf = torch.zeros(C, ld, device=DEV)
+        buf[:, :P] = params
+        res = [torch.randn(P, device=DEV, generator=torch.Generator(device=DEV).manual_seed(c)) * 0.01
+               for c in range(C)]
+        out = torch.empty(P, device=DEV)
+        ops.compress_accumulate(buf[:, :P], glob, res, w, ids, method, 1234, out)
+        torch.cuda.synchronize()
+        outs.append((out, torch.stack(res)))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    r0 = torch.stack([torch.randn(P, device=DEV, generator=torch.Generator(device=DEV).manual_seed(c)) * 0.01
+                      for c in range(C)])
+    ref = (w.view(-1, 1) * (params + r0)).sum(0)   # compression error within the quantiser's resolution
+    tol = 0.02 if method == "int8" else 0.1
+    assert float((outs[0][0] - ref).abs().max() / ref.abs().max()) < tol
