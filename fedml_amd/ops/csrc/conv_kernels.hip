@@ -1192,7 +1192,9 @@ static int dispatch_nt(int nout, const ConvArgs& a, int C, hipStream_t s) {
 
 // =====================================================================================
 // fp32 1×1 / stride-1 "expand" forward: the bottleneck's last conv, planes → 4·planes (ResNet-56/110: 16 → 64 at
-// 32², 32 → 128 at 16², 64 → 256 at 8²), y = conv(pro(x)) − K with the BN statistics of the stored y.
+// 32², 32 → 128 at 16², 64 → 256 at 8²), y = conv(pro(x)) − K with the BN statistics of the stored y
+// (reference block: python/fedml/model/cv/resnet.py:110 conv3, :127 in forward; its conv1, :106 / :119, is the
+// block-output-forming kernel below).
 //
 // The generic conv_gemm_kernel pads K to 32 (half of every 16-channel layer's MFMAs multiply zeros), stages each
 // 16 × 64 output tile through LDS and keeps one 1-KB operand load in flight per wave: 3.8–4.0 TB/s on a layer that
