@@ -1552,10 +1552,13 @@ static int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return e ? atoi(e) : dflt;
 }
-static int wg_target() {
-  static int v = -1;
-  if (v < 0) v = std::max(64, env_int("FEDML_AMD_C1X_WGS", 2048));
-  return v;
+// measured at C = 100 (profiles/r6_c1x_wgs.txt): 8192 workgroups for the 32² expand (473 → 428 µs) and the 16²
+// block-output-forming kernels (588 → 552, 627 → 569 µs); 2048 for the rest (the 8² block-output kernel 304 → 349 µs
+// and the 16² expand 248 → 262 µs at 8192)
+static int wg_target(int dflt) {
+  static int v = -2;
+  if (v == -2) v = env_int("FEDML_AMD_C1X_WGS", -1);
+  return std::max(64, v > 0 ? v : dflt);
 }
 // expand: ≥ 128 px per wave (13 clients, 8² stage: 41 → 34 µs per call); block-output-forming: no minimum (its
 // 8² stage measured 63 → 80 µs at 128) — profiles/r6_c1x_sizing.txt
@@ -1582,7 +1585,7 @@ static int launch_t(const ConvArgs& a, int C, hipStream_t stream) {
   const int groups = (M + 16 * U - 1) / (16 * U);
   // ≈ 2048 workgroups over the launch (8 per CU), ≥ 2 pixel groups per wave
   const int pc = fa_plan_c(C);
-  const int wgs_target = std::max(1, (wg_target() + pc - 1) / pc);
+  const int wgs_target = std::max(1, (wg_target(CIN == 16 ? 8192 : 2048) + pc - 1) / pc);
   const int gpw = std::max(std::max(2, min_px_per_wave(true) / (16 * U)), (groups + wgs_target * R - 1) / (wgs_target * R));
   const int gx = (groups + R * gpw - 1) / (R * gpw);
   hipLaunchKernelGGL((conv1x1_expand_f32_kernel<CIN, S, PRO, U>), dim3(gx, C), dim3(256), 0, stream, a, gpw,
@@ -1619,7 +1622,7 @@ template <int CIN, int COUT, bool BOUT = true>
 static int launch_pbout_t(const ConvArgs& a, int C, hipStream_t stream) {
   const int tiles = a.Nb * a.Ho * a.Wo / 16;
   const int pc = fa_plan_c(C);
-  const int wgs_target = std::max(1, (wg_target() + pc - 1) / pc);
+  const int wgs_target = std::max(1, (wg_target(CIN == 128 ? 8192 : 2048) + pc - 1) / pc);
   const int gpw = std::max(min_px_per_wave(false) / 16, (tiles + wgs_target * 4 - 1) / (wgs_target * 4));
   const int gx = (tiles + 4 * gpw - 1) / (4 * gpw);
   hipLaunchKernelGGL((conv1x1_pbout_f32_kernel<CIN, COUT, BOUT>), dim3(gx, C), dim3(256), 0, stream, a, gpw,
